@@ -1,0 +1,186 @@
+"""Decode benchmark: Gemma-3 4B Q4_0 greedy decode tokens/s on MI355X.
+
+BASELINE.json metric: "decode tokens/sec + achieved HBM GB/s vs roofline,
+Gemma-3 4B Q4_0" on configs[2] (4B, 512-token prefill + 256 decode).
+A step = one greedy decode token (main.cpp:172-224) of the full model:
+embedding, 34 layers (norms, Q4_0 GEMVs, rope, attention over the whole
+history, GELU), final norm, F16 logits GEMV, argmax -- all device-resident,
+one hipGraph replay per token, the token fed back on the device.
+
+Weights: random-init with the exact gemma-3-4b-it-q4_0 architecture (no
+checkpoints offline); prompt: seeded synthetic token ids.
+
+Single process per GPU.  With --gpus N (torchrun) every rank decodes its own
+independent stream (replicas; tensor-parallel row sharding is DESIGN.md
+section 8's next step), barrier + max-over-ranks timing, value = total tok/s.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=256)
+    p.add_argument("--warmup", type=int, default=16)
+    p.add_argument("--prefill", type=int, default=512)
+    p.add_argument("--config", default="gemma-3-4b")
+    p.add_argument("--exact", action="store_true")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-decode", type=int, default=24, help="decode tokens in the CPU baseline sample")
+    p.add_argument("--kernel-reps", type=int, default=2)
+    return p.parse_args()
+
+
+class Dist:
+    def __init__(self, n):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.pg = None
+        if self.world > 1:
+            import torch.distributed as dist  # gloo only: the GPU is driven by libllmi, not torch
+            dist.init_process_group("gloo")
+            self.dist = dist
+
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
+
+    def max(self, v: float) -> float:
+        if self.world == 1:
+            return v
+        import torch
+        t = torch.tensor([v], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+
+def cpu_baseline(g, cfg, n_decode: int):
+    """The reference's own Model::forward (oracle/_ref, built from its sources)
+    on this host's cores; falls back to the oracle restatement ("port")."""
+    from oracle import bind
+    threads = min(os.cpu_count() or 1, 16)
+    kind = "reference"
+    try:
+        eng = bind.Reference(n_threads=threads)
+        m = eng.model(g)
+    except Exception:
+        kind = "port"
+        eng = bind.Oracle()
+        m = eng.model(g, n_threads=threads, max_ctx=64)
+    prompt = [2] + list(range(100, 107))
+    lg = m.forward(np.array(prompt, np.int32), 0)
+    tok, pos = int(np.argmax(lg)), len(prompt)
+    t0 = time.perf_counter()
+    for _ in range(n_decode):
+        lg = m.forward(np.array([tok], np.int32), pos)
+        tok, pos = int(np.argmax(lg)), pos + 1
+    dt = time.perf_counter() - t0
+    del m
+    return {"value": n_decode / dt, "unit": "tokens/s", "cores": threads, "kind": kind,
+            "sample": f"{cfg.name} Q4_0 synthetic GGUF, {len(prompt)}-token prompt then {n_decode} greedy decode "
+                      f"tokens via Model::forward (short context: CPU attention cost at pos 512+ not included)"}
+
+
+def main():
+    a = parse()
+    d = Dist(a.gpus)
+    # load the HIP library before anything could pull in torch's HIP runtime
+    from llm_inference_amd import _lib
+    _lib.lib()
+    from llm_inference_amd.model import Model
+    from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
+
+    cfg = CONFIGS[a.config]
+    t0 = time.time()
+    g = build_gemma3_gguf(cfg, seed=1234)
+    t_build = time.time() - t0
+    max_ctx = a.prefill + a.warmup + a.steps + 8
+    m = Model(g, device=d.local if a.gpus > 1 else 0, exact=a.exact, max_ctx=max_ctx)
+    info = m.info
+    rng = np.random.default_rng(99 + d.rank)
+    prompt = np.concatenate([[2], rng.integers(4, cfg.vocab, a.prefill - 1)]).astype(np.int32)
+    t0 = time.time()
+    m.forward(prompt, 0, want_logits=False)
+    t_prefill = time.time() - t0
+    first = m.last_argmax
+    pos = a.prefill
+    if a.warmup:
+        m.enqueue(first, pos, a.warmup)
+        toks = m.sync(a.warmup)
+        first, pos = int(toks[-1]), pos + a.warmup
+    d.barrier()
+    m.sync()
+    t0 = time.perf_counter()
+    m.enqueue(first, pos, a.steps)
+    toks = m.sync(a.steps)
+    el = time.perf_counter() - t0
+    d.barrier()
+    el = d.max(el)
+    value = a.steps * d.world / el
+    ms = el * 1000.0 / a.steps
+
+    # dominant kernel: the Q4_0 GEMV family (weights swept in decode order, HIP events)
+    us, by = m.time_kernel(0, a.kernel_reps)
+    us_l, by_l = m.time_kernel(1, 2)
+    ach = by / (us * 1e-6) / 1e9
+    mean_ctx = pos + a.steps / 2
+    tok_bytes = info.bytes_per_token + info.kv_bytes_per_pos * mean_ctx
+    out = {
+        "metric": "decode tokens/sec (Gemma-3 4B Q4_0 shape, greedy)",
+        "value": round(value, 3),
+        "unit": "tokens/s",
+        "n_gpus": d.world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "q4_0 x q8_0 int8-dot, fp32 accumulate; f16 logits",
+        "data": "synthetic (random-init weights of the gemma-3-4b-it-q4_0 architecture, seeded prompt ids)",
+        "config": {
+            "workload": f"{cfg.name}-q4_0 greedy decode after a {a.prefill}-token prefill (BASELINE configs[2])",
+            "prefill_tokens": a.prefill, "decode_tokens": a.steps, "mode": "exact" if a.exact else "fast",
+            "parallelism": f"replicas{d.world}" if d.world > 1 else "single",
+            "kernels_per_token": info.kernels_per_token,
+        },
+        "hbm": {
+            "bytes_per_token": int(tok_bytes),
+            "achieved_GBps": round(tok_bytes * value / d.world / 1e9, 1),
+            "frac_of_peak": round(tok_bytes * value / d.world / 1e9 / PEAK_HBM_GBS, 4),
+        },
+        "roofline": {
+            "kernel": "gemv_q4_0_fast (all Q4_0 GEMV launches of one token, decode order)",
+            "bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": None,
+            "us_per_launch": round(us, 3), "bytes_per_launch": int(by),
+        },
+        "logits_gemv": {"us": round(us_l, 2), "GBps": round(by_l / (us_l * 1e-6) / 1e9, 1)},
+        "timing_detail": {"synthetic_build_s": round(t_build, 1), "prefill_s": round(t_prefill, 2)},
+    }
+    if d.rank == 0 and d.world == 1 and not a.no_cpu_baseline:
+        m.close()
+        try:
+            out["cpu_baseline"] = cpu_baseline(g, cfg, a.cpu_decode)
+        except Exception as e:  # report, never hide
+            out["cpu_baseline"] = {"error": repr(e)}
+    if d.rank == 0:
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

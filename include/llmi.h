@@ -1,0 +1,142 @@
+/*
+ * llmi.h -- C ABI of the MI355X-native decode path for corywalker/llm_inference.
+ *
+ * Library: llm_inference_amd/libllmi.so (HIP, gfx950).  Plain C types only:
+ * pointers, sizes, status codes.  No exceptions cross this boundary; every
+ * entry point returns llmi_status (0 = OK) and llmi_last_error() holds the
+ * reference's own message text for the failure (thread-local).
+ *
+ * Two layers:
+ *  (1) ops.h drop-in (host buffers, synchronous: results are complete on
+ *      return, like the reference's fork/join GEMVs, ops.cpp:450).  One entry
+ *      point per reference function; the reference line each one replaces is
+ *      cited.  The C++ overloads with the reference's exact signatures live in
+ *      include/llmi_ops_compat.h (INTEGRATION.md shows the Bazel wiring).
+ *  (2) device session: the whole Gemma-3 forward of Model::forward
+ *      (model.cpp:706-1049) resident on one MI355X, weights uploaded once from
+ *      the caller's GGUF bytes (the GGUF loader/format is unchanged), each
+ *      decode token replayed as one hipGraph.
+ *
+ * Numerics: LLMI_EXACT selects kernels that reproduce the reference's AVX2
+ * operation order bit-for-bit (GEMVs, quantizers, norms, rope, f16 vector ops);
+ * the default (fast) kernels reassociate reductions across a wavefront and
+ * are checked to the tolerances stated in DESIGN.md.
+ */
+#ifndef LLMI_H
+#define LLMI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+  LLMI_OK = 0,
+  LLMI_E_SIZE = 1,   /* input size mismatch: ops.cpp:196-198 ("input vector size mismatch") */
+  LLMI_E_TYPE = 2,   /* unsupported tensor type: ops.cpp:953-954 */
+  LLMI_E_ARG = 3,    /* invalid argument (e.g. eps <= 0: ops.cpp:29-32, which exit(1)s) */
+  LLMI_E_HIP = 4,    /* HIP runtime failure */
+  LLMI_E_GGUF = 5,   /* malformed GGUF / missing metadata: gguf.cpp:276-277, model.cpp:64-66 */
+  LLMI_E_NODEV = 6,  /* no usable gfx950 device */
+  LLMI_E_RANGE = 7   /* context overflow / token id out of range */
+} llmi_status;
+
+/* flags */
+#define LLMI_EXACT 1u      /* bit-exact AVX2-order kernels */
+#define LLMI_NO_GRAPH 2u   /* session: launch kernels eagerly instead of one hipGraph per token */
+
+const char* llmi_last_error(void);
+int llmi_version(void);
+
+/* ---------------------------------------------------------------------------
+ * (1) ops.h drop-in -- host pointers, synchronous
+ * ------------------------------------------------------------------------- */
+/* init_ops(int n_threads), ops.cpp:21-24: selects the HIP device instead of a
+ * thread count; must precede the other calls (implicitly device 0 otherwise). */
+int llmi_init_ops(int device);
+
+/* mat_vec_mul, ops.cpp:933-956 (+ mat_vec_mul_fp16, ops.cpp:455-612, for
+ * type 1 = F16): o[n_rows] = W[n_rows x n_cols] * x.  W is in GGUF block
+ * layout (row-major blocks, ops.h:11-31/89-102), types Q4_0 2, Q5_0 6, Q8_0 8,
+ * Q4_K 12, Q6_K 14, BF16 30, F16 1.  x_len must equal n_cols. */
+int llmi_mat_vec_mul(uint32_t type, const void* w, size_t n_rows, size_t n_cols, const float* x, size_t x_len,
+                     float* o, uint32_t flags);
+
+/* Weight handles: upload (and repack) a GGUF weight once, then multiply many
+ * times -- what the compat layer does per TensorInfo (keyed by its mmap
+ * pointer) so a model.cpp-driven decode moves only x and o per call. */
+typedef struct llmi_weight llmi_weight;
+int llmi_weight_create(uint32_t type, const void* w, size_t n_rows, size_t n_cols, llmi_weight** out);
+int llmi_weight_mat_vec_mul(const llmi_weight* w, const float* x, size_t x_len, float* o, uint32_t flags);
+/* device-pointer form on a caller stream (hipStream_t passed as void*) */
+int llmi_weight_mat_vec_mul_dev(const llmi_weight* w, const float* x_dev, float* o_dev, uint32_t flags,
+                                void* stream);
+void llmi_weight_destroy(llmi_weight* w);
+
+int llmi_quantize_row_q8_0(const float* x, size_t n, void* y);  /* ops.cpp:116-139, 34-B BlockQ8_0 out */
+int llmi_quantize_row_q8_k(const float* x, size_t n, void* y);  /* ops.cpp:142-178, 292-B block_q8_K out */
+/* dequantize_{q4_k,q6_k,q8_0,q5_0}_row, ops.cpp:958-1082 (+F16/F32) */
+int llmi_dequantize_row(uint32_t type, const void* blocks, size_t n_cols, float* o);
+int llmi_rms_norm(float* o, const float* x, size_t n, double eps, uint32_t flags); /* ops.cpp:28-43 */
+int llmi_softmax(float* x, size_t n);                                              /* ops.cpp:45-62 */
+/* rope, ops.cpp:67-95; t is [n_tokens][n_heads][head_dim] contiguous, in place */
+int llmi_rope(float* t, size_t n_tokens, size_t n_heads, size_t head_dim, int n_rot, float freq_base,
+              float freq_scale, int pos);
+int llmi_scale(float* t, size_t n, float s);                                      /* ops.cpp:97-105 */
+int llmi_vec_scale_f16(uint16_t* y, size_t n, float v);                           /* ops.cpp:1084-1089 */
+int llmi_vec_mad_f16(uint16_t* y, const uint16_t* x, size_t n, float v);          /* ops.cpp:1091-1099 */
+
+/* ---------------------------------------------------------------------------
+ * (2) device session (Gemma-3 GGUF)
+ * ------------------------------------------------------------------------- */
+typedef struct llmi_session llmi_session;
+
+typedef struct {
+  int device;          /* HIP device ordinal */
+  uint32_t flags;      /* LLMI_EXACT | LLMI_NO_GRAPH */
+  int max_ctx;         /* KV-cache capacity in positions (default 4096) */
+  int attn_split;      /* fast attention split count (0 = auto) */
+} llmi_session_opts;
+
+/* Parses the GGUF (format of gguf.cpp:274-304, hparams of model.cpp:58-167)
+ * and uploads every weight.  The bytes are only read during the call. */
+int llmi_session_create(const void* gguf, size_t size, const llmi_session_opts* opts, llmi_session** out);
+void llmi_session_destroy(llmi_session* s);
+
+/* Model::forward(tokens, pos) (model.cpp:706): runs n_tokens tokens at
+ * positions pos..pos+n_tokens-1 and returns the LAST token's logits
+ * (vocab floats, may be NULL) and its greedy argmax (may be NULL). */
+int llmi_session_forward(llmi_session* s, const int32_t* tokens, int n_tokens, int pos, float* logits,
+                         int32_t* argmax);
+
+/* Greedy decode loop of main.cpp:172-224 kept on the device: token `first`
+ * at position `pos`, then n_steps forwards, each feeding its argmax to the
+ * next without a host round trip.  out_tokens[i] = argmax after step i. */
+int llmi_session_generate(llmi_session* s, int32_t first, int pos, int n_steps, int32_t* out_tokens);
+
+/* Enqueue n_steps decode steps without waiting (bench); llmi_session_sync
+ * waits and copies the produced tokens (may be NULL). */
+int llmi_session_enqueue(llmi_session* s, int32_t first, int pos, int n_steps);
+int llmi_session_sync(llmi_session* s, int32_t* out_tokens, int n);
+
+typedef struct {
+  int n_layer, n_embd, n_ff, n_head, n_head_kv, head_dim, vocab, max_ctx;
+  size_t weight_bytes;        /* device bytes of all uploaded weights */
+  size_t bytes_per_token;     /* algorithmic HBM bytes of one decode token, KV excluded */
+  size_t kv_bytes_per_pos;    /* + this many bytes per attended position */
+  int kernels_per_token;      /* launches captured in the decode graph */
+} llmi_session_info;
+int llmi_session_get_info(const llmi_session* s, llmi_session_info* info);
+
+/* Benchmark hook: time `reps` launches of the session's dominant kernel
+ * family (0 = Q4_0/Q8_0 GEMV over every layer's weights in decode order,
+ * 1 = F16 logits GEMV) with HIP events on the session stream.  Returns the
+ * mean microseconds per launch and the mean algorithmic bytes per launch. */
+int llmi_session_time_kernel(llmi_session* s, int which, int reps, double* us_per_launch, double* bytes_per_launch);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,63 @@
+"""Build libllmi.so (HIP, gfx950) in-tree with hipcc.
+
+    python -m llm_inference_amd.build [--force]
+
+Every translation unit is compiled with -ffp-contract=off (the numerics
+contract of csrc/common.h) for --offload-arch=gfx950 only, in parallel, then
+linked into llm_inference_amd/libllmi.so next to this file (git-ignored, but
+shipped to the GPU box with the repo snapshot).
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+OBJ = os.path.join(HERE, "_build")
+LIB = os.path.join(HERE, "libllmi.so")
+SOURCES = ["k_gemv.hip", "k_elem.hip", "k_attn.hip", "k_session.hip", "session.cpp", "capi.cpp"]
+HEADERS = ["common.h", "kernels.h", "attn.h", "session_kernels.h", "session.h", "gguf_reader.h"]
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "--offload-arch=gfx950", "-Wall",
+         "-Wno-unused-function", "-Wno-unused-variable", "-Wno-unused-result"]
+
+
+def _mtime(p):
+    return os.path.getmtime(p) if os.path.exists(p) else 0.0
+
+
+def _compile(src: str) -> str:
+    out = os.path.join(OBJ, os.path.splitext(src)[0] + ".o")
+    cmd = [HIPCC] + FLAGS + ["-x", "hip", "-c", os.path.join(CSRC, src), "-o", out]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr[-4000:]}")
+    return out
+
+
+def build(force: bool = False, jobs: int = 0) -> str:
+    os.makedirs(OBJ, exist_ok=True)
+    hdr_t = max(_mtime(os.path.join(CSRC, h)) for h in HEADERS + ["../../include/llmi.h"])
+    todo = []
+    for s in SOURCES:
+        o = os.path.join(OBJ, os.path.splitext(s)[0] + ".o")
+        if force or _mtime(o) < max(_mtime(os.path.join(CSRC, s)), hdr_t):
+            todo.append(s)
+    jobs = jobs or min(len(todo) or 1, os.cpu_count() or 4, 8)
+    if todo:
+        with cf.ThreadPoolExecutor(jobs) as ex:
+            list(ex.map(_compile, todo))
+    objs = [os.path.join(OBJ, os.path.splitext(s)[0] + ".o") for s in SOURCES]
+    if force or todo or _mtime(LIB) < max(_mtime(o) for o in objs):
+        cmd = [HIPCC, "-shared", "-fPIC", "--offload-arch=gfx950", "-o", LIB] + objs
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stderr[-4000:]}")
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv))

@@ -1,0 +1,39 @@
+// attn.h -- argument blocks for the attention-side kernels (k_attn.hip).
+#pragma once
+
+#include "kernels.h"
+
+namespace llmi {
+
+struct QKVArgs {
+  const float* qkv;       // fused QKV GEMV output: q at 0, k at k_off, v at v_off
+  int k_off, v_off;
+  int n_head, n_head_kv, head_dim;
+  const float* q_norm_w;  // [head_dim] f32 (attn_q_norm.weight)
+  const float* k_norm_w;  // [head_dim] f32 (attn_k_norm.weight)
+  const float* rope_cs;   // [max_ctx][head_dim/2][2] (cos, sin) for this layer's base
+  float attn_scale;       // 1/sqrt(head_dim) (model.cpp:120)
+  double eps;
+  float* q_out;           // [n_head][head_dim]
+  uint16_t* k_cache;      // [n_head_kv][max_ctx][head_dim]
+  uint16_t* v_cache;
+  int max_ctx;
+  const int* d_pos;       // device position of this token
+};
+
+struct AttnArgs {
+  const float* q;         // [n_head][head_dim], normed/roped/scaled
+  const uint16_t* k_cache;
+  const uint16_t* v_cache;
+  int n_head, n_head_kv, head_dim, max_ctx;
+  const int* d_pos;       // keys 0..*d_pos are attended (no window: model.cpp:501)
+  float* partial;         // fast path scratch [n_head][nsplit][head_dim + 2]
+  float* out;             // [n_head][head_dim]
+};
+
+void launch_qk_norm_rope_kv(const QKVArgs& a, bool exact, hipStream_t s);
+// exact: attn_exact_kernel -> out.  fast: partial + combine (-> out, and
+// Q8_0 blocks of out when q8 != nullptr).
+void launch_attention(const AttnArgs& a, bool exact, int nsplit, const Q8Act* q8, hipStream_t s);
+
+}  // namespace llmi

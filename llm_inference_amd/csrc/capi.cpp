@@ -1,0 +1,394 @@
+// capi.cpp -- extern "C" entry points of include/llmi.h.
+//
+// Error contract: no C++ exception crosses the ABI; every call returns an
+// llmi_status and stores the message (the reference's own wording where it
+// has one) for llmi_last_error().
+#include <cmath>
+#include <mutex>
+#include <vector>
+
+#include "session.h"
+
+using namespace llmi;
+
+namespace {
+
+thread_local std::string g_err;
+
+struct Ctx {
+  int device = -1;
+  hipStream_t stream = nullptr;
+  // grow-only scratch for the host-pointer ops API
+  std::vector<std::pair<void*, size_t>> bufs;
+  void* get(int slot, size_t bytes) {
+    if ((int)bufs.size() <= slot) bufs.resize(slot + 1, {nullptr, 0});
+    auto& b = bufs[slot];
+    if (b.second < bytes) {
+      if (b.first) LLMI_HIP(hipFree(b.first));
+      LLMI_HIP(hipMalloc(&b.first, bytes + 256));
+      b.second = bytes;
+    }
+    return b.first;
+  }
+};
+
+Ctx& ctx() {
+  static thread_local Ctx c;
+  if (c.device < 0) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) throw status_error(LLMI_E_NODEV, "no HIP device");
+    c.device = 0;
+    LLMI_HIP(hipSetDevice(0));
+    LLMI_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+  }
+  return c;
+}
+
+template <typename F>
+int guard(F&& f) {
+  try {
+    f();
+    return LLMI_OK;
+  } catch (const status_error& e) {
+    g_err = e.what();
+    return e.code;
+  } catch (const hip_error& e) {
+    g_err = e.what();
+    return LLMI_E_HIP;
+  } catch (const gguf_error& e) {
+    g_err = e.what();
+    return LLMI_E_GGUF;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return std::string(e.what()).find("unsupported tensor type") != std::string::npos ? LLMI_E_TYPE : LLMI_E_ARG;
+  }
+}
+
+const char* type_fn(uint32_t t) {
+  switch (t) {
+    case T_Q4_0: return "mat_vec_mul_q4_0";
+    case T_Q4_K: return "mat_vec_mul_q4_k";
+    case T_Q6_K: return "mat_vec_mul_q6_k";
+    case T_Q8_0: return "mat_vec_mul_q8_0";
+    case T_Q5_0: return "mat_vec_mul_q5_0";
+    case T_BF16: return "mat_vec_mul_bf16";
+    case T_F16: return "mat_vec_mul_fp16";
+    default: return "mat_vec_mul";
+  }
+}
+
+void check_shape(uint32_t type, size_t n_rows, size_t n_cols, size_t x_len) {
+  if (!gemv_type_supported(type))
+    throw status_error(LLMI_E_TYPE, "mat_vec_mul: unsupported tensor type " + std::to_string(type));
+  if (x_len != n_cols) throw status_error(LLMI_E_SIZE, std::string(type_fn(type)) + ": input vector size mismatch");
+  const size_t blk = (type == T_Q4_K || type == T_Q6_K) ? 256 : (type == T_F16 || type == T_BF16) ? 1 : 32;
+  if (n_cols % blk) throw status_error(LLMI_E_SIZE, std::string(type_fn(type)) + ": n_cols not a block multiple");
+  if (n_rows > (size_t)INT32_MAX || n_cols > (size_t)INT32_MAX)
+    throw status_error(LLMI_E_SIZE, "matrix too large");
+}
+
+// activation for weight type `t` from device x (scratch slots 10..13)
+ActBuf make_act(Ctx& c, uint32_t t, const float* x_dev, int n, hipStream_t s) {
+  ActBuf a;
+  a.xf = x_dev;
+  if (t == T_Q4_0 || t == T_Q8_0) {
+    a.q8.qs = (int8_t*)c.get(10, n);
+    a.q8.d = (uint16_t*)c.get(11, (n / 32 + 1) * 2);
+    a.q8.nsum8 = (int32_t*)c.get(12, (n / 32 + 1) * 4);
+    launch_quantize_q8_0(x_dev, n, a.q8, s);
+  } else if (t == T_Q4_K || t == T_Q6_K) {
+    a.q8k = (uint8_t*)c.get(13, (size_t)(n / 256 + 1) * 292);
+    launch_quantize_q8_k(x_dev, n, a.q8k, s);
+  } else if (t == T_F16) {
+    a.x16 = (uint16_t*)c.get(14, (size_t)n * 2);
+    launch_round_f16(x_dev, n, a.x16, s);
+  }
+  return a;
+}
+
+}  // namespace
+
+struct llmi_weight {
+  DevWeight w;
+};
+struct llmi_session {
+  Session* s;
+};
+
+extern "C" {
+
+const char* llmi_last_error(void) { return g_err.c_str(); }
+int llmi_version(void) { return 1; }
+
+int llmi_init_ops(int device) {
+  return guard([&] {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n)
+      throw status_error(LLMI_E_NODEV, "no HIP device " + std::to_string(device));
+    Ctx& c = ctx();
+    if (c.device != device) {
+      if (c.stream) LLMI_HIP(hipStreamDestroy(c.stream));
+      for (auto& b : c.bufs)
+        if (b.first) (void)hipFree(b.first);
+      c.bufs.clear();
+      c.device = device;
+      LLMI_HIP(hipSetDevice(device));
+      LLMI_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+    }
+  });
+}
+
+int llmi_weight_create(uint32_t type, const void* w, size_t n_rows, size_t n_cols, llmi_weight** out) {
+  return guard([&] {
+    if (!w || !out) throw status_error(LLMI_E_ARG, "null pointer");
+    check_shape(type, n_rows, n_cols, n_cols);
+    Ctx& c = ctx();
+    auto* h = new llmi_weight;
+    try {
+      h->w = alloc_weight(type, (int)n_rows, (int)n_cols);
+      upload_rows(h->w, 0, w, (int)n_rows, c.stream);
+    } catch (...) {
+      free_weight(h->w);
+      delete h;
+      throw;
+    }
+    *out = h;
+  });
+}
+
+void llmi_weight_destroy(llmi_weight* w) {
+  if (!w) return;
+  free_weight(w->w);
+  delete w;
+}
+
+int llmi_weight_mat_vec_mul_dev(const llmi_weight* w, const float* x_dev, float* o_dev, uint32_t flags,
+                                void* stream) {
+  return guard([&] {
+    Ctx& c = ctx();
+    hipStream_t s = stream ? (hipStream_t)stream : c.stream;
+    ActBuf a = make_act(c, w->w.type, x_dev, w->w.cols, s);
+    launch_gemv(w->w, a, o_dev, (flags & LLMI_EXACT) ? GEMV_EXACT : GEMV_FAST, s);
+  });
+}
+
+int llmi_weight_mat_vec_mul(const llmi_weight* w, const float* x, size_t x_len, float* o, uint32_t flags) {
+  return guard([&] {
+    if (!w || !x || !o) throw status_error(LLMI_E_ARG, "null pointer");
+    check_shape(w->w.type, w->w.rows, w->w.cols, x_len);
+    Ctx& c = ctx();
+    float* xd = (float*)c.get(0, x_len * 4);
+    float* od = (float*)c.get(1, (size_t)w->w.rows * 4);
+    LLMI_HIP(hipMemcpyAsync(xd, x, x_len * 4, hipMemcpyHostToDevice, c.stream));
+    ActBuf a = make_act(c, w->w.type, xd, (int)x_len, c.stream);
+    launch_gemv(w->w, a, od, (flags & LLMI_EXACT) ? GEMV_EXACT : GEMV_FAST, c.stream);
+    LLMI_HIP(hipMemcpyAsync(o, od, (size_t)w->w.rows * 4, hipMemcpyDeviceToHost, c.stream));
+    LLMI_HIP(hipStreamSynchronize(c.stream));
+  });
+}
+
+int llmi_mat_vec_mul(uint32_t type, const void* w, size_t n_rows, size_t n_cols, const float* x, size_t x_len,
+                     float* o, uint32_t flags) {
+  return guard([&] {
+    if (!w || !x || !o) throw status_error(LLMI_E_ARG, "null pointer");
+    check_shape(type, n_rows, n_cols, x_len);
+    if (n_rows == 0) return;
+    llmi_weight* h = nullptr;
+    int rc = llmi_weight_create(type, w, n_rows, n_cols, &h);
+    if (rc) throw status_error(rc, g_err);
+    rc = llmi_weight_mat_vec_mul(h, x, x_len, o, flags);
+    llmi_weight_destroy(h);
+    if (rc) throw status_error(rc, g_err);
+  });
+}
+
+int llmi_quantize_row_q8_0(const float* x, size_t n, void* y) {
+  return guard([&] {
+    if (n % 32) throw status_error(LLMI_E_SIZE, "quantize_row_q8_0: size % 32 != 0");
+    Ctx& c = ctx();
+    float* xd = (float*)c.get(0, n * 4);
+    Q8Act q{(int8_t*)c.get(10, n), (uint16_t*)c.get(11, (n / 32 + 1) * 2), (int32_t*)c.get(12, (n / 32 + 1) * 4),
+            (int)(n / 32)};
+    LLMI_HIP(hipMemcpyAsync(xd, x, n * 4, hipMemcpyHostToDevice, c.stream));
+    launch_quantize_q8_0(xd, (int)n, q, c.stream);
+    std::vector<int8_t> qs(n);
+    std::vector<uint16_t> d(n / 32);
+    LLMI_HIP(hipMemcpyAsync(qs.data(), q.qs, n, hipMemcpyDeviceToHost, c.stream));
+    LLMI_HIP(hipMemcpyAsync(d.data(), q.d, n / 32 * 2, hipMemcpyDeviceToHost, c.stream));
+    LLMI_HIP(hipStreamSynchronize(c.stream));
+    uint8_t* out = (uint8_t*)y;  // BlockQ8_0 {f16 d; i8 qs[32]} (ops.h:89-92)
+    for (size_t b = 0; b < n / 32; b++) {
+      std::memcpy(out + b * 34, &d[b], 2);
+      std::memcpy(out + b * 34 + 2, &qs[b * 32], 32);
+    }
+  });
+}
+
+int llmi_quantize_row_q8_k(const float* x, size_t n, void* y) {
+  return guard([&] {
+    if (n % 256) throw status_error(LLMI_E_SIZE, "quantize_row_q8_k: size % 256 != 0");
+    Ctx& c = ctx();
+    float* xd = (float*)c.get(0, n * 4);
+    uint8_t* yd = (uint8_t*)c.get(13, n / 256 * 292);
+    LLMI_HIP(hipMemcpyAsync(xd, x, n * 4, hipMemcpyHostToDevice, c.stream));
+    launch_quantize_q8_k(xd, (int)n, yd, c.stream);
+    LLMI_HIP(hipMemcpyAsync(y, yd, n / 256 * 292, hipMemcpyDeviceToHost, c.stream));
+    LLMI_HIP(hipStreamSynchronize(c.stream));
+  });
+}
+
+int llmi_dequantize_row(uint32_t type, const void* blocks, size_t n_cols, float* o) {
+  return guard([&] {
+    if (type != T_Q4_K && type != T_Q6_K && type != T_Q8_0 && type != T_Q5_0 && type != T_F16 && type != T_F32)
+      throw status_error(LLMI_E_TYPE, "dequantize: unsupported tensor type " + std::to_string(type));
+    Ctx& c = ctx();
+    const size_t rb = gguf_bytes(type, 1, n_cols);
+    uint8_t* bd = (uint8_t*)c.get(2, rb);
+    float* od = (float*)c.get(1, n_cols * 4);
+    int32_t* idd = (int32_t*)c.get(3, 4);
+    LLMI_HIP(hipMemcpyAsync(bd, blocks, rb, hipMemcpyHostToDevice, c.stream));
+    LLMI_HIP(hipMemsetAsync(idd, 0, 4, c.stream));
+    launch_dequantize_rows(type, bd, rb, idd, 1, (int)n_cols, 1.0f, od, c.stream);
+    LLMI_HIP(hipMemcpyAsync(o, od, n_cols * 4, hipMemcpyDeviceToHost, c.stream));
+    LLMI_HIP(hipStreamSynchronize(c.stream));
+  });
+}
+
+int llmi_rms_norm(float* o, const float* x, size_t n, double eps, uint32_t flags) {
+  return guard([&] {
+    if (eps <= 0) throw status_error(LLMI_E_ARG, "Error: eps must be > 0 in rms_norm.");  // ops.cpp:29-32
+    Ctx& c = ctx();
+    float* xd = (float*)c.get(0, n * 4);
+    float* od = (float*)c.get(1, n * 4);
+    LLMI_HIP(hipMemcpyAsync(xd, x, n * 4, hipMemcpyHostToDevice, c.stream));
+    launch_rms_norm(xd, nullptr, od, (int)n, 1, eps, (flags & LLMI_EXACT) != 0, c.stream);
+    LLMI_HIP(hipMemcpyAsync(o, od, n * 4, hipMemcpyDeviceToHost, c.stream));
+    LLMI_HIP(hipStreamSynchronize(c.stream));
+  });
+}
+
+int llmi_softmax(float* x, size_t n) {
+  return guard([&] {
+    Ctx& c = ctx();
+    float* xd = (float*)c.get(0, n * 4);
+    LLMI_HIP(hipMemcpyAsync(xd, x, n * 4, hipMemcpyHostToDevice, c.stream));
+    launch_softmax(xd, (int)n, c.stream);
+    LLMI_HIP(hipMemcpyAsync(x, xd, n * 4, hipMemcpyDeviceToHost, c.stream));
+    LLMI_HIP(hipStreamSynchronize(c.stream));
+  });
+}
+
+int llmi_rope(float* t, size_t n_tokens, size_t n_heads, size_t head_dim, int n_rot, float freq_base,
+              float freq_scale, int pos) {
+  return guard([&] {
+    if (n_rot <= 0 || (size_t)n_rot > head_dim || n_rot % 2)
+      throw status_error(LLMI_E_ARG, "rope: invalid n_rot");
+    if (n_tokens == 0 || n_heads == 0) return;
+    Ctx& c = ctx();
+    const int half = n_rot / 2;
+    std::vector<float> cs(n_tokens * half * 2);  // ops.cpp:79-83, host glibc
+    for (size_t tk = 0; tk < n_tokens; tk++)
+      for (int i = 0; i < half; i++) {
+        const float freq = 1.0f / powf(freq_base, (float)(2 * i) / (float)n_rot);
+        const float val = ((float)(uint32_t)(pos + (uint32_t)tk) * freq) / freq_scale;
+        cs[(tk * half + i) * 2] = cosf(val);
+        cs[(tk * half + i) * 2 + 1] = sinf(val);
+      }
+    const size_t n = n_tokens * n_heads * head_dim;
+    float* td = (float*)c.get(0, n * 4);
+    float* csd = (float*)c.get(4, cs.size() * 4);
+    LLMI_HIP(hipMemcpyAsync(td, t, n * 4, hipMemcpyHostToDevice, c.stream));
+    LLMI_HIP(hipMemcpyAsync(csd, cs.data(), cs.size() * 4, hipMemcpyHostToDevice, c.stream));
+    launch_rope(td, (int)(n_tokens * n_heads), (int)head_dim, n_rot, csd, (int)n_heads, c.stream);
+    LLMI_HIP(hipMemcpyAsync(t, td, n * 4, hipMemcpyDeviceToHost, c.stream));
+    LLMI_HIP(hipStreamSynchronize(c.stream));
+  });
+}
+
+int llmi_scale(float* t, size_t n, float sc) {
+  return guard([&] {
+    Ctx& c = ctx();
+    float* td = (float*)c.get(0, n * 4);
+    LLMI_HIP(hipMemcpyAsync(td, t, n * 4, hipMemcpyHostToDevice, c.stream));
+    launch_scale(td, (int)n, sc, c.stream);
+    LLMI_HIP(hipMemcpyAsync(t, td, n * 4, hipMemcpyDeviceToHost, c.stream));
+    LLMI_HIP(hipStreamSynchronize(c.stream));
+  });
+}
+
+int llmi_vec_scale_f16(uint16_t* y, size_t n, float v) {
+  return guard([&] {
+    Ctx& c = ctx();
+    uint16_t* yd = (uint16_t*)c.get(0, n * 2);
+    LLMI_HIP(hipMemcpyAsync(yd, y, n * 2, hipMemcpyHostToDevice, c.stream));
+    launch_vec_scale_f16(yd, (int)n, v, c.stream);
+    LLMI_HIP(hipMemcpyAsync(y, yd, n * 2, hipMemcpyDeviceToHost, c.stream));
+    LLMI_HIP(hipStreamSynchronize(c.stream));
+  });
+}
+
+int llmi_vec_mad_f16(uint16_t* y, const uint16_t* x, size_t n, float v) {
+  return guard([&] {
+    Ctx& c = ctx();
+    uint16_t* yd = (uint16_t*)c.get(0, n * 2);
+    uint16_t* xd = (uint16_t*)c.get(1, n * 2);
+    LLMI_HIP(hipMemcpyAsync(yd, y, n * 2, hipMemcpyHostToDevice, c.stream));
+    LLMI_HIP(hipMemcpyAsync(xd, x, n * 2, hipMemcpyHostToDevice, c.stream));
+    launch_vec_mad_f16(yd, xd, (int)n, v, c.stream);
+    LLMI_HIP(hipMemcpyAsync(y, yd, n * 2, hipMemcpyDeviceToHost, c.stream));
+    LLMI_HIP(hipStreamSynchronize(c.stream));
+  });
+}
+
+// ---- session ----
+int llmi_session_create(const void* gguf, size_t size, const llmi_session_opts* opts, llmi_session** out) {
+  return guard([&] {
+    if (!gguf || !out) throw status_error(LLMI_E_ARG, "null pointer");
+    llmi_session_opts o{0, 0, 4096, 0};
+    if (opts) o = *opts;
+    auto* h = new llmi_session{nullptr};
+    try {
+      h->s = new Session((const uint8_t*)gguf, size, o);
+    } catch (...) {
+      delete h;
+      throw;
+    }
+    *out = h;
+  });
+}
+
+void llmi_session_destroy(llmi_session* s) {
+  if (!s) return;
+  delete s->s;
+  delete s;
+}
+
+int llmi_session_forward(llmi_session* s, const int32_t* tokens, int n_tokens, int pos, float* logits,
+                         int32_t* argmax) {
+  return guard([&] { s->s->forward(tokens, n_tokens, pos, logits, argmax); });
+}
+
+int llmi_session_generate(llmi_session* s, int32_t first, int pos, int n_steps, int32_t* out_tokens) {
+  return guard([&] {
+    s->s->enqueue(first, pos, n_steps);
+    s->s->sync(out_tokens, n_steps);
+  });
+}
+
+int llmi_session_enqueue(llmi_session* s, int32_t first, int pos, int n_steps) {
+  return guard([&] { s->s->enqueue(first, pos, n_steps); });
+}
+
+int llmi_session_sync(llmi_session* s, int32_t* out_tokens, int n) {
+  return guard([&] { s->s->sync(out_tokens, n); });
+}
+
+int llmi_session_get_info(const llmi_session* s, llmi_session_info* info) {
+  return guard([&] { s->s->info(info); });
+}
+
+int llmi_session_time_kernel(llmi_session* s, int which, int reps, double* us, double* bytes) {
+  return guard([&] { s->s->time_kernel(which, reps, us, bytes); });
+}
+
+}  // extern "C"

@@ -1,0 +1,120 @@
+// common.h -- shared device/host helpers for the gfx950 decode kernels.
+//
+// Numerics contract: this library is compiled with -ffp-contract=off; every
+// fused multiply-add that the reference's pinned build contracts is written as
+// an explicit fmaf() (see oracle/llmi_oracle.c for the CPU statement of the
+// same arithmetic).  Kernels named *_exact reproduce the reference's AVX2
+// operation order bit-for-bit; *_fast kernels reassociate reductions across a
+// wavefront and are checked to a stated tolerance.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <cstdio>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+namespace llmi {
+
+constexpr int WAVE = 64;
+
+// ggml tensor type ids (reference gguf.h:30-46)
+enum : uint32_t { T_F32 = 0, T_F16 = 1, T_Q4_0 = 2, T_Q5_0 = 6, T_Q8_0 = 8, T_Q4_K = 12, T_Q6_K = 14, T_BF16 = 30 };
+
+struct hip_error : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+#define LLMI_HIP(call)                                                                           \
+  do {                                                                                           \
+    hipError_t e_ = (call);                                                                      \
+    if (e_ != hipSuccess)                                                                        \
+      throw ::llmi::hip_error(std::string(#call) + ": " + hipGetErrorString(e_) + " @" __FILE__); \
+  } while (0)
+
+// ---------------------------------------------------------------------------
+// fp16 conversions.  The reference uses ggml's software conversions
+// (gguf.cpp:40-95): exact IEEE binary16<->binary32, round-to-nearest-even,
+// NaN -> 0x7E00.  gfx950's v_cvt_f16_f32 / v_cvt_f32_f16 give the same bits
+// for every non-NaN input (checked by tests/test_hip_ops.py against the
+// reference's 65536-entry table and its RNE edge cases); the ggml form is kept
+// for the NaN-exact path.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float h2f(uint16_t h) {
+  return (float)__builtin_bit_cast(_Float16, h);
+}
+__device__ __forceinline__ uint16_t f2h(float f) {
+  return __builtin_bit_cast(uint16_t, (_Float16)f);
+}
+__device__ __forceinline__ uint16_t f2h_ggml(float f) {  // gguf.cpp:68-95
+  float base = (fabsf(f) * 0x1.0p+112f) * 0x1.0p-110f;
+  const uint32_t w = __float_as_uint(f);
+  const uint32_t shl1_w = w + w;
+  const uint32_t sign = w & 0x80000000u;
+  uint32_t bias = shl1_w & 0xFF000000u;
+  if (bias < 0x71000000u) bias = 0x71000000u;
+  base = __uint_as_float((bias >> 1) + 0x07800000u) + base;
+  const uint32_t bits = __float_as_uint(base);
+  const uint32_t nonsign = ((bits >> 13) & 0x00007C00u) + (bits & 0x00000FFFu);
+  return (uint16_t)((sign >> 16) | (shl1_w > 0xFF000000u ? 0x7E00u : nonsign));
+}
+
+// nearest_int with the product fused into the magic add, exactly as the
+// reference's compiler emits it (ops.cpp:107-113,135-136: vfmadd132ss).
+__device__ __forceinline__ int nearest_int_fma(float a, float b) {
+  return (int)(__float_as_uint(fmaf(a, b, 12582912.f)) & 0x007fffffu) - 0x00400000;
+}
+
+__device__ __forceinline__ int sdot4(int a, int b, int c) { return __builtin_amdgcn_sdot4(a, b, c, false); }
+
+// streamed-once weight loads: non-temporal 16-B global loads (MI355X_MICROARCH
+// 'nt-weights': once-read decode weights should not displace L2 lines)
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ld_nt(const uint4* p) {
+  const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ int4 ld_nt(const int4* p) {
+  const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
+  return make_int4((int)v.x, (int)v.y, (int)v.z, (int)v.w);
+}
+
+// ---------------------------------------------------------------------------
+// wave-level reductions (64 lanes).  Fixed xor-butterfly order, so results
+// are deterministic run to run.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+
+// orderable key for argmax with "first maximal index wins" (std::max_element,
+// reference main.cpp:193-194): larger value first, then smaller index.
+__device__ __forceinline__ unsigned long long argmax_key(float v, uint32_t idx) {
+  uint32_t u = __float_as_uint(v);
+  u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  return ((unsigned long long)u << 32) | (0xFFFFFFFFu - idx);
+}
+__host__ __device__ inline uint32_t argmax_key_index(unsigned long long k) {
+  return 0xFFFFFFFFu - (uint32_t)(k & 0xFFFFFFFFull);
+}
+
+// Q8_0 activation vector in device layout (ops.h:89-92 restated SoA):
+//   qs [nb][32] int8   d [nb] f16 bits   dsum [nb] int32 (= -8 * sum(qs), the
+//   Q4_0 zero-point correction, ops.cpp:385-388)
+struct Q8Act {
+  int8_t* qs;
+  uint16_t* d;
+  int32_t* nsum8;
+  int nb;
+};
+
+}  // namespace llmi

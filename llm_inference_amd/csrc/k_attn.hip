@@ -1,0 +1,267 @@
+// k_attn.hip -- per-head q/k norm + rope + KV append, and decode attention.
+//
+// KV cache layout (per layer): [n_head_kv][max_ctx][head_dim] f16, so one
+// head's history is one contiguous stream.  The current position lives in
+// device memory (d_pos) so a whole decode step can be replayed as one
+// hipGraph without re-capturing.
+#include "attn.h"
+
+namespace llmi {
+
+// ---------------------------------------------------------------------------
+// q/k per-head rms_norm * weight (model.cpp:762,792), NEOX rope at pos
+// (model.cpp:764,794), q *= 1/sqrt(head_dim) (model.cpp:767), K and V rows
+// rounded to f16 into the cache (model.cpp:442-474).
+// grid = n_head + n_head_kv blocks of 256 threads; head_dim <= 256.
+// ---------------------------------------------------------------------------
+template <bool EXACT>
+__global__ __launch_bounds__(256) void qk_norm_rope_kv_kernel(QKVArgs a) {
+  __shared__ float s_x[256];
+  __shared__ float s_part[4];
+  __shared__ float s_scale;
+  const int t = threadIdx.x;
+  const int hd = a.head_dim;
+  const int pos = *a.d_pos;
+  const bool is_q = blockIdx.x < (unsigned)a.n_head;
+  const int h = is_q ? blockIdx.x : blockIdx.x - a.n_head;
+  const float* src = a.qkv + (is_q ? (size_t)h * hd : (size_t)a.k_off + (size_t)h * hd);
+  const float* nw = is_q ? a.q_norm_w : a.k_norm_w;
+  const float v = t < hd ? src[t] : 0.0f;
+  if (t < hd) s_x[t] = v;
+  __syncthreads();
+  if (EXACT) {
+    if (t == 0) {
+      float sum = 0.0f;
+      for (int i = 0; i < hd; i++) sum = fmaf(s_x[i], s_x[i], sum);
+      s_scale = 1.0f / sqrtf((float)((double)(sum / (float)hd) + a.eps));
+    }
+  } else {
+    float sum = wave_sum(v * v);
+    if ((t & 63) == 0) s_part[t >> 6] = sum;
+    __syncthreads();
+    if (t == 0) {
+      const float tot = (s_part[0] + s_part[1]) + (s_part[2] + s_part[3]);
+      s_scale = 1.0f / sqrtf((float)((double)(tot / (float)hd) + a.eps));
+    }
+  }
+  __syncthreads();
+  const float nv = t < hd ? (s_scale * v) * nw[t] : 0.0f;
+  __syncthreads();
+  if (t < hd) s_x[t] = nv;
+  __syncthreads();
+  const int half = hd / 2;
+  const float* cs = a.rope_cs + (size_t)pos * half * 2;
+  float r = nv;
+  if (t < half) {
+    const float c = cs[2 * t], sn = cs[2 * t + 1];
+    r = fmaf(s_x[t], c, -(s_x[t + half] * sn));
+  } else if (t < hd) {
+    const float c = cs[2 * (t - half)], sn = cs[2 * (t - half) + 1];
+    r = fmaf(s_x[t - half], sn, s_x[t] * c);
+  }
+  if (t < hd) {
+    if (is_q) {
+      a.q_out[(size_t)h * hd + t] = r * a.attn_scale;
+    } else {
+      const size_t ci = ((size_t)h * a.max_ctx + pos) * hd + t;
+      a.k_cache[ci] = f2h_ggml(r);
+      a.v_cache[ci] = f2h_ggml(a.qkv[(size_t)a.v_off + (size_t)h * hd + t]);
+    }
+  }
+}
+
+void launch_qk_norm_rope_kv(const QKVArgs& a, bool exact, hipStream_t s) {
+  const dim3 grid(a.n_head + a.n_head_kv);
+  if (exact)
+    hipLaunchKernelGGL(qk_norm_rope_kv_kernel<true>, grid, dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(qk_norm_rope_kv_kernel<false>, grid, dim3(256), 0, s, a);
+  LLMI_HIP(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------
+// exact attention (model.cpp:481-547): one block per query head, keys in
+// order; score = sequential double sum of exact f32 products f16(k)*f16(q);
+// online max with double/float compares as in the reference; f16 V
+// accumulator rounded every step (vec_scale_f16 / vec_mad_f16).
+// expf is the device libm's (documented ulp-level difference from glibc).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void attn_exact_kernel(AttnArgs a) {
+  __shared__ float s_prod[256];
+  __shared__ float s_e, s_pe;
+  __shared__ int s_resc;
+  const int t = threadIdx.x, hd = a.head_dim;
+  const int h = blockIdx.x;
+  const int hkv = h / (a.n_head / a.n_head_kv);
+  const int n_keys = *a.d_pos + 1;
+  const float q16 = t < hd ? h2f(f2h_ggml(a.q[(size_t)h * hd + t])) : 0.0f;
+  uint16_t vacc = f2h_ggml(0.0f);
+  float s_acc = 0.0f, max_score = -INFINITY;
+  const uint16_t* kb = a.k_cache + (size_t)hkv * a.max_ctx * hd;
+  const uint16_t* vb = a.v_cache + (size_t)hkv * a.max_ctx * hd;
+  for (int tk = 0; tk < n_keys; tk++) {
+    if (t < hd) s_prod[t] = h2f(kb[(size_t)tk * hd + t]) * q16;
+    __syncthreads();
+    if (t == 0) {
+      double score = 0.0;
+      for (int i = 0; i < hd; i++) score += (double)s_prod[i];
+      const float prev = max_score;
+      float e, pe;
+      int resc;
+      if (score > (double)prev) {
+        max_score = (float)score;
+        e = 1.0f;
+        pe = expf(prev - max_score);
+        resc = 1;
+      } else {
+        e = expf((float)(score - (double)max_score));
+        pe = 1.0f;
+        resc = 0;
+      }
+      s_acc = s_acc * pe + e;
+      s_e = e; s_pe = pe; s_resc = resc;
+    }
+    __syncthreads();
+    if (t < hd) {
+      if (s_resc) vacc = f2h_ggml(h2f(vacc) * s_pe);
+      vacc = f2h_ggml(fmaf(h2f(vb[(size_t)tk * hd + t]), s_e, h2f(vacc)));
+    }
+    __syncthreads();
+  }
+  __shared__ float s_inv;
+  if (t == 0) s_inv = s_acc == 0.0f ? 0.0f : 1.0f / s_acc;
+  __syncthreads();
+  if (t < hd) a.out[(size_t)h * hd + t] = h2f(vacc) * s_inv;
+}
+
+// ---------------------------------------------------------------------------
+// fast split-K attention ("flash-decoding"): grid (n_head, n_split), one wave
+// per block.  Block c walks key tiles c, c+n_split, ... of 64 keys (lane per
+// key for QK^T, lane per head-dim slice for PV), keeping an online-softmax
+// partial (m, l, acc[hd]) in fp32.  attn_combine merges the n_split partials.
+// ---------------------------------------------------------------------------
+template <int HD>
+__global__ __launch_bounds__(64) void attn_partial_kernel(AttnArgs a) {
+  constexpr int DPL = HD / 64;  // head dims per lane in the PV phase
+  __shared__ __attribute__((aligned(16))) uint16_t s_q[HD];
+  __shared__ float s_p[64];
+  const int lane = threadIdx.x;
+  const int h = blockIdx.x, c = blockIdx.y, nsplit = gridDim.y;
+  const int hkv = h / (a.n_head / a.n_head_kv);
+  const int n_keys = *a.d_pos + 1;
+  for (int i = lane; i < HD; i += 64) s_q[i] = f2h_ggml(a.q[(size_t)h * HD + i]);
+  __syncthreads();
+  const uint4* kb = reinterpret_cast<const uint4*>(a.k_cache + (size_t)hkv * a.max_ctx * HD);
+  const uint16_t* vb = a.v_cache + (size_t)hkv * a.max_ctx * HD;
+  float m_run = -INFINITY, l_run = 0.0f;
+  float acc[DPL];
+#pragma unroll
+  for (int d = 0; d < DPL; d++) acc[d] = 0.0f;
+  typedef _Float16 h2t __attribute__((ext_vector_type(2)));
+  for (int tile = c; tile * 64 < n_keys; tile += nsplit) {
+    const int key = tile * 64 + lane;
+    float sc = -INFINITY;
+    if (key < n_keys) {
+      const uint4* kr = kb + (size_t)key * (HD / 8);
+      const uint4* qv = reinterpret_cast<const uint4*>(s_q);
+      float s0 = 0.0f, s1 = 0.0f;
+#pragma unroll 8
+      for (int i = 0; i < HD / 8; i++) {
+        const uint4 kk = kr[i], qq = qv[i];
+        s0 = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2t, kk.x), __builtin_bit_cast(h2t, qq.x), s0, false);
+        s1 = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2t, kk.y), __builtin_bit_cast(h2t, qq.y), s1, false);
+        s0 = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2t, kk.z), __builtin_bit_cast(h2t, qq.z), s0, false);
+        s1 = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2t, kk.w), __builtin_bit_cast(h2t, qq.w), s1, false);
+      }
+      sc = s0 + s1;
+    }
+    const float m_tile = wave_max(sc);
+    const float m_new = fmaxf(m_run, m_tile);
+    const float p = key < n_keys ? expf(sc - m_new) : 0.0f;
+    const float alpha = expf(m_run - m_new);  // m_run = -inf on the first tile -> 0
+    l_run = l_run * alpha + wave_sum(p);
+    m_run = m_new;
+    s_p[lane] = p;
+    __syncthreads();
+    const int nk = min(64, n_keys - tile * 64);
+#pragma unroll
+    for (int d = 0; d < DPL; d++) acc[d] *= alpha;
+    for (int j = 0; j < nk; j++) {
+      const float pj = s_p[j];
+      const uint16_t* vr = vb + (size_t)(tile * 64 + j) * HD + lane * DPL;
+      if (DPL == 4) {
+        const uint2 vv = *reinterpret_cast<const uint2*>(vr);
+        acc[0] = fmaf(pj, h2f((uint16_t)(vv.x & 0xFFFF)), acc[0]);
+        acc[1] = fmaf(pj, h2f((uint16_t)(vv.x >> 16)), acc[1]);
+        acc[DPL > 2 ? 2 : 0] = fmaf(pj, h2f((uint16_t)(vv.y & 0xFFFF)), acc[DPL > 2 ? 2 : 0]);
+        acc[DPL > 3 ? 3 : 0] = fmaf(pj, h2f((uint16_t)(vv.y >> 16)), acc[DPL > 3 ? 3 : 0]);
+      } else {
+#pragma unroll
+        for (int d = 0; d < DPL; d++) acc[d] = fmaf(pj, h2f(vr[d]), acc[d]);
+      }
+    }
+    __syncthreads();
+  }
+  float* part = a.partial + ((size_t)h * nsplit + c) * (HD + 2);
+#pragma unroll
+  for (int d = 0; d < DPL; d++) part[lane * DPL + d] = acc[d];
+  if (lane == 0) { part[HD] = m_run; part[HD + 1] = l_run; }
+}
+
+// merge split partials per head; optionally quantize the head's output to
+// Q8_0 blocks for the O projection (head_dim % 32 == 0).
+__global__ __launch_bounds__(256) void attn_combine_kernel(AttnArgs a, int nsplit, Q8Act q8) {
+  const int h = blockIdx.x, t = threadIdx.x, hd = a.head_dim;
+  const float* part = a.partial + (size_t)h * nsplit * (hd + 2);
+  float M = -INFINITY;
+  for (int c = 0; c < nsplit; c++) M = fmaxf(M, part[(size_t)c * (hd + 2) + hd]);
+  float L = 0.0f, o = 0.0f;
+  for (int c = 0; c < nsplit; c++) {
+    const float* pc = part + (size_t)c * (hd + 2);
+    const float lc = pc[hd + 1];
+    if (lc == 0.0f) continue;
+    const float wc = expf(pc[hd] - M);
+    L = fmaf(lc, wc, L);
+    if (t < hd) o = fmaf(pc[t], wc, o);
+  }
+  const float val = t < hd ? o / L : 0.0f;
+  if (t < hd) a.out[(size_t)h * hd + t] = val;
+  if (q8.qs != nullptr && t < hd) {  // ops.cpp:116-139 per 32-element block
+    float amax = fabsf(val);
+#pragma unroll
+    for (int off = 16; off >= 1; off >>= 1) amax = fmaxf(amax, __shfl_xor(amax, off));
+    const float dd = amax / 127.0f;
+    const float id = dd != 0.0f ? 1.0f / dd : 0.0f;
+    const int q = nearest_int_fma(val, id);
+    int sum = q;
+#pragma unroll
+    for (int off = 16; off >= 1; off >>= 1) sum += __shfl_xor(sum, off);
+    const int gi = h * hd + t;
+    q8.qs[gi] = (int8_t)q;
+    if ((t & 31) == 0) {
+      q8.d[gi >> 5] = f2h_ggml(dd);
+      q8.nsum8[gi >> 5] = -8 * sum;
+    }
+  }
+}
+
+void launch_attention(const AttnArgs& a, bool exact, int nsplit, const Q8Act* q8, hipStream_t s) {
+  if (exact) {
+    hipLaunchKernelGGL(attn_exact_kernel, dim3(a.n_head), dim3(256), 0, s, a);
+    LLMI_HIP(hipGetLastError());
+    return;
+  }
+  const dim3 grid(a.n_head, nsplit);
+  switch (a.head_dim) {
+    case 64: hipLaunchKernelGGL(attn_partial_kernel<64>, grid, dim3(64), 0, s, a); break;
+    case 128: hipLaunchKernelGGL(attn_partial_kernel<128>, grid, dim3(64), 0, s, a); break;
+    case 256: hipLaunchKernelGGL(attn_partial_kernel<256>, grid, dim3(64), 0, s, a); break;
+    default: throw std::runtime_error("attention: unsupported head_dim " + std::to_string(a.head_dim));
+  }
+  LLMI_HIP(hipGetLastError());
+  Q8Act none{};
+  hipLaunchKernelGGL(attn_combine_kernel, dim3(a.n_head), dim3(256), 0, s, a, nsplit, q8 ? *q8 : none);
+  LLMI_HIP(hipGetLastError());
+}
+
+}  // namespace llmi

@@ -1,0 +1,472 @@
+// k_gemv.hip -- quantized / f16 GEMV kernels for gfx950 (MI355X).
+//
+// Two families per weight type:
+//   *_exact : the reference's AVX2 operation order, bit-for-bit
+//             (Q4_0 ops.cpp:364-399, F16 ops.cpp:541-586, Q8_0 ops.cpp:806-824,
+//             Q4_K 643-691, Q6_K 727-770, Q5_0 856-879, BF16 908-917).
+//   *_fast  : HBM-streaming kernels.  One wavefront walks R whole rows as a
+//             flat list of (row, block) items, one 16-B block per lane per
+//             pass (a full 1 KiB coalesced load per wave-instruction against
+//             the repacked SoA layout), integer v_dot4 for Q4_0/Q8_0 blocks,
+//             per-row fp32 partials reduced across the wave at the end.
+#include "kernels.h"
+
+namespace llmi {
+
+__device__ __forceinline__ int nib_lo(uint32_t w) { return (int)(w & 0x0F0F0F0Fu); }
+__device__ __forceinline__ int nib_hi(uint32_t w) { return (int)((w >> 4) & 0x0F0F0F0Fu); }
+
+// ===========================================================================
+// Q4_0 x Q8_0
+// ===========================================================================
+// exact: 8 lanes per row; lane j keeps the reference's AVX2 accumulator j
+// (integer dot of elements 4j..4j+3 of every block, fma over blocks in order),
+// then the hsum_float_8 tree ((a0+a4)+(a2+a6))+((a1+a5)+(a3+a7)).
+__global__ __launch_bounds__(256) void gemv_q4_0_exact(const uint32_t* __restrict__ qs,
+                                                       const uint16_t* __restrict__ wd, int rows, int nb,
+                                                       const int32_t* __restrict__ xqs,
+                                                       const uint16_t* __restrict__ xd, float* __restrict__ out) {
+  const int gl = blockIdx.x * blockDim.x + threadIdx.x;
+  const int row = gl >> 3, j = gl & 7;
+  float acc = 0.0f;
+  if (row < rows) {
+    const uint32_t* q = qs + (size_t)row * nb * 4 + (j & 3);
+    const uint16_t* d = wd + (size_t)row * nb;
+    for (int b = 0; b < nb; b++) {
+      const uint32_t w = q[(size_t)b * 4];
+      const int nib = j < 4 ? nib_lo(w) : nib_hi(w);
+      const int xv = xqs[b * 8 + j];
+      const int isum = sdot4(nib, xv, sdot4((int)0xF8F8F8F8u, xv, 0));  // sum (nib-8)*x
+      const float sc = h2f(d[b]) * h2f(xd[b]);
+      acc = fmaf(sc, (float)isum, acc);
+    }
+  }
+  float t = acc + __shfl_xor(acc, 4);
+  t = t + __shfl_xor(t, 2);
+  t = t + __shfl_xor(t, 1);
+  if (row < rows && j == 0) out[row] = t;
+}
+
+// fast: R rows per wave, flat (row, block) items, 64 items per pass.
+template <int R>
+__global__ __launch_bounds__(256) void gemv_q4_0_fast(const uint4* __restrict__ qs, const uint16_t* __restrict__ wd,
+                                                      int rows, int nb, const int8_t* __restrict__ xqs,
+                                                      const uint16_t* __restrict__ xd,
+                                                      const int32_t* __restrict__ xnsum8, float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * R;
+  if (row0 >= rows) return;
+  const int nrows = min(R, rows - row0);
+  const int total = nrows * nb;
+  const size_t f0 = (size_t)row0 * nb;
+  float acc[R];
+#pragma unroll
+  for (int k = 0; k < R; k++) acc[k] = 0.0f;
+  int r = lane / nb, b = lane - (lane / nb) * nb;
+#pragma unroll 4
+  for (int f = lane; f < total; f += 64) {
+    const uint4 q = ld_nt(qs + f0 + f);
+    const float dw = h2f(__builtin_nontemporal_load(wd + f0 + f));
+    const int4* xp = reinterpret_cast<const int4*>(xqs + b * 32);
+    const int4 x0 = xp[0], x1 = xp[1];
+    int is = xnsum8[b];
+    is = sdot4(nib_lo(q.x), x0.x, is);
+    is = sdot4(nib_lo(q.y), x0.y, is);
+    is = sdot4(nib_lo(q.z), x0.z, is);
+    is = sdot4(nib_lo(q.w), x0.w, is);
+    is = sdot4(nib_hi(q.x), x1.x, is);
+    is = sdot4(nib_hi(q.y), x1.y, is);
+    is = sdot4(nib_hi(q.z), x1.z, is);
+    is = sdot4(nib_hi(q.w), x1.w, is);
+    const float v = (dw * h2f(xd[b])) * (float)is;
+#pragma unroll
+    for (int k = 0; k < R; k++) acc[k] += (k == r) ? v : 0.0f;
+    b += 64;
+    while (b >= nb) { b -= nb; r++; }
+  }
+#pragma unroll
+  for (int k = 0; k < R; k++) {
+    const float sum = wave_sum(acc[k]);
+    if (lane == 0 && k < nrows) out[row0 + k] = sum;
+  }
+}
+
+// ===========================================================================
+// Q8_0 x Q8_0
+// ===========================================================================
+// exact: one thread per row, single fp32 chain (ops.cpp:812-821):
+//   row = fmaf((float)dot * d_w, d_x, row)
+__global__ __launch_bounds__(256) void gemv_q8_0_exact(const int4* __restrict__ qs, const uint16_t* __restrict__ wd,
+                                                       int rows, int nb, const int4* __restrict__ xqs,
+                                                       const uint16_t* __restrict__ xd, float* __restrict__ out) {
+  const int row = blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= rows) return;
+  float sum = 0.0f;
+  for (int b = 0; b < nb; b++) {
+    const int4 w0 = qs[((size_t)row * nb + b) * 2], w1 = qs[((size_t)row * nb + b) * 2 + 1];
+    const int4 x0 = xqs[b * 2], x1 = xqs[b * 2 + 1];
+    int dot = sdot4(w0.x, x0.x, 0);
+    dot = sdot4(w0.y, x0.y, dot); dot = sdot4(w0.z, x0.z, dot); dot = sdot4(w0.w, x0.w, dot);
+    dot = sdot4(w1.x, x1.x, dot); dot = sdot4(w1.y, x1.y, dot); dot = sdot4(w1.z, x1.z, dot);
+    dot = sdot4(w1.w, x1.w, dot);
+    sum = fmaf((float)dot * h2f(wd[(size_t)row * nb + b]), h2f(xd[b]), sum);
+  }
+  out[row] = sum;
+}
+
+template <int R>
+__global__ __launch_bounds__(256) void gemv_q8_0_fast(const int4* __restrict__ qs, const uint16_t* __restrict__ wd,
+                                                      int rows, int nb, const int4* __restrict__ xqs,
+                                                      const uint16_t* __restrict__ xd, float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * R;
+  if (row0 >= rows) return;
+  const int nrows = min(R, rows - row0);
+  const int total = nrows * nb;
+  const size_t f0 = (size_t)row0 * nb;
+  float acc[R];
+#pragma unroll
+  for (int k = 0; k < R; k++) acc[k] = 0.0f;
+  int r = lane / nb, b = lane - (lane / nb) * nb;
+#pragma unroll 2
+  for (int f = lane; f < total; f += 64) {
+    const int4 w0 = ld_nt(qs + (f0 + f) * 2);
+    const int4 w1 = ld_nt(qs + (f0 + f) * 2 + 1);
+    const int4 x0 = xqs[b * 2], x1 = xqs[b * 2 + 1];
+    int dot = sdot4(w0.x, x0.x, 0);
+    dot = sdot4(w0.y, x0.y, dot); dot = sdot4(w0.z, x0.z, dot); dot = sdot4(w0.w, x0.w, dot);
+    dot = sdot4(w1.x, x1.x, dot); dot = sdot4(w1.y, x1.y, dot); dot = sdot4(w1.z, x1.z, dot);
+    dot = sdot4(w1.w, x1.w, dot);
+    const float v = (h2f(wd[f0 + f]) * h2f(xd[b])) * (float)dot;
+#pragma unroll
+    for (int k = 0; k < R; k++) acc[k] += (k == r) ? v : 0.0f;
+    b += 64;
+    while (b >= nb) { b -= nb; r++; }
+  }
+#pragma unroll
+  for (int k = 0; k < R; k++) {
+    const float sum = wave_sum(acc[k]);
+    if (lane == 0 && k < nrows) out[row0 + k] = sum;
+  }
+}
+
+// ===========================================================================
+// F16 (logits)
+// ===========================================================================
+typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ half2_t as_h2(uint32_t v) { return __builtin_bit_cast(half2_t, v); }
+
+// exact: 4 lanes per row (lane l = AVX2 accumulator register sum[l], 8 fp32
+// lanes m each), chunk loop in order, then (S0+S1)+(S2+S3), t_m = V_m+V_m+4,
+// (t0+t1)+(t2+t3), then the serial scalar tail (ops.cpp:557-583).
+__global__ __launch_bounds__(256) void gemv_f16_exact(const uint4* __restrict__ w, int rows, int cols,
+                                                      const uint16_t* __restrict__ x16, float* __restrict__ out) {
+  const int gl = blockIdx.x * blockDim.x + threadIdx.x;
+  const int row = gl >> 2, l = gl & 3;
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int np = cols & ~31;
+  if (row < rows) {
+    const uint16_t* wr = reinterpret_cast<const uint16_t*>(w) + (size_t)row * cols;
+    for (int k = 0; k < np; k += 32) {
+      uint16_t wv[8], xv[8];
+      if ((cols & 7) == 0) {
+        *reinterpret_cast<uint4*>(wv) = *reinterpret_cast<const uint4*>(wr + k + 8 * l);
+        *reinterpret_cast<uint4*>(xv) = *reinterpret_cast<const uint4*>(x16 + k + 8 * l);
+      } else {
+#pragma unroll
+        for (int m = 0; m < 8; m++) { wv[m] = wr[k + 8 * l + m]; xv[m] = x16[k + 8 * l + m]; }
+      }
+#pragma unroll
+      for (int m = 0; m < 8; m++) s[m] = fmaf(h2f(wv[m]), h2f(xv[m]), s[m]);
+    }
+  }
+  float v[8];
+#pragma unroll
+  for (int m = 0; m < 8; m++) {
+    const float a = s[m] + __shfl_xor(s[m], 1);  // l0: S0+S1, l2: S2+S3
+    v[m] = a + __shfl_xor(a, 2);                 // l0: (S0+S1)+(S2+S3)
+  }
+  if (row < rows && l == 0) {
+    const float t0 = v[0] + v[4], t1 = v[1] + v[5], t2 = v[2] + v[6], t3 = v[3] + v[7];
+    float r = (t0 + t1) + (t2 + t3);
+    const uint16_t* wr = reinterpret_cast<const uint16_t*>(w) + (size_t)row * cols;
+    for (int k = np; k < cols; k++) r = fmaf(h2f(wr[k]), h2f(x16[k]), r);
+    out[row] = r;
+  }
+}
+
+__device__ __forceinline__ float dot8_f16(uint4 w, uint4 x, float acc) {
+  acc = __builtin_amdgcn_fdot2(as_h2(w.x), as_h2(x.x), acc, false);
+  acc = __builtin_amdgcn_fdot2(as_h2(w.y), as_h2(x.y), acc, false);
+  acc = __builtin_amdgcn_fdot2(as_h2(w.z), as_h2(x.z), acc, false);
+  acc = __builtin_amdgcn_fdot2(as_h2(w.w), as_h2(x.w), acc, false);
+  return acc;
+}
+
+// fast, cols % 512 == 0 (P = cols/512 passes per row): x chunks held in
+// registers for the whole kernel, grid-stride over rows, argmax folded in.
+template <int P>
+__global__ __launch_bounds__(256) void gemv_f16_fast_rows(const uint4* __restrict__ w, int rows,
+                                                          const uint4* __restrict__ x16, float* __restrict__ out,
+                                                          unsigned long long* __restrict__ amax_key) {
+  const int lane = threadIdx.x & 63;
+  const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int nwaves = gridDim.x * 4;
+  uint4 xr[P];
+#pragma unroll
+  for (int p = 0; p < P; p++) xr[p] = x16[p * 64 + lane];
+  float best = -INFINITY;
+  int best_i = 0x7fffffff;
+  for (int row = wave; row < rows; row += nwaves) {
+    const uint4* wr = w + (size_t)row * (P * 64);
+    uint4 wv[P];
+#pragma unroll
+    for (int p = 0; p < P; p++) wv[p] = ld_nt(wr + p * 64 + lane);
+    float acc = 0.0f;
+#pragma unroll
+    for (int p = 0; p < P; p++) acc = dot8_f16(wv[p], xr[p], acc);
+    acc = wave_sum(acc);
+    if (lane == 0) {
+      out[row] = acc;
+      if (acc > best) { best = acc; best_i = row; }
+    }
+  }
+  if (amax_key != nullptr && lane == 0 && best_i != 0x7fffffff) atomicMax(amax_key, argmax_key(best, best_i));
+}
+
+// fast, general cols (cols % 8 == 0): flat (row, chunk) items like Q4_0.
+template <int R>
+__global__ __launch_bounds__(256) void gemv_f16_fast(const uint4* __restrict__ w, int rows, int nc,
+                                                     const uint4* __restrict__ x16, float* __restrict__ out,
+                                                     unsigned long long* __restrict__ amax_key) {
+  const int lane = threadIdx.x & 63;
+  const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * R;
+  if (row0 >= rows) return;
+  const int nrows = min(R, rows - row0);
+  const int total = nrows * nc;
+  const size_t f0 = (size_t)row0 * nc;
+  float acc[R];
+#pragma unroll
+  for (int k = 0; k < R; k++) acc[k] = 0.0f;
+  int r = lane / nc, c = lane - (lane / nc) * nc;
+#pragma unroll 4
+  for (int f = lane; f < total; f += 64) {
+    const float v = dot8_f16(ld_nt(w + f0 + f), x16[c], 0.0f);
+#pragma unroll
+    for (int k = 0; k < R; k++) acc[k] += (k == r) ? v : 0.0f;
+    c += 64;
+    while (c >= nc) { c -= nc; r++; }
+  }
+  float best = -INFINITY;
+  int best_i = 0x7fffffff;
+#pragma unroll
+  for (int k = 0; k < R; k++) {
+    const float sum = wave_sum(acc[k]);
+    if (lane == 0 && k < nrows) {
+      out[row0 + k] = sum;
+      if (sum > best) { best = sum; best_i = row0 + k; }
+    }
+  }
+  if (amax_key != nullptr && lane == 0 && best_i != 0x7fffffff) atomicMax(amax_key, argmax_key(best, best_i));
+}
+
+// ===========================================================================
+// K-quants, Q5_0, BF16: exact single-chain kernels (one thread per row)
+// ===========================================================================
+__device__ __forceinline__ uint16_t ld16(const uint8_t* p) { return (uint16_t)p[0] | ((uint16_t)p[1] << 8); }
+__device__ __forceinline__ void scale_min_k4(int j, const uint8_t* q, int& d, int& m) {  // ops.cpp:633-641
+  if (j < 4) { d = q[j] & 63; m = q[j + 4] & 63; }
+  else { d = (q[j + 4] & 0xF) | ((q[j - 4] >> 6) << 4); m = (q[j + 4] >> 4) | ((q[j - 0] >> 6) << 4); }
+}
+
+__global__ __launch_bounds__(256) void gemv_q4_k_exact(const uint8_t* __restrict__ wq, int rows, int nb,
+                                                       const uint8_t* __restrict__ xk, float* __restrict__ out) {
+  const int row = blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= rows) return;
+  float sum = 0.0f;
+  for (int b = 0; b < nb; b++) {
+    const uint8_t* blk = wq + ((size_t)row * nb + b) * 144;
+    const uint8_t* xb = xk + (size_t)b * 292;
+    const float xdv = *reinterpret_cast<const float*>(xb);
+    const float d = h2f(ld16(blk)) * xdv;
+    const float mn = h2f(ld16(blk + 2)) * xdv;
+    const uint8_t* q4 = blk + 16;
+    const int8_t* q8 = reinterpret_cast<const int8_t*>(xb + 4);
+    const int16_t* bs = reinterpret_cast<const int16_t*>(xb + 260);
+    int is = 0;
+    for (int j = 0; j < 256; j += 64) {
+      int s, m;
+      scale_min_k4(is, blk + 4, s, m);
+      float d1 = d * (float)s, m1 = mn * (float)m;
+      int a = 0;
+      for (int l = 0; l < 32; ++l) a += (q4[l] & 0xF) * q8[l];
+      sum = sum + fmaf((float)a, d1, -(m1 * (float)(bs[is * 2] + bs[is * 2 + 1])));
+      scale_min_k4(is + 1, blk + 4, s, m);
+      d1 = d * (float)s; m1 = mn * (float)m;
+      a = 0;
+      for (int l = 0; l < 32; ++l) a += (q4[l] >> 4) * q8[l + 32];
+      sum = sum + fmaf((float)a, d1, -(m1 * (float)(bs[(is + 1) * 2] + bs[(is + 1) * 2 + 1])));
+      q4 += 32; q8 += 64; is += 2;
+    }
+  }
+  out[row] = sum;
+}
+
+__global__ __launch_bounds__(256) void gemv_q6_k_exact(const uint8_t* __restrict__ wq, int rows, int nb,
+                                                       const uint8_t* __restrict__ xk, float* __restrict__ out) {
+  const int row = blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= rows) return;
+  float sum = 0.0f;
+  for (int b = 0; b < nb; b++) {
+    const uint8_t* blk = wq + ((size_t)row * nb + b) * 210;
+    const uint8_t* xb = xk + (size_t)b * 292;
+    const float d = h2f(ld16(blk + 208)) * *reinterpret_cast<const float*>(xb);
+    const uint8_t* ql = blk;
+    const uint8_t* qh = blk + 128;
+    const int8_t* sc = reinterpret_cast<const int8_t*>(blk + 192);
+    const int8_t* xq = reinterpret_cast<const int8_t*>(xb + 4);
+    for (int n = 0; n < 256; n += 128) {
+      int part = 0;
+      for (int l = 0; l < 32; ++l) {
+        const int is = l / 16;
+        const int q1 = (int8_t)((ql[l + 0] & 0xF) | (((qh[l] >> 0) & 3) << 4)) - 32;
+        const int q2 = (int8_t)((ql[l + 32] & 0xF) | (((qh[l] >> 2) & 3) << 4)) - 32;
+        const int q3 = (int8_t)((ql[l + 0] >> 4) | (((qh[l] >> 4) & 3) << 4)) - 32;
+        const int q4 = (int8_t)((ql[l + 32] >> 4) | (((qh[l] >> 6) & 3) << 4)) - 32;
+        part += sc[is + 0] * q1 * xq[l + 0];
+        part += sc[is + 2] * q2 * xq[l + 32];
+        part += sc[is + 4] * q3 * xq[l + 64];
+        part += sc[is + 6] * q4 * xq[l + 96];
+      }
+      sum = fmaf((float)part, d, sum);
+      ql += 64; qh += 32; sc += 8; xq += 128;
+    }
+  }
+  out[row] = sum;
+}
+
+__global__ __launch_bounds__(256) void gemv_q5_0_exact(const uint8_t* __restrict__ wq, int rows, int nb,
+                                                       const float* __restrict__ x, float* __restrict__ out) {
+  const int row = blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= rows) return;
+  float sum = 0.0f;
+  for (int b = 0; b < nb; b++) {
+    const uint8_t* blk = wq + ((size_t)row * nb + b) * 22;
+    const float d = h2f(ld16(blk));
+    const uint32_t qh = (uint32_t)blk[2] | ((uint32_t)blk[3] << 8) | ((uint32_t)blk[4] << 16) | ((uint32_t)blk[5] << 24);
+    for (int i = 0; i < 16; ++i) {
+      const uint8_t ql = blk[6 + i];
+      const int q0 = (ql & 0x0F) | (((qh >> (i + 0)) & 1) << 4);
+      const int q1 = (ql >> 4) | (((qh >> (i + 16)) & 1) << 4);
+      sum = fmaf(d * (float)(q0 - 16), x[b * 32 + i], sum);
+      sum = fmaf(d * (float)(q1 - 16), x[b * 32 + i + 16], sum);
+    }
+  }
+  out[row] = sum;
+}
+
+__global__ __launch_bounds__(256) void gemv_bf16_exact(const uint16_t* __restrict__ w, int rows, int cols,
+                                                       const float* __restrict__ x, float* __restrict__ out) {
+  const int row = blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= rows) return;
+  float sum = 0.0f;
+  const uint16_t* wr = w + (size_t)row * cols;
+  for (int c = 0; c < cols; c++) sum = fmaf(__uint_as_float((uint32_t)wr[c] << 16), x[c], sum);
+  out[row] = sum;
+}
+
+// ===========================================================================
+// launcher
+// ===========================================================================
+static int rows_per_wave(int items_per_row) {
+  // smallest R in {1,2,4,8} with R*items a multiple of 64 (full passes),
+  // capped at 8 (then the last pass is partially masked)
+  int R = 1;
+  while (R < 8 && (R * items_per_row) % 64 != 0) R *= 2;
+  return R;
+}
+
+#define LLMI_DISPATCH_R(R, KERNEL, GRID, ...)                                              \
+  switch (R) {                                                                               \
+    case 1: hipLaunchKernelGGL(KERNEL<1>, GRID, dim3(256), 0, s, __VA_ARGS__); break;        \
+    case 2: hipLaunchKernelGGL(KERNEL<2>, GRID, dim3(256), 0, s, __VA_ARGS__); break;        \
+    case 4: hipLaunchKernelGGL(KERNEL<4>, GRID, dim3(256), 0, s, __VA_ARGS__); break;        \
+    default: hipLaunchKernelGGL(KERNEL<8>, GRID, dim3(256), 0, s, __VA_ARGS__); break;       \
+  }
+
+void launch_gemv(const DevWeight& w, const ActBuf& x, float* o, GemvMode mode, hipStream_t s,
+                 unsigned long long* amax_key) {
+  const int rows = w.rows;
+  if (rows == 0) return;
+  switch (w.type) {
+    case T_Q4_0: {
+      const int nb = w.cols / 32;
+      if (mode == GEMV_EXACT) {
+        hipLaunchKernelGGL(gemv_q4_0_exact, dim3((rows * 8 + 255) / 256), dim3(256), 0, s,
+                           (const uint32_t*)w.qs, w.d, rows, nb, (const int32_t*)x.q8.qs, x.q8.d, o);
+      } else {
+        const int R = rows_per_wave(nb);
+        const dim3 grid((rows + 4 * R - 1) / (4 * R));
+        LLMI_DISPATCH_R(R, gemv_q4_0_fast, grid, (const uint4*)w.qs, w.d, rows, nb, x.q8.qs, x.q8.d, x.q8.nsum8, o);
+      }
+      break;
+    }
+    case T_Q8_0: {
+      const int nb = w.cols / 32;
+      if (mode == GEMV_EXACT) {
+        hipLaunchKernelGGL(gemv_q8_0_exact, dim3((rows + 255) / 256), dim3(256), 0, s, (const int4*)w.qs, w.d, rows,
+                           nb, (const int4*)x.q8.qs, x.q8.d, o);
+      } else {
+        const int R = rows_per_wave(nb);
+        const dim3 grid((rows + 4 * R - 1) / (4 * R));
+        LLMI_DISPATCH_R(R, gemv_q8_0_fast, grid, (const int4*)w.qs, w.d, rows, nb, (const int4*)x.q8.qs, x.q8.d, o);
+      }
+      break;
+    }
+    case T_F16: {
+      if (mode == GEMV_EXACT || (w.cols % 8) != 0) {
+        hipLaunchKernelGGL(gemv_f16_exact, dim3((rows * 4 + 255) / 256), dim3(256), 0, s, (const uint4*)w.qs, rows,
+                           w.cols, x.x16, o);
+        // argmax for the exact path is taken by the caller from the logits
+      } else if (w.cols % 512 == 0 && w.cols / 512 <= 12) {
+        const int P = w.cols / 512;
+        const int waves = std::min(rows, 256 * 32);
+        const dim3 grid((waves + 3) / 4);
+        switch (P) {
+#define LLMI_F16P(N) \
+  case N: hipLaunchKernelGGL(gemv_f16_fast_rows<N>, grid, dim3(256), 0, s, (const uint4*)w.qs, rows, (const uint4*)x.x16, o, amax_key); break;
+          LLMI_F16P(1) LLMI_F16P(2) LLMI_F16P(3) LLMI_F16P(4) LLMI_F16P(5) LLMI_F16P(6)
+          LLMI_F16P(7) LLMI_F16P(8) LLMI_F16P(9) LLMI_F16P(10) LLMI_F16P(11) LLMI_F16P(12)
+#undef LLMI_F16P
+        }
+      } else {
+        const int nc = w.cols / 8;
+        const int R = rows_per_wave(nc);
+        const dim3 grid((rows + 4 * R - 1) / (4 * R));
+        LLMI_DISPATCH_R(R, gemv_f16_fast, grid, (const uint4*)w.qs, rows, nc, (const uint4*)x.x16, o, amax_key);
+      }
+      break;
+    }
+    case T_Q4_K:
+      hipLaunchKernelGGL(gemv_q4_k_exact, dim3((rows + 255) / 256), dim3(256), 0, s, (const uint8_t*)w.qs, rows,
+                         w.cols / 256, x.q8k, o);
+      break;
+    case T_Q6_K:
+      hipLaunchKernelGGL(gemv_q6_k_exact, dim3((rows + 255) / 256), dim3(256), 0, s, (const uint8_t*)w.qs, rows,
+                         w.cols / 256, x.q8k, o);
+      break;
+    case T_Q5_0:
+      hipLaunchKernelGGL(gemv_q5_0_exact, dim3((rows + 255) / 256), dim3(256), 0, s, (const uint8_t*)w.qs, rows,
+                         w.cols / 32, x.xf, o);
+      break;
+    case T_BF16:
+      hipLaunchKernelGGL(gemv_bf16_exact, dim3((rows + 255) / 256), dim3(256), 0, s, (const uint16_t*)w.qs, rows,
+                         w.cols, x.xf, o);
+      break;
+    default:
+      throw std::runtime_error("mat_vec_mul: unsupported tensor type " + std::to_string(w.type));
+  }
+  LLMI_HIP(hipGetLastError());
+}
+
+}  // namespace llmi

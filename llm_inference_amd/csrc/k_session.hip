@@ -1,0 +1,340 @@
+// k_session.hip -- weight upload/repack and the fused glue kernels of the
+// decode step (residual + norms, GELU + quantize, argmax, token feedback).
+#include "session_kernels.h"
+
+namespace llmi {
+
+// ---------------------------------------------------------------------------
+// weight upload: GGUF blocks -> device SoA layout (kernels.h)
+// ---------------------------------------------------------------------------
+__global__ void repack_q4_0_kernel(const uint8_t* __restrict__ src, size_t n_blocks, uint4* __restrict__ qs,
+                                   uint16_t* __restrict__ d) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_blocks) return;
+  const uint8_t* b = src + i * 18;
+  d[i] = (uint16_t)(b[0] | (b[1] << 8));
+  uint32_t w[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+    w[k] = (uint32_t)b[2 + 4 * k] | ((uint32_t)b[3 + 4 * k] << 8) | ((uint32_t)b[4 + 4 * k] << 16) |
+           ((uint32_t)b[5 + 4 * k] << 24);
+  qs[i] = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+__global__ void repack_q8_0_kernel(const uint8_t* __restrict__ src, size_t n_blocks, uint4* __restrict__ qs,
+                                   uint16_t* __restrict__ d) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_blocks) return;
+  const uint8_t* b = src + i * 34;
+  d[i] = (uint16_t)(b[0] | (b[1] << 8));
+  uint32_t w[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++)
+    w[k] = (uint32_t)b[2 + 4 * k] | ((uint32_t)b[3 + 4 * k] << 8) | ((uint32_t)b[4 + 4 * k] << 16) |
+           ((uint32_t)b[5 + 4 * k] << 24);
+  qs[2 * i] = make_uint4(w[0], w[1], w[2], w[3]);
+  qs[2 * i + 1] = make_uint4(w[4], w[5], w[6], w[7]);
+}
+
+size_t gguf_bytes(uint32_t type, size_t rows, size_t cols) {
+  switch (type) {
+    case T_F32: return rows * cols * 4;
+    case T_F16: case T_BF16: return rows * cols * 2;
+    case T_Q4_0: return rows * (cols / 32) * 18;
+    case T_Q5_0: return rows * (cols / 32) * 22;
+    case T_Q8_0: return rows * (cols / 32) * 34;
+    case T_Q4_K: return rows * (cols / 256) * 144;
+    case T_Q6_K: return rows * (cols / 256) * 210;
+    default: return 0;
+  }
+}
+
+bool gemv_type_supported(uint32_t type) {
+  return type == T_Q4_0 || type == T_Q8_0 || type == T_F16 || type == T_Q4_K || type == T_Q6_K || type == T_Q5_0 ||
+         type == T_BF16;
+}
+
+// Upload `rows` rows of a GGUF weight (host bytes in block layout) to the
+// device, appending after `dst_row0` rows of an existing allocation `w`
+// (used to fuse q|k|v and gate|up into one GEMV).  w must be pre-allocated.
+void upload_rows(DevWeight& w, int dst_row0, const void* host, int rows, hipStream_t s) {
+  const size_t bytes = gguf_bytes(w.type, rows, w.cols);
+  if (w.type == T_Q4_0 || w.type == T_Q8_0) {
+    const int nb = w.cols / 32;
+    const size_t nblk = (size_t)rows * nb;
+    void* tmp = nullptr;
+    LLMI_HIP(hipMalloc(&tmp, bytes));
+    LLMI_HIP(hipMemcpyAsync(tmp, host, bytes, hipMemcpyHostToDevice, s));
+    const size_t b0 = (size_t)dst_row0 * nb;
+    if (w.type == T_Q4_0)
+      hipLaunchKernelGGL(repack_q4_0_kernel, dim3((nblk + 255) / 256), dim3(256), 0, s, (const uint8_t*)tmp, nblk,
+                         (uint4*)w.qs + b0, w.d + b0);
+    else
+      hipLaunchKernelGGL(repack_q8_0_kernel, dim3((nblk + 255) / 256), dim3(256), 0, s, (const uint8_t*)tmp, nblk,
+                         (uint4*)w.qs + 2 * b0, w.d + b0);
+    LLMI_HIP(hipGetLastError());
+    LLMI_HIP(hipStreamSynchronize(s));
+    LLMI_HIP(hipFree(tmp));
+  } else {
+    const size_t off = gguf_bytes(w.type, dst_row0, w.cols);
+    LLMI_HIP(hipMemcpyAsync((uint8_t*)w.qs + off, host, bytes, hipMemcpyHostToDevice, s));
+    LLMI_HIP(hipStreamSynchronize(s));
+  }
+}
+
+DevWeight alloc_weight(uint32_t type, int rows, int cols) {
+  if (!gemv_type_supported(type))
+    throw std::runtime_error("mat_vec_mul: unsupported tensor type " + std::to_string(type));
+  DevWeight w;
+  w.type = type;
+  w.rows = rows;
+  w.cols = cols;
+  w.bytes = gguf_bytes(type, rows, cols);
+  if (type == T_Q4_0 || type == T_Q8_0) {
+    const size_t nblk = (size_t)rows * (cols / 32);
+    LLMI_HIP(hipMalloc(&w.qs, nblk * (type == T_Q4_0 ? 16 : 32) + 64));
+    LLMI_HIP(hipMalloc((void**)&w.d, nblk * 2 + 64));
+  } else {
+    LLMI_HIP(hipMalloc(&w.qs, w.bytes + 64));
+  }
+  return w;
+}
+
+void free_weight(DevWeight& w) {
+  if (w.qs) (void)hipFree(w.qs);
+  if (w.d) (void)hipFree(w.d);
+  w.qs = nullptr;
+  w.d = nullptr;
+}
+
+// ---------------------------------------------------------------------------
+// block-wide sum helper (<= 1024 threads), fixed order
+// ---------------------------------------------------------------------------
+__device__ float block_sum(float v, float* sh) {
+  const int t = threadIdx.x, nw = blockDim.x >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if ((t & 63) == 0) sh[t >> 6] = v;
+  __syncthreads();
+  float tot = 0.0f;
+  for (int i = 0; i < nw; i++) tot += sh[i];
+  return tot;
+}
+
+// serial (reference-order) sum of squares: sum = fma(v, v, sum) in index order
+__device__ float serial_sumsq(const float* x, int n, float* sh) {
+  __shared__ float s_r;
+  if (threadIdx.x == 0) {
+    float sum = 0.0f;
+    for (int i = 0; i < n; i++) sum = fmaf(x[i], x[i], sum);
+    s_r = sum;
+  }
+  __syncthreads();
+  const float r = s_r;
+  __syncthreads();
+  (void)sh;
+  return r;
+}
+
+__device__ __forceinline__ float rms_scale(float sum, int n, double eps) {  // ops.cpp:37-38
+  return 1.0f / sqrtf((float)((double)(sum / (float)n) + eps));
+}
+
+// ---------------------------------------------------------------------------
+// Fused residual step (model.cpp:843-858 / 915-924 + next run_norm):
+//   a = rms_norm(y) * w_post             (post_attention / post_ffw norm)
+//   h = resid + a ; resid = h            (residual add)
+//   xn = rms_norm(h) * w_next            (ffn_norm / next layer attn_norm /
+//                                         output_norm)
+// One block of 1024 threads; values staged in LDS (n <= 8192).
+// ---------------------------------------------------------------------------
+template <bool EXACT>
+__global__ __launch_bounds__(1024) void residual_norm_kernel(const float* __restrict__ y,
+                                                             const float* __restrict__ w_post,
+                                                             float* __restrict__ resid,
+                                                             const float* __restrict__ w_next,
+                                                             float* __restrict__ xn, int n, double eps) {
+  extern __shared__ float s_h[];
+  __shared__ float sh[16];
+  const int t = threadIdx.x;
+  float sq = 0.0f;
+  // pass 1: y -> LDS, sum of squares
+  for (int i = t; i < n; i += blockDim.x) {
+    const float v = y[i];
+    s_h[i] = v;
+    sq = fmaf(v, v, sq);
+  }
+  __syncthreads();
+  const float s1 = EXACT ? serial_sumsq(s_h, n, sh) : block_sum(sq, sh);
+  const float sc1 = rms_scale(s1, n, eps);
+  float sq2 = 0.0f;
+  for (int i = t; i < n; i += blockDim.x) {
+    const float a = w_post ? (sc1 * s_h[i]) * w_post[i] : s_h[i];
+    const float h = resid[i] + a;
+    resid[i] = h;
+    s_h[i] = h;
+    sq2 = fmaf(h, h, sq2);
+  }
+  __syncthreads();
+  const float s2 = EXACT ? serial_sumsq(s_h, n, sh) : block_sum(sq2, sh);
+  const float sc2 = rms_scale(s2, n, eps);
+  for (int i = t; i < n; i += blockDim.x) xn[i] = (sc2 * s_h[i]) * w_next[i];
+}
+
+void launch_residual_norm(const float* y, const float* w_post, float* resid, const float* w_next, float* xn, int n,
+                          double eps, bool exact, hipStream_t s) {
+  const size_t lds = (size_t)n * 4;
+  if (exact)
+    hipLaunchKernelGGL(residual_norm_kernel<true>, dim3(1), dim3(1024), lds, s, y, w_post, resid, w_next, xn, n, eps);
+  else
+    hipLaunchKernelGGL(residual_norm_kernel<false>, dim3(1), dim3(1024), lds, s, y, w_post, resid, w_next, xn, n, eps);
+  LLMI_HIP(hipGetLastError());
+}
+
+// embedding row * sqrt(n_embd) (model.cpp:240-344) + first attn_norm
+template <bool EXACT>
+__global__ __launch_bounds__(1024) void embed_norm_kernel(uint32_t type, const uint8_t* __restrict__ table,
+                                                          size_t row_bytes, const int32_t* __restrict__ d_token,
+                                                          float emb_scale, float* __restrict__ resid,
+                                                          const float* __restrict__ w, float* __restrict__ xn, int n,
+                                                          double eps);
+
+// ---------------------------------------------------------------------------
+// GELU(tanh)(gate) * up (model.cpp:892-899) fused with quantize_row_q8_0 of the
+// result (ops.cpp:116-139) for the down projection: one 32-lane half-wave per
+// Q8_0 block.  Also writes the f32 hidden vector (parity/debug).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float gelu_mul1(float x, float u) {
+  const float c = __uint_as_float(0x3F4C4229u);  // sqrtf((float)(2.0 / M_PI))
+  const float inner = x + ((0.044715f * x) * x) * x;
+  return ((0.5f * x) * (1.0f + tanhf(c * inner))) * u;
+}
+
+__global__ __launch_bounds__(256) void gelu_quant_kernel(const float* __restrict__ gu, int n, float* __restrict__ hid,
+                                                         int8_t* __restrict__ qs, uint16_t* __restrict__ d,
+                                                         int32_t* __restrict__ nsum8) {
+  const int gl = blockIdx.x * blockDim.x + threadIdx.x;
+  const int blk = gl >> 5, e = gl & 31;
+  const bool ok = gl < n;
+  const float v = ok ? gelu_mul1(gu[gl], gu[n + gl]) : 0.0f;
+  if (ok) hid[gl] = v;
+  if (qs == nullptr) return;
+  float amax = fabsf(v);
+#pragma unroll
+  for (int o = 16; o >= 1; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o));
+  const float dd = amax / 127.0f;
+  const float id = dd != 0.0f ? 1.0f / dd : 0.0f;
+  const int q = nearest_int_fma(v, id);
+  int sm = q;
+#pragma unroll
+  for (int o = 16; o >= 1; o >>= 1) sm += __shfl_xor(sm, o);
+  if (ok) {
+    qs[gl] = (int8_t)q;
+    if (e == 0) {
+      d[blk] = f2h_ggml(dd);
+      nsum8[blk] = -8 * sm;
+    }
+  }
+}
+
+void launch_gelu_quant(const float* gu, int n, float* hid, const Q8Act* q8, hipStream_t s) {
+  hipLaunchKernelGGL(gelu_quant_kernel, dim3((n + 255) / 256), dim3(256), 0, s, gu, n, hid, q8 ? q8->qs : nullptr,
+                     q8 ? q8->d : nullptr, q8 ? q8->nsum8 : nullptr);
+  LLMI_HIP(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------
+// argmax (first maximal index, main.cpp:193-194) folded into a 64-bit key
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void argmax_kernel(const float* __restrict__ x, int n,
+                                                      unsigned long long* __restrict__ key) {
+  unsigned long long best = 0;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const unsigned long long k = argmax_key(x[i], (uint32_t)i);
+    best = k > best ? k : best;
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const unsigned long long other = __shfl_xor(best, o);
+    best = other > best ? other : best;
+  }
+  if ((threadIdx.x & 63) == 0) atomicMax(key, best);
+}
+
+void launch_argmax(const float* x, int n, unsigned long long* key, hipStream_t s) {
+  hipLaunchKernelGGL(argmax_kernel, dim3(64), dim3(1024), 0, s, x, n, key);
+  LLMI_HIP(hipGetLastError());
+}
+
+// token feedback: next token = argmax, pos += 1, record, reset key
+__global__ void finalize_token_kernel(unsigned long long* key, int32_t* d_token, int32_t* d_pos, int32_t* ring,
+                                      int32_t* ring_idx, int ring_cap) {
+  const uint32_t tok = argmax_key_index(*key);
+  *key = 0;
+  *d_token = (int32_t)tok;
+  *d_pos = *d_pos + 1;
+  const int i = *ring_idx;
+  if (i < ring_cap) ring[i] = (int32_t)tok;
+  *ring_idx = i + 1;
+}
+
+void launch_finalize_token(unsigned long long* key, int32_t* d_token, int32_t* d_pos, int32_t* ring,
+                           int32_t* ring_idx, int ring_cap, hipStream_t s) {
+  hipLaunchKernelGGL(finalize_token_kernel, dim3(1), dim3(1), 0, s, key, d_token, d_pos, ring, ring_idx, ring_cap);
+  LLMI_HIP(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------
+// embedding lookup + scale + first attn_norm, in one block
+// ---------------------------------------------------------------------------
+__device__ float deq_embed(uint32_t type, const uint8_t* row, int i);
+
+template <bool EXACT>
+__global__ __launch_bounds__(1024) void embed_norm_kernel(uint32_t type, const uint8_t* __restrict__ table,
+                                                          size_t row_bytes, const int32_t* __restrict__ d_token,
+                                                          float emb_scale, float* __restrict__ resid,
+                                                          const float* __restrict__ w, float* __restrict__ xn, int n,
+                                                          double eps) {
+  extern __shared__ float s_h[];
+  __shared__ float sh[16];
+  const int t = threadIdx.x;
+  const uint8_t* row = table + (size_t)(*d_token) * row_bytes;
+  float sq = 0.0f;
+  for (int i = t; i < n; i += blockDim.x) {
+    const float v = deq_embed(type, row, i) * emb_scale;
+    resid[i] = v;
+    s_h[i] = v;
+    sq = fmaf(v, v, sq);
+  }
+  __syncthreads();
+  const float s1 = EXACT ? serial_sumsq(s_h, n, sh) : block_sum(sq, sh);
+  const float sc = rms_scale(s1, n, eps);
+  for (int i = t; i < n; i += blockDim.x) xn[i] = (sc * s_h[i]) * w[i];
+}
+
+__device__ float deq_embed(uint32_t type, const uint8_t* row, int i) {
+  switch (type) {
+    case T_F16: return h2f(reinterpret_cast<const uint16_t*>(row)[i]);
+    case T_F32: return reinterpret_cast<const float*>(row)[i];
+    case T_Q8_0: {
+      const uint8_t* b = row + (i / 32) * 34;
+      return h2f((uint16_t)(b[0] | (b[1] << 8))) * (float)(int8_t)b[2 + (i & 31)];
+    }
+    default: return 0.0f;  // Q6_K/Q4_K/Q5_0 tables use launch_dequantize_rows + rms_norm
+  }
+}
+
+void launch_embed_norm(uint32_t type, const uint8_t* table, size_t row_bytes, const int32_t* d_token,
+                       float emb_scale, float* resid, const float* w, float* xn, int n, double eps, bool exact,
+                       hipStream_t s) {
+  const size_t lds = (size_t)n * 4;
+  if (exact)
+    hipLaunchKernelGGL(embed_norm_kernel<true>, dim3(1), dim3(1024), lds, s, type, table, row_bytes, d_token,
+                       emb_scale, resid, w, xn, n, eps);
+  else
+    hipLaunchKernelGGL(embed_norm_kernel<false>, dim3(1), dim3(1024), lds, s, type, table, row_bytes, d_token,
+                       emb_scale, resid, w, xn, n, eps);
+  LLMI_HIP(hipGetLastError());
+}
+
+}  // namespace llmi

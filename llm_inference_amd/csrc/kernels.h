@@ -1,0 +1,61 @@
+// kernels.h -- host-side launchers for the gfx950 decode kernels.
+// All launchers are asynchronous on `s` and capture-safe (no allocation, no
+// synchronization), so the session can record them into one hipGraph.
+#pragma once
+
+#include "common.h"
+
+namespace llmi {
+
+// ---- device weight layouts (repacked once at upload) -------
+// Q4_0 : qs [rows][nb][16] B (16-B aligned), d [rows][nb] f16
+// Q8_0 : qs [rows][nb][32] B (16-B aligned), d [rows][nb] f16
+// F16  : [rows][cols] f16 (cols % 8 == 0 for the vector kernels)
+// Q4_K / Q6_K / Q5_0 / BF16 : the GGUF block bytes, unchanged
+struct DevWeight {
+  uint32_t type = 0;
+  int rows = 0, cols = 0;
+  void* qs = nullptr;      // quants (or raw blocks / f16 / bf16 data)
+  uint16_t* d = nullptr;   // per-block scales (Q4_0/Q8_0 only)
+  size_t bytes = 0;        // algorithmic bytes (GGUF size of the tensor)
+};
+
+// Activation prepared for a weight type (device scratch):
+//   Q8_0 : Q8Act {qs[nb][32], d[nb], nsum8[nb]}
+//   Q8_K : raw 292-B blocks (ops.h:98-102)
+//   F16  : x rounded to f16 (ops.cpp:542-551)
+struct ActBuf {
+  Q8Act q8{};
+  uint8_t* q8k = nullptr;
+  uint16_t* x16 = nullptr;
+  const float* xf = nullptr;  // raw f32 x (Q5_0 / BF16 consume it directly)
+};
+
+enum GemvMode { GEMV_EXACT = 0, GEMV_FAST = 1 };
+
+// quantizers (bit-exact with ops.cpp:116-178)
+void launch_quantize_q8_0(const float* x, int n, Q8Act out, hipStream_t s);
+void launch_quantize_q8_k(const float* x, int n, uint8_t* out, hipStream_t s);
+void launch_round_f16(const float* x, int n, uint16_t* out, hipStream_t s);
+
+// o[rows] = W x.  For F16 with amax_key != nullptr the kernel also folds a
+// first-index argmax over the outputs into *amax_key (must be pre-zeroed).
+void launch_gemv(const DevWeight& w, const ActBuf& x, float* o, GemvMode mode, hipStream_t s,
+                 unsigned long long* amax_key = nullptr);
+
+// elementwise / norms
+// o = rms_norm(x) [* w if w]  per row of n, n_rows rows; exact = serial FMA sum
+void launch_rms_norm(const float* x, const float* w, float* o, int n, int n_rows, double eps, bool exact,
+                     hipStream_t s);
+void launch_softmax(float* x, int n, hipStream_t s);
+// NEOX rope on t[n_rows][head_dim] (row r uses table row r / rows_per_pos):
+// cs = [n_pos][n_rot/2][2] (cos, sin) precomputed on the host with glibc
+void launch_rope(float* t, int n_rows, int head_dim, int n_rot, const float* cs, int rows_per_pos, hipStream_t s);
+void launch_scale(float* t, int n, float sc, hipStream_t s);
+void launch_vec_scale_f16(uint16_t* y, int n, float v, hipStream_t s);
+void launch_vec_mad_f16(uint16_t* y, const uint16_t* x, int n, float v, hipStream_t s);
+void launch_gelu_mul(const float* g, const float* u, float* o, int n, hipStream_t s);
+void launch_dequantize_rows(uint32_t type, const uint8_t* blocks, size_t row_bytes, const int32_t* row_ids,
+                            int n_ids, int n_cols, float scale, float* o, hipStream_t s);
+
+}  // namespace llmi

@@ -1,0 +1,468 @@
+// session.cpp -- the Gemma-3 forward of Model::forward (model.cpp:706-1049)
+// resident on one MI355X.  Weights are parsed from the caller's GGUF bytes
+// (loader semantics of gguf.cpp / model.cpp:58-238) and uploaded once; each
+// token is one replay of a captured hipGraph whose kernels read the token id
+// and position from device memory, so a greedy decode never returns to the
+// host between tokens.
+#include "session.h"
+
+#include <cmath>
+#include <cstring>
+
+namespace llmi {
+
+static int meta_u32(const GGUFView& g, const std::string& k, bool required, int dflt = 0) {
+  const GValue* v = g.find(k);
+  if (!v) {
+    if (required) throw status_error(LLMI_E_GGUF, "Failed to find metadata key: " + k);  // model.cpp:64-66
+    return dflt;
+  }
+  return (int)v->u32;
+}
+
+void Session::load_hparams(const GGUFView& g) {  // model.cpp:58-167
+  const GValue* a = g.find("general.architecture");
+  if (!a) throw status_error(LLMI_E_GGUF, "Failed to find metadata key: general.architecture");
+  hp_.arch = a->str;
+  const std::string p = hp_.arch + ".";
+  hp_.n_layer = meta_u32(g, p + "block_count", true);
+  hp_.n_embd = meta_u32(g, p + "embedding_length", true);
+  hp_.n_ff = meta_u32(g, p + "feed_forward_length", true);
+  hp_.n_head = meta_u32(g, p + "attention.head_count", true);
+  hp_.n_head_kv = meta_u32(g, p + "attention.head_count_kv", true);
+  const GValue* eps = g.find(p + "attention.layer_norm_rms_epsilon");
+  const GValue* rb = g.find(p + "rope.freq_base");
+  if (!eps) throw status_error(LLMI_E_GGUF, "Failed to find metadata key: " + p + "attention.layer_norm_rms_epsilon");
+  if (!rb) throw status_error(LLMI_E_GGUF, "Failed to find metadata key: " + p + "rope.freq_base");
+  hp_.eps = (double)eps->f32();  // f32 metadata widened to double (model.cpp:84-85)
+  hp_.rope_base = rb->f32();
+  hp_.rope_scale = 1.0f;         // model.cpp:87-92
+  hp_.hd_k = meta_u32(g, p + "attention.key_length", false, hp_.n_embd / hp_.n_head);
+  hp_.hd_k_swa = meta_u32(g, p + "attention.key_length_swa", false, hp_.hd_k);
+  hp_.hd_v = meta_u32(g, p + "attention.value_length", false, hp_.hd_k);
+  hp_.hd_v_swa = meta_u32(g, p + "attention.value_length_swa", false, hp_.hd_v);
+  hp_.attn_scale = 1.0f / std::sqrt(float(hp_.hd_k));  // model.cpp:120
+  if (const GValue* sw = g.find(p + "attention.sliding_window_pattern"))
+    for (const auto& v : sw->arr) hp_.swa_layers.push_back((v.u32 & 0xFF) != 0);
+  for (const char* k : {"attention.logit_softcapping", "attention.final_logit_softcapping"})
+    if (const GValue* v = g.find(p + k))
+      if (v->f32() > 0.0f) throw status_error(LLMI_E_GGUF, std::string("unsupported: ") + p + k);
+  if (hp_.arch == "gemma4" || g.find(p + "embedding_length_per_layer_input") || g.find(p + "attention.shared_kv_layers"))
+    throw status_error(LLMI_E_GGUF, "unsupported architecture features (Gemma-4 per-layer/shared-KV)");
+  if (hp_.hd_k != hp_.hd_v || hp_.hd_k_swa != hp_.hd_v_swa)
+    throw status_error(LLMI_E_GGUF, "key_length != value_length is not supported");
+  if (hp_.n_head % hp_.n_head_kv) throw status_error(LLMI_E_GGUF, "head_count % head_count_kv != 0");
+}
+
+float* Session::dev_f32_copy(const GGUFView& g, const GTensor* t, int n) {
+  if (!t) return nullptr;
+  if (t->type != T_F32) throw status_error(LLMI_E_TYPE, "norm weight " + t->name + " is not F32");
+  if ((int)t->shape[0] < n) throw status_error(LLMI_E_SIZE, "norm weight " + t->name + " too short");
+  float* d = dalloc<float>(t->shape[0]);
+  LLMI_HIP(hipMemcpy(d, g.tensor_data(*t), t->shape[0] * 4, hipMemcpyHostToDevice));
+  return d;
+}
+
+// one GEMV part per tensor, or a fused part when every tensor shares type/cols
+static std::vector<GemvPart> make_parts(const GGUFView& g, const std::vector<const GTensor*>& ts, hipStream_t s,
+                                        size_t& wbytes) {
+  std::vector<GemvPart> parts;
+  bool same = true;
+  for (auto* t : ts) same &= t->type == ts[0]->type && t->shape[0] == ts[0]->shape[0];
+  auto check = [](const GTensor* t) {
+    if (!gemv_type_supported(t->type))
+      throw status_error(LLMI_E_TYPE, "mat_vec_mul: unsupported tensor type " + std::to_string(t->type));
+  };
+  if (same) {
+    int rows = 0;
+    for (auto* t : ts) { check(t); rows += (int)t->shape[1]; }
+    GemvPart p;
+    p.w = alloc_weight(ts[0]->type, rows, (int)ts[0]->shape[0]);
+    int r0 = 0;
+    for (auto* t : ts) {
+      upload_rows(p.w, r0, g.tensor_data(*t), (int)t->shape[1], s);
+      r0 += (int)t->shape[1];
+    }
+    wbytes += p.w.bytes;
+    parts.push_back(p);
+  } else {
+    int off = 0;
+    for (auto* t : ts) {
+      check(t);
+      GemvPart p;
+      p.w = alloc_weight(t->type, (int)t->shape[1], (int)t->shape[0]);
+      upload_rows(p.w, 0, g.tensor_data(*t), (int)t->shape[1], s);
+      p.out_off = off;
+      off += (int)t->shape[1];
+      wbytes += p.w.bytes;
+      parts.push_back(p);
+    }
+  }
+  return parts;
+}
+
+void Session::upload(const GGUFView& g) {  // model.cpp:169-238 tensor map
+  const GTensor* te = g.tensor("token_embd.weight");
+  const GTensor* on = g.tensor("output_norm.weight");
+  if (!te || !on) throw status_error(LLMI_E_GGUF, "missing token_embd.weight / output_norm.weight");
+  vocab_ = (int)te->shape[1];
+  if ((int)te->shape[0] != hp_.n_embd) throw status_error(LLMI_E_SIZE, "token_embd width != embedding_length");
+  // embed_tokens supports F16/Q6_K/Q8_0/Q5_0 (model.cpp:247-331), the logits
+  // path F16/Q6_K/Q4_K/Q8_0/Q5_0 (model.cpp:999-1034): the intersection
+  if (te->type != T_F16 && te->type != T_Q6_K && te->type != T_Q8_0 && te->type != T_Q5_0)
+    throw status_error(LLMI_E_TYPE, "Error: embed_tokens: Unsupported token embedding tensor type: " +
+                                        std::to_string(te->type));
+  embd_ = alloc_weight(te->type, vocab_, hp_.n_embd);
+  upload_rows(embd_, 0, g.tensor_data(*te), vocab_, stream_);
+  embd_row_bytes_ = gguf_bytes(te->type, 1, hp_.n_embd);
+  embd_raw_ = (const uint8_t*)embd_.qs;
+  if (te->type == T_Q8_0) {  // the GEMV copy is repacked; keep GGUF rows for lookups
+    uint8_t* raw = dalloc<uint8_t>(embd_.bytes);
+    LLMI_HIP(hipMemcpy(raw, g.tensor_data(*te), embd_.bytes, hipMemcpyHostToDevice));
+    embd_raw_ = raw;
+  }
+  weight_bytes_ += embd_.bytes;
+  out_norm_ = dev_f32_copy(g, on, hp_.n_embd);
+  L_.resize(hp_.n_layer);
+  for (int l = 0; l < hp_.n_layer; l++) {
+    auto T = [&](const char* n, bool req = true) -> const GTensor* {
+      const std::string name = "blk." + std::to_string(l) + "." + n;
+      const GTensor* t = g.tensor(name);
+      if (!t && req) throw status_error(LLMI_E_GGUF, "missing tensor " + name);
+      return t;
+    };
+    auto T2 = [&](const char* a, const char* b) { const GTensor* t = T(a, false); return t ? t : T(b, false); };
+    LayerDev& Ld = L_[l];
+    Ld.is_swa = l < (int)hp_.swa_layers.size() ? hp_.swa_layers[l] : (l % 6 < 5);  // model.cpp:723-729
+    Ld.hd = Ld.is_swa ? hp_.hd_k_swa : hp_.hd_k;
+    const GTensor *q = T("attn_q.weight"), *k = T("attn_k.weight"), *v = T("attn_v.weight");
+    if ((int)q->shape[1] < hp_.n_head * Ld.hd || (int)k->shape[1] < hp_.n_head_kv * Ld.hd ||
+        (int)v->shape[1] < hp_.n_head_kv * Ld.hd)
+      throw status_error(LLMI_E_SIZE, "attention projection rows < heads * head_dim");
+    Ld.qkv = make_parts(g, {q, k, v}, stream_, weight_bytes_);
+    Ld.k_off = (int)q->shape[1];
+    Ld.v_off = (int)(q->shape[1] + k->shape[1]);
+    Ld.qkv_rows = (int)(q->shape[1] + k->shape[1] + v->shape[1]);
+    const GTensor* o = T("attn_output.weight");
+    if ((int)o->shape[0] != hp_.n_head * Ld.hd || (int)o->shape[1] != hp_.n_embd)
+      throw status_error(LLMI_E_SIZE, "mat_vec_mul_q4_0: input vector size mismatch (attn_output)");
+    Ld.o = make_parts(g, {o}, stream_, weight_bytes_)[0];
+    const GTensor *gt = T("ffn_gate.weight"), *up = T("ffn_up.weight"), *dn = T("ffn_down.weight");
+    if ((int)gt->shape[1] != hp_.n_ff || (int)up->shape[1] != hp_.n_ff || (int)dn->shape[0] != hp_.n_ff)
+      throw status_error(LLMI_E_SIZE, "ffn shapes do not match feed_forward_length");
+    Ld.gate_up = make_parts(g, {gt, up}, stream_, weight_bytes_);
+    Ld.down = make_parts(g, {dn}, stream_, weight_bytes_)[0];
+    Ld.attn_norm = dev_f32_copy(g, T("attn_norm.weight"), hp_.n_embd);
+    Ld.q_norm = dev_f32_copy(g, T("attn_q_norm.weight"), Ld.hd);
+    Ld.k_norm = dev_f32_copy(g, T("attn_k_norm.weight"), Ld.hd);
+    Ld.ffn_norm = dev_f32_copy(g, T("ffn_norm.weight"), hp_.n_embd);
+    Ld.post_attn_norm = dev_f32_copy(g, T2("post_attention_norm.weight", "attn_post_norm.weight"), hp_.n_embd);
+    Ld.post_ffw_norm = dev_f32_copy(g, T2("post_ffw_norm.weight", "ffn_post_norm.weight"), hp_.n_embd);
+    const size_t kv = (size_t)hp_.n_head_kv * max_ctx_ * Ld.hd;
+    Ld.kc = dalloc<uint16_t>(kv);
+    Ld.vc = dalloc<uint16_t>(kv);
+  }
+}
+
+void Session::alloc_buffers() {
+  const int E = hp_.n_embd, F = hp_.n_ff;
+  int maxq = 0, maxqkv = 0, maxhd = 0;
+  for (auto& l : L_) {
+    maxq = std::max(maxq, hp_.n_head * l.hd);
+    maxqkv = std::max(maxqkv, l.qkv_rows);
+    maxhd = std::max(maxhd, l.hd);
+  }
+  const int maxcols = std::max({E, F, maxq, vocab_ > 0 ? E : 0});
+  resid_ = dalloc<float>(E);
+  xn_ = dalloc<float>(E);
+  qkv_ = dalloc<float>(maxqkv);
+  q_ = dalloc<float>(maxq);
+  attn_ = dalloc<float>(maxq);
+  part_ = dalloc<float>((size_t)hp_.n_head * nsplit_ * (maxhd + 2));
+  o_out_ = dalloc<float>(E);
+  gu_ = dalloc<float>(2 * (size_t)F);
+  hid_ = dalloc<float>(F);
+  d_out_ = dalloc<float>(E);
+  logits_ = dalloc<float>(vocab_);
+  act_.q8.qs = dalloc<int8_t>(maxcols);
+  act_.q8.d = dalloc<uint16_t>(maxcols / 32 + 1);
+  act_.q8.nsum8 = dalloc<int32_t>(maxcols / 32 + 1);
+  act_.q8k = dalloc<uint8_t>((size_t)(maxcols / 256 + 1) * 292);
+  act_.x16 = dalloc<uint16_t>(maxcols);
+  d_token_ = dalloc<int32_t>(1);
+  d_pos_ = dalloc<int32_t>(1);
+  ring_ = dalloc<int32_t>(max_ctx_);
+  ring_idx_ = dalloc<int32_t>(1);
+  amax_key_ = dalloc<unsigned long long>(1);
+  LLMI_HIP(hipHostMalloc((void**)&h_stage_, 64, hipHostMallocDefault));
+}
+
+void Session::build_rope_tables() {
+  // (cos, sin) of ((float)pos * freq_i) / freq_scale with freq_i =
+  // 1/powf(base, (float)(2i)/n_rot), glibc on the host exactly like
+  // ops.cpp:79-83; one table per rope base used by the layers.
+  auto make = [&](float base, int hd) {
+    const int half = hd / 2;
+    std::vector<float> h((size_t)max_ctx_ * half * 2);
+    for (int i = 0; i < half; i++) {
+      const float freq = 1.0f / powf(base, (float)(2 * i) / (float)hd);
+      for (int p = 0; p < max_ctx_; p++) {
+        const float val = ((float)(uint32_t)p * freq) / hp_.rope_scale;
+        h[((size_t)p * half + i) * 2] = cosf(val);
+        h[((size_t)p * half + i) * 2 + 1] = sinf(val);
+      }
+    }
+    float* d = dalloc<float>(h.size());
+    LLMI_HIP(hipMemcpy(d, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+    return d;
+  };
+  rope_swa_ = make(10000.0f, hp_.hd_k_swa);  // model.cpp:732
+  rope_glb_ = make(hp_.rope_base, hp_.hd_k);
+}
+
+Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts) : opts_(opts) {
+  exact_ = (opts.flags & LLMI_EXACT) != 0;
+  use_graph_ = (opts.flags & LLMI_NO_GRAPH) == 0;
+  max_ctx_ = opts.max_ctx > 0 ? opts.max_ctx : 4096;
+  nsplit_ = opts.attn_split > 0 ? opts.attn_split : 32;
+  LLMI_HIP(hipSetDevice(opts.device));
+  LLMI_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  try {
+    GGUFView g(gguf, size);
+    load_hparams(g);
+    upload(g);
+    alloc_buffers();
+    build_rope_tables();
+  } catch (const gguf_error& e) {
+    this->~Session();
+    throw status_error(LLMI_E_GGUF, e.what());
+  } catch (...) {
+    this->~Session();
+    throw;
+  }
+}
+
+Session::~Session() {
+  if (graph_exec_) (void)hipGraphExecDestroy(graph_exec_);
+  if (graph_) (void)hipGraphDestroy(graph_);
+  graph_exec_ = nullptr;
+  graph_ = nullptr;
+  for (auto& l : L_) {
+    for (auto& p : l.qkv) free_weight(p.w);
+    for (auto& p : l.gate_up) free_weight(p.w);
+    free_weight(l.o.w);
+    free_weight(l.down.w);
+  }
+  L_.clear();
+  free_weight(embd_);
+  for (void* p : allocs_) (void)hipFree(p);
+  allocs_.clear();
+  if (h_stage_) (void)hipHostFree(h_stage_);
+  h_stage_ = nullptr;
+  if (stream_) (void)hipStreamDestroy(stream_);
+  stream_ = nullptr;
+}
+
+// Activation format each weight type consumes (ops.cpp:209-210, 630-631, 724-725, 542-551)
+void Session::prepare_act(uint32_t wtype, const float* x, int n, ActBuf& act, hipStream_t s) {
+  act.xf = x;
+  switch (wtype) {
+    case T_Q4_0: case T_Q8_0: launch_quantize_q8_0(x, n, act.q8, s); kernels_per_token_++; break;
+    case T_Q4_K: case T_Q6_K: launch_quantize_q8_k(x, n, act.q8k, s); kernels_per_token_++; break;
+    case T_F16: launch_round_f16(x, n, act.x16, s); kernels_per_token_++; break;
+    default: break;  // Q5_0 / BF16 read f32 x directly
+  }
+}
+
+void Session::gemv_parts(const std::vector<GemvPart>& parts, const float* x, int n_in, float* out, hipStream_t s,
+                         bool x_ready) {
+  uint32_t prepared = 0xFFFFFFFFu;
+  for (const auto& p : parts) {
+    const uint32_t kind = (p.w.type == T_Q8_0) ? T_Q4_0 : (p.w.type == T_Q6_K ? T_Q4_K : p.w.type);
+    if (!(x_ready && kind == T_Q4_0) && kind != prepared) prepare_act(p.w.type, x, n_in, act_, s);
+    act_.xf = x;
+    prepared = kind;
+    launch_gemv(p.w, act_, out + p.out_off, exact_ ? GEMV_EXACT : GEMV_FAST, s);
+    kernels_per_token_++;
+  }
+}
+
+// One decode token.  Reads *d_token_/*d_pos_, ends with the token feedback.
+void Session::record_step(hipStream_t s) {
+  kernels_per_token_ = 0;
+  const int E = hp_.n_embd, F = hp_.n_ff;
+  const float emb_scale = std::sqrt(static_cast<float>(E));  // model.cpp:337-338
+  if (embd_.type == T_F16 || embd_.type == T_Q8_0) {
+    launch_embed_norm(embd_.type, embd_raw_, embd_row_bytes_, d_token_, emb_scale, resid_, L_[0].attn_norm, xn_, E,
+                      hp_.eps, exact_, s);
+    kernels_per_token_++;
+  } else {
+    launch_dequantize_rows(embd_.type, embd_raw_, embd_row_bytes_, d_token_, 1, E, emb_scale, resid_, s);
+    launch_rms_norm(resid_, L_[0].attn_norm, xn_, E, 1, hp_.eps, exact_, s);
+    kernels_per_token_ += 2;
+  }
+  for (int l = 0; l < hp_.n_layer; l++) {
+    LayerDev& Ld = L_[l];
+    const int hd = Ld.hd;
+    gemv_parts(Ld.qkv, xn_, E, qkv_, s, false);
+    QKVArgs qa{qkv_, Ld.k_off, Ld.v_off, hp_.n_head, hp_.n_head_kv, hd, Ld.q_norm, Ld.k_norm,
+               Ld.is_swa ? rope_swa_ : rope_glb_, hp_.attn_scale, hp_.eps, q_, Ld.kc, Ld.vc, max_ctx_, d_pos_};
+    launch_qk_norm_rope_kv(qa, exact_, s);
+    AttnArgs aa{q_, Ld.kc, Ld.vc, hp_.n_head, hp_.n_head_kv, hd, max_ctx_, d_pos_, part_, attn_};
+    const bool o_q8 = Ld.o.w.type == T_Q4_0 || Ld.o.w.type == T_Q8_0;
+    const bool fused_q8 = !exact_ && o_q8 && hd % 32 == 0;
+    launch_attention(aa, exact_, nsplit_, fused_q8 ? &act_.q8 : nullptr, s);
+    kernels_per_token_ += exact_ ? 2 : 3;
+    gemv_parts({Ld.o}, attn_, hp_.n_head * hd, o_out_, s, fused_q8);
+    launch_residual_norm(o_out_, Ld.post_attn_norm, resid_, Ld.ffn_norm, xn_, E, hp_.eps, exact_, s);
+    kernels_per_token_++;
+    gemv_parts(Ld.gate_up, xn_, E, gu_, s, false);
+    const bool d_q8 = Ld.down.w.type == T_Q4_0 || Ld.down.w.type == T_Q8_0;
+    launch_gelu_quant(gu_, F, hid_, d_q8 ? &act_.q8 : nullptr, s);
+    kernels_per_token_++;
+    gemv_parts({Ld.down}, hid_, F, d_out_, s, d_q8);
+    const float* w_next = l + 1 < hp_.n_layer ? L_[l + 1].attn_norm : out_norm_;
+    launch_residual_norm(d_out_, Ld.post_ffw_norm, resid_, w_next, xn_, E, hp_.eps, exact_, s);
+    kernels_per_token_++;
+  }
+  // logits (model.cpp:993-1034): F16 table -> mat_vec_mul_fp16, else mat_vec_mul
+  prepare_act(embd_.type, xn_, E, act_, s);
+  const bool fold = !exact_ && embd_.type == T_F16 && E % 8 == 0;
+  launch_gemv(embd_, act_, logits_, exact_ ? GEMV_EXACT : GEMV_FAST, s, fold ? amax_key_ : nullptr);
+  kernels_per_token_++;
+  if (!fold) {
+    launch_argmax(logits_, vocab_, amax_key_, s);
+    kernels_per_token_++;
+  }
+  launch_finalize_token(amax_key_, d_token_, d_pos_, ring_, ring_idx_, max_ctx_, s);
+  kernels_per_token_++;
+}
+
+void Session::ensure_graph() {
+  if (!use_graph_ || graph_exec_) return;
+  LLMI_HIP(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
+  try {
+    record_step(stream_);
+  } catch (...) {
+    hipGraph_t g;
+    (void)hipStreamEndCapture(stream_, &g);
+    throw;
+  }
+  LLMI_HIP(hipStreamEndCapture(stream_, &graph_));
+  LLMI_HIP(hipGraphInstantiate(&graph_exec_, graph_, nullptr, nullptr, 0));
+}
+
+void Session::run_step() {
+  if (use_graph_) {
+    ensure_graph();
+    LLMI_HIP(hipGraphLaunch(graph_exec_, stream_));
+  } else {
+    record_step(stream_);
+  }
+}
+
+void Session::set_token_pos(int32_t token, int pos, bool reset_ring) {
+  LLMI_HIP(hipStreamSynchronize(stream_));  // h_stage_ reuse
+  h_stage_[0] = token;
+  h_stage_[1] = pos;
+  h_stage_[2] = 0;
+  LLMI_HIP(hipMemcpyAsync(d_token_, &h_stage_[0], 4, hipMemcpyHostToDevice, stream_));
+  LLMI_HIP(hipMemcpyAsync(d_pos_, &h_stage_[1], 4, hipMemcpyHostToDevice, stream_));
+  if (reset_ring) LLMI_HIP(hipMemcpyAsync(ring_idx_, &h_stage_[2], 4, hipMemcpyHostToDevice, stream_));
+}
+
+void Session::forward(const int32_t* tokens, int n, int pos, float* logits, int32_t* argmax) {
+  if (n <= 0) throw status_error(LLMI_E_ARG, "forward: no tokens");
+  if (pos < 0 || pos + n > max_ctx_) throw status_error(LLMI_E_RANGE, "forward: context overflow");
+  for (int i = 0; i < n; i++)
+    if (tokens[i] < 0 || tokens[i] >= vocab_) throw status_error(LLMI_E_RANGE, "forward: token id out of range");
+  for (int i = 0; i < n; i++) {
+    set_token_pos(tokens[i], pos + i, i == 0);
+    run_step();
+  }
+  if (logits) LLMI_HIP(hipMemcpyAsync(logits, logits_, (size_t)vocab_ * 4, hipMemcpyDeviceToHost, stream_));
+  if (argmax) LLMI_HIP(hipMemcpyAsync(argmax, d_token_, 4, hipMemcpyDeviceToHost, stream_));
+  LLMI_HIP(hipStreamSynchronize(stream_));
+}
+
+void Session::enqueue(int32_t first, int pos, int n_steps) {
+  if (first < 0 || first >= vocab_) throw status_error(LLMI_E_RANGE, "token id out of range");
+  if (pos < 0 || pos + n_steps > max_ctx_) throw status_error(LLMI_E_RANGE, "generate: context overflow");
+  set_token_pos(first, pos, true);
+  for (int i = 0; i < n_steps; i++) run_step();
+}
+
+void Session::sync(int32_t* out, int n) {
+  if (out && n > 0) LLMI_HIP(hipMemcpyAsync(out, ring_, (size_t)std::min(n, max_ctx_) * 4, hipMemcpyDeviceToHost, stream_));
+  LLMI_HIP(hipStreamSynchronize(stream_));
+}
+
+void Session::info(llmi_session_info* o) const {
+  o->n_layer = hp_.n_layer;
+  o->n_embd = hp_.n_embd;
+  o->n_ff = hp_.n_ff;
+  o->n_head = hp_.n_head;
+  o->n_head_kv = hp_.n_head_kv;
+  o->head_dim = hp_.hd_k;
+  o->vocab = vocab_;
+  o->max_ctx = max_ctx_;
+  o->weight_bytes = weight_bytes_;
+  size_t b = embd_.bytes;
+  for (const auto& l : L_) {
+    for (const auto& p : l.qkv) b += p.w.bytes;
+    for (const auto& p : l.gate_up) b += p.w.bytes;
+    b += l.o.w.bytes + l.down.w.bytes;
+  }
+  o->bytes_per_token = b;
+  size_t kv = 0;
+  for (const auto& l : L_) kv += (size_t)2 * hp_.n_head_kv * l.hd * 2;
+  o->kv_bytes_per_pos = kv;
+  o->kernels_per_token = kernels_per_token_;
+}
+
+void Session::time_kernel(int which, int reps, double* us, double* bytes) {
+  // launches of the dominant kernel family, each bracketed by its own event
+  // pair on the session stream (torch.cuda.Event would only see torch's
+  // stream), weights swept in decode order so every launch streams from HBM
+  std::vector<const DevWeight*> ws;
+  if (which == 0) {
+    for (const auto& l : L_) {
+      for (const auto& p : l.qkv) ws.push_back(&p.w);
+      ws.push_back(&l.o.w);
+      for (const auto& p : l.gate_up) ws.push_back(&p.w);
+      ws.push_back(&l.down.w);
+    }
+  } else {
+    ws.push_back(&embd_);
+  }
+  std::vector<hipEvent_t> ev(2 * ws.size() * reps);
+  for (auto& e : ev) LLMI_HIP(hipEventCreate(&e));
+  LLMI_HIP(hipStreamSynchronize(stream_));
+  size_t k = 0;
+  double tot_bytes = 0;
+  for (int r = 0; r < reps; r++)
+    for (const DevWeight* w : ws) {
+      LLMI_HIP(hipEventRecord(ev[k++], stream_));
+      launch_gemv(*w, act_, (w == &embd_ || w->rows > 2 * hp_.n_ff) ? logits_ : gu_,
+                  exact_ ? GEMV_EXACT : GEMV_FAST, stream_,
+                  w == &embd_ ? amax_key_ : nullptr);
+      LLMI_HIP(hipEventRecord(ev[k++], stream_));
+      tot_bytes += (double)w->bytes;
+    }
+  LLMI_HIP(hipStreamSynchronize(stream_));
+  double tot_ms = 0;
+  for (size_t i = 0; i < k; i += 2) {
+    float ms = 0;
+    LLMI_HIP(hipEventElapsedTime(&ms, ev[i], ev[i + 1]));
+    tot_ms += ms;
+  }
+  for (auto& e : ev) (void)hipEventDestroy(e);
+  const double n = (double)(k / 2);
+  *us = tot_ms * 1000.0 / n;
+  *bytes = tot_bytes / n;
+  // leave the argmax key clean for the next decode step
+  LLMI_HIP(hipMemsetAsync(amax_key_, 0, 8, stream_));
+  LLMI_HIP(hipStreamSynchronize(stream_));
+}
+
+}  // namespace llmi

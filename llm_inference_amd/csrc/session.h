@@ -1,0 +1,105 @@
+// session.h -- device-resident Gemma-3 decode session (behind llmi_session_*).
+#pragma once
+
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/llmi.h"
+#include "gguf_reader.h"
+#include "session_kernels.h"
+
+namespace llmi {
+
+struct status_error : std::runtime_error {
+  int code;
+  status_error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+struct HParams {  // model.h:22-43 (Gemma-3 subset)
+  std::string arch;
+  int n_layer = 0, n_embd = 0, n_ff = 0, n_head = 0, n_head_kv = 0;
+  int hd_k = 0, hd_k_swa = 0, hd_v = 0, hd_v_swa = 0;
+  double eps = 0;
+  float rope_base = 0, rope_scale = 1.0f, attn_scale = 1.0f;
+  std::vector<bool> swa_layers;
+};
+
+struct GemvPart {  // one weight GEMV writing rows [out_off, out_off + rows)
+  DevWeight w;
+  int out_off = 0;
+};
+
+struct LayerDev {
+  std::vector<GemvPart> qkv;  // 1 part when q|k|v share a type (fused), else 3
+  int k_off = 0, v_off = 0, qkv_rows = 0;
+  GemvPart o;
+  std::vector<GemvPart> gate_up;  // 1 part (fused rows [gate; up]) or 2
+  GemvPart down;
+  float *attn_norm = nullptr, *q_norm = nullptr, *k_norm = nullptr;
+  float *post_attn_norm = nullptr, *ffn_norm = nullptr, *post_ffw_norm = nullptr;
+  bool is_swa = false;
+  int hd = 0;
+  uint16_t *kc = nullptr, *vc = nullptr;
+};
+
+class Session {
+ public:
+  Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts);
+  ~Session();
+
+  void forward(const int32_t* tokens, int n_tokens, int pos, float* logits, int32_t* argmax);
+  void enqueue(int32_t first, int pos, int n_steps);
+  void sync(int32_t* out_tokens, int n);
+  void info(llmi_session_info* out) const;
+  void time_kernel(int which, int reps, double* us, double* bytes);
+
+ private:
+  void load_hparams(const GGUFView& g);
+  void upload(const GGUFView& g);
+  void alloc_buffers();
+  void build_rope_tables();
+  void record_step(hipStream_t s);
+  void prepare_act(uint32_t wtype, const float* x, int n, ActBuf& act, hipStream_t s);
+  void gemv_parts(const std::vector<GemvPart>& parts, const float* x, int n_in, float* out, hipStream_t s,
+                  bool x_ready);
+  void set_token_pos(int32_t token, int pos, bool reset_ring);
+  void ensure_graph();
+  void run_step();
+  float* dev_f32_copy(const GGUFView& g, const GTensor* t, int n);
+  template <typename T>
+  T* dalloc(size_t count) {
+    void* p = nullptr;
+    LLMI_HIP(hipMalloc(&p, count * sizeof(T) + 64));
+    LLMI_HIP(hipMemset(p, 0, count * sizeof(T) + 64));
+    allocs_.push_back(p);
+    return static_cast<T*>(p);
+  }
+
+  llmi_session_opts opts_;
+  bool exact_ = false, use_graph_ = true;
+  int nsplit_ = 32;
+  HParams hp_;
+  int vocab_ = 0, max_ctx_ = 4096;
+  hipStream_t stream_ = nullptr;
+  std::vector<void*> allocs_;
+  std::vector<LayerDev> L_;
+  DevWeight embd_;            // token_embd (logits GEMV + embedding rows)
+  size_t embd_row_bytes_ = 0;
+  const uint8_t* embd_raw_ = nullptr;  // GGUF-layout rows for embedding lookups
+  float* out_norm_ = nullptr;
+  float *rope_swa_ = nullptr, *rope_glb_ = nullptr;
+  // activations
+  float *resid_ = nullptr, *xn_ = nullptr, *qkv_ = nullptr, *q_ = nullptr, *attn_ = nullptr, *part_ = nullptr;
+  float *o_out_ = nullptr, *gu_ = nullptr, *hid_ = nullptr, *d_out_ = nullptr, *logits_ = nullptr;
+  ActBuf act_{};
+  int32_t *d_token_ = nullptr, *d_pos_ = nullptr, *ring_ = nullptr, *ring_idx_ = nullptr;
+  unsigned long long* amax_key_ = nullptr;
+  int32_t* h_stage_ = nullptr;  // pinned: token, pos, ring_idx
+  hipGraph_t graph_ = nullptr;
+  hipGraphExec_t graph_exec_ = nullptr;
+  int kernels_per_token_ = 0;
+  size_t weight_bytes_ = 0;
+};
+
+}  // namespace llmi

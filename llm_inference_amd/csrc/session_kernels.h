@@ -1,0 +1,25 @@
+// session_kernels.h -- weight upload and the fused decode-step glue kernels.
+#pragma once
+
+#include "attn.h"
+#include "kernels.h"
+
+namespace llmi {
+
+size_t gguf_bytes(uint32_t type, size_t rows, size_t cols);
+bool gemv_type_supported(uint32_t type);
+DevWeight alloc_weight(uint32_t type, int rows, int cols);
+void upload_rows(DevWeight& w, int dst_row0, const void* host, int rows, hipStream_t s);
+void free_weight(DevWeight& w);
+
+void launch_residual_norm(const float* y, const float* w_post, float* resid, const float* w_next, float* xn, int n,
+                          double eps, bool exact, hipStream_t s);
+void launch_embed_norm(uint32_t type, const uint8_t* table, size_t row_bytes, const int32_t* d_token,
+                       float emb_scale, float* resid, const float* w, float* xn, int n, double eps, bool exact,
+                       hipStream_t s);
+void launch_gelu_quant(const float* gu, int n, float* hid, const Q8Act* q8, hipStream_t s);
+void launch_argmax(const float* x, int n, unsigned long long* key, hipStream_t s);
+void launch_finalize_token(unsigned long long* key, int32_t* d_token, int32_t* d_pos, int32_t* ring,
+                           int32_t* ring_idx, int ring_cap, hipStream_t s);
+
+}  // namespace llmi

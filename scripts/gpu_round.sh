@@ -1,0 +1,35 @@
+#!/bin/bash
+# One GPU-box session: GPU tests, smoke, bench (+ optional rocprof).  Every GPU
+# step has its own time limit; after a fault/abort/timeout nothing else runs.
+# usage: scripts/gpu_round.sh [tests] [smoke] [bench] [prof] [pmc]
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+want() { for a in "${ARGS[@]}"; do [ "$a" = "$1" ] && return 0; done; return 1; }
+ARGS=("$@")
+fatal() {  # exit codes that mean the GPU step crashed / hung
+  case "$1" in 124|134|137|139|-6|-11) return 0 ;; *) return 1 ;; esac
+}
+run() {  # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  echo "== $name ($(date +%T))"
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"
+  tail -n 25 "gpurun_out/$name.log"
+  if fatal $rc; then echo "FATAL in $name: stopping"; exit $rc; fi
+  return 0
+}
+want tests && run pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider
+want smoke && run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+want bench && run bench 900 python bench.py
+if want prof; then
+  run rocprof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- \
+    python3 bench.py --steps 64 --warmup 4 --prefill 128 --no-cpu-baseline
+fi
+if want pmc; then
+  run pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- \
+    python3 bench.py --steps 16 --warmup 2 --prefill 64 --no-cpu-baseline --kernel-reps 1
+fi
+echo "== done"

@@ -1,0 +1,130 @@
+"""HIP ops through the C ABI (include/llmi.h) vs the golden vectors of the
+reference (tests/golden) and the oracle.
+
+Tolerances (stated here):
+  * exact kernels (LLMI_EXACT): bit-identical to the reference for GEMV
+    (all types), quantize_row_q8_0/_k, rms_norm, rope, scale,
+    vec_scale_f16/vec_mad_f16, dequantize.
+  * fast GEMV: |o - o_ref| <= 1e-4 * max|o_ref| + 1e-6 (fp32 reassociation of
+    the same exact integer block dots).
+  * softmax: device expf, rtol 2e-6.
+"""
+import numpy as np
+import pytest
+
+import cases as K
+from llm_inference_amd.gguf import TensorType as T
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ops():
+    from llm_inference_amd import ops as O
+    O.init_ops(0)
+    return O
+
+
+def bits(a):
+    a = np.asarray(a)
+    return a.view(np.uint32) if a.dtype == np.float32 else a
+
+
+@pytest.mark.parametrize("name,tt,r,c", K.GEMV_CASES, ids=[c[0] for c in K.GEMV_CASES])
+def test_gemv_exact_bitwise(ops, golden_ops, name, tt, r, c):
+    w, x = K.gemv_inputs(name, tt, r, c)
+    o = ops.mat_vec_mul_raw(tt, w, r, c, x, exact=True)
+    np.testing.assert_array_equal(bits(o), bits(golden_ops[f"gemv__{name}__o"]))
+
+
+@pytest.mark.parametrize("name,tt,r,c", K.GEMV_CASES, ids=[c[0] for c in K.GEMV_CASES])
+def test_gemv_fast_tolerance(ops, golden_ops, name, tt, r, c):
+    w, x = K.gemv_inputs(name, tt, r, c)
+    o = ops.mat_vec_mul_raw(tt, w, r, c, x, exact=False)
+    ref = golden_ops[f"gemv__{name}__o"]
+    assert np.abs(o - ref).max() <= 1e-4 * np.abs(ref).max() + 1e-6
+
+
+def test_device_weight_reuse(ops, golden_ops):
+    name, tt, r, c = K.GEMV_CASES[1]
+    w, x = K.gemv_inputs(name, tt, r, c)
+    dw = ops.DeviceWeight(tt, w, r, c)
+    for _ in range(3):
+        np.testing.assert_array_equal(bits(dw(x, exact=True)), bits(golden_ops[f"gemv__{name}__o"]))
+
+
+@pytest.mark.parametrize("i", range(len(K.QUANT_CASES)))
+def test_quantize_bitwise(ops, golden_ops, i):
+    kind, n = K.QUANT_CASES[i]
+    x = K.quant_input(kind, n, i)
+    y = ops.quantize_row_q8_0(x) if kind == "q8_0" else ops.quantize_row_q8_k(x)
+    np.testing.assert_array_equal(y, golden_ops[f"quant__{kind}_{n}__y"])
+
+
+@pytest.mark.parametrize("n", K.NORM_CASES)
+def test_rms_norm(ops, golden_ops, n):
+    x = K.norm_input(n)
+    ref = golden_ops[f"rms__{n}"]
+    np.testing.assert_array_equal(bits(ops.rms_norm(None, x, float(np.float32(1e-6)), exact=True)), bits(ref))
+    fast = ops.rms_norm(None, x, float(np.float32(1e-6)), exact=False)
+    np.testing.assert_allclose(fast, ref, rtol=2e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("case", K.ROPE_CASES)
+def test_rope_bitwise(ops, golden_ops, case):
+    nt, nh, hd, base, pos = case
+    got = ops.rope(K.rope_input(nt, nh, hd), hd, base, 1.0, pos)
+    np.testing.assert_array_equal(bits(got), bits(golden_ops[f"rope__{nt}_{nh}_{hd}_{int(base)}_{pos}"]))
+
+
+@pytest.mark.parametrize("tt,n", K.DEQ_CASES)
+def test_dequantize_bitwise(ops, golden_ops, tt, n):
+    np.testing.assert_array_equal(bits(ops.dequantize_row(tt, K.deq_input(tt, n), n)), bits(golden_ops[f"deq__{tt}_{n}"]))
+
+
+def test_vec_f16_and_scale(ops, golden_ops):
+    rng = np.random.default_rng(6000)
+    y = rng.standard_normal(256).astype(np.float16).view(np.uint16)
+    xv = rng.standard_normal(256).astype(np.float16).view(np.uint16)
+    np.testing.assert_array_equal(ops.vec_scale_f16(y, 0.3712), golden_ops["vec__scale"])
+    np.testing.assert_array_equal(ops.vec_mad_f16(y, xv, 0.8123), golden_ops["vec__mad"])
+    t = np.arange(24, dtype=np.float32).reshape(2, 3, 4)
+    np.testing.assert_array_equal(ops.scale(t, 0.37), (t * np.float32(0.37)).astype(np.float32))
+
+
+@pytest.mark.parametrize("n", K.NORM_CASES)
+def test_softmax(ops, golden_ops, n):
+    np.testing.assert_allclose(ops.softmax(K.norm_input(n)), golden_ops[f"softmax__{n}"], rtol=2e-6, atol=1e-9)
+
+
+def test_error_behaviour(ops):
+    w = np.zeros(18 * 4, np.uint8)
+    with pytest.raises(RuntimeError, match="mat_vec_mul_q4_0: input vector size mismatch"):
+        ops.mat_vec_mul_raw(T.Q4_0, w, 4, 32, np.zeros(31, np.float32))
+    with pytest.raises(RuntimeError, match="unsupported tensor type 3"):
+        ops.mat_vec_mul_raw(3, w, 4, 32, np.zeros(32, np.float32))
+    with pytest.raises(RuntimeError, match="eps must be > 0"):
+        ops.rms_norm(None, np.ones(4, np.float32), 0.0)
+
+
+def test_known_answers(ops):
+    # ops_test.cpp:17-93 analytic checks
+    o = ops.rms_norm(None, [1, 2, 3, 4], float(np.float32(1e-5)))
+    ss = np.float32(1.0) / np.sqrt(np.float32(7.5) + np.float32(1e-5))
+    np.testing.assert_allclose(o, ss * np.array([1, 2, 3, 4], np.float32), atol=1e-6)
+    t = ops.rope([[[1, 2, 3, 4]]], 4, 10000.0, 1.0, 1)
+    assert abs(t[0, 0, 0] - -1.984111) < 1e-4 and abs(t[0, 0, 2] - 2.462337) < 1e-4
+    w = np.array([0x3c00, 0x4000, 0x4200, 0x4400, 0x4500, 0x4600, 0x4700, 0x4800], np.uint16)
+    o = ops.mat_vec_mul_fp16(None, w, [0.5] * 4, 2, 4)
+    np.testing.assert_allclose(o, [5.0, 13.0], atol=1e-3)
+
+
+def test_q4_0_large_random_vs_oracle(ops, oracle):
+    # full 4B ffn_down shape (2560 x 10240): exact bitwise vs oracle, fast in tolerance
+    from llm_inference_amd.synthetic import random_tensor
+    w = random_tensor(T.Q4_0, 2560, 10240, seed=11)
+    x = np.random.default_rng(12).standard_normal(10240).astype(np.float32)
+    ref = oracle.mat_vec_mul(T.Q4_0, w, 2560, 10240, x)
+    np.testing.assert_array_equal(bits(ops.mat_vec_mul_raw(T.Q4_0, w, 2560, 10240, x, exact=True)), bits(ref))
+    fast = ops.mat_vec_mul_raw(T.Q4_0, w, 2560, 10240, x)
+    assert np.abs(fast - ref).max() <= 1e-4 * np.abs(ref).max() + 1e-6
