@@ -142,7 +142,8 @@ __global__ __launch_bounds__(256) void attn_exact_kernel(AttnArgs a) {
 // ---------------------------------------------------------------------------
 template <int HD>
 __global__ __launch_bounds__(64) void attn_partial_kernel(AttnArgs a) {
-  constexpr int DPL = HD / 64;  // head dims per lane in the PV phase
+  constexpr int DPL = HD >= 64 ? HD / 64 : 1;  // head dims per lane in the PV phase
+  const bool pv_lane = (lane * DPL) < HD;
   __shared__ __attribute__((aligned(16))) uint16_t s_q[HD];
   __shared__ float s_p[64];
   const int lane = threadIdx.x;
@@ -186,15 +187,15 @@ __global__ __launch_bounds__(64) void attn_partial_kernel(AttnArgs a) {
     const int nk = min(64, n_keys - tile * 64);
 #pragma unroll
     for (int d = 0; d < DPL; d++) acc[d] *= alpha;
-    for (int j = 0; j < nk; j++) {
+    for (int j = 0; j < nk && pv_lane; j++) {
       const float pj = s_p[j];
       const uint16_t* vr = vb + (size_t)(tile * 64 + j) * HD + lane * DPL;
-      if (DPL == 4) {
+      if constexpr (DPL == 4) {
         const uint2 vv = *reinterpret_cast<const uint2*>(vr);
         acc[0] = fmaf(pj, h2f((uint16_t)(vv.x & 0xFFFF)), acc[0]);
         acc[1] = fmaf(pj, h2f((uint16_t)(vv.x >> 16)), acc[1]);
-        acc[DPL > 2 ? 2 : 0] = fmaf(pj, h2f((uint16_t)(vv.y & 0xFFFF)), acc[DPL > 2 ? 2 : 0]);
-        acc[DPL > 3 ? 3 : 0] = fmaf(pj, h2f((uint16_t)(vv.y >> 16)), acc[DPL > 3 ? 3 : 0]);
+        acc[2] = fmaf(pj, h2f((uint16_t)(vv.y & 0xFFFF)), acc[2]);
+        acc[3] = fmaf(pj, h2f((uint16_t)(vv.y >> 16)), acc[3]);
       } else {
 #pragma unroll
         for (int d = 0; d < DPL; d++) acc[d] = fmaf(pj, h2f(vr[d]), acc[d]);
@@ -203,8 +204,10 @@ __global__ __launch_bounds__(64) void attn_partial_kernel(AttnArgs a) {
     __syncthreads();
   }
   float* part = a.partial + ((size_t)h * nsplit + c) * (HD + 2);
+  if (pv_lane) {
 #pragma unroll
-  for (int d = 0; d < DPL; d++) part[lane * DPL + d] = acc[d];
+    for (int d = 0; d < DPL; d++) part[lane * DPL + d] = acc[d];
+  }
   if (lane == 0) { part[HD] = m_run; part[HD + 1] = l_run; }
 }
 
@@ -253,6 +256,8 @@ void launch_attention(const AttnArgs& a, bool exact, int nsplit, const Q8Act* q8
   }
   const dim3 grid(a.n_head, nsplit);
   switch (a.head_dim) {
+    case 16: hipLaunchKernelGGL(attn_partial_kernel<16>, grid, dim3(64), 0, s, a); break;
+    case 32: hipLaunchKernelGGL(attn_partial_kernel<32>, grid, dim3(64), 0, s, a); break;
     case 64: hipLaunchKernelGGL(attn_partial_kernel<64>, grid, dim3(64), 0, s, a); break;
     case 128: hipLaunchKernelGGL(attn_partial_kernel<128>, grid, dim3(64), 0, s, a); break;
     case 256: hipLaunchKernelGGL(attn_partial_kernel<256>, grid, dim3(64), 0, s, a); break;

@@ -21,12 +21,12 @@ class Model:
                  use_graph: bool = True, attn_split: int = 0):
         buf = gguf if isinstance(gguf, np.ndarray) else np.frombuffer(gguf, np.uint8)
         buf = np.ascontiguousarray(buf)
-        self.gguf = GGUFFile(buf)  # host-side metadata view (tokenizer etc.)
         opts = SessionOpts(device, (LLMI_EXACT if exact else 0) | (0 if use_graph else LLMI_NO_GRAPH),
                            max_ctx, attn_split)
         h = C.c_void_p()
         check(lib().llmi_session_create(ptr(buf), buf.size, C.byref(opts), C.byref(h)))
         self.h = h
+        self.gguf = GGUFFile(buf)  # host-side metadata view (tokenizer etc.)
         self.info = self.get_info()
         self.vocab = self.info.vocab
 

@@ -58,6 +58,7 @@ class Oracle:
         L.orc_model_forward.argtypes = [C.c_void_p, _i32p, C.c_int, C.c_int, _f32p]
         L.orc_model_vocab.argtypes = [C.c_void_p]
         L.orc_model_destroy.argtypes = [C.c_void_p]
+        L.orc_model_set_attn_f64.argtypes = [C.c_void_p, C.c_int]
         L.orc_last_error.restype = C.c_char_p
 
     # --- ops ---
@@ -133,8 +134,10 @@ class Oracle:
         return out
 
     # --- model ---
-    def model(self, gguf: np.ndarray, n_threads: int = 8, max_ctx: int = 1024):
-        return OracleModel(self, gguf, n_threads, max_ctx)
+    def model(self, gguf: np.ndarray, n_threads: int = 8, max_ctx: int = 1024, attn_f64: bool = False):
+        m = OracleModel(self, gguf, n_threads, max_ctx)
+        self.lib.orc_model_set_attn_f64(m.h, int(attn_f64))
+        return m
 
 
 class OracleModel:

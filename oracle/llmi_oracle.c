@@ -511,6 +511,30 @@ void orc_attn_head(const float* q, const uint16_t* k, const uint16_t* v, size_t 
   free(vacc); free(q16);
 }
 
+/* NOT the reference: the same attention in float64 math (no f16 V
+ * accumulator rounding).  Used only to pin the fast GPU path, whose fp32
+ * split-K accumulation is closer to exact math than the reference itself
+ * (whose f16 accumulator carries ~1e-3 absolute error). */
+void orc_attn_head_f64(const float* q, const uint16_t* k, const uint16_t* v, size_t n_keys, size_t hd,
+                       float* out) {
+  pthread_once(&g_table_once, table_init);
+  double* s = (double*)malloc(sizeof(double) * n_keys);
+  double mx = -INFINITY, l = 0.0;
+  for (size_t t = 0; t < n_keys; t++) {
+    double sc = 0.0;
+    for (size_t i = 0; i < hd; i++) sc += (double)F16(k[t * hd + i]) * (double)F16(orc_f32_to_f16(q[i]));
+    s[t] = sc;
+    if (sc > mx) mx = sc;
+  }
+  for (size_t t = 0; t < n_keys; t++) { s[t] = exp(s[t] - mx); l += s[t]; }
+  for (size_t i = 0; i < hd; i++) {
+    double a = 0.0;
+    for (size_t t = 0; t < n_keys; t++) a += s[t] * (double)F16(v[t * hd + i]);
+    out[i] = (float)(a / l);
+  }
+  free(s);
+}
+
 /* ------------------------------------------------------------------ */
 /* minimal GGUF v3 reader (gguf.cpp:195-304)                           */
 /* ------------------------------------------------------------------ */
@@ -577,7 +601,7 @@ struct orc_model {
   int n_swa; uint8_t swa[ORC_MAX_LAYERS];
   orc_layer L[ORC_MAX_LAYERS];
   int tok_embd, out_norm, vocab;
-  int n_threads, max_ctx, n_cached;
+  int n_threads, max_ctx, n_cached, attn_f64;
   uint16_t* kc[ORC_MAX_LAYERS]; uint16_t* vc[ORC_MAX_LAYERS];
 };
 
@@ -704,6 +728,7 @@ void orc_model_destroy(orc_model* m) {
 }
 
 int orc_model_vocab(const orc_model* m) { return m->vocab; }
+void orc_model_set_attn_f64(orc_model* m, int on) { m->attn_f64 = on; }
 
 static int mm(const orc_model* m, int ti, const float* x, float* o) {
   const orc_tensor* T = &m->t[ti];
@@ -787,7 +812,8 @@ int orc_model_forward(orc_model* m, const int* tokens, int T, int pos, float* lo
             memcpy(kh + (size_t)tk * hk, &m->kc[l][((size_t)tk * HK + hkv) * hk], 2 * hk);
             memcpy(vh + (size_t)tk * hv, &m->vc[l][((size_t)tk * HK + hkv) * hv], 2 * hv);
           }
-          orc_attn_head(qv + ((size_t)t * H + h) * hk, kh, vh, nk, hv, att + ((size_t)t * H + h) * hv);
+          (m->attn_f64 ? orc_attn_head_f64 : orc_attn_head)(qv + ((size_t)t * H + h) * hk, kh, vh, nk, hv,
+                                                            att + ((size_t)t * H + h) * hv);
         }
       free(kh); free(vh);
     }

@@ -91,6 +91,11 @@ void orc_model_destroy(orc_model* m);
 int orc_model_forward(orc_model* m, const int* tokens, int n_tokens, int pos,
                       float* logits);
 int orc_model_vocab(const orc_model* m);
+/* test-only variant: float64 attention math instead of the reference's f16
+ * accumulator (orc_attn_head_f64) -- pins the GPU fast path, NOT the reference */
+void orc_model_set_attn_f64(orc_model* m, int on);
+void orc_attn_head_f64(const float* q, const uint16_t* k, const uint16_t* v, size_t n_keys, size_t head_dim,
+                       float* out);
 const char* orc_last_error(void);
 
 #ifdef __cplusplus

@@ -1,11 +1,15 @@
 """Device session (whole Gemma-3 forward on the GPU) vs the reference.
 
 Tolerances:
-  * logits: |dlogit| <= 3e-3 absolute -- the reference's own ModelTest
-    tolerance (model_test.cpp:422);
-  * greedy token ids: identical to the reference/oracle;
-Exact mode differs from the reference only through device expf (attention)
-and tanhf (GELU) ulps; fast mode additionally reassociates fp32 sums.
+  exact mode (LLMI_EXACT): |dlogit| <= 3e-3 vs the reference -- the
+    reference's own ModelTest tolerance (model_test.cpp:422).  Remaining
+    differences are device expf (attention) / tanhf (GELU) ulps.
+  fast mode: the attention accumulates P.V in fp32 (split-K), while the
+    reference keeps an f16 accumulator rounded at every key (model.cpp:484,
+    ops.cpp:1091-1099), itself ~1e-3 away from exact math.  So fast mode is
+    pinned TWICE: |dlogit| <= 3e-3 vs the oracle with float64 attention math
+    (orc_model_set_attn_f64), and |dlogit| <= 6e-2 vs the reference.
+  both modes: greedy token ids identical to the reference.
 """
 import os
 
@@ -14,6 +18,7 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FAST_VS_REF = 6e-2
 
 
 @pytest.fixture(scope="module", params=[True, False], ids=["exact", "fast"])
@@ -21,57 +26,69 @@ def exact(request):
     return request.param
 
 
-def test_model_test_gguf(golden_models, exact):
+def check(got, ref, ideal, exact):
+    if exact:
+        np.testing.assert_allclose(got, ref, atol=3e-3, rtol=0)
+    else:
+        np.testing.assert_allclose(got, ideal, atol=3e-3, rtol=0)
+        np.testing.assert_allclose(got, ref, atol=FAST_VS_REF, rtol=0)
+
+
+def test_model_test_gguf(oracle, golden_models, exact):
     from llm_inference_amd.model import Model
     g = open(os.path.join(ROOT, "tests", "golden", "model_test.gguf"), "rb").read()
+    ideal = oracle.model(np.frombuffer(g, np.uint8), n_threads=2, max_ctx=8, attn_f64=True)
     m = Model(g, exact=exact, max_ctx=64)
     l1 = m.forward([1], 0)
-    np.testing.assert_allclose(l1, golden_models["model_test__l1"], atol=3e-3, rtol=0)
-    for i, v in [(0, 2.9909527), (1, -0.216222), (8, 1.6922607), (9, -2.588623)]:  # model_test.cpp:426-432
-        assert abs(l1[i] - v) < 0.003 + 2e-3
-    nt = int(np.argmax(l1))
+    check(l1, golden_models["model_test__l1"], ideal.forward([1], 0), exact)
+    if exact:
+        for i, v in [(0, 2.9909527), (1, -0.216222), (8, 1.6922607), (9, -2.588623)]:  # model_test.cpp:426-432
+            assert abs(l1[i] - v) < 0.003 + 2e-3
+    nt = int(np.argmax(golden_models["model_test__l1"]))
     assert m.last_argmax == nt
     l2 = m.forward([nt], 1)
-    np.testing.assert_allclose(l2, golden_models["model_test__l2"], atol=3e-3, rtol=0)
+    check(l2, golden_models["model_test__l2"], ideal.forward([nt], 1), exact)
 
 
-def test_tiny_prefill_and_greedy(golden_models, exact):
+def test_tiny_prefill_and_greedy(oracle, golden_models, exact):
     from llm_inference_amd.model import Model
     from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
     g = build_gemma3_gguf(CONFIGS["tiny"], seed=7, swa_pattern=[True, False, True])
+    ideal = oracle.model(g, n_threads=4, max_ctx=64, attn_f64=True)
     m = Model(g, exact=exact, max_ctx=128)
     prompt = golden_models["tiny__prompt"]
     ref_logits, ref_toks = golden_models["tiny__logits"], golden_models["tiny__tokens"]
     lg = m.forward(prompt, 0)
-    np.testing.assert_allclose(lg, ref_logits[0], atol=3e-3, rtol=0)
+    check(lg, ref_logits[0], ideal.forward(prompt, 0), exact)
     assert m.last_argmax == ref_toks[0]
     # device-resident greedy loop (no host round trip between tokens)
     toks = m.generate(int(ref_toks[0]), len(prompt), len(ref_toks) - 1)
     assert toks.tolist() == ref_toks[1:].tolist()
-    # forward() path reproduces the logits of each step too
+    # eager (no graph) forward() path, step by step
     m2 = Model(g, exact=exact, max_ctx=128, use_graph=False)
     m2.forward(prompt, 0)
     pos = len(prompt)
     for i in range(1, len(ref_toks)):
         lg = m2.forward([int(ref_toks[i - 1])], pos)
+        check(lg, ref_logits[i], ideal.forward([int(ref_toks[i - 1])], pos), exact)
         pos += 1
-        np.testing.assert_allclose(lg, ref_logits[i], atol=3e-3, rtol=0)
 
 
 @pytest.mark.parametrize("cfg_name", ["mini-1b", "mini-4b"])
 def test_mini_models_vs_oracle(oracle, cfg_name, exact):
     """Real Gemma-3 1B/4B layer shapes (2 layers, small vocab): 12-token prompt,
-    then 12 greedy tokens; ids identical, logits within 3e-3 of the oracle."""
+    then 12 greedy tokens; ids identical to the oracle (= reference, pinned)."""
     from llm_inference_amd.model import Model
     from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
     cfg = CONFIGS[cfg_name]
     g = build_gemma3_gguf(cfg, seed=3)
     om = oracle.model(g, n_threads=8, max_ctx=64)
+    ideal = oracle.model(g, n_threads=8, max_ctx=64, attn_f64=True)
     m = Model(g, exact=exact, max_ctx=64)
     prompt = np.random.default_rng(5).integers(4, cfg.vocab, 12).astype(np.int32)
     ref = om.forward(prompt, 0)
     got = m.forward(prompt, 0)
-    np.testing.assert_allclose(got, ref, atol=3e-3, rtol=0)
+    check(got, ref, ideal.forward(prompt, 0), exact)
     toks_ref = [int(np.argmax(ref))]
     pos = len(prompt)
     for _ in range(11):
