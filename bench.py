@@ -41,6 +41,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-decode", type=int, default=24, help="decode tokens in the CPU baseline sample")
     p.add_argument("--kernel-reps", type=int, default=2)
+    p.add_argument("--no-graph", action="store_true", help="eager launches (for kernel tracers)")
     return p.parse_args()
 
 
@@ -109,7 +110,7 @@ def main():
     g = build_gemma3_gguf(cfg, seed=1234)
     t_build = time.time() - t0
     max_ctx = a.prefill + a.warmup + a.steps + 8
-    m = Model(g, device=d.local if a.gpus > 1 else 0, exact=a.exact, max_ctx=max_ctx)
+    m = Model(g, device=d.local if a.gpus > 1 else 0, exact=a.exact, max_ctx=max_ctx, use_graph=not a.no_graph)
     info = m.info
     rng = np.random.default_rng(99 + d.rank)
     prompt = np.concatenate([[2], rng.integers(4, cfg.vocab, a.prefill - 1)]).astype(np.int32)

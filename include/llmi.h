@@ -88,6 +88,16 @@ int llmi_scale(float* t, size_t n, float s);                                    
 int llmi_vec_scale_f16(uint16_t* y, size_t n, float v);                           /* ops.cpp:1084-1089 */
 int llmi_vec_mad_f16(uint16_t* y, const uint16_t* x, size_t n, float v);          /* ops.cpp:1091-1099 */
 
+/* Decode attention of Model::run_attn (model.cpp:478-550) for one query
+ * token against an f16 KV history: q [n_head][head_dim] f32 (already
+ * normed/roped/scaled), k/v [n_head_kv][n_keys][head_dim] f16 bits, out
+ * [n_head][head_dim] f32.  LLMI_EXACT = the reference's sequential algorithm
+ * (double scores, f16 V accumulator); default = split-K fp32. */
+int llmi_attention(const float* q, const uint16_t* k, const uint16_t* v, int n_head, int n_head_kv, int n_keys,
+                   int head_dim, float* out, uint32_t flags);
+/* GELU(tanh)(gate) * up, model.cpp:892-899 */
+int llmi_gelu_mul(const float* gate, const float* up, size_t n, float* out);
+
 /* ---------------------------------------------------------------------------
  * (2) device session (Gemma-3 GGUF)
  * ------------------------------------------------------------------------- */

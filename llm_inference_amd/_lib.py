@@ -61,7 +61,9 @@ _SIGS = {
     "llmi_scale": (C.c_int, [_vp, _sz, _f32]),
     "llmi_vec_scale_f16": (C.c_int, [_vp, _sz, _f32]),
     "llmi_vec_mad_f16": (C.c_int, [_vp, _vp, _sz, _f32]),
-    "llmi_session_create": (C.c_int, [_vp, _sz, C.POINTER(SessionOpts), C.POINTER(_vp)]),
+    "llmi_attention": (C.c_int, [_vp, _vp, _vp, C.c_int, C.c_int, C.c_int, C.c_int, _vp, _u32]),
+    "llmi_gelu_mul": (C.c_int, [_vp, _vp, _sz, _vp]),
+    "llmi_session_create":(C.c_int, [_vp, _sz, C.POINTER(SessionOpts), C.POINTER(_vp)]),
     "llmi_session_destroy": (None, [_vp]),
     "llmi_session_forward": (C.c_int, [_vp, _vp, C.c_int, C.c_int, _vp, _vp]),
     "llmi_session_generate": (C.c_int, [_vp, _i32, C.c_int, C.c_int, _vp]),

@@ -340,6 +340,46 @@ int llmi_vec_mad_f16(uint16_t* y, const uint16_t* x, size_t n, float v) {
   });
 }
 
+int llmi_attention(const float* q, const uint16_t* k, const uint16_t* v, int n_head, int n_head_kv, int n_keys,
+                   int head_dim, float* out, uint32_t flags) {
+  return guard([&] {
+    if (n_head <= 0 || n_head_kv <= 0 || n_head % n_head_kv || n_keys <= 0 || head_dim <= 0 || head_dim > 256 ||
+        head_dim % 8)
+      throw status_error(LLMI_E_ARG, "attention: invalid shape");
+    Ctx& c = ctx();
+    const size_t nq = (size_t)n_head * head_dim, nkv = (size_t)n_head_kv * n_keys * head_dim;
+    const int nsplit = 32;
+    float* qd = (float*)c.get(0, nq * 4);
+    float* od = (float*)c.get(1, nq * 4);
+    uint16_t* kd = (uint16_t*)c.get(2, nkv * 2);
+    uint16_t* vd = (uint16_t*)c.get(3, nkv * 2);
+    float* pd = (float*)c.get(4, (size_t)n_head * nsplit * (head_dim + 2) * 4);
+    int32_t* posd = (int32_t*)c.get(5, 4);
+    const int32_t pos = n_keys - 1;
+    LLMI_HIP(hipMemcpyAsync(qd, q, nq * 4, hipMemcpyHostToDevice, c.stream));
+    LLMI_HIP(hipMemcpyAsync(kd, k, nkv * 2, hipMemcpyHostToDevice, c.stream));
+    LLMI_HIP(hipMemcpyAsync(vd, v, nkv * 2, hipMemcpyHostToDevice, c.stream));
+    LLMI_HIP(hipMemcpyAsync(posd, &pos, 4, hipMemcpyHostToDevice, c.stream));
+    AttnArgs a{qd, kd, vd, n_head, n_head_kv, head_dim, n_keys, posd, pd, od};
+    launch_attention(a, (flags & LLMI_EXACT) != 0, nsplit, nullptr, c.stream);
+    LLMI_HIP(hipMemcpyAsync(out, od, nq * 4, hipMemcpyDeviceToHost, c.stream));
+    LLMI_HIP(hipStreamSynchronize(c.stream));
+  });
+}
+
+int llmi_gelu_mul(const float* gate, const float* up, size_t n, float* out) {
+  return guard([&] {
+    Ctx& c = ctx();
+    float* gd = (float*)c.get(0, n * 8);
+    float* od = (float*)c.get(1, n * 4);
+    LLMI_HIP(hipMemcpyAsync(gd, gate, n * 4, hipMemcpyHostToDevice, c.stream));
+    LLMI_HIP(hipMemcpyAsync(gd + n, up, n * 4, hipMemcpyHostToDevice, c.stream));
+    launch_gelu_quant(gd, (int)n, od, nullptr, c.stream);
+    LLMI_HIP(hipMemcpyAsync(out, od, n * 4, hipMemcpyDeviceToHost, c.stream));
+    LLMI_HIP(hipStreamSynchronize(c.stream));
+  });
+}
+
 // ---- session ----
 int llmi_session_create(const void* gguf, size_t size, const llmi_session_opts* opts, llmi_session** out) {
   return guard([&] {

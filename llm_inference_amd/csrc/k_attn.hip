@@ -143,10 +143,10 @@ __global__ __launch_bounds__(256) void attn_exact_kernel(AttnArgs a) {
 template <int HD>
 __global__ __launch_bounds__(64) void attn_partial_kernel(AttnArgs a) {
   constexpr int DPL = HD >= 64 ? HD / 64 : 1;  // head dims per lane in the PV phase
-  const bool pv_lane = (lane * DPL) < HD;
   __shared__ __attribute__((aligned(16))) uint16_t s_q[HD];
   __shared__ float s_p[64];
   const int lane = threadIdx.x;
+  const bool pv_lane = (lane * DPL) < HD;
   const int h = blockIdx.x, c = blockIdx.y, nsplit = gridDim.y;
   const int hkv = h / (a.n_head / a.n_head_kv);
   const int n_keys = *a.d_pos + 1;

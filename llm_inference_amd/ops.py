@@ -150,6 +150,28 @@ def vec_mad_f16(y, x, v: float) -> np.ndarray:
     return y
 
 
+def attention(q, k, v, exact: bool = False) -> np.ndarray:
+    """Decode attention of Model::run_attn (model.cpp:478-550).
+    q: [n_head, hd] f32; k, v: [n_head_kv, n_keys, hd] uint16 f16 bits."""
+    q = _f32(q)
+    k = np.ascontiguousarray(k, np.uint16)
+    v = np.ascontiguousarray(v, np.uint16)
+    n_head, hd = q.shape
+    n_kv, n_keys, _ = k.shape
+    out = np.zeros_like(q)
+    check(lib().llmi_attention(ptr(q), ptr(k), ptr(v), n_head, n_kv, n_keys, hd, ptr(out),
+                               LLMI_EXACT if exact else 0))
+    return out
+
+
+def gelu_mul(gate, up) -> np.ndarray:
+    """GELU(tanh)(gate) * up, model.cpp:892-899."""
+    g, u = _f32(gate), _f32(up)
+    out = np.zeros_like(g)
+    check(lib().llmi_gelu_mul(ptr(g), ptr(u), g.size, ptr(out)))
+    return out
+
+
 class DeviceWeight:
     """A GGUF weight uploaded once (llmi_weight_create); multiply many times."""
 

@@ -21,15 +21,15 @@ run() {  # name timeout cmd...
   if fatal $rc; then echo "FATAL in $name: stopping"; exit $rc; fi
   return 0
 }
-want tests && run pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider
+want tests && run pytest_gpu 900 python -m pytest tests -m gpu -q -rP -p no:cacheprovider
 want smoke && run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 want bench && run bench 900 python bench.py
 if want prof; then
-  run rocprof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- \
-    python3 bench.py --steps 64 --warmup 4 --prefill 128 --no-cpu-baseline
+  run rocprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- \
+    python3 bench.py --steps 64 --warmup 4 --prefill 512 --no-cpu-baseline --no-graph
 fi
 if want pmc; then
-  run pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- \
-    python3 bench.py --steps 16 --warmup 2 --prefill 64 --no-cpu-baseline --kernel-reps 1
+  run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- \
+    python3 bench.py --steps 16 --warmup 2 --prefill 64 --no-cpu-baseline --kernel-reps 1 --no-graph
 fi
 echo "== done"

@@ -128,3 +128,41 @@ def test_q4_0_large_random_vs_oracle(ops, oracle):
     np.testing.assert_array_equal(bits(ops.mat_vec_mul_raw(T.Q4_0, w, 2560, 10240, x, exact=True)), bits(ref))
     fast = ops.mat_vec_mul_raw(T.Q4_0, w, 2560, 10240, x)
     assert np.abs(fast - ref).max() <= 1e-4 * np.abs(ref).max() + 1e-6
+
+
+@pytest.mark.parametrize("hd,n_head,n_kv,n_keys", [(256, 8, 4, 12), (256, 4, 1, 77), (128, 8, 4, 300),
+                                                   (64, 4, 2, 1), (16, 2, 1, 5), (256, 8, 4, 700)])
+def test_attention(ops, oracle, hd, n_head, n_kv, n_keys):
+    """exact: the reference algorithm (f16 V accumulator); differs from the
+    oracle only via device expf ulps -> <= 2 f16 ulps of the output scale.
+    fast: split-K fp32, pinned to the float64-math oracle (atol 2e-5*max)."""
+    import ctypes as C
+    rng = np.random.default_rng(hd * 1000 + n_keys)
+    q = (rng.standard_normal((n_head, hd)) * 0.08).astype(np.float32)
+    k = rng.standard_normal((n_kv, n_keys, hd)).astype(np.float16).view(np.uint16)
+    v = rng.standard_normal((n_kv, n_keys, hd)).astype(np.float16).view(np.uint16)
+    L = oracle.lib
+    f32p = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
+    u16p = np.ctypeslib.ndpointer(np.uint16, flags="C_CONTIGUOUS")
+    L.orc_attn_head_f64.argtypes = [f32p, u16p, u16p, C.c_size_t, C.c_size_t, f32p]
+    ref = np.zeros_like(q)
+    ideal = np.zeros_like(q)
+    for h in range(n_head):
+        g = h // (n_head // n_kv)
+        ref[h] = oracle.attn_head(q[h], k[g], v[g])
+        L.orc_attn_head_f64(np.ascontiguousarray(q[h]), np.ascontiguousarray(k[g]), np.ascontiguousarray(v[g]),
+                            n_keys, hd, ideal[h])
+    ex = ops.attention(q, k, v, exact=True)
+    fa = ops.attention(q, k, v, exact=False)
+    scale = np.abs(ref).max()
+    print(f"exact-vs-ref {np.abs(ex - ref).max():.3g}  fast-vs-f64 {np.abs(fa - ideal).max():.3g}  "
+          f"ref-vs-f64 {np.abs(ref - ideal).max():.3g}")
+    assert np.abs(ex - ref).max() <= 2 * 2.0 ** -10 * scale
+    assert np.abs(fa - ideal).max() <= 2e-5 * scale
+
+
+def test_gelu_mul(ops, oracle):
+    rng = np.random.default_rng(77)
+    g = (rng.standard_normal(10240) * 3).astype(np.float32)
+    u = rng.standard_normal(10240).astype(np.float32)
+    np.testing.assert_allclose(ops.gelu_mul(g, u), oracle.gelu_mul(g, u), rtol=2e-6, atol=1e-7)
