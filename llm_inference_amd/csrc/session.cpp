@@ -222,6 +222,14 @@ void Session::build_rope_tables() {
 
 Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts) : opts_(opts) {
   exact_ = (opts.flags & LLMI_EXACT) != 0;
+  ex_gemv_ = ex_norm_ = ex_attn_ = ex_logits_ = exact_;
+  if (const char* e = getenv("LLMI_EXACT_PARTS")) {  // diagnostics: mix exact/fast kernel families
+    const std::string s(e);
+    ex_gemv_ = s.find("gemv") != std::string::npos;
+    ex_norm_ = s.find("norm") != std::string::npos;
+    ex_attn_ = s.find("attn") != std::string::npos;
+    ex_logits_ = s.find("logits") != std::string::npos;
+  }
   use_graph_ = (opts.flags & LLMI_NO_GRAPH) == 0;
   max_ctx_ = opts.max_ctx > 0 ? opts.max_ctx : 4096;
   nsplit_ = opts.attn_split > 0 ? opts.attn_split : 32;
@@ -282,7 +290,7 @@ void Session::gemv_parts(const std::vector<GemvPart>& parts, const float* x, int
     if (!(x_ready && kind == T_Q4_0) && kind != prepared) prepare_act(p.w.type, x, n_in, act_, s);
     act_.xf = x;
     prepared = kind;
-    launch_gemv(p.w, act_, out + p.out_off, exact_ ? GEMV_EXACT : GEMV_FAST, s);
+    launch_gemv(p.w, act_, out + p.out_off, ex_gemv_ ? GEMV_EXACT : GEMV_FAST, s);
     kernels_per_token_++;
   }
 }
@@ -294,11 +302,11 @@ void Session::record_step(hipStream_t s) {
   const float emb_scale = std::sqrt(static_cast<float>(E));  // model.cpp:337-338
   if (embd_.type == T_F16 || embd_.type == T_Q8_0) {
     launch_embed_norm(embd_.type, embd_raw_, embd_row_bytes_, d_token_, emb_scale, resid_, L_[0].attn_norm, xn_, E,
-                      hp_.eps, exact_, s);
+                      hp_.eps, ex_norm_, s);
     kernels_per_token_++;
   } else {
     launch_dequantize_rows(embd_.type, embd_raw_, embd_row_bytes_, d_token_, 1, E, emb_scale, resid_, s);
-    launch_rms_norm(resid_, L_[0].attn_norm, xn_, E, 1, hp_.eps, exact_, s);
+    launch_rms_norm(resid_, L_[0].attn_norm, xn_, E, 1, hp_.eps, ex_norm_, s);
     kernels_per_token_ += 2;
   }
   for (int l = 0; l < hp_.n_layer; l++) {
@@ -307,14 +315,14 @@ void Session::record_step(hipStream_t s) {
     gemv_parts(Ld.qkv, xn_, E, qkv_, s, false);
     QKVArgs qa{qkv_, Ld.k_off, Ld.v_off, hp_.n_head, hp_.n_head_kv, hd, Ld.q_norm, Ld.k_norm,
                Ld.is_swa ? rope_swa_ : rope_glb_, hp_.attn_scale, hp_.eps, q_, Ld.kc, Ld.vc, max_ctx_, d_pos_};
-    launch_qk_norm_rope_kv(qa, exact_, s);
+    launch_qk_norm_rope_kv(qa, ex_norm_, s);
     AttnArgs aa{q_, Ld.kc, Ld.vc, hp_.n_head, hp_.n_head_kv, hd, max_ctx_, d_pos_, part_, attn_};
     const bool o_q8 = Ld.o.w.type == T_Q4_0 || Ld.o.w.type == T_Q8_0;
-    const bool fused_q8 = !exact_ && o_q8 && hd % 32 == 0;
-    launch_attention(aa, exact_, nsplit_, fused_q8 ? &act_.q8 : nullptr, s);
-    kernels_per_token_ += exact_ ? 2 : 3;
+    const bool fused_q8 = !ex_attn_ && o_q8 && hd % 32 == 0;
+    launch_attention(aa, ex_attn_, nsplit_, fused_q8 ? &act_.q8 : nullptr, s);
+    kernels_per_token_ += ex_attn_ ? 2 : 3;
     gemv_parts({Ld.o}, attn_, hp_.n_head * hd, o_out_, s, fused_q8);
-    launch_residual_norm(o_out_, Ld.post_attn_norm, resid_, Ld.ffn_norm, xn_, E, hp_.eps, exact_, s);
+    launch_residual_norm(o_out_, Ld.post_attn_norm, resid_, Ld.ffn_norm, xn_, E, hp_.eps, ex_norm_, s);
     kernels_per_token_++;
     gemv_parts(Ld.gate_up, xn_, E, gu_, s, false);
     const bool d_q8 = Ld.down.w.type == T_Q4_0 || Ld.down.w.type == T_Q8_0;
@@ -322,13 +330,13 @@ void Session::record_step(hipStream_t s) {
     kernels_per_token_++;
     gemv_parts({Ld.down}, hid_, F, d_out_, s, d_q8);
     const float* w_next = l + 1 < hp_.n_layer ? L_[l + 1].attn_norm : out_norm_;
-    launch_residual_norm(d_out_, Ld.post_ffw_norm, resid_, w_next, xn_, E, hp_.eps, exact_, s);
+    launch_residual_norm(d_out_, Ld.post_ffw_norm, resid_, w_next, xn_, E, hp_.eps, ex_norm_, s);
     kernels_per_token_++;
   }
   // logits (model.cpp:993-1034): F16 table -> mat_vec_mul_fp16, else mat_vec_mul
   prepare_act(embd_.type, xn_, E, act_, s);
-  const bool fold = !exact_ && embd_.type == T_F16 && E % 8 == 0;
-  launch_gemv(embd_, act_, logits_, exact_ ? GEMV_EXACT : GEMV_FAST, s, fold ? amax_key_ : nullptr);
+  const bool fold = !ex_logits_ && embd_.type == T_F16 && E % 8 == 0;
+  launch_gemv(embd_, act_, logits_, ex_logits_ ? GEMV_EXACT : GEMV_FAST, s, fold ? amax_key_ : nullptr);
   kernels_per_token_++;
   if (!fold) {
     launch_argmax(logits_, vocab_, amax_key_, s);

@@ -78,6 +78,7 @@ class Session {
 
   llmi_session_opts opts_;
   bool exact_ = false, use_graph_ = true;
+  bool ex_gemv_ = false, ex_norm_ = false, ex_attn_ = false, ex_logits_ = false;  // per kernel family
   int nsplit_ = 32;
   HParams hp_;
   int vocab_ = 0, max_ctx_ = 4096;
