@@ -34,6 +34,9 @@ struct AttnArgs {
 void launch_qk_norm_rope_kv(const QKVArgs& a, bool exact, hipStream_t s);
 // exact: attn_exact_kernel -> out.  fast: partial + combine (-> out, and
 // Q8_0 blocks of out when q8 != nullptr).
-void launch_attention(const AttnArgs& a, bool exact, int nsplit, const Q8Act* q8, hipStream_t s);
+// fused != nullptr (fast path only): the partial kernel also does the q/k
+// norm + rope + q scale + KV append of qk_norm_rope_kv (one launch fewer).
+void launch_attention(const AttnArgs& a, bool exact, int nsplit, const Q8Act* q8, hipStream_t s,
+                      const QKVArgs* fused = nullptr);
 
 }  // namespace llmi

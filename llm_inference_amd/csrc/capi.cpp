@@ -92,9 +92,8 @@ ActBuf make_act(Ctx& c, uint32_t t, const float* x_dev, int n, hipStream_t s) {
   ActBuf a;
   a.xf = x_dev;
   if (t == T_Q4_0 || t == T_Q8_0) {
-    a.q8.qs = (int8_t*)c.get(10, n);
-    a.q8.d = (uint16_t*)c.get(11, (n / 32 + 1) * 2);
-    a.q8.nsum8 = (int32_t*)c.get(12, (n / 32 + 1) * 4);
+    a.q8.xb = (XBlock*)c.get(10, (size_t)(n / 32 + 1) * sizeof(XBlock));
+    a.q8.nb = n / 32;
     launch_quantize_q8_0(x_dev, n, a.q8, s);
   } else if (t == T_Q4_K || t == T_Q6_K) {
     a.q8k = (uint8_t*)c.get(13, (size_t)(n / 256 + 1) * 292);
@@ -207,19 +206,19 @@ int llmi_quantize_row_q8_0(const float* x, size_t n, void* y) {
     if (n % 32) throw status_error(LLMI_E_SIZE, "quantize_row_q8_0: size % 32 != 0");
     Ctx& c = ctx();
     float* xd = (float*)c.get(0, n * 4);
-    Q8Act q{(int8_t*)c.get(10, n), (uint16_t*)c.get(11, (n / 32 + 1) * 2), (int32_t*)c.get(12, (n / 32 + 1) * 4),
-            (int)(n / 32)};
+    Q8Act q;
+    q.xb = (XBlock*)c.get(10, (n / 32 + 1) * sizeof(XBlock));
+    q.nb = (int)(n / 32);
     LLMI_HIP(hipMemcpyAsync(xd, x, n * 4, hipMemcpyHostToDevice, c.stream));
     launch_quantize_q8_0(xd, (int)n, q, c.stream);
-    std::vector<int8_t> qs(n);
-    std::vector<uint16_t> d(n / 32);
-    LLMI_HIP(hipMemcpyAsync(qs.data(), q.qs, n, hipMemcpyDeviceToHost, c.stream));
-    LLMI_HIP(hipMemcpyAsync(d.data(), q.d, n / 32 * 2, hipMemcpyDeviceToHost, c.stream));
+    std::vector<XBlock> xb(n / 32);
+    LLMI_HIP(hipMemcpyAsync(xb.data(), q.xb, n / 32 * sizeof(XBlock), hipMemcpyDeviceToHost, c.stream));
     LLMI_HIP(hipStreamSynchronize(c.stream));
     uint8_t* out = (uint8_t*)y;  // BlockQ8_0 {f16 d; i8 qs[32]} (ops.h:89-92)
     for (size_t b = 0; b < n / 32; b++) {
-      std::memcpy(out + b * 34, &d[b], 2);
-      std::memcpy(out + b * 34 + 2, &qs[b * 32], 32);
+      const _Float16 dh = (_Float16)xb[b].d;  // exact: d holds an f16 value
+      std::memcpy(out + b * 34, &dh, 2);
+      std::memcpy(out + b * 34 + 2, &xb[b].lo, 32);
     }
   });
 }

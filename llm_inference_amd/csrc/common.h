@@ -107,14 +107,50 @@ __host__ __device__ inline uint32_t argmax_key_index(unsigned long long k) {
   return 0xFFFFFFFFu - (uint32_t)(k & 0xFFFFFFFFull);
 }
 
-// Q8_0 activation vector in device layout (ops.h:89-92 restated SoA):
-//   qs [nb][32] int8   d [nb] f16 bits   dsum [nb] int32 (= -8 * sum(qs), the
-//   Q4_0 zero-point correction, ops.cpp:385-388)
-struct Q8Act {
-  int8_t* qs;
-  uint16_t* d;
-  int32_t* nsum8;
-  int nb;
+// One Q8_0 activation block in device layout (BlockQ8_0 of ops.h:89-92,
+// restated for 16-B loads): 48 bytes =
+//   q[32] int8 | d f32 (= f16(amax/127) widened: exactly the value the
+//   reference multiplies with, ops.cpp:380-381) | nsum8 = -8 * sum(q) (the Q4_0
+//   zero-point term, so sum((nib-8)*q) = dot4(nib, q) + nsum8) | pad
+struct XBlock {
+  int4 lo;  // q[0..15]
+  int4 hi;  // q[16..31]
+  float d;
+  int nsum8;
+  int pad0, pad1;
 };
+static_assert(sizeof(XBlock) == 48, "XBlock layout");
+
+struct Q8Act {
+  XBlock* xb = nullptr;
+  int nb = 0;
+};
+
+// quantize_row_q8_0 (ops.cpp:116-139) of one 32-element block held by 32
+// consecutive lanes (element = lane & 31), bit-exact: amax (order-free),
+// d = amax/127 (IEEE), id = 1/d from the UNROUNDED d, q = nearest_int(fma(x,
+// id, 1.5*2^23)), stored scale = f16(d).  Every lane of the 32-lane group must
+// execute this (shuffles); `ok` masks the stores.
+__device__ __forceinline__ void q8_block_store(float v, bool ok, XBlock* blk, int e) {
+  float amax = fabsf(v);
+#pragma unroll
+  for (int o = 16; o >= 1; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o));
+  const float dd = amax / 127.0f;
+  const float id = dd != 0.0f ? 1.0f / dd : 0.0f;
+  const int q = nearest_int_fma(v, id);
+  int s = q;
+#pragma unroll
+  for (int o = 16; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+  if (ok) {
+    reinterpret_cast<int8_t*>(blk)[e] = (int8_t)q;
+    if (e == 0) {
+      blk->d = h2f(f2h_ggml(dd));
+      blk->nsum8 = -8 * s;
+    }
+  }
+}
+
+// f / nb for f < 2^20, nb < 2^12 by one mul-hi (magic = 2^32/nb + 1)
+__host__ __device__ inline uint32_t div_magic(uint32_t nb) { return (uint32_t)((1ull << 32) / nb + 1); }
 
 }  // namespace llmi

@@ -140,17 +140,86 @@ __global__ __launch_bounds__(256) void attn_exact_kernel(AttnArgs a) {
 // key for QK^T, lane per head-dim slice for PV), keeping an online-softmax
 // partial (m, l, acc[hd]) in fp32.  attn_combine merges the n_split partials.
 // ---------------------------------------------------------------------------
+// q/k head row norm (model.cpp:762/792, fast sum) + NEOX rope at the table row
+// `cs` (ops.cpp:88-91 contraction) for a row held DPL elements per lane.
 template <int HD>
-__global__ __launch_bounds__(64) void attn_partial_kernel(AttnArgs a) {
+__device__ __forceinline__ void norm_rope_row(const float* __restrict__ src, const float* __restrict__ nw,
+                                              const float* __restrict__ cs, double eps, float (&out)[HD >= 64 ? HD / 64 : 1]) {
+  constexpr int DPL = HD >= 64 ? HD / 64 : 1;
+  constexpr int PX = HD >= 64 ? 32 : HD / 2;  // lane holding element i +- HD/2
+  const int lane = threadIdx.x & 63;
+  const bool ok = lane * DPL < HD;
+  float v[DPL];
+  float ss = 0.0f;
+#pragma unroll
+  for (int d = 0; d < DPL; d++) {
+    v[d] = ok ? src[lane * DPL + d] : 0.0f;
+    ss = fmaf(v[d], v[d], ss);
+  }
+  ss = wave_sum(ss);
+  const float sc = 1.0f / sqrtf((float)((double)(ss / (float)HD) + eps));
+#pragma unroll
+  for (int d = 0; d < DPL; d++) {
+    const int i = lane * DPL + d;
+    const float n = ok ? (sc * v[d]) * nw[i] : 0.0f;
+    const float pn = __shfl_xor(n, PX);
+    const int j = i < HD / 2 ? i : i - HD / 2;
+    const float c = ok ? cs[2 * j] : 0.0f, s = ok ? cs[2 * j + 1] : 0.0f;
+    out[d] = i < HD / 2 ? fmaf(n, c, -(pn * s)) : fmaf(pn, s, n * c);
+  }
+}
+
+// FUSED (session fast path): the block also performs the q/k per-head norm,
+// rope and q scale of qk_norm_rope_kv_kernel, and the KV append of the current
+// position: the block whose tile holds `pos` computes k/v of this token in
+// registers, scores/accumulates that key from registers (no global write ->
+// read hand-off inside the launch) and writes it to the cache for later steps.
+template <int HD, bool FUSED>
+__global__ __launch_bounds__(64) void attn_partial_kernel(AttnArgs a, QKVArgs qa) {
   constexpr int DPL = HD >= 64 ? HD / 64 : 1;  // head dims per lane in the PV phase
   __shared__ __attribute__((aligned(16))) uint16_t s_q[HD];
   __shared__ float s_p[64];
   const int lane = threadIdx.x;
   const bool pv_lane = (lane * DPL) < HD;
   const int h = blockIdx.x, c = blockIdx.y, nsplit = gridDim.y;
-  const int hkv = h / (a.n_head / a.n_head_kv);
-  const int n_keys = *a.d_pos + 1;
-  for (int i = lane; i < HD; i += 64) s_q[i] = f2h_ggml(a.q[(size_t)h * HD + i]);
+  const int group = a.n_head / a.n_head_kv;
+  const int hkv = h / group;
+  const int pos = *a.d_pos;
+  const int n_keys = pos + 1;
+  const bool own_new = FUSED && (pos / 64) % nsplit == c;
+  float knew[DPL], vnew[DPL];
+  float s_new = 0.0f;
+  if (FUSED) {
+    const float* cs = qa.rope_cs + (size_t)pos * (HD / 2) * 2;
+    float qr[DPL];
+    norm_rope_row<HD>(qa.qkv + (size_t)h * HD, qa.q_norm_w, cs, qa.eps, qr);
+#pragma unroll
+    for (int d = 0; d < DPL; d++)
+      if (pv_lane) s_q[lane * DPL + d] = f2h_ggml(qr[d] * qa.attn_scale);
+    if (own_new) {
+      norm_rope_row<HD>(qa.qkv + qa.k_off + (size_t)hkv * HD, qa.k_norm_w, cs, qa.eps, knew);
+      float part = 0.0f;
+#pragma unroll
+      for (int d = 0; d < DPL; d++) {
+        const uint16_t k16 = f2h_ggml(knew[d]);
+        const uint16_t v16 = f2h_ggml(pv_lane ? qa.qkv[qa.v_off + (size_t)hkv * HD + lane * DPL + d] : 0.0f);
+        knew[d] = h2f(k16);
+        vnew[d] = h2f(v16);
+        if (pv_lane && h % group == 0) {  // one writer per kv head
+          const size_t ci = ((size_t)hkv * a.max_ctx + pos) * HD + lane * DPL + d;
+          qa.k_cache[ci] = k16;
+          qa.v_cache[ci] = v16;
+        }
+      }
+      __syncthreads();  // s_q complete
+#pragma unroll
+      for (int d = 0; d < DPL; d++)
+        if (pv_lane) part = fmaf(knew[d], h2f(s_q[lane * DPL + d]), part);
+      s_new = wave_sum(part);
+    }
+  } else {
+    for (int i = lane; i < HD; i += 64) s_q[i] = f2h_ggml(a.q[(size_t)h * HD + i]);
+  }
   __syncthreads();
   const uint4* kb = reinterpret_cast<const uint4*>(a.k_cache + (size_t)hkv * a.max_ctx * HD);
   const uint16_t* vb = a.v_cache + (size_t)hkv * a.max_ctx * HD;
@@ -162,7 +231,9 @@ __global__ __launch_bounds__(64) void attn_partial_kernel(AttnArgs a) {
   for (int tile = c; tile * 64 < n_keys; tile += nsplit) {
     const int key = tile * 64 + lane;
     float sc = -INFINITY;
-    if (key < n_keys) {
+    if (FUSED && key == pos) {
+      sc = s_new;
+    } else if (key < n_keys) {
       const uint4* kr = kb + (size_t)key * (HD / 8);
       const uint4* qv = reinterpret_cast<const uint4*>(s_q);
       float s0 = 0.0f, s1 = 0.0f;
@@ -187,10 +258,14 @@ __global__ __launch_bounds__(64) void attn_partial_kernel(AttnArgs a) {
     const int nk = min(64, n_keys - tile * 64);
 #pragma unroll
     for (int d = 0; d < DPL; d++) acc[d] *= alpha;
+#pragma unroll 8
     for (int j = 0; j < nk && pv_lane; j++) {
       const float pj = s_p[j];
       const uint16_t* vr = vb + (size_t)(tile * 64 + j) * HD + lane * DPL;
-      if constexpr (DPL == 4) {
+      if (FUSED && tile * 64 + j == pos) {
+#pragma unroll
+        for (int d = 0; d < DPL; d++) acc[d] = fmaf(pj, vnew[d], acc[d]);
+      } else if constexpr (DPL == 4) {
         const uint2 vv = *reinterpret_cast<const uint2*>(vr);
         acc[0] = fmaf(pj, h2f((uint16_t)(vv.x & 0xFFFF)), acc[0]);
         acc[1] = fmaf(pj, h2f((uint16_t)(vv.x >> 16)), acc[1]);
@@ -213,59 +288,66 @@ __global__ __launch_bounds__(64) void attn_partial_kernel(AttnArgs a) {
 
 // merge split partials per head; optionally quantize the head's output to
 // Q8_0 blocks for the O projection (head_dim % 32 == 0).
-__global__ __launch_bounds__(256) void attn_combine_kernel(AttnArgs a, int nsplit, Q8Act q8) {
+// NSPLIT is a compile-time constant so every partial's (m, l, acc[t]) load is
+// issued in one batch (one memory round trip instead of NSPLIT).
+template <int NSPLIT>
+__global__ __launch_bounds__(256) void attn_combine_kernel(AttnArgs a, Q8Act q8) {
   const int h = blockIdx.x, t = threadIdx.x, hd = a.head_dim;
-  const float* part = a.partial + (size_t)h * nsplit * (hd + 2);
-  float M = -INFINITY;
-  for (int c = 0; c < nsplit; c++) M = fmaxf(M, part[(size_t)c * (hd + 2) + hd]);
-  float L = 0.0f, o = 0.0f;
-  for (int c = 0; c < nsplit; c++) {
+  const float* part = a.partial + (size_t)h * NSPLIT * (hd + 2);
+  float m[NSPLIT], l[NSPLIT], v[NSPLIT];
+#pragma unroll
+  for (int c = 0; c < NSPLIT; c++) {
     const float* pc = part + (size_t)c * (hd + 2);
-    const float lc = pc[hd + 1];
-    if (lc == 0.0f) continue;
-    const float wc = expf(pc[hd] - M);
-    L = fmaf(lc, wc, L);
-    if (t < hd) o = fmaf(pc[t], wc, o);
+    m[c] = pc[hd];
+    l[c] = pc[hd + 1];
+    v[c] = t < hd ? pc[t] : 0.0f;
+  }
+  float M = -INFINITY;
+#pragma unroll
+  for (int c = 0; c < NSPLIT; c++) M = fmaxf(M, m[c]);
+  float L = 0.0f, o = 0.0f;
+#pragma unroll
+  for (int c = 0; c < NSPLIT; c++) {
+    const float wc = l[c] == 0.0f ? 0.0f : expf(m[c] - M);
+    L = fmaf(l[c], wc, L);
+    o = fmaf(v[c], wc, o);
   }
   const float val = t < hd ? o / L : 0.0f;
   if (t < hd) a.out[(size_t)h * hd + t] = val;
-  if (q8.qs != nullptr && t < hd) {  // ops.cpp:116-139 per 32-element block
-    float amax = fabsf(val);
-#pragma unroll
-    for (int off = 16; off >= 1; off >>= 1) amax = fmaxf(amax, __shfl_xor(amax, off));
-    const float dd = amax / 127.0f;
-    const float id = dd != 0.0f ? 1.0f / dd : 0.0f;
-    const int q = nearest_int_fma(val, id);
-    int sum = q;
-#pragma unroll
-    for (int off = 16; off >= 1; off >>= 1) sum += __shfl_xor(sum, off);
-    const int gi = h * hd + t;
-    q8.qs[gi] = (int8_t)q;
-    if ((t & 31) == 0) {
-      q8.d[gi >> 5] = f2h_ggml(dd);
-      q8.nsum8[gi >> 5] = -8 * sum;
-    }
-  }
+  if (q8.xb != nullptr && t < hd) q8_block_store(val, true, q8.xb + ((h * hd + t) >> 5), t & 31);  // ops.cpp:116-139
 }
 
-void launch_attention(const AttnArgs& a, bool exact, int nsplit, const Q8Act* q8, hipStream_t s) {
+template <int HD>
+static void launch_partial(const AttnArgs& a, const QKVArgs* fused, int nsplit, hipStream_t s) {
+  const dim3 grid(a.n_head, nsplit);
+  if (fused)
+    hipLaunchKernelGGL((attn_partial_kernel<HD, true>), grid, dim3(64), 0, s, a, *fused);
+  else
+    hipLaunchKernelGGL((attn_partial_kernel<HD, false>), grid, dim3(64), 0, s, a, QKVArgs{});
+}
+
+void launch_attention(const AttnArgs& a, bool exact, int nsplit, const Q8Act* q8, hipStream_t s,
+                      const QKVArgs* fused) {
   if (exact) {
     hipLaunchKernelGGL(attn_exact_kernel, dim3(a.n_head), dim3(256), 0, s, a);
     LLMI_HIP(hipGetLastError());
     return;
   }
-  const dim3 grid(a.n_head, nsplit);
+  if (nsplit != 16 && nsplit != 32) throw std::runtime_error("attention: nsplit must be 16 or 32");
   switch (a.head_dim) {
-    case 16: hipLaunchKernelGGL(attn_partial_kernel<16>, grid, dim3(64), 0, s, a); break;
-    case 32: hipLaunchKernelGGL(attn_partial_kernel<32>, grid, dim3(64), 0, s, a); break;
-    case 64: hipLaunchKernelGGL(attn_partial_kernel<64>, grid, dim3(64), 0, s, a); break;
-    case 128: hipLaunchKernelGGL(attn_partial_kernel<128>, grid, dim3(64), 0, s, a); break;
-    case 256: hipLaunchKernelGGL(attn_partial_kernel<256>, grid, dim3(64), 0, s, a); break;
+    case 16: launch_partial<16>(a, fused, nsplit, s); break;
+    case 32: launch_partial<32>(a, fused, nsplit, s); break;
+    case 64: launch_partial<64>(a, fused, nsplit, s); break;
+    case 128: launch_partial<128>(a, fused, nsplit, s); break;
+    case 256: launch_partial<256>(a, fused, nsplit, s); break;
     default: throw std::runtime_error("attention: unsupported head_dim " + std::to_string(a.head_dim));
   }
   LLMI_HIP(hipGetLastError());
-  Q8Act none{};
-  hipLaunchKernelGGL(attn_combine_kernel, dim3(a.n_head), dim3(256), 0, s, a, nsplit, q8 ? *q8 : none);
+  const Q8Act qq = q8 ? *q8 : Q8Act{};
+  if (nsplit == 16)
+    hipLaunchKernelGGL(attn_combine_kernel<16>, dim3(a.n_head), dim3(256), 0, s, a, qq);
+  else
+    hipLaunchKernelGGL(attn_combine_kernel<32>, dim3(a.n_head), dim3(256), 0, s, a, qq);
   LLMI_HIP(hipGetLastError());
 }
 

@@ -12,32 +12,15 @@ namespace llmi {
 // Also emits nsum8 = -8 * sum(q) for the Q4_0 zero-point (exact integer).
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void quantize_q8_0_kernel(const float* __restrict__ x, int n,
-                                                            int8_t* __restrict__ qs, uint16_t* __restrict__ d,
-                                                            int32_t* __restrict__ nsum8) {
+                                                            XBlock* __restrict__ xb) {
   const int gl = blockIdx.x * blockDim.x + threadIdx.x;
-  const int blk = gl >> 5, e = gl & 31;
+  const int blk = gl >> 5;
   const bool ok = blk < n / 32;
-  const float v = ok ? x[gl] : 0.0f;
-  float amax = fabsf(v);
-#pragma unroll
-  for (int o = 16; o >= 1; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o));
-  const float dd = amax / 127.0f;
-  const float id = dd != 0.0f ? 1.0f / dd : 0.0f;
-  const int q = nearest_int_fma(v, id);
-  int s = q;
-#pragma unroll
-  for (int o = 16; o >= 1; o >>= 1) s += __shfl_xor(s, o);
-  if (ok) {
-    qs[gl] = (int8_t)q;
-    if (e == 0) {
-      d[blk] = f2h_ggml(dd);
-      nsum8[blk] = -8 * s;
-    }
-  }
+  q8_block_store(ok ? x[gl] : 0.0f, ok, xb + (ok ? blk : 0), gl & 31);
 }
 
 void launch_quantize_q8_0(const float* x, int n, Q8Act out, hipStream_t s) {
-  hipLaunchKernelGGL(quantize_q8_0_kernel, dim3((n + 255) / 256), dim3(256), 0, s, x, n, out.qs, out.d, out.nsum8);
+  hipLaunchKernelGGL(quantize_q8_0_kernel, dim3((n + 255) / 256), dim3(256), 0, s, x, n, out.xb);
   LLMI_HIP(hipGetLastError());
 }
 

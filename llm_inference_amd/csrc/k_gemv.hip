@@ -4,17 +4,22 @@
 //   *_exact : the reference's AVX2 operation order, bit-for-bit
 //             (Q4_0 ops.cpp:364-399, F16 ops.cpp:541-586, Q8_0 ops.cpp:806-824,
 //             Q4_K 643-691, Q6_K 727-770, Q5_0 856-879, BF16 908-917).
-//   *_fast  : HBM-streaming kernels.  One wavefront walks R whole rows as a
-//             flat list of (row, block) items, one 16-B block per lane per
-//             pass (a full 1 KiB coalesced load per wave-instruction against
-//             the repacked SoA layout), integer v_dot4 for Q4_0/Q8_0 blocks,
-//             per-row fp32 partials reduced across the wave at the end.
+//   *_fast  : HBM-streaming kernels.  A wavefront owns R whole rows and walks
+//             them as a flat list of (row, block) items, one block per lane
+//             per pass, so every weight wave-instruction is one coalesced
+//             1 KiB (Q4_0: 64 x 16-B quants) non-temporal load.  All P passes
+//             of a chunk are issued before any is consumed (loads in flight,
+//             no data-dependent control flow between them); the (row, block)
+//             of an item comes from one mul-hi, not a division loop.  Q4_0 and
+//             Q8_0 block dots are exact integer v_dot4; only the fp32
+//             accumulation across blocks and the wave reduction reassociate.
 #include "kernels.h"
 
 namespace llmi {
 
 __device__ __forceinline__ int nib_lo(uint32_t w) { return (int)(w & 0x0F0F0F0Fu); }
 __device__ __forceinline__ int nib_hi(uint32_t w) { return (int)((w >> 4) & 0x0F0F0F0Fu); }
+__device__ __forceinline__ uint16_t ld_nt16(const uint16_t* p) { return __builtin_nontemporal_load(p); }
 
 // ===========================================================================
 // Q4_0 x Q8_0
@@ -24,8 +29,7 @@ __device__ __forceinline__ int nib_hi(uint32_t w) { return (int)((w >> 4) & 0x0F
 // then the hsum_float_8 tree ((a0+a4)+(a2+a6))+((a1+a5)+(a3+a7)).
 __global__ __launch_bounds__(256) void gemv_q4_0_exact(const uint32_t* __restrict__ qs,
                                                        const uint16_t* __restrict__ wd, int rows, int nb,
-                                                       const int32_t* __restrict__ xqs,
-                                                       const uint16_t* __restrict__ xd, float* __restrict__ out) {
+                                                       const XBlock* __restrict__ xb, float* __restrict__ out) {
   const int gl = blockIdx.x * blockDim.x + threadIdx.x;
   const int row = gl >> 3, j = gl & 7;
   float acc = 0.0f;
@@ -35,9 +39,9 @@ __global__ __launch_bounds__(256) void gemv_q4_0_exact(const uint32_t* __restric
     for (int b = 0; b < nb; b++) {
       const uint32_t w = q[(size_t)b * 4];
       const int nib = j < 4 ? nib_lo(w) : nib_hi(w);
-      const int xv = xqs[b * 8 + j];
+      const int xv = reinterpret_cast<const int*>(xb + b)[j];
       const int isum = sdot4(nib, xv, sdot4((int)0xF8F8F8F8u, xv, 0));  // sum (nib-8)*x
-      const float sc = h2f(d[b]) * h2f(xd[b]);
+      const float sc = h2f(d[b]) * xb[b].d;
       acc = fmaf(sc, (float)isum, acc);
     }
   }
@@ -47,48 +51,67 @@ __global__ __launch_bounds__(256) void gemv_q4_0_exact(const uint32_t* __restric
   if (row < rows && j == 0) out[row] = t;
 }
 
-// fast: R rows per wave, flat (row, block) items, 64 items per pass.
 template <int R>
+__device__ __forceinline__ void acc_add(float (&acc)[R], int r, float v) {
+#pragma unroll
+  for (int k = 0; k < R; k++) acc[k] += (k == r) ? v : 0.0f;
+}
+
+template <int R>
+__device__ __forceinline__ void rows_out(float (&acc)[R], int lane, int row0, int nrows, float* out) {
+#pragma unroll
+  for (int k = 0; k < R; k++) {
+    const float s = wave_sum(acc[k]);
+    if (lane == 0 && k < nrows) out[row0 + k] = s;
+  }
+}
+
+// fast: R rows per wave, P passes (64 items each) issued per chunk.
+template <int R, int P>
 __global__ __launch_bounds__(256) void gemv_q4_0_fast(const uint4* __restrict__ qs, const uint16_t* __restrict__ wd,
-                                                      int rows, int nb, const int8_t* __restrict__ xqs,
-                                                      const uint16_t* __restrict__ xd,
-                                                      const int32_t* __restrict__ xnsum8, float* __restrict__ out) {
+                                                      int rows, int nb, uint32_t magic, const XBlock* __restrict__ xb,
+                                                      float* __restrict__ out) {
   const int lane = threadIdx.x & 63;
   const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * R;
   if (row0 >= rows) return;
   const int nrows = min(R, rows - row0);
   const int total = nrows * nb;
-  const size_t f0 = (size_t)row0 * nb;
+  const uint4* qw = qs + (size_t)row0 * nb;
+  const uint16_t* dw = wd + (size_t)row0 * nb;
   float acc[R];
 #pragma unroll
   for (int k = 0; k < R; k++) acc[k] = 0.0f;
-  int r = lane / nb, b = lane - (lane / nb) * nb;
-#pragma unroll 4
-  for (int f = lane; f < total; f += 64) {
-    const uint4 q = ld_nt(qs + f0 + f);
-    const float dw = h2f(__builtin_nontemporal_load(wd + f0 + f));
-    const int4* xp = reinterpret_cast<const int4*>(xqs + b * 32);
-    const int4 x0 = xp[0], x1 = xp[1];
-    int is = xnsum8[b];
-    is = sdot4(nib_lo(q.x), x0.x, is);
-    is = sdot4(nib_lo(q.y), x0.y, is);
-    is = sdot4(nib_lo(q.z), x0.z, is);
-    is = sdot4(nib_lo(q.w), x0.w, is);
-    is = sdot4(nib_hi(q.x), x1.x, is);
-    is = sdot4(nib_hi(q.y), x1.y, is);
-    is = sdot4(nib_hi(q.z), x1.z, is);
-    is = sdot4(nib_hi(q.w), x1.w, is);
-    const float v = (dw * h2f(xd[b])) * (float)is;
+  for (int c0 = 0; c0 < total; c0 += 64 * P) {
+    uint4 q[P];
+    float sw[P];
+    int rr[P], bb[P];
 #pragma unroll
-    for (int k = 0; k < R; k++) acc[k] += (k == r) ? v : 0.0f;
-    b += 64;
-    while (b >= nb) { b -= nb; r++; }
-  }
+    for (int p = 0; p < P; p++) {
+      const int f = c0 + p * 64 + lane;
+      const int fc = f < total ? f : 0;
+      const int r = (int)__umulhi((uint32_t)fc, magic);
+      rr[p] = f < total ? r : R;
+      bb[p] = fc - r * nb;
+      q[p] = ld_nt(qw + fc);
+      sw[p] = h2f(ld_nt16(dw + fc));
+    }
 #pragma unroll
-  for (int k = 0; k < R; k++) {
-    const float sum = wave_sum(acc[k]);
-    if (lane == 0 && k < nrows) out[row0 + k] = sum;
+    for (int p = 0; p < P; p++) {
+      const int4* xp = reinterpret_cast<const int4*>(xb + bb[p]);
+      const int4 x0 = xp[0], x1 = xp[1], x2 = xp[2];
+      int is = x2.y;  // nsum8
+      is = sdot4(nib_lo(q[p].x), x0.x, is);
+      is = sdot4(nib_lo(q[p].y), x0.y, is);
+      is = sdot4(nib_lo(q[p].z), x0.z, is);
+      is = sdot4(nib_lo(q[p].w), x0.w, is);
+      is = sdot4(nib_hi(q[p].x), x1.x, is);
+      is = sdot4(nib_hi(q[p].y), x1.y, is);
+      is = sdot4(nib_hi(q[p].z), x1.z, is);
+      is = sdot4(nib_hi(q[p].w), x1.w, is);
+      acc_add<R>(acc, rr[p], (sw[p] * __int_as_float(x2.x)) * (float)is);
+    }
   }
+  rows_out<R>(acc, lane, row0, nrows, out);
 }
 
 // ===========================================================================
@@ -97,57 +120,64 @@ __global__ __launch_bounds__(256) void gemv_q4_0_fast(const uint4* __restrict__ 
 // exact: one thread per row, single fp32 chain (ops.cpp:812-821):
 //   row = fmaf((float)dot * d_w, d_x, row)
 __global__ __launch_bounds__(256) void gemv_q8_0_exact(const int4* __restrict__ qs, const uint16_t* __restrict__ wd,
-                                                       int rows, int nb, const int4* __restrict__ xqs,
-                                                       const uint16_t* __restrict__ xd, float* __restrict__ out) {
+                                                       int rows, int nb, const XBlock* __restrict__ xb,
+                                                       float* __restrict__ out) {
   const int row = blockIdx.x * blockDim.x + threadIdx.x;
   if (row >= rows) return;
   float sum = 0.0f;
   for (int b = 0; b < nb; b++) {
     const int4 w0 = qs[((size_t)row * nb + b) * 2], w1 = qs[((size_t)row * nb + b) * 2 + 1];
-    const int4 x0 = xqs[b * 2], x1 = xqs[b * 2 + 1];
+    const int4 x0 = xb[b].lo, x1 = xb[b].hi;
     int dot = sdot4(w0.x, x0.x, 0);
     dot = sdot4(w0.y, x0.y, dot); dot = sdot4(w0.z, x0.z, dot); dot = sdot4(w0.w, x0.w, dot);
     dot = sdot4(w1.x, x1.x, dot); dot = sdot4(w1.y, x1.y, dot); dot = sdot4(w1.z, x1.z, dot);
     dot = sdot4(w1.w, x1.w, dot);
-    sum = fmaf((float)dot * h2f(wd[(size_t)row * nb + b]), h2f(xd[b]), sum);
+    sum = fmaf((float)dot * h2f(wd[(size_t)row * nb + b]), xb[b].d, sum);
   }
   out[row] = sum;
 }
 
-template <int R>
+template <int R, int P>
 __global__ __launch_bounds__(256) void gemv_q8_0_fast(const int4* __restrict__ qs, const uint16_t* __restrict__ wd,
-                                                      int rows, int nb, const int4* __restrict__ xqs,
-                                                      const uint16_t* __restrict__ xd, float* __restrict__ out) {
+                                                      int rows, int nb, uint32_t magic, const XBlock* __restrict__ xb,
+                                                      float* __restrict__ out) {
   const int lane = threadIdx.x & 63;
   const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * R;
   if (row0 >= rows) return;
   const int nrows = min(R, rows - row0);
   const int total = nrows * nb;
-  const size_t f0 = (size_t)row0 * nb;
+  const int4* qw = qs + (size_t)row0 * nb * 2;
+  const uint16_t* dw = wd + (size_t)row0 * nb;
   float acc[R];
 #pragma unroll
   for (int k = 0; k < R; k++) acc[k] = 0.0f;
-  int r = lane / nb, b = lane - (lane / nb) * nb;
-#pragma unroll 2
-  for (int f = lane; f < total; f += 64) {
-    const int4 w0 = ld_nt(qs + (f0 + f) * 2);
-    const int4 w1 = ld_nt(qs + (f0 + f) * 2 + 1);
-    const int4 x0 = xqs[b * 2], x1 = xqs[b * 2 + 1];
-    int dot = sdot4(w0.x, x0.x, 0);
-    dot = sdot4(w0.y, x0.y, dot); dot = sdot4(w0.z, x0.z, dot); dot = sdot4(w0.w, x0.w, dot);
-    dot = sdot4(w1.x, x1.x, dot); dot = sdot4(w1.y, x1.y, dot); dot = sdot4(w1.z, x1.z, dot);
-    dot = sdot4(w1.w, x1.w, dot);
-    const float v = (h2f(wd[f0 + f]) * h2f(xd[b])) * (float)dot;
+  for (int c0 = 0; c0 < total; c0 += 64 * P) {
+    int4 w0[P], w1[P];
+    float sw[P];
+    int rr[P], bb[P];
 #pragma unroll
-    for (int k = 0; k < R; k++) acc[k] += (k == r) ? v : 0.0f;
-    b += 64;
-    while (b >= nb) { b -= nb; r++; }
-  }
+    for (int p = 0; p < P; p++) {
+      const int f = c0 + p * 64 + lane;
+      const int fc = f < total ? f : 0;
+      const int r = (int)__umulhi((uint32_t)fc, magic);
+      rr[p] = f < total ? r : R;
+      bb[p] = fc - r * nb;
+      w0[p] = ld_nt(qw + 2 * fc);
+      w1[p] = ld_nt(qw + 2 * fc + 1);
+      sw[p] = h2f(ld_nt16(dw + fc));
+    }
 #pragma unroll
-  for (int k = 0; k < R; k++) {
-    const float sum = wave_sum(acc[k]);
-    if (lane == 0 && k < nrows) out[row0 + k] = sum;
+    for (int p = 0; p < P; p++) {
+      const int4* xp = reinterpret_cast<const int4*>(xb + bb[p]);
+      const int4 x0 = xp[0], x1 = xp[1], x2 = xp[2];
+      int dot = sdot4(w0[p].x, x0.x, 0);
+      dot = sdot4(w0[p].y, x0.y, dot); dot = sdot4(w0[p].z, x0.z, dot); dot = sdot4(w0[p].w, x0.w, dot);
+      dot = sdot4(w1[p].x, x1.x, dot); dot = sdot4(w1[p].y, x1.y, dot); dot = sdot4(w1[p].z, x1.z, dot);
+      dot = sdot4(w1[p].w, x1.w, dot);
+      acc_add<R>(acc, rr[p], (sw[p] * __int_as_float(x2.x)) * (float)dot);
+    }
   }
+  rows_out<R>(acc, lane, row0, nrows, out);
 }
 
 // ===========================================================================
@@ -235,8 +265,8 @@ __global__ __launch_bounds__(256) void gemv_f16_fast_rows(const uint4* __restric
 }
 
 // fast, general cols (cols % 8 == 0): flat (row, chunk) items like Q4_0.
-template <int R>
-__global__ __launch_bounds__(256) void gemv_f16_fast(const uint4* __restrict__ w, int rows, int nc,
+template <int R, int P>
+__global__ __launch_bounds__(256) void gemv_f16_fast(const uint4* __restrict__ w, int rows, int nc, uint32_t magic,
                                                      const uint4* __restrict__ x16, float* __restrict__ out,
                                                      unsigned long long* __restrict__ amax_key) {
   const int lane = threadIdx.x & 63;
@@ -244,18 +274,24 @@ __global__ __launch_bounds__(256) void gemv_f16_fast(const uint4* __restrict__ w
   if (row0 >= rows) return;
   const int nrows = min(R, rows - row0);
   const int total = nrows * nc;
-  const size_t f0 = (size_t)row0 * nc;
+  const uint4* wr = w + (size_t)row0 * nc;
   float acc[R];
 #pragma unroll
   for (int k = 0; k < R; k++) acc[k] = 0.0f;
-  int r = lane / nc, c = lane - (lane / nc) * nc;
-#pragma unroll 4
-  for (int f = lane; f < total; f += 64) {
-    const float v = dot8_f16(ld_nt(w + f0 + f), x16[c], 0.0f);
+  for (int c0 = 0; c0 < total; c0 += 64 * P) {
+    uint4 wv[P];
+    int rr[P], cc[P];
 #pragma unroll
-    for (int k = 0; k < R; k++) acc[k] += (k == r) ? v : 0.0f;
-    c += 64;
-    while (c >= nc) { c -= nc; r++; }
+    for (int p = 0; p < P; p++) {
+      const int f = c0 + p * 64 + lane;
+      const int fc = f < total ? f : 0;
+      const int r = (int)__umulhi((uint32_t)fc, magic);
+      rr[p] = f < total ? r : R;
+      cc[p] = fc - r * nc;
+      wv[p] = ld_nt(wr + fc);
+    }
+#pragma unroll
+    for (int p = 0; p < P; p++) acc_add<R>(acc, rr[p], dot8_f16(wv[p], x16[cc[p]], 0.0f));
   }
   float best = -INFINITY;
   int best_i = 0x7fffffff;
@@ -286,13 +322,13 @@ __global__ __launch_bounds__(256) void gemv_q4_k_exact(const uint8_t* __restrict
   float sum = 0.0f;
   for (int b = 0; b < nb; b++) {
     const uint8_t* blk = wq + ((size_t)row * nb + b) * 144;
-    const uint8_t* xb = xk + (size_t)b * 292;
-    const float xdv = *reinterpret_cast<const float*>(xb);
+    const uint8_t* xbk = xk + (size_t)b * 292;
+    const float xdv = *reinterpret_cast<const float*>(xbk);
     const float d = h2f(ld16(blk)) * xdv;
     const float mn = h2f(ld16(blk + 2)) * xdv;
     const uint8_t* q4 = blk + 16;
-    const int8_t* q8 = reinterpret_cast<const int8_t*>(xb + 4);
-    const int16_t* bs = reinterpret_cast<const int16_t*>(xb + 260);
+    const int8_t* q8 = reinterpret_cast<const int8_t*>(xbk + 4);
+    const int16_t* bs = reinterpret_cast<const int16_t*>(xbk + 260);
     int is = 0;
     for (int j = 0; j < 256; j += 64) {
       int s, m;
@@ -319,12 +355,12 @@ __global__ __launch_bounds__(256) void gemv_q6_k_exact(const uint8_t* __restrict
   float sum = 0.0f;
   for (int b = 0; b < nb; b++) {
     const uint8_t* blk = wq + ((size_t)row * nb + b) * 210;
-    const uint8_t* xb = xk + (size_t)b * 292;
-    const float d = h2f(ld16(blk + 208)) * *reinterpret_cast<const float*>(xb);
+    const uint8_t* xbk = xk + (size_t)b * 292;
+    const float d = h2f(ld16(blk + 208)) * *reinterpret_cast<const float*>(xbk);
     const uint8_t* ql = blk;
     const uint8_t* qh = blk + 128;
     const int8_t* sc = reinterpret_cast<const int8_t*>(blk + 192);
-    const int8_t* xq = reinterpret_cast<const int8_t*>(xb + 4);
+    const int8_t* xq = reinterpret_cast<const int8_t*>(xbk + 4);
     for (int n = 0; n < 256; n += 128) {
       int part = 0;
       for (int l = 0; l < 32; ++l) {
@@ -378,20 +414,43 @@ __global__ __launch_bounds__(256) void gemv_bf16_exact(const uint16_t* __restric
 // ===========================================================================
 // launcher
 // ===========================================================================
+// smallest R in {1,2,4,8} with R*items a multiple of 64 (full passes), capped
+// at 8 (then the last pass is partially masked)
 static int rows_per_wave(int items_per_row) {
-  // smallest R in {1,2,4,8} with R*items a multiple of 64 (full passes),
-  // capped at 8 (then the last pass is partially masked)
   int R = 1;
   while (R < 8 && (R * items_per_row) % 64 != 0) R *= 2;
   return R;
 }
+// passes issued per chunk: all of them up to 8
+static int passes_per_chunk(int R, int items_per_row) {
+  const int passes = (R * items_per_row + 63) / 64;
+  return passes >= 8 ? 8 : (passes >= 6 ? 6 : (passes >= 4 ? passes : (passes == 3 ? 4 : passes)));
+}
 
-#define LLMI_DISPATCH_R(R, KERNEL, GRID, ...)                                              \
-  switch (R) {                                                                               \
-    case 1: hipLaunchKernelGGL(KERNEL<1>, GRID, dim3(256), 0, s, __VA_ARGS__); break;        \
-    case 2: hipLaunchKernelGGL(KERNEL<2>, GRID, dim3(256), 0, s, __VA_ARGS__); break;        \
-    case 4: hipLaunchKernelGGL(KERNEL<4>, GRID, dim3(256), 0, s, __VA_ARGS__); break;        \
-    default: hipLaunchKernelGGL(KERNEL<8>, GRID, dim3(256), 0, s, __VA_ARGS__); break;       \
+template <template <int, int> class K>
+struct dummy {};
+
+#define LLMI_RP_CASE(KER, R, P, GRID, ...) \
+  case R * 16 + P: hipLaunchKernelGGL((KER<R, P>), GRID, dim3(256), 0, s, __VA_ARGS__); break;
+#define LLMI_RP_SWITCH(KER, R, P, GRID, ...)                                                                   \
+  switch ((R) * 16 + (P)) {                                                                                     \
+    LLMI_RP_CASE(KER, 1, 1, GRID, __VA_ARGS__) LLMI_RP_CASE(KER, 1, 2, GRID, __VA_ARGS__)                       \
+    LLMI_RP_CASE(KER, 1, 4, GRID, __VA_ARGS__) LLMI_RP_CASE(KER, 1, 5, GRID, __VA_ARGS__)                       \
+    LLMI_RP_CASE(KER, 1, 6, GRID, __VA_ARGS__) LLMI_RP_CASE(KER, 1, 7, GRID, __VA_ARGS__)                       \
+    LLMI_RP_CASE(KER, 1, 8, GRID, __VA_ARGS__)                                                                  \
+    LLMI_RP_CASE(KER, 2, 1, GRID, __VA_ARGS__) LLMI_RP_CASE(KER, 2, 2, GRID, __VA_ARGS__)                       \
+    LLMI_RP_CASE(KER, 2, 4, GRID, __VA_ARGS__) LLMI_RP_CASE(KER, 2, 5, GRID, __VA_ARGS__)                       \
+    LLMI_RP_CASE(KER, 2, 6, GRID, __VA_ARGS__) LLMI_RP_CASE(KER, 2, 7, GRID, __VA_ARGS__)                       \
+    LLMI_RP_CASE(KER, 2, 8, GRID, __VA_ARGS__)                                                                  \
+    LLMI_RP_CASE(KER, 4, 1, GRID, __VA_ARGS__) LLMI_RP_CASE(KER, 4, 2, GRID, __VA_ARGS__)                       \
+    LLMI_RP_CASE(KER, 4, 4, GRID, __VA_ARGS__) LLMI_RP_CASE(KER, 4, 5, GRID, __VA_ARGS__)                       \
+    LLMI_RP_CASE(KER, 4, 6, GRID, __VA_ARGS__) LLMI_RP_CASE(KER, 4, 7, GRID, __VA_ARGS__)                       \
+    LLMI_RP_CASE(KER, 4, 8, GRID, __VA_ARGS__)                                                                  \
+    LLMI_RP_CASE(KER, 8, 1, GRID, __VA_ARGS__) LLMI_RP_CASE(KER, 8, 2, GRID, __VA_ARGS__)                       \
+    LLMI_RP_CASE(KER, 8, 4, GRID, __VA_ARGS__) LLMI_RP_CASE(KER, 8, 5, GRID, __VA_ARGS__)                       \
+    LLMI_RP_CASE(KER, 8, 6, GRID, __VA_ARGS__) LLMI_RP_CASE(KER, 8, 7, GRID, __VA_ARGS__)                       \
+    LLMI_RP_CASE(KER, 8, 8, GRID, __VA_ARGS__)                                                                  \
+    default: throw std::runtime_error("gemv: no kernel for R/P");                                               \
   }
 
 void launch_gemv(const DevWeight& w, const ActBuf& x, float* o, GemvMode mode, hipStream_t s,
@@ -399,27 +458,25 @@ void launch_gemv(const DevWeight& w, const ActBuf& x, float* o, GemvMode mode, h
   const int rows = w.rows;
   if (rows == 0) return;
   switch (w.type) {
-    case T_Q4_0: {
-      const int nb = w.cols / 32;
-      if (mode == GEMV_EXACT) {
-        hipLaunchKernelGGL(gemv_q4_0_exact, dim3((rows * 8 + 255) / 256), dim3(256), 0, s,
-                           (const uint32_t*)w.qs, w.d, rows, nb, (const int32_t*)x.q8.qs, x.q8.d, o);
-      } else {
-        const int R = rows_per_wave(nb);
-        const dim3 grid((rows + 4 * R - 1) / (4 * R));
-        LLMI_DISPATCH_R(R, gemv_q4_0_fast, grid, (const uint4*)w.qs, w.d, rows, nb, x.q8.qs, x.q8.d, x.q8.nsum8, o);
-      }
-      break;
-    }
+    case T_Q4_0:
     case T_Q8_0: {
       const int nb = w.cols / 32;
       if (mode == GEMV_EXACT) {
-        hipLaunchKernelGGL(gemv_q8_0_exact, dim3((rows + 255) / 256), dim3(256), 0, s, (const int4*)w.qs, w.d, rows,
-                           nb, (const int4*)x.q8.qs, x.q8.d, o);
+        if (w.type == T_Q4_0)
+          hipLaunchKernelGGL(gemv_q4_0_exact, dim3((rows * 8 + 255) / 256), dim3(256), 0, s,
+                             (const uint32_t*)w.qs, w.d, rows, nb, x.q8.xb, o);
+        else
+          hipLaunchKernelGGL(gemv_q8_0_exact, dim3((rows + 255) / 256), dim3(256), 0, s, (const int4*)w.qs, w.d, rows,
+                             nb, x.q8.xb, o);
       } else {
-        const int R = rows_per_wave(nb);
+        const int R = rows_per_wave(nb), P = passes_per_chunk(R, nb);
         const dim3 grid((rows + 4 * R - 1) / (4 * R));
-        LLMI_DISPATCH_R(R, gemv_q8_0_fast, grid, (const int4*)w.qs, w.d, rows, nb, (const int4*)x.q8.qs, x.q8.d, o);
+        const uint32_t mg = div_magic(nb);
+        if (w.type == T_Q4_0) {
+          LLMI_RP_SWITCH(gemv_q4_0_fast, R, P, grid, (const uint4*)w.qs, w.d, rows, nb, mg, x.q8.xb, o)
+        } else {
+          LLMI_RP_SWITCH(gemv_q8_0_fast, R, P, grid, (const int4*)w.qs, w.d, rows, nb, mg, x.q8.xb, o)
+        }
       }
       break;
     }
@@ -441,9 +498,10 @@ void launch_gemv(const DevWeight& w, const ActBuf& x, float* o, GemvMode mode, h
         }
       } else {
         const int nc = w.cols / 8;
-        const int R = rows_per_wave(nc);
+        const int R = rows_per_wave(nc), P = passes_per_chunk(R, nc);
         const dim3 grid((rows + 4 * R - 1) / (4 * R));
-        LLMI_DISPATCH_R(R, gemv_f16_fast, grid, (const uint4*)w.qs, rows, nc, (const uint4*)x.x16, o, amax_key);
+        LLMI_RP_SWITCH(gemv_f16_fast, R, P, grid, (const uint4*)w.qs, rows, nc, div_magic(nc), (const uint4*)x.x16,
+                       o, amax_key)
       }
       break;
     }

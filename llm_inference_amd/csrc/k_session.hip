@@ -146,48 +146,83 @@ __device__ __forceinline__ float rms_scale(float sum, int n, double eps) {  // o
 //   h = resid + a ; resid = h            (residual add)
 //   xn = rms_norm(h) * w_next            (ffn_norm / next layer attn_norm /
 //                                         output_norm)
-// One block of 1024 threads; values staged in LDS (n <= 8192).
+// One block of 1024 threads, every operand prefetched into registers up front
+// (one memory round trip), n <= 8192.  Also emits the next GEMV's activation:
+// Q8_0 blocks (quantize_row_q8_0 semantics) and/or f16-rounded x (logits).
 // ---------------------------------------------------------------------------
+constexpr int NORM_EPT = 8;  // elements per thread (n <= 8192)
+
+__device__ __forceinline__ void norm_outputs(const float (&xv)[NORM_EPT], int n, const NormOut& out) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < NORM_EPT; k++) {
+    const int i = t + k * 1024;
+    const bool ok = i < n;
+    if (ok) out.xn[i] = xv[k];
+    if (out.x16 && ok) out.x16[i] = f2h_ggml(xv[k]);
+    if (out.q8 && k * 1024 < n) q8_block_store(xv[k], ok, out.q8 + (ok ? (i >> 5) : 0), i & 31);
+  }
+}
+
+template <bool EXACT>
+__device__ __forceinline__ float sumsq_regs(const float (&v)[NORM_EPT], int n, float* s_h, float* sh) {
+  if (EXACT) {  // stage, then the reference's serial fma chain (ops.cpp:33-36)
+#pragma unroll
+    for (int k = 0; k < NORM_EPT; k++)
+      if (threadIdx.x + k * 1024 < n) s_h[threadIdx.x + k * 1024] = v[k];
+    __syncthreads();
+    return serial_sumsq(s_h, n, sh);
+  }
+  float sq = 0.0f;
+#pragma unroll
+  for (int k = 0; k < NORM_EPT; k++) sq = fmaf(v[k], v[k], sq);
+  return block_sum(sq, sh);
+}
+
 template <bool EXACT>
 __global__ __launch_bounds__(1024) void residual_norm_kernel(const float* __restrict__ y,
                                                              const float* __restrict__ w_post,
                                                              float* __restrict__ resid,
-                                                             const float* __restrict__ w_next,
-                                                             float* __restrict__ xn, int n, double eps) {
-  extern __shared__ float s_h[];
+                                                             const float* __restrict__ w_next, NormOut out, int n,
+                                                             double eps) {
+  extern __shared__ float s_h[];  // exact mode staging only
   __shared__ float sh[16];
   const int t = threadIdx.x;
-  float sq = 0.0f;
-  // pass 1: y -> LDS, sum of squares
-  for (int i = t; i < n; i += blockDim.x) {
-    const float v = y[i];
-    s_h[i] = v;
-    sq = fmaf(v, v, sq);
+  float yv[NORM_EPT], rv[NORM_EPT], wp[NORM_EPT], wn[NORM_EPT];
+#pragma unroll
+  for (int k = 0; k < NORM_EPT; k++) {
+    const int i = t + k * 1024;
+    const bool ok = i < n;
+    yv[k] = ok ? y[i] : 0.0f;
+    rv[k] = ok ? resid[i] : 0.0f;
+    wp[k] = (ok && w_post) ? w_post[i] : 0.0f;
+    wn[k] = ok ? w_next[i] : 0.0f;
   }
-  __syncthreads();
-  const float s1 = EXACT ? serial_sumsq(s_h, n, sh) : block_sum(sq, sh);
-  const float sc1 = rms_scale(s1, n, eps);
-  float sq2 = 0.0f;
-  for (int i = t; i < n; i += blockDim.x) {
-    const float a = w_post ? (sc1 * s_h[i]) * w_post[i] : s_h[i];
-    const float h = resid[i] + a;
-    resid[i] = h;
-    s_h[i] = h;
-    sq2 = fmaf(h, h, sq2);
+  const float sc1 = rms_scale(sumsq_regs<EXACT>(yv, n, s_h, sh), n, eps);
+  float hv[NORM_EPT];
+#pragma unroll
+  for (int k = 0; k < NORM_EPT; k++) {
+    const int i = t + k * 1024;
+    const float a = w_post ? (sc1 * yv[k]) * wp[k] : yv[k];
+    hv[k] = rv[k] + a;
+    if (i < n) resid[i] = hv[k];
   }
-  __syncthreads();
-  const float s2 = EXACT ? serial_sumsq(s_h, n, sh) : block_sum(sq2, sh);
-  const float sc2 = rms_scale(s2, n, eps);
-  for (int i = t; i < n; i += blockDim.x) xn[i] = (sc2 * s_h[i]) * w_next[i];
+  if (EXACT) __syncthreads();  // s_h reuse
+  const float sc2 = rms_scale(sumsq_regs<EXACT>(hv, n, s_h, sh), n, eps);
+  float xv[NORM_EPT];
+#pragma unroll
+  for (int k = 0; k < NORM_EPT; k++) xv[k] = (sc2 * hv[k]) * wn[k];
+  norm_outputs(xv, n, out);
 }
 
-void launch_residual_norm(const float* y, const float* w_post, float* resid, const float* w_next, float* xn, int n,
-                          double eps, bool exact, hipStream_t s) {
-  const size_t lds = (size_t)n * 4;
+void launch_residual_norm(const float* y, const float* w_post, float* resid, const float* w_next, const NormOut& out,
+                          int n, double eps, bool exact, hipStream_t s) {
+  if (n > 1024 * NORM_EPT) throw std::runtime_error("residual_norm: n_embd > 8192");
   if (exact)
-    hipLaunchKernelGGL(residual_norm_kernel<true>, dim3(1), dim3(1024), lds, s, y, w_post, resid, w_next, xn, n, eps);
+    hipLaunchKernelGGL(residual_norm_kernel<true>, dim3(1), dim3(1024), (size_t)n * 4, s, y, w_post, resid, w_next, out,
+                       n, eps);
   else
-    hipLaunchKernelGGL(residual_norm_kernel<false>, dim3(1), dim3(1024), lds, s, y, w_post, resid, w_next, xn, n, eps);
+    hipLaunchKernelGGL(residual_norm_kernel<false>, dim3(1), dim3(1024), 0, s, y, w_post, resid, w_next, out, n, eps);
   LLMI_HIP(hipGetLastError());
 }
 
@@ -211,35 +246,16 @@ __device__ __forceinline__ float gelu_mul1(float x, float u) {
 }
 
 __global__ __launch_bounds__(256) void gelu_quant_kernel(const float* __restrict__ gu, int n, float* __restrict__ hid,
-                                                         int8_t* __restrict__ qs, uint16_t* __restrict__ d,
-                                                         int32_t* __restrict__ nsum8) {
+                                                         XBlock* __restrict__ xb) {
   const int gl = blockIdx.x * blockDim.x + threadIdx.x;
-  const int blk = gl >> 5, e = gl & 31;
   const bool ok = gl < n;
   const float v = ok ? gelu_mul1(gu[gl], gu[n + gl]) : 0.0f;
   if (ok) hid[gl] = v;
-  if (qs == nullptr) return;
-  float amax = fabsf(v);
-#pragma unroll
-  for (int o = 16; o >= 1; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o));
-  const float dd = amax / 127.0f;
-  const float id = dd != 0.0f ? 1.0f / dd : 0.0f;
-  const int q = nearest_int_fma(v, id);
-  int sm = q;
-#pragma unroll
-  for (int o = 16; o >= 1; o >>= 1) sm += __shfl_xor(sm, o);
-  if (ok) {
-    qs[gl] = (int8_t)q;
-    if (e == 0) {
-      d[blk] = f2h_ggml(dd);
-      nsum8[blk] = -8 * sm;
-    }
-  }
+  if (xb != nullptr) q8_block_store(v, ok && (gl >> 5) < n / 32, xb + (ok ? (gl >> 5) : 0), gl & 31);
 }
 
 void launch_gelu_quant(const float* gu, int n, float* hid, const Q8Act* q8, hipStream_t s) {
-  hipLaunchKernelGGL(gelu_quant_kernel, dim3((n + 255) / 256), dim3(256), 0, s, gu, n, hid, q8 ? q8->qs : nullptr,
-                     q8 ? q8->d : nullptr, q8 ? q8->nsum8 : nullptr);
+  hipLaunchKernelGGL(gelu_quant_kernel, dim3((n + 255) / 256), dim3(256), 0, s, gu, n, hid, q8 ? q8->xb : nullptr);
   LLMI_HIP(hipGetLastError());
 }
 
@@ -293,23 +309,26 @@ template <bool EXACT>
 __global__ __launch_bounds__(1024) void embed_norm_kernel(uint32_t type, const uint8_t* __restrict__ table,
                                                           size_t row_bytes, const int32_t* __restrict__ d_token,
                                                           float emb_scale, float* __restrict__ resid,
-                                                          const float* __restrict__ w, float* __restrict__ xn, int n,
+                                                          const float* __restrict__ w, NormOut out, int n,
                                                           double eps) {
-  extern __shared__ float s_h[];
+  extern __shared__ float s_h[];  // exact mode staging only
   __shared__ float sh[16];
   const int t = threadIdx.x;
   const uint8_t* row = table + (size_t)(*d_token) * row_bytes;
-  float sq = 0.0f;
-  for (int i = t; i < n; i += blockDim.x) {
-    const float v = deq_embed(type, row, i) * emb_scale;
-    resid[i] = v;
-    s_h[i] = v;
-    sq = fmaf(v, v, sq);
+  float ev[NORM_EPT], wv[NORM_EPT];
+#pragma unroll
+  for (int k = 0; k < NORM_EPT; k++) {
+    const int i = t + k * 1024;
+    const bool ok = i < n;
+    ev[k] = ok ? deq_embed(type, row, i) * emb_scale : 0.0f;
+    wv[k] = ok ? w[i] : 0.0f;
+    if (ok) resid[i] = ev[k];
   }
-  __syncthreads();
-  const float s1 = EXACT ? serial_sumsq(s_h, n, sh) : block_sum(sq, sh);
-  const float sc = rms_scale(s1, n, eps);
-  for (int i = t; i < n; i += blockDim.x) xn[i] = (sc * s_h[i]) * w[i];
+  const float sc = rms_scale(sumsq_regs<EXACT>(ev, n, s_h, sh), n, eps);
+  float xv[NORM_EPT];
+#pragma unroll
+  for (int k = 0; k < NORM_EPT; k++) xv[k] = (sc * ev[k]) * wv[k];
+  norm_outputs(xv, n, out);
 }
 
 __device__ float deq_embed(uint32_t type, const uint8_t* row, int i) {
@@ -325,15 +344,15 @@ __device__ float deq_embed(uint32_t type, const uint8_t* row, int i) {
 }
 
 void launch_embed_norm(uint32_t type, const uint8_t* table, size_t row_bytes, const int32_t* d_token,
-                       float emb_scale, float* resid, const float* w, float* xn, int n, double eps, bool exact,
-                       hipStream_t s) {
-  const size_t lds = (size_t)n * 4;
+                       float emb_scale, float* resid, const float* w, const NormOut& out, int n, double eps,
+                       bool exact, hipStream_t s) {
+  if (n > 1024 * NORM_EPT) throw std::runtime_error("embed_norm: n_embd > 8192");
   if (exact)
-    hipLaunchKernelGGL(embed_norm_kernel<true>, dim3(1), dim3(1024), lds, s, type, table, row_bytes, d_token,
-                       emb_scale, resid, w, xn, n, eps);
+    hipLaunchKernelGGL(embed_norm_kernel<true>, dim3(1), dim3(1024), (size_t)n * 4, s, type, table, row_bytes, d_token,
+                       emb_scale, resid, w, out, n, eps);
   else
-    hipLaunchKernelGGL(embed_norm_kernel<false>, dim3(1), dim3(1024), lds, s, type, table, row_bytes, d_token,
-                       emb_scale, resid, w, xn, n, eps);
+    hipLaunchKernelGGL(embed_norm_kernel<false>, dim3(1), dim3(1024), 0, s, type, table, row_bytes, d_token,
+                       emb_scale, resid, w, out, n, eps);
   LLMI_HIP(hipGetLastError());
 }
 

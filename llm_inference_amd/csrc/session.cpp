@@ -184,9 +184,8 @@ void Session::alloc_buffers() {
   hid_ = dalloc<float>(F);
   d_out_ = dalloc<float>(E);
   logits_ = dalloc<float>(vocab_);
-  act_.q8.qs = dalloc<int8_t>(maxcols);
-  act_.q8.d = dalloc<uint16_t>(maxcols / 32 + 1);
-  act_.q8.nsum8 = dalloc<int32_t>(maxcols / 32 + 1);
+  act_.q8.xb = dalloc<XBlock>(maxcols / 32 + 1);
+  act_.q8.nb = maxcols / 32;
   act_.q8k = dalloc<uint8_t>((size_t)(maxcols / 256 + 1) * 292);
   act_.x16 = dalloc<uint16_t>(maxcols);
   d_token_ = dalloc<int32_t>(1);
@@ -232,7 +231,8 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
   }
   use_graph_ = (opts.flags & LLMI_NO_GRAPH) == 0;
   max_ctx_ = opts.max_ctx > 0 ? opts.max_ctx : 4096;
-  nsplit_ = opts.attn_split > 0 ? opts.attn_split : 32;
+  nsplit_ = opts.attn_split > 0 ? opts.attn_split : 16;
+  if (nsplit_ != 16 && nsplit_ != 32) throw status_error(LLMI_E_ARG, "attn_split must be 16 or 32");
   LLMI_HIP(hipSetDevice(opts.device));
   LLMI_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   try {
@@ -300,9 +300,23 @@ void Session::record_step(hipStream_t s) {
   kernels_per_token_ = 0;
   const int E = hp_.n_embd, F = hp_.n_ff;
   const float emb_scale = std::sqrt(static_cast<float>(E));  // model.cpp:337-338
+  auto is_q8 = [](uint32_t t) { return t == T_Q4_0 || t == T_Q8_0; };
+  // a norm feeding GEMV parts also writes their Q8_0 activation when every
+  // part consumes Q8_0 (one fewer launch); x16 for the F16 logits GEMV
+  auto nout = [&](const std::vector<GemvPart>& consumer) {
+    NormOut o;
+    o.xn = xn_;
+    bool q8 = !consumer.empty();
+    for (const auto& p : consumer) q8 &= is_q8(p.w.type);
+    if (q8) o.q8 = act_.q8.xb;
+    return o;
+  };
+  bool x_q8 = false;  // xn_'s Q8_0 blocks are already in act_
   if (embd_.type == T_F16 || embd_.type == T_Q8_0) {
-    launch_embed_norm(embd_.type, embd_raw_, embd_row_bytes_, d_token_, emb_scale, resid_, L_[0].attn_norm, xn_, E,
+    const NormOut o = nout(L_[0].qkv);
+    launch_embed_norm(embd_.type, embd_raw_, embd_row_bytes_, d_token_, emb_scale, resid_, L_[0].attn_norm, o, E,
                       hp_.eps, ex_norm_, s);
+    x_q8 = o.q8 != nullptr;
     kernels_per_token_++;
   } else {
     launch_dequantize_rows(embd_.type, embd_raw_, embd_row_bytes_, d_token_, 1, E, emb_scale, resid_, s);
@@ -312,29 +326,39 @@ void Session::record_step(hipStream_t s) {
   for (int l = 0; l < hp_.n_layer; l++) {
     LayerDev& Ld = L_[l];
     const int hd = Ld.hd;
-    gemv_parts(Ld.qkv, xn_, E, qkv_, s, false);
+    gemv_parts(Ld.qkv, xn_, E, qkv_, s, x_q8);
     QKVArgs qa{qkv_, Ld.k_off, Ld.v_off, hp_.n_head, hp_.n_head_kv, hd, Ld.q_norm, Ld.k_norm,
                Ld.is_swa ? rope_swa_ : rope_glb_, hp_.attn_scale, hp_.eps, q_, Ld.kc, Ld.vc, max_ctx_, d_pos_};
-    launch_qk_norm_rope_kv(qa, ex_norm_, s);
+    const bool fuse_qk = !ex_attn_ && !ex_norm_;  // norm/rope/KV-append inside the attention launch
+    if (!fuse_qk) {
+      launch_qk_norm_rope_kv(qa, ex_norm_, s);
+      kernels_per_token_++;
+    }
     AttnArgs aa{q_, Ld.kc, Ld.vc, hp_.n_head, hp_.n_head_kv, hd, max_ctx_, d_pos_, part_, attn_};
-    const bool o_q8 = Ld.o.w.type == T_Q4_0 || Ld.o.w.type == T_Q8_0;
+    const bool o_q8 = is_q8(Ld.o.w.type);
     const bool fused_q8 = !ex_attn_ && o_q8 && hd % 32 == 0;
-    launch_attention(aa, ex_attn_, nsplit_, fused_q8 ? &act_.q8 : nullptr, s);
-    kernels_per_token_ += ex_attn_ ? 2 : 3;
+    launch_attention(aa, ex_attn_, nsplit_, fused_q8 ? &act_.q8 : nullptr, s, fuse_qk ? &qa : nullptr);
+    kernels_per_token_ += ex_attn_ ? 1 : 2;
     gemv_parts({Ld.o}, attn_, hp_.n_head * hd, o_out_, s, fused_q8);
-    launch_residual_norm(o_out_, Ld.post_attn_norm, resid_, Ld.ffn_norm, xn_, E, hp_.eps, ex_norm_, s);
+    NormOut o1 = nout(Ld.gate_up);
+    launch_residual_norm(o_out_, Ld.post_attn_norm, resid_, Ld.ffn_norm, o1, E, hp_.eps, ex_norm_, s);
     kernels_per_token_++;
-    gemv_parts(Ld.gate_up, xn_, E, gu_, s, false);
+    gemv_parts(Ld.gate_up, xn_, E, gu_, s, o1.q8 != nullptr);
     const bool d_q8 = Ld.down.w.type == T_Q4_0 || Ld.down.w.type == T_Q8_0;
     launch_gelu_quant(gu_, F, hid_, d_q8 ? &act_.q8 : nullptr, s);
     kernels_per_token_++;
     gemv_parts({Ld.down}, hid_, F, d_out_, s, d_q8);
-    const float* w_next = l + 1 < hp_.n_layer ? L_[l + 1].attn_norm : out_norm_;
-    launch_residual_norm(d_out_, Ld.post_ffw_norm, resid_, w_next, xn_, E, hp_.eps, ex_norm_, s);
+    const bool last = l + 1 == hp_.n_layer;
+    const float* w_next = last ? out_norm_ : L_[l + 1].attn_norm;
+    NormOut o2 = last ? NormOut{} : nout(L_[l + 1].qkv);
+    o2.xn = xn_;
+    if (last && embd_.type == T_F16) o2.x16 = act_.x16;  // logits input, ops.cpp:542-551
+    launch_residual_norm(d_out_, Ld.post_ffw_norm, resid_, w_next, o2, E, hp_.eps, ex_norm_, s);
+    x_q8 = o2.q8 != nullptr;
     kernels_per_token_++;
   }
   // logits (model.cpp:993-1034): F16 table -> mat_vec_mul_fp16, else mat_vec_mul
-  prepare_act(embd_.type, xn_, E, act_, s);
+  if (embd_.type != T_F16) prepare_act(embd_.type, xn_, E, act_, s);
   const bool fold = !ex_logits_ && embd_.type == T_F16 && E % 8 == 0;
   launch_gemv(embd_, act_, logits_, ex_logits_ ? GEMV_EXACT : GEMV_FAST, s, fold ? amax_key_ : nullptr);
   kernels_per_token_++;

@@ -12,11 +12,18 @@ DevWeight alloc_weight(uint32_t type, int rows, int cols);
 void upload_rows(DevWeight& w, int dst_row0, const void* host, int rows, hipStream_t s);
 void free_weight(DevWeight& w);
 
-void launch_residual_norm(const float* y, const float* w_post, float* resid, const float* w_next, float* xn, int n,
-                          double eps, bool exact, hipStream_t s);
+// outputs of a norm that feeds a GEMV: xn (always), plus optionally the Q8_0
+// blocks and/or the f16-rounded copy the next GEMV consumes
+struct NormOut {
+  float* xn = nullptr;
+  XBlock* q8 = nullptr;
+  uint16_t* x16 = nullptr;
+};
+void launch_residual_norm(const float* y, const float* w_post, float* resid, const float* w_next, const NormOut& out,
+                          int n, double eps, bool exact, hipStream_t s);
 void launch_embed_norm(uint32_t type, const uint8_t* table, size_t row_bytes, const int32_t* d_token,
-                       float emb_scale, float* resid, const float* w, float* xn, int n, double eps, bool exact,
-                       hipStream_t s);
+                       float emb_scale, float* resid, const float* w, const NormOut& out, int n, double eps,
+                       bool exact, hipStream_t s);
 void launch_gelu_quant(const float* gu, int n, float* hid, const Q8Act* q8, hipStream_t s);
 void launch_argmax(const float* x, int n, unsigned long long* key, hipStream_t s);
 void launch_finalize_token(unsigned long long* key, int32_t* d_token, int32_t* d_pos, int32_t* ring,
