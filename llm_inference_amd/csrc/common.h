@@ -151,6 +151,11 @@ __device__ __forceinline__ void q8_block_store(float v, bool ok, XBlock* blk, in
 }
 
 // f / nb for f < 2^20, nb < 2^12 by one mul-hi (magic = 2^32/nb + 1)
-__host__ __device__ inline uint32_t div_magic(uint32_t nb) { return (uint32_t)((1ull << 32) / nb + 1); }
+// f / nb by multiply-high for the small f of one wave's chunk; nb == 1 has
+// no 32-bit magic and is encoded as 0
+__host__ __device__ inline uint32_t div_magic(uint32_t nb) { return nb == 1 ? 0u : (uint32_t)((1ull << 32) / nb + 1); }
+__device__ __forceinline__ int div_by_magic(int f, uint32_t magic) {
+  return magic ? (int)__umulhi((uint32_t)f, magic) : f;
+}
 
 }  // namespace llmi

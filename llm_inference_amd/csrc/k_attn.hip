@@ -135,10 +135,10 @@ __global__ __launch_bounds__(256) void attn_exact_kernel(AttnArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// fast split-K attention ("flash-decoding"): grid (n_head, n_split), one wave
-// per block.  Block c walks key tiles c, c+n_split, ... of 64 keys (lane per
-// key for QK^T, lane per head-dim slice for PV), keeping an online-softmax
-// partial (m, l, acc[hd]) in fp32.  attn_combine merges the n_split partials.
+// fast split-K attention ("flash-decoding"): grid (n_head_kv, n_split).
+// Work-group c walks key tiles c, c+n_split, ... of 64 keys keeping an
+// online-softmax partial (m, l, acc[hd]) per query head in fp32;
+// attn_combine merges the n_split partials.
 // ---------------------------------------------------------------------------
 // q/k head row norm (model.cpp:762/792, fast sum) + NEOX rope at the table row
 // `cs` (ops.cpp:88-91 contraction) for a row held DPL elements per lane.
@@ -169,121 +169,173 @@ __device__ __forceinline__ void norm_rope_row(const float* __restrict__ src, con
   }
 }
 
-// FUSED (session fast path): the block also performs the q/k per-head norm,
-// rope and q scale of qk_norm_rope_kv_kernel, and the KV append of the current
-// position: the block whose tile holds `pos` computes k/v of this token in
-// registers, scores/accumulates that key from registers (no global write ->
-// read hand-off inside the launch) and writes it to the cache for later steps.
-template <int HD, bool FUSED>
-__global__ __launch_bounds__(64) void attn_partial_kernel(AttnArgs a, QKVArgs qa) {
-  constexpr int DPL = HD >= 64 ? HD / 64 : 1;  // head dims per lane in the PV phase
-  __shared__ __attribute__((aligned(16))) uint16_t s_q[HD];
-  __shared__ float s_p[64];
-  const int lane = threadIdx.x;
-  const bool pv_lane = (lane * DPL) < HD;
-  const int h = blockIdx.x, c = blockIdx.y, nsplit = gridDim.y;
-  const int group = a.n_head / a.n_head_kv;
-  const int hkv = h / group;
+// One work-group of 256 threads per (kv head, split) covering all G = n_head /
+// n_head_kv query heads of that kv head, so each K/V tile is read from HBM
+// once per split.  Per 64-key tile: every thread issues its 16-byte K and V
+// chunk loads together (the tile is one contiguous 2*64*HD*2-byte stream),
+// stores them to LDS, then
+//   QK^T: TP threads per (query head, key) pair, interleaved 16-byte chunks,
+//         v_dot2 f16 products in fp32, K rows padded by TP*16 bytes so the
+//         ds_read_b128 of 16 lanes hit 16 distinct bank groups;
+//   softmax: wave g keeps head g's running (m, l);
+//   PV: thread owns one head dim (for all G heads) over a key residue class.
+// FUSED (session fast path): the work-group also performs the q/k per-head
+// norm, rope and q scale of qk_norm_rope_kv_kernel and the KV append of this
+// token; the split owning `pos` substitutes the new k/v rows from LDS for the
+// cache rows it is writing in the same launch.
+template <int HD, int G, bool FUSED>
+__global__ __launch_bounds__(256) void attn_partial_kernel(AttnArgs a, QKVArgs qa) {
+  constexpr int CH = HD / 8;                         // 16-byte chunks per row
+  constexpr int TP0 = 4 / G;                         // threads per (head, key) pair
+  constexpr int TP = TP0 < CH ? TP0 : CH;
+  constexpr int KS = HD + 8 * TP;                    // padded K row stride (halves)
+  constexpr int NLD = (64 * CH + 255) / 256;         // chunk loads per thread per tile
+  constexpr int KP = 256 / HD;                       // key residue classes in PV
+  __shared__ __attribute__((aligned(16))) uint16_t s_k[64 * KS];
+  __shared__ __attribute__((aligned(16))) uint16_t s_v[64 * HD];
+  __shared__ __attribute__((aligned(16))) uint16_t s_q[G][HD];
+  __shared__ __attribute__((aligned(16))) uint16_t s_new[FUSED ? 2 : 1][FUSED ? HD : 8];
+  __shared__ float s_p[G][64];
+  __shared__ float s_alpha[G];
+  __shared__ float s_red[KP > 1 ? KP * G * HD : 1];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int hkv = blockIdx.x, c = blockIdx.y, nsplit = gridDim.y;
   const int pos = *a.d_pos;
   const int n_keys = pos + 1;
   const bool own_new = FUSED && (pos / 64) % nsplit == c;
-  float knew[DPL], vnew[DPL];
-  float s_new = 0.0f;
   if (FUSED) {
     const float* cs = qa.rope_cs + (size_t)pos * (HD / 2) * 2;
-    float qr[DPL];
-    norm_rope_row<HD>(qa.qkv + (size_t)h * HD, qa.q_norm_w, cs, qa.eps, qr);
-#pragma unroll
-    for (int d = 0; d < DPL; d++)
-      if (pv_lane) s_q[lane * DPL + d] = f2h_ggml(qr[d] * qa.attn_scale);
-    if (own_new) {
-      norm_rope_row<HD>(qa.qkv + qa.k_off + (size_t)hkv * HD, qa.k_norm_w, cs, qa.eps, knew);
-      float part = 0.0f;
-#pragma unroll
-      for (int d = 0; d < DPL; d++) {
-        const uint16_t k16 = f2h_ggml(knew[d]);
-        const uint16_t v16 = f2h_ggml(pv_lane ? qa.qkv[qa.v_off + (size_t)hkv * HD + lane * DPL + d] : 0.0f);
-        knew[d] = h2f(k16);
-        vnew[d] = h2f(v16);
-        if (pv_lane && h % group == 0) {  // one writer per kv head
-          const size_t ci = ((size_t)hkv * a.max_ctx + pos) * HD + lane * DPL + d;
-          qa.k_cache[ci] = k16;
-          qa.v_cache[ci] = v16;
-        }
-      }
-      __syncthreads();  // s_q complete
+    constexpr int DPL = HD >= 64 ? HD / 64 : 1;
+    const bool ok = lane * DPL < HD;
+    if (w < G) {
+      float qr[DPL];
+      norm_rope_row<HD>(qa.qkv + (size_t)(hkv * G + w) * HD, qa.q_norm_w, cs, qa.eps, qr);
 #pragma unroll
       for (int d = 0; d < DPL; d++)
-        if (pv_lane) part = fmaf(knew[d], h2f(s_q[lane * DPL + d]), part);
-      s_new = wave_sum(part);
+        if (ok) s_q[w][lane * DPL + d] = f2h_ggml(qr[d] * qa.attn_scale);
+    }
+    if (own_new && w == (G & 3)) {
+      float kr[DPL];
+      norm_rope_row<HD>(qa.qkv + qa.k_off + (size_t)hkv * HD, qa.k_norm_w, cs, qa.eps, kr);
+#pragma unroll
+      for (int d = 0; d < DPL; d++) {
+        const uint16_t k16 = f2h_ggml(kr[d]);
+        if (ok) {
+          s_new[0][lane * DPL + d] = k16;
+          qa.k_cache[((size_t)hkv * a.max_ctx + pos) * HD + lane * DPL + d] = k16;
+        }
+      }
+    }
+    if (own_new && w == ((G + 1) & 3)) {
+      for (int i = lane; i < HD; i += 64) {
+        const uint16_t v16 = f2h_ggml(qa.qkv[qa.v_off + (size_t)hkv * HD + i]);
+        s_new[FUSED ? 1 : 0][i] = v16;
+        qa.v_cache[((size_t)hkv * a.max_ctx + pos) * HD + i] = v16;
+      }
     }
   } else {
-    for (int i = lane; i < HD; i += 64) s_q[i] = f2h_ggml(a.q[(size_t)h * HD + i]);
+    for (int i = t; i < G * HD; i += 256) s_q[i / HD][i % HD] = f2h_ggml(a.q[(size_t)hkv * G * HD + i]);
   }
-  __syncthreads();
   const uint4* kb = reinterpret_cast<const uint4*>(a.k_cache + (size_t)hkv * a.max_ctx * HD);
-  const uint16_t* vb = a.v_cache + (size_t)hkv * a.max_ctx * HD;
-  float m_run = -INFINITY, l_run = 0.0f;
-  float acc[DPL];
+  const uint4* vb = reinterpret_cast<const uint4*>(a.v_cache + (size_t)hkv * a.max_ctx * HD);
+  float m_run = -INFINITY, l_run = 0.0f;  // head w's running max / sum (waves w < G)
+  float acc[G];
 #pragma unroll
-  for (int d = 0; d < DPL; d++) acc[d] = 0.0f;
+  for (int g = 0; g < G; g++) acc[g] = 0.0f;
+  const int d_own = t % HD, kp = t / HD;
   typedef _Float16 h2t __attribute__((ext_vector_type(2)));
   for (int tile = c; tile * 64 < n_keys; tile += nsplit) {
-    const int key = tile * 64 + lane;
-    float sc = -INFINITY;
-    if (FUSED && key == pos) {
-      sc = s_new;
-    } else if (key < n_keys) {
-      const uint4* kr = kb + (size_t)key * (HD / 8);
-      const uint4* qv = reinterpret_cast<const uint4*>(s_q);
+    uint4 kr[NLD], vr[NLD];
+#pragma unroll
+    for (int i = 0; i < NLD; i++) {
+      const int k = i * 256 + t;
+      const int key = tile * 64 + k / CH;
+      kr[i] = make_uint4(0, 0, 0, 0);
+      vr[i] = make_uint4(0, 0, 0, 0);
+      if (k < 64 * CH && key < n_keys) {
+        const size_t gi = (size_t)tile * 64 * CH + k;
+        kr[i] = kb[gi];
+        vr[i] = vb[gi];
+      }
+    }
+    __syncthreads();  // previous tile's LDS reads done (and, first time, s_q / s_new written)
+#pragma unroll
+    for (int i = 0; i < NLD; i++) {
+      const int k = i * 256 + t;
+      const int j = k / CH, pc = k % CH;
+      if (k < 64 * CH && !(FUSED && tile * 64 + j == pos)) {
+        *reinterpret_cast<uint4*>(&s_k[j * KS + pc * 8]) = kr[i];
+        *reinterpret_cast<uint4*>(&s_v[j * HD + pc * 8]) = vr[i];
+      }
+    }
+    if (FUSED && tile == pos / 64 && t < CH) {  // the new row, written in this launch
+      const int j = pos % 64;
+      *reinterpret_cast<uint4*>(&s_k[j * KS + t * 8]) = reinterpret_cast<const uint4*>(s_new[0])[t];
+      *reinterpret_cast<uint4*>(&s_v[j * HD + t * 8]) = reinterpret_cast<const uint4*>(s_new[FUSED ? 1 : 0])[t];
+    }
+    __syncthreads();
+    if (t < G * 64 * TP) {
+      const int pr = t / TP, part = t % TP;
+      const int g = pr / 64, j = pr % 64;
+      const uint4* krow = reinterpret_cast<const uint4*>(&s_k[j * KS]);
+      const uint4* qrow = reinterpret_cast<const uint4*>(s_q[g]);
       float s0 = 0.0f, s1 = 0.0f;
-#pragma unroll 8
-      for (int i = 0; i < HD / 8; i++) {
-        const uint4 kk = kr[i], qq = qv[i];
+#pragma unroll
+      for (int i = 0; i < CH / TP; i++) {
+        const uint4 kk = krow[i * TP + part], qq = qrow[i * TP + part];
         s0 = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2t, kk.x), __builtin_bit_cast(h2t, qq.x), s0, false);
         s1 = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2t, kk.y), __builtin_bit_cast(h2t, qq.y), s1, false);
         s0 = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2t, kk.z), __builtin_bit_cast(h2t, qq.z), s0, false);
         s1 = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2t, kk.w), __builtin_bit_cast(h2t, qq.w), s1, false);
       }
-      sc = s0 + s1;
+      float sc = s0 + s1;
+#pragma unroll
+      for (int o = 1; o < TP; o <<= 1) sc += __shfl_xor(sc, o);
+      if (part == 0) s_p[g][j] = tile * 64 + j < n_keys ? sc : -INFINITY;
     }
-    const float m_tile = wave_max(sc);
-    const float m_new = fmaxf(m_run, m_tile);
-    const float p = key < n_keys ? expf(sc - m_new) : 0.0f;
-    const float alpha = expf(m_run - m_new);  // m_run = -inf on the first tile -> 0
-    l_run = l_run * alpha + wave_sum(p);
-    m_run = m_new;
-    s_p[lane] = p;
     __syncthreads();
-    const int nk = min(64, n_keys - tile * 64);
+    if (w < G) {
+      const float sc = s_p[w][lane];
+      const float m_new = fmaxf(m_run, wave_max(sc));
+      const float p = expf(sc - m_new);  // masked keys: exp(-inf) = 0
+      const float alpha = expf(m_run - m_new);  // first tile: exp(-inf) = 0
+      l_run = l_run * alpha + wave_sum(p);
+      m_run = m_new;
+      s_p[w][lane] = p;
+      if (lane == 0) s_alpha[w] = alpha;
+    }
+    __syncthreads();
 #pragma unroll
-    for (int d = 0; d < DPL; d++) acc[d] *= alpha;
+    for (int g = 0; g < G; g++) acc[g] *= s_alpha[g];
 #pragma unroll 8
-    for (int j = 0; j < nk && pv_lane; j++) {
-      const float pj = s_p[j];
-      const uint16_t* vr = vb + (size_t)(tile * 64 + j) * HD + lane * DPL;
-      if (FUSED && tile * 64 + j == pos) {
+    for (int j = kp; j < 64; j += KP) {
+      const float v = h2f(s_v[j * HD + d_own]);
 #pragma unroll
-        for (int d = 0; d < DPL; d++) acc[d] = fmaf(pj, vnew[d], acc[d]);
-      } else if constexpr (DPL == 4) {
-        const uint2 vv = *reinterpret_cast<const uint2*>(vr);
-        acc[0] = fmaf(pj, h2f((uint16_t)(vv.x & 0xFFFF)), acc[0]);
-        acc[1] = fmaf(pj, h2f((uint16_t)(vv.x >> 16)), acc[1]);
-        acc[2] = fmaf(pj, h2f((uint16_t)(vv.y & 0xFFFF)), acc[2]);
-        acc[3] = fmaf(pj, h2f((uint16_t)(vv.y >> 16)), acc[3]);
-      } else {
+      for (int g = 0; g < G; g++) acc[g] = fmaf(s_p[g][j], v, acc[g]);
+    }
+  }
+  if constexpr (KP > 1) {
 #pragma unroll
-        for (int d = 0; d < DPL; d++) acc[d] = fmaf(pj, h2f(vr[d]), acc[d]);
+    for (int g = 0; g < G; g++) s_red[(kp * G + g) * HD + d_own] = acc[g];
+    __syncthreads();
+    if (kp == 0) {
+#pragma unroll
+      for (int g = 0; g < G; g++) {
+        float s = acc[g];
+        for (int r = 1; r < KP; r++) s += s_red[(r * G + g) * HD + d_own];
+        acc[g] = s;
       }
     }
-    __syncthreads();
   }
-  float* part = a.partial + ((size_t)h * nsplit + c) * (HD + 2);
-  if (pv_lane) {
+  if (kp == 0) {
 #pragma unroll
-    for (int d = 0; d < DPL; d++) part[lane * DPL + d] = acc[d];
+    for (int g = 0; g < G; g++) a.partial[((size_t)(hkv * G + g) * nsplit + c) * (HD + 2) + d_own] = acc[g];
   }
-  if (lane == 0) { part[HD] = m_run; part[HD + 1] = l_run; }
+  if (w < G && lane == 0) {
+    float* part = a.partial + ((size_t)(hkv * G + w) * nsplit + c) * (HD + 2);
+    part[HD] = m_run;
+    part[HD + 1] = l_run;
+  }
 }
 
 // merge split partials per head; optionally quantize the head's output to
@@ -317,13 +369,23 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(AttnArgs a, Q8Act q8)
   if (q8.xb != nullptr && t < hd) q8_block_store(val, true, q8.xb + ((h * hd + t) >> 5), t & 31);  // ops.cpp:116-139
 }
 
+template <int HD, int G>
+static void launch_partial_g(const AttnArgs& a, const QKVArgs* fused, int nsplit, hipStream_t s) {
+  const dim3 grid(a.n_head_kv, nsplit);
+  if (fused)
+    hipLaunchKernelGGL((attn_partial_kernel<HD, G, true>), grid, dim3(256), 0, s, a, *fused);
+  else
+    hipLaunchKernelGGL((attn_partial_kernel<HD, G, false>), grid, dim3(256), 0, s, a, QKVArgs{});
+}
+
 template <int HD>
 static void launch_partial(const AttnArgs& a, const QKVArgs* fused, int nsplit, hipStream_t s) {
-  const dim3 grid(a.n_head, nsplit);
-  if (fused)
-    hipLaunchKernelGGL((attn_partial_kernel<HD, true>), grid, dim3(64), 0, s, a, *fused);
-  else
-    hipLaunchKernelGGL((attn_partial_kernel<HD, false>), grid, dim3(64), 0, s, a, QKVArgs{});
+  switch (a.n_head / a.n_head_kv) {
+    case 1: launch_partial_g<HD, 1>(a, fused, nsplit, s); break;
+    case 2: launch_partial_g<HD, 2>(a, fused, nsplit, s); break;
+    case 4: launch_partial_g<HD, 4>(a, fused, nsplit, s); break;
+    default: throw std::runtime_error("attention: GQA group must be 1, 2 or 4");
+  }
 }
 
 void launch_attention(const AttnArgs& a, bool exact, int nsplit, const Q8Act* q8, hipStream_t s,
@@ -333,7 +395,8 @@ void launch_attention(const AttnArgs& a, bool exact, int nsplit, const Q8Act* q8
     LLMI_HIP(hipGetLastError());
     return;
   }
-  if (nsplit != 16 && nsplit != 32) throw std::runtime_error("attention: nsplit must be 16 or 32");
+  if (nsplit != 16 && nsplit != 32 && nsplit != 64) throw std::runtime_error("attention: nsplit must be 16, 32 or 64");
+  if (a.n_head_kv <= 0 || a.n_head % a.n_head_kv != 0) throw std::runtime_error("attention: n_head % n_head_kv != 0");
   switch (a.head_dim) {
     case 16: launch_partial<16>(a, fused, nsplit, s); break;
     case 32: launch_partial<32>(a, fused, nsplit, s); break;
@@ -346,8 +409,10 @@ void launch_attention(const AttnArgs& a, bool exact, int nsplit, const Q8Act* q8
   const Q8Act qq = q8 ? *q8 : Q8Act{};
   if (nsplit == 16)
     hipLaunchKernelGGL(attn_combine_kernel<16>, dim3(a.n_head), dim3(256), 0, s, a, qq);
-  else
+  else if (nsplit == 32)
     hipLaunchKernelGGL(attn_combine_kernel<32>, dim3(a.n_head), dim3(256), 0, s, a, qq);
+  else
+    hipLaunchKernelGGL(attn_combine_kernel<64>, dim3(a.n_head), dim3(256), 0, s, a, qq);
   LLMI_HIP(hipGetLastError());
 }
 

@@ -89,7 +89,7 @@ __global__ __launch_bounds__(256) void gemv_q4_0_fast(const uint4* __restrict__ 
     for (int p = 0; p < P; p++) {
       const int f = c0 + p * 64 + lane;
       const int fc = f < total ? f : 0;
-      const int r = (int)__umulhi((uint32_t)fc, magic);
+      const int r = div_by_magic(fc, magic);
       rr[p] = f < total ? r : R;
       bb[p] = fc - r * nb;
       q[p] = ld_nt(qw + fc);
@@ -159,7 +159,7 @@ __global__ __launch_bounds__(256) void gemv_q8_0_fast(const int4* __restrict__ q
     for (int p = 0; p < P; p++) {
       const int f = c0 + p * 64 + lane;
       const int fc = f < total ? f : 0;
-      const int r = (int)__umulhi((uint32_t)fc, magic);
+      const int r = div_by_magic(fc, magic);
       rr[p] = f < total ? r : R;
       bb[p] = fc - r * nb;
       w0[p] = ld_nt(qw + 2 * fc);
@@ -285,7 +285,7 @@ __global__ __launch_bounds__(256) void gemv_f16_fast(const uint4* __restrict__ w
     for (int p = 0; p < P; p++) {
       const int f = c0 + p * 64 + lane;
       const int fc = f < total ? f : 0;
-      const int r = (int)__umulhi((uint32_t)fc, magic);
+      const int r = div_by_magic(fc, magic);
       rr[p] = f < total ? r : R;
       cc[p] = fc - r * nc;
       wv[p] = ld_nt(wr + fc);

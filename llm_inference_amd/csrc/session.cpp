@@ -231,8 +231,8 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
   }
   use_graph_ = (opts.flags & LLMI_NO_GRAPH) == 0;
   max_ctx_ = opts.max_ctx > 0 ? opts.max_ctx : 4096;
-  nsplit_ = opts.attn_split > 0 ? opts.attn_split : 16;
-  if (nsplit_ != 16 && nsplit_ != 32) throw status_error(LLMI_E_ARG, "attn_split must be 16 or 32");
+  nsplit_ = opts.attn_split > 0 ? opts.attn_split : 32;
+  if (nsplit_ != 16 && nsplit_ != 32 && nsplit_ != 64) throw status_error(LLMI_E_ARG, "attn_split must be 16, 32 or 64");
   LLMI_HIP(hipSetDevice(opts.device));
   LLMI_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   try {

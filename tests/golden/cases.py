@@ -25,8 +25,11 @@ GEMV_CASES = [
     ("q4_0_6912", T.Q4_0, 40, 6912),      # 1B ffn_down
     ("q4_0_5376", T.Q4_0, 40, 5376),      # 27B q/k/v/gate/up
     ("q4_0_96", T.Q4_0, 7, 96),           # ragged tiny: 3 blocks, 7 rows
+    ("q4_0_32", T.Q4_0, 5, 32),           # one block per row (ModelTest n_embd)
+    ("q4_0_64", T.Q4_0, 9, 64),
     ("q8_0_1152", T.Q8_0, 64, 1152),
     ("q8_0_2560", T.Q8_0, 64, 2560),
+    ("q8_0_32", T.Q8_0, 3, 32),
     ("q4_k_2560", T.Q4_K, 64, 2560),
     ("q6_k_2560", T.Q6_K, 64, 2560),
     ("q6_k_10240", T.Q6_K, 24, 10240),

@@ -12,8 +12,10 @@ Tolerances:
     differences are amplified on random-init models: the reference vs the
     same reference with float64 attention differ by up to 3.7e-2 on mini-1b
     (scripts/diag_parts.py).  Fast mode is therefore held to |dlogit| <=
-    6e-2 vs the reference (the reference's own attention-rounding spread,
-    x1.6), with greedy token ids identical.
+    6e-2 vs the oracle with float64 attention, and vs the reference to
+    6e-2 + |reference - f64-attention oracle| on the same input (the
+    reference's own attention rounding; 8.4e-2 on ModelTest's 2nd token),
+    with greedy token ids identical.
   both modes: greedy token ids identical to the reference.
 """
 import os
@@ -37,7 +39,11 @@ def check(got, ref, ideal, exact):
     else:
         print(f"fast: vs_ref {np.abs(got - ref).max():.3g} vs_f64attn {np.abs(got - ideal).max():.3g} "
               f"(ref vs f64attn {np.abs(ref - ideal).max():.3g})")
-        np.testing.assert_allclose(got, ref, atol=FAST_VS_REF, rtol=0)
+        # the f64-attention restatement is the target; vs the reference itself
+        # the budget grows by the reference's own attention-rounding deviation
+        # measured on this very input (|ref - ideal|)
+        np.testing.assert_allclose(got, ideal, atol=FAST_VS_REF, rtol=0)
+        np.testing.assert_allclose(got, ref, atol=FAST_VS_REF + float(np.abs(ref - ideal).max()), rtol=0)
 
 
 def test_model_test_gguf(oracle, golden_models, exact):
