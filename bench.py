@@ -166,7 +166,7 @@ def main():
             "frac_of_peak": round(tok_bytes * value / d.world / 1e9 / PEAK_HBM_GBS, 4),
         },
         "roofline": {
-            "kernel": "gemv_q4_0_fast (all Q4_0 GEMV launches of one token, decode order)",
+            "kernel": "Q4_0 projection GEMVs of one token in decode order (gemv_q4_0_layer on the fast path: qkv, o, gate_up+GELU, down)",
             "bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
             "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": None,
             "us_per_launch": round(us, 3), "bytes_per_launch": int(by),

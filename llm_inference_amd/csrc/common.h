@@ -67,6 +67,13 @@ __device__ __forceinline__ int nearest_int_fma(float a, float b) {
   return (int)(__float_as_uint(fmaf(a, b, 12582912.f)) & 0x007fffffu) - 0x00400000;
 }
 
+// GELU(tanh)(x) * u (model.cpp:892-899; model.cpp is built without FMA)
+__device__ __forceinline__ float gelu_mul1(float x, float u) {
+  const float c = __uint_as_float(0x3F4C4229u);  // sqrtf((float)(2.0 / M_PI)) = 0.79788452f
+  const float inner = x + ((0.044715f * x) * x) * x;
+  return ((0.5f * x) * (1.0f + tanhf(c * inner))) * u;
+}
+
 __device__ __forceinline__ int sdot4(int a, int b, int c) { return __builtin_amdgcn_sdot4(a, b, c, false); }
 
 // streamed-once weight loads: non-temporal 16-B global loads (MI355X_MICROARCH
@@ -150,7 +157,6 @@ __device__ __forceinline__ void q8_block_store(float v, bool ok, XBlock* blk, in
   }
 }
 
-// f / nb for f < 2^20, nb < 2^12 by one mul-hi (magic = 2^32/nb + 1)
 // f / nb by multiply-high for the small f of one wave's chunk; nb == 1 has
 // no 32-bit magic and is encoded as 0
 __host__ __device__ inline uint32_t div_magic(uint32_t nb) { return nb == 1 ? 0u : (uint32_t)((1ull << 32) / nb + 1); }

@@ -202,12 +202,6 @@ void launch_vec_mad_f16(uint16_t* y, const uint16_t* x, int n, float v, hipStrea
   LLMI_HIP(hipGetLastError());
 }
 
-// GELU(tanh) * up (model.cpp:892-899; model.cpp is built without FMA)
-__device__ __forceinline__ float gelu_mul1(float x, float u) {
-  const float c = __uint_as_float(0x3F4C4229u);  // sqrtf((float)(2.0 / M_PI)) = 0.79788452f
-  const float inner = x + ((0.044715f * x) * x) * x;
-  return ((0.5f * x) * (1.0f + tanhf(c * inner))) * u;
-}
 __global__ void gelu_mul_kernel(const float* g, const float* u, float* o, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) o[i] = gelu_mul1(g[i], u[i]);

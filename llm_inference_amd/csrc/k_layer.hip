@@ -1,0 +1,262 @@
+// k_layer.hip -- the decode step's Q4_0 GEMVs with their neighbours fused in.
+//
+// One launch per projection instead of norm / quantize / GEMV / GELU launches:
+//   PRO  : the residual step that precedes the GEMV (model.cpp:843-858 and
+//          915-924 + the next run_norm) is recomputed by every work-group from
+//          the previous GEMV's output -- h = resid + rms(y)*w_post,
+//          x = rms(h)*w_next, Q8_0 blocks of x (ops.cpp:116-139) -- straight
+//          into LDS.  Work-group 0 publishes h (resid_out, a ping-pong buffer:
+//          the other work-groups of the same launch still read resid_in).
+//   !PRO : the activation's Q8_0 blocks are copied global -> LDS once per WG.
+//   GELU : gate/up rows are interleaved in groups of 32 at upload, so a WG of
+//          64 rows owns gate[32k..32k+31] and up[32k..32k+31]; it finishes
+//          GELU(gate)*up (model.cpp:892-899) for those 32 hidden units and
+//          their Q8_0 block for the down projection.
+// The weight stream is the gemv_q4_0_fast scheme (k_gemv.hip): a wave owns R
+// rows as a flat (row, block) item list, one 16-B non-temporal load per lane
+// per pass, a chunk of P passes in flight; the first chunk is issued before
+// the prologue so its HBM latency hides the prologue's L2 round trip, and
+// each later chunk is issued before the previous one is consumed.
+#include "session_kernels.h"
+
+namespace llmi {
+
+namespace {
+
+constexpr int PRO_EPT = 12;  // prologue elements per thread (n <= 12 * threads)
+
+__device__ __forceinline__ uint16_t ld_nt16(const uint16_t* p) { return __builtin_nontemporal_load(p); }
+__device__ __forceinline__ int nib_lo(uint32_t w) { return (int)(w & 0x0F0F0F0Fu); }
+__device__ __forceinline__ int nib_hi(uint32_t w) { return (int)((w >> 4) & 0x0F0F0F0Fu); }
+
+template <int NW>
+__device__ __forceinline__ float wg_sum(float v, float* red) {  // fixed order, identical in every WG
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  float s = 0.0f;
+#pragma unroll
+  for (int i = 0; i < NW; i++) s += red[i];
+  return s;
+}
+
+__device__ __forceinline__ float rms_scale_d(float sum, int n, double eps) {  // ops.cpp:37-38
+  return 1.0f / sqrtf((float)((double)(sum / (float)n) + eps));
+}
+
+template <int P>
+struct Chunk {
+  uint4 q[P];
+  float sw[P];
+  int rr[P], bb[P];
+};
+
+template <int R, int P>
+__device__ __forceinline__ void load_chunk(Chunk<P>& c, const uint4* qw, const uint16_t* dw, int c0, int total,
+                                           int nb, uint32_t magic, int lane) {
+#pragma unroll
+  for (int p = 0; p < P; p++) {
+    const int f = c0 + p * 64 + lane;
+    const int fc = f < total ? f : 0;
+    const int r = div_by_magic(fc, magic);
+    c.rr[p] = f < total ? r : R;
+    c.bb[p] = fc - r * nb;
+    c.q[p] = ld_nt(qw + fc);
+    c.sw[p] = h2f(ld_nt16(dw + fc));
+  }
+}
+
+template <int R, int P>
+__device__ __forceinline__ void eat_chunk(const Chunk<P>& c, const XBlock* s_x, float (&acc)[R]) {
+#pragma unroll
+  for (int p = 0; p < P; p++) {
+    const int4* xp = reinterpret_cast<const int4*>(s_x + c.bb[p]);
+    const int4 x0 = xp[0], x1 = xp[1], x2 = xp[2];
+    int is = x2.y;  // nsum8
+    is = sdot4(nib_lo(c.q[p].x), x0.x, is);
+    is = sdot4(nib_lo(c.q[p].y), x0.y, is);
+    is = sdot4(nib_lo(c.q[p].z), x0.z, is);
+    is = sdot4(nib_lo(c.q[p].w), x0.w, is);
+    is = sdot4(nib_hi(c.q[p].x), x1.x, is);
+    is = sdot4(nib_hi(c.q[p].y), x1.y, is);
+    is = sdot4(nib_hi(c.q[p].z), x1.z, is);
+    is = sdot4(nib_hi(c.q[p].w), x1.w, is);
+    const float v = (c.sw[p] * __int_as_float(x2.x)) * (float)is;
+#pragma unroll
+    for (int k = 0; k < R; k++) acc[k] += (k == c.rr[p]) ? v : 0.0f;
+  }
+}
+
+template <int R, int NW, int P, bool PRO, bool GELU>
+__global__ __launch_bounds__(NW * 64) void gemv_q4_0_layer(LayerGemv a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
+  XBlock* s_x = reinterpret_cast<XBlock*>(s_dyn);
+  __shared__ float s_red[2][NW];
+  __shared__ float s_rows[GELU ? 64 : 1];
+  constexpr int T = NW * 64;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int nb = a.nb;
+  const int row0 = (blockIdx.x * NW + w) * R;
+  const int nrows = max(0, min(R, a.rows - row0));
+  const int total = nrows * nb;
+  const uint4* qw = a.qs + (size_t)min(row0, a.rows - 1) * nb;
+  const uint16_t* dw = a.wd + (size_t)min(row0, a.rows - 1) * nb;
+
+  Chunk<P> ca, cb;
+  if (total > 0) load_chunk<R, P>(ca, qw, dw, 0, total, nb, a.magic, lane);
+
+  if constexpr (PRO) {
+    const int n = a.n;
+    float yv[PRO_EPT], rv[PRO_EPT], wp[PRO_EPT], wn[PRO_EPT];
+#pragma unroll
+    for (int k = 0; k < PRO_EPT; k++) {
+      const int i = t + k * T;
+      const bool ok = i < n;
+      yv[k] = ok ? a.y[i] : 0.0f;
+      rv[k] = ok ? a.resid_in[i] : 0.0f;
+      wp[k] = ok ? a.w_post[i] : 0.0f;
+      wn[k] = ok ? a.w_next[i] : 0.0f;
+    }
+    float ss = 0.0f;
+#pragma unroll
+    for (int k = 0; k < PRO_EPT; k++) ss = fmaf(yv[k], yv[k], ss);
+    const float sc1 = rms_scale_d(wg_sum<NW>(ss, s_red[0]), n, a.eps);
+    float ss2 = 0.0f;
+#pragma unroll
+    for (int k = 0; k < PRO_EPT; k++) {
+      const float h = rv[k] + (sc1 * yv[k]) * wp[k];
+      rv[k] = h;
+      ss2 = fmaf(h, h, ss2);
+      const int i = t + k * T;
+      if (blockIdx.x == 0 && i < n) a.resid_out[i] = h;
+    }
+    const float sc2 = rms_scale_d(wg_sum<NW>(ss2, s_red[1]), n, a.eps);
+#pragma unroll
+    for (int k = 0; k < PRO_EPT; k++) {
+      const int i = t + k * T;
+      if (k * T >= n) break;
+      const bool ok = i < n;
+      const float xv = (sc2 * rv[k]) * wn[k];
+      if (blockIdx.x == 0 && ok && a.xn_out) a.xn_out[i] = xv;
+      q8_block_store(xv, ok, s_x + (ok ? (i >> 5) : 0), i & 31);
+    }
+  } else {
+    const uint4* src = reinterpret_cast<const uint4*>(a.xg);
+    uint4* dst = reinterpret_cast<uint4*>(s_x);
+    for (int i = t; i < nb * 3; i += T) dst[i] = src[i];
+  }
+  __syncthreads();
+
+  float acc[R];
+#pragma unroll
+  for (int k = 0; k < R; k++) acc[k] = 0.0f;
+  constexpr int CH = 64 * P;
+  for (int c0 = 0; c0 < total; c0 += 2 * CH) {
+    if (c0 + CH < total) load_chunk<R, P>(cb, qw, dw, c0 + CH, total, nb, a.magic, lane);
+    eat_chunk<R, P>(ca, s_x, acc);
+    if (c0 + CH >= total) break;
+    if (c0 + 2 * CH < total) load_chunk<R, P>(ca, qw, dw, c0 + 2 * CH, total, nb, a.magic, lane);
+    eat_chunk<R, P>(cb, s_x, acc);
+  }
+
+  if constexpr (GELU) {
+#pragma unroll
+    for (int k = 0; k < R; k++) {
+      const float s = wave_sum(acc[k]);
+      if (lane == 0) s_rows[w * R + k] = s;
+    }
+    __syncthreads();
+    if (t < 32) {
+      const int j = blockIdx.x * 32 + t;  // hidden unit
+      const float v = gelu_mul1(s_rows[t], s_rows[32 + t]);
+      a.hid[j] = v;
+      q8_block_store(v, true, a.hq8 + blockIdx.x, t);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < R; k++) {
+      const float s = wave_sum(acc[k]);
+      if (lane == 0 && k < nrows) a.out[row0 + k] = s;
+    }
+  }
+}
+
+int rows_per_wave_l(int nb) {
+  int R = 1;
+  while (R < 8 && (R * nb) % 64 != 0) R *= 2;
+  return R;
+}
+
+// passes per chunk: split the wave's passes into ceil(passes/8) equal chunks,
+// rounded up to an instantiated P
+int passes_for(int R, int nb) {
+  const int passes = (R * nb + 63) / 64;
+  const int chunks = (passes + 7) / 8;
+  const int p = (passes + chunks - 1) / chunks;
+  return p == 3 ? 4 : p;
+}
+
+template <int R, int NW, bool PRO, bool GELU>
+void launch_rp(int P, dim3 grid, size_t lds, const LayerGemv& a, hipStream_t s) {
+  switch (P) {
+#define LLMI_L_CASE(PP) \
+  case PP: hipLaunchKernelGGL((gemv_q4_0_layer<R, NW, PP, PRO, GELU>), grid, dim3(NW * 64), lds, s, a); break;
+    LLMI_L_CASE(1) LLMI_L_CASE(2) LLMI_L_CASE(4) LLMI_L_CASE(5) LLMI_L_CASE(6) LLMI_L_CASE(7) LLMI_L_CASE(8)
+#undef LLMI_L_CASE
+    default: throw std::runtime_error("layer gemv: no kernel for P=" + std::to_string(P));
+  }
+}
+
+template <int NW, bool PRO, bool GELU>
+void launch_r(int R, int P, dim3 grid, size_t lds, const LayerGemv& a, hipStream_t s) {
+  switch (R) {
+    case 1: launch_rp<1, NW, PRO, GELU>(P, grid, lds, a, s); break;
+    case 2: launch_rp<2, NW, PRO, GELU>(P, grid, lds, a, s); break;
+    case 4: launch_rp<4, NW, PRO, GELU>(P, grid, lds, a, s); break;
+    case 8: launch_rp<8, NW, PRO, GELU>(P, grid, lds, a, s); break;
+    default: throw std::runtime_error("layer gemv: bad R");
+  }
+}
+
+}  // namespace
+
+bool layer_gemv_supported(const DevWeight& w, bool pro, bool gelu, int n_pro) {
+  if (w.type != T_Q4_0 || w.cols % 32 != 0 || w.rows <= 0) return false;
+  const int nb = w.cols / 32;
+  if ((size_t)nb * sizeof(XBlock) > 64 * 1024) return false;
+  if (pro && n_pro > PRO_EPT * 512) return false;
+  if (pro && n_pro != w.cols) return false;
+  if (gelu && w.rows % 64 != 0) return false;
+  return true;
+}
+
+void launch_layer_gemv(const DevWeight& w, LayerGemv a, bool pro, bool gelu, hipStream_t s) {
+  a.qs = reinterpret_cast<const uint4*>(w.qs);
+  a.wd = w.d;
+  a.rows = w.rows;
+  a.nb = w.cols / 32;
+  a.magic = div_magic(a.nb);
+  if (pro) a.n = w.cols;
+  const size_t lds = (size_t)a.nb * sizeof(XBlock);
+  if (gelu) {  // 8 waves x 8 rows = 64 interleaved gate/up rows per WG
+    if (!pro) throw std::runtime_error("layer gemv: GELU epilogue needs the norm prologue");
+    const int P = passes_for(8, a.nb);
+    launch_rp<8, 8, true, true>(P, dim3(w.rows / 64), lds, a, s);
+  } else {
+    const int R = rows_per_wave_l(a.nb), P = passes_for(R, a.nb);
+    const bool wide = pro && a.n > PRO_EPT * 256;  // 512-thread WGs for n_embd > 3072
+    if (wide) {
+      const dim3 grid((w.rows + 8 * R - 1) / (8 * R));
+      launch_r<8, true, false>(R, P, grid, lds, a, s);
+    } else {
+      const dim3 grid((w.rows + 4 * R - 1) / (4 * R));
+      if (pro)
+        launch_r<4, true, false>(R, P, grid, lds, a, s);
+      else
+        launch_r<4, false, false>(R, P, grid, lds, a, s);
+    }
+  }
+  LLMI_HIP(hipGetLastError());
+}
+
+}  // namespace llmi

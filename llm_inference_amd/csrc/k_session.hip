@@ -239,12 +239,6 @@ __global__ __launch_bounds__(1024) void embed_norm_kernel(uint32_t type, const u
 // result (ops.cpp:116-139) for the down projection: one 32-lane half-wave per
 // Q8_0 block.  Also writes the f32 hidden vector (parity/debug).
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ float gelu_mul1(float x, float u) {
-  const float c = __uint_as_float(0x3F4C4229u);  // sqrtf((float)(2.0 / M_PI))
-  const float inner = x + ((0.044715f * x) * x) * x;
-  return ((0.5f * x) * (1.0f + tanhf(c * inner))) * u;
-}
-
 __global__ __launch_bounds__(256) void gelu_quant_kernel(const float* __restrict__ gu, int n, float* __restrict__ hid,
                                                          XBlock* __restrict__ xb) {
   const int gl = blockIdx.x * blockDim.x + threadIdx.x;

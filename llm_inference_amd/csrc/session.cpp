@@ -150,8 +150,32 @@ void Session::upload(const GGUFView& g) {  // model.cpp:169-238 tensor map
     const GTensor *gt = T("ffn_gate.weight"), *up = T("ffn_up.weight"), *dn = T("ffn_down.weight");
     if ((int)gt->shape[1] != hp_.n_ff || (int)up->shape[1] != hp_.n_ff || (int)dn->shape[0] != hp_.n_ff)
       throw status_error(LLMI_E_SIZE, "ffn shapes do not match feed_forward_length");
-    Ld.gate_up = make_parts(g, {gt, up}, stream_, weight_bytes_);
+    if (fuse_layers_ && gt->type == T_Q4_0 && up->type == T_Q4_0 && gt->shape[0] == up->shape[0] && hp_.n_ff % 32 == 0) {
+      // rows interleaved in groups of 32 (gate 32k.., up 32k..) for the fused
+      // GELU epilogue of gemv_q4_0_layer (k_layer.hip)
+      const int cols = (int)gt->shape[0], F = hp_.n_ff;
+      const size_t rb = gguf_bytes(T_Q4_0, 1, cols);
+      std::vector<uint8_t> il((size_t)2 * F * rb);
+      const uint8_t *sg = (const uint8_t*)g.tensor_data(*gt), *su = (const uint8_t*)g.tensor_data(*up);
+      for (int k = 0; k < F / 32; k++) {
+        std::memcpy(&il[(size_t)(64 * k) * rb], sg + (size_t)(32 * k) * rb, 32 * rb);
+        std::memcpy(&il[(size_t)(64 * k + 32) * rb], su + (size_t)(32 * k) * rb, 32 * rb);
+      }
+      GemvPart p;
+      p.w = alloc_weight(T_Q4_0, 2 * F, cols);
+      upload_rows(p.w, 0, il.data(), 2 * F, stream_);
+      weight_bytes_ += p.w.bytes;
+      Ld.gate_up = {p};
+      Ld.gu_interleaved = true;
+    } else {
+      Ld.gate_up = make_parts(g, {gt, up}, stream_, weight_bytes_);
+    }
     Ld.down = make_parts(g, {dn}, stream_, weight_bytes_)[0];
+    Ld.fused = Ld.gu_interleaved && Ld.qkv.size() == 1 &&
+               layer_gemv_supported(Ld.qkv[0].w, true, false, hp_.n_embd) &&
+               layer_gemv_supported(Ld.o.w, false, false, 0) &&
+               layer_gemv_supported(Ld.gate_up[0].w, true, true, hp_.n_embd) &&
+               layer_gemv_supported(Ld.down.w, false, false, 0);
     Ld.attn_norm = dev_f32_copy(g, T("attn_norm.weight"), hp_.n_embd);
     Ld.q_norm = dev_f32_copy(g, T("attn_q_norm.weight"), Ld.hd);
     Ld.k_norm = dev_f32_copy(g, T("attn_k_norm.weight"), Ld.hd);
@@ -174,6 +198,8 @@ void Session::alloc_buffers() {
   }
   const int maxcols = std::max({E, F, maxq, vocab_ > 0 ? E : 0});
   resid_ = dalloc<float>(E);
+  resid2_ = dalloc<float>(E);
+  resid_scratch_ = dalloc<float>(E);
   xn_ = dalloc<float>(E);
   qkv_ = dalloc<float>(maxqkv);
   q_ = dalloc<float>(maxq);
@@ -229,6 +255,7 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
     ex_attn_ = s.find("attn") != std::string::npos;
     ex_logits_ = s.find("logits") != std::string::npos;
   }
+  fuse_layers_ = !ex_gemv_ && !ex_norm_ && getenv("LLMI_NO_FUSE") == nullptr;
   use_graph_ = (opts.flags & LLMI_NO_GRAPH) == 0;
   max_ctx_ = opts.max_ctx > 0 ? opts.max_ctx : 4096;
   nsplit_ = opts.attn_split > 0 ? opts.attn_split : 32;
@@ -298,7 +325,7 @@ void Session::gemv_parts(const std::vector<GemvPart>& parts, const float* x, int
 // One decode token.  Reads *d_token_/*d_pos_, ends with the token feedback.
 void Session::record_step(hipStream_t s) {
   kernels_per_token_ = 0;
-  const int E = hp_.n_embd, F = hp_.n_ff;
+  const int E = hp_.n_embd;
   const float emb_scale = std::sqrt(static_cast<float>(E));  // model.cpp:337-338
   auto is_q8 = [](uint32_t t) { return t == T_Q4_0 || t == T_Q8_0; };
   // a norm feeding GEMV parts also writes their Q8_0 activation when every
@@ -323,6 +350,109 @@ void Session::record_step(hipStream_t s) {
     launch_rms_norm(resid_, L_[0].attn_norm, xn_, E, 1, hp_.eps, ex_norm_, s);
     kernels_per_token_ += 2;
   }
+  bool fused = fuse_layers_;
+  for (const auto& l : L_) fused &= l.fused;
+  if (fused) {
+    record_layers_fused(s, x_q8);
+  } else {
+    record_layers(s, x_q8);
+  }
+  // logits (model.cpp:993-1034): F16 table -> mat_vec_mul_fp16, else mat_vec_mul
+  if (embd_.type != T_F16) prepare_act(embd_.type, xn_, E, act_, s);
+  const bool fold = !ex_logits_ && embd_.type == T_F16 && E % 8 == 0;
+  launch_gemv(embd_, act_, logits_, ex_logits_ ? GEMV_EXACT : GEMV_FAST, s, fold ? amax_key_ : nullptr);
+  kernels_per_token_++;
+  if (!fold) {
+    launch_argmax(logits_, vocab_, amax_key_, s);
+    kernels_per_token_++;
+  }
+  launch_finalize_token(amax_key_, d_token_, d_pos_, ring_, ring_idx_, max_ctx_, s);
+  kernels_per_token_++;
+}
+
+// Fast path with every projection a gemv_q4_0_layer launch: 6 launches per
+// layer (qkv [+ residual/norm prologue], attention partial, combine, o,
+// gate_up [+ prologue + GELU epilogue], down).  The residual stream
+// ping-pongs between resid_ and resid2_ (a prologue's work-group 0 writes the
+// buffer its sibling work-groups are not reading).
+void Session::record_layers_fused(hipStream_t s, bool x_q8) {
+  const int E = hp_.n_embd;
+  float* cur = resid_;
+  float* other = resid2_;
+  for (int l = 0; l < hp_.n_layer; l++) {
+    LayerDev& Ld = L_[l];
+    const int hd = Ld.hd;
+    LayerGemv g;
+    if (l == 0) {
+      if (!x_q8) {
+        launch_quantize_q8_0(xn_, E, act_.q8, s);
+        kernels_per_token_++;
+      }
+      g.xg = act_.q8.xb;
+      g.out = qkv_;
+      launch_layer_gemv(Ld.qkv[0].w, g, false, false, s);
+    } else {
+      g.y = d_out_;
+      g.w_post = L_[l - 1].post_ffw_norm;
+      g.resid_in = cur;
+      g.resid_out = other;
+      g.w_next = Ld.attn_norm;
+      g.eps = hp_.eps;
+      g.out = qkv_;
+      launch_layer_gemv(Ld.qkv[0].w, g, true, false, s);
+      std::swap(cur, other);
+    }
+    kernels_per_token_++;
+    QKVArgs qa{qkv_, Ld.k_off, Ld.v_off, hp_.n_head, hp_.n_head_kv, hd, Ld.q_norm, Ld.k_norm,
+               Ld.is_swa ? rope_swa_ : rope_glb_, hp_.attn_scale, hp_.eps, q_, Ld.kc, Ld.vc, max_ctx_, d_pos_};
+    AttnArgs aa{q_, Ld.kc, Ld.vc, hp_.n_head, hp_.n_head_kv, hd, max_ctx_, d_pos_, part_, attn_};
+    const bool q8_in_combine = hd % 32 == 0;
+    launch_attention(aa, false, nsplit_, q8_in_combine ? &act_.q8 : nullptr, s, &qa);
+    kernels_per_token_ += 2;
+    if (!q8_in_combine) {
+      launch_quantize_q8_0(attn_, hp_.n_head * hd, act_.q8, s);
+      kernels_per_token_++;
+    }
+    LayerGemv go;
+    go.xg = act_.q8.xb;
+    go.out = o_out_;
+    launch_layer_gemv(Ld.o.w, go, false, false, s);
+    LayerGemv gg;
+    gg.y = o_out_;
+    gg.w_post = Ld.post_attn_norm;
+    gg.resid_in = cur;
+    gg.resid_out = other;
+    gg.w_next = Ld.ffn_norm;
+    gg.eps = hp_.eps;
+    gg.hid = hid_;
+    gg.hq8 = act_.q8.xb;
+    launch_layer_gemv(Ld.gate_up[0].w, gg, true, true, s);
+    std::swap(cur, other);
+    LayerGemv gd;
+    gd.xg = act_.q8.xb;
+    gd.out = d_out_;
+    launch_layer_gemv(Ld.down.w, gd, false, false, s);
+    kernels_per_token_ += 3;
+  }
+  // final residual + output_norm (-> xn_, and f16 x for an F16 logits table)
+  NormOut o2;
+  o2.xn = xn_;
+  if (embd_.type == T_F16) o2.x16 = act_.x16;
+  launch_residual_norm(d_out_, L_.back().post_ffw_norm, cur, out_norm_, o2, E, hp_.eps, false, s);
+  kernels_per_token_++;
+}
+
+void Session::record_layers(hipStream_t s, bool x_q8) {
+  const int E = hp_.n_embd, F = hp_.n_ff;
+  auto is_q8 = [](uint32_t t) { return t == T_Q4_0 || t == T_Q8_0; };
+  auto nout = [&](const std::vector<GemvPart>& consumer) {
+    NormOut o;
+    o.xn = xn_;
+    bool q8 = !consumer.empty();
+    for (const auto& p : consumer) q8 &= is_q8(p.w.type);
+    if (q8) o.q8 = act_.q8.xb;
+    return o;
+  };
   for (int l = 0; l < hp_.n_layer; l++) {
     LayerDev& Ld = L_[l];
     const int hd = Ld.hd;
@@ -357,17 +487,6 @@ void Session::record_step(hipStream_t s) {
     x_q8 = o2.q8 != nullptr;
     kernels_per_token_++;
   }
-  // logits (model.cpp:993-1034): F16 table -> mat_vec_mul_fp16, else mat_vec_mul
-  if (embd_.type != T_F16) prepare_act(embd_.type, xn_, E, act_, s);
-  const bool fold = !ex_logits_ && embd_.type == T_F16 && E % 8 == 0;
-  launch_gemv(embd_, act_, logits_, ex_logits_ ? GEMV_EXACT : GEMV_FAST, s, fold ? amax_key_ : nullptr);
-  kernels_per_token_++;
-  if (!fold) {
-    launch_argmax(logits_, vocab_, amax_key_, s);
-    kernels_per_token_++;
-  }
-  launch_finalize_token(amax_key_, d_token_, d_pos_, ring_, ring_idx_, max_ctx_, s);
-  kernels_per_token_++;
 }
 
 void Session::ensure_graph() {
@@ -457,7 +576,43 @@ void Session::time_kernel(int which, int reps, double* us, double* bytes) {
   // pair on the session stream (torch.cuda.Event would only see torch's
   // stream), weights swept in decode order so every launch streams from HBM
   std::vector<const DevWeight*> ws;
-  if (which == 0) {
+  bool fused = fuse_layers_;
+  for (const auto& l : L_) fused &= l.fused;
+  // the fused path's launches (gemv_q4_0_layer) with their real arguments,
+  // except that the prologue's residual write goes to a scratch buffer
+  std::vector<std::pair<LayerGemv, int>> fl;  // (args, mode: 0 plain, 1 pro, 2 pro+gelu)
+  if (which == 0 && fused) {
+    for (size_t i = 0; i < L_.size(); i++) {
+      const LayerDev& Ld = L_[i];
+      LayerGemv q;
+      q.y = d_out_;
+      q.w_post = i ? L_[i - 1].post_ffw_norm : Ld.post_ffw_norm;
+      q.resid_in = resid_;
+      q.resid_out = resid_scratch_;
+      q.w_next = Ld.attn_norm;
+      q.eps = hp_.eps;
+      q.out = qkv_;
+      fl.push_back({q, 1});
+      ws.push_back(&Ld.qkv[0].w);
+      LayerGemv o;
+      o.xg = act_.q8.xb;
+      o.out = o_out_;
+      fl.push_back({o, 0});
+      ws.push_back(&Ld.o.w);
+      LayerGemv gu = q;
+      gu.w_next = Ld.ffn_norm;
+      gu.out = nullptr;
+      gu.hid = hid_;
+      gu.hq8 = act_.q8.xb;
+      fl.push_back({gu, 2});
+      ws.push_back(&Ld.gate_up[0].w);
+      LayerGemv d;
+      d.xg = act_.q8.xb;
+      d.out = d_out_;
+      fl.push_back({d, 0});
+      ws.push_back(&Ld.down.w);
+    }
+  } else if (which == 0) {
     for (const auto& l : L_) {
       for (const auto& p : l.qkv) ws.push_back(&p.w);
       ws.push_back(&l.o.w);
@@ -473,11 +628,14 @@ void Session::time_kernel(int which, int reps, double* us, double* bytes) {
   size_t k = 0;
   double tot_bytes = 0;
   for (int r = 0; r < reps; r++)
-    for (const DevWeight* w : ws) {
+    for (size_t j = 0; j < ws.size(); j++) {
+      const DevWeight* w = ws[j];
       LLMI_HIP(hipEventRecord(ev[k++], stream_));
-      launch_gemv(*w, act_, (w == &embd_ || w->rows > 2 * hp_.n_ff) ? logits_ : gu_,
-                  exact_ ? GEMV_EXACT : GEMV_FAST, stream_,
-                  w == &embd_ ? amax_key_ : nullptr);
+      if (!fl.empty())
+        launch_layer_gemv(*w, fl[j].first, fl[j].second >= 1, fl[j].second == 2, stream_);
+      else
+        launch_gemv(*w, act_, (w == &embd_ || w->rows > 2 * hp_.n_ff) ? logits_ : gu_,
+                    exact_ ? GEMV_EXACT : GEMV_FAST, stream_, w == &embd_ ? amax_key_ : nullptr);
       LLMI_HIP(hipEventRecord(ev[k++], stream_));
       tot_bytes += (double)w->bytes;
     }

@@ -39,6 +39,8 @@ struct LayerDev {
   float *attn_norm = nullptr, *q_norm = nullptr, *k_norm = nullptr;
   float *post_attn_norm = nullptr, *ffn_norm = nullptr, *post_ffw_norm = nullptr;
   bool is_swa = false;
+  bool gu_interleaved = false;  // gate_up rows in groups of 32 (k_layer.hip GELU epilogue)
+  bool fused = false;           // every projection runs as gemv_q4_0_layer
   int hd = 0;
   uint16_t *kc = nullptr, *vc = nullptr;
 };
@@ -60,6 +62,8 @@ class Session {
   void alloc_buffers();
   void build_rope_tables();
   void record_step(hipStream_t s);
+  void record_layers(hipStream_t s, bool x_q8);
+  void record_layers_fused(hipStream_t s, bool x_q8);
   void prepare_act(uint32_t wtype, const float* x, int n, ActBuf& act, hipStream_t s);
   void gemv_parts(const std::vector<GemvPart>& parts, const float* x, int n_in, float* out, hipStream_t s,
                   bool x_ready);
@@ -78,6 +82,7 @@ class Session {
 
   llmi_session_opts opts_;
   bool exact_ = false, use_graph_ = true;
+  bool fuse_layers_ = false;  // fast path: norms / GELU folded into the Q4_0 GEMVs
   bool ex_gemv_ = false, ex_norm_ = false, ex_attn_ = false, ex_logits_ = false;  // per kernel family
   int nsplit_ = 32;
   HParams hp_;
@@ -91,6 +96,7 @@ class Session {
   float* out_norm_ = nullptr;
   float *rope_swa_ = nullptr, *rope_glb_ = nullptr;
   // activations
+  float *resid2_ = nullptr, *resid_scratch_ = nullptr;
   float *resid_ = nullptr, *xn_ = nullptr, *qkv_ = nullptr, *q_ = nullptr, *attn_ = nullptr, *part_ = nullptr;
   float *o_out_ = nullptr, *gu_ = nullptr, *hid_ = nullptr, *d_out_ = nullptr, *logits_ = nullptr;
   ActBuf act_{};

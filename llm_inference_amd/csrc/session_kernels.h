@@ -25,6 +25,28 @@ void launch_embed_norm(uint32_t type, const uint8_t* table, size_t row_bytes, co
                        float emb_scale, float* resid, const float* w, const NormOut& out, int n, double eps,
                        bool exact, hipStream_t s);
 void launch_gelu_quant(const float* gu, int n, float* hid, const Q8Act* q8, hipStream_t s);
+// Q4_0 GEMV with the decode step's neighbours fused in (k_layer.hip)
+struct LayerGemv {
+  const uint4* qs = nullptr;  // set by launch_layer_gemv from the weight
+  const uint16_t* wd = nullptr;
+  int rows = 0, nb = 0;
+  uint32_t magic = 0;
+  const XBlock* xg = nullptr;  // !pro: the activation's Q8_0 blocks
+  // pro: resid_out = resid_in + rms(y) * w_post; x = rms(resid_out) * w_next
+  const float* y = nullptr;
+  const float* w_post = nullptr;
+  const float* resid_in = nullptr;
+  float* resid_out = nullptr;
+  const float* w_next = nullptr;
+  float* xn_out = nullptr;  // optional copy of x (work-group 0)
+  int n = 0;
+  double eps = 0;
+  float* out = nullptr;     // !gelu: [rows]
+  float* hid = nullptr;     // gelu: [rows / 2] and its Q8_0 blocks
+  XBlock* hq8 = nullptr;
+};
+bool layer_gemv_supported(const DevWeight& w, bool pro, bool gelu, int n_pro);
+void launch_layer_gemv(const DevWeight& w, LayerGemv a, bool pro, bool gelu, hipStream_t s);
 void launch_argmax(const float* x, int n, unsigned long long* key, hipStream_t s);
 void launch_finalize_token(unsigned long long* key, int32_t* d_token, int32_t* d_pos, int32_t* ring,
                            int32_t* ring_idx, int ring_cap, hipStream_t s);

@@ -124,3 +124,23 @@ def test_session_errors():
     assert ei.value.status == "E_RANGE"
     with pytest.raises(LLMIError):
         m.forward([10], 0)  # vocab is 10
+
+
+def test_unfused_fast_path_matches_fused(oracle, monkeypatch):
+    """LLMI_NO_FUSE=1 selects the separate norm / GELU launches; both fast
+    layouts agree to reassociation noise and give the reference's ids."""
+    from llm_inference_amd.model import Model
+    from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
+    cfg = CONFIGS["mini-4b"]
+    g = build_gemma3_gguf(cfg, seed=11)
+    prompt = np.random.default_rng(2).integers(4, cfg.vocab, 9).astype(np.int32)
+    fused = Model(g, exact=False, max_ctx=64)
+    lf = fused.forward(prompt, 0)
+    monkeypatch.setenv("LLMI_NO_FUSE", "1")
+    plain = Model(g, exact=False, max_ctx=64)
+    lp = plain.forward(prompt, 0)
+    assert fused.get_info().kernels_per_token < plain.get_info().kernels_per_token
+    np.testing.assert_allclose(lf, lp, atol=FAST_VS_REF, rtol=0)
+    ideal = oracle.model(g, n_threads=8, max_ctx=64, attn_f64=True)
+    np.testing.assert_allclose(lf, ideal.forward(prompt, 0), atol=FAST_VS_REF, rtol=0)
+    assert int(np.argmax(lf)) == int(np.argmax(lp))
