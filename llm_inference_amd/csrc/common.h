@@ -88,6 +88,12 @@ __device__ __forceinline__ int4 ld_nt(const int4* p) {
   return make_int4((int)v.x, (int)v.y, (int)v.z, (int)v.w);
 }
 
+__device__ __forceinline__ uint16_t ld_nt16(const uint16_t* p) { return __builtin_nontemporal_load(p); }
+
+// Q4_0 nibbles of 4 packed bytes: low = elements 0..15, high = 16..31 (ops.cpp:334-340)
+__device__ __forceinline__ int nib_lo(uint32_t w) { return (int)(w & 0x0F0F0F0Fu); }
+__device__ __forceinline__ int nib_hi(uint32_t w) { return (int)((w >> 4) & 0x0F0F0F0Fu); }
+
 // ---------------------------------------------------------------------------
 // wave-level reductions (64 lanes).  Fixed xor-butterfly order, so results
 // are deterministic run to run.

@@ -17,9 +17,6 @@
 
 namespace llmi {
 
-__device__ __forceinline__ int nib_lo(uint32_t w) { return (int)(w & 0x0F0F0F0Fu); }
-__device__ __forceinline__ int nib_hi(uint32_t w) { return (int)((w >> 4) & 0x0F0F0F0Fu); }
-__device__ __forceinline__ uint16_t ld_nt16(const uint16_t* p) { return __builtin_nontemporal_load(p); }
 
 // ===========================================================================
 // Q4_0 x Q8_0

@@ -25,9 +25,6 @@ namespace {
 
 constexpr int PRO_EPT = 12;  // prologue elements per thread (n <= 12 * threads)
 
-__device__ __forceinline__ uint16_t ld_nt16(const uint16_t* p) { return __builtin_nontemporal_load(p); }
-__device__ __forceinline__ int nib_lo(uint32_t w) { return (int)(w & 0x0F0F0F0Fu); }
-__device__ __forceinline__ int nib_hi(uint32_t w) { return (int)((w >> 4) & 0x0F0F0F0Fu); }
 
 template <int NW>
 __device__ __forceinline__ float wg_sum(float v, float* red) {  // fixed order, identical in every WG
@@ -114,7 +111,7 @@ __global__ __launch_bounds__(NW * 64) void gemv_q4_0_layer(LayerGemv a) {
       const bool ok = i < n;
       yv[k] = ok ? a.y[i] : 0.0f;
       rv[k] = ok ? a.resid_in[i] : 0.0f;
-      wp[k] = ok ? a.w_post[i] : 0.0f;
+      wp[k] = (ok && a.w_post) ? a.w_post[i] : 0.0f;
       wn[k] = ok ? a.w_next[i] : 0.0f;
     }
     float ss = 0.0f;
@@ -124,7 +121,7 @@ __global__ __launch_bounds__(NW * 64) void gemv_q4_0_layer(LayerGemv a) {
     float ss2 = 0.0f;
 #pragma unroll
     for (int k = 0; k < PRO_EPT; k++) {
-      const float h = rv[k] + (sc1 * yv[k]) * wp[k];
+      const float h = rv[k] + (a.w_post ? (sc1 * yv[k]) * wp[k] : yv[k]);  // no post-norm: plain add
       rv[k] = h;
       ss2 = fmaf(h, h, ss2);
       const int i = t + k * T;
@@ -231,6 +228,10 @@ bool layer_gemv_supported(const DevWeight& w, bool pro, bool gelu, int n_pro) {
 }
 
 void launch_layer_gemv(const DevWeight& w, LayerGemv a, bool pro, bool gelu, hipStream_t s) {
+  if (!layer_gemv_supported(w, pro, gelu, pro ? w.cols : 0)) throw std::runtime_error("layer gemv: unsupported weight");
+  if (pro ? (!a.y || !a.resid_in || !a.resid_out || !a.w_next || a.resid_in == a.resid_out) : !a.xg)
+    throw std::runtime_error("layer gemv: missing prologue operand");
+  if (gelu ? (!a.hid || !a.hq8) : !a.out) throw std::runtime_error("layer gemv: missing output");
   a.qs = reinterpret_cast<const uint4*>(w.qs);
   a.wd = w.d;
   a.rows = w.rows;

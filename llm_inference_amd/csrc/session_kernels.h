@@ -32,7 +32,8 @@ struct LayerGemv {
   int rows = 0, nb = 0;
   uint32_t magic = 0;
   const XBlock* xg = nullptr;  // !pro: the activation's Q8_0 blocks
-  // pro: resid_out = resid_in + rms(y) * w_post; x = rms(resid_out) * w_next
+  // pro: resid_out = resid_in + rms(y) * w_post (y itself when w_post is
+  // null); x = rms(resid_out) * w_next
   const float* y = nullptr;
   const float* w_post = nullptr;
   const float* resid_in = nullptr;

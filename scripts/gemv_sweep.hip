@@ -1,0 +1,197 @@
+// gemv_sweep.hip -- standalone microbenchmark of the Q4_0 decode GEMV variants
+// (development tool, not part of the product).  Every timed launch reads a
+// different copy of the weight (copies x bytes > the 256 MB MALL), so each
+// launch streams from HBM as in a real decode step.
+//
+// build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -Iinclude \
+//        scripts/gemv_sweep.hip -o scripts/gemv_sweep
+// run:   scripts/gemv_sweep [reps]
+#include "../llm_inference_amd/csrc/k_gemv.hip"
+#include "../llm_inference_amd/csrc/k_layer.hip"
+
+#include <vector>
+
+using namespace llmi;
+
+namespace {
+
+__global__ void fill_kernel(uint32_t* p, size_t n, uint32_t seed) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    uint32_t h = (uint32_t)i * 2654435761u ^ seed;
+    h ^= h >> 13;
+    h *= 0x5bd1e995u;
+    h ^= h >> 15;
+    p[i] = h;
+  }
+}
+__global__ void fill_scales(uint16_t* p, size_t n) {  // small positive f16 scales
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    p[i] = 0x2000 + (uint16_t)(i & 0xFF);
+}
+
+// pure streaming read of the same bytes (qs + d), 16 B per lane per load,
+// P loads in flight: the achievable-bandwidth reference for this layout
+template <int P>
+__global__ __launch_bounds__(256) void stream_kernel(const uint4* __restrict__ q, size_t n16, float* out) {
+  uint32_t acc = 0;
+  const size_t stride = (size_t)gridDim.x * 256 * P;
+  for (size_t base = blockIdx.x * (size_t)256 * P + threadIdx.x; base < n16; base += stride) {
+    uint4 v[P];
+#pragma unroll
+    for (int p = 0; p < P; p++) {
+      const size_t i = base + (size_t)p * 256;
+      v[p] = i < n16 ? ld_nt(q + i) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int p = 0; p < P; p++) acc ^= v[p].x ^ v[p].y ^ v[p].z ^ v[p].w;
+  }
+  if (acc == 0x12345678u) out[0] = 1.0f;
+}
+
+struct Shape {
+  const char* name;
+  int rows, cols;
+};
+
+DevWeight alloc_q4(int rows, int cols) {
+  DevWeight w;
+  w.type = T_Q4_0;
+  w.rows = rows;
+  w.cols = cols;
+  const size_t nblk = (size_t)rows * (cols / 32);
+  w.bytes = nblk * 18;
+  LLMI_HIP(hipMalloc(&w.qs, nblk * 16 + 64));
+  LLMI_HIP(hipMalloc((void**)&w.d, nblk * 2 + 64));
+  return w;
+}
+
+float* dmalloc_f(size_t n) {
+  float* p;
+  LLMI_HIP(hipMalloc(&p, n * 4 + 256));
+  LLMI_HIP(hipMemset(p, 0, n * 4 + 256));
+  return p;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  const int reps = argc > 1 ? atoi(argv[1]) : 200;
+  LLMI_HIP(hipSetDevice(0));
+  hipStream_t s;
+  LLMI_HIP(hipStreamCreate(&s));
+  const Shape shapes[] = {{"4b.qkv", 4096, 2560}, {"4b.o", 2560, 2048}, {"4b.gate_up", 20480, 2560},
+                          {"4b.down", 2560, 10240}, {"1b.gate_up", 13824, 1152}, {"27b.down", 5376, 21504}};
+  hipEvent_t e0, e1;
+  LLMI_HIP(hipEventCreate(&e0));
+  LLMI_HIP(hipEventCreate(&e1));
+  for (const Shape& sh : shapes) {
+    const size_t wbytes = (size_t)sh.rows * (sh.cols / 32) * 18;
+    const int copies = (int)std::max<size_t>(2, (size_t)(1536ull << 20) / wbytes + 1);
+    std::vector<DevWeight> ws(copies);
+    for (int c = 0; c < copies; c++) {
+      ws[c] = alloc_q4(sh.rows, sh.cols);
+      const size_t nblk = (size_t)sh.rows * (sh.cols / 32);
+      hipLaunchKernelGGL(fill_kernel, dim3(1024), dim3(256), 0, s, (uint32_t*)ws[c].qs, nblk * 4, (uint32_t)c);
+      hipLaunchKernelGGL(fill_scales, dim3(1024), dim3(256), 0, s, ws[c].d, nblk);
+    }
+    const int nb = sh.cols / 32;
+    XBlock* xb;
+    LLMI_HIP(hipMalloc(&xb, (size_t)(nb + 1) * sizeof(XBlock)));
+    hipLaunchKernelGGL(fill_kernel, dim3(64), dim3(256), 0, s, (uint32_t*)xb, (size_t)(nb + 1) * 12, 7u);
+    float* out = dmalloc_f(sh.rows);
+    float* y = dmalloc_f(sh.cols);
+    float* r0 = dmalloc_f(sh.cols);
+    float* r1 = dmalloc_f(sh.cols);
+    float* wn = dmalloc_f(sh.cols);
+    float* hid = dmalloc_f(sh.rows);
+    XBlock* hq;
+    LLMI_HIP(hipMalloc(&hq, (size_t)(sh.rows / 32 + 1) * sizeof(XBlock)));
+    LLMI_HIP(hipStreamSynchronize(s));
+    ActBuf act{};
+    act.q8.xb = xb;
+    act.q8.nb = nb;
+
+    auto timeit = [&](const char* label, auto&& launch) {
+      for (int i = 0; i < copies; i++) launch(ws[i % copies]);
+      LLMI_HIP(hipStreamSynchronize(s));
+      LLMI_HIP(hipEventRecord(e0, s));
+      for (int i = 0; i < reps; i++) launch(ws[i % copies]);
+      LLMI_HIP(hipEventRecord(e1, s));
+      LLMI_HIP(hipEventSynchronize(e1));
+      float ms = 0;
+      LLMI_HIP(hipEventElapsedTime(&ms, e0, e1));
+      const double us = ms * 1000.0 / reps;
+      printf("%-12s %-34s %8.2f us  %7.1f GB/s\n", sh.name, label, us, wbytes / (us * 1e-6) / 1e9);
+      fflush(stdout);
+    };
+    timeit("stream<8> (qs only, 2048 WG)", [&](const DevWeight& w) {
+      hipLaunchKernelGGL(stream_kernel<8>, dim3(2048), dim3(256), 0, s, (const uint4*)w.qs,
+                         (size_t)sh.rows * nb, out);
+    });
+    timeit("stream<4> (qs only, 1024 WG)", [&](const DevWeight& w) {
+      hipLaunchKernelGGL(stream_kernel<4>, dim3(1024), dim3(256), 0, s, (const uint4*)w.qs,
+                         (size_t)sh.rows * nb, out);
+    });
+    timeit("gemv_q4_0_fast (k_gemv)", [&](const DevWeight& w) { launch_gemv(w, act, out, GEMV_FAST, s); });
+    LayerGemv plain;
+    plain.xg = xb;
+    plain.out = out;
+    timeit("layer plain", [&](const DevWeight& w) { launch_layer_gemv(w, plain, false, false, s); });
+    LayerGemv pro;
+    pro.y = y;
+    pro.resid_in = r0;
+    pro.resid_out = r1;
+    pro.w_post = wn;
+    pro.w_next = wn;
+    pro.eps = 1e-6;
+    pro.out = out;
+    if (sh.cols <= 6144) timeit("layer pro", [&](const DevWeight& w) { launch_layer_gemv(w, pro, true, false, s); });
+    LayerGemv gl = pro;
+    gl.out = nullptr;
+    gl.hid = hid;
+    gl.hq8 = hq;
+    if (sh.rows % 64 == 0 && sh.cols <= 6144)
+      timeit("layer pro+gelu", [&](const DevWeight& w) { launch_layer_gemv(w, gl, true, true, s); });
+    // geometry variants of the plain kernel
+    const uint32_t mg = div_magic(nb);
+    auto geo = [&](const char* label, auto kern, int rows_per_wg, int threads) {
+      LayerGemv a = plain;
+      a.wd = nullptr;
+      timeit(label, [&](const DevWeight& w) {
+        a.qs = (const uint4*)w.qs;
+        a.wd = w.d;
+        a.rows = w.rows;
+        a.nb = nb;
+        a.magic = mg;
+        hipLaunchKernelGGL(kern, dim3((w.rows + rows_per_wg - 1) / rows_per_wg), dim3(threads),
+                           (size_t)nb * sizeof(XBlock), s, a);
+      });
+    };
+    if (nb % 64 == 0) {
+      geo("plain R1 NW4 P1", gemv_q4_0_layer<1, 4, 1, false, false>, 4, 256);
+      geo("plain R1 NW8 P1", gemv_q4_0_layer<1, 8, 1, false, false>, 8, 512);
+    }
+    if ((4 * nb) % 64 == 0) {
+      geo("plain R4 NW4 P5", gemv_q4_0_layer<4, 4, 5, false, false>, 16, 256);
+      geo("plain R4 NW2 P5", gemv_q4_0_layer<4, 2, 5, false, false>, 8, 128);
+      geo("plain R4 NW1 P5", gemv_q4_0_layer<4, 1, 5, false, false>, 4, 64);
+      geo("plain R4 NW8 P5", gemv_q4_0_layer<4, 8, 5, false, false>, 32, 512);
+    }
+    geo("plain R8 NW4 P5", gemv_q4_0_layer<8, 4, 5, false, false>, 32, 256);
+    geo("plain R2 NW4 P5", gemv_q4_0_layer<2, 4, 5, false, false>, 8, 256);
+    for (auto& w : ws) {
+      (void)hipFree(w.qs);
+      (void)hipFree(w.d);
+    }
+    (void)hipFree(xb);
+    (void)hipFree(out);
+    (void)hipFree(y);
+    (void)hipFree(r0);
+    (void)hipFree(r1);
+    (void)hipFree(wn);
+    (void)hipFree(hid);
+    (void)hipFree(hq);
+  }
+  printf("done\n");
+  return 0;
+}
