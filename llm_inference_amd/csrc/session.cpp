@@ -256,6 +256,7 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
     ex_logits_ = s.find("logits") != std::string::npos;
   }
   fuse_layers_ = !ex_gemv_ && !ex_norm_ && getenv("LLMI_NO_FUSE") == nullptr;
+  if (const char* d = getenv("LLMI_DUP")) dup_ = d;  // diagnostics: launch these kernels twice
   use_graph_ = (opts.flags & LLMI_NO_GRAPH) == 0;
   max_ctx_ = opts.max_ctx > 0 ? opts.max_ctx : 4096;
   nsplit_ = opts.attn_split > 0 ? opts.attn_split : 32;
@@ -360,7 +361,8 @@ void Session::record_step(hipStream_t s) {
   // logits (model.cpp:993-1034): F16 table -> mat_vec_mul_fp16, else mat_vec_mul
   if (embd_.type != T_F16) prepare_act(embd_.type, xn_, E, act_, s);
   const bool fold = !ex_logits_ && embd_.type == T_F16 && E % 8 == 0;
-  launch_gemv(embd_, act_, logits_, ex_logits_ ? GEMV_EXACT : GEMV_FAST, s, fold ? amax_key_ : nullptr);
+  for (int r = 0; r < dup("logits"); r++)
+    launch_gemv(embd_, act_, logits_, ex_logits_ ? GEMV_EXACT : GEMV_FAST, s, fold ? amax_key_ : nullptr);
   kernels_per_token_++;
   if (!fold) {
     launch_argmax(logits_, vocab_, amax_key_, s);
@@ -390,7 +392,7 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
       }
       g.xg = act_.q8.xb;
       g.out = qkv_;
-      launch_layer_gemv(Ld.qkv[0].w, g, false, false, s);
+      for (int r = 0; r < dup("qkv"); r++) launch_layer_gemv(Ld.qkv[0].w, g, false, false, s);
     } else {
       g.y = d_out_;
       g.w_post = L_[l - 1].post_ffw_norm;
@@ -399,7 +401,7 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
       g.w_next = Ld.attn_norm;
       g.eps = hp_.eps;
       g.out = qkv_;
-      launch_layer_gemv(Ld.qkv[0].w, g, true, false, s);
+      for (int r = 0; r < dup("qkv"); r++) launch_layer_gemv(Ld.qkv[0].w, g, true, false, s);
       std::swap(cur, other);
     }
     kernels_per_token_++;
@@ -407,7 +409,8 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
                Ld.is_swa ? rope_swa_ : rope_glb_, hp_.attn_scale, hp_.eps, q_, Ld.kc, Ld.vc, max_ctx_, d_pos_};
     AttnArgs aa{q_, Ld.kc, Ld.vc, hp_.n_head, hp_.n_head_kv, hd, max_ctx_, d_pos_, part_, attn_};
     const bool q8_in_combine = hd % 32 == 0;
-    launch_attention(aa, false, nsplit_, q8_in_combine ? &act_.q8 : nullptr, s, &qa);
+    for (int r = 0; r < dup("attn"); r++)
+      launch_attention(aa, false, nsplit_, q8_in_combine ? &act_.q8 : nullptr, s, &qa);
     kernels_per_token_ += 2;
     if (!q8_in_combine) {
       launch_quantize_q8_0(attn_, hp_.n_head * hd, act_.q8, s);
@@ -416,7 +419,7 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
     LayerGemv go;
     go.xg = act_.q8.xb;
     go.out = o_out_;
-    launch_layer_gemv(Ld.o.w, go, false, false, s);
+    for (int r = 0; r < dup("o_proj"); r++) launch_layer_gemv(Ld.o.w, go, false, false, s);
     LayerGemv gg;
     gg.y = o_out_;
     gg.w_post = Ld.post_attn_norm;
@@ -426,12 +429,12 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
     gg.eps = hp_.eps;
     gg.hid = hid_;
     gg.hq8 = act_.q8.xb;
-    launch_layer_gemv(Ld.gate_up[0].w, gg, true, true, s);
+    for (int r = 0; r < dup("gate_up"); r++) launch_layer_gemv(Ld.gate_up[0].w, gg, true, true, s);
     std::swap(cur, other);
     LayerGemv gd;
     gd.xg = act_.q8.xb;
     gd.out = d_out_;
-    launch_layer_gemv(Ld.down.w, gd, false, false, s);
+    for (int r = 0; r < dup("down"); r++) launch_layer_gemv(Ld.down.w, gd, false, false, s);
     kernels_per_token_ += 3;
   }
   // final residual + output_norm (-> xn_, and f16 x for an F16 logits table)
@@ -456,7 +459,7 @@ void Session::record_layers(hipStream_t s, bool x_q8) {
   for (int l = 0; l < hp_.n_layer; l++) {
     LayerDev& Ld = L_[l];
     const int hd = Ld.hd;
-    gemv_parts(Ld.qkv, xn_, E, qkv_, s, x_q8);
+    for (int r = 0; r < dup("qkv"); r++) gemv_parts(Ld.qkv, xn_, E, qkv_, s, x_q8);
     QKVArgs qa{qkv_, Ld.k_off, Ld.v_off, hp_.n_head, hp_.n_head_kv, hd, Ld.q_norm, Ld.k_norm,
                Ld.is_swa ? rope_swa_ : rope_glb_, hp_.attn_scale, hp_.eps, q_, Ld.kc, Ld.vc, max_ctx_, d_pos_};
     const bool fuse_qk = !ex_attn_ && !ex_norm_;  // norm/rope/KV-append inside the attention launch
@@ -467,17 +470,22 @@ void Session::record_layers(hipStream_t s, bool x_q8) {
     AttnArgs aa{q_, Ld.kc, Ld.vc, hp_.n_head, hp_.n_head_kv, hd, max_ctx_, d_pos_, part_, attn_};
     const bool o_q8 = is_q8(Ld.o.w.type);
     const bool fused_q8 = !ex_attn_ && o_q8 && hd % 32 == 0;
-    launch_attention(aa, ex_attn_, nsplit_, fused_q8 ? &act_.q8 : nullptr, s, fuse_qk ? &qa : nullptr);
+    for (int r = 0; r < dup("attn"); r++)
+      launch_attention(aa, ex_attn_, nsplit_, fused_q8 ? &act_.q8 : nullptr, s, fuse_qk ? &qa : nullptr);
     kernels_per_token_ += ex_attn_ ? 1 : 2;
-    gemv_parts({Ld.o}, attn_, hp_.n_head * hd, o_out_, s, fused_q8);
+    for (int r = 0; r < dup("o_proj"); r++) gemv_parts({Ld.o}, attn_, hp_.n_head * hd, o_out_, s, fused_q8);
     NormOut o1 = nout(Ld.gate_up);
     launch_residual_norm(o_out_, Ld.post_attn_norm, resid_, Ld.ffn_norm, o1, E, hp_.eps, ex_norm_, s);
+    if (dup("norm") > 1) {  // ablation: same launch on a scratch copy of the residual
+      LLMI_HIP(hipMemcpyAsync(resid_scratch_, resid_, (size_t)E * 4, hipMemcpyDeviceToDevice, s));
+      launch_residual_norm(o_out_, Ld.post_attn_norm, resid_scratch_, Ld.ffn_norm, o1, E, hp_.eps, ex_norm_, s);
+    }
     kernels_per_token_++;
-    gemv_parts(Ld.gate_up, xn_, E, gu_, s, o1.q8 != nullptr);
+    for (int r = 0; r < dup("gate_up"); r++) gemv_parts(Ld.gate_up, xn_, E, gu_, s, o1.q8 != nullptr);
     const bool d_q8 = Ld.down.w.type == T_Q4_0 || Ld.down.w.type == T_Q8_0;
-    launch_gelu_quant(gu_, F, hid_, d_q8 ? &act_.q8 : nullptr, s);
+    for (int r = 0; r < dup("gelu"); r++) launch_gelu_quant(gu_, F, hid_, d_q8 ? &act_.q8 : nullptr, s);
     kernels_per_token_++;
-    gemv_parts({Ld.down}, hid_, F, d_out_, s, d_q8);
+    for (int r = 0; r < dup("down"); r++) gemv_parts({Ld.down}, hid_, F, d_out_, s, d_q8);
     const bool last = l + 1 == hp_.n_layer;
     const float* w_next = last ? out_norm_ : L_[l + 1].attn_norm;
     NormOut o2 = last ? NormOut{} : nout(L_[l + 1].qkv);

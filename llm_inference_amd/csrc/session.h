@@ -67,6 +67,9 @@ class Session {
   void prepare_act(uint32_t wtype, const float* x, int n, ActBuf& act, hipStream_t s);
   void gemv_parts(const std::vector<GemvPart>& parts, const float* x, int n_in, float* out, hipStream_t s,
                   bool x_ready);
+  // LLMI_DUP ablation (diagnostics): kernel families launched twice per step,
+  // so the step-time delta is that family's in-graph cost
+  int dup(const char* k) const { return dup_.find(k) != std::string::npos ? 2 : 1; }
   void set_token_pos(int32_t token, int pos, bool reset_ring);
   void ensure_graph();
   void run_step();
@@ -106,6 +109,7 @@ class Session {
   hipGraph_t graph_ = nullptr;
   hipGraphExec_t graph_exec_ = nullptr;
   int kernels_per_token_ = 0;
+  std::string dup_;
   size_t weight_bytes_ = 0;
 };
 

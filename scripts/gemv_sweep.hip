@@ -111,15 +111,27 @@ int main(int argc, char** argv) {
     act.q8.xb = xb;
     act.q8.nb = nb;
 
+    // reps launches captured into one hipGraph (device-side cost per launch,
+    // including the kernel boundary, without the host launch rate)
     auto timeit = [&](const char* label, auto&& launch) {
       for (int i = 0; i < copies; i++) launch(ws[i % copies]);
       LLMI_HIP(hipStreamSynchronize(s));
-      LLMI_HIP(hipEventRecord(e0, s));
+      hipGraph_t g;
+      hipGraphExec_t ge;
+      LLMI_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
       for (int i = 0; i < reps; i++) launch(ws[i % copies]);
+      LLMI_HIP(hipStreamEndCapture(s, &g));
+      LLMI_HIP(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+      LLMI_HIP(hipGraphLaunch(ge, s));
+      LLMI_HIP(hipStreamSynchronize(s));
+      LLMI_HIP(hipEventRecord(e0, s));
+      LLMI_HIP(hipGraphLaunch(ge, s));
       LLMI_HIP(hipEventRecord(e1, s));
       LLMI_HIP(hipEventSynchronize(e1));
       float ms = 0;
       LLMI_HIP(hipEventElapsedTime(&ms, e0, e1));
+      (void)hipGraphExecDestroy(ge);
+      (void)hipGraphDestroy(g);
       const double us = ms * 1000.0 / reps;
       printf("%-12s %-34s %8.2f us  %7.1f GB/s\n", sh.name, label, us, wbytes / (us * 1e-6) / 1e9);
       fflush(stdout);

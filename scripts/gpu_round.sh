@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU-box session: GPU tests, smoke, bench (+ optional rocprof).  Every GPU
 # step has its own time limit; after a fault/abort/timeout nothing else runs.
-# usage: scripts/gpu_round.sh [tests] [smoke] [sweep] [bench] [prof] [pmc]
+# usage: scripts/gpu_round.sh [tests] [smoke] [sweep] [ablate] [bench] [prof] [pmc]
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -24,6 +24,7 @@ run() {  # name timeout cmd...
 want tests && run pytest_gpu 900 python -m pytest tests -m gpu -q -rP -p no:cacheprovider
 want smoke && run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 want sweep && run gemv_sweep 300 scripts/gemv_sweep 200
+want ablate && run ablate_run 900 bash scripts/ablate.sh
 want bench && run bench 900 python bench.py
 if want prof; then
   run rocprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- \
