@@ -95,18 +95,65 @@ __device__ __forceinline__ int nib_lo(uint32_t w) { return (int)(w & 0x0F0F0F0Fu
 __device__ __forceinline__ int nib_hi(uint32_t w) { return (int)((w >> 4) & 0x0F0F0F0Fu); }
 
 // ---------------------------------------------------------------------------
-// wave-level reductions (64 lanes).  Fixed xor-butterfly order, so results
-// are deterministic run to run.
+// wave-level reductions (64 lanes) on DPP lane swizzles + readlane, no LDS
+// round trips.  Fixed order: quad butterflies, row mirror, row half-mirror
+// (every lane of a 16-lane row then holds the row total, bit-identical since
+// a+b == b+a), then the four row totals combined as (r0+r1)+(r2+r3).
+// Deterministic run to run; call from wave-uniform control flow.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(dpp_i<CTRL>(__float_as_int(v)));
+}
+constexpr int DPP_QUAD_1032 = 0xB1, DPP_QUAD_2301 = 0x4E, DPP_ROW_MIRROR = 0x140, DPP_ROW_HALF_MIRROR = 0x141;
+
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_f<DPP_QUAD_1032>(v);
+  v += dpp_f<DPP_QUAD_2301>(v);
+  v += dpp_f<DPP_ROW_MIRROR>(v);
+  v += dpp_f<DPP_ROW_HALF_MIRROR>(v);
   return v;
 }
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+__device__ __forceinline__ float row16_max(float v) {
+  v = fmaxf(v, dpp_f<DPP_QUAD_1032>(v));
+  v = fmaxf(v, dpp_f<DPP_QUAD_2301>(v));
+  v = fmaxf(v, dpp_f<DPP_ROW_MIRROR>(v));
+  v = fmaxf(v, dpp_f<DPP_ROW_HALF_MIRROR>(v));
   return v;
+}
+__device__ __forceinline__ int row16_isum(int v) {
+  v += dpp_i<DPP_QUAD_1032>(v);
+  v += dpp_i<DPP_QUAD_2301>(v);
+  v += dpp_i<DPP_ROW_MIRROR>(v);
+  v += dpp_i<DPP_ROW_HALF_MIRROR>(v);
+  return v;
+}
+__device__ __forceinline__ float lane_f(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ float wave_sum(float v) {
+  v = row16_sum(v);
+  return (lane_f(v, 0) + lane_f(v, 16)) + (lane_f(v, 32) + lane_f(v, 48));
+}
+__device__ __forceinline__ float wave_max(float v) {
+  v = row16_max(v);
+  return fmaxf(fmaxf(lane_f(v, 0), lane_f(v, 16)), fmaxf(lane_f(v, 32), lane_f(v, 48)));
+}
+// 32-lane (half-wave) reductions: each half gets its own total
+__device__ __forceinline__ float half_max(float v) {
+  v = row16_max(v);
+  const float lo = fmaxf(lane_f(v, 0), lane_f(v, 16)), hi = fmaxf(lane_f(v, 32), lane_f(v, 48));
+  return (threadIdx.x & 32) ? hi : lo;
+}
+__device__ __forceinline__ int half_isum(int v) {
+  v = row16_isum(v);
+  const int lo = __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16);
+  const int hi = __builtin_amdgcn_readlane(v, 32) + __builtin_amdgcn_readlane(v, 48);
+  return (threadIdx.x & 32) ? hi : lo;
 }
 
 // orderable key for argmax with "first maximal index wins" (std::max_element,
@@ -143,17 +190,14 @@ struct Q8Act {
 // consecutive lanes (element = lane & 31), bit-exact: amax (order-free),
 // d = amax/127 (IEEE), id = 1/d from the UNROUNDED d, q = nearest_int(fma(x,
 // id, 1.5*2^23)), stored scale = f16(d).  Every lane of the 32-lane group must
-// execute this (shuffles); `ok` masks the stores.
+// execute this (lane swizzles), and the group is a half-wave (lanes 0-31 or
+// 32-63); `ok` masks the stores.
 __device__ __forceinline__ void q8_block_store(float v, bool ok, XBlock* blk, int e) {
-  float amax = fabsf(v);
-#pragma unroll
-  for (int o = 16; o >= 1; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o));
+  const float amax = half_max(fabsf(v));  // max and integer sum: order-free, exact
   const float dd = amax / 127.0f;
   const float id = dd != 0.0f ? 1.0f / dd : 0.0f;
   const int q = nearest_int_fma(v, id);
-  int s = q;
-#pragma unroll
-  for (int o = 16; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+  const int s = half_isum(q);
   if (ok) {
     reinterpret_cast<int8_t*>(blk)[e] = (int8_t)q;
     if (e == 0) {
@@ -166,8 +210,8 @@ __device__ __forceinline__ void q8_block_store(float v, bool ok, XBlock* blk, in
 // f / nb by multiply-high for the small f of one wave's chunk; nb == 1 has
 // no 32-bit magic and is encoded as 0
 __host__ __device__ inline uint32_t div_magic(uint32_t nb) { return nb == 1 ? 0u : (uint32_t)((1ull << 32) / nb + 1); }
-__device__ __forceinline__ int div_by_magic(int f, uint32_t magic) {
-  return magic ? (int)__umulhi((uint32_t)f, magic) : f;
+__device__ __forceinline__ int div_by_magic(int f, uint32_t magic) {  // branch-free
+  return (int)(__umulhi((uint32_t)f, magic) + ((uint32_t)f & (magic ? 0u : 0xFFFFFFFFu)));
 }
 
 }  // namespace llmi

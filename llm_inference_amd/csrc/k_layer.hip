@@ -24,6 +24,7 @@ namespace llmi {
 namespace {
 
 constexpr int PRO_EPT = 12;  // prologue elements per thread (n <= 12 * threads)
+constexpr int X_LD = 8;      // 16-B activation loads per thread (nb * 3 <= 8 * threads)
 
 
 template <int NW>
@@ -42,9 +43,9 @@ __device__ __forceinline__ float rms_scale_d(float sum, int n, double eps) {  //
 }
 
 template <int P>
-struct Chunk {
+struct Chunk {  // raw loaded words: converting at load time would wait for them
   uint4 q[P];
-  float sw[P];
+  uint16_t sw[P];
   int rr[P], bb[P];
 };
 
@@ -59,7 +60,7 @@ __device__ __forceinline__ void load_chunk(Chunk<P>& c, const uint4* qw, const u
     c.rr[p] = f < total ? r : R;
     c.bb[p] = fc - r * nb;
     c.q[p] = ld_nt(qw + fc);
-    c.sw[p] = h2f(ld_nt16(dw + fc));
+    c.sw[p] = ld_nt16(dw + fc);
   }
 }
 
@@ -78,7 +79,7 @@ __device__ __forceinline__ void eat_chunk(const Chunk<P>& c, const XBlock* s_x, 
     is = sdot4(nib_hi(c.q[p].y), x1.y, is);
     is = sdot4(nib_hi(c.q[p].z), x1.z, is);
     is = sdot4(nib_hi(c.q[p].w), x1.w, is);
-    const float v = (c.sw[p] * __int_as_float(x2.x)) * (float)is;
+    const float v = (h2f(c.sw[p]) * __int_as_float(x2.x)) * (float)is;
 #pragma unroll
     for (int k = 0; k < R; k++) acc[k] += (k == c.rr[p]) ? v : 0.0f;
   }
@@ -100,9 +101,9 @@ __global__ __launch_bounds__(NW * 64) void gemv_q4_0_layer(LayerGemv a) {
   const uint16_t* dw = a.wd + (size_t)min(row0, a.rows - 1) * nb;
 
   Chunk<P> ca, cb;
-  if (total > 0) load_chunk<R, P>(ca, qw, dw, 0, total, nb, a.magic, lane);
-
   if constexpr (PRO) {
+    // prologue operands first: loads return in issue order, so issuing them
+    // ahead of the weight chunk lets the norm run while the weights stream
     const int n = a.n;
     float yv[PRO_EPT], rv[PRO_EPT], wp[PRO_EPT], wn[PRO_EPT];
 #pragma unroll
@@ -114,6 +115,8 @@ __global__ __launch_bounds__(NW * 64) void gemv_q4_0_layer(LayerGemv a) {
       wp[k] = (ok && a.w_post) ? a.w_post[i] : 0.0f;
       wn[k] = ok ? a.w_next[i] : 0.0f;
     }
+    load_chunk<R, P>(ca, qw, dw, 0, total, nb, a.magic, lane);  // unconditional (valid clamped rows): a
+    // branch here would merge wait counts to vmcnt(0) at the first prologue use
     float ss = 0.0f;
 #pragma unroll
     for (int k = 0; k < PRO_EPT; k++) ss = fmaf(yv[k], yv[k], ss);
@@ -138,9 +141,17 @@ __global__ __launch_bounds__(NW * 64) void gemv_q4_0_layer(LayerGemv a) {
       q8_block_store(xv, ok, s_x + (ok ? (i >> 5) : 0), i & 31);
     }
   } else {
+    // x blocks -> LDS: clamped unconditional loads (no branch between them
+    // and the weight loads, so the stores wait only for their own data)
     const uint4* src = reinterpret_cast<const uint4*>(a.xg);
     uint4* dst = reinterpret_cast<uint4*>(s_x);
-    for (int i = t; i < nb * 3; i += T) dst[i] = src[i];
+    const int n16 = nb * 3;
+    uint4 xr[X_LD];
+#pragma unroll
+    for (int k = 0; k < X_LD; k++) xr[k] = src[min(t + k * T, n16 - 1)];
+    load_chunk<R, P>(ca, qw, dw, 0, total, nb, a.magic, lane);
+#pragma unroll
+    for (int k = 0; k < X_LD; k++) dst[min(t + k * T, n16)] = xr[k];  // slot n16: LDS pad (discarded)
   }
   __syncthreads();
 
@@ -220,7 +231,7 @@ void launch_r(int R, int P, dim3 grid, size_t lds, const LayerGemv& a, hipStream
 bool layer_gemv_supported(const DevWeight& w, bool pro, bool gelu, int n_pro) {
   if (w.type != T_Q4_0 || w.cols % 32 != 0 || w.rows <= 0) return false;
   const int nb = w.cols / 32;
-  if ((size_t)nb * sizeof(XBlock) > 64 * 1024) return false;
+  if ((size_t)nb * sizeof(XBlock) > 64 * 1024 || nb * 3 > X_LD * 256) return false;
   if (pro && n_pro > PRO_EPT * 512) return false;
   if (pro && n_pro != w.cols) return false;
   if (gelu && w.rows % 64 != 0) return false;
@@ -238,7 +249,7 @@ void launch_layer_gemv(const DevWeight& w, LayerGemv a, bool pro, bool gelu, hip
   a.nb = w.cols / 32;
   a.magic = div_magic(a.nb);
   if (pro) a.n = w.cols;
-  const size_t lds = (size_t)a.nb * sizeof(XBlock);
+  const size_t lds = (size_t)a.nb * sizeof(XBlock) + 16;  // + pad slot of the x copy
   if (gelu) {  // 8 waves x 8 rows = 64 interleaved gate/up rows per WG
     if (!pro) throw std::runtime_error("layer gemv: GELU epilogue needs the norm prologue");
     const int P = passes_for(8, a.nb);

@@ -476,10 +476,8 @@ void Session::record_layers(hipStream_t s, bool x_q8) {
     for (int r = 0; r < dup("o_proj"); r++) gemv_parts({Ld.o}, attn_, hp_.n_head * hd, o_out_, s, fused_q8);
     NormOut o1 = nout(Ld.gate_up);
     launch_residual_norm(o_out_, Ld.post_attn_norm, resid_, Ld.ffn_norm, o1, E, hp_.eps, ex_norm_, s);
-    if (dup("norm") > 1) {  // ablation: same launch on a scratch copy of the residual
-      LLMI_HIP(hipMemcpyAsync(resid_scratch_, resid_, (size_t)E * 4, hipMemcpyDeviceToDevice, s));
+    if (dup("norm") > 1)  // ablation: the same launch on a scratch residual (values irrelevant)
       launch_residual_norm(o_out_, Ld.post_attn_norm, resid_scratch_, Ld.ffn_norm, o1, E, hp_.eps, ex_norm_, s);
-    }
     kernels_per_token_++;
     for (int r = 0; r < dup("gate_up"); r++) gemv_parts(Ld.gate_up, xn_, E, gu_, s, o1.q8 != nullptr);
     const bool d_q8 = Ld.down.w.type == T_Q4_0 || Ld.down.w.type == T_Q8_0;

@@ -176,7 +176,7 @@ int main(int argc, char** argv) {
         a.nb = nb;
         a.magic = mg;
         hipLaunchKernelGGL(kern, dim3((w.rows + rows_per_wg - 1) / rows_per_wg), dim3(threads),
-                           (size_t)nb * sizeof(XBlock), s, a);
+                           (size_t)nb * sizeof(XBlock) + 16, s, a);
       });
     };
     if (nb % 64 == 0) {
