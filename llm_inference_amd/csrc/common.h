@@ -207,6 +207,40 @@ __device__ __forceinline__ void q8_block_store(float v, bool ok, XBlock* blk, in
   }
 }
 
+// The same quantization of one block by ONE thread (no cross-lane traffic):
+// used where a whole vector is staged in LDS and each thread owns a block.
+// Bit-identical to q8_block_store (max and integer sums are order-free).
+__device__ __forceinline__ void q8_block_serial(const float* __restrict__ x32, XBlock* __restrict__ blk) {
+  float v[32];
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const float4 f = reinterpret_cast<const float4*>(x32)[k];
+    v[4 * k] = f.x; v[4 * k + 1] = f.y; v[4 * k + 2] = f.z; v[4 * k + 3] = f.w;
+  }
+  float amax = 0.0f;
+#pragma unroll
+  for (int k = 0; k < 32; k++) amax = fmaxf(amax, fabsf(v[k]));
+  const float dd = amax / 127.0f;
+  const float id = dd != 0.0f ? 1.0f / dd : 0.0f;
+  int s = 0;
+  uint32_t w[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    uint32_t pk = 0;
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      const int q = nearest_int_fma(v[4 * k + e], id);
+      s += q;
+      pk |= (uint32_t)(q & 0xFF) << (8 * e);
+    }
+    w[k] = pk;
+  }
+  blk->lo = make_int4((int)w[0], (int)w[1], (int)w[2], (int)w[3]);
+  blk->hi = make_int4((int)w[4], (int)w[5], (int)w[6], (int)w[7]);
+  blk->d = h2f(f2h_ggml(dd));
+  blk->nsum8 = -8 * s;
+}
+
 // f / nb by multiply-high for the small f of one wave's chunk; nb == 1 has
 // no 32-bit magic and is encoded as 0
 __host__ __device__ inline uint32_t div_magic(uint32_t nb) { return nb == 1 ? 0u : (uint32_t)((1ull << 32) / nb + 1); }

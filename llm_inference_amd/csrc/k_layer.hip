@@ -23,8 +23,6 @@ namespace llmi {
 
 namespace {
 
-constexpr int PRO_EPT = 12;  // prologue elements per thread (n <= 12 * threads)
-constexpr int X_LD = 8;      // 16-B activation loads per thread (nb * 3 <= 8 * threads)
 
 
 template <int NW>
@@ -85,8 +83,11 @@ __device__ __forceinline__ void eat_chunk(const Chunk<P>& c, const XBlock* s_x, 
   }
 }
 
-template <int R, int NW, int P, bool PRO, bool GELU>
+// E: prologue elements per thread (PRO) or 16-B x loads per thread (!PRO);
+// MULTI: the wave's items span more than one chunk of P passes
+template <int R, int NW, int P, int E, bool PRO, bool GELU, bool MULTI>
 __global__ __launch_bounds__(NW * 64) void gemv_q4_0_layer(LayerGemv a) {
+  constexpr int EPT = E, X_LD = E;
   extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
   XBlock* s_x = reinterpret_cast<XBlock*>(s_dyn);
   __shared__ float s_red[2][NW];
@@ -105,9 +106,9 @@ __global__ __launch_bounds__(NW * 64) void gemv_q4_0_layer(LayerGemv a) {
     // prologue operands first: loads return in issue order, so issuing them
     // ahead of the weight chunk lets the norm run while the weights stream
     const int n = a.n;
-    float yv[PRO_EPT], rv[PRO_EPT], wp[PRO_EPT], wn[PRO_EPT];
+    float yv[EPT], rv[EPT], wp[EPT], wn[EPT];
 #pragma unroll
-    for (int k = 0; k < PRO_EPT; k++) {
+    for (int k = 0; k < EPT; k++) {
       const int i = t + k * T;
       const bool ok = i < n;
       yv[k] = ok ? a.y[i] : 0.0f;
@@ -119,11 +120,11 @@ __global__ __launch_bounds__(NW * 64) void gemv_q4_0_layer(LayerGemv a) {
     // branch here would merge wait counts to vmcnt(0) at the first prologue use
     float ss = 0.0f;
 #pragma unroll
-    for (int k = 0; k < PRO_EPT; k++) ss = fmaf(yv[k], yv[k], ss);
+    for (int k = 0; k < EPT; k++) ss = fmaf(yv[k], yv[k], ss);
     const float sc1 = rms_scale_d(wg_sum<NW>(ss, s_red[0]), n, a.eps);
     float ss2 = 0.0f;
 #pragma unroll
-    for (int k = 0; k < PRO_EPT; k++) {
+    for (int k = 0; k < EPT; k++) {
       const float h = rv[k] + (a.w_post ? (sc1 * yv[k]) * wp[k] : yv[k]);  // no post-norm: plain add
       rv[k] = h;
       ss2 = fmaf(h, h, ss2);
@@ -131,15 +132,20 @@ __global__ __launch_bounds__(NW * 64) void gemv_q4_0_layer(LayerGemv a) {
       if (blockIdx.x == 0 && i < n) a.resid_out[i] = h;
     }
     const float sc2 = rms_scale_d(wg_sum<NW>(ss2, s_red[1]), n, a.eps);
+    // x staged as f32 in LDS, then one thread per Q8_0 block (no cross-lane
+    // reductions on this latency-critical path)
+    float* s_xf = reinterpret_cast<float*>(s_dyn + (size_t)nb * sizeof(XBlock) + 16);
 #pragma unroll
-    for (int k = 0; k < PRO_EPT; k++) {
+    for (int k = 0; k < EPT; k++) {
       const int i = t + k * T;
-      if (k * T >= n) break;
-      const bool ok = i < n;
       const float xv = (sc2 * rv[k]) * wn[k];
-      if (blockIdx.x == 0 && ok && a.xn_out) a.xn_out[i] = xv;
-      q8_block_store(xv, ok, s_x + (ok ? (i >> 5) : 0), i & 31);
+      if (i < n) {
+        s_xf[i] = xv;
+        if (blockIdx.x == 0 && a.xn_out) a.xn_out[i] = xv;
+      }
     }
+    __syncthreads();
+    for (int b = t; b < nb; b += T) q8_block_serial(s_xf + 32 * b, s_x + b);
   } else {
     // x blocks -> LDS: clamped unconditional loads (no branch between them
     // and the weight loads, so the stores wait only for their own data)
@@ -158,13 +164,17 @@ __global__ __launch_bounds__(NW * 64) void gemv_q4_0_layer(LayerGemv a) {
   float acc[R];
 #pragma unroll
   for (int k = 0; k < R; k++) acc[k] = 0.0f;
-  constexpr int CH = 64 * P;
-  for (int c0 = 0; c0 < total; c0 += 2 * CH) {
-    if (c0 + CH < total) load_chunk<R, P>(cb, qw, dw, c0 + CH, total, nb, a.magic, lane);
+  if constexpr (!MULTI) {
     eat_chunk<R, P>(ca, s_x, acc);
-    if (c0 + CH >= total) break;
-    if (c0 + 2 * CH < total) load_chunk<R, P>(ca, qw, dw, c0 + 2 * CH, total, nb, a.magic, lane);
-    eat_chunk<R, P>(cb, s_x, acc);
+  } else {
+    constexpr int CH = 64 * P;
+    for (int c0 = 0; c0 < total; c0 += 2 * CH) {
+      if (c0 + CH < total) load_chunk<R, P>(cb, qw, dw, c0 + CH, total, nb, a.magic, lane);
+      eat_chunk<R, P>(ca, s_x, acc);
+      if (c0 + CH >= total) break;
+      if (c0 + 2 * CH < total) load_chunk<R, P>(ca, qw, dw, c0 + 2 * CH, total, nb, a.magic, lane);
+      eat_chunk<R, P>(cb, s_x, acc);
+    }
   }
 
   if constexpr (GELU) {
@@ -189,53 +199,68 @@ __global__ __launch_bounds__(NW * 64) void gemv_q4_0_layer(LayerGemv a) {
   }
 }
 
-int rows_per_wave_l(int nb) {
-  int R = 1;
-  while (R < 8 && (R * nb) % 64 != 0) R *= 2;
-  return R;
+// ---- launch table ----------------------------------------------------------
+// One instantiation per (activation length, role) of the Gemma-3 1B/4B/12B/27B
+// projections; shapes outside the table take the unfused path (session.cpp).
+//   R: rows per wave (R * nb a multiple of 64 where possible), P: passes per
+//   chunk, E: see the kernel, NW: waves per WG (8 when the prologue's vector
+//   exceeds 12 elements per thread of a 256-thread WG, and for GELU: 64 rows).
+enum { ROLE_PLAIN = 0, ROLE_PRO = 1, ROLE_GELU = 2 };
+
+using LaunchFn = void (*)(dim3, size_t, const LayerGemv&, hipStream_t);
+
+template <int R, int NW, int P, int E, int ROLE, bool MULTI>
+void launch_cfg(dim3 grid, size_t lds, const LayerGemv& a, hipStream_t s) {
+  hipLaunchKernelGGL((gemv_q4_0_layer<R, NW, P, E, ROLE != ROLE_PLAIN, ROLE == ROLE_GELU, MULTI>), grid, dim3(NW * 64),
+                     lds, s, a);
 }
 
-// passes per chunk: split the wave's passes into ceil(passes/8) equal chunks,
-// rounded up to an instantiated P
-int passes_for(int R, int nb) {
-  const int passes = (R * nb + 63) / 64;
-  const int chunks = (passes + 7) / 8;
-  const int p = (passes + chunks - 1) / chunks;
-  return p == 3 ? 4 : p;
-}
+struct LayerCfg {
+  int nb, role, R, NW, P;
+  bool multi;
+  LaunchFn fn;
+};
 
-template <int R, int NW, bool PRO, bool GELU>
-void launch_rp(int P, dim3 grid, size_t lds, const LayerGemv& a, hipStream_t s) {
-  switch (P) {
-#define LLMI_L_CASE(PP) \
-  case PP: hipLaunchKernelGGL((gemv_q4_0_layer<R, NW, PP, PRO, GELU>), grid, dim3(NW * 64), lds, s, a); break;
-    LLMI_L_CASE(1) LLMI_L_CASE(2) LLMI_L_CASE(4) LLMI_L_CASE(5) LLMI_L_CASE(6) LLMI_L_CASE(7) LLMI_L_CASE(8)
-#undef LLMI_L_CASE
-    default: throw std::runtime_error("layer gemv: no kernel for P=" + std::to_string(P));
-  }
-}
+#define LLMI_LCFG(NB, ROLE, R, NW, P, E, MULTI) {NB, ROLE, R, NW, P, MULTI, launch_cfg<R, NW, P, E, ROLE, MULTI>}
+const LayerCfg kLayerCfgs[] = {
+    // plain: x blocks copied to LDS (E = 16-B loads per thread = ceil(3 nb / 256))
+    LLMI_LCFG(32, ROLE_PLAIN, 2, 4, 1, 1, false),    // 1B o (4 x 256)
+    LLMI_LCFG(36, ROLE_PLAIN, 8, 4, 5, 1, false),    // 1B qkv, layer 0
+    LLMI_LCFG(64, ROLE_PLAIN, 1, 4, 1, 1, false),    // 4B o (8 x 256)
+    LLMI_LCFG(80, ROLE_PLAIN, 4, 4, 5, 1, false),    // 4B qkv, layer 0
+    LLMI_LCFG(120, ROLE_PLAIN, 8, 4, 8, 2, true),    // 12B qkv, layer 0
+    LLMI_LCFG(128, ROLE_PLAIN, 1, 4, 2, 2, false),   // 12B / 27B o (16 x 256, 32 x 128)
+    LLMI_LCFG(168, ROLE_PLAIN, 8, 4, 7, 2, true),    // 27B qkv, layer 0
+    LLMI_LCFG(216, ROLE_PLAIN, 8, 4, 7, 4, true),    // 1B down
+    LLMI_LCFG(320, ROLE_PLAIN, 1, 4, 5, 4, false),   // 4B down
+    LLMI_LCFG(480, ROLE_PLAIN, 2, 4, 8, 8, true),    // 12B down
+    LLMI_LCFG(672, ROLE_PLAIN, 2, 4, 7, 8, true),    // 27B down
+    // residual + norm prologue (E = prologue elements per thread)
+    LLMI_LCFG(36, ROLE_PRO, 8, 4, 5, 12, false),
+    LLMI_LCFG(80, ROLE_PRO, 4, 4, 5, 12, false),
+    LLMI_LCFG(120, ROLE_PRO, 8, 8, 8, 12, true),
+    LLMI_LCFG(168, ROLE_PRO, 8, 8, 7, 12, true),
+    // prologue + GELU epilogue: 8 waves x 8 rows = 64 interleaved gate/up rows
+    LLMI_LCFG(36, ROLE_GELU, 8, 8, 5, 6, false),
+    LLMI_LCFG(80, ROLE_GELU, 8, 8, 5, 6, true),
+    LLMI_LCFG(120, ROLE_GELU, 8, 8, 8, 12, true),
+    LLMI_LCFG(168, ROLE_GELU, 8, 8, 7, 12, true),
+};
+#undef LLMI_LCFG
 
-template <int NW, bool PRO, bool GELU>
-void launch_r(int R, int P, dim3 grid, size_t lds, const LayerGemv& a, hipStream_t s) {
-  switch (R) {
-    case 1: launch_rp<1, NW, PRO, GELU>(P, grid, lds, a, s); break;
-    case 2: launch_rp<2, NW, PRO, GELU>(P, grid, lds, a, s); break;
-    case 4: launch_rp<4, NW, PRO, GELU>(P, grid, lds, a, s); break;
-    case 8: launch_rp<8, NW, PRO, GELU>(P, grid, lds, a, s); break;
-    default: throw std::runtime_error("layer gemv: bad R");
-  }
+const LayerCfg* find_cfg(int nb, int role) {
+  for (const auto& c : kLayerCfgs)
+    if (c.nb == nb && c.role == role) return &c;
+  return nullptr;
 }
 
 }  // namespace
 
 bool layer_gemv_supported(const DevWeight& w, bool pro, bool gelu, int n_pro) {
   if (w.type != T_Q4_0 || w.cols % 32 != 0 || w.rows <= 0) return false;
-  const int nb = w.cols / 32;
-  if ((size_t)nb * sizeof(XBlock) > 64 * 1024 || nb * 3 > X_LD * 256) return false;
-  if (pro && n_pro > PRO_EPT * 512) return false;
   if (pro && n_pro != w.cols) return false;
-  if (gelu && w.rows % 64 != 0) return false;
-  return true;
+  if (gelu && (!pro || w.rows % 64 != 0)) return false;
+  return find_cfg(w.cols / 32, gelu ? ROLE_GELU : (pro ? ROLE_PRO : ROLE_PLAIN)) != nullptr;
 }
 
 void launch_layer_gemv(const DevWeight& w, LayerGemv a, bool pro, bool gelu, hipStream_t s) {
@@ -243,31 +268,18 @@ void launch_layer_gemv(const DevWeight& w, LayerGemv a, bool pro, bool gelu, hip
   if (pro ? (!a.y || !a.resid_in || !a.resid_out || !a.w_next || a.resid_in == a.resid_out) : !a.xg)
     throw std::runtime_error("layer gemv: missing prologue operand");
   if (gelu ? (!a.hid || !a.hq8) : !a.out) throw std::runtime_error("layer gemv: missing output");
+  const LayerCfg& c = *find_cfg(w.cols / 32, gelu ? ROLE_GELU : (pro ? ROLE_PRO : ROLE_PLAIN));
+  if (!c.multi && c.R * (w.cols / 32) > 64 * c.P) throw std::runtime_error("layer gemv: table entry needs MULTI");
   a.qs = reinterpret_cast<const uint4*>(w.qs);
   a.wd = w.d;
   a.rows = w.rows;
   a.nb = w.cols / 32;
   a.magic = div_magic(a.nb);
   if (pro) a.n = w.cols;
-  const size_t lds = (size_t)a.nb * sizeof(XBlock) + 16;  // + pad slot of the x copy
-  if (gelu) {  // 8 waves x 8 rows = 64 interleaved gate/up rows per WG
-    if (!pro) throw std::runtime_error("layer gemv: GELU epilogue needs the norm prologue");
-    const int P = passes_for(8, a.nb);
-    launch_rp<8, 8, true, true>(P, dim3(w.rows / 64), lds, a, s);
-  } else {
-    const int R = rows_per_wave_l(a.nb), P = passes_for(R, a.nb);
-    const bool wide = pro && a.n > PRO_EPT * 256;  // 512-thread WGs for n_embd > 3072
-    if (wide) {
-      const dim3 grid((w.rows + 8 * R - 1) / (8 * R));
-      launch_r<8, true, false>(R, P, grid, lds, a, s);
-    } else {
-      const dim3 grid((w.rows + 4 * R - 1) / (4 * R));
-      if (pro)
-        launch_r<4, true, false>(R, P, grid, lds, a, s);
-      else
-        launch_r<4, false, false>(R, P, grid, lds, a, s);
-    }
-  }
+  // x blocks + pad slot of the x copy (+ the f32 x staging of the prologue)
+  const size_t lds = (size_t)a.nb * sizeof(XBlock) + 16 + (pro ? (size_t)a.n * 4 : 0);
+  const int rows_per_wg = c.NW * c.R;
+  c.fn(dim3((w.rows + rows_per_wg - 1) / rows_per_wg), lds, a, s);
   LLMI_HIP(hipGetLastError());
 }
 

@@ -152,15 +152,27 @@ __device__ __forceinline__ float rms_scale(float sum, int n, double eps) {  // o
 // ---------------------------------------------------------------------------
 constexpr int NORM_EPT = 8;  // elements per thread (n <= 8192)
 
-__device__ __forceinline__ void norm_outputs(const float (&xv)[NORM_EPT], int n, const NormOut& out) {
+// s_h: n floats of LDS (free again: callers are past their last use of it).
+// Q8_0 blocks: x staged in LDS, one thread per block (q8_block_serial).
+__device__ __forceinline__ void norm_outputs(const float (&xv)[NORM_EPT], int n, const NormOut& out, float* s_h) {
   const int t = threadIdx.x;
+  __syncthreads();  // s_h reuse
 #pragma unroll
   for (int k = 0; k < NORM_EPT; k++) {
     const int i = t + k * 1024;
-    const bool ok = i < n;
-    if (ok) out.xn[i] = xv[k];
-    if (out.x16 && ok) out.x16[i] = f2h_ggml(xv[k]);
-    if (out.q8 && k * 1024 < n) q8_block_store(xv[k], ok, out.q8 + (ok ? (i >> 5) : 0), i & 31);
+    if (i < n) {
+      out.xn[i] = xv[k];
+      s_h[i] = xv[k];
+      if (out.x16) out.x16[i] = f2h_ggml(xv[k]);
+    }
+  }
+  if (out.q8) {
+    __syncthreads();
+    for (int b = t; b < n / 32; b += 1024) {
+      XBlock blk;
+      q8_block_serial(s_h + 32 * b, &blk);
+      out.q8[b] = blk;
+    }
   }
 }
 
@@ -185,7 +197,7 @@ __global__ __launch_bounds__(1024) void residual_norm_kernel(const float* __rest
                                                              float* __restrict__ resid,
                                                              const float* __restrict__ w_next, NormOut out, int n,
                                                              double eps) {
-  extern __shared__ float s_h[];  // exact mode staging only
+  extern __shared__ float s_h[];  // [n]: exact-mode sum staging, then the Q8_0 staging
   __shared__ float sh[16];
   const int t = threadIdx.x;
   float yv[NORM_EPT], rv[NORM_EPT], wp[NORM_EPT], wn[NORM_EPT];
@@ -212,7 +224,7 @@ __global__ __launch_bounds__(1024) void residual_norm_kernel(const float* __rest
   float xv[NORM_EPT];
 #pragma unroll
   for (int k = 0; k < NORM_EPT; k++) xv[k] = (sc2 * hv[k]) * wn[k];
-  norm_outputs(xv, n, out);
+  norm_outputs(xv, n, out, s_h);
 }
 
 void launch_residual_norm(const float* y, const float* w_post, float* resid, const float* w_next, const NormOut& out,
@@ -222,7 +234,8 @@ void launch_residual_norm(const float* y, const float* w_post, float* resid, con
     hipLaunchKernelGGL(residual_norm_kernel<true>, dim3(1), dim3(1024), (size_t)n * 4, s, y, w_post, resid, w_next, out,
                        n, eps);
   else
-    hipLaunchKernelGGL(residual_norm_kernel<false>, dim3(1), dim3(1024), 0, s, y, w_post, resid, w_next, out, n, eps);
+    hipLaunchKernelGGL(residual_norm_kernel<false>, dim3(1), dim3(1024), (size_t)n * 4, s, y, w_post, resid, w_next,
+                       out, n, eps);
   LLMI_HIP(hipGetLastError());
 }
 
@@ -305,7 +318,7 @@ __global__ __launch_bounds__(1024) void embed_norm_kernel(uint32_t type, const u
                                                           float emb_scale, float* __restrict__ resid,
                                                           const float* __restrict__ w, NormOut out, int n,
                                                           double eps) {
-  extern __shared__ float s_h[];  // exact mode staging only
+  extern __shared__ float s_h[];  // [n]: exact-mode sum staging, then the Q8_0 staging
   __shared__ float sh[16];
   const int t = threadIdx.x;
   const uint8_t* row = table + (size_t)(*d_token) * row_bytes;
@@ -322,7 +335,7 @@ __global__ __launch_bounds__(1024) void embed_norm_kernel(uint32_t type, const u
   float xv[NORM_EPT];
 #pragma unroll
   for (int k = 0; k < NORM_EPT; k++) xv[k] = (sc * ev[k]) * wv[k];
-  norm_outputs(xv, n, out);
+  norm_outputs(xv, n, out, s_h);
 }
 
 __device__ float deq_embed(uint32_t type, const uint8_t* row, int i) {
@@ -345,7 +358,7 @@ void launch_embed_norm(uint32_t type, const uint8_t* table, size_t row_bytes, co
     hipLaunchKernelGGL(embed_norm_kernel<true>, dim3(1), dim3(1024), (size_t)n * 4, s, type, table, row_bytes, d_token,
                        emb_scale, resid, w, out, n, eps);
   else
-    hipLaunchKernelGGL(embed_norm_kernel<false>, dim3(1), dim3(1024), 0, s, type, table, row_bytes, d_token,
+    hipLaunchKernelGGL(embed_norm_kernel<false>, dim3(1), dim3(1024), (size_t)n * 4, s, type, table, row_bytes, d_token,
                        emb_scale, resid, w, out, n, eps);
   LLMI_HIP(hipGetLastError());
 }
