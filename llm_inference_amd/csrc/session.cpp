@@ -150,7 +150,24 @@ void Session::upload(const GGUFView& g) {  // model.cpp:169-238 tensor map
     const GTensor *gt = T("ffn_gate.weight"), *up = T("ffn_up.weight"), *dn = T("ffn_down.weight");
     if ((int)gt->shape[1] != hp_.n_ff || (int)up->shape[1] != hp_.n_ff || (int)dn->shape[0] != hp_.n_ff)
       throw status_error(LLMI_E_SIZE, "ffn shapes do not match feed_forward_length");
-    if (fuse_layers_ && gt->type == T_Q4_0 && up->type == T_Q4_0 && gt->shape[0] == up->shape[0] && hp_.n_ff % 32 == 0) {
+    // the fused layer path (k_layer.hip) needs every projection in its launch
+    // table; decided from the GGUF shapes before upload because it changes
+    // the gate/up row order
+    auto shape_ok = [](const GTensor* t, int rows, bool pro, bool gelu, int n_pro) {
+      DevWeight w;
+      w.type = t->type;
+      w.rows = rows;
+      w.cols = (int)t->shape[0];
+      return layer_gemv_supported(w, pro, gelu, n_pro);
+    };
+    const bool qkv_same = q->type == k->type && q->type == v->type && q->shape[0] == k->shape[0] &&
+                          q->shape[0] == v->shape[0];
+    const bool want_fused =
+        fuse_layers_ && qkv_same && gt->type == T_Q4_0 && up->type == T_Q4_0 && gt->shape[0] == up->shape[0] &&
+        hp_.n_ff % 32 == 0 && shape_ok(q, (int)(q->shape[1] + k->shape[1] + v->shape[1]), true, false, hp_.n_embd) &&
+        shape_ok(o, (int)o->shape[1], false, false, 0) && shape_ok(gt, 2 * hp_.n_ff, true, true, hp_.n_embd) &&
+        shape_ok(dn, (int)dn->shape[1], false, false, 0);
+    if (want_fused) {
       // rows interleaved in groups of 32 (gate 32k.., up 32k..) for the fused
       // GELU epilogue of gemv_q4_0_layer (k_layer.hip)
       const int cols = (int)gt->shape[0], F = hp_.n_ff;

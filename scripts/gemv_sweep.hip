@@ -148,7 +148,9 @@ int main(int argc, char** argv) {
     LayerGemv plain;
     plain.xg = xb;
     plain.out = out;
-    timeit("layer plain", [&](const DevWeight& w) { launch_layer_gemv(w, plain, false, false, s); });
+    DevWeight probe = ws[0];
+    if (layer_gemv_supported(probe, false, false, 0))
+      timeit("layer plain", [&](const DevWeight& w) { launch_layer_gemv(w, plain, false, false, s); });
     LayerGemv pro;
     pro.y = y;
     pro.resid_in = r0;
@@ -157,12 +159,13 @@ int main(int argc, char** argv) {
     pro.w_next = wn;
     pro.eps = 1e-6;
     pro.out = out;
-    if (sh.cols <= 6144) timeit("layer pro", [&](const DevWeight& w) { launch_layer_gemv(w, pro, true, false, s); });
+    if (layer_gemv_supported(probe, true, false, sh.cols))
+      timeit("layer pro", [&](const DevWeight& w) { launch_layer_gemv(w, pro, true, false, s); });
     LayerGemv gl = pro;
     gl.out = nullptr;
     gl.hid = hid;
     gl.hq8 = hq;
-    if (sh.rows % 64 == 0 && sh.cols <= 6144)
+    if (layer_gemv_supported(probe, true, true, sh.cols))
       timeit("layer pro+gelu", [&](const DevWeight& w) { launch_layer_gemv(w, gl, true, true, s); });
     // geometry variants of the plain kernel
     const uint32_t mg = div_magic(nb);
