@@ -107,7 +107,7 @@ typedef struct {
   int device;          /* HIP device ordinal */
   uint32_t flags;      /* LLMI_EXACT | LLMI_NO_GRAPH */
   int max_ctx;         /* KV-cache capacity in positions (default 4096) */
-  int attn_split;      /* fast attention split count (0 = auto) */
+  int attn_split;      /* fast attention key-range splits: 0 = default (32, the only value) */
 } llmi_session_opts;
 
 /* Parses the GGUF (format of gguf.cpp:274-304, hparams of model.cpp:58-167)

@@ -21,22 +21,26 @@ struct QKVArgs {
   const int* d_pos;       // device position of this token
 };
 
+constexpr int ATTN_NSPLIT = 32;  // key-range splits of the fast attention (work-groups per kv head)
+
 struct AttnArgs {
   const float* q;         // [n_head][head_dim], normed/roped/scaled
   const uint16_t* k_cache;
   const uint16_t* v_cache;
   int n_head, n_head_kv, head_dim, max_ctx;
   const int* d_pos;       // keys 0..*d_pos are attended (no window: model.cpp:501)
-  float* partial;         // fast path scratch [n_head][nsplit][head_dim + 2]
+  float* partial;         // fast path scratch [n_head][ATTN_NSPLIT][head_dim + 2]
   float* out;             // [n_head][head_dim]
+  unsigned* ticket;       // fast path: [n_head_kv] zeroed counters (reset by the kernel)
+  XBlock* q8;             // optional: Q8_0 blocks of out (head_dim % 32 == 0)
 };
 
 void launch_qk_norm_rope_kv(const QKVArgs& a, bool exact, hipStream_t s);
-// exact: attn_exact_kernel -> out.  fast: partial + combine (-> out, and
-// Q8_0 blocks of out when q8 != nullptr).
-// fused != nullptr (fast path only): the partial kernel also does the q/k
-// norm + rope + q scale + KV append of qk_norm_rope_kv (one launch fewer).
-void launch_attention(const AttnArgs& a, bool exact, int nsplit, const Q8Act* q8, hipStream_t s,
-                      const QKVArgs* fused = nullptr);
+// exact: attn_exact_kernel -> out.  fast: one split-K launch whose last
+// work-group per kv head merges the partials (-> out, and Q8_0 blocks of out
+// when a.q8 != nullptr and head_dim % 32 == 0).
+// fused != nullptr (fast path only): the kernel also does the q/k norm +
+// rope + q scale + KV append of qk_norm_rope_kv (one launch fewer).
+void launch_attention(const AttnArgs& a, bool exact, hipStream_t s, const QKVArgs* fused = nullptr);
 
 }  // namespace llmi

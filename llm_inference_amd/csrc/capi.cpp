@@ -347,7 +347,7 @@ int llmi_attention(const float* q, const uint16_t* k, const uint16_t* v, int n_h
       throw status_error(LLMI_E_ARG, "attention: invalid shape");
     Ctx& c = ctx();
     const size_t nq = (size_t)n_head * head_dim, nkv = (size_t)n_head_kv * n_keys * head_dim;
-    const int nsplit = 32;
+    const int nsplit = ATTN_NSPLIT;
     float* qd = (float*)c.get(0, nq * 4);
     float* od = (float*)c.get(1, nq * 4);
     uint16_t* kd = (uint16_t*)c.get(2, nkv * 2);
@@ -359,8 +359,10 @@ int llmi_attention(const float* q, const uint16_t* k, const uint16_t* v, int n_h
     LLMI_HIP(hipMemcpyAsync(kd, k, nkv * 2, hipMemcpyHostToDevice, c.stream));
     LLMI_HIP(hipMemcpyAsync(vd, v, nkv * 2, hipMemcpyHostToDevice, c.stream));
     LLMI_HIP(hipMemcpyAsync(posd, &pos, 4, hipMemcpyHostToDevice, c.stream));
-    AttnArgs a{qd, kd, vd, n_head, n_head_kv, head_dim, n_keys, posd, pd, od};
-    launch_attention(a, (flags & LLMI_EXACT) != 0, nsplit, nullptr, c.stream);
+    unsigned* td = (unsigned*)c.get(6, (size_t)n_head_kv * 4);
+    LLMI_HIP(hipMemsetAsync(td, 0, (size_t)n_head_kv * 4, c.stream));
+    AttnArgs a{qd, kd, vd, n_head, n_head_kv, head_dim, n_keys, posd, pd, od, td, nullptr};
+    launch_attention(a, (flags & LLMI_EXACT) != 0, c.stream);
     LLMI_HIP(hipMemcpyAsync(out, od, nq * 4, hipMemcpyDeviceToHost, c.stream));
     LLMI_HIP(hipStreamSynchronize(c.stream));
   });

@@ -135,45 +135,71 @@ __global__ __launch_bounds__(256) void attn_exact_kernel(AttnArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// fast split-K attention ("flash-decoding"): grid (n_head_kv, n_split).
-// Work-group c walks key tiles c, c+n_split, ... of 64 keys keeping an
-// online-softmax partial (m, l, acc[hd]) per query head in fp32;
-// attn_combine merges the n_split partials.
+// fast split-K attention ("flash-decoding"), ONE launch: grid (n_head_kv,
+// ATTN_NSPLIT).  Work-group c walks key tiles c, c+NSPLIT, ... of 64 keys
+// keeping an online-softmax partial (m, l, acc[hd]) per query head in fp32;
+// the last work-group of each kv head to finish (agent-scope ticket) merges
+// the NSPLIT partials, writes the heads' outputs and their Q8_0 blocks.
 // ---------------------------------------------------------------------------
 // q/k head row norm (model.cpp:762/792, fast sum) + NEOX rope at the table row
-// `cs` (ops.cpp:88-91 contraction) for a row held DPL elements per lane.
+// `cs` (ops.cpp:88-91 contraction) for a row held DPL elements per lane, in two
+// steps so the row's loads can be issued ahead of the K/V tile loads and the
+// arithmetic run while the tile is in flight.
 template <int HD>
-__device__ __forceinline__ void norm_rope_row(const float* __restrict__ src, const float* __restrict__ nw,
-                                              const float* __restrict__ cs, double eps, float (&out)[HD >= 64 ? HD / 64 : 1]) {
-  constexpr int DPL = HD >= 64 ? HD / 64 : 1;
+struct RowLd {
+  static constexpr int DPL = HD >= 64 ? HD / 64 : 1;
+  float v[DPL], nw[DPL], c[DPL], s[DPL];
+};
+
+template <int HD>
+__device__ __forceinline__ void row_load(RowLd<HD>& r, const float* __restrict__ src, const float* __restrict__ nw,
+                                         const float* __restrict__ cs) {
+  constexpr int DPL = RowLd<HD>::DPL;
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 0; d < DPL; d++) {
+    const int i = min(lane * DPL + d, HD - 1);  // clamped, unconditional loads (lanes >= HD are masked later)
+    const int j = i < HD / 2 ? i : i - HD / 2;
+    r.v[d] = src[i];
+    r.nw[d] = nw[i];
+    r.c[d] = cs[2 * j];
+    r.s[d] = cs[2 * j + 1];
+  }
+}
+
+template <int HD>
+__device__ __forceinline__ void row_finish(const RowLd<HD>& r, double eps, float (&out)[RowLd<HD>::DPL]) {
+  constexpr int DPL = RowLd<HD>::DPL;
   constexpr int PX = HD >= 64 ? 32 : HD / 2;  // lane holding element i +- HD/2
   const int lane = threadIdx.x & 63;
   const bool ok = lane * DPL < HD;
-  float v[DPL];
   float ss = 0.0f;
 #pragma unroll
-  for (int d = 0; d < DPL; d++) {
-    v[d] = ok ? src[lane * DPL + d] : 0.0f;
-    ss = fmaf(v[d], v[d], ss);
-  }
+  for (int d = 0; d < DPL; d++) ss = ok ? fmaf(r.v[d], r.v[d], ss) : ss;
   ss = wave_sum(ss);
   const float sc = 1.0f / sqrtf((float)((double)(ss / (float)HD) + eps));
 #pragma unroll
   for (int d = 0; d < DPL; d++) {
     const int i = lane * DPL + d;
-    const float n = ok ? (sc * v[d]) * nw[i] : 0.0f;
+    const float n = ok ? (sc * r.v[d]) * r.nw[d] : 0.0f;
     const float pn = __shfl_xor(n, PX);
-    const int j = i < HD / 2 ? i : i - HD / 2;
-    const float c = ok ? cs[2 * j] : 0.0f, s = ok ? cs[2 * j + 1] : 0.0f;
-    out[d] = i < HD / 2 ? fmaf(n, c, -(pn * s)) : fmaf(pn, s, n * c);
+    out[d] = i < HD / 2 ? fmaf(n, r.c[d], -(pn * r.s[d])) : fmaf(pn, r.s[d], n * r.c[d]);
   }
+}
+
+__device__ __forceinline__ void st_sc1(float* p, float v) {  // write-through store (cross-CU hand-off)
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // One work-group of 256 threads per (kv head, split) covering all G = n_head /
 // n_head_kv query heads of that kv head, so each K/V tile is read from HBM
 // once per split.  Per 64-key tile: every thread issues its 16-byte K and V
-// chunk loads together (the tile is one contiguous 2*64*HD*2-byte stream),
-// stores them to LDS, then
+// chunk loads together (the tile is one contiguous 2*64*HD*2-byte stream;
+// the first tile before the q/k prologue, each next tile right after the
+// current one is in LDS), then
 //   QK^T: TP threads per (query head, key) pair, interleaved 16-byte chunks,
 //         v_dot2 f16 products in fp32, K rows padded by TP*16 bytes so the
 //         ds_read_b128 of 16 lanes hit 16 distinct bank groups;
@@ -183,14 +209,20 @@ __device__ __forceinline__ void norm_rope_row(const float* __restrict__ src, con
 // norm, rope and q scale of qk_norm_rope_kv_kernel and the KV append of this
 // token; the split owning `pos` substitutes the new k/v rows from LDS for the
 // cache rows it is writing in the same launch.
+// Hand-off of the partials to the merging work-group (MI355X_MICROARCH
+// hand-off table, first row): sc1 stores, every storing wave's vmcnt(0),
+// a workgroup barrier, one agent-scope add per work-group; the work-group
+// whose add returns NSPLIT-1 reads every partial with sc1 loads.
 template <int HD, int G, bool FUSED>
-__global__ __launch_bounds__(256) void attn_partial_kernel(AttnArgs a, QKVArgs qa) {
+__global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa) {
+  constexpr int NS = ATTN_NSPLIT;
   constexpr int CH = HD / 8;                         // 16-byte chunks per row
   constexpr int TP0 = 4 / G;                         // threads per (head, key) pair
   constexpr int TP = TP0 < CH ? TP0 : CH;
   constexpr int KS = HD + 8 * TP;                    // padded K row stride (halves)
   constexpr int NLD = (64 * CH + 255) / 256;         // chunk loads per thread per tile
   constexpr int KP = 256 / HD;                       // key residue classes in PV
+  constexpr int DPL = RowLd<HD>::DPL;
   __shared__ __attribute__((aligned(16))) uint16_t s_k[64 * KS];
   __shared__ __attribute__((aligned(16))) uint16_t s_v[64 * HD];
   __shared__ __attribute__((aligned(16))) uint16_t s_q[G][HD];
@@ -198,67 +230,92 @@ __global__ __launch_bounds__(256) void attn_partial_kernel(AttnArgs a, QKVArgs q
   __shared__ float s_p[G][64];
   __shared__ float s_alpha[G];
   __shared__ float s_red[KP > 1 ? KP * G * HD : 1];
+  __shared__ float s_ml[G][NS][2];
+  __shared__ int s_last;
+  static_assert(64 * KS * 2 >= G * HD * 4, "s_k doubles as the merged-output staging");
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int hkv = blockIdx.x, c = blockIdx.y, nsplit = gridDim.y;
+  const int hkv = blockIdx.x, c = blockIdx.y;
   const int pos = *a.d_pos;
   const int n_keys = pos + 1;
-  const bool own_new = FUSED && (pos / 64) % nsplit == c;
+  const bool own_new = FUSED && (pos / 64) % NS == c;
+  const uint4* kb = reinterpret_cast<const uint4*>(a.k_cache + (size_t)hkv * a.max_ctx * HD);
+  const uint4* vb = reinterpret_cast<const uint4*>(a.v_cache + (size_t)hkv * a.max_ctx * HD);
+  uint4 kr[NLD], vr[NLD];
+  // unconditional loads of tile `tl` (rows clamped into the cache); keys past
+  // n_keys are zeroed (the cache beyond pos may hold stale or NaN bits)
+  auto load_tile = [&](int tl) {
+#pragma unroll
+    for (int i = 0; i < NLD; i++) {
+      const int k = min(i * 256 + t, 64 * CH - 1);
+      const int key = min(tl * 64 + k / CH, a.max_ctx - 1);
+      const size_t gi = (size_t)key * CH + k % CH;
+      kr[i] = kb[gi];
+      vr[i] = vb[gi];
+    }
+  };
+  auto mask_tile = [&](int tl) {
+#pragma unroll
+    for (int i = 0; i < NLD; i++) {
+      const bool ok = tl * 64 + (i * 256 + t) / CH < n_keys;
+      if (!ok) kr[i] = make_uint4(0, 0, 0, 0);
+      if (!ok) vr[i] = make_uint4(0, 0, 0, 0);
+    }
+  };
+
+  // ---- prologue loads, then the first tile, then the prologue arithmetic ----
+  const float* cs = FUSED ? qa.rope_cs + (size_t)pos * (HD / 2) * 2 : nullptr;
+  RowLd<HD> rq, rk;
+  float vrow[DPL];
   if (FUSED) {
-    const float* cs = qa.rope_cs + (size_t)pos * (HD / 2) * 2;
-    constexpr int DPL = HD >= 64 ? HD / 64 : 1;
+    if (w < G) row_load<HD>(rq, qa.qkv + (size_t)(hkv * G + w) * HD, qa.q_norm_w, cs);
+    if (w == (G & 3)) row_load<HD>(rk, qa.qkv + qa.k_off + (size_t)hkv * HD, qa.k_norm_w, cs);
+    if (w == ((G + 1) & 3)) {
+#pragma unroll
+      for (int d = 0; d < DPL; d++) vrow[d] = qa.qkv[qa.v_off + (size_t)hkv * HD + min(lane * DPL + d, HD - 1)];
+    }
+  }
+  int tile = c;
+  load_tile(tile);
+  if (FUSED) {
     const bool ok = lane * DPL < HD;
     if (w < G) {
       float qr[DPL];
-      norm_rope_row<HD>(qa.qkv + (size_t)(hkv * G + w) * HD, qa.q_norm_w, cs, qa.eps, qr);
+      row_finish<HD>(rq, qa.eps, qr);
 #pragma unroll
       for (int d = 0; d < DPL; d++)
         if (ok) s_q[w][lane * DPL + d] = f2h_ggml(qr[d] * qa.attn_scale);
     }
-    if (own_new && w == (G & 3)) {
-      float kr[DPL];
-      norm_rope_row<HD>(qa.qkv + qa.k_off + (size_t)hkv * HD, qa.k_norm_w, cs, qa.eps, kr);
+    if (w == (G & 3)) {
+      float kn[DPL];
+      row_finish<HD>(rk, qa.eps, kn);
 #pragma unroll
       for (int d = 0; d < DPL; d++) {
-        const uint16_t k16 = f2h_ggml(kr[d]);
-        if (ok) {
-          s_new[0][lane * DPL + d] = k16;
-          qa.k_cache[((size_t)hkv * a.max_ctx + pos) * HD + lane * DPL + d] = k16;
-        }
+        const uint16_t k16 = f2h_ggml(kn[d]);
+        if (ok) s_new[0][lane * DPL + d] = k16;
+        if (ok && own_new) qa.k_cache[((size_t)hkv * a.max_ctx + pos) * HD + lane * DPL + d] = k16;
       }
     }
-    if (own_new && w == ((G + 1) & 3)) {
-      for (int i = lane; i < HD; i += 64) {
-        const uint16_t v16 = f2h_ggml(qa.qkv[qa.v_off + (size_t)hkv * HD + i]);
-        s_new[FUSED ? 1 : 0][i] = v16;
-        qa.v_cache[((size_t)hkv * a.max_ctx + pos) * HD + i] = v16;
+    if (w == ((G + 1) & 3)) {
+#pragma unroll
+      for (int d = 0; d < DPL; d++) {
+        const uint16_t v16 = f2h_ggml(vrow[d]);
+        if (ok) s_new[FUSED ? 1 : 0][lane * DPL + d] = v16;
+        if (ok && own_new) qa.v_cache[((size_t)hkv * a.max_ctx + pos) * HD + lane * DPL + d] = v16;
       }
     }
   } else {
     for (int i = t; i < G * HD; i += 256) s_q[i / HD][i % HD] = f2h_ggml(a.q[(size_t)hkv * G * HD + i]);
   }
-  const uint4* kb = reinterpret_cast<const uint4*>(a.k_cache + (size_t)hkv * a.max_ctx * HD);
-  const uint4* vb = reinterpret_cast<const uint4*>(a.v_cache + (size_t)hkv * a.max_ctx * HD);
+
   float m_run = -INFINITY, l_run = 0.0f;  // head w's running max / sum (waves w < G)
   float acc[G];
 #pragma unroll
   for (int g = 0; g < G; g++) acc[g] = 0.0f;
   const int d_own = t % HD, kp = t / HD;
   typedef _Float16 h2t __attribute__((ext_vector_type(2)));
-  for (int tile = c; tile * 64 < n_keys; tile += nsplit) {
-    uint4 kr[NLD], vr[NLD];
-#pragma unroll
-    for (int i = 0; i < NLD; i++) {
-      const int k = i * 256 + t;
-      const int key = tile * 64 + k / CH;
-      kr[i] = make_uint4(0, 0, 0, 0);
-      vr[i] = make_uint4(0, 0, 0, 0);
-      if (k < 64 * CH && key < n_keys) {
-        const size_t gi = (size_t)tile * 64 * CH + k;
-        kr[i] = kb[gi];
-        vr[i] = vb[gi];
-      }
-    }
-    __syncthreads();  // previous tile's LDS reads done (and, first time, s_q / s_new written)
+  for (; tile * 64 < n_keys; tile += NS) {
+    mask_tile(tile);
+    __syncthreads();  // previous tile's LDS reads done (first time: s_q / s_new written)
 #pragma unroll
     for (int i = 0; i < NLD; i++) {
       const int k = i * 256 + t;
@@ -274,6 +331,7 @@ __global__ __launch_bounds__(256) void attn_partial_kernel(AttnArgs a, QKVArgs q
       *reinterpret_cast<uint4*>(&s_v[j * HD + t * 8]) = reinterpret_cast<const uint4*>(s_new[FUSED ? 1 : 0])[t];
     }
     __syncthreads();
+    if ((tile + NS) * 64 < n_keys) load_tile(tile + NS);  // next tile in flight during this one's math
     if (t < G * 64 * TP) {
       const int pr = t / TP, part = t % TP;
       const int g = pr / 64, j = pr % 64;
@@ -327,92 +385,94 @@ __global__ __launch_bounds__(256) void attn_partial_kernel(AttnArgs a, QKVArgs q
       }
     }
   }
+
+  // ---- publish the partial, take a ticket --------------------------------
+  float* part0 = a.partial + (size_t)hkv * G * NS * (HD + 2);  // [G][NS][HD + 2]
   if (kp == 0) {
 #pragma unroll
-    for (int g = 0; g < G; g++) a.partial[((size_t)(hkv * G + g) * nsplit + c) * (HD + 2) + d_own] = acc[g];
+    for (int g = 0; g < G; g++) st_sc1(part0 + ((size_t)g * NS + c) * (HD + 2) + d_own, acc[g]);
   }
   if (w < G && lane == 0) {
-    float* part = a.partial + ((size_t)(hkv * G + w) * nsplit + c) * (HD + 2);
-    part[HD] = m_run;
-    part[HD + 1] = l_run;
+    st_sc1(part0 + ((size_t)w * NS + c) * (HD + 2) + HD, m_run);
+    st_sc1(part0 + ((size_t)w * NS + c) * (HD + 2) + HD + 1, l_run);
   }
-}
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0)
+    s_last = __hip_atomic_fetch_add(a.ticket + hkv, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == NS - 1;
+  __syncthreads();
+  if (!s_last) return;
 
-// merge split partials per head; optionally quantize the head's output to
-// Q8_0 blocks for the O projection (head_dim % 32 == 0).
-// NSPLIT is a compile-time constant so every partial's (m, l, acc[t]) load is
-// issued in one batch (one memory round trip instead of NSPLIT).
-template <int NSPLIT>
-__global__ __launch_bounds__(256) void attn_combine_kernel(AttnArgs a, Q8Act q8) {
-  const int h = blockIdx.x, t = threadIdx.x, hd = a.head_dim;
-  const float* part = a.partial + (size_t)h * NSPLIT * (hd + 2);
-  float m[NSPLIT], l[NSPLIT], v[NSPLIT];
-#pragma unroll
-  for (int c = 0; c < NSPLIT; c++) {
-    const float* pc = part + (size_t)c * (hd + 2);
-    m[c] = pc[hd];
-    l[c] = pc[hd + 1];
-    v[c] = t < hd ? pc[t] : 0.0f;
+  // ---- last work-group: merge the NS partials of the G heads -------------
+  for (int i = t; i < G * NS * 2; i += 256) {
+    const int g = i / (NS * 2), cc = (i / 2) % NS, e = i & 1;
+    s_ml[g][cc][e] = ld_sc1(part0 + ((size_t)g * NS + cc) * (HD + 2) + HD + e);
   }
-  float M = -INFINITY;
+  __syncthreads();
+  float* s_out = reinterpret_cast<float*>(s_k);  // [G][HD]
+  for (int idx = t; idx < G * HD; idx += 256) {
+    const int g = idx / HD, d = idx % HD;
+    const float* pg = part0 + (size_t)g * NS * (HD + 2) + d;
+    float v[NS];
 #pragma unroll
-  for (int c = 0; c < NSPLIT; c++) M = fmaxf(M, m[c]);
-  float L = 0.0f, o = 0.0f;
+    for (int cc = 0; cc < NS; cc++) v[cc] = ld_sc1(pg + (size_t)cc * (HD + 2));
+    float M = -INFINITY;
 #pragma unroll
-  for (int c = 0; c < NSPLIT; c++) {
-    const float wc = l[c] == 0.0f ? 0.0f : expf(m[c] - M);
-    L = fmaf(l[c], wc, L);
-    o = fmaf(v[c], wc, o);
+    for (int cc = 0; cc < NS; cc++) M = fmaxf(M, s_ml[g][cc][0]);
+    float L = 0.0f, o = 0.0f;
+#pragma unroll
+    for (int cc = 0; cc < NS; cc++) {
+      const float l = s_ml[g][cc][1];
+      const float wc = l == 0.0f ? 0.0f : expf(s_ml[g][cc][0] - M);
+      L = fmaf(l, wc, L);
+      o = fmaf(v[cc], wc, o);
+    }
+    const float val = o / L;
+    a.out[((size_t)hkv * G + g) * HD + d] = val;
+    s_out[idx] = val;
   }
-  const float val = t < hd ? o / L : 0.0f;
-  if (t < hd) a.out[(size_t)h * hd + t] = val;
-  if (q8.xb != nullptr && t < hd) q8_block_store(val, true, q8.xb + ((h * hd + t) >> 5), t & 31);  // ops.cpp:116-139
+  if (a.q8 != nullptr && HD % 32 == 0) {  // Q8_0 blocks of the heads' outputs (ops.cpp:116-139)
+    __syncthreads();
+    for (int b = t; b < G * HD / 32; b += 256) q8_block_serial(s_out + 32 * b, a.q8 + (size_t)hkv * G * HD / 32 + b);
+  }
+  if (t == 0) __hip_atomic_store(a.ticket + hkv, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
 }
 
 template <int HD, int G>
-static void launch_partial_g(const AttnArgs& a, const QKVArgs* fused, int nsplit, hipStream_t s) {
-  const dim3 grid(a.n_head_kv, nsplit);
+static void launch_split_g(const AttnArgs& a, const QKVArgs* fused, hipStream_t s) {
+  const dim3 grid(a.n_head_kv, ATTN_NSPLIT);
   if (fused)
-    hipLaunchKernelGGL((attn_partial_kernel<HD, G, true>), grid, dim3(256), 0, s, a, *fused);
+    hipLaunchKernelGGL((attn_split_kernel<HD, G, true>), grid, dim3(256), 0, s, a, *fused);
   else
-    hipLaunchKernelGGL((attn_partial_kernel<HD, G, false>), grid, dim3(256), 0, s, a, QKVArgs{});
+    hipLaunchKernelGGL((attn_split_kernel<HD, G, false>), grid, dim3(256), 0, s, a, QKVArgs{});
 }
 
 template <int HD>
-static void launch_partial(const AttnArgs& a, const QKVArgs* fused, int nsplit, hipStream_t s) {
+static void launch_split(const AttnArgs& a, const QKVArgs* fused, hipStream_t s) {
   switch (a.n_head / a.n_head_kv) {
-    case 1: launch_partial_g<HD, 1>(a, fused, nsplit, s); break;
-    case 2: launch_partial_g<HD, 2>(a, fused, nsplit, s); break;
-    case 4: launch_partial_g<HD, 4>(a, fused, nsplit, s); break;
+    case 1: launch_split_g<HD, 1>(a, fused, s); break;
+    case 2: launch_split_g<HD, 2>(a, fused, s); break;
+    case 4: launch_split_g<HD, 4>(a, fused, s); break;
     default: throw std::runtime_error("attention: GQA group must be 1, 2 or 4");
   }
 }
 
-void launch_attention(const AttnArgs& a, bool exact, int nsplit, const Q8Act* q8, hipStream_t s,
-                      const QKVArgs* fused) {
+void launch_attention(const AttnArgs& a, bool exact, hipStream_t s, const QKVArgs* fused) {
   if (exact) {
     hipLaunchKernelGGL(attn_exact_kernel, dim3(a.n_head), dim3(256), 0, s, a);
     LLMI_HIP(hipGetLastError());
     return;
   }
-  if (nsplit != 16 && nsplit != 32 && nsplit != 64) throw std::runtime_error("attention: nsplit must be 16, 32 or 64");
   if (a.n_head_kv <= 0 || a.n_head % a.n_head_kv != 0) throw std::runtime_error("attention: n_head % n_head_kv != 0");
+  if (!a.partial || !a.ticket || !a.out) throw std::runtime_error("attention: missing partial / ticket / out buffer");
   switch (a.head_dim) {
-    case 16: launch_partial<16>(a, fused, nsplit, s); break;
-    case 32: launch_partial<32>(a, fused, nsplit, s); break;
-    case 64: launch_partial<64>(a, fused, nsplit, s); break;
-    case 128: launch_partial<128>(a, fused, nsplit, s); break;
-    case 256: launch_partial<256>(a, fused, nsplit, s); break;
+    case 16: launch_split<16>(a, fused, s); break;
+    case 32: launch_split<32>(a, fused, s); break;
+    case 64: launch_split<64>(a, fused, s); break;
+    case 128: launch_split<128>(a, fused, s); break;
+    case 256: launch_split<256>(a, fused, s); break;
     default: throw std::runtime_error("attention: unsupported head_dim " + std::to_string(a.head_dim));
   }
-  LLMI_HIP(hipGetLastError());
-  const Q8Act qq = q8 ? *q8 : Q8Act{};
-  if (nsplit == 16)
-    hipLaunchKernelGGL(attn_combine_kernel<16>, dim3(a.n_head), dim3(256), 0, s, a, qq);
-  else if (nsplit == 32)
-    hipLaunchKernelGGL(attn_combine_kernel<32>, dim3(a.n_head), dim3(256), 0, s, a, qq);
-  else
-    hipLaunchKernelGGL(attn_combine_kernel<64>, dim3(a.n_head), dim3(256), 0, s, a, qq);
   LLMI_HIP(hipGetLastError());
 }
 

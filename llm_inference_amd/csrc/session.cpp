@@ -221,7 +221,8 @@ void Session::alloc_buffers() {
   qkv_ = dalloc<float>(maxqkv);
   q_ = dalloc<float>(maxq);
   attn_ = dalloc<float>(maxq);
-  part_ = dalloc<float>((size_t)hp_.n_head * nsplit_ * (maxhd + 2));
+  part_ = dalloc<float>((size_t)hp_.n_head * ATTN_NSPLIT * (maxhd + 2));
+  ticket_ = dalloc<unsigned>(hp_.n_head_kv);  // zeroed; the attention kernel resets it after use
   o_out_ = dalloc<float>(E);
   gu_ = dalloc<float>(2 * (size_t)F);
   hid_ = dalloc<float>(F);
@@ -276,8 +277,8 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
   if (const char* d = getenv("LLMI_DUP")) dup_ = d;  // diagnostics: launch these kernels twice
   use_graph_ = (opts.flags & LLMI_NO_GRAPH) == 0;
   max_ctx_ = opts.max_ctx > 0 ? opts.max_ctx : 4096;
-  nsplit_ = opts.attn_split > 0 ? opts.attn_split : 32;
-  if (nsplit_ != 16 && nsplit_ != 32 && nsplit_ != 64) throw status_error(LLMI_E_ARG, "attn_split must be 16, 32 or 64");
+  if (opts.attn_split != 0 && opts.attn_split != ATTN_NSPLIT)
+    throw status_error(LLMI_E_ARG, "attn_split must be 0 or " + std::to_string(ATTN_NSPLIT));
   LLMI_HIP(hipSetDevice(opts.device));
   LLMI_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   try {
@@ -424,11 +425,11 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
     kernels_per_token_++;
     QKVArgs qa{qkv_, Ld.k_off, Ld.v_off, hp_.n_head, hp_.n_head_kv, hd, Ld.q_norm, Ld.k_norm,
                Ld.is_swa ? rope_swa_ : rope_glb_, hp_.attn_scale, hp_.eps, q_, Ld.kc, Ld.vc, max_ctx_, d_pos_};
-    AttnArgs aa{q_, Ld.kc, Ld.vc, hp_.n_head, hp_.n_head_kv, hd, max_ctx_, d_pos_, part_, attn_};
     const bool q8_in_combine = hd % 32 == 0;
-    for (int r = 0; r < dup("attn"); r++)
-      launch_attention(aa, false, nsplit_, q8_in_combine ? &act_.q8 : nullptr, s, &qa);
-    kernels_per_token_ += 2;
+    AttnArgs aa{q_, Ld.kc, Ld.vc, hp_.n_head, hp_.n_head_kv, hd, max_ctx_, d_pos_, part_, attn_,
+                ticket_, q8_in_combine ? act_.q8.xb : nullptr};
+    for (int r = 0; r < dup("attn"); r++) launch_attention(aa, false, s, &qa);
+    kernels_per_token_++;
     if (!q8_in_combine) {
       launch_quantize_q8_0(attn_, hp_.n_head * hd, act_.q8, s);
       kernels_per_token_++;
@@ -484,12 +485,12 @@ void Session::record_layers(hipStream_t s, bool x_q8) {
       launch_qk_norm_rope_kv(qa, ex_norm_, s);
       kernels_per_token_++;
     }
-    AttnArgs aa{q_, Ld.kc, Ld.vc, hp_.n_head, hp_.n_head_kv, hd, max_ctx_, d_pos_, part_, attn_};
     const bool o_q8 = is_q8(Ld.o.w.type);
     const bool fused_q8 = !ex_attn_ && o_q8 && hd % 32 == 0;
-    for (int r = 0; r < dup("attn"); r++)
-      launch_attention(aa, ex_attn_, nsplit_, fused_q8 ? &act_.q8 : nullptr, s, fuse_qk ? &qa : nullptr);
-    kernels_per_token_ += ex_attn_ ? 1 : 2;
+    AttnArgs aa{q_, Ld.kc, Ld.vc, hp_.n_head, hp_.n_head_kv, hd, max_ctx_, d_pos_, part_, attn_,
+                ticket_, fused_q8 ? act_.q8.xb : nullptr};
+    for (int r = 0; r < dup("attn"); r++) launch_attention(aa, ex_attn_, s, fuse_qk ? &qa : nullptr);
+    kernels_per_token_++;
     for (int r = 0; r < dup("o_proj"); r++) gemv_parts({Ld.o}, attn_, hp_.n_head * hd, o_out_, s, fused_q8);
     NormOut o1 = nout(Ld.gate_up);
     launch_residual_norm(o_out_, Ld.post_attn_norm, resid_, Ld.ffn_norm, o1, E, hp_.eps, ex_norm_, s);

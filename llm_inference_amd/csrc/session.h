@@ -87,7 +87,6 @@ class Session {
   bool exact_ = false, use_graph_ = true;
   bool fuse_layers_ = false;  // fast path: norms / GELU folded into the Q4_0 GEMVs
   bool ex_gemv_ = false, ex_norm_ = false, ex_attn_ = false, ex_logits_ = false;  // per kernel family
-  int nsplit_ = 32;
   HParams hp_;
   int vocab_ = 0, max_ctx_ = 4096;
   hipStream_t stream_ = nullptr;
@@ -100,6 +99,7 @@ class Session {
   float *rope_swa_ = nullptr, *rope_glb_ = nullptr;
   // activations
   float *resid2_ = nullptr, *resid_scratch_ = nullptr;
+  unsigned* ticket_ = nullptr;
   float *resid_ = nullptr, *xn_ = nullptr, *qkv_ = nullptr, *q_ = nullptr, *attn_ = nullptr, *part_ = nullptr;
   float *o_out_ = nullptr, *gu_ = nullptr, *hid_ = nullptr, *d_out_ = nullptr, *logits_ = nullptr;
   ActBuf act_{};
