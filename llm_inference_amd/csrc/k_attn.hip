@@ -403,10 +403,12 @@ __global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa)
   __syncthreads();
   if (!s_last) return;
 
-  // ---- last work-group: merge the NS partials of the G heads -------------
+  // ---- last work-group: merge the partials of the G heads ----------------
+  // splits c >= nvalid own no key (l = 0, weight 0): not read
+  const int nvalid = min(NS, (n_keys + 63) / 64);
   for (int i = t; i < G * NS * 2; i += 256) {
     const int g = i / (NS * 2), cc = (i / 2) % NS, e = i & 1;
-    s_ml[g][cc][e] = ld_sc1(part0 + ((size_t)g * NS + cc) * (HD + 2) + HD + e);
+    s_ml[g][cc][e] = cc < nvalid ? ld_sc1(part0 + ((size_t)g * NS + cc) * (HD + 2) + HD + e) : 0.0f;
   }
   __syncthreads();
   float* s_out = reinterpret_cast<float*>(s_k);  // [G][HD]
@@ -415,10 +417,10 @@ __global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa)
     const float* pg = part0 + (size_t)g * NS * (HD + 2) + d;
     float v[NS];
 #pragma unroll
-    for (int cc = 0; cc < NS; cc++) v[cc] = ld_sc1(pg + (size_t)cc * (HD + 2));
+    for (int cc = 0; cc < NS; cc++) v[cc] = cc < nvalid ? ld_sc1(pg + (size_t)cc * (HD + 2)) : 0.0f;
     float M = -INFINITY;
 #pragma unroll
-    for (int cc = 0; cc < NS; cc++) M = fmaxf(M, s_ml[g][cc][0]);
+    for (int cc = 0; cc < NS; cc++) M = cc < nvalid ? fmaxf(M, s_ml[g][cc][0]) : M;
     float L = 0.0f, o = 0.0f;
 #pragma unroll
     for (int cc = 0; cc < NS; cc++) {
