@@ -214,7 +214,9 @@ __device__ __forceinline__ void attn_merge(const AttnArgs& a, int hkv, int n_key
     const float* pg = part0 + (size_t)g * NS * (HD + 2) + d;
     float v[NS];
 #pragma unroll
-    for (int cc = 0; cc < NS; cc++) v[cc] = cc < nvalid ? ld_sc1(pg + (size_t)cc * (HD + 2)) : 0.0f;
+    for (int cc = 0; cc < NS; cc++) v[cc] = ld_sc1(pg + (size_t)min(cc, nvalid - 1) * (HD + 2));  // one batch
+#pragma unroll
+    for (int cc = 0; cc < NS; cc++) v[cc] = cc < nvalid ? v[cc] : 0.0f;
     float M = -INFINITY;
 #pragma unroll
     for (int cc = 0; cc < NS; cc++) M = cc < nvalid ? fmaxf(M, s_ml[g][cc][0]) : M;
