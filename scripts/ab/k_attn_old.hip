@@ -1,0 +1,479 @@
+// k_attn.hip -- per-head q/k norm + rope + KV append, and decode attention.
+//
+// KV cache layout (per layer): [n_head_kv][max_ctx][head_dim] f16, so one
+// head's history is one contiguous stream.  The current position lives in
+// device memory (d_pos) so a whole decode step can be replayed as one
+// hipGraph without re-capturing.
+#include "attn.h"
+
+namespace llmi {
+
+// ---------------------------------------------------------------------------
+// q/k per-head rms_norm * weight (model.cpp:762,792), NEOX rope at pos
+// (model.cpp:764,794), q *= 1/sqrt(head_dim) (model.cpp:767), K and V rows
+// rounded to f16 into the cache (model.cpp:442-474).
+// grid = n_head + n_head_kv blocks of 256 threads; head_dim <= 256.
+// ---------------------------------------------------------------------------
+template <bool EXACT>
+__global__ __launch_bounds__(256) void qk_norm_rope_kv_kernel(QKVArgs a) {
+  __shared__ float s_x[256];
+  __shared__ float s_part[4];
+  __shared__ float s_scale;
+  const int t = threadIdx.x;
+  const int hd = a.head_dim;
+  const int pos = *a.d_pos;
+  const bool is_q = blockIdx.x < (unsigned)a.n_head;
+  const int h = is_q ? blockIdx.x : blockIdx.x - a.n_head;
+  const float* src = a.qkv + (is_q ? (size_t)h * hd : (size_t)a.k_off + (size_t)h * hd);
+  const float* nw = is_q ? a.q_norm_w : a.k_norm_w;
+  const float v = t < hd ? src[t] : 0.0f;
+  if (t < hd) s_x[t] = v;
+  __syncthreads();
+  if (EXACT) {
+    if (t == 0) {
+      float sum = 0.0f;
+      for (int i = 0; i < hd; i++) sum = fmaf(s_x[i], s_x[i], sum);
+      s_scale = 1.0f / sqrtf((float)((double)(sum / (float)hd) + a.eps));
+    }
+  } else {
+    float sum = wave_sum(v * v);
+    if ((t & 63) == 0) s_part[t >> 6] = sum;
+    __syncthreads();
+    if (t == 0) {
+      const float tot = (s_part[0] + s_part[1]) + (s_part[2] + s_part[3]);
+      s_scale = 1.0f / sqrtf((float)((double)(tot / (float)hd) + a.eps));
+    }
+  }
+  __syncthreads();
+  const float nv = t < hd ? (s_scale * v) * nw[t] : 0.0f;
+  __syncthreads();
+  if (t < hd) s_x[t] = nv;
+  __syncthreads();
+  const int half = hd / 2;
+  const float* cs = a.rope_cs + (size_t)pos * half * 2;
+  float r = nv;
+  if (t < half) {
+    const float c = cs[2 * t], sn = cs[2 * t + 1];
+    r = fmaf(s_x[t], c, -(s_x[t + half] * sn));
+  } else if (t < hd) {
+    const float c = cs[2 * (t - half)], sn = cs[2 * (t - half) + 1];
+    r = fmaf(s_x[t - half], sn, s_x[t] * c);
+  }
+  if (t < hd) {
+    if (is_q) {
+      a.q_out[(size_t)h * hd + t] = r * a.attn_scale;
+    } else {
+      const size_t ci = ((size_t)h * a.max_ctx + pos) * hd + t;
+      a.k_cache[ci] = f2h_ggml(r);
+      a.v_cache[ci] = f2h_ggml(a.qkv[(size_t)a.v_off + (size_t)h * hd + t]);
+    }
+  }
+}
+
+void launch_qk_norm_rope_kv(const QKVArgs& a, bool exact, hipStream_t s) {
+  const dim3 grid(a.n_head + a.n_head_kv);
+  if (exact)
+    hipLaunchKernelGGL(qk_norm_rope_kv_kernel<true>, grid, dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(qk_norm_rope_kv_kernel<false>, grid, dim3(256), 0, s, a);
+  LLMI_HIP(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------
+// exact attention (model.cpp:481-547): one block per query head, keys in
+// order; score = sequential double sum of exact f32 products f16(k)*f16(q);
+// online max with double/float compares as in the reference; f16 V
+// accumulator rounded every step (vec_scale_f16 / vec_mad_f16).
+// expf is the device libm's (documented ulp-level difference from glibc).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void attn_exact_kernel(AttnArgs a) {
+  __shared__ float s_prod[256];
+  __shared__ float s_e, s_pe;
+  __shared__ int s_resc;
+  const int t = threadIdx.x, hd = a.head_dim;
+  const int h = blockIdx.x;
+  const int hkv = h / (a.n_head / a.n_head_kv);
+  const int n_keys = *a.d_pos + 1;
+  const float q16 = t < hd ? h2f(f2h_ggml(a.q[(size_t)h * hd + t])) : 0.0f;
+  uint16_t vacc = f2h_ggml(0.0f);
+  float s_acc = 0.0f, max_score = -INFINITY;
+  const uint16_t* kb = a.k_cache + (size_t)hkv * a.max_ctx * hd;
+  const uint16_t* vb = a.v_cache + (size_t)hkv * a.max_ctx * hd;
+  for (int tk = 0; tk < n_keys; tk++) {
+    if (t < hd) s_prod[t] = h2f(kb[(size_t)tk * hd + t]) * q16;
+    __syncthreads();
+    if (t == 0) {
+      double score = 0.0;
+      for (int i = 0; i < hd; i++) score += (double)s_prod[i];
+      const float prev = max_score;
+      float e, pe;
+      int resc;
+      if (score > (double)prev) {
+        max_score = (float)score;
+        e = 1.0f;
+        pe = expf(prev - max_score);
+        resc = 1;
+      } else {
+        e = expf((float)(score - (double)max_score));
+        pe = 1.0f;
+        resc = 0;
+      }
+      s_acc = s_acc * pe + e;
+      s_e = e; s_pe = pe; s_resc = resc;
+    }
+    __syncthreads();
+    if (t < hd) {
+      if (s_resc) vacc = f2h_ggml(h2f(vacc) * s_pe);
+      vacc = f2h_ggml(fmaf(h2f(vb[(size_t)tk * hd + t]), s_e, h2f(vacc)));
+    }
+    __syncthreads();
+  }
+  __shared__ float s_inv;
+  if (t == 0) s_inv = s_acc == 0.0f ? 0.0f : 1.0f / s_acc;
+  __syncthreads();
+  if (t < hd) a.out[(size_t)h * hd + t] = h2f(vacc) * s_inv;
+}
+
+// ---------------------------------------------------------------------------
+// fast split-K attention ("flash-decoding"), ONE launch: grid (n_head_kv,
+// ATTN_NSPLIT).  Work-group c walks key tiles c, c+NSPLIT, ... of 64 keys
+// keeping an online-softmax partial (m, l, acc[hd]) per query head in fp32;
+// the last work-group of each kv head to finish (agent-scope ticket) merges
+// the NSPLIT partials, writes the heads' outputs and their Q8_0 blocks.
+// ---------------------------------------------------------------------------
+// q/k head row norm (model.cpp:762/792, fast sum) + NEOX rope at the table row
+// `cs` (ops.cpp:88-91 contraction) for a row held DPL elements per lane, in two
+// steps so the row's loads can be issued ahead of the K/V tile loads and the
+// arithmetic run while the tile is in flight.
+template <int HD>
+struct RowLd {
+  static constexpr int DPL = HD >= 64 ? HD / 64 : 1;
+  float v[DPL], nw[DPL], c[DPL], s[DPL];
+};
+
+template <int HD>
+__device__ __forceinline__ void row_load(RowLd<HD>& r, const float* __restrict__ src, const float* __restrict__ nw,
+                                         const float* __restrict__ cs) {
+  constexpr int DPL = RowLd<HD>::DPL;
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 0; d < DPL; d++) {
+    const int i = min(lane * DPL + d, HD - 1);  // clamped, unconditional loads (lanes >= HD are masked later)
+    const int j = i < HD / 2 ? i : i - HD / 2;
+    r.v[d] = src[i];
+    r.nw[d] = nw[i];
+    r.c[d] = cs[2 * j];
+    r.s[d] = cs[2 * j + 1];
+  }
+}
+
+template <int HD>
+__device__ __forceinline__ void row_finish(const RowLd<HD>& r, double eps, float (&out)[RowLd<HD>::DPL]) {
+  constexpr int DPL = RowLd<HD>::DPL;
+  constexpr int PX = HD >= 64 ? 32 : HD / 2;  // lane holding element i +- HD/2
+  const int lane = threadIdx.x & 63;
+  const bool ok = lane * DPL < HD;
+  float ss = 0.0f;
+#pragma unroll
+  for (int d = 0; d < DPL; d++) ss = ok ? fmaf(r.v[d], r.v[d], ss) : ss;
+  ss = wave_sum(ss);
+  const float sc = 1.0f / sqrtf((float)((double)(ss / (float)HD) + eps));
+#pragma unroll
+  for (int d = 0; d < DPL; d++) {
+    const int i = lane * DPL + d;
+    const float n = ok ? (sc * r.v[d]) * r.nw[d] : 0.0f;
+    const float pn = __shfl_xor(n, PX);
+    out[d] = i < HD / 2 ? fmaf(n, r.c[d], -(pn * r.s[d])) : fmaf(pn, r.s[d], n * r.c[d]);
+  }
+}
+
+__device__ __forceinline__ void st_sc1(float* p, float v) {  // write-through store (cross-CU hand-off)
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One work-group of 256 threads per (kv head, split) covering all G = n_head /
+// n_head_kv query heads of that kv head, so each K/V tile is read from HBM
+// once per split.  Per 64-key tile: every thread issues its 16-byte K and V
+// chunk loads together (the tile is one contiguous 2*64*HD*2-byte stream;
+// the first tile before the q/k prologue, each next tile right after the
+// current one is in LDS), then
+//   QK^T: TP threads per (query head, key) pair, interleaved 16-byte chunks,
+//         v_dot2 f16 products in fp32, K rows padded by TP*16 bytes so the
+//         ds_read_b128 of 16 lanes hit 16 distinct bank groups;
+//   softmax: wave g keeps head g's running (m, l);
+//   PV: thread owns one head dim (for all G heads) over a key residue class.
+// FUSED (session fast path): the work-group also performs the q/k per-head
+// norm, rope and q scale of qk_norm_rope_kv_kernel and the KV append of this
+// token; the split owning `pos` substitutes the new k/v rows from LDS for the
+// cache rows it is writing in the same launch.
+// Hand-off of the partials to the merging work-group (MI355X_MICROARCH
+// hand-off table, first row): sc1 stores, every storing wave's vmcnt(0),
+// a workgroup barrier, one agent-scope add per work-group; the work-group
+// whose add returns NSPLIT-1 reads every partial with sc1 loads.
+template <int HD, int G, bool FUSED>
+__global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa) {
+  constexpr int NS = ATTN_NSPLIT;
+  constexpr int CH = HD / 8;                         // 16-byte chunks per row
+  constexpr int TP0 = 4 / G;                         // threads per (head, key) pair
+  constexpr int TP = TP0 < CH ? TP0 : CH;
+  constexpr int KS = HD + 8 * TP;                    // padded K row stride (halves)
+  constexpr int NLD = (64 * CH + 255) / 256;         // chunk loads per thread per tile
+  constexpr int KP = 256 / HD;                       // key residue classes in PV
+  constexpr int DPL = RowLd<HD>::DPL;
+  __shared__ __attribute__((aligned(16))) uint16_t s_k[64 * KS];
+  __shared__ __attribute__((aligned(16))) uint16_t s_v[64 * HD];
+  __shared__ __attribute__((aligned(16))) uint16_t s_q[G][HD];
+  __shared__ __attribute__((aligned(16))) uint16_t s_new[FUSED ? 2 : 1][FUSED ? HD : 8];
+  __shared__ float s_p[G][64];
+  __shared__ float s_alpha[G];
+  __shared__ float s_red[KP > 1 ? KP * G * HD : 1];
+  __shared__ float s_ml[G][NS][2];
+  __shared__ int s_last;
+  static_assert(64 * KS * 2 >= G * HD * 4, "s_k doubles as the merged-output staging");
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int hkv = blockIdx.x, c = blockIdx.y;
+  const int pos = *a.d_pos;
+  const int n_keys = pos + 1;
+  const bool own_new = FUSED && (pos / 64) % NS == c;
+  const uint4* kb = reinterpret_cast<const uint4*>(a.k_cache + (size_t)hkv * a.max_ctx * HD);
+  const uint4* vb = reinterpret_cast<const uint4*>(a.v_cache + (size_t)hkv * a.max_ctx * HD);
+  uint4 kr[NLD], vr[NLD];
+  // unconditional loads of tile `tl` (rows clamped into the cache); keys past
+  // n_keys are zeroed (the cache beyond pos may hold stale or NaN bits)
+  auto load_tile = [&](int tl) {
+#pragma unroll
+    for (int i = 0; i < NLD; i++) {
+      const int k = min(i * 256 + t, 64 * CH - 1);
+      const int key = min(tl * 64 + k / CH, a.max_ctx - 1);
+      const size_t gi = (size_t)key * CH + k % CH;
+      kr[i] = kb[gi];
+      vr[i] = vb[gi];
+    }
+  };
+  auto mask_tile = [&](int tl) {
+#pragma unroll
+    for (int i = 0; i < NLD; i++) {
+      const bool ok = tl * 64 + (i * 256 + t) / CH < n_keys;
+      if (!ok) kr[i] = make_uint4(0, 0, 0, 0);
+      if (!ok) vr[i] = make_uint4(0, 0, 0, 0);
+    }
+  };
+
+  // ---- prologue loads, then the first tile, then the prologue arithmetic ----
+  const float* cs = FUSED ? qa.rope_cs + (size_t)pos * (HD / 2) * 2 : nullptr;
+  RowLd<HD> rq, rk;
+  float vrow[DPL];
+  if (FUSED) {
+    if (w < G) row_load<HD>(rq, qa.qkv + (size_t)(hkv * G + w) * HD, qa.q_norm_w, cs);
+    if (w == (G & 3)) row_load<HD>(rk, qa.qkv + qa.k_off + (size_t)hkv * HD, qa.k_norm_w, cs);
+    if (w == ((G + 1) & 3)) {
+#pragma unroll
+      for (int d = 0; d < DPL; d++) vrow[d] = qa.qkv[qa.v_off + (size_t)hkv * HD + min(lane * DPL + d, HD - 1)];
+    }
+  }
+  int tile = c;
+  load_tile(tile);
+  if (FUSED) {
+    const bool ok = lane * DPL < HD;
+    if (w < G) {
+      float qr[DPL];
+      row_finish<HD>(rq, qa.eps, qr);
+#pragma unroll
+      for (int d = 0; d < DPL; d++)
+        if (ok) s_q[w][lane * DPL + d] = f2h_ggml(qr[d] * qa.attn_scale);
+    }
+    if (w == (G & 3)) {
+      float kn[DPL];
+      row_finish<HD>(rk, qa.eps, kn);
+#pragma unroll
+      for (int d = 0; d < DPL; d++) {
+        const uint16_t k16 = f2h_ggml(kn[d]);
+        if (ok) s_new[0][lane * DPL + d] = k16;
+        if (ok && own_new) qa.k_cache[((size_t)hkv * a.max_ctx + pos) * HD + lane * DPL + d] = k16;
+      }
+    }
+    if (w == ((G + 1) & 3)) {
+#pragma unroll
+      for (int d = 0; d < DPL; d++) {
+        const uint16_t v16 = f2h_ggml(vrow[d]);
+        if (ok) s_new[FUSED ? 1 : 0][lane * DPL + d] = v16;
+        if (ok && own_new) qa.v_cache[((size_t)hkv * a.max_ctx + pos) * HD + lane * DPL + d] = v16;
+      }
+    }
+  } else {
+    for (int i = t; i < G * HD; i += 256) s_q[i / HD][i % HD] = f2h_ggml(a.q[(size_t)hkv * G * HD + i]);
+  }
+
+  float m_run = -INFINITY, l_run = 0.0f;  // head w's running max / sum (waves w < G)
+  float acc[G];
+#pragma unroll
+  for (int g = 0; g < G; g++) acc[g] = 0.0f;
+  const int d_own = t % HD, kp = t / HD;
+  typedef _Float16 h2t __attribute__((ext_vector_type(2)));
+  for (; tile * 64 < n_keys; tile += NS) {
+    mask_tile(tile);
+    __syncthreads();  // previous tile's LDS reads done (first time: s_q / s_new written)
+#pragma unroll
+    for (int i = 0; i < NLD; i++) {
+      const int k = i * 256 + t;
+      const int j = k / CH, pc = k % CH;
+      if (k < 64 * CH && !(FUSED && tile * 64 + j == pos)) {
+        *reinterpret_cast<uint4*>(&s_k[j * KS + pc * 8]) = kr[i];
+        *reinterpret_cast<uint4*>(&s_v[j * HD + pc * 8]) = vr[i];
+      }
+    }
+    if (FUSED && tile == pos / 64 && t < CH) {  // the new row, written in this launch
+      const int j = pos % 64;
+      *reinterpret_cast<uint4*>(&s_k[j * KS + t * 8]) = reinterpret_cast<const uint4*>(s_new[0])[t];
+      *reinterpret_cast<uint4*>(&s_v[j * HD + t * 8]) = reinterpret_cast<const uint4*>(s_new[FUSED ? 1 : 0])[t];
+    }
+    __syncthreads();
+    if ((tile + NS) * 64 < n_keys) load_tile(tile + NS);  // next tile in flight during this one's math
+    if (t < G * 64 * TP) {
+      const int pr = t / TP, part = t % TP;
+      const int g = pr / 64, j = pr % 64;
+      const uint4* krow = reinterpret_cast<const uint4*>(&s_k[j * KS]);
+      const uint4* qrow = reinterpret_cast<const uint4*>(s_q[g]);
+      float s0 = 0.0f, s1 = 0.0f;
+#pragma unroll
+      for (int i = 0; i < CH / TP; i++) {
+        const uint4 kk = krow[i * TP + part], qq = qrow[i * TP + part];
+        s0 = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2t, kk.x), __builtin_bit_cast(h2t, qq.x), s0, false);
+        s1 = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2t, kk.y), __builtin_bit_cast(h2t, qq.y), s1, false);
+        s0 = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2t, kk.z), __builtin_bit_cast(h2t, qq.z), s0, false);
+        s1 = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2t, kk.w), __builtin_bit_cast(h2t, qq.w), s1, false);
+      }
+      float sc = s0 + s1;
+#pragma unroll
+      for (int o = 1; o < TP; o <<= 1) sc += __shfl_xor(sc, o);
+      if (part == 0) s_p[g][j] = tile * 64 + j < n_keys ? sc : -INFINITY;
+    }
+    __syncthreads();
+    if (w < G) {
+      const float sc = s_p[w][lane];
+      const float m_new = fmaxf(m_run, wave_max(sc));
+      const float p = expf(sc - m_new);  // masked keys: exp(-inf) = 0
+      const float alpha = expf(m_run - m_new);  // first tile: exp(-inf) = 0
+      l_run = l_run * alpha + wave_sum(p);
+      m_run = m_new;
+      s_p[w][lane] = p;
+      if (lane == 0) s_alpha[w] = alpha;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int g = 0; g < G; g++) acc[g] *= s_alpha[g];
+#pragma unroll 8
+    for (int j = kp; j < 64; j += KP) {
+      const float v = h2f(s_v[j * HD + d_own]);
+#pragma unroll
+      for (int g = 0; g < G; g++) acc[g] = fmaf(s_p[g][j], v, acc[g]);
+    }
+  }
+  if constexpr (KP > 1) {
+#pragma unroll
+    for (int g = 0; g < G; g++) s_red[(kp * G + g) * HD + d_own] = acc[g];
+    __syncthreads();
+    if (kp == 0) {
+#pragma unroll
+      for (int g = 0; g < G; g++) {
+        float s = acc[g];
+        for (int r = 1; r < KP; r++) s += s_red[(r * G + g) * HD + d_own];
+        acc[g] = s;
+      }
+    }
+  }
+
+  // ---- publish the partial, take a ticket --------------------------------
+  float* part0 = a.partial + (size_t)hkv * G * NS * (HD + 2);  // [G][NS][HD + 2]
+  if (kp == 0) {
+#pragma unroll
+    for (int g = 0; g < G; g++) st_sc1(part0 + ((size_t)g * NS + c) * (HD + 2) + d_own, acc[g]);
+  }
+  if (w < G && lane == 0) {
+    st_sc1(part0 + ((size_t)w * NS + c) * (HD + 2) + HD, m_run);
+    st_sc1(part0 + ((size_t)w * NS + c) * (HD + 2) + HD + 1, l_run);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0)
+    s_last = __hip_atomic_fetch_add(a.ticket + hkv, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == NS - 1;
+  __syncthreads();
+  if (!s_last) return;
+
+  // ---- last work-group: merge the NS partials of the G heads -------------
+  for (int i = t; i < G * NS * 2; i += 256) {
+    const int g = i / (NS * 2), cc = (i / 2) % NS, e = i & 1;
+    s_ml[g][cc][e] = ld_sc1(part0 + ((size_t)g * NS + cc) * (HD + 2) + HD + e);
+  }
+  __syncthreads();
+  float* s_out = reinterpret_cast<float*>(s_k);  // [G][HD]
+  for (int idx = t; idx < G * HD; idx += 256) {
+    const int g = idx / HD, d = idx % HD;
+    const float* pg = part0 + (size_t)g * NS * (HD + 2) + d;
+    float v[NS];
+#pragma unroll
+    for (int cc = 0; cc < NS; cc++) v[cc] = ld_sc1(pg + (size_t)cc * (HD + 2));
+    float M = -INFINITY;
+#pragma unroll
+    for (int cc = 0; cc < NS; cc++) M = fmaxf(M, s_ml[g][cc][0]);
+    float L = 0.0f, o = 0.0f;
+#pragma unroll
+    for (int cc = 0; cc < NS; cc++) {
+      const float l = s_ml[g][cc][1];
+      const float wc = l == 0.0f ? 0.0f : expf(s_ml[g][cc][0] - M);
+      L = fmaf(l, wc, L);
+      o = fmaf(v[cc], wc, o);
+    }
+    const float val = o / L;
+    a.out[((size_t)hkv * G + g) * HD + d] = val;
+    s_out[idx] = val;
+  }
+  if (a.q8 != nullptr && HD % 32 == 0) {  // Q8_0 blocks of the heads' outputs (ops.cpp:116-139)
+    __syncthreads();
+    for (int b = t; b < G * HD / 32; b += 256) q8_block_serial(s_out + 32 * b, a.q8 + (size_t)hkv * G * HD / 32 + b);
+  }
+  if (t == 0) __hip_atomic_store(a.ticket + hkv, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+}
+
+template <int HD, int G>
+static void launch_split_g(const AttnArgs& a, const QKVArgs* fused, hipStream_t s) {
+  const dim3 grid(a.n_head_kv, ATTN_NSPLIT);
+  if (fused)
+    hipLaunchKernelGGL((attn_split_kernel<HD, G, true>), grid, dim3(256), 0, s, a, *fused);
+  else
+    hipLaunchKernelGGL((attn_split_kernel<HD, G, false>), grid, dim3(256), 0, s, a, QKVArgs{});
+}
+
+template <int HD>
+static void launch_split(const AttnArgs& a, const QKVArgs* fused, hipStream_t s) {
+  switch (a.n_head / a.n_head_kv) {
+    case 1: launch_split_g<HD, 1>(a, fused, s); break;
+    case 2: launch_split_g<HD, 2>(a, fused, s); break;
+    case 4: launch_split_g<HD, 4>(a, fused, s); break;
+    default: throw std::runtime_error("attention: GQA group must be 1, 2 or 4");
+  }
+}
+
+void launch_attention(const AttnArgs& a, bool exact, hipStream_t s, const QKVArgs* fused) {
+  if (exact) {
+    hipLaunchKernelGGL(attn_exact_kernel, dim3(a.n_head), dim3(256), 0, s, a);
+    LLMI_HIP(hipGetLastError());
+    return;
+  }
+  if (a.n_head_kv <= 0 || a.n_head % a.n_head_kv != 0) throw std::runtime_error("attention: n_head % n_head_kv != 0");
+  if (!a.partial || !a.ticket || !a.out) throw std::runtime_error("attention: missing partial / ticket / out buffer");
+  switch (a.head_dim) {
+    case 16: launch_split<16>(a, fused, s); break;
+    case 32: launch_split<32>(a, fused, s); break;
+    case 64: launch_split<64>(a, fused, s); break;
+    case 128: launch_split<128>(a, fused, s); break;
+    case 256: launch_split<256>(a, fused, s); break;
+    default: throw std::runtime_error("attention: unsupported head_dim " + std::to_string(a.head_dim));
+  }
+  LLMI_HIP(hipGetLastError());
+}
+
+}  // namespace llmi
