@@ -194,50 +194,6 @@ __device__ __forceinline__ float ld_sc1(const float* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// merge the ATTN_NSPLIT partials of kv head hkv's G query heads (sc1 loads);
-// splits c >= nvalid own no key (l = 0, weight 0) and are not read.
-// s_out: G*HD floats of LDS; s_ml: [G][NSPLIT][2] of LDS.
-template <int HD, int G>
-__device__ __forceinline__ void attn_merge(const AttnArgs& a, int hkv, int n_keys, float* s_out,
-                                           float (*s_ml)[ATTN_NSPLIT][2]) {
-  constexpr int NS = ATTN_NSPLIT;
-  const int t = threadIdx.x;
-  const float* part0 = a.partial + (size_t)hkv * G * NS * (HD + 2);  // [G][NS][HD + 2]
-  const int nvalid = min(NS, (n_keys + 63) / 64);
-  for (int i = t; i < G * NS * 2; i += 256) {
-    const int g = i / (NS * 2), cc = (i / 2) % NS, e = i & 1;
-    s_ml[g][cc][e] = cc < nvalid ? ld_sc1(part0 + ((size_t)g * NS + cc) * (HD + 2) + HD + e) : 0.0f;
-  }
-  __syncthreads();
-  for (int idx = t; idx < G * HD; idx += 256) {
-    const int g = idx / HD, d = idx % HD;
-    const float* pg = part0 + (size_t)g * NS * (HD + 2) + d;
-    float v[NS];
-#pragma unroll
-    for (int cc = 0; cc < NS; cc++) v[cc] = ld_sc1(pg + (size_t)min(cc, nvalid - 1) * (HD + 2));  // one batch
-#pragma unroll
-    for (int cc = 0; cc < NS; cc++) v[cc] = cc < nvalid ? v[cc] : 0.0f;
-    float M = -INFINITY;
-#pragma unroll
-    for (int cc = 0; cc < NS; cc++) M = cc < nvalid ? fmaxf(M, s_ml[g][cc][0]) : M;
-    float L = 0.0f, o = 0.0f;
-#pragma unroll
-    for (int cc = 0; cc < NS; cc++) {
-      const float l = s_ml[g][cc][1];
-      const float wc = l == 0.0f ? 0.0f : expf(s_ml[g][cc][0] - M);
-      L = fmaf(l, wc, L);
-      o = fmaf(v[cc], wc, o);
-    }
-    const float val = o / L;
-    a.out[((size_t)hkv * G + g) * HD + d] = val;
-    s_out[idx] = val;
-  }
-  if (a.q8 != nullptr && HD % 32 == 0) {  // Q8_0 blocks of the heads' outputs (ops.cpp:116-139)
-    __syncthreads();
-    for (int b = t; b < G * HD / 32; b += 256) q8_block_serial(s_out + 32 * b, a.q8 + (size_t)hkv * G * HD / 32 + b);
-  }
-}
-
 // One work-group of 256 threads per (kv head, split) covering all G = n_head /
 // n_head_kv query heads of that kv head, so each K/V tile is read from HBM
 // once per split.  Per 64-key tile: every thread issues its 16-byte K and V
@@ -257,7 +213,7 @@ __device__ __forceinline__ void attn_merge(const AttnArgs& a, int hkv, int n_key
 // hand-off table, first row): sc1 stores, every storing wave's vmcnt(0),
 // a workgroup barrier, one agent-scope add per work-group; the work-group
 // whose add returns NSPLIT-1 reads every partial with sc1 loads.
-template <int HD, int G, bool FUSED, bool MERGE>
+template <int HD, int G, bool FUSED>
 __global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa) {
   constexpr int NS = ATTN_NSPLIT;
   constexpr int CH = HD / 8;                         // 16-byte chunks per row
@@ -440,7 +396,6 @@ __global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa)
     st_sc1(part0 + ((size_t)w * NS + c) * (HD + 2) + HD, m_run);
     st_sc1(part0 + ((size_t)w * NS + c) * (HD + 2) + HD + 1, l_run);
   }
-  if (!MERGE) return;  // attn_merge_kernel follows as its own launch
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (t == 0)
@@ -448,39 +403,48 @@ __global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa)
   __syncthreads();
   if (!s_last) return;
 
-  attn_merge<HD, G>(a, hkv, n_keys, reinterpret_cast<float*>(s_k), s_ml);
+  // ---- last work-group: merge the NS partials of the G heads -------------
+  for (int i = t; i < G * NS * 2; i += 256) {
+    const int g = i / (NS * 2), cc = (i / 2) % NS, e = i & 1;
+    s_ml[g][cc][e] = ld_sc1(part0 + ((size_t)g * NS + cc) * (HD + 2) + HD + e);
+  }
+  __syncthreads();
+  float* s_out = reinterpret_cast<float*>(s_k);  // [G][HD]
+  for (int idx = t; idx < G * HD; idx += 256) {
+    const int g = idx / HD, d = idx % HD;
+    const float* pg = part0 + (size_t)g * NS * (HD + 2) + d;
+    float v[NS];
+#pragma unroll
+    for (int cc = 0; cc < NS; cc++) v[cc] = ld_sc1(pg + (size_t)cc * (HD + 2));
+    float M = -INFINITY;
+#pragma unroll
+    for (int cc = 0; cc < NS; cc++) M = fmaxf(M, s_ml[g][cc][0]);
+    float L = 0.0f, o = 0.0f;
+#pragma unroll
+    for (int cc = 0; cc < NS; cc++) {
+      const float l = s_ml[g][cc][1];
+      const float wc = l == 0.0f ? 0.0f : expf(s_ml[g][cc][0] - M);
+      L = fmaf(l, wc, L);
+      o = fmaf(v[cc], wc, o);
+    }
+    const float val = o / L;
+    a.out[((size_t)hkv * G + g) * HD + d] = val;
+    s_out[idx] = val;
+  }
+  if (a.q8 != nullptr && HD % 32 == 0) {  // Q8_0 blocks of the heads' outputs (ops.cpp:116-139)
+    __syncthreads();
+    for (int b = t; b < G * HD / 32; b += 256) q8_block_serial(s_out + 32 * b, a.q8 + (size_t)hkv * G * HD / 32 + b);
+  }
   if (t == 0) __hip_atomic_store(a.ticket + hkv, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
-}
-
-template <int HD, int G>
-__global__ __launch_bounds__(256) void attn_merge_kernel(AttnArgs a) {
-  __shared__ __attribute__((aligned(16))) float s_out[G * HD];
-  __shared__ float s_ml[G][ATTN_NSPLIT][2];
-  attn_merge<HD, G>(a, blockIdx.x, *a.d_pos + 1, s_out, s_ml);
-}
-
-// merge inside the split launch (ticket) unless LLMI_ATTN_MERGE_LAUNCH is set
-// (diagnostics: the merge as its own launch)
-static bool merge_launch() {
-  static const bool v = getenv("LLMI_ATTN_MERGE_LAUNCH") != nullptr;
-  return v;
 }
 
 template <int HD, int G>
 static void launch_split_g(const AttnArgs& a, const QKVArgs* fused, hipStream_t s) {
   const dim3 grid(a.n_head_kv, ATTN_NSPLIT);
-  if (merge_launch()) {
-    if (fused)
-      hipLaunchKernelGGL((attn_split_kernel<HD, G, true, false>), grid, dim3(256), 0, s, a, *fused);
-    else
-      hipLaunchKernelGGL((attn_split_kernel<HD, G, false, false>), grid, dim3(256), 0, s, a, QKVArgs{});
-    hipLaunchKernelGGL((attn_merge_kernel<HD, G>), dim3(a.n_head_kv), dim3(256), 0, s, a);
-    return;
-  }
   if (fused)
-    hipLaunchKernelGGL((attn_split_kernel<HD, G, true, true>), grid, dim3(256), 0, s, a, *fused);
+    hipLaunchKernelGGL((attn_split_kernel<HD, G, true>), grid, dim3(256), 0, s, a, *fused);
   else
-    hipLaunchKernelGGL((attn_split_kernel<HD, G, false, true>), grid, dim3(256), 0, s, a, QKVArgs{});
+    hipLaunchKernelGGL((attn_split_kernel<HD, G, false>), grid, dim3(256), 0, s, a, QKVArgs{});
 }
 
 template <int HD>

@@ -17,8 +17,6 @@ one() {  # label, env...
 }
 one fused LLMI_X=0
 for k in qkv attn o_proj gate_up down logits; do one "fused+dup:$k" LLMI_DUP=$k; done
-one fused+merge_launch LLMI_ATTN_MERGE_LAUNCH=1
-one fused+merge_launch+dup:attn LLMI_ATTN_MERGE_LAUNCH=1 LLMI_DUP=attn
 one unfused LLMI_NO_FUSE=1
 for k in qkv norm gate_up gelu down; do one "unfused+dup:$k" LLMI_NO_FUSE=1 LLMI_DUP=$k; done
 echo done | tee -a "$out"
