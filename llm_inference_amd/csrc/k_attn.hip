@@ -204,7 +204,7 @@ __device__ __forceinline__ float ld_sc1(const float* p) {
 //         v_dot2 f16 products in fp32, K rows padded by TP*16 bytes so the
 //         ds_read_b128 of 16 lanes hit 16 distinct bank groups;
 //   softmax: wave g keeps head g's running (m, l);
-//   PV: thread owns one head dim (for all G heads) over a key residue class.
+//   PV: thread owns 4 head dims (for all G heads) over a key residue class.
 // FUSED (session fast path): the work-group also performs the q/k per-head
 // norm, rope and q scale of qk_norm_rope_kv_kernel and the KV append of this
 // token; the split owning `pos` substitutes the new k/v rows from LDS for the
@@ -221,7 +221,8 @@ __global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa)
   constexpr int TP = TP0 < CH ? TP0 : CH;
   constexpr int KS = HD + 8 * TP;                    // padded K row stride (halves)
   constexpr int NLD = (64 * CH + 255) / 256;         // chunk loads per thread per tile
-  constexpr int KP = 256 / HD;                       // key residue classes in PV
+  constexpr int NTD = HD / 4;                        // PV: 4 head dims per thread, NTD threads per key class
+  constexpr int KP = 256 / NTD;                      // key residue classes in PV
   constexpr int DPL = RowLd<HD>::DPL;
   __shared__ __attribute__((aligned(16))) uint16_t s_k[64 * KS];
   __shared__ __attribute__((aligned(16))) uint16_t s_v[64 * HD];
@@ -229,7 +230,7 @@ __global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa)
   __shared__ __attribute__((aligned(16))) uint16_t s_new[FUSED ? 2 : 1][FUSED ? HD : 8];
   __shared__ float s_p[G][64];
   __shared__ float s_alpha[G];
-  __shared__ float s_red[KP > 1 ? KP * G * HD : 1];
+  __shared__ __attribute__((aligned(16))) float s_red[KP > 1 ? KP * G * HD : 4];
   __shared__ float s_ml[G][NS][2];
   __shared__ int s_last;
   static_assert(64 * KS * 2 >= G * HD * 4, "s_k doubles as the merged-output staging");
@@ -308,10 +309,12 @@ __global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa)
   }
 
   float m_run = -INFINITY, l_run = 0.0f;  // head w's running max / sum (waves w < G)
-  float acc[G];
+  float acc[G][4];
 #pragma unroll
-  for (int g = 0; g < G; g++) acc[g] = 0.0f;
-  const int d_own = t % HD, kp = t / HD;
+  for (int g = 0; g < G; g++)
+#pragma unroll
+    for (int e = 0; e < 4; e++) acc[g][e] = 0.0f;
+  const int d_own = 4 * (t % NTD), kp = t / NTD;
   typedef _Float16 h2t __attribute__((ext_vector_type(2)));
   for (; tile * 64 < n_keys; tile += NS) {
     mask_tile(tile);
@@ -364,25 +367,42 @@ __global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa)
     }
     __syncthreads();
 #pragma unroll
-    for (int g = 0; g < G; g++) acc[g] *= s_alpha[g];
-#pragma unroll 8
-    for (int j = kp; j < 64; j += KP) {
-      const float v = h2f(s_v[j * HD + d_own]);
+    for (int g = 0; g < G; g++) {
+      const float al = s_alpha[g];
 #pragma unroll
-      for (int g = 0; g < G; g++) acc[g] = fmaf(s_p[g][j], v, acc[g]);
+      for (int e = 0; e < 4; e++) acc[g][e] *= al;
+    }
+#pragma unroll 4
+    for (int j = kp; j < 64; j += KP) {
+      const uint2 vv = *reinterpret_cast<const uint2*>(&s_v[j * HD + d_own]);
+      const float v0 = h2f((uint16_t)(vv.x & 0xFFFF)), v1 = h2f((uint16_t)(vv.x >> 16));
+      const float v2 = h2f((uint16_t)(vv.y & 0xFFFF)), v3 = h2f((uint16_t)(vv.y >> 16));
+#pragma unroll
+      for (int g = 0; g < G; g++) {
+        const float p = s_p[g][j];
+        acc[g][0] = fmaf(p, v0, acc[g][0]);
+        acc[g][1] = fmaf(p, v1, acc[g][1]);
+        acc[g][2] = fmaf(p, v2, acc[g][2]);
+        acc[g][3] = fmaf(p, v3, acc[g][3]);
+      }
     }
   }
   if constexpr (KP > 1) {
 #pragma unroll
-    for (int g = 0; g < G; g++) s_red[(kp * G + g) * HD + d_own] = acc[g];
+    for (int g = 0; g < G; g++)
+      *reinterpret_cast<float4*>(&s_red[(kp * G + g) * HD + d_own]) =
+          make_float4(acc[g][0], acc[g][1], acc[g][2], acc[g][3]);
     __syncthreads();
     if (kp == 0) {
 #pragma unroll
-      for (int g = 0; g < G; g++) {
-        float s = acc[g];
-        for (int r = 1; r < KP; r++) s += s_red[(r * G + g) * HD + d_own];
-        acc[g] = s;
-      }
+      for (int g = 0; g < G; g++)
+        for (int r = 1; r < KP; r++) {
+          const float4 o = *reinterpret_cast<const float4*>(&s_red[(r * G + g) * HD + d_own]);
+          acc[g][0] += o.x;
+          acc[g][1] += o.y;
+          acc[g][2] += o.z;
+          acc[g][3] += o.w;
+        }
     }
   }
 
@@ -390,7 +410,9 @@ __global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa)
   float* part0 = a.partial + (size_t)hkv * G * NS * (HD + 2);  // [G][NS][HD + 2]
   if (kp == 0) {
 #pragma unroll
-    for (int g = 0; g < G; g++) st_sc1(part0 + ((size_t)g * NS + c) * (HD + 2) + d_own, acc[g]);
+    for (int g = 0; g < G; g++)
+#pragma unroll
+      for (int e = 0; e < 4; e++) st_sc1(part0 + ((size_t)g * NS + c) * (HD + 2) + d_own + e, acc[g][e]);
   }
   if (w < G && lane == 0) {
     st_sc1(part0 + ((size_t)w * NS + c) * (HD + 2) + HD, m_run);
