@@ -213,6 +213,20 @@ __device__ __forceinline__ float ld_sc1(const float* p) {
 // hand-off table, first row): sc1 stores, every storing wave's vmcnt(0),
 // a workgroup barrier, one agent-scope add per work-group; the work-group
 // whose add returns NSPLIT-1 reads every partial with sc1 loads.
+#ifdef LLMI_ATTN_TRACE  // development: per-work-group phase timestamps (scripts/ab)
+__device__ unsigned long long* g_attn_trace = nullptr;
+void attn_set_trace(unsigned long long* p) { LLMI_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_attn_trace), &p, sizeof(p))); }
+#define ATTN_MARK(ph)                                                                                  \
+  do {                                                                                                 \
+    if (g_attn_trace && threadIdx.x == 0)                                                             \
+      g_attn_trace[((size_t)blockIdx.x * gridDim.y + blockIdx.y) * 8 + (ph)] = wall_clock64();        \
+  } while (0)
+#else
+#define ATTN_MARK(ph) \
+  do {                \
+  } while (0)
+#endif
+
 template <int HD, int G, bool FUSED>
 __global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa) {
   constexpr int NS = ATTN_NSPLIT;
@@ -235,6 +249,7 @@ __global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa)
   __shared__ int s_last;
   static_assert(64 * KS * 2 >= G * HD * 4, "s_k doubles as the merged-output staging");
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  ATTN_MARK(0);
   const int hkv = blockIdx.x, c = blockIdx.y;
   const int pos = *a.d_pos;
   const int n_keys = pos + 1;
@@ -316,6 +331,7 @@ __global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa)
     for (int e = 0; e < 4; e++) acc[g][e] = 0.0f;
   const int d_own = 4 * (t % NTD), kp = t / NTD;
   typedef _Float16 h2t __attribute__((ext_vector_type(2)));
+  ATTN_MARK(1);
   for (; tile * 64 < n_keys; tile += NS) {
     mask_tile(tile);
     __syncthreads();  // previous tile's LDS reads done (first time: s_q / s_new written)
@@ -334,6 +350,7 @@ __global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa)
       *reinterpret_cast<uint4*>(&s_v[j * HD + t * 8]) = reinterpret_cast<const uint4*>(s_new[FUSED ? 1 : 0])[t];
     }
     __syncthreads();
+    ATTN_MARK(2);
     if ((tile + NS) * 64 < n_keys) load_tile(tile + NS);  // next tile in flight during this one's math
     if (t < G * 64 * TP) {
       const int pr = t / TP, part = t % TP;
@@ -406,6 +423,7 @@ __global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa)
     }
   }
 
+  ATTN_MARK(3);
   // ---- publish the partial, take a ticket --------------------------------
   float* part0 = a.partial + (size_t)hkv * G * NS * (HD + 2);  // [G][NS][HD + 2]
   if (kp == 0) {
@@ -423,6 +441,7 @@ __global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa)
   if (t == 0)
     s_last = __hip_atomic_fetch_add(a.ticket + hkv, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == NS - 1;
   __syncthreads();
+  ATTN_MARK(4);
   if (!s_last) return;
 
   // ---- last work-group: merge the NS partials of the G heads -------------
@@ -457,6 +476,7 @@ __global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa)
     __syncthreads();
     for (int b = t; b < G * HD / 32; b += 256) q8_block_serial(s_out + 32 * b, a.q8 + (size_t)hkv * G * HD / 32 + b);
   }
+  ATTN_MARK(5);
   if (t == 0) __hip_atomic_store(a.ticket + hkv, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
 }
 

@@ -4,6 +4,7 @@
 // 200 launches captured in one hipGraph.
 #include "../../llm_inference_amd/csrc/attn.h"
 
+#include <algorithm>
 #include <vector>
 
 namespace llmi_old {
@@ -13,6 +14,9 @@ void launch_attention(const AttnArgs& a, bool exact, hipStream_t s, const QKVArg
 }  // namespace llmi_old
 
 using namespace llmi;
+namespace llmi {
+void attn_set_trace(unsigned long long* p);
+}
 
 __global__ void fill_h(uint16_t* p, size_t n, uint32_t seed) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
@@ -100,6 +104,32 @@ int main(int argc, char** argv) {
       fflush(stdout);
       (void)hipGraphExecDestroy(ge);
       (void)hipGraphDestroy(g);
+    }
+  }
+  // phase trace of one launch per position (current version), 100 MHz ticks
+  unsigned long long* tr = dm<unsigned long long>((size_t)n_kv * ATTN_NSPLIT * 8);
+  std::vector<unsigned long long> h((size_t)n_kv * ATTN_NSPLIT * 8);
+  for (int pos : {700, 4000}) {
+    LLMI_HIP(hipMemcpy(dpos, &pos, 4, hipMemcpyHostToDevice));
+    LLMI_HIP(hipMemset(tr, 0, h.size() * 8));
+    attn_set_trace(tr);
+    QKVArgs qa{qkv, n_head * HD, (n_head + n_kv) * HD, n_head, n_kv, HD, nw, nw, cs, 0.0625f, 1e-6, q,
+               kc[3], vc[3], max_ctx, dpos};
+    AttnArgs a{q, kc[3], vc[3], n_head, n_kv, HD, max_ctx, dpos, part, out, ticket, q8};
+    launch_attention(a, false, s, &qa);
+    LLMI_HIP(hipStreamSynchronize(s));
+    attn_set_trace(nullptr);
+    LLMI_HIP(hipMemcpy(h.data(), tr, h.size() * 8, hipMemcpyDeviceToHost));
+    unsigned long long t0 = ~0ull;
+    for (size_t b = 0; b < h.size() / 8; b++) t0 = std::min(t0, h[b * 8]);
+    printf("pos %d: per work-group phase times in us from the first work-group start\n", pos);
+    printf("  wg(hkv,c)  start  prolog  tile1  loopend ticket merged\n");
+    for (size_t b = 0; b < h.size() / 8; b++) {
+      if ((b % ATTN_NSPLIT) > 12 && (b % ATTN_NSPLIT) != ATTN_NSPLIT - 1) continue;
+      printf("  (%d,%2d)", (int)(b / ATTN_NSPLIT), (int)(b % ATTN_NSPLIT));
+      for (int ph = 0; ph < 6; ph++)
+        printf(" %7.2f", h[b * 8 + ph] ? (h[b * 8 + ph] - t0) / 100.0 : -1.0);
+      printf("\n");
     }
   }
   printf("done\n");
