@@ -24,7 +24,9 @@ _i32p = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
 
 def build(ref: bool = True) -> None:
     """Compile the oracle (and, when the reference sources exist, _ref)."""
-    targets = ["all"] + (["ref"] if ref and os.path.isdir(REF_SRC) else [])
+    # "dropin": the reference's model.cpp/gguf.cpp with integration/ops_mi355x.cpp
+    # in place of ops.cpp (needs llm_inference_amd/libllmi.so built first)
+    targets = ["all"] + (["ref", "dropin"] if ref and os.path.isdir(REF_SRC) else [])
     subprocess.run(["make", "-s", "-C", HERE] + targets, check=True)
 
 

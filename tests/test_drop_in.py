@@ -1,0 +1,55 @@
+"""The drop-in boundary end to end: the REFERENCE's own model.cpp/gguf.cpp,
+compiled unchanged with integration/ops_mi355x.cpp in place of ops.cpp
+(oracle/Makefile target `dropin`, output oracle/_ref/dropin_mi355x), runs
+Model::forward with every ops.h call served by libllmi.so on the GPU.
+
+Exact mode (the compat layer's default): GEMVs, quantizers, norms, rope and
+the f16 attention vector ops are bit-identical to the reference's AVX2
+kernels; the remaining arithmetic (attention scores, softmax bookkeeping,
+GELU) is the reference's own CPU code.  So the logits must equal the
+reference's fixtures (tests/golden/model_ref.npz, recorded from the reference
+build) to 1e-5 and the greedy ids exactly.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "oracle", "_ref", "dropin_mi355x")
+
+
+def run(gguf_path, n_decode, prompt):
+    if not os.path.exists(BIN):
+        pytest.skip("oracle/_ref/dropin_mi355x not built (needs /root/reference at build time)")
+    out = subprocess.run([BIN, gguf_path, str(n_decode)] + [str(int(t)) for t in prompt], capture_output=True,
+                         text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    rows = []
+    for line in out.stdout.splitlines():
+        f = line.split()
+        assert f[0] == "logits"
+        rows.append((int(f[1]), int(f[2]), np.array([float(v) for v in f[3:]], np.float32)))
+    return rows
+
+
+def test_dropin_model_test_gguf(golden_models):
+    rows = run(os.path.join(ROOT, "tests", "golden", "model_test.gguf"), 1, [1])
+    (p0, a0, l0), (p1, a1, l1) = rows
+    np.testing.assert_allclose(l0, golden_models["model_test__l1"], atol=1e-5, rtol=0)
+    assert a0 == int(np.argmax(golden_models["model_test__l1"]))
+    np.testing.assert_allclose(l1, golden_models["model_test__l2"], atol=1e-5, rtol=0)
+
+
+def test_dropin_tiny_greedy(golden_models, tmp_path):
+    from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
+    g = build_gemma3_gguf(CONFIGS["tiny"], seed=7, swa_pattern=[True, False, True])
+    path = tmp_path / "tiny.gguf"
+    path.write_bytes(bytes(g))
+    ref_logits, ref_toks = golden_models["tiny__logits"], golden_models["tiny__tokens"]
+    rows = run(str(path), len(ref_toks) - 1, golden_models["tiny__prompt"])
+    assert [a for _, a, _ in rows] == ref_toks.tolist()
+    for i, (_, _, lg) in enumerate(rows):
+        np.testing.assert_allclose(lg, ref_logits[i][:16], atol=1e-5, rtol=0)
