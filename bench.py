@@ -45,6 +45,19 @@ def parse():
     return p.parse_args()
 
 
+def pmc_traffic():
+    """HBM bytes per launch of the Q4_0 projection family from the committed
+    rocprofv3 --pmc FETCH_SIZE pass (profiles/, x2 gfx950 correction; see
+    scripts/pmc_summary.py); None when no such profile is committed."""
+    import glob
+    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "*pmc_fetch*.json")))
+    if not files:
+        return None, None
+    fam = json.load(open(files[-1])).get("q4_0_layer_family", {})
+    b = fam.get("hbm_bytes_per_launch")
+    return (round(b), os.path.relpath(files[-1], os.path.dirname(os.path.abspath(__file__)))) if b else (None, None)
+
+
 class Dist:
     def __init__(self, n):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -138,6 +151,7 @@ def main():
     # dominant kernel: the Q4_0 GEMV family (weights swept in decode order, HIP events)
     us, by = m.time_kernel(0, a.kernel_reps)
     us_l, by_l = m.time_kernel(1, 2)
+    traffic, traffic_src = pmc_traffic()
     ach = by / (us * 1e-6) / 1e9
     mean_ctx = pos + a.steps / 2
     tok_bytes = info.bytes_per_token + info.kv_bytes_per_pos * mean_ctx
@@ -168,7 +182,8 @@ def main():
         "roofline": {
             "kernel": "Q4_0 projection GEMVs of one token in decode order (gemv_q4_0_layer on the fast path: qkv, o, gate_up+GELU, down)",
             "bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-            "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": None,
+            "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": traffic, "traffic_unit": "bytes per launch",
+            "traffic_source": traffic_src,
             "us_per_launch": round(us, 3), "bytes_per_launch": int(by),
         },
         "logits_gemv": {"us": round(us_l, 2), "GBps": round(by_l / (us_l * 1e-6) / 1e9, 1)},

@@ -33,5 +33,7 @@ fi
 if want pmc; then
   run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- \
     python3 bench.py --steps 16 --warmup 2 --prefill 64 --no-cpu-baseline --kernel-reps 1 --no-graph
+  python3 scripts/pmc_summary.py gpurun_out/pmc_fetch/run_counter_collection.csv gpurun_out/pmc_fetch_summary.json \
+    > gpurun_out/pmc_summary.log 2>&1
 fi
 echo "== done"
