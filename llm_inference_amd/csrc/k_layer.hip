@@ -19,6 +19,8 @@
 // each later chunk is issued before the previous one is consumed.
 #include "session_kernels.h"
 
+#include <hip/hip_ext.h>
+
 namespace llmi {
 
 namespace {
@@ -211,6 +213,13 @@ using LaunchFn = void (*)(dim3, size_t, const LayerGemv&, hipStream_t);
 
 template <int R, int NW, int P, int E, int ROLE, bool MULTI>
 void launch_cfg(dim3 grid, size_t lds, const LayerGemv& a, hipStream_t s) {
+  KernelTiming& kt = kernel_timing();
+  if (kt.start) {
+    hipExtLaunchKernelGGL((gemv_q4_0_layer<R, NW, P, E, ROLE != ROLE_PLAIN, ROLE == ROLE_GELU, MULTI>), grid,
+                          dim3(NW * 64), (uint32_t)lds, s, kt.start, kt.stop, 0u, a);
+    kt = KernelTiming{};
+    return;
+  }
   hipLaunchKernelGGL((gemv_q4_0_layer<R, NW, P, E, ROLE != ROLE_PLAIN, ROLE == ROLE_GELU, MULTI>), grid, dim3(NW * 64),
                      lds, s, a);
 }
@@ -255,6 +264,11 @@ const LayerCfg* find_cfg(int nb, int role) {
 }
 
 }  // namespace
+
+KernelTiming& kernel_timing() {
+  thread_local KernelTiming kt;
+  return kt;
+}
 
 bool layer_gemv_supported(const DevWeight& w, bool pro, bool gelu, int n_pro) {
   if (w.type != T_Q4_0 || w.cols % 32 != 0 || w.rows <= 0) return false;

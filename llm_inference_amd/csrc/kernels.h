@@ -33,6 +33,15 @@ struct ActBuf {
 
 enum GemvMode { GEMV_EXACT = 0, GEMV_FAST = 1 };
 
+// Kernel timing hook (bench): when set, the next instrumented launch on this
+// thread records start/stop through hipExtLaunchKernel -- the events are
+// signalled by the kernel's own dispatch, so the elapsed time is the kernel's
+// duration as rocprofv3 reports it (no launch gap) -- and clears the hook.
+struct KernelTiming {
+  hipEvent_t start = nullptr, stop = nullptr;
+};
+KernelTiming& kernel_timing();
+
 // quantizers (bit-exact with ops.cpp:116-178)
 void launch_quantize_q8_0(const float* x, int n, Q8Act out, hipStream_t s);
 void launch_quantize_q8_k(const float* x, int n, uint8_t* out, hipStream_t s);

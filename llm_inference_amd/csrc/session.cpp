@@ -654,13 +654,16 @@ void Session::time_kernel(int which, int reps, double* us, double* bytes) {
   for (int r = 0; r < reps; r++)
     for (size_t j = 0; j < ws.size(); j++) {
       const DevWeight* w = ws[j];
-      LLMI_HIP(hipEventRecord(ev[k++], stream_));
-      if (!fl.empty())
+      if (!fl.empty()) {  // dispatch-signalled events: the kernel's own duration (= rocprofv3's)
+        kernel_timing() = KernelTiming{ev[k], ev[k + 1]};
+        k += 2;
         launch_layer_gemv(*w, fl[j].first, fl[j].second >= 1, fl[j].second == 2, stream_);
-      else
+      } else {
+        LLMI_HIP(hipEventRecord(ev[k++], stream_));
         launch_gemv(*w, act_, (w == &embd_ || w->rows > 2 * hp_.n_ff) ? logits_ : gu_,
                     exact_ ? GEMV_EXACT : GEMV_FAST, stream_, w == &embd_ ? amax_key_ : nullptr);
-      LLMI_HIP(hipEventRecord(ev[k++], stream_));
+        LLMI_HIP(hipEventRecord(ev[k++], stream_));
+      }
       tot_bytes += (double)w->bytes;
     }
   LLMI_HIP(hipStreamSynchronize(stream_));
