@@ -43,32 +43,34 @@ __device__ __forceinline__ float rms_scale_d(float sum, int n, double eps) {  //
 }
 
 template <int P>
-struct Chunk {  // raw loaded words: converting at load time would wait for them
-  uint4 q[P];
+struct Chunk {  // raw loaded words only: (row, block) are recomputed when eaten, and
+  uint4 q[P];   // converting scales at load time would wait for them
   uint16_t sw[P];
-  int rr[P], bb[P];
 };
 
-template <int R, int P>
+template <int P>
 __device__ __forceinline__ void load_chunk(Chunk<P>& c, const uint4* qw, const uint16_t* dw, int c0, int total,
-                                           int nb, uint32_t magic, int lane) {
+                                           int lane) {
 #pragma unroll
   for (int p = 0; p < P; p++) {
     const int f = c0 + p * 64 + lane;
-    const int fc = f < total ? f : 0;
-    const int r = div_by_magic(fc, magic);
-    c.rr[p] = f < total ? r : R;
-    c.bb[p] = fc - r * nb;
+    const int fc = f < total ? f : 0;  // clamped: always a valid address
     c.q[p] = ld_nt(qw + fc);
     c.sw[p] = ld_nt16(dw + fc);
   }
 }
 
 template <int R, int P>
-__device__ __forceinline__ void eat_chunk(const Chunk<P>& c, const XBlock* s_x, float (&acc)[R]) {
+__device__ __forceinline__ void eat_chunk(const Chunk<P>& c, int c0, int total, int nb, uint32_t magic, int lane,
+                                          const XBlock* s_x, float (&acc)[R]) {
 #pragma unroll
   for (int p = 0; p < P; p++) {
-    const int4* xp = reinterpret_cast<const int4*>(s_x + c.bb[p]);
+    const int f = c0 + p * 64 + lane;
+    const int fc = f < total ? f : 0;
+    const int r = div_by_magic(fc, magic);
+    const int rr = f < total ? r : R;  // items past the wave's rows add to no row
+    const int bb = fc - r * nb;
+    const int4* xp = reinterpret_cast<const int4*>(s_x + bb);
     const int4 x0 = xp[0], x1 = xp[1], x2 = xp[2];
     int is = x2.y;  // nsum8
     is = sdot4(nib_lo(c.q[p].x), x0.x, is);
@@ -81,12 +83,13 @@ __device__ __forceinline__ void eat_chunk(const Chunk<P>& c, const XBlock* s_x, 
     is = sdot4(nib_hi(c.q[p].w), x1.w, is);
     const float v = (h2f(c.sw[p]) * __int_as_float(x2.x)) * (float)is;
 #pragma unroll
-    for (int k = 0; k < R; k++) acc[k] += (k == c.rr[p]) ? v : 0.0f;
+    for (int k = 0; k < R; k++) acc[k] += (k == rr) ? v : 0.0f;
+    // keep the scheduler from hoisting every pass's LDS x reads up front
+    // (it would hold 12 VGPRs per pass live; other waves hide the LDS latency)
+    __builtin_amdgcn_sched_barrier(0);
   }
 }
 
-// E: prologue elements per thread (PRO) or 16-B x loads per thread (!PRO);
-// MULTI: the wave's items span more than one chunk of P passes
 template <int R, int NW, int P, int E, bool PRO, bool GELU, bool MULTI>
 __global__ __launch_bounds__(NW * 64) void gemv_q4_0_layer(LayerGemv a) {
   constexpr int EPT = E, X_LD = E;
@@ -118,8 +121,9 @@ __global__ __launch_bounds__(NW * 64) void gemv_q4_0_layer(LayerGemv a) {
       wp[k] = (ok && a.w_post) ? a.w_post[i] : 0.0f;
       wn[k] = ok ? a.w_next[i] : 0.0f;
     }
-    load_chunk<R, P>(ca, qw, dw, 0, total, nb, a.magic, lane);  // unconditional (valid clamped rows): a
+    load_chunk<P>(ca, qw, dw, 0, total, lane);  // unconditional (valid clamped rows): a
     // branch here would merge wait counts to vmcnt(0) at the first prologue use
+    if constexpr (MULTI) load_chunk<P>(cb, qw, dw, 64 * P, total, lane);  // both chunks in flight
     float ss = 0.0f;
 #pragma unroll
     for (int k = 0; k < EPT; k++) ss = fmaf(yv[k], yv[k], ss);
@@ -157,7 +161,8 @@ __global__ __launch_bounds__(NW * 64) void gemv_q4_0_layer(LayerGemv a) {
     uint4 xr[X_LD];
 #pragma unroll
     for (int k = 0; k < X_LD; k++) xr[k] = src[min(t + k * T, n16 - 1)];
-    load_chunk<R, P>(ca, qw, dw, 0, total, nb, a.magic, lane);
+    load_chunk<P>(ca, qw, dw, 0, total, lane);
+    if constexpr (MULTI) load_chunk<P>(cb, qw, dw, 64 * P, total, lane);
 #pragma unroll
     for (int k = 0; k < X_LD; k++) dst[min(t + k * T, n16)] = xr[k];  // slot n16: LDS pad (discarded)
   }
@@ -167,15 +172,17 @@ __global__ __launch_bounds__(NW * 64) void gemv_q4_0_layer(LayerGemv a) {
 #pragma unroll
   for (int k = 0; k < R; k++) acc[k] = 0.0f;
   if constexpr (!MULTI) {
-    eat_chunk<R, P>(ca, s_x, acc);
+    eat_chunk<R, P>(ca, 0, total, nb, a.magic, lane, s_x, acc);
   } else {
+    // chunks 0 and 1 were issued before the prologue; each later chunk is
+    // issued as soon as its register buffer has been consumed
     constexpr int CH = 64 * P;
     for (int c0 = 0; c0 < total; c0 += 2 * CH) {
-      if (c0 + CH < total) load_chunk<R, P>(cb, qw, dw, c0 + CH, total, nb, a.magic, lane);
-      eat_chunk<R, P>(ca, s_x, acc);
+      eat_chunk<R, P>(ca, c0, total, nb, a.magic, lane, s_x, acc);
+      if (c0 + 2 * CH < total) load_chunk<P>(ca, qw, dw, c0 + 2 * CH, total, lane);
       if (c0 + CH >= total) break;
-      if (c0 + 2 * CH < total) load_chunk<R, P>(ca, qw, dw, c0 + 2 * CH, total, nb, a.magic, lane);
-      eat_chunk<R, P>(cb, s_x, acc);
+      eat_chunk<R, P>(cb, c0 + CH, total, nb, a.magic, lane, s_x, acc);
+      if (c0 + 3 * CH < total) load_chunk<P>(cb, qw, dw, c0 + 3 * CH, total, lane);
     }
   }
 
@@ -249,10 +256,10 @@ const LayerCfg kLayerCfgs[] = {
     LLMI_LCFG(80, ROLE_PRO, 4, 4, 5, 12, false),
     LLMI_LCFG(120, ROLE_PRO, 8, 8, 8, 12, true),
     LLMI_LCFG(168, ROLE_PRO, 8, 8, 7, 12, true),
-    // prologue + GELU epilogue: 8 waves x 8 rows = 64 interleaved gate/up rows
+    // prologue + GELU epilogue: NW x R = 64 interleaved gate/up rows per work-group
     LLMI_LCFG(36, ROLE_GELU, 8, 8, 5, 6, false),
-    LLMI_LCFG(80, ROLE_GELU, 8, 8, 5, 6, true),
-    LLMI_LCFG(120, ROLE_GELU, 8, 8, 8, 12, true),
+    LLMI_LCFG(80, ROLE_GELU, 4, 16, 5, 3, false),    // 16 waves x 4 rows: one 5-pass chunk per wave
+    LLMI_LCFG(120, ROLE_GELU, 4, 16, 8, 6, false),
     LLMI_LCFG(168, ROLE_GELU, 8, 8, 7, 12, true),
 };
 #undef LLMI_LCFG
