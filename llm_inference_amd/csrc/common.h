@@ -210,13 +210,7 @@ __device__ __forceinline__ void q8_block_store(float v, bool ok, XBlock* blk, in
 // The same quantization of one block by ONE thread (no cross-lane traffic):
 // used where a whole vector is staged in LDS and each thread owns a block.
 // Bit-identical to q8_block_store (max and integer sums are order-free).
-__device__ __forceinline__ void q8_block_serial(const float* __restrict__ x32, XBlock* __restrict__ blk) {
-  float v[32];
-#pragma unroll
-  for (int k = 0; k < 8; k++) {
-    const float4 f = reinterpret_cast<const float4*>(x32)[k];
-    v[4 * k] = f.x; v[4 * k + 1] = f.y; v[4 * k + 2] = f.z; v[4 * k + 3] = f.w;
-  }
+__device__ __forceinline__ void q8_block_from_regs(const float (&v)[32], XBlock* __restrict__ blk) {
   float amax = 0.0f;
 #pragma unroll
   for (int k = 0; k < 32; k++) amax = fmaxf(amax, fabsf(v[k]));
@@ -239,6 +233,15 @@ __device__ __forceinline__ void q8_block_serial(const float* __restrict__ x32, X
   blk->hi = make_int4((int)w[4], (int)w[5], (int)w[6], (int)w[7]);
   blk->d = h2f(f2h_ggml(dd));
   blk->nsum8 = -8 * s;
+}
+__device__ __forceinline__ void q8_block_serial(const float* __restrict__ x32, XBlock* __restrict__ blk) {
+  float v[32];
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const float4 f = reinterpret_cast<const float4*>(x32)[k];
+    v[4 * k] = f.x; v[4 * k + 1] = f.y; v[4 * k + 2] = f.z; v[4 * k + 3] = f.w;
+  }
+  q8_block_from_regs(v, blk);
 }
 
 // f / nb by multiply-high for the small f of one wave's chunk; nb == 1 has

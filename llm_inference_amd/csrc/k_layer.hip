@@ -1,22 +1,25 @@
 // k_layer.hip -- the decode step's Q4_0 GEMVs with their neighbours fused in.
 //
-// One launch per projection instead of norm / quantize / GEMV / GELU launches:
-//   PRO  : the residual step that precedes the GEMV (model.cpp:843-858 and
-//          915-924 + the next run_norm) is recomputed by every work-group from
-//          the previous GEMV's output -- h = resid + rms(y)*w_post,
-//          x = rms(h)*w_next, Q8_0 blocks of x (ops.cpp:116-139) -- straight
-//          into LDS.  Work-group 0 publishes h (resid_out, a ping-pong buffer:
-//          the other work-groups of the same launch still read resid_in).
-//   !PRO : the activation's Q8_0 blocks are copied global -> LDS once per WG.
-//   GELU : gate/up rows are interleaved in groups of 32 at upload, so a WG of
-//          64 rows owns gate[32k..32k+31] and up[32k..32k+31]; it finishes
-//          GELU(gate)*up (model.cpp:892-899) for those 32 hidden units and
-//          their Q8_0 block for the down projection.
+// One launch per projection instead of norm / quantize / GEMV / GELU launches.
+// Roles (what a work-group does around the weight stream):
+//   PLAIN : the activation's Q8_0 blocks are copied global -> LDS.
+//   PRO   : the residual step that precedes the GEMV (model.cpp:843-858 and
+//           915-924 + the next run_norm) is recomputed by every work-group
+//           from the previous GEMV's output -- h = resid + rms(y)*w_post,
+//           x = rms(h)*w_next, Q8_0 blocks of x (ops.cpp:116-139) -- into LDS.
+//           Work-group 0 publishes h (resid_out, a ping-pong buffer: the other
+//           work-groups of the same launch still read resid_in).
+//   GELU  : PRO, and gate/up rows interleaved in groups of H at upload, so a
+//           work-group of 2H rows owns gate[Hb..Hb+H) and up[Hb..Hb+H) and
+//           finishes GELU(gate)*up (model.cpp:892-899) for those H units.
+//   QUANT : the f32 activation (the GELU output) is quantized to Q8_0 blocks
+//           into LDS, one block per thread (no cross-lane reductions).
+// Geometry: one fat work-group per CU where the prologue is per-work-group
+// work (PRO/GELU/QUANT), so that work is done 256 times, not once per 16 rows.
 // The weight stream is the gemv_q4_0_fast scheme (k_gemv.hip): a wave owns R
 // rows as a flat (row, block) item list, one 16-B non-temporal load per lane
-// per pass, a chunk of P passes in flight; the first chunk is issued before
-// the prologue so its HBM latency hides the prologue's L2 round trip, and
-// each later chunk is issued before the previous one is consumed.
+// per pass, a chunk of P passes in flight; prologue loads are issued first,
+// then the first weight chunk(s), so the prologue runs while weights stream.
 #include "session_kernels.h"
 
 #include <hip/hip_ext.h>
@@ -90,13 +93,16 @@ __device__ __forceinline__ void eat_chunk(const Chunk<P>& c, int c0, int total, 
   }
 }
 
-template <int R, int NW, int P, int E, bool PRO, bool GELU, bool MULTI>
+enum { ROLE_PLAIN = LAYER_PLAIN, ROLE_PRO = LAYER_PRO, ROLE_GELU = LAYER_GELU, ROLE_QUANT = LAYER_QUANT };
+
+template <int R, int NW, int P, int E, int ROLE, bool MULTI>
 __global__ __launch_bounds__(NW * 64) void gemv_q4_0_layer(LayerGemv a) {
+  constexpr bool PRO = ROLE == ROLE_PRO || ROLE == ROLE_GELU, GELU = ROLE == ROLE_GELU;
   constexpr int EPT = E, X_LD = E;
   extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
   XBlock* s_x = reinterpret_cast<XBlock*>(s_dyn);
   __shared__ float s_red[2][NW];
-  __shared__ float s_rows[GELU ? 64 : 1];
+  __shared__ float s_rows[GELU ? NW * R : 1];
   constexpr int T = NW * 64;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int nb = a.nb;
@@ -152,6 +158,25 @@ __global__ __launch_bounds__(NW * 64) void gemv_q4_0_layer(LayerGemv a) {
     }
     __syncthreads();
     for (int b = t; b < nb; b += T) q8_block_serial(s_xf + 32 * b, s_x + b);
+  } else if constexpr (ROLE == ROLE_QUANT) {
+    // one Q8_0 block per thread: its 32 floats loaded before the weights,
+    // quantized while they stream (blocks beyond T handled afterwards)
+    const float4* yb = reinterpret_cast<const float4*>(a.y);
+    float4 xr[8];
+    const int b0 = min(t, nb - 1);
+#pragma unroll
+    for (int k = 0; k < 8; k++) xr[k] = yb[b0 * 8 + k];
+    load_chunk<P>(ca, qw, dw, 0, total, lane);
+    if constexpr (MULTI) load_chunk<P>(cb, qw, dw, 64 * P, total, lane);
+    if (t < nb) {
+      float v[32];
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        v[4 * k] = xr[k].x; v[4 * k + 1] = xr[k].y; v[4 * k + 2] = xr[k].z; v[4 * k + 3] = xr[k].w;
+      }
+      q8_block_from_regs(v, s_x + t);
+    }
+    for (int b = t + T; b < nb; b += T) q8_block_serial(a.y + 32 * b, s_x + b);
   } else {
     // x blocks -> LDS: clamped unconditional loads (no branch between them
     // and the weight loads, so the stores wait only for their own data)
@@ -193,12 +218,8 @@ __global__ __launch_bounds__(NW * 64) void gemv_q4_0_layer(LayerGemv a) {
       if (lane == 0) s_rows[w * R + k] = s;
     }
     __syncthreads();
-    if (t < 32) {
-      const int j = blockIdx.x * 32 + t;  // hidden unit
-      const float v = gelu_mul1(s_rows[t], s_rows[32 + t]);
-      a.hid[j] = v;
-      q8_block_store(v, true, a.hq8 + blockIdx.x, t);
-    }
+    constexpr int H = NW * R / 2;  // hidden units of this work-group
+    if (t < H) a.hid[blockIdx.x * H + t] = gelu_mul1(s_rows[t], s_rows[H + t]);
   } else {
 #pragma unroll
     for (int k = 0; k < R; k++) {
@@ -211,56 +232,57 @@ __global__ __launch_bounds__(NW * 64) void gemv_q4_0_layer(LayerGemv a) {
 // ---- launch table ----------------------------------------------------------
 // One instantiation per (activation length, role) of the Gemma-3 1B/4B/12B/27B
 // projections; shapes outside the table take the unfused path (session.cpp).
-//   R: rows per wave (R * nb a multiple of 64 where possible), P: passes per
-//   chunk, E: see the kernel, NW: waves per WG (8 when the prologue's vector
-//   exceeds 12 elements per thread of a 256-thread WG, and for GELU: 64 rows).
-enum { ROLE_PLAIN = 0, ROLE_PRO = 1, ROLE_GELU = 2 };
-
+// Geometry aims at ~256 work-groups (one per CU) so per-work-group prologue
+// work is done once per CU and every CU streams the same bytes:
+//   R: rows per wave, NW: waves per work-group, P: passes (64 items) per
+//   chunk, MULTI: more than one chunk per wave,
+//   E: PLAIN -- 16-B x loads per thread (ceil(3 nb / 64 NW));
+//      PRO/GELU -- prologue elements per thread (ceil(32 nb / 64 NW)); QUANT -- unused.
 using LaunchFn = void (*)(dim3, size_t, const LayerGemv&, hipStream_t);
 
 template <int R, int NW, int P, int E, int ROLE, bool MULTI>
 void launch_cfg(dim3 grid, size_t lds, const LayerGemv& a, hipStream_t s) {
   KernelTiming& kt = kernel_timing();
   if (kt.start) {
-    hipExtLaunchKernelGGL((gemv_q4_0_layer<R, NW, P, E, ROLE != ROLE_PLAIN, ROLE == ROLE_GELU, MULTI>), grid,
-                          dim3(NW * 64), (uint32_t)lds, s, kt.start, kt.stop, 0u, a);
+    hipExtLaunchKernelGGL((gemv_q4_0_layer<R, NW, P, E, ROLE, MULTI>), grid, dim3(NW * 64), (uint32_t)lds, s, kt.start,
+                          kt.stop, 0u, a);
     kt = KernelTiming{};
     return;
   }
-  hipLaunchKernelGGL((gemv_q4_0_layer<R, NW, P, E, ROLE != ROLE_PLAIN, ROLE == ROLE_GELU, MULTI>), grid, dim3(NW * 64),
-                     lds, s, a);
+  hipLaunchKernelGGL((gemv_q4_0_layer<R, NW, P, E, ROLE, MULTI>), grid, dim3(NW * 64), lds, s, a);
 }
 
 struct LayerCfg {
-  int nb, role, R, NW, P;
+  int nb, role, R, NW, P, E;
   bool multi;
   LaunchFn fn;
 };
 
-#define LLMI_LCFG(NB, ROLE, R, NW, P, E, MULTI) {NB, ROLE, R, NW, P, MULTI, launch_cfg<R, NW, P, E, ROLE, MULTI>}
+#define LLMI_LCFG(NB, ROLE, R, NW, P, E, MULTI) {NB, ROLE, R, NW, P, E, MULTI, launch_cfg<R, NW, P, E, ROLE, MULTI>}
 const LayerCfg kLayerCfgs[] = {
-    // plain: x blocks copied to LDS (E = 16-B loads per thread = ceil(3 nb / 256))
-    LLMI_LCFG(32, ROLE_PLAIN, 2, 4, 1, 1, false),    // 1B o (4 x 256)
-    LLMI_LCFG(36, ROLE_PLAIN, 8, 4, 5, 1, false),    // 1B qkv, layer 0
-    LLMI_LCFG(64, ROLE_PLAIN, 1, 4, 1, 1, false),    // 4B o (8 x 256)
-    LLMI_LCFG(80, ROLE_PLAIN, 4, 4, 5, 1, false),    // 4B qkv, layer 0
-    LLMI_LCFG(120, ROLE_PLAIN, 8, 4, 8, 2, true),    // 12B qkv, layer 0
-    LLMI_LCFG(128, ROLE_PLAIN, 1, 4, 2, 2, false),   // 12B / 27B o (16 x 256, 32 x 128)
-    LLMI_LCFG(168, ROLE_PLAIN, 8, 4, 7, 2, true),    // 27B qkv, layer 0
-    LLMI_LCFG(216, ROLE_PLAIN, 8, 4, 7, 4, true),    // 1B down
-    LLMI_LCFG(320, ROLE_PLAIN, 1, 4, 5, 4, false),   // 4B down
-    LLMI_LCFG(480, ROLE_PLAIN, 2, 4, 8, 8, true),    // 12B down
-    LLMI_LCFG(672, ROLE_PLAIN, 2, 4, 7, 8, true),    // 27B down
-    // residual + norm prologue (E = prologue elements per thread)
-    LLMI_LCFG(36, ROLE_PRO, 8, 4, 5, 12, false),
-    LLMI_LCFG(80, ROLE_PRO, 4, 4, 5, 12, false),
-    LLMI_LCFG(120, ROLE_PRO, 8, 8, 8, 12, true),
-    LLMI_LCFG(168, ROLE_PRO, 8, 8, 7, 12, true),
-    // prologue + GELU epilogue: NW x R = 64 interleaved gate/up rows per work-group
-    LLMI_LCFG(36, ROLE_GELU, 8, 8, 5, 6, false),
-    LLMI_LCFG(80, ROLE_GELU, 4, 16, 5, 3, false),    // 16 waves x 4 rows: one 5-pass chunk per wave
-    LLMI_LCFG(120, ROLE_GELU, 4, 16, 8, 6, false),
-    LLMI_LCFG(168, ROLE_GELU, 8, 8, 7, 12, true),
+    // PLAIN: x blocks copied to LDS
+    LLMI_LCFG(32, ROLE_PLAIN, 2, 2, 1, 1, false),     // 1B o        1152 rows -> 288 WGs
+    LLMI_LCFG(36, ROLE_PLAIN, 8, 1, 5, 2, false),     // 1B qkv l0   1536 rows -> 192 WGs
+    LLMI_LCFG(64, ROLE_PLAIN, 1, 10, 1, 1, false),    // 4B o        2560 rows -> 256 WGs
+    LLMI_LCFG(80, ROLE_PLAIN, 4, 4, 5, 1, false),     // 4B qkv l0   4096 rows -> 256 WGs
+    LLMI_LCFG(120, ROLE_PLAIN, 8, 4, 8, 2, true),     // 12B qkv l0  8192 rows -> 256 WGs
+    LLMI_LCFG(128, ROLE_PLAIN, 1, 15, 2, 1, false),   // 12B/27B o   3840/5376 rows -> 256/359 WGs
+    LLMI_LCFG(168, ROLE_PLAIN, 8, 4, 7, 2, true),     // 27B qkv l0  8192 rows -> 256 WGs
+    // PRO: residual + norm prologue
+    LLMI_LCFG(36, ROLE_PRO, 8, 2, 5, 9, false),       // 1B qkv      96 WGs
+    LLMI_LCFG(80, ROLE_PRO, 4, 4, 5, 10, false),      // 4B qkv      256 WGs
+    LLMI_LCFG(120, ROLE_PRO, 8, 4, 8, 15, true),      // 12B qkv     256 WGs
+    LLMI_LCFG(168, ROLE_PRO, 4, 8, 6, 11, true),      // 27B qkv     256 WGs
+    // GELU: prologue + GELU epilogue, 2H = R NW interleaved gate/up rows per WG
+    LLMI_LCFG(36, ROLE_GELU, 6, 9, 4, 2, false),      // 1B  13824 rows, H 27 -> 256 WGs
+    LLMI_LCFG(80, ROLE_GELU, 5, 16, 7, 3, false),     // 4B  20480 rows, H 40 -> 256 WGs
+    LLMI_LCFG(120, ROLE_GELU, 8, 15, 8, 4, true),     // 12B 30720 rows, H 60 -> 256 WGs
+    LLMI_LCFG(168, ROLE_GELU, 12, 14, 8, 6, true),    // 27B 43008 rows, H 84 -> 256 WGs
+    // QUANT: f32 activation quantized into LDS (down projection)
+    LLMI_LCFG(216, ROLE_QUANT, 2, 2, 7, 1, false),    // 1B down     1152 rows -> 288 WGs
+    LLMI_LCFG(320, ROLE_QUANT, 1, 10, 5, 1, false),   // 4B down     2560 rows -> 256 WGs
+    LLMI_LCFG(480, ROLE_QUANT, 1, 15, 8, 1, false),   // 12B down    3840 rows -> 256 WGs
+    LLMI_LCFG(672, ROLE_QUANT, 1, 16, 6, 1, true),    // 27B down    5376 rows -> 336 WGs
 };
 #undef LLMI_LCFG
 
@@ -277,28 +299,40 @@ KernelTiming& kernel_timing() {
   return kt;
 }
 
-bool layer_gemv_supported(const DevWeight& w, bool pro, bool gelu, int n_pro) {
+bool layer_gemv_supported(const DevWeight& w, int role) {
   if (w.type != T_Q4_0 || w.cols % 32 != 0 || w.rows <= 0) return false;
-  if (pro && n_pro != w.cols) return false;
-  if (gelu && (!pro || w.rows % 64 != 0)) return false;
-  return find_cfg(w.cols / 32, gelu ? ROLE_GELU : (pro ? ROLE_PRO : ROLE_PLAIN)) != nullptr;
+  const LayerCfg* c = find_cfg(w.cols / 32, role);
+  if (!c) return false;
+  if (role == LAYER_GELU && w.rows % (c->R * c->NW) != 0) return false;
+  return true;
 }
 
-void launch_layer_gemv(const DevWeight& w, LayerGemv a, bool pro, bool gelu, hipStream_t s) {
-  if (!layer_gemv_supported(w, pro, gelu, pro ? w.cols : 0)) throw std::runtime_error("layer gemv: unsupported weight");
-  if (pro ? (!a.y || !a.resid_in || !a.resid_out || !a.w_next || a.resid_in == a.resid_out) : !a.xg)
+int layer_gemv_gelu_group(int cols) {
+  const LayerCfg* c = cols % 32 == 0 ? find_cfg(cols / 32, LAYER_GELU) : nullptr;
+  return c ? c->R * c->NW / 2 : 0;
+}
+
+void launch_layer_gemv(const DevWeight& w, LayerGemv a, int role, hipStream_t s) {
+  if (!layer_gemv_supported(w, role)) throw std::runtime_error("layer gemv: unsupported weight");
+  const bool pro = role == LAYER_PRO || role == LAYER_GELU;
+  if (pro && (!a.y || !a.resid_in || !a.resid_out || !a.w_next || a.resid_in == a.resid_out))
     throw std::runtime_error("layer gemv: missing prologue operand");
-  if (gelu ? (!a.hid || !a.hq8) : !a.out) throw std::runtime_error("layer gemv: missing output");
-  const LayerCfg& c = *find_cfg(w.cols / 32, gelu ? ROLE_GELU : (pro ? ROLE_PRO : ROLE_PLAIN));
-  if (!c.multi && c.R * (w.cols / 32) > 64 * c.P) throw std::runtime_error("layer gemv: table entry needs MULTI");
+  if (role == LAYER_PLAIN && !a.xg) throw std::runtime_error("layer gemv: missing activation blocks");
+  if (role == LAYER_QUANT && !a.y) throw std::runtime_error("layer gemv: missing activation");
+  if (role == LAYER_GELU ? !a.hid : !a.out) throw std::runtime_error("layer gemv: missing output");
+  const LayerCfg& c = *find_cfg(w.cols / 32, role);
+  const int nb = w.cols / 32;
+  if (!c.multi && c.R * nb > 64 * c.P) throw std::runtime_error("layer gemv: table entry needs MULTI");
+  if (pro && w.cols > c.E * c.NW * 64) throw std::runtime_error("layer gemv: prologue E too small");
+  if (role == LAYER_PLAIN && 3 * nb > c.E * c.NW * 64) throw std::runtime_error("layer gemv: x copy E too small");
   a.qs = reinterpret_cast<const uint4*>(w.qs);
   a.wd = w.d;
   a.rows = w.rows;
-  a.nb = w.cols / 32;
-  a.magic = div_magic(a.nb);
-  if (pro) a.n = w.cols;
+  a.nb = nb;
+  a.magic = div_magic(nb);
+  a.n = w.cols;
   // x blocks + pad slot of the x copy (+ the f32 x staging of the prologue)
-  const size_t lds = (size_t)a.nb * sizeof(XBlock) + 16 + (pro ? (size_t)a.n * 4 : 0);
+  const size_t lds = (size_t)nb * sizeof(XBlock) + 16 + (pro ? (size_t)w.cols * 4 : 0);
   const int rows_per_wg = c.NW * c.R;
   c.fn(dim3((w.rows + rows_per_wg - 1) / rows_per_wg), lds, a, s);
   LLMI_HIP(hipGetLastError());

@@ -153,30 +153,34 @@ void Session::upload(const GGUFView& g) {  // model.cpp:169-238 tensor map
     // the fused layer path (k_layer.hip) needs every projection in its launch
     // table; decided from the GGUF shapes before upload because it changes
     // the gate/up row order
-    auto shape_ok = [](const GTensor* t, int rows, bool pro, bool gelu, int n_pro) {
+    auto shape_ok = [](const GTensor* t, int rows, int role) {
       DevWeight w;
       w.type = t->type;
       w.rows = rows;
       w.cols = (int)t->shape[0];
-      return layer_gemv_supported(w, pro, gelu, n_pro);
+      return layer_gemv_supported(w, role);
     };
     const bool qkv_same = q->type == k->type && q->type == v->type && q->shape[0] == k->shape[0] &&
                           q->shape[0] == v->shape[0];
     const bool want_fused =
         fuse_layers_ && qkv_same && gt->type == T_Q4_0 && up->type == T_Q4_0 && gt->shape[0] == up->shape[0] &&
-        hp_.n_ff % 32 == 0 && shape_ok(q, (int)(q->shape[1] + k->shape[1] + v->shape[1]), true, false, hp_.n_embd) &&
-        shape_ok(o, (int)o->shape[1], false, false, 0) && shape_ok(gt, 2 * hp_.n_ff, true, true, hp_.n_embd) &&
-        shape_ok(dn, (int)dn->shape[1], false, false, 0);
+        (int)q->shape[0] == hp_.n_embd && (int)gt->shape[0] == hp_.n_embd &&
+        shape_ok(q, (int)(q->shape[1] + k->shape[1] + v->shape[1]), LAYER_PRO) &&
+        shape_ok(q, (int)(q->shape[1] + k->shape[1] + v->shape[1]), LAYER_PLAIN) &&
+        shape_ok(o, (int)o->shape[1], LAYER_PLAIN) && shape_ok(gt, 2 * hp_.n_ff, LAYER_GELU) &&
+        shape_ok(dn, (int)dn->shape[1], LAYER_QUANT);
     if (want_fused) {
-      // rows interleaved in groups of 32 (gate 32k.., up 32k..) for the fused
-      // GELU epilogue of gemv_q4_0_layer (k_layer.hip)
+      // rows interleaved in groups of H (gate H k.., up H k..) for the fused
+      // GELU epilogue of gemv_q4_0_layer (k_layer.hip): a work-group of 2H
+      // rows owns matching gate and up rows
       const int cols = (int)gt->shape[0], F = hp_.n_ff;
+      const int H = layer_gemv_gelu_group(cols);
       const size_t rb = gguf_bytes(T_Q4_0, 1, cols);
       std::vector<uint8_t> il((size_t)2 * F * rb);
       const uint8_t *sg = (const uint8_t*)g.tensor_data(*gt), *su = (const uint8_t*)g.tensor_data(*up);
-      for (int k = 0; k < F / 32; k++) {
-        std::memcpy(&il[(size_t)(64 * k) * rb], sg + (size_t)(32 * k) * rb, 32 * rb);
-        std::memcpy(&il[(size_t)(64 * k + 32) * rb], su + (size_t)(32 * k) * rb, 32 * rb);
+      for (int k = 0; k < F / H; k++) {
+        std::memcpy(&il[(size_t)(2 * H * k) * rb], sg + (size_t)(H * k) * rb, H * rb);
+        std::memcpy(&il[(size_t)(2 * H * k + H) * rb], su + (size_t)(H * k) * rb, H * rb);
       }
       GemvPart p;
       p.w = alloc_weight(T_Q4_0, 2 * F, cols);
@@ -188,11 +192,9 @@ void Session::upload(const GGUFView& g) {  // model.cpp:169-238 tensor map
       Ld.gate_up = make_parts(g, {gt, up}, stream_, weight_bytes_);
     }
     Ld.down = make_parts(g, {dn}, stream_, weight_bytes_)[0];
-    Ld.fused = Ld.gu_interleaved && Ld.qkv.size() == 1 &&
-               layer_gemv_supported(Ld.qkv[0].w, true, false, hp_.n_embd) &&
-               layer_gemv_supported(Ld.o.w, false, false, 0) &&
-               layer_gemv_supported(Ld.gate_up[0].w, true, true, hp_.n_embd) &&
-               layer_gemv_supported(Ld.down.w, false, false, 0);
+    Ld.fused = Ld.gu_interleaved && Ld.qkv.size() == 1 && layer_gemv_supported(Ld.qkv[0].w, LAYER_PRO) &&
+               layer_gemv_supported(Ld.qkv[0].w, LAYER_PLAIN) && layer_gemv_supported(Ld.o.w, LAYER_PLAIN) &&
+               layer_gemv_supported(Ld.gate_up[0].w, LAYER_GELU) && layer_gemv_supported(Ld.down.w, LAYER_QUANT);
     Ld.attn_norm = dev_f32_copy(g, T("attn_norm.weight"), hp_.n_embd);
     Ld.q_norm = dev_f32_copy(g, T("attn_q_norm.weight"), Ld.hd);
     Ld.k_norm = dev_f32_copy(g, T("attn_k_norm.weight"), Ld.hd);
@@ -390,9 +392,9 @@ void Session::record_step(hipStream_t s) {
   kernels_per_token_++;
 }
 
-// Fast path with every projection a gemv_q4_0_layer launch: 6 launches per
-// layer (qkv [+ residual/norm prologue], attention partial, combine, o,
-// gate_up [+ prologue + GELU epilogue], down).  The residual stream
+// Fast path with every projection a gemv_q4_0_layer launch: 5 launches per
+// layer (qkv [+ residual/norm prologue], attention, o, gate_up [+ prologue +
+// GELU epilogue], down [+ Q8_0 of the GELU output]).  The residual stream
 // ping-pongs between resid_ and resid2_ (a prologue's work-group 0 writes the
 // buffer its sibling work-groups are not reading).
 void Session::record_layers_fused(hipStream_t s, bool x_q8) {
@@ -410,7 +412,7 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
       }
       g.xg = act_.q8.xb;
       g.out = qkv_;
-      for (int r = 0; r < dup("qkv"); r++) launch_layer_gemv(Ld.qkv[0].w, g, false, false, s);
+      for (int r = 0; r < dup("qkv"); r++) launch_layer_gemv(Ld.qkv[0].w, g, LAYER_PLAIN, s);
     } else {
       g.y = d_out_;
       g.w_post = L_[l - 1].post_ffw_norm;
@@ -419,7 +421,7 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
       g.w_next = Ld.attn_norm;
       g.eps = hp_.eps;
       g.out = qkv_;
-      for (int r = 0; r < dup("qkv"); r++) launch_layer_gemv(Ld.qkv[0].w, g, true, false, s);
+      for (int r = 0; r < dup("qkv"); r++) launch_layer_gemv(Ld.qkv[0].w, g, LAYER_PRO, s);
       std::swap(cur, other);
     }
     kernels_per_token_++;
@@ -437,7 +439,7 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
     LayerGemv go;
     go.xg = act_.q8.xb;
     go.out = o_out_;
-    for (int r = 0; r < dup("o_proj"); r++) launch_layer_gemv(Ld.o.w, go, false, false, s);
+    for (int r = 0; r < dup("o_proj"); r++) launch_layer_gemv(Ld.o.w, go, LAYER_PLAIN, s);
     LayerGemv gg;
     gg.y = o_out_;
     gg.w_post = Ld.post_attn_norm;
@@ -446,13 +448,12 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
     gg.w_next = Ld.ffn_norm;
     gg.eps = hp_.eps;
     gg.hid = hid_;
-    gg.hq8 = act_.q8.xb;
-    for (int r = 0; r < dup("gate_up"); r++) launch_layer_gemv(Ld.gate_up[0].w, gg, true, true, s);
+    for (int r = 0; r < dup("gate_up"); r++) launch_layer_gemv(Ld.gate_up[0].w, gg, LAYER_GELU, s);
     std::swap(cur, other);
     LayerGemv gd;
-    gd.xg = act_.q8.xb;
+    gd.y = hid_;  // QUANT: GELU output quantized per block in the down launch
     gd.out = d_out_;
-    for (int r = 0; r < dup("down"); r++) launch_layer_gemv(Ld.down.w, gd, false, false, s);
+    for (int r = 0; r < dup("down"); r++) launch_layer_gemv(Ld.down.w, gd, LAYER_QUANT, s);
     kernels_per_token_ += 3;
   }
   // final residual + output_norm (-> xn_, and f16 x for an F16 logits table)
@@ -604,7 +605,7 @@ void Session::time_kernel(int which, int reps, double* us, double* bytes) {
   for (const auto& l : L_) fused &= l.fused;
   // the fused path's launches (gemv_q4_0_layer) with their real arguments,
   // except that the prologue's residual write goes to a scratch buffer
-  std::vector<std::pair<LayerGemv, int>> fl;  // (args, mode: 0 plain, 1 pro, 2 pro+gelu)
+  std::vector<std::pair<LayerGemv, int>> fl;  // (args, LayerRole)
   if (which == 0 && fused) {
     for (size_t i = 0; i < L_.size(); i++) {
       const LayerDev& Ld = L_[i];
@@ -616,24 +617,23 @@ void Session::time_kernel(int which, int reps, double* us, double* bytes) {
       q.w_next = Ld.attn_norm;
       q.eps = hp_.eps;
       q.out = qkv_;
-      fl.push_back({q, 1});
+      fl.push_back({q, LAYER_PRO});
       ws.push_back(&Ld.qkv[0].w);
       LayerGemv o;
       o.xg = act_.q8.xb;
       o.out = o_out_;
-      fl.push_back({o, 0});
+      fl.push_back({o, LAYER_PLAIN});
       ws.push_back(&Ld.o.w);
       LayerGemv gu = q;
       gu.w_next = Ld.ffn_norm;
       gu.out = nullptr;
       gu.hid = hid_;
-      gu.hq8 = act_.q8.xb;
-      fl.push_back({gu, 2});
+      fl.push_back({gu, LAYER_GELU});
       ws.push_back(&Ld.gate_up[0].w);
       LayerGemv d;
-      d.xg = act_.q8.xb;
+      d.y = hid_;
       d.out = d_out_;
-      fl.push_back({d, 0});
+      fl.push_back({d, LAYER_QUANT});
       ws.push_back(&Ld.down.w);
     }
   } else if (which == 0) {
@@ -657,7 +657,7 @@ void Session::time_kernel(int which, int reps, double* us, double* bytes) {
       if (!fl.empty()) {  // dispatch-signalled events: the kernel's own duration (= rocprofv3's)
         kernel_timing() = KernelTiming{ev[k], ev[k + 1]};
         k += 2;
-        launch_layer_gemv(*w, fl[j].first, fl[j].second >= 1, fl[j].second == 2, stream_);
+        launch_layer_gemv(*w, fl[j].first, fl[j].second, stream_);
       } else {
         LLMI_HIP(hipEventRecord(ev[k++], stream_));
         launch_gemv(*w, act_, (w == &embd_ || w->rows > 2 * hp_.n_ff) ? logits_ : gu_,

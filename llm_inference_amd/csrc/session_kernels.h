@@ -26,14 +26,15 @@ void launch_embed_norm(uint32_t type, const uint8_t* table, size_t row_bytes, co
                        bool exact, hipStream_t s);
 void launch_gelu_quant(const float* gu, int n, float* hid, const Q8Act* q8, hipStream_t s);
 // Q4_0 GEMV with the decode step's neighbours fused in (k_layer.hip)
+enum LayerRole { LAYER_PLAIN = 0, LAYER_PRO = 1, LAYER_GELU = 2, LAYER_QUANT = 3 };
 struct LayerGemv {
   const uint4* qs = nullptr;  // set by launch_layer_gemv from the weight
   const uint16_t* wd = nullptr;
   int rows = 0, nb = 0;
   uint32_t magic = 0;
-  const XBlock* xg = nullptr;  // !pro: the activation's Q8_0 blocks
-  // pro: resid_out = resid_in + rms(y) * w_post (y itself when w_post is
-  // null); x = rms(resid_out) * w_next
+  const XBlock* xg = nullptr;  // PLAIN: the activation's Q8_0 blocks
+  // PRO / GELU: resid_out = resid_in + rms(y) * w_post (y itself when w_post
+  // is null); x = rms(resid_out) * w_next.  QUANT: x = y.
   const float* y = nullptr;
   const float* w_post = nullptr;
   const float* resid_in = nullptr;
@@ -42,12 +43,13 @@ struct LayerGemv {
   float* xn_out = nullptr;  // optional copy of x (work-group 0)
   int n = 0;
   double eps = 0;
-  float* out = nullptr;     // !gelu: [rows]
-  float* hid = nullptr;     // gelu: [rows / 2] and its Q8_0 blocks
-  XBlock* hq8 = nullptr;
+  float* out = nullptr;     // PLAIN / PRO / QUANT: [rows]
+  float* hid = nullptr;     // GELU: [rows / 2] = GELU(gate) * up
 };
-bool layer_gemv_supported(const DevWeight& w, bool pro, bool gelu, int n_pro);
-void launch_layer_gemv(const DevWeight& w, LayerGemv a, bool pro, bool gelu, hipStream_t s);
+bool layer_gemv_supported(const DevWeight& w, int role);
+// GELU role: hidden units per work-group (the gate/up interleave group), 0 if unsupported
+int layer_gemv_gelu_group(int cols);
+void launch_layer_gemv(const DevWeight& w, LayerGemv a, int role, hipStream_t s);
 void launch_argmax(const float* x, int n, unsigned long long* key, hipStream_t s);
 void launch_finalize_token(unsigned long long* key, int32_t* d_token, int32_t* d_pos, int32_t* ring,
                            int32_t* ring_idx, int ring_cap, hipStream_t s);

@@ -149,8 +149,8 @@ int main(int argc, char** argv) {
     plain.xg = xb;
     plain.out = out;
     DevWeight probe = ws[0];
-    if (layer_gemv_supported(probe, false, false, 0))
-      timeit("layer plain", [&](const DevWeight& w) { launch_layer_gemv(w, plain, false, false, s); });
+    if (layer_gemv_supported(probe, LAYER_PLAIN))
+      timeit("layer plain", [&](const DevWeight& w) { launch_layer_gemv(w, plain, LAYER_PLAIN, s); });
     LayerGemv pro;
     pro.y = y;
     pro.resid_in = r0;
@@ -159,14 +159,18 @@ int main(int argc, char** argv) {
     pro.w_next = wn;
     pro.eps = 1e-6;
     pro.out = out;
-    if (layer_gemv_supported(probe, true, false, sh.cols))
-      timeit("layer pro", [&](const DevWeight& w) { launch_layer_gemv(w, pro, true, false, s); });
+    if (layer_gemv_supported(probe, LAYER_PRO))
+      timeit("layer pro", [&](const DevWeight& w) { launch_layer_gemv(w, pro, LAYER_PRO, s); });
     LayerGemv gl = pro;
     gl.out = nullptr;
     gl.hid = hid;
-    gl.hq8 = hq;
-    if (layer_gemv_supported(probe, true, true, sh.cols))
-      timeit("layer pro+gelu", [&](const DevWeight& w) { launch_layer_gemv(w, gl, true, true, s); });
+    if (layer_gemv_supported(probe, LAYER_GELU))
+      timeit("layer pro+gelu", [&](const DevWeight& w) { launch_layer_gemv(w, gl, LAYER_GELU, s); });
+    LayerGemv qz;
+    qz.y = y;
+    qz.out = out;
+    if (layer_gemv_supported(probe, LAYER_QUANT))
+      timeit("layer quant", [&](const DevWeight& w) { launch_layer_gemv(w, qz, LAYER_QUANT, s); });
     // geometry variants of the plain kernel
     const uint32_t mg = div_magic(nb);
     auto geo = [&](const char* label, auto kern, int rows_per_wg, int threads) {
@@ -183,17 +187,17 @@ int main(int argc, char** argv) {
       });
     };
     if (nb % 64 == 0) {
-      geo("plain R1 NW4 P1", gemv_q4_0_layer<1, 4, 1, 4, false, false, true>, 4, 256);
-      geo("plain R1 NW8 P1", gemv_q4_0_layer<1, 8, 1, 4, false, false, true>, 8, 512);
+      geo("plain R1 NW4 P1", gemv_q4_0_layer<1, 4, 1, 4, 0, true>, 4, 256);
+      geo("plain R1 NW8 P1", gemv_q4_0_layer<1, 8, 1, 4, 0, true>, 8, 512);
     }
     if ((4 * nb) % 64 == 0) {
-      geo("plain R4 NW4 P5", gemv_q4_0_layer<4, 4, 5, 4, false, false, true>, 16, 256);
-      geo("plain R4 NW2 P5", gemv_q4_0_layer<4, 2, 5, 4, false, false, true>, 8, 128);
-      geo("plain R4 NW1 P5", gemv_q4_0_layer<4, 1, 5, 4, false, false, true>, 4, 64);
-      geo("plain R4 NW8 P5", gemv_q4_0_layer<4, 8, 5, 4, false, false, true>, 32, 512);
+      geo("plain R4 NW4 P5", gemv_q4_0_layer<4, 4, 5, 4, 0, true>, 16, 256);
+      geo("plain R4 NW2 P5", gemv_q4_0_layer<4, 2, 5, 4, 0, true>, 8, 128);
+      geo("plain R4 NW1 P5", gemv_q4_0_layer<4, 1, 5, 4, 0, true>, 4, 64);
+      geo("plain R4 NW8 P5", gemv_q4_0_layer<4, 8, 5, 4, 0, true>, 32, 512);
     }
-    geo("plain R8 NW4 P5", gemv_q4_0_layer<8, 4, 5, 4, false, false, true>, 32, 256);
-    geo("plain R2 NW4 P5", gemv_q4_0_layer<2, 4, 5, 4, false, false, true>, 8, 256);
+    geo("plain R8 NW4 P5", gemv_q4_0_layer<8, 4, 5, 4, 0, true>, 32, 256);
+    geo("plain R2 NW4 P5", gemv_q4_0_layer<2, 4, 5, 4, 0, true>, 8, 256);
     for (auto& w : ws) {
       (void)hipFree(w.qs);
       (void)hipFree(w.d);
