@@ -244,6 +244,36 @@ __device__ __forceinline__ void q8_block_serial(const float* __restrict__ x32, X
   q8_block_from_regs(v, blk);
 }
 
+// The same quantization with a block spread over the 4 lanes of a DPP quad
+// (lane & 3 = sub owns elements 8 sub .. 8 sub + 7): quad max / integer sum
+// by two DPP steps each.  Bit-identical to q8_block_store (order-free max
+// and integer sums).  All 4 lanes of every quad must execute it.
+__device__ __forceinline__ void q8_block_quad(const float (&v)[8], int sub, XBlock* __restrict__ blk) {
+  float amax = 0.0f;
+#pragma unroll
+  for (int k = 0; k < 8; k++) amax = fmaxf(amax, fabsf(v[k]));
+  amax = fmaxf(amax, dpp_f<DPP_QUAD_1032>(amax));
+  amax = fmaxf(amax, dpp_f<DPP_QUAD_2301>(amax));
+  const float dd = amax / 127.0f;
+  const float id = dd != 0.0f ? 1.0f / dd : 0.0f;
+  int s = 0;
+  uint32_t w0 = 0, w1 = 0;
+#pragma unroll
+  for (int e = 0; e < 4; e++) {
+    const int q0 = nearest_int_fma(v[e], id), q1 = nearest_int_fma(v[4 + e], id);
+    s += q0 + q1;
+    w0 |= (uint32_t)(q0 & 0xFF) << (8 * e);
+    w1 |= (uint32_t)(q1 & 0xFF) << (8 * e);
+  }
+  s += dpp_i<DPP_QUAD_1032>(s);
+  s += dpp_i<DPP_QUAD_2301>(s);
+  reinterpret_cast<uint2*>(blk)[sub] = make_uint2(w0, w1);  // q[8 sub .. 8 sub + 7]
+  if (sub == 0) {
+    blk->d = h2f(f2h_ggml(dd));
+    blk->nsum8 = -8 * s;
+  }
+}
+
 // f / nb by multiply-high for the small f of one wave's chunk; nb == 1 has
 // no 32-bit magic and is encoded as 0
 __host__ __device__ inline uint32_t div_magic(uint32_t nb) { return nb == 1 ? 0u : (uint32_t)((1ull << 32) / nb + 1); }

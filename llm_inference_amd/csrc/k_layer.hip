@@ -157,26 +157,33 @@ __global__ __launch_bounds__(NW * 64) void gemv_q4_0_layer(LayerGemv a) {
       }
     }
     __syncthreads();
-    for (int b = t; b < nb; b += T) q8_block_serial(s_xf + 32 * b, s_x + b);
+    for (int i = t; i < 4 * nb; i += T) {  // quads of lanes per block (T is a multiple of 64)
+      const float4 f0 = reinterpret_cast<const float4*>(s_xf)[2 * i], f1 = reinterpret_cast<const float4*>(s_xf)[2 * i + 1];
+      const float v[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+      q8_block_quad(v, i & 3, s_x + (i >> 2));
+    }
   } else if constexpr (ROLE == ROLE_QUANT) {
-    // one Q8_0 block per thread: its 32 floats loaded before the weights,
-    // quantized while they stream (blocks beyond T handled afterwards)
+    // a DPP quad of lanes per Q8_0 block (8 floats each): the first E rounds'
+    // floats are loaded before the weights and quantized while they stream
     const float4* yb = reinterpret_cast<const float4*>(a.y);
-    float4 xr[8];
-    const int b0 = min(t, nb - 1);
+    float4 xr[E][2];
 #pragma unroll
-    for (int k = 0; k < 8; k++) xr[k] = yb[b0 * 8 + k];
+    for (int r = 0; r < E; r++) {
+      const int i = min(t + r * T, 4 * nb - 1);
+      xr[r][0] = yb[2 * i];
+      xr[r][1] = yb[2 * i + 1];
+    }
     load_chunk<P>(ca, qw, dw, 0, total, lane);
     if constexpr (MULTI) load_chunk<P>(cb, qw, dw, 64 * P, total, lane);
-    if (t < nb) {
-      float v[32];
 #pragma unroll
-      for (int k = 0; k < 8; k++) {
-        v[4 * k] = xr[k].x; v[4 * k + 1] = xr[k].y; v[4 * k + 2] = xr[k].z; v[4 * k + 3] = xr[k].w;
+    for (int r = 0; r < E; r++) {
+      const int i = t + r * T;
+      if (r * T < 4 * nb) {  // uniform: whole quads are in or out together (4 nb, T multiples of 4)
+        const float v[8] = {xr[r][0].x, xr[r][0].y, xr[r][0].z, xr[r][0].w,
+                            xr[r][1].x, xr[r][1].y, xr[r][1].z, xr[r][1].w};
+        if (i < 4 * nb) q8_block_quad(v, i & 3, s_x + (i >> 2));
       }
-      q8_block_from_regs(v, s_x + t);
     }
-    for (int b = t + T; b < nb; b += T) q8_block_serial(a.y + 32 * b, s_x + b);
   } else {
     // x blocks -> LDS: clamped unconditional loads (no branch between them
     // and the weight loads, so the stores wait only for their own data)
@@ -237,7 +244,8 @@ __global__ __launch_bounds__(NW * 64) void gemv_q4_0_layer(LayerGemv a) {
 //   R: rows per wave, NW: waves per work-group, P: passes (64 items) per
 //   chunk, MULTI: more than one chunk per wave,
 //   E: PLAIN -- 16-B x loads per thread (ceil(3 nb / 64 NW));
-//      PRO/GELU -- prologue elements per thread (ceil(32 nb / 64 NW)); QUANT -- unused.
+//      PRO/GELU -- prologue elements per thread (ceil(32 nb / 64 NW));
+//      QUANT -- rounds of 8-float quad lanes (ceil(4 nb / 64 NW)).
 using LaunchFn = void (*)(dim3, size_t, const LayerGemv&, hipStream_t);
 
 template <int R, int NW, int P, int E, int ROLE, bool MULTI>
@@ -279,10 +287,10 @@ const LayerCfg kLayerCfgs[] = {
     LLMI_LCFG(120, ROLE_GELU, 8, 15, 8, 4, true),     // 12B 30720 rows, H 60 -> 256 WGs
     LLMI_LCFG(168, ROLE_GELU, 12, 14, 8, 6, true),    // 27B 43008 rows, H 84 -> 256 WGs
     // QUANT: f32 activation quantized into LDS (down projection)
-    LLMI_LCFG(216, ROLE_QUANT, 2, 2, 7, 1, false),    // 1B down     1152 rows -> 288 WGs
-    LLMI_LCFG(320, ROLE_QUANT, 1, 10, 5, 1, false),   // 4B down     2560 rows -> 256 WGs
-    LLMI_LCFG(480, ROLE_QUANT, 1, 15, 8, 1, false),   // 12B down    3840 rows -> 256 WGs
-    LLMI_LCFG(672, ROLE_QUANT, 1, 16, 6, 1, true),    // 27B down    5376 rows -> 336 WGs
+    LLMI_LCFG(216, ROLE_QUANT, 2, 2, 7, 7, false),    // 1B down     1152 rows -> 288 WGs
+    LLMI_LCFG(320, ROLE_QUANT, 1, 10, 5, 2, false),   // 4B down     2560 rows -> 256 WGs
+    LLMI_LCFG(480, ROLE_QUANT, 1, 15, 8, 2, false),   // 12B down    3840 rows -> 256 WGs
+    LLMI_LCFG(672, ROLE_QUANT, 1, 16, 6, 3, true),    // 27B down    5376 rows -> 336 WGs
 };
 #undef LLMI_LCFG
 
@@ -325,6 +333,7 @@ void launch_layer_gemv(const DevWeight& w, LayerGemv a, int role, hipStream_t s)
   if (!c.multi && c.R * nb > 64 * c.P) throw std::runtime_error("layer gemv: table entry needs MULTI");
   if (pro && w.cols > c.E * c.NW * 64) throw std::runtime_error("layer gemv: prologue E too small");
   if (role == LAYER_PLAIN && 3 * nb > c.E * c.NW * 64) throw std::runtime_error("layer gemv: x copy E too small");
+  if (role == LAYER_QUANT && 4 * nb > c.E * c.NW * 64) throw std::runtime_error("layer gemv: quant E too small");
   a.qs = reinterpret_cast<const uint4*>(w.qs);
   a.wd = w.d;
   a.rows = w.rows;
