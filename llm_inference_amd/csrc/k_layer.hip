@@ -93,11 +93,24 @@ __device__ __forceinline__ void eat_chunk(const Chunk<P>& c, int c0, int total, 
   }
 }
 
+#ifdef LLMI_LAYER_TRACE  // development: per-work-group phase timestamps (scripts/gemv_sweep)
+__device__ unsigned long long* g_layer_trace = nullptr;
+#define LAYER_MARK(ph)                                                                                     \
+  do {                                                                                                     \
+    if (g_layer_trace && threadIdx.x == 0) g_layer_trace[(size_t)blockIdx.x * 8 + (ph)] = wall_clock64(); \
+  } while (0)
+#else
+#define LAYER_MARK(ph) \
+  do {                 \
+  } while (0)
+#endif
+
 enum { ROLE_PLAIN = LAYER_PLAIN, ROLE_PRO = LAYER_PRO, ROLE_GELU = LAYER_GELU, ROLE_QUANT = LAYER_QUANT };
 
 template <int R, int NW, int P, int E, int ROLE, bool MULTI>
 __global__ __launch_bounds__(NW * 64) void gemv_q4_0_layer(LayerGemv a) {
   constexpr bool PRO = ROLE == ROLE_PRO || ROLE == ROLE_GELU, GELU = ROLE == ROLE_GELU;
+  LAYER_MARK(0);
   constexpr int EPT = E, X_LD = E;
   extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
   XBlock* s_x = reinterpret_cast<XBlock*>(s_dyn);
@@ -133,7 +146,9 @@ __global__ __launch_bounds__(NW * 64) void gemv_q4_0_layer(LayerGemv a) {
     float ss = 0.0f;
 #pragma unroll
     for (int k = 0; k < EPT; k++) ss = fmaf(yv[k], yv[k], ss);
+    LAYER_MARK(1);
     const float sc1 = rms_scale_d(wg_sum<NW>(ss, s_red[0]), n, a.eps);
+    LAYER_MARK(2);
     float ss2 = 0.0f;
 #pragma unroll
     for (int k = 0; k < EPT; k++) {
@@ -144,6 +159,7 @@ __global__ __launch_bounds__(NW * 64) void gemv_q4_0_layer(LayerGemv a) {
       if (blockIdx.x == 0 && i < n) a.resid_out[i] = h;
     }
     const float sc2 = rms_scale_d(wg_sum<NW>(ss2, s_red[1]), n, a.eps);
+    LAYER_MARK(3);
     // x staged as f32 in LDS, then one thread per Q8_0 block (no cross-lane
     // reductions on this latency-critical path)
     float* s_xf = reinterpret_cast<float*>(s_dyn + (size_t)nb * sizeof(XBlock) + 16);
@@ -200,6 +216,7 @@ __global__ __launch_bounds__(NW * 64) void gemv_q4_0_layer(LayerGemv a) {
   }
   __syncthreads();
 
+  LAYER_MARK(4);
   float acc[R];
 #pragma unroll
   for (int k = 0; k < R; k++) acc[k] = 0.0f;
@@ -218,6 +235,7 @@ __global__ __launch_bounds__(NW * 64) void gemv_q4_0_layer(LayerGemv a) {
     }
   }
 
+  LAYER_MARK(5);
   if constexpr (GELU) {
 #pragma unroll
     for (int k = 0; k < R; k++) {
@@ -234,6 +252,7 @@ __global__ __launch_bounds__(NW * 64) void gemv_q4_0_layer(LayerGemv a) {
       if (lane == 0 && k < nrows) a.out[row0 + k] = s;
     }
   }
+  LAYER_MARK(6);
 }
 
 // ---- launch table ----------------------------------------------------------
@@ -301,6 +320,10 @@ const LayerCfg* find_cfg(int nb, int role) {
 }
 
 }  // namespace
+
+#ifdef LLMI_LAYER_TRACE
+void layer_set_trace(unsigned long long* p) { LLMI_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_layer_trace), &p, sizeof(p))); }
+#endif
 
 KernelTiming& kernel_timing() {
   thread_local KernelTiming kt;

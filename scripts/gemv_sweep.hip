@@ -9,9 +9,13 @@
 #include "../llm_inference_amd/csrc/k_gemv.hip"
 #include "../llm_inference_amd/csrc/k_layer.hip"
 
+#include <algorithm>
 #include <vector>
 
 using namespace llmi;
+namespace llmi {
+void layer_set_trace(unsigned long long* p);
+}
 
 namespace {
 
@@ -171,6 +175,46 @@ int main(int argc, char** argv) {
     qz.out = out;
     if (layer_gemv_supported(probe, LAYER_QUANT))
       timeit("layer quant", [&](const DevWeight& w) { launch_layer_gemv(w, qz, LAYER_QUANT, s); });
+    // phase trace of one launch per role (100 MHz ticks, from the first WG start)
+    {
+      unsigned long long* tr;
+      const size_t nslot = 4096 * 8;
+      LLMI_HIP(hipMalloc(&tr, nslot * 8));
+      std::vector<unsigned long long> h(nslot);
+      auto trace = [&](const char* label, auto&& launch) {
+        if (!layer_gemv_supported(probe, 0)) {}
+        LLMI_HIP(hipMemset(tr, 0, nslot * 8));
+        LLMI_HIP(hipStreamSynchronize(s));
+        layer_set_trace(tr);
+        for (int i = 0; i < 24; i++) launch(ws[i % copies]);  // the last of a back-to-back run is kept
+        LLMI_HIP(hipStreamSynchronize(s));
+        layer_set_trace(nullptr);
+        LLMI_HIP(hipMemcpy(h.data(), tr, nslot * 8, hipMemcpyDeviceToHost));
+        unsigned long long t0 = ~0ull, tend = 0;
+        int nwg = 0;
+        double ph[8] = {0};
+        int cnt[8] = {0};
+        for (size_t b = 0; b < nslot / 8; b++) {
+          if (!h[b * 8]) continue;
+          nwg++;
+          t0 = std::min(t0, h[b * 8]);
+        }
+        for (size_t b = 0; b < nslot / 8; b++) {
+          if (!h[b * 8]) continue;
+          for (int k = 0; k < 7; k++)
+            if (h[b * 8 + k]) { ph[k] += (h[b * 8 + k] - t0) / 100.0; cnt[k]++; }
+          tend = std::max(tend, h[b * 8 + 6]);
+        }
+        printf("%-12s trace %-18s wgs=%d span=%.2f us  mean phase times (us):", sh.name, label, nwg, (tend - t0) / 100.0);
+        for (int k = 0; k < 7; k++) printf(" p%d=%.2f", k, cnt[k] ? ph[k] / cnt[k] : -1.0);
+        printf("\n");
+      };
+      if (layer_gemv_supported(probe, LAYER_PLAIN)) trace("plain", [&](const DevWeight& w) { launch_layer_gemv(w, plain, LAYER_PLAIN, s); });
+      if (layer_gemv_supported(probe, LAYER_PRO)) trace("pro", [&](const DevWeight& w) { launch_layer_gemv(w, pro, LAYER_PRO, s); });
+      if (layer_gemv_supported(probe, LAYER_GELU)) trace("gelu", [&](const DevWeight& w) { launch_layer_gemv(w, gl, LAYER_GELU, s); });
+      if (layer_gemv_supported(probe, LAYER_QUANT)) trace("quant", [&](const DevWeight& w) { launch_layer_gemv(w, qz, LAYER_QUANT, s); });
+      (void)hipFree(tr);
+    }
     // geometry variants of the plain kernel
     const uint32_t mg = div_magic(nb);
     auto geo = [&](const char* label, auto kern, int rows_per_wg, int threads) {
