@@ -291,6 +291,9 @@ __global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa)
     }
   }
   int tile = c;
+  // every wave's q/k/v row loads enter the CU's memory queue ahead of the
+  // K/V tile (HBM) loads, so the prologue is not stuck behind the tile misses
+  __builtin_amdgcn_s_barrier();
   load_tile(tile);
   if (FUSED) {
     const bool ok = lane * DPL < HD;
