@@ -18,8 +18,9 @@
 // work (PRO/GELU/QUANT), so that work is done 256 times, not once per 16 rows.
 // The weight stream is the gemv_q4_0_fast scheme (k_gemv.hip): a wave owns R
 // rows as a flat (row, block) item list, one 16-B non-temporal load per lane
-// per pass, a chunk of P passes in flight; prologue loads are issued first,
-// then the first weight chunk(s), so the prologue runs while weights stream.
+// per pass, a chunk of P passes in flight.  The activation (with its
+// prologue) is complete in LDS before the weights are issued (see the note at
+// the weight issue).
 #include "session_kernels.h"
 
 #include <hip/hip_ext.h>
@@ -140,13 +141,6 @@ __global__ __launch_bounds__(NW * 64) void gemv_q4_0_layer(LayerGemv a) {
       wp[k] = (ok && a.w_post) ? a.w_post[i] : 0.0f;
       wn[k] = ok ? a.w_next[i] : 0.0f;
     }
-    // every wave's prologue loads enter the CU's memory queue before any
-    // wave's weight loads: without this barrier the late waves' small L2 hits
-    // sit behind the early waves' HBM misses (phase trace: +3.7 us)
-    __builtin_amdgcn_s_barrier();
-    load_chunk<P>(ca, qw, dw, 0, total, lane);  // unconditional (valid clamped rows): a
-    // branch here would merge wait counts to vmcnt(0) at the first prologue use
-    if constexpr (MULTI) load_chunk<P>(cb, qw, dw, 64 * P, total, lane);  // both chunks in flight
     float ss = 0.0f;
 #pragma unroll
     for (int k = 0; k < EPT; k++) ss = fmaf(yv[k], yv[k], ss);
@@ -193,9 +187,6 @@ __global__ __launch_bounds__(NW * 64) void gemv_q4_0_layer(LayerGemv a) {
       xr[r][0] = yb[2 * i];
       xr[r][1] = yb[2 * i + 1];
     }
-    __builtin_amdgcn_s_barrier();  // activation loads of all waves ahead of the weight stream
-    load_chunk<P>(ca, qw, dw, 0, total, lane);
-    if constexpr (MULTI) load_chunk<P>(cb, qw, dw, 64 * P, total, lane);
 #pragma unroll
     for (int r = 0; r < E; r++) {
       const int i = t + r * T;
@@ -214,13 +205,17 @@ __global__ __launch_bounds__(NW * 64) void gemv_q4_0_layer(LayerGemv a) {
     uint4 xr[X_LD];
 #pragma unroll
     for (int k = 0; k < X_LD; k++) xr[k] = src[min(t + k * T, n16 - 1)];
-    __builtin_amdgcn_s_barrier();  // activation loads of all waves ahead of the weight stream
-    load_chunk<P>(ca, qw, dw, 0, total, lane);
-    if constexpr (MULTI) load_chunk<P>(cb, qw, dw, 64 * P, total, lane);
 #pragma unroll
     for (int k = 0; k < X_LD; k++) dst[min(t + k * T, n16)] = xr[k];  // slot n16: LDS pad (discarded)
   }
+  // The activation is complete in LDS BEFORE the weight stream is issued.
+  // Issuing weights first does not overlap anything: a CU accepts its waves'
+  // weight loads only as fast as its miss queue drains, so any barrier after
+  // the weight issue (the prologue's reductions, the x hand-off) waits for
+  // most of the CU's weight bytes (phase trace: +2.5-4 us per launch).
   __syncthreads();
+  load_chunk<P>(ca, qw, dw, 0, total, lane);  // unconditional (valid clamped rows)
+  if constexpr (MULTI) load_chunk<P>(cb, qw, dw, 64 * P, total, lane);
 
   LAYER_MARK(4);
   float acc[R];
