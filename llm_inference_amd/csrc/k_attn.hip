@@ -453,6 +453,7 @@ __global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa)
     s_ml[g][cc][e] = ld_sc1(part0 + ((size_t)g * NS + cc) * (HD + 2) + HD + e);
   }
   __syncthreads();
+  ATTN_MARK(6);
   float* s_out = reinterpret_cast<float*>(s_k);  // [G][HD]
   for (int idx = t; idx < G * HD; idx += 256) {
     const int g = idx / HD, d = idx % HD;
@@ -475,6 +476,7 @@ __global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa)
     a.out[((size_t)hkv * G + g) * HD + d] = val;
     s_out[idx] = val;
   }
+  ATTN_MARK(7);
   if (a.q8 != nullptr && HD % 32 == 0) {  // Q8_0 blocks of the heads' outputs (ops.cpp:116-139)
     __syncthreads();
     for (int b = t; b < G * HD / 32; b += 256) q8_block_serial(s_out + 32 * b, a.q8 + (size_t)hkv * G * HD / 32 + b);

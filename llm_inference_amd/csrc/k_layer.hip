@@ -108,7 +108,10 @@ __device__ unsigned long long* g_layer_trace = nullptr;
 
 enum { ROLE_PLAIN = LAYER_PLAIN, ROLE_PRO = LAYER_PRO, ROLE_GELU = LAYER_GELU, ROLE_QUANT = LAYER_QUANT };
 
-template <int R, int NW, int P, int E, int ROLE, bool MULTI>
+// EARLY: issue the weight stream right after the activation loads (small
+// weight slices per CU: the issue stall is short and the latency overlaps);
+// otherwise after the activation is complete in LDS (see the weight issue).
+template <int R, int NW, int P, int E, int ROLE, bool MULTI, bool EARLY>
 __global__ __launch_bounds__(NW * 64) void gemv_q4_0_layer(LayerGemv a) {
   constexpr bool PRO = ROLE == ROLE_PRO || ROLE == ROLE_GELU, GELU = ROLE == ROLE_GELU;
   LAYER_MARK(0);
@@ -127,6 +130,10 @@ __global__ __launch_bounds__(NW * 64) void gemv_q4_0_layer(LayerGemv a) {
   const uint16_t* dw = a.wd + (size_t)min(row0, a.rows - 1) * nb;
 
   Chunk<P> ca, cb;
+  auto issue_weights = [&]() {
+    load_chunk<P>(ca, qw, dw, 0, total, lane);  // unconditional (valid clamped rows)
+    if constexpr (MULTI) load_chunk<P>(cb, qw, dw, 64 * P, total, lane);
+  };
   if constexpr (PRO) {
     // prologue operands first: loads return in issue order, so issuing them
     // ahead of the weight chunk lets the norm run while the weights stream
@@ -141,6 +148,7 @@ __global__ __launch_bounds__(NW * 64) void gemv_q4_0_layer(LayerGemv a) {
       wp[k] = (ok && a.w_post) ? a.w_post[i] : 0.0f;
       wn[k] = ok ? a.w_next[i] : 0.0f;
     }
+    if constexpr (EARLY) issue_weights();
     float ss = 0.0f;
 #pragma unroll
     for (int k = 0; k < EPT; k++) ss = fmaf(yv[k], yv[k], ss);
@@ -187,6 +195,7 @@ __global__ __launch_bounds__(NW * 64) void gemv_q4_0_layer(LayerGemv a) {
       xr[r][0] = yb[2 * i];
       xr[r][1] = yb[2 * i + 1];
     }
+    if constexpr (EARLY) issue_weights();
 #pragma unroll
     for (int r = 0; r < E; r++) {
       const int i = t + r * T;
@@ -205,6 +214,7 @@ __global__ __launch_bounds__(NW * 64) void gemv_q4_0_layer(LayerGemv a) {
     uint4 xr[X_LD];
 #pragma unroll
     for (int k = 0; k < X_LD; k++) xr[k] = src[min(t + k * T, n16 - 1)];
+    if constexpr (EARLY) issue_weights();
 #pragma unroll
     for (int k = 0; k < X_LD; k++) dst[min(t + k * T, n16)] = xr[k];  // slot n16: LDS pad (discarded)
   }
@@ -214,8 +224,7 @@ __global__ __launch_bounds__(NW * 64) void gemv_q4_0_layer(LayerGemv a) {
   // the weight issue (the prologue's reductions, the x hand-off) waits for
   // most of the CU's weight bytes (phase trace: +2.5-4 us per launch).
   __syncthreads();
-  load_chunk<P>(ca, qw, dw, 0, total, lane);  // unconditional (valid clamped rows)
-  if constexpr (MULTI) load_chunk<P>(cb, qw, dw, 64 * P, total, lane);
+  if constexpr (!EARLY) issue_weights();
 
   LAYER_MARK(4);
   float acc[R];
@@ -262,22 +271,22 @@ __global__ __launch_bounds__(NW * 64) void gemv_q4_0_layer(LayerGemv a) {
 // Geometry aims at ~256 work-groups (one per CU) so per-work-group prologue
 // work is done once per CU and every CU streams the same bytes:
 //   R: rows per wave, NW: waves per work-group, P: passes (64 items) per
-//   chunk, MULTI: more than one chunk per wave,
+//   chunk, MULTI: more than one chunk per wave, EARLY: see the kernel,
 //   E: PLAIN -- 16-B x loads per thread (ceil(3 nb / 64 NW));
 //      PRO/GELU -- prologue elements per thread (ceil(32 nb / 64 NW));
 //      QUANT -- rounds of 8-float quad lanes (ceil(4 nb / 64 NW)).
 using LaunchFn = void (*)(dim3, size_t, const LayerGemv&, hipStream_t);
 
-template <int R, int NW, int P, int E, int ROLE, bool MULTI>
+template <int R, int NW, int P, int E, int ROLE, bool MULTI, bool EARLY>
 void launch_cfg(dim3 grid, size_t lds, const LayerGemv& a, hipStream_t s) {
   KernelTiming& kt = kernel_timing();
   if (kt.start) {
-    hipExtLaunchKernelGGL((gemv_q4_0_layer<R, NW, P, E, ROLE, MULTI>), grid, dim3(NW * 64), (uint32_t)lds, s, kt.start,
-                          kt.stop, 0u, a);
+    hipExtLaunchKernelGGL((gemv_q4_0_layer<R, NW, P, E, ROLE, MULTI, EARLY>), grid, dim3(NW * 64), (uint32_t)lds, s,
+                          kt.start, kt.stop, 0u, a);
     kt = KernelTiming{};
     return;
   }
-  hipLaunchKernelGGL((gemv_q4_0_layer<R, NW, P, E, ROLE, MULTI>), grid, dim3(NW * 64), lds, s, a);
+  hipLaunchKernelGGL((gemv_q4_0_layer<R, NW, P, E, ROLE, MULTI, EARLY>), grid, dim3(NW * 64), lds, s, a);
 }
 
 struct LayerCfg {
@@ -286,31 +295,32 @@ struct LayerCfg {
   LaunchFn fn;
 };
 
-#define LLMI_LCFG(NB, ROLE, R, NW, P, E, MULTI) {NB, ROLE, R, NW, P, E, MULTI, launch_cfg<R, NW, P, E, ROLE, MULTI>}
+#define LLMI_LCFG(NB, ROLE, R, NW, P, E, MULTI, EARLY) \
+  {NB, ROLE, R, NW, P, E, MULTI, launch_cfg<R, NW, P, E, ROLE, MULTI, EARLY>}
 const LayerCfg kLayerCfgs[] = {
     // PLAIN: x blocks copied to LDS
-    LLMI_LCFG(32, ROLE_PLAIN, 2, 2, 1, 1, false),     // 1B o        1152 rows -> 288 WGs
-    LLMI_LCFG(36, ROLE_PLAIN, 8, 1, 5, 2, false),     // 1B qkv l0   1536 rows -> 192 WGs
-    LLMI_LCFG(64, ROLE_PLAIN, 1, 10, 1, 1, false),    // 4B o        2560 rows -> 256 WGs
-    LLMI_LCFG(80, ROLE_PLAIN, 4, 4, 5, 1, false),     // 4B qkv l0   4096 rows -> 256 WGs
-    LLMI_LCFG(120, ROLE_PLAIN, 8, 4, 8, 2, true),     // 12B qkv l0  8192 rows -> 256 WGs
-    LLMI_LCFG(128, ROLE_PLAIN, 1, 15, 2, 1, false),   // 12B/27B o   3840/5376 rows -> 256/359 WGs
-    LLMI_LCFG(168, ROLE_PLAIN, 8, 4, 7, 2, true),     // 27B qkv l0  8192 rows -> 256 WGs
+    LLMI_LCFG(32, ROLE_PLAIN, 2, 2, 1, 1, false, true),     // 1B o        1152 rows -> 288 WGs
+    LLMI_LCFG(36, ROLE_PLAIN, 8, 1, 5, 2, false, true),     // 1B qkv l0   1536 rows -> 192 WGs
+    LLMI_LCFG(64, ROLE_PLAIN, 1, 10, 1, 1, false, true),    // 4B o        2560 rows -> 256 WGs
+    LLMI_LCFG(80, ROLE_PLAIN, 4, 4, 5, 1, false, true),     // 4B qkv l0   4096 rows -> 256 WGs
+    LLMI_LCFG(120, ROLE_PLAIN, 8, 4, 8, 2, true, true),     // 12B qkv l0  8192 rows -> 256 WGs
+    LLMI_LCFG(128, ROLE_PLAIN, 1, 15, 2, 1, false, true),   // 12B/27B o   3840/5376 rows -> 256/359 WGs
+    LLMI_LCFG(168, ROLE_PLAIN, 8, 4, 7, 2, true, true),     // 27B qkv l0  8192 rows -> 256 WGs
     // PRO: residual + norm prologue
-    LLMI_LCFG(36, ROLE_PRO, 8, 2, 5, 9, false),       // 1B qkv      96 WGs
-    LLMI_LCFG(80, ROLE_PRO, 4, 4, 5, 10, false),      // 4B qkv      256 WGs
-    LLMI_LCFG(120, ROLE_PRO, 8, 4, 8, 15, true),      // 12B qkv     256 WGs
-    LLMI_LCFG(168, ROLE_PRO, 4, 8, 6, 11, true),      // 27B qkv     256 WGs
+    LLMI_LCFG(36, ROLE_PRO, 8, 2, 5, 9, false, true),       // 1B qkv      96 WGs
+    LLMI_LCFG(80, ROLE_PRO, 4, 4, 5, 10, false, true),      // 4B qkv      256 WGs
+    LLMI_LCFG(120, ROLE_PRO, 8, 4, 8, 15, true, true),      // 12B qkv     256 WGs
+    LLMI_LCFG(168, ROLE_PRO, 4, 8, 6, 11, true, true),      // 27B qkv     256 WGs
     // GELU: prologue + GELU epilogue, 2H = R NW interleaved gate/up rows per WG
-    LLMI_LCFG(36, ROLE_GELU, 6, 9, 4, 2, false),      // 1B  13824 rows, H 27 -> 256 WGs
-    LLMI_LCFG(80, ROLE_GELU, 5, 16, 7, 3, false),     // 4B  20480 rows, H 40 -> 256 WGs
-    LLMI_LCFG(120, ROLE_GELU, 8, 15, 8, 4, true),     // 12B 30720 rows, H 60 -> 256 WGs
-    LLMI_LCFG(168, ROLE_GELU, 12, 14, 8, 6, true),    // 27B 43008 rows, H 84 -> 256 WGs
+    LLMI_LCFG(36, ROLE_GELU, 6, 9, 4, 2, false, false),      // 1B  13824 rows, H 27 -> 256 WGs
+    LLMI_LCFG(80, ROLE_GELU, 5, 16, 7, 3, false, false),     // 4B  20480 rows, H 40 -> 256 WGs
+    LLMI_LCFG(120, ROLE_GELU, 8, 15, 8, 4, true, false),     // 12B 30720 rows, H 60 -> 256 WGs
+    LLMI_LCFG(168, ROLE_GELU, 12, 14, 8, 6, true, false),    // 27B 43008 rows, H 84 -> 256 WGs
     // QUANT: f32 activation quantized into LDS (down projection)
-    LLMI_LCFG(216, ROLE_QUANT, 2, 2, 7, 7, false),    // 1B down     1152 rows -> 288 WGs
-    LLMI_LCFG(320, ROLE_QUANT, 1, 10, 5, 2, false),   // 4B down     2560 rows -> 256 WGs
-    LLMI_LCFG(480, ROLE_QUANT, 1, 15, 8, 2, false),   // 12B down    3840 rows -> 256 WGs
-    LLMI_LCFG(672, ROLE_QUANT, 1, 16, 6, 3, true),    // 27B down    5376 rows -> 336 WGs
+    LLMI_LCFG(216, ROLE_QUANT, 2, 2, 7, 7, false, true),    // 1B down     1152 rows -> 288 WGs
+    LLMI_LCFG(320, ROLE_QUANT, 1, 10, 5, 2, false, true),   // 4B down     2560 rows -> 256 WGs
+    LLMI_LCFG(480, ROLE_QUANT, 1, 15, 8, 2, false, true),   // 12B down    3840 rows -> 256 WGs
+    LLMI_LCFG(672, ROLE_QUANT, 1, 16, 6, 3, true, true),    // 27B down    5376 rows -> 336 WGs
 };
 #undef LLMI_LCFG
 

@@ -123,11 +123,11 @@ int main(int argc, char** argv) {
     unsigned long long t0 = ~0ull;
     for (size_t b = 0; b < h.size() / 8; b++) t0 = std::min(t0, h[b * 8]);
     printf("pos %d: per work-group phase times in us from the first work-group start\n", pos);
-    printf("  wg(hkv,c)  start  prolog  tile1  loopend ticket merged\n");
+    printf("  wg(hkv,c)  start  prolog  tile1  loopend ticket merged  ml_in  v_done\n");
     for (size_t b = 0; b < h.size() / 8; b++) {
-      if ((b % ATTN_NSPLIT) > 12 && (b % ATTN_NSPLIT) != ATTN_NSPLIT - 1) continue;
+      if ((b % ATTN_NSPLIT) > 12 && (b % ATTN_NSPLIT) != ATTN_NSPLIT - 1 && !h[b * 8 + 5]) continue;
       printf("  (%d,%2d)", (int)(b / ATTN_NSPLIT), (int)(b % ATTN_NSPLIT));
-      for (int ph = 0; ph < 6; ph++)
+      for (int ph = 0; ph < 8; ph++)
         printf(" %7.2f", h[b * 8 + ph] ? (h[b * 8 + ph] - t0) / 100.0 : -1.0);
       printf("\n");
     }

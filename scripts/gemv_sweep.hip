@@ -231,17 +231,17 @@ int main(int argc, char** argv) {
       });
     };
     if (nb % 64 == 0) {
-      geo("plain R1 NW4 P1", gemv_q4_0_layer<1, 4, 1, 4, 0, true>, 4, 256);
-      geo("plain R1 NW8 P1", gemv_q4_0_layer<1, 8, 1, 4, 0, true>, 8, 512);
+      geo("plain R1 NW4 P1", gemv_q4_0_layer<1, 4, 1, 4, 0, true, true>, 4, 256);
+      geo("plain R1 NW8 P1", gemv_q4_0_layer<1, 8, 1, 4, 0, true, true>, 8, 512);
     }
     if ((4 * nb) % 64 == 0) {
-      geo("plain R4 NW4 P5", gemv_q4_0_layer<4, 4, 5, 4, 0, true>, 16, 256);
-      geo("plain R4 NW2 P5", gemv_q4_0_layer<4, 2, 5, 4, 0, true>, 8, 128);
-      geo("plain R4 NW1 P5", gemv_q4_0_layer<4, 1, 5, 4, 0, true>, 4, 64);
-      geo("plain R4 NW8 P5", gemv_q4_0_layer<4, 8, 5, 4, 0, true>, 32, 512);
+      geo("plain R4 NW4 P5", gemv_q4_0_layer<4, 4, 5, 4, 0, true, true>, 16, 256);
+      geo("plain R4 NW2 P5", gemv_q4_0_layer<4, 2, 5, 4, 0, true, true>, 8, 128);
+      geo("plain R4 NW1 P5", gemv_q4_0_layer<4, 1, 5, 4, 0, true, true>, 4, 64);
+      geo("plain R4 NW8 P5", gemv_q4_0_layer<4, 8, 5, 4, 0, true, true>, 32, 512);
     }
-    geo("plain R8 NW4 P5", gemv_q4_0_layer<8, 4, 5, 4, 0, true>, 32, 256);
-    geo("plain R2 NW4 P5", gemv_q4_0_layer<2, 4, 5, 4, 0, true>, 8, 256);
+    geo("plain R8 NW4 P5", gemv_q4_0_layer<8, 4, 5, 4, 0, true, true>, 32, 256);
+    geo("plain R2 NW4 P5", gemv_q4_0_layer<2, 4, 5, 4, 0, true, true>, 8, 256);
     for (auto& w : ws) {
       (void)hipFree(w.qs);
       (void)hipFree(w.d);
