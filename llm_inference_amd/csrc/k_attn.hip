@@ -291,9 +291,6 @@ __global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa)
     }
   }
   int tile = c;
-  // every wave's q/k/v row loads enter the CU's memory queue ahead of the
-  // K/V tile (HBM) loads, so the prologue is not stuck behind the tile misses
-  __builtin_amdgcn_s_barrier();
   load_tile(tile);
   if (FUSED) {
     const bool ok = lane * DPL < HD;
@@ -448,38 +445,69 @@ __global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa)
   if (!s_last) return;
 
   // ---- last work-group: merge the NS partials of the G heads -------------
-  for (int i = t; i < G * NS * 2; i += 256) {
-    const int g = i / (NS * 2), cc = (i / 2) % NS, e = i & 1;
-    s_ml[g][cc][e] = ld_sc1(part0 + ((size_t)g * NS + cc) * (HD + 2) + HD + e);
+  // One batch of loads: every thread's partial accumulators for its (g, d)
+  // outputs and the (m, l) pairs; the per-split weights are computed once per
+  // (g, split) instead of per output.  Arithmetic (and order) as before:
+  // w_c = l_c ? exp(m_c - M) : 0, L = sum_c fma(l_c, w_c), o = sum_c fma(v_c, w_c).
+  constexpr int PAIRS = (G * HD + 255) / 256;
+  float v[PAIRS][NS];
+#pragma unroll
+  for (int p = 0; p < PAIRS; p++) {
+    const int idx = min(t + p * 256, G * HD - 1);
+    const float* pg = part0 + (size_t)(idx / HD) * NS * (HD + 2) + idx % HD;
+#pragma unroll
+    for (int cc = 0; cc < NS; cc++) v[p][cc] = ld_sc1(pg + (size_t)cc * (HD + 2));
+  }
+  float mv = 0.0f, lv = 0.0f;
+  if (t < G * NS) {
+    const float* pm = part0 + ((size_t)(t / NS) * NS + t % NS) * (HD + 2) + HD;
+    mv = ld_sc1(pm);
+    lv = ld_sc1(pm + 1);
+  }
+  __shared__ float s_wt[G][NS];
+  __shared__ float s_L[G];
+  if (t < G * NS) {
+    s_ml[t / NS][t % NS][0] = mv;
+    s_ml[t / NS][t % NS][1] = lv;
   }
   __syncthreads();
   ATTN_MARK(6);
-  float* s_out = reinterpret_cast<float*>(s_k);  // [G][HD]
-  for (int idx = t; idx < G * HD; idx += 256) {
-    const int g = idx / HD, d = idx % HD;
-    const float* pg = part0 + (size_t)g * NS * (HD + 2) + d;
-    float v[NS];
-#pragma unroll
-    for (int cc = 0; cc < NS; cc++) v[cc] = ld_sc1(pg + (size_t)cc * (HD + 2));
+  if (t < G * NS) {
+    const int g = t / NS;
     float M = -INFINITY;
 #pragma unroll
     for (int cc = 0; cc < NS; cc++) M = fmaxf(M, s_ml[g][cc][0]);
-    float L = 0.0f, o = 0.0f;
+    s_wt[g][t % NS] = lv == 0.0f ? 0.0f : expf(mv - M);
+  }
+  __syncthreads();
+  if (t < G) {
+    float L = 0.0f;
+    for (int cc = 0; cc < NS; cc++) L = fmaf(s_ml[t][cc][1], s_wt[t][cc], L);
+    s_L[t] = L;
+  }
+  __syncthreads();
+  float* s_out = reinterpret_cast<float*>(s_k);  // [G][HD]
 #pragma unroll
-    for (int cc = 0; cc < NS; cc++) {
-      const float l = s_ml[g][cc][1];
-      const float wc = l == 0.0f ? 0.0f : expf(s_ml[g][cc][0] - M);
-      L = fmaf(l, wc, L);
-      o = fmaf(v[cc], wc, o);
+  for (int p = 0; p < PAIRS; p++) {
+    const int idx = t + p * 256;
+    if (idx < G * HD) {
+      const int g = idx / HD;
+      float o = 0.0f;
+#pragma unroll
+      for (int cc = 0; cc < NS; cc++) o = fmaf(v[p][cc], s_wt[g][cc], o);
+      const float val = o / s_L[g];
+      a.out[(size_t)hkv * G * HD + idx] = val;
+      s_out[idx] = val;
     }
-    const float val = o / L;
-    a.out[((size_t)hkv * G + g) * HD + d] = val;
-    s_out[idx] = val;
   }
   ATTN_MARK(7);
-  if (a.q8 != nullptr && HD % 32 == 0) {  // Q8_0 blocks of the heads' outputs (ops.cpp:116-139)
+  if (a.q8 != nullptr && HD % 32 == 0) {  // Q8_0 blocks of the heads' outputs (ops.cpp:116-139), 4 lanes per block
     __syncthreads();
-    for (int b = t; b < G * HD / 32; b += 256) q8_block_serial(s_out + 32 * b, a.q8 + (size_t)hkv * G * HD / 32 + b);
+    for (int i = t; i < G * HD / 8; i += 256) {
+      const float4 f0 = reinterpret_cast<const float4*>(s_out)[2 * i], f1 = reinterpret_cast<const float4*>(s_out)[2 * i + 1];
+      const float vv[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+      q8_block_quad(vv, i & 3, a.q8 + (size_t)hkv * G * HD / 32 + (i >> 2));
+    }
   }
   ATTN_MARK(5);
   if (t == 0) __hip_atomic_store(a.ticket + hkv, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
