@@ -52,6 +52,17 @@ __global__ __launch_bounds__(256) void stream_kernel(const uint4* __restrict__ q
   if (acc == 0x12345678u) out[0] = 1.0f;
 }
 
+// default-policy (allocating) read of a weight's qs and d: warms the MALL
+__global__ __launch_bounds__(256) void prefetch_kernel(const uint4* __restrict__ q, size_t n16,
+                                                       const uint4* __restrict__ d, size_t nd16, float* out) {
+  uint32_t acc = 0;
+  for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < n16 + nd16; i += (size_t)gridDim.x * 256) {
+    const uint4 v = i < n16 ? q[i] : d[i - n16];
+    acc ^= v.x ^ v.y ^ v.z ^ v.w;
+  }
+  if (acc == 0x12345678u) out[0] = 1.0f;
+}
+
 struct Shape {
   const char* name;
   int rows, cols;
@@ -175,6 +186,21 @@ int main(int argc, char** argv) {
     qz.out = out;
     if (layer_gemv_supported(probe, LAYER_QUANT))
       timeit("layer quant", [&](const DevWeight& w) { launch_layer_gemv(w, qz, LAYER_QUANT, s); });
+    // MALL experiment: a default-policy prefetch of the same weight right
+    // before the GEMV (as a forked graph branch would do during attention)
+    {
+      auto pre = [&](const DevWeight& w) {
+        hipLaunchKernelGGL(prefetch_kernel, dim3(512), dim3(256), 0, s, (const uint4*)w.qs, (size_t)sh.rows * nb,
+                           (const uint4*)w.d, (size_t)sh.rows * nb * 2 / 16, out);
+      };
+      timeit("prefetch only", pre);
+      if (layer_gemv_supported(probe, LAYER_PLAIN))
+        timeit("prefetch + layer plain", [&](const DevWeight& w) { pre(w); launch_layer_gemv(w, plain, LAYER_PLAIN, s); });
+      if (layer_gemv_supported(probe, LAYER_GELU))
+        timeit("prefetch + layer gelu", [&](const DevWeight& w) { pre(w); launch_layer_gemv(w, gl, LAYER_GELU, s); });
+      if (layer_gemv_supported(probe, LAYER_QUANT))
+        timeit("prefetch + layer quant", [&](const DevWeight& w) { pre(w); launch_layer_gemv(w, qz, LAYER_QUANT, s); });
+    }
     // phase trace of one launch per role (100 MHz ticks, from the first WG start)
     {
       unsigned long long* tr;
