@@ -13,9 +13,11 @@
 #include <vector>
 
 using namespace llmi;
+#ifdef LLMI_LAYER_TRACE
 namespace llmi {
 void layer_set_trace(unsigned long long* p);
 }
+#endif
 
 namespace {
 
@@ -201,6 +203,7 @@ int main(int argc, char** argv) {
       if (layer_gemv_supported(probe, LAYER_QUANT))
         timeit("prefetch + layer quant", [&](const DevWeight& w) { pre(w); launch_layer_gemv(w, qz, LAYER_QUANT, s); });
     }
+#ifdef LLMI_LAYER_TRACE
     // phase trace of one launch per role (100 MHz ticks, from the first WG start)
     {
       unsigned long long* tr;
@@ -241,6 +244,7 @@ int main(int argc, char** argv) {
       if (layer_gemv_supported(probe, LAYER_QUANT)) trace("quant", [&](const DevWeight& w) { launch_layer_gemv(w, qz, LAYER_QUANT, s); });
       (void)hipFree(tr);
     }
+#endif
     // geometry variants of the plain kernel
     const uint32_t mg = div_magic(nb);
     auto geo = [&](const char* label, auto kern, int rows_per_wg, int threads) {
