@@ -304,7 +304,7 @@ const LayerCfg kLayerCfgs[] = {
     LLMI_LCFG(64, ROLE_PLAIN, 1, 10, 1, 1, false, true),    // 4B o        2560 rows -> 256 WGs
     LLMI_LCFG(80, ROLE_PLAIN, 4, 4, 5, 1, false, true),     // 4B qkv l0   4096 rows -> 256 WGs
     LLMI_LCFG(120, ROLE_PLAIN, 8, 4, 8, 2, true, true),     // 12B qkv l0  8192 rows -> 256 WGs
-    LLMI_LCFG(128, ROLE_PLAIN, 1, 15, 2, 1, false, true),   // 12B/27B o   3840/5376 rows -> 256/359 WGs
+    LLMI_LCFG(128, ROLE_PLAIN, 1, 8, 2, 1, false, true),    // 12B/27B o   3840/5376 rows -> 480/672 WGs
     LLMI_LCFG(168, ROLE_PLAIN, 8, 4, 7, 2, true, true),     // 27B qkv l0  8192 rows -> 256 WGs
     // PRO: residual + norm prologue
     LLMI_LCFG(36, ROLE_PRO, 8, 2, 5, 9, false, true),       // 1B qkv      96 WGs
@@ -314,13 +314,13 @@ const LayerCfg kLayerCfgs[] = {
     // GELU: prologue + GELU epilogue, 2H = R NW interleaved gate/up rows per WG
     LLMI_LCFG(36, ROLE_GELU, 6, 9, 4, 2, false, false),      // 1B  13824 rows, H 27 -> 256 WGs
     LLMI_LCFG(80, ROLE_GELU, 5, 16, 7, 3, false, false),     // 4B  20480 rows, H 40 -> 256 WGs
-    LLMI_LCFG(120, ROLE_GELU, 8, 15, 8, 4, true, false),     // 12B 30720 rows, H 60 -> 256 WGs
-    LLMI_LCFG(168, ROLE_GELU, 12, 14, 8, 6, true, false),    // 27B 43008 rows, H 84 -> 256 WGs
+    LLMI_LCFG(120, ROLE_GELU, 8, 8, 8, 8, true, false),      // 12B 30720 rows, H 32 -> 480 WGs
+    LLMI_LCFG(168, ROLE_GELU, 8, 8, 7, 11, true, false),     // 27B 43008 rows, H 32 -> 672 WGs
     // QUANT: f32 activation quantized into LDS (down projection)
     LLMI_LCFG(216, ROLE_QUANT, 2, 2, 7, 7, false, true),    // 1B down     1152 rows -> 288 WGs
     LLMI_LCFG(320, ROLE_QUANT, 1, 10, 5, 2, false, true),   // 4B down     2560 rows -> 256 WGs
-    LLMI_LCFG(480, ROLE_QUANT, 1, 15, 8, 2, false, true),   // 12B down    3840 rows -> 256 WGs
-    LLMI_LCFG(672, ROLE_QUANT, 1, 16, 6, 3, true, true),    // 27B down    5376 rows -> 336 WGs
+    LLMI_LCFG(480, ROLE_QUANT, 1, 8, 8, 4, false, true),    // 12B down    3840 rows -> 480 WGs
+    LLMI_LCFG(672, ROLE_QUANT, 1, 8, 6, 6, true, true),     // 27B down    5376 rows -> 672 WGs
 };
 #undef LLMI_LCFG
 
