@@ -10,9 +10,12 @@ one hipGraph replay per token, the token fed back on the device.
 Weights: random-init with the exact gemma-3-4b-it-q4_0 architecture (no
 checkpoints offline); prompt: seeded synthetic token ids.
 
-Single process per GPU.  With --gpus N (torchrun) every rank decodes its own
-independent stream (replicas; tensor-parallel row sharding is DESIGN.md
-section 8's next step), barrier + max-over-ranks timing, value = total tok/s.
+Single process per GPU.  With --gpus N (torchrun) the default is the north
+star's row-sharded decode: ONE greedy stream, each rank holding 1/N of every
+projection's output rows, slices all-gathered over RCCL after each projection
+(include/llmi.h tp_*; "scaling": "strong", value = that stream's tok/s).
+--mode replicas instead decodes N independent streams (value = total tok/s,
+"scaling": "weak").  Barrier + max-over-ranks timing either way.
 """
 from __future__ import annotations
 
@@ -42,6 +45,8 @@ def parse():
     p.add_argument("--cpu-decode", type=int, default=24, help="decode tokens in the CPU baseline sample")
     p.add_argument("--kernel-reps", type=int, default=2)
     p.add_argument("--no-graph", action="store_true", help="eager launches (for kernel tracers)")
+    p.add_argument("--mode", choices=["tp", "replicas"], default="tp",
+                   help="N>1: row-sharded tensor parallel (one stream) or independent replicas")
     return p.parse_args()
 
 
@@ -72,6 +77,14 @@ class Dist:
     def barrier(self):
         if self.world > 1:
             self.dist.barrier()
+
+    def broadcast(self, obj):
+        """rank 0's object on every rank (the RCCL unique id)."""
+        if self.world == 1:
+            return obj
+        box = [obj]
+        self.dist.broadcast_object_list(box, src=0)
+        return box[0]
 
     def max(self, v: float) -> float:
         if self.world == 1:
@@ -115,17 +128,22 @@ def main():
     # load the HIP library before anything could pull in torch's HIP runtime
     from llm_inference_amd import _lib
     _lib.lib()
-    from llm_inference_amd.model import Model
+    from llm_inference_amd.model import Model, tp_unique_id
     from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
+    tp = d.world > 1 and a.mode == "tp"
 
     cfg = CONFIGS[a.config]
     t0 = time.time()
     g = build_gemma3_gguf(cfg, seed=1234)
     t_build = time.time() - t0
     max_ctx = a.prefill + a.warmup + a.steps + 8
-    m = Model(g, device=d.local if a.gpus > 1 else 0, exact=a.exact, max_ctx=max_ctx, use_graph=not a.no_graph)
+    tp_kw = {}
+    if tp:  # one RCCL communicator over the node's GPUs
+        tp_kw = dict(tp_rank=d.rank, tp_size=d.world, tp_id=d.broadcast(tp_unique_id() if d.rank == 0 else None))
+    m = Model(g, device=d.local if a.gpus > 1 else 0, exact=a.exact, max_ctx=max_ctx, use_graph=not a.no_graph,
+              **tp_kw)
     info = m.info
-    rng = np.random.default_rng(99 + d.rank)
+    rng = np.random.default_rng(99 + (0 if tp else d.rank))  # tensor-parallel ranks decode the same stream
     prompt = np.concatenate([[2], rng.integers(4, cfg.vocab, a.prefill - 1)]).astype(np.int32)
     t0 = time.time()
     m.forward(prompt, 0, want_logits=False)
@@ -145,7 +163,7 @@ def main():
     d.barrier()
     el = d.max(el)
     info = m.get_info()  # kernels_per_token is known once the step graph exists
-    value = a.steps * d.world / el
+    value = a.steps * (1 if tp else d.world) / el
     ms = el * 1000.0 / a.steps
 
     # dominant kernel: the Q4_0 GEMV family (weights swept in decode order, HIP events)
@@ -164,20 +182,22 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": round(ms, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if tp else "weak",
         "vs_baseline": None,
         "dtype": "q4_0 x q8_0 int8-dot, fp32 accumulate; f16 logits",
         "data": "synthetic (random-init weights of the gemma-3-4b-it-q4_0 architecture, seeded prompt ids)",
         "config": {
             "workload": f"{cfg.name}-q4_0 greedy decode after a {a.prefill}-token prefill (BASELINE configs[2])",
             "prefill_tokens": a.prefill, "decode_tokens": a.steps, "mode": "exact" if a.exact else "fast",
-            "parallelism": f"replicas{d.world}" if d.world > 1 else "single",
+            "parallelism": (f"tp{d.world} (row-sharded, RCCL all-gather)" if tp else f"replicas{d.world}")
+                           if d.world > 1 else "single",
             "kernels_per_token": info.kernels_per_token,
         },
         "hbm": {
             "bytes_per_token": int(tok_bytes),
-            "achieved_GBps": round(tok_bytes * value / d.world / 1e9, 1),
-            "frac_of_peak": round(tok_bytes * value / d.world / 1e9 / PEAK_HBM_GBS, 4),
+            # per GPU: this rank's bytes of one token x tokens/s of its stream
+            "achieved_GBps": round(tok_bytes * value / (1 if tp else d.world) / 1e9, 1),
+            "frac_of_peak": round(tok_bytes * value / (1 if tp else d.world) / 1e9 / PEAK_HBM_GBS, 4),
         },
         "roofline": {
             "kernel": "Q4_0 projection GEMVs of one token in decode order (gemv_q4_0_layer on the fast path: qkv, o, gate_up+GELU, down)",

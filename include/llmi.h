@@ -102,13 +102,31 @@ int llmi_gelu_mul(const float* gate, const float* up, size_t n, float* out);
  * (2) device session (Gemma-3 GGUF)
  * ------------------------------------------------------------------------- */
 typedef struct llmi_session llmi_session;
+typedef struct llmi_tp_group llmi_tp_group;
 
 typedef struct {
   int device;          /* HIP device ordinal */
   uint32_t flags;      /* LLMI_EXACT | LLMI_NO_GRAPH */
   int max_ctx;         /* KV-cache capacity in positions (default 4096) */
   int attn_split;      /* fast attention key-range splits: 0 = default (32, the only value) */
+  /* Row-sharded tensor parallelism (north star: "weights shard row-wise across
+   * the 8 GPUs of one node with an RCCL all-gather"; the reference itself is
+   * single-device).  Active when tp_id or tp_group is non-NULL: this session
+   * is rank tp_rank of tp_size and holds 1/tp_size of every projection's
+   * output rows (q/k/v heads, o/down rows, gate/up hidden units, vocabulary
+   * rows); after each projection the slices are all-gathered.  Fast kernels
+   * only (not with LLMI_EXACT).  Every rank must make the same session calls. */
+  int tp_rank, tp_size;
+  const void* tp_id;        /* LLMI_TP_ID_BYTES from llmi_tp_unique_id on one rank: RCCL over xGMI */
+  llmi_tp_group* tp_group;  /* or: ranks on one device in one process (tests; one host thread per rank) */
 } llmi_session_opts;
+
+#define LLMI_TP_ID_BYTES 128
+/* new RCCL communicator id (ncclGetUniqueId); distribute it to every rank */
+int llmi_tp_unique_id(void* out);
+/* single-device group of `size` ranks: device-to-device slice copies */
+int llmi_tp_group_create(int size, llmi_tp_group** out);
+void llmi_tp_group_destroy(llmi_tp_group* g);
 
 /* Parses the GGUF (format of gguf.cpp:274-304, hparams of model.cpp:58-167)
  * and uploads every weight.  The bytes are only read during the call. */
@@ -137,6 +155,7 @@ typedef struct {
   size_t bytes_per_token;     /* algorithmic HBM bytes of one decode token, KV excluded */
   size_t kv_bytes_per_pos;    /* + this many bytes per attended position */
   int kernels_per_token;      /* launches captured in the decode graph */
+  int tp_rank, tp_size;       /* weight_bytes / bytes_per_token / kv_bytes_per_pos are this rank's */
 } llmi_session_info;
 int llmi_session_get_info(const llmi_session* s, llmi_session_info* info);
 

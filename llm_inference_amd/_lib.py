@@ -29,15 +29,20 @@ class LLMIError(RuntimeError):
         self.status = STATUS.get(code, str(code))
 
 
+TP_ID_BYTES = 128
+
+
 class SessionOpts(C.Structure):
-    _fields_ = [("device", C.c_int), ("flags", C.c_uint32), ("max_ctx", C.c_int), ("attn_split", C.c_int)]
+    _fields_ = [("device", C.c_int), ("flags", C.c_uint32), ("max_ctx", C.c_int), ("attn_split", C.c_int),
+                ("tp_rank", C.c_int), ("tp_size", C.c_int), ("tp_id", C.c_void_p), ("tp_group", C.c_void_p)]
 
 
 class SessionInfo(C.Structure):
     _fields_ = [("n_layer", C.c_int), ("n_embd", C.c_int), ("n_ff", C.c_int), ("n_head", C.c_int),
                 ("n_head_kv", C.c_int), ("head_dim", C.c_int), ("vocab", C.c_int), ("max_ctx", C.c_int),
                 ("weight_bytes", C.c_size_t), ("bytes_per_token", C.c_size_t),
-                ("kv_bytes_per_pos", C.c_size_t), ("kernels_per_token", C.c_int)]
+                ("kv_bytes_per_pos", C.c_size_t), ("kernels_per_token", C.c_int),
+                ("tp_rank", C.c_int), ("tp_size", C.c_int)]
 
 
 _lib = None
@@ -65,6 +70,9 @@ _SIGS = {
     "llmi_gelu_mul": (C.c_int, [_vp, _vp, _sz, _vp]),
     "llmi_session_create":(C.c_int, [_vp, _sz, C.POINTER(SessionOpts), C.POINTER(_vp)]),
     "llmi_session_destroy": (None, [_vp]),
+    "llmi_tp_unique_id": (C.c_int, [_vp]),
+    "llmi_tp_group_create": (C.c_int, [C.c_int, C.POINTER(_vp)]),
+    "llmi_tp_group_destroy": (None, [_vp]),
     "llmi_session_forward": (C.c_int, [_vp, _vp, C.c_int, C.c_int, _vp, _vp]),
     "llmi_session_generate": (C.c_int, [_vp, _i32, C.c_int, C.c_int, _vp]),
     "llmi_session_enqueue": (C.c_int, [_vp, _i32, C.c_int, C.c_int]),

@@ -18,8 +18,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OBJ = os.path.join(HERE, "_build")
 LIB = os.path.join(HERE, "libllmi.so")
-SOURCES = ["k_gemv.hip", "k_layer.hip", "k_elem.hip", "k_attn.hip", "k_session.hip", "session.cpp", "capi.cpp"]
-HEADERS = ["common.h", "kernels.h", "attn.h", "session_kernels.h", "session.h", "gguf_reader.h"]
+SOURCES = ["k_gemv.hip", "k_layer.hip", "k_elem.hip", "k_attn.hip", "k_session.hip", "session.cpp", "collective.cpp", "capi.cpp"]
+HEADERS = ["common.h", "kernels.h", "attn.h", "session_kernels.h", "session.h", "gguf_reader.h", "collective.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "--offload-arch=gfx950", "-Wall",
          "-Wno-unused-function", "-Wno-unused-variable", "-Wno-unused-result"]
@@ -52,7 +52,8 @@ def build(force: bool = False, jobs: int = 0) -> str:
             list(ex.map(_compile, todo))
     objs = [os.path.join(OBJ, os.path.splitext(s)[0] + ".o") for s in SOURCES]
     if force or todo or _mtime(LIB) < max(_mtime(o) for o in objs):
-        cmd = [HIPCC, "-shared", "-fPIC", "--offload-arch=gfx950", "-o", LIB] + objs
+        cmd = [HIPCC, "-shared", "-fPIC", "--offload-arch=gfx950", "-o", LIB] + objs + [
+            "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-4000:]}")

@@ -385,7 +385,7 @@ int llmi_gelu_mul(const float* gate, const float* up, size_t n, float* out) {
 int llmi_session_create(const void* gguf, size_t size, const llmi_session_opts* opts, llmi_session** out) {
   return guard([&] {
     if (!gguf || !out) throw status_error(LLMI_E_ARG, "null pointer");
-    llmi_session_opts o{0, 0, 4096, 0};
+    llmi_session_opts o{0, 0, 4096, 0, 0, 1, nullptr, nullptr};
     if (opts) o = *opts;
     auto* h = new llmi_session{nullptr};
     try {
@@ -423,6 +423,22 @@ int llmi_session_enqueue(llmi_session* s, int32_t first, int pos, int n_steps) {
 int llmi_session_sync(llmi_session* s, int32_t* out_tokens, int n) {
   return guard([&] { s->s->sync(out_tokens, n); });
 }
+
+int llmi_tp_unique_id(void* out) {
+  return guard([&] {
+    if (!out) throw status_error(LLMI_E_ARG, "null pointer");
+    rccl_unique_id(out);
+  });
+}
+
+int llmi_tp_group_create(int size, llmi_tp_group** out) {
+  return guard([&] {
+    if (!out || size < 1) throw status_error(LLMI_E_ARG, "tp group: size < 1");
+    *out = reinterpret_cast<llmi_tp_group*>(new LocalGroup(size));
+  });
+}
+
+void llmi_tp_group_destroy(llmi_tp_group* g) { delete reinterpret_cast<LocalGroup*>(g); }
 
 int llmi_session_get_info(const llmi_session* s, llmi_session_info* info) {
   return guard([&] { s->s->info(info); });

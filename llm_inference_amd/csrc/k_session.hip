@@ -289,11 +289,23 @@ void launch_argmax(const float* x, int n, unsigned long long* key, hipStream_t s
   LLMI_HIP(hipGetLastError());
 }
 
-// token feedback: next token = argmax, pos += 1, record, reset key
-__global__ void finalize_token_kernel(unsigned long long* key, int32_t* d_token, int32_t* d_pos, int32_t* ring,
-                                      int32_t* ring_idx, int ring_cap) {
-  const uint32_t tok = argmax_key_index(*key);
-  *key = 0;
+// token feedback: next token = argmax, pos += 1, record, reset key.  With
+// row-sharded logits key q holds the best of vocabulary
+// rows [q * shard, (q + 1) * shard) by local index; the winner is re-keyed by
+// global index so ties resolve to the lowest id, as the whole-vocab argmax.
+__global__ void finalize_token_kernel(unsigned long long* keys, int n_keys, int shard, int32_t* d_token,
+                                      int32_t* d_pos, int32_t* ring, int32_t* ring_idx, int ring_cap) {
+  unsigned long long best = keys[0];
+  keys[0] = 0;
+  for (int q = 1; q < n_keys; q++) {
+    const unsigned long long k = keys[q];
+    keys[q] = 0;
+    if (k == 0) continue;
+    const uint32_t gi = (uint32_t)q * (uint32_t)shard + argmax_key_index(k);
+    const unsigned long long kg = (k & 0xFFFFFFFF00000000ull) | (0xFFFFFFFFu - gi);
+    if (kg > best) best = kg;
+  }
+  const uint32_t tok = argmax_key_index(best);
   *d_token = (int32_t)tok;
   *d_pos = *d_pos + 1;
   const int i = *ring_idx;
@@ -301,9 +313,10 @@ __global__ void finalize_token_kernel(unsigned long long* key, int32_t* d_token,
   *ring_idx = i + 1;
 }
 
-void launch_finalize_token(unsigned long long* key, int32_t* d_token, int32_t* d_pos, int32_t* ring,
-                           int32_t* ring_idx, int ring_cap, hipStream_t s) {
-  hipLaunchKernelGGL(finalize_token_kernel, dim3(1), dim3(1), 0, s, key, d_token, d_pos, ring, ring_idx, ring_cap);
+void launch_finalize_token(unsigned long long* keys, int n_keys, int shard, int32_t* d_token, int32_t* d_pos,
+                           int32_t* ring, int32_t* ring_idx, int ring_cap, hipStream_t s) {
+  hipLaunchKernelGGL(finalize_token_kernel, dim3(1), dim3(1), 0, s, keys, n_keys, shard, d_token, d_pos, ring,
+                     ring_idx, ring_cap);
   LLMI_HIP(hipGetLastError());
 }
 

@@ -63,42 +63,76 @@ float* Session::dev_f32_copy(const GGUFView& g, const GTensor* t, int n) {
   return d;
 }
 
-// one GEMV part per tensor, or a fused part when every tensor shares type/cols
-static std::vector<GemvPart> make_parts(const GGUFView& g, const std::vector<const GTensor*>& ts, hipStream_t s,
+// rows [r0, r0 + n) of one GGUF weight
+struct RowSlice {
+  const GTensor* t;
+  int r0, n;
+};
+static RowSlice all_rows(const GTensor* t) { return RowSlice{t, 0, (int)t->shape[1]}; }
+static const void* slice_data(const GGUFView& g, const RowSlice& r) {
+  return (const uint8_t*)g.tensor_data(*r.t) + gguf_bytes(r.t->type, r.r0, (int)r.t->shape[0]);
+}
+
+// one GEMV part per slice, or a fused part when every slice shares type/cols
+static std::vector<GemvPart> make_parts(const GGUFView& g, const std::vector<RowSlice>& ts, hipStream_t s,
                                         size_t& wbytes) {
   std::vector<GemvPart> parts;
   bool same = true;
-  for (auto* t : ts) same &= t->type == ts[0]->type && t->shape[0] == ts[0]->shape[0];
+  for (auto& r : ts) same &= r.t->type == ts[0].t->type && r.t->shape[0] == ts[0].t->shape[0];
   auto check = [](const GTensor* t) {
     if (!gemv_type_supported(t->type))
       throw status_error(LLMI_E_TYPE, "mat_vec_mul: unsupported tensor type " + std::to_string(t->type));
   };
   if (same) {
     int rows = 0;
-    for (auto* t : ts) { check(t); rows += (int)t->shape[1]; }
+    for (auto& r : ts) { check(r.t); rows += r.n; }
     GemvPart p;
-    p.w = alloc_weight(ts[0]->type, rows, (int)ts[0]->shape[0]);
+    p.w = alloc_weight(ts[0].t->type, rows, (int)ts[0].t->shape[0]);
     int r0 = 0;
-    for (auto* t : ts) {
-      upload_rows(p.w, r0, g.tensor_data(*t), (int)t->shape[1], s);
-      r0 += (int)t->shape[1];
+    for (auto& r : ts) {
+      upload_rows(p.w, r0, slice_data(g, r), r.n, s);
+      r0 += r.n;
     }
     wbytes += p.w.bytes;
     parts.push_back(p);
   } else {
     int off = 0;
-    for (auto* t : ts) {
-      check(t);
+    for (auto& r : ts) {
+      check(r.t);
       GemvPart p;
-      p.w = alloc_weight(t->type, (int)t->shape[1], (int)t->shape[0]);
-      upload_rows(p.w, 0, g.tensor_data(*t), (int)t->shape[1], s);
+      p.w = alloc_weight(r.t->type, r.n, (int)r.t->shape[0]);
+      upload_rows(p.w, 0, slice_data(g, r), r.n, s);
       p.out_off = off;
-      off += (int)t->shape[1];
+      off += r.n;
       wbytes += p.w.bytes;
       parts.push_back(p);
     }
   }
   return parts;
+}
+
+// Row shards of a tensor-parallel rank.  q heads split
+// evenly; kv heads split evenly when they divide, else each rank keeps the one
+// kv head its q heads read (replicated K/V rows, as the reference's GQA
+// mapping head / (n_head / n_head_kv), model.cpp:478-550, requires).
+void Session::setup_tp() {
+  const int G = tp_size_, r = tp_rank_;
+  if (hp_.n_head % G) throw status_error(LLMI_E_ARG, "tensor parallel: head_count % tp_size != 0");
+  nh_ = hp_.n_head / G;
+  const int grp = hp_.n_head / hp_.n_head_kv;
+  if (hp_.n_head_kv % G == 0) {
+    nkv_ = hp_.n_head_kv / G;
+    kv0_ = r * nkv_;
+  } else if (grp % nh_ == 0) {
+    nkv_ = 1;
+    kv0_ = r * nh_ / grp;
+  } else {
+    throw status_error(LLMI_E_ARG, "tensor parallel: q heads of a rank span several kv heads");
+  }
+  if (hp_.n_embd % G || hp_.n_ff % G)
+    throw status_error(LLMI_E_ARG, "tensor parallel: embedding_length / feed_forward_length % tp_size != 0");
+  e_sh_ = hp_.n_embd / G;
+  f_sh_ = hp_.n_ff / G;
 }
 
 void Session::upload(const GGUFView& g) {  // model.cpp:169-238 tensor map
@@ -122,6 +156,17 @@ void Session::upload(const GGUFView& g) {  // model.cpp:169-238 tensor map
     embd_raw_ = raw;
   }
   weight_bytes_ += embd_.bytes;
+  v_sh_ = (vocab_ + tp_size_ - 1) / tp_size_;
+  v_rows_ = std::min(v_sh_, vocab_ - tp_rank_ * v_sh_);
+  if (v_rows_ <= 0) throw status_error(LLMI_E_ARG, "tensor parallel: tp_size > vocabulary rows");
+  if (tp_) {  // this rank's vocabulary rows for the logits GEMV (embd_ stays whole for lookups)
+    logits_w_ = alloc_weight(te->type, v_rows_, hp_.n_embd);
+    upload_rows(logits_w_, 0, slice_data(g, RowSlice{te, tp_rank_ * v_sh_, v_rows_}), v_rows_, stream_);
+    own_logits_w_ = true;
+    weight_bytes_ += logits_w_.bytes;
+  } else {
+    logits_w_ = embd_;
+  }
   out_norm_ = dev_f32_copy(g, on, hp_.n_embd);
   L_.resize(hp_.n_layer);
   for (int l = 0; l < hp_.n_layer; l++) {
@@ -139,14 +184,19 @@ void Session::upload(const GGUFView& g) {  // model.cpp:169-238 tensor map
     if ((int)q->shape[1] < hp_.n_head * Ld.hd || (int)k->shape[1] < hp_.n_head_kv * Ld.hd ||
         (int)v->shape[1] < hp_.n_head_kv * Ld.hd)
       throw status_error(LLMI_E_SIZE, "attention projection rows < heads * head_dim");
-    Ld.qkv = make_parts(g, {q, k, v}, stream_, weight_bytes_);
-    Ld.k_off = (int)q->shape[1];
-    Ld.v_off = (int)(q->shape[1] + k->shape[1]);
-    Ld.qkv_rows = (int)(q->shape[1] + k->shape[1] + v->shape[1]);
+    const int hd = Ld.hd, r = tp_rank_;
+    const std::vector<RowSlice> qkv_rows =
+        tp_ ? std::vector<RowSlice>{{q, r * nh_ * hd, nh_ * hd}, {k, kv0_ * hd, nkv_ * hd}, {v, kv0_ * hd, nkv_ * hd}}
+            : std::vector<RowSlice>{all_rows(q), all_rows(k), all_rows(v)};
+    Ld.qkv = make_parts(g, qkv_rows, stream_, weight_bytes_);
+    Ld.k_off = qkv_rows[0].n;
+    Ld.v_off = qkv_rows[0].n + qkv_rows[1].n;
+    Ld.qkv_rows = qkv_rows[0].n + qkv_rows[1].n + qkv_rows[2].n;
     const GTensor* o = T("attn_output.weight");
     if ((int)o->shape[0] != hp_.n_head * Ld.hd || (int)o->shape[1] != hp_.n_embd)
       throw status_error(LLMI_E_SIZE, "mat_vec_mul_q4_0: input vector size mismatch (attn_output)");
-    Ld.o = make_parts(g, {o}, stream_, weight_bytes_)[0];
+    const RowSlice o_rows = tp_ ? RowSlice{o, r * e_sh_, e_sh_} : all_rows(o);
+    Ld.o = make_parts(g, {o_rows}, stream_, weight_bytes_)[0];
     const GTensor *gt = T("ffn_gate.weight"), *up = T("ffn_up.weight"), *dn = T("ffn_down.weight");
     if ((int)gt->shape[1] != hp_.n_ff || (int)up->shape[1] != hp_.n_ff || (int)dn->shape[0] != hp_.n_ff)
       throw status_error(LLMI_E_SIZE, "ffn shapes do not match feed_forward_length");
@@ -165,19 +215,23 @@ void Session::upload(const GGUFView& g) {  // model.cpp:169-238 tensor map
     const bool want_fused =
         fuse_layers_ && qkv_same && gt->type == T_Q4_0 && up->type == T_Q4_0 && gt->shape[0] == up->shape[0] &&
         (int)q->shape[0] == hp_.n_embd && (int)gt->shape[0] == hp_.n_embd &&
-        shape_ok(q, (int)(q->shape[1] + k->shape[1] + v->shape[1]), LAYER_PRO) &&
-        shape_ok(q, (int)(q->shape[1] + k->shape[1] + v->shape[1]), LAYER_PLAIN) &&
-        shape_ok(o, (int)o->shape[1], LAYER_PLAIN) && shape_ok(gt, 2 * hp_.n_ff, LAYER_GELU) &&
-        shape_ok(dn, (int)dn->shape[1], LAYER_QUANT);
+        shape_ok(q, Ld.qkv_rows, LAYER_PRO) && shape_ok(q, Ld.qkv_rows, LAYER_PLAIN) &&
+        shape_ok(o, o_rows.n, LAYER_PLAIN) && shape_ok(gt, 2 * (tp_ ? f_sh_ : hp_.n_ff), LAYER_GELU) &&
+        shape_ok(dn, tp_ ? e_sh_ : (int)dn->shape[1], LAYER_QUANT);
+    if (tp_ && !want_fused)
+      throw status_error(LLMI_E_ARG, "tensor parallel: layer " + std::to_string(l) +
+                                         " shards are not in the fused Q4_0 launch table");
     if (want_fused) {
       // rows interleaved in groups of H (gate H k.., up H k..) for the fused
       // GELU epilogue of gemv_q4_0_layer (k_layer.hip): a work-group of 2H
-      // rows owns matching gate and up rows
-      const int cols = (int)gt->shape[0], F = hp_.n_ff;
+      // rows owns matching gate and up rows.  A tensor-parallel rank keeps
+      // hidden units [rank * F, (rank + 1) * F).
+      const int cols = (int)gt->shape[0], F = tp_ ? f_sh_ : hp_.n_ff;
       const int H = layer_gemv_gelu_group(cols);
       const size_t rb = gguf_bytes(T_Q4_0, 1, cols);
       std::vector<uint8_t> il((size_t)2 * F * rb);
-      const uint8_t *sg = (const uint8_t*)g.tensor_data(*gt), *su = (const uint8_t*)g.tensor_data(*up);
+      const size_t h0 = (size_t)r * F * rb;
+      const uint8_t *sg = (const uint8_t*)g.tensor_data(*gt) + h0, *su = (const uint8_t*)g.tensor_data(*up) + h0;
       for (int k = 0; k < F / H; k++) {
         std::memcpy(&il[(size_t)(2 * H * k) * rb], sg + (size_t)(H * k) * rb, H * rb);
         std::memcpy(&il[(size_t)(2 * H * k + H) * rb], su + (size_t)(H * k) * rb, H * rb);
@@ -189,9 +243,9 @@ void Session::upload(const GGUFView& g) {  // model.cpp:169-238 tensor map
       Ld.gate_up = {p};
       Ld.gu_interleaved = true;
     } else {
-      Ld.gate_up = make_parts(g, {gt, up}, stream_, weight_bytes_);
+      Ld.gate_up = make_parts(g, {all_rows(gt), all_rows(up)}, stream_, weight_bytes_);
     }
-    Ld.down = make_parts(g, {dn}, stream_, weight_bytes_)[0];
+    Ld.down = make_parts(g, {tp_ ? RowSlice{dn, r * e_sh_, e_sh_} : all_rows(dn)}, stream_, weight_bytes_)[0];
     Ld.fused = Ld.gu_interleaved && Ld.qkv.size() == 1 && layer_gemv_supported(Ld.qkv[0].w, LAYER_PRO) &&
                layer_gemv_supported(Ld.qkv[0].w, LAYER_PLAIN) && layer_gemv_supported(Ld.o.w, LAYER_PLAIN) &&
                layer_gemv_supported(Ld.gate_up[0].w, LAYER_GELU) && layer_gemv_supported(Ld.down.w, LAYER_QUANT);
@@ -201,7 +255,7 @@ void Session::upload(const GGUFView& g) {  // model.cpp:169-238 tensor map
     Ld.ffn_norm = dev_f32_copy(g, T("ffn_norm.weight"), hp_.n_embd);
     Ld.post_attn_norm = dev_f32_copy(g, T2("post_attention_norm.weight", "attn_post_norm.weight"), hp_.n_embd);
     Ld.post_ffw_norm = dev_f32_copy(g, T2("post_ffw_norm.weight", "ffn_post_norm.weight"), hp_.n_embd);
-    const size_t kv = (size_t)hp_.n_head_kv * max_ctx_ * Ld.hd;
+    const size_t kv = (size_t)nkv_ * max_ctx_ * Ld.hd;
     Ld.kc = dalloc<uint16_t>(kv);
     Ld.vc = dalloc<uint16_t>(kv);
   }
@@ -229,7 +283,7 @@ void Session::alloc_buffers() {
   gu_ = dalloc<float>(2 * (size_t)F);
   hid_ = dalloc<float>(F);
   d_out_ = dalloc<float>(E);
-  logits_ = dalloc<float>(vocab_);
+  logits_ = dalloc<float>((size_t)tp_size_ * v_sh_);
   act_.q8.xb = dalloc<XBlock>(maxcols / 32 + 1);
   act_.q8.nb = maxcols / 32;
   act_.q8k = dalloc<uint8_t>((size_t)(maxcols / 256 + 1) * 292);
@@ -238,7 +292,7 @@ void Session::alloc_buffers() {
   d_pos_ = dalloc<int32_t>(1);
   ring_ = dalloc<int32_t>(max_ctx_);
   ring_idx_ = dalloc<int32_t>(1);
-  amax_key_ = dalloc<unsigned long long>(1);
+  amax_key_ = dalloc<unsigned long long>(tp_size_);  // one argmax key per rank's vocabulary slice
   LLMI_HIP(hipHostMalloc((void**)&h_stage_, 64, hipHostMallocDefault));
 }
 
@@ -281,24 +335,41 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
   max_ctx_ = opts.max_ctx > 0 ? opts.max_ctx : 4096;
   if (opts.attn_split != 0 && opts.attn_split != ATTN_NSPLIT)
     throw status_error(LLMI_E_ARG, "attn_split must be 0 or " + std::to_string(ATTN_NSPLIT));
+  tp_ = opts.tp_id != nullptr || opts.tp_group != nullptr;
+  if (tp_) {
+    tp_rank_ = opts.tp_rank;
+    tp_size_ = opts.tp_size;
+    if (tp_size_ < 1 || tp_rank_ < 0 || tp_rank_ >= tp_size_)
+      throw status_error(LLMI_E_ARG, "tensor parallel: tp_rank / tp_size out of range");
+    if (!fuse_layers_ || !dup_.empty())
+      throw status_error(LLMI_E_ARG, "tensor parallel needs the fused fast path (no LLMI_EXACT / LLMI_NO_FUSE)");
+  }
   LLMI_HIP(hipSetDevice(opts.device));
   LLMI_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   try {
+    if (tp_) {
+      coll_ = opts.tp_group ? make_local(reinterpret_cast<LocalGroup*>(opts.tp_group), tp_rank_)
+                            : make_rccl(tp_rank_, tp_size_, opts.tp_id);
+      if (!coll_->graph_safe()) use_graph_ = false;
+    }
     GGUFView g(gguf, size);
     load_hparams(g);
+    setup_tp();
     upload(g);
     alloc_buffers();
     build_rope_tables();
   } catch (const gguf_error& e) {
-    this->~Session();
+    release();
     throw status_error(LLMI_E_GGUF, e.what());
   } catch (...) {
-    this->~Session();
+    release();
     throw;
   }
 }
 
-Session::~Session() {
+Session::~Session() { release(); }
+
+void Session::release() {
   if (graph_exec_) (void)hipGraphExecDestroy(graph_exec_);
   if (graph_) (void)hipGraphDestroy(graph_);
   graph_exec_ = nullptr;
@@ -310,11 +381,14 @@ Session::~Session() {
     free_weight(l.down.w);
   }
   L_.clear();
+  if (own_logits_w_) free_weight(logits_w_);
+  own_logits_w_ = false;
   free_weight(embd_);
   for (void* p : allocs_) (void)hipFree(p);
   allocs_.clear();
   if (h_stage_) (void)hipHostFree(h_stage_);
   h_stage_ = nullptr;
+  coll_.reset();
   if (stream_) (void)hipStreamDestroy(stream_);
   stream_ = nullptr;
 }
@@ -373,22 +447,28 @@ void Session::record_step(hipStream_t s) {
   }
   bool fused = fuse_layers_;
   for (const auto& l : L_) fused &= l.fused;
+  if (tp_ && !fused) throw status_error(LLMI_E_ARG, "tensor parallel needs the fused layer path");
   if (fused) {
     record_layers_fused(s, x_q8);
   } else {
     record_layers(s, x_q8);
   }
   // logits (model.cpp:993-1034): F16 table -> mat_vec_mul_fp16, else mat_vec_mul
+  // (a tensor-parallel rank: its vocabulary rows, its own argmax key, then
+  // the keys all-gathered and reduced in finalize)
   if (embd_.type != T_F16) prepare_act(embd_.type, xn_, E, act_, s);
   const bool fold = !ex_logits_ && embd_.type == T_F16 && E % 8 == 0;
+  float* lg = logits_ + (size_t)tp_rank_ * v_sh_;
+  unsigned long long* key = amax_key_ + tp_rank_;
   for (int r = 0; r < dup("logits"); r++)
-    launch_gemv(embd_, act_, logits_, ex_logits_ ? GEMV_EXACT : GEMV_FAST, s, fold ? amax_key_ : nullptr);
+    launch_gemv(logits_w_, act_, lg, ex_logits_ ? GEMV_EXACT : GEMV_FAST, s, fold ? key : nullptr);
   kernels_per_token_++;
   if (!fold) {
-    launch_argmax(logits_, vocab_, amax_key_, s);
+    launch_argmax(lg, v_rows_, key, s);
     kernels_per_token_++;
   }
-  launch_finalize_token(amax_key_, d_token_, d_pos_, ring_, ring_idx_, max_ctx_, s);
+  if (tp_) coll_->all_gather(amax_key_, sizeof(unsigned long long), s);
+  launch_finalize_token(amax_key_, tp_size_, v_sh_, d_token_, d_pos_, ring_, ring_idx_, max_ctx_, s);
   kernels_per_token_++;
 }
 
@@ -425,21 +505,26 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
       std::swap(cur, other);
     }
     kernels_per_token_++;
-    QKVArgs qa{qkv_, Ld.k_off, Ld.v_off, hp_.n_head, hp_.n_head_kv, hd, Ld.q_norm, Ld.k_norm,
+    // this rank's heads (all of them without tensor parallelism)
+    QKVArgs qa{qkv_, Ld.k_off, Ld.v_off, nh_, nkv_, hd, Ld.q_norm, Ld.k_norm,
                Ld.is_swa ? rope_swa_ : rope_glb_, hp_.attn_scale, hp_.eps, q_, Ld.kc, Ld.vc, max_ctx_, d_pos_};
     const bool q8_in_combine = hd % 32 == 0;
-    AttnArgs aa{q_, Ld.kc, Ld.vc, hp_.n_head, hp_.n_head_kv, hd, max_ctx_, d_pos_, part_, attn_,
-                ticket_, q8_in_combine ? act_.q8.xb : nullptr};
+    if (tp_ && !q8_in_combine) throw status_error(LLMI_E_ARG, "tensor parallel: head_dim % 32 != 0");
+    const int hb = nh_ * hd / 32;  // Q8_0 blocks of this rank's heads
+    AttnArgs aa{q_, Ld.kc, Ld.vc, nh_, nkv_, hd, max_ctx_, d_pos_, part_, attn_,
+                ticket_, q8_in_combine ? act_.q8.xb + (size_t)tp_rank_ * hb : nullptr};
     for (int r = 0; r < dup("attn"); r++) launch_attention(aa, false, s, &qa);
     kernels_per_token_++;
     if (!q8_in_combine) {
       launch_quantize_q8_0(attn_, hp_.n_head * hd, act_.q8, s);
       kernels_per_token_++;
     }
+    if (tp_) coll_->all_gather(act_.q8.xb, (size_t)hb * sizeof(XBlock), s);
     LayerGemv go;
     go.xg = act_.q8.xb;
-    go.out = o_out_;
+    go.out = o_out_ + (size_t)tp_rank_ * e_sh_;
     for (int r = 0; r < dup("o_proj"); r++) launch_layer_gemv(Ld.o.w, go, LAYER_PLAIN, s);
+    if (tp_) coll_->all_gather(o_out_, (size_t)e_sh_ * sizeof(float), s);
     LayerGemv gg;
     gg.y = o_out_;
     gg.w_post = Ld.post_attn_norm;
@@ -447,13 +532,15 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
     gg.resid_out = other;
     gg.w_next = Ld.ffn_norm;
     gg.eps = hp_.eps;
-    gg.hid = hid_;
+    gg.hid = hid_ + (size_t)tp_rank_ * f_sh_;
     for (int r = 0; r < dup("gate_up"); r++) launch_layer_gemv(Ld.gate_up[0].w, gg, LAYER_GELU, s);
     std::swap(cur, other);
+    if (tp_) coll_->all_gather(hid_, (size_t)f_sh_ * sizeof(float), s);
     LayerGemv gd;
     gd.y = hid_;  // QUANT: GELU output quantized per block in the down launch
-    gd.out = d_out_;
+    gd.out = d_out_ + (size_t)tp_rank_ * e_sh_;
     for (int r = 0; r < dup("down"); r++) launch_layer_gemv(Ld.down.w, gd, LAYER_QUANT, s);
+    if (tp_) coll_->all_gather(d_out_, (size_t)e_sh_ * sizeof(float), s);
     kernels_per_token_ += 3;
   }
   // final residual + output_norm (-> xn_, and f16 x for an F16 logits table)
@@ -556,6 +643,8 @@ void Session::forward(const int32_t* tokens, int n, int pos, float* logits, int3
     set_token_pos(tokens[i], pos + i, i == 0);
     run_step();
   }
+  // every rank of a tensor-parallel group gathers the full logits (collective)
+  if (tp_) coll_->all_gather(logits_, (size_t)v_sh_ * sizeof(float), stream_);
   if (logits) LLMI_HIP(hipMemcpyAsync(logits, logits_, (size_t)vocab_ * 4, hipMemcpyDeviceToHost, stream_));
   if (argmax) LLMI_HIP(hipMemcpyAsync(argmax, d_token_, 4, hipMemcpyDeviceToHost, stream_));
   LLMI_HIP(hipStreamSynchronize(stream_));
@@ -583,7 +672,9 @@ void Session::info(llmi_session_info* o) const {
   o->vocab = vocab_;
   o->max_ctx = max_ctx_;
   o->weight_bytes = weight_bytes_;
-  size_t b = embd_.bytes;
+  o->tp_rank = tp_rank_;
+  o->tp_size = tp_size_;
+  size_t b = logits_w_.bytes;  // this rank's bytes
   for (const auto& l : L_) {
     for (const auto& p : l.qkv) b += p.w.bytes;
     for (const auto& p : l.gate_up) b += p.w.bytes;
@@ -591,7 +682,7 @@ void Session::info(llmi_session_info* o) const {
   }
   o->bytes_per_token = b;
   size_t kv = 0;
-  for (const auto& l : L_) kv += (size_t)2 * hp_.n_head_kv * l.hd * 2;
+  for (const auto& l : L_) kv += (size_t)2 * nkv_ * l.hd * 2;
   o->kv_bytes_per_pos = kv;
   o->kernels_per_token = kernels_per_token_;
 }
@@ -644,7 +735,7 @@ void Session::time_kernel(int which, int reps, double* us, double* bytes) {
       ws.push_back(&l.down.w);
     }
   } else {
-    ws.push_back(&embd_);
+    ws.push_back(&logits_w_);
   }
   std::vector<hipEvent_t> ev(2 * ws.size() * reps);
   for (auto& e : ev) LLMI_HIP(hipEventCreate(&e));
@@ -660,8 +751,8 @@ void Session::time_kernel(int which, int reps, double* us, double* bytes) {
         launch_layer_gemv(*w, fl[j].first, fl[j].second, stream_);
       } else {
         LLMI_HIP(hipEventRecord(ev[k++], stream_));
-        launch_gemv(*w, act_, (w == &embd_ || w->rows > 2 * hp_.n_ff) ? logits_ : gu_,
-                    exact_ ? GEMV_EXACT : GEMV_FAST, stream_, w == &embd_ ? amax_key_ : nullptr);
+        launch_gemv(*w, act_, (w == &logits_w_ || w->rows > 2 * hp_.n_ff) ? logits_ : gu_,
+                    exact_ ? GEMV_EXACT : GEMV_FAST, stream_, w == &logits_w_ ? amax_key_ : nullptr);
         LLMI_HIP(hipEventRecord(ev[k++], stream_));
       }
       tot_bytes += (double)w->bytes;
@@ -678,7 +769,7 @@ void Session::time_kernel(int which, int reps, double* us, double* bytes) {
   *us = tot_ms * 1000.0 / n;
   *bytes = tot_bytes / n;
   // leave the argmax key clean for the next decode step
-  LLMI_HIP(hipMemsetAsync(amax_key_, 0, 8, stream_));
+  LLMI_HIP(hipMemsetAsync(amax_key_, 0, 8 * (size_t)tp_size_, stream_));
   LLMI_HIP(hipStreamSynchronize(stream_));
 }
 

@@ -1,11 +1,13 @@
 // session.h -- device-resident Gemma-3 decode session (behind llmi_session_*).
 #pragma once
 
+#include <memory>
 #include <string>
 #include <utility>
 #include <vector>
 
 #include "../../include/llmi.h"
+#include "collective.h"
 #include "gguf_reader.h"
 #include "session_kernels.h"
 
@@ -49,6 +51,8 @@ class Session {
  public:
   Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts);
   ~Session();
+  Session(const Session&) = delete;
+  Session& operator=(const Session&) = delete;
 
   void forward(const int32_t* tokens, int n_tokens, int pos, float* logits, int32_t* argmax);
   void enqueue(int32_t first, int pos, int n_steps);
@@ -57,7 +61,9 @@ class Session {
   void time_kernel(int which, int reps, double* us, double* bytes);
 
  private:
+  void release();
   void load_hparams(const GGUFView& g);
+  void setup_tp();
   void upload(const GGUFView& g);
   void alloc_buffers();
   void build_rope_tables();
@@ -111,6 +117,16 @@ class Session {
   int kernels_per_token_ = 0;
   std::string dup_;
   size_t weight_bytes_ = 0;
+  // row-sharded tensor parallelism; tp_ = false and G = 1
+  // for a whole-model session.  This rank owns q heads [rank*nh_, +nh_),
+  // kv heads [kv0_, +nkv_), o/down rows [rank*e_sh_, +e_sh_), hidden units
+  // [rank*f_sh_, +f_sh_) and vocabulary rows [rank*v_sh_, +v_rows_)
+  bool tp_ = false;
+  int tp_rank_ = 0, tp_size_ = 1;
+  std::unique_ptr<Collective> coll_;
+  int nh_ = 0, nkv_ = 0, kv0_ = 0, e_sh_ = 0, f_sh_ = 0, v_sh_ = 0, v_rows_ = 0;
+  DevWeight logits_w_;  // the logits GEMV's rows: embd_ itself, or this rank's slice
+  bool own_logits_w_ = false;
 };
 
 }  // namespace llmi

@@ -51,7 +51,7 @@ bool layer_gemv_supported(const DevWeight& w, int role);
 int layer_gemv_gelu_group(int cols);
 void launch_layer_gemv(const DevWeight& w, LayerGemv a, int role, hipStream_t s);
 void launch_argmax(const float* x, int n, unsigned long long* key, hipStream_t s);
-void launch_finalize_token(unsigned long long* key, int32_t* d_token, int32_t* d_pos, int32_t* ring,
-                           int32_t* ring_idx, int ring_cap, hipStream_t s);
+void launch_finalize_token(unsigned long long* keys, int n_keys, int shard, int32_t* d_token, int32_t* d_pos,
+                           int32_t* ring, int32_t* ring_idx, int ring_cap, hipStream_t s);
 
 }  // namespace llmi

@@ -12,17 +12,54 @@ from typing import Optional, Sequence
 
 import numpy as np
 
-from ._lib import LLMI_EXACT, LLMI_NO_GRAPH, SessionInfo, SessionOpts, check, lib, ptr
+from ._lib import LLMI_EXACT, LLMI_NO_GRAPH, TP_ID_BYTES, SessionInfo, SessionOpts, check, lib, ptr
 from .gguf import GGUFFile
+
+
+def tp_unique_id() -> bytes:
+    """A new RCCL communicator id (rank 0 makes it and sends it to the others)."""
+    b = C.create_string_buffer(TP_ID_BYTES)
+    check(lib().llmi_tp_unique_id(b))
+    return b.raw
+
+
+class TPGroup:
+    """Ranks of one tensor-parallel group sharing ONE device (tests: RCCL
+    refuses two ranks per GPU).  Each rank's session is driven by its own
+    host thread; the all-gathers are device-to-device copies."""
+
+    def __init__(self, size: int):
+        h = C.c_void_p()
+        check(lib().llmi_tp_group_create(size, C.byref(h)))
+        self.h = h
+        self.size = size
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().llmi_tp_group_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
 
 
 class Model:
     def __init__(self, gguf, device: int = 0, exact: bool = False, max_ctx: int = 4096,
-                 use_graph: bool = True, attn_split: int = 0):
+                 use_graph: bool = True, attn_split: int = 0, tp_rank: int = 0, tp_size: int = 1,
+                 tp_id: Optional[bytes] = None, tp_group: Optional["TPGroup"] = None):
+        """tp_id (RCCL, one process per GPU) or tp_group (ranks on one device,
+        one host thread each) makes this session rank tp_rank of a row-sharded
+        tensor-parallel group of tp_size (include/llmi.h)."""
         buf = gguf if isinstance(gguf, np.ndarray) else np.frombuffer(gguf, np.uint8)
         buf = np.ascontiguousarray(buf)
+        self._tp_id = C.create_string_buffer(bytes(tp_id), TP_ID_BYTES) if tp_id is not None else None
+        if tp_id is not None and len(tp_id) != TP_ID_BYTES:
+            raise ValueError(f"tp_id must be {TP_ID_BYTES} bytes")
+        self._tp_group = tp_group  # keep the group alive as long as the session
         opts = SessionOpts(device, (LLMI_EXACT if exact else 0) | (0 if use_graph else LLMI_NO_GRAPH),
-                           max_ctx, attn_split)
+                           max_ctx, attn_split, tp_rank, tp_size,
+                           C.cast(self._tp_id, C.c_void_p) if self._tp_id is not None else None,
+                           tp_group.h.value if tp_group is not None else None)
         h = C.c_void_p()
         check(lib().llmi_session_create(ptr(buf), buf.size, C.byref(opts), C.byref(h)))
         self.h = h

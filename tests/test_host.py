@@ -57,7 +57,9 @@ def _dist_worker(rank, world, port, q):
     import bench
     d = bench.Dist(world)
     d.barrier()
-    q.put((rank, d.max(1.5 + rank)))
+    # the RCCL unique id travels from rank 0 to every rank (bench.py --mode tp)
+    tid = d.broadcast(bytes(range(128)) if rank == 0 else None)
+    q.put((rank, (d.max(1.5 + rank), tid == bytes(range(128)))))
     d.dist.destroy_process_group()
 
 
@@ -76,4 +78,4 @@ def test_bench_dist_gloo_world2():
     for p in ps:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert res == {0: 2.5, 1: 2.5}  # max over ranks, as bench.py reports
+    assert res == {0: (2.5, True), 1: (2.5, True)}  # max over ranks, as bench.py reports; id broadcast
