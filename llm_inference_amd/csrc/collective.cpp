@@ -89,7 +89,20 @@ class LocalCollective : public Collective {
   LocalGroup* g_;
 };
 
+// diagnostics (LLMI_TP_SOLO): one rank of a sharded group with the exchange
+// left out, to time a rank's own kernels on a single GPU
+class NullCollective : public Collective {
+ public:
+  using Collective::Collective;
+  bool graph_safe() const override { return true; }
+  void all_gather(void*, size_t, hipStream_t) override {}
+};
+
 }  // namespace
+
+std::unique_ptr<Collective> make_null(int rank, int size) {
+  return std::unique_ptr<Collective>(new NullCollective(rank, size));
+}
 
 LocalGroup::LocalGroup(int n_) : n(n_), joined(n_, false), bufs(n_, nullptr), ready(n_, nullptr), done(n_, nullptr) {
   if (n_ < 1) throw std::runtime_error("local group: size < 1");

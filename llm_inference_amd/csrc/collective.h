@@ -62,5 +62,7 @@ struct LocalGroup {
 };
 
 std::unique_ptr<Collective> make_local(LocalGroup* g, int rank);
+// no exchange at all (diagnostics only: per-rank kernel time of a shard)
+std::unique_ptr<Collective> make_null(int rank, int size);
 
 }  // namespace llmi

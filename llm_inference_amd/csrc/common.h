@@ -90,6 +90,27 @@ __device__ __forceinline__ int4 ld_nt(const int4* p) {
 
 __device__ __forceinline__ uint16_t ld_nt16(const uint16_t* p) { return __builtin_nontemporal_load(p); }
 
+// Buffer (SRD) loads: a 32-bit per-lane offset + a wave-uniform SGPR offset
+// instead of a 64-bit address per load (fewer VGPRs for long load chains),
+// and loads past `bytes` return 0.  The descriptor inputs are made provably
+// wave-uniform (readfirstlane) so it lives in SGPRs (guide T8/T20).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uint32_t bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  const uint32_t n = __builtin_amdgcn_readfirstlane(bytes);
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0, (int)n,
+                                           0x00020000);
+}
+constexpr int BUF_NT = 2;  // cache-policy bit: non-temporal (streamed once)
+__device__ __forceinline__ uint4 buf_ld16(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, BUF_NT);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint16_t buf_ld2(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return __builtin_amdgcn_raw_buffer_load_b16(r, voff, soff, BUF_NT);
+}
+
 // Q4_0 nibbles of 4 packed bytes: low = elements 0..15, high = 16..31 (ops.cpp:334-340)
 __device__ __forceinline__ int nib_lo(uint32_t w) { return (int)(w & 0x0F0F0F0Fu); }
 __device__ __forceinline__ int nib_hi(uint32_t w) { return (int)((w >> 4) & 0x0F0F0F0Fu); }

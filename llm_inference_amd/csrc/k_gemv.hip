@@ -261,6 +261,56 @@ __global__ __launch_bounds__(256) void gemv_f16_fast_rows(const uint4* __restric
   if (amax_key != nullptr && lane == 0 && best_i != 0x7fffffff) atomicMax(amax_key, argmax_key(best, best_i));
 }
 
+// fast, cols % 128 == 0 and cols <= 6144 (the logits tables: 1152/2560/3840/
+// 5376 wide): P full passes of 64 lanes x 8 halves + a partial pass of T
+// lanes (T = 16/32/48).  x in registers for the whole kernel; grid-stride
+// over rows with the next row's loads in flight while the current row is
+// reduced (the row loop is otherwise one memory latency per row); argmax
+// folded in.
+template <int P, int T>
+__global__ __launch_bounds__(256) void gemv_f16_rows_pipe(const uint4* __restrict__ w, int rows,
+                                                          const uint4* __restrict__ x16, float* __restrict__ out,
+                                                          unsigned long long* __restrict__ amax_key) {
+  constexpr int NP = P + (T ? 1 : 0);
+  constexpr int RU4 = P * 64 + T;  // uint4 per row
+  const int lane = threadIdx.x & 63;
+  const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int nwaves = gridDim.x * 4;
+  const int tl = T ? lane % (T ? T : 64) : lane;  // partial pass: lanes >= T re-read lane % T and drop it
+  uint4 xr[NP];
+#pragma unroll
+  for (int p = 0; p < NP; p++) xr[p] = x16[p * 64 + (p < P ? lane : tl)];
+  auto load_row = [&](uint4 (&v)[NP], int row) {
+    const uint4* wr = w + (size_t)row * RU4;
+#pragma unroll
+    for (int p = 0; p < NP; p++) v[p] = ld_nt(wr + p * 64 + (p < P ? lane : tl));
+  };
+  float best = -INFINITY;
+  int best_i = 0x7fffffff;
+  int row = wave;
+  uint4 cur[NP];
+  load_row(cur, min(row, rows - 1));
+  for (; row < rows; row += nwaves) {
+    uint4 nxt[NP];
+    load_row(nxt, min(row + nwaves, rows - 1));  // clamped: the last one re-reads a row just read
+    float acc = 0.0f;
+#pragma unroll
+    for (int p = 0; p < P; p++) acc = dot8_f16(cur[p], xr[p], acc);
+    if constexpr (T != 0) {
+      const float t = dot8_f16(cur[P], xr[P], 0.0f);
+      acc += lane < T ? t : 0.0f;
+    }
+    acc = wave_sum(acc);
+    if (lane == 0) {
+      out[row] = acc;
+      if (acc > best) { best = acc; best_i = row; }
+    }
+#pragma unroll
+    for (int p = 0; p < NP; p++) cur[p] = nxt[p];
+  }
+  if (amax_key != nullptr && lane == 0 && best_i != 0x7fffffff) atomicMax(amax_key, argmax_key(best, best_i));
+}
+
 // fast, general cols (cols % 8 == 0): flat (row, chunk) items like Q4_0.
 template <int R, int P>
 __global__ __launch_bounds__(256) void gemv_f16_fast(const uint4* __restrict__ w, int rows, int nc, uint32_t magic,
@@ -454,6 +504,7 @@ void launch_gemv(const DevWeight& w, const ActBuf& x, float* o, GemvMode mode, h
                  unsigned long long* amax_key) {
   const int rows = w.rows;
   if (rows == 0) return;
+  if (w.slab) throw std::runtime_error("gemv: slab-major weights are read by the layer kernels only");
   switch (w.type) {
     case T_Q4_0:
     case T_Q8_0: {
@@ -482,15 +533,24 @@ void launch_gemv(const DevWeight& w, const ActBuf& x, float* o, GemvMode mode, h
         hipLaunchKernelGGL(gemv_f16_exact, dim3((rows * 4 + 255) / 256), dim3(256), 0, s, (const uint4*)w.qs, rows,
                            w.cols, x.x16, o);
         // argmax for the exact path is taken by the caller from the logits
-      } else if (w.cols % 512 == 0 && w.cols / 512 <= 12) {
-        const int P = w.cols / 512;
-        const int waves = std::min(rows, 256 * 32);
+      } else if (w.cols % 128 == 0 && w.cols <= 6144) {
+        const int u4 = w.cols / 8, P = u4 / 64, T = u4 % 64;  // T in {0, 16, 32, 48}
+        // 8 waves per CU for 2560+ wide rows, 16 below (scripts/f16_sweep: the
+        // pipelined row loop wants few long-lived waves; 4B/27B tables and
+        // their 1/8 vocabulary shards 2-30% faster than 32 waves per CU)
+        const int waves = std::min(rows, w.cols >= 2560 ? 256 * 8 : 256 * 16);
         const dim3 grid((waves + 3) / 4);
-        switch (P) {
-#define LLMI_F16P(N) \
-  case N: hipLaunchKernelGGL(gemv_f16_fast_rows<N>, grid, dim3(256), 0, s, (const uint4*)w.qs, rows, (const uint4*)x.x16, o, amax_key); break;
-          LLMI_F16P(1) LLMI_F16P(2) LLMI_F16P(3) LLMI_F16P(4) LLMI_F16P(5) LLMI_F16P(6)
-          LLMI_F16P(7) LLMI_F16P(8) LLMI_F16P(9) LLMI_F16P(10) LLMI_F16P(11) LLMI_F16P(12)
+        switch (P * 4 + T / 16) {
+#define LLMI_F16P(PP, TT)                                                                                  \
+  case PP * 4 + TT / 16:                                                                                   \
+    hipLaunchKernelGGL((gemv_f16_rows_pipe<PP, TT>), grid, dim3(256), 0, s, (const uint4*)w.qs, rows,     \
+                       (const uint4*)x.x16, o, amax_key);                                                  \
+    break;
+#define LLMI_F16P4(PP) LLMI_F16P(PP, 0) LLMI_F16P(PP, 16) LLMI_F16P(PP, 32) LLMI_F16P(PP, 48)
+          LLMI_F16P(0, 16) LLMI_F16P(0, 32) LLMI_F16P(0, 48) LLMI_F16P4(1) LLMI_F16P4(2) LLMI_F16P4(3)
+          LLMI_F16P4(4) LLMI_F16P4(5) LLMI_F16P4(6) LLMI_F16P4(7) LLMI_F16P4(8) LLMI_F16P4(9) LLMI_F16P4(10)
+          LLMI_F16P4(11) LLMI_F16P(12, 0)
+#undef LLMI_F16P4
 #undef LLMI_F16P
         }
       } else {

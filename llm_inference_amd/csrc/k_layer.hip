@@ -94,6 +94,75 @@ __device__ __forceinline__ void eat_chunk(const Chunk<P>& c, int c0, int total, 
   }
 }
 
+// Row-bound lanes (RB): R = 64 / L rows per wave, lane = k L + j works on row
+// k only, blocks j, j + L, j + 2L, ...  A pass (64 lanes) covers L consecutive
+// blocks of each of the wave's R rows (R full 128-B lines of quants), so a
+// lane needs no (row, block) division and keeps ONE accumulator: about a
+// third of the flat mapping's VALU work per block (PMC: the flat mapping's
+// per-item row select and division kept the VALU ~50% busy at 4.5 TB/s).
+// Lane offsets are affine in the pass index for both weight layouts:
+// q at voq + pass * sq, scale at vod + pass * sd (see the kernel).
+template <int R, int P>
+__device__ __forceinline__ void load_chunk_rb(Chunk<P>& c, __amdgpu_buffer_rsrc_t rq, __amdgpu_buffer_rsrc_t rd,
+                                              int voq, int vod, int sq, int sd, int pass0, int npass) {
+#pragma unroll
+  for (int p = 0; p < P; p++) {
+    // blocks past the row's end read the next row / slab (masked when eaten)
+    // or, past the matrix, 0 from the descriptor's bound; passes past the last
+    // one are sent out of bounds (0, no memory traffic) so the loads stay
+    // unconditional (all of the offset in voffset: the range check does not
+    // cover soffset)
+    const int pi = pass0 + p;
+    const bool in = pi < npass;
+    c.q[p] = buf_ld16(rq, in ? voq + pi * sq : (1 << 30), 0);
+    c.sw[p] = buf_ld2(rd, in ? vod + pi * sd : (1 << 30), 0);
+  }
+}
+
+template <int R, int P>
+__device__ __forceinline__ void eat_chunk_rb(const Chunk<P>& c, int pass0, int nb, int j, bool row_ok,
+                                             const XBlock* s_x, float& acc) {
+  constexpr int L = 64 / R;
+#pragma unroll
+  for (int p = 0; p < P; p++) {
+    const int b = (pass0 + p) * L + j;
+    const bool ok = row_ok && b < nb;
+    const int4* xp = reinterpret_cast<const int4*>(s_x + (b < nb ? b : nb - 1));
+    const int4 x0 = xp[0], x1 = xp[1], x2 = xp[2];
+    int is = x2.y;  // nsum8
+    is = sdot4(nib_lo(c.q[p].x), x0.x, is);
+    is = sdot4(nib_lo(c.q[p].y), x0.y, is);
+    is = sdot4(nib_lo(c.q[p].z), x0.z, is);
+    is = sdot4(nib_lo(c.q[p].w), x0.w, is);
+    is = sdot4(nib_hi(c.q[p].x), x1.x, is);
+    is = sdot4(nib_hi(c.q[p].y), x1.y, is);
+    is = sdot4(nib_hi(c.q[p].z), x1.z, is);
+    is = sdot4(nib_hi(c.q[p].w), x1.w, is);
+    const float v = (h2f(c.sw[p]) * __int_as_float(x2.x)) * (float)is;
+    acc += ok ? v : 0.0f;
+    // compiler fence: keeps each pass's LDS x reads next to their use (hoisted,
+    // they hold ~10 VGPRs per pass live across the chunk)
+    asm volatile("" ::: "memory");
+  }
+}
+
+// sum over each row's L lanes; row k's total ends up in lane k L (R >= 4) or
+// is returned for every k through `tot` (R <= 2)
+template <int R>
+__device__ __forceinline__ float rb_row_sums(float v, float (&tot)[R <= 2 ? R : 1]) {
+  constexpr int L = 64 / R;
+  if constexpr (L >= 2) v += dpp_f<DPP_QUAD_1032>(v);
+  if constexpr (L >= 4) v += dpp_f<DPP_QUAD_2301>(v);
+  if constexpr (L >= 8) v += dpp_f<DPP_ROW_HALF_MIRROR>(v);
+  if constexpr (L >= 16) v += dpp_f<DPP_ROW_MIRROR>(v);
+  if constexpr (R == 1) tot[0] = (lane_f(v, 0) + lane_f(v, 16)) + (lane_f(v, 32) + lane_f(v, 48));
+  if constexpr (R == 2) {
+    tot[0] = lane_f(v, 0) + lane_f(v, 16);
+    tot[1] = lane_f(v, 32) + lane_f(v, 48);
+  }
+  return v;
+}
+
 #ifdef LLMI_LAYER_TRACE  // development: per-work-group phase timestamps (scripts/gemv_sweep)
 __device__ unsigned long long* g_layer_trace = nullptr;
 #define LAYER_MARK(ph)                                                                                     \
@@ -114,6 +183,8 @@ enum { ROLE_PLAIN = LAYER_PLAIN, ROLE_PRO = LAYER_PRO, ROLE_GELU = LAYER_GELU, R
 template <int R, int NW, int P, int E, int ROLE, bool MULTI, bool EARLY>
 __global__ __launch_bounds__(NW * 64) void gemv_q4_0_layer(LayerGemv a) {
   constexpr bool PRO = ROLE == ROLE_PRO || ROLE == ROLE_GELU, GELU = ROLE == ROLE_GELU;
+  constexpr bool RB = R == 1 || R == 2 || R == 4 || R == 8 || R == 16;  // row-bound lanes, else flat items
+  constexpr int L = RB ? 64 / R : 64;
   LAYER_MARK(0);
   constexpr int EPT = E, X_LD = E;
   extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
@@ -128,11 +199,44 @@ __global__ __launch_bounds__(NW * 64) void gemv_q4_0_layer(LayerGemv a) {
   const int total = nrows * nb;
   const uint4* qw = a.qs + (size_t)min(row0, a.rows - 1) * nb;
   const uint16_t* dw = a.wd + (size_t)min(row0, a.rows - 1) * nb;
+  // RB: this lane's row.  Row-major blocks: descriptors over the wave's rows
+  // (wave-uniform base), block b of row k at (k nb + b) x 16 B.  Slab-major
+  // (a.slab, nb % 8 == 0, L % 8 == 0): slabs of 8 blocks x all rows, block b
+  // of row r at ((b / 8) rows + r) x 128 + (b % 8) x 16 B, so a pass of every
+  // wave reads inside the same slab and the chip sweeps memory in order.
+  const int rk = lane / L, rj = lane % L;
+  const bool row_ok = rk < nrows;
+  const int wrow0 = (blockIdx.x * NW + __builtin_amdgcn_readfirstlane(w)) * R;
+  const int wrows = max(0, a.rows - wrow0);
+  __amdgpu_buffer_rsrc_t rq, rd;
+  int voq, vod, sq, sd;
+  if (a.slab) {
+    rq = buf_rsrc(a.qs, (uint32_t)a.rows * nb * 16);
+    rd = buf_rsrc(a.wd, (uint32_t)a.rows * nb * 2);
+    const int r = wrow0 + rk;
+    voq = ((rj >> 3) * a.rows + r) * 128 + (rj & 7) * 16;
+    vod = ((rj >> 3) * a.rows + r) * 16 + (rj & 7) * 2;
+    sq = (L / 8) * a.rows * 128;
+    sd = (L / 8) * a.rows * 16;
+  } else {
+    rq = buf_rsrc(a.qs + (size_t)min(wrow0, a.rows) * nb, (uint32_t)wrows * nb * 16);
+    rd = buf_rsrc(a.wd + (size_t)min(wrow0, a.rows) * nb, (uint32_t)wrows * nb * 2);
+    voq = (rk * nb + rj) * 16;
+    vod = (rk * nb + rj) * 2;
+    sq = L * 16;
+    sd = L * 2;
+  }
+  const int npass = (nb + L - 1) / L;
 
   Chunk<P> ca, cb;
   auto issue_weights = [&]() {
-    load_chunk<P>(ca, qw, dw, 0, total, lane);  // unconditional (valid clamped rows)
-    if constexpr (MULTI) load_chunk<P>(cb, qw, dw, 64 * P, total, lane);
+    if constexpr (RB) {
+      load_chunk_rb<R, P>(ca, rq, rd, voq, vod, sq, sd, 0, npass);
+      if constexpr (MULTI) load_chunk_rb<R, P>(cb, rq, rd, voq, vod, sq, sd, P, npass);
+    } else {
+      load_chunk<P>(ca, qw, dw, 0, total, lane);  // unconditional (valid clamped rows)
+      if constexpr (MULTI) load_chunk<P>(cb, qw, dw, 64 * P, total, lane);
+    }
   };
   if constexpr (PRO) {
     // prologue operands first: loads return in issue order, so issuing them
@@ -227,6 +331,45 @@ __global__ __launch_bounds__(NW * 64) void gemv_q4_0_layer(LayerGemv a) {
   if constexpr (!EARLY) issue_weights();
 
   LAYER_MARK(4);
+  if constexpr (RB) {
+    float acc1 = 0.0f;
+    if constexpr (!MULTI) {
+      eat_chunk_rb<R, P>(ca, 0, nb, rj, row_ok, s_x, acc1);
+    } else {
+      // unconditional loads (out-of-range passes return 0 without traffic):
+      // no loop-carried phis, so the chunk registers are not copied
+      for (int p0 = 0; p0 < npass; p0 += 2 * P) {
+        eat_chunk_rb<R, P>(ca, p0, nb, rj, row_ok, s_x, acc1);
+        load_chunk_rb<R, P>(ca, rq, rd, voq, vod, sq, sd, p0 + 2 * P, npass);
+        eat_chunk_rb<R, P>(cb, p0 + P, nb, rj, row_ok, s_x, acc1);
+        load_chunk_rb<R, P>(cb, rq, rd, voq, vod, sq, sd, p0 + 3 * P, npass);
+      }
+    }
+    LAYER_MARK(5);
+    float tot[R <= 2 ? R : 1];
+    const float v = rb_row_sums<R>(acc1, tot);
+    if constexpr (GELU) {
+      if constexpr (R <= 2) {
+        if (lane == 0)
+          for (int k = 0; k < R; k++) s_rows[w * R + k] = tot[k];
+      } else {
+        if (rj == 0) s_rows[w * R + rk] = v;
+      }
+      __syncthreads();
+      constexpr int H = NW * R / 2;  // hidden units of this work-group
+      if (t < H) a.hid[blockIdx.x * H + t] = gelu_mul1(s_rows[t], s_rows[H + t]);
+    } else {
+      if constexpr (R <= 2) {
+        if (lane == 0)
+          for (int k = 0; k < R; k++)
+            if (k < nrows) a.out[row0 + k] = tot[k];
+      } else {
+        if (rj == 0 && row_ok) a.out[row0 + rk] = v;
+      }
+    }
+    LAYER_MARK(6);
+    return;
+  }
   float acc[R];
 #pragma unroll
   for (int k = 0; k < R; k++) acc[k] = 0.0f;
@@ -292,35 +435,39 @@ void launch_cfg(dim3 grid, size_t lds, const LayerGemv& a, hipStream_t s) {
 struct LayerCfg {
   int nb, role, R, NW, P, E;
   bool multi;
+  int slab;  // weight layout this entry reads (sweep: slab pays for R >= 4 on big matrices)
   LaunchFn fn;
 };
 
-#define LLMI_LCFG(NB, ROLE, R, NW, P, E, MULTI, EARLY) \
-  {NB, ROLE, R, NW, P, E, MULTI, launch_cfg<R, NW, P, E, ROLE, MULTI, EARLY>}
+#define LLMI_LCFG(NB, ROLE, R, NW, P, E, MULTI, EARLY, SLAB) \
+  {NB, ROLE, R, NW, P, E, MULTI, SLAB, launch_cfg<R, NW, P, E, ROLE, MULTI, EARLY>}
+// (scripts/gemv_sweep: 4B gate_up GELU 9.1 -> 8.5 us with R8 NW10 slab; 27B
+// gate_up 35.8 -> 26.3 us with R8 NW8 P4 slab, qkv 10.4 -> 10.0 us, down
+// 24 -> 17-19.5 us issuing the weights after the quantized x is in LDS)
 const LayerCfg kLayerCfgs[] = {
     // PLAIN: x blocks copied to LDS
-    LLMI_LCFG(32, ROLE_PLAIN, 2, 2, 1, 1, false, true),     // 1B o        1152 rows -> 288 WGs
-    LLMI_LCFG(36, ROLE_PLAIN, 8, 1, 5, 2, false, true),     // 1B qkv l0   1536 rows -> 192 WGs
-    LLMI_LCFG(64, ROLE_PLAIN, 1, 10, 1, 1, false, true),    // 4B o        2560 rows -> 256 WGs
-    LLMI_LCFG(80, ROLE_PLAIN, 4, 4, 5, 1, false, true),     // 4B qkv l0   4096 rows -> 256 WGs
-    LLMI_LCFG(120, ROLE_PLAIN, 8, 4, 8, 2, true, true),     // 12B qkv l0  8192 rows -> 256 WGs
-    LLMI_LCFG(128, ROLE_PLAIN, 1, 8, 2, 1, false, true),    // 12B/27B o   3840/5376 rows -> 480/672 WGs
-    LLMI_LCFG(168, ROLE_PLAIN, 8, 4, 7, 2, true, true),     // 27B qkv l0  8192 rows -> 256 WGs
+    LLMI_LCFG(32, ROLE_PLAIN, 2, 2, 1, 1, false, true, 0),     // 1B o        1152 rows -> 288 WGs
+    LLMI_LCFG(36, ROLE_PLAIN, 8, 1, 5, 2, false, true, 0),     // 1B qkv l0   1536 rows -> 192 WGs
+    LLMI_LCFG(64, ROLE_PLAIN, 1, 10, 1, 1, false, true, 0),    // 4B o        2560 rows -> 256 WGs
+    LLMI_LCFG(80, ROLE_PLAIN, 4, 4, 5, 1, false, true, 0),     // 4B qkv l0   4096 rows -> 256 WGs
+    LLMI_LCFG(120, ROLE_PLAIN, 8, 4, 8, 2, true, true, 0),     // 12B qkv l0  8192 rows -> 256 WGs
+    LLMI_LCFG(128, ROLE_PLAIN, 1, 8, 2, 1, false, true, 0),    // 12B/27B o   3840/5376 rows -> 480/672 WGs
+    LLMI_LCFG(168, ROLE_PLAIN, 8, 4, 7, 2, true, true, 1),     // 27B qkv l0  8192 rows -> 256 WGs
     // PRO: residual + norm prologue
-    LLMI_LCFG(36, ROLE_PRO, 8, 2, 5, 9, false, true),       // 1B qkv      96 WGs
-    LLMI_LCFG(80, ROLE_PRO, 4, 4, 5, 10, false, true),      // 4B qkv      256 WGs
-    LLMI_LCFG(120, ROLE_PRO, 8, 4, 8, 15, true, true),      // 12B qkv     256 WGs
-    LLMI_LCFG(168, ROLE_PRO, 4, 8, 6, 11, true, true),      // 27B qkv     256 WGs
+    LLMI_LCFG(36, ROLE_PRO, 8, 2, 5, 9, false, true, 0),       // 1B qkv      96 WGs
+    LLMI_LCFG(80, ROLE_PRO, 4, 4, 5, 10, false, true, 0),      // 4B qkv      256 WGs
+    LLMI_LCFG(120, ROLE_PRO, 8, 4, 8, 15, true, true, 0),      // 12B qkv     256 WGs
+    LLMI_LCFG(168, ROLE_PRO, 4, 8, 6, 11, true, true, 1),      // 27B qkv     256 WGs
     // GELU: prologue + GELU epilogue, 2H = R NW interleaved gate/up rows per WG
-    LLMI_LCFG(36, ROLE_GELU, 6, 9, 4, 2, false, false),      // 1B  13824 rows, H 27 -> 256 WGs
-    LLMI_LCFG(80, ROLE_GELU, 5, 16, 7, 3, false, false),     // 4B  20480 rows, H 40 -> 256 WGs
-    LLMI_LCFG(120, ROLE_GELU, 8, 8, 8, 8, true, false),      // 12B 30720 rows, H 32 -> 480 WGs
-    LLMI_LCFG(168, ROLE_GELU, 8, 8, 7, 11, true, false),     // 27B 43008 rows, H 32 -> 672 WGs
+    LLMI_LCFG(36, ROLE_GELU, 6, 9, 4, 2, false, false, 0),     // 1B  13824 rows, H 27 -> 256 WGs
+    LLMI_LCFG(80, ROLE_GELU, 8, 10, 10, 4, false, false, 1),   // 4B  20480 rows, H 40 -> 256 WGs
+    LLMI_LCFG(120, ROLE_GELU, 8, 8, 8, 8, true, false, 0),     // 12B 30720 rows, H 32 -> 480 WGs
+    LLMI_LCFG(168, ROLE_GELU, 8, 8, 4, 11, true, false, 1),    // 27B 43008 rows, H 32 -> 672 WGs
     // QUANT: f32 activation quantized into LDS (down projection)
-    LLMI_LCFG(216, ROLE_QUANT, 2, 2, 7, 7, false, true),    // 1B down     1152 rows -> 288 WGs
-    LLMI_LCFG(320, ROLE_QUANT, 1, 10, 5, 2, false, true),   // 4B down     2560 rows -> 256 WGs
-    LLMI_LCFG(480, ROLE_QUANT, 1, 8, 8, 4, false, true),    // 12B down    3840 rows -> 480 WGs
-    LLMI_LCFG(672, ROLE_QUANT, 1, 8, 6, 6, true, true),     // 27B down    5376 rows -> 672 WGs
+    LLMI_LCFG(216, ROLE_QUANT, 2, 2, 7, 7, false, true, 0),    // 1B down     1152 rows -> 288 WGs
+    LLMI_LCFG(320, ROLE_QUANT, 1, 10, 5, 2, false, true, 0),   // 4B down     2560 rows -> 256 WGs
+    LLMI_LCFG(480, ROLE_QUANT, 1, 8, 8, 4, false, true, 0),    // 12B down    3840 rows -> 480 WGs
+    LLMI_LCFG(672, ROLE_QUANT, 1, 8, 6, 6, true, false, 0),    // 27B down    5376 rows -> 672 WGs
 };
 #undef LLMI_LCFG
 
@@ -349,6 +496,11 @@ bool layer_gemv_supported(const DevWeight& w, int role) {
   return true;
 }
 
+int layer_gemv_slab(const DevWeight& w, int role) {
+  const LayerCfg* c = w.cols % 32 == 0 ? find_cfg(w.cols / 32, role) : nullptr;
+  return c ? c->slab : 0;
+}
+
 int layer_gemv_gelu_group(int cols) {
   const LayerCfg* c = cols % 32 == 0 ? find_cfg(cols / 32, LAYER_GELU) : nullptr;
   return c ? c->R * c->NW / 2 : 0;
@@ -364,12 +516,16 @@ void launch_layer_gemv(const DevWeight& w, LayerGemv a, int role, hipStream_t s)
   if (role == LAYER_GELU ? !a.hid : !a.out) throw std::runtime_error("layer gemv: missing output");
   const LayerCfg& c = *find_cfg(w.cols / 32, role);
   const int nb = w.cols / 32;
-  if (!c.multi && c.R * nb > 64 * c.P) throw std::runtime_error("layer gemv: table entry needs MULTI");
+  const bool rb = c.R == 1 || c.R == 2 || c.R == 4 || c.R == 8 || c.R == 16;
+  if (!c.multi && (rb ? (nb + 64 / c.R - 1) / (64 / c.R) > c.P : c.R * nb > 64 * c.P))
+    throw std::runtime_error("layer gemv: table entry needs MULTI");
   if (pro && w.cols > c.E * c.NW * 64) throw std::runtime_error("layer gemv: prologue E too small");
   if (role == LAYER_PLAIN && 3 * nb > c.E * c.NW * 64) throw std::runtime_error("layer gemv: x copy E too small");
   if (role == LAYER_QUANT && 4 * nb > c.E * c.NW * 64) throw std::runtime_error("layer gemv: quant E too small");
+  if (w.slab != c.slab) throw std::runtime_error("layer gemv: weight layout does not match the launch table");
   a.qs = reinterpret_cast<const uint4*>(w.qs);
   a.wd = w.d;
+  a.slab = w.slab;
   a.rows = w.rows;
   a.nb = nb;
   a.magic = div_magic(nb);

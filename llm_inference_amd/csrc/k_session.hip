@@ -100,6 +100,35 @@ DevWeight alloc_weight(uint32_t type, int rows, int cols) {
   return w;
 }
 
+__global__ void slab_permute_kernel(const uint4* __restrict__ qs, const uint16_t* __restrict__ d, int rows, int nb,
+                                    uint4* __restrict__ qs2, uint16_t* __restrict__ d2) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // source block (row-major)
+  if (i >= (size_t)rows * nb) return;
+  const int r = (int)(i / nb), b = (int)(i % nb);
+  const size_t j = ((size_t)(b >> 3) * rows + r) * 8 + (b & 7);
+  qs2[j] = qs[i];
+  d2[j] = d[i];
+}
+
+void to_slab_layout(DevWeight& w, hipStream_t s) {
+  if (w.type != T_Q4_0 || w.cols % 256 != 0 || w.slab) throw std::runtime_error("to_slab_layout: Q4_0, cols % 256");
+  const int nb = w.cols / 32;
+  const size_t nblk = (size_t)w.rows * nb;
+  void* q2 = nullptr;
+  uint16_t* d2 = nullptr;
+  LLMI_HIP(hipMalloc(&q2, nblk * 16 + 64));
+  LLMI_HIP(hipMalloc((void**)&d2, nblk * 2 + 64));
+  hipLaunchKernelGGL(slab_permute_kernel, dim3((nblk + 255) / 256), dim3(256), 0, s, (const uint4*)w.qs, w.d, w.rows,
+                     nb, (uint4*)q2, d2);
+  LLMI_HIP(hipGetLastError());
+  LLMI_HIP(hipStreamSynchronize(s));
+  (void)hipFree(w.qs);
+  (void)hipFree(w.d);
+  w.qs = q2;
+  w.d = d2;
+  w.slab = 1;
+}
+
 void free_weight(DevWeight& w) {
   if (w.qs) (void)hipFree(w.qs);
   if (w.d) (void)hipFree(w.d);

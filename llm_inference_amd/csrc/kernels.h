@@ -18,6 +18,7 @@ struct DevWeight {
   void* qs = nullptr;      // quants (or raw blocks / f16 / bf16 data)
   uint16_t* d = nullptr;   // per-block scales (Q4_0/Q8_0 only)
   size_t bytes = 0;        // algorithmic bytes (GGUF size of the tensor)
+  int slab = 0;            // Q4_0 only: 1 = slab-major blocks (to_slab_layout; layer kernels only)
 };
 
 // Activation prepared for a weight type (device scratch):

@@ -203,6 +203,12 @@ void Session::upload(const GGUFView& g) {  // model.cpp:169-238 tensor map
     // the fused layer path (k_layer.hip) needs every projection in its launch
     // table; decided from the GGUF shapes before upload because it changes
     // the gate/up row order
+    auto slab_of = [](const GTensor* t, int role) {
+      DevWeight w;
+      w.type = t->type;
+      w.cols = (int)t->shape[0];
+      return layer_gemv_slab(w, role);
+    };
     auto shape_ok = [](const GTensor* t, int rows, int role) {
       DevWeight w;
       w.type = t->type;
@@ -216,6 +222,7 @@ void Session::upload(const GGUFView& g) {  // model.cpp:169-238 tensor map
         fuse_layers_ && qkv_same && gt->type == T_Q4_0 && up->type == T_Q4_0 && gt->shape[0] == up->shape[0] &&
         (int)q->shape[0] == hp_.n_embd && (int)gt->shape[0] == hp_.n_embd &&
         shape_ok(q, Ld.qkv_rows, LAYER_PRO) && shape_ok(q, Ld.qkv_rows, LAYER_PLAIN) &&
+        slab_of(q, LAYER_PRO) == slab_of(q, LAYER_PLAIN) &&  // one qkv layout serves both roles
         shape_ok(o, o_rows.n, LAYER_PLAIN) && shape_ok(gt, 2 * (tp_ ? f_sh_ : hp_.n_ff), LAYER_GELU) &&
         shape_ok(dn, tp_ ? e_sh_ : (int)dn->shape[1], LAYER_QUANT);
     if (tp_ && !want_fused)
@@ -258,6 +265,34 @@ void Session::upload(const GGUFView& g) {  // model.cpp:169-238 tensor map
     const size_t kv = (size_t)nkv_ * max_ctx_ * Ld.hd;
     Ld.kc = dalloc<uint16_t>(kv);
     Ld.vc = dalloc<uint16_t>(kv);
+  }
+  // The fused path runs only when EVERY layer fits it; otherwise the layers
+  // that were prepared for it go back to the plain gate/up order.
+  bool all_fused = fuse_layers_;
+  for (const auto& Ld : L_) all_fused &= Ld.fused;
+  for (int l = 0; l < hp_.n_layer && !all_fused; l++) {
+    LayerDev& Ld = L_[l];
+    Ld.fused = false;
+    if (!Ld.gu_interleaved) continue;
+    const std::string b = "blk." + std::to_string(l) + ".";
+    for (auto& p : Ld.gate_up) {
+      weight_bytes_ -= p.w.bytes;
+      free_weight(p.w);
+    }
+    Ld.gate_up = make_parts(g, {all_rows(g.tensor(b + "ffn_gate.weight")), all_rows(g.tensor(b + "ffn_up.weight"))},
+                            stream_, weight_bytes_);
+    Ld.gu_interleaved = false;
+  }
+  if (all_fused) {  // the weight layouts the fused launch-table entries read
+    auto relayout = [&](DevWeight& w, int role) {
+      if (layer_gemv_slab(w, role)) to_slab_layout(w, stream_);
+    };
+    for (auto& Ld : L_) {
+      relayout(Ld.qkv[0].w, LAYER_PRO);
+      relayout(Ld.o.w, LAYER_PLAIN);
+      relayout(Ld.gate_up[0].w, LAYER_GELU);
+      relayout(Ld.down.w, LAYER_QUANT);
+    }
   }
 }
 
@@ -335,7 +370,9 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
   max_ctx_ = opts.max_ctx > 0 ? opts.max_ctx : 4096;
   if (opts.attn_split != 0 && opts.attn_split != ATTN_NSPLIT)
     throw status_error(LLMI_E_ARG, "attn_split must be 0 or " + std::to_string(ATTN_NSPLIT));
-  tp_ = opts.tp_id != nullptr || opts.tp_group != nullptr;
+  // LLMI_TP_SOLO (diagnostics): rank tp_rank of tp_size alone, no exchange
+  const bool tp_solo = getenv("LLMI_TP_SOLO") != nullptr && opts.tp_size > 1 && !opts.tp_id && !opts.tp_group;
+  tp_ = opts.tp_id != nullptr || opts.tp_group != nullptr || tp_solo;
   if (tp_) {
     tp_rank_ = opts.tp_rank;
     tp_size_ = opts.tp_size;
@@ -348,8 +385,9 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
   LLMI_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   try {
     if (tp_) {
-      coll_ = opts.tp_group ? make_local(reinterpret_cast<LocalGroup*>(opts.tp_group), tp_rank_)
-                            : make_rccl(tp_rank_, tp_size_, opts.tp_id);
+      coll_ = tp_solo         ? make_null(tp_rank_, tp_size_)
+              : opts.tp_group ? make_local(reinterpret_cast<LocalGroup*>(opts.tp_group), tp_rank_)
+                              : make_rccl(tp_rank_, tp_size_, opts.tp_id);
       if (!coll_->graph_safe()) use_graph_ = false;
     }
     GGUFView g(gguf, size);

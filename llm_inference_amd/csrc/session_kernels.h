@@ -11,6 +11,9 @@ bool gemv_type_supported(uint32_t type);
 DevWeight alloc_weight(uint32_t type, int rows, int cols);
 void upload_rows(DevWeight& w, int dst_row0, const void* host, int rows, hipStream_t s);
 void free_weight(DevWeight& w);
+// Q4_0 row-major blocks -> slab-major (k_layer.hip's a.slab layout): slabs of
+// 8 blocks x all rows, block b of row r at (b / 8) rows 8 + r 8 + b % 8.
+void to_slab_layout(DevWeight& w, hipStream_t s);
 
 // outputs of a norm that feeds a GEMV: xn (always), plus optionally the Q8_0
 // blocks and/or the f16-rounded copy the next GEMV consumes
@@ -32,6 +35,7 @@ struct LayerGemv {
   const uint16_t* wd = nullptr;
   int rows = 0, nb = 0;
   uint32_t magic = 0;
+  int slab = 0;                // weight layout: 0 row-major blocks, 1 slab-major (DevWeight::slab)
   const XBlock* xg = nullptr;  // PLAIN: the activation's Q8_0 blocks
   // PRO / GELU: resid_out = resid_in + rms(y) * w_post (y itself when w_post
   // is null); x = rms(resid_out) * w_next.  QUANT: x = y.
@@ -47,6 +51,8 @@ struct LayerGemv {
   float* hid = nullptr;     // GELU: [rows / 2] = GELU(gate) * up
 };
 bool layer_gemv_supported(const DevWeight& w, int role);
+// the weight layout the launch-table entry for (w's shape, role) reads
+int layer_gemv_slab(const DevWeight& w, int role);
 // GELU role: hidden units per work-group (the gate/up interleave group), 0 if unsupported
 int layer_gemv_gelu_group(int cols);
 void launch_layer_gemv(const DevWeight& w, LayerGemv a, int role, hipStream_t s);

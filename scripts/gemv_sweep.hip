@@ -10,6 +10,7 @@
 #include "../llm_inference_amd/csrc/k_layer.hip"
 
 #include <algorithm>
+#include <cstring>
 #include <vector>
 
 using namespace llmi;
@@ -93,15 +94,18 @@ float* dmalloc_f(size_t n) {
 
 int main(int argc, char** argv) {
   const int reps = argc > 1 ? atoi(argv[1]) : 200;
+  const char* only = argc > 2 ? argv[2] : nullptr;  // substring filter on shape names
   LLMI_HIP(hipSetDevice(0));
   hipStream_t s;
   LLMI_HIP(hipStreamCreate(&s));
   const Shape shapes[] = {{"4b.qkv", 4096, 2560}, {"4b.o", 2560, 2048}, {"4b.gate_up", 20480, 2560},
-                          {"4b.down", 2560, 10240}, {"1b.gate_up", 13824, 1152}, {"27b.down", 5376, 21504}};
+                          {"4b.down", 2560, 10240}, {"1b.gate_up", 13824, 1152}, {"27b.qkv", 8192, 5376}, {"27b.o", 5376, 4096},
+                          {"27b.gate_up", 43008, 5376}, {"27b.down", 5376, 21504}};
   hipEvent_t e0, e1;
   LLMI_HIP(hipEventCreate(&e0));
   LLMI_HIP(hipEventCreate(&e1));
   for (const Shape& sh : shapes) {
+    if (only && !strstr(sh.name, only)) continue;
     const size_t wbytes = (size_t)sh.rows * (sh.cols / 32) * 18;
     const int copies = (int)std::max<size_t>(2, (size_t)(1536ull << 20) / wbytes + 1);
     std::vector<DevWeight> ws(copies);
@@ -133,6 +137,12 @@ int main(int argc, char** argv) {
     auto timeit = [&](const char* label, auto&& launch) {
       for (int i = 0; i < copies; i++) launch(ws[i % copies]);
       LLMI_HIP(hipStreamSynchronize(s));
+      if (getenv("LLMI_SWEEP_EAGER")) {  // for rocprofv3 --pmc: plain launches, no graph
+        for (int i = 0; i < 8; i++) launch(ws[i % copies]);
+        LLMI_HIP(hipStreamSynchronize(s));
+        printf("%-12s %-34s (eager)\n", sh.name, label);
+        return;
+      }
       hipGraph_t g;
       hipGraphExec_t ge;
       LLMI_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
@@ -153,6 +163,13 @@ int main(int argc, char** argv) {
       printf("%-12s %-34s %8.2f us  %7.1f GB/s\n", sh.name, label, us, wbytes / (us * 1e-6) / 1e9);
       fflush(stdout);
     };
+    // the layout a table entry reads (the sweep's weights are random: only
+    // the addressing differs)
+    auto lw = [&](const DevWeight& w, int role) {
+      DevWeight x = w;
+      x.slab = layer_gemv_slab(w, role);
+      return x;
+    };
     timeit("stream<8> (qs only, 2048 WG)", [&](const DevWeight& w) {
       hipLaunchKernelGGL(stream_kernel<8>, dim3(2048), dim3(256), 0, s, (const uint4*)w.qs,
                          (size_t)sh.rows * nb, out);
@@ -167,7 +184,7 @@ int main(int argc, char** argv) {
     plain.out = out;
     DevWeight probe = ws[0];
     if (layer_gemv_supported(probe, LAYER_PLAIN))
-      timeit("layer plain", [&](const DevWeight& w) { launch_layer_gemv(w, plain, LAYER_PLAIN, s); });
+      timeit("layer plain", [&](const DevWeight& w) { launch_layer_gemv(lw(w, LAYER_PLAIN), plain, LAYER_PLAIN, s); });
     LayerGemv pro;
     pro.y = y;
     pro.resid_in = r0;
@@ -177,17 +194,17 @@ int main(int argc, char** argv) {
     pro.eps = 1e-6;
     pro.out = out;
     if (layer_gemv_supported(probe, LAYER_PRO))
-      timeit("layer pro", [&](const DevWeight& w) { launch_layer_gemv(w, pro, LAYER_PRO, s); });
+      timeit("layer pro", [&](const DevWeight& w) { launch_layer_gemv(lw(w, LAYER_PRO), pro, LAYER_PRO, s); });
     LayerGemv gl = pro;
     gl.out = nullptr;
     gl.hid = hid;
     if (layer_gemv_supported(probe, LAYER_GELU))
-      timeit("layer pro+gelu", [&](const DevWeight& w) { launch_layer_gemv(w, gl, LAYER_GELU, s); });
+      timeit("layer pro+gelu", [&](const DevWeight& w) { launch_layer_gemv(lw(w, LAYER_GELU), gl, LAYER_GELU, s); });
     LayerGemv qz;
     qz.y = y;
     qz.out = out;
     if (layer_gemv_supported(probe, LAYER_QUANT))
-      timeit("layer quant", [&](const DevWeight& w) { launch_layer_gemv(w, qz, LAYER_QUANT, s); });
+      timeit("layer quant", [&](const DevWeight& w) { launch_layer_gemv(lw(w, LAYER_QUANT), qz, LAYER_QUANT, s); });
     // MALL experiment: a default-policy prefetch of the same weight right
     // before the GEMV (as a forked graph branch would do during attention)
     {
@@ -197,11 +214,11 @@ int main(int argc, char** argv) {
       };
       timeit("prefetch only", pre);
       if (layer_gemv_supported(probe, LAYER_PLAIN))
-        timeit("prefetch + layer plain", [&](const DevWeight& w) { pre(w); launch_layer_gemv(w, plain, LAYER_PLAIN, s); });
+        timeit("prefetch + layer plain", [&](const DevWeight& w) { pre(w); launch_layer_gemv(lw(w, LAYER_PLAIN), plain, LAYER_PLAIN, s); });
       if (layer_gemv_supported(probe, LAYER_GELU))
-        timeit("prefetch + layer gelu", [&](const DevWeight& w) { pre(w); launch_layer_gemv(w, gl, LAYER_GELU, s); });
+        timeit("prefetch + layer gelu", [&](const DevWeight& w) { pre(w); launch_layer_gemv(lw(w, LAYER_GELU), gl, LAYER_GELU, s); });
       if (layer_gemv_supported(probe, LAYER_QUANT))
-        timeit("prefetch + layer quant", [&](const DevWeight& w) { pre(w); launch_layer_gemv(w, qz, LAYER_QUANT, s); });
+        timeit("prefetch + layer quant", [&](const DevWeight& w) { pre(w); launch_layer_gemv(lw(w, LAYER_QUANT), qz, LAYER_QUANT, s); });
     }
 #ifdef LLMI_LAYER_TRACE
     // phase trace of one launch per role (100 MHz ticks, from the first WG start)
@@ -238,10 +255,10 @@ int main(int argc, char** argv) {
         for (int k = 0; k < 7; k++) printf(" p%d=%.2f", k, cnt[k] ? ph[k] / cnt[k] : -1.0);
         printf("\n");
       };
-      if (layer_gemv_supported(probe, LAYER_PLAIN)) trace("plain", [&](const DevWeight& w) { launch_layer_gemv(w, plain, LAYER_PLAIN, s); });
-      if (layer_gemv_supported(probe, LAYER_PRO)) trace("pro", [&](const DevWeight& w) { launch_layer_gemv(w, pro, LAYER_PRO, s); });
-      if (layer_gemv_supported(probe, LAYER_GELU)) trace("gelu", [&](const DevWeight& w) { launch_layer_gemv(w, gl, LAYER_GELU, s); });
-      if (layer_gemv_supported(probe, LAYER_QUANT)) trace("quant", [&](const DevWeight& w) { launch_layer_gemv(w, qz, LAYER_QUANT, s); });
+      if (layer_gemv_supported(probe, LAYER_PLAIN)) trace("plain", [&](const DevWeight& w) { launch_layer_gemv(lw(w, LAYER_PLAIN), plain, LAYER_PLAIN, s); });
+      if (layer_gemv_supported(probe, LAYER_PRO)) trace("pro", [&](const DevWeight& w) { launch_layer_gemv(lw(w, LAYER_PRO), pro, LAYER_PRO, s); });
+      if (layer_gemv_supported(probe, LAYER_GELU)) trace("gelu", [&](const DevWeight& w) { launch_layer_gemv(lw(w, LAYER_GELU), gl, LAYER_GELU, s); });
+      if (layer_gemv_supported(probe, LAYER_QUANT)) trace("quant", [&](const DevWeight& w) { launch_layer_gemv(lw(w, LAYER_QUANT), qz, LAYER_QUANT, s); });
       (void)hipFree(tr);
     }
 #endif
@@ -272,6 +289,119 @@ int main(int argc, char** argv) {
     }
     geo("plain R8 NW4 P5", gemv_q4_0_layer<8, 4, 5, 4, 0, true, true>, 32, 256);
     geo("plain R2 NW4 P5", gemv_q4_0_layer<2, 4, 5, 4, 0, true, true>, 8, 256);
+    // role variants: (args, role LDS) with explicit geometry
+    auto geo_role = [&](const char* label, auto kern, int rows_per_wg, int threads, LayerGemv a, bool pro_lds) {
+      if (sh.rows % rows_per_wg) return;
+      timeit(label, [&](const DevWeight& w) {
+        a.qs = (const uint4*)w.qs;
+        a.wd = w.d;
+        a.rows = w.rows;
+        a.nb = nb;
+        a.magic = mg;
+        a.n = sh.cols;
+        const size_t lds = (size_t)nb * sizeof(XBlock) + 16 + (pro_lds ? (size_t)sh.cols * 4 : 0);
+        hipLaunchKernelGGL(kern, dim3((w.rows + rows_per_wg - 1) / rows_per_wg), dim3(threads), lds, s, a);
+      });
+    };
+    // slab-major layout variants (addressing only: the sweep's weights are random)
+    if (nb % 8 == 0) {
+      LayerGemv ps = plain, gs = gl, qs2 = qz;
+      ps.slab = gs.slab = qs2.slab = 1;
+      if (nb == 168) {
+        geo_role("SLAB plain R8 NW4 P7 M", gemv_q4_0_layer<8, 4, 7, 4, 0, true, true>, 32, 256, ps, false);
+        geo_role("SLAB plain R4 NW8 P6 M", gemv_q4_0_layer<4, 8, 6, 2, 0, true, true>, 32, 512, ps, false);
+        geo_role("SLAB gelu R8 NW8 P7 E11 M", gemv_q4_0_layer<8, 8, 7, 11, 2, true, false>, 64, 512, gs, true);
+        geo_role("SLAB gelu R8 NW8 P4 E11 M", gemv_q4_0_layer<8, 8, 4, 11, 2, true, false>, 64, 512, gs, true);
+      }
+      if (nb == 672) {
+        geo_role("SLAB quant R1 NW8 P6 E6 M late", gemv_q4_0_layer<1, 8, 6, 6, 3, true, false>, 8, 512, qs2, false);
+        geo_role("SLAB plain R1 NW8 P6 M", gemv_q4_0_layer<1, 8, 6, 4, 0, true, true>, 8, 512, ps, false);
+        geo_role("SLAB plain R2 NW4 P5", gemv_q4_0_layer<2, 4, 5, 4, 0, true, true>, 8, 256, ps, false);
+      }
+      if (nb == 80) {
+        geo_role("SLAB plain R4 NW4 P5 (4b table)", gemv_q4_0_layer<4, 4, 5, 1, 0, false, true>, 16, 256, ps, false);
+        geo_role("SLAB plain R8 NW4 P5", gemv_q4_0_layer<8, 4, 5, 4, 0, true, true>, 32, 256, ps, false);
+      }
+      if (nb == 320) {
+        geo_role("SLAB quant R1 NW10 P5 (4b table)", gemv_q4_0_layer<1, 10, 5, 2, 3, false, true>, 10, 640, qs2, false);
+        geo_role("SLAB plain R1 NW4 P5 M", gemv_q4_0_layer<1, 4, 5, 4, 0, true, true>, 4, 256, ps, false);
+      }
+    }
+    if (nb == 80) {  // 4B gate_up / qkv (x 2560)
+      LayerGemv gs = gl, ps = pro;
+      gs.slab = ps.slab = 1;
+      geo_role("gelu R5 NW16 P7 E3 (table, flat)", gemv_q4_0_layer<5, 16, 7, 3, 2, false, false>, 80, 1024, gl, true);
+      geo_role("gelu R8 NW10 P10 E4", gemv_q4_0_layer<8, 10, 10, 4, 2, false, false>, 80, 640, gl, true);
+      geo_role("gelu R8 NW10 P10 E4 early", gemv_q4_0_layer<8, 10, 10, 4, 2, false, true>, 80, 640, gl, true);
+      geo_role("gelu R8 NW8 P10 E5", gemv_q4_0_layer<8, 8, 10, 5, 2, false, false>, 64, 512, gl, true);
+      geo_role("gelu R4 NW16 P5 E3", gemv_q4_0_layer<4, 16, 5, 3, 2, false, false>, 64, 1024, gl, true);
+      geo_role("gelu R8 NW5 P10 E8", gemv_q4_0_layer<8, 5, 10, 8, 2, false, false>, 40, 320, gl, true);
+      geo_role("SLAB gelu R8 NW10 P10 E4", gemv_q4_0_layer<8, 10, 10, 4, 2, false, false>, 80, 640, gs, true);
+      geo_role("SLAB gelu R8 NW8 P10 E5", gemv_q4_0_layer<8, 8, 10, 5, 2, false, false>, 64, 512, gs, true);
+      geo_role("SLAB gelu R4 NW16 P5 E3", gemv_q4_0_layer<4, 16, 5, 3, 2, false, false>, 64, 1024, gs, true);
+      geo_role("pro R4 NW4 P5 E10 (table)", gemv_q4_0_layer<4, 4, 5, 10, 1, false, true>, 16, 256, pro, true);
+      geo_role("pro R8 NW2 P10 E20", gemv_q4_0_layer<8, 2, 10, 20, 1, false, true>, 16, 128, pro, true);
+      geo_role("pro R2 NW8 P3 E5", gemv_q4_0_layer<2, 8, 3, 5, 1, false, true>, 16, 512, pro, true);
+      geo_role("pro R4 NW8 P5 E5", gemv_q4_0_layer<4, 8, 5, 5, 1, false, true>, 32, 512, pro, true);
+      geo_role("SLAB pro R4 NW4 P5 E10", gemv_q4_0_layer<4, 4, 5, 10, 1, false, true>, 16, 256, ps, true);
+      geo_role("SLAB pro R8 NW2 P10 E20", gemv_q4_0_layer<8, 2, 10, 20, 1, false, true>, 16, 128, ps, true);
+    }
+    if (nb == 320) {  // 4B down (x 10240)
+      geo_role("quant R1 NW10 P5 E2 (table)", gemv_q4_0_layer<1, 10, 5, 2, 3, false, true>, 10, 640, qz, false);
+      geo_role("quant R1 NW10 P5 E2 late", gemv_q4_0_layer<1, 10, 5, 2, 3, false, false>, 10, 640, qz, false);
+      geo_role("quant R1 NW8 P5 E3", gemv_q4_0_layer<1, 8, 5, 3, 3, false, true>, 8, 512, qz, false);
+      geo_role("quant R2 NW5 P10 E4", gemv_q4_0_layer<2, 5, 10, 4, 3, false, true>, 10, 320, qz, false);
+      geo_role("quant R2 NW8 P10 E3", gemv_q4_0_layer<2, 8, 10, 3, 3, false, true>, 16, 512, qz, false);
+      geo_role("quant R1 NW16 P5 E2", gemv_q4_0_layer<1, 16, 5, 2, 3, false, true>, 16, 1024, qz, false);
+    }
+    if (nb == 168) {  // 27B PRO (qkv) variants
+      LayerGemv ps = pro;
+      ps.slab = 1;
+      geo_role("pro R4 NW8 P6 E11 M (table)", gemv_q4_0_layer<4, 8, 6, 11, 1, true, true>, 32, 512, pro, true);
+      geo_role("pro R4 NW8 P6 E11 M late", gemv_q4_0_layer<4, 8, 6, 11, 1, true, false>, 32, 512, pro, true);
+      geo_role("SLAB pro R4 NW8 P6 E11 M", gemv_q4_0_layer<4, 8, 6, 11, 1, true, true>, 32, 512, ps, true);
+      geo_role("SLAB pro R8 NW4 P7 E21 M", gemv_q4_0_layer<8, 4, 7, 21, 1, true, true>, 32, 256, ps, true);
+      geo_role("SLAB pro R8 NW8 P4 E11 M", gemv_q4_0_layer<8, 8, 4, 11, 1, true, true>, 64, 512, ps, true);
+      geo_role("SLAB pro R8 NW8 P4 E11 M late", gemv_q4_0_layer<8, 8, 4, 11, 1, true, false>, 64, 512, ps, true);
+      geo_role("SLAB pro R8 NW4 P4 E21 M", gemv_q4_0_layer<8, 4, 4, 21, 1, true, true>, 32, 256, ps, true);
+      geo_role("SLAB gelu R8 NW8 P4 E11 M early", gemv_q4_0_layer<8, 8, 4, 11, 2, true, true>, 64, 512, [&] { LayerGemv g = gl; g.slab = 1; return g; }(), true);
+      geo_role("SLAB gelu R8 NW4 P4 E21 M", gemv_q4_0_layer<8, 4, 4, 21, 2, true, false>, 32, 256, [&] { LayerGemv g = gl; g.slab = 1; return g; }(), true);
+      geo_role("SLAB plain R8 NW4 P4 M", gemv_q4_0_layer<8, 4, 4, 2, 0, true, true>, 32, 256, [&] { LayerGemv g = plain; g.slab = 1; return g; }(), false);
+    }
+    if (nb == 128) {  // 27B o (x 4096)
+      LayerGemv ps = plain;
+      ps.slab = 1;
+      geo_role("plain R1 NW8 P2 E1 (table)", gemv_q4_0_layer<1, 8, 2, 1, 0, false, true>, 8, 512, plain, false);
+      geo_role("plain R1 NW4 P2 E2", gemv_q4_0_layer<1, 4, 2, 2, 0, false, true>, 4, 256, plain, false);
+      geo_role("plain R2 NW4 P4 E2", gemv_q4_0_layer<2, 4, 4, 2, 0, false, true>, 8, 256, plain, false);
+      geo_role("plain R4 NW4 P8 E2", gemv_q4_0_layer<4, 4, 8, 2, 0, false, true>, 16, 256, plain, false);
+      geo_role("SLAB plain R4 NW4 P8 E2", gemv_q4_0_layer<4, 4, 8, 2, 0, false, true>, 16, 256, ps, false);
+      geo_role("SLAB plain R8 NW4 P8 M", gemv_q4_0_layer<8, 4, 8, 2, 0, true, true>, 32, 256, ps, false);
+      geo_role("SLAB plain R8 NW2 P8 M", gemv_q4_0_layer<8, 2, 8, 3, 0, true, true>, 16, 128, ps, false);
+    }
+    if (nb == 168) {  // 27B gate_up / qkv (x 5376)
+      geo_role("gelu R8 NW8 P7 E11 M (table)", gemv_q4_0_layer<8, 8, 7, 11, 2, true, false>, 64, 512, gl, true);
+      geo_role("gelu R8 NW8 P7 E11 M early", gemv_q4_0_layer<8, 8, 7, 11, 2, true, true>, 64, 512, gl, true);
+      geo_role("gelu R4 NW8 P6 E11 M", gemv_q4_0_layer<4, 8, 6, 11, 2, true, false>, 32, 512, gl, true);
+      geo_role("gelu R8 NW4 P7 E21 M", gemv_q4_0_layer<8, 4, 7, 21, 2, true, false>, 32, 256, gl, true);
+      geo_role("gelu R8 NW8 P4 E11 M", gemv_q4_0_layer<8, 8, 4, 11, 2, true, false>, 64, 512, gl, true);
+      geo_role("gelu R8 NW8 P11 E11 M", gemv_q4_0_layer<8, 8, 11, 11, 2, true, false>, 64, 512, gl, true);
+      geo_role("gelu R16 NW8 P7 E11 M", gemv_q4_0_layer<16, 8, 7, 11, 2, true, false>, 128, 512, gl, true);
+      geo_role("plain R8 NW8 P7 M", gemv_q4_0_layer<8, 8, 7, 2, 0, true, true>, 64, 512, plain, false);
+      geo_role("plain R4 NW8 P6 M", gemv_q4_0_layer<4, 8, 6, 2, 0, true, true>, 32, 512, plain, false);
+      geo_role("plain R2 NW8 P6 M", gemv_q4_0_layer<2, 8, 6, 2, 0, true, true>, 16, 512, plain, false);
+      geo_role("plain R8 NW4 P7 M", gemv_q4_0_layer<8, 4, 7, 4, 0, true, true>, 32, 256, plain, false);
+    }
+    if (nb == 672) {  // 27B down (x 21504)
+      geo_role("quant R1 NW8 P6 E6 M (table)", gemv_q4_0_layer<1, 8, 6, 6, 3, true, true>, 8, 512, qz, false);
+      geo_role("quant R1 NW8 P6 E6 M late", gemv_q4_0_layer<1, 8, 6, 6, 3, true, false>, 8, 512, qz, false);
+      geo_role("quant R2 NW8 P6 E6 M", gemv_q4_0_layer<2, 8, 6, 6, 3, true, true>, 16, 512, qz, false);
+      geo_role("quant R1 NW4 P6 E11 M", gemv_q4_0_layer<1, 4, 6, 11, 3, true, true>, 4, 256, qz, false);
+      geo_role("quant R1 NW8 P11 E6 M", gemv_q4_0_layer<1, 8, 11, 6, 3, true, true>, 8, 512, qz, false);
+      geo_role("quant R1 NW16 P6 E3 M", gemv_q4_0_layer<1, 16, 6, 3, 3, true, true>, 16, 1024, qz, false);
+      geo_role("plain R1 NW8 P6 M", gemv_q4_0_layer<1, 8, 6, 4, 0, true, true>, 8, 512, plain, false);
+      geo_role("plain R2 NW8 P6 M", gemv_q4_0_layer<2, 8, 6, 8, 0, true, true>, 16, 512, plain, false);
+    }
     for (auto& w : ws) {
       (void)hipFree(w.qs);
       (void)hipFree(w.d);

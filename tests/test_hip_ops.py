@@ -167,3 +167,18 @@ def test_gelu_mul(ops, oracle):
     g = (rng.standard_normal(10240) * 3).astype(np.float32)
     u = rng.standard_normal(10240).astype(np.float32)
     np.testing.assert_allclose(ops.gelu_mul(g, u), oracle.gelu_mul(g, u), rtol=2e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("cols", [128, 384, 1152, 2560, 3840, 5376, 6144])
+@pytest.mark.parametrize("rows", [1, 97, 9000])
+def test_f16_logits_widths(ops, rows, cols):
+    """Fast F16 GEMV (the logits table) at every width class of the pipelined
+    row kernel (cols/8 = 64 P + T lanes, T = 0/16/32/48): vs float64 math on
+    the same f16-rounded x (ops.cpp:542-551 rounds x to f16), within the fast
+    GEMV budget of the module docstring."""
+    rng = np.random.default_rng(rows * 7 + cols)
+    w = rng.standard_normal((rows, cols)).astype(np.float16)
+    x = rng.standard_normal(cols).astype(np.float32)
+    o = ops.mat_vec_mul_raw(T.F16, w.view(np.uint16), rows, cols, x, exact=False)
+    ref = w.astype(np.float64) @ x.astype(np.float16).astype(np.float64)
+    assert np.abs(o - ref).max() <= 1e-4 * np.abs(ref).max() + 1e-6
