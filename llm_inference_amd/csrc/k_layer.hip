@@ -175,15 +175,31 @@ __device__ unsigned long long* g_layer_trace = nullptr;
   } while (0)
 #endif
 
-enum { ROLE_PLAIN = LAYER_PLAIN, ROLE_PRO = LAYER_PRO, ROLE_GELU = LAYER_GELU, ROLE_QUANT = LAYER_QUANT };
+enum { ROLE_PLAIN = LAYER_PLAIN, ROLE_PRO = LAYER_PRO, ROLE_GELU = LAYER_GELU, ROLE_QUANT = LAYER_QUANT,
+       // PRO / GELU with E extra HELPER waves that do the prologue while the
+       // NW streaming waves' weight loads are already in flight
+       ROLE_PRO_H = 4, ROLE_GELU_H = 5 };
+constexpr bool role_help(int r) { return r == ROLE_PRO_H || r == ROLE_GELU_H; }
+constexpr int HELP_K4 = 6;  // float4 per helper lane and operand: n <= E * 256 * HELP_K4
 
 // EARLY: issue the weight stream right after the activation loads (small
 // weight slices per CU: the issue stall is short and the latency overlaps);
 // otherwise after the activation is complete in LDS (see the weight issue).
+//
+// HELPER roles (ROLE_PRO_H / ROLE_GELU_H, E = NH helper waves after the NW
+// streaming waves): the helpers issue the prologue operand loads, one raw
+// s_barrier puts them ahead of the weight stream in the CU's queue, then the
+// streaming waves issue their weights while the helpers run the residual/norm
+// (partial sums exchanged through LDS with a counter, no workgroup barrier)
+// and quantize x into LDS; a second raw s_barrier hands x over.  The norm's
+// latency hides under the weights' instead of preceding them.
 template <int R, int NW, int P, int E, int ROLE, bool MULTI, bool EARLY>
-__global__ __launch_bounds__(NW * 64) void gemv_q4_0_layer(LayerGemv a) {
-  constexpr bool PRO = ROLE == ROLE_PRO || ROLE == ROLE_GELU, GELU = ROLE == ROLE_GELU;
+__global__ __launch_bounds__(NW * 64 + (role_help(ROLE) ? E * 64 : 0)) void gemv_q4_0_layer(LayerGemv a) {
+  constexpr bool HELP = role_help(ROLE);
+  constexpr bool PRO = ROLE == ROLE_PRO || ROLE == ROLE_GELU || HELP;
+  constexpr bool GELU = ROLE == ROLE_GELU || ROLE == ROLE_GELU_H;
   constexpr bool RB = R == 1 || R == 2 || R == 4 || R == 8 || R == 16;  // row-bound lanes, else flat items
+  static_assert(!HELP || RB, "helper roles use the row-bound stream");
   constexpr int L = RB ? 64 / R : 64;
   LAYER_MARK(0);
   constexpr int EPT = E, X_LD = E;
@@ -238,7 +254,102 @@ __global__ __launch_bounds__(NW * 64) void gemv_q4_0_layer(LayerGemv a) {
       if constexpr (MULTI) load_chunk<P>(cb, qw, dw, 64 * P, total, lane);
     }
   };
-  if constexpr (PRO) {
+  const bool helper = HELP && w >= NW;
+  if constexpr (HELP) {
+    constexpr int NH = E;
+    __shared__ float s_hred[2][NH];
+    __shared__ int s_hcnt[2];
+    float* s_xf = reinterpret_cast<float*>(s_dyn + (size_t)nb * sizeof(XBlock) + 16);
+    const int n = a.n, hi = w - NW, seg = n / NH, e0 = hi * seg;
+    float4 hy[HELP_K4], hr[HELP_K4], hp[HELP_K4], hn[HELP_K4];
+    if (helper) {
+      if (hi == 0 && lane < 2) s_hcnt[lane] = 0;
+#pragma unroll
+      for (int k = 0; k < HELP_K4; k++) {
+        const int i = e0 + min((k * 64 + lane) * 4, seg - 4);  // clamped, masked below
+        hy[k] = *reinterpret_cast<const float4*>(a.y + i);
+        hr[k] = *reinterpret_cast<const float4*>(a.resid_in + i);
+        hp[k] = a.w_post ? *reinterpret_cast<const float4*>(a.w_post + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+        hn[k] = *reinterpret_cast<const float4*>(a.w_next + i);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the counter reset, before the barrier
+    }
+    __builtin_amdgcn_s_barrier();  // helpers' operand loads are queued ahead of the weights
+    if (!helper) {
+      issue_weights();
+    } else {
+      // helper partial sums -> LDS; every helper adds them in the same order
+      auto hsum = [&](int ph, float part) -> float {
+        if constexpr (NH == 1) return part;
+        if (lane == 0) {
+          s_hred[ph][hi] = part;
+          __hip_atomic_fetch_add(&s_hcnt[ph], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        while (__hip_atomic_load(&s_hcnt[ph], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < NH)
+          __builtin_amdgcn_s_sleep(1);
+        float tot = 0.0f;
+#pragma unroll
+        for (int j = 0; j < NH; j++) tot += s_hred[ph][j];
+        return tot;
+      };
+      float ss = 0.0f;
+#pragma unroll
+      for (int k = 0; k < HELP_K4; k++) {
+        if ((k * 64 + lane) * 4 < seg) {
+          ss = fmaf(hy[k].x, hy[k].x, ss);
+          ss = fmaf(hy[k].y, hy[k].y, ss);
+          ss = fmaf(hy[k].z, hy[k].z, ss);
+          ss = fmaf(hy[k].w, hy[k].w, ss);
+        }
+      }
+      const float sc1 = rms_scale_d(hsum(0, wave_sum(ss)), n, a.eps);
+      float ss2 = 0.0f;
+#pragma unroll
+      for (int k = 0; k < HELP_K4; k++) {
+        float4& h = hr[k];
+        if (a.w_post) {
+          h.x += (sc1 * hy[k].x) * hp[k].x;
+          h.y += (sc1 * hy[k].y) * hp[k].y;
+          h.z += (sc1 * hy[k].z) * hp[k].z;
+          h.w += (sc1 * hy[k].w) * hp[k].w;
+        } else {  // no post-norm: plain add
+          h.x += hy[k].x;
+          h.y += hy[k].y;
+          h.z += hy[k].z;
+          h.w += hy[k].w;
+        }
+        const int i = e0 + (k * 64 + lane) * 4;
+        if ((k * 64 + lane) * 4 < seg) {
+          ss2 = fmaf(h.x, h.x, ss2);
+          ss2 = fmaf(h.y, h.y, ss2);
+          ss2 = fmaf(h.z, h.z, ss2);
+          ss2 = fmaf(h.w, h.w, ss2);
+          if (blockIdx.x == 0) *reinterpret_cast<float4*>(a.resid_out + i) = h;
+        }
+      }
+      const float sc2 = rms_scale_d(hsum(1, wave_sum(ss2)), n, a.eps);
+#pragma unroll
+      for (int k = 0; k < HELP_K4; k++) {
+        const int i = e0 + (k * 64 + lane) * 4;
+        if ((k * 64 + lane) * 4 < seg) {
+          const float4 x = make_float4((sc2 * hr[k].x) * hn[k].x, (sc2 * hr[k].y) * hn[k].y,
+                                       (sc2 * hr[k].z) * hn[k].z, (sc2 * hr[k].w) * hn[k].w);
+          *reinterpret_cast<float4*>(s_xf + i) = x;
+          if (blockIdx.x == 0 && a.xn_out) *reinterpret_cast<float4*>(a.xn_out + i) = x;
+        }
+      }
+      // this helper's Q8_0 blocks (seg % 32 == 0), a DPP quad per block; the
+      // wave's own LDS writes above are ordered before these reads
+      for (int i = lane; i < seg / 8; i += 64) {
+        const float4 f0 = reinterpret_cast<const float4*>(s_xf + e0)[2 * i];
+        const float4 f1 = reinterpret_cast<const float4*>(s_xf + e0)[2 * i + 1];
+        const float v[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+        q8_block_quad(v, i & 3, s_x + e0 / 32 + (i >> 2));
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();  // x blocks complete in LDS (no vmcnt wait: the weights stay in flight)
+  } else if constexpr (PRO) {
     // prologue operands first: loads return in issue order, so issuing them
     // ahead of the weight chunk lets the norm run while the weights stream
     const int n = a.n;
@@ -327,13 +438,18 @@ __global__ __launch_bounds__(NW * 64) void gemv_q4_0_layer(LayerGemv a) {
   // weight loads only as fast as its miss queue drains, so any barrier after
   // the weight issue (the prologue's reductions, the x hand-off) waits for
   // most of the CU's weight bytes (phase trace: +2.5-4 us per launch).
-  __syncthreads();
-  if constexpr (!EARLY) issue_weights();
+  // (HELPER roles: handled above.)
+  if constexpr (!HELP) {
+    __syncthreads();
+    if constexpr (!EARLY) issue_weights();
+  }
 
   LAYER_MARK(4);
   if constexpr (RB) {
     float acc1 = 0.0f;
-    if constexpr (!MULTI) {
+    if (helper) {
+      // helpers have no rows
+    } else if constexpr (!MULTI) {
       eat_chunk_rb<R, P>(ca, 0, nb, rj, row_ok, s_x, acc1);
     } else {
       // unconditional loads (out-of-range passes return 0 without traffic):
@@ -349,16 +465,18 @@ __global__ __launch_bounds__(NW * 64) void gemv_q4_0_layer(LayerGemv a) {
     float tot[R <= 2 ? R : 1];
     const float v = rb_row_sums<R>(acc1, tot);
     if constexpr (GELU) {
-      if constexpr (R <= 2) {
-        if (lane == 0)
-          for (int k = 0; k < R; k++) s_rows[w * R + k] = tot[k];
-      } else {
-        if (rj == 0) s_rows[w * R + rk] = v;
+      if (!helper) {
+        if constexpr (R <= 2) {
+          if (lane == 0)
+            for (int k = 0; k < R; k++) s_rows[w * R + k] = tot[k];
+        } else {
+          if (rj == 0) s_rows[w * R + rk] = v;
+        }
       }
       __syncthreads();
       constexpr int H = NW * R / 2;  // hidden units of this work-group
       if (t < H) a.hid[blockIdx.x * H + t] = gelu_mul1(s_rows[t], s_rows[H + t]);
-    } else {
+    } else if (!helper) {
       if constexpr (R <= 2) {
         if (lane == 0)
           for (int k = 0; k < R; k++)
@@ -422,25 +540,31 @@ using LaunchFn = void (*)(dim3, size_t, const LayerGemv&, hipStream_t);
 
 template <int R, int NW, int P, int E, int ROLE, bool MULTI, bool EARLY>
 void launch_cfg(dim3 grid, size_t lds, const LayerGemv& a, hipStream_t s) {
+  const dim3 block(NW * 64 + (role_help(ROLE) ? E * 64 : 0));
   KernelTiming& kt = kernel_timing();
   if (kt.start) {
-    hipExtLaunchKernelGGL((gemv_q4_0_layer<R, NW, P, E, ROLE, MULTI, EARLY>), grid, dim3(NW * 64), (uint32_t)lds, s,
+    hipExtLaunchKernelGGL((gemv_q4_0_layer<R, NW, P, E, ROLE, MULTI, EARLY>), grid, block, (uint32_t)lds, s,
                           kt.start, kt.stop, 0u, a);
     kt = KernelTiming{};
     return;
   }
-  hipLaunchKernelGGL((gemv_q4_0_layer<R, NW, P, E, ROLE, MULTI, EARLY>), grid, dim3(NW * 64), lds, s, a);
+  hipLaunchKernelGGL((gemv_q4_0_layer<R, NW, P, E, ROLE, MULTI, EARLY>), grid, block, lds, s, a);
 }
 
 struct LayerCfg {
   int nb, role, R, NW, P, E;
   bool multi;
   int slab;  // weight layout this entry reads (sweep: slab pays for R >= 4 on big matrices)
+  bool help;  // PRO/GELU with E helper waves (role_help)
   LaunchFn fn;
 };
 
 #define LLMI_LCFG(NB, ROLE, R, NW, P, E, MULTI, EARLY, SLAB) \
-  {NB, ROLE, R, NW, P, E, MULTI, SLAB, launch_cfg<R, NW, P, E, ROLE, MULTI, EARLY>}
+  {NB, ROLE, R, NW, P, E, MULTI, SLAB, false, launch_cfg<R, NW, P, E, ROLE, MULTI, EARLY>}
+// PRO / GELU entries with NH helper waves (template role ROLE_PRO_H / ROLE_GELU_H)
+#define LLMI_LCFGH(NB, ROLE, R, NW, P, NH, MULTI, SLAB) \
+  {NB, ROLE, R, NW, P, NH, MULTI, SLAB, true,          \
+   launch_cfg<R, NW, P, NH, ROLE == ROLE_PRO ? ROLE_PRO_H : ROLE_GELU_H, MULTI, true>}
 // (scripts/gemv_sweep: 4B gate_up GELU 9.1 -> 8.5 us with R8 NW10 slab; 27B
 // gate_up 35.8 -> 26.3 us with R8 NW8 P4 slab, qkv 10.4 -> 10.0 us, down
 // 24 -> 17-19.5 us issuing the weights after the quantized x is in LDS)
@@ -519,7 +643,9 @@ void launch_layer_gemv(const DevWeight& w, LayerGemv a, int role, hipStream_t s)
   const bool rb = c.R == 1 || c.R == 2 || c.R == 4 || c.R == 8 || c.R == 16;
   if (!c.multi && (rb ? (nb + 64 / c.R - 1) / (64 / c.R) > c.P : c.R * nb > 64 * c.P))
     throw std::runtime_error("layer gemv: table entry needs MULTI");
-  if (pro && w.cols > c.E * c.NW * 64) throw std::runtime_error("layer gemv: prologue E too small");
+  if (pro && !c.help && w.cols > c.E * c.NW * 64) throw std::runtime_error("layer gemv: prologue E too small");
+  if (pro && c.help && (w.cols % (c.E * 32) != 0 || w.cols > c.E * 256 * HELP_K4))
+    throw std::runtime_error("layer gemv: helper segments must be whole Q8_0 blocks within HELP_K4");
   if (role == LAYER_PLAIN && 3 * nb > c.E * c.NW * 64) throw std::runtime_error("layer gemv: x copy E too small");
   if (role == LAYER_QUANT && 4 * nb > c.E * c.NW * 64) throw std::runtime_error("layer gemv: quant E too small");
   if (w.slab != c.slab) throw std::runtime_error("layer gemv: weight layout does not match the launch table");

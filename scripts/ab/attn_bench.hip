@@ -14,9 +14,11 @@ void launch_attention(const AttnArgs& a, bool exact, hipStream_t s, const QKVArg
 }  // namespace llmi_old
 
 using namespace llmi;
+#ifdef LLMI_ATTN_TRACE
 namespace llmi {
 void attn_set_trace(unsigned long long* p);
 }
+#endif
 
 __global__ void fill_h(uint16_t* p, size_t n, uint32_t seed) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
@@ -106,6 +108,7 @@ int main(int argc, char** argv) {
       (void)hipGraphDestroy(g);
     }
   }
+#ifdef LLMI_ATTN_TRACE
   // phase trace of one launch per position (current version), 100 MHz ticks
   unsigned long long* tr = dm<unsigned long long>((size_t)n_kv * ATTN_NSPLIT * 8);
   std::vector<unsigned long long> h((size_t)n_kv * ATTN_NSPLIT * 8);
@@ -132,6 +135,7 @@ int main(int argc, char** argv) {
       printf("\n");
     }
   }
+#endif
   printf("done\n");
   return 0;
 }

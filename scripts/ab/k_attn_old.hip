@@ -4,7 +4,7 @@
 // head's history is one contiguous stream.  The current position lives in
 // device memory (d_pos) so a whole decode step can be replayed as one
 // hipGraph without re-capturing.
-#include "attn.h"
+#include "../../llm_inference_amd/csrc/attn.h"
 
 namespace llmi {
 
@@ -204,7 +204,7 @@ __device__ __forceinline__ float ld_sc1(const float* p) {
 //         v_dot2 f16 products in fp32, K rows padded by TP*16 bytes so the
 //         ds_read_b128 of 16 lanes hit 16 distinct bank groups;
 //   softmax: wave g keeps head g's running (m, l);
-//   PV: thread owns one head dim (for all G heads) over a key residue class.
+//   PV: thread owns 4 head dims (for all G heads) over a key residue class.
 // FUSED (session fast path): the work-group also performs the q/k per-head
 // norm, rope and q scale of qk_norm_rope_kv_kernel and the KV append of this
 // token; the split owning `pos` substitutes the new k/v rows from LDS for the
@@ -213,6 +213,20 @@ __device__ __forceinline__ float ld_sc1(const float* p) {
 // hand-off table, first row): sc1 stores, every storing wave's vmcnt(0),
 // a workgroup barrier, one agent-scope add per work-group; the work-group
 // whose add returns NSPLIT-1 reads every partial with sc1 loads.
+#ifdef LLMI_ATTN_TRACE  // development: per-work-group phase timestamps (scripts/ab)
+__device__ unsigned long long* g_attn_trace = nullptr;
+void attn_set_trace(unsigned long long* p) { LLMI_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_attn_trace), &p, sizeof(p))); }
+#define ATTN_MARK(ph)                                                                                  \
+  do {                                                                                                 \
+    if (g_attn_trace && threadIdx.x == 0)                                                             \
+      g_attn_trace[((size_t)blockIdx.x * gridDim.y + blockIdx.y) * 8 + (ph)] = wall_clock64();        \
+  } while (0)
+#else
+#define ATTN_MARK(ph) \
+  do {                \
+  } while (0)
+#endif
+
 template <int HD, int G, bool FUSED>
 __global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa) {
   constexpr int NS = ATTN_NSPLIT;
@@ -221,7 +235,8 @@ __global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa)
   constexpr int TP = TP0 < CH ? TP0 : CH;
   constexpr int KS = HD + 8 * TP;                    // padded K row stride (halves)
   constexpr int NLD = (64 * CH + 255) / 256;         // chunk loads per thread per tile
-  constexpr int KP = 256 / HD;                       // key residue classes in PV
+  constexpr int NTD = HD / 4;                        // PV: 4 head dims per thread, NTD threads per key class
+  constexpr int KP = 256 / NTD;                      // key residue classes in PV
   constexpr int DPL = RowLd<HD>::DPL;
   __shared__ __attribute__((aligned(16))) uint16_t s_k[64 * KS];
   __shared__ __attribute__((aligned(16))) uint16_t s_v[64 * HD];
@@ -229,11 +244,12 @@ __global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa)
   __shared__ __attribute__((aligned(16))) uint16_t s_new[FUSED ? 2 : 1][FUSED ? HD : 8];
   __shared__ float s_p[G][64];
   __shared__ float s_alpha[G];
-  __shared__ float s_red[KP > 1 ? KP * G * HD : 1];
+  __shared__ __attribute__((aligned(16))) float s_red[KP > 1 ? KP * G * HD : 4];
   __shared__ float s_ml[G][NS][2];
   __shared__ int s_last;
   static_assert(64 * KS * 2 >= G * HD * 4, "s_k doubles as the merged-output staging");
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  ATTN_MARK(0);
   const int hkv = blockIdx.x, c = blockIdx.y;
   const int pos = *a.d_pos;
   const int n_keys = pos + 1;
@@ -308,11 +324,14 @@ __global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa)
   }
 
   float m_run = -INFINITY, l_run = 0.0f;  // head w's running max / sum (waves w < G)
-  float acc[G];
+  float acc[G][4];
 #pragma unroll
-  for (int g = 0; g < G; g++) acc[g] = 0.0f;
-  const int d_own = t % HD, kp = t / HD;
+  for (int g = 0; g < G; g++)
+#pragma unroll
+    for (int e = 0; e < 4; e++) acc[g][e] = 0.0f;
+  const int d_own = 4 * (t % NTD), kp = t / NTD;
   typedef _Float16 h2t __attribute__((ext_vector_type(2)));
+  ATTN_MARK(1);
   for (; tile * 64 < n_keys; tile += NS) {
     mask_tile(tile);
     __syncthreads();  // previous tile's LDS reads done (first time: s_q / s_new written)
@@ -331,6 +350,7 @@ __global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa)
       *reinterpret_cast<uint4*>(&s_v[j * HD + t * 8]) = reinterpret_cast<const uint4*>(s_new[FUSED ? 1 : 0])[t];
     }
     __syncthreads();
+    ATTN_MARK(2);
     if ((tile + NS) * 64 < n_keys) load_tile(tile + NS);  // next tile in flight during this one's math
     if (t < G * 64 * TP) {
       const int pr = t / TP, part = t % TP;
@@ -364,33 +384,53 @@ __global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa)
     }
     __syncthreads();
 #pragma unroll
-    for (int g = 0; g < G; g++) acc[g] *= s_alpha[g];
-#pragma unroll 8
-    for (int j = kp; j < 64; j += KP) {
-      const float v = h2f(s_v[j * HD + d_own]);
+    for (int g = 0; g < G; g++) {
+      const float al = s_alpha[g];
 #pragma unroll
-      for (int g = 0; g < G; g++) acc[g] = fmaf(s_p[g][j], v, acc[g]);
+      for (int e = 0; e < 4; e++) acc[g][e] *= al;
+    }
+#pragma unroll 4
+    for (int j = kp; j < 64; j += KP) {
+      const uint2 vv = *reinterpret_cast<const uint2*>(&s_v[j * HD + d_own]);
+      const float v0 = h2f((uint16_t)(vv.x & 0xFFFF)), v1 = h2f((uint16_t)(vv.x >> 16));
+      const float v2 = h2f((uint16_t)(vv.y & 0xFFFF)), v3 = h2f((uint16_t)(vv.y >> 16));
+#pragma unroll
+      for (int g = 0; g < G; g++) {
+        const float p = s_p[g][j];
+        acc[g][0] = fmaf(p, v0, acc[g][0]);
+        acc[g][1] = fmaf(p, v1, acc[g][1]);
+        acc[g][2] = fmaf(p, v2, acc[g][2]);
+        acc[g][3] = fmaf(p, v3, acc[g][3]);
+      }
     }
   }
   if constexpr (KP > 1) {
 #pragma unroll
-    for (int g = 0; g < G; g++) s_red[(kp * G + g) * HD + d_own] = acc[g];
+    for (int g = 0; g < G; g++)
+      *reinterpret_cast<float4*>(&s_red[(kp * G + g) * HD + d_own]) =
+          make_float4(acc[g][0], acc[g][1], acc[g][2], acc[g][3]);
     __syncthreads();
     if (kp == 0) {
 #pragma unroll
-      for (int g = 0; g < G; g++) {
-        float s = acc[g];
-        for (int r = 1; r < KP; r++) s += s_red[(r * G + g) * HD + d_own];
-        acc[g] = s;
-      }
+      for (int g = 0; g < G; g++)
+        for (int r = 1; r < KP; r++) {
+          const float4 o = *reinterpret_cast<const float4*>(&s_red[(r * G + g) * HD + d_own]);
+          acc[g][0] += o.x;
+          acc[g][1] += o.y;
+          acc[g][2] += o.z;
+          acc[g][3] += o.w;
+        }
     }
   }
 
+  ATTN_MARK(3);
   // ---- publish the partial, take a ticket --------------------------------
   float* part0 = a.partial + (size_t)hkv * G * NS * (HD + 2);  // [G][NS][HD + 2]
   if (kp == 0) {
 #pragma unroll
-    for (int g = 0; g < G; g++) st_sc1(part0 + ((size_t)g * NS + c) * (HD + 2) + d_own, acc[g]);
+    for (int g = 0; g < G; g++)
+#pragma unroll
+      for (int e = 0; e < 4; e++) st_sc1(part0 + ((size_t)g * NS + c) * (HD + 2) + d_own + e, acc[g][e]);
   }
   if (w < G && lane == 0) {
     st_sc1(part0 + ((size_t)w * NS + c) * (HD + 2) + HD, m_run);
@@ -401,40 +441,75 @@ __global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa)
   if (t == 0)
     s_last = __hip_atomic_fetch_add(a.ticket + hkv, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == NS - 1;
   __syncthreads();
+  ATTN_MARK(4);
   if (!s_last) return;
 
   // ---- last work-group: merge the NS partials of the G heads -------------
-  for (int i = t; i < G * NS * 2; i += 256) {
-    const int g = i / (NS * 2), cc = (i / 2) % NS, e = i & 1;
-    s_ml[g][cc][e] = ld_sc1(part0 + ((size_t)g * NS + cc) * (HD + 2) + HD + e);
+  // One batch of loads: every thread's partial accumulators for its (g, d)
+  // outputs and the (m, l) pairs; the per-split weights are computed once per
+  // (g, split) instead of per output.  Arithmetic (and order) as before:
+  // w_c = l_c ? exp(m_c - M) : 0, L = sum_c fma(l_c, w_c), o = sum_c fma(v_c, w_c).
+  constexpr int PAIRS = (G * HD + 255) / 256;
+  float v[PAIRS][NS];
+#pragma unroll
+  for (int p = 0; p < PAIRS; p++) {
+    const int idx = min(t + p * 256, G * HD - 1);
+    const float* pg = part0 + (size_t)(idx / HD) * NS * (HD + 2) + idx % HD;
+#pragma unroll
+    for (int cc = 0; cc < NS; cc++) v[p][cc] = ld_sc1(pg + (size_t)cc * (HD + 2));
+  }
+  float mv = 0.0f, lv = 0.0f;
+  if (t < G * NS) {
+    const float* pm = part0 + ((size_t)(t / NS) * NS + t % NS) * (HD + 2) + HD;
+    mv = ld_sc1(pm);
+    lv = ld_sc1(pm + 1);
+  }
+  __shared__ float s_wt[G][NS];
+  __shared__ float s_L[G];
+  if (t < G * NS) {
+    s_ml[t / NS][t % NS][0] = mv;
+    s_ml[t / NS][t % NS][1] = lv;
   }
   __syncthreads();
-  float* s_out = reinterpret_cast<float*>(s_k);  // [G][HD]
-  for (int idx = t; idx < G * HD; idx += 256) {
-    const int g = idx / HD, d = idx % HD;
-    const float* pg = part0 + (size_t)g * NS * (HD + 2) + d;
-    float v[NS];
-#pragma unroll
-    for (int cc = 0; cc < NS; cc++) v[cc] = ld_sc1(pg + (size_t)cc * (HD + 2));
+  ATTN_MARK(6);
+  if (t < G * NS) {
+    const int g = t / NS;
     float M = -INFINITY;
 #pragma unroll
     for (int cc = 0; cc < NS; cc++) M = fmaxf(M, s_ml[g][cc][0]);
-    float L = 0.0f, o = 0.0f;
+    s_wt[g][t % NS] = lv == 0.0f ? 0.0f : expf(mv - M);
+  }
+  __syncthreads();
+  if (t < G) {
+    float L = 0.0f;
+    for (int cc = 0; cc < NS; cc++) L = fmaf(s_ml[t][cc][1], s_wt[t][cc], L);
+    s_L[t] = L;
+  }
+  __syncthreads();
+  float* s_out = reinterpret_cast<float*>(s_k);  // [G][HD]
 #pragma unroll
-    for (int cc = 0; cc < NS; cc++) {
-      const float l = s_ml[g][cc][1];
-      const float wc = l == 0.0f ? 0.0f : expf(s_ml[g][cc][0] - M);
-      L = fmaf(l, wc, L);
-      o = fmaf(v[cc], wc, o);
+  for (int p = 0; p < PAIRS; p++) {
+    const int idx = t + p * 256;
+    if (idx < G * HD) {
+      const int g = idx / HD;
+      float o = 0.0f;
+#pragma unroll
+      for (int cc = 0; cc < NS; cc++) o = fmaf(v[p][cc], s_wt[g][cc], o);
+      const float val = o / s_L[g];
+      a.out[(size_t)hkv * G * HD + idx] = val;
+      s_out[idx] = val;
     }
-    const float val = o / L;
-    a.out[((size_t)hkv * G + g) * HD + d] = val;
-    s_out[idx] = val;
   }
-  if (a.q8 != nullptr && HD % 32 == 0) {  // Q8_0 blocks of the heads' outputs (ops.cpp:116-139)
+  ATTN_MARK(7);
+  if (a.q8 != nullptr && HD % 32 == 0) {  // Q8_0 blocks of the heads' outputs (ops.cpp:116-139), 4 lanes per block
     __syncthreads();
-    for (int b = t; b < G * HD / 32; b += 256) q8_block_serial(s_out + 32 * b, a.q8 + (size_t)hkv * G * HD / 32 + b);
+    for (int i = t; i < G * HD / 8; i += 256) {
+      const float4 f0 = reinterpret_cast<const float4*>(s_out)[2 * i], f1 = reinterpret_cast<const float4*>(s_out)[2 * i + 1];
+      const float vv[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+      q8_block_quad(vv, i & 3, a.q8 + (size_t)hkv * G * HD / 32 + (i >> 2));
+    }
   }
+  ATTN_MARK(5);
   if (t == 0) __hip_atomic_store(a.ticket + hkv, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
 }
 

@@ -337,6 +337,19 @@ int main(int argc, char** argv) {
       geo_role("gelu R4 NW16 P5 E3", gemv_q4_0_layer<4, 16, 5, 3, 2, false, false>, 64, 1024, gl, true);
       geo_role("gelu R8 NW5 P10 E8", gemv_q4_0_layer<8, 5, 10, 8, 2, false, false>, 40, 320, gl, true);
       geo_role("SLAB gelu R8 NW10 P10 E4", gemv_q4_0_layer<8, 10, 10, 4, 2, false, false>, 80, 640, gs, true);
+      geo_role("SLAB gelu R4 NW4 P5 E10 (H8)", gemv_q4_0_layer<4, 4, 5, 10, 2, false, false>, 16, 256, gs, true);
+      geo_role("SLAB gelu R4 NW4 P5 E10 (H8) early", gemv_q4_0_layer<4, 4, 5, 10, 2, false, true>, 16, 256, gs, true);
+      geo_role("SLAB gelu R8 NW4 P10 E10 (H16)", gemv_q4_0_layer<8, 4, 10, 10, 2, false, false>, 32, 256, gs, true);
+      geo_role("SLAB gelu R8 NW4 P10 E10 (H16) early", gemv_q4_0_layer<8, 4, 10, 10, 2, false, true>, 32, 256, gs, true);
+      geo_role("SLAB gelu R4 NW8 P5 E5 (H16)", gemv_q4_0_layer<4, 8, 5, 5, 2, false, false>, 32, 512, gs, true);
+      geo_role("SLAB plain R8 NW10 P10", gemv_q4_0_layer<8, 10, 10, 1, 0, false, true>, 80, 640, [&] { LayerGemv g = plain; g.slab = 1; return g; }(), false);
+      geo_role("SLAB gelu R8 NW10 P10 H1", gemv_q4_0_layer<8, 10, 10, 1, 5, false, true>, 80, 704, gs, true);
+      geo_role("SLAB gelu R8 NW10 P10 H2", gemv_q4_0_layer<8, 10, 10, 2, 5, false, true>, 80, 768, gs, true);
+      geo_role("gelu R8 NW10 P10 H2", gemv_q4_0_layer<8, 10, 10, 2, 5, false, true>, 80, 768, gl, true);
+      geo_role("SLAB gelu R8 NW5 P10 H2", gemv_q4_0_layer<8, 5, 10, 2, 5, false, true>, 40, 448, gs, true);
+      geo_role("pro R4 NW4 P5 H1", gemv_q4_0_layer<4, 4, 5, 1, 4, false, true>, 16, 320, pro, true);
+      geo_role("pro R4 NW4 P5 H2", gemv_q4_0_layer<4, 4, 5, 2, 4, false, true>, 16, 384, pro, true);
+      geo_role("pro R8 NW4 P10 H2", gemv_q4_0_layer<8, 4, 10, 2, 4, false, true>, 32, 384, pro, true);
       geo_role("SLAB gelu R8 NW8 P10 E5", gemv_q4_0_layer<8, 8, 10, 5, 2, false, false>, 64, 512, gs, true);
       geo_role("SLAB gelu R4 NW16 P5 E3", gemv_q4_0_layer<4, 16, 5, 3, 2, false, false>, 64, 1024, gs, true);
       geo_role("pro R4 NW4 P5 E10 (table)", gemv_q4_0_layer<4, 4, 5, 10, 1, false, true>, 16, 256, pro, true);
@@ -360,6 +373,9 @@ int main(int argc, char** argv) {
       geo_role("pro R4 NW8 P6 E11 M (table)", gemv_q4_0_layer<4, 8, 6, 11, 1, true, true>, 32, 512, pro, true);
       geo_role("pro R4 NW8 P6 E11 M late", gemv_q4_0_layer<4, 8, 6, 11, 1, true, false>, 32, 512, pro, true);
       geo_role("SLAB pro R4 NW8 P6 E11 M", gemv_q4_0_layer<4, 8, 6, 11, 1, true, true>, 32, 512, ps, true);
+      geo_role("SLAB pro R4 NW8 P6 H4 M", gemv_q4_0_layer<4, 8, 6, 4, 4, true, true>, 32, 768, ps, true);
+      geo_role("SLAB gelu R8 NW8 P4 H4 M", gemv_q4_0_layer<8, 8, 4, 4, 5, true, true>, 64, 768, [&] { LayerGemv g = gl; g.slab = 1; return g; }(), true);
+      geo_role("SLAB gelu R8 NW8 P4 H7 M", gemv_q4_0_layer<8, 8, 4, 7, 5, true, true>, 64, 960, [&] { LayerGemv g = gl; g.slab = 1; return g; }(), true);
       geo_role("SLAB pro R8 NW4 P7 E21 M", gemv_q4_0_layer<8, 4, 7, 21, 1, true, true>, 32, 256, ps, true);
       geo_role("SLAB pro R8 NW8 P4 E11 M", gemv_q4_0_layer<8, 8, 4, 11, 1, true, true>, 64, 512, ps, true);
       geo_role("SLAB pro R8 NW8 P4 E11 M late", gemv_q4_0_layer<8, 8, 4, 11, 1, true, false>, 64, 512, ps, true);
