@@ -207,7 +207,9 @@ def main():
             "us_per_launch": round(us, 3), "bytes_per_launch": int(by),
         },
         "logits_gemv": {"us": round(us_l, 2), "GBps": round(by_l / (us_l * 1e-6) / 1e9, 1)},
-        "timing_detail": {"synthetic_build_s": round(t_build, 1), "prefill_s": round(t_prefill, 2)},
+        "timing_detail": {"synthetic_build_s": round(t_build, 1), "prefill_s": round(t_prefill, 4),
+                          "prefill_tokens_per_s": round(a.prefill / t_prefill, 1),
+                          "prefill_mode": "batched int8-MFMA" if info.batched_prefill else "token loop"},
     }
     if d.rank == 0 and d.world == 1 and not a.no_cpu_baseline:
         m.close()

@@ -135,7 +135,11 @@ void llmi_session_destroy(llmi_session* s);
 
 /* Model::forward(tokens, pos) (model.cpp:706): runs n_tokens tokens at
  * positions pos..pos+n_tokens-1 and returns the LAST token's logits
- * (vocab floats, may be NULL) and its greedy argmax (may be NULL). */
+ * (vocab floats, may be NULL) and its greedy argmax (may be NULL).
+ * Fast sessions on one device run n_tokens > 1 as a batched prefill (int8
+ * MFMA GEMMs over the tokens, causal attention over the cache) instead of
+ * the reference's token loop (model.cpp:752-756); LLMI_NO_PREFILL=1 in the
+ * environment forces the token loop. */
 int llmi_session_forward(llmi_session* s, const int32_t* tokens, int n_tokens, int pos, float* logits,
                          int32_t* argmax);
 
@@ -156,6 +160,7 @@ typedef struct {
   size_t kv_bytes_per_pos;    /* + this many bytes per attended position */
   int kernels_per_token;      /* launches captured in the decode graph */
   int tp_rank, tp_size;       /* weight_bytes / bytes_per_token / kv_bytes_per_pos are this rank's */
+  int batched_prefill;        /* 1: llmi_session_forward runs n_tokens > 1 as a batched (MFMA) prefill */
 } llmi_session_info;
 int llmi_session_get_info(const llmi_session* s, llmi_session_info* info);
 

@@ -396,6 +396,16 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
     upload(g);
     alloc_buffers();
     build_rope_tables();
+    // batched prefill: the fast fused layout on one device, shapes the
+    // prefill kernels cover (otherwise forward() runs the token loop)
+    bool pf = fuse_layers_ && !tp_ && (embd_.type == T_F16 || embd_.type == T_Q8_0) && hp_.n_embd <= 8192 &&
+              hp_.n_embd % 32 == 0 && hp_.n_ff % 32 == 0;
+    for (const auto& l : L_)
+      pf = pf && l.fused && (l.hd == 64 || l.hd == 128 || l.hd == 256) && prefill_gemm_supported(l.qkv[0].w) &&
+           prefill_gemm_supported(l.o.w) && prefill_gemm_supported(l.gate_up[0].w) &&
+           prefill_gemm_supported(l.down.w);
+    const int grp = nkv_ > 0 ? nh_ / nkv_ : 0;
+    prefill_ok_ = pf && (grp == 1 || grp == 2 || grp == 4);
   } catch (const gguf_error& e) {
     release();
     throw status_error(LLMI_E_GGUF, e.what());
@@ -491,6 +501,11 @@ void Session::record_step(hipStream_t s) {
   } else {
     record_layers(s, x_q8);
   }
+  record_logits(s);
+}
+
+void Session::record_logits(hipStream_t s) {
+  const int E = hp_.n_embd;
   // logits (model.cpp:993-1034): F16 table -> mat_vec_mul_fp16, else mat_vec_mul
   // (a tensor-parallel rank: its vocabulary rows, its own argmax key, then
   // the keys all-gathered and reduced in finalize)
@@ -508,6 +523,121 @@ void Session::record_step(hipStream_t s) {
   if (tp_) coll_->all_gather(amax_key_, sizeof(unsigned long long), s);
   launch_finalize_token(amax_key_, tp_size_, v_sh_, d_token_, d_pos_, ring_, ring_idx_, max_ctx_, s);
   kernels_per_token_++;
+}
+
+void Session::ensure_prefill_buffers(int cap) {
+  if (cap <= pf_cap_) return;
+  const int E = hp_.n_embd, F = hp_.n_ff;
+  int maxq = 0, maxqkv = 0;
+  for (const auto& l : L_) {
+    maxq = std::max(maxq, hp_.n_head * l.hd);
+    maxqkv = std::max(maxqkv, l.qkv_rows);
+  }
+  pf_xs_ = std::max({E, F, maxq}) / 32;
+  pf_ostride_ = std::max({maxqkv, E, 2 * F});
+  // grow-only; the previous chunk buffers stay allocated until the session ends
+  pf_tokens_ = dalloc<int32_t>(cap);
+  pf_resid_ = dalloc<float>((size_t)cap * E);
+  pf_out_ = dalloc<float>((size_t)cap * pf_ostride_);
+  pf_xq_ = dalloc<XBlock>((size_t)cap * pf_xs_);
+  pf_q_ = dalloc<uint16_t>((size_t)cap * maxq);
+  pf_cap_ = cap;
+}
+
+// Batched prefill of n prompt tokens at positions pos.. (chunks of up to
+// LLMI_PREFILL_CHUNK, default 256): per layer one MFMA GEMM per projection
+// over the chunk, per-token norms / rope / KV append, causal attention over
+// the cache; the last token's logits then go through the decode tail.
+void Session::prefill(const int32_t* tokens, int n, int pos) {
+  hipStream_t s = stream_;
+  const int E = hp_.n_embd, F = hp_.n_ff;
+  int chunk = 256;
+  if (const char* c = getenv("LLMI_PREFILL_CHUNK")) chunk = std::max(1, atoi(c));
+  ensure_prefill_buffers(std::min(chunk, n));
+  const int XS = pf_xs_;
+  const float emb_scale = std::sqrt(static_cast<float>(E));  // model.cpp:337-338
+  for (int c0 = 0; c0 < n; c0 += pf_cap_) {
+    const int T = std::min(pf_cap_, n - c0), p0 = pos + c0;
+    const bool last_chunk = c0 + T == n;
+    LLMI_HIP(hipMemcpyAsync(pf_tokens_, tokens + c0, (size_t)T * 4, hipMemcpyHostToDevice, s));
+    PrefillNorm en;
+    en.table = embd_raw_;
+    en.emb_type = embd_.type;
+    en.row_bytes = embd_row_bytes_;
+    en.tokens = pf_tokens_;
+    en.emb_scale = emb_scale;
+    en.resid = pf_resid_;
+    en.w_next = L_[0].attn_norm;
+    en.xq = pf_xq_;
+    en.xstride = XS;
+    en.n = E;
+    en.eps = hp_.eps;
+    launch_prefill_norm(en, T, s);
+    for (int l = 0; l < hp_.n_layer; l++) {
+      const LayerDev& Ld = L_[l];
+      const int hd = Ld.hd;
+      launch_prefill_gemm(Ld.qkv[0].w, pf_xq_, XS, T, pf_out_, Ld.qkv_rows, s);
+      PrefillQK qk;
+      qk.qkv = pf_out_;
+      qk.qkv_stride = Ld.qkv_rows;
+      qk.k_off = Ld.k_off;
+      qk.v_off = Ld.v_off;
+      qk.n_head = nh_;
+      qk.n_head_kv = nkv_;
+      qk.head_dim = hd;
+      qk.q_norm_w = Ld.q_norm;
+      qk.k_norm_w = Ld.k_norm;
+      qk.rope_cs = Ld.is_swa ? rope_swa_ : rope_glb_;
+      qk.attn_scale = hp_.attn_scale;
+      qk.eps = hp_.eps;
+      qk.q_out = pf_q_;
+      qk.k_cache = Ld.kc;
+      qk.v_cache = Ld.vc;
+      qk.max_ctx = max_ctx_;
+      qk.pos0 = p0;
+      launch_prefill_qk(qk, T, s);
+      PrefillAttn at;
+      at.q = pf_q_;
+      at.k_cache = Ld.kc;
+      at.v_cache = Ld.vc;
+      at.n_head = nh_;
+      at.n_head_kv = nkv_;
+      at.head_dim = hd;
+      at.max_ctx = max_ctx_;
+      at.pos0 = p0;
+      at.xq = pf_xq_;
+      at.xstride = XS;
+      launch_prefill_attn(at, T, s);
+      launch_prefill_gemm(Ld.o.w, pf_xq_, XS, T, pf_out_, E, s);
+      PrefillNorm rn;  // post-attention norm + residual, then ffn_norm
+      rn.y = pf_out_;
+      rn.w_post = Ld.post_attn_norm;
+      rn.resid = pf_resid_;
+      rn.w_next = Ld.ffn_norm;
+      rn.xq = pf_xq_;
+      rn.xstride = XS;
+      rn.n = E;
+      rn.eps = hp_.eps;
+      launch_prefill_norm(rn, T, s);
+      launch_prefill_gemm(Ld.gate_up[0].w, pf_xq_, XS, T, pf_out_, 2 * F, s);
+      launch_prefill_gelu(pf_out_, F, layer_gemv_gelu_group(Ld.gate_up[0].w.cols), pf_xq_, XS, T, s);
+      launch_prefill_gemm(Ld.down.w, pf_xq_, XS, T, pf_out_, E, s);
+      if (l + 1 < hp_.n_layer) {  // post-ffw norm + residual, then the next attn_norm
+        PrefillNorm fn = rn;
+        fn.w_post = Ld.post_ffw_norm;
+        fn.w_next = L_[l + 1].attn_norm;
+        launch_prefill_norm(fn, T, s);
+      }
+    }
+    if (last_chunk) {  // the last token: final residual + output_norm -> logits (decode tail)
+      NormOut o2;
+      o2.xn = xn_;
+      if (embd_.type == T_F16) o2.x16 = act_.x16;
+      launch_residual_norm(pf_out_ + (size_t)(T - 1) * E, L_.back().post_ffw_norm, pf_resid_ + (size_t)(T - 1) * E,
+                           out_norm_, o2, E, hp_.eps, false, s);
+      record_logits(s);
+    }
+  }
 }
 
 // Fast path with every projection a gemv_q4_0_layer launch: 5 launches per
@@ -677,9 +807,14 @@ void Session::forward(const int32_t* tokens, int n, int pos, float* logits, int3
   if (pos < 0 || pos + n > max_ctx_) throw status_error(LLMI_E_RANGE, "forward: context overflow");
   for (int i = 0; i < n; i++)
     if (tokens[i] < 0 || tokens[i] >= vocab_) throw status_error(LLMI_E_RANGE, "forward: token id out of range");
-  for (int i = 0; i < n; i++) {
-    set_token_pos(tokens[i], pos + i, i == 0);
-    run_step();
+  if (n > 1 && prefill_ok_ && getenv("LLMI_NO_PREFILL") == nullptr) {
+    set_token_pos(tokens[n - 1], pos + n - 1, true);  // what the token loop leaves behind
+    prefill(tokens, n, pos);
+  } else {
+    for (int i = 0; i < n; i++) {
+      set_token_pos(tokens[i], pos + i, i == 0);
+      run_step();
+    }
   }
   // every rank of a tensor-parallel group gathers the full logits (collective)
   if (tp_) coll_->all_gather(logits_, (size_t)v_sh_ * sizeof(float), stream_);
@@ -712,6 +847,7 @@ void Session::info(llmi_session_info* o) const {
   o->weight_bytes = weight_bytes_;
   o->tp_rank = tp_rank_;
   o->tp_size = tp_size_;
+  o->batched_prefill = prefill_ok_ ? 1 : 0;
   size_t b = logits_w_.bytes;  // this rank's bytes
   for (const auto& l : L_) {
     for (const auto& p : l.qkv) b += p.w.bytes;

@@ -68,6 +68,9 @@ class Session {
   void alloc_buffers();
   void build_rope_tables();
   void record_step(hipStream_t s);
+  void record_logits(hipStream_t s);  // xn_ / act_.x16 -> logits, argmax key, token feedback
+  void prefill(const int32_t* tokens, int n, int pos);  // batched (k_prefill.hip)
+  void ensure_prefill_buffers(int cap);
   void record_layers(hipStream_t s, bool x_q8);
   void record_layers_fused(hipStream_t s, bool x_q8);
   void prepare_act(uint32_t wtype, const float* x, int n, ActBuf& act, hipStream_t s);
@@ -127,6 +130,13 @@ class Session {
   int nh_ = 0, nkv_ = 0, kv0_ = 0, e_sh_ = 0, f_sh_ = 0, v_sh_ = 0, v_rows_ = 0;
   DevWeight logits_w_;  // the logits GEMV's rows: embd_ itself, or this rank's slice
   bool own_logits_w_ = false;
+  // batched prefill (fast fused path, one device): chunk buffers
+  bool prefill_ok_ = false;
+  int pf_cap_ = 0, pf_xs_ = 0, pf_ostride_ = 0;
+  int32_t* pf_tokens_ = nullptr;
+  float *pf_resid_ = nullptr, *pf_out_ = nullptr;
+  XBlock* pf_xq_ = nullptr;
+  uint16_t* pf_q_ = nullptr;
 };
 
 }  // namespace llmi

@@ -51,6 +51,55 @@ struct LayerGemv {
   float* hid = nullptr;     // GELU: [rows / 2] = GELU(gate) * up
 };
 bool layer_gemv_supported(const DevWeight& w, int role);
+// ---- batched prefill (k_prefill.hip) ----
+struct PrefillNorm {  // per token: embedding (table != null) or residual + norm, then x -> Q8_0
+  const uint8_t* table = nullptr;
+  uint32_t emb_type = 0;
+  size_t row_bytes = 0;
+  const int32_t* tokens = nullptr;
+  float emb_scale = 1.0f;
+  const float* y = nullptr;       // [T][n] projection output (residual mode)
+  const float* w_post = nullptr;  // null: plain residual add
+  float* resid = nullptr;         // [T][n] in/out
+  const float* w_next = nullptr;
+  XBlock* xq = nullptr;           // [T][xstride] out
+  int xstride = 0, n = 0;
+  double eps = 0;
+};
+struct PrefillGemm {
+  const uint4* qs = nullptr;
+  const uint16_t* wd = nullptr;
+  int rows = 0, nb = 0, slab = 0;
+  const XBlock* x = nullptr;
+  int xstride = 0, T = 0;
+  float* out = nullptr;
+  int ostride = 0;
+};
+struct PrefillQK {
+  const float* qkv = nullptr;  // [T][qkv_stride]
+  int qkv_stride = 0, k_off = 0, v_off = 0, n_head = 0, n_head_kv = 0, head_dim = 0;
+  const float *q_norm_w = nullptr, *k_norm_w = nullptr, *rope_cs = nullptr;
+  float attn_scale = 1.0f;
+  double eps = 0;
+  uint16_t* q_out = nullptr;  // [T][n_head][head_dim] f16, scaled
+  uint16_t *k_cache = nullptr, *v_cache = nullptr;
+  int max_ctx = 0, pos0 = 0;
+};
+struct PrefillAttn {
+  const uint16_t* q = nullptr;
+  const uint16_t *k_cache = nullptr, *v_cache = nullptr;
+  int n_head = 0, n_head_kv = 0, head_dim = 0, max_ctx = 0, pos0 = 0;
+  XBlock* xq = nullptr;  // [T][xstride]: the heads' outputs as Q8_0 blocks
+  int xstride = 0;
+};
+void launch_prefill_norm(const PrefillNorm& a, int T, hipStream_t s);
+bool prefill_gemm_supported(const DevWeight& w);
+void launch_prefill_gemm(const DevWeight& w, const XBlock* x, int xstride, int T, float* out, int ostride,
+                         hipStream_t s);
+void launch_prefill_qk(const PrefillQK& a, int T, hipStream_t s);
+void launch_prefill_attn(const PrefillAttn& a, int T, hipStream_t s);
+void launch_prefill_gelu(const float* gu, int F, int H, XBlock* xq, int xstride, int T, hipStream_t s);
+
 // the weight layout the launch-table entry for (w's shape, role) reads
 int layer_gemv_slab(const DevWeight& w, int role);
 // GELU role: hidden units per work-group (the gate/up interleave group), 0 if unsupported

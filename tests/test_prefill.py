@@ -1,0 +1,68 @@
+"""Batched prefill (llm_inference_amd/csrc/k_prefill.hip).
+
+forward(prompt) with n > 1 tokens runs the prompt as one batch: int8 MFMA
+GEMMs over the tokens, per-token norms / rope / KV append, causal attention
+over the cache.  Checked here:
+  * the same logits bit for bit whatever the chunking (a token's GEMM row and
+    attention do not depend on the other tokens of the chunk);
+  * against the token loop (LLMI_NO_PREFILL=1, the decode kernels): the fast
+    mode budget of tests/test_hip_model.py (6e-2) and the same greedy ids;
+  * against the oracle (the reference, pinned) through
+    tests/test_hip_model.py::test_mini_models_vs_oracle, whose forward(prompt)
+    now runs this path and whose greedy continuation reads the KV cache the
+    prefill wrote.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+FAST_VS_REF = 6e-2
+
+
+def _model(g, monkeypatch, no_prefill=False, chunk=None, max_ctx=1024):
+    from llm_inference_amd.model import Model
+    if no_prefill:
+        monkeypatch.setenv("LLMI_NO_PREFILL", "1")
+    else:
+        monkeypatch.delenv("LLMI_NO_PREFILL", raising=False)
+    if chunk:
+        monkeypatch.setenv("LLMI_PREFILL_CHUNK", str(chunk))
+    else:
+        monkeypatch.delenv("LLMI_PREFILL_CHUNK", raising=False)
+    return Model(g, exact=False, max_ctx=max_ctx)
+
+
+@pytest.mark.parametrize("cfg_name,n_prompt", [("mini-1b", 40), ("mini-4b", 300)])
+def test_prefill_vs_token_loop(cfg_name, n_prompt, monkeypatch):
+    from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
+    cfg = CONFIGS[cfg_name]
+    g = build_gemma3_gguf(cfg, seed=21)
+    prompt = np.random.default_rng(3).integers(4, cfg.vocab, n_prompt).astype(np.int32)
+    mp = _model(g, monkeypatch)
+    assert mp.get_info().batched_prefill == 1
+    lp = mp.forward(prompt, 0)
+    ids_p = mp.generate(int(np.argmax(lp)), n_prompt, 8)
+    ml = _model(g, monkeypatch, no_prefill=True)
+    ll = ml.forward(prompt, 0)
+    ids_l = ml.generate(int(np.argmax(ll)), n_prompt, 8)
+    d = float(np.abs(lp - ll).max())
+    print(f"{cfg_name} n={n_prompt}: max|prefill - token loop| = {d:.3g}")
+    assert d <= FAST_VS_REF
+    assert int(np.argmax(lp)) == int(np.argmax(ll))
+    assert ids_p.tolist() == ids_l.tolist()
+
+
+def test_prefill_chunking_is_exact(monkeypatch):
+    from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
+    cfg = CONFIGS["mini-4b"]
+    g = build_gemma3_gguf(cfg, seed=5)
+    prompt = np.random.default_rng(9).integers(4, cfg.vocab, 150).astype(np.int32)
+    ref = _model(g, monkeypatch).forward(prompt, 0)
+    for chunk in (1, 7, 64, 129):
+        got = _model(g, monkeypatch, chunk=chunk).forward(prompt, 0)
+        np.testing.assert_array_equal(got, ref)
+    # a prompt continued at a later position (keys from an earlier forward)
+    m = _model(g, monkeypatch)
+    m.forward(prompt[:100], 0)
+    tail = m.forward(prompt[100:], 100)
+    np.testing.assert_array_equal(tail, ref)

@@ -48,12 +48,15 @@ def _run_ranks(g, tp, prompt, n_gen, max_ctx=64):
 
 @pytest.mark.parametrize("cfg_name,tp", [("mini-1b", 2), ("mini-1b", 4), ("mini-4b", 2), ("mini-4b", 4),
                                          ("mini-4b", 8)])
-def test_sharded_matches_whole_model(cfg_name, tp):
+def test_sharded_matches_whole_model(cfg_name, tp, monkeypatch):
     from llm_inference_amd.model import Model
     from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
     cfg = CONFIGS[cfg_name]
     g = build_gemma3_gguf(cfg, seed=3)
     prompt = np.random.default_rng(5).integers(4, cfg.vocab, 12).astype(np.int32)
+    # sharded sessions run the prompt through the decode kernels (the batched
+    # prefill is single-device): compare with the whole model doing the same
+    monkeypatch.setenv("LLMI_NO_PREFILL", "1")
     whole = Model(g, exact=False, max_ctx=64)
     ref = whole.forward(prompt, 0)
     ref_toks = whole.generate(int(np.argmax(ref)), len(prompt), 11)
@@ -73,13 +76,14 @@ def test_sharded_matches_whole_model(cfg_name, tp):
         assert np.array_equal(lg, out[0][0])
 
 
-def test_rccl_single_rank_in_graph():
+def test_rccl_single_rank_in_graph(monkeypatch):
     """ncclAllGather captured into the per-token hipGraph (one-rank
     communicator): identical to the whole-model session."""
     from llm_inference_amd.model import Model, tp_unique_id
     from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
     cfg = CONFIGS["mini-4b"]
     g = build_gemma3_gguf(cfg, seed=4)
+    monkeypatch.setenv("LLMI_NO_PREFILL", "1")  # the sharded session decodes the prompt token by token
     prompt = np.random.default_rng(1).integers(4, cfg.vocab, 6).astype(np.int32)
     whole = Model(g, exact=False, max_ctx=64)
     ref = whole.forward(prompt, 0)
