@@ -47,6 +47,8 @@ def parse():
     p.add_argument("--no-graph", action="store_true", help="eager launches (for kernel tracers)")
     p.add_argument("--mode", choices=["tp", "replicas"], default="tp",
                    help="N>1: row-sharded tensor parallel (one stream) or independent replicas")
+    p.add_argument("--quant", choices=["q4_0", "q4_k_m", "q8_0"], default="q4_0",
+                   help="weight types: q4_0 (headline), q4_k_m (Q4_K + Q6_K v/down), q8_0 (BASELINE configs[3])")
     return p.parse_args()
 
 
@@ -134,7 +136,10 @@ def main():
 
     cfg = CONFIGS[a.config]
     t0 = time.time()
-    g = build_gemma3_gguf(cfg, seed=1234)
+    from llm_inference_amd.gguf import TensorType as TT
+    qkw = {"q4_0": {}, "q4_k_m": dict(wtype=TT.Q4_K, wtypes={"v": TT.Q6_K, "down": TT.Q6_K}),
+           "q8_0": dict(wtype=TT.Q8_0)}[a.quant]
+    g = build_gemma3_gguf(cfg, seed=1234, **qkw)
     t_build = time.time() - t0
     max_ctx = a.prefill + a.warmup + a.steps + 8
     tp_kw = {}
@@ -174,7 +179,8 @@ def main():
     mean_ctx = pos + a.steps / 2
     tok_bytes = info.bytes_per_token + info.kv_bytes_per_pos * mean_ctx
     out = {
-        "metric": "decode tokens/sec (Gemma-3 4B Q4_0 shape, greedy)",
+        "metric": ("decode tokens/sec (Gemma-3 4B Q4_0 shape, greedy)" if (a.config, a.quant) == ("gemma-3-4b", "q4_0")
+                   else f"decode tokens/sec ({cfg.name} {a.quant} shape, greedy)"),
         "value": round(value, 3),
         "unit": "tokens/s",
         "n_gpus": d.world,
@@ -187,7 +193,7 @@ def main():
         "dtype": "q4_0 x q8_0 int8-dot, fp32 accumulate; f16 logits",
         "data": "synthetic (random-init weights of the gemma-3-4b-it-q4_0 architecture, seeded prompt ids)",
         "config": {
-            "workload": f"{cfg.name}-q4_0 greedy decode after a {a.prefill}-token prefill (BASELINE configs[2])",
+            "workload": f"{cfg.name}-{a.quant} greedy decode after a {a.prefill}-token prefill (BASELINE configs[2])",
             "prefill_tokens": a.prefill, "decode_tokens": a.steps, "mode": "exact" if a.exact else "fast",
             "parallelism": (f"tp{d.world} (row-sharded, RCCL all-gather)" if tp else f"replicas{d.world}")
                            if d.world > 1 else "single",

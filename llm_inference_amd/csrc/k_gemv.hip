@@ -428,6 +428,108 @@ __global__ __launch_bounds__(256) void gemv_q6_k_exact(const uint8_t* __restrict
   out[row] = sum;
 }
 
+// ---- fast K-quant GEMVs: row-bound lanes (R rows per wave, L = 64/R lanes
+// per row), one 32-element sub-block per lane per pass, integer 4-way dots
+// against the Q8_K activation (ops.cpp:142-178), fp32 per-lane sums reduced
+// across the row's lanes (the reference's order is kept only by the exact
+// kernels above).
+__device__ __forceinline__ int ld_i32u(const uint8_t* p) {  // 4-byte aligned
+  return *reinterpret_cast<const int*>(p);
+}
+
+template <int R>
+__device__ __forceinline__ float kq_row_sum(float v) {  // sum over the row's L lanes, result in every lane of it
+  constexpr int L = 64 / R;
+  if constexpr (L >= 2) v += dpp_f<DPP_QUAD_1032>(v);
+  if constexpr (L >= 4) v += dpp_f<DPP_QUAD_2301>(v);
+  if constexpr (L >= 8) v += dpp_f<DPP_ROW_HALF_MIRROR>(v);
+  if constexpr (L >= 16) v += dpp_f<DPP_ROW_MIRROR>(v);
+  if constexpr (L >= 32) v += __shfl_xor(v, 16);
+  if constexpr (L >= 64) v += __shfl_xor(v, 32);
+  return v;
+}
+
+// Q4_K (ops.cpp:614-697): 144-B super-blocks of 256: d, dmin (f16), 12 bytes of
+// 6-bit scales/mins, 128 bytes of nibbles (sub-block 2c: low nibbles of
+// qs[32c..32c+31], 2c+1: their high nibbles)
+template <int R>
+__global__ __launch_bounds__(256) void gemv_q4_k_fast(const uint8_t* __restrict__ wq, int rows, int nsb,
+                                                      const uint8_t* __restrict__ xk, float* __restrict__ out) {
+  constexpr int L = 64 / R;
+  const int lane = threadIdx.x & 63, wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int row = wave * R + lane / L, j = lane % L;
+  const uint8_t* wr = wq + (size_t)min(row, rows - 1) * nsb * 144;
+  float acc = 0.0f;
+  for (int u = j; u < nsb * 8; u += L) {
+    const int b = u >> 3, sb = u & 7;
+    const uint8_t* blk = wr + (size_t)b * 144;
+    const uint4 hdr = *reinterpret_cast<const uint4*>(blk);
+    const uint4 q0 = *reinterpret_cast<const uint4*>(blk + 16 + 32 * (sb >> 1));
+    const uint4 q1 = *reinterpret_cast<const uint4*>(blk + 32 + 32 * (sb >> 1));
+    const uint8_t* xb = xk + (size_t)b * 292;
+    const float xd = *reinterpret_cast<const float*>(xb);
+    const uint8_t* xq = xb + 4 + 32 * sb;
+    const int16_t* bs = reinterpret_cast<const int16_t*>(xb + 260);
+    const int sh = (sb & 1) * 4;
+    int a = 0;
+    a = sdot4((int)((q0.x >> sh) & 0x0F0F0F0Fu), ld_i32u(xq + 0), a);
+    a = sdot4((int)((q0.y >> sh) & 0x0F0F0F0Fu), ld_i32u(xq + 4), a);
+    a = sdot4((int)((q0.z >> sh) & 0x0F0F0F0Fu), ld_i32u(xq + 8), a);
+    a = sdot4((int)((q0.w >> sh) & 0x0F0F0F0Fu), ld_i32u(xq + 12), a);
+    a = sdot4((int)((q1.x >> sh) & 0x0F0F0F0Fu), ld_i32u(xq + 16), a);
+    a = sdot4((int)((q1.y >> sh) & 0x0F0F0F0Fu), ld_i32u(xq + 20), a);
+    a = sdot4((int)((q1.z >> sh) & 0x0F0F0F0Fu), ld_i32u(xq + 24), a);
+    a = sdot4((int)((q1.w >> sh) & 0x0F0F0F0Fu), ld_i32u(xq + 28), a);
+    uint8_t scb[12];
+    __builtin_memcpy(scb, reinterpret_cast<const uint8_t*>(&hdr) + 4, 12);
+    int sc, mn;
+    scale_min_k4(sb, scb, sc, mn);
+    const float d = h2f((uint16_t)(hdr.x & 0xFFFF)) * xd, dmin = h2f((uint16_t)(hdr.x >> 16)) * xd;
+    acc += fmaf((float)a, d * (float)sc, -((dmin * (float)mn) * (float)(bs[2 * sb] + bs[2 * sb + 1])));
+  }
+  acc = kq_row_sum<R>(acc);
+  if (j == 0 && row < rows) out[row] = acc;
+}
+
+// Q6_K (ops.cpp:699-785): 210-B super-blocks: ql[128], qh[64], int8 scales[16]
+// (one per 16 elements), d (f16).  Lane sub-block m (elements 32m..32m+31):
+// half n = m / 4, quarter jq = m % 4 -> ql[64n + 32(jq & 1) + l] nibble jq >= 2,
+// qh[32n + l] bits 2jq..2jq+1, scales[8n + 2jq + (l >= 16)].
+template <int R>
+__global__ __launch_bounds__(256) void gemv_q6_k_fast(const uint8_t* __restrict__ wq, int rows, int nsb,
+                                                      const uint8_t* __restrict__ xk, float* __restrict__ out) {
+  constexpr int L = 64 / R;
+  const int lane = threadIdx.x & 63, wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int row = wave * R + lane / L, j = lane % L;
+  const uint8_t* wr = wq + (size_t)min(row, rows - 1) * nsb * 210;
+  float acc = 0.0f;
+  for (int u = j; u < nsb * 8; u += L) {
+    const int b = u >> 3, m = u & 7, n = m >> 2, jq = m & 3;
+    const uint8_t* blk = wr + (size_t)b * 210;  // 210-B blocks: 2-byte alignment only
+    const uint8_t* ql = blk + 64 * n + 32 * (jq & 1);
+    const uint8_t* qh = blk + 128 + 32 * n;
+    const int8_t* sc = reinterpret_cast<const int8_t*>(blk + 192 + 8 * n + 2 * jq);
+    const uint8_t* xb = xk + (size_t)b * 292;
+    const float xd = *reinterpret_cast<const float*>(xb);
+    const uint8_t* xq = xb + 4 + 32 * m;
+    const int lsh = (jq >> 1) * 4, hsh = 2 * jq;
+    int dot[2] = {0, 0};
+#pragma unroll
+    for (int w4 = 0; w4 < 8; w4++) {
+      const uint32_t lw = (uint32_t)ql[4 * w4] | ((uint32_t)ql[4 * w4 + 1] << 8) | ((uint32_t)ql[4 * w4 + 2] << 16) |
+                          ((uint32_t)ql[4 * w4 + 3] << 24);
+      const uint32_t hw = (uint32_t)qh[4 * w4] | ((uint32_t)qh[4 * w4 + 1] << 8) | ((uint32_t)qh[4 * w4 + 2] << 16) |
+                          ((uint32_t)qh[4 * w4 + 3] << 24);
+      const uint32_t v = ((lw >> lsh) & 0x0F0F0F0Fu) | (((hw >> hsh) & 0x03030303u) << 4);  // 0..63 per byte
+      const int q = (int)((v + 0x60606060u) ^ 0x80808080u);                                   // - 32 per byte
+      dot[w4 >> 2] = sdot4(q, ld_i32u(xq + 4 * w4), dot[w4 >> 2]);
+    }
+    acc = fmaf((float)(sc[0] * dot[0] + sc[1] * dot[1]), h2f((uint16_t)(blk[208] | (blk[209] << 8))) * xd, acc);
+  }
+  acc = kq_row_sum<R>(acc);
+  if (j == 0 && row < rows) out[row] = acc;
+}
+
 __global__ __launch_bounds__(256) void gemv_q5_0_exact(const uint8_t* __restrict__ wq, int rows, int nb,
                                                        const float* __restrict__ x, float* __restrict__ out) {
   const int row = blockIdx.x * blockDim.x + threadIdx.x;
@@ -563,13 +665,32 @@ void launch_gemv(const DevWeight& w, const ActBuf& x, float* o, GemvMode mode, h
       break;
     }
     case T_Q4_K:
-      hipLaunchKernelGGL(gemv_q4_k_exact, dim3((rows + 255) / 256), dim3(256), 0, s, (const uint8_t*)w.qs, rows,
-                         w.cols / 256, x.q8k, o);
+    case T_Q6_K: {
+      const int nsb = w.cols / 256;
+      if (mode == GEMV_EXACT) {
+        if (w.type == T_Q4_K)
+          hipLaunchKernelGGL(gemv_q4_k_exact, dim3((rows + 255) / 256), dim3(256), 0, s, (const uint8_t*)w.qs, rows,
+                             nsb, x.q8k, o);
+        else
+          hipLaunchKernelGGL(gemv_q6_k_exact, dim3((rows + 255) / 256), dim3(256), 0, s, (const uint8_t*)w.qs, rows,
+                             nsb, x.q8k, o);
+        break;
+      }
+      // lanes per row: enough for one pass over the row's 8 nsb sub-blocks
+      const int units = nsb * 8;
+      const int R = units >= 64 ? 1 : units >= 32 ? 2 : units >= 16 ? 4 : 8;
+      const dim3 grid((rows + 4 * R - 1) / (4 * R));
+#define LLMI_KQ(RR)                                                                                             \
+  case RR:                                                                                                      \
+    if (w.type == T_Q4_K)                                                                                       \
+      hipLaunchKernelGGL(gemv_q4_k_fast<RR>, grid, dim3(256), 0, s, (const uint8_t*)w.qs, rows, nsb, x.q8k, o); \
+    else                                                                                                        \
+      hipLaunchKernelGGL(gemv_q6_k_fast<RR>, grid, dim3(256), 0, s, (const uint8_t*)w.qs, rows, nsb, x.q8k, o); \
+    break;
+      switch (R) { LLMI_KQ(1) LLMI_KQ(2) LLMI_KQ(4) LLMI_KQ(8) }
+#undef LLMI_KQ
       break;
-    case T_Q6_K:
-      hipLaunchKernelGGL(gemv_q6_k_exact, dim3((rows + 255) / 256), dim3(256), 0, s, (const uint8_t*)w.qs, rows,
-                         w.cols / 256, x.q8k, o);
-      break;
+    }
     case T_Q5_0:
       hipLaunchKernelGGL(gemv_q5_0_exact, dim3((rows + 255) / 256), dim3(256), 0, s, (const uint8_t*)w.qs, rows,
                          w.cols / 32, x.xf, o);

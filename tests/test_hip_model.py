@@ -144,3 +144,35 @@ def test_unfused_fast_path_matches_fused(oracle, monkeypatch):
     ideal = oracle.model(g, n_threads=8, max_ctx=64, attn_f64=True)
     np.testing.assert_allclose(lf, ideal.forward(prompt, 0), atol=FAST_VS_REF, rtol=0)
     assert int(np.argmax(lf)) == int(np.argmax(lp))
+
+
+@pytest.mark.parametrize("quant", ["q4_k_m", "q8_0"])
+def test_kquant_and_q8_models_vs_oracle(oracle, quant, exact):
+    """BASELINE configs[3]: Gemma-3 4B Q4_K_M (Q4_K projections, Q6_K v/down)
+    and 1B Q8_0 layer shapes through the session (unfused path: Q8_K / Q8_0
+    activations, fast K-quant GEMVs in fast mode), vs the oracle: greedy ids
+    identical, logits within the module's tolerances."""
+    from llm_inference_amd.gguf import TensorType as TT
+    from llm_inference_amd.model import Model
+    from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
+    if quant == "q4_k_m":
+        cfg = CONFIGS["mini-4b"]
+        g = build_gemma3_gguf(cfg, seed=8, wtype=TT.Q4_K, wtypes={"v": TT.Q6_K, "down": TT.Q6_K})
+    else:
+        cfg = CONFIGS["mini-1b"]
+        g = build_gemma3_gguf(cfg, seed=8, wtype=TT.Q8_0, embd_type=TT.Q8_0)
+    om = oracle.model(g, n_threads=8, max_ctx=64)
+    ideal = oracle.model(g, n_threads=8, max_ctx=64, attn_f64=True)
+    m = Model(g, exact=exact, max_ctx=64)
+    prompt = np.random.default_rng(4).integers(4, cfg.vocab, 10).astype(np.int32)
+    ref = om.forward(prompt, 0)
+    got = m.forward(prompt, 0)
+    check(got, ref, ideal.forward(prompt, 0), exact)
+    toks_ref = [int(np.argmax(ref))]
+    pos = len(prompt)
+    for _ in range(6):
+        lg = om.forward([toks_ref[-1]], pos)
+        pos += 1
+        toks_ref.append(int(np.argmax(lg)))
+    toks = m.generate(int(np.argmax(got)), len(prompt), 6)
+    assert [int(np.argmax(got))] + toks.tolist() == toks_ref
