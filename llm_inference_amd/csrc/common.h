@@ -170,6 +170,11 @@ __device__ __forceinline__ float half_max(float v) {
   const float lo = fmaxf(lane_f(v, 0), lane_f(v, 16)), hi = fmaxf(lane_f(v, 32), lane_f(v, 48));
   return (threadIdx.x & 32) ? hi : lo;
 }
+__device__ __forceinline__ float half_sum(float v) {
+  v = row16_sum(v);
+  const float lo = lane_f(v, 0) + lane_f(v, 16), hi = lane_f(v, 32) + lane_f(v, 48);
+  return (threadIdx.x & 32) ? hi : lo;
+}
 __device__ __forceinline__ int half_isum(int v) {
   v = row16_isum(v);
   const int lo = __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16);

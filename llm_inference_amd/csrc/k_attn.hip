@@ -151,19 +151,49 @@ struct RowLd {
   float v[DPL], nw[DPL], c[DPL], s[DPL];
 };
 
+template <int N>
+__device__ __forceinline__ void ld_vec(float (&dst)[N], const float* __restrict__ p) {  // N consecutive floats
+  if constexpr (N == 4) {
+    const float4 v = *reinterpret_cast<const float4*>(p);
+    dst[0] = v.x; dst[1] = v.y; dst[2] = v.z; dst[3] = v.w;
+  } else if constexpr (N == 2) {
+    const float2 v = *reinterpret_cast<const float2*>(p);
+    dst[0] = v.x; dst[1] = v.y;
+  } else {
+#pragma unroll
+    for (int d = 0; d < N; d++) dst[d] = p[d];
+  }
+}
+
 template <int HD>
 __device__ __forceinline__ void row_load(RowLd<HD>& r, const float* __restrict__ src, const float* __restrict__ nw,
                                          const float* __restrict__ cs) {
   constexpr int DPL = RowLd<HD>::DPL;
   const int lane = threadIdx.x & 63;
+  // elements i0 .. i0 + DPL - 1, one vector load per operand (lanes past the
+  // row re-read its last elements: unconditional loads, masked later)
+  const int i0 = min(lane, HD / DPL - 1) * DPL;
+  const int j0 = i0 < HD / 2 ? i0 : i0 - HD / 2;  // DPL divides HD / 2
+  ld_vec<DPL>(r.v, src + i0);
+  ld_vec<DPL>(r.nw, nw + i0);
+  // (cos, sin) pairs of elements j0 .. j0 + DPL - 1: 2 DPL consecutive floats
+  float cs2[2 * DPL];
+  if constexpr (DPL == 4) {
+    float lo[4], hi[4];
+    ld_vec<4>(lo, cs + 2 * j0);
+    ld_vec<4>(hi, cs + 2 * j0 + 4);
+#pragma unroll
+    for (int d = 0; d < 4; d++) {
+      cs2[d] = lo[d];
+      cs2[4 + d] = hi[d];
+    }
+  } else {
+    ld_vec<2 * DPL>(cs2, cs + 2 * j0);
+  }
 #pragma unroll
   for (int d = 0; d < DPL; d++) {
-    const int i = min(lane * DPL + d, HD - 1);  // clamped, unconditional loads (lanes >= HD are masked later)
-    const int j = i < HD / 2 ? i : i - HD / 2;
-    r.v[d] = src[i];
-    r.nw[d] = nw[i];
-    r.c[d] = cs[2 * j];
-    r.s[d] = cs[2 * j + 1];
+    r.c[d] = cs2[2 * d];
+    r.s[d] = cs2[2 * d + 1];
   }
 }
 
@@ -227,33 +257,45 @@ void attn_set_trace(unsigned long long* p) { LLMI_HIP(hipMemcpyToSymbol(HIP_SYMB
   } while (0)
 #endif
 
-template <int HD, int G, bool FUSED>
-__global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa) {
+template <int G>
+constexpr int attn_tp() {  // threads per (query head, key) pair in QK^T
+  return 4 / G;
+}
+template <int HD, int G>
+constexpr int attn_ks() {  // padded K row stride (halves)
+  return HD + 8 * (attn_tp<G>() < HD / 8 ? attn_tp<G>() : HD / 8);
+}
+template <int HD, int G>
+constexpr int attn_kp() {  // PV key residue classes
+  return 256 / (HD / 4);
+}
+
+template <int HD, int G, bool FUSED, int TK>
+__device__ __forceinline__ void attn_split_body(const AttnArgs& a, const QKVArgs& qa, uint16_t* __restrict__ s_k,
+                                                uint16_t* __restrict__ s_v, float* __restrict__ s_red) {
   constexpr int NS = ATTN_NSPLIT;
+  static_assert(TK == 32 || TK == 64, "key tile: 32 or 64 keys");
   constexpr int CH = HD / 8;                         // 16-byte chunks per row
   constexpr int TP0 = 4 / G;                         // threads per (head, key) pair
   constexpr int TP = TP0 < CH ? TP0 : CH;
   constexpr int KS = HD + 8 * TP;                    // padded K row stride (halves)
-  constexpr int NLD = (64 * CH + 255) / 256;         // chunk loads per thread per tile
+  constexpr int NLD = (TK * CH + 255) / 256;         // chunk loads per thread per tile
   constexpr int NTD = HD / 4;                        // PV: 4 head dims per thread, NTD threads per key class
   constexpr int KP = 256 / NTD;                      // key residue classes in PV
   constexpr int DPL = RowLd<HD>::DPL;
-  __shared__ __attribute__((aligned(16))) uint16_t s_k[64 * KS];
-  __shared__ __attribute__((aligned(16))) uint16_t s_v[64 * HD];
+  static_assert(KS == attn_ks<HD, G>() && KP == attn_kp<HD, G>(), "LDS carve-up");
   __shared__ __attribute__((aligned(16))) uint16_t s_q[G][HD];
   __shared__ __attribute__((aligned(16))) uint16_t s_new[FUSED ? 2 : 1][FUSED ? HD : 8];
-  __shared__ float s_p[G][64];
+  __shared__ float s_p[G][TK];
   __shared__ float s_alpha[G];
-  __shared__ __attribute__((aligned(16))) float s_red[KP > 1 ? KP * G * HD : 4];
-  __shared__ float s_ml[G][NS][2];
   __shared__ int s_last;
-  static_assert(64 * KS * 2 >= G * HD * 4, "s_k doubles as the merged-output staging");
+  __shared__ __attribute__((aligned(16))) float s_outbuf[TK * KS * 2 >= G * HD * 4 ? 1 : G * HD];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   ATTN_MARK(0);
   const int hkv = blockIdx.x, c = blockIdx.y;
   const int pos = *a.d_pos;
   const int n_keys = pos + 1;
-  const bool own_new = FUSED && (pos / 64) % NS == c;
+  const bool own_new = FUSED && (pos / TK) % NS == c;
   const uint4* kb = reinterpret_cast<const uint4*>(a.k_cache + (size_t)hkv * a.max_ctx * HD);
   const uint4* vb = reinterpret_cast<const uint4*>(a.v_cache + (size_t)hkv * a.max_ctx * HD);
   uint4 kr[NLD], vr[NLD];
@@ -262,8 +304,8 @@ __global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa)
   auto load_tile = [&](int tl) {
 #pragma unroll
     for (int i = 0; i < NLD; i++) {
-      const int k = min(i * 256 + t, 64 * CH - 1);
-      const int key = min(tl * 64 + k / CH, a.max_ctx - 1);
+      const int k = min(i * 256 + t, TK * CH - 1);
+      const int key = min(tl * TK + k / CH, a.max_ctx - 1);
       const size_t gi = (size_t)key * CH + k % CH;
       kr[i] = kb[gi];
       vr[i] = vb[gi];
@@ -272,7 +314,7 @@ __global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa)
   auto mask_tile = [&](int tl) {
 #pragma unroll
     for (int i = 0; i < NLD; i++) {
-      const bool ok = tl * 64 + (i * 256 + t) / CH < n_keys;
+      const bool ok = tl * TK + (i * 256 + t) / CH < n_keys;
       if (!ok) kr[i] = make_uint4(0, 0, 0, 0);
       if (!ok) vr[i] = make_uint4(0, 0, 0, 0);
     }
@@ -286,8 +328,7 @@ __global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa)
     if (w < G) row_load<HD>(rq, qa.qkv + (size_t)(hkv * G + w) * HD, qa.q_norm_w, cs);
     if (w == (G & 3)) row_load<HD>(rk, qa.qkv + qa.k_off + (size_t)hkv * HD, qa.k_norm_w, cs);
     if (w == ((G + 1) & 3)) {
-#pragma unroll
-      for (int d = 0; d < DPL; d++) vrow[d] = qa.qkv[qa.v_off + (size_t)hkv * HD + min(lane * DPL + d, HD - 1)];
+      ld_vec<DPL>(vrow, qa.qkv + qa.v_off + (size_t)hkv * HD + min(lane, HD / DPL - 1) * DPL);
     }
   }
   int tile = c;
@@ -332,29 +373,29 @@ __global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa)
   const int d_own = 4 * (t % NTD), kp = t / NTD;
   typedef _Float16 h2t __attribute__((ext_vector_type(2)));
   ATTN_MARK(1);
-  for (; tile * 64 < n_keys; tile += NS) {
+  for (; tile * TK < n_keys; tile += NS) {
     mask_tile(tile);
     __syncthreads();  // previous tile's LDS reads done (first time: s_q / s_new written)
 #pragma unroll
     for (int i = 0; i < NLD; i++) {
       const int k = i * 256 + t;
       const int j = k / CH, pc = k % CH;
-      if (k < 64 * CH && !(FUSED && tile * 64 + j == pos)) {
+      if (k < TK * CH && !(FUSED && tile * TK + j == pos)) {
         *reinterpret_cast<uint4*>(&s_k[j * KS + pc * 8]) = kr[i];
         *reinterpret_cast<uint4*>(&s_v[j * HD + pc * 8]) = vr[i];
       }
     }
-    if (FUSED && tile == pos / 64 && t < CH) {  // the new row, written in this launch
-      const int j = pos % 64;
+    if (FUSED && tile == pos / TK && t < CH) {  // the new row, written in this launch
+      const int j = pos % TK;
       *reinterpret_cast<uint4*>(&s_k[j * KS + t * 8]) = reinterpret_cast<const uint4*>(s_new[0])[t];
       *reinterpret_cast<uint4*>(&s_v[j * HD + t * 8]) = reinterpret_cast<const uint4*>(s_new[FUSED ? 1 : 0])[t];
     }
     __syncthreads();
     ATTN_MARK(2);
-    if ((tile + NS) * 64 < n_keys) load_tile(tile + NS);  // next tile in flight during this one's math
-    if (t < G * 64 * TP) {
+    if ((tile + NS) * TK < n_keys) load_tile(tile + NS);  // next tile in flight during this one's math
+    if (t < G * TK * TP) {
       const int pr = t / TP, part = t % TP;
-      const int g = pr / 64, j = pr % 64;
+      const int g = pr / TK, j = pr % TK;
       const uint4* krow = reinterpret_cast<const uint4*>(&s_k[j * KS]);
       const uint4* qrow = reinterpret_cast<const uint4*>(s_q[g]);
       float s0 = 0.0f, s1 = 0.0f;
@@ -369,17 +410,17 @@ __global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa)
       float sc = s0 + s1;
 #pragma unroll
       for (int o = 1; o < TP; o <<= 1) sc += __shfl_xor(sc, o);
-      if (part == 0) s_p[g][j] = tile * 64 + j < n_keys ? sc : -INFINITY;
+      if (part == 0) s_p[g][j] = tile * TK + j < n_keys ? sc : -INFINITY;
     }
     __syncthreads();
     if (w < G) {
-      const float sc = s_p[w][lane];
+      const float sc = lane < TK ? s_p[w][lane] : -INFINITY;
       const float m_new = fmaxf(m_run, wave_max(sc));
       const float p = expf(sc - m_new);  // masked keys: exp(-inf) = 0
       const float alpha = expf(m_run - m_new);  // first tile: exp(-inf) = 0
       l_run = l_run * alpha + wave_sum(p);
       m_run = m_new;
-      s_p[w][lane] = p;
+      if (lane < TK) s_p[w][lane] = p;
       if (lane == 0) s_alpha[w] = alpha;
     }
     __syncthreads();
@@ -390,7 +431,7 @@ __global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa)
       for (int e = 0; e < 4; e++) acc[g][e] *= al;
     }
 #pragma unroll 4
-    for (int j = kp; j < 64; j += KP) {
+    for (int j = kp; j < TK; j += KP) {
       const uint2 vv = *reinterpret_cast<const uint2*>(&s_v[j * HD + d_own]);
       const float v0 = h2f((uint16_t)(vv.x & 0xFFFF)), v1 = h2f((uint16_t)(vv.x >> 16));
       const float v2 = h2f((uint16_t)(vv.y & 0xFFFF)), v3 = h2f((uint16_t)(vv.y >> 16));
@@ -445,10 +486,19 @@ __global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa)
   if (!s_last) return;
 
   // ---- last work-group: merge the NS partials of the G heads -------------
-  // One batch of loads: every thread's partial accumulators for its (g, d)
-  // outputs and the (m, l) pairs; the per-split weights are computed once per
-  // (g, split) instead of per output.  Arithmetic (and order) as before:
-  // w_c = l_c ? exp(m_c - M) : 0, L = sum_c fma(l_c, w_c), o = sum_c fma(v_c, w_c).
+  // One batch of loads: the (m, l) pairs first (the weights are reduced while
+  // the rest lands), then every thread's partial accumulators for its (g, d)
+  // outputs.  w_c = l_c ? exp(m_c - M) : 0, L = sum_c l_c w_c (half-wave
+  // tree), o = sum_c fma(v_c, w_c) in split order, out = o / L.
+  // per (head g, split cc) weight w = l ? exp(m - M_g) : 0 and L_g = sum l w,
+  // by half-wave reductions: lane t holds split t % NS of head t / NS (NS = 32)
+  static_assert(NS == 32, "merge reductions are half-wave wide");
+  float mv = -INFINITY, lv = 0.0f;
+  if (t < G * NS) {
+    const float* pm = part0 + ((size_t)(t / NS) * NS + t % NS) * (HD + 2) + HD;
+    mv = ld_sc1(pm);
+    lv = ld_sc1(pm + 1);
+  }
   constexpr int PAIRS = (G * HD + 255) / 256;
   float v[PAIRS][NS];
 #pragma unroll
@@ -458,35 +508,20 @@ __global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa)
 #pragma unroll
     for (int cc = 0; cc < NS; cc++) v[p][cc] = ld_sc1(pg + (size_t)cc * (HD + 2));
   }
-  float mv = 0.0f, lv = 0.0f;
-  if (t < G * NS) {
-    const float* pm = part0 + ((size_t)(t / NS) * NS + t % NS) * (HD + 2) + HD;
-    mv = ld_sc1(pm);
-    lv = ld_sc1(pm + 1);
-  }
   __shared__ float s_wt[G][NS];
   __shared__ float s_L[G];
-  if (t < G * NS) {
-    s_ml[t / NS][t % NS][0] = mv;
-    s_ml[t / NS][t % NS][1] = lv;
-  }
-  __syncthreads();
   ATTN_MARK(6);
-  if (t < G * NS) {
-    const int g = t / NS;
-    float M = -INFINITY;
-#pragma unroll
-    for (int cc = 0; cc < NS; cc++) M = fmaxf(M, s_ml[g][cc][0]);
-    s_wt[g][t % NS] = lv == 0.0f ? 0.0f : expf(mv - M);
+  if (w < (G * NS + 63) / 64) {  // whole waves
+    const float M = half_max(mv);
+    const float wt = lv == 0.0f ? 0.0f : expf(mv - M);
+    const float L = half_sum(lv * wt);
+    if (t < G * NS) {
+      s_wt[t / NS][t % NS] = wt;
+      if (t % NS == 0) s_L[t / NS] = L;
+    }
   }
   __syncthreads();
-  if (t < G) {
-    float L = 0.0f;
-    for (int cc = 0; cc < NS; cc++) L = fmaf(s_ml[t][cc][1], s_wt[t][cc], L);
-    s_L[t] = L;
-  }
-  __syncthreads();
-  float* s_out = reinterpret_cast<float*>(s_k);  // [G][HD]
+  float* s_out = TK * KS * 2 >= G * HD * 4 ? reinterpret_cast<float*>(s_k) : s_outbuf;  // [G][HD]
 #pragma unroll
   for (int p = 0; p < PAIRS; p++) {
     const int idx = t + p * 256;
@@ -511,6 +546,25 @@ __global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa)
   }
   ATTN_MARK(5);
   if (t == 0) __hip_atomic_store(a.ticket + hkv, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+}
+
+// Key tiles of 32 keys while every split owns at most one tile (short
+// context: half the bytes per work-group before its first score), 64 keys
+// beyond (fewer tile rounds per split).  scripts/ab A/B, 4B shapes: pos 100
+// 7.8 vs 9.0 us, pos 700 8.3 vs 9.2 us with 32-key tiles; 64-key tiles win
+// from pos ~1000 (2000: 9.9 vs 10.2 us).
+template <int HD, int G, bool FUSED>
+__global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa) {
+  // K/V tiles and the PV reduction buffer sized once for 64-key tiles (the
+  // two bodies share them: LDS size sets how fast work-groups are dispatched)
+  constexpr int KS = attn_ks<HD, G>(), KP = attn_kp<HD, G>();
+  __shared__ __attribute__((aligned(16))) uint16_t s_k[64 * KS];
+  __shared__ __attribute__((aligned(16))) uint16_t s_v[64 * HD];
+  __shared__ __attribute__((aligned(16))) float s_red[KP > 1 ? KP * G * HD : 4];
+  if (*a.d_pos + 1 <= 32 * ATTN_NSPLIT)
+    attn_split_body<HD, G, FUSED, 32>(a, qa, s_k, s_v, s_red);
+  else
+    attn_split_body<HD, G, FUSED, 64>(a, qa, s_k, s_v, s_red);
 }
 
 template <int HD, int G>

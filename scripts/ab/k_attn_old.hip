@@ -4,7 +4,7 @@
 // head's history is one contiguous stream.  The current position lives in
 // device memory (d_pos) so a whole decode step can be replayed as one
 // hipGraph without re-capturing.
-#include "../../llm_inference_amd/csrc/attn.h"
+#include "attn.h"
 
 namespace llmi {
 
