@@ -351,53 +351,92 @@ __global__ __launch_bounds__(NW * 64 + (role_help(ROLE) ? E * 64 : 0)) void gemv
     __builtin_amdgcn_s_barrier();  // x blocks complete in LDS (no vmcnt wait: the weights stay in flight)
   } else if constexpr (PRO) {
     // prologue operands first: loads return in issue order, so issuing them
-    // ahead of the weight chunk lets the norm run while the weights stream
-    const int n = a.n;
-    float yv[EPT], rv[EPT], wp[EPT], wn[EPT];
+    // ahead of the weight chunk lets the norm run while the weights stream.
+    // A DPP quad of lanes per Q8_0 block (lane t & 3 owns elements 8 (t & 3)
+    // .. + 7 of block t / 4 + k T / 4): vector loads, and x is quantized from
+    // registers (no f32 staging of x in LDS).
+    constexpr int QB = T / 4;         // blocks per round
+    constexpr int EB = (E + 7) / 8;   // rounds: E = ceil(32 nb / T)
+    const int n = a.n, sub = t & 3;
+    float4 y4[EB][2], r4[EB][2], p4[EB][2], n4[EB][2];
 #pragma unroll
-    for (int k = 0; k < EPT; k++) {
-      const int i = t + k * T;
-      const bool ok = i < n;
-      yv[k] = ok ? a.y[i] : 0.0f;
-      rv[k] = ok ? a.resid_in[i] : 0.0f;
-      wp[k] = (ok && a.w_post) ? a.w_post[i] : 0.0f;
-      wn[k] = ok ? a.w_next[i] : 0.0f;
+    for (int k = 0; k < EB; k++) {
+      const int b = min(t / 4 + k * QB, nb - 1);  // clamped: unconditional loads
+      const int e = b * 32 + sub * 8;
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        y4[k][h] = *reinterpret_cast<const float4*>(a.y + e + 4 * h);
+        r4[k][h] = *reinterpret_cast<const float4*>(a.resid_in + e + 4 * h);
+        p4[k][h] = a.w_post ? *reinterpret_cast<const float4*>(a.w_post + e + 4 * h) : make_float4(0.f, 0.f, 0.f, 0.f);
+        n4[k][h] = *reinterpret_cast<const float4*>(a.w_next + e + 4 * h);
+      }
     }
     if constexpr (EARLY) issue_weights();
+    auto in_row = [&](int k) { return t / 4 + k * QB < nb; };
     float ss = 0.0f;
 #pragma unroll
-    for (int k = 0; k < EPT; k++) ss = fmaf(yv[k], yv[k], ss);
+    for (int k = 0; k < EB; k++) {
+      if (in_row(k)) {
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+          ss = fmaf(y4[k][h].x, y4[k][h].x, ss);
+          ss = fmaf(y4[k][h].y, y4[k][h].y, ss);
+          ss = fmaf(y4[k][h].z, y4[k][h].z, ss);
+          ss = fmaf(y4[k][h].w, y4[k][h].w, ss);
+        }
+      }
+    }
     LAYER_MARK(1);
     const float sc1 = rms_scale_d(wg_sum<NW>(ss, s_red[0]), n, a.eps);
     LAYER_MARK(2);
     float ss2 = 0.0f;
 #pragma unroll
-    for (int k = 0; k < EPT; k++) {
-      const float h = rv[k] + (a.w_post ? (sc1 * yv[k]) * wp[k] : yv[k]);  // no post-norm: plain add
-      rv[k] = h;
-      ss2 = fmaf(h, h, ss2);
-      const int i = t + k * T;
-      if (blockIdx.x == 0 && i < n) a.resid_out[i] = h;
+    for (int k = 0; k < EB; k++) {
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        float4& r = r4[k][h];
+        const float4 y = y4[k][h], wp = p4[k][h];
+        if (a.w_post) {
+          r.x += (sc1 * y.x) * wp.x;
+          r.y += (sc1 * y.y) * wp.y;
+          r.z += (sc1 * y.z) * wp.z;
+          r.w += (sc1 * y.w) * wp.w;
+        } else {  // no post-norm: plain add
+          r.x += y.x;
+          r.y += y.y;
+          r.z += y.z;
+          r.w += y.w;
+        }
+        if (in_row(k)) {
+          ss2 = fmaf(r.x, r.x, ss2);
+          ss2 = fmaf(r.y, r.y, ss2);
+          ss2 = fmaf(r.z, r.z, ss2);
+          ss2 = fmaf(r.w, r.w, ss2);
+          if (blockIdx.x == 0) *reinterpret_cast<float4*>(a.resid_out + (t / 4 + k * QB) * 32 + sub * 8 + 4 * h) = r;
+        }
+      }
     }
     const float sc2 = rms_scale_d(wg_sum<NW>(ss2, s_red[1]), n, a.eps);
     LAYER_MARK(3);
-    // x staged as f32 in LDS, then one thread per Q8_0 block (no cross-lane
-    // reductions on this latency-critical path)
-    float* s_xf = reinterpret_cast<float*>(s_dyn + (size_t)nb * sizeof(XBlock) + 16);
 #pragma unroll
-    for (int k = 0; k < EPT; k++) {
-      const int i = t + k * T;
-      const float xv = (sc2 * rv[k]) * wn[k];
-      if (i < n) {
-        s_xf[i] = xv;
-        if (blockIdx.x == 0 && a.xn_out) a.xn_out[i] = xv;
+    for (int k = 0; k < EB; k++) {
+      float v[8];
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const float4 r = r4[k][h], wn = n4[k][h];
+        v[4 * h + 0] = (sc2 * r.x) * wn.x;
+        v[4 * h + 1] = (sc2 * r.y) * wn.y;
+        v[4 * h + 2] = (sc2 * r.z) * wn.z;
+        v[4 * h + 3] = (sc2 * r.w) * wn.w;
       }
-    }
-    __syncthreads();
-    for (int i = t; i < 4 * nb; i += T) {  // quads of lanes per block (T is a multiple of 64)
-      const float4 f0 = reinterpret_cast<const float4*>(s_xf)[2 * i], f1 = reinterpret_cast<const float4*>(s_xf)[2 * i + 1];
-      const float v[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
-      q8_block_quad(v, i & 3, s_x + (i >> 2));
+      if (in_row(k)) {  // whole quads (one block per quad)
+        const int b = t / 4 + k * QB;
+        q8_block_quad(v, sub, s_x + b);
+        if (blockIdx.x == 0 && a.xn_out) {
+          *reinterpret_cast<float4*>(a.xn_out + b * 32 + sub * 8) = make_float4(v[0], v[1], v[2], v[3]);
+          *reinterpret_cast<float4*>(a.xn_out + b * 32 + sub * 8 + 4) = make_float4(v[4], v[5], v[6], v[7]);
+        }
+      }
     }
   } else if constexpr (ROLE == ROLE_QUANT) {
     // a DPP quad of lanes per Q8_0 block (8 floats each): the first E rounds'
