@@ -4,6 +4,11 @@
 #include "kernels.h"
 
 namespace llmi {
+struct LayerGemv;
+struct BlockSync;
+}
+
+namespace llmi {
 
 struct QKVArgs {
   const float* qkv;       // fused QKV GEMV output: q at 0, k at k_off, v at v_off
@@ -42,5 +47,11 @@ void launch_qk_norm_rope_kv(const QKVArgs& a, bool exact, hipStream_t s);
 // fused != nullptr (fast path only): the kernel also does the q/k norm +
 // rope + q scale + KV append of qk_norm_rope_kv (one launch fewer).
 void launch_attention(const AttnArgs& a, bool exact, hipStream_t s, const QKVArgs* fused = nullptr);
+// qkv GEMV (qrole LAYER_PLAIN / LAYER_PRO) + fused attention + o GEMV in one
+// launch (k_attn.hip, attention block); qg.out must be qa.qkv, og.xg must be
+// aa.q8.  attn_block_supported: a launch-table entry exists for the shapes.
+bool attn_block_supported(const DevWeight& wqkv, const DevWeight& wo, int head_dim, int n_head, int n_head_kv);
+void launch_attn_block(const DevWeight& wqkv, LayerGemv qg, int qrole, const DevWeight& wo, LayerGemv og,
+                       const AttnArgs& aa, const QKVArgs& qa, BlockSync bs, hipStream_t s);
 
 }  // namespace llmi

@@ -111,6 +111,72 @@ __device__ __forceinline__ uint16_t buf_ld2(__amdgpu_buffer_rsrc_t r, int voff, 
   return __builtin_amdgcn_raw_buffer_load_b16(r, voff, soff, BUF_NT);
 }
 
+// Cross-work-group hand-off primitives (MI355X_MICROARCH hand-off table,
+// first row): the producer stores every handed-off byte write-through (sc1),
+// drains (vmcnt(0)) and one lane adds to an agent-scope counter; the consumer
+// polls the counter with sc1 loads from one lane, joins a workgroup barrier
+// and reads the bytes with sc1 loads only.
+constexpr int BUF_SC1 = 16;  // cache-policy bit: sc1 (bypasses L1; producers' sc1 stores write through)
+__device__ __forceinline__ uint4 buf_ld16_sc1(__amdgpu_buffer_rsrc_t r, int voff) {
+  const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, BUF_SC1);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void st_sc1(float* p, float v) {  // write-through store (cross-CU hand-off)
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld_sc1(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+constexpr int BLOCK_SPIN_LIMIT = 1 << 21;  // ~0.1-0.3 s of s_sleep polls: a wait that never ends is a bug
+// Counters are kept in BLOCK_REP replicas BLOCK_REP_STRIDE words apart (own
+// lines): a signal adds to every replica with one wave instruction, a waiter
+// polls the replica of its work-group index -- hundreds of pollers on ONE
+// line saturate it (MI355X_MICROARCH 'dequeue': ~88 operations/us per word)
+// and stall the adds they wait for.
+constexpr int BLOCK_REP = 8;
+constexpr int BLOCK_REP_STRIDE = 64;  // 256 B
+// One lane polls c[replica] >= target (bounded: on timeout *err = 1 and the
+// step's results are invalid, but the grid still drains), then every wave of
+// the work-group passes a barrier.  The compiler fences keep every later load
+// of the handed-off bytes behind the barrier.
+__device__ __forceinline__ void block_wait(const unsigned* c, unsigned target, int* err, int who) {
+  if (threadIdx.x == 0) {
+    const unsigned* r = c + (who % BLOCK_REP) * BLOCK_REP_STRIDE;
+    int n = 0;
+    while (__hip_atomic_load(r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(4);
+      if (++n >= BLOCK_SPIN_LIMIT) {
+        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+// development trace of the attention block: phase clock of work-group blockIdx.x
+#define BLK_MARK(bs, ph)                                                                              \
+  do {                                                                                               \
+    if ((bs).trace && threadIdx.x == 0) (bs).trace[(size_t)blockIdx.x * 8 + (ph)] = wall_clock64(); \
+  } while (0)
+// after this work-group's sc1 stores: drain every wave, then one add per replica
+__device__ __forceinline__ void block_signal(unsigned* c) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x < BLOCK_REP)
+    __hip_atomic_fetch_add(c + threadIdx.x * BLOCK_REP_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Q4_0 nibbles of 4 packed bytes: low = elements 0..15, high = 16..31 (ops.cpp:334-340)
 __device__ __forceinline__ int nib_lo(uint32_t w) { return (int)(w & 0x0F0F0F0Fu); }
 __device__ __forceinline__ int nib_hi(uint32_t w) { return (int)((w >> 4) & 0x0F0F0F0Fu); }

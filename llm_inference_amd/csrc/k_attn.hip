@@ -5,6 +5,7 @@
 // device memory (d_pos) so a whole decode step can be replayed as one
 // hipGraph without re-capturing.
 #include "attn.h"
+#include "layer_body.h"
 
 namespace llmi {
 
@@ -165,7 +166,25 @@ __device__ __forceinline__ void ld_vec(float (&dst)[N], const float* __restrict_
   }
 }
 
-template <int HD>
+// N consecutive floats at base[off..] with sc1 loads (a row handed off inside
+// the launch, k_block: base wave-uniform)
+template <int N>
+__device__ __forceinline__ void ld_vec_sc1(float (&dst)[N], const float* base, int off) {
+  if constexpr (N == 4) {
+    const uint4 v = buf_ld16_sc1(buf_rsrc(base, 1u << 20), off * 4);
+    dst[0] = __uint_as_float(v.x); dst[1] = __uint_as_float(v.y);
+    dst[2] = __uint_as_float(v.z); dst[3] = __uint_as_float(v.w);
+  } else if constexpr (N == 2) {
+    const uint64_t v = ld_sc1(reinterpret_cast<const uint64_t*>(base + off));
+    dst[0] = __uint_as_float((uint32_t)v);
+    dst[1] = __uint_as_float((uint32_t)(v >> 32));
+  } else {
+#pragma unroll
+    for (int d = 0; d < N; d++) dst[d] = ld_sc1(base + off + d);
+  }
+}
+
+template <int HD, bool SC1 = false>
 __device__ __forceinline__ void row_load(RowLd<HD>& r, const float* __restrict__ src, const float* __restrict__ nw,
                                          const float* __restrict__ cs) {
   constexpr int DPL = RowLd<HD>::DPL;
@@ -174,7 +193,8 @@ __device__ __forceinline__ void row_load(RowLd<HD>& r, const float* __restrict__
   // row re-read its last elements: unconditional loads, masked later)
   const int i0 = min(lane, HD / DPL - 1) * DPL;
   const int j0 = i0 < HD / 2 ? i0 : i0 - HD / 2;  // DPL divides HD / 2
-  ld_vec<DPL>(r.v, src + i0);
+  if constexpr (SC1) ld_vec_sc1<DPL>(r.v, src, i0);
+  else ld_vec<DPL>(r.v, src + i0);
   ld_vec<DPL>(r.nw, nw + i0);
   // (cos, sin) pairs of elements j0 .. j0 + DPL - 1: 2 DPL consecutive floats
   float cs2[2 * DPL];
@@ -217,12 +237,6 @@ __device__ __forceinline__ void row_finish(const RowLd<HD>& r, double eps, float
   }
 }
 
-__device__ __forceinline__ void st_sc1(float* p, float v) {  // write-through store (cross-CU hand-off)
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float ld_sc1(const float* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // One work-group of 256 threads per (kv head, split) covering all G = n_head /
 // n_head_kv query heads of that kv head, so each K/V tile is read from HBM
@@ -270,9 +284,17 @@ constexpr int attn_kp() {  // PV key residue classes
   return 256 / (HD / 4);
 }
 
-template <int HD, int G, bool FUSED, int TK>
+// BLK (the attention-block kernel below): (hkv, c) come from the block's
+// role split; the first K/V tile is issued, then the work-group waits for the
+// qkv work-groups of its kv head (bs.cnt[hkv]) and reads the q/k/v rows with
+// sc1 loads; the merging work-group publishes the Q8_0 blocks write-through
+// and adds to bs.cnt[n_kv] for the o projection.
+template <int HD, int G, bool FUSED, int TK, bool BLK = false>
 __device__ __forceinline__ void attn_split_body(const AttnArgs& a, const QKVArgs& qa, uint16_t* __restrict__ s_k,
-                                                uint16_t* __restrict__ s_v, float* __restrict__ s_red) {
+                                                uint16_t* __restrict__ s_v, float* __restrict__ s_red,
+                                                const int hkv, const int c, const BlockSync& bs) {
+  static_assert(!BLK || FUSED, "BLK implies FUSED");
+  BLK_MARK(bs, 0);
   constexpr int NS = ATTN_NSPLIT;
   static_assert(TK == 32 || TK == 64, "key tile: 32 or 64 keys");
   constexpr int CH = HD / 8;                         // 16-byte chunks per row
@@ -292,7 +314,6 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, const QKVArgs
   __shared__ __attribute__((aligned(16))) float s_outbuf[TK * KS * 2 >= G * HD * 4 ? 1 : G * HD];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   ATTN_MARK(0);
-  const int hkv = blockIdx.x, c = blockIdx.y;
   const int pos = *a.d_pos;
   const int n_keys = pos + 1;
   const bool own_new = FUSED && (pos / TK) % NS == c;
@@ -324,7 +345,7 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, const QKVArgs
   const float* cs = FUSED ? qa.rope_cs + (size_t)pos * (HD / 2) * 2 : nullptr;
   RowLd<HD> rq, rk;
   float vrow[DPL];
-  if (FUSED) {
+  if (FUSED && !BLK) {
     if (w < G) row_load<HD>(rq, qa.qkv + (size_t)(hkv * G + w) * HD, qa.q_norm_w, cs);
     if (w == (G & 3)) row_load<HD>(rk, qa.qkv + qa.k_off + (size_t)hkv * HD, qa.k_norm_w, cs);
     if (w == ((G + 1) & 3)) {
@@ -333,6 +354,13 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, const QKVArgs
   }
   int tile = c;
   load_tile(tile);
+  if constexpr (BLK) {  // the history tile is in flight; now the rows of this token
+    block_wait(bs.cnt + hkv * BLOCK_REP * BLOCK_REP_STRIDE, bs.qkv_target, bs.err, c);
+    BLK_MARK(bs, 1);
+    if (w < G) row_load<HD, true>(rq, qa.qkv + (size_t)(hkv * G + w) * HD, qa.q_norm_w, cs);
+    if (w == (G & 3)) row_load<HD, true>(rk, qa.qkv + qa.k_off + (size_t)hkv * HD, qa.k_norm_w, cs);
+    if (w == ((G + 1) & 3)) ld_vec_sc1<DPL>(vrow, qa.qkv + qa.v_off + (size_t)hkv * HD, min(lane, HD / DPL - 1) * DPL);
+  }
   if (FUSED) {
     const bool ok = lane * DPL < HD;
     if (w < G) {
@@ -373,6 +401,7 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, const QKVArgs
   const int d_own = 4 * (t % NTD), kp = t / NTD;
   typedef _Float16 h2t __attribute__((ext_vector_type(2)));
   ATTN_MARK(1);
+  BLK_MARK(bs, 2);
   for (; tile * TK < n_keys; tile += NS) {
     mask_tile(tile);
     __syncthreads();  // previous tile's LDS reads done (first time: s_q / s_new written)
@@ -483,6 +512,7 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, const QKVArgs
     s_last = __hip_atomic_fetch_add(a.ticket + hkv, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == NS - 1;
   __syncthreads();
   ATTN_MARK(4);
+  BLK_MARK(bs, 3);
   if (!s_last) return;
 
   // ---- last work-group: merge the NS partials of the G heads -------------
@@ -538,10 +568,20 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, const QKVArgs
   ATTN_MARK(7);
   if (a.q8 != nullptr && HD % 32 == 0) {  // Q8_0 blocks of the heads' outputs (ops.cpp:116-139), 4 lanes per block
     __syncthreads();
+    constexpr int NBK = HD % 32 == 0 ? G * HD / 32 : 1;
+    __shared__ __attribute__((aligned(16))) XBlock s_q8[BLK ? NBK : 1];
     for (int i = t; i < G * HD / 8; i += 256) {
       const float4 f0 = reinterpret_cast<const float4*>(s_out)[2 * i], f1 = reinterpret_cast<const float4*>(s_out)[2 * i + 1];
       const float vv[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
-      q8_block_quad(vv, i & 3, a.q8 + (size_t)hkv * G * HD / 32 + (i >> 2));
+      q8_block_quad(vv, i & 3, BLK ? s_q8 + (i >> 2) : a.q8 + (size_t)hkv * G * HD / 32 + (i >> 2));
+    }
+    if constexpr (BLK) {  // write-through copy, then the o projection's counter
+      __syncthreads();
+      uint32_t* dst = reinterpret_cast<uint32_t*>(a.q8 + (size_t)hkv * NBK);
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(s_q8);
+      for (int i = t; i < NBK * 12; i += 256) st_sc1(dst + i, src[i]);
+      block_signal(bs.cnt + bs.n_kv * BLOCK_REP * BLOCK_REP_STRIDE);
+      BLK_MARK(bs, 4);
     }
   }
   ATTN_MARK(5);
@@ -562,9 +602,9 @@ __global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa)
   __shared__ __attribute__((aligned(16))) uint16_t s_v[64 * HD];
   __shared__ __attribute__((aligned(16))) float s_red[KP > 1 ? KP * G * HD : 4];
   if (*a.d_pos + 1 <= 32 * ATTN_NSPLIT)
-    attn_split_body<HD, G, FUSED, 32>(a, qa, s_k, s_v, s_red);
+    attn_split_body<HD, G, FUSED, 32>(a, qa, s_k, s_v, s_red, blockIdx.x, blockIdx.y, BlockSync{});
   else
-    attn_split_body<HD, G, FUSED, 64>(a, qa, s_k, s_v, s_red);
+    attn_split_body<HD, G, FUSED, 64>(a, qa, s_k, s_v, s_red, blockIdx.x, blockIdx.y, BlockSync{});
 }
 
 template <int HD, int G>
@@ -602,6 +642,150 @@ void launch_attention(const AttnArgs& a, bool exact, hipStream_t s, const QKVArg
     case 256: launch_split<256>(a, fused, s); break;
     default: throw std::runtime_error("attention: unsupported head_dim " + std::to_string(a.head_dim));
   }
+  LLMI_HIP(hipGetLastError());
+}
+
+
+// ---------------------------------------------------------------------------
+// Attention block: the qkv projection, attention and the o projection of one
+// decode layer in ONE launch (fast single-device path).  Work-group roles by
+// index: [0, nq) the qkv GEMV (layer_body, PLAIN for layer 0 else PRO:
+// residual + norms + Q8_0 in the prologue), [nq, nq + n_kv NSPLIT) the split
+// attention (attn_split_body, 32-key tiles), then the o GEMV (layer_body
+// PLAIN).  Every hand-off goes one way, from lower to higher work-group
+// indices: the qkv work-groups of a kv head add to bs.cnt[h] once their rows
+// are written through; that head's attention work-groups issue their first
+// K/V tile, then wait for it; the merging work-group of each head adds to
+// bs.cnt[n_kv]; the o work-groups issue their weight slices, then wait for all
+// n_kv merges.  So the o weights and the K/V history stream while the qkv
+// GEMV runs instead of after two kernel boundaries.  Waits are bounded
+// (common.h block_wait: a timeout sets bs.err, the host reports it) and the
+// counters are zeroed by the next launch of the step (the gate/up GEMV's
+// work-group 0: LayerGemv::reset).  Numerics are those of the three separate
+// kernels (same bodies, same per-row order).
+// ---------------------------------------------------------------------------
+namespace {
+
+template <int HD, int G>
+constexpr size_t block_attn_lds() {  // s_k + s_v (32-key tiles) + s_red
+  return (size_t)32 * attn_ks<HD, G>() * 2 + (size_t)32 * HD * 2 +
+         (attn_kp<HD, G>() > 1 ? (size_t)attn_kp<HD, G>() * G * HD * 4 : 16);
+}
+
+template <int HD, int G, int QR, int QP, int QE, int QROLE, int OR, int OP, int OE>
+__global__ __launch_bounds__(256) void attn_block_kernel(LayerGemv qg, LayerGemv og, AttnArgs aa, QKVArgs qa,
+                                                        BlockSync bs, int nq) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
+  int b = blockIdx.x;
+  if (b < nq) {
+    layer_body<QR, 4, QP, QE, QROLE, false, true, SYNC_SIG>(qg, b, s_dyn, bs);
+    return;
+  }
+  b -= nq;
+  const int na = aa.n_head_kv * ATTN_NSPLIT;
+  if (b < na) {
+    constexpr int KS = attn_ks<HD, G>();
+    uint16_t* s_k = reinterpret_cast<uint16_t*>(s_dyn);
+    uint16_t* s_v = s_k + 32 * KS;
+    float* s_red = reinterpret_cast<float*>(s_v + 32 * HD);
+    attn_split_body<HD, G, true, 32, true>(aa, qa, s_k, s_v, s_red, b % aa.n_head_kv, b / aa.n_head_kv, bs);
+    return;
+  }
+  b -= na;
+  layer_body<OR, 4, OP, OE, ROLE_PLAIN, false, true, SYNC_WAIT>(og, b, s_dyn, bs);
+}
+
+using BlockFn = void (*)(dim3, size_t, const LayerGemv&, const LayerGemv&, const AttnArgs&, const QKVArgs&,
+                         const BlockSync&, int, hipStream_t);
+
+template <int HD, int G, int QR, int QP, int QE, int QROLE, int OR, int OP, int OE>
+void block_launch(dim3 grid, size_t lds, const LayerGemv& qg, const LayerGemv& og, const AttnArgs& aa,
+                  const QKVArgs& qa, const BlockSync& bs, int nq, hipStream_t s) {
+  hipLaunchKernelGGL((attn_block_kernel<HD, G, QR, QP, QE, QROLE, OR, OP, OE>), grid, dim3(256), lds, s, qg, og, aa,
+                     qa, bs, nq);
+}
+
+struct BlockCfg {
+  int nb_qkv, nb_o, hd, g, qrole;
+  int QR, QP, QE, OR, OP, OE;
+  size_t attn_lds;
+  BlockFn fn;
+};
+#define LLMI_BCFG(NBQ, NBO, HD, G, QROLE, QR, QP, QE, OR, OP, OE)                                \
+  {NBQ, NBO, HD, G, QROLE, QR, QP, QE, OR, OP, OE, block_attn_lds<HD, G>(),                      \
+   block_launch<HD, G, QR, QP, QE, QROLE, OR, OP, OE>}
+// qkv: 4 waves x QR rows per work-group (rows per work-group must divide
+// head_dim); o: 4 waves x OR rows.  E as in k_layer.hip's table.
+const BlockCfg kBlockCfgs[] = {
+    LLMI_BCFG(80, 64, 256, 2, ROLE_PRO, 4, 5, 10, 4, 4, 1),    // 4B:  qkv 4096 rows -> 256 WGs, o 2560 -> 160
+    LLMI_BCFG(80, 64, 256, 2, ROLE_PLAIN, 4, 5, 1, 4, 4, 1),   // 4B layer 0
+    LLMI_BCFG(36, 32, 256, 4, ROLE_PRO, 4, 3, 5, 4, 2, 1),     // 1B:  qkv 1536 rows -> 96 WGs, o 1152 -> 72
+    LLMI_BCFG(36, 32, 256, 4, ROLE_PLAIN, 4, 3, 1, 4, 2, 1),   // 1B layer 0
+};
+#undef LLMI_BCFG
+
+const BlockCfg* find_block_cfg(int nb_qkv, int nb_o, int hd, int g, int qrole) {
+  for (const auto& c : kBlockCfgs)
+    if (c.nb_qkv == nb_qkv && c.nb_o == nb_o && c.hd == hd && c.g == g && c.qrole == qrole) return &c;
+  return nullptr;
+}
+
+void fill_gemv(const DevWeight& w, LayerGemv& a) {
+  a.qs = reinterpret_cast<const uint4*>(w.qs);
+  a.wd = w.d;
+  a.slab = w.slab;
+  a.rows = w.rows;
+  a.nb = w.cols / 32;
+  a.magic = div_magic(a.nb);
+  a.n = w.cols;
+}
+
+}  // namespace
+
+bool attn_block_supported(const DevWeight& wqkv, const DevWeight& wo, int head_dim, int n_head, int n_head_kv) {
+  if (wqkv.type != T_Q4_0 || wo.type != T_Q4_0 || wqkv.slab || wo.slab) return false;
+  if (wqkv.cols % 32 || wo.cols % 32 || n_head_kv <= 0 || n_head % n_head_kv) return false;
+  const int g = n_head / n_head_kv;
+  for (int role : {(int)ROLE_PLAIN, (int)ROLE_PRO}) {
+    const BlockCfg* c = find_block_cfg(wqkv.cols / 32, wo.cols / 32, head_dim, g, role);
+    if (!c || head_dim % (4 * c->QR) != 0) return false;
+  }
+  return wqkv.rows == (n_head + 2 * n_head_kv) * head_dim && wo.cols == n_head * head_dim;
+}
+
+void launch_attn_block(const DevWeight& wqkv, LayerGemv qg, int qrole, const DevWeight& wo, LayerGemv og,
+                       const AttnArgs& aa, const QKVArgs& qa, BlockSync bs, hipStream_t s) {
+  if (!attn_block_supported(wqkv, wo, aa.head_dim, aa.n_head, aa.n_head_kv))
+    throw std::runtime_error("attention block: unsupported shapes");
+  const int g = aa.n_head / aa.n_head_kv, hd = aa.head_dim;
+  const BlockCfg& c = *find_block_cfg(wqkv.cols / 32, wo.cols / 32, hd, g, qrole);
+  if (!bs.cnt || !bs.err || !aa.q8 || !aa.partial || !aa.ticket || !qa.qkv || qa.qkv != qg.out)
+    throw std::runtime_error("attention block: missing buffers");
+  if (qrole == ROLE_PRO ? (!qg.y || !qg.resid_in || !qg.resid_out || !qg.w_next || qg.resid_in == qg.resid_out)
+                        : !qg.xg)
+    throw std::runtime_error("attention block: missing qkv operands");
+  if (og.xg != aa.q8 || !og.out) throw std::runtime_error("attention block: o projection must read the merged blocks");
+  fill_gemv(wqkv, qg);
+  fill_gemv(wo, og);
+  const int nbq = qg.nb, nbo = og.nb;
+  // one pass group per lane (no MULTI) and enough prologue / x-copy slots
+  auto passes = [](int nb, int R) { return (nb + 64 / R - 1) / (64 / R); };
+  if (passes(nbq, c.QR) > c.QP || passes(nbo, c.OR) > c.OP) throw std::runtime_error("attention block: P too small");
+  if (qrole == ROLE_PRO ? wqkv.cols > c.QE * 256 : 3 * nbq > c.QE * 256) throw std::runtime_error("attention block: qkv E");
+  if (3 * nbo > c.OE * 256) throw std::runtime_error("attention block: o E");
+  bs.n_kv = aa.n_head_kv;
+  bs.q_rows = g * hd;
+  bs.k_off = qa.k_off;
+  bs.v_off = qa.v_off;
+  bs.hd = hd;
+  const int rpw_q = 4 * c.QR, rpw_o = 4 * c.OR;
+  bs.qkv_target = (unsigned)((g + 2) * hd / rpw_q);
+  const int nq = (wqkv.rows + rpw_q - 1) / rpw_q;
+  const int no = (wo.rows + rpw_o - 1) / rpw_o;
+  const size_t lds_q = (size_t)nbq * sizeof(XBlock) + 16 + (qrole == ROLE_PRO ? (size_t)wqkv.cols * 4 : 0);
+  const size_t lds_o = (size_t)nbo * sizeof(XBlock) + 16;
+  const size_t lds = std::max({lds_q, lds_o, c.attn_lds});
+  c.fn(dim3(nq + aa.n_head_kv * ATTN_NSPLIT + no), lds, qg, og, aa, qa, bs, nq, s);
   LLMI_HIP(hipGetLastError());
 }
 

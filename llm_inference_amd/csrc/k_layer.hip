@@ -25,544 +25,19 @@
 
 #include <hip/hip_ext.h>
 
+#include "layer_body.h"
+
 namespace llmi {
 
 namespace {
 
-
-
-template <int NW>
-__device__ __forceinline__ float wg_sum(float v, float* red) {  // fixed order, identical in every WG
-  v = wave_sum(v);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-  __syncthreads();
-  float s = 0.0f;
-#pragma unroll
-  for (int i = 0; i < NW; i++) s += red[i];
-  return s;
-}
-
-__device__ __forceinline__ float rms_scale_d(float sum, int n, double eps) {  // ops.cpp:37-38
-  return 1.0f / sqrtf((float)((double)(sum / (float)n) + eps));
-}
-
-template <int P>
-struct Chunk {  // raw loaded words only: (row, block) are recomputed when eaten, and
-  uint4 q[P];   // converting scales at load time would wait for them
-  uint16_t sw[P];
-};
-
-template <int P>
-__device__ __forceinline__ void load_chunk(Chunk<P>& c, const uint4* qw, const uint16_t* dw, int c0, int total,
-                                           int lane) {
-#pragma unroll
-  for (int p = 0; p < P; p++) {
-    const int f = c0 + p * 64 + lane;
-    const int fc = f < total ? f : 0;  // clamped: always a valid address
-    c.q[p] = ld_nt(qw + fc);
-    c.sw[p] = ld_nt16(dw + fc);
-  }
-}
-
-template <int R, int P>
-__device__ __forceinline__ void eat_chunk(const Chunk<P>& c, int c0, int total, int nb, uint32_t magic, int lane,
-                                          const XBlock* s_x, float (&acc)[R]) {
-#pragma unroll
-  for (int p = 0; p < P; p++) {
-    const int f = c0 + p * 64 + lane;
-    const int fc = f < total ? f : 0;
-    const int r = div_by_magic(fc, magic);
-    const int rr = f < total ? r : R;  // items past the wave's rows add to no row
-    const int bb = fc - r * nb;
-    const int4* xp = reinterpret_cast<const int4*>(s_x + bb);
-    const int4 x0 = xp[0], x1 = xp[1], x2 = xp[2];
-    int is = x2.y;  // nsum8
-    is = sdot4(nib_lo(c.q[p].x), x0.x, is);
-    is = sdot4(nib_lo(c.q[p].y), x0.y, is);
-    is = sdot4(nib_lo(c.q[p].z), x0.z, is);
-    is = sdot4(nib_lo(c.q[p].w), x0.w, is);
-    is = sdot4(nib_hi(c.q[p].x), x1.x, is);
-    is = sdot4(nib_hi(c.q[p].y), x1.y, is);
-    is = sdot4(nib_hi(c.q[p].z), x1.z, is);
-    is = sdot4(nib_hi(c.q[p].w), x1.w, is);
-    const float v = (h2f(c.sw[p]) * __int_as_float(x2.x)) * (float)is;
-#pragma unroll
-    for (int k = 0; k < R; k++) acc[k] += (k == rr) ? v : 0.0f;
-    // keep the scheduler from hoisting every pass's LDS x reads up front
-    // (it would hold 12 VGPRs per pass live; other waves hide the LDS latency)
-    __builtin_amdgcn_sched_barrier(0);
-  }
-}
-
-// Row-bound lanes (RB): R = 64 / L rows per wave, lane = k L + j works on row
-// k only, blocks j, j + L, j + 2L, ...  A pass (64 lanes) covers L consecutive
-// blocks of each of the wave's R rows (R full 128-B lines of quants), so a
-// lane needs no (row, block) division and keeps ONE accumulator: about a
-// third of the flat mapping's VALU work per block (PMC: the flat mapping's
-// per-item row select and division kept the VALU ~50% busy at 4.5 TB/s).
-// Lane offsets are affine in the pass index for both weight layouts:
-// q at voq + pass * sq, scale at vod + pass * sd (see the kernel).
-template <int R, int P>
-__device__ __forceinline__ void load_chunk_rb(Chunk<P>& c, __amdgpu_buffer_rsrc_t rq, __amdgpu_buffer_rsrc_t rd,
-                                              int voq, int vod, int sq, int sd, int pass0, int npass) {
-#pragma unroll
-  for (int p = 0; p < P; p++) {
-    // blocks past the row's end read the next row / slab (masked when eaten)
-    // or, past the matrix, 0 from the descriptor's bound; passes past the last
-    // one are sent out of bounds (0, no memory traffic) so the loads stay
-    // unconditional (all of the offset in voffset: the range check does not
-    // cover soffset)
-    const int pi = pass0 + p;
-    const bool in = pi < npass;
-    c.q[p] = buf_ld16(rq, in ? voq + pi * sq : (1 << 30), 0);
-    c.sw[p] = buf_ld2(rd, in ? vod + pi * sd : (1 << 30), 0);
-  }
-}
-
-template <int R, int P>
-__device__ __forceinline__ void eat_chunk_rb(const Chunk<P>& c, int pass0, int nb, int j, bool row_ok,
-                                             const XBlock* s_x, float& acc) {
-  constexpr int L = 64 / R;
-#pragma unroll
-  for (int p = 0; p < P; p++) {
-    const int b = (pass0 + p) * L + j;
-    const bool ok = row_ok && b < nb;
-    const int4* xp = reinterpret_cast<const int4*>(s_x + (b < nb ? b : nb - 1));
-    const int4 x0 = xp[0], x1 = xp[1], x2 = xp[2];
-    int is = x2.y;  // nsum8
-    is = sdot4(nib_lo(c.q[p].x), x0.x, is);
-    is = sdot4(nib_lo(c.q[p].y), x0.y, is);
-    is = sdot4(nib_lo(c.q[p].z), x0.z, is);
-    is = sdot4(nib_lo(c.q[p].w), x0.w, is);
-    is = sdot4(nib_hi(c.q[p].x), x1.x, is);
-    is = sdot4(nib_hi(c.q[p].y), x1.y, is);
-    is = sdot4(nib_hi(c.q[p].z), x1.z, is);
-    is = sdot4(nib_hi(c.q[p].w), x1.w, is);
-    const float v = (h2f(c.sw[p]) * __int_as_float(x2.x)) * (float)is;
-    acc += ok ? v : 0.0f;
-    // compiler fence: keeps each pass's LDS x reads next to their use (hoisted,
-    // they hold ~10 VGPRs per pass live across the chunk)
-    asm volatile("" ::: "memory");
-  }
-}
-
-// sum over each row's L lanes; row k's total ends up in lane k L (R >= 4) or
-// is returned for every k through `tot` (R <= 2)
-template <int R>
-__device__ __forceinline__ float rb_row_sums(float v, float (&tot)[R <= 2 ? R : 1]) {
-  constexpr int L = 64 / R;
-  if constexpr (L >= 2) v += dpp_f<DPP_QUAD_1032>(v);
-  if constexpr (L >= 4) v += dpp_f<DPP_QUAD_2301>(v);
-  if constexpr (L >= 8) v += dpp_f<DPP_ROW_HALF_MIRROR>(v);
-  if constexpr (L >= 16) v += dpp_f<DPP_ROW_MIRROR>(v);
-  if constexpr (R == 1) tot[0] = (lane_f(v, 0) + lane_f(v, 16)) + (lane_f(v, 32) + lane_f(v, 48));
-  if constexpr (R == 2) {
-    tot[0] = lane_f(v, 0) + lane_f(v, 16);
-    tot[1] = lane_f(v, 32) + lane_f(v, 48);
-  }
-  return v;
-}
-
-#ifdef LLMI_LAYER_TRACE  // development: per-work-group phase timestamps (scripts/gemv_sweep)
-__device__ unsigned long long* g_layer_trace = nullptr;
-#define LAYER_MARK(ph)                                                                                     \
-  do {                                                                                                     \
-    if (g_layer_trace && threadIdx.x == 0) g_layer_trace[(size_t)blockIdx.x * 8 + (ph)] = wall_clock64(); \
-  } while (0)
-#else
-#define LAYER_MARK(ph) \
-  do {                 \
-  } while (0)
-#endif
-
-enum { ROLE_PLAIN = LAYER_PLAIN, ROLE_PRO = LAYER_PRO, ROLE_GELU = LAYER_GELU, ROLE_QUANT = LAYER_QUANT,
-       // PRO / GELU with E extra HELPER waves that do the prologue while the
-       // NW streaming waves' weight loads are already in flight
-       ROLE_PRO_H = 4, ROLE_GELU_H = 5 };
-constexpr bool role_help(int r) { return r == ROLE_PRO_H || r == ROLE_GELU_H; }
-constexpr int HELP_K4 = 6;  // float4 per helper lane and operand: n <= E * 256 * HELP_K4
-
-// EARLY: issue the weight stream right after the activation loads (small
-// weight slices per CU: the issue stall is short and the latency overlaps);
-// otherwise after the activation is complete in LDS (see the weight issue).
-//
-// HELPER roles (ROLE_PRO_H / ROLE_GELU_H, E = NH helper waves after the NW
-// streaming waves): the helpers issue the prologue operand loads, one raw
-// s_barrier puts them ahead of the weight stream in the CU's queue, then the
-// streaming waves issue their weights while the helpers run the residual/norm
-// (partial sums exchanged through LDS with a counter, no workgroup barrier)
-// and quantize x into LDS; a second raw s_barrier hands x over.  The norm's
-// latency hides under the weights' instead of preceding them.
 template <int R, int NW, int P, int E, int ROLE, bool MULTI, bool EARLY>
 __global__ __launch_bounds__(NW * 64 + (role_help(ROLE) ? E * 64 : 0)) void gemv_q4_0_layer(LayerGemv a) {
-  constexpr bool HELP = role_help(ROLE);
-  constexpr bool PRO = ROLE == ROLE_PRO || ROLE == ROLE_GELU || HELP;
-  constexpr bool GELU = ROLE == ROLE_GELU || ROLE == ROLE_GELU_H;
-  constexpr bool RB = R == 1 || R == 2 || R == 4 || R == 8 || R == 16;  // row-bound lanes, else flat items
-  static_assert(!HELP || RB, "helper roles use the row-bound stream");
-  constexpr int L = RB ? 64 / R : 64;
-  LAYER_MARK(0);
-  constexpr int EPT = E, X_LD = E;
   extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
-  XBlock* s_x = reinterpret_cast<XBlock*>(s_dyn);
-  __shared__ float s_red[2][NW];
-  __shared__ float s_rows[GELU ? NW * R : 1];
-  constexpr int T = NW * 64;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int nb = a.nb;
-  const int row0 = (blockIdx.x * NW + w) * R;
-  const int nrows = max(0, min(R, a.rows - row0));
-  const int total = nrows * nb;
-  const uint4* qw = a.qs + (size_t)min(row0, a.rows - 1) * nb;
-  const uint16_t* dw = a.wd + (size_t)min(row0, a.rows - 1) * nb;
-  // RB: this lane's row.  Row-major blocks: descriptors over the wave's rows
-  // (wave-uniform base), block b of row k at (k nb + b) x 16 B.  Slab-major
-  // (a.slab, nb % 8 == 0, L % 8 == 0): slabs of 8 blocks x all rows, block b
-  // of row r at ((b / 8) rows + r) x 128 + (b % 8) x 16 B, so a pass of every
-  // wave reads inside the same slab and the chip sweeps memory in order.
-  const int rk = lane / L, rj = lane % L;
-  const bool row_ok = rk < nrows;
-  const int wrow0 = (blockIdx.x * NW + __builtin_amdgcn_readfirstlane(w)) * R;
-  const int wrows = max(0, a.rows - wrow0);
-  __amdgpu_buffer_rsrc_t rq, rd;
-  int voq, vod, sq, sd;
-  if (a.slab) {
-    rq = buf_rsrc(a.qs, (uint32_t)a.rows * nb * 16);
-    rd = buf_rsrc(a.wd, (uint32_t)a.rows * nb * 2);
-    const int r = wrow0 + rk;
-    voq = ((rj >> 3) * a.rows + r) * 128 + (rj & 7) * 16;
-    vod = ((rj >> 3) * a.rows + r) * 16 + (rj & 7) * 2;
-    sq = (L / 8) * a.rows * 128;
-    sd = (L / 8) * a.rows * 16;
-  } else {
-    rq = buf_rsrc(a.qs + (size_t)min(wrow0, a.rows) * nb, (uint32_t)wrows * nb * 16);
-    rd = buf_rsrc(a.wd + (size_t)min(wrow0, a.rows) * nb, (uint32_t)wrows * nb * 2);
-    voq = (rk * nb + rj) * 16;
-    vod = (rk * nb + rj) * 2;
-    sq = L * 16;
-    sd = L * 2;
-  }
-  const int npass = (nb + L - 1) / L;
-
-  Chunk<P> ca, cb;
-  auto issue_weights = [&]() {
-    if constexpr (RB) {
-      load_chunk_rb<R, P>(ca, rq, rd, voq, vod, sq, sd, 0, npass);
-      if constexpr (MULTI) load_chunk_rb<R, P>(cb, rq, rd, voq, vod, sq, sd, P, npass);
-    } else {
-      load_chunk<P>(ca, qw, dw, 0, total, lane);  // unconditional (valid clamped rows)
-      if constexpr (MULTI) load_chunk<P>(cb, qw, dw, 64 * P, total, lane);
-    }
-  };
-  const bool helper = HELP && w >= NW;
-  if constexpr (HELP) {
-    constexpr int NH = E;
-    __shared__ float s_hred[2][NH];
-    __shared__ int s_hcnt[2];
-    float* s_xf = reinterpret_cast<float*>(s_dyn + (size_t)nb * sizeof(XBlock) + 16);
-    const int n = a.n, hi = w - NW, seg = n / NH, e0 = hi * seg;
-    float4 hy[HELP_K4], hr[HELP_K4], hp[HELP_K4], hn[HELP_K4];
-    if (helper) {
-      if (hi == 0 && lane < 2) s_hcnt[lane] = 0;
-#pragma unroll
-      for (int k = 0; k < HELP_K4; k++) {
-        const int i = e0 + min((k * 64 + lane) * 4, seg - 4);  // clamped, masked below
-        hy[k] = *reinterpret_cast<const float4*>(a.y + i);
-        hr[k] = *reinterpret_cast<const float4*>(a.resid_in + i);
-        hp[k] = a.w_post ? *reinterpret_cast<const float4*>(a.w_post + i) : make_float4(0.f, 0.f, 0.f, 0.f);
-        hn[k] = *reinterpret_cast<const float4*>(a.w_next + i);
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the counter reset, before the barrier
-    }
-    __builtin_amdgcn_s_barrier();  // helpers' operand loads are queued ahead of the weights
-    if (!helper) {
-      issue_weights();
-    } else {
-      // helper partial sums -> LDS; every helper adds them in the same order
-      auto hsum = [&](int ph, float part) -> float {
-        if constexpr (NH == 1) return part;
-        if (lane == 0) {
-          s_hred[ph][hi] = part;
-          __hip_atomic_fetch_add(&s_hcnt[ph], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-        while (__hip_atomic_load(&s_hcnt[ph], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < NH)
-          __builtin_amdgcn_s_sleep(1);
-        float tot = 0.0f;
-#pragma unroll
-        for (int j = 0; j < NH; j++) tot += s_hred[ph][j];
-        return tot;
-      };
-      float ss = 0.0f;
-#pragma unroll
-      for (int k = 0; k < HELP_K4; k++) {
-        if ((k * 64 + lane) * 4 < seg) {
-          ss = fmaf(hy[k].x, hy[k].x, ss);
-          ss = fmaf(hy[k].y, hy[k].y, ss);
-          ss = fmaf(hy[k].z, hy[k].z, ss);
-          ss = fmaf(hy[k].w, hy[k].w, ss);
-        }
-      }
-      const float sc1 = rms_scale_d(hsum(0, wave_sum(ss)), n, a.eps);
-      float ss2 = 0.0f;
-#pragma unroll
-      for (int k = 0; k < HELP_K4; k++) {
-        float4& h = hr[k];
-        if (a.w_post) {
-          h.x += (sc1 * hy[k].x) * hp[k].x;
-          h.y += (sc1 * hy[k].y) * hp[k].y;
-          h.z += (sc1 * hy[k].z) * hp[k].z;
-          h.w += (sc1 * hy[k].w) * hp[k].w;
-        } else {  // no post-norm: plain add
-          h.x += hy[k].x;
-          h.y += hy[k].y;
-          h.z += hy[k].z;
-          h.w += hy[k].w;
-        }
-        const int i = e0 + (k * 64 + lane) * 4;
-        if ((k * 64 + lane) * 4 < seg) {
-          ss2 = fmaf(h.x, h.x, ss2);
-          ss2 = fmaf(h.y, h.y, ss2);
-          ss2 = fmaf(h.z, h.z, ss2);
-          ss2 = fmaf(h.w, h.w, ss2);
-          if (blockIdx.x == 0) *reinterpret_cast<float4*>(a.resid_out + i) = h;
-        }
-      }
-      const float sc2 = rms_scale_d(hsum(1, wave_sum(ss2)), n, a.eps);
-#pragma unroll
-      for (int k = 0; k < HELP_K4; k++) {
-        const int i = e0 + (k * 64 + lane) * 4;
-        if ((k * 64 + lane) * 4 < seg) {
-          const float4 x = make_float4((sc2 * hr[k].x) * hn[k].x, (sc2 * hr[k].y) * hn[k].y,
-                                       (sc2 * hr[k].z) * hn[k].z, (sc2 * hr[k].w) * hn[k].w);
-          *reinterpret_cast<float4*>(s_xf + i) = x;
-          if (blockIdx.x == 0 && a.xn_out) *reinterpret_cast<float4*>(a.xn_out + i) = x;
-        }
-      }
-      // this helper's Q8_0 blocks (seg % 32 == 0), a DPP quad per block; the
-      // wave's own LDS writes above are ordered before these reads
-      for (int i = lane; i < seg / 8; i += 64) {
-        const float4 f0 = reinterpret_cast<const float4*>(s_xf + e0)[2 * i];
-        const float4 f1 = reinterpret_cast<const float4*>(s_xf + e0)[2 * i + 1];
-        const float v[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
-        q8_block_quad(v, i & 3, s_x + e0 / 32 + (i >> 2));
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();  // x blocks complete in LDS (no vmcnt wait: the weights stay in flight)
-  } else if constexpr (PRO) {
-    // prologue operands first: loads return in issue order, so issuing them
-    // ahead of the weight chunk lets the norm run while the weights stream.
-    // A DPP quad of lanes per Q8_0 block (lane t & 3 owns elements 8 (t & 3)
-    // .. + 7 of block t / 4 + k T / 4): vector loads, and x is quantized from
-    // registers (no f32 staging of x in LDS).
-    constexpr int QB = T / 4;         // blocks per round
-    constexpr int EB = (E + 7) / 8;   // rounds: E = ceil(32 nb / T)
-    const int n = a.n, sub = t & 3;
-    float4 y4[EB][2], r4[EB][2], p4[EB][2], n4[EB][2];
-#pragma unroll
-    for (int k = 0; k < EB; k++) {
-      const int b = min(t / 4 + k * QB, nb - 1);  // clamped: unconditional loads
-      const int e = b * 32 + sub * 8;
-#pragma unroll
-      for (int h = 0; h < 2; h++) {
-        y4[k][h] = *reinterpret_cast<const float4*>(a.y + e + 4 * h);
-        r4[k][h] = *reinterpret_cast<const float4*>(a.resid_in + e + 4 * h);
-        p4[k][h] = a.w_post ? *reinterpret_cast<const float4*>(a.w_post + e + 4 * h) : make_float4(0.f, 0.f, 0.f, 0.f);
-        n4[k][h] = *reinterpret_cast<const float4*>(a.w_next + e + 4 * h);
-      }
-    }
-    if constexpr (EARLY) issue_weights();
-    auto in_row = [&](int k) { return t / 4 + k * QB < nb; };
-    float ss = 0.0f;
-#pragma unroll
-    for (int k = 0; k < EB; k++) {
-      if (in_row(k)) {
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-          ss = fmaf(y4[k][h].x, y4[k][h].x, ss);
-          ss = fmaf(y4[k][h].y, y4[k][h].y, ss);
-          ss = fmaf(y4[k][h].z, y4[k][h].z, ss);
-          ss = fmaf(y4[k][h].w, y4[k][h].w, ss);
-        }
-      }
-    }
-    LAYER_MARK(1);
-    const float sc1 = rms_scale_d(wg_sum<NW>(ss, s_red[0]), n, a.eps);
-    LAYER_MARK(2);
-    float ss2 = 0.0f;
-#pragma unroll
-    for (int k = 0; k < EB; k++) {
-#pragma unroll
-      for (int h = 0; h < 2; h++) {
-        float4& r = r4[k][h];
-        const float4 y = y4[k][h], wp = p4[k][h];
-        if (a.w_post) {
-          r.x += (sc1 * y.x) * wp.x;
-          r.y += (sc1 * y.y) * wp.y;
-          r.z += (sc1 * y.z) * wp.z;
-          r.w += (sc1 * y.w) * wp.w;
-        } else {  // no post-norm: plain add
-          r.x += y.x;
-          r.y += y.y;
-          r.z += y.z;
-          r.w += y.w;
-        }
-        if (in_row(k)) {
-          ss2 = fmaf(r.x, r.x, ss2);
-          ss2 = fmaf(r.y, r.y, ss2);
-          ss2 = fmaf(r.z, r.z, ss2);
-          ss2 = fmaf(r.w, r.w, ss2);
-          if (blockIdx.x == 0) *reinterpret_cast<float4*>(a.resid_out + (t / 4 + k * QB) * 32 + sub * 8 + 4 * h) = r;
-        }
-      }
-    }
-    const float sc2 = rms_scale_d(wg_sum<NW>(ss2, s_red[1]), n, a.eps);
-    LAYER_MARK(3);
-#pragma unroll
-    for (int k = 0; k < EB; k++) {
-      float v[8];
-#pragma unroll
-      for (int h = 0; h < 2; h++) {
-        const float4 r = r4[k][h], wn = n4[k][h];
-        v[4 * h + 0] = (sc2 * r.x) * wn.x;
-        v[4 * h + 1] = (sc2 * r.y) * wn.y;
-        v[4 * h + 2] = (sc2 * r.z) * wn.z;
-        v[4 * h + 3] = (sc2 * r.w) * wn.w;
-      }
-      if (in_row(k)) {  // whole quads (one block per quad)
-        const int b = t / 4 + k * QB;
-        q8_block_quad(v, sub, s_x + b);
-        if (blockIdx.x == 0 && a.xn_out) {
-          *reinterpret_cast<float4*>(a.xn_out + b * 32 + sub * 8) = make_float4(v[0], v[1], v[2], v[3]);
-          *reinterpret_cast<float4*>(a.xn_out + b * 32 + sub * 8 + 4) = make_float4(v[4], v[5], v[6], v[7]);
-        }
-      }
-    }
-  } else if constexpr (ROLE == ROLE_QUANT) {
-    // a DPP quad of lanes per Q8_0 block (8 floats each): the first E rounds'
-    // floats are loaded before the weights and quantized while they stream
-    const float4* yb = reinterpret_cast<const float4*>(a.y);
-    float4 xr[E][2];
-#pragma unroll
-    for (int r = 0; r < E; r++) {
-      const int i = min(t + r * T, 4 * nb - 1);
-      xr[r][0] = yb[2 * i];
-      xr[r][1] = yb[2 * i + 1];
-    }
-    if constexpr (EARLY) issue_weights();
-#pragma unroll
-    for (int r = 0; r < E; r++) {
-      const int i = t + r * T;
-      if (r * T < 4 * nb) {  // uniform: whole quads are in or out together (4 nb, T multiples of 4)
-        const float v[8] = {xr[r][0].x, xr[r][0].y, xr[r][0].z, xr[r][0].w,
-                            xr[r][1].x, xr[r][1].y, xr[r][1].z, xr[r][1].w};
-        if (i < 4 * nb) q8_block_quad(v, i & 3, s_x + (i >> 2));
-      }
-    }
-  } else {
-    // x blocks -> LDS: clamped unconditional loads (no branch between them
-    // and the weight loads, so the stores wait only for their own data)
-    const uint4* src = reinterpret_cast<const uint4*>(a.xg);
-    uint4* dst = reinterpret_cast<uint4*>(s_x);
-    const int n16 = nb * 3;
-    uint4 xr[X_LD];
-#pragma unroll
-    for (int k = 0; k < X_LD; k++) xr[k] = src[min(t + k * T, n16 - 1)];
-    if constexpr (EARLY) issue_weights();
-#pragma unroll
-    for (int k = 0; k < X_LD; k++) dst[min(t + k * T, n16)] = xr[k];  // slot n16: LDS pad (discarded)
-  }
-  // The activation is complete in LDS BEFORE the weight stream is issued.
-  // Issuing weights first does not overlap anything: a CU accepts its waves'
-  // weight loads only as fast as its miss queue drains, so any barrier after
-  // the weight issue (the prologue's reductions, the x hand-off) waits for
-  // most of the CU's weight bytes (phase trace: +2.5-4 us per launch).
-  // (HELPER roles: handled above.)
-  if constexpr (!HELP) {
-    __syncthreads();
-    if constexpr (!EARLY) issue_weights();
-  }
-
-  LAYER_MARK(4);
-  if constexpr (RB) {
-    float acc1 = 0.0f;
-    if (helper) {
-      // helpers have no rows
-    } else if constexpr (!MULTI) {
-      eat_chunk_rb<R, P>(ca, 0, nb, rj, row_ok, s_x, acc1);
-    } else {
-      // unconditional loads (out-of-range passes return 0 without traffic):
-      // no loop-carried phis, so the chunk registers are not copied
-      for (int p0 = 0; p0 < npass; p0 += 2 * P) {
-        eat_chunk_rb<R, P>(ca, p0, nb, rj, row_ok, s_x, acc1);
-        load_chunk_rb<R, P>(ca, rq, rd, voq, vod, sq, sd, p0 + 2 * P, npass);
-        eat_chunk_rb<R, P>(cb, p0 + P, nb, rj, row_ok, s_x, acc1);
-        load_chunk_rb<R, P>(cb, rq, rd, voq, vod, sq, sd, p0 + 3 * P, npass);
-      }
-    }
-    LAYER_MARK(5);
-    float tot[R <= 2 ? R : 1];
-    const float v = rb_row_sums<R>(acc1, tot);
-    if constexpr (GELU) {
-      if (!helper) {
-        if constexpr (R <= 2) {
-          if (lane == 0)
-            for (int k = 0; k < R; k++) s_rows[w * R + k] = tot[k];
-        } else {
-          if (rj == 0) s_rows[w * R + rk] = v;
-        }
-      }
-      __syncthreads();
-      constexpr int H = NW * R / 2;  // hidden units of this work-group
-      if (t < H) a.hid[blockIdx.x * H + t] = gelu_mul1(s_rows[t], s_rows[H + t]);
-    } else if (!helper) {
-      if constexpr (R <= 2) {
-        if (lane == 0)
-          for (int k = 0; k < R; k++)
-            if (k < nrows) a.out[row0 + k] = tot[k];
-      } else {
-        if (rj == 0 && row_ok) a.out[row0 + rk] = v;
-      }
-    }
-    LAYER_MARK(6);
-    return;
-  }
-  float acc[R];
-#pragma unroll
-  for (int k = 0; k < R; k++) acc[k] = 0.0f;
-  if constexpr (!MULTI) {
-    eat_chunk<R, P>(ca, 0, total, nb, a.magic, lane, s_x, acc);
-  } else {
-    // chunks 0 and 1 were issued before the prologue; each later chunk is
-    // issued as soon as its register buffer has been consumed
-    constexpr int CH = 64 * P;
-    for (int c0 = 0; c0 < total; c0 += 2 * CH) {
-      eat_chunk<R, P>(ca, c0, total, nb, a.magic, lane, s_x, acc);
-      if (c0 + 2 * CH < total) load_chunk<P>(ca, qw, dw, c0 + 2 * CH, total, lane);
-      if (c0 + CH >= total) break;
-      eat_chunk<R, P>(cb, c0 + CH, total, nb, a.magic, lane, s_x, acc);
-      if (c0 + 3 * CH < total) load_chunk<P>(cb, qw, dw, c0 + 3 * CH, total, lane);
-    }
-  }
-
-  LAYER_MARK(5);
-  if constexpr (GELU) {
-#pragma unroll
-    for (int k = 0; k < R; k++) {
-      const float s = wave_sum(acc[k]);
-      if (lane == 0) s_rows[w * R + k] = s;
-    }
-    __syncthreads();
-    constexpr int H = NW * R / 2;  // hidden units of this work-group
-    if (t < H) a.hid[blockIdx.x * H + t] = gelu_mul1(s_rows[t], s_rows[H + t]);
-  } else {
-#pragma unroll
-    for (int k = 0; k < R; k++) {
-      const float s = wave_sum(acc[k]);
-      if (lane == 0 && k < nrows) a.out[row0 + k] = s;
-    }
-  }
-  LAYER_MARK(6);
+  // the attention-block kernel's counters of this layer, for its next launch
+  if (a.reset && blockIdx.x == 0)
+    for (int i = threadIdx.x; i < a.n_reset; i += blockDim.x) a.reset[(size_t)i * BLOCK_REP_STRIDE] = 0u;
+  layer_body<R, NW, P, E, ROLE, MULTI, EARLY>(a, blockIdx.x, s_dyn, BlockSync{});
 }
 
 // ---- launch table ----------------------------------------------------------

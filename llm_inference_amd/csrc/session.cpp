@@ -7,6 +7,7 @@
 #include "session.h"
 
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 
 namespace llmi {
@@ -406,6 +407,25 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
            prefill_gemm_supported(l.down.w);
     const int grp = nkv_ > 0 ? nh_ / nkv_ : 0;
     prefill_ok_ = pf && (grp == 1 || grp == 2 || grp == 4);
+    // attention block (qkv + attention + o in one launch): the fused fast
+    // path on one device, shapes in k_attn.hip's table; LLMI_NO_BLOCK=1 keeps
+    // the three launches (A/B)
+    bool blk = fuse_layers_ && !tp_ && dup_.empty() && getenv("LLMI_NO_BLOCK") == nullptr &&
+               (grp == 1 || grp == 2 || grp == 4);
+    for (const auto& l : L_)
+      blk = blk && l.fused && l.hd % 32 == 0 && attn_block_supported(l.qkv[0].w, l.o.w, l.hd, nh_, nkv_);
+    block_ = blk;
+    if (block_) {
+      blk_cnt_ = dalloc<unsigned>((size_t)hp_.n_layer * (nkv_ + 1) * BLOCK_REP * BLOCK_REP_STRIDE);
+      blk_err_ = dalloc<int>(2);
+      if (const char* tr = getenv("LLMI_BLOCK_TRACE")) {  // development: per-work-group phase clocks of one layer
+        blk_trace_layer_ = atoi(tr);
+        blk_trace_ = dalloc<unsigned long long>(4096 * 8);
+      }
+      int maxhd = 0;
+      for (const auto& l : L_) maxhd = std::max(maxhd, l.hd);
+      blk_xo_ = dalloc<XBlock>((size_t)nh_ * maxhd / 32 + 1);
+    }
   } catch (const gguf_error& e) {
     release();
     throw status_error(LLMI_E_GGUF, e.what());
@@ -652,46 +672,81 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
   for (int l = 0; l < hp_.n_layer; l++) {
     LayerDev& Ld = L_[l];
     const int hd = Ld.hd;
-    LayerGemv g;
-    if (l == 0) {
-      if (!x_q8) {
-        launch_quantize_q8_0(xn_, E, act_.q8, s);
+    unsigned* cnt = block_ ? blk_cnt_ + (size_t)l * (nkv_ + 1) * BLOCK_REP * BLOCK_REP_STRIDE : nullptr;
+    if (block_) {  // qkv + attention + o: one launch (k_attn.hip attention block)
+      LayerGemv g;
+      int qrole = LAYER_PLAIN;
+      if (l == 0) {
+        if (!x_q8) {
+          launch_quantize_q8_0(xn_, E, act_.q8, s);
+          kernels_per_token_++;
+        }
+        g.xg = act_.q8.xb;
+      } else {
+        qrole = LAYER_PRO;
+        g.y = d_out_;
+        g.w_post = L_[l - 1].post_ffw_norm;
+        g.resid_in = cur;
+        g.resid_out = other;
+        g.w_next = Ld.attn_norm;
+        g.eps = hp_.eps;
+        std::swap(cur, other);
+      }
+      g.out = qkv_;
+      QKVArgs qa{qkv_, Ld.k_off, Ld.v_off, nh_, nkv_, hd, Ld.q_norm, Ld.k_norm,
+                 Ld.is_swa ? rope_swa_ : rope_glb_, hp_.attn_scale, hp_.eps, q_, Ld.kc, Ld.vc, max_ctx_, d_pos_};
+      AttnArgs aa{q_, Ld.kc, Ld.vc, nh_, nkv_, hd, max_ctx_, d_pos_, part_, attn_, ticket_, blk_xo_};
+      LayerGemv go;
+      go.xg = blk_xo_;
+      go.out = o_out_;
+      BlockSync bs;
+      bs.cnt = cnt;
+      bs.err = blk_err_;
+      if (blk_trace_ && l == blk_trace_layer_) bs.trace = blk_trace_;
+      launch_attn_block(Ld.qkv[0].w, g, qrole, Ld.o.w, go, aa, qa, bs, s);
+      kernels_per_token_++;
+    } else {
+      LayerGemv g;
+      if (l == 0) {
+        if (!x_q8) {
+          launch_quantize_q8_0(xn_, E, act_.q8, s);
+          kernels_per_token_++;
+        }
+        g.xg = act_.q8.xb;
+        g.out = qkv_;
+        for (int r = 0; r < dup("qkv"); r++) launch_layer_gemv(Ld.qkv[0].w, g, LAYER_PLAIN, s);
+      } else {
+        g.y = d_out_;
+        g.w_post = L_[l - 1].post_ffw_norm;
+        g.resid_in = cur;
+        g.resid_out = other;
+        g.w_next = Ld.attn_norm;
+        g.eps = hp_.eps;
+        g.out = qkv_;
+        for (int r = 0; r < dup("qkv"); r++) launch_layer_gemv(Ld.qkv[0].w, g, LAYER_PRO, s);
+        std::swap(cur, other);
+      }
+      kernels_per_token_++;
+      // this rank's heads (all of them without tensor parallelism)
+      QKVArgs qa{qkv_, Ld.k_off, Ld.v_off, nh_, nkv_, hd, Ld.q_norm, Ld.k_norm,
+                 Ld.is_swa ? rope_swa_ : rope_glb_, hp_.attn_scale, hp_.eps, q_, Ld.kc, Ld.vc, max_ctx_, d_pos_};
+      const bool q8_in_combine = hd % 32 == 0;
+      if (tp_ && !q8_in_combine) throw status_error(LLMI_E_ARG, "tensor parallel: head_dim % 32 != 0");
+      const int hb = nh_ * hd / 32;  // Q8_0 blocks of this rank's heads
+      AttnArgs aa{q_, Ld.kc, Ld.vc, nh_, nkv_, hd, max_ctx_, d_pos_, part_, attn_,
+                  ticket_, q8_in_combine ? act_.q8.xb + (size_t)tp_rank_ * hb : nullptr};
+      for (int r = 0; r < dup("attn"); r++) launch_attention(aa, false, s, &qa);
+      kernels_per_token_++;
+      if (!q8_in_combine) {
+        launch_quantize_q8_0(attn_, hp_.n_head * hd, act_.q8, s);
         kernels_per_token_++;
       }
-      g.xg = act_.q8.xb;
-      g.out = qkv_;
-      for (int r = 0; r < dup("qkv"); r++) launch_layer_gemv(Ld.qkv[0].w, g, LAYER_PLAIN, s);
-    } else {
-      g.y = d_out_;
-      g.w_post = L_[l - 1].post_ffw_norm;
-      g.resid_in = cur;
-      g.resid_out = other;
-      g.w_next = Ld.attn_norm;
-      g.eps = hp_.eps;
-      g.out = qkv_;
-      for (int r = 0; r < dup("qkv"); r++) launch_layer_gemv(Ld.qkv[0].w, g, LAYER_PRO, s);
-      std::swap(cur, other);
+      if (tp_) coll_->all_gather(act_.q8.xb, (size_t)hb * sizeof(XBlock), s);
+      LayerGemv go;
+      go.xg = act_.q8.xb;
+      go.out = o_out_ + (size_t)tp_rank_ * e_sh_;
+      for (int r = 0; r < dup("o_proj"); r++) launch_layer_gemv(Ld.o.w, go, LAYER_PLAIN, s);
     }
-    kernels_per_token_++;
-    // this rank's heads (all of them without tensor parallelism)
-    QKVArgs qa{qkv_, Ld.k_off, Ld.v_off, nh_, nkv_, hd, Ld.q_norm, Ld.k_norm,
-               Ld.is_swa ? rope_swa_ : rope_glb_, hp_.attn_scale, hp_.eps, q_, Ld.kc, Ld.vc, max_ctx_, d_pos_};
-    const bool q8_in_combine = hd % 32 == 0;
-    if (tp_ && !q8_in_combine) throw status_error(LLMI_E_ARG, "tensor parallel: head_dim % 32 != 0");
-    const int hb = nh_ * hd / 32;  // Q8_0 blocks of this rank's heads
-    AttnArgs aa{q_, Ld.kc, Ld.vc, nh_, nkv_, hd, max_ctx_, d_pos_, part_, attn_,
-                ticket_, q8_in_combine ? act_.q8.xb + (size_t)tp_rank_ * hb : nullptr};
-    for (int r = 0; r < dup("attn"); r++) launch_attention(aa, false, s, &qa);
-    kernels_per_token_++;
-    if (!q8_in_combine) {
-      launch_quantize_q8_0(attn_, hp_.n_head * hd, act_.q8, s);
-      kernels_per_token_++;
-    }
-    if (tp_) coll_->all_gather(act_.q8.xb, (size_t)hb * sizeof(XBlock), s);
-    LayerGemv go;
-    go.xg = act_.q8.xb;
-    go.out = o_out_ + (size_t)tp_rank_ * e_sh_;
-    for (int r = 0; r < dup("o_proj"); r++) launch_layer_gemv(Ld.o.w, go, LAYER_PLAIN, s);
     if (tp_) coll_->all_gather(o_out_, (size_t)e_sh_ * sizeof(float), s);
     LayerGemv gg;
     gg.y = o_out_;
@@ -701,6 +756,8 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
     gg.w_next = Ld.ffn_norm;
     gg.eps = hp_.eps;
     gg.hid = hid_ + (size_t)tp_rank_ * f_sh_;
+    gg.reset = cnt;  // the attention block's counters of this layer, zeroed for its next launch
+    gg.n_reset = cnt ? (nkv_ + 1) * BLOCK_REP : 0;  // replicas, BLOCK_REP_STRIDE apart
     for (int r = 0; r < dup("gate_up"); r++) launch_layer_gemv(Ld.gate_up[0].w, gg, LAYER_GELU, s);
     std::swap(cur, other);
     if (tp_) coll_->all_gather(hid_, (size_t)f_sh_ * sizeof(float), s);
@@ -709,7 +766,7 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
     gd.out = d_out_ + (size_t)tp_rank_ * e_sh_;
     for (int r = 0; r < dup("down"); r++) launch_layer_gemv(Ld.down.w, gd, LAYER_QUANT, s);
     if (tp_) coll_->all_gather(d_out_, (size_t)e_sh_ * sizeof(float), s);
-    kernels_per_token_ += 3;
+    kernels_per_token_ += block_ ? 2 : 3;  // (o, when not in the attention block,) gate_up, down
   }
   // final residual + output_norm (-> xn_, and f16 x for an F16 logits table)
   NormOut o2;
@@ -821,6 +878,7 @@ void Session::forward(const int32_t* tokens, int n, int pos, float* logits, int3
   if (logits) LLMI_HIP(hipMemcpyAsync(logits, logits_, (size_t)vocab_ * 4, hipMemcpyDeviceToHost, stream_));
   if (argmax) LLMI_HIP(hipMemcpyAsync(argmax, d_token_, 4, hipMemcpyDeviceToHost, stream_));
   LLMI_HIP(hipStreamSynchronize(stream_));
+  check_device_error();
 }
 
 void Session::enqueue(int32_t first, int pos, int n_steps) {
@@ -833,6 +891,25 @@ void Session::enqueue(int32_t first, int pos, int n_steps) {
 void Session::sync(int32_t* out, int n) {
   if (out && n > 0) LLMI_HIP(hipMemcpyAsync(out, ring_, (size_t)std::min(n, max_ctx_) * 4, hipMemcpyDeviceToHost, stream_));
   LLMI_HIP(hipStreamSynchronize(stream_));
+  check_device_error();
+}
+
+// a bounded in-kernel wait that gave up (k_attn.hip attention block): the
+// results since the last check are invalid -- report it, never return them
+void Session::check_device_error() {
+  if (blk_trace_) {  // development: append the last traced launch (work-group x 8 clocks) to LLMI_BLOCK_TRACE_OUT
+    std::vector<unsigned long long> h(4096 * 8);
+    LLMI_HIP(hipMemcpy(h.data(), blk_trace_, h.size() * 8, hipMemcpyDeviceToHost));
+    if (const char* path = getenv("LLMI_BLOCK_TRACE_OUT"))
+      if (FILE* f = fopen(path, "ab")) {
+        fwrite(h.data(), 8, h.size(), f);
+        fclose(f);
+      }
+  }
+  if (!blk_err_) return;
+  int e = 0;
+  LLMI_HIP(hipMemcpy(&e, blk_err_, sizeof(e), hipMemcpyDeviceToHost));
+  if (e) throw status_error(LLMI_E_HIP, "attention block: a cross-work-group wait timed out (device results invalid)");
 }
 
 void Session::info(llmi_session_info* o) const {

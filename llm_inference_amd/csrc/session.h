@@ -95,6 +95,13 @@ class Session {
   llmi_session_opts opts_;
   bool exact_ = false, use_graph_ = true;
   bool fuse_layers_ = false;  // fast path: norms / GELU folded into the Q4_0 GEMVs
+  bool block_ = false;        // fast path: qkv + attention + o as one launch per layer (k_attn.hip)
+  unsigned* blk_cnt_ = nullptr;  // [n_layer][n_kv + 1] attention-block counters
+  int* blk_err_ = nullptr;       // set by a bounded wait that gave up
+  unsigned long long* blk_trace_ = nullptr;  // LLMI_BLOCK_TRACE (development)
+  int blk_trace_layer_ = -1;
+  XBlock* blk_xo_ = nullptr;     // attention output Q8_0 blocks (layer 0's qkv still reads act_.q8 in the launch)
+  void check_device_error();
   bool ex_gemv_ = false, ex_norm_ = false, ex_attn_ = false, ex_logits_ = false;  // per kernel family
   HParams hp_;
   int vocab_ = 0, max_ctx_ = 4096;

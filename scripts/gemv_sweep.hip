@@ -55,6 +55,10 @@ __global__ __launch_bounds__(256) void stream_kernel(const uint4* __restrict__ q
   if (acc == 0x12345678u) out[0] = 1.0f;
 }
 
+__global__ void empty_kernel(float* out) {
+  if (threadIdx.x == 1023) out[0] = 1.0f;
+}
+
 // default-policy (allocating) read of a weight's qs and d: warms the MALL
 __global__ __launch_bounds__(256) void prefetch_kernel(const uint4* __restrict__ q, size_t n16,
                                                        const uint4* __restrict__ d, size_t nd16, float* out) {
@@ -170,6 +174,8 @@ int main(int argc, char** argv) {
       x.slab = layer_gemv_slab(w, role);
       return x;
     };
+    timeit("empty kernel (1 WG)", [&](const DevWeight&) { hipLaunchKernelGGL(empty_kernel, dim3(1), dim3(64), 0, s, out); });
+    timeit("empty kernel (256 WG)", [&](const DevWeight&) { hipLaunchKernelGGL(empty_kernel, dim3(256), dim3(256), 0, s, out); });
     timeit("stream<8> (qs only, 2048 WG)", [&](const DevWeight& w) {
       hipLaunchKernelGGL(stream_kernel<8>, dim3(2048), dim3(256), 0, s, (const uint4*)w.qs,
                          (size_t)sh.rows * nb, out);
@@ -185,6 +191,8 @@ int main(int argc, char** argv) {
     DevWeight probe = ws[0];
     if (layer_gemv_supported(probe, LAYER_PLAIN))
       timeit("layer plain", [&](const DevWeight& w) { launch_layer_gemv(lw(w, LAYER_PLAIN), plain, LAYER_PLAIN, s); });
+    if (layer_gemv_supported(probe, LAYER_PLAIN))
+  timeit("layer plain, same weight (cache-hot)", [&](const DevWeight&) { launch_layer_gemv(lw(ws[0], LAYER_PLAIN), plain, LAYER_PLAIN, s); });
     LayerGemv pro;
     pro.y = y;
     pro.resid_in = r0;

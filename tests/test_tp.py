@@ -57,6 +57,9 @@ def test_sharded_matches_whole_model(cfg_name, tp, monkeypatch):
     # sharded sessions run the prompt through the decode kernels (the batched
     # prefill is single-device): compare with the whole model doing the same
     monkeypatch.setenv("LLMI_NO_PREFILL", "1")
+    # ... and the same per-projection launches (the single-device attention
+    # block reduces the o projection in another lane order; tests/test_block.py)
+    monkeypatch.setenv("LLMI_NO_BLOCK", "1")
     whole = Model(g, exact=False, max_ctx=64)
     ref = whole.forward(prompt, 0)
     ref_toks = whole.generate(int(np.argmax(ref)), len(prompt), 11)
@@ -84,6 +87,7 @@ def test_rccl_single_rank_in_graph(monkeypatch):
     cfg = CONFIGS["mini-4b"]
     g = build_gemma3_gguf(cfg, seed=4)
     monkeypatch.setenv("LLMI_NO_PREFILL", "1")  # the sharded session decodes the prompt token by token
+    monkeypatch.setenv("LLMI_NO_BLOCK", "1")  # and runs the per-projection launches
     prompt = np.random.default_rng(1).integers(4, cfg.vocab, 6).astype(np.int32)
     whole = Model(g, exact=False, max_ctx=64)
     ref = whole.forward(prompt, 0)
