@@ -19,10 +19,12 @@ CSRC = os.path.join(HERE, "csrc")
 OBJ = os.path.join(HERE, "_build")
 LIB = os.path.join(HERE, "libllmi.so")
 SOURCES = ["k_gemv.hip", "k_layer.hip", "k_elem.hip", "k_attn.hip", "k_session.hip", "k_prefill.hip", "session.cpp", "collective.cpp", "capi.cpp"]
-HEADERS = ["common.h", "kernels.h", "attn.h", "session_kernels.h", "session.h", "gguf_reader.h", "collective.h"]
+HEADERS = ["common.h", "kernels.h", "attn.h", "layer_body.h", "session_kernels.h", "session.h", "gguf_reader.h", "collective.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "--offload-arch=gfx950", "-Wall",
          "-Wno-unused-function", "-Wno-unused-variable", "-Wno-unused-result"]
+if os.environ.get("LLMI_BLOCK_TRACE_BUILD"):  # development: block-kernel phase clocks (scripts/block_trace.py)
+    FLAGS.append("-DLLMI_BLOCK_TRACE")
 
 
 def _mtime(p):

@@ -103,6 +103,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uin
                                            0x00020000);
 }
 constexpr int BUF_NT = 2;  // cache-policy bit: non-temporal (streamed once)
+__device__ __forceinline__ float4 buf_ldf4(__amdgpu_buffer_rsrc_t r, int voff) {  // default policy (re-read data)
+  const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0);
+  return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+}
 __device__ __forceinline__ uint4 buf_ld16(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
   const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, BUF_NT);
   return make_uint4(v.x, v.y, v.z, v.w);
@@ -111,11 +115,11 @@ __device__ __forceinline__ uint16_t buf_ld2(__amdgpu_buffer_rsrc_t r, int voff, 
   return __builtin_amdgcn_raw_buffer_load_b16(r, voff, soff, BUF_NT);
 }
 
-// Cross-work-group hand-off primitives (MI355X_MICROARCH hand-off table,
-// first row): the producer stores every handed-off byte write-through (sc1),
-// drains (vmcnt(0)) and one lane adds to an agent-scope counter; the consumer
-// polls the counter with sc1 loads from one lane, joins a workgroup barrier
-// and reads the bytes with sc1 loads only.
+// Cross-work-group hand-off primitives.  Counter form (MI355X_MICROARCH
+// hand-off table, first row; the split attention's partials): the producer
+// stores every handed-off byte write-through (sc1), drains (vmcnt(0)) and one
+// lane adds to an agent-scope counter; the consumer learns it from the counter
+// and reads the bytes with sc1 loads only.  Granule form: below.
 constexpr int BUF_SC1 = 16;  // cache-policy bit: sc1 (bypasses L1; producers' sc1 stores write through)
 __device__ __forceinline__ uint4 buf_ld16_sc1(__amdgpu_buffer_rsrc_t r, int voff) {
   const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, BUF_SC1);
@@ -136,46 +140,62 @@ __device__ __forceinline__ float ld_sc1(const float* p) {
 __device__ __forceinline__ uint64_t ld_sc1(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-constexpr int BLOCK_SPIN_LIMIT = 1 << 21;  // ~0.1-0.3 s of s_sleep polls: a wait that never ends is a bug
-// Counters are kept in BLOCK_REP replicas BLOCK_REP_STRIDE words apart (own
-// lines): a signal adds to every replica with one wave instruction, a waiter
-// polls the replica of its work-group index -- hundreds of pollers on ONE
-// line saturate it (MI355X_MICROARCH 'dequeue': ~88 operations/us per word)
-// and stall the adds they wait for.
-constexpr int BLOCK_REP = 8;
-constexpr int BLOCK_REP_STRIDE = 64;  // 256 B
-// One lane polls c[replica] >= target (bounded: on timeout *err = 1 and the
-// step's results are invalid, but the grid still drains), then every wave of
-// the work-group passes a barrier.  The compiler fences keep every later load
-// of the handed-off bytes behind the barrier.
-__device__ __forceinline__ void block_wait(const unsigned* c, unsigned target, int* err, int who) {
-  if (threadIdx.x == 0) {
-    const unsigned* r = c + (who % BLOCK_REP) * BLOCK_REP_STRIDE;
-    int n = 0;
-    while (__hip_atomic_load(r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      __builtin_amdgcn_s_sleep(4);
-      if (++n >= BLOCK_SPIN_LIMIT) {
-        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-  }
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
+// Data-tagged granules (MI355X_MICROARCH hand-off price list, handoff-1to1;
+// cdna_hip_programming.md Guideline 16 R2): each 32-bit word travels as ONE
+// 8-byte write-through store {value, tag}; the consumer re-loads it (sc1)
+// until the tag is this launch's, so a hand-off costs one store + one load --
+// no drain, no counter, no flag.  Tags never repeat for a buffer (the
+// producer's epoch + 1, the epoch advancing once per launch), and the
+// buffers start zeroed (epoch 0 -> tag 1).
+constexpr int BLOCK_SPIN_LIMIT = 1 << 21;  // ~0.1-0.3 s of polls: a wait that never ends is a bug
+__device__ __forceinline__ void st_granule(uint2* g, uint32_t v, uint32_t tag) {
+  st_sc1(reinterpret_cast<uint64_t*>(g), ((uint64_t)tag << 32) | v);
 }
-// development trace of the attention block: phase clock of work-group blockIdx.x
+// N (1, 2 or 4) consecutive granules at g[off..] (g wave-uniform) -> values;
+// bounded: on timeout *err = 1 and the values are garbage (results invalid,
+// but the grid drains)
+template <int N>
+__device__ __forceinline__ void ld_granules(uint32_t (&v)[N], const uint2* g, int off, uint32_t tag, int* err) {
+  const __amdgpu_buffer_rsrc_t r = buf_rsrc(g, 1u << 30);
+  int n = 0;
+  for (;;) {
+    bool ok;
+    if constexpr (N == 4) {
+      const uint4 a = buf_ld16_sc1(r, off * 8), b = buf_ld16_sc1(r, off * 8 + 16);
+      v[0] = a.x; v[1] = a.z; v[2] = b.x; v[3] = b.z;
+      ok = (a.y == tag) & (a.w == tag) & (b.y == tag) & (b.w == tag);
+    } else if constexpr (N == 2) {
+      const uint4 a = buf_ld16_sc1(r, off * 8);
+      v[0] = a.x; v[1] = a.z;
+      ok = (a.y == tag) & (a.w == tag);
+    } else {
+      const uint64_t a = ld_sc1(reinterpret_cast<const uint64_t*>(g + off));
+      v[0] = (uint32_t)a;
+      ok = (uint32_t)(a >> 32) == tag;
+    }
+    if (ok) break;
+    if (++n >= BLOCK_SPIN_LIMIT) {
+      __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");  // re-load every time
+  }
+}
+
+// development trace of the block kernels (builds with -DLLMI_BLOCK_TRACE
+// only: the runtime test alone costs the layer bodies ~100 VGPRs): phase
+// clock of work-group blockIdx.x
+#ifdef LLMI_BLOCK_TRACE
 #define BLK_MARK(bs, ph)                                                                              \
   do {                                                                                               \
     if ((bs).trace && threadIdx.x == 0) (bs).trace[(size_t)blockIdx.x * 8 + (ph)] = wall_clock64(); \
   } while (0)
-// after this work-group's sc1 stores: drain every wave, then one add per replica
-__device__ __forceinline__ void block_signal(unsigned* c) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x < BLOCK_REP)
-    __hip_atomic_fetch_add(c + threadIdx.x * BLOCK_REP_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
+#else
+#define BLK_MARK(bs, ph) \
+  do {                   \
+  } while (0)
+#endif
 
 // Q4_0 nibbles of 4 packed bytes: low = elements 0..15, high = 16..31 (ops.cpp:334-340)
 __device__ __forceinline__ int nib_lo(uint32_t w) { return (int)(w & 0x0F0F0F0Fu); }

@@ -166,25 +166,7 @@ __device__ __forceinline__ void ld_vec(float (&dst)[N], const float* __restrict_
   }
 }
 
-// N consecutive floats at base[off..] with sc1 loads (a row handed off inside
-// the launch, k_block: base wave-uniform)
-template <int N>
-__device__ __forceinline__ void ld_vec_sc1(float (&dst)[N], const float* base, int off) {
-  if constexpr (N == 4) {
-    const uint4 v = buf_ld16_sc1(buf_rsrc(base, 1u << 20), off * 4);
-    dst[0] = __uint_as_float(v.x); dst[1] = __uint_as_float(v.y);
-    dst[2] = __uint_as_float(v.z); dst[3] = __uint_as_float(v.w);
-  } else if constexpr (N == 2) {
-    const uint64_t v = ld_sc1(reinterpret_cast<const uint64_t*>(base + off));
-    dst[0] = __uint_as_float((uint32_t)v);
-    dst[1] = __uint_as_float((uint32_t)(v >> 32));
-  } else {
-#pragma unroll
-    for (int d = 0; d < N; d++) dst[d] = ld_sc1(base + off + d);
-  }
-}
-
-template <int HD, bool SC1 = false>
+template <int HD>
 __device__ __forceinline__ void row_load(RowLd<HD>& r, const float* __restrict__ src, const float* __restrict__ nw,
                                          const float* __restrict__ cs) {
   constexpr int DPL = RowLd<HD>::DPL;
@@ -193,8 +175,7 @@ __device__ __forceinline__ void row_load(RowLd<HD>& r, const float* __restrict__
   // row re-read its last elements: unconditional loads, masked later)
   const int i0 = min(lane, HD / DPL - 1) * DPL;
   const int j0 = i0 < HD / 2 ? i0 : i0 - HD / 2;  // DPL divides HD / 2
-  if constexpr (SC1) ld_vec_sc1<DPL>(r.v, src, i0);
-  else ld_vec<DPL>(r.v, src + i0);
+  if (src) ld_vec<DPL>(r.v, src + i0);
   ld_vec<DPL>(r.nw, nw + i0);
   // (cos, sin) pairs of elements j0 .. j0 + DPL - 1: 2 DPL consecutive floats
   float cs2[2 * DPL];
@@ -215,6 +196,19 @@ __device__ __forceinline__ void row_load(RowLd<HD>& r, const float* __restrict__
     r.c[d] = cs2[2 * d];
     r.s[d] = cs2[2 * d + 1];
   }
+}
+
+// row_load with the row itself read from granules (the attention block)
+template <int HD>
+__device__ __forceinline__ void row_load_gr(RowLd<HD>& r, const uint2* g, const float* __restrict__ nw,
+                                            const float* __restrict__ cs, uint32_t tag, int* err) {
+  constexpr int DPL = RowLd<HD>::DPL;
+  row_load<HD>(r, nullptr, nw, cs);  // (nw, cs); the row comes from g
+  const int lane = threadIdx.x & 63;
+  uint32_t u[DPL];
+  ld_granules<DPL>(u, g, min(lane, HD / DPL - 1) * DPL, tag, err);
+#pragma unroll
+  for (int d = 0; d < DPL; d++) r.v[d] = __uint_as_float(u[d]);
 }
 
 template <int HD>
@@ -285,15 +279,16 @@ constexpr int attn_kp() {  // PV key residue classes
 }
 
 // BLK (the attention-block kernel below): (hkv, c) come from the block's
-// role split; the first K/V tile is issued, then the work-group waits for the
-// qkv work-groups of its kv head (bs.cnt[hkv]) and reads the q/k/v rows with
-// sc1 loads; the merging work-group publishes the Q8_0 blocks write-through
-// and adds to bs.cnt[n_kv] for the o projection.
+// role split; the first K/V tile is issued, then the work-group reads this
+// token's q/k/v rows from their granules (re-loading until the qkv
+// work-groups' tags arrive); the merging work-group publishes the heads'
+// Q8_0 blocks as granules for the o projection.
 template <int HD, int G, bool FUSED, int TK, bool BLK = false>
 __device__ __forceinline__ void attn_split_body(const AttnArgs& a, const QKVArgs& qa, uint16_t* __restrict__ s_k,
                                                 uint16_t* __restrict__ s_v, float* __restrict__ s_red,
                                                 const int hkv, const int c, const BlockSync& bs) {
   static_assert(!BLK || FUSED, "BLK implies FUSED");
+  const uint32_t btag = BLK ? *bs.epoch + 1u : 0u;  // granule tag, loaded up front
   BLK_MARK(bs, 0);
   constexpr int NS = ATTN_NSPLIT;
   static_assert(TK == 32 || TK == 64, "key tile: 32 or 64 keys");
@@ -354,12 +349,17 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, const QKVArgs
   }
   int tile = c;
   load_tile(tile);
-  if constexpr (BLK) {  // the history tile is in flight; now the rows of this token
-    block_wait(bs.cnt + hkv * BLOCK_REP * BLOCK_REP_STRIDE, bs.qkv_target, bs.err, c);
+  if constexpr (BLK) {  // the history tile is in flight; now this token's rows, from their granules
+    const uint32_t tag = btag;
+    if (w < G) row_load_gr<HD>(rq, bs.g_qkv + (size_t)(hkv * G + w) * HD, qa.q_norm_w, cs, tag, bs.err);
+    if (w == (G & 3)) row_load_gr<HD>(rk, bs.g_qkv + qa.k_off + (size_t)hkv * HD, qa.k_norm_w, cs, tag, bs.err);
+    if (w == ((G + 1) & 3)) {
+      uint32_t u[DPL];
+      ld_granules<DPL>(u, bs.g_qkv + qa.v_off + (size_t)hkv * HD, min(lane, HD / DPL - 1) * DPL, tag, bs.err);
+#pragma unroll
+      for (int d = 0; d < DPL; d++) vrow[d] = __uint_as_float(u[d]);
+    }
     BLK_MARK(bs, 1);
-    if (w < G) row_load<HD, true>(rq, qa.qkv + (size_t)(hkv * G + w) * HD, qa.q_norm_w, cs);
-    if (w == (G & 3)) row_load<HD, true>(rk, qa.qkv + qa.k_off + (size_t)hkv * HD, qa.k_norm_w, cs);
-    if (w == ((G + 1) & 3)) ld_vec_sc1<DPL>(vrow, qa.qkv + qa.v_off + (size_t)hkv * HD, min(lane, HD / DPL - 1) * DPL);
   }
   if (FUSED) {
     const bool ok = lane * DPL < HD;
@@ -575,12 +575,12 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, const QKVArgs
       const float vv[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
       q8_block_quad(vv, i & 3, BLK ? s_q8 + (i >> 2) : a.q8 + (size_t)hkv * G * HD / 32 + (i >> 2));
     }
-    if constexpr (BLK) {  // write-through copy, then the o projection's counter
+    if constexpr (BLK) {  // the blocks' words as granules for the o projection
       __syncthreads();
-      uint32_t* dst = reinterpret_cast<uint32_t*>(a.q8 + (size_t)hkv * NBK);
+      const uint32_t tag = btag;
+      uint2* dst = bs.g_xo + (size_t)hkv * NBK * 12;
       const uint32_t* src = reinterpret_cast<const uint32_t*>(s_q8);
-      for (int i = t; i < NBK * 12; i += 256) st_sc1(dst + i, src[i]);
-      block_signal(bs.cnt + bs.n_kv * BLOCK_REP * BLOCK_REP_STRIDE);
+      for (int i = t; i < NBK * 12; i += 256) st_granule(dst + i, src[i], tag);
       BLK_MARK(bs, 4);
     }
   }
@@ -653,16 +653,18 @@ void launch_attention(const AttnArgs& a, bool exact, hipStream_t s, const QKVArg
 // residual + norms + Q8_0 in the prologue), [nq, nq + n_kv NSPLIT) the split
 // attention (attn_split_body, 32-key tiles), then the o GEMV (layer_body
 // PLAIN).  Every hand-off goes one way, from lower to higher work-group
-// indices: the qkv work-groups of a kv head add to bs.cnt[h] once their rows
-// are written through; that head's attention work-groups issue their first
-// K/V tile, then wait for it; the merging work-group of each head adds to
-// bs.cnt[n_kv]; the o work-groups issue their weight slices, then wait for all
-// n_kv merges.  So the o weights and the K/V history stream while the qkv
-// GEMV runs instead of after two kernel boundaries.  Waits are bounded
-// (common.h block_wait: a timeout sets bs.err, the host reports it) and the
-// counters are zeroed by the next launch of the step (the gate/up GEMV's
-// work-group 0: LayerGemv::reset).  Numerics are those of the three separate
-// kernels (same bodies, same per-row order).
+// indices, as data-tagged granules (common.h): the qkv work-groups store their
+// rows as {value, tag}; a kv head's attention work-groups issue their first
+// K/V tile, then re-load the head's q/k/v row granules until the tags are this
+// launch's; the split partials meet in the last-arriving work-group per head
+// (agent ticket, as in the standalone kernel), which stores the heads' Q8_0
+// blocks as granules; the o work-groups issue their weight slices, then
+// re-load the block granules.  So the o weights and the K/V history stream
+// while the qkv GEMV runs, and no hand-off waits on a drain or a counter.
+// The tag is the layer's launch count + 1 (BlockSync::epoch, advanced by the
+// gate_up launch that follows); waits are bounded (a timeout sets bs.err, the
+// host reports it).  Numerics are those of the three separate kernels (same
+// bodies, same per-row order) except the o rows' lane order (R4).
 // ---------------------------------------------------------------------------
 namespace {
 
@@ -759,7 +761,8 @@ void launch_attn_block(const DevWeight& wqkv, LayerGemv qg, int qrole, const Dev
     throw std::runtime_error("attention block: unsupported shapes");
   const int g = aa.n_head / aa.n_head_kv, hd = aa.head_dim;
   const BlockCfg& c = *find_block_cfg(wqkv.cols / 32, wo.cols / 32, hd, g, qrole);
-  if (!bs.cnt || !bs.err || !aa.q8 || !aa.partial || !aa.ticket || !qa.qkv || qa.qkv != qg.out)
+  if (!bs.epoch || !bs.g_qkv || !bs.g_xo || !bs.err || !aa.q8 || !aa.partial || !aa.ticket || !qa.qkv ||
+      qa.qkv != qg.out)
     throw std::runtime_error("attention block: missing buffers");
   if (qrole == ROLE_PRO ? (!qg.y || !qg.resid_in || !qg.resid_out || !qg.w_next || qg.resid_in == qg.resid_out)
                         : !qg.xg)
@@ -773,13 +776,7 @@ void launch_attn_block(const DevWeight& wqkv, LayerGemv qg, int qrole, const Dev
   if (passes(nbq, c.QR) > c.QP || passes(nbo, c.OR) > c.OP) throw std::runtime_error("attention block: P too small");
   if (qrole == ROLE_PRO ? wqkv.cols > c.QE * 256 : 3 * nbq > c.QE * 256) throw std::runtime_error("attention block: qkv E");
   if (3 * nbo > c.OE * 256) throw std::runtime_error("attention block: o E");
-  bs.n_kv = aa.n_head_kv;
-  bs.q_rows = g * hd;
-  bs.k_off = qa.k_off;
-  bs.v_off = qa.v_off;
-  bs.hd = hd;
   const int rpw_q = 4 * c.QR, rpw_o = 4 * c.OR;
-  bs.qkv_target = (unsigned)((g + 2) * hd / rpw_q);
   const int nq = (wqkv.rows + rpw_q - 1) / rpw_q;
   const int no = (wo.rows + rpw_o - 1) / rpw_o;
   const size_t lds_q = (size_t)nbq * sizeof(XBlock) + 16 + (qrole == ROLE_PRO ? (size_t)wqkv.cols * 4 : 0);

@@ -34,9 +34,8 @@ namespace {
 template <int R, int NW, int P, int E, int ROLE, bool MULTI, bool EARLY>
 __global__ __launch_bounds__(NW * 64 + (role_help(ROLE) ? E * 64 : 0)) void gemv_q4_0_layer(LayerGemv a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
-  // the attention-block kernel's counters of this layer, for its next launch
-  if (a.reset && blockIdx.x == 0)
-    for (int i = threadIdx.x; i < a.n_reset; i += blockDim.x) a.reset[(size_t)i * BLOCK_REP_STRIDE] = 0u;
+  // the attention block's granule tag of this layer, for its next launch
+  if (a.epoch && blockIdx.x == 0 && threadIdx.x == 0) *a.epoch += 1u;
   layer_body<R, NW, P, E, ROLE, MULTI, EARLY>(a, blockIdx.x, s_dyn, BlockSync{});
 }
 
@@ -176,5 +175,6 @@ void launch_layer_gemv(const DevWeight& w, LayerGemv a, int role, hipStream_t s)
   c.fn(dim3((w.rows + rows_per_wg - 1) / rows_per_wg), lds, a, s);
   LLMI_HIP(hipGetLastError());
 }
+
 
 }  // namespace llmi

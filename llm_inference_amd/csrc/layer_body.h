@@ -1,5 +1,5 @@
 // layer_body.h -- device code of the decode step's Q4_0 layer GEMVs
-// (k_layer.hip), shared with the attention-block kernel (k_block.hip).
+// (k_layer.hip), shared with the attention-block kernel (k_attn.hip).
 #pragma once
 
 #include "session_kernels.h"
@@ -173,14 +173,12 @@ constexpr int HELP_K4 = 6;  // float4 per helper lane and operand: n <= E * 256 
 // (partial sums exchanged through LDS with a counter, no workgroup barrier)
 // and quantize x into LDS; a second raw s_barrier hands x over.  The norm's
 // latency hides under the weights' instead of preceding them.
-// SYNC (the attention-block kernel, k_block.hip; 0 everywhere else):
-//   SYNC_SIG  -- rows are published write-through (sc1) and, after every
-//                wave's stores have drained, one lane adds to the kv-head
-//                group's counter bs.cnt[group(row0)];
-//   SYNC_WAIT -- (PLAIN) the weight stream is issued first, then one lane
-//                polls bs.cnt[bs.n_kv] (attention merges done) and the x
-//                blocks are read with sc1 loads (MI355X_MICROARCH hand-off
-//                table, first row).
+// SYNC (the attention-block kernel in k_attn.hip; 0 everywhere else):
+//   SYNC_SIG  -- the qkv rows are published as data-tagged granules (bs.g_qkv);
+//   SYNC_WAIT -- (PLAIN) the weight stream is issued first, then the o
+//                projection's x blocks are read from their granules
+//                (bs.g_xo), each lane re-loading until the tags are this
+//                launch's.
 template <int R, int NW, int P, int E, int ROLE, bool MULTI, bool EARLY, int SYNC = 0>
 __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, unsigned char* s_dyn,
                                            const BlockSync& bs) {
@@ -200,17 +198,15 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int nb = a.nb;
   const int row0 = (bid * NW + w) * R;
-  static_assert(SYNC != SYNC_SIG || (ROLE == ROLE_PLAIN || ROLE == ROLE_PRO), "SIG: qkv roles only");
-  static_assert(SYNC != SYNC_WAIT || ROLE == ROLE_PLAIN, "WAIT: PLAIN role only");
+  static_assert(SYNC != SYNC_SIG || ROLE == ROLE_PLAIN || ROLE == ROLE_PRO, "SIG: qkv roles (-> g_qkv)");
+  static_assert(SYNC != SYNC_WAIT || ROLE == ROLE_PLAIN, "WAIT: the o projection (<- g_xo)");
+  // this launch's granule tag, loaded up front (its latency hides under the prologue)
+  const uint32_t btag = SYNC != 0 ? *bs.epoch + 1u : 0u;
   // SIG: rows are published write-through; the work-group's rows lie in one
   // kv head's group (host-checked: rows per work-group divide head_dim)
   auto put_out = [&](float* p, float v) {
-    if constexpr (SYNC == SYNC_SIG) st_sc1(p, v);
+    if constexpr (SYNC == SYNC_SIG) st_granule(bs.g_qkv + (p - a.out), __float_as_uint(v), btag);
     else *p = v;
-  };
-  auto sig_group = [&]() -> int {
-    const int r = bid * NW * R;
-    return r < bs.k_off ? r / bs.q_rows : (r < bs.v_off ? (r - bs.k_off) / bs.hd : (r - bs.v_off) / bs.hd);
   };
   const int nrows = max(0, min(R, a.rows - row0));
   const int total = nrows * nb;
@@ -360,16 +356,22 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
     constexpr int EB = (E + 7) / 8;   // rounds: E = ceil(32 nb / T)
     const int n = a.n, sub = t & 3;
     float4 y4[EB][2], r4[EB][2], p4[EB][2], n4[EB][2];
+    // buffer loads: slots past the last block are sent out of bounds (0, no
+    // memory traffic; 37.5 % of the 4B qkv slots, 50 % of gate_up's) while
+    // every load stays unconditional
+    const uint32_t vbytes = (uint32_t)nb * 128;
+    const __amdgpu_buffer_rsrc_t ry = buf_rsrc(a.y, vbytes), rr = buf_rsrc(a.resid_in, vbytes),
+                                 rp = buf_rsrc(a.w_post, a.w_post ? vbytes : 0u), rn = buf_rsrc(a.w_next, vbytes);
 #pragma unroll
     for (int k = 0; k < EB; k++) {
-      const int b = min(t / 4 + k * QB, nb - 1);  // clamped: unconditional loads
-      const int e = b * 32 + sub * 8;
+      const int b = t / 4 + k * QB;
+      const int off = b < nb ? (b * 32 + sub * 8) * 4 : (1 << 30);
 #pragma unroll
       for (int h = 0; h < 2; h++) {
-        y4[k][h] = *reinterpret_cast<const float4*>(a.y + e + 4 * h);
-        r4[k][h] = *reinterpret_cast<const float4*>(a.resid_in + e + 4 * h);
-        p4[k][h] = a.w_post ? *reinterpret_cast<const float4*>(a.w_post + e + 4 * h) : make_float4(0.f, 0.f, 0.f, 0.f);
-        n4[k][h] = *reinterpret_cast<const float4*>(a.w_next + e + 4 * h);
+        y4[k][h] = buf_ldf4(ry, off + 16 * h);
+        r4[k][h] = buf_ldf4(rr, off + 16 * h);
+        p4[k][h] = buf_ldf4(rp, off + 16 * h);
+        n4[k][h] = buf_ldf4(rn, off + 16 * h);
       }
     }
     if constexpr (EARLY) issue_weights();
@@ -388,8 +390,10 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
       }
     }
     LAYER_MARK(1);
+    BLK_MARK(bs, 5);
     const float sc1 = rms_scale_d(wg_sum<NW>(ss, s_red[0]), n, a.eps);
     LAYER_MARK(2);
+    BLK_MARK(bs, 6);
     float ss2 = 0.0f;
 #pragma unroll
     for (int k = 0; k < EB; k++) {
@@ -419,6 +423,7 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
     }
     const float sc2 = rms_scale_d(wg_sum<NW>(ss2, s_red[1]), n, a.eps);
     LAYER_MARK(3);
+    BLK_MARK(bs, 7);
 #pragma unroll
     for (int k = 0; k < EB; k++) {
       float v[8];
@@ -470,11 +475,14 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
     if constexpr (SYNC == SYNC_WAIT) {
       // the weights are independent of the hand-off: in flight before the wait
       issue_weights();
-      block_wait(bs.cnt + bs.n_kv * BLOCK_REP * BLOCK_REP_STRIDE, (unsigned)bs.n_kv, bs.err, bid);
-      BLK_MARK(bs, 4);
-      const __amdgpu_buffer_rsrc_t rx = buf_rsrc(a.xg, (uint32_t)n16 * 16);
+      const uint32_t tag = btag;
 #pragma unroll
-      for (int k = 0; k < X_LD; k++) xr[k] = buf_ld16_sc1(rx, min(t + k * T, n16 - 1) * 16);
+      for (int k = 0; k < X_LD; k++) {
+        uint32_t v[4];
+        ld_granules<4>(v, bs.g_xo, min(t + k * T, n16 - 1) * 4, tag, bs.err);
+        xr[k] = make_uint4(v[0], v[1], v[2], v[3]);
+      }
+      BLK_MARK(bs, 4);
     } else {
 #pragma unroll
       for (int k = 0; k < X_LD; k++) xr[k] = src[min(t + k * T, n16 - 1)];
@@ -537,7 +545,6 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
         if (rj == 0 && row_ok) put_out(a.out + row0 + rk, v);
       }
     }
-    if constexpr (SYNC == SYNC_SIG) block_signal(bs.cnt + sig_group() * BLOCK_REP * BLOCK_REP_STRIDE);
     BLK_MARK(bs, 3);
     LAYER_MARK(6);
     return;
@@ -577,7 +584,6 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
       if (lane == 0 && k < nrows) put_out(a.out + row0 + k, s);
     }
   }
-  if constexpr (SYNC == SYNC_SIG) block_signal(bs.cnt + sig_group() * BLOCK_REP * BLOCK_REP_STRIDE);
   LAYER_MARK(6);
 }
 

@@ -416,7 +416,16 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
       blk = blk && l.fused && l.hd % 32 == 0 && attn_block_supported(l.qkv[0].w, l.o.w, l.hd, nh_, nkv_);
     block_ = blk;
     if (block_) {
-      blk_cnt_ = dalloc<unsigned>((size_t)hp_.n_layer * (nkv_ + 1) * BLOCK_REP * BLOCK_REP_STRIDE);
+      int maxrows = 0, maxhd0 = 0;
+      for (const auto& l : L_) {
+        maxrows = std::max(maxrows, l.qkv_rows);
+        maxhd0 = std::max(maxhd0, l.hd);
+      }
+      blk_epoch_ = dalloc<unsigned>(hp_.n_layer);
+      blk_gqkv_stride_ = (size_t)maxrows;
+      blk_gxo_stride_ = (size_t)nh_ * maxhd0 / 32 * 12;
+      blk_gqkv_ = dalloc<uint2>((size_t)hp_.n_layer * blk_gqkv_stride_);
+      blk_gxo_ = dalloc<uint2>((size_t)hp_.n_layer * blk_gxo_stride_);
       blk_err_ = dalloc<int>(2);
       if (const char* tr = getenv("LLMI_BLOCK_TRACE")) {  // development: per-work-group phase clocks of one layer
         blk_trace_layer_ = atoi(tr);
@@ -672,7 +681,7 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
   for (int l = 0; l < hp_.n_layer; l++) {
     LayerDev& Ld = L_[l];
     const int hd = Ld.hd;
-    unsigned* cnt = block_ ? blk_cnt_ + (size_t)l * (nkv_ + 1) * BLOCK_REP * BLOCK_REP_STRIDE : nullptr;
+    unsigned* epoch = block_ ? blk_epoch_ + l : nullptr;
     if (block_) {  // qkv + attention + o: one launch (k_attn.hip attention block)
       LayerGemv g;
       int qrole = LAYER_PLAIN;
@@ -700,7 +709,9 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
       go.xg = blk_xo_;
       go.out = o_out_;
       BlockSync bs;
-      bs.cnt = cnt;
+      bs.epoch = epoch;
+      bs.g_qkv = blk_gqkv_ + (size_t)l * blk_gqkv_stride_;
+      bs.g_xo = blk_gxo_ + (size_t)l * blk_gxo_stride_;
       bs.err = blk_err_;
       if (blk_trace_ && l == blk_trace_layer_) bs.trace = blk_trace_;
       launch_attn_block(Ld.qkv[0].w, g, qrole, Ld.o.w, go, aa, qa, bs, s);
@@ -756,8 +767,7 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
     gg.w_next = Ld.ffn_norm;
     gg.eps = hp_.eps;
     gg.hid = hid_ + (size_t)tp_rank_ * f_sh_;
-    gg.reset = cnt;  // the attention block's counters of this layer, zeroed for its next launch
-    gg.n_reset = cnt ? (nkv_ + 1) * BLOCK_REP : 0;  // replicas, BLOCK_REP_STRIDE apart
+    gg.epoch = epoch;  // advances the attention block's granule tag of this layer
     for (int r = 0; r < dup("gate_up"); r++) launch_layer_gemv(Ld.gate_up[0].w, gg, LAYER_GELU, s);
     std::swap(cur, other);
     if (tp_) coll_->all_gather(hid_, (size_t)f_sh_ * sizeof(float), s);

@@ -96,7 +96,10 @@ class Session {
   bool exact_ = false, use_graph_ = true;
   bool fuse_layers_ = false;  // fast path: norms / GELU folded into the Q4_0 GEMVs
   bool block_ = false;        // fast path: qkv + attention + o as one launch per layer (k_attn.hip)
-  unsigned* blk_cnt_ = nullptr;  // [n_layer][n_kv + 1] attention-block counters
+  unsigned* blk_epoch_ = nullptr;  // [n_layer] attention-block launch counts (granule tags)
+  uint2* blk_gqkv_ = nullptr;      // [n_layer][qkv rows] granules
+  uint2* blk_gxo_ = nullptr;       // [n_layer][n_head * hd / 32 * 12] granules
+  size_t blk_gqkv_stride_ = 0, blk_gxo_stride_ = 0;
   int* blk_err_ = nullptr;       // set by a bounded wait that gave up
   unsigned long long* blk_trace_ = nullptr;  // LLMI_BLOCK_TRACE (development)
   int blk_trace_layer_ = -1;

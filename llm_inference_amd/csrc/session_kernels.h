@@ -49,19 +49,16 @@ struct LayerGemv {
   double eps = 0;
   float* out = nullptr;     // PLAIN / PRO / QUANT: [rows]
   float* hid = nullptr;     // GELU: [rows / 2] = GELU(gate) * up
-  unsigned* reset = nullptr;  // optional: work-group 0 zeroes reset[i * BLOCK_REP_STRIDE], i < n_reset (BlockSync counters)
-  int n_reset = 0;
+  unsigned* epoch = nullptr;  // optional: work-group 0 advances *epoch (the attention block's granule tag)
 };
-// Cross-work-group hand-offs of the attention-block kernel (k_block.hip):
-// qkv rows -> the kv head's attention work-groups -> the o projection.
+// Cross-work-group hand-offs of the attention-block kernel (k_attn.hip):
+// qkv rows -> the kv head's attention work-groups -> the o projection, as
+// data-tagged granules (common.h st_granule / ld_granules) in per-layer buffers.
 struct BlockSync {
-  unsigned* cnt = nullptr;  // [n_kv + 1][BLOCK_REP replicas, BLOCK_REP_STRIDE apart]: per kv head, qkv
-                            // work-groups done; then attention merges done
-  int* err = nullptr;       // set when a bounded wait gives up (the step's results are invalid)
-  int n_kv = 0;
-  int q_rows = 0;           // q rows per kv head (G * head_dim)
-  int k_off = 0, v_off = 0, hd = 0;
-  unsigned qkv_target = 0;  // qkv work-groups per kv head
+  const unsigned* epoch = nullptr;  // this layer's launch count (advanced by the gate_up launch): tag = *epoch + 1
+  uint2* g_qkv = nullptr;           // [qkv rows] granules of the qkv GEMV output
+  uint2* g_xo = nullptr;            // [n_head * head_dim / 32][12] granules of the attention output's Q8_0 blocks
+  int* err = nullptr;               // set when a bounded wait gives up (the step's results are invalid)
   unsigned long long* trace = nullptr;  // development: [work-group][8] wall clocks (LLMI_BLOCK_TRACE)
 };
 bool layer_gemv_supported(const DevWeight& w, int role);
