@@ -12,7 +12,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libllmi.so")
+# LLMI_LIB: an alternate build (development, e.g. the block-trace variant)
+LIB_PATH = os.environ.get("LLMI_LIB") or os.path.join(HERE, "libllmi.so")
 
 LLMI_EXACT = 1
 LLMI_NO_GRAPH = 2

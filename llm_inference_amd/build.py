@@ -24,7 +24,9 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "--offload-arch=gfx950", "-Wall",
          "-Wno-unused-function", "-Wno-unused-variable", "-Wno-unused-result"]
 if os.environ.get("LLMI_BLOCK_TRACE_BUILD"):  # development: block-kernel phase clocks (scripts/block_trace.py)
-    FLAGS.append("-DLLMI_BLOCK_TRACE")
+    FLAGS.append("-DLLMI_BLOCK_TRACE")  # into its own objects + libllmi_trace.so (load with LLMI_LIB=...)
+    OBJ = os.path.join(HERE, "_build_trace")
+    LIB = os.path.join(HERE, "libllmi_trace.so")
 
 
 def _mtime(p):
