@@ -42,6 +42,8 @@ def parse():
     p.add_argument("--config", default="gemma-3-4b")
     p.add_argument("--exact", action="store_true")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--full-logits", action="store_true",
+                   help="decode loop: full F16 logits GEMV + argmax instead of int8 screening + exact rescoring")
     p.add_argument("--cpu-decode", type=int, default=24, help="decode tokens in the CPU baseline sample")
     p.add_argument("--kernel-reps", type=int, default=2)
     p.add_argument("--no-graph", action="store_true", help="eager launches (for kernel tracers)")
@@ -126,6 +128,8 @@ def cpu_baseline(g, cfg, n_decode: int):
 
 def main():
     a = parse()
+    if a.full_logits:
+        os.environ["LLMI_FULL_LOGITS"] = "1"
     d = Dist(a.gpus)
     # load the HIP library before anything could pull in torch's HIP runtime
     from llm_inference_amd import _lib
@@ -174,10 +178,13 @@ def main():
     # dominant kernel: the Q4_0 GEMV family (weights swept in decode order, HIP events)
     us, by = m.time_kernel(0, a.kernel_reps)
     us_l, by_l = m.time_kernel(1, 2)
+    us_s, by_s = m.time_kernel(2, 8) if info.screened_logits else (0.0, 0.0)
     traffic, traffic_src = pmc_traffic()
     ach = by / (us * 1e-6) / 1e9
     mean_ctx = pos + a.steps / 2
     tok_bytes = info.bytes_per_token + info.kv_bytes_per_pos * mean_ctx
+    if info.screened_logits:  # the decode loop streams the int8 screening table instead of the F16 one
+        tok_bytes += info.screen_bytes - info.vocab * info.n_embd * 2
     out = {
         "metric": ("decode tokens/sec (Gemma-3 4B Q4_0 shape, greedy)" if (a.config, a.quant) == ("gemma-3-4b", "q4_0")
                    else f"decode tokens/sec ({cfg.name} {a.quant} shape, greedy)"),
@@ -213,6 +220,10 @@ def main():
             "us_per_launch": round(us, 3), "bytes_per_launch": int(by),
         },
         "logits_gemv": {"us": round(us_l, 2), "GBps": round(by_l / (us_l * 1e-6) / 1e9, 1)},
+        "token_selection": ({"mode": "int8 screening + exact f16 rescoring of the candidates (ids = full F16 GEMV argmax)",
+                             "us": round(us_s, 2), "bytes": int(by_s),
+                             "GBps": round(by_s / (us_s * 1e-6) / 1e9, 1) if us_s else None}
+                            if info.screened_logits else {"mode": "full F16 logits GEMV + argmax"}),
         "timing_detail": {"synthetic_build_s": round(t_build, 1), "prefill_s": round(t_prefill, 4),
                           "prefill_tokens_per_s": round(a.prefill / t_prefill, 1),
                           "prefill_mode": "batched int8-MFMA" if info.batched_prefill else "token loop"},

@@ -161,12 +161,16 @@ typedef struct {
   int kernels_per_token;      /* launches captured in the decode graph */
   int tp_rank, tp_size;       /* weight_bytes / bytes_per_token / kv_bytes_per_pos are this rank's */
   int batched_prefill;        /* 1: llmi_session_forward runs n_tokens > 1 as a batched (MFMA) prefill */
+  int screened_logits;        /* 1: llmi_session_enqueue/generate pick each greedy token by int8 screening +
+                                 exact f16 rescoring (same ids as the full F16 logits GEMV; forward keeps it) */
+  size_t screen_bytes;        /* bytes of the int8 screening table streamed per decode-loop token */
 } llmi_session_info;
 int llmi_session_get_info(const llmi_session* s, llmi_session_info* info);
 
 /* Benchmark hook: time `reps` launches of the session's dominant kernel
  * family (0 = Q4_0/Q8_0 GEMV over every layer's weights in decode order,
- * 1 = F16 logits GEMV) with HIP events on the session stream.  Returns the
+ * 1 = F16 logits GEMV, 2 = the decode loop's screened token selection) with
+ * HIP events on the session stream.  Returns the
  * mean microseconds per launch and the mean algorithmic bytes per launch. */
 int llmi_session_time_kernel(llmi_session* s, int which, int reps, double* us_per_launch, double* bytes_per_launch);
 

@@ -43,7 +43,8 @@ class SessionInfo(C.Structure):
                 ("n_head_kv", C.c_int), ("head_dim", C.c_int), ("vocab", C.c_int), ("max_ctx", C.c_int),
                 ("weight_bytes", C.c_size_t), ("bytes_per_token", C.c_size_t),
                 ("kv_bytes_per_pos", C.c_size_t), ("kernels_per_token", C.c_int),
-                ("tp_rank", C.c_int), ("tp_size", C.c_int), ("batched_prefill", C.c_int)]
+                ("tp_rank", C.c_int), ("tp_size", C.c_int), ("batched_prefill", C.c_int),
+                ("screened_logits", C.c_int), ("screen_bytes", C.c_size_t)]
 
 
 _lib = None

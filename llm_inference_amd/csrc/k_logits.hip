@@ -1,0 +1,344 @@
+// k_logits.hip -- greedy token selection by bounded screening + exact rescoring.
+//
+// The reference picks the next token as the first maximal logit of the F16
+// token_embd GEMV (model.cpp:1019-1028 -> mat_vec_mul_fp16 ops.cpp:455-612,
+// then std::max_element, main.cpp:193-194).  The fast path's F16 GEMV
+// (k_gemv.hip gemv_f16_rows_pipe) reads the whole 1.34 GB table (4B) per
+// token.  For the token id alone (the decode loop, llmi_session_enqueue) this
+// file gets the SAME id from about half the bytes:
+//
+//   1. screen_prep: x16 (the f16-rounded final-norm output the F16 GEMV
+//      multiplies with) -> Q8 blocks qx = rint(x / dx), dx = amax / 127, and
+//      per block the bound weight c_b (below);
+//   2. screen_gemv: an int8 copy of the table (per 32-block f16 scale d, made
+//      once at load by quantize_table_q8) -> per row approx_r = sum_b d dx
+//      isum_b and B_r = sum_b d_rb c_b; hi_r = approx_r + B_r + A is stored,
+//      M = max_r (approx_r - B_r - A) is reduced by atomicMax;
+//   3. screen_rescore: every row with hi_r >= M is recomputed EXACTLY as
+//      gemv_f16_rows_pipe computes it (same lanes, same fdot2 chain, same
+//      wave_sum) and reduced to the first-index argmax key (argmax_key).
+//
+// Why it is the same token: |fast_r - approx_r| <= B_r + A for every row,
+// where fast_r is the F16 GEMV's value.  c_b = 0.5 |x_b|_1 (the table's
+// rounding to d q, |w - d q| <= d/2 since d is rounded UP from amax/127) +
+// 127.5 E_b (E_b = sum |x - dx qx|, |w| <= 127 d) + 127.5 k u (|x_b|_1 + E_b)
+// (f32 rounding of both computations, k = n + 32, u = 2^-24), widened by
+// 2^-10 and rounded up; A = 2^-14 |x|_1 covers f16/f32 denormal flushing.  If
+// r* is the fast path's first maximal row and m attains M, then
+// fast_r* >= fast_m >= approx_m - B_m - A = M and approx_r* + B_r* + A >=
+// fast_r* >= M: r* (and every row tying with it) is a candidate, and the
+// candidates are rescored with the fast path's exact arithmetic.  Worst case
+// (e.g. x = 0: every row ties) every row is rescored: slower, never wrong.
+// tests/test_logits_screen.py checks ids against the full GEMV, ties included.
+#include "session_kernels.h"
+
+namespace llmi {
+
+namespace {
+
+constexpr float SCREEN_DENORM = 6.103515625e-05f;  // 2^-14: smallest normal f16
+
+__device__ __forceinline__ float dot8_h(uint4 w, uint4 x, float acc) {  // = k_gemv.hip dot8_f16
+  typedef _Float16 h2t __attribute__((ext_vector_type(2)));
+  acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2t, w.x), __builtin_bit_cast(h2t, x.x), acc, false);
+  acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2t, w.y), __builtin_bit_cast(h2t, x.y), acc, false);
+  acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2t, w.z), __builtin_bit_cast(h2t, x.z), acc, false);
+  acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2t, w.w), __builtin_bit_cast(h2t, x.w), acc, false);
+  return acc;
+}
+
+__device__ __forceinline__ unsigned fkey(float f) {  // order-preserving float -> uint (0 below every float)
+  const unsigned u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float fkey_inv(unsigned k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
+}
+
+// ---- load time: the table's int8 copy --------------------------------------
+// one thread per (row, 32-block): d = f16 rounded UP from amax / 127 (so
+// |q| <= 127 and |w - d q| <= d / 2 even for subnormal scales), q = rint(w / d)
+__global__ void quantize_table_q8_kernel(const uint16_t* __restrict__ w, size_t n_blocks, int nb,
+                                         uint4* __restrict__ qs, uint16_t* __restrict__ d) {
+  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= n_blocks) return;
+  const uint4* src = reinterpret_cast<const uint4*>(w + i * 32);
+  float v[32];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const uint4 u = src[k];
+    const uint32_t ws[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      v[k * 8 + 2 * j] = h2f((uint16_t)(ws[j] & 0xFFFF));
+      v[k * 8 + 2 * j + 1] = h2f((uint16_t)(ws[j] >> 16));
+    }
+  }
+  float amax = 0.0f;
+#pragma unroll
+  for (int k = 0; k < 32; k++) amax = fmaxf(amax, fabsf(v[k]));
+  const float want = amax / 127.0f;
+  uint16_t dh = f2h_ggml(want);
+  if (h2f(dh) < want) dh = (uint16_t)(dh + 1);  // positive f16: next representable value up
+  const float df = h2f(dh);
+  uint32_t packed[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    uint32_t p = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int q = df > 0.0f ? (int)fminf(127.0f, fmaxf(-127.0f, rintf(v[4 * k + j] / df))) : 0;
+      p |= (uint32_t)(q & 0xFF) << (8 * j);
+    }
+    packed[k] = p;
+  }
+  qs[2 * i] = make_uint4(packed[0], packed[1], packed[2], packed[3]);
+  qs[2 * i + 1] = make_uint4(packed[4], packed[5], packed[6], packed[7]);
+  d[i] = dh;
+  (void)nb;
+}
+
+// ---- per token --------------------------------------------------------------
+// one work-group: thread b < nb quantizes block b of x16 and computes c_b in
+// f64; thread 0 resets M.  xs[b] = {qx[32], dx, c_b / 2, A, pad}.
+__global__ __launch_bounds__(256) void screen_prep_kernel(const uint16_t* __restrict__ x16, int n, ScreenX* __restrict__ xs,
+                                                          unsigned* __restrict__ m_key) {
+  __shared__ double s_l1[256];
+  const int b = threadIdx.x, nb = n / 32;
+  double l1 = 0.0;
+  if (b < nb) {
+    float v[32];
+    float amax = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 32; i++) {
+      v[i] = h2f(x16[b * 32 + i]);
+      amax = fmaxf(amax, fabsf(v[i]));
+    }
+    const float dx = amax / 127.0f;
+    double e = 0.0, den = 0.0;
+    uint32_t packed[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 32; i++) {
+      const int q = dx > 0.0f ? (int)fminf(127.0f, fmaxf(-127.0f, rintf(v[i] / dx))) : 0;
+      packed[i / 4] |= (uint32_t)(q & 0xFF) << (8 * (i % 4));
+      l1 += fabs((double)v[i]);
+      e += fabs((double)v[i] - (double)dx * (double)q);
+      if (fabsf(v[i]) < SCREEN_DENORM) den += fabs((double)v[i]);
+    }
+    const double k_u = (double)(n + 32) * 0x1p-24;
+    double c = 0.5 * l1 + 127.5 * e + 127.5 * k_u * (l1 + e) + 127.5 * den;
+    c *= 1.0 + 0x1p-10;
+    ScreenX o;
+    o.lo = make_int4((int)packed[0], (int)packed[1], (int)packed[2], (int)packed[3]);
+    o.hi = make_int4((int)packed[4], (int)packed[5], (int)packed[6], (int)packed[7]);
+    o.dx = dx;
+    o.c_half = __double2float_ru(0.5 * c);
+    o.a = 0.0f;
+    o.pad = 0.0f;
+    xs[b] = o;
+  }
+  s_l1[b] = l1;
+  __syncthreads();
+  if (b == 0) {
+    double tot = 0.0;
+    for (int i = 0; i < nb; i++) tot += s_l1[i];
+    // A: denormal flushing of the table's f16 values (2^-14 per |x|), doubled
+    xs[nb].a = __double2float_ru(2.0 * (double)SCREEN_DENORM * tot * (1.0 + 0x1p-10));
+    *m_key = 0u;
+  }
+}
+
+// Screening GEMV: half a wave per row (lane j of a half owns 16-B chunks j,
+// j + 32, ... of the row's int8 quants = half-blocks), grid-stride over row
+// pairs with the next pair's loads in flight (as gemv_f16_rows_pipe).
+// CPL: 16-B chunks per lane, ceil(2 nb / 32) (5 for 2560 columns; chunks
+// past the row's 2 nb contribute nothing).
+template <int CPL>
+__global__ __launch_bounds__(256) void screen_gemv_kernel(const uint4* __restrict__ qs, const uint16_t* __restrict__ d,
+                                                          int rows, int nb, const ScreenX* __restrict__ xs,
+                                                          float* __restrict__ hi, unsigned* __restrict__ m_key) {
+  const int NC = 2 * nb;  // 16-B chunks per row
+  const int lane = threadIdx.x & 63, j = lane & 31, half = lane >> 5;
+  int pair = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int npairs = gridDim.x * 4;
+  int4 xq[CPL];
+  float xd[CPL], xc[CPL];
+#pragma unroll
+  for (int p = 0; p < CPL; p++) {
+    const int c = p * 32 + j, b = min(c, NC - 1) >> 1;
+    const bool ok = c < NC;
+    const int4* xb = reinterpret_cast<const int4*>(xs + b);
+    xq[p] = ok ? ((c & 1) ? xb[1] : xb[0]) : make_int4(0, 0, 0, 0);
+    xd[p] = ok ? xs[b].dx : 0.0f;
+    xc[p] = ok ? xs[b].c_half : 0.0f;
+  }
+  const float A = xs[nb].a;
+  float mloc = -INFINITY;
+  auto load = [&](uint4 (&q)[CPL], uint16_t (&s)[CPL], int r) {
+    const uint4* qr = qs + (size_t)r * NC;
+    const uint16_t* dr = d + (size_t)r * nb;
+#pragma unroll
+    for (int p = 0; p < CPL; p++) {
+      const int c = min(p * 32 + j, NC - 1);  // clamped (masked by x = 0)
+      q[p] = ld_nt(qr + c);
+      s[p] = dr[c >> 1];
+    }
+  };
+  int row = 2 * pair + half;
+  uint4 cq[CPL];
+  uint16_t cs[CPL];
+  load(cq, cs, min(row, rows - 1));
+  for (; 2 * pair < rows; pair += npairs, row += 2 * npairs) {
+    uint4 nq[CPL];
+    uint16_t ns[CPL];
+    load(nq, ns, min(row + 2 * npairs, rows - 1));
+    float ap = 0.0f, bp = 0.0f;
+#pragma unroll
+    for (int p = 0; p < CPL; p++) {
+      int is = 0;
+      is = sdot4((int)cq[p].x, xq[p].x, is);
+      is = sdot4((int)cq[p].y, xq[p].y, is);
+      is = sdot4((int)cq[p].z, xq[p].z, is);
+      is = sdot4((int)cq[p].w, xq[p].w, is);
+      const float dw = h2f(cs[p]);
+      ap += dw * (xd[p] * (float)is);
+      bp += dw * xc[p];
+    }
+    ap = half_sum(ap);
+    bp = half_sum(bp) * (1.0f + 0x1p-10f);
+    if (j == 0 && row < rows) {
+      hi[row] = (ap + bp) + A;
+      mloc = fmaxf(mloc, (ap - bp) - A);
+    }
+#pragma unroll
+    for (int p = 0; p < CPL; p++) {
+      cq[p] = nq[p];
+      cs[p] = ns[p];
+    }
+  }
+  mloc = wave_max(mloc);
+  if (lane == 0 && mloc > -INFINITY) atomicMax(m_key, fkey(mloc));
+}
+
+// Rescoring: each work-group scans its slice of hi[] for candidates (hi >= M)
+// into LDS, then its waves recompute those rows exactly as
+// gemv_f16_rows_pipe<P, T> does and fold the first-index argmax key.
+template <int P, int T>
+__global__ __launch_bounds__(256) void screen_rescore_kernel(const uint4* __restrict__ w, int rows,
+                                                             const uint4* __restrict__ x16, const float* __restrict__ hi,
+                                                             const unsigned* __restrict__ m_key, int slice,
+                                                             unsigned long long* __restrict__ amax_key) {
+  constexpr int NP = P + (T ? 1 : 0);
+  constexpr int RU4 = P * 64 + T;
+  extern __shared__ int s_cand[];  // [slice]
+  __shared__ int s_n;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  if (t == 0) s_n = 0;
+  __syncthreads();
+  const float M = fkey_inv(*m_key);
+  const int r0 = blockIdx.x * slice, r1 = min(rows, r0 + slice);
+  for (int r = r0 + t; r < r1; r += 256)
+    if (hi[r] >= M) s_cand[atomicAdd(&s_n, 1)] = r;
+  __syncthreads();
+  const int n = s_n;
+  if (n == 0) return;
+  const int tl = T ? lane % (T ? T : 64) : lane;
+  uint4 xr[NP];
+#pragma unroll
+  for (int p = 0; p < NP; p++) xr[p] = x16[p * 64 + (p < P ? lane : tl)];
+  unsigned long long best = 0;
+  for (int k = wave; k < n; k += 4) {
+    const int row = s_cand[k];
+    const uint4* wr = w + (size_t)row * RU4;
+    uint4 cur[NP];
+#pragma unroll
+    for (int p = 0; p < NP; p++) cur[p] = ld_nt(wr + p * 64 + (p < P ? lane : tl));
+    float acc = 0.0f;
+#pragma unroll
+    for (int p = 0; p < P; p++) acc = dot8_h(cur[p], xr[p], acc);
+    if constexpr (T != 0) {
+      const float tt = dot8_h(cur[P], xr[P], 0.0f);
+      acc += lane < T ? tt : 0.0f;
+    }
+    acc = wave_sum(acc);
+    const unsigned long long key = argmax_key(acc, (uint32_t)row);
+    best = key > best ? key : best;
+  }
+  if (lane == 0 && best) atomicMax(amax_key, best);
+}
+
+constexpr int RESCORE_SLICE = 1024;
+
+}  // namespace
+
+// the shapes whose fast F16 GEMV is gemv_f16_rows_pipe (k_gemv.hip
+// launch_gemv): the rescoring reproduces exactly that kernel's rows
+bool screen_supported(const DevWeight& table) {
+  return table.type == T_F16 && table.cols % 128 == 0 && table.cols >= 128 && table.cols <= 6144 && table.rows > 0;
+}
+
+void alloc_screen_table(const DevWeight& table, ScreenTable& st, hipStream_t s) {
+  const int nb = table.cols / 32;
+  const size_t n_blocks = (size_t)table.rows * nb;
+  LLMI_HIP(hipMalloc(&st.qs, n_blocks * 32));
+  LLMI_HIP(hipMalloc(&st.d, n_blocks * 2 + 64));
+  LLMI_HIP(hipMalloc(&st.xs, (size_t)(nb + 1) * sizeof(ScreenX)));
+  LLMI_HIP(hipMalloc(&st.hi, (size_t)table.rows * 4));
+  LLMI_HIP(hipMalloc(&st.m_key, 64));
+  LLMI_HIP(hipMemsetAsync(st.xs, 0, (size_t)(nb + 1) * sizeof(ScreenX), s));
+  st.rows = table.rows;
+  st.cols = table.cols;
+  st.bytes = n_blocks * 34;
+  hipLaunchKernelGGL(quantize_table_q8_kernel, dim3((unsigned)((n_blocks + 255) / 256)), dim3(256), 0, s,
+                     reinterpret_cast<const uint16_t*>(table.qs), n_blocks, nb, reinterpret_cast<uint4*>(st.qs), st.d);
+  LLMI_HIP(hipGetLastError());
+}
+
+void free_screen_table(ScreenTable& st) {
+  for (void* p : {(void*)st.qs, (void*)st.d, (void*)st.xs, (void*)st.hi, (void*)st.m_key})
+    if (p) (void)hipFree(p);
+  st = ScreenTable{};
+}
+
+void launch_screen_argmax(const DevWeight& table, const ScreenTable& st, const uint16_t* x16,
+                          unsigned long long* amax_key, hipStream_t s) {
+  if (table.rows != st.rows || table.cols != st.cols) throw std::runtime_error("screen: table mismatch");
+  if (!screen_supported(table)) throw std::runtime_error("screen: unsupported logits table");
+  const int n = table.cols, nb = n / 32;
+  hipLaunchKernelGGL(screen_prep_kernel, dim3(1), dim3(256), 0, s, x16, n, st.xs, st.m_key);
+  const int cpl = (2 * nb + 31) / 32;
+  const int rows = table.rows;
+  const dim3 grid((std::min((rows + 1) / 2, 256 * 8) + 3) / 4);
+  switch (cpl) {
+#define LLMI_SCR(C)                                                                                               \
+  case C:                                                                                                         \
+    hipLaunchKernelGGL(screen_gemv_kernel<C>, grid, dim3(256), 0, s, reinterpret_cast<const uint4*>(st.qs), st.d, \
+                       rows, nb, st.xs, st.hi, st.m_key);                                                         \
+    break;
+    LLMI_SCR(1) LLMI_SCR(2) LLMI_SCR(3) LLMI_SCR(4) LLMI_SCR(5) LLMI_SCR(6) LLMI_SCR(7) LLMI_SCR(8) LLMI_SCR(9)
+    LLMI_SCR(10) LLMI_SCR(11) LLMI_SCR(12)
+#undef LLMI_SCR
+    default: throw std::runtime_error("screen: unsupported n_embd");
+  }
+  LLMI_HIP(hipGetLastError());
+  const int u4 = n / 8, P = u4 / 64, T = u4 % 64;
+  const dim3 rg((rows + RESCORE_SLICE - 1) / RESCORE_SLICE);
+  const size_t lds = RESCORE_SLICE * sizeof(int);
+  switch (P * 4 + T / 16) {
+#define LLMI_RSC(PP, TT)                                                                                          \
+  case PP * 4 + TT / 16:                                                                                          \
+    hipLaunchKernelGGL((screen_rescore_kernel<PP, TT>), rg, dim3(256), lds, s,                                   \
+                       reinterpret_cast<const uint4*>(table.qs), rows, reinterpret_cast<const uint4*>(x16), st.hi, \
+                       st.m_key, RESCORE_SLICE, amax_key);                                                        \
+    break;
+#define LLMI_RSC4(PP) LLMI_RSC(PP, 0) LLMI_RSC(PP, 16) LLMI_RSC(PP, 32) LLMI_RSC(PP, 48)
+    LLMI_RSC(0, 16) LLMI_RSC(0, 32) LLMI_RSC(0, 48) LLMI_RSC4(1) LLMI_RSC4(2) LLMI_RSC4(3) LLMI_RSC4(4) LLMI_RSC4(5)
+    LLMI_RSC4(6) LLMI_RSC4(7) LLMI_RSC4(8) LLMI_RSC4(9) LLMI_RSC4(10) LLMI_RSC4(11) LLMI_RSC(12, 0)
+#undef LLMI_RSC4
+#undef LLMI_RSC
+    default: throw std::runtime_error("screen: unsupported logits width for the rescoring kernel");
+  }
+  LLMI_HIP(hipGetLastError());
+}
+
+}  // namespace llmi

@@ -415,6 +415,11 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
     for (const auto& l : L_)
       blk = blk && l.fused && l.hd % 32 == 0 && attn_block_supported(l.qkv[0].w, l.o.w, l.hd, nh_, nkv_);
     block_ = blk;
+    // greedy token ids by screening (k_logits.hip): the fast F16 logits path
+    // on one device; LLMI_FULL_LOGITS=1 keeps the full GEMV in the decode loop
+    screen_ = !ex_logits_ && !tp_ && embd_.type == T_F16 && logits_w_.type == T_F16 && screen_supported(logits_w_) &&
+              getenv("LLMI_FULL_LOGITS") == nullptr;
+    if (screen_) alloc_screen_table(logits_w_, scr_, stream_);
     if (block_) {
       int maxrows = 0, maxhd0 = 0;
       for (const auto& l : L_) {
@@ -451,6 +456,11 @@ void Session::release() {
   if (graph_) (void)hipGraphDestroy(graph_);
   graph_exec_ = nullptr;
   graph_ = nullptr;
+  if (graph_gen_exec_) (void)hipGraphExecDestroy(graph_gen_exec_);
+  if (graph_gen_) (void)hipGraphDestroy(graph_gen_);
+  graph_gen_exec_ = nullptr;
+  graph_gen_ = nullptr;
+  free_screen_table(scr_);
   for (auto& l : L_) {
     for (auto& p : l.qkv) free_weight(p.w);
     for (auto& p : l.gate_up) free_weight(p.w);
@@ -495,7 +505,7 @@ void Session::gemv_parts(const std::vector<GemvPart>& parts, const float* x, int
 }
 
 // One decode token.  Reads *d_token_/*d_pos_, ends with the token feedback.
-void Session::record_step(hipStream_t s) {
+void Session::record_step(hipStream_t s, bool gen) {
   kernels_per_token_ = 0;
   const int E = hp_.n_embd;
   const float emb_scale = std::sqrt(static_cast<float>(E));  // model.cpp:337-338
@@ -530,10 +540,10 @@ void Session::record_step(hipStream_t s) {
   } else {
     record_layers(s, x_q8);
   }
-  record_logits(s);
+  record_logits(s, gen);
 }
 
-void Session::record_logits(hipStream_t s) {
+void Session::record_logits(hipStream_t s, bool gen) {
   const int E = hp_.n_embd;
   // logits (model.cpp:993-1034): F16 table -> mat_vec_mul_fp16, else mat_vec_mul
   // (a tensor-parallel rank: its vocabulary rows, its own argmax key, then
@@ -542,9 +552,14 @@ void Session::record_logits(hipStream_t s) {
   const bool fold = !ex_logits_ && embd_.type == T_F16 && E % 8 == 0;
   float* lg = logits_ + (size_t)tp_rank_ * v_sh_;
   unsigned long long* key = amax_key_ + tp_rank_;
-  for (int r = 0; r < dup("logits"); r++)
-    launch_gemv(logits_w_, act_, lg, ex_logits_ ? GEMV_EXACT : GEMV_FAST, s, fold ? key : nullptr);
-  kernels_per_token_++;
+  if (gen && screen_) {  // token id only: int8 screening + exact rescoring of the candidates
+    launch_screen_argmax(logits_w_, scr_, act_.x16, key, s);
+    kernels_per_token_ += 3;
+  } else {
+    for (int r = 0; r < dup("logits"); r++)
+      launch_gemv(logits_w_, act_, lg, ex_logits_ ? GEMV_EXACT : GEMV_FAST, s, fold ? key : nullptr);
+    kernels_per_token_++;
+  }
   if (!fold) {
     launch_argmax(lg, v_rows_, key, s);
     kernels_per_token_++;
@@ -836,26 +851,31 @@ void Session::record_layers(hipStream_t s, bool x_q8) {
   }
 }
 
-void Session::ensure_graph() {
-  if (!use_graph_ || graph_exec_) return;
+void Session::ensure_graph(bool gen) {
+  hipGraph_t& g = gen ? graph_gen_ : graph_;
+  hipGraphExec_t& ge = gen ? graph_gen_exec_ : graph_exec_;
+  if (!use_graph_ || ge) return;
   LLMI_HIP(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
   try {
-    record_step(stream_);
+    record_step(stream_, gen);
   } catch (...) {
-    hipGraph_t g;
-    (void)hipStreamEndCapture(stream_, &g);
+    hipGraph_t gg;
+    (void)hipStreamEndCapture(stream_, &gg);
     throw;
   }
-  LLMI_HIP(hipStreamEndCapture(stream_, &graph_));
-  LLMI_HIP(hipGraphInstantiate(&graph_exec_, graph_, nullptr, nullptr, 0));
+  LLMI_HIP(hipStreamEndCapture(stream_, &g));
+  LLMI_HIP(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
 }
 
-void Session::run_step() {
+// gen: a decode-loop step (only the token id is kept); otherwise the full
+// logits vector is produced (forward)
+void Session::run_step(bool gen) {
+  gen = gen && screen_;
   if (use_graph_) {
-    ensure_graph();
-    LLMI_HIP(hipGraphLaunch(graph_exec_, stream_));
+    ensure_graph(gen);
+    LLMI_HIP(hipGraphLaunch(gen ? graph_gen_exec_ : graph_exec_, stream_));
   } else {
-    record_step(stream_);
+    record_step(stream_, gen);
   }
 }
 
@@ -895,7 +915,7 @@ void Session::enqueue(int32_t first, int pos, int n_steps) {
   if (first < 0 || first >= vocab_) throw status_error(LLMI_E_RANGE, "token id out of range");
   if (pos < 0 || pos + n_steps > max_ctx_) throw status_error(LLMI_E_RANGE, "generate: context overflow");
   set_token_pos(first, pos, true);
-  for (int i = 0; i < n_steps; i++) run_step();
+  for (int i = 0; i < n_steps; i++) run_step(true);
 }
 
 void Session::sync(int32_t* out, int n) {
@@ -935,6 +955,8 @@ void Session::info(llmi_session_info* o) const {
   o->tp_rank = tp_rank_;
   o->tp_size = tp_size_;
   o->batched_prefill = prefill_ok_ ? 1 : 0;
+  o->screened_logits = screen_ ? 1 : 0;
+  o->screen_bytes = screen_ ? scr_.bytes : 0;
   size_t b = logits_w_.bytes;  // this rank's bytes
   for (const auto& l : L_) {
     for (const auto& p : l.qkv) b += p.w.bytes;
@@ -949,6 +971,31 @@ void Session::info(llmi_session_info* o) const {
 }
 
 void Session::time_kernel(int which, int reps, double* us, double* bytes) {
+  if (which == 2) {  // the decode loop's token selection: prep + screening GEMV + rescoring
+    *us = *bytes = 0.0;
+    if (!screen_ || reps <= 0) return;
+    std::vector<hipEvent_t> ev(2 * (size_t)reps);
+    for (auto& e : ev) LLMI_HIP(hipEventCreate(&e));
+    LLMI_HIP(hipStreamSynchronize(stream_));
+    for (int r = 0; r < reps; r++) {
+      LLMI_HIP(hipEventRecord(ev[2 * r], stream_));
+      launch_screen_argmax(logits_w_, scr_, act_.x16, amax_key_, stream_);
+      LLMI_HIP(hipEventRecord(ev[2 * r + 1], stream_));
+    }
+    LLMI_HIP(hipStreamSynchronize(stream_));
+    double tot = 0;
+    for (int r = 0; r < reps; r++) {
+      float ms = 0;
+      LLMI_HIP(hipEventElapsedTime(&ms, ev[2 * r], ev[2 * r + 1]));
+      tot += ms;
+    }
+    for (auto& e : ev) (void)hipEventDestroy(e);
+    *us = tot * 1000.0 / reps;
+    *bytes = (double)scr_.bytes;
+    LLMI_HIP(hipMemsetAsync(amax_key_, 0, 8 * (size_t)tp_size_, stream_));
+    LLMI_HIP(hipStreamSynchronize(stream_));
+    return;
+  }
   // launches of the dominant kernel family, each bracketed by its own event
   // pair on the session stream (torch.cuda.Event would only see torch's
   // stream), weights swept in decode order so every launch streams from HBM

@@ -67,8 +67,9 @@ class Session {
   void upload(const GGUFView& g);
   void alloc_buffers();
   void build_rope_tables();
-  void record_step(hipStream_t s);
-  void record_logits(hipStream_t s);  // xn_ / act_.x16 -> logits, argmax key, token feedback
+  // gen: the decode loop's step (token id only: screened logits when screen_)
+  void record_step(hipStream_t s, bool gen = false);
+  void record_logits(hipStream_t s, bool gen = false);  // xn_ / act_.x16 -> logits, argmax key, token feedback
   void prefill(const int32_t* tokens, int n, int pos);  // batched (k_prefill.hip)
   void ensure_prefill_buffers(int cap);
   void record_layers(hipStream_t s, bool x_q8);
@@ -80,8 +81,8 @@ class Session {
   // so the step-time delta is that family's in-graph cost
   int dup(const char* k) const { return dup_.find(k) != std::string::npos ? 2 : 1; }
   void set_token_pos(int32_t token, int pos, bool reset_ring);
-  void ensure_graph();
-  void run_step();
+  void ensure_graph(bool gen);
+  void run_step(bool gen = false);
   float* dev_f32_copy(const GGUFView& g, const GTensor* t, int n);
   template <typename T>
   T* dalloc(size_t count) {
@@ -127,6 +128,10 @@ class Session {
   int32_t* h_stage_ = nullptr;  // pinned: token, pos, ring_idx
   hipGraph_t graph_ = nullptr;
   hipGraphExec_t graph_exec_ = nullptr;
+  hipGraph_t graph_gen_ = nullptr;          // the decode loop's step (screened token selection)
+  hipGraphExec_t graph_gen_exec_ = nullptr;
+  bool screen_ = false;                     // k_logits.hip: token ids by screening + exact rescoring
+  ScreenTable scr_;
   int kernels_per_token_ = 0;
   std::string dup_;
   size_t weight_bytes_ = 0;

@@ -117,6 +117,28 @@ int layer_gemv_slab(const DevWeight& w, int role);
 int layer_gemv_gelu_group(int cols);
 void launch_layer_gemv(const DevWeight& w, LayerGemv a, int role, hipStream_t s);
 void launch_argmax(const float* x, int n, unsigned long long* key, hipStream_t s);
+// Greedy token by bounded screening + exact rescoring (k_logits.hip): the
+// same first-index argmax as the fast F16 logits GEMV, from an int8 copy of
+// the table plus the candidate rows re-read in f16.
+struct ScreenX {  // one 32-block of x16 quantized: qx[32], dx, c_b / 2; .a of entry nb = A
+  int4 lo, hi;
+  float dx, c_half, a, pad;
+};
+static_assert(sizeof(ScreenX) == 48, "ScreenX layout");
+struct ScreenTable {
+  uint8_t* qs = nullptr;     // [rows][nb][32] int8
+  uint16_t* d = nullptr;     // [rows][nb] f16 scales (rounded up)
+  ScreenX* xs = nullptr;     // [nb + 1] per token
+  float* hi = nullptr;       // [rows] upper bounds
+  unsigned* m_key = nullptr; // max lower bound (order-preserving key)
+  int rows = 0, cols = 0;
+  size_t bytes = 0;          // qs + d bytes streamed per token
+};
+bool screen_supported(const DevWeight& table);
+void alloc_screen_table(const DevWeight& table, ScreenTable& st, hipStream_t s);
+void free_screen_table(ScreenTable& st);
+void launch_screen_argmax(const DevWeight& table, const ScreenTable& st, const uint16_t* x16,
+                          unsigned long long* amax_key, hipStream_t s);
 void launch_finalize_token(unsigned long long* keys, int n_keys, int shard, int32_t* d_token, int32_t* d_pos,
                            int32_t* ring, int32_t* ring_idx, int ring_cap, hipStream_t s);
 
