@@ -286,6 +286,7 @@ void alloc_screen_table(const DevWeight& table, ScreenTable& st, hipStream_t s) 
   LLMI_HIP(hipMalloc(&st.hi, (size_t)table.rows * 4));
   LLMI_HIP(hipMalloc(&st.m_key, 64));
   LLMI_HIP(hipMemsetAsync(st.xs, 0, (size_t)(nb + 1) * sizeof(ScreenX), s));
+  LLMI_HIP(hipMemsetAsync(st.m_key, 0, 64, s));
   st.rows = table.rows;
   st.cols = table.cols;
   st.bytes = n_blocks * 34;

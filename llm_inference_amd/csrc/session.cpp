@@ -416,8 +416,9 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
       blk = blk && l.fused && l.hd % 32 == 0 && attn_block_supported(l.qkv[0].w, l.o.w, l.hd, nh_, nkv_);
     block_ = blk;
     // greedy token ids by screening (k_logits.hip): the fast F16 logits path
-    // on one device; LLMI_FULL_LOGITS=1 keeps the full GEMV in the decode loop
-    screen_ = !ex_logits_ && !tp_ && embd_.type == T_F16 && logits_w_.type == T_F16 && screen_supported(logits_w_) &&
+    // (a tensor-parallel rank screens its vocabulary shard; the keys meet in
+    // finalize as before); LLMI_FULL_LOGITS=1 keeps the full GEMV in the loop
+    screen_ = !ex_logits_ && embd_.type == T_F16 && logits_w_.type == T_F16 && screen_supported(logits_w_) &&
               getenv("LLMI_FULL_LOGITS") == nullptr;
     if (screen_) alloc_screen_table(logits_w_, scr_, stream_);
     if (block_) {
