@@ -31,12 +31,12 @@ namespace llmi {
 
 namespace {
 
-template <int R, int NW, int P, int E, int ROLE, bool MULTI, bool EARLY>
+template <int R, int NW, int P, int E, int ROLE, bool MULTI, bool EARLY, int PE = 0>
 __global__ __launch_bounds__(NW * 64 + (role_help(ROLE) ? E * 64 : 0)) void gemv_q4_0_layer(LayerGemv a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
   // the attention block's granule tag of this layer, for its next launch
   if (a.epoch && blockIdx.x == 0 && threadIdx.x == 0) *a.epoch += 1u;
-  layer_body<R, NW, P, E, ROLE, MULTI, EARLY>(a, blockIdx.x, s_dyn, BlockSync{});
+  layer_body<R, NW, P, E, ROLE, MULTI, EARLY, 0, PE>(a, blockIdx.x, s_dyn, BlockSync{});
 }
 
 // ---- launch table ----------------------------------------------------------
@@ -51,17 +51,17 @@ __global__ __launch_bounds__(NW * 64 + (role_help(ROLE) ? E * 64 : 0)) void gemv
 //      QUANT -- rounds of 8-float quad lanes (ceil(4 nb / 64 NW)).
 using LaunchFn = void (*)(dim3, size_t, const LayerGemv&, hipStream_t);
 
-template <int R, int NW, int P, int E, int ROLE, bool MULTI, bool EARLY>
+template <int R, int NW, int P, int E, int ROLE, bool MULTI, bool EARLY, int PE = 0>
 void launch_cfg(dim3 grid, size_t lds, const LayerGemv& a, hipStream_t s) {
   const dim3 block(NW * 64 + (role_help(ROLE) ? E * 64 : 0));
   KernelTiming& kt = kernel_timing();
   if (kt.start) {
-    hipExtLaunchKernelGGL((gemv_q4_0_layer<R, NW, P, E, ROLE, MULTI, EARLY>), grid, block, (uint32_t)lds, s,
+    hipExtLaunchKernelGGL((gemv_q4_0_layer<R, NW, P, E, ROLE, MULTI, EARLY, PE>), grid, block, (uint32_t)lds, s,
                           kt.start, kt.stop, 0u, a);
     kt = KernelTiming{};
     return;
   }
-  hipLaunchKernelGGL((gemv_q4_0_layer<R, NW, P, E, ROLE, MULTI, EARLY>), grid, block, lds, s, a);
+  hipLaunchKernelGGL((gemv_q4_0_layer<R, NW, P, E, ROLE, MULTI, EARLY, PE>), grid, block, lds, s, a);
 }
 
 struct LayerCfg {
@@ -74,11 +74,16 @@ struct LayerCfg {
 
 #define LLMI_LCFG(NB, ROLE, R, NW, P, E, MULTI, EARLY, SLAB) \
   {NB, ROLE, R, NW, P, E, MULTI, SLAB, false, launch_cfg<R, NW, P, E, ROLE, MULTI, EARLY>}
+// late roles with the first PE passes issued right after the prologue's loads
+#define LLMI_LCFGP(NB, ROLE, R, NW, P, E, SLAB, PE) \
+  {NB, ROLE, R, NW, P, E, false, SLAB, false, launch_cfg<R, NW, P, E, ROLE, false, false, PE>}
 // PRO / GELU entries with NH helper waves (template role ROLE_PRO_H / ROLE_GELU_H)
 #define LLMI_LCFGH(NB, ROLE, R, NW, P, NH, MULTI, SLAB) \
   {NB, ROLE, R, NW, P, NH, MULTI, SLAB, true,          \
    launch_cfg<R, NW, P, NH, ROLE == ROLE_PRO ? ROLE_PRO_H : ROLE_GELU_H, MULTI, true>}
-// (scripts/gemv_sweep: 4B gate_up GELU 9.1 -> 8.5 us with R8 NW10 slab; 27B
+// (scripts/gemv_sweep: 4B gate_up GELU 9.1 -> 8.5 us with R8 NW10 slab, 7.8
+// us issuing 7 of its 10 passes before the prologue (PE7; all 10: 8.8 us);
+// 4B down 5.8 -> 5.4 us with PE3 (of 5) instead of EARLY; 27B
 // gate_up 35.8 -> 26.3 us with R8 NW8 P4 slab, qkv 10.4 -> 10.0 us, down
 // 24 -> 17-19.5 us issuing the weights after the quantized x is in LDS)
 const LayerCfg kLayerCfgs[] = {
@@ -97,12 +102,12 @@ const LayerCfg kLayerCfgs[] = {
     LLMI_LCFG(168, ROLE_PRO, 4, 8, 6, 11, true, true, 1),      // 27B qkv     256 WGs
     // GELU: prologue + GELU epilogue, 2H = R NW interleaved gate/up rows per WG
     LLMI_LCFG(36, ROLE_GELU, 6, 9, 4, 2, false, false, 0),     // 1B  13824 rows, H 27 -> 256 WGs
-    LLMI_LCFG(80, ROLE_GELU, 8, 10, 10, 4, false, false, 1),   // 4B  20480 rows, H 40 -> 256 WGs
+    LLMI_LCFGP(80, ROLE_GELU, 8, 10, 10, 4, 1, 7),            // 4B  20480 rows, H 40 -> 256 WGs (PE7: 8.4 -> 7.8 us)
     LLMI_LCFG(120, ROLE_GELU, 8, 8, 8, 8, true, false, 0),     // 12B 30720 rows, H 32 -> 480 WGs
     LLMI_LCFG(168, ROLE_GELU, 8, 8, 4, 11, true, false, 1),    // 27B 43008 rows, H 32 -> 672 WGs
     // QUANT: f32 activation quantized into LDS (down projection)
     LLMI_LCFG(216, ROLE_QUANT, 2, 2, 7, 7, false, true, 0),    // 1B down     1152 rows -> 288 WGs
-    LLMI_LCFG(320, ROLE_QUANT, 1, 10, 5, 2, false, true, 0),   // 4B down     2560 rows -> 256 WGs
+    LLMI_LCFGP(320, ROLE_QUANT, 1, 10, 5, 2, 0, 3),           // 4B down     2560 rows -> 256 WGs (PE3: 5.8 -> 5.4 us)
     LLMI_LCFG(480, ROLE_QUANT, 1, 8, 8, 4, false, true, 0),    // 12B down    3840 rows -> 480 WGs
     LLMI_LCFG(672, ROLE_QUANT, 1, 8, 6, 6, true, false, 0),    // 27B down    5376 rows -> 672 WGs
 };

@@ -98,6 +98,18 @@ __device__ __forceinline__ void load_chunk_rb(Chunk<P>& c, __amdgpu_buffer_rsrc_
   }
 }
 
+// passes [P0, P1) of a chunk only (the rest issued by another call)
+template <int R, int P, int P0, int P1>
+__device__ __forceinline__ void load_chunk_rb_part(Chunk<P>& c, __amdgpu_buffer_rsrc_t rq, __amdgpu_buffer_rsrc_t rd,
+                                                   int voq, int vod, int sq, int sd, int npass) {
+#pragma unroll
+  for (int p = P0; p < P1; p++) {
+    const bool in = p < npass;
+    c.q[p] = buf_ld16(rq, in ? voq + p * sq : (1 << 30), 0);
+    c.sw[p] = buf_ld2(rd, in ? vod + p * sd : (1 << 30), 0);
+  }
+}
+
 template <int R, int P>
 __device__ __forceinline__ void eat_chunk_rb(const Chunk<P>& c, int pass0, int nb, int j, bool row_ok,
                                              const XBlock* s_x, float& acc) {
@@ -179,7 +191,11 @@ constexpr int HELP_K4 = 6;  // float4 per helper lane and operand: n <= E * 256 
 //                projection's x blocks are read from their granules
 //                (bs.g_xo), each lane re-loading until the tags are this
 //                launch's.
-template <int R, int NW, int P, int E, int ROLE, bool MULTI, bool EARLY, int SYNC = 0>
+// PE (late roles, !EARLY): the first PE passes of the weight chunk are issued
+// right after the prologue's operand loads, the rest once x is in LDS -- a
+// CU's first weight bytes stream during the prologue without stalling its
+// waves at the issue (PE small against the CU's in-flight capacity).
+template <int R, int NW, int P, int E, int ROLE, bool MULTI, bool EARLY, int SYNC = 0, int PE = 0>
 __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, unsigned char* s_dyn,
                                            const BlockSync& bs) {
   constexpr bool HELP = role_help(ROLE);
@@ -188,6 +204,7 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
   constexpr bool RB = R == 1 || R == 2 || R == 4 || R == 8 || R == 16;  // row-bound lanes, else flat items
   static_assert(!HELP || RB, "helper roles use the row-bound stream");
   constexpr int L = RB ? 64 / R : 64;
+  static_assert(PE == 0 || (RB && !MULTI && !EARLY && PE < P), "PE: single-chunk row-bound late roles");
   LAYER_MARK(0);
   BLK_MARK(bs, 0);
   constexpr int EPT = E, X_LD = E;
@@ -250,6 +267,13 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
       load_chunk<P>(ca, qw, dw, 0, total, lane);  // unconditional (valid clamped rows)
       if constexpr (MULTI) load_chunk<P>(cb, qw, dw, 64 * P, total, lane);
     }
+  };
+  auto issue_head = [&]() {  // passes [0, PE)
+    if constexpr (PE > 0) load_chunk_rb_part<R, P, 0, PE>(ca, rq, rd, voq, vod, sq, sd, npass);
+  };
+  auto issue_tail = [&]() {  // passes [PE, P), or everything
+    if constexpr (PE > 0) load_chunk_rb_part<R, P, PE, P>(ca, rq, rd, voq, vod, sq, sd, npass);
+    else issue_weights();
   };
   const bool helper = HELP && w >= NW;
   if constexpr (HELP) {
@@ -375,6 +399,7 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
       }
     }
     if constexpr (EARLY) issue_weights();
+    else issue_head();
     auto in_row = [&](int k) { return t / 4 + k * QB < nb; };
     float ss = 0.0f;
 #pragma unroll
@@ -456,6 +481,7 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
       xr[r][1] = yb[2 * i + 1];
     }
     if constexpr (EARLY) issue_weights();
+    else issue_head();
 #pragma unroll
     for (int r = 0; r < E; r++) {
       const int i = t + r * T;
@@ -499,7 +525,7 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
   // (HELPER roles: handled above.)
   if constexpr (!HELP) {
     __syncthreads();
-    if constexpr (!EARLY && SYNC != SYNC_WAIT) issue_weights();
+    if constexpr (!EARLY && SYNC != SYNC_WAIT) issue_tail();
   }
 
   LAYER_MARK(4);

@@ -345,6 +345,15 @@ int main(int argc, char** argv) {
       geo_role("gelu R4 NW16 P5 E3", gemv_q4_0_layer<4, 16, 5, 3, 2, false, false>, 64, 1024, gl, true);
       geo_role("gelu R8 NW5 P10 E8", gemv_q4_0_layer<8, 5, 10, 8, 2, false, false>, 40, 320, gl, true);
       geo_role("SLAB gelu R8 NW10 P10 E4", gemv_q4_0_layer<8, 10, 10, 4, 2, false, false>, 80, 640, gs, true);
+      geo_role("SLAB gelu R8 NW10 P10 E4 PE1", gemv_q4_0_layer<8, 10, 10, 4, 2, false, false, 1>, 80, 640, gs, true);
+      geo_role("SLAB gelu R8 NW10 P10 E4 PE2", gemv_q4_0_layer<8, 10, 10, 4, 2, false, false, 2>, 80, 640, gs, true);
+      geo_role("SLAB gelu R8 NW10 P10 E4 PE3", gemv_q4_0_layer<8, 10, 10, 4, 2, false, false, 3>, 80, 640, gs, true);
+      geo_role("SLAB gelu R8 NW10 P10 E4 PE5", gemv_q4_0_layer<8, 10, 10, 4, 2, false, false, 5>, 80, 640, gs, true);
+      geo_role("SLAB gelu R8 NW10 P10 E4 PE7", gemv_q4_0_layer<8, 10, 10, 4, 2, false, false, 7>, 80, 640, gs, true);
+      geo_role("SLAB gelu R8 NW10 P10 E4 PE8", gemv_q4_0_layer<8, 10, 10, 4, 2, false, false, 8>, 80, 640, gs, true);
+      geo_role("SLAB gelu R8 NW10 P10 E4 PE9", gemv_q4_0_layer<8, 10, 10, 4, 2, false, false, 9>, 80, 640, gs, true);
+      geo_role("SLAB gelu R8 NW10 P10 E4 early", gemv_q4_0_layer<8, 10, 10, 4, 2, false, true>, 80, 640, gs, true);
+      geo_role("SLAB gelu R8 NW10 P10 E4 again", gemv_q4_0_layer<8, 10, 10, 4, 2, false, false>, 80, 640, gs, true);
       geo_role("SLAB gelu R4 NW4 P5 E10 (H8)", gemv_q4_0_layer<4, 4, 5, 10, 2, false, false>, 16, 256, gs, true);
       geo_role("SLAB gelu R4 NW4 P5 E10 (H8) early", gemv_q4_0_layer<4, 4, 5, 10, 2, false, true>, 16, 256, gs, true);
       geo_role("SLAB gelu R8 NW4 P10 E10 (H16)", gemv_q4_0_layer<8, 4, 10, 10, 2, false, false>, 32, 256, gs, true);
@@ -361,6 +370,10 @@ int main(int argc, char** argv) {
       geo_role("SLAB gelu R8 NW8 P10 E5", gemv_q4_0_layer<8, 8, 10, 5, 2, false, false>, 64, 512, gs, true);
       geo_role("SLAB gelu R4 NW16 P5 E3", gemv_q4_0_layer<4, 16, 5, 3, 2, false, false>, 64, 1024, gs, true);
       geo_role("pro R4 NW4 P5 E10 (table)", gemv_q4_0_layer<4, 4, 5, 10, 1, false, true>, 16, 256, pro, true);
+      geo_role("pro R4 NW4 P5 E10 late", gemv_q4_0_layer<4, 4, 5, 10, 1, false, false>, 16, 256, pro, true);
+      geo_role("pro R4 NW4 P5 E10 PE2", gemv_q4_0_layer<4, 4, 5, 10, 1, false, false, 2>, 16, 256, pro, true);
+      geo_role("pro R4 NW4 P5 E10 PE3", gemv_q4_0_layer<4, 4, 5, 10, 1, false, false, 3>, 16, 256, pro, true);
+      geo_role("pro R4 NW4 P5 E10 PE4", gemv_q4_0_layer<4, 4, 5, 10, 1, false, false, 4>, 16, 256, pro, true);
       geo_role("pro R8 NW2 P10 E20", gemv_q4_0_layer<8, 2, 10, 20, 1, false, true>, 16, 128, pro, true);
       geo_role("pro R2 NW8 P3 E5", gemv_q4_0_layer<2, 8, 3, 5, 1, false, true>, 16, 512, pro, true);
       geo_role("pro R4 NW8 P5 E5", gemv_q4_0_layer<4, 8, 5, 5, 1, false, true>, 32, 512, pro, true);
@@ -370,6 +383,12 @@ int main(int argc, char** argv) {
     if (nb == 320) {  // 4B down (x 10240)
       geo_role("quant R1 NW10 P5 E2 (table)", gemv_q4_0_layer<1, 10, 5, 2, 3, false, true>, 10, 640, qz, false);
       geo_role("quant R1 NW10 P5 E2 late", gemv_q4_0_layer<1, 10, 5, 2, 3, false, false>, 10, 640, qz, false);
+      geo_role("quant R1 NW10 P5 E2 PE1", gemv_q4_0_layer<1, 10, 5, 2, 3, false, false, 1>, 10, 640, qz, false);
+      geo_role("quant R1 NW10 P5 E2 PE2", gemv_q4_0_layer<1, 10, 5, 2, 3, false, false, 2>, 10, 640, qz, false);
+      geo_role("quant R1 NW10 P5 E2 PE3", gemv_q4_0_layer<1, 10, 5, 2, 3, false, false, 3>, 10, 640, qz, false);
+      geo_role("quant R1 NW10 P5 E2 PE4", gemv_q4_0_layer<1, 10, 5, 2, 3, false, false, 4>, 10, 640, qz, false);
+      geo_role("quant R1 NW10 P5 E2 PE3 b", gemv_q4_0_layer<1, 10, 5, 2, 3, false, false, 3>, 10, 640, qz, false);
+      geo_role("quant R1 NW10 P5 E2 (table) b", gemv_q4_0_layer<1, 10, 5, 2, 3, false, true>, 10, 640, qz, false);
       geo_role("quant R1 NW8 P5 E3", gemv_q4_0_layer<1, 8, 5, 3, 3, false, true>, 8, 512, qz, false);
       geo_role("quant R2 NW5 P10 E4", gemv_q4_0_layer<2, 5, 10, 4, 3, false, true>, 10, 320, qz, false);
       geo_role("quant R2 NW8 P10 E3", gemv_q4_0_layer<2, 8, 10, 3, 3, false, true>, 16, 512, qz, false);
