@@ -309,7 +309,8 @@ void launch_screen_argmax(const DevWeight& table, const ScreenTable& st, const u
   hipLaunchKernelGGL(screen_prep_kernel, dim3(1), dim3(256), 0, s, x16, n, st.xs, st.m_key);
   const int cpl = (2 * nb + 31) / 32;
   const int rows = table.rows;
-  const dim3 grid((std::min((rows + 1) / 2, 256 * 8) + 3) / 4);
+  static const int wpc = getenv("LLMI_SCREEN_WPC") ? atoi(getenv("LLMI_SCREEN_WPC")) : 8;  // waves per CU (A/B)
+  const dim3 grid((std::min((rows + 1) / 2, 256 * wpc) + 3) / 4);
   switch (cpl) {
 #define LLMI_SCR(C)                                                                                               \
   case C:                                                                                                         \

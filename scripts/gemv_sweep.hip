@@ -350,7 +350,13 @@ int main(int argc, char** argv) {
       geo_role("SLAB gelu R8 NW10 P10 E4 PE3", gemv_q4_0_layer<8, 10, 10, 4, 2, false, false, 3>, 80, 640, gs, true);
       geo_role("SLAB gelu R8 NW10 P10 E4 PE5", gemv_q4_0_layer<8, 10, 10, 4, 2, false, false, 5>, 80, 640, gs, true);
       geo_role("SLAB gelu R8 NW10 P10 E4 PE7", gemv_q4_0_layer<8, 10, 10, 4, 2, false, false, 7>, 80, 640, gs, true);
+      geo_role("SLAB gelu R8 NW10 P10 E4 PE6", gemv_q4_0_layer<8, 10, 10, 4, 2, false, false, 6>, 80, 640, gs, true);
       geo_role("SLAB gelu R8 NW10 P10 E4 PE8", gemv_q4_0_layer<8, 10, 10, 4, 2, false, false, 8>, 80, 640, gs, true);
+      geo_role("SLAB gelu R4 NW8 P5 E5 (H16) PE3", gemv_q4_0_layer<4, 8, 5, 5, 2, false, false, 3>, 32, 512, gs, true);
+      geo_role("SLAB gelu R4 NW8 P5 E5 (H16) PE4", gemv_q4_0_layer<4, 8, 5, 5, 2, false, false, 4>, 32, 512, gs, true);
+      geo_role("SLAB gelu R8 NW8 P10 E5 PE7", gemv_q4_0_layer<8, 8, 10, 5, 2, false, false, 7>, 64, 512, gs, true);
+      geo_role("SLAB gelu R8 NW5 P10 E8 PE7", gemv_q4_0_layer<8, 5, 10, 8, 2, false, false, 7>, 40, 320, gs, true);
+      geo_role("SLAB gelu R4 NW16 P5 E3 PE3", gemv_q4_0_layer<4, 16, 5, 3, 2, false, false, 3>, 64, 1024, gs, true);
       geo_role("SLAB gelu R8 NW10 P10 E4 PE9", gemv_q4_0_layer<8, 10, 10, 4, 2, false, false, 9>, 80, 640, gs, true);
       geo_role("SLAB gelu R8 NW10 P10 E4 early", gemv_q4_0_layer<8, 10, 10, 4, 2, false, true>, 80, 640, gs, true);
       geo_role("SLAB gelu R8 NW10 P10 E4 again", gemv_q4_0_layer<8, 10, 10, 4, 2, false, false>, 80, 640, gs, true);
