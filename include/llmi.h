@@ -143,6 +143,17 @@ void llmi_session_destroy(llmi_session* s);
 int llmi_session_forward(llmi_session* s, const int32_t* tokens, int n_tokens, int pos, float* logits,
                          int32_t* argmax);
 
+/* Layer-by-layer triage: llmi_session_forward's token
+ * loop, one token at a time with eager launches, appending the
+ * intermediates the reference prints under --verbose (model.cpp VERBOSE
+ * print_tensor calls: inp_scaled, attn_norm-L, Qcur-L, Kcur-L, Vcur-L,
+ * kqv_out-L, "attention results (node_30 for MUL_MAT)-L", sa_out-L,
+ * ffn_norm-L, ffn_geglu-L, ffn_out-L, l_out-L, result_norm, result_output)
+ * to the text file `path` in tensor.h's print_tensor format, so the two
+ * dumps pair by name and occurrence (scripts/compare_dumps.py, the
+ * compare_tensors.py counterpart).  Slow; the results equal forward's. */
+int llmi_session_dump(llmi_session* s, const int32_t* tokens, int n_tokens, int pos, const char* path);
+
 /* Greedy decode loop of main.cpp:172-224 kept on the device: token `first`
  * at position `pos`, then n_steps forwards, each feeding its argmax to the
  * next without a host round trip.  out_tokens[i] = argmax after step i. */

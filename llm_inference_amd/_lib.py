@@ -77,6 +77,7 @@ _SIGS = {
     "llmi_tp_group_destroy": (None, [_vp]),
     "llmi_session_forward": (C.c_int, [_vp, _vp, C.c_int, C.c_int, _vp, _vp]),
     "llmi_session_generate": (C.c_int, [_vp, _i32, C.c_int, C.c_int, _vp]),
+    "llmi_session_dump": (C.c_int, [_vp, _vp, C.c_int, C.c_int, C.c_char_p]),
     "llmi_session_enqueue": (C.c_int, [_vp, _i32, C.c_int, C.c_int]),
     "llmi_session_sync": (C.c_int, [_vp, _vp, C.c_int]),
     "llmi_session_get_info": (C.c_int, [_vp, C.POINTER(SessionInfo)]),

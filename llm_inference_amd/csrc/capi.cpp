@@ -409,6 +409,10 @@ int llmi_session_forward(llmi_session* s, const int32_t* tokens, int n_tokens, i
   return guard([&] { s->s->forward(tokens, n_tokens, pos, logits, argmax); });
 }
 
+int llmi_session_dump(llmi_session* s, const int32_t* tokens, int n_tokens, int pos, const char* path) {
+  return guard([&] { s->s->forward_dump(tokens, n_tokens, pos, path); });
+}
+
 int llmi_session_generate(llmi_session* s, int32_t first, int pos, int n_steps, int32_t* out_tokens) {
   return guard([&] {
     s->s->enqueue(first, pos, n_steps);

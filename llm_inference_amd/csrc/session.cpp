@@ -533,6 +533,8 @@ void Session::record_step(hipStream_t s, bool gen) {
     launch_rms_norm(resid_, L_[0].attn_norm, xn_, E, 1, hp_.eps, ex_norm_, s);
     kernels_per_token_ += 2;
   }
+  dump("inp_scaled", resid_, E, s);  // model.cpp:711-713
+  dump("attn_norm-0", xn_, E, s);
   bool fused = fuse_layers_;
   for (const auto& l : L_) fused &= l.fused;
   if (tp_ && !fused) throw status_error(LLMI_E_ARG, "tensor parallel needs the fused layer path");
@@ -560,6 +562,7 @@ void Session::record_logits(hipStream_t s, bool gen) {
     for (int r = 0; r < dup("logits"); r++)
       launch_gemv(logits_w_, act_, lg, ex_logits_ ? GEMV_EXACT : GEMV_FAST, s, fold ? key : nullptr);
     kernels_per_token_++;
+    dump("result_output", lg, v_rows_, s);  // model.cpp:1046
   }
   if (!fold) {
     launch_argmax(lg, v_rows_, key, s);
@@ -698,7 +701,8 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
     LayerDev& Ld = L_[l];
     const int hd = Ld.hd;
     unsigned* epoch = block_ ? blk_epoch_ + l : nullptr;
-    if (block_) {  // qkv + attention + o: one launch (k_attn.hip attention block)
+    const std::string L = std::to_string(l);
+    if (block_ && !dump_) {  // qkv + attention + o: one launch (k_attn.hip attention block)
       LayerGemv g;
       int qrole = LAYER_PLAIN;
       if (l == 0) {
@@ -750,10 +754,16 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
         g.w_next = Ld.attn_norm;
         g.eps = hp_.eps;
         g.out = qkv_;
+        if (dump_) g.xn_out = xn_;
         for (int r = 0; r < dup("qkv"); r++) launch_layer_gemv(Ld.qkv[0].w, g, LAYER_PRO, s);
+        dump("l_out-" + std::to_string(l - 1), other, E, s);
+        dump("attn_norm-" + L, xn_, E, s);
         std::swap(cur, other);
       }
       kernels_per_token_++;
+      dump("Qcur-" + L, qkv_, nh_ * hd, s);
+      dump("Kcur-" + L, qkv_ + Ld.k_off, nkv_ * hd, s);
+      dump("Vcur-" + L, qkv_ + Ld.v_off, nkv_ * hd, s);
       // this rank's heads (all of them without tensor parallelism)
       QKVArgs qa{qkv_, Ld.k_off, Ld.v_off, nh_, nkv_, hd, Ld.q_norm, Ld.k_norm,
                  Ld.is_swa ? rope_swa_ : rope_glb_, hp_.attn_scale, hp_.eps, q_, Ld.kc, Ld.vc, max_ctx_, d_pos_};
@@ -764,6 +774,7 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
                   ticket_, q8_in_combine ? act_.q8.xb + (size_t)tp_rank_ * hb : nullptr};
       for (int r = 0; r < dup("attn"); r++) launch_attention(aa, false, s, &qa);
       kernels_per_token_++;
+      dump("kqv_out-" + L, attn_, nh_ * hd, s);
       if (!q8_in_combine) {
         launch_quantize_q8_0(attn_, hp_.n_head * hd, act_.q8, s);
         kernels_per_token_++;
@@ -773,6 +784,7 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
       go.xg = act_.q8.xb;
       go.out = o_out_ + (size_t)tp_rank_ * e_sh_;
       for (int r = 0; r < dup("o_proj"); r++) launch_layer_gemv(Ld.o.w, go, LAYER_PLAIN, s);
+      dump("attention results (node_30 for MUL_MAT)-" + L, o_out_, E, s);
     }
     if (tp_) coll_->all_gather(o_out_, (size_t)e_sh_ * sizeof(float), s);
     LayerGemv gg;
@@ -784,7 +796,11 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
     gg.eps = hp_.eps;
     gg.hid = hid_ + (size_t)tp_rank_ * f_sh_;
     gg.epoch = epoch;  // advances the attention block's granule tag of this layer
+    if (dump_) gg.xn_out = xn_;
     for (int r = 0; r < dup("gate_up"); r++) launch_layer_gemv(Ld.gate_up[0].w, gg, LAYER_GELU, s);
+    dump("sa_out-" + L, other, E, s);
+    dump("ffn_norm-" + L, xn_, E, s);
+    dump("ffn_geglu-" + L, hid_, hp_.n_ff, s);
     std::swap(cur, other);
     if (tp_) coll_->all_gather(hid_, (size_t)f_sh_ * sizeof(float), s);
     LayerGemv gd;
@@ -792,6 +808,7 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
     gd.out = d_out_ + (size_t)tp_rank_ * e_sh_;
     for (int r = 0; r < dup("down"); r++) launch_layer_gemv(Ld.down.w, gd, LAYER_QUANT, s);
     if (tp_) coll_->all_gather(d_out_, (size_t)e_sh_ * sizeof(float), s);
+    dump("ffn_out-" + L, d_out_, E, s);
     kernels_per_token_ += block_ ? 2 : 3;  // (o, when not in the attention block,) gate_up, down
   }
   // final residual + output_norm (-> xn_, and f16 x for an F16 logits table)
@@ -800,6 +817,8 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
   if (embd_.type == T_F16) o2.x16 = act_.x16;
   launch_residual_norm(d_out_, L_.back().post_ffw_norm, cur, out_norm_, o2, E, hp_.eps, false, s);
   kernels_per_token_++;
+  dump("l_out-" + std::to_string(hp_.n_layer - 1), cur, E, s);
+  dump("result_norm", xn_, E, s);
 }
 
 void Session::record_layers(hipStream_t s, bool x_q8) {
@@ -817,6 +836,10 @@ void Session::record_layers(hipStream_t s, bool x_q8) {
     LayerDev& Ld = L_[l];
     const int hd = Ld.hd;
     for (int r = 0; r < dup("qkv"); r++) gemv_parts(Ld.qkv, xn_, E, qkv_, s, x_q8);
+    const std::string L = std::to_string(l);
+    dump("Qcur-" + L, qkv_, hp_.n_head * hd, s);
+    dump("Kcur-" + L, qkv_ + Ld.k_off, hp_.n_head_kv * hd, s);
+    dump("Vcur-" + L, qkv_ + Ld.v_off, hp_.n_head_kv * hd, s);
     QKVArgs qa{qkv_, Ld.k_off, Ld.v_off, hp_.n_head, hp_.n_head_kv, hd, Ld.q_norm, Ld.k_norm,
                Ld.is_swa ? rope_swa_ : rope_glb_, hp_.attn_scale, hp_.eps, q_, Ld.kc, Ld.vc, max_ctx_, d_pos_};
     const bool fuse_qk = !ex_attn_ && !ex_norm_;  // norm/rope/KV-append inside the attention launch
@@ -830,9 +853,13 @@ void Session::record_layers(hipStream_t s, bool x_q8) {
                 ticket_, fused_q8 ? act_.q8.xb : nullptr};
     for (int r = 0; r < dup("attn"); r++) launch_attention(aa, ex_attn_, s, fuse_qk ? &qa : nullptr);
     kernels_per_token_++;
+    dump("kqv_out-" + L, attn_, hp_.n_head * hd, s);
     for (int r = 0; r < dup("o_proj"); r++) gemv_parts({Ld.o}, attn_, hp_.n_head * hd, o_out_, s, fused_q8);
+    dump("attention results (node_30 for MUL_MAT)-" + L, o_out_, E, s);
     NormOut o1 = nout(Ld.gate_up);
     launch_residual_norm(o_out_, Ld.post_attn_norm, resid_, Ld.ffn_norm, o1, E, hp_.eps, ex_norm_, s);
+    dump("sa_out-" + L, resid_, E, s);
+    dump("ffn_norm-" + L, xn_, E, s);
     if (dup("norm") > 1)  // ablation: the same launch on a scratch residual (values irrelevant)
       launch_residual_norm(o_out_, Ld.post_attn_norm, resid_scratch_, Ld.ffn_norm, o1, E, hp_.eps, ex_norm_, s);
     kernels_per_token_++;
@@ -840,7 +867,9 @@ void Session::record_layers(hipStream_t s, bool x_q8) {
     const bool d_q8 = Ld.down.w.type == T_Q4_0 || Ld.down.w.type == T_Q8_0;
     for (int r = 0; r < dup("gelu"); r++) launch_gelu_quant(gu_, F, hid_, d_q8 ? &act_.q8 : nullptr, s);
     kernels_per_token_++;
+    dump("ffn_geglu-" + L, hid_, F, s);
     for (int r = 0; r < dup("down"); r++) gemv_parts({Ld.down}, hid_, F, d_out_, s, d_q8);
+    dump("ffn_out-" + L, d_out_, E, s);
     const bool last = l + 1 == hp_.n_layer;
     const float* w_next = last ? out_norm_ : L_[l + 1].attn_norm;
     NormOut o2 = last ? NormOut{} : nout(L_[l + 1].qkv);
@@ -849,6 +878,8 @@ void Session::record_layers(hipStream_t s, bool x_q8) {
     launch_residual_norm(d_out_, Ld.post_ffw_norm, resid_, w_next, o2, E, hp_.eps, ex_norm_, s);
     x_q8 = o2.q8 != nullptr;
     kernels_per_token_++;
+    dump("l_out-" + L, resid_, E, s);
+    dump(last ? std::string("result_norm") : "attn_norm-" + std::to_string(l + 1), xn_, E, s);
   }
 }
 
@@ -909,6 +940,58 @@ void Session::forward(const int32_t* tokens, int n, int pos, float* logits, int3
   if (logits) LLMI_HIP(hipMemcpyAsync(logits, logits_, (size_t)vocab_ * 4, hipMemcpyDeviceToHost, stream_));
   if (argmax) LLMI_HIP(hipMemcpyAsync(argmax, d_token_, 4, hipMemcpyDeviceToHost, stream_));
   LLMI_HIP(hipStreamSynchronize(stream_));
+  check_device_error();
+}
+
+// tensor.h print_tensor_generic for a {n, 1, 1, 1} tensor: 3 leading and 3
+// trailing values ("%12.4f") around "..., " when n > 6, then the float
+// left-to-right sum (std::accumulate) as "sum = %.6f"
+void Session::dump(const std::string& name, const float* dev, int n, hipStream_t s) {
+  if (!dump_) return;
+  LLMI_HIP(hipStreamSynchronize(s));
+  std::vector<float> h((size_t)n);
+  LLMI_HIP(hipMemcpy(h.data(), dev, (size_t)n * 4, hipMemcpyDeviceToHost));
+  std::fprintf(dump_, "%s = {%d, 1, 1, 1}\n    [\n     [\n      [", name.c_str(), n);
+  for (int i = 0; i < n; i++) {
+    if (i == 3 && n > 6) {
+      std::fprintf(dump_, "..., ");
+      i = n - 3;
+    }
+    std::fprintf(dump_, "%12.4f", h[(size_t)i]);
+    if (i < n - 1) std::fprintf(dump_, ", ");
+  }
+  float sum = 0.0f;
+  for (float v : h) sum += v;
+  std::fprintf(dump_, "],\n     ],\n    ]\n    sum = %.6f\n", sum);
+}
+
+void Session::forward_dump(const int32_t* tokens, int n, int pos, const char* path) {
+  if (n <= 0) throw status_error(LLMI_E_ARG, "dump: no tokens");
+  if (pos < 0 || pos + n > max_ctx_) throw status_error(LLMI_E_RANGE, "dump: context overflow");
+  for (int i = 0; i < n; i++)
+    if (tokens[i] < 0 || tokens[i] >= vocab_) throw status_error(LLMI_E_RANGE, "dump: token id out of range");
+  if (tp_) throw status_error(LLMI_E_ARG, "dump: one device only");
+  std::FILE* f = std::fopen(path, "a");
+  if (!f) throw status_error(LLMI_E_ARG, std::string("dump: cannot open ") + path);
+  const bool graph = use_graph_;
+  use_graph_ = false;  // eager: every launch can be followed by a copy
+  dump_ = f;
+  auto done = [&] {
+    dump_ = nullptr;
+    use_graph_ = graph;
+    std::fclose(f);
+  };
+  try {
+    for (int i = 0; i < n; i++) {
+      set_token_pos(tokens[i], pos + i, i == 0);
+      record_step(stream_, false);
+    }
+    LLMI_HIP(hipStreamSynchronize(stream_));
+  } catch (...) {
+    done();
+    throw;
+  }
+  done();
   check_device_error();
 }
 

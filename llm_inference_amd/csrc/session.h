@@ -1,6 +1,7 @@
 // session.h -- device-resident Gemma-3 decode session (behind llmi_session_*).
 #pragma once
 
+#include <cstdio>
 #include <memory>
 #include <string>
 #include <utility>
@@ -55,6 +56,7 @@ class Session {
   Session& operator=(const Session&) = delete;
 
   void forward(const int32_t* tokens, int n_tokens, int pos, float* logits, int32_t* argmax);
+  void forward_dump(const int32_t* tokens, int n_tokens, int pos, const char* path);
   void enqueue(int32_t first, int pos, int n_steps);
   void sync(int32_t* out_tokens, int n);
   void info(llmi_session_info* out) const;
@@ -82,6 +84,9 @@ class Session {
   int dup(const char* k) const { return dup_.find(k) != std::string::npos ? 2 : 1; }
   void set_token_pos(int32_t token, int pos, bool reset_ring);
   void ensure_graph(bool gen);
+  // llmi_session_dump: eager steps with print_tensor-format dumps (dump_ set)
+  std::FILE* dump_ = nullptr;
+  void dump(const std::string& name, const float* dev, int n, hipStream_t s);
   void run_step(bool gen = false);
   float* dev_f32_copy(const GGUFView& g, const GTensor* t, int n);
   template <typename T>

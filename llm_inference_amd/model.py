@@ -80,6 +80,12 @@ class Model:
         self.last_argmax = int(am[0])
         return lg
 
+    def dump(self, tokens: Sequence[int], pos: int, path: str) -> None:
+        """llmi_session_dump: forward one token at a time, appending the
+        reference's --verbose intermediates (print_tensor format) to `path`."""
+        t = np.ascontiguousarray(tokens, np.int32)
+        check(lib().llmi_session_dump(self.h, ptr(t), t.size, pos, path.encode()))
+
     def generate(self, first: int, pos: int, n_steps: int) -> np.ndarray:
         out = np.zeros(max(n_steps, 1), np.int32)
         check(lib().llmi_session_generate(self.h, first, pos, n_steps, ptr(out)))

@@ -16,6 +16,8 @@
 #include <string>
 #include <vector>
 
+#include <iostream>
+
 #include "gguf.h"
 #include "model.h"
 #include "ops.h"
@@ -46,6 +48,12 @@ static std::vector<uint8_t> one_tensor_gguf(uint32_t type, const void* data, siz
 extern "C" {
 
 const char* ref_last_error() { return g_err.c_str(); }
+// --verbose of main.cpp:39-51: the model's VERBOSE print_tensor dumps go to stdout
+void ref_set_verbose(int on) {
+  verbose_g = on != 0;
+  std::cout.flush();
+}
+void ref_flush() { std::cout.flush(); }
 void ref_init_ops(int n_threads) { init_ops(n_threads); }
 float ref_f16_to_f32(uint16_t h) { return f16_to_f32(h); }
 uint16_t ref_f32_to_f16(float f) { return f32_to_f16(f); }
