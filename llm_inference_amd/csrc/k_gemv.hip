@@ -564,10 +564,13 @@ __global__ __launch_bounds__(256) void gemv_bf16_exact(const uint16_t* __restric
 // launcher
 // ===========================================================================
 // smallest R in {1,2,4,8} with R*items a multiple of 64 (full passes), capped
-// at 8 (then the last pass is partially masked)
-static int rows_per_wave(int items_per_row) {
+// at 8 (then the last pass is partially masked), and lowered again until the
+// grid has a 4-wave work-group per CU (wide rows over few rows, e.g. the 1B
+// down projection 1152 x 216 blocks, ran on 36 work-groups at R = 8)
+static int rows_per_wave(int items_per_row, int rows) {
   int R = 1;
   while (R < 8 && (R * items_per_row) % 64 != 0) R *= 2;
+  while (R > 1 && rows / (4 * R) < 256) R /= 2;
   return R;
 }
 // passes issued per chunk: all of them up to 8
@@ -619,7 +622,7 @@ void launch_gemv(const DevWeight& w, const ActBuf& x, float* o, GemvMode mode, h
           hipLaunchKernelGGL(gemv_q8_0_exact, dim3((rows + 255) / 256), dim3(256), 0, s, (const int4*)w.qs, w.d, rows,
                              nb, x.q8.xb, o);
       } else {
-        const int R = rows_per_wave(nb), P = passes_per_chunk(R, nb);
+        const int R = rows_per_wave(nb, rows), P = passes_per_chunk(R, nb);
         const dim3 grid((rows + 4 * R - 1) / (4 * R));
         const uint32_t mg = div_magic(nb);
         if (w.type == T_Q4_0) {
@@ -657,7 +660,7 @@ void launch_gemv(const DevWeight& w, const ActBuf& x, float* o, GemvMode mode, h
         }
       } else {
         const int nc = w.cols / 8;
-        const int R = rows_per_wave(nc), P = passes_per_chunk(R, nc);
+        const int R = rows_per_wave(nc, rows), P = passes_per_chunk(R, nc);
         const dim3 grid((rows + 4 * R - 1) / (4 * R));
         LLMI_RP_SWITCH(gemv_f16_fast, R, P, grid, (const uint4*)w.qs, rows, nc, div_magic(nc), (const uint4*)x.x16,
                        o, amax_key)
