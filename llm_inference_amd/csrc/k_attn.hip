@@ -531,12 +531,19 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, const QKVArgs
   }
   constexpr int PAIRS = (G * HD + 255) / 256;
   float v[PAIRS][NS];
+  // splits that own no key (c TK >= n_keys: m = -inf, l = 0, zero
+  // accumulator, weight 0) are read out of bounds -- 0 without memory
+  // traffic, and the loads stay unconditional (8-15 of 32 at pos 512-768)
+  const int n_act = min(NS, (n_keys + TK - 1) / TK);
+  const __amdgpu_buffer_rsrc_t rpart = buf_rsrc(part0, (uint32_t)(G * NS * (HD + 2) * 4));
 #pragma unroll
   for (int p = 0; p < PAIRS; p++) {
     const int idx = min(t + p * 256, G * HD - 1);
-    const float* pg = part0 + (size_t)(idx / HD) * NS * (HD + 2) + idx % HD;
+    const int eg = (idx / HD) * NS * (HD + 2) + idx % HD;
 #pragma unroll
-    for (int cc = 0; cc < NS; cc++) v[p][cc] = ld_sc1(pg + (size_t)cc * (HD + 2));
+    for (int cc = 0; cc < NS; cc++)
+      v[p][cc] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+          rpart, cc < n_act ? (eg + cc * (HD + 2)) * 4 : (1 << 30), 0, BUF_SC1));
   }
   __shared__ float s_wt[G][NS];
   __shared__ float s_L[G];
