@@ -31,12 +31,12 @@ namespace llmi {
 
 namespace {
 
-template <int R, int NW, int P, int E, int ROLE, bool MULTI, bool EARLY, int PE = 0>
+template <int R, int NW, int P, int E, int ROLE, bool MULTI, bool EARLY, int PE = 0, bool W8 = false>
 __global__ __launch_bounds__(NW * 64 + (role_help(ROLE) ? E * 64 : 0)) void gemv_q4_0_layer(LayerGemv a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
   // the attention block's granule tag of this layer, for its next launch
   if (a.epoch && blockIdx.x == 0 && threadIdx.x == 0) *a.epoch += 1u;
-  layer_body<R, NW, P, E, ROLE, MULTI, EARLY, 0, PE>(a, blockIdx.x, s_dyn, BlockSync{});
+  layer_body<R, NW, P, E, ROLE, MULTI, EARLY, 0, PE, W8>(a, blockIdx.x, s_dyn, BlockSync{});
 }
 
 // ---- launch table ----------------------------------------------------------
@@ -51,17 +51,17 @@ __global__ __launch_bounds__(NW * 64 + (role_help(ROLE) ? E * 64 : 0)) void gemv
 //      QUANT -- rounds of 8-float quad lanes (ceil(4 nb / 64 NW)).
 using LaunchFn = void (*)(dim3, size_t, const LayerGemv&, hipStream_t);
 
-template <int R, int NW, int P, int E, int ROLE, bool MULTI, bool EARLY, int PE = 0>
+template <int R, int NW, int P, int E, int ROLE, bool MULTI, bool EARLY, int PE = 0, bool W8 = false>
 void launch_cfg(dim3 grid, size_t lds, const LayerGemv& a, hipStream_t s) {
   const dim3 block(NW * 64 + (role_help(ROLE) ? E * 64 : 0));
   KernelTiming& kt = kernel_timing();
   if (kt.start) {
-    hipExtLaunchKernelGGL((gemv_q4_0_layer<R, NW, P, E, ROLE, MULTI, EARLY, PE>), grid, block, (uint32_t)lds, s,
+    hipExtLaunchKernelGGL((gemv_q4_0_layer<R, NW, P, E, ROLE, MULTI, EARLY, PE, W8>), grid, block, (uint32_t)lds, s,
                           kt.start, kt.stop, 0u, a);
     kt = KernelTiming{};
     return;
   }
-  hipLaunchKernelGGL((gemv_q4_0_layer<R, NW, P, E, ROLE, MULTI, EARLY, PE>), grid, block, lds, s, a);
+  hipLaunchKernelGGL((gemv_q4_0_layer<R, NW, P, E, ROLE, MULTI, EARLY, PE, W8>), grid, block, lds, s, a);
 }
 
 struct LayerCfg {
@@ -70,6 +70,7 @@ struct LayerCfg {
   int slab;  // weight layout this entry reads (sweep: slab pays for R >= 4 on big matrices)
   bool help;  // PRO/GELU with E helper waves (role_help)
   LaunchFn fn;
+  bool w8 = false;  // Q8_0 weights (P counts half-block passes)
 };
 
 #define LLMI_LCFG(NB, ROLE, R, NW, P, E, MULTI, EARLY, SLAB) \
@@ -77,6 +78,9 @@ struct LayerCfg {
 // late roles with the first PE passes issued right after the prologue's loads
 #define LLMI_LCFGP(NB, ROLE, R, NW, P, E, SLAB, PE) \
   {NB, ROLE, R, NW, P, E, false, SLAB, false, launch_cfg<R, NW, P, E, ROLE, false, false, PE>}
+// Q8_0 weights: row-major, single chunk (P passes of 16-B half blocks)
+#define LLMI_LCFG8(NB, ROLE, R, NW, P, E, EARLY) \
+  {NB, ROLE, R, NW, P, E, false, 0, false, launch_cfg<R, NW, P, E, ROLE, false, EARLY, 0, true>, true}
 // PRO / GELU entries with NH helper waves (template role ROLE_PRO_H / ROLE_GELU_H)
 #define LLMI_LCFGH(NB, ROLE, R, NW, P, NH, MULTI, SLAB) \
   {NB, ROLE, R, NW, P, NH, MULTI, SLAB, true,          \
@@ -110,12 +114,19 @@ const LayerCfg kLayerCfgs[] = {
     LLMI_LCFGP(320, ROLE_QUANT, 1, 10, 5, 2, 0, 3),           // 4B down     2560 rows -> 256 WGs (PE3: 5.8 -> 5.4 us)
     LLMI_LCFG(480, ROLE_QUANT, 1, 8, 8, 4, false, true, 0),    // 12B down    3840 rows -> 480 WGs
     LLMI_LCFG(672, ROLE_QUANT, 1, 8, 6, 6, true, false, 0),    // 27B down    5376 rows -> 672 WGs
+    // Q8_0 weights (Gemma-3 1B Q8_0, BASELINE configs[3]): 2 nb half-block units per row
+    LLMI_LCFG8(36, ROLE_PLAIN, 4, 2, 5, 1, true),     // 1B qkv l0   1536 rows -> 192 WGs
+    LLMI_LCFG8(36, ROLE_PRO, 4, 4, 5, 5, true),       // 1B qkv      96 WGs
+    LLMI_LCFG8(32, ROLE_PLAIN, 1, 4, 1, 1, true),     // 1B o        1152 rows -> 288 WGs
+    LLMI_LCFG8(36, ROLE_GELU, 8, 8, 9, 3, false),     // 1B gate_up  13824 rows, H 32 -> 216 WGs
+    LLMI_LCFG8(216, ROLE_QUANT, 1, 4, 7, 4, true),    // 1B down     1152 rows -> 288 WGs
 };
 #undef LLMI_LCFG
 
-const LayerCfg* find_cfg(int nb, int role) {
+const LayerCfg* find_cfg(int nb, int role, uint32_t type = T_Q4_0) {
+  if (type != T_Q4_0 && type != T_Q8_0) return nullptr;
   for (const auto& c : kLayerCfgs)
-    if (c.nb == nb && c.role == role) return &c;
+    if (c.nb == nb && c.role == role && c.w8 == (type == T_Q8_0)) return &c;
   return nullptr;
 }
 
@@ -131,20 +142,20 @@ KernelTiming& kernel_timing() {
 }
 
 bool layer_gemv_supported(const DevWeight& w, int role) {
-  if (w.type != T_Q4_0 || w.cols % 32 != 0 || w.rows <= 0) return false;
-  const LayerCfg* c = find_cfg(w.cols / 32, role);
+  if ((w.type != T_Q4_0 && w.type != T_Q8_0) || w.cols % 32 != 0 || w.rows <= 0) return false;
+  const LayerCfg* c = find_cfg(w.cols / 32, role, w.type);
   if (!c) return false;
   if (role == LAYER_GELU && w.rows % (c->R * c->NW) != 0) return false;
   return true;
 }
 
 int layer_gemv_slab(const DevWeight& w, int role) {
-  const LayerCfg* c = w.cols % 32 == 0 ? find_cfg(w.cols / 32, role) : nullptr;
+  const LayerCfg* c = w.cols % 32 == 0 ? find_cfg(w.cols / 32, role, w.type) : nullptr;
   return c ? c->slab : 0;
 }
 
-int layer_gemv_gelu_group(int cols) {
-  const LayerCfg* c = cols % 32 == 0 ? find_cfg(cols / 32, LAYER_GELU) : nullptr;
+int layer_gemv_gelu_group(int cols, uint32_t type) {
+  const LayerCfg* c = cols % 32 == 0 ? find_cfg(cols / 32, LAYER_GELU, type) : nullptr;
   return c ? c->R * c->NW / 2 : 0;
 }
 
@@ -156,10 +167,10 @@ void launch_layer_gemv(const DevWeight& w, LayerGemv a, int role, hipStream_t s)
   if (role == LAYER_PLAIN && !a.xg) throw std::runtime_error("layer gemv: missing activation blocks");
   if (role == LAYER_QUANT && !a.y) throw std::runtime_error("layer gemv: missing activation");
   if (role == LAYER_GELU ? !a.hid : !a.out) throw std::runtime_error("layer gemv: missing output");
-  const LayerCfg& c = *find_cfg(w.cols / 32, role);
-  const int nb = w.cols / 32;
+  const LayerCfg& c = *find_cfg(w.cols / 32, role, w.type);
+  const int nb = w.cols / 32, nu = c.w8 ? 2 * nb : nb;  // 16-B units per row
   const bool rb = c.R == 1 || c.R == 2 || c.R == 4 || c.R == 8 || c.R == 16;
-  if (!c.multi && (rb ? (nb + 64 / c.R - 1) / (64 / c.R) > c.P : c.R * nb > 64 * c.P))
+  if (!c.multi && (rb ? (nu + 64 / c.R - 1) / (64 / c.R) > c.P : c.R * nb > 64 * c.P))
     throw std::runtime_error("layer gemv: table entry needs MULTI");
   if (pro && !c.help && w.cols > c.E * c.NW * 64) throw std::runtime_error("layer gemv: prologue E too small");
   if (pro && c.help && (w.cols % (c.E * 32) != 0 || w.cols > c.E * 256 * HELP_K4))

@@ -110,6 +110,32 @@ __device__ __forceinline__ void load_chunk_rb_part(Chunk<P>& c, __amdgpu_buffer_
   }
 }
 
+// Q8_0 weights (W8): a lane's 16-B unit is HALF a block (unit u = block
+// u / 2, elements 16 (u % 2) ..; L is even, so the half is lane-fixed: j % 2),
+// dotted with the matching half of the activation block; no zero point
+template <int R, int P>
+__device__ __forceinline__ void eat_chunk_rb_w8(const Chunk<P>& c, int pass0, int nb, int j, bool row_ok,
+                                                const XBlock* s_x, float& acc) {
+  constexpr int L = 64 / R;
+  static_assert(L % 2 == 0, "W8: even lanes per row");
+  const int nu = 2 * nb;
+#pragma unroll
+  for (int p = 0; p < P; p++) {
+    const int u = (pass0 + p) * L + j;
+    const bool ok = row_ok && u < nu;
+    const XBlock* xb = s_x + (u < nu ? u >> 1 : nb - 1);
+    const int4 xq = *reinterpret_cast<const int4*>(reinterpret_cast<const char*>(xb) + (j & 1) * 16);
+    const float dx = xb->d;
+    int is = sdot4((int)c.q[p].x, xq.x, 0);
+    is = sdot4((int)c.q[p].y, xq.y, is);
+    is = sdot4((int)c.q[p].z, xq.z, is);
+    is = sdot4((int)c.q[p].w, xq.w, is);
+    const float v = (h2f(c.sw[p]) * dx) * (float)is;
+    acc += ok ? v : 0.0f;
+    asm volatile("" ::: "memory");
+  }
+}
+
 template <int R, int P>
 __device__ __forceinline__ void eat_chunk_rb(const Chunk<P>& c, int pass0, int nb, int j, bool row_ok,
                                              const XBlock* s_x, float& acc) {
@@ -195,7 +221,8 @@ constexpr int HELP_K4 = 6;  // float4 per helper lane and operand: n <= E * 256 
 // right after the prologue's operand loads, the rest once x is in LDS -- a
 // CU's first weight bytes stream during the prologue without stalling its
 // waves at the issue (PE small against the CU's in-flight capacity).
-template <int R, int NW, int P, int E, int ROLE, bool MULTI, bool EARLY, int SYNC = 0, int PE = 0>
+// W8: Q8_0 weights (qs [rows][nb][32 B], row-major) instead of Q4_0.
+template <int R, int NW, int P, int E, int ROLE, bool MULTI, bool EARLY, int SYNC = 0, int PE = 0, bool W8 = false>
 __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, unsigned char* s_dyn,
                                            const BlockSync& bs) {
   constexpr bool HELP = role_help(ROLE);
@@ -205,6 +232,7 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
   static_assert(!HELP || RB, "helper roles use the row-bound stream");
   constexpr int L = RB ? 64 / R : 64;
   static_assert(PE == 0 || (RB && !MULTI && !EARLY && PE < P), "PE: single-chunk row-bound late roles");
+  static_assert(!W8 || (RB && R <= 16), "W8: row-bound lanes");
   LAYER_MARK(0);
   BLK_MARK(bs, 0);
   constexpr int EPT = E, X_LD = E;
@@ -248,6 +276,14 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
     vod = ((rj >> 3) * a.rows + r) * 16 + (rj & 7) * 2;
     sq = (L / 8) * a.rows * 128;
     sd = (L / 8) * a.rows * 16;
+  } else if constexpr (W8) {  // 16-B units = half blocks; the scale of unit u is block u / 2's
+    const int nu = 2 * nb;
+    rq = buf_rsrc(a.qs + (size_t)min(wrow0, a.rows) * nu, (uint32_t)wrows * nu * 16);
+    rd = buf_rsrc(a.wd + (size_t)min(wrow0, a.rows) * nb, (uint32_t)wrows * nb * 2);
+    voq = (rk * nu + rj) * 16;
+    vod = (rk * nb + (rj >> 1)) * 2;
+    sq = L * 16;
+    sd = L;  // (L / 2) scales of 2 B per pass
   } else {
     rq = buf_rsrc(a.qs + (size_t)min(wrow0, a.rows) * nb, (uint32_t)wrows * nb * 16);
     rd = buf_rsrc(a.wd + (size_t)min(wrow0, a.rows) * nb, (uint32_t)wrows * nb * 2);
@@ -256,7 +292,7 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
     sq = L * 16;
     sd = L * 2;
   }
-  const int npass = (nb + L - 1) / L;
+  const int npass = ((W8 ? 2 * nb : nb) + L - 1) / L;
 
   Chunk<P> ca, cb;
   auto issue_weights = [&]() {
@@ -535,14 +571,17 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
     if (helper) {
       // helpers have no rows
     } else if constexpr (!MULTI) {
-      eat_chunk_rb<R, P>(ca, 0, nb, rj, row_ok, s_x, acc1);
+      if constexpr (W8) eat_chunk_rb_w8<R, P>(ca, 0, nb, rj, row_ok, s_x, acc1);
+      else eat_chunk_rb<R, P>(ca, 0, nb, rj, row_ok, s_x, acc1);
     } else {
       // unconditional loads (out-of-range passes return 0 without traffic):
       // no loop-carried phis, so the chunk registers are not copied
       for (int p0 = 0; p0 < npass; p0 += 2 * P) {
-        eat_chunk_rb<R, P>(ca, p0, nb, rj, row_ok, s_x, acc1);
+        if constexpr (W8) eat_chunk_rb_w8<R, P>(ca, p0, nb, rj, row_ok, s_x, acc1);
+        else eat_chunk_rb<R, P>(ca, p0, nb, rj, row_ok, s_x, acc1);
         load_chunk_rb<R, P>(ca, rq, rd, voq, vod, sq, sd, p0 + 2 * P, npass);
-        eat_chunk_rb<R, P>(cb, p0 + P, nb, rj, row_ok, s_x, acc1);
+        if constexpr (W8) eat_chunk_rb_w8<R, P>(cb, p0 + P, nb, rj, row_ok, s_x, acc1);
+        else eat_chunk_rb<R, P>(cb, p0 + P, nb, rj, row_ok, s_x, acc1);
         load_chunk_rb<R, P>(cb, rq, rd, voq, vod, sq, sd, p0 + 3 * P, npass);
       }
     }

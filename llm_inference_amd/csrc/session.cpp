@@ -220,7 +220,8 @@ void Session::upload(const GGUFView& g) {  // model.cpp:169-238 tensor map
     const bool qkv_same = q->type == k->type && q->type == v->type && q->shape[0] == k->shape[0] &&
                           q->shape[0] == v->shape[0];
     const bool want_fused =
-        fuse_layers_ && qkv_same && gt->type == T_Q4_0 && up->type == T_Q4_0 && gt->shape[0] == up->shape[0] &&
+        fuse_layers_ && qkv_same && (gt->type == T_Q4_0 || gt->type == T_Q8_0) && up->type == gt->type &&
+        gt->shape[0] == up->shape[0] &&
         (int)q->shape[0] == hp_.n_embd && (int)gt->shape[0] == hp_.n_embd &&
         shape_ok(q, Ld.qkv_rows, LAYER_PRO) && shape_ok(q, Ld.qkv_rows, LAYER_PLAIN) &&
         slab_of(q, LAYER_PRO) == slab_of(q, LAYER_PLAIN) &&  // one qkv layout serves both roles
@@ -235,8 +236,8 @@ void Session::upload(const GGUFView& g) {  // model.cpp:169-238 tensor map
       // rows owns matching gate and up rows.  A tensor-parallel rank keeps
       // hidden units [rank * F, (rank + 1) * F).
       const int cols = (int)gt->shape[0], F = tp_ ? f_sh_ : hp_.n_ff;
-      const int H = layer_gemv_gelu_group(cols);
-      const size_t rb = gguf_bytes(T_Q4_0, 1, cols);
+      const int H = layer_gemv_gelu_group(cols, gt->type);
+      const size_t rb = gguf_bytes(gt->type, 1, cols);
       std::vector<uint8_t> il((size_t)2 * F * rb);
       const size_t h0 = (size_t)r * F * rb;
       const uint8_t *sg = (const uint8_t*)g.tensor_data(*gt) + h0, *su = (const uint8_t*)g.tensor_data(*up) + h0;
@@ -245,7 +246,7 @@ void Session::upload(const GGUFView& g) {  // model.cpp:169-238 tensor map
         std::memcpy(&il[(size_t)(2 * H * k + H) * rb], su + (size_t)(H * k) * rb, H * rb);
       }
       GemvPart p;
-      p.w = alloc_weight(T_Q4_0, 2 * F, cols);
+      p.w = alloc_weight(gt->type, 2 * F, cols);
       upload_rows(p.w, 0, il.data(), 2 * F, stream_);
       weight_bytes_ += p.w.bytes;
       Ld.gate_up = {p};
@@ -668,7 +669,7 @@ void Session::prefill(const int32_t* tokens, int n, int pos) {
       rn.eps = hp_.eps;
       launch_prefill_norm(rn, T, s);
       launch_prefill_gemm(Ld.gate_up[0].w, pf_xq_, XS, T, pf_out_, 2 * F, s);
-      launch_prefill_gelu(pf_out_, F, layer_gemv_gelu_group(Ld.gate_up[0].w.cols), pf_xq_, XS, T, s);
+      launch_prefill_gelu(pf_out_, F, layer_gemv_gelu_group(Ld.gate_up[0].w.cols, Ld.gate_up[0].w.type), pf_xq_, XS, T, s);
       launch_prefill_gemm(Ld.down.w, pf_xq_, XS, T, pf_out_, E, s);
       if (l + 1 < hp_.n_layer) {  // post-ffw norm + residual, then the next attn_norm
         PrefillNorm fn = rn;

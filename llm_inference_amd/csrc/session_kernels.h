@@ -114,7 +114,7 @@ void launch_prefill_gelu(const float* gu, int F, int H, XBlock* xq, int xstride,
 // the weight layout the launch-table entry for (w's shape, role) reads
 int layer_gemv_slab(const DevWeight& w, int role);
 // GELU role: hidden units per work-group (the gate/up interleave group), 0 if unsupported
-int layer_gemv_gelu_group(int cols);
+int layer_gemv_gelu_group(int cols, uint32_t type = T_Q4_0);
 void launch_layer_gemv(const DevWeight& w, LayerGemv a, int role, hipStream_t s);
 void launch_argmax(const float* x, int n, unsigned long long* key, hipStream_t s);
 // Greedy token by bounded screening + exact rescoring (k_logits.hip): the

@@ -148,10 +148,11 @@ def test_unfused_fast_path_matches_fused(oracle, monkeypatch):
 
 @pytest.mark.parametrize("quant", ["q4_k_m", "q8_0"])
 def test_kquant_and_q8_models_vs_oracle(oracle, quant, exact):
-    """BASELINE configs[3]: Gemma-3 4B Q4_K_M (Q4_K projections, Q6_K v/down)
-    and 1B Q8_0 layer shapes through the session (unfused path: Q8_K / Q8_0
-    activations, fast K-quant GEMVs in fast mode), vs the oracle: greedy ids
-    identical, logits within the module's tolerances."""
+    """BASELINE configs[3]: Gemma-3 4B Q4_K_M (Q4_K projections, Q6_K v/down;
+    per-projection path: Q8_K activations, fast K-quant GEMVs) and 1B Q8_0
+    layer shapes (fast mode: the fused layer launches with Q8_0 weights) through
+    the session, vs the oracle: greedy ids identical, logits within the
+    module's tolerances."""
     from llm_inference_amd.gguf import TensorType as TT
     from llm_inference_amd.model import Model
     from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
@@ -176,3 +177,26 @@ def test_kquant_and_q8_models_vs_oracle(oracle, quant, exact):
         toks_ref.append(int(np.argmax(lg)))
     toks = m.generate(int(np.argmax(got)), len(prompt), 6)
     assert [int(np.argmax(got))] + toks.tolist() == toks_ref
+
+
+def test_q8_0_fused_matches_unfused(oracle, monkeypatch):
+    """Q8_0 weights in the fused layer launch table (k_layer.hip W8 entries:
+    half-block units, no zero point) against the per-projection Q8_0 path."""
+    from llm_inference_amd.gguf import TensorType as TT
+    from llm_inference_amd.model import Model
+    from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
+    cfg = CONFIGS["mini-1b"]
+    g = build_gemma3_gguf(cfg, seed=12, wtype=TT.Q8_0)
+    prompt = np.random.default_rng(5).integers(4, cfg.vocab, 9).astype(np.int32)
+    fused = Model(g, exact=False, max_ctx=64)
+    lf = fused.forward(prompt, 0)
+    monkeypatch.setenv("LLMI_NO_FUSE", "1")
+    plain = Model(g, exact=False, max_ctx=64)
+    lp = plain.forward(prompt, 0)
+    assert fused.get_info().kernels_per_token < plain.get_info().kernels_per_token
+    np.testing.assert_allclose(lf, lp, atol=FAST_VS_REF, rtol=0)
+    ideal = oracle.model(g, n_threads=8, max_ctx=64, attn_f64=True)
+    np.testing.assert_allclose(lf, ideal.forward(prompt, 0), atol=FAST_VS_REF, rtol=0)
+    first = int(np.argmax(lf))
+    assert first == int(np.argmax(lp))
+    assert fused.generate(first, len(prompt), 8).tolist() == plain.generate(first, len(prompt), 8).tolist()
