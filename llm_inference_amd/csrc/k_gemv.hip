@@ -513,13 +513,23 @@ __global__ __launch_bounds__(256) void gemv_q6_k_fast(const uint8_t* __restrict_
     const float xd = *reinterpret_cast<const float*>(xb);
     const uint8_t* xq = xb + 4 + 32 * m;
     const int lsh = (jq >> 1) * 4, hsh = 2 * jq;
+    // 210-B blocks are only 2-byte aligned: the 32 bytes of ql / qh come from 9
+    // aligned dwords each, realigned with v_alignbyte (72 byte loads -> 18
+    // dword loads; the 9th dword stays inside the block)
+    const uint32_t* lw4 = reinterpret_cast<const uint32_t*>(reinterpret_cast<uintptr_t>(ql) & ~(uintptr_t)3);
+    const uint32_t* hw4 = reinterpret_cast<const uint32_t*>(reinterpret_cast<uintptr_t>(qh) & ~(uintptr_t)3);
+    const uint32_t lal = (uint32_t)(reinterpret_cast<uintptr_t>(ql) & 3), hal = (uint32_t)(reinterpret_cast<uintptr_t>(qh) & 3);
+    uint32_t lraw[9], hraw[9];
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+      lraw[k] = lw4[k];
+      hraw[k] = hw4[k];
+    }
     int dot[2] = {0, 0};
 #pragma unroll
     for (int w4 = 0; w4 < 8; w4++) {
-      const uint32_t lw = (uint32_t)ql[4 * w4] | ((uint32_t)ql[4 * w4 + 1] << 8) | ((uint32_t)ql[4 * w4 + 2] << 16) |
-                          ((uint32_t)ql[4 * w4 + 3] << 24);
-      const uint32_t hw = (uint32_t)qh[4 * w4] | ((uint32_t)qh[4 * w4 + 1] << 8) | ((uint32_t)qh[4 * w4 + 2] << 16) |
-                          ((uint32_t)qh[4 * w4 + 3] << 24);
+      const uint32_t lw = __builtin_amdgcn_alignbyte(lraw[w4 + 1], lraw[w4], lal);
+      const uint32_t hw = __builtin_amdgcn_alignbyte(hraw[w4 + 1], hraw[w4], hal);
       const uint32_t v = ((lw >> lsh) & 0x0F0F0F0Fu) | (((hw >> hsh) & 0x03030303u) << 4);  // 0..63 per byte
       const int q = (int)((v + 0x60606060u) ^ 0x80808080u);                                   // - 32 per byte
       dot[w4 >> 2] = sdot4(q, ld_i32u(xq + 4 * w4), dot[w4 >> 2]);
