@@ -105,12 +105,12 @@ const LayerCfg kLayerCfgs[] = {
     LLMI_LCFG(120, ROLE_PRO, 8, 4, 8, 15, true, true, 0),      // 12B qkv     256 WGs
     LLMI_LCFG(168, ROLE_PRO, 4, 8, 6, 11, true, true, 1),      // 27B qkv     256 WGs
     // GELU: prologue + GELU epilogue, 2H = R NW interleaved gate/up rows per WG
-    LLMI_LCFG(36, ROLE_GELU, 6, 9, 4, 2, false, false, 0),     // 1B  13824 rows, H 27 -> 256 WGs
+    LLMI_LCFGP(36, ROLE_GELU, 8, 8, 5, 3, 0, 3),              // 1B  13824 rows, H 32 -> 216 WGs (PE3: 5.9 -> 5.1 us)
     LLMI_LCFGP(80, ROLE_GELU, 8, 10, 10, 4, 1, 7),            // 4B  20480 rows, H 40 -> 256 WGs (PE7: 8.4 -> 7.8 us)
     LLMI_LCFG(120, ROLE_GELU, 8, 8, 8, 8, true, false, 0),     // 12B 30720 rows, H 32 -> 480 WGs
     LLMI_LCFG(168, ROLE_GELU, 8, 8, 4, 11, true, false, 1),    // 27B 43008 rows, H 32 -> 672 WGs
     // QUANT: f32 activation quantized into LDS (down projection)
-    LLMI_LCFG(216, ROLE_QUANT, 2, 2, 7, 7, false, true, 0),    // 1B down     1152 rows -> 288 WGs
+    LLMI_LCFG(216, ROLE_QUANT, 1, 4, 4, 4, false, true, 0),    // 1B down     1152 rows -> 288 WGs (6.5 -> 5.0 us)
     LLMI_LCFGP(320, ROLE_QUANT, 1, 10, 5, 2, 0, 3),           // 4B down     2560 rows -> 256 WGs (PE3: 5.8 -> 5.4 us)
     LLMI_LCFG(480, ROLE_QUANT, 1, 8, 8, 4, false, true, 0),    // 12B down    3840 rows -> 480 WGs
     LLMI_LCFG(672, ROLE_QUANT, 1, 8, 6, 6, true, false, 0),    // 27B down    5376 rows -> 672 WGs

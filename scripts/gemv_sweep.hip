@@ -103,7 +103,7 @@ int main(int argc, char** argv) {
   hipStream_t s;
   LLMI_HIP(hipStreamCreate(&s));
   const Shape shapes[] = {{"4b.qkv", 4096, 2560}, {"4b.o", 2560, 2048}, {"4b.gate_up", 20480, 2560},
-                          {"4b.down", 2560, 10240}, {"1b.gate_up", 13824, 1152}, {"27b.qkv", 8192, 5376}, {"27b.o", 5376, 4096},
+                          {"4b.down", 2560, 10240}, {"1b.gate_up", 13824, 1152}, {"1b.down", 1152, 6912}, {"27b.qkv", 8192, 5376}, {"27b.o", 5376, 4096},
                           {"27b.gate_up", 43008, 5376}, {"27b.down", 5376, 21504}};
   hipEvent_t e0, e1;
   LLMI_HIP(hipEventCreate(&e0));
@@ -385,6 +385,23 @@ int main(int argc, char** argv) {
       geo_role("pro R4 NW8 P5 E5", gemv_q4_0_layer<4, 8, 5, 5, 1, false, true>, 32, 512, pro, true);
       geo_role("SLAB pro R4 NW4 P5 E10", gemv_q4_0_layer<4, 4, 5, 10, 1, false, true>, 16, 256, ps, true);
       geo_role("SLAB pro R8 NW2 P10 E20", gemv_q4_0_layer<8, 2, 10, 20, 1, false, true>, 16, 128, ps, true);
+    }
+    if (nb == 36) {  // 1B gate_up (x 1152)
+      geo_role("1b gelu R6 NW9 P4 E2 (table, flat)", gemv_q4_0_layer<6, 9, 4, 2, 2, false, false>, 54, 576, gl, true);
+      geo_role("1b gelu R8 NW8 P5 E3", gemv_q4_0_layer<8, 8, 5, 3, 2, false, false>, 64, 512, gl, true);
+      geo_role("1b gelu R8 NW8 P5 E3 PE2", gemv_q4_0_layer<8, 8, 5, 3, 2, false, false, 2>, 64, 512, gl, true);
+      geo_role("1b gelu R8 NW8 P5 E3 PE3", gemv_q4_0_layer<8, 8, 5, 3, 2, false, false, 3>, 64, 512, gl, true);
+      geo_role("1b gelu R8 NW8 P5 E3 PE4", gemv_q4_0_layer<8, 8, 5, 3, 2, false, false, 4>, 64, 512, gl, true);
+      geo_role("1b gelu R6 NW9 P4 E2 again", gemv_q4_0_layer<6, 9, 4, 2, 2, false, false>, 54, 576, gl, true);
+    }
+    if (nb == 216) {  // 1B down (x 6912)
+      geo_role("1b quant R2 NW2 P7 E7 (table)", gemv_q4_0_layer<2, 2, 7, 7, 3, false, true>, 4, 128, qz, false);
+      geo_role("1b quant R2 NW2 P7 E7 late", gemv_q4_0_layer<2, 2, 7, 7, 3, false, false>, 4, 128, qz, false);
+      geo_role("1b quant R2 NW2 P7 E7 PE3", gemv_q4_0_layer<2, 2, 7, 7, 3, false, false, 3>, 4, 128, qz, false);
+      geo_role("1b quant R2 NW2 P7 E7 PE5", gemv_q4_0_layer<2, 2, 7, 7, 3, false, false, 5>, 4, 128, qz, false);
+      geo_role("1b quant R1 NW4 P4 E4", gemv_q4_0_layer<1, 4, 4, 4, 3, false, true>, 4, 256, qz, false);
+      geo_role("1b quant R1 NW4 P4 E4 PE2", gemv_q4_0_layer<1, 4, 4, 4, 3, false, false, 2>, 4, 256, qz, false);
+      geo_role("1b quant R2 NW2 P7 E7 (table) b", gemv_q4_0_layer<2, 2, 7, 7, 3, false, true>, 4, 128, qz, false);
     }
     if (nb == 320) {  // 4B down (x 10240)
       geo_role("quant R1 NW10 P5 E2 (table)", gemv_q4_0_layer<1, 10, 5, 2, 3, false, true>, 10, 640, qz, false);
