@@ -410,6 +410,11 @@ int main(int argc, char** argv) {
       geo_role("quant R1 NW10 P5 E2 PE2", gemv_q4_0_layer<1, 10, 5, 2, 3, false, false, 2>, 10, 640, qz, false);
       geo_role("quant R1 NW10 P5 E2 PE3", gemv_q4_0_layer<1, 10, 5, 2, 3, false, false, 3>, 10, 640, qz, false);
       geo_role("quant R1 NW10 P5 E2 PE4", gemv_q4_0_layer<1, 10, 5, 2, 3, false, false, 4>, 10, 640, qz, false);
+      geo_role("quant R1 NW4 P5 E5", gemv_q4_0_layer<1, 4, 5, 5, 3, false, true>, 4, 256, qz, false);
+      geo_role("quant R1 NW4 P5 E5 PE3", gemv_q4_0_layer<1, 4, 5, 5, 3, false, false, 3>, 4, 256, qz, false);
+      geo_role("quant R1 NW8 P5 E3 PE3", gemv_q4_0_layer<1, 8, 5, 3, 3, false, false, 3>, 8, 512, qz, false);
+      geo_role("quant R1 NW5 P5 E4 PE3", gemv_q4_0_layer<1, 5, 5, 4, 3, false, false, 3>, 5, 320, qz, false);
+      geo_role("quant R2 NW5 P10 E4 PE6", gemv_q4_0_layer<2, 5, 10, 4, 3, false, false, 6>, 10, 320, qz, false);
       geo_role("quant R1 NW10 P5 E2 PE3 b", gemv_q4_0_layer<1, 10, 5, 2, 3, false, false, 3>, 10, 640, qz, false);
       geo_role("quant R1 NW10 P5 E2 (table) b", gemv_q4_0_layer<1, 10, 5, 2, 3, false, true>, 10, 640, qz, false);
       geo_role("quant R1 NW8 P5 E3", gemv_q4_0_layer<1, 8, 5, 3, 3, false, true>, 8, 512, qz, false);
