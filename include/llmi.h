@@ -154,6 +154,21 @@ int llmi_session_forward(llmi_session* s, const int32_t* tokens, int n_tokens, i
  * compare_tensors.py counterpart).  Slow; the results equal forward's. */
 int llmi_session_dump(llmi_session* s, const int32_t* tokens, int n_tokens, int pos, const char* path);
 
+/* Op-level parity taps (test hook; the per-op counterpart of
+ * llmi_session_dump).  Runs the SAME kernels the decode graph (or, for
+ * n_tokens > 1 on a batched-prefill session, the prefill) launches, eagerly,
+ * and after each launch copies the buffers it produced to the host and calls
+ * fn(user, name, layer, data, bytes) -- e.g. "qkv_g" (the attention block's
+ * q|k|v rows as {value, tag} granules), "attn", "xo_g", "o", "kc"/"vc" (the
+ * layer's KV cache), "ffn_resid", "ffn_norm", "hid", "down", "result_norm",
+ * "logits"/"token"; the prefill taps its GEMM inputs ("pf_x_<proj>", Q8_0
+ * blocks) and outputs ("pf_<proj>").  flags bit 0: the decode-loop step
+ * (screened token selection) instead of forward's full logits.  Slow; the
+ * session's state advances exactly as llmi_session_forward's. */
+typedef void (*llmi_trace_fn)(void* user, const char* name, int layer, const void* data, size_t bytes);
+int llmi_session_trace(llmi_session* s, const int32_t* tokens, int n_tokens, int pos, uint32_t flags,
+                       llmi_trace_fn fn, void* user);
+
 /* Greedy decode loop of main.cpp:172-224 kept on the device: token `first`
  * at position `pos`, then n_steps forwards, each feeding its argmax to the
  * next without a host round trip.  out_tokens[i] = argmax after step i. */

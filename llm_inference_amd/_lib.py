@@ -38,6 +38,9 @@ class SessionOpts(C.Structure):
                 ("tp_rank", C.c_int), ("tp_size", C.c_int), ("tp_id", C.c_void_p), ("tp_group", C.c_void_p)]
 
 
+TRACE_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_char_p, C.c_int, C.c_void_p, C.c_size_t)
+
+
 class SessionInfo(C.Structure):
     _fields_ = [("n_layer", C.c_int), ("n_embd", C.c_int), ("n_ff", C.c_int), ("n_head", C.c_int),
                 ("n_head_kv", C.c_int), ("head_dim", C.c_int), ("vocab", C.c_int), ("max_ctx", C.c_int),
@@ -79,6 +82,7 @@ _SIGS = {
     "llmi_session_generate": (C.c_int, [_vp, _i32, C.c_int, C.c_int, _vp]),
     "llmi_session_dump": (C.c_int, [_vp, _vp, C.c_int, C.c_int, C.c_char_p]),
     "llmi_session_enqueue": (C.c_int, [_vp, _i32, C.c_int, C.c_int]),
+    "llmi_session_trace": (C.c_int, [_vp, _vp, C.c_int, C.c_int, _u32, _vp, _vp]),
     "llmi_session_sync": (C.c_int, [_vp, _vp, C.c_int]),
     "llmi_session_get_info": (C.c_int, [_vp, C.POINTER(SessionInfo)]),
     "llmi_session_time_kernel": (C.c_int, [_vp, C.c_int, C.c_int, C.POINTER(_f64), C.POINTER(_f64)]),

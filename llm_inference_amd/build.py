@@ -27,6 +27,11 @@ if os.environ.get("LLMI_BLOCK_TRACE_BUILD"):  # development: block-kernel phase 
     FLAGS.append("-DLLMI_BLOCK_TRACE")  # into its own objects + libllmi_trace.so (load with LLMI_LIB=...)
     OBJ = os.path.join(HERE, "_build_trace")
     LIB = os.path.join(HERE, "libllmi_trace.so")
+# development A/B builds: LLMI_VARIANT=name LLMI_EXTRA_FLAGS="-D..." -> libllmi_<name>.so (load with LLMI_LIB=...)
+if os.environ.get("LLMI_VARIANT"):
+    FLAGS += os.environ.get("LLMI_EXTRA_FLAGS", "").split()
+    OBJ = os.path.join(HERE, "_build_" + os.environ["LLMI_VARIANT"])
+    LIB = os.path.join(HERE, "libllmi_" + os.environ["LLMI_VARIANT"] + ".so")
 
 
 def _mtime(p):

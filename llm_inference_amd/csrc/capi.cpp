@@ -413,6 +413,14 @@ int llmi_session_dump(llmi_session* s, const int32_t* tokens, int n_tokens, int 
   return guard([&] { s->s->forward_dump(tokens, n_tokens, pos, path); });
 }
 
+int llmi_session_trace(llmi_session* s, const int32_t* tokens, int n_tokens, int pos, uint32_t flags,
+                       llmi_trace_fn fn, void* user) {
+  return guard([&] {
+    if (!s || !tokens || !fn) throw status_error(LLMI_E_ARG, "null pointer");
+    s->s->forward_trace(tokens, n_tokens, pos, (flags & 1u) != 0, fn, user);
+  });
+}
+
 int llmi_session_generate(llmi_session* s, int32_t first, int pos, int n_steps, int32_t* out_tokens) {
   return guard([&] {
     s->s->enqueue(first, pos, n_steps);

@@ -102,7 +102,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uin
   return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0, (int)n,
                                            0x00020000);
 }
-constexpr int BUF_NT = 2;  // cache-policy bit: non-temporal (streamed once)
+#ifndef LLMI_WEIGHT_POLICY
+#define LLMI_WEIGHT_POLICY 2
+#endif
+constexpr int BUF_NT = LLMI_WEIGHT_POLICY;  // cache-policy bits of streamed weights: 2 = non-temporal (streamed once)
 __device__ __forceinline__ float4 buf_ldf4(__amdgpu_buffer_rsrc_t r, int voff) {  // default policy (re-read data)
   const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0);
   return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));

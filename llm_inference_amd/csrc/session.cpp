@@ -296,6 +296,25 @@ void Session::upload(const GGUFView& g) {  // model.cpp:169-238 tensor map
       relayout(Ld.down.w, LAYER_QUANT);
     }
   }
+  // LLMI_SHARE_LAYERS=N (diagnostics, timing only -- results are wrong): layer
+  // l >= N reads layer l % N's weights, so the per-token weight working set
+  // is N layers (cache-residency experiments)
+  if (const char* sh = getenv("LLMI_SHARE_LAYERS")) {
+    const int N = std::max(1, atoi(sh));
+    for (int l = N; l < hp_.n_layer; l++) {
+      LayerDev& Ld = L_[l];
+      for (auto& p : Ld.qkv) free_weight(p.w);
+      for (auto& p : Ld.gate_up) free_weight(p.w);
+      free_weight(Ld.o.w);
+      free_weight(Ld.down.w);
+      const LayerDev& S = L_[l % N];
+      Ld.qkv = S.qkv;
+      Ld.o = S.o;
+      Ld.gate_up = S.gate_up;
+      Ld.down = S.down;
+      Ld.aliased = true;
+    }
+  }
 }
 
 void Session::alloc_buffers() {
@@ -464,6 +483,7 @@ void Session::release() {
   graph_gen_ = nullptr;
   free_screen_table(scr_);
   for (auto& l : L_) {
+    if (l.aliased) continue;  // LLMI_SHARE_LAYERS: another layer's weights
     for (auto& p : l.qkv) free_weight(p.w);
     for (auto& p : l.gate_up) free_weight(p.w);
     free_weight(l.o.w);
@@ -536,6 +556,9 @@ void Session::record_step(hipStream_t s, bool gen) {
   }
   dump("inp_scaled", resid_, E, s);  // model.cpp:711-713
   dump("attn_norm-0", xn_, E, s);
+  tap("inp_scaled", -1, resid_, (size_t)E * 4, s);
+  tap("attn_norm", 0, xn_, (size_t)E * 4, s);
+  if (x_q8) tap("xq", 0, act_.q8.xb, (size_t)(E / 32) * sizeof(XBlock), s);
   bool fused = fuse_layers_;
   for (const auto& l : L_) fused &= l.fused;
   if (tp_ && !fused) throw status_error(LLMI_E_ARG, "tensor parallel needs the fused layer path");
@@ -559,11 +582,13 @@ void Session::record_logits(hipStream_t s, bool gen) {
   if (gen && screen_) {  // token id only: int8 screening + exact rescoring of the candidates
     launch_screen_argmax(logits_w_, scr_, act_.x16, key, s);
     kernels_per_token_ += 3;
+    tap("x16", -1, act_.x16, (size_t)E * 2, s);
   } else {
     for (int r = 0; r < dup("logits"); r++)
       launch_gemv(logits_w_, act_, lg, ex_logits_ ? GEMV_EXACT : GEMV_FAST, s, fold ? key : nullptr);
     kernels_per_token_++;
     dump("result_output", lg, v_rows_, s);  // model.cpp:1046
+    tap("logits", -1, lg, (size_t)v_rows_ * 4, s);
   }
   if (!fold) {
     launch_argmax(lg, v_rows_, key, s);
@@ -572,6 +597,7 @@ void Session::record_logits(hipStream_t s, bool gen) {
   if (tp_) coll_->all_gather(amax_key_, sizeof(unsigned long long), s);
   launch_finalize_token(amax_key_, tp_size_, v_sh_, d_token_, d_pos_, ring_, ring_idx_, max_ctx_, s);
   kernels_per_token_++;
+  tap("token", -1, d_token_, 4, s);
 }
 
 void Session::ensure_prefill_buffers(int cap) {
@@ -625,7 +651,9 @@ void Session::prefill(const int32_t* tokens, int n, int pos) {
     for (int l = 0; l < hp_.n_layer; l++) {
       const LayerDev& Ld = L_[l];
       const int hd = Ld.hd;
+      tap("pf_x_qkv", l, pf_xq_, (size_t)T * XS * sizeof(XBlock), s);
       launch_prefill_gemm(Ld.qkv[0].w, pf_xq_, XS, T, pf_out_, Ld.qkv_rows, s);
+      tap("pf_qkv", l, pf_out_, (size_t)T * Ld.qkv_rows * 4, s);
       PrefillQK qk;
       qk.qkv = pf_out_;
       qk.qkv_stride = Ld.qkv_rows;
@@ -657,7 +685,12 @@ void Session::prefill(const int32_t* tokens, int n, int pos) {
       at.xq = pf_xq_;
       at.xstride = XS;
       launch_prefill_attn(at, T, s);
+      tap("pf_q", l, pf_q_, (size_t)T * nh_ * hd * 2, s);
+      tap("kc", l, Ld.kc, (size_t)nkv_ * max_ctx_ * hd * 2, s);
+      tap("vc", l, Ld.vc, (size_t)nkv_ * max_ctx_ * hd * 2, s);
+      tap("pf_x_o", l, pf_xq_, (size_t)T * XS * sizeof(XBlock), s);
       launch_prefill_gemm(Ld.o.w, pf_xq_, XS, T, pf_out_, E, s);
+      tap("pf_o", l, pf_out_, (size_t)T * E * 4, s);
       PrefillNorm rn;  // post-attention norm + residual, then ffn_norm
       rn.y = pf_out_;
       rn.w_post = Ld.post_attn_norm;
@@ -668,14 +701,20 @@ void Session::prefill(const int32_t* tokens, int n, int pos) {
       rn.n = E;
       rn.eps = hp_.eps;
       launch_prefill_norm(rn, T, s);
+      tap("pf_resid_attn", l, pf_resid_, (size_t)T * E * 4, s);
+      tap("pf_x_gate_up", l, pf_xq_, (size_t)T * XS * sizeof(XBlock), s);
       launch_prefill_gemm(Ld.gate_up[0].w, pf_xq_, XS, T, pf_out_, 2 * F, s);
+      tap("pf_gate_up", l, pf_out_, (size_t)T * 2 * F * 4, s);
       launch_prefill_gelu(pf_out_, F, layer_gemv_gelu_group(Ld.gate_up[0].w.cols, Ld.gate_up[0].w.type), pf_xq_, XS, T, s);
+      tap("pf_x_down", l, pf_xq_, (size_t)T * XS * sizeof(XBlock), s);
       launch_prefill_gemm(Ld.down.w, pf_xq_, XS, T, pf_out_, E, s);
+      tap("pf_down", l, pf_out_, (size_t)T * E * 4, s);
       if (l + 1 < hp_.n_layer) {  // post-ffw norm + residual, then the next attn_norm
         PrefillNorm fn = rn;
         fn.w_post = Ld.post_ffw_norm;
         fn.w_next = L_[l + 1].attn_norm;
         launch_prefill_norm(fn, T, s);
+        tap("pf_resid_ffn", l, pf_resid_, (size_t)T * E * 4, s);
       }
     }
     if (last_chunk) {  // the last token: final residual + output_norm -> logits (decode tail)
@@ -735,8 +774,21 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
       bs.g_xo = blk_gxo_ + (size_t)l * blk_gxo_stride_;
       bs.err = blk_err_;
       if (blk_trace_ && l == blk_trace_layer_) bs.trace = blk_trace_;
+      if (trace_fn_ && qrole == LAYER_PRO) g.xn_out = xn_;
       launch_attn_block(Ld.qkv[0].w, g, qrole, Ld.o.w, go, aa, qa, bs, s);
       kernels_per_token_++;
+      if (trace_fn_) {  // the launch's products: residual / norm (prologue), q|k|v and xo granules, attention, o
+        if (qrole == LAYER_PRO) {
+          tap("attn_resid", l, cur, (size_t)E * 4, s);
+          tap("attn_norm", l, xn_, (size_t)E * 4, s);
+        }
+        tap("qkv_g", l, bs.g_qkv, (size_t)Ld.qkv_rows * 8, s);
+        tap("attn", l, attn_, (size_t)nh_ * hd * 4, s);
+        tap("xo_g", l, bs.g_xo, (size_t)nh_ * hd / 32 * 12 * 8, s);
+        tap("o", l, o_out_, (size_t)E * 4, s);
+        tap("kc", l, Ld.kc, (size_t)nkv_ * max_ctx_ * hd * 2, s);
+        tap("vc", l, Ld.vc, (size_t)nkv_ * max_ctx_ * hd * 2, s);
+      }
     } else {
       LayerGemv g;
       if (l == 0) {
@@ -755,13 +807,16 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
         g.w_next = Ld.attn_norm;
         g.eps = hp_.eps;
         g.out = qkv_;
-        if (dump_) g.xn_out = xn_;
+        if (dump_ || trace_fn_) g.xn_out = xn_;
         for (int r = 0; r < dup("qkv"); r++) launch_layer_gemv(Ld.qkv[0].w, g, LAYER_PRO, s);
+        tap("attn_resid", l, other, (size_t)E * 4, s);
+        tap("attn_norm", l, xn_, (size_t)E * 4, s);
         dump("l_out-" + std::to_string(l - 1), other, E, s);
         dump("attn_norm-" + L, xn_, E, s);
         std::swap(cur, other);
       }
       kernels_per_token_++;
+      tap("qkv", l, qkv_, (size_t)Ld.qkv_rows * 4, s);
       dump("Qcur-" + L, qkv_, nh_ * hd, s);
       dump("Kcur-" + L, qkv_ + Ld.k_off, nkv_ * hd, s);
       dump("Vcur-" + L, qkv_ + Ld.v_off, nkv_ * hd, s);
@@ -775,6 +830,9 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
                   ticket_, q8_in_combine ? act_.q8.xb + (size_t)tp_rank_ * hb : nullptr};
       for (int r = 0; r < dup("attn"); r++) launch_attention(aa, false, s, &qa);
       kernels_per_token_++;
+      tap("attn", l, attn_, (size_t)nh_ * hd * 4, s);
+      tap("kc", l, Ld.kc, (size_t)nkv_ * max_ctx_ * hd * 2, s);
+      tap("vc", l, Ld.vc, (size_t)nkv_ * max_ctx_ * hd * 2, s);
       dump("kqv_out-" + L, attn_, nh_ * hd, s);
       if (!q8_in_combine) {
         launch_quantize_q8_0(attn_, hp_.n_head * hd, act_.q8, s);
@@ -784,7 +842,9 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
       LayerGemv go;
       go.xg = act_.q8.xb;
       go.out = o_out_ + (size_t)tp_rank_ * e_sh_;
+      tap("xo", l, act_.q8.xb, (size_t)hp_.n_head * hd / 32 * sizeof(XBlock), s);
       for (int r = 0; r < dup("o_proj"); r++) launch_layer_gemv(Ld.o.w, go, LAYER_PLAIN, s);
+      tap("o", l, o_out_, (size_t)E * 4, s);
       dump("attention results (node_30 for MUL_MAT)-" + L, o_out_, E, s);
     }
     if (tp_) coll_->all_gather(o_out_, (size_t)e_sh_ * sizeof(float), s);
@@ -797,8 +857,11 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
     gg.eps = hp_.eps;
     gg.hid = hid_ + (size_t)tp_rank_ * f_sh_;
     gg.epoch = epoch;  // advances the attention block's granule tag of this layer
-    if (dump_) gg.xn_out = xn_;
+    if (dump_ || trace_fn_) gg.xn_out = xn_;
     for (int r = 0; r < dup("gate_up"); r++) launch_layer_gemv(Ld.gate_up[0].w, gg, LAYER_GELU, s);
+    tap("ffn_resid", l, other, (size_t)E * 4, s);
+    tap("ffn_norm", l, xn_, (size_t)E * 4, s);
+    tap("hid", l, hid_, (size_t)hp_.n_ff * 4, s);
     dump("sa_out-" + L, other, E, s);
     dump("ffn_norm-" + L, xn_, E, s);
     dump("ffn_geglu-" + L, hid_, hp_.n_ff, s);
@@ -808,6 +871,7 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
     gd.y = hid_;  // QUANT: GELU output quantized per block in the down launch
     gd.out = d_out_ + (size_t)tp_rank_ * e_sh_;
     for (int r = 0; r < dup("down"); r++) launch_layer_gemv(Ld.down.w, gd, LAYER_QUANT, s);
+    tap("down", l, d_out_, (size_t)E * 4, s);
     if (tp_) coll_->all_gather(d_out_, (size_t)e_sh_ * sizeof(float), s);
     dump("ffn_out-" + L, d_out_, E, s);
     kernels_per_token_ += block_ ? 2 : 3;  // (o, when not in the attention block,) gate_up, down
@@ -818,6 +882,8 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
   if (embd_.type == T_F16) o2.x16 = act_.x16;
   launch_residual_norm(d_out_, L_.back().post_ffw_norm, cur, out_norm_, o2, E, hp_.eps, false, s);
   kernels_per_token_++;
+  tap("final_resid", -1, cur, (size_t)E * 4, s);
+  tap("result_norm", -1, xn_, (size_t)E * 4, s);
   dump("l_out-" + std::to_string(hp_.n_layer - 1), cur, E, s);
   dump("result_norm", xn_, E, s);
 }
@@ -964,6 +1030,51 @@ void Session::dump(const std::string& name, const float* dev, int n, hipStream_t
   float sum = 0.0f;
   for (float v : h) sum += v;
   std::fprintf(dump_, "],\n     ],\n    ]\n    sum = %.6f\n", sum);
+}
+
+void Session::tap(const char* name, int layer, const void* dev, size_t bytes, hipStream_t s) {
+  if (!trace_fn_) return;
+  LLMI_HIP(hipStreamSynchronize(s));
+  std::vector<uint8_t> h(bytes);
+  LLMI_HIP(hipMemcpy(h.data(), dev, bytes, hipMemcpyDeviceToHost));
+  trace_fn_(trace_user_, name, layer, h.data(), bytes);
+}
+
+// llmi_session_trace: the launches of forward() (batched prefill for n > 1
+// when the session runs it, else the token loop) or of one decode-loop step
+// (gen), eager, each followed by host copies of what it produced
+void Session::forward_trace(const int32_t* tokens, int n, int pos, bool gen, llmi_trace_fn fn, void* user) {
+  if (n <= 0) throw status_error(LLMI_E_ARG, "trace: no tokens");
+  if (pos < 0 || pos + n > max_ctx_) throw status_error(LLMI_E_RANGE, "trace: context overflow");
+  for (int i = 0; i < n; i++)
+    if (tokens[i] < 0 || tokens[i] >= vocab_) throw status_error(LLMI_E_RANGE, "trace: token id out of range");
+  if (tp_) throw status_error(LLMI_E_ARG, "trace: one device only");
+  const bool graph = use_graph_;
+  use_graph_ = false;
+  trace_fn_ = fn;
+  trace_user_ = user;
+  auto done = [&] {
+    trace_fn_ = nullptr;
+    trace_user_ = nullptr;
+    use_graph_ = graph;
+  };
+  try {
+    if (n > 1 && prefill_ok_ && getenv("LLMI_NO_PREFILL") == nullptr) {
+      set_token_pos(tokens[n - 1], pos + n - 1, true);
+      prefill(tokens, n, pos);
+    } else {
+      for (int i = 0; i < n; i++) {
+        set_token_pos(tokens[i], pos + i, i == 0);
+        record_step(stream_, gen && screen_);
+      }
+    }
+    LLMI_HIP(hipStreamSynchronize(stream_));
+  } catch (...) {
+    done();
+    throw;
+  }
+  done();
+  check_device_error();
 }
 
 void Session::forward_dump(const int32_t* tokens, int n, int pos, const char* path) {

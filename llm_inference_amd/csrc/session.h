@@ -44,6 +44,7 @@ struct LayerDev {
   bool is_swa = false;
   bool gu_interleaved = false;  // gate_up rows in groups of 32 (k_layer.hip GELU epilogue)
   bool fused = false;           // every projection runs as gemv_q4_0_layer
+  bool aliased = false;         // LLMI_SHARE_LAYERS diagnostics: weights owned by another layer
   int hd = 0;
   uint16_t *kc = nullptr, *vc = nullptr;
 };
@@ -57,6 +58,7 @@ class Session {
 
   void forward(const int32_t* tokens, int n_tokens, int pos, float* logits, int32_t* argmax);
   void forward_dump(const int32_t* tokens, int n_tokens, int pos, const char* path);
+  void forward_trace(const int32_t* tokens, int n_tokens, int pos, bool gen, llmi_trace_fn fn, void* user);
   void enqueue(int32_t first, int pos, int n_steps);
   void sync(int32_t* out_tokens, int n);
   void info(llmi_session_info* out) const;
@@ -87,6 +89,10 @@ class Session {
   // llmi_session_dump: eager steps with print_tensor-format dumps (dump_ set)
   std::FILE* dump_ = nullptr;
   void dump(const std::string& name, const float* dev, int n, hipStream_t s);
+  // llmi_session_trace: host copies of what each launch produced (eager steps)
+  llmi_trace_fn trace_fn_ = nullptr;
+  void* trace_user_ = nullptr;
+  void tap(const char* name, int layer, const void* dev, size_t bytes, hipStream_t s);
   void run_step(bool gen = false);
   float* dev_f32_copy(const GGUFView& g, const GTensor* t, int n);
   template <typename T>

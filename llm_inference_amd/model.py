@@ -12,7 +12,7 @@ from typing import Optional, Sequence
 
 import numpy as np
 
-from ._lib import LLMI_EXACT, LLMI_NO_GRAPH, TP_ID_BYTES, SessionInfo, SessionOpts, check, lib, ptr
+from ._lib import LLMI_EXACT, LLMI_NO_GRAPH, TP_ID_BYTES, TRACE_FN, SessionInfo, SessionOpts, check, lib, ptr
 from .gguf import GGUFFile
 
 
@@ -85,6 +85,21 @@ class Model:
         reference's --verbose intermediates (print_tensor format) to `path`."""
         t = np.ascontiguousarray(tokens, np.int32)
         check(lib().llmi_session_dump(self.h, ptr(t), t.size, pos, path.encode()))
+
+    def trace(self, tokens: Sequence[int], pos: int, gen: bool = False) -> list:
+        """llmi_session_trace: run the launches forward() (or, gen=True, one
+        decode-loop step) performs, eagerly, and return what each launch
+        produced as [(name, layer, bytes)] in launch order (op-level parity
+        tests compare each against the oracle from the device's own inputs)."""
+        t = np.ascontiguousarray(tokens, np.int32)
+        out = []
+
+        def cb(_user, name, layer, data, nbytes):
+            out.append((name.decode(), int(layer), C.string_at(data, nbytes)))
+
+        fn = TRACE_FN(cb)  # kept alive for the duration of the call
+        check(lib().llmi_session_trace(self.h, ptr(t), t.size, pos, 1 if gen else 0, fn, None))
+        return out
 
     def generate(self, first: int, pos: int, n_steps: int) -> np.ndarray:
         out = np.zeros(max(n_steps, 1), np.int32)

@@ -50,6 +50,7 @@ CONFIGS: Dict[str, Gemma3Config] = {
     # reduced shapes for tests (same head/GQA structure, few layers, small vocab)
     "mini-4b": Gemma3Config("mini-4b", 2, 2560, 10240, 8, 4, 256, 4096),
     "mini-1b": Gemma3Config("mini-1b", 2, 1152, 6912, 4, 1, 256, 2048),
+    "mini-27b": Gemma3Config("mini-27b", 2, 5376, 21504, 32, 16, 128, 4096),
     "tiny": Gemma3Config("tiny", 3, 256, 512, 4, 2, 64, 512),
 }
 

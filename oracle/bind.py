@@ -46,6 +46,7 @@ class Oracle:
         L.orc_quantize_row_q8_0.argtypes = [_f32p, C.c_size_t, C.c_void_p]
         L.orc_quantize_row_q8_k.argtypes = [_f32p, C.c_size_t, C.c_void_p]
         L.orc_mat_vec_mul.argtypes = [C.c_uint32, C.c_void_p, C.c_size_t, C.c_size_t, _f32p, _f32p, C.c_int]
+        L.orc_mat_vec_mul_q8.argtypes = [C.c_uint32, C.c_void_p, C.c_size_t, C.c_size_t, C.c_void_p, _f32p, C.c_int]
         L.orc_dequantize_row.argtypes = [C.c_uint32, C.c_void_p, C.c_size_t, _f32p]
         L.orc_rms_norm.argtypes = [_f32p, _f32p, C.c_size_t, C.c_double]
         L.orc_softmax.argtypes = [_f32p, C.c_size_t]
@@ -55,6 +56,7 @@ class Oracle:
         L.orc_vec_mad_f16.argtypes = [_u16p, _u16p, C.c_size_t, C.c_float]
         L.orc_gelu_mul.argtypes = [_f32p, _f32p, _f32p, C.c_size_t]
         L.orc_attn_head.argtypes = [_f32p, _u16p, _u16p, C.c_size_t, C.c_size_t, _f32p]
+        L.orc_attn_head_f64.argtypes = [_f32p, _u16p, _u16p, C.c_size_t, C.c_size_t, _f32p]
         L.orc_model_create.restype = C.c_void_p
         L.orc_model_create.argtypes = [C.c_void_p, C.c_size_t, C.c_int, C.c_int]
         L.orc_model_forward.argtypes = [C.c_void_p, _i32p, C.c_int, C.c_int, _f32p]
@@ -86,6 +88,24 @@ class Oracle:
         if self.lib.orc_mat_vec_mul(ttype, _ptr(w), n_rows, n_cols, x, o, n_threads) != 0:
             raise RuntimeError(self.lib.orc_last_error().decode())
         return o
+
+    def mat_vec_mul_q8(self, ttype, w, n_rows, n_cols, xq, n_threads=8):
+        """Q4_0/Q8_0 rows x an already-quantized activation (34-B BlockQ8_0 row)."""
+        w = np.ascontiguousarray(w)
+        xq = np.ascontiguousarray(xq, np.uint8)
+        assert xq.size == n_cols // 32 * 34
+        o = np.zeros(n_rows, np.float32)
+        if self.lib.orc_mat_vec_mul_q8(ttype, _ptr(w), n_rows, n_cols, _ptr(xq), o, n_threads) != 0:
+            raise RuntimeError(self.lib.orc_last_error().decode())
+        return o
+
+    def attn_head_f64(self, q, k, v):
+        """float64-accumulating restatement (pins the fast path, not the reference)."""
+        q = np.ascontiguousarray(q, np.float32)
+        out = np.zeros_like(q)
+        self.lib.orc_attn_head_f64(q, np.ascontiguousarray(k, np.uint16), np.ascontiguousarray(v, np.uint16),
+                                   k.shape[0], q.size, out)
+        return out
 
     def dequantize_row(self, ttype, blocks, n_cols):
         o = np.zeros(n_cols, np.float32)

@@ -311,6 +311,9 @@ static void* gemv_worker(void* arg) {
   return NULL;
 }
 
+static void gemv_run(uint32_t type, const void* w, size_t rb, size_t n_rows, size_t n_cols, const void* xprep,
+                     const float* x, float* o, int n_threads);
+
 int orc_mat_vec_mul(uint32_t type, const void* w, size_t n_rows, size_t n_cols,
                     const float* x, float* o, int n_threads) {
   pthread_once(&g_table_once, table_init);
@@ -328,6 +331,24 @@ int orc_mat_vec_mul(uint32_t type, const void* w, size_t n_rows, size_t n_cols,
     for (size_t j = 0; j < n_cols; j++) x16[j] = orc_f32_to_f16(x[j]);
     xprep = x16;
   }
+  gemv_run(type, w, rb, n_rows, n_cols, xprep, x, o, n_threads);
+  free(xprep);
+  return 0;
+}
+
+/* The Q4_0 / Q8_0 row loops of mat_vec_mul (ops.cpp:364-399, 806-824) on an
+ * activation that is ALREADY a row of 34-B BlockQ8_0 (ops.h:89-92): the
+ * op-level tests feed the device's own quantized inputs (prefill GEMM). */
+int orc_mat_vec_mul_q8(uint32_t type, const void* w, size_t n_rows, size_t n_cols, const void* xq, float* o,
+                       int n_threads) {
+  pthread_once(&g_table_once, table_init);
+  if (type != ORC_Q4_0 && type != ORC_Q8_0) return ORC_FAIL("mat_vec_mul_q8: type %u is not Q4_0/Q8_0", type);
+  gemv_run(type, w, orc_row_bytes(type, n_cols), n_rows, n_cols, xq, NULL, o, n_threads);
+  return 0;
+}
+
+static void gemv_run(uint32_t type, const void* w, size_t rb, size_t n_rows, size_t n_cols, const void* xprep,
+                     const float* x, float* o, int n_threads) {
   if (n_threads < 1) n_threads = 1;
   const size_t chunk = (n_rows + n_threads - 1) / n_threads;
   gemv_job jobs[256];
@@ -344,8 +365,6 @@ int orc_mat_vec_mul(uint32_t type, const void* w, size_t n_rows, size_t n_cols,
     for (int t = 0; t < nj; t++) pthread_create(&th[t], NULL, gemv_worker, &jobs[t]);
     for (int t = 0; t < nj; t++) pthread_join(th[t], NULL);
   }
-  free(xprep);
-  return 0;
 }
 
 int orc_dequantize_row(uint32_t type, const void* blocks, size_t n_cols, float* o) {

@@ -56,6 +56,9 @@ int orc_mat_vec_mul(uint32_t type, const void* w, size_t n_rows, size_t n_cols,
 
 /* one row of a quantized embedding table -> f32: ops.cpp:958-1082 (Q4_K,
  * Q6_K, Q8_0, Q5_0); F16/F32 handled too (model.cpp:247-257) */
+/* Q4_0 / Q8_0 rows against an already-quantized activation (34-B BlockQ8_0) */
+int orc_mat_vec_mul_q8(uint32_t type, const void* w, size_t n_rows, size_t n_cols, const void* xq, float* o,
+                       int n_threads);
 int orc_dequantize_row(uint32_t type, const void* blocks, size_t n_cols,
                        float* o);
 
