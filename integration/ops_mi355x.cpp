@@ -53,16 +53,54 @@ struct WeightKeyHash {
   }
 };
 
+// Sampled content fingerprint of a weight's bytes (FNV-1a over 64 evenly
+// spaced 64-byte windows and the length): a buffer freed and reallocated at
+// the same address with other contents (model_test.cpp:394/410/463 builds
+// several Models from heap vectors in one process) gets a new upload instead
+// of the previous tensor's device copy.
+uint64_t fingerprint(const void* data, size_t bytes) {
+  const uint8_t* p = static_cast<const uint8_t*>(data);
+  uint64_t h = 1469598103934665603ull ^ bytes;
+  const size_t win = 64, n = bytes < win ? 1 : 64;
+  for (size_t i = 0; i < n; i++) {
+    const size_t off = bytes <= win ? 0 : (bytes - win) * i / (n - 1 ? n - 1 : 1);
+    for (size_t j = 0; j < win && off + j < bytes; j++) h = (h ^ p[off + j]) * 1099511628211ull;
+  }
+  return h;
+}
+
+size_t weight_bytes(uint32_t type, size_t rows, size_t cols) {
+  switch (type) {
+    case 2: return rows * cols / 32 * 18;    // Q4_0
+    case 6: return rows * cols / 32 * 22;    // Q5_0
+    case 8: return rows * cols / 32 * 34;    // Q8_0
+    case 12: return rows * cols / 256 * 144; // Q4_K
+    case 14: return rows * cols / 256 * 210; // Q6_K
+    default: return rows * cols * 2;         // F16 / BF16
+  }
+}
+
+struct Cached {
+  llmi_weight* w;
+  uint64_t fp;
+};
+
+std::mutex g_cache_mu;
+std::unordered_map<WeightKey, Cached, WeightKeyHash> g_cache;
+
 llmi_weight* cached_weight(uint32_t type, const void* data, size_t rows, size_t cols) {
-  static std::mutex mu;
-  static std::unordered_map<WeightKey, llmi_weight*, WeightKeyHash> cache;
-  std::lock_guard<std::mutex> lock(mu);
+  std::lock_guard<std::mutex> lock(g_cache_mu);
   const WeightKey key{data, type, rows, cols};
-  auto it = cache.find(key);
-  if (it != cache.end()) return it->second;
+  const uint64_t fp = fingerprint(data, weight_bytes(type, rows, cols));
+  auto it = g_cache.find(key);
+  if (it != g_cache.end()) {
+    if (it->second.fp == fp) return it->second.w;
+    llmi_weight_destroy(it->second.w);  // same address, other contents: stale
+    g_cache.erase(it);
+  }
   llmi_weight* w = nullptr;
   check(llmi_weight_create(type, data, rows, cols, &w));
-  cache.emplace(key, w);
+  g_cache.emplace(key, Cached{w, fp});
   return w;
 }
 
@@ -97,6 +135,14 @@ void unflatten(const std::vector<float>& f, tensor_3& t, size_t n0, size_t n1, s
 }
 
 }  // namespace
+
+// Drops every cached device weight (e.g. after a GGUFFile is unmapped);
+// extern "C" so a host that owns the model lifetime can call it.
+extern "C" void llmi_ops_flush_weights(void) {
+  std::lock_guard<std::mutex> lock(g_cache_mu);
+  for (auto& kv : g_cache) llmi_weight_destroy(kv.second.w);
+  g_cache.clear();
+}
 
 void init_ops(int /*n_threads*/) { check(llmi_init_ops(0)); }  // ops.cpp:21-24: device 0 instead of a pool
 

@@ -18,6 +18,8 @@ thread_local std::string g_err;
 struct Ctx {
   int device = -1;
   hipStream_t stream = nullptr;
+  // orders a caller stream against this context's scratch (device-pointer GEMV)
+  hipEvent_t ev_in = nullptr, ev_out = nullptr;
   // grow-only scratch for the host-pointer ops API
   std::vector<std::pair<void*, size_t>> bufs;
   void* get(int slot, size_t bytes) {
@@ -164,10 +166,28 @@ void llmi_weight_destroy(llmi_weight* w) {
 int llmi_weight_mat_vec_mul_dev(const llmi_weight* w, const float* x_dev, float* o_dev, uint32_t flags,
                                 void* stream) {
   return guard([&] {
+    if (!w || !x_dev || !o_dev) throw status_error(LLMI_E_ARG, "null pointer");
+    check_shape(w->w.type, w->w.rows, w->w.cols, w->w.cols);
     Ctx& c = ctx();
     hipStream_t s = stream ? (hipStream_t)stream : c.stream;
+    // the activation goes through this thread's scratch slots, which the
+    // host-pointer calls use on c.stream: a caller stream first waits for
+    // c.stream's earlier work, and c.stream then waits for this call, so calls
+    // on any mix of streams touch the scratch one at a time
+    if (s != c.stream) {
+      if (!c.ev_in) {
+        LLMI_HIP(hipEventCreateWithFlags(&c.ev_in, hipEventDisableTiming));
+        LLMI_HIP(hipEventCreateWithFlags(&c.ev_out, hipEventDisableTiming));
+      }
+      LLMI_HIP(hipEventRecord(c.ev_in, c.stream));
+      LLMI_HIP(hipStreamWaitEvent(s, c.ev_in, 0));
+    }
     ActBuf a = make_act(c, w->w.type, x_dev, w->w.cols, s);
     launch_gemv(w->w, a, o_dev, (flags & LLMI_EXACT) ? GEMV_EXACT : GEMV_FAST, s);
+    if (s != c.stream) {
+      LLMI_HIP(hipEventRecord(c.ev_out, s));
+      LLMI_HIP(hipStreamWaitEvent(c.stream, c.ev_out, 0));
+    }
   });
 }
 

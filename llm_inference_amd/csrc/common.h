@@ -16,6 +16,8 @@
 #include <stdexcept>
 #include <string>
 
+#include "glibc_math.h"
+
 namespace llmi {
 
 constexpr int WAVE = 64;
@@ -67,11 +69,13 @@ __device__ __forceinline__ int nearest_int_fma(float a, float b) {
   return (int)(__float_as_uint(fmaf(a, b, 12582912.f)) & 0x007fffffu) - 0x00400000;
 }
 
-// GELU(tanh)(x) * u (model.cpp:892-899; model.cpp is built without FMA)
+// GELU(tanh)(x) * u (model.cpp:892-899; no contraction in the reference's
+// build of this expression), with glibc's own tanhf (glibc_math.h): bit-exact
+// with the reference for the same gate/up inputs
 __device__ __forceinline__ float gelu_mul1(float x, float u) {
   const float c = __uint_as_float(0x3F4C4229u);  // sqrtf((float)(2.0 / M_PI)) = 0.79788452f
   const float inner = x + ((0.044715f * x) * x) * x;
-  return ((0.5f * x) * (1.0f + tanhf(c * inner))) * u;
+  return ((0.5f * x) * (1.0f + llmi_glibc::tanhf(c * inner))) * u;
 }
 
 __device__ __forceinline__ int sdot4(int a, int b, int c) { return __builtin_amdgcn_sdot4(a, b, c, false); }

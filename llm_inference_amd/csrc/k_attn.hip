@@ -85,7 +85,7 @@ void launch_qk_norm_rope_kv(const QKVArgs& a, bool exact, hipStream_t s) {
 // order; score = sequential double sum of exact f32 products f16(k)*f16(q);
 // online max with double/float compares as in the reference; f16 V
 // accumulator rounded every step (vec_scale_f16 / vec_mad_f16).
-// expf is the device libm's (documented ulp-level difference from glibc).
+// expf is glibc's own algorithm (glibc_math.h), so the step is bit-exact.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void attn_exact_kernel(AttnArgs a) {
   __shared__ float s_prod[256];
@@ -112,10 +112,10 @@ __global__ __launch_bounds__(256) void attn_exact_kernel(AttnArgs a) {
       if (score > (double)prev) {
         max_score = (float)score;
         e = 1.0f;
-        pe = expf(prev - max_score);
+        pe = llmi_glibc::expf(prev - max_score);
         resc = 1;
       } else {
-        e = expf((float)(score - (double)max_score));
+        e = llmi_glibc::expf((float)(score - (double)max_score));
         pe = 1.0f;
         resc = 0;
       }

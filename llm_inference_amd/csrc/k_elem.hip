@@ -144,7 +144,7 @@ __global__ void softmax_kernel(float* x, int n) {
   float mx = x[0];
   for (int i = 0; i < n; i++) if (x[i] > mx) mx = x[i];
   float sum = 0.0f;
-  for (int i = 0; i < n; i++) { x[i] = expf(x[i] - mx); sum += x[i]; }
+  for (int i = 0; i < n; i++) { x[i] = llmi_glibc::expf(x[i] - mx); sum += x[i]; }
   for (int i = 0; i < n; i++) x[i] /= sum;
 }
 void launch_softmax(float* x, int n, hipStream_t s) {

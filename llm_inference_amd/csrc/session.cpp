@@ -1135,7 +1135,10 @@ void Session::check_device_error() {
   if (!blk_err_) return;
   int e = 0;
   LLMI_HIP(hipMemcpy(&e, blk_err_, sizeof(e), hipMemcpyDeviceToHost));
-  if (e) throw status_error(LLMI_E_HIP, "attention block: a cross-work-group wait timed out (device results invalid)");
+  if (e) {  // reported once: the flag is cleared so the session's next call starts clean
+    LLMI_HIP(hipMemset(blk_err_, 0, sizeof(int)));
+    throw status_error(LLMI_E_HIP, "attention block: a cross-work-group wait timed out (device results invalid)");
+  }
 }
 
 void Session::info(llmi_session_info* o) const {

@@ -63,11 +63,20 @@ def _f16_bits(x: np.ndarray) -> np.ndarray:
 
 
 def fill_random(out: np.ndarray, ttype: int, n_rows: int, n_cols: int, rng: np.random.Generator,
-                scale_lo: float = 0.002, scale_hi: float = 0.02) -> None:
-    """Fill ``out`` (uint8 view of exactly the tensor's bytes) with random blocks."""
+                scale_lo: float = 0.002, scale_hi: float = 0.02, centered: bool = False) -> None:
+    """Fill ``out`` (uint8 view of exactly the tensor's bytes) with random blocks.
+    centered: Q4_0 nibbles uniform on 1..15 (q - 8 symmetric, zero mean, like
+    trained weights) instead of 0..15 (mean -0.5: every projection then adds a
+    fixed common-mode direction and a deep random model decodes one token
+    forever)."""
     if ttype == TensorType.Q4_0:
         blk = out.reshape(-1, 18)
-        blk[:, 2:] = rng.integers(0, 256, size=(blk.shape[0], 16), dtype=np.uint8)
+        if centered:
+            lo = rng.integers(1, 16, size=(blk.shape[0], 16), dtype=np.uint8)
+            hi = rng.integers(1, 16, size=(blk.shape[0], 16), dtype=np.uint8)
+            blk[:, 2:] = lo | (hi << 4)
+        else:
+            blk[:, 2:] = rng.integers(0, 256, size=(blk.shape[0], 16), dtype=np.uint8)
         blk[:, 0:2] = _f16_bits(rng.uniform(scale_lo, scale_hi, blk.shape[0])).view(np.uint8).reshape(-1, 2)
     elif ttype == TensorType.Q8_0:
         blk = out.reshape(-1, 34)
@@ -88,9 +97,13 @@ def fill_random(out: np.ndarray, ttype: int, n_rows: int, n_cols: int, rng: np.r
         blk[:, 192:208] = rng.integers(-64, 64, size=(blk.shape[0], 16), dtype=np.int8).view(np.uint8)
         blk[:, 208:210] = _f16_bits(rng.uniform(scale_lo, scale_hi, blk.shape[0]) / 64).view(np.uint8).reshape(-1, 2)
     elif ttype in (TensorType.F16,):
-        # sign | exponent in [7, 11] (|w| ~ 2^-8 .. 2^-4) | random mantissa
+        # sign | exponent in [7, 11] (|w| ~ 2^-8 .. 2^-4) | random mantissa;
+        # centered: [4, 8] (|w| ~ 2^-11 .. 2^-7), so with tied embeddings the
+        # token's own row no longer dominates the final state and greedy
+        # decoding does not just repeat its input
         bits = rng.integers(0, 1 << 16, size=out.size // 2, dtype=np.uint16)
-        exp = (rng.integers(7, 12, size=bits.size, dtype=np.uint16) << 10)
+        e0 = 4 if centered else 7
+        exp = (rng.integers(e0, e0 + 5, size=bits.size, dtype=np.uint16) << 10)
         out.view(np.uint16)[:] = (bits & np.uint16(0x83FF)) | exp
     elif ttype == TensorType.BF16:
         v = rng.normal(0, 0.02, size=out.size // 2).astype(np.float32)
@@ -112,7 +125,7 @@ def random_tensor(ttype: int, n_rows: int, n_cols: int, seed: int = 0, **kw) -> 
 # ---------------------------------------------------------------------------
 def build_gemma3_gguf(cfg: Gemma3Config, seed: int = 0, wtype: int = TensorType.Q4_0,
                       embd_type: int = TensorType.F16, wtypes: Optional[Dict[str, int]] = None,
-                      swa_pattern: Optional[list] = None) -> np.ndarray:
+                      swa_pattern: Optional[list] = None, centered: bool = False) -> np.ndarray:
     """Random-init Gemma-3 GGUF with the tensor names/shapes model.cpp maps
     (model.cpp:169-238).  Returns the whole file as a uint8 numpy array."""
     rng = np.random.default_rng(seed)
@@ -167,7 +180,7 @@ def build_gemma3_gguf(cfg: Gemma3Config, seed: int = 0, wtype: int = TensorType.
             v.view(np.float32)[:] = rng.uniform(0.6, 1.4, size=v.size // 4).astype(np.float32)
         else:
             n_rows = shape[1] if len(shape) > 1 else 1
-            fill_random(v, tt, n_rows, shape[0], rng)
+            fill_random(v, tt, n_rows, shape[0], rng, centered=centered)
     return buf
 
 

@@ -30,6 +30,8 @@ def run(gguf_path, n_decode, prompt):
     rows = []
     for line in out.stdout.splitlines():
         f = line.split()
+        if f[0] == "model":  # several files in one process: a separator line per model
+            continue
         assert f[0] == "logits"
         rows.append((int(f[1]), int(f[2]), np.array([float(v) for v in f[3:]], np.float32)))
     return rows
@@ -53,3 +55,29 @@ def test_dropin_tiny_greedy(golden_models, tmp_path):
     assert [a for _, a, _ in rows] == ref_toks.tolist()
     for i, (_, _, lg) in enumerate(rows):
         np.testing.assert_allclose(lg, ref_logits[i][:16], atol=1e-5, rtol=0)
+
+
+def test_dropin_two_models_one_process(oracle, tmp_path):
+    """Two same-shape GGUFs (different seeds) run one after another in ONE
+    process (model_test.cpp:394/410/463 builds several Models from heap
+    buffers the same way): the second model's freed-and-reused addresses must
+    not serve the first model's cached device weights (ops_mi355x.cpp content
+    fingerprint).  Each model's logits equal the oracle's (= the reference's)
+    for its own file."""
+    from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
+    cfg = CONFIGS["tiny"]
+    paths, models = [], []
+    for seed in (7, 8):
+        g = build_gemma3_gguf(cfg, seed=seed, swa_pattern=[True, False, True])
+        p = tmp_path / f"m{seed}.gguf"
+        p.write_bytes(bytes(g))
+        paths.append(str(p))
+        models.append(oracle.model(g, n_threads=4, max_ctx=64))
+    prompt = [2, 17, 301, 44, 9]
+    rows = run(",".join(paths), 2, prompt)
+    assert len(rows) == 2 * 3
+    for mi, om in enumerate(models):
+        lg = om.forward(prompt, 0)
+        _, a, l0 = rows[3 * mi]
+        assert a == int(np.argmax(lg))
+        np.testing.assert_allclose(l0, lg[:16], atol=1e-5, rtol=0)
