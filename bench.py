@@ -44,7 +44,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--full-logits", action="store_true",
                    help="decode loop: full F16 logits GEMV + argmax instead of int8 screening + exact rescoring")
-    p.add_argument("--cpu-decode", type=int, default=24, help="decode tokens in the CPU baseline sample")
+    p.add_argument("--cpu-decode", type=int, default=32, help="decode tokens in the CPU baseline sample")
     p.add_argument("--kernel-reps", type=int, default=2)
     p.add_argument("--no-graph", action="store_true", help="eager launches (for kernel tracers)")
     p.add_argument("--mode", choices=["tp", "replicas"], default="tp",
@@ -54,17 +54,19 @@ def parse():
     return p.parse_args()
 
 
-def pmc_traffic():
-    """HBM bytes per launch of the Q4_0 projection family from the committed
-    rocprofv3 --pmc FETCH_SIZE pass (profiles/, x2 gfx950 correction; see
-    scripts/pmc_summary.py); None when no such profile is committed."""
+def pmc_traffic(kernel_substr: str):
+    """HBM bytes per launch of the kernel whose name contains kernel_substr,
+    from the newest committed rocprofv3 --pmc FETCH_SIZE pass (profiles/,
+    x2 gfx950 correction: scripts/pmc_summary.py); (None, None) when absent."""
     import glob
-    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "*pmc_fetch*.json")))
-    if not files:
-        return None, None
-    fam = json.load(open(files[-1])).get("q4_0_layer_family", {})
-    b = fam.get("hbm_bytes_per_launch")
-    return (round(b), os.path.relpath(files[-1], os.path.dirname(os.path.abspath(__file__)))) if b else (None, None)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_fetch*.json")))
+    for f in reversed(files):
+        ks = json.load(open(f)).get("kernels", {})
+        hits = [v for k, v in ks.items() if kernel_substr in k]
+        if hits:
+            v = max(hits, key=lambda h: h["dispatches"])
+            return round(v["hbm_bytes_mean"]), os.path.relpath(f, ROOT)
+    return None, None
 
 
 class Dist:
@@ -99,31 +101,128 @@ class Dist:
         return float(t.item())
 
 
-def cpu_baseline(g, cfg, n_decode: int):
-    """The reference's own Model::forward (oracle/_ref, built from its sources)
-    on this host's cores; falls back to the oracle restatement ("port")."""
-    from oracle import bind
-    threads = min(os.cpu_count() or 1, 16)
-    kind = "reference"
+def _cpu_model_name():
     try:
-        eng = bind.Reference(n_threads=threads)
-        m = eng.model(g)
-    except Exception:
-        kind = "port"
-        eng = bind.Oracle()
-        m = eng.model(g, n_threads=threads, max_ctx=64)
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_share() -> int:
+    """Host threads this process may use: the CPU affinity, capped at the
+    GPU box's per-GPU share (16: the box's nproc counts the whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(n, int(os.environ.get("LLMI_CPU_SHARE", "16"))))
+
+
+def cpu_baseline(g, cfg, n_decode: int, gpu_ids=None, mean_ctx=None):
+    """BASELINE.md section 4 on this host: the reference's own Model::forward
+    (oracle/_ref, built from its sources) -- or, where the reference is not
+    built, the oracle restatement ("port") -- timed on a bounded sample.
+
+    * decode rate at `threads` (this process's CPU share) and at half of it
+      (the reference's default is hw/2, main.cpp:12), 8-token prompt then
+      n_decode greedy tokens, per-step wall clock;
+    * the per-position attention cost from a linear fit of those per-step
+      times (the reference's run_attn is single-threaded and O(pos)), and the
+      rate extrapolated to the GPU run's mean context;
+    * GEMV-only timings at the 4B shapes (mat_vec_mul / mat_vec_mul_fp16);
+    * configs[0]: Gemma-3 1B Q4_0, --predict 64;
+    * the CPU's greedy ids vs the GPU's on the same prompt (gpu_ids)."""
+    from oracle import bind
+    from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf, random_tensor
+    from llm_inference_amd.gguf import TensorType as TT
+    threads = cpu_share()
+
+    def engine(n):
+        try:
+            return "reference", bind.Reference(n_threads=n)
+        except Exception:
+            return "port", bind.Oracle()
+
+    def model(eng, kind, gg, n):
+        return eng.model(gg) if kind == "reference" else eng.model(gg, n_threads=n, max_ctx=128)
+
     prompt = [2] + list(range(100, 107))
-    lg = m.forward(np.array(prompt, np.int32), 0)
+    out = {"cores": threads, "cpu_model": _cpu_model_name(), "compiler": "g++ -std=c++17 -O2 -DNDEBUG -mavx2 -mfma -mf16c (BUILD:41-53)"}
+    runs = {}
+    for n in (threads, max(1, threads // 2)):
+        kind, eng = engine(n)
+        m = model(eng, kind, g, n)
+        lg = m.forward(np.array(prompt, np.int32), 0)
+        tok, pos, ids, per = int(np.argmax(lg)), len(prompt), [int(np.argmax(lg))], []
+        for _ in range(n_decode):
+            t0 = time.perf_counter()
+            lg = m.forward(np.array([tok], np.int32), pos)
+            per.append(time.perf_counter() - t0)
+            tok, pos = int(np.argmax(lg)), pos + 1
+            ids.append(tok)
+        del m
+        runs[n] = (kind, per, ids)
+    kind, per, ids = runs[threads]
+    per = np.array(per)
+    x = np.arange(len(prompt), len(prompt) + len(per))
+    slope, icpt = np.polyfit(x, per, 1)
+    out.update({
+        "value": round(len(per) / per.sum(), 3), "unit": "tokens/s", "kind": kind,
+        "sample": f"{cfg.name} synthetic GGUF, {len(prompt)}-token prompt then {len(per)} greedy decode tokens "
+                  f"(pos {len(prompt)}-{len(prompt) + len(per) - 1}) via Model::forward on {threads} threads",
+        "half_threads": {"threads": max(1, threads // 2),
+                         "value": round(len(runs[max(1, threads // 2)][1]) / sum(runs[max(1, threads // 2)][1]), 3)},
+        "attention_s_per_position": float(max(slope, 0.0)),
+        "step_s_at_pos0": float(icpt),
+    })
+    if mean_ctx:  # the linear fit extrapolated to the GPU run's mean context (an estimate, not a measurement)
+        out["estimated_at_gpu_mean_context"] = {
+            "position": int(mean_ctx), "value": round(1.0 / (icpt + max(slope, 0.0) * mean_ctx), 3),
+            "unit": "tokens/s", "how": "step time = a + b * pos fitted to the measured per-step times"}
+    out["ids"] = ids
+    if gpu_ids is not None:
+        k = min(len(ids), len(gpu_ids))
+        same = [a == b for a, b in zip(ids[:k], gpu_ids[:k])]
+        out["id_check"] = {"steps": k, "identical": all(same),
+                           "first_difference": (same.index(False) if not all(same) else None)}
+    # GEMV-only (the reference's mat_vec_mul, 4B shapes; BASELINE.md section 4 / SURVEY section 6)
+    kind_t, eng = engine(threads)
+    gemv = {}
+    rng = np.random.default_rng(1)
+    for name, tt, rows, cols in (("q4_0 2560->2048", TT.Q4_0, 2048, 2560), ("q4_0 2560->10240", TT.Q4_0, 10240, 2560),
+                                 ("q4_0 10240->2560", TT.Q4_0, 2560, 10240), ("f16 2560->262208", TT.F16, 262208, 2560)):
+        w = random_tensor(tt, rows, cols, seed=3)
+        xv = rng.standard_normal(cols).astype(np.float32)
+        reps = 5 if tt == TT.F16 else 50
+        if kind_t == "reference":
+            dt = eng.time_gemv(tt, w, rows, cols, xv, reps)
+        else:
+            eng.mat_vec_mul(tt, w, rows, cols, xv, threads)
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                eng.mat_vec_mul(tt, w, rows, cols, xv, threads)
+            dt = (time.perf_counter() - t0) / reps
+        gemv[name] = {"us": round(dt * 1e6, 1), "GBps": round(w.nbytes / dt / 1e9, 1)}
+    out["gemv_only"] = gemv
+    # configs[0]: gemma-3-1b Q4_0, --predict 64, on the CPU
+    c1 = CONFIGS["gemma-3-1b"]
+    g1 = build_gemma3_gguf(c1, seed=1234)
+    kind1, eng1 = engine(threads)
+    m1 = model(eng1, kind1, g1, threads)
+    lg = m1.forward(np.array(prompt, np.int32), 0)
     tok, pos = int(np.argmax(lg)), len(prompt)
     t0 = time.perf_counter()
-    for _ in range(n_decode):
-        lg = m.forward(np.array([tok], np.int32), pos)
+    for _ in range(63):  # 64 tokens emitted = 63 forwards after the prompt (main.cpp:169-234)
+        lg = m1.forward(np.array([tok], np.int32), pos)
         tok, pos = int(np.argmax(lg)), pos + 1
     dt = time.perf_counter() - t0
-    del m
-    return {"value": n_decode / dt, "unit": "tokens/s", "cores": threads, "kind": kind,
-            "sample": f"{cfg.name} Q4_0 synthetic GGUF, {len(prompt)}-token prompt then {n_decode} greedy decode "
-                      f"tokens via Model::forward (short context: CPU attention cost at pos 512+ not included)"}
+    del m1
+    out["configs0_gemma3_1b_predict64"] = {"value": round(63 / dt, 3), "unit": "tokens/s", "threads": threads,
+                                           "kind": kind1}
+    return out
 
 
 def main():
@@ -175,19 +274,50 @@ def main():
     value = a.steps * (1 if tp else d.world) / el
     ms = el * 1000.0 / a.steps
 
-    # dominant kernel: the Q4_0 GEMV family (weights swept in decode order, HIP events)
-    us, by = m.time_kernel(0, a.kernel_reps)
+    # Per-family kernel time of the timed graph: every family relaunched with
+    # its decode-step arguments, one launch per layer in decode order, each
+    # timed by events its own dispatch signals (Model.time_kernel); the
+    # dominant family by time per token is the roofline kernel.  The attention
+    # block reads the KV history at the position the decode loop ended on.
+    L = info.n_layer
+    fams = {}
+    for name, which, per_tok, kern in (("attention_block", 0, L, "attn_block_kernel"),
+                                       ("gate_up", 3, L, "gemv_q4_0_layer"),
+                                       ("down", 4, L, "gemv_q4_0_layer"),
+                                       ("token_selection", 2, 1, "screen_gemv_kernel")):
+        if which == 2 and not info.screened_logits:
+            continue
+        us_f, by_f = m.time_kernel(which, a.kernel_reps if which != 2 else 8)
+        if us_f <= 0:
+            continue
+        fams[name] = {"us_per_launch": round(us_f, 3), "launches_per_token": per_tok,
+                      "us_per_token": round(us_f * per_tok, 1), "bytes_per_launch": int(by_f),
+                      "GBps": round(by_f / (us_f * 1e-6) / 1e9, 1),
+                      "frac": round(by_f / (us_f * 1e-6) / 1e9 / PEAK_HBM_GBS, 4), "kernel": kern}
     us_l, by_l = m.time_kernel(1, 2)
-    us_s, by_s = m.time_kernel(2, 8) if info.screened_logits else (0.0, 0.0)
-    traffic, traffic_src = pmc_traffic()
-    ach = by / (us * 1e-6) / 1e9
-    mean_ctx = pos + a.steps / 2
+    dom_name = max(fams, key=lambda k: fams[k]["us_per_token"]) if fams else None
+    dom = fams.get(dom_name, {})
+    kpat = {"attention_block": "attn_block_kernel", "gate_up": "gemv_q4_0_layer<8, 10, 10",
+            "down": "gemv_q4_0_layer<1, 10, 5", "token_selection": "screen_gemv_kernel"}.get(dom_name, "-")
+    traffic, traffic_src = pmc_traffic(kpat)
+    mean_ctx = pos - a.steps / 2
     tok_bytes = info.bytes_per_token + info.kv_bytes_per_pos * mean_ctx
     if info.screened_logits:  # the decode loop streams the int8 screening table instead of the F16 one
         tok_bytes += info.screen_bytes - info.vocab * info.n_embd * 2
+    # BASELINE.json / SURVEY 8(d) definition: every linear weight + the F16
+    # logits table + KV read per token (4B: 3147.4 MB + 139.3 KB x L)
+    base_bytes = info.bytes_per_token + info.kv_bytes_per_pos * mean_ctx
+    per_gpu = 1 if tp else d.world
+    qname = {"q4_0": "Q4_0", "q4_k_m": "Q4_K_M", "q8_0": "Q8_0"}[a.quant]
+    base_cfg = {("gemma-3-4b", "q4_0"): "configs[2]", ("gemma-3-1b", "q4_0"): "configs[1]",
+                ("gemma-3-4b", "q4_k_m"): "configs[3]", ("gemma-3-1b", "q8_0"): "configs[3]",
+                ("gemma-3-27b", "q4_0"): "configs[4]"}.get((a.config, a.quant), "not a BASELINE config")
+    dtypes = {"q4_0": "q4_0 x q8_0 int8 dot, fp32 accumulate", "q8_0": "q8_0 x q8_0 int8 dot, fp32 accumulate",
+              "q4_k_m": "q4_k/q6_k x q8_k int8 dot, fp32 accumulate"}[a.quant]
     out = {
-        "metric": ("decode tokens/sec (Gemma-3 4B Q4_0 shape, greedy)" if (a.config, a.quant) == ("gemma-3-4b", "q4_0")
-                   else f"decode tokens/sec ({cfg.name} {a.quant} shape, greedy)"),
+        "metric": ("decode tokens/sec + achieved HBM GB/s vs roofline, Gemma-3 4B Q4_0"  # BASELINE.json
+                   if (a.config, a.quant) == ("gemma-3-4b", "q4_0") else
+                   f"decode tokens/sec + achieved HBM GB/s vs roofline, Gemma-3 {cfg.name.split('-')[-1].upper()} {qname}"),
         "value": round(value, 3),
         "unit": "tokens/s",
         "n_gpus": d.world,
@@ -196,11 +326,14 @@ def main():
         "ms_per_step": round(ms, 4),
         "higher_is_better": True,
         "scaling": "strong" if tp else "weak",
+        # BASELINE.md's only published figure is a 1B CPU number on unstated
+        # hardware, not this metric: no ratio is claimed
         "vs_baseline": None,
-        "dtype": "q4_0 x q8_0 int8-dot, fp32 accumulate; f16 logits",
-        "data": "synthetic (random-init weights of the gemma-3-4b-it-q4_0 architecture, seeded prompt ids)",
+        "dtype": dtypes + ("; exact (reference operation order)" if a.exact else "") + "; f16 logits table",
+        "data": f"synthetic (random-init weights of the {cfg.name}-it {qname} architecture, seeded prompt ids)",
         "config": {
-            "workload": f"{cfg.name}-{a.quant} greedy decode after a {a.prefill}-token prefill (BASELINE configs[2])",
+            "workload": f"{cfg.name}-{a.quant} greedy decode after a {a.prefill}-token prefill "
+                        f"(BASELINE {base_cfg})",
             "prefill_tokens": a.prefill, "decode_tokens": a.steps, "mode": "exact" if a.exact else "fast",
             "parallelism": (f"tp{d.world} (row-sharded, RCCL all-gather)" if tp else f"replicas{d.world}")
                            if d.world > 1 else "single",
@@ -208,30 +341,40 @@ def main():
         },
         "hbm": {
             "bytes_per_token": int(tok_bytes),
-            # per GPU: this rank's bytes of one token x tokens/s of its stream
-            "achieved_GBps": round(tok_bytes * value / (1 if tp else d.world) / 1e9, 1),
-            "frac_of_peak": round(tok_bytes * value / (1 if tp else d.world) / 1e9 / PEAK_HBM_GBS, 4),
+            "bytes_definition": "bytes the decode loop streams: weights + KV at the mean position + int8 screening table",
+            "achieved_GBps": round(tok_bytes * value / per_gpu / 1e9, 1),
+            "frac_of_peak": round(tok_bytes * value / per_gpu / 1e9 / PEAK_HBM_GBS, 4),
+            "baseline_bytes_per_token": int(base_bytes),
+            "baseline_definition": "BASELINE/SURVEY 8(d): weights + full F16 logits table + KV at the mean position",
+            "baseline_achieved_GBps": round(base_bytes * value / per_gpu / 1e9, 1),
+            "baseline_frac_of_peak": round(base_bytes * value / per_gpu / 1e9 / PEAK_HBM_GBS, 4),
         },
-        "roofline": {
-            "kernel": "Q4_0 projection GEMVs of one token in decode order (gemv_q4_0_layer on the fast path: qkv, o, gate_up+GELU, down)",
-            "bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-            "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": traffic, "traffic_unit": "bytes per launch",
+        "roofline": ({
+            "kernel": f"{dom_name}: the dominant kernel of the timed decode graph by time per token",
+            "bound": "hbm", "achieved": dom["GBps"], "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": dom["frac"], "traffic": traffic, "traffic_unit": "HBM bytes per launch (FETCH_SIZE x2)",
             "traffic_source": traffic_src,
-            "us_per_launch": round(us, 3), "bytes_per_launch": int(by),
-        },
+            "us_per_launch": dom["us_per_launch"], "bytes_per_launch": dom["bytes_per_launch"],
+            "position": pos,
+        } if dom else None),
+        "kernel_families": fams,
         "logits_gemv": {"us": round(us_l, 2), "GBps": round(by_l / (us_l * 1e-6) / 1e9, 1)},
-        "token_selection": ({"mode": "int8 screening + exact f16 rescoring of the candidates (ids = full F16 GEMV argmax)",
-                             "us": round(us_s, 2), "bytes": int(by_s),
-                             "GBps": round(by_s / (us_s * 1e-6) / 1e9, 1) if us_s else None}
-                            if info.screened_logits else {"mode": "full F16 logits GEMV + argmax"}),
+        "token_selection_mode": ("int8 screening + exact f16 rescoring of the candidates (ids = full F16 GEMV argmax)"
+                                 if info.screened_logits else "full F16 logits GEMV + argmax"),
         "timing_detail": {"synthetic_build_s": round(t_build, 1), "prefill_s": round(t_prefill, 4),
                           "prefill_tokens_per_s": round(a.prefill / t_prefill, 1),
                           "prefill_mode": "batched int8-MFMA" if info.batched_prefill else "token loop"},
     }
+    gpu_ids = None
+    if d.rank == 0 and d.world == 1 and not a.no_cpu_baseline:
+        # the CPU sample's prompt on the GPU too: the same greedy ids?
+        cp = np.array([2] + list(range(100, 107)), np.int32)
+        lg = m.forward(cp, 0, want_logits=False)
+        gpu_ids = [m.last_argmax] + m.generate(m.last_argmax, len(cp), a.cpu_decode).tolist()
     if d.rank == 0 and d.world == 1 and not a.no_cpu_baseline:
         m.close()
         try:
-            out["cpu_baseline"] = cpu_baseline(g, cfg, a.cpu_decode)
+            out["cpu_baseline"] = cpu_baseline(g, cfg, a.cpu_decode, gpu_ids, mean_ctx)
         except Exception as e:  # report, never hide
             out["cpu_baseline"] = {"error": repr(e)}
     if d.rank == 0:

@@ -10,8 +10,9 @@
  *  (1) ops.h drop-in (host buffers, synchronous: results are complete on
  *      return, like the reference's fork/join GEMVs, ops.cpp:450).  One entry
  *      point per reference function; the reference line each one replaces is
- *      cited.  The C++ overloads with the reference's exact signatures live in
- *      include/llmi_ops_compat.h (INTEGRATION.md shows the Bazel wiring).
+ *      cited.  The C++ functions with the reference's exact ops.h signatures
+ *      are integration/ops_mi355x.cpp, built in place of ops.cpp
+ *      (INTEGRATION.md shows the Bazel wiring).
  *  (2) device session: the whole Gemma-3 forward of Model::forward
  *      (model.cpp:706-1049) resident on one MI355X, weights uploaded once from
  *      the caller's GGUF bytes (the GGUF loader/format is unchanged), each
@@ -193,11 +194,16 @@ typedef struct {
 } llmi_session_info;
 int llmi_session_get_info(const llmi_session* s, llmi_session_info* info);
 
-/* Benchmark hook: time `reps` launches of the session's dominant kernel
- * family (0 = Q4_0/Q8_0 GEMV over every layer's weights in decode order,
- * 1 = F16 logits GEMV, 2 = the decode loop's screened token selection) with
- * HIP events on the session stream.  Returns the
- * mean microseconds per launch and the mean algorithmic bytes per launch. */
+/* Benchmark hook: time `reps` passes over one decode kernel family, every
+ * launch with the real arguments of the decode step and bracketed by HIP
+ * events its own dispatch signals, on the session stream:
+ *   0 = attention block (qkv + attention + o, one launch per layer; KV
+ *       history read at the session's current position),
+ *   1 = F16 logits GEMV, 2 = the decode loop's screened token selection,
+ *   3 = gate_up (+ norm prologue + GELU), 4 = down (+ Q8_0 prologue),
+ *   5 = qkv / o / gate_up / down as standalone layer GEMVs (round-1 family).
+ * Returns the mean microseconds and the mean algorithmic bytes per launch
+ * (0 / 0 when the family does not exist on this session). */
 int llmi_session_time_kernel(llmi_session* s, int which, int reps, double* us_per_launch, double* bytes_per_launch);
 
 #ifdef __cplusplus

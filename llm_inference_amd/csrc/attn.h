@@ -53,5 +53,6 @@ void launch_attention(const AttnArgs& a, bool exact, hipStream_t s, const QKVArg
 bool attn_block_supported(const DevWeight& wqkv, const DevWeight& wo, int head_dim, int n_head, int n_head_kv);
 void launch_attn_block(const DevWeight& wqkv, LayerGemv qg, int qrole, const DevWeight& wo, LayerGemv og,
                        const AttnArgs& aa, const QKVArgs& qa, BlockSync bs, hipStream_t s);
+void launch_bump_epoch(unsigned* epoch, hipStream_t s);
 
 }  // namespace llmi

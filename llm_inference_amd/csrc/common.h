@@ -70,12 +70,15 @@ __device__ __forceinline__ int nearest_int_fma(float a, float b) {
 }
 
 // GELU(tanh)(x) * u (model.cpp:892-899; no contraction in the reference's
-// build of this expression), with glibc's own tanhf (glibc_math.h): bit-exact
-// with the reference for the same gate/up inputs
+// build of this expression).  EXACT: glibc's own tanhf (glibc_math.h),
+// bit-exact with the reference for the same gate/up inputs; fast: the device
+// libm's tanhf (ulp-level differences; glibc's correctly-rounded divisions
+// cost the fused gate_up epilogue 0.6 us per launch, A/B in DESIGN.md)
+template <bool EXACT = false>
 __device__ __forceinline__ float gelu_mul1(float x, float u) {
   const float c = __uint_as_float(0x3F4C4229u);  // sqrtf((float)(2.0 / M_PI)) = 0.79788452f
   const float inner = x + ((0.044715f * x) * x) * x;
-  return ((0.5f * x) * (1.0f + llmi_glibc::tanhf(c * inner))) * u;
+  return ((0.5f * x) * (1.0f + (EXACT ? llmi_glibc::tanhf(c * inner) : tanhf(c * inner)))) * u;
 }
 
 __device__ __forceinline__ int sdot4(int a, int b, int c) { return __builtin_amdgcn_sdot4(a, b, c, false); }

@@ -204,7 +204,7 @@ void launch_vec_mad_f16(uint16_t* y, const uint16_t* x, int n, float v, hipStrea
 
 __global__ void gelu_mul_kernel(const float* g, const float* u, float* o, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) o[i] = gelu_mul1(g[i], u[i]);
+  if (i < n) o[i] = gelu_mul1<true>(g[i], u[i]);
 }
 void launch_gelu_mul(const float* g, const float* u, float* o, int n, hipStream_t s) {
   hipLaunchKernelGGL(gelu_mul_kernel, dim3((n + 255) / 256), dim3(256), 0, s, g, u, o, n);

@@ -279,13 +279,14 @@ __global__ __launch_bounds__(1024) void embed_norm_kernel(uint32_t type, const u
 // ---------------------------------------------------------------------------
 // GELU(tanh)(gate) * up (model.cpp:892-899) fused with quantize_row_q8_0 of the
 // result (ops.cpp:116-139) for the down projection: one 32-lane half-wave per
-// Q8_0 block.  Also writes the f32 hidden vector (parity/debug).
+// Q8_0 block.  Also writes the f32 hidden vector (parity/debug).  Bit-exact
+// GELU (glibc tanhf): this launch serves exact mode and the ops.h surface.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void gelu_quant_kernel(const float* __restrict__ gu, int n, float* __restrict__ hid,
                                                          XBlock* __restrict__ xb) {
   const int gl = blockIdx.x * blockDim.x + threadIdx.x;
   const bool ok = gl < n;
-  const float v = ok ? gelu_mul1(gu[gl], gu[n + gl]) : 0.0f;
+  const float v = ok ? gelu_mul1<true>(gu[gl], gu[n + gl]) : 0.0f;  // the unfused / exact path: glibc tanhf
   if (ok) hid[gl] = v;
   if (xb != nullptr) q8_block_store(v, ok && (gl >> 5) < n / 32, xb + (ok ? (gl >> 5) : 0), gl & 31);
 }

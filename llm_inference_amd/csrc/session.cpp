@@ -7,6 +7,7 @@
 #include "session.h"
 
 #include <cmath>
+#include <functional>
 #include <cstdio>
 #include <cstring>
 
@@ -1170,6 +1171,31 @@ void Session::info(llmi_session_info* o) const {
 }
 
 void Session::time_kernel(int which, int reps, double* us, double* bytes) {
+  if (which == 1) {  // F16 logits GEMV (forward's full logits)
+    *us = *bytes = 0.0;
+    if (reps <= 0) return;
+    std::vector<hipEvent_t> ev(2 * (size_t)reps);
+    for (auto& e : ev) LLMI_HIP(hipEventCreate(&e));
+    LLMI_HIP(hipStreamSynchronize(stream_));
+    for (int r = 0; r < reps; r++) {
+      LLMI_HIP(hipEventRecord(ev[2 * r], stream_));
+      launch_gemv(logits_w_, act_, logits_, exact_ ? GEMV_EXACT : GEMV_FAST, stream_, amax_key_);
+      LLMI_HIP(hipEventRecord(ev[2 * r + 1], stream_));
+    }
+    LLMI_HIP(hipStreamSynchronize(stream_));
+    double tot = 0;
+    for (int r = 0; r < reps; r++) {
+      float ms = 0;
+      LLMI_HIP(hipEventElapsedTime(&ms, ev[2 * r], ev[2 * r + 1]));
+      tot += ms;
+    }
+    for (auto& e : ev) (void)hipEventDestroy(e);
+    *us = tot * 1000.0 / reps;
+    *bytes = (double)logits_w_.bytes;
+    LLMI_HIP(hipMemsetAsync(amax_key_, 0, 8 * (size_t)tp_size_, stream_));
+    LLMI_HIP(hipStreamSynchronize(stream_));
+    return;
+  }
   if (which == 2) {  // the decode loop's token selection: prep + screening GEMV + rescoring
     *us = *bytes = 0.0;
     if (!screen_ || reps <= 0) return;
@@ -1195,87 +1221,107 @@ void Session::time_kernel(int which, int reps, double* us, double* bytes) {
     LLMI_HIP(hipStreamSynchronize(stream_));
     return;
   }
-  // launches of the dominant kernel family, each bracketed by its own event
-  // pair on the session stream (torch.cuda.Event would only see torch's
-  // stream), weights swept in decode order so every launch streams from HBM
-  std::vector<const DevWeight*> ws;
+  // launches of one decode kernel family, each bracketed by events that its
+  // own dispatch signals (hipExtLaunchKernel: the kernel's duration as
+  // rocprofv3 reports it, no launch gap), on the session stream
+  // (torch.cuda.Event would only see torch's stream), layers in decode order
+  // so every launch streams its own weights from HBM.  Real arguments; the
+  // prologues' residual writes go to a scratch buffer.
+  //   0: attention block (qkv + attention + o; KV history at the current pos)
+  //   3: gate_up (prologue + GELU)   4: down (QUANT)
+  //   5: the r01 family: qkv PRO, o PLAIN, gate_up, down as standalone launches
   bool fused = fuse_layers_;
   for (const auto& l : L_) fused &= l.fused;
-  // the fused path's launches (gemv_q4_0_layer) with their real arguments,
-  // except that the prologue's residual write goes to a scratch buffer
-  std::vector<std::pair<LayerGemv, int>> fl;  // (args, LayerRole)
-  if (which == 0 && fused) {
-    for (size_t i = 0; i < L_.size(); i++) {
-      const LayerDev& Ld = L_[i];
-      LayerGemv q;
-      q.y = d_out_;
-      q.w_post = i ? L_[i - 1].post_ffw_norm : Ld.post_ffw_norm;
-      q.resid_in = resid_;
-      q.resid_out = resid_scratch_;
-      q.w_next = Ld.attn_norm;
-      q.eps = hp_.eps;
-      q.out = qkv_;
-      fl.push_back({q, LAYER_PRO});
-      ws.push_back(&Ld.qkv[0].w);
+  if (!fused || (which == 0 && !block_) || which < 0 || which > 5 || reps <= 0) {
+    *us = *bytes = 0.0;
+    return;
+  }
+  LLMI_HIP(hipStreamSynchronize(stream_));
+  int pos = 0;
+  LLMI_HIP(hipMemcpy(&pos, d_pos_, 4, hipMemcpyDeviceToHost));
+  struct Item {
+    std::function<void()> launch;
+    double bytes;
+  };
+  std::vector<Item> items;
+  for (size_t i = 0; i < L_.size(); i++) {
+    LayerDev& Ld = L_[i];
+    const int hd = Ld.hd;
+    LayerGemv q;
+    q.y = d_out_;
+    q.w_post = i ? L_[i - 1].post_ffw_norm : Ld.post_ffw_norm;
+    q.resid_in = resid_;
+    q.resid_out = resid_scratch_;
+    q.w_next = Ld.attn_norm;
+    q.eps = hp_.eps;
+    q.out = qkv_;
+    if (which == 0) {
+      const double kv = 2.0 * nkv_ * hd * 2.0 * (pos + 1);
+      items.push_back({[this, &Ld, q, hd, i]() {
+                         QKVArgs qa{qkv_, Ld.k_off, Ld.v_off, nh_, nkv_, hd, Ld.q_norm, Ld.k_norm,
+                                    Ld.is_swa ? rope_swa_ : rope_glb_, hp_.attn_scale, hp_.eps, q_, Ld.kc, Ld.vc,
+                                    max_ctx_, d_pos_};
+                         AttnArgs aa{q_, Ld.kc, Ld.vc, nh_, nkv_, hd, max_ctx_, d_pos_, part_, attn_, ticket_, blk_xo_};
+                         LayerGemv go;
+                         go.xg = blk_xo_;
+                         go.out = o_out_;
+                         BlockSync bs;
+                         bs.epoch = blk_epoch_ + i;
+                         bs.g_qkv = blk_gqkv_ + i * blk_gqkv_stride_;
+                         bs.g_xo = blk_gxo_ + i * blk_gxo_stride_;
+                         bs.err = blk_err_;
+                         launch_attn_block(Ld.qkv[0].w, q, LAYER_PRO, Ld.o.w, go, aa, qa, bs, stream_);
+                       },
+                       (double)Ld.qkv[0].w.bytes + (double)Ld.o.w.bytes + kv});
+    }
+    if (which == 5) {
+      items.push_back({[this, &Ld, q]() { launch_layer_gemv(Ld.qkv[0].w, q, LAYER_PRO, stream_); },
+                       (double)Ld.qkv[0].w.bytes});
       LayerGemv o;
       o.xg = act_.q8.xb;
       o.out = o_out_;
-      fl.push_back({o, LAYER_PLAIN});
-      ws.push_back(&Ld.o.w);
+      items.push_back({[this, &Ld, o]() { launch_layer_gemv(Ld.o.w, o, LAYER_PLAIN, stream_); }, (double)Ld.o.w.bytes});
+    }
+    if (which == 3 || which == 5) {
       LayerGemv gu = q;
       gu.w_next = Ld.ffn_norm;
       gu.out = nullptr;
       gu.hid = hid_;
-      fl.push_back({gu, LAYER_GELU});
-      ws.push_back(&Ld.gate_up[0].w);
+      items.push_back({[this, &Ld, gu]() { launch_layer_gemv(Ld.gate_up[0].w, gu, LAYER_GELU, stream_); },
+                       (double)Ld.gate_up[0].w.bytes});
+    }
+    if (which == 4 || which == 5) {
       LayerGemv d;
       d.y = hid_;
       d.out = d_out_;
-      fl.push_back({d, LAYER_QUANT});
-      ws.push_back(&Ld.down.w);
+      items.push_back({[this, &Ld, d]() { launch_layer_gemv(Ld.down.w, d, LAYER_QUANT, stream_); },
+                       (double)Ld.down.w.bytes});
     }
-  } else if (which == 0) {
-    for (const auto& l : L_) {
-      for (const auto& p : l.qkv) ws.push_back(&p.w);
-      ws.push_back(&l.o.w);
-      for (const auto& p : l.gate_up) ws.push_back(&p.w);
-      ws.push_back(&l.down.w);
-    }
-  } else {
-    ws.push_back(&logits_w_);
   }
-  std::vector<hipEvent_t> ev(2 * ws.size() * reps);
+  std::vector<hipEvent_t> ev(2 * items.size() * reps);
   for (auto& e : ev) LLMI_HIP(hipEventCreate(&e));
-  LLMI_HIP(hipStreamSynchronize(stream_));
   size_t k = 0;
   double tot_bytes = 0;
   for (int r = 0; r < reps; r++)
-    for (size_t j = 0; j < ws.size(); j++) {
-      const DevWeight* w = ws[j];
-      if (!fl.empty()) {  // dispatch-signalled events: the kernel's own duration (= rocprofv3's)
-        kernel_timing() = KernelTiming{ev[k], ev[k + 1]};
-        k += 2;
-        launch_layer_gemv(*w, fl[j].first, fl[j].second, stream_);
-      } else {
-        LLMI_HIP(hipEventRecord(ev[k++], stream_));
-        launch_gemv(*w, act_, (w == &logits_w_ || w->rows > 2 * hp_.n_ff) ? logits_ : gu_,
-                    exact_ ? GEMV_EXACT : GEMV_FAST, stream_, w == &logits_w_ ? amax_key_ : nullptr);
-        LLMI_HIP(hipEventRecord(ev[k++], stream_));
-      }
-      tot_bytes += (double)w->bytes;
+    for (size_t j = 0; j < items.size(); j++) {
+      if (which == 0) launch_bump_epoch(blk_epoch_ + j, stream_);  // fresh granule tags: every hand-off waits
+      kernel_timing() = KernelTiming{ev[k], ev[k + 1]};
+      k += 2;
+      items[j].launch();
+      tot_bytes += items[j].bytes;
     }
   LLMI_HIP(hipStreamSynchronize(stream_));
+  check_device_error();
   double tot_ms = 0;
-  for (size_t i = 0; i < k; i += 2) {
+  for (size_t e = 0; e < k; e += 2) {
     float ms = 0;
-    LLMI_HIP(hipEventElapsedTime(&ms, ev[i], ev[i + 1]));
+    LLMI_HIP(hipEventElapsedTime(&ms, ev[e], ev[e + 1]));
     tot_ms += ms;
   }
   for (auto& e : ev) (void)hipEventDestroy(e);
   const double n = (double)(k / 2);
   *us = tot_ms * 1000.0 / n;
   *bytes = tot_bytes / n;
-  // leave the argmax key clean for the next decode step
   LLMI_HIP(hipMemsetAsync(amax_key_, 0, 8 * (size_t)tp_size_, stream_));
   LLMI_HIP(hipStreamSynchronize(stream_));
 }

@@ -211,6 +211,10 @@ class Reference:
         L.ref_model_destroy.argtypes = [C.c_void_p]
         L.ref_model_tokenize.argtypes = [C.c_void_p, C.c_char_p, C.c_int, _i32p, C.c_int]
         L.ref_last_error.restype = C.c_char_p
+        L.ref_gemv_prepare.restype = C.c_void_p
+        L.ref_gemv_prepare.argtypes = [C.c_uint32, C.c_void_p, C.c_size_t, C.c_size_t, C.c_size_t]
+        L.ref_gemv_run.argtypes = [C.c_void_p, _f32p, C.c_void_p]
+        L.ref_gemv_free.argtypes = [C.c_void_p]
 
     def quantize_q8_0(self, x):
         x = np.ascontiguousarray(x, np.float32)
@@ -231,6 +235,23 @@ class Reference:
         if self.lib.ref_mat_vec_mul(ttype, _ptr(w), w.nbytes, n_rows, n_cols, x, o) != 0:
             raise RuntimeError(self.lib.ref_last_error().decode())
         return o
+
+    def time_gemv(self, ttype, w, n_rows, n_cols, x, reps):
+        """Mean seconds of the reference's mat_vec_mul (or mat_vec_mul_fp16 for
+        F16) on a weight prepared once (no per-call copies)."""
+        import time
+        w = np.ascontiguousarray(w)
+        h = self.lib.ref_gemv_prepare(ttype, _ptr(w), w.nbytes, n_rows, n_cols)
+        if not h:
+            raise RuntimeError(self.lib.ref_last_error().decode())
+        x = np.ascontiguousarray(x, np.float32)
+        self.lib.ref_gemv_run(h, x, None)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            self.lib.ref_gemv_run(h, x, None)
+        dt = (time.perf_counter() - t0) / reps
+        self.lib.ref_gemv_free(h)
+        return dt
 
     def dequantize_row(self, ttype, blocks, n_cols):
         o = np.zeros(n_cols, np.float32)

@@ -93,6 +93,55 @@ int ref_mat_vec_mul(uint32_t type, const void* w, size_t w_bytes, size_t n_rows,
   }
 }
 
+// A prepared GEMV for timing the reference's kernels alone (the bench's
+// GEMV-only CPU baseline): the one-tensor GGUF (or the F16 vector) is built
+// once, then ref_gemv_run calls mat_vec_mul / mat_vec_mul_fp16 on it.
+struct RefGemv {
+  uint32_t type;
+  size_t rows, cols;
+  std::vector<uint8_t> buf;
+  GGUFFile* f = nullptr;
+  std::vector<uint16_t> w16;
+  std::vector<float> x, o;
+};
+
+void* ref_gemv_prepare(uint32_t type, const void* w, size_t w_bytes, size_t n_rows, size_t n_cols) {
+  try {
+    auto* g = new RefGemv{type, n_rows, n_cols};
+    if (type == (uint32_t)GGUFTensorType::F16) {
+      g->w16.assign((const uint16_t*)w, (const uint16_t*)w + n_rows * n_cols);
+    } else {
+      g->buf = one_tensor_gguf(type, w, w_bytes, n_cols, n_rows);
+      g->f = new GGUFFile(g->buf.data(), g->buf.size());
+    }
+    g->x.resize(n_cols);
+    return g;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return nullptr;
+  }
+}
+
+int ref_gemv_run(void* h, const float* x, float* o) {
+  auto* g = (RefGemv*)h;
+  try {
+    memcpy(g->x.data(), x, g->cols * sizeof(float));
+    if (g->f) mat_vec_mul(g->o, g->f->get_tensor_infos()[0], *g->f, g->x);
+    else mat_vec_mul_fp16(g->o, g->w16, g->x, g->rows, g->cols);
+    if (o) memcpy(o, g->o.data(), g->rows * sizeof(float));
+    return 0;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return -1;
+  }
+}
+
+void ref_gemv_free(void* h) {
+  auto* g = (RefGemv*)h;
+  delete g->f;
+  delete g;
+}
+
 int ref_dequantize_row(uint32_t type, const void* blocks, size_t n_cols, float* o) {
   std::vector<float> ov;
   const uint8_t* p = (const uint8_t*)blocks;

@@ -16,7 +16,7 @@ Tolerances (per tensor, why):
                      exact; only the f32 sum of nb block terms is reassociated
                      (nb * 2^-24 relative to the term magnitude, far below).
   norms / residuals  rtol 2e-6 of max: the squared-sum tree vs the serial fmaf chain.
-  attention          vs the float64 restatement 2e-5 of max (fp32 split-K);
+  attention          vs the float64 restatement 2e-5 of max x sqrt(keys / 256) (fp32 split-K);
                      vs the reference's f16-accumulator algorithm: that algorithm's
                      own drift from exact math (measured on the same inputs) + 4e-5.
   Q8_0 blocks        bit-identical (same floats in, ops.cpp:116-139 exactly).
@@ -145,7 +145,8 @@ class OpChecker:
         got = attn_dev.reshape(nh, hd)
         ref64 = np.stack([self.orc.attn_head_f64(qr[h], kc[h // g, : pos + 1], vc[h // g, : pos + 1]) for h in range(nh)])
         refr = np.stack([self.orc.attn_head(qr[h], kc[h // g, : pos + 1], vc[h // g, : pos + 1]) for h in range(nh)])
-        self.note("attention_vs_f64", rel_err(got, ref64), ATTN_F64_RTOL)
+        # fp32 split-K sums: rounding grows like sqrt(keys) (2e-5 up to 256 keys)
+        self.note("attention_vs_f64", rel_err(got, ref64), ATTN_F64_RTOL * math.sqrt(max(1.0, (pos + 1) / 256.0)))
         # the reference's own f16 V accumulator drifts from exact math with the
         # key count (~1e-3 at 256 keys, ~7e-3 at 1100): the fast path may differ
         # from it by that drift plus its own distance to exact math
