@@ -627,7 +627,11 @@ void Session::ensure_prefill_buffers(int cap) {
 void Session::prefill(const int32_t* tokens, int n, int pos) {
   hipStream_t s = stream_;
   const int E = hp_.n_embd, F = hp_.n_ff;
-  int chunk = 256;
+  // 512 tokens per chunk: the prefill GEMMs' weight tiles are re-read once per
+  // 64-token tile, their activation tiles once per 64-row tile, and a longer
+  // chunk fills the chip with more work-groups (4B, 512-token prompt: 21.4 ms
+  // at 256-token chunks, 17.4 ms at 512)
+  int chunk = 512;
   if (const char* c = getenv("LLMI_PREFILL_CHUNK")) chunk = std::max(1, atoi(c));
   ensure_prefill_buffers(std::min(chunk, n));
   const int XS = pf_xs_;
