@@ -125,7 +125,8 @@ def random_tensor(ttype: int, n_rows: int, n_cols: int, seed: int = 0, **kw) -> 
 # ---------------------------------------------------------------------------
 def build_gemma3_gguf(cfg: Gemma3Config, seed: int = 0, wtype: int = TensorType.Q4_0,
                       embd_type: int = TensorType.F16, wtypes: Optional[Dict[str, int]] = None,
-                      swa_pattern: Optional[list] = None, centered: bool = False) -> np.ndarray:
+                      swa_pattern: Optional[list] = None, centered: bool = False,
+                      pieces: Optional[list] = None) -> np.ndarray:
     """Random-init Gemma-3 GGUF with the tensor names/shapes model.cpp maps
     (model.cpp:169-238).  Returns the whole file as a uint8 numpy array."""
     rng = np.random.default_rng(seed)
@@ -144,6 +145,8 @@ def build_gemma3_gguf(cfg: Gemma3Config, seed: int = 0, wtype: int = TensorType.
     if swa_pattern is not None:
         b.add_meta(f"{a}.attention.sliding_window_pattern", [bool(x) for x in swa_pattern])
     toks = ["<pad>", "<eos>", "<bos>", "<unk>"] + [f"t{i}" for i in range(4, cfg.vocab)]
+    for i, p in enumerate(pieces or []):  # real vocabulary pieces at ids 4.. (the tokenizer's greedy longest match)
+        toks[4 + i] = p
     b.add_meta("tokenizer.ggml.tokens", toks)
     b.add_meta("tokenizer.ggml.bos_token_id", 2)
     b.add_meta("tokenizer.ggml.eos_token_id", 1)

@@ -26,7 +26,7 @@ def build(ref: bool = True) -> None:
     """Compile the oracle (and, when the reference sources exist, _ref)."""
     # "dropin": the reference's model.cpp/gguf.cpp with integration/ops_mi355x.cpp
     # in place of ops.cpp (needs llm_inference_amd/libllmi.so built first)
-    targets = ["all"] + (["ref", "dropin"] if ref and os.path.isdir(REF_SRC) else [])
+    targets = ["all"] + (["ref", "dropin", "mainloop"] if ref and os.path.isdir(REF_SRC) else [])
     subprocess.run(["make", "-s", "-C", HERE] + targets, check=True)
 
 
