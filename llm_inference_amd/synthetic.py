@@ -187,6 +187,103 @@ def build_gemma3_gguf(cfg: Gemma3Config, seed: int = 0, wtype: int = TensorType.
     return buf
 
 
+@dataclass(frozen=True)
+class Gemma4Config:
+    """Gemma-4 structure the reference supports (model.cpp:58-167, 568-704,
+    706-980): per-layer token embeddings + their model projection, shared KV
+    for the last layers, V RMSNorm, per-layer output scale, attention scale 1,
+    separate sliding-window / global head dims."""
+    name: str
+    n_layer: int
+    n_embd: int
+    n_ff: int
+    n_head: int
+    n_head_kv: int
+    head_dim: int       # global layers (attention.key_length)
+    head_dim_swa: int   # sliding-window layers (attention.key_length_swa)
+    n_embd_per_layer: int
+    shared_kv_layers: int
+    vocab: int
+    rope_base: float = 1000000.0
+    eps: float = 1e-6
+
+
+CONFIGS4: Dict[str, Gemma4Config] = {
+    "tiny4": Gemma4Config("tiny4", 4, 256, 512, 4, 1, 128, 64, 64, 2, 512),
+    "mini4": Gemma4Config("mini4", 6, 1536, 6144, 8, 1, 256, 256, 256, 2, 4096),
+}
+
+
+def build_gemma4_gguf(cfg: Gemma4Config, seed: int = 0, wtype: int = TensorType.Q4_0,
+                      ple_type: int = TensorType.BF16, table_type: int = TensorType.F16,
+                      swa_pattern: Optional[list] = None, centered: bool = True) -> np.ndarray:
+    """Random-init GGUF with the reference's Gemma-4 tensor map
+    (model.cpp:169-238): token_embd_per_layer [n_embd_per_layer * n_layer,
+    vocab], per_layer_model_proj [n_embd -> n_embd_per_layer * n_layer],
+    per_layer_proj_norm; per layer inp_gate / proj (the per-layer embedding
+    step) and post_norm, out_scale; no attn_k / attn_v for the shared-KV
+    layers (model.cpp:775-777 never reads them)."""
+    rng = np.random.default_rng(seed)
+    b = GGUFBuilder(align_tensors=True)
+    a = "gemma4"
+    L, E, F, Ep = cfg.n_layer, cfg.n_embd, cfg.n_ff, cfg.n_embd_per_layer
+    pattern = swa_pattern if swa_pattern is not None else [(l % 6) < 5 for l in range(L)]
+    b.add_meta("general.architecture", a)
+    for k, v in (("block_count", L), ("embedding_length", E), ("feed_forward_length", F),
+                 ("attention.head_count", cfg.n_head), ("attention.head_count_kv", cfg.n_head_kv),
+                 ("attention.key_length", cfg.head_dim), ("attention.value_length", cfg.head_dim),
+                 ("attention.key_length_swa", cfg.head_dim_swa), ("attention.value_length_swa", cfg.head_dim_swa),
+                 ("embedding_length_per_layer_input", Ep), ("attention.shared_kv_layers", cfg.shared_kv_layers)):
+        b.add_meta(f"{a}.{k}", int(v))
+    b.add_meta(f"{a}.attention.layer_norm_rms_epsilon", float(cfg.eps))
+    b.add_meta(f"{a}.rope.freq_base", float(cfg.rope_base))
+    b.add_meta(f"{a}.attention.sliding_window_pattern", [bool(x) for x in pattern])
+    toks = ["<pad>", "<eos>", "<bos>", "<unk>"] + [f"t{i}" for i in range(4, cfg.vocab)]
+    b.add_meta("tokenizer.ggml.tokens", toks)
+    b.add_meta("tokenizer.ggml.bos_token_id", 2)
+    b.add_meta("tokenizer.ggml.eos_token_id", 1)
+    kv_from = L - cfg.shared_kv_layers
+    specs = [("token_embd.weight", [E, cfg.vocab], TensorType.F16),
+             ("output_norm.weight", [E], TensorType.F32),
+             ("per_layer_token_embd.weight", [Ep * L, cfg.vocab], table_type),
+             ("per_layer_model_proj.weight", [E, Ep * L], ple_type),
+             ("per_layer_proj_norm.weight", [Ep], TensorType.F32)]
+    for l in range(L):
+        p = f"blk.{l}."
+        hd = cfg.head_dim_swa if pattern[l] else cfg.head_dim
+        specs += [(p + "attn_norm.weight", [E], TensorType.F32),
+                  (p + "attn_q.weight", [E, cfg.n_head * hd], wtype)]
+        if l < kv_from:
+            specs += [(p + "attn_k.weight", [E, cfg.n_head_kv * hd], wtype),
+                      (p + "attn_v.weight", [E, cfg.n_head_kv * hd], wtype),
+                      (p + "attn_k_norm.weight", [hd], TensorType.F32)]
+        specs += [(p + "attn_q_norm.weight", [hd], TensorType.F32),
+                  (p + "attn_output.weight", [cfg.n_head * hd, E], wtype),
+                  (p + "post_attention_norm.weight", [E], TensorType.F32),
+                  (p + "ffn_norm.weight", [E], TensorType.F32),
+                  (p + "ffn_gate.weight", [E, F], wtype),
+                  (p + "ffn_up.weight", [E, F], wtype),
+                  (p + "ffn_down.weight", [F, E], wtype),
+                  (p + "post_ffw_norm.weight", [E], TensorType.F32),
+                  (p + "inp_gate.weight", [E, Ep], ple_type),
+                  (p + "proj.weight", [Ep, E], ple_type),
+                  (p + "post_norm.weight", [E], TensorType.F32),
+                  (p + "layer_output_scale.weight", [1], TensorType.F32)]
+    for name, shape, tt in specs:
+        b.add_tensor(name, shape, tt)
+    buf, views = b.finalize()
+    for name, shape, tt in specs:
+        v = views[name]
+        if name.endswith("layer_output_scale.weight"):
+            v.view(np.float32)[:] = rng.uniform(0.5, 1.0, size=1).astype(np.float32)
+        elif tt == TensorType.F32:
+            v.view(np.float32)[:] = rng.uniform(0.6, 1.4, size=v.size // 4).astype(np.float32)
+        else:
+            n_rows = shape[1] if len(shape) > 1 else 1
+            fill_random(v, tt, n_rows, shape[0], rng, centered=centered)
+    return buf
+
+
 def bytes_per_token(cfg: Gemma3Config, wtype: int = TensorType.Q4_0,
                     embd_type: int = TensorType.F16) -> Dict[str, int]:
     """Algorithmic HBM bytes of one decode token,

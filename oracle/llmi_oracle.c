@@ -610,6 +610,7 @@ static int skip_value(rdr* r, uint32_t type, gval* out) {
 #define ORC_MAX_LAYERS 128
 typedef struct {
   int attn_norm, q, k, v, o, q_norm, k_norm, post_attn_norm, ffn_norm, gate, up, down, post_ffw_norm;
+  int out_scale, ple_gate, ple_proj, ple_post_norm;  /* Gemma-4 (model.cpp:215-228) */
 } orc_layer;
 
 struct orc_model {
@@ -620,6 +621,8 @@ struct orc_model {
   int n_swa; uint8_t swa[ORC_MAX_LAYERS];
   orc_layer L[ORC_MAX_LAYERS];
   int tok_embd, out_norm, vocab;
+  int gemma4, n_epl, kv_from;                     /* model.cpp:117-166: per-layer embd width, shared-KV start */
+  int ple_table, ple_model_proj, ple_proj_norm;   /* model.cpp:181-188 */
   int n_threads, max_ctx, n_cached, attn_f64;
   uint16_t* kc[ORC_MAX_LAYERS]; uint16_t* vc[ORC_MAX_LAYERS];
 };
@@ -669,6 +672,9 @@ orc_model* orc_model_create(const uint8_t* g, size_t size, int n_threads, int ma
     else if (KEY("attention.value_length")) m->hd_v = (int)v.u32;
     else if (KEY("attention.value_length_swa")) m->hd_v_swa = (int)v.u32;
     else if (KEY("attention.logit_softcapping")) memcpy(&m->attn_softcap, &v.u32, 4);
+    else if (KEY("embedding_length_per_layer") || KEY("embedding_length_per_layer_input")) {
+      if (KEY("embedding_length_per_layer") || m->n_epl == 0) m->n_epl = (int)v.u32;  /* model.cpp:148-157 */
+    } else if (KEY("attention.shared_kv_layers")) m->kv_from = -(int)v.u32 - 2;   /* resolved below */
     else if (KEY("final_logit_softcapping") || KEY("attention.final_logit_softcapping")) {
       if (KEY("attention.final_logit_softcapping")) memcpy(&m->final_softcap, &v.u32, 4);
     } else if (KEY("attention.sliding_window_pattern") && ty == 9) {
@@ -688,12 +694,16 @@ orc_model* orc_model_create(const uint8_t* g, size_t size, int n_threads, int ma
   if (m->hd_v < 0) m->hd_v = m->hd_k;
   if (m->hd_v_swa < 0) m->hd_v_swa = m->hd_v;
   m->attn_scale = 1.0f / sqrtf((float)m->hd_k);
+  m->gemma4 = strcmp(arch, "gemma4") == 0;
+  if (m->gemma4) m->attn_scale = 1.0f;                       /* model.cpp:119-122 */
+  m->kv_from = m->kv_from <= -2 ? m->n_layer - (-m->kv_from - 2) : -1;  /* model.cpp:159-166 */
   if (m->hd_k != m->hd_v || m->hd_k_swa != m->hd_v_swa) {  /* run_attn dots over n_embd_head_v */
     ORC_FAIL("key_length != value_length is not supported"); free(m); return NULL;
   }
   /* tensor infos */
   m->t = (orc_tensor*)calloc(nt ? nt : 1, sizeof(orc_tensor)); m->nt = (int)nt;
   m->tok_embd = m->out_norm = -1;
+  m->ple_table = m->ple_model_proj = m->ple_proj_norm = -1;
   for (int l = 0; l < ORC_MAX_LAYERS; l++) memset(&m->L[l], 0xff, sizeof(orc_layer));
   for (uint64_t i = 0; i < nt && !r.err; i++) {
     orc_tensor* T = &m->t[i];
@@ -710,6 +720,9 @@ orc_model* orc_model_create(const uint8_t* g, size_t size, int n_threads, int ma
     const char* n = m->t[i].name;
     if (!strcmp(n, "token_embd.weight")) m->tok_embd = i;
     else if (!strcmp(n, "output_norm.weight")) m->out_norm = i;
+    else if (!strcmp(n, "token_embd_per_layer.weight") || !strcmp(n, "per_layer_token_embd.weight")) m->ple_table = i;
+    else if (!strcmp(n, "per_layer_model_proj.weight")) m->ple_model_proj = i;
+    else if (!strcmp(n, "per_layer_proj_norm.weight")) m->ple_proj_norm = i;
     else if (!strncmp(n, "blk.", 4)) {
       char* end; const long li = strtol(n + 4, &end, 10);
       if (*end != '.' || li < 0 || li >= m->n_layer) continue;
@@ -727,10 +740,21 @@ orc_model* orc_model_create(const uint8_t* g, size_t size, int n_threads, int ma
       else if (!strcmp(p, "post_ffw_norm.weight") || !strcmp(p, "ffn_post_norm.weight")) L->post_ffw_norm = i;
       else if (!strcmp(p, "attn_k_norm.weight")) L->k_norm = i;
       else if (!strcmp(p, "attn_q_norm.weight")) L->q_norm = i;
+      else if (!strcmp(p, "out_scale.weight") || !strcmp(p, "layer_output_scale.weight")) L->out_scale = i;
+      else if (!strcmp(p, "per_layer_inp_gate.weight") || !strcmp(p, "inp_gate.weight")) L->ple_gate = i;
+      else if (!strcmp(p, "per_layer_proj.weight") || !strcmp(p, "proj.weight")) L->ple_proj = i;
+      else if (!strcmp(p, "per_layer_post_norm.weight") || !strcmp(p, "post_norm.weight")) L->ple_post_norm = i;
     }
   }
   if (m->tok_embd < 0 || m->out_norm < 0) { ORC_FAIL("missing token_embd/output_norm"); orc_model_destroy(m); return NULL; }
   m->vocab = (int)m->t[m->tok_embd].shape[1];
+  /* shared KV (model.cpp:832-835): layer l >= kv_from reads kv_from-2 (SWA) or
+     kv_from-1 (global); the source must be of the same kind (same head dims) */
+  for (int l = m->kv_from < 0 ? m->n_layer : m->kv_from; l < m->n_layer; l++) {
+    const int sw = l < m->n_swa ? m->swa[l] : (l % 6 < 5), src = m->kv_from - (sw ? 2 : 1);
+    const int ssw = src >= 0 ? (src < m->n_swa ? m->swa[src] : (src % 6 < 5)) : -1;
+    if (ssw != sw) { ORC_FAIL("shared-KV layer %d reads layer %d of another attention kind", l, src); orc_model_destroy(m); return NULL; }
+  }
   for (int l = 0; l < m->n_layer; l++) {
     const int hd = m->hd_k > m->hd_k_swa ? m->hd_k : m->hd_k_swa;
     const int hv = m->hd_v > m->hd_v_swa ? m->hd_v : m->hd_v_swa;
@@ -778,9 +802,41 @@ int orc_model_forward(orc_model* m, const int* tokens, int T, int pos, float* lo
   size_t mx = (size_t)(m->n_ff > E ? m->n_ff : E);
   for (int l = 0; l < m->n_layer; l++) {
     const orc_layer* L = &m->L[l];
-    const size_t r[] = {m->t[L->q].shape[1], m->t[L->k].shape[1], m->t[L->v].shape[1], m->t[L->o].shape[1],
-                        m->t[L->gate].shape[1], m->t[L->down].shape[1]};
+    const size_t r[] = {m->t[L->q].shape[1], L->k >= 0 ? m->t[L->k].shape[1] : 0, L->v >= 0 ? m->t[L->v].shape[1] : 0,
+                        m->t[L->o].shape[1], m->t[L->gate].shape[1], m->t[L->down].shape[1]};
     for (int i = 0; i < 6; i++) if (r[i] > mx) mx = r[i];
+  }
+  /* Gemma-4 per-layer inputs (model.cpp:568-704): [T][n_layer][n_epl] */
+  const int NL = m->n_layer, EP = m->n_epl;
+  float* inp_pl = NULL;
+  if (m->ple_table >= 0) {
+    const orc_tensor* pt = &m->t[m->ple_table];
+    const size_t row_el = (size_t)EP * NL, row_b = orc_row_bytes(pt->type, row_el);
+    const float sc = sqrtf((float)EP);
+    inp_pl = (float*)malloc(sizeof(float) * T * row_el);
+    float* proj = (float*)malloc(sizeof(float) * row_el);
+    float* nx = (float*)malloc(sizeof(float) * EP);
+    for (int t = 0; t < T; t++) {
+      float* row = inp_pl + (size_t)t * row_el;
+      if (orc_dequantize_row(pt->type, tdata(m, m->ple_table) + (size_t)tokens[t] * row_b, row_el, row)) {
+        free(hs); free(inp_pl); free(proj); free(nx); return -1;
+      }
+      for (size_t i = 0; i < row_el; i++) row[i] *= sc;
+    }
+    if (m->ple_model_proj >= 0) {
+      const float ps = 1.0f / sqrtf((float)E), is = 1.0f / sqrtf(2.0f);
+      const float* nw = (const float*)tdata(m, m->ple_proj_norm);
+      for (int t = 0; t < T; t++) {
+        mm(m, m->ple_model_proj, hs + (size_t)t * E, proj);
+        for (size_t i = 0; i < row_el; i++) proj[i] *= ps;
+        for (int l = 0; l < NL; l++) {
+          orc_rms_norm(nx, proj + (size_t)l * EP, EP, (double)m->eps_f);
+          float* d = inp_pl + (size_t)t * row_el + (size_t)l * EP;
+          for (int i = 0; i < EP; i++) d[i] = (nx[i] * nw[i] + d[i]) * is;
+        }
+      }
+    }
+    free(proj); free(nx);
   }
   float* xn = (float*)malloc(sizeof(float) * mx);
   float* qv = (float*)malloc(sizeof(float) * T * mx);
@@ -798,26 +854,36 @@ int orc_model_forward(orc_model* m, const int* tokens, int T, int pos, float* lo
     const float base = is_swa ? 10000.0f : m->rope_base;
     const int hk = is_swa ? m->hd_k_swa : m->hd_k, hv = is_swa ? m->hd_v_swa : m->hd_v;
     const int H = m->n_head, HK = m->n_head_kv;
+    /* shared KV (model.cpp:775-777, 832-835): the last layers read an earlier layer's cache */
+    const int has_kv = m->kv_from < 0 || l < m->kv_from;
+    const int src = has_kv ? l : m->kv_from - (is_swa ? 2 : 1);
     for (int t = 0; t < T; t++) {
       norm_w(m, L->attn_norm, hs + t * E, xn, E);
       rc |= mm(m, L->q, xn, tmp); memcpy(qv + (size_t)t * H * hk, tmp, sizeof(float) * H * hk);
-      rc |= mm(m, L->k, xn, tmp); memcpy(kv + (size_t)t * HK * hk, tmp, sizeof(float) * HK * hk);
-      rc |= mm(m, L->v, xn, tmp); memcpy(vv + (size_t)t * HK * hv, tmp, sizeof(float) * HK * hv);
+      if (has_kv) {
+        rc |= mm(m, L->k, xn, tmp); memcpy(kv + (size_t)t * HK * hk, tmp, sizeof(float) * HK * hk);
+        rc |= mm(m, L->v, xn, tmp); memcpy(vv + (size_t)t * HK * hv, tmp, sizeof(float) * HK * hv);
+      }
     }
     /* per-head q/k norms (model.cpp:762,792), rope, q scale (model.cpp:767) */
     for (int t = 0; t < T; t++) {
       for (int h = 0; h < H; h++) { float* p = qv + ((size_t)t * H + h) * hk; norm_w(m, L->q_norm, p, tmp, hk); memcpy(p, tmp, 4 * hk); }
-      for (int h = 0; h < HK; h++) { float* p = kv + ((size_t)t * HK + h) * hk; norm_w(m, L->k_norm, p, tmp, hk); memcpy(p, tmp, 4 * hk); }
+      if (has_kv)
+        for (int h = 0; h < HK; h++) { float* p = kv + ((size_t)t * HK + h) * hk; norm_w(m, L->k_norm, p, tmp, hk); memcpy(p, tmp, 4 * hk); }
+      if (has_kv && m->gemma4)  /* V RMSNorm without weight (model.cpp:813-829) */
+        for (int h = 0; h < HK; h++) { float* p = vv + ((size_t)t * HK + h) * hv; orc_rms_norm(tmp, p, hv, (double)m->eps_f); memcpy(p, tmp, 4 * hv); }
     }
     orc_rope(qv, T, H, hk, hk, base, 1.0f, pos);
     orc_scale(qv, (size_t)T * H * hk, m->attn_scale);
-    orc_rope(kv, T, HK, hk, hk, base, 1.0f, pos);
-    /* KV append as f16 (model.cpp:442-474): cache [pos][kvh][hd] */
-    for (int t = 0; t < T; t++)
-      for (int h = 0; h < HK; h++) {
-        for (int i = 0; i < hk; i++) m->kc[l][((size_t)(pos + t) * HK + h) * hk + i] = orc_f32_to_f16(kv[((size_t)t * HK + h) * hk + i]);
-        for (int i = 0; i < hv; i++) m->vc[l][((size_t)(pos + t) * HK + h) * hv + i] = orc_f32_to_f16(vv[((size_t)t * HK + h) * hv + i]);
-      }
+    if (has_kv) {
+      orc_rope(kv, T, HK, hk, hk, base, 1.0f, pos);
+      /* KV append as f16 (model.cpp:442-474): cache [pos][kvh][hd] */
+      for (int t = 0; t < T; t++)
+        for (int h = 0; h < HK; h++) {
+          for (int i = 0; i < hk; i++) m->kc[l][((size_t)(pos + t) * HK + h) * hk + i] = orc_f32_to_f16(kv[((size_t)t * HK + h) * hk + i]);
+          for (int i = 0; i < hv; i++) m->vc[l][((size_t)(pos + t) * HK + h) * hv + i] = orc_f32_to_f16(vv[((size_t)t * HK + h) * hv + i]);
+        }
+    }
     /* attention (model.cpp:478-550): gather per-kv-head contiguous history */
     {
       const int nk_max = pos + T;
@@ -828,8 +894,8 @@ int orc_model_forward(orc_model* m, const int* tokens, int T, int pos, float* lo
           const int hkv = h / (H / HK);
           const int nk = pos + t + 1;
           for (int tk = 0; tk < nk; tk++) {
-            memcpy(kh + (size_t)tk * hk, &m->kc[l][((size_t)tk * HK + hkv) * hk], 2 * hk);
-            memcpy(vh + (size_t)tk * hv, &m->vc[l][((size_t)tk * HK + hkv) * hv], 2 * hv);
+            memcpy(kh + (size_t)tk * hk, &m->kc[src][((size_t)tk * HK + hkv) * hk], 2 * hk);
+            memcpy(vh + (size_t)tk * hv, &m->vc[src][((size_t)tk * HK + hkv) * hv], 2 * hv);
           }
           (m->attn_f64 ? orc_attn_head_f64 : orc_attn_head)(qv + ((size_t)t * H + h) * hk, kh, vh, nk, hv,
                                                             att + ((size_t)t * H + h) * hv);
@@ -850,6 +916,19 @@ int orc_model_forward(orc_model* m, const int* tokens, int T, int pos, float* lo
       rc |= mm(m, L->down, hb, tmp);
       if (L->post_ffw_norm >= 0) { norm_w(m, L->post_ffw_norm, tmp, xn, E); memcpy(tmp, xn, 4 * E); }
       for (int j = 0; j < E; j++) hs[t * E + j] += tmp[j];
+      if (inp_pl) {  /* per-layer embedding (model.cpp:926-966) */
+        float* h = hs + (size_t)t * E;
+        rc |= mm(m, L->ple_gate, h, g);
+        orc_gelu_mul(u, g, inp_pl + (size_t)t * EP * NL + (size_t)l * EP, EP);
+        rc |= mm(m, L->ple_proj, u, tmp);
+        orc_rms_norm(xn, tmp, E, (double)m->eps_f);
+        const float* pw = (const float*)tdata(m, L->ple_post_norm);
+        for (int j = 0; j < E; j++) h[j] += xn[j] * pw[j];
+      }
+      if (L->out_scale >= 0) {  /* layer output scale (model.cpp:968-977) */
+        const float os = *(const float*)tdata(m, L->out_scale);
+        for (int j = 0; j < E; j++) hs[t * E + j] *= os;
+      }
     }
   }
   if (rc == 0) {  /* final norm on last token + logits (model.cpp:983-1041) */
@@ -858,6 +937,6 @@ int orc_model_forward(orc_model* m, const int* tokens, int T, int pos, float* lo
     if (rc == 0 && m->final_softcap > 0.0f)
       for (int i = 0; i < m->vocab; i++) logits[i] = m->final_softcap * tanhf(logits[i] / m->final_softcap);
   }
-  free(hs); free(xn); free(qv); free(kv); free(vv); free(att); free(tmp); free(g); free(u); free(hb);
+  free(hs); free(xn); free(qv); free(kv); free(vv); free(att); free(tmp); free(g); free(u); free(hb); free(inp_pl);
   return rc;
 }
