@@ -111,7 +111,9 @@ int main(int argc, char** argv) {
   for (const Shape& sh : shapes) {
     if (only && !strstr(sh.name, only)) continue;
     const size_t wbytes = (size_t)sh.rows * (sh.cols / 32) * 18;
-    const int copies = (int)std::max<size_t>(2, (size_t)(1536ull << 20) / wbytes + 1);
+    int copies = (int)std::max<size_t>(2, (size_t)(1536ull << 20) / wbytes + 1);
+    // LLMI_SWEEP_COPIES=1: every launch re-reads the same (cache-resident) copy
+    if (const char* e = getenv("LLMI_SWEEP_COPIES")) copies = std::max(1, atoi(e));
     std::vector<DevWeight> ws(copies);
     for (int c = 0; c < copies; c++) {
       ws[c] = alloc_q4(sh.rows, sh.cols);

@@ -21,7 +21,7 @@ run() {  # name timeout cmd...
   if fatal $rc; then echo "FATAL in $name: stopping"; exit $rc; fi
   return 0
 }
-want tests && run pytest_gpu 900 python -m pytest tests -m gpu -q -rP -p no:cacheprovider
+want tests && run pytest_gpu 1000 python -u -m pytest tests -m gpu -x -v -rP -p no:cacheprovider --timeout 300 --timeout-method thread
 want smoke && run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 want sweep && run gemv_sweep 300 scripts/gemv_sweep 200
 want ablate && run ablate_run 900 bash scripts/ablate.sh
