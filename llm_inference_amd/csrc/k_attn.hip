@@ -727,10 +727,12 @@ struct BlockCfg {
   int QR, QP, QE, OR, OP, OE;
   size_t attn_lds;
   BlockFn fn;
+  const void* kern;  // the kernel (occupancy query)
 };
 #define LLMI_BCFG(NBQ, NBO, HD, G, QROLE, QR, QP, QE, OR, OP, OE)                                \
   {NBQ, NBO, HD, G, QROLE, QR, QP, QE, OR, OP, OE, block_attn_lds<HD, G>(),                      \
-   block_launch<HD, G, QR, QP, QE, QROLE, OR, OP, OE>}
+   block_launch<HD, G, QR, QP, QE, QROLE, OR, OP, OE>,                                            \
+   reinterpret_cast<const void*>(&attn_block_kernel<HD, G, QR, QP, QE, QROLE, OR, OP, OE>)}
 // qkv: 4 waves x QR rows per work-group (rows per work-group must divide
 // head_dim); o: 4 waves x OR rows.  E as in k_layer.hip's table.
 const BlockCfg kBlockCfgs[] = {
@@ -768,6 +770,45 @@ void launch_bump_epoch(unsigned* e, hipStream_t s) {  // bench: a fresh granule 
   LLMI_HIP(hipGetLastError());
 }
 
+// grid and dynamic LDS of one attention-block launch (qkv WGs, attention WGs, o WGs)
+struct BlockGeom {
+  int nq, na, no;
+  size_t lds;
+};
+static BlockGeom block_geom(const BlockCfg& c, const DevWeight& wqkv, const DevWeight& wo, int n_head_kv, int qrole) {
+  BlockGeom g;
+  g.nq = (wqkv.rows + 4 * c.QR - 1) / (4 * c.QR);
+  g.na = n_head_kv * ATTN_NSPLIT;
+  g.no = (wo.rows + 4 * c.OR - 1) / (4 * c.OR);
+  const size_t lds_q = (size_t)(wqkv.cols / 32) * sizeof(XBlock) + 16 + (qrole == ROLE_PRO ? (size_t)wqkv.cols * 4 : 0);
+  const size_t lds_o = (size_t)(wo.cols / 32) * sizeof(XBlock) + 16;
+  g.lds = std::max({lds_q, lds_o, c.attn_lds});
+  return g;
+}
+
+// Deadlock freedom.  The block's waits go one way only: attention
+// work-groups wait for qkv work-groups' granules, o work-groups for the
+// merged blocks; no producer ever waits for a consumer.  HIP promises no
+// dispatch order (MI355X_MICROARCH, correctness boundaries), so the launch is
+// admitted only if EVERY work-group of the grid can be resident at once:
+// then each producer holds (or will get) a slot regardless of which
+// work-groups were dispatched first, and all spins end.  The occupancy API can
+// report one block per CU too many at these SGPR counts (98-100, same table),
+// so one block per CU is kept in reserve.  A wait that still overruns its
+// bound sets bs.err (reported, never silently used).
+static bool block_co_resident(const BlockCfg& c, const BlockGeom& g) {
+  static int n_cu = 0;
+  if (n_cu == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return false;
+  }
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, c.kern, 256, g.lds) != hipSuccess) return false;
+  const long capacity = (long)std::max(0, per_cu - 1) * n_cu;
+  return g.nq + g.na + g.no <= capacity;
+}
+
 bool attn_block_supported(const DevWeight& wqkv, const DevWeight& wo, int head_dim, int n_head, int n_head_kv) {
   if (wqkv.type != T_Q4_0 || wo.type != T_Q4_0 || wqkv.slab || wo.slab) return false;
   if (wqkv.cols % 32 || wo.cols % 32 || n_head_kv <= 0 || n_head % n_head_kv) return false;
@@ -775,6 +816,7 @@ bool attn_block_supported(const DevWeight& wqkv, const DevWeight& wo, int head_d
   for (int role : {(int)ROLE_PLAIN, (int)ROLE_PRO}) {
     const BlockCfg* c = find_block_cfg(wqkv.cols / 32, wo.cols / 32, head_dim, g, role);
     if (!c || head_dim % (4 * c->QR) != 0) return false;
+    if (!block_co_resident(*c, block_geom(*c, wqkv, wo, n_head_kv, role))) return false;
   }
   return wqkv.rows == (n_head + 2 * n_head_kv) * head_dim && wo.cols == n_head * head_dim;
 }
@@ -800,13 +842,8 @@ void launch_attn_block(const DevWeight& wqkv, LayerGemv qg, int qrole, const Dev
   if (passes(nbq, c.QR) > c.QP || passes(nbo, c.OR) > c.OP) throw std::runtime_error("attention block: P too small");
   if (qrole == ROLE_PRO ? wqkv.cols > c.QE * 256 : 3 * nbq > c.QE * 256) throw std::runtime_error("attention block: qkv E");
   if (3 * nbo > c.OE * 256) throw std::runtime_error("attention block: o E");
-  const int rpw_q = 4 * c.QR, rpw_o = 4 * c.OR;
-  const int nq = (wqkv.rows + rpw_q - 1) / rpw_q;
-  const int no = (wo.rows + rpw_o - 1) / rpw_o;
-  const size_t lds_q = (size_t)nbq * sizeof(XBlock) + 16 + (qrole == ROLE_PRO ? (size_t)wqkv.cols * 4 : 0);
-  const size_t lds_o = (size_t)nbo * sizeof(XBlock) + 16;
-  const size_t lds = std::max({lds_q, lds_o, c.attn_lds});
-  c.fn(dim3(nq + aa.n_head_kv * ATTN_NSPLIT + no), lds, qg, og, aa, qa, bs, nq, s);
+  const BlockGeom bg = block_geom(c, wqkv, wo, aa.n_head_kv, qrole);
+  c.fn(dim3(bg.nq + bg.na + bg.no), bg.lds, qg, og, aa, qa, bs, bg.nq, s);
   LLMI_HIP(hipGetLastError());
 }
 
