@@ -24,6 +24,8 @@ struct QKVArgs {
   uint16_t* v_cache;
   int max_ctx;
   const int* d_pos;       // device position of this token
+  int has_kv = 1;         // 0: shared-KV layer (model.cpp:775-777): q only, the cache is another layer's
+  int v_norm = 0;         // 1: RMSNorm (no weight) of each V row before the append (Gemma-4, model.cpp:813-829)
 };
 
 constexpr int ATTN_NSPLIT = 32;  // key-range splits of the fast attention (work-groups per kv head)

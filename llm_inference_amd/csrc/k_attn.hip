@@ -16,6 +16,30 @@ namespace llmi {
 // rounded to f16 into the cache (model.cpp:442-474).
 // grid = n_head + n_head_kv blocks of 256 threads; head_dim <= 256.
 // ---------------------------------------------------------------------------
+// rms_norm scale of one head row held as v (thread t < hd) and s_x (ops.cpp:28-43)
+template <bool EXACT>
+__device__ __forceinline__ float head_rms_scale(float v, const float* s_x, int hd, double eps, float* s_part,
+                                                float* s_scale) {
+  const int t = threadIdx.x;
+  if (EXACT) {
+    if (t == 0) {
+      float sum = 0.0f;
+      for (int i = 0; i < hd; i++) sum = fmaf(s_x[i], s_x[i], sum);
+      *s_scale = 1.0f / sqrtf((float)((double)(sum / (float)hd) + eps));
+    }
+  } else {
+    float sum = wave_sum(v * v);
+    if ((t & 63) == 0) s_part[t >> 6] = sum;
+    __syncthreads();
+    if (t == 0) {
+      const float tot = (s_part[0] + s_part[1]) + (s_part[2] + s_part[3]);
+      *s_scale = 1.0f / sqrtf((float)((double)(tot / (float)hd) + eps));
+    }
+  }
+  __syncthreads();
+  return *s_scale;
+}
+
 template <bool EXACT>
 __global__ __launch_bounds__(256) void qk_norm_rope_kv_kernel(QKVArgs a) {
   __shared__ float s_x[256];
@@ -31,23 +55,8 @@ __global__ __launch_bounds__(256) void qk_norm_rope_kv_kernel(QKVArgs a) {
   const float v = t < hd ? src[t] : 0.0f;
   if (t < hd) s_x[t] = v;
   __syncthreads();
-  if (EXACT) {
-    if (t == 0) {
-      float sum = 0.0f;
-      for (int i = 0; i < hd; i++) sum = fmaf(s_x[i], s_x[i], sum);
-      s_scale = 1.0f / sqrtf((float)((double)(sum / (float)hd) + a.eps));
-    }
-  } else {
-    float sum = wave_sum(v * v);
-    if ((t & 63) == 0) s_part[t >> 6] = sum;
-    __syncthreads();
-    if (t == 0) {
-      const float tot = (s_part[0] + s_part[1]) + (s_part[2] + s_part[3]);
-      s_scale = 1.0f / sqrtf((float)((double)(tot / (float)hd) + a.eps));
-    }
-  }
-  __syncthreads();
-  const float nv = t < hd ? (s_scale * v) * nw[t] : 0.0f;
+  const float sc = head_rms_scale<EXACT>(v, s_x, hd, a.eps, s_part, &s_scale);
+  const float nv = t < hd ? (sc * v) * nw[t] : 0.0f;
   __syncthreads();
   if (t < hd) s_x[t] = nv;
   __syncthreads();
@@ -67,13 +76,23 @@ __global__ __launch_bounds__(256) void qk_norm_rope_kv_kernel(QKVArgs a) {
     } else {
       const size_t ci = ((size_t)h * a.max_ctx + pos) * hd + t;
       a.k_cache[ci] = f2h_ggml(r);
-      a.v_cache[ci] = f2h_ggml(a.qkv[(size_t)a.v_off + (size_t)h * hd + t]);
     }
+  }
+  if (!is_q) {  // the V row: as projected, or RMS-normalised without weight (Gemma-4)
+    const float vv = t < hd ? a.qkv[(size_t)a.v_off + (size_t)h * hd + t] : 0.0f;
+    float vo = vv;
+    if (a.v_norm) {
+      __syncthreads();  // s_x reuse
+      if (t < hd) s_x[t] = vv;
+      __syncthreads();
+      vo = head_rms_scale<EXACT>(vv, s_x, hd, a.eps, s_part, &s_scale) * vv;
+    }
+    if (t < hd) a.v_cache[((size_t)h * a.max_ctx + pos) * hd + t] = f2h_ggml(vo);
   }
 }
 
 void launch_qk_norm_rope_kv(const QKVArgs& a, bool exact, hipStream_t s) {
-  const dim3 grid(a.n_head + a.n_head_kv);
+  const dim3 grid(a.n_head + (a.has_kv ? a.n_head_kv : 0));
   if (exact)
     hipLaunchKernelGGL(qk_norm_rope_kv_kernel<true>, grid, dim3(256), 0, s, a);
   else
@@ -284,7 +303,10 @@ constexpr int attn_kp() {  // PV key residue classes
 // token's q/k/v rows from their granules (re-loading until the qkv
 // work-groups' tags arrive); the merging work-group publishes the heads'
 // Q8_0 blocks as granules for the o projection.
-template <int HD, int G, bool FUSED, int TK, bool BLK = false>
+// KVD: virtual kv heads per cache head (GQA groups of 8 run as two work-group
+// sets of 4 q heads over the same cache head: hkv indexes the q-head group,
+// hkv / KVD the cache)
+template <int HD, int G, bool FUSED, int TK, bool BLK = false, int KVD = 1>
 __device__ __forceinline__ void attn_split_body(const AttnArgs& a, const QKVArgs& qa, uint16_t* __restrict__ s_k,
                                                 uint16_t* __restrict__ s_v, float* __restrict__ s_red,
                                                 const int hkv, const int c, const BlockSync& bs) {
@@ -313,8 +335,10 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, const QKVArgs
   const int pos = *a.d_pos;
   const int n_keys = pos + 1;
   const bool own_new = FUSED && (pos / TK) % NS == c;
-  const uint4* kb = reinterpret_cast<const uint4*>(a.k_cache + (size_t)hkv * a.max_ctx * HD);
-  const uint4* vb = reinterpret_cast<const uint4*>(a.v_cache + (size_t)hkv * a.max_ctx * HD);
+  const int hkc = hkv / KVD;  // cache head
+  static_assert(KVD == 1 || !FUSED, "virtual kv heads: the KV append runs in its own launch");
+  const uint4* kb = reinterpret_cast<const uint4*>(a.k_cache + (size_t)hkc * a.max_ctx * HD);
+  const uint4* vb = reinterpret_cast<const uint4*>(a.v_cache + (size_t)hkc * a.max_ctx * HD);
   uint4 kr[NLD], vr[NLD];
   // unconditional loads of tile `tl` (rows clamped into the cache); keys past
   // n_keys are zeroed (the cache beyond pos may hold stale or NaN bits)
@@ -601,7 +625,7 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, const QKVArgs
 // beyond (fewer tile rounds per split).  scripts/ab A/B, 4B shapes: pos 100
 // 7.8 vs 9.0 us, pos 700 8.3 vs 9.2 us with 32-key tiles; 64-key tiles win
 // from pos ~1000 (2000: 9.9 vs 10.2 us).
-template <int HD, int G, bool FUSED>
+template <int HD, int G, bool FUSED, int KVD = 1>
 __global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa) {
   // K/V tiles and the PV reduction buffer sized once for 64-key tiles (the
   // two bodies share them: LDS size sets how fast work-groups are dispatched)
@@ -610,9 +634,9 @@ __global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa)
   __shared__ __attribute__((aligned(16))) uint16_t s_v[64 * HD];
   __shared__ __attribute__((aligned(16))) float s_red[KP > 1 ? KP * G * HD : 4];
   if (*a.d_pos + 1 <= 32 * ATTN_NSPLIT)
-    attn_split_body<HD, G, FUSED, 32>(a, qa, s_k, s_v, s_red, blockIdx.x, blockIdx.y, BlockSync{});
+    attn_split_body<HD, G, FUSED, 32, false, KVD>(a, qa, s_k, s_v, s_red, blockIdx.x, blockIdx.y, BlockSync{});
   else
-    attn_split_body<HD, G, FUSED, 64>(a, qa, s_k, s_v, s_red, blockIdx.x, blockIdx.y, BlockSync{});
+    attn_split_body<HD, G, FUSED, 64, false, KVD>(a, qa, s_k, s_v, s_red, blockIdx.x, blockIdx.y, BlockSync{});
 }
 
 template <int HD, int G>
@@ -624,13 +648,24 @@ static void launch_split_g(const AttnArgs& a, const QKVArgs* fused, hipStream_t 
     hipLaunchKernelGGL((attn_split_kernel<HD, G, false>), grid, dim3(256), 0, s, a, QKVArgs{});
 }
 
+// GQA group 8 (Gemma-4 E2B: 8 q heads on one kv head): two sets of
+// work-groups of 4 q heads each read the same cache head (the history is
+// read twice; the 4-head body's registers and LDS are unchanged)
+template <int HD>
+static void launch_split_g8(const AttnArgs& a, const QKVArgs* fused, hipStream_t s) {
+  if (fused) throw std::runtime_error("attention: GQA group 8 runs the unfused q/k launch");
+  const dim3 grid(a.n_head_kv * 2, ATTN_NSPLIT);
+  hipLaunchKernelGGL((attn_split_kernel<HD, 4, false, 2>), grid, dim3(256), 0, s, a, QKVArgs{});
+}
+
 template <int HD>
 static void launch_split(const AttnArgs& a, const QKVArgs* fused, hipStream_t s) {
   switch (a.n_head / a.n_head_kv) {
     case 1: launch_split_g<HD, 1>(a, fused, s); break;
     case 2: launch_split_g<HD, 2>(a, fused, s); break;
     case 4: launch_split_g<HD, 4>(a, fused, s); break;
-    default: throw std::runtime_error("attention: GQA group must be 1, 2 or 4");
+    case 8: launch_split_g8<HD>(a, fused, s); break;
+    default: throw std::runtime_error("attention: GQA group must be 1, 2, 4 or 8");
   }
 }
 

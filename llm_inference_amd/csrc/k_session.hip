@@ -225,7 +225,7 @@ __global__ __launch_bounds__(1024) void residual_norm_kernel(const float* __rest
                                                              const float* __restrict__ w_post,
                                                              float* __restrict__ resid,
                                                              const float* __restrict__ w_next, NormOut out, int n,
-                                                             double eps) {
+                                                             double eps, float post_scale) {
   extern __shared__ float s_h[];  // [n]: exact-mode sum staging, then the Q8_0 staging
   __shared__ float sh[16];
   const int t = threadIdx.x;
@@ -246,6 +246,7 @@ __global__ __launch_bounds__(1024) void residual_norm_kernel(const float* __rest
     const int i = t + k * 1024;
     const float a = w_post ? (sc1 * yv[k]) * wp[k] : yv[k];
     hv[k] = rv[k] + a;
+    if (post_scale != 1.0f) hv[k] = hv[k] * post_scale;  // Gemma-4 layer output scale (model.cpp:968-977)
     if (i < n) resid[i] = hv[k];
   }
   if (EXACT) __syncthreads();  // s_h reuse
@@ -257,14 +258,58 @@ __global__ __launch_bounds__(1024) void residual_norm_kernel(const float* __rest
 }
 
 void launch_residual_norm(const float* y, const float* w_post, float* resid, const float* w_next, const NormOut& out,
-                          int n, double eps, bool exact, hipStream_t s) {
+                          int n, double eps, bool exact, hipStream_t s, float post_scale) {
   if (n > 1024 * NORM_EPT) throw std::runtime_error("residual_norm: n_embd > 8192");
   if (exact)
     hipLaunchKernelGGL(residual_norm_kernel<true>, dim3(1), dim3(1024), (size_t)n * 4, s, y, w_post, resid, w_next, out,
-                       n, eps);
+                       n, eps, post_scale);
   else
     hipLaunchKernelGGL(residual_norm_kernel<false>, dim3(1), dim3(1024), (size_t)n * 4, s, y, w_post, resid, w_next,
-                       out, n, eps);
+                       out, n, eps, post_scale);
+  LLMI_HIP(hipGetLastError());
+}
+
+// Gemma-4 per-layer inputs, second half of project_per_layer_inputs
+// (model.cpp:676-701): per layer l, nx = rms_norm(proj[l]) (ops.cpp:28-43),
+// inp[l] = (nx * nw + inp[l]) * (1 / sqrt(2)).  proj was scaled by
+// 1/sqrt(n_embd) by the caller (model.cpp:651-652).  One 256-thread block per layer.
+template <bool EXACT>
+__global__ __launch_bounds__(256) void ple_combine_kernel(const float* __restrict__ proj, const float* __restrict__ nw,
+                                                          float* __restrict__ inp, int ep, double eps) {
+  __shared__ float sh[16];
+  const float* p = proj + (size_t)blockIdx.x * ep;
+  float* d = inp + (size_t)blockIdx.x * ep;
+  float sum;
+  if (EXACT) {
+    sum = serial_sumsq(p, ep, sh);
+  } else {
+    float sq = 0.0f;
+    for (int i = threadIdx.x; i < ep; i += blockDim.x) sq = fmaf(p[i], p[i], sq);
+    sum = block_sum(sq, sh);
+  }
+  const float sc = rms_scale(sum, ep, eps);
+  const float is = 1.0f / sqrtf(2.0f);
+  for (int i = threadIdx.x; i < ep; i += blockDim.x) {
+    const float nx = sc * p[i];
+    d[i] = (nx * nw[i] + d[i]) * is;
+  }
+}
+
+void launch_ple_combine(const float* proj, const float* nw, float* inp, int n_layer, int n_epl, double eps, bool exact,
+                        hipStream_t s) {
+  if (exact)
+    hipLaunchKernelGGL(ple_combine_kernel<true>, dim3(n_layer), dim3(256), 0, s, proj, nw, inp, n_epl, eps);
+  else
+    hipLaunchKernelGGL(ple_combine_kernel<false>, dim3(n_layer), dim3(256), 0, s, proj, nw, inp, n_epl, eps);
+  LLMI_HIP(hipGetLastError());
+}
+
+__global__ void softcap_kernel(float* x, int n, float cap) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) x[i] = cap * llmi_glibc::tanhf(x[i] / cap);
+}
+void launch_softcap(float* x, int n, float cap, hipStream_t s) {
+  hipLaunchKernelGGL(softcap_kernel, dim3((n + 255) / 256), dim3(256), 0, s, x, n, cap);
   LLMI_HIP(hipGetLastError());
 }
 

@@ -46,11 +46,18 @@ void Session::load_hparams(const GGUFView& g) {  // model.cpp:58-167
   hp_.attn_scale = 1.0f / std::sqrt(float(hp_.hd_k));  // model.cpp:120
   if (const GValue* sw = g.find(p + "attention.sliding_window_pattern"))
     for (const auto& v : sw->arr) hp_.swa_layers.push_back((v.u32 & 0xFF) != 0);
-  for (const char* k : {"attention.logit_softcapping", "attention.final_logit_softcapping"})
-    if (const GValue* v = g.find(p + k))
-      if (v->f32() > 0.0f) throw status_error(LLMI_E_GGUF, std::string("unsupported: ") + p + k);
-  if (hp_.arch == "gemma4" || g.find(p + "embedding_length_per_layer_input") || g.find(p + "attention.shared_kv_layers"))
-    throw status_error(LLMI_E_GGUF, "unsupported architecture features (Gemma-4 per-layer/shared-KV)");
+  if (const GValue* v = g.find(p + "attention.logit_softcapping"))
+    if (v->f32() > 0.0f) throw status_error(LLMI_E_GGUF, "unsupported: " + p + "attention.logit_softcapping");
+  if (const GValue* v = g.find(p + "attention.final_logit_softcapping")) hp_.final_softcap = v->f32();
+  // Gemma-4 (model.cpp:119-122, 148-166): attention scale 1, per-layer
+  // embedding width, the first layer that reads an earlier layer's cache
+  hp_.gemma4 = hp_.arch == "gemma4";
+  if (hp_.gemma4) hp_.attn_scale = 1.0f;
+  const GValue* epl = g.find(p + "embedding_length_per_layer");
+  if (!epl) epl = g.find(p + "embedding_length_per_layer_input");
+  hp_.n_epl = epl ? (int)epl->u32 : 0;
+  if (const GValue* sk = g.find(p + "attention.shared_kv_layers")) hp_.kv_from = hp_.n_layer - (int)sk->u32;
+  if (hp_.gemma4 || hp_.kv_from >= 0 || hp_.n_epl > 0) fuse_layers_ = false;  // Gemma-3 launch tables only
   if (hp_.hd_k != hp_.hd_v || hp_.hd_k_swa != hp_.hd_v_swa)
     throw status_error(LLMI_E_GGUF, "key_length != value_length is not supported");
   if (hp_.n_head % hp_.n_head_kv) throw status_error(LLMI_E_GGUF, "head_count % head_count_kv != 0");
@@ -170,6 +177,34 @@ void Session::upload(const GGUFView& g) {  // model.cpp:169-238 tensor map
     logits_w_ = embd_;
   }
   out_norm_ = dev_f32_copy(g, on, hp_.n_embd);
+  // Gemma-4 per-layer token embeddings (model.cpp:178-188, 568-704)
+  const GTensor* pt = g.tensor("token_embd_per_layer.weight");
+  if (!pt) pt = g.tensor("per_layer_token_embd.weight");
+  if (pt) {
+    if (tp_) throw status_error(LLMI_E_ARG, "tensor parallel: per-layer embeddings are not supported");
+    const int row_el = hp_.n_epl * hp_.n_layer;
+    if (pt->type != T_F16 && pt->type != T_Q6_K && pt->type != T_Q4_K)
+      throw status_error(LLMI_E_TYPE, "Error: get_per_layer_inputs: Unsupported tensor type: " +
+                                          std::to_string(pt->type));
+    if (hp_.n_epl <= 0 || (int)pt->shape[0] != row_el || (int)pt->shape[1] < vocab_)
+      throw status_error(LLMI_E_SIZE, "per-layer token embedding shape != [n_epl * n_layer, vocab]");
+    ple_table_.type = pt->type;
+    ple_table_.rows = (int)pt->shape[1];
+    ple_table_.cols = row_el;
+    ple_row_bytes_ = gguf_bytes(pt->type, 1, row_el);
+    ple_table_.bytes = ple_row_bytes_ * pt->shape[1];
+    uint8_t* raw = dalloc<uint8_t>(ple_table_.bytes);
+    LLMI_HIP(hipMemcpy(raw, g.tensor_data(*pt), ple_table_.bytes, hipMemcpyHostToDevice));
+    ple_table_.qs = raw;
+    if (const GTensor* mp = g.tensor("per_layer_model_proj.weight")) {
+      if ((int)mp->shape[0] != hp_.n_embd || (int)mp->shape[1] != row_el)
+        throw status_error(LLMI_E_SIZE, "per_layer_model_proj shape != [n_embd, n_epl * n_layer]");
+      ple_model_proj_ = make_parts(g, {all_rows(mp)}, stream_, weight_bytes_);
+      const GTensor* pn = g.tensor("per_layer_proj_norm.weight");
+      if (!pn) throw status_error(LLMI_E_GGUF, "missing per_layer_proj_norm.weight");
+      ple_proj_norm_ = dev_f32_copy(g, pn, hp_.n_epl);
+    }
+  }
   L_.resize(hp_.n_layer);
   for (int l = 0; l < hp_.n_layer; l++) {
     auto T = [&](const char* n, bool req = true) -> const GTensor* {
@@ -182,18 +217,32 @@ void Session::upload(const GGUFView& g) {  // model.cpp:169-238 tensor map
     LayerDev& Ld = L_[l];
     Ld.is_swa = l < (int)hp_.swa_layers.size() ? hp_.swa_layers[l] : (l % 6 < 5);  // model.cpp:723-729
     Ld.hd = Ld.is_swa ? hp_.hd_k_swa : hp_.hd_k;
-    const GTensor *q = T("attn_q.weight"), *k = T("attn_k.weight"), *v = T("attn_v.weight");
-    if ((int)q->shape[1] < hp_.n_head * Ld.hd || (int)k->shape[1] < hp_.n_head_kv * Ld.hd ||
-        (int)v->shape[1] < hp_.n_head_kv * Ld.hd)
+    // shared KV (model.cpp:775-777, 832-835): no K/V projections; the cache of
+    // layer kv_from - 2 (SWA) or kv_from - 1 (global) is read instead
+    Ld.has_kv = hp_.kv_from < 0 || l < hp_.kv_from;
+    if (!Ld.has_kv) {
+      if (tp_) throw status_error(LLMI_E_ARG, "tensor parallel: shared-KV layers are not supported");
+      Ld.kv_src = hp_.kv_from - (Ld.is_swa ? 2 : 1);
+      if (Ld.kv_src < 0 || Ld.kv_src >= l || !L_[Ld.kv_src].has_kv || L_[Ld.kv_src].is_swa != Ld.is_swa)
+        throw status_error(LLMI_E_GGUF, "shared-KV layer " + std::to_string(l) + " reads layer " +
+                                            std::to_string(Ld.kv_src) + " (no cache of the same attention kind)");
+    }
+    const GTensor* q = T("attn_q.weight");
+    const GTensor* k = Ld.has_kv ? T("attn_k.weight") : nullptr;
+    const GTensor* v = Ld.has_kv ? T("attn_v.weight") : nullptr;
+    if ((int)q->shape[1] < hp_.n_head * Ld.hd ||
+        (Ld.has_kv && ((int)k->shape[1] < hp_.n_head_kv * Ld.hd || (int)v->shape[1] < hp_.n_head_kv * Ld.hd)))
       throw status_error(LLMI_E_SIZE, "attention projection rows < heads * head_dim");
     const int hd = Ld.hd, r = tp_rank_;
     const std::vector<RowSlice> qkv_rows =
-        tp_ ? std::vector<RowSlice>{{q, r * nh_ * hd, nh_ * hd}, {k, kv0_ * hd, nkv_ * hd}, {v, kv0_ * hd, nkv_ * hd}}
-            : std::vector<RowSlice>{all_rows(q), all_rows(k), all_rows(v)};
+        !Ld.has_kv ? std::vector<RowSlice>{all_rows(q)}
+        : tp_ ? std::vector<RowSlice>{{q, r * nh_ * hd, nh_ * hd}, {k, kv0_ * hd, nkv_ * hd}, {v, kv0_ * hd, nkv_ * hd}}
+              : std::vector<RowSlice>{all_rows(q), all_rows(k), all_rows(v)};
     Ld.qkv = make_parts(g, qkv_rows, stream_, weight_bytes_);
     Ld.k_off = qkv_rows[0].n;
-    Ld.v_off = qkv_rows[0].n + qkv_rows[1].n;
-    Ld.qkv_rows = qkv_rows[0].n + qkv_rows[1].n + qkv_rows[2].n;
+    Ld.v_off = Ld.has_kv ? qkv_rows[0].n + qkv_rows[1].n : qkv_rows[0].n;
+    Ld.qkv_rows = 0;
+    for (const auto& rs : qkv_rows) Ld.qkv_rows += rs.n;
     const GTensor* o = T("attn_output.weight");
     if ((int)o->shape[0] != hp_.n_head * Ld.hd || (int)o->shape[1] != hp_.n_embd)
       throw status_error(LLMI_E_SIZE, "mat_vec_mul_q4_0: input vector size mismatch (attn_output)");
@@ -218,7 +267,7 @@ void Session::upload(const GGUFView& g) {  // model.cpp:169-238 tensor map
       w.cols = (int)t->shape[0];
       return layer_gemv_supported(w, role);
     };
-    const bool qkv_same = q->type == k->type && q->type == v->type && q->shape[0] == k->shape[0] &&
+    const bool qkv_same = Ld.has_kv && q->type == k->type && q->type == v->type && q->shape[0] == k->shape[0] &&
                           q->shape[0] == v->shape[0];
     const bool want_fused =
         fuse_layers_ && qkv_same && (gt->type == T_Q4_0 || gt->type == T_Q8_0) && up->type == gt->type &&
@@ -261,13 +310,35 @@ void Session::upload(const GGUFView& g) {  // model.cpp:169-238 tensor map
                layer_gemv_supported(Ld.gate_up[0].w, LAYER_GELU) && layer_gemv_supported(Ld.down.w, LAYER_QUANT);
     Ld.attn_norm = dev_f32_copy(g, T("attn_norm.weight"), hp_.n_embd);
     Ld.q_norm = dev_f32_copy(g, T("attn_q_norm.weight"), Ld.hd);
-    Ld.k_norm = dev_f32_copy(g, T("attn_k_norm.weight"), Ld.hd);
+    Ld.k_norm = Ld.has_kv ? dev_f32_copy(g, T("attn_k_norm.weight"), Ld.hd) : nullptr;
     Ld.ffn_norm = dev_f32_copy(g, T("ffn_norm.weight"), hp_.n_embd);
     Ld.post_attn_norm = dev_f32_copy(g, T2("post_attention_norm.weight", "attn_post_norm.weight"), hp_.n_embd);
     Ld.post_ffw_norm = dev_f32_copy(g, T2("post_ffw_norm.weight", "ffn_post_norm.weight"), hp_.n_embd);
-    const size_t kv = (size_t)nkv_ * max_ctx_ * Ld.hd;
-    Ld.kc = dalloc<uint16_t>(kv);
-    Ld.vc = dalloc<uint16_t>(kv);
+    if (Ld.has_kv) {
+      const size_t kv = (size_t)nkv_ * max_ctx_ * Ld.hd;
+      Ld.kc = dalloc<uint16_t>(kv);
+      Ld.vc = dalloc<uint16_t>(kv);
+    } else {
+      Ld.kc = L_[Ld.kv_src].kc;
+      Ld.vc = L_[Ld.kv_src].vc;
+    }
+    // Gemma-4 per-layer embedding step and output scale (model.cpp:215-233, 926-977)
+    if (ple_table_.qs) {
+      const GTensor* pg = T2("per_layer_inp_gate.weight", "inp_gate.weight");
+      const GTensor* pp = T2("per_layer_proj.weight", "proj.weight");
+      const GTensor* pn = T2("per_layer_post_norm.weight", "post_norm.weight");
+      if (!pg || !pp || !pn) throw status_error(LLMI_E_GGUF, "missing per-layer embedding tensors in layer " + std::to_string(l));
+      if ((int)pg->shape[0] != hp_.n_embd || (int)pg->shape[1] != hp_.n_epl || (int)pp->shape[0] != hp_.n_epl ||
+          (int)pp->shape[1] != hp_.n_embd)
+        throw status_error(LLMI_E_SIZE, "per-layer embedding projection shapes in layer " + std::to_string(l));
+      Ld.ple_gate = make_parts(g, {all_rows(pg)}, stream_, weight_bytes_)[0];
+      Ld.ple_proj = make_parts(g, {all_rows(pp)}, stream_, weight_bytes_)[0];
+      Ld.ple_post_norm = dev_f32_copy(g, pn, hp_.n_embd);
+    }
+    if (const GTensor* os = T2("out_scale.weight", "layer_output_scale.weight")) {
+      if (os->type != T_F32) throw status_error(LLMI_E_TYPE, "layer output scale is not F32");
+      std::memcpy(&Ld.out_scale, g.tensor_data(*os), 4);
+    }
   }
   // The fused path runs only when EVERY layer fits it; otherwise the layers
   // that were prepared for it go back to the plain gate/up order.
@@ -335,7 +406,7 @@ void Session::alloc_buffers() {
   q_ = dalloc<float>(maxq);
   attn_ = dalloc<float>(maxq);
   part_ = dalloc<float>((size_t)hp_.n_head * ATTN_NSPLIT * (maxhd + 2));
-  ticket_ = dalloc<unsigned>(hp_.n_head_kv);  // zeroed; the attention kernel resets it after use
+  ticket_ = dalloc<unsigned>(hp_.n_head);  // per (virtual) kv head, zeroed; the attention kernel resets it after use
   o_out_ = dalloc<float>(E);
   gu_ = dalloc<float>(2 * (size_t)F);
   hid_ = dalloc<float>(F);
@@ -350,6 +421,14 @@ void Session::alloc_buffers() {
   ring_ = dalloc<int32_t>(max_ctx_);
   ring_idx_ = dalloc<int32_t>(1);
   amax_key_ = dalloc<unsigned long long>(tp_size_);  // one argmax key per rank's vocabulary slice
+  if (ple_table_.qs) {
+    const size_t row_el = (size_t)hp_.n_epl * hp_.n_layer;
+    inp_pl_ = dalloc<float>(row_el);
+    ple_proj_out_ = dalloc<float>(row_el);
+    ple_g_ = dalloc<float>(hp_.n_epl);
+    ple_u_ = dalloc<float>(hp_.n_epl);
+    ple_tmp_ = dalloc<float>(E);
+  }
   LLMI_HIP(hipHostMalloc((void**)&h_stage_, 64, hipHostMallocDefault));
 }
 
@@ -440,6 +519,7 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
     // (a tensor-parallel rank screens its vocabulary shard; the keys meet in
     // finalize as before); LLMI_FULL_LOGITS=1 keeps the full GEMV in the loop
     screen_ = !ex_logits_ && embd_.type == T_F16 && logits_w_.type == T_F16 && screen_supported(logits_w_) &&
+              hp_.final_softcap <= 0.0f &&
               getenv("LLMI_FULL_LOGITS") == nullptr;
     if (screen_) alloc_screen_table(logits_w_, scr_, stream_);
     if (block_) {
@@ -489,8 +569,13 @@ void Session::release() {
     for (auto& p : l.gate_up) free_weight(p.w);
     free_weight(l.o.w);
     free_weight(l.down.w);
+    free_weight(l.ple_gate.w);
+    free_weight(l.ple_proj.w);
   }
   L_.clear();
+  for (auto& p : ple_model_proj_) free_weight(p.w);
+  ple_model_proj_.clear();
+  ple_table_ = DevWeight{};  // its bytes are an allocs_ entry
   if (own_logits_w_) free_weight(logits_w_);
   own_logits_w_ = false;
   free_weight(embd_);
@@ -556,6 +641,19 @@ void Session::record_step(hipStream_t s, bool gen) {
     kernels_per_token_ += 2;
   }
   dump("inp_scaled", resid_, E, s);  // model.cpp:711-713
+  if (ple_table_.qs) {  // Gemma-4 per-layer inputs (model.cpp:715-719, 568-704)
+    const int NL = hp_.n_layer, EP = hp_.n_epl;
+    launch_dequantize_rows(ple_table_.type, (const uint8_t*)ple_table_.qs, ple_row_bytes_, d_token_, 1, NL * EP,
+                           std::sqrt((float)EP), inp_pl_, s);
+    kernels_per_token_++;
+    if (!ple_model_proj_.empty()) {
+      gemv_parts(ple_model_proj_, resid_, E, ple_proj_out_, s, false);
+      launch_scale(ple_proj_out_, NL * EP, 1.0f / std::sqrt((float)E), s);
+      launch_ple_combine(ple_proj_out_, ple_proj_norm_, inp_pl_, NL, EP, hp_.eps, ex_norm_, s);
+      kernels_per_token_ += 2;
+      if (ple_model_proj_[0].w.type != T_BF16 && ple_model_proj_[0].w.type != T_F32) x_q8 = false;  // act_ reused
+    }
+  }
   dump("attn_norm-0", xn_, E, s);
   tap("inp_scaled", -1, resid_, (size_t)E * 4, s);
   tap("attn_norm", 0, xn_, (size_t)E * 4, s);
@@ -577,7 +675,7 @@ void Session::record_logits(hipStream_t s, bool gen) {
   // (a tensor-parallel rank: its vocabulary rows, its own argmax key, then
   // the keys all-gathered and reduced in finalize)
   if (embd_.type != T_F16) prepare_act(embd_.type, xn_, E, act_, s);
-  const bool fold = !ex_logits_ && embd_.type == T_F16 && E % 8 == 0;
+  const bool fold = !ex_logits_ && embd_.type == T_F16 && E % 8 == 0 && hp_.final_softcap <= 0.0f;
   float* lg = logits_ + (size_t)tp_rank_ * v_sh_;
   unsigned long long* key = amax_key_ + tp_rank_;
   if (gen && screen_) {  // token id only: int8 screening + exact rescoring of the candidates
@@ -588,6 +686,10 @@ void Session::record_logits(hipStream_t s, bool gen) {
     for (int r = 0; r < dup("logits"); r++)
       launch_gemv(logits_w_, act_, lg, ex_logits_ ? GEMV_EXACT : GEMV_FAST, s, fold ? key : nullptr);
     kernels_per_token_++;
+    if (hp_.final_softcap > 0.0f) {  // model.cpp:1036-1041
+      launch_softcap(lg, v_rows_, hp_.final_softcap, s);
+      kernels_per_token_++;
+    }
     dump("result_output", lg, v_rows_, s);  // model.cpp:1046
     tap("logits", -1, lg, (size_t)v_rows_ * 4, s);
   }
@@ -910,11 +1012,16 @@ void Session::record_layers(hipStream_t s, bool x_q8) {
     for (int r = 0; r < dup("qkv"); r++) gemv_parts(Ld.qkv, xn_, E, qkv_, s, x_q8);
     const std::string L = std::to_string(l);
     dump("Qcur-" + L, qkv_, hp_.n_head * hd, s);
-    dump("Kcur-" + L, qkv_ + Ld.k_off, hp_.n_head_kv * hd, s);
-    dump("Vcur-" + L, qkv_ + Ld.v_off, hp_.n_head_kv * hd, s);
+    if (Ld.has_kv) {
+      dump("Kcur-" + L, qkv_ + Ld.k_off, hp_.n_head_kv * hd, s);
+      dump("Vcur-" + L, qkv_ + Ld.v_off, hp_.n_head_kv * hd, s);
+    }
     QKVArgs qa{qkv_, Ld.k_off, Ld.v_off, hp_.n_head, hp_.n_head_kv, hd, Ld.q_norm, Ld.k_norm,
                Ld.is_swa ? rope_swa_ : rope_glb_, hp_.attn_scale, hp_.eps, q_, Ld.kc, Ld.vc, max_ctx_, d_pos_};
-    const bool fuse_qk = !ex_attn_ && !ex_norm_;  // norm/rope/KV-append inside the attention launch
+    qa.has_kv = Ld.has_kv;
+    qa.v_norm = hp_.gemma4 && Ld.has_kv;  // model.cpp:813-829
+    // norm/rope/KV-append inside the attention launch (Gemma-3 rows only)
+    const bool fuse_qk = !ex_attn_ && !ex_norm_ && Ld.has_kv && !qa.v_norm && hp_.n_head <= 4 * hp_.n_head_kv;
     if (!fuse_qk) {
       launch_qk_norm_rope_kv(qa, ex_norm_, s);
       kernels_per_token_++;
@@ -947,7 +1054,17 @@ void Session::record_layers(hipStream_t s, bool x_q8) {
     NormOut o2 = last ? NormOut{} : nout(L_[l + 1].qkv);
     o2.xn = xn_;
     if (last && embd_.type == T_F16) o2.x16 = act_.x16;  // logits input, ops.cpp:542-551
-    launch_residual_norm(d_out_, Ld.post_ffw_norm, resid_, w_next, o2, E, hp_.eps, ex_norm_, s);
+    if (ple_table_.qs) {  // Gemma-4 per-layer embedding step (model.cpp:926-966), then the output scale
+      const int EP = hp_.n_epl;
+      launch_residual_norm(d_out_, Ld.post_ffw_norm, resid_, w_next, NormOut{xn_}, E, hp_.eps, ex_norm_, s);
+      gemv_parts({Ld.ple_gate}, resid_, E, ple_g_, s, false);
+      launch_gelu_mul(ple_g_, inp_pl_ + (size_t)l * EP, ple_u_, EP, s);
+      gemv_parts({Ld.ple_proj}, ple_u_, EP, ple_tmp_, s, false);
+      launch_residual_norm(ple_tmp_, Ld.ple_post_norm, resid_, w_next, o2, E, hp_.eps, ex_norm_, s, Ld.out_scale);
+      kernels_per_token_ += 3;
+    } else {
+      launch_residual_norm(d_out_, Ld.post_ffw_norm, resid_, w_next, o2, E, hp_.eps, ex_norm_, s, Ld.out_scale);
+    }
     x_q8 = o2.q8 != nullptr;
     kernels_per_token_++;
     dump("l_out-" + L, resid_, E, s);

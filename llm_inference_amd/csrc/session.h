@@ -26,6 +26,11 @@ struct HParams {  // model.h:22-43 (Gemma-3 subset)
   double eps = 0;
   float rope_base = 0, rope_scale = 1.0f, attn_scale = 1.0f;
   std::vector<bool> swa_layers;
+  // Gemma-4 (model.cpp:117-166)
+  bool gemma4 = false;
+  int n_epl = 0;             // embedding_length_per_layer(_input)
+  int kv_from = -1;          // n_layer_kv_from_start: layers >= kv_from read an earlier layer's cache
+  float final_softcap = 0;   // attention.final_logit_softcapping
 };
 
 struct GemvPart {  // one weight GEMV writing rows [out_off, out_off + rows)
@@ -47,6 +52,12 @@ struct LayerDev {
   bool aliased = false;         // LLMI_SHARE_LAYERS diagnostics: weights owned by another layer
   int hd = 0;
   uint16_t *kc = nullptr, *vc = nullptr;
+  // Gemma-4
+  bool has_kv = true;            // false: shared-KV layer, kc/vc alias layer kv_src's cache
+  int kv_src = -1;
+  GemvPart ple_gate, ple_proj;   // per-layer embedding step (model.cpp:926-966), BF16 usually
+  float* ple_post_norm = nullptr;
+  float out_scale = 1.0f;        // layer output scale (model.cpp:968-977)
 };
 
 class Session {
@@ -110,6 +121,12 @@ class Session {
   bool block_ = false;        // fast path: qkv + attention + o as one launch per layer (k_attn.hip)
   unsigned* blk_epoch_ = nullptr;  // [n_layer] attention-block launch counts (granule tags)
   uint2* blk_gqkv_ = nullptr;      // [n_layer][qkv rows] granules
+  // Gemma-4 per-layer inputs (model.cpp:568-704)
+  DevWeight ple_table_{};          // raw GGUF rows [vocab][n_layer * n_epl] (F16 / Q6_K / Q4_K), lookups only
+  size_t ple_row_bytes_ = 0;
+  std::vector<GemvPart> ple_model_proj_;  // n_embd -> n_layer * n_epl (optional)
+  float* ple_proj_norm_ = nullptr;
+  float *inp_pl_ = nullptr, *ple_proj_out_ = nullptr, *ple_g_ = nullptr, *ple_u_ = nullptr, *ple_tmp_ = nullptr;
   uint2* blk_gxo_ = nullptr;       // [n_layer][n_head * hd / 32 * 12] granules
   size_t blk_gqkv_stride_ = 0, blk_gxo_stride_ = 0;
   int* blk_err_ = nullptr;       // set by a bounded wait that gave up

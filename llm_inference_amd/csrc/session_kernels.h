@@ -22,8 +22,16 @@ struct NormOut {
   XBlock* q8 = nullptr;
   uint16_t* x16 = nullptr;
 };
+// resid = (resid + rms(y) * w_post) * post_scale (y itself when w_post is null;
+// post_scale: Gemma-4 layer output scale, 1 = none); outputs rms(resid) * w_next
 void launch_residual_norm(const float* y, const float* w_post, float* resid, const float* w_next, const NormOut& out,
-                          int n, double eps, bool exact, hipStream_t s);
+                          int n, double eps, bool exact, hipStream_t s, float post_scale = 1.0f);
+// Gemma-4 per-layer inputs (model.cpp:676-701): inp[l][i] = (rms(proj[l])[i] * nw[i] + inp[l][i]) / sqrt(2),
+// proj already scaled by 1/sqrt(n_embd); one work-group per layer
+void launch_ple_combine(const float* proj, const float* nw, float* inp, int n_layer, int n_epl, double eps, bool exact,
+                        hipStream_t s);
+// final logit soft-capping (model.cpp:1036-1041): x = cap * tanhf(x / cap), glibc tanhf
+void launch_softcap(float* x, int n, float cap, hipStream_t s);
 void launch_embed_norm(uint32_t type, const uint8_t* table, size_t row_bytes, const int32_t* d_token,
                        float emb_scale, float* resid, const float* w, const NormOut& out, int n, double eps,
                        bool exact, hipStream_t s);

@@ -132,7 +132,8 @@ def test_q4_0_large_random_vs_oracle(ops, oracle):
 
 @pytest.mark.parametrize("hd,n_head,n_kv,n_keys", [(256, 8, 4, 12), (256, 4, 1, 77), (128, 8, 4, 300),
                                                    (64, 4, 2, 1), (16, 2, 1, 5), (256, 8, 4, 700),
-                                                   (128, 4, 2, 64 * 32 * 2 + 37)])  # > 1 tile per split
+                                                   (128, 4, 2, 64 * 32 * 2 + 37),  # > 1 tile per split
+                                                   (256, 8, 1, 300), (256, 16, 2, 1200)])  # GQA 8 (Gemma-4)
 def test_attention(ops, oracle, hd, n_head, n_kv, n_keys):
     """exact: the reference algorithm (f16 V accumulator); differs from the
     oracle only via device expf ulps -> <= 2 f16 ulps of the output scale.
