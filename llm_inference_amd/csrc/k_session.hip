@@ -181,6 +181,50 @@ __device__ __forceinline__ float rms_scale(float sum, int n, double eps) {  // o
 // ---------------------------------------------------------------------------
 constexpr int NORM_EPT = 8;  // elements per thread (n <= 8192)
 
+// Q8_K of one 256-element super-block (quantize_row_q8_k, ops.cpp:142-178,
+// as quantize_q8_k_kernel): a group of 256 threads (threadIdx.x / 256) reads
+// element threadIdx.x % 256 of xs.  Every thread of the block calls it (two
+// block-wide barriers); groups with active == false only take part in them.
+__device__ void q8k_group(const float* xs, bool active, uint8_t* blk, float* s_ax, int* s_ix) {
+  const int t = threadIdx.x, tl = t & 255, lane = t & 63, w = t >> 6, g4 = (t >> 8) * 4;
+  const float v = active ? xs[tl] : 0.0f;
+  float ax = fabsf(v);
+  int ix = tl;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {  // max |x|, first index on ties (strict > scan)
+    const float oa = __shfl_xor(ax, o);
+    const int oi = __shfl_xor(ix, o);
+    if (oa > ax || (oa == ax && oi < ix)) { ax = oa; ix = oi; }
+  }
+  if (lane == 0) { s_ax[w] = ax; s_ix[w] = ix; }
+  __syncthreads();
+  float amax = s_ax[g4];
+  int imax = s_ix[g4];
+  for (int k = 1; k < 4; k++)
+    if (s_ax[g4 + k] > amax || (s_ax[g4 + k] == amax && s_ix[g4 + k] < imax)) { amax = s_ax[g4 + k]; imax = s_ix[g4 + k]; }
+  __syncthreads();  // s_ax / s_ix free for the next call
+  if (!active) return;  // no barriers below
+  if (amax == 0.0f) {  // ops.cpp:158-163
+    blk[4 + tl] = 0;
+    if (tl < 16) { blk[260 + 2 * tl] = 0; blk[261 + 2 * tl] = 0; }
+    if (tl == 0) *reinterpret_cast<float*>(blk) = 0.0f;
+    return;
+  }
+  const float iscale = -127.f / xs[imax];
+  int q = nearest_int_fma(iscale, v);
+  q = q < -128 ? -128 : (q > 127 ? 127 : q);
+  blk[4 + tl] = (uint8_t)(int8_t)q;
+  int sum = q;  // 16-lane group sums -> bsums
+#pragma unroll
+  for (int o = 8; o >= 1; o >>= 1) sum += __shfl_xor(sum, o);
+  if ((tl & 15) == 0) {
+    const int16_t s16 = (int16_t)sum;
+    blk[260 + 2 * (tl >> 4)] = (uint8_t)(s16 & 0xFF);
+    blk[261 + 2 * (tl >> 4)] = (uint8_t)((uint16_t)s16 >> 8);
+  }
+  if (tl == 0) *reinterpret_cast<float*>(blk) = 1.0f / iscale;
+}
+
 // s_h: n floats of LDS (free again: callers are past their last use of it).
 // Q8_0 blocks: x staged in LDS, one thread per block (q8_block_serial).
 __device__ __forceinline__ void norm_outputs(const float (&xv)[NORM_EPT], int n, const NormOut& out, float* s_h) {
@@ -201,6 +245,51 @@ __device__ __forceinline__ void norm_outputs(const float (&xv)[NORM_EPT], int n,
       XBlock blk;
       q8_block_serial(s_h + 32 * b, &blk);
       out.q8[b] = blk;
+    }
+  }
+  if (out.q8k) {  // one wave per Q8_K super-block (n % 256 == 0: host-checked), no block barriers
+    __syncthreads();
+    const int lane = t & 63;
+    for (int sb = t >> 6; sb < n / 256; sb += 16) {
+      const float* xs = s_h + sb * 256;
+      uint8_t* blk = out.q8k + (size_t)sb * 292;
+      float v[4], ax = -1.0f;
+      int ix = 0;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {  // element lane + 64 k; first index of the max |x| (strict > scan)
+        v[k] = xs[lane + 64 * k];
+        if (fabsf(v[k]) > ax) { ax = fabsf(v[k]); ix = lane + 64 * k; }
+      }
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) {
+        const float oa = __shfl_xor(ax, o);
+        const int oi = __shfl_xor(ix, o);
+        if (oa > ax || (oa == ax && oi < ix)) { ax = oa; ix = oi; }
+      }
+      if (ax == 0.0f) {  // ops.cpp:158-163
+#pragma unroll
+        for (int k = 0; k < 4; k++) blk[4 + lane + 64 * k] = 0;
+        if (lane < 32) blk[260 + lane] = 0;
+        if (lane == 0) *reinterpret_cast<float*>(blk) = 0.0f;
+        continue;
+      }
+      const float iscale = -127.f / xs[ix];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        int q = nearest_int_fma(iscale, v[k]);
+        q = q < -128 ? -128 : (q > 127 ? 127 : q);
+        blk[4 + lane + 64 * k] = (uint8_t)(int8_t)q;
+        int sum = q;  // elements 64 k + 16 (lane / 16) .. + 15: bsums[4 k + lane / 16]
+#pragma unroll
+        for (int o = 8; o >= 1; o >>= 1) sum += __shfl_xor(sum, o);
+        if ((lane & 15) == 0) {
+          const int16_t s16 = (int16_t)sum;
+          const int j = 4 * k + (lane >> 4);
+          blk[260 + 2 * j] = (uint8_t)(s16 & 0xFF);
+          blk[261 + 2 * j] = (uint8_t)((uint16_t)s16 >> 8);
+        }
+      }
+      if (lane == 0) *reinterpret_cast<float*>(blk) = 1.0f / iscale;
     }
   }
 }
@@ -336,8 +425,27 @@ __global__ __launch_bounds__(256) void gelu_quant_kernel(const float* __restrict
   if (xb != nullptr) q8_block_store(v, ok && (gl >> 5) < n / 32, xb + (ok ? (gl >> 5) : 0), gl & 31);
 }
 
-void launch_gelu_quant(const float* gu, int n, float* hid, const Q8Act* q8, hipStream_t s) {
-  hipLaunchKernelGGL(gelu_quant_kernel, dim3((n + 255) / 256), dim3(256), 0, s, gu, n, hid, q8 ? q8->xb : nullptr);
+// the same with the GELU output's Q8_K super-blocks (one block = one super-block)
+__global__ __launch_bounds__(256) void gelu_quant_k_kernel(const float* __restrict__ gu, int n, float* __restrict__ hid,
+                                                           uint8_t* __restrict__ q8k) {
+  __shared__ float s_x[256];
+  __shared__ float s_ax[4];
+  __shared__ int s_ix[4];
+  const int gl = blockIdx.x * 256 + threadIdx.x;
+  const float v = gelu_mul1<true>(gu[gl], gu[n + gl]);
+  hid[gl] = v;
+  s_x[threadIdx.x] = v;
+  __syncthreads();
+  q8k_group(s_x, true, q8k + (size_t)blockIdx.x * 292, s_ax, s_ix);
+}
+
+void launch_gelu_quant(const float* gu, int n, float* hid, const Q8Act* q8, hipStream_t s, uint8_t* q8k) {
+  if (q8k) {
+    if (n % 256 || q8) throw std::runtime_error("gelu_quant: Q8_K output needs n % 256 == 0 and no Q8_0 output");
+    hipLaunchKernelGGL(gelu_quant_k_kernel, dim3(n / 256), dim3(256), 0, s, gu, n, hid, q8k);
+  } else {
+    hipLaunchKernelGGL(gelu_quant_kernel, dim3((n + 255) / 256), dim3(256), 0, s, gu, n, hid, q8 ? q8->xb : nullptr);
+  }
   LLMI_HIP(hipGetLastError());
 }
 

@@ -105,16 +105,26 @@ static std::vector<GemvPart> make_parts(const GGUFView& g, const std::vector<Row
     wbytes += p.w.bytes;
     parts.push_back(p);
   } else {
+    // runs of consecutive slices sharing type and width become one part
+    // (Q4_K_M: q|k Q4_K in one launch, v Q6_K in another)
     int off = 0;
-    for (auto& r : ts) {
-      check(r.t);
+    for (size_t i = 0; i < ts.size();) {
+      size_t j = i + 1;
+      while (j < ts.size() && ts[j].t->type == ts[i].t->type && ts[j].t->shape[0] == ts[i].t->shape[0]) j++;
+      int rows = 0;
+      for (size_t k = i; k < j; k++) { check(ts[k].t); rows += ts[k].n; }
       GemvPart p;
-      p.w = alloc_weight(r.t->type, r.n, (int)r.t->shape[0]);
-      upload_rows(p.w, 0, slice_data(g, r), r.n, s);
+      p.w = alloc_weight(ts[i].t->type, rows, (int)ts[i].t->shape[0]);
+      int r0 = 0;
+      for (size_t k = i; k < j; k++) {
+        upload_rows(p.w, r0, slice_data(g, ts[k]), ts[k].n, s);
+        r0 += ts[k].n;
+      }
       p.out_off = off;
-      off += r.n;
+      off += rows;
       wbytes += p.w.bytes;
       parts.push_back(p);
+      i = j;
     }
   }
   return parts;
@@ -604,7 +614,8 @@ void Session::gemv_parts(const std::vector<GemvPart>& parts, const float* x, int
   uint32_t prepared = 0xFFFFFFFFu;
   for (const auto& p : parts) {
     const uint32_t kind = (p.w.type == T_Q8_0) ? T_Q4_0 : (p.w.type == T_Q6_K ? T_Q4_K : p.w.type);
-    if (!(x_ready && kind == T_Q4_0) && kind != prepared) prepare_act(p.w.type, x, n_in, act_, s);
+    // x_ready: act_ already holds x in the format this kind reads (Q8_0 or Q8_K, the producer chose it)
+    if (!(x_ready && (kind == T_Q4_0 || kind == T_Q4_K)) && kind != prepared) prepare_act(p.w.type, x, n_in, act_, s);
     act_.xf = x;
     prepared = kind;
     launch_gemv(p.w, act_, out + p.out_off, ex_gemv_ ? GEMV_EXACT : GEMV_FAST, s);
@@ -623,9 +634,13 @@ void Session::record_step(hipStream_t s, bool gen) {
   auto nout = [&](const std::vector<GemvPart>& consumer) {
     NormOut o;
     o.xn = xn_;
-    bool q8 = !consumer.empty();
-    for (const auto& p : consumer) q8 &= is_q8(p.w.type);
+    bool q8 = !consumer.empty(), q8k = !consumer.empty();
+    for (const auto& p : consumer) {
+      q8 &= is_q8(p.w.type);
+      q8k &= (p.w.type == T_Q4_K || p.w.type == T_Q6_K) && p.w.cols % 256 == 0;
+    }
     if (q8) o.q8 = act_.q8.xb;
+    if (q8k && !ex_norm_) o.q8k = act_.q8k;  // exact mode keeps the reference's separate quantize launch
     return o;
   };
   bool x_q8 = false;  // xn_'s Q8_0 blocks are already in act_
@@ -633,7 +648,7 @@ void Session::record_step(hipStream_t s, bool gen) {
     const NormOut o = nout(L_[0].qkv);
     launch_embed_norm(embd_.type, embd_raw_, embd_row_bytes_, d_token_, emb_scale, resid_, L_[0].attn_norm, o, E,
                       hp_.eps, ex_norm_, s);
-    x_q8 = o.q8 != nullptr;
+    x_q8 = o.q8 != nullptr || o.q8k != nullptr;
     kernels_per_token_++;
   } else {
     launch_dequantize_rows(embd_.type, embd_raw_, embd_row_bytes_, d_token_, 1, E, emb_scale, resid_, s);
@@ -1001,9 +1016,13 @@ void Session::record_layers(hipStream_t s, bool x_q8) {
   auto nout = [&](const std::vector<GemvPart>& consumer) {
     NormOut o;
     o.xn = xn_;
-    bool q8 = !consumer.empty();
-    for (const auto& p : consumer) q8 &= is_q8(p.w.type);
+    bool q8 = !consumer.empty(), q8k = !consumer.empty();
+    for (const auto& p : consumer) {
+      q8 &= is_q8(p.w.type);
+      q8k &= (p.w.type == T_Q4_K || p.w.type == T_Q6_K) && p.w.cols % 256 == 0;
+    }
     if (q8) o.q8 = act_.q8.xb;
+    if (q8k && !ex_norm_) o.q8k = act_.q8k;  // exact mode keeps the reference's separate quantize launch
     return o;
   };
   for (int l = 0; l < hp_.n_layer; l++) {
@@ -1042,12 +1061,15 @@ void Session::record_layers(hipStream_t s, bool x_q8) {
     if (dup("norm") > 1)  // ablation: the same launch on a scratch residual (values irrelevant)
       launch_residual_norm(o_out_, Ld.post_attn_norm, resid_scratch_, Ld.ffn_norm, o1, E, hp_.eps, ex_norm_, s);
     kernels_per_token_++;
-    for (int r = 0; r < dup("gate_up"); r++) gemv_parts(Ld.gate_up, xn_, E, gu_, s, o1.q8 != nullptr);
+    for (int r = 0; r < dup("gate_up"); r++)
+      gemv_parts(Ld.gate_up, xn_, E, gu_, s, o1.q8 != nullptr || o1.q8k != nullptr);
     const bool d_q8 = Ld.down.w.type == T_Q4_0 || Ld.down.w.type == T_Q8_0;
-    for (int r = 0; r < dup("gelu"); r++) launch_gelu_quant(gu_, F, hid_, d_q8 ? &act_.q8 : nullptr, s);
+    const bool d_q8k = !ex_norm_ && (Ld.down.w.type == T_Q4_K || Ld.down.w.type == T_Q6_K) && F % 256 == 0;
+    for (int r = 0; r < dup("gelu"); r++)
+      launch_gelu_quant(gu_, F, hid_, d_q8 ? &act_.q8 : nullptr, s, d_q8k ? act_.q8k : nullptr);
     kernels_per_token_++;
     dump("ffn_geglu-" + L, hid_, F, s);
-    for (int r = 0; r < dup("down"); r++) gemv_parts({Ld.down}, hid_, F, d_out_, s, d_q8);
+    for (int r = 0; r < dup("down"); r++) gemv_parts({Ld.down}, hid_, F, d_out_, s, d_q8 || d_q8k);
     dump("ffn_out-" + L, d_out_, E, s);
     const bool last = l + 1 == hp_.n_layer;
     const float* w_next = last ? out_norm_ : L_[l + 1].attn_norm;
@@ -1065,7 +1087,7 @@ void Session::record_layers(hipStream_t s, bool x_q8) {
     } else {
       launch_residual_norm(d_out_, Ld.post_ffw_norm, resid_, w_next, o2, E, hp_.eps, ex_norm_, s, Ld.out_scale);
     }
-    x_q8 = o2.q8 != nullptr;
+    x_q8 = o2.q8 != nullptr || o2.q8k != nullptr;
     kernels_per_token_++;
     dump("l_out-" + L, resid_, E, s);
     dump(last ? std::string("result_norm") : "attn_norm-" + std::to_string(l + 1), xn_, E, s);

@@ -21,6 +21,7 @@ struct NormOut {
   float* xn = nullptr;
   XBlock* q8 = nullptr;
   uint16_t* x16 = nullptr;
+  uint8_t* q8k = nullptr;  // Q8_K super-blocks (292 B, quantize_row_q8_k) for Q4_K / Q6_K consumers
 };
 // resid = (resid + rms(y) * w_post) * post_scale (y itself when w_post is null;
 // post_scale: Gemma-4 layer output scale, 1 = none); outputs rms(resid) * w_next
@@ -35,7 +36,8 @@ void launch_softcap(float* x, int n, float cap, hipStream_t s);
 void launch_embed_norm(uint32_t type, const uint8_t* table, size_t row_bytes, const int32_t* d_token,
                        float emb_scale, float* resid, const float* w, const NormOut& out, int n, double eps,
                        bool exact, hipStream_t s);
-void launch_gelu_quant(const float* gu, int n, float* hid, const Q8Act* q8, hipStream_t s);
+// q8k (n % 256 == 0): the GELU output's Q8_K super-blocks for a Q4_K / Q6_K down projection
+void launch_gelu_quant(const float* gu, int n, float* hid, const Q8Act* q8, hipStream_t s, uint8_t* q8k = nullptr);
 // Q4_0 GEMV with the decode step's neighbours fused in (k_layer.hip)
 enum LayerRole { LAYER_PLAIN = 0, LAYER_PRO = 1, LAYER_GELU = 2, LAYER_QUANT = 3 };
 struct LayerGemv {
