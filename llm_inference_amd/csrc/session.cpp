@@ -509,8 +509,10 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
     build_rope_tables();
     // batched prefill: the fast fused layout on one device, shapes the
     // prefill kernels cover (otherwise forward() runs the token loop)
-    bool pf = fuse_layers_ && !tp_ && (embd_.type == T_F16 || embd_.type == T_Q8_0) && hp_.n_embd <= 8192 &&
-              hp_.n_embd % 32 == 0 && hp_.n_ff % 32 == 0;
+    // (a tensor-parallel rank: its shards' GEMMs, the slices all-gathered per
+    // projection; Q8_0 block slices need 32-aligned head and hidden shards)
+    bool pf = fuse_layers_ && (embd_.type == T_F16 || embd_.type == T_Q8_0) && hp_.n_embd <= 8192 &&
+              hp_.n_embd % 32 == 0 && hp_.n_ff % 32 == 0 && (!tp_ || (f_sh_ % 32 == 0 && coll_));
     for (const auto& l : L_)
       pf = pf && l.fused && (l.hd == 64 || l.hd == 128 || l.hd == 256) && prefill_gemm_supported(l.qkv[0].w) &&
            prefill_gemm_supported(l.o.w) && prefill_gemm_supported(l.gate_up[0].w) &&
@@ -734,6 +736,8 @@ void Session::ensure_prefill_buffers(int cap) {
   pf_out_ = dalloc<float>((size_t)cap * pf_ostride_);
   pf_xq_ = dalloc<XBlock>((size_t)cap * pf_xs_);
   pf_q_ = dalloc<uint16_t>((size_t)cap * maxq);
+  if (tp_)  // all-gather staging: the largest exchanged [T][row] activation (f32 rows or Q8_0 block rows)
+    pf_gather_ = dalloc<uint8_t>((size_t)cap * std::max((size_t)E * 4, (size_t)pf_xs_ * sizeof(XBlock)));
   pf_cap_ = cap;
 }
 
@@ -741,6 +745,22 @@ void Session::ensure_prefill_buffers(int cap) {
 // LLMI_PREFILL_CHUNK, default 256): per layer one MFMA GEMM per projection
 // over the chunk, per-token norms / rope / KV append, causal attention over
 // the cache; the last token's logits then go through the decode tail.
+// Tensor-parallel prefill exchange: every rank has written its column slice
+// [T][slice_b bytes] at column rank * slice_b of buf (row pitch pitch_b);
+// packs it into pf_gather_, all-gathers the per-rank [T][slice_b] blocks and
+// scatters every rank's block back to its columns of buf.
+void Session::gather_cols(void* buf, size_t pitch_b, size_t slice_b, int T, hipStream_t s) {
+  const size_t blk = slice_b * T;
+  uint8_t* g = reinterpret_cast<uint8_t*>(pf_gather_);
+  uint8_t* b = reinterpret_cast<uint8_t*>(buf);
+  LLMI_HIP(hipMemcpy2DAsync(g + tp_rank_ * blk, slice_b, b + tp_rank_ * slice_b, pitch_b, slice_b, T,
+                            hipMemcpyDeviceToDevice, s));
+  coll_->all_gather(g, blk, s);
+  for (int r = 0; r < tp_size_; r++)
+    if (r != tp_rank_)
+      LLMI_HIP(hipMemcpy2DAsync(b + r * slice_b, pitch_b, g + r * blk, slice_b, slice_b, T, hipMemcpyDeviceToDevice, s));
+}
+
 void Session::prefill(const int32_t* tokens, int n, int pos) {
   hipStream_t s = stream_;
   const int E = hp_.n_embd, F = hp_.n_ff;
@@ -752,6 +772,7 @@ void Session::prefill(const int32_t* tokens, int n, int pos) {
   if (const char* c = getenv("LLMI_PREFILL_CHUNK")) chunk = std::max(1, atoi(c));
   ensure_prefill_buffers(std::min(chunk, n));
   const int XS = pf_xs_;
+  const int r = tp_rank_;  // tensor parallel: this rank's column slices (0 on one device)
   const float emb_scale = std::sqrt(static_cast<float>(E));  // model.cpp:337-338
   for (int c0 = 0; c0 < n; c0 += pf_cap_) {
     const int T = std::min(pf_cap_, n - c0), p0 = pos + c0;
@@ -804,14 +825,17 @@ void Session::prefill(const int32_t* tokens, int n, int pos) {
       at.head_dim = hd;
       at.max_ctx = max_ctx_;
       at.pos0 = p0;
-      at.xq = pf_xq_;
+      const int hb = nh_ * hd / 32;  // this rank's heads' Q8_0 blocks per token
+      at.xq = pf_xq_ + (size_t)r * hb;
       at.xstride = XS;
       launch_prefill_attn(at, T, s);
+      if (tp_) gather_cols(pf_xq_, (size_t)XS * sizeof(XBlock), (size_t)hb * sizeof(XBlock), T, s);
       tap("pf_q", l, pf_q_, (size_t)T * nh_ * hd * 2, s);
       tap("kc", l, Ld.kc, (size_t)nkv_ * max_ctx_ * hd * 2, s);
       tap("vc", l, Ld.vc, (size_t)nkv_ * max_ctx_ * hd * 2, s);
       tap("pf_x_o", l, pf_xq_, (size_t)T * XS * sizeof(XBlock), s);
-      launch_prefill_gemm(Ld.o.w, pf_xq_, XS, T, pf_out_, E, s);
+      launch_prefill_gemm(Ld.o.w, pf_xq_, XS, T, pf_out_ + (size_t)r * e_sh_, E, s);
+      if (tp_) gather_cols(pf_out_, (size_t)E * 4, (size_t)e_sh_ * 4, T, s);
       tap("pf_o", l, pf_out_, (size_t)T * E * 4, s);
       PrefillNorm rn;  // post-attention norm + residual, then ffn_norm
       rn.y = pf_out_;
@@ -825,11 +849,15 @@ void Session::prefill(const int32_t* tokens, int n, int pos) {
       launch_prefill_norm(rn, T, s);
       tap("pf_resid_attn", l, pf_resid_, (size_t)T * E * 4, s);
       tap("pf_x_gate_up", l, pf_xq_, (size_t)T * XS * sizeof(XBlock), s);
-      launch_prefill_gemm(Ld.gate_up[0].w, pf_xq_, XS, T, pf_out_, 2 * F, s);
+      const int FL = tp_ ? f_sh_ : F;  // this rank's hidden units
+      launch_prefill_gemm(Ld.gate_up[0].w, pf_xq_, XS, T, pf_out_, 2 * FL, s);
       tap("pf_gate_up", l, pf_out_, (size_t)T * 2 * F * 4, s);
-      launch_prefill_gelu(pf_out_, F, layer_gemv_gelu_group(Ld.gate_up[0].w.cols, Ld.gate_up[0].w.type), pf_xq_, XS, T, s);
+      launch_prefill_gelu(pf_out_, FL, layer_gemv_gelu_group(Ld.gate_up[0].w.cols, Ld.gate_up[0].w.type),
+                          pf_xq_ + (size_t)r * (FL / 32), XS, T, s);
+      if (tp_) gather_cols(pf_xq_, (size_t)XS * sizeof(XBlock), (size_t)(FL / 32) * sizeof(XBlock), T, s);
       tap("pf_x_down", l, pf_xq_, (size_t)T * XS * sizeof(XBlock), s);
-      launch_prefill_gemm(Ld.down.w, pf_xq_, XS, T, pf_out_, E, s);
+      launch_prefill_gemm(Ld.down.w, pf_xq_, XS, T, pf_out_ + (size_t)r * e_sh_, E, s);
+      if (tp_) gather_cols(pf_out_, (size_t)E * 4, (size_t)e_sh_ * 4, T, s);
       tap("pf_down", l, pf_out_, (size_t)T * E * 4, s);
       if (l + 1 < hp_.n_layer) {  // post-ffw norm + residual, then the next attn_norm
         PrefillNorm fn = rn;

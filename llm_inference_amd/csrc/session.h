@@ -86,6 +86,7 @@ class Session {
   void record_step(hipStream_t s, bool gen = false);
   void record_logits(hipStream_t s, bool gen = false);  // xn_ / act_.x16 -> logits, argmax key, token feedback
   void prefill(const int32_t* tokens, int n, int pos);  // batched (k_prefill.hip)
+  void gather_cols(void* buf, size_t pitch_b, size_t slice_b, int T, hipStream_t s);
   void ensure_prefill_buffers(int cap);
   void record_layers(hipStream_t s, bool x_q8);
   void record_layers_fused(hipStream_t s, bool x_q8);
@@ -180,6 +181,7 @@ class Session {
   float *pf_resid_ = nullptr, *pf_out_ = nullptr;
   XBlock* pf_xq_ = nullptr;
   uint16_t* pf_q_ = nullptr;
+  uint8_t* pf_gather_ = nullptr;  // tensor parallel: all-gather staging of the prefill slices
 };
 
 }  // namespace llmi
