@@ -107,52 +107,102 @@ void launch_qk_norm_rope_kv(const QKVArgs& a, bool exact, hipStream_t s) {
 // accumulator rounded every step (vec_scale_f16 / vec_mad_f16).
 // expf is glibc's own algorithm (glibc_math.h), so the step is bit-exact.
 // ---------------------------------------------------------------------------
+// The serial loop is split into three exact parallel steps per chunk of keys:
+//  (1) scores: thread per key, the reference's sequential double sum;
+//  (2) the online max's decisions: the reference's running max after key j
+//      is always fl(R_j), fl = rounding to float, R_j = max(s_0..s_j) in
+//      double (induction over "s > (double)M ? M = (float)s" with monotone
+//      rounding), so an exclusive prefix max in double gives every key's
+//      branch and its e / pe (glibc expf) independently;
+//  (3) per head dim, the f16 accumulator over the chunk's keys in order, and
+//      s_acc = s_acc * pe + e in order (one thread).
+constexpr int ATTN_EX_CH = 1024;  // keys per chunk (LDS: scores f64 + e, pe, branch)
 __global__ __launch_bounds__(256) void attn_exact_kernel(AttnArgs a) {
-  __shared__ float s_prod[256];
-  __shared__ float s_e, s_pe;
-  __shared__ int s_resc;
+  __shared__ float s_q[256];
+  __shared__ double s_sc[ATTN_EX_CH];
+  __shared__ float s_e[ATTN_EX_CH], s_pe[ATTN_EX_CH];
+  __shared__ unsigned char s_up[ATTN_EX_CH];
+  __shared__ double s_tmax[256];
+  __shared__ float s_sacc;
   const int t = threadIdx.x, hd = a.head_dim;
   const int h = blockIdx.x;
   const int hkv = h / (a.n_head / a.n_head_kv);
   const int n_keys = *a.d_pos + 1;
-  const float q16 = t < hd ? h2f(f2h_ggml(a.q[(size_t)h * hd + t])) : 0.0f;
+  if (t < hd) s_q[t] = h2f(f2h_ggml(a.q[(size_t)h * hd + t]));
   uint16_t vacc = f2h_ggml(0.0f);
-  float s_acc = 0.0f, max_score = -INFINITY;
+  float s_acc = 0.0f;
+  double run_max = -INFINITY;  // R over the previous chunks
   const uint16_t* kb = a.k_cache + (size_t)hkv * a.max_ctx * hd;
   const uint16_t* vb = a.v_cache + (size_t)hkv * a.max_ctx * hd;
-  for (int tk = 0; tk < n_keys; tk++) {
-    if (t < hd) s_prod[t] = h2f(kb[(size_t)tk * hd + t]) * q16;
-    __syncthreads();
-    if (t == 0) {
-      double score = 0.0;
-      for (int i = 0; i < hd; i++) score += (double)s_prod[i];
-      const float prev = max_score;
-      float e, pe;
-      int resc;
-      if (score > (double)prev) {
-        max_score = (float)score;
-        e = 1.0f;
-        pe = llmi_glibc::expf(prev - max_score);
-        resc = 1;
-      } else {
-        e = llmi_glibc::expf((float)(score - (double)max_score));
-        pe = 1.0f;
-        resc = 0;
-      }
-      s_acc = s_acc * pe + e;
-      s_e = e; s_pe = pe; s_resc = resc;
-    }
-    __syncthreads();
-    if (t < hd) {
-      if (s_resc) vacc = f2h_ggml(h2f(vacc) * s_pe);
-      vacc = f2h_ggml(fmaf(h2f(vb[(size_t)tk * hd + t]), s_e, h2f(vacc)));
-    }
-    __syncthreads();
-  }
-  __shared__ float s_inv;
-  if (t == 0) s_inv = s_acc == 0.0f ? 0.0f : 1.0f / s_acc;
   __syncthreads();
-  if (t < hd) a.out[(size_t)h * hd + t] = h2f(vacc) * s_inv;
+  for (int c0 = 0; c0 < n_keys; c0 += ATTN_EX_CH) {
+    const int nk = min(ATTN_EX_CH, n_keys - c0);
+    // (1) scores, 4 consecutive keys per thread
+    constexpr int KPT = ATTN_EX_CH / 256;
+    double tmax = -INFINITY;
+    for (int k = 0; k < KPT; k++) {
+      const int j = t * KPT + k;
+      if (j >= nk) break;
+      const uint16_t* kr = kb + (size_t)(c0 + j) * hd;
+      double score = 0.0;
+      if (hd % 8 == 0) {  // 16-B loads of the row (rows are 16-B aligned), same summation order
+        for (int i = 0; i < hd; i += 8) {
+          const uint4 w = *reinterpret_cast<const uint4*>(kr + i);
+          const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+          for (int e = 0; e < 4; e++) {
+            score += (double)(h2f((uint16_t)(ww[e] & 0xFFFF)) * s_q[i + 2 * e]);
+            score += (double)(h2f((uint16_t)(ww[e] >> 16)) * s_q[i + 2 * e + 1]);
+          }
+        }
+      } else {
+        for (int i = 0; i < hd; i++) score += (double)(h2f(kr[i]) * s_q[i]);
+      }
+      s_sc[j] = score;
+      tmax = fmax(tmax, score);
+    }
+    s_tmax[t] = tmax;
+    __syncthreads();
+    // (2) exclusive prefix max over the threads' maxima (Hillis-Steele, max is exact), then per key
+    for (int o = 1; o < 256; o <<= 1) {
+      const double v = t >= o ? s_tmax[t - o] : -INFINITY;
+      __syncthreads();
+      s_tmax[t] = fmax(s_tmax[t], v);
+      __syncthreads();
+    }
+    double pm = fmax(run_max, t > 0 ? s_tmax[t - 1] : -INFINITY);  // max of every key before this thread's first
+    for (int k = 0; k < KPT; k++) {
+      const int j = t * KPT + k;
+      if (j >= nk) break;
+      const double score = s_sc[j];
+      const float prev = (float)pm;  // the reference's max_score before key j
+      if (score > (double)prev) {
+        s_e[j] = 1.0f;
+        s_pe[j] = llmi_glibc::expf(prev - (float)score);
+        s_up[j] = 1;
+      } else {
+        s_e[j] = llmi_glibc::expf((float)(score - (double)prev));
+        s_pe[j] = 1.0f;
+        s_up[j] = 0;
+      }
+      pm = fmax(pm, score);
+    }
+    run_max = fmax(run_max, s_tmax[255]);
+    __syncthreads();
+    // (3) the accumulators, keys in order
+    if (t < hd) {
+      for (int j = 0; j < nk; j++) {
+        if (s_up[j]) vacc = f2h_ggml(h2f(vacc) * s_pe[j]);
+        vacc = f2h_ggml(fmaf(h2f(vb[(size_t)(c0 + j) * hd + t]), s_e[j], h2f(vacc)));
+      }
+    }
+    if (t == 0)
+      for (int j = 0; j < nk; j++) s_acc = s_acc * s_pe[j] + s_e[j];
+    __syncthreads();  // the chunk's LDS is reused by the next one
+  }
+  if (t == 0) s_sacc = s_acc == 0.0f ? 0.0f : 1.0f / s_acc;
+  __syncthreads();
+  if (t < hd) a.out[(size_t)h * hd + t] = h2f(vacc) * s_sacc;
 }
 
 // ---------------------------------------------------------------------------
