@@ -26,13 +26,13 @@ want smoke && run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 want sweep && run gemv_sweep 300 scripts/gemv_sweep 200
 want ablate && run ablate_run 900 bash scripts/ablate.sh
 want bench && run bench 900 python bench.py
-if want prof; then
+if want prof; then  # the timed decode graph itself (hipGraph replay), after a 512-token prefill
   run rocprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- \
-    python3 bench.py --steps 64 --warmup 4 --prefill 512 --no-cpu-baseline --no-graph
+    python3 bench.py --steps 64 --warmup 4 --prefill 512 --no-cpu-baseline
 fi
 if want pmc; then
   run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- \
-    python3 bench.py --steps 16 --warmup 2 --prefill 64 --no-cpu-baseline --kernel-reps 1 --no-graph
+    python3 bench.py --steps 16 --warmup 2 --prefill 512 --no-cpu-baseline --kernel-reps 1
   python3 scripts/pmc_summary.py gpurun_out/pmc_fetch/run_counter_collection.csv gpurun_out/pmc_fetch_summary.json \
     > gpurun_out/pmc_summary.log 2>&1
 fi
