@@ -396,6 +396,52 @@ __device__ __forceinline__ void q8_block_quad(const float (&v)[8], int sub, XBlo
   }
 }
 
+// quantize_row_q8_k (ops.cpp:142-178) of one 256-element super-block held by a
+// half-wave (lanes 0-31 or 32-63), each DPP quad one 32-element block (lane
+// & 3 = sub owns elements 8 sub .. 8 sub + 7 of block (lane >> 2) & 7), into
+// 8 XBlocks in the K-quant convention: q = the Q8_K quants, d = the
+// super-block's d (the same in its 8 blocks), nsum8 = sum of the block's q
+// (the reference's bsums of its two 16-groups).  max: the signed value of the
+// first element with the largest |x| (strict > scan), as quantize_q8_k_kernel.
+// Every lane of the half-wave must execute it.
+__device__ __forceinline__ void q8k_block_quad(const float (&v)[8], int sub, XBlock* __restrict__ blk) {
+  const int e0 = ((int)(threadIdx.x >> 2) & 7) * 32 + sub * 8;
+  float ax = -1.0f, sv = 0.0f;
+  int ix = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++)
+    if (fabsf(v[k]) > ax) { ax = fabsf(v[k]); ix = e0 + k; sv = v[k]; }
+#pragma unroll
+  for (int o = 1; o < 32; o <<= 1) {
+    const float oa = __shfl_xor(ax, o), os = __shfl_xor(sv, o);
+    const int oi = __shfl_xor(ix, o);
+    if (oa > ax || (oa == ax && oi < ix)) { ax = oa; ix = oi; sv = os; }
+  }
+  uint32_t w0 = 0, w1 = 0;
+  int s = 0;
+  float d = 0.0f;
+  if (ax != 0.0f) {  // ops.cpp:158-163: an all-zero super-block stays 0
+    const float iscale = -127.f / sv;
+    d = 1.0f / iscale;
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      int q0 = nearest_int_fma(iscale, v[e]), q1 = nearest_int_fma(iscale, v[4 + e]);
+      q0 = q0 < -128 ? -128 : (q0 > 127 ? 127 : q0);
+      q1 = q1 < -128 ? -128 : (q1 > 127 ? 127 : q1);
+      s += q0 + q1;
+      w0 |= (uint32_t)(q0 & 0xFF) << (8 * e);
+      w1 |= (uint32_t)(q1 & 0xFF) << (8 * e);
+    }
+  }
+  s += dpp_i<DPP_QUAD_1032>(s);
+  s += dpp_i<DPP_QUAD_2301>(s);
+  reinterpret_cast<uint2*>(blk)[sub] = make_uint2(w0, w1);
+  if (sub == 0) {
+    blk->d = d;
+    blk->nsum8 = s;
+  }
+}
+
 // f / nb by multiply-high for the small f of one wave's chunk; nb == 1 has
 // no 32-bit magic and is encoded as 0
 __host__ __device__ inline uint32_t div_magic(uint32_t nb) { return nb == 1 ? 0u : (uint32_t)((1ull << 32) / nb + 1); }

@@ -655,7 +655,8 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, const QKVArgs
     for (int i = t; i < G * HD / 8; i += 256) {
       const float4 f0 = reinterpret_cast<const float4*>(s_out)[2 * i], f1 = reinterpret_cast<const float4*>(s_out)[2 * i + 1];
       const float vv[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
-      q8_block_quad(vv, i & 3, BLK ? s_q8 + (i >> 2) : a.q8 + (size_t)hkv * G * HD / 32 + (i >> 2));
+      if (!BLK && a.q8k) q8k_block_quad(vv, i & 3, a.q8 + (size_t)hkv * G * HD / 32 + (i >> 2));
+      else q8_block_quad(vv, i & 3, BLK ? s_q8 + (i >> 2) : a.q8 + (size_t)hkv * G * HD / 32 + (i >> 2));
     }
     if constexpr (BLK) {  // the blocks' words as granules for the o projection
       __syncthreads();
@@ -727,6 +728,8 @@ void launch_attention(const AttnArgs& a, bool exact, hipStream_t s, const QKVArg
   }
   if (a.n_head_kv <= 0 || a.n_head % a.n_head_kv != 0) throw std::runtime_error("attention: n_head % n_head_kv != 0");
   if (!a.partial || !a.ticket || !a.out) throw std::runtime_error("attention: missing partial / ticket / out buffer");
+  if (a.q8k && (a.n_head / a.n_head_kv) * a.head_dim % 256 != 0 && (a.n_head / a.n_head_kv) != 8)
+    throw std::runtime_error("attention: Q8_K output needs whole super-blocks per kv head");
   switch (a.head_dim) {
     case 16: launch_split<16>(a, fused, s); break;
     case 32: launch_split<32>(a, fused, s); break;

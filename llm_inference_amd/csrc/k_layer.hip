@@ -31,12 +31,25 @@ namespace llmi {
 
 namespace {
 
-template <int R, int NW, int P, int E, int ROLE, bool MULTI, bool EARLY, int PE = 0, bool W8 = false>
+template <int R, int NW, int P, int E, int ROLE, bool MULTI, bool EARLY, int PE = 0, bool W8 = false, int WT = 0>
 __global__ __launch_bounds__(NW * 64 + (role_help(ROLE) ? E * 64 : 0)) void gemv_q4_0_layer(LayerGemv a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
   // the attention block's granule tag of this layer, for its next launch
   if (a.epoch && blockIdx.x == 0 && threadIdx.x == 0) *a.epoch += 1u;
-  layer_body<R, NW, P, E, ROLE, MULTI, EARLY, 0, PE, W8>(a, blockIdx.x, s_dyn, BlockSync{});
+  layer_body<R, NW, P, E, ROLE, MULTI, EARLY, 0, PE, W8, WT>(a, blockIdx.x, s_dyn, BlockSync{});
+}
+
+// K-quant q|k|v of two weight types in one launch (Q4_K_M: q, k Q4_K, v Q6_K):
+// work-groups [0, nwg_a) stream the first weight, the rest the second; both
+// run the same prologue (b has no resid_out / xn_out: work-group 0 of a
+// publishes them)
+template <int R, int NW, int P, int E, int ROLE, bool EARLY, int PE, int WTA, int WTB>
+__global__ __launch_bounds__(NW * 64) void gemv_kq2_layer(LayerGemv a, LayerGemv b, int nwg_a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
+  if ((int)blockIdx.x < nwg_a)
+    layer_body<R, NW, P, E, ROLE, false, EARLY, 0, PE, false, WTA>(a, blockIdx.x, s_dyn, BlockSync{});
+  else
+    layer_body<R, NW, P, E, ROLE, false, EARLY, 0, PE, false, WTB>(b, blockIdx.x - nwg_a, s_dyn, BlockSync{});
 }
 
 // ---- launch table ----------------------------------------------------------
@@ -50,18 +63,32 @@ __global__ __launch_bounds__(NW * 64 + (role_help(ROLE) ? E * 64 : 0)) void gemv
 //      PRO/GELU -- prologue elements per thread (ceil(32 nb / 64 NW));
 //      QUANT -- rounds of 8-float quad lanes (ceil(4 nb / 64 NW)).
 using LaunchFn = void (*)(dim3, size_t, const LayerGemv&, hipStream_t);
+using Launch2Fn = void (*)(dim3, size_t, const LayerGemv&, const LayerGemv&, int, hipStream_t);
 
-template <int R, int NW, int P, int E, int ROLE, bool MULTI, bool EARLY, int PE = 0, bool W8 = false>
+template <int R, int NW, int P, int E, int ROLE, bool MULTI, bool EARLY, int PE = 0, bool W8 = false, int WT = 0>
 void launch_cfg(dim3 grid, size_t lds, const LayerGemv& a, hipStream_t s) {
   const dim3 block(NW * 64 + (role_help(ROLE) ? E * 64 : 0));
   KernelTiming& kt = kernel_timing();
   if (kt.start) {
-    hipExtLaunchKernelGGL((gemv_q4_0_layer<R, NW, P, E, ROLE, MULTI, EARLY, PE, W8>), grid, block, (uint32_t)lds, s,
-                          kt.start, kt.stop, 0u, a);
+    hipExtLaunchKernelGGL((gemv_q4_0_layer<R, NW, P, E, ROLE, MULTI, EARLY, PE, W8, WT>), grid, block, (uint32_t)lds,
+                          s, kt.start, kt.stop, 0u, a);
     kt = KernelTiming{};
     return;
   }
-  hipLaunchKernelGGL((gemv_q4_0_layer<R, NW, P, E, ROLE, MULTI, EARLY, PE, W8>), grid, block, lds, s, a);
+  hipLaunchKernelGGL((gemv_q4_0_layer<R, NW, P, E, ROLE, MULTI, EARLY, PE, W8, WT>), grid, block, lds, s, a);
+}
+
+template <int R, int NW, int P, int E, int ROLE, bool EARLY, int PE, int WTA, int WTB>
+void launch_cfg2(dim3 grid, size_t lds, const LayerGemv& a, const LayerGemv& b, int nwg_a, hipStream_t s) {
+  hipLaunchKernelGGL((gemv_kq2_layer<R, NW, P, E, ROLE, EARLY, PE, WTA, WTB>), grid, dim3(NW * 64), lds, s, a, b, nwg_a);
+}
+// the two-weight launch exists for the qkv roles of the Q4_K entries only
+template <int R, int NW, int P, int E, int ROLE, bool EARLY, int PE, int WT>
+constexpr Launch2Fn fn2_of() {
+  if constexpr ((ROLE == ROLE_PRO || ROLE == ROLE_PLAIN) && WT == WT_Q4_K)
+    return launch_cfg2<R, NW, P, E, ROLE, EARLY, PE, WT_Q4_K, WT_Q6_K>;
+  else
+    return nullptr;
 }
 
 struct LayerCfg {
@@ -71,6 +98,8 @@ struct LayerCfg {
   bool help;  // PRO/GELU with E helper waves (role_help)
   LaunchFn fn;
   bool w8 = false;  // Q8_0 weights (P counts half-block passes)
+  int wt = 0;       // kq weights: WT_Q4_K / WT_Q6_K
+  Launch2Fn fn2 = nullptr;  // kq: q|k Q4_K + v Q6_K in one launch (PRO / PLAIN qkv entries)
 };
 
 #define LLMI_LCFG(NB, ROLE, R, NW, P, E, MULTI, EARLY, SLAB) \
@@ -79,6 +108,12 @@ struct LayerCfg {
 #define LLMI_LCFGP(NB, ROLE, R, NW, P, E, SLAB, PE) \
   {NB, ROLE, R, NW, P, E, false, SLAB, false, launch_cfg<R, NW, P, E, ROLE, false, false, PE>}
 // Q8_0 weights: row-major, single chunk (P passes of 16-B half blocks)
+// kq entries, one per weight type (+ the q|k Q4_K, v Q6_K launch for qkv roles)
+#define LLMI_LCFGK1(NB, ROLE, R, NW, P, E, EARLY, PE, WT)                                          \
+  {NB, ROLE, R, NW, P, E, false, 0, false, launch_cfg<R, NW, P, E, ROLE, false, EARLY, PE, false, WT>, false, WT, \
+   fn2_of<R, NW, P, E, ROLE, EARLY, PE, WT>()}
+#define LLMI_LCFGK(NB, ROLE, R, NW, P, E, EARLY, PE)              \
+  LLMI_LCFGK1(NB, ROLE, R, NW, P, E, EARLY, PE, WT_Q4_K), LLMI_LCFGK1(NB, ROLE, R, NW, P, E, EARLY, PE, WT_Q6_K)
 #define LLMI_LCFG8(NB, ROLE, R, NW, P, E, EARLY) \
   {NB, ROLE, R, NW, P, E, false, 0, false, launch_cfg<R, NW, P, E, ROLE, false, EARLY, 0, true>, true}
 // PRO / GELU entries with NH helper waves (template role ROLE_PRO_H / ROLE_GELU_H)
@@ -120,13 +155,22 @@ const LayerCfg kLayerCfgs[] = {
     LLMI_LCFG8(32, ROLE_PLAIN, 1, 4, 1, 1, true),     // 1B o        1152 rows -> 288 WGs
     LLMI_LCFG8(36, ROLE_GELU, 8, 8, 9, 3, false),     // 1B gate_up  13824 rows, H 32 -> 216 WGs
     LLMI_LCFG8(216, ROLE_QUANT, 1, 4, 7, 4, true),    // 1B down     1152 rows -> 288 WGs
+    // K-quant weights in the kq layout (Gemma-3 4B Q4_K_M, BASELINE configs[3]): the Q4_0 4B
+    // geometry (a 32-element sub-block per 16-B unit, as a Q4_0 block), row-major
+    LLMI_LCFGK(80, ROLE_PLAIN, 4, 4, 5, 1, true, 0),      // 4B qkv l0   4096 rows -> 256 WGs
+    LLMI_LCFGK(80, ROLE_PRO, 4, 4, 5, 10, true, 0),       // 4B qkv      256 WGs
+    LLMI_LCFGK(64, ROLE_PLAIN, 1, 10, 1, 1, true, 0),     // 4B o        2560 rows -> 256 WGs
+    LLMI_LCFGK(80, ROLE_GELU, 8, 10, 10, 4, false, 7),    // 4B gate_up  20480 rows, H 40 -> 256 WGs
+    LLMI_LCFGK(320, ROLE_QUANT, 1, 10, 5, 2, false, 3),   // 4B down     2560 rows -> 256 WGs
 };
 #undef LLMI_LCFG
 
+int wt_of(uint32_t type) { return type == T_Q4_K ? WT_Q4_K : type == T_Q6_K ? WT_Q6_K : 0; }
+
 const LayerCfg* find_cfg(int nb, int role, uint32_t type = T_Q4_0) {
-  if (type != T_Q4_0 && type != T_Q8_0) return nullptr;
+  if (type != T_Q4_0 && type != T_Q8_0 && type != T_Q4_K && type != T_Q6_K) return nullptr;
   for (const auto& c : kLayerCfgs)
-    if (c.nb == nb && c.role == role && c.w8 == (type == T_Q8_0)) return &c;
+    if (c.nb == nb && c.role == role && c.w8 == (type == T_Q8_0) && c.wt == wt_of(type)) return &c;
   return nullptr;
 }
 
@@ -142,7 +186,8 @@ KernelTiming& kernel_timing() {
 }
 
 bool layer_gemv_supported(const DevWeight& w, int role) {
-  if ((w.type != T_Q4_0 && w.type != T_Q8_0) || w.cols % 32 != 0 || w.rows <= 0) return false;
+  const bool k = w.type == T_Q4_K || w.type == T_Q6_K;
+  if ((w.type != T_Q4_0 && w.type != T_Q8_0 && !k) || w.cols % (k ? 256 : 32) != 0 || w.rows <= 0) return false;
   const LayerCfg* c = find_cfg(w.cols / 32, role, w.type);
   if (!c) return false;
   if (role == LAYER_GELU && w.rows % (c->R * c->NW) != 0) return false;
@@ -178,8 +223,11 @@ void launch_layer_gemv(const DevWeight& w, LayerGemv a, int role, hipStream_t s)
   if (role == LAYER_PLAIN && 3 * nb > c.E * c.NW * 64) throw std::runtime_error("layer gemv: x copy E too small");
   if (role == LAYER_QUANT && 4 * nb > c.E * c.NW * 64) throw std::runtime_error("layer gemv: quant E too small");
   if (w.slab != c.slab) throw std::runtime_error("layer gemv: weight layout does not match the launch table");
+  if (c.wt && !w.kq) throw std::runtime_error("layer gemv: K-quant weight not in the kq layout");
   a.qs = reinterpret_cast<const uint4*>(w.qs);
   a.wd = w.d;
+  a.kdd = w.kdd;
+  a.kqh = w.kqh;
   a.slab = w.slab;
   a.rows = w.rows;
   a.nb = nb;
@@ -189,6 +237,69 @@ void launch_layer_gemv(const DevWeight& w, LayerGemv a, int role, hipStream_t s)
   const size_t lds = (size_t)nb * sizeof(XBlock) + 16 + (pro ? (size_t)w.cols * 4 : 0);
   const int rows_per_wg = c.NW * c.R;
   c.fn(dim3((w.rows + rows_per_wg - 1) / rows_per_wg), lds, a, s);
+  LLMI_HIP(hipGetLastError());
+}
+
+// q|k (Q4_K) and v (Q6_K) rows of one q|k|v projection in one launch: the
+// outputs are contiguous (b's rows follow a's)
+bool layer_gemv2_supported(const DevWeight& wa, const DevWeight& wb, int role) {
+  if (wa.type != T_Q4_K || wb.type != T_Q6_K || wa.cols != wb.cols || wa.cols % 256) return false;
+  if (!layer_gemv_supported(wa, role) || !layer_gemv_supported(wb, role)) return false;
+  const LayerCfg* c = find_cfg(wa.cols / 32, role, wa.type);
+  return c && c->fn2 && wa.rows % (c->NW * c->R) == 0;
+}
+
+void launch_layer_gemv2(const DevWeight& wa, const DevWeight& wb, LayerGemv a, int role, hipStream_t s) {
+  if (!layer_gemv2_supported(wa, wb, role) || !wa.kq || !wb.kq) throw std::runtime_error("layer gemv2: unsupported");
+  if (role == LAYER_PRO && (!a.y || !a.resid_in || !a.resid_out || !a.w_next || a.resid_in == a.resid_out))
+    throw std::runtime_error("layer gemv2: missing prologue operand");
+  if (role == LAYER_PLAIN && !a.xg) throw std::runtime_error("layer gemv2: missing activation blocks");
+  if (role != LAYER_PRO && role != LAYER_PLAIN) throw std::runtime_error("layer gemv2: qkv roles only");
+  const LayerCfg& c = *find_cfg(wa.cols / 32, role, wa.type);
+  const int nb = wa.cols / 32;
+  if ((nb + 64 / c.R - 1) / (64 / c.R) > c.P) throw std::runtime_error("layer gemv2: P too small");
+  if (role == LAYER_PRO && wa.cols > c.E * c.NW * 64) throw std::runtime_error("layer gemv2: prologue E too small");
+  if (role == LAYER_PLAIN && 3 * nb > c.E * c.NW * 64) throw std::runtime_error("layer gemv2: x copy E too small");
+  a.rows = wa.rows;
+  a.nb = nb;
+  a.magic = div_magic(nb);
+  a.n = wa.cols;
+  a.slab = 0;
+  LayerGemv b = a;
+  a.qs = reinterpret_cast<const uint4*>(wa.qs);
+  a.wd = wa.d;
+  a.kdd = wa.kdd;
+  a.kqh = wa.kqh;
+  b.qs = reinterpret_cast<const uint4*>(wb.qs);
+  b.wd = wb.d;
+  b.kdd = wb.kdd;
+  b.kqh = wb.kqh;
+  b.rows = wb.rows;
+  b.out = a.out + wa.rows;
+  b.resid_out = nullptr;
+  b.xn_out = nullptr;
+  b.epoch = nullptr;
+  const int rpw = c.NW * c.R, nwa = wa.rows / rpw, nwb = (wb.rows + rpw - 1) / rpw;
+  const size_t lds = (size_t)nb * sizeof(XBlock) + 16 + (role == LAYER_PRO ? (size_t)wa.cols * 4 : 0);
+  c.fn2(dim3(nwa + nwb), lds, a, b, nwa, s);
+  LLMI_HIP(hipGetLastError());
+}
+
+// x -> Q8_K quants in XBlocks (q8k_block_quad: d = super-block d, nsum8 = block sum) for a
+// PLAIN kq launch; 64 threads = 2 super-blocks per work-group, n % 256 == 0
+__global__ __launch_bounds__(64) void quantize_q8k_xblocks_kernel(const float* __restrict__ x, int n,
+                                                                   XBlock* __restrict__ xb) {
+  const int t = threadIdx.x, sbk = blockIdx.x * 2 + (t >> 5);
+  const bool ok = sbk * 256 < n;  // whole half-waves in or out
+  const int b = sbk * 8 + ((t >> 2) & 7), sub = t & 3;
+  float v[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) v[k] = ok ? x[b * 32 + sub * 8 + k] : 0.0f;
+  if (ok) q8k_block_quad(v, sub, xb + b);
+}
+void launch_quantize_q8k_xblocks(const float* x, int n, XBlock* xb, hipStream_t s) {
+  if (n % 256) throw std::runtime_error("quantize_q8k_xblocks: n % 256 != 0");
+  hipLaunchKernelGGL(quantize_q8k_xblocks_kernel, dim3((n / 256 + 1) / 2), dim3(64), 0, s, x, n, xb);
   LLMI_HIP(hipGetLastError());
 }
 

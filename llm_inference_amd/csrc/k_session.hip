@@ -132,8 +132,107 @@ void to_slab_layout(DevWeight& w, hipStream_t s) {
 void free_weight(DevWeight& w) {
   if (w.qs) (void)hipFree(w.qs);
   if (w.d) (void)hipFree(w.d);
+  if (w.kdd) (void)hipFree(w.kdd);
+  if (w.kqh) (void)hipFree(w.kqh);
   w.qs = nullptr;
   w.d = nullptr;
+  w.kdd = nullptr;
+  w.kqh = nullptr;
+}
+
+// ---- GGUF K-quant rows -> the kq layout (kernels.h), one thread per sub-block
+__device__ __forceinline__ void kq_scale_min(int j, const uint8_t* q, int& d, int& m) {  // get_scale_min_k4 (ops.cpp)
+  if (j < 4) {
+    d = q[j] & 63;
+    m = q[j + 4] & 63;
+  } else {
+    d = (q[j + 4] & 0xF) | ((q[j - 4] >> 6) << 4);
+    m = (q[j + 4] >> 4) | ((q[j] >> 6) << 4);
+  }
+}
+
+__global__ void repack_q4_k_kernel(const uint8_t* __restrict__ src, size_t n_sub, uint4* __restrict__ qs,
+                                   uint16_t* __restrict__ sc, uint32_t* __restrict__ dd) {
+  const size_t u = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // sub-block (row-major: row * nsub + j)
+  if (u >= n_sub) return;
+  const size_t sbk = u / 8;
+  const int j = (int)(u % 8);
+  const uint8_t* b = src + sbk * 144;
+  const uint8_t* q = b + 16 + 32 * (j / 2);
+  const int sh = (j & 1) * 4;
+  uint32_t w[4];
+  for (int k = 0; k < 4; k++) {
+    uint32_t v = 0;
+    for (int i = 0; i < 4; i++) {
+      const int e = 4 * k + i;  // byte e: element e (low nibble), element 16 + e (high nibble)
+      v |= (uint32_t)(((q[e] >> sh) & 0xF) | (((q[16 + e] >> sh) & 0xF) << 4)) << (8 * i);
+    }
+    w[k] = v;
+  }
+  qs[u] = make_uint4(w[0], w[1], w[2], w[3]);
+  int d6, m6;
+  kq_scale_min(j, b + 4, d6, m6);
+  sc[u] = (uint16_t)(d6 | (m6 << 8));
+  if (j == 0) dd[sbk] = (uint32_t)b[0] | ((uint32_t)b[1] << 8) | ((uint32_t)b[2] << 16) | ((uint32_t)b[3] << 24);
+}
+
+__global__ void repack_q6_k_kernel(const uint8_t* __restrict__ src, size_t n_sub, uint4* __restrict__ qs,
+                                   uint16_t* __restrict__ sc, uint32_t* __restrict__ dd, uint2* __restrict__ qh) {
+  const size_t u = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= n_sub) return;
+  const size_t sbk = u / 8;
+  const int m = (int)(u % 8), n = m / 4, jq = m % 4;
+  const uint8_t* b = src + sbk * 210;
+  const uint8_t* ql = b + 64 * n + 32 * (jq & 1);
+  const uint8_t* qhb = b + 128 + 32 * n;
+  auto q6 = [&](int l) {  // element l of the sub-block, 0..63
+    return ((ql[l] >> (4 * (jq >> 1))) & 0xF) | (((qhb[l] >> (2 * jq)) & 3) << 4);
+  };
+  uint32_t w[4];
+  uint32_t h[2] = {0u, 0u};
+  for (int k = 0; k < 4; k++) {
+    uint32_t v = 0;
+    for (int i = 0; i < 4; i++) {
+      const int e = 4 * k + i;
+      const int lo = q6(e), hi = q6(16 + e);
+      v |= (uint32_t)((lo & 0xF) | ((hi & 0xF) << 4)) << (8 * i);
+      h[0] |= (uint32_t)(lo >> 4) << (8 * i + 2 * k);
+      h[1] |= (uint32_t)(hi >> 4) << (8 * i + 2 * k);
+    }
+    w[k] = v;
+  }
+  qs[u] = make_uint4(w[0], w[1], w[2], w[3]);
+  qh[u] = make_uint2(h[0], h[1]);
+  const uint8_t* scb = b + 192 + 8 * n + 2 * jq;
+  sc[u] = (uint16_t)(scb[0] | (scb[1] << 8));
+  if (m == 0) dd[sbk] = (uint32_t)b[208] | ((uint32_t)b[209] << 8);
+}
+
+void to_kq_layout(DevWeight& w, hipStream_t s) {
+  if ((w.type != T_Q4_K && w.type != T_Q6_K) || w.kq || w.cols % 256) throw std::runtime_error("to_kq_layout: weight");
+  const size_t nsb = (size_t)w.rows * (w.cols / 256), nsub = nsb * 8;
+  uint4* qs;
+  uint16_t* sc;
+  uint32_t* dd;
+  uint2* qh = nullptr;
+  LLMI_HIP(hipMalloc(&qs, nsub * 16 + 64));
+  LLMI_HIP(hipMalloc(&sc, nsub * 2 + 64));
+  LLMI_HIP(hipMalloc(&dd, nsb * 4 + 64));
+  const dim3 grid((unsigned)((nsub + 255) / 256));
+  if (w.type == T_Q4_K) {
+    hipLaunchKernelGGL(repack_q4_k_kernel, grid, dim3(256), 0, s, (const uint8_t*)w.qs, nsub, qs, sc, dd);
+  } else {
+    LLMI_HIP(hipMalloc(&qh, nsub * 8 + 64));
+    hipLaunchKernelGGL(repack_q6_k_kernel, grid, dim3(256), 0, s, (const uint8_t*)w.qs, nsub, qs, sc, dd, qh);
+  }
+  LLMI_HIP(hipGetLastError());
+  LLMI_HIP(hipStreamSynchronize(s));
+  LLMI_HIP(hipFree(w.qs));
+  w.qs = qs;
+  w.d = sc;
+  w.kdd = dd;
+  w.kqh = qh;
+  w.kq = 1;
 }
 
 // ---------------------------------------------------------------------------

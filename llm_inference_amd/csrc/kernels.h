@@ -12,13 +12,22 @@ namespace llmi {
 // Q8_0 : qs [rows][nb][32] B (16-B aligned), d [rows][nb] f16
 // F16  : [rows][cols] f16 (cols % 8 == 0 for the vector kernels)
 // Q4_K / Q6_K / Q5_0 / BF16 : the GGUF block bytes, unchanged
+// Q4_K / Q6_K, kq (fused fast path, to_kq_layout): 32-element sub-blocks u
+//   qs  [rows][nsub][16] B  nibbles in the Q4_0 order (byte i: elements i, 16 + i)
+//   d   [rows][nsub] u16    Q4_K: 6-bit scale | 6-bit min << 8; Q6_K: int8 scales of elements 0-15 | 16-31 << 8
+//   kdd [rows][nsb] u32     Q4_K: f16 d | f16 dmin << 16; Q6_K: f16 d
+//   kqh [rows][nsub] 8 B    Q6_K: the high 2 bits, word w of elements 4w + b (b = byte) at bits 8b + 2w
+//                           (first dword: elements 0-15, second: 16-31)
 struct DevWeight {
   uint32_t type = 0;
   int rows = 0, cols = 0;
   void* qs = nullptr;      // quants (or raw blocks / f16 / bf16 data)
-  uint16_t* d = nullptr;   // per-block scales (Q4_0/Q8_0 only)
+  uint16_t* d = nullptr;   // per-block scales (Q4_0/Q8_0 only; kq: per sub-block scale words)
   size_t bytes = 0;        // algorithmic bytes (GGUF size of the tensor)
   int slab = 0;            // Q4_0 only: 1 = slab-major blocks (to_slab_layout; layer kernels only)
+  int kq = 0;              // Q4_K / Q6_K: 1 = the kq layout above (layer kernels only)
+  uint32_t* kdd = nullptr;
+  uint2* kqh = nullptr;
 };
 
 // Activation prepared for a weight type (device scratch):

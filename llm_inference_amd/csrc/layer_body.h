@@ -163,6 +163,84 @@ __device__ __forceinline__ void eat_chunk_rb(const Chunk<P>& c, int pass0, int n
   }
 }
 
+// ---- K-quant weights in the kq layout (kernels.h): WT 1 = Q4_K, 2 = Q6_K ----
+// A lane's 16-B unit is one 32-element sub-block u (like a Q4_0 block), plus
+// its scale word (the Chunk's sw), the super-block's d / dmin word and, for
+// Q6_K, the 8 bytes of high bits.  The activation blocks in LDS hold Q8_K
+// quants (q8k_block_quad: d = the super-block's d, nsum8 = the block's sum).
+enum { WT_Q4_0 = 0, WT_Q4_K = 1, WT_Q6_K = 2 };
+template <int P, int WT>
+struct ChunkX : Chunk<P> {
+  uint32_t dd[WT ? P : 1];
+  uint2 qh[WT == WT_Q6_K ? P : 1];
+};
+struct KqOff {  // lane offsets (bytes) and per-pass strides of the four kq arrays
+  __amdgpu_buffer_rsrc_t rdd, rqh;
+  int vdd, vqh, sdd, sqh;
+};
+template <int P, int WT, int P0, int P1>
+__device__ __forceinline__ void load_chunk_kq(ChunkX<P, WT>& c, __amdgpu_buffer_rsrc_t rq, __amdgpu_buffer_rsrc_t rd,
+                                              const KqOff& k, int voq, int vod, int sq, int sd, int pass0, int npass) {
+#pragma unroll
+  for (int p = P0; p < P1; p++) {
+    const int pi = pass0 + p;
+    const bool in = pi < npass;
+    c.q[p] = buf_ld16(rq, in ? voq + pi * sq : (1 << 30), 0);
+    c.sw[p] = buf_ld2(rd, in ? vod + pi * sd : (1 << 30), 0);
+    c.dd[p] = __builtin_amdgcn_raw_buffer_load_b32(k.rdd, in ? k.vdd + pi * k.sdd : (1 << 30), 0, BUF_NT);
+    if constexpr (WT == WT_Q6_K) {
+      typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+      const u32x2_t h = __builtin_amdgcn_raw_buffer_load_b64(k.rqh, in ? k.vqh + pi * k.sqh : (1 << 30), 0, BUF_NT);
+      c.qh[p] = make_uint2(h.x, h.y);
+    }
+  }
+}
+__device__ __forceinline__ int q6_bytes(uint32_t nib4, uint32_t h, int k) {  // 4 six-bit values - 32, as signed bytes
+  const uint32_t v = nib4 | (((h >> (2 * k)) & 0x03030303u) << 4);  // 0..63 per byte
+  return (int)((v + 0x60606060u) ^ 0x80808080u);
+}
+template <int R, int P, int WT>
+__device__ __forceinline__ void eat_chunk_kq(const ChunkX<P, WT>& c, int pass0, int nb, int j, bool row_ok,
+                                             const XBlock* s_x, float& acc) {
+  constexpr int L = 64 / R;
+#pragma unroll
+  for (int p = 0; p < P; p++) {
+    const int u = (pass0 + p) * L + j;
+    const bool ok = row_ok && u < nb;
+    const int4* xp = reinterpret_cast<const int4*>(s_x + (u < nb ? u : nb - 1));
+    const int4 x0 = xp[0], x1 = xp[1], x2 = xp[2];
+    const float xd = __int_as_float(x2.x);
+    const uint4 q = c.q[p];
+    float v;
+    if constexpr (WT == WT_Q4_K) {  // ops.cpp:614-697: fmaf(d sc, isum, -(dmin m bsum)) per sub-block
+      int is = sdot4(nib_lo(q.x), x0.x, 0);
+      is = sdot4(nib_lo(q.y), x0.y, is);
+      is = sdot4(nib_lo(q.z), x0.z, is);
+      is = sdot4(nib_lo(q.w), x0.w, is);
+      is = sdot4(nib_hi(q.x), x1.x, is);
+      is = sdot4(nib_hi(q.y), x1.y, is);
+      is = sdot4(nib_hi(q.z), x1.z, is);
+      is = sdot4(nib_hi(q.w), x1.w, is);
+      const float d = h2f((uint16_t)(c.dd[p] & 0xFFFF)) * xd, mn = h2f((uint16_t)(c.dd[p] >> 16)) * xd;
+      v = fmaf(d * (float)(c.sw[p] & 0xFF), (float)is, -((mn * (float)(c.sw[p] >> 8)) * (float)x2.y));
+    } else {  // Q6_K (ops.cpp:699-785): d * (sc0 isum0 + sc1 isum1), elements 0-15 / 16-31
+      const uint2 h = c.qh[p];
+      int i0 = sdot4(q6_bytes((uint32_t)nib_lo(q.x), h.x, 0), x0.x, 0);
+      i0 = sdot4(q6_bytes((uint32_t)nib_lo(q.y), h.x, 1), x0.y, i0);
+      i0 = sdot4(q6_bytes((uint32_t)nib_lo(q.z), h.x, 2), x0.z, i0);
+      i0 = sdot4(q6_bytes((uint32_t)nib_lo(q.w), h.x, 3), x0.w, i0);
+      int i1 = sdot4(q6_bytes((uint32_t)nib_hi(q.x), h.y, 0), x1.x, 0);
+      i1 = sdot4(q6_bytes((uint32_t)nib_hi(q.y), h.y, 1), x1.y, i1);
+      i1 = sdot4(q6_bytes((uint32_t)nib_hi(q.z), h.y, 2), x1.z, i1);
+      i1 = sdot4(q6_bytes((uint32_t)nib_hi(q.w), h.y, 3), x1.w, i1);
+      const int part = (int)(int8_t)(c.sw[p] & 0xFF) * i0 + (int)(int8_t)(c.sw[p] >> 8) * i1;
+      v = (h2f((uint16_t)(c.dd[p] & 0xFFFF)) * xd) * (float)part;
+    }
+    acc += ok ? v : 0.0f;
+    asm volatile("" ::: "memory");
+  }
+}
+
 // sum over each row's L lanes; row k's total ends up in lane k L (R >= 4) or
 // is returned for every k through `tot` (R <= 2)
 template <int R>
@@ -222,7 +300,10 @@ constexpr int HELP_K4 = 6;  // float4 per helper lane and operand: n <= E * 256 
 // CU's first weight bytes stream during the prologue without stalling its
 // waves at the issue (PE small against the CU's in-flight capacity).
 // W8: Q8_0 weights (qs [rows][nb][32 B], row-major) instead of Q4_0.
-template <int R, int NW, int P, int E, int ROLE, bool MULTI, bool EARLY, int SYNC = 0, int PE = 0, bool W8 = false>
+// WT: K-quant weights in the kq layout (WT_Q4_K / WT_Q6_K; row-major, single
+// chunk, R <= 8): the activation blocks hold Q8_K quants (q8k_block_quad).
+template <int R, int NW, int P, int E, int ROLE, bool MULTI, bool EARLY, int SYNC = 0, int PE = 0, bool W8 = false,
+          int WT = 0>
 __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, unsigned char* s_dyn,
                                            const BlockSync& bs) {
   constexpr bool HELP = role_help(ROLE);
@@ -233,6 +314,7 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
   constexpr int L = RB ? 64 / R : 64;
   static_assert(PE == 0 || (RB && !MULTI && !EARLY && PE < P), "PE: single-chunk row-bound late roles");
   static_assert(!W8 || (RB && R <= 16), "W8: row-bound lanes");
+  static_assert(WT == 0 || (RB && R <= 8 && !MULTI && !HELP && !W8 && SYNC == 0), "kq: single-chunk row-bound lanes");
   LAYER_MARK(0);
   BLK_MARK(bs, 0);
   constexpr int EPT = E, X_LD = E;
@@ -268,7 +350,24 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
   const int wrows = max(0, a.rows - wrow0);
   __amdgpu_buffer_rsrc_t rq, rd;
   int voq, vod, sq, sd;
-  if (a.slab) {
+  KqOff kq{};
+  if constexpr (WT != 0) {  // kq layout: row-major sub-blocks, super-block words, Q6_K high bits
+    const int nsb = nb / 8;
+    rq = buf_rsrc(a.qs + (size_t)min(wrow0, a.rows) * nb, (uint32_t)wrows * nb * 16);
+    rd = buf_rsrc(a.wd + (size_t)min(wrow0, a.rows) * nb, (uint32_t)wrows * nb * 2);
+    voq = (rk * nb + rj) * 16;
+    vod = (rk * nb + rj) * 2;
+    sq = L * 16;
+    sd = L * 2;
+    kq.rdd = buf_rsrc(a.kdd + (size_t)min(wrow0, a.rows) * nsb, (uint32_t)wrows * nsb * 4);
+    kq.vdd = (rk * nsb + (rj >> 3)) * 4;
+    kq.sdd = (L / 8) * 4;
+    if constexpr (WT == WT_Q6_K) {
+      kq.rqh = buf_rsrc(a.kqh + (size_t)min(wrow0, a.rows) * nb, (uint32_t)wrows * nb * 8);
+      kq.vqh = (rk * nb + rj) * 8;
+      kq.sqh = L * 8;
+    }
+  } else if (a.slab) {
     rq = buf_rsrc(a.qs, (uint32_t)a.rows * nb * 16);
     rd = buf_rsrc(a.wd, (uint32_t)a.rows * nb * 2);
     const int r = wrow0 + rk;
@@ -294,9 +393,11 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
   }
   const int npass = ((W8 ? 2 * nb : nb) + L - 1) / L;
 
-  Chunk<P> ca, cb;
+  ChunkX<P, WT> ca, cb;
   auto issue_weights = [&]() {
-    if constexpr (RB) {
+    if constexpr (WT != 0) {
+      load_chunk_kq<P, WT, 0, P>(ca, rq, rd, kq, voq, vod, sq, sd, 0, npass);
+    } else if constexpr (RB) {
       load_chunk_rb<R, P>(ca, rq, rd, voq, vod, sq, sd, 0, npass);
       if constexpr (MULTI) load_chunk_rb<R, P>(cb, rq, rd, voq, vod, sq, sd, P, npass);
     } else {
@@ -305,10 +406,12 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
     }
   };
   auto issue_head = [&]() {  // passes [0, PE)
-    if constexpr (PE > 0) load_chunk_rb_part<R, P, 0, PE>(ca, rq, rd, voq, vod, sq, sd, npass);
+    if constexpr (PE > 0 && WT != 0) load_chunk_kq<P, WT, 0, PE>(ca, rq, rd, kq, voq, vod, sq, sd, 0, npass);
+    else if constexpr (PE > 0) load_chunk_rb_part<R, P, 0, PE>(ca, rq, rd, voq, vod, sq, sd, npass);
   };
   auto issue_tail = [&]() {  // passes [PE, P), or everything
-    if constexpr (PE > 0) load_chunk_rb_part<R, P, PE, P>(ca, rq, rd, voq, vod, sq, sd, npass);
+    if constexpr (PE > 0 && WT != 0) load_chunk_kq<P, WT, PE, P>(ca, rq, rd, kq, voq, vod, sq, sd, 0, npass);
+    else if constexpr (PE > 0) load_chunk_rb_part<R, P, PE, P>(ca, rq, rd, voq, vod, sq, sd, npass);
     else issue_weights();
   };
   const bool helper = HELP && w >= NW;
@@ -478,7 +581,7 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
           ss2 = fmaf(r.y, r.y, ss2);
           ss2 = fmaf(r.z, r.z, ss2);
           ss2 = fmaf(r.w, r.w, ss2);
-          if (bid == 0) *reinterpret_cast<float4*>(a.resid_out + (t / 4 + k * QB) * 32 + sub * 8 + 4 * h) = r;
+          if (bid == 0 && a.resid_out) *reinterpret_cast<float4*>(a.resid_out + (t / 4 + k * QB) * 32 + sub * 8 + 4 * h) = r;
         }
       }
     }
@@ -496,9 +599,10 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
         v[4 * h + 2] = (sc2 * r.z) * wn.z;
         v[4 * h + 3] = (sc2 * r.w) * wn.w;
       }
-      if (in_row(k)) {  // whole quads (one block per quad)
+      if (in_row(k)) {  // whole quads (one block per quad); kq: whole half-waves (one super-block each)
         const int b = t / 4 + k * QB;
-        q8_block_quad(v, sub, s_x + b);
+        if constexpr (WT != 0) q8k_block_quad(v, sub, s_x + b);
+        else q8_block_quad(v, sub, s_x + b);
         if (bid == 0 && a.xn_out) {
           *reinterpret_cast<float4*>(a.xn_out + b * 32 + sub * 8) = make_float4(v[0], v[1], v[2], v[3]);
           *reinterpret_cast<float4*>(a.xn_out + b * 32 + sub * 8 + 4) = make_float4(v[4], v[5], v[6], v[7]);
@@ -524,7 +628,10 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
       if (r * T < 4 * nb) {  // uniform: whole quads are in or out together (4 nb, T multiples of 4)
         const float v[8] = {xr[r][0].x, xr[r][0].y, xr[r][0].z, xr[r][0].w,
                             xr[r][1].x, xr[r][1].y, xr[r][1].z, xr[r][1].w};
-        if (i < 4 * nb) q8_block_quad(v, i & 3, s_x + (i >> 2));
+        if (i < 4 * nb) {
+          if constexpr (WT != 0) q8k_block_quad(v, i & 3, s_x + (i >> 2));
+          else q8_block_quad(v, i & 3, s_x + (i >> 2));
+        }
       }
     }
   } else {
@@ -571,7 +678,8 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
     if (helper) {
       // helpers have no rows
     } else if constexpr (!MULTI) {
-      if constexpr (W8) eat_chunk_rb_w8<R, P>(ca, 0, nb, rj, row_ok, s_x, acc1);
+      if constexpr (WT != 0) eat_chunk_kq<R, P, WT>(ca, 0, nb, rj, row_ok, s_x, acc1);
+      else if constexpr (W8) eat_chunk_rb_w8<R, P>(ca, 0, nb, rj, row_ok, s_x, acc1);
       else eat_chunk_rb<R, P>(ca, 0, nb, rj, row_ok, s_x, acc1);
     } else {
       // unconditional loads (out-of-range passes return 0 without traffic):

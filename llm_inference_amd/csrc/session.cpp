@@ -279,7 +279,7 @@ void Session::upload(const GGUFView& g) {  // model.cpp:169-238 tensor map
     };
     const bool qkv_same = Ld.has_kv && q->type == k->type && q->type == v->type && q->shape[0] == k->shape[0] &&
                           q->shape[0] == v->shape[0];
-    const bool want_fused =
+    bool want_fused =
         fuse_layers_ && qkv_same && (gt->type == T_Q4_0 || gt->type == T_Q8_0) && up->type == gt->type &&
         gt->shape[0] == up->shape[0] &&
         (int)q->shape[0] == hp_.n_embd && (int)gt->shape[0] == hp_.n_embd &&
@@ -287,6 +287,29 @@ void Session::upload(const GGUFView& g) {  // model.cpp:169-238 tensor map
         slab_of(q, LAYER_PRO) == slab_of(q, LAYER_PLAIN) &&  // one qkv layout serves both roles
         shape_ok(o, o_rows.n, LAYER_PLAIN) && shape_ok(gt, 2 * (tp_ ? f_sh_ : hp_.n_ff), LAYER_GELU) &&
         shape_ok(dn, tp_ ? e_sh_ : (int)dn->shape[1], LAYER_QUANT);
+    // K-quant layers (Q4_K_M: q, k, o, gate, up Q4_K; v, down Q6_K or Q4_K) in the kq launch table,
+    // one device: q|k and v in one launch when v is Q6_K
+    auto kq_t = [](const GTensor* t) { return t && (t->type == T_Q4_K || t->type == T_Q6_K); };
+    bool kq_path = fuse_layers_ && !tp_ && Ld.has_kv && q->type == T_Q4_K && k->type == T_Q4_K && kq_t(v) &&
+                   kq_t(o) && kq_t(gt) && up->type == gt->type && kq_t(dn) && q->shape[0] == k->shape[0] &&
+                   q->shape[0] == v->shape[0] && (int)q->shape[0] == hp_.n_embd && (int)gt->shape[0] == hp_.n_embd &&
+                   shape_ok(o, o_rows.n, LAYER_PLAIN) && shape_ok(gt, 2 * hp_.n_ff, LAYER_GELU) &&
+                   shape_ok(dn, (int)dn->shape[1], LAYER_QUANT) && (hp_.n_head * Ld.hd) % 256 == 0;
+    if (kq_path) {
+      if (v->type == T_Q4_K) {
+        kq_path = shape_ok(q, Ld.qkv_rows, LAYER_PRO) && shape_ok(q, Ld.qkv_rows, LAYER_PLAIN);
+      } else {
+        DevWeight wa, wb;
+        wa.type = T_Q4_K;
+        wa.rows = qkv_rows[0].n + qkv_rows[1].n;
+        wa.cols = (int)q->shape[0];
+        wb.type = T_Q6_K;
+        wb.rows = qkv_rows[2].n;
+        wb.cols = wa.cols;
+        kq_path = layer_gemv2_supported(wa, wb, LAYER_PRO) && layer_gemv2_supported(wa, wb, LAYER_PLAIN);
+      }
+    }
+    want_fused = want_fused || kq_path;
     if (tp_ && !want_fused)
       throw status_error(LLMI_E_ARG, "tensor parallel: layer " + std::to_string(l) +
                                          " shards are not in the fused Q4_0 launch table");
@@ -315,8 +338,11 @@ void Session::upload(const GGUFView& g) {  // model.cpp:169-238 tensor map
       Ld.gate_up = make_parts(g, {all_rows(gt), all_rows(up)}, stream_, weight_bytes_);
     }
     Ld.down = make_parts(g, {tp_ ? RowSlice{dn, r * e_sh_, e_sh_} : all_rows(dn)}, stream_, weight_bytes_)[0];
-    Ld.fused = Ld.gu_interleaved && Ld.qkv.size() == 1 && layer_gemv_supported(Ld.qkv[0].w, LAYER_PRO) &&
-               layer_gemv_supported(Ld.qkv[0].w, LAYER_PLAIN) && layer_gemv_supported(Ld.o.w, LAYER_PLAIN) &&
+    const bool qkv_ok =
+        Ld.qkv.size() == 1 ? layer_gemv_supported(Ld.qkv[0].w, LAYER_PRO) && layer_gemv_supported(Ld.qkv[0].w, LAYER_PLAIN)
+        : Ld.qkv.size() == 2 && layer_gemv2_supported(Ld.qkv[0].w, Ld.qkv[1].w, LAYER_PRO) &&
+              layer_gemv2_supported(Ld.qkv[0].w, Ld.qkv[1].w, LAYER_PLAIN);
+    Ld.fused = Ld.gu_interleaved && qkv_ok && layer_gemv_supported(Ld.o.w, LAYER_PLAIN) &&
                layer_gemv_supported(Ld.gate_up[0].w, LAYER_GELU) && layer_gemv_supported(Ld.down.w, LAYER_QUANT);
     Ld.attn_norm = dev_f32_copy(g, T("attn_norm.weight"), hp_.n_embd);
     Ld.q_norm = dev_f32_copy(g, T("attn_q_norm.weight"), Ld.hd);
@@ -369,10 +395,11 @@ void Session::upload(const GGUFView& g) {  // model.cpp:169-238 tensor map
   }
   if (all_fused) {  // the weight layouts the fused launch-table entries read
     auto relayout = [&](DevWeight& w, int role) {
-      if (layer_gemv_slab(w, role)) to_slab_layout(w, stream_);
+      if (w.type == T_Q4_K || w.type == T_Q6_K) to_kq_layout(w, stream_);
+      else if (layer_gemv_slab(w, role)) to_slab_layout(w, stream_);
     };
     for (auto& Ld : L_) {
-      relayout(Ld.qkv[0].w, LAYER_PRO);
+      for (auto& p : Ld.qkv) relayout(p.w, LAYER_PRO);
       relayout(Ld.o.w, LAYER_PLAIN);
       relayout(Ld.gate_up[0].w, LAYER_GELU);
       relayout(Ld.down.w, LAYER_QUANT);
@@ -941,14 +968,22 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
       }
     } else {
       LayerGemv g;
+      const bool kq = Ld.qkv[0].w.kq != 0;  // K-quant layer: Q8_K activations in XBlocks
+      auto qkv_launch = [&](const LayerGemv& gg, int role) {
+        if (Ld.qkv.size() == 2) launch_layer_gemv2(Ld.qkv[0].w, Ld.qkv[1].w, gg, role, s);
+        else launch_layer_gemv(Ld.qkv[0].w, gg, role, s);
+      };
       if (l == 0) {
-        if (!x_q8) {
+        if (kq) {
+          launch_quantize_q8k_xblocks(xn_, E, act_.q8.xb, s);
+          kernels_per_token_++;
+        } else if (!x_q8) {
           launch_quantize_q8_0(xn_, E, act_.q8, s);
           kernels_per_token_++;
         }
         g.xg = act_.q8.xb;
         g.out = qkv_;
-        for (int r = 0; r < dup("qkv"); r++) launch_layer_gemv(Ld.qkv[0].w, g, LAYER_PLAIN, s);
+        for (int r = 0; r < dup("qkv"); r++) qkv_launch(g, LAYER_PLAIN);
       } else {
         g.y = d_out_;
         g.w_post = L_[l - 1].post_ffw_norm;
@@ -958,7 +993,7 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
         g.eps = hp_.eps;
         g.out = qkv_;
         if (dump_ || trace_fn_) g.xn_out = xn_;
-        for (int r = 0; r < dup("qkv"); r++) launch_layer_gemv(Ld.qkv[0].w, g, LAYER_PRO, s);
+        for (int r = 0; r < dup("qkv"); r++) qkv_launch(g, LAYER_PRO);
         tap("attn_resid", l, other, (size_t)E * 4, s);
         tap("attn_norm", l, xn_, (size_t)E * 4, s);
         dump("l_out-" + std::to_string(l - 1), other, E, s);
@@ -978,6 +1013,7 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
       const int hb = nh_ * hd / 32;  // Q8_0 blocks of this rank's heads
       AttnArgs aa{q_, Ld.kc, Ld.vc, nh_, nkv_, hd, max_ctx_, d_pos_, part_, attn_,
                   ticket_, q8_in_combine ? act_.q8.xb + (size_t)tp_rank_ * hb : nullptr};
+      aa.q8k = Ld.o.w.kq ? 1 : 0;  // the kq o projection reads Q8_K quants
       for (int r = 0; r < dup("attn"); r++) launch_attention(aa, false, s, &qa);
       kernels_per_token_++;
       tap("attn", l, attn_, (size_t)nh_ * hd * 4, s);

@@ -14,6 +14,8 @@ void free_weight(DevWeight& w);
 // Q4_0 row-major blocks -> slab-major (k_layer.hip's a.slab layout): slabs of
 // 8 blocks x all rows, block b of row r at (b / 8) rows 8 + r 8 + b % 8.
 void to_slab_layout(DevWeight& w, hipStream_t s);
+// Q4_K / Q6_K GGUF rows -> the kq sub-block layout of the fused layer kernels (kernels.h)
+void to_kq_layout(DevWeight& w, hipStream_t s);
 
 // outputs of a norm that feeds a GEMV: xn (always), plus optionally the Q8_0
 // blocks and/or the f16-rounded copy the next GEMV consumes
@@ -60,6 +62,8 @@ struct LayerGemv {
   float* out = nullptr;     // PLAIN / PRO / QUANT: [rows]
   float* hid = nullptr;     // GELU: [rows / 2] = GELU(gate) * up
   unsigned* epoch = nullptr;  // optional: work-group 0 advances *epoch (the attention block's granule tag)
+  const uint32_t* kdd = nullptr;  // kq weights (Q4_K / Q6_K): super-block d words, Q6_K high bits
+  const uint2* kqh = nullptr;
 };
 // Cross-work-group hand-offs of the attention-block kernel (k_attn.hip):
 // qkv rows -> the kv head's attention work-groups -> the o projection, as
@@ -126,6 +130,11 @@ int layer_gemv_slab(const DevWeight& w, int role);
 // GELU role: hidden units per work-group (the gate/up interleave group), 0 if unsupported
 int layer_gemv_gelu_group(int cols, uint32_t type = T_Q4_0);
 void launch_layer_gemv(const DevWeight& w, LayerGemv a, int role, hipStream_t s);
+// K-quant q|k (Q4_K) + v (Q6_K), both in the kq layout, in one launch (qkv roles)
+bool layer_gemv2_supported(const DevWeight& wa, const DevWeight& wb, int role);
+void launch_layer_gemv2(const DevWeight& wa, const DevWeight& wb, LayerGemv a, int role, hipStream_t s);
+// Q8_K quants of x in XBlocks (the activation of a PLAIN kq layer launch), n % 256 == 0
+void launch_quantize_q8k_xblocks(const float* x, int n, XBlock* xb, hipStream_t s);
 void launch_argmax(const float* x, int n, unsigned long long* key, hipStream_t s);
 // Greedy token by bounded screening + exact rescoring (k_logits.hip): the
 // same first-index argmax as the fast F16 logits GEMV, from an int8 copy of

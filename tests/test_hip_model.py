@@ -200,3 +200,32 @@ def test_q8_0_fused_matches_unfused(oracle, monkeypatch):
     first = int(np.argmax(lf))
     assert first == int(np.argmax(lp))
     assert fused.generate(first, len(prompt), 8).tolist() == plain.generate(first, len(prompt), 8).tolist()
+
+
+@pytest.mark.parametrize("vtype", ["q6_k", "q4_k"])
+def test_kquant_fused_matches_unfused(oracle, monkeypatch, vtype):
+    """K-quant weights in the fused layer launch table (k_layer.hip kq entries:
+    Q4_K / Q6_K rows repacked into 32-element sub-blocks, Q8_K activations
+    quantized in the launches' prologues; q|k Q4_K + v Q6_K in one launch)
+    against the per-projection K-quant path and the f64-attention oracle."""
+    from llm_inference_amd.gguf import TensorType as TT
+    from llm_inference_amd.model import Model
+    from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
+    cfg = CONFIGS["mini-4b"]
+    vt = TT.Q6_K if vtype == "q6_k" else TT.Q4_K
+    g = build_gemma3_gguf(cfg, seed=17, wtype=TT.Q4_K, wtypes={"v": vt, "down": vt})
+    prompt = np.random.default_rng(6).integers(4, cfg.vocab, 9).astype(np.int32)
+    fused = Model(g, exact=False, max_ctx=64)
+    lf = fused.forward(prompt, 0)
+    monkeypatch.setenv("LLMI_NO_FUSE", "1")
+    plain = Model(g, exact=False, max_ctx=64)
+    lp = plain.forward(prompt, 0)
+    print(f"{vtype}: kernels per token fused {fused.get_info().kernels_per_token} vs "
+          f"{plain.get_info().kernels_per_token}; |fused - unfused| {float(np.abs(lf - lp).max()):.3g}")
+    assert fused.get_info().kernels_per_token < plain.get_info().kernels_per_token
+    np.testing.assert_allclose(lf, lp, atol=FAST_VS_REF, rtol=0)
+    ideal = oracle.model(g, n_threads=8, max_ctx=64, attn_f64=True)
+    np.testing.assert_allclose(lf, ideal.forward(prompt, 0), atol=FAST_VS_REF, rtol=0)
+    first = int(np.argmax(lf))
+    assert first == int(np.argmax(lp))
+    assert fused.generate(first, len(prompt), 8).tolist() == plain.generate(first, len(prompt), 8).tolist()
