@@ -53,8 +53,11 @@ void launch_attention(const AttnArgs& a, bool exact, hipStream_t s, const QKVArg
 // qkv GEMV (qrole LAYER_PLAIN / LAYER_PRO) + fused attention + o GEMV in one
 // launch (k_attn.hip, attention block); qg.out must be qa.qkv, og.xg must be
 // aa.q8.  attn_block_supported: a launch-table entry exists for the shapes.
-bool attn_block_supported(const DevWeight& wqkv, const DevWeight& wo, int head_dim, int n_head, int n_head_kv);
-void launch_attn_block(const DevWeight& wqkv, LayerGemv qg, int qrole, const DevWeight& wo, LayerGemv og,
+// wqkv_b: the second qkv weight of a q|k Q4_K + v Q6_K layer (kq layout), or null
+bool attn_block_supported(const DevWeight& wqkv, const DevWeight* wqkv_b, const DevWeight& wo, int head_dim,
+                          int n_head, int n_head_kv);
+void launch_attn_block(const DevWeight& wqkv, const DevWeight* wqkv_b, LayerGemv qg, int qrole, const DevWeight& wo,
+                       LayerGemv og,
                        const AttnArgs& aa, const QKVArgs& qa, BlockSync bs, hipStream_t s);
 void launch_bump_epoch(unsigned* epoch, hipStream_t s);
 

@@ -655,8 +655,9 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, const QKVArgs
     for (int i = t; i < G * HD / 8; i += 256) {
       const float4 f0 = reinterpret_cast<const float4*>(s_out)[2 * i], f1 = reinterpret_cast<const float4*>(s_out)[2 * i + 1];
       const float vv[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
-      if (!BLK && a.q8k) q8k_block_quad(vv, i & 3, a.q8 + (size_t)hkv * G * HD / 32 + (i >> 2));
-      else q8_block_quad(vv, i & 3, BLK ? s_q8 + (i >> 2) : a.q8 + (size_t)hkv * G * HD / 32 + (i >> 2));
+      XBlock* xb = BLK ? s_q8 + (i >> 2) : a.q8 + (size_t)hkv * G * HD / 32 + (i >> 2);
+      if (a.q8k) q8k_block_quad(vv, i & 3, xb);
+      else q8_block_quad(vv, i & 3, xb);
     }
     if constexpr (BLK) {  // the blocks' words as granules for the o projection
       __syncthreads();
@@ -770,13 +771,26 @@ constexpr size_t block_attn_lds() {  // s_k + s_v (32-key tiles) + s_red
          (attn_kp<HD, G>() > 1 ? (size_t)attn_kp<HD, G>() * G * HD * 4 : 16);
 }
 
-template <int HD, int G, int QR, int QP, int QE, int QROLE, int OR, int OP, int OE>
+// WTQ / WTO: weight formats of qkv and o (layer_body WT: 0 Q4_0, or kq Q4_K /
+// Q6_K); WTQB != 0: the qkv rows from nqa work-groups on are a second weight
+// of that format (Q4_K_M: q|k Q4_K, v Q6_K), granules and outputs continuing
+// after the first weight's rows
+template <int HD, int G, int QR, int QP, int QE, int QROLE, int OR, int OP, int OE, int WTQ = 0, int WTQB = 0,
+          int WTO = 0>
 __global__ __launch_bounds__(256) void attn_block_kernel(LayerGemv qg, LayerGemv og, AttnArgs aa, QKVArgs qa,
-                                                        BlockSync bs, int nq) {
+                                                        BlockSync bs, int nq, LayerGemv qgb, int nqa) {
   extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
   int b = blockIdx.x;
   if (b < nq) {
-    layer_body<QR, 4, QP, QE, QROLE, false, true, SYNC_SIG>(qg, b, s_dyn, bs);
+    if constexpr (WTQB != 0) {
+      if (b >= nqa) {
+        BlockSync bsb = bs;
+        bsb.g_qkv += qg.rows;
+        layer_body<QR, 4, QP, QE, QROLE, false, true, SYNC_SIG, 0, false, WTQB>(qgb, b - nqa, s_dyn, bsb);
+        return;
+      }
+    }
+    layer_body<QR, 4, QP, QE, QROLE, false, true, SYNC_SIG, 0, false, WTQ>(qg, b, s_dyn, bs);
     return;
   }
   b -= nq;
@@ -790,24 +804,24 @@ __global__ __launch_bounds__(256) void attn_block_kernel(LayerGemv qg, LayerGemv
     return;
   }
   b -= na;
-  layer_body<OR, 4, OP, OE, ROLE_PLAIN, false, true, SYNC_WAIT>(og, b, s_dyn, bs);
+  layer_body<OR, 4, OP, OE, ROLE_PLAIN, false, true, SYNC_WAIT, 0, false, WTO>(og, b, s_dyn, bs);
 }
 
 using BlockFn = void (*)(dim3, size_t, const LayerGemv&, const LayerGemv&, const AttnArgs&, const QKVArgs&,
-                         const BlockSync&, int, hipStream_t);
+                         const BlockSync&, int, const LayerGemv&, int, hipStream_t);
 
-template <int HD, int G, int QR, int QP, int QE, int QROLE, int OR, int OP, int OE>
+template <int HD, int G, int QR, int QP, int QE, int QROLE, int OR, int OP, int OE, int WTQ, int WTQB, int WTO>
 void block_launch(dim3 grid, size_t lds, const LayerGemv& qg, const LayerGemv& og, const AttnArgs& aa,
-                  const QKVArgs& qa, const BlockSync& bs, int nq, hipStream_t s) {
+                  const QKVArgs& qa, const BlockSync& bs, int nq, const LayerGemv& qgb, int nqa, hipStream_t s) {
   KernelTiming& kt = kernel_timing();
   if (kt.start) {  // bench: events signalled by this dispatch itself (its duration as rocprofv3 reports it)
-    hipExtLaunchKernelGGL((attn_block_kernel<HD, G, QR, QP, QE, QROLE, OR, OP, OE>), grid, dim3(256), (uint32_t)lds,
-                          s, kt.start, kt.stop, 0u, qg, og, aa, qa, bs, nq);
+    hipExtLaunchKernelGGL((attn_block_kernel<HD, G, QR, QP, QE, QROLE, OR, OP, OE, WTQ, WTQB, WTO>), grid, dim3(256),
+                          (uint32_t)lds, s, kt.start, kt.stop, 0u, qg, og, aa, qa, bs, nq, qgb, nqa);
     kt = KernelTiming{};
     return;
   }
-  hipLaunchKernelGGL((attn_block_kernel<HD, G, QR, QP, QE, QROLE, OR, OP, OE>), grid, dim3(256), lds, s, qg, og, aa,
-                     qa, bs, nq);
+  hipLaunchKernelGGL((attn_block_kernel<HD, G, QR, QP, QE, QROLE, OR, OP, OE, WTQ, WTQB, WTO>), grid, dim3(256), lds, s,
+                     qg, og, aa, qa, bs, nq, qgb, nqa);
 }
 
 struct BlockCfg {
@@ -816,11 +830,15 @@ struct BlockCfg {
   size_t attn_lds;
   BlockFn fn;
   const void* kern;  // the kernel (occupancy query)
+  int wtq, wtqb, wto;  // weight formats (layer_body WT): qkv, second qkv weight (0: none), o
 };
-#define LLMI_BCFG(NBQ, NBO, HD, G, QROLE, QR, QP, QE, OR, OP, OE)                                \
-  {NBQ, NBO, HD, G, QROLE, QR, QP, QE, OR, OP, OE, block_attn_lds<HD, G>(),                      \
-   block_launch<HD, G, QR, QP, QE, QROLE, OR, OP, OE>,                                            \
-   reinterpret_cast<const void*>(&attn_block_kernel<HD, G, QR, QP, QE, QROLE, OR, OP, OE>)}
+#define LLMI_BCFGW(NBQ, NBO, HD, G, QROLE, QR, QP, QE, OR, OP, OE, WTQ, WTQB, WTO)                          \
+  {NBQ, NBO, HD, G, QROLE, QR, QP, QE, OR, OP, OE, block_attn_lds<HD, G>(),                                  \
+   block_launch<HD, G, QR, QP, QE, QROLE, OR, OP, OE, WTQ, WTQB, WTO>,                                        \
+   reinterpret_cast<const void*>(&attn_block_kernel<HD, G, QR, QP, QE, QROLE, OR, OP, OE, WTQ, WTQB, WTO>), WTQ, \
+   WTQB, WTO}
+#define LLMI_BCFG(NBQ, NBO, HD, G, QROLE, QR, QP, QE, OR, OP, OE) \
+  LLMI_BCFGW(NBQ, NBO, HD, G, QROLE, QR, QP, QE, OR, OP, OE, 0, 0, 0)
 // qkv: 4 waves x QR rows per work-group (rows per work-group must divide
 // head_dim); o: 4 waves x OR rows.  E as in k_layer.hip's table.
 const BlockCfg kBlockCfgs[] = {
@@ -831,18 +849,34 @@ const BlockCfg kBlockCfgs[] = {
     LLMI_BCFG(80, 64, 256, 2, ROLE_PLAIN, 4, 5, 1, 8, 8, 1),   // 4B layer 0
     LLMI_BCFG(36, 32, 256, 4, ROLE_PRO, 4, 3, 5, 4, 2, 1),     // 1B:  qkv 1536 rows -> 96 WGs, o 1152 -> 72
     LLMI_BCFG(36, 32, 256, 4, ROLE_PLAIN, 4, 3, 1, 4, 2, 1),   // 1B layer 0
+    // 4B Q4_K_M (kq weights): q|k Q4_K + v Q6_K, or all Q4_K; o Q4_K; the Q4_0 geometry
+    LLMI_BCFGW(80, 64, 256, 2, ROLE_PRO, 4, 5, 10, 8, 8, 1, WT_Q4_K, WT_Q6_K, WT_Q4_K),
+    LLMI_BCFGW(80, 64, 256, 2, ROLE_PLAIN, 4, 5, 1, 8, 8, 1, WT_Q4_K, WT_Q6_K, WT_Q4_K),
+    LLMI_BCFGW(80, 64, 256, 2, ROLE_PRO, 4, 5, 10, 8, 8, 1, WT_Q4_K, 0, WT_Q4_K),
+    LLMI_BCFGW(80, 64, 256, 2, ROLE_PLAIN, 4, 5, 1, 8, 8, 1, WT_Q4_K, 0, WT_Q4_K),
 };
 #undef LLMI_BCFG
+#undef LLMI_BCFGW
 
-const BlockCfg* find_block_cfg(int nb_qkv, int nb_o, int hd, int g, int qrole) {
+int wt_of_w(const DevWeight* w) {
+  if (!w) return 0;
+  return w->type == T_Q4_K ? WT_Q4_K : w->type == T_Q6_K ? WT_Q6_K : 0;
+}
+
+const BlockCfg* find_block_cfg(int nb_qkv, int nb_o, int hd, int g, int qrole, int wtq = 0, int wtqb = 0,
+                               int wto = 0) {
   for (const auto& c : kBlockCfgs)
-    if (c.nb_qkv == nb_qkv && c.nb_o == nb_o && c.hd == hd && c.g == g && c.qrole == qrole) return &c;
+    if (c.nb_qkv == nb_qkv && c.nb_o == nb_o && c.hd == hd && c.g == g && c.qrole == qrole && c.wtq == wtq &&
+        c.wtqb == wtqb && c.wto == wto)
+      return &c;
   return nullptr;
 }
 
 void fill_gemv(const DevWeight& w, LayerGemv& a) {
   a.qs = reinterpret_cast<const uint4*>(w.qs);
   a.wd = w.d;
+  a.kdd = w.kdd;
+  a.kqh = w.kqh;
   a.slab = w.slab;
   a.rows = w.rows;
   a.nb = w.cols / 32;
@@ -863,9 +897,10 @@ struct BlockGeom {
   int nq, na, no;
   size_t lds;
 };
-static BlockGeom block_geom(const BlockCfg& c, const DevWeight& wqkv, const DevWeight& wo, int n_head_kv, int qrole) {
+static BlockGeom block_geom(const BlockCfg& c, const DevWeight& wqkv, const DevWeight* wqkv_b, const DevWeight& wo,
+                            int n_head_kv, int qrole) {
   BlockGeom g;
-  g.nq = (wqkv.rows + 4 * c.QR - 1) / (4 * c.QR);
+  g.nq = (wqkv.rows + (wqkv_b ? wqkv_b->rows : 0) + 4 * c.QR - 1) / (4 * c.QR);
   g.na = n_head_kv * ATTN_NSPLIT;
   g.no = (wo.rows + 4 * c.OR - 1) / (4 * c.OR);
   const size_t lds_q = (size_t)(wqkv.cols / 32) * sizeof(XBlock) + 16 + (qrole == ROLE_PRO ? (size_t)wqkv.cols * 4 : 0);
@@ -897,24 +932,32 @@ static bool block_co_resident(const BlockCfg& c, const BlockGeom& g) {
   return g.nq + g.na + g.no <= capacity;
 }
 
-bool attn_block_supported(const DevWeight& wqkv, const DevWeight& wo, int head_dim, int n_head, int n_head_kv) {
-  if (wqkv.type != T_Q4_0 || wo.type != T_Q4_0 || wqkv.slab || wo.slab) return false;
+bool attn_block_supported(const DevWeight& wqkv, const DevWeight* wqkv_b, const DevWeight& wo, int head_dim,
+                          int n_head, int n_head_kv) {
+  const bool q40 = wqkv.type == T_Q4_0 && wo.type == T_Q4_0 && !wqkv_b && !wqkv.slab && !wo.slab;
+  const bool kq = wqkv.kq && wo.kq && (!wqkv_b || (wqkv_b->kq && wqkv_b->cols == wqkv.cols));
+  if (!q40 && !kq) return false;
   if (wqkv.cols % 32 || wo.cols % 32 || n_head_kv <= 0 || n_head % n_head_kv) return false;
   const int g = n_head / n_head_kv;
   for (int role : {(int)ROLE_PLAIN, (int)ROLE_PRO}) {
-    const BlockCfg* c = find_block_cfg(wqkv.cols / 32, wo.cols / 32, head_dim, g, role);
+    const BlockCfg* c = find_block_cfg(wqkv.cols / 32, wo.cols / 32, head_dim, g, role, wt_of_w(&wqkv),
+                                       wt_of_w(wqkv_b), wt_of_w(&wo));
     if (!c || head_dim % (4 * c->QR) != 0) return false;
-    if (!block_co_resident(*c, block_geom(*c, wqkv, wo, n_head_kv, role))) return false;
+    if (wqkv_b && wqkv.rows % (4 * c->QR) != 0) return false;
+    if (!block_co_resident(*c, block_geom(*c, wqkv, wqkv_b, wo, n_head_kv, role))) return false;
   }
-  return wqkv.rows == (n_head + 2 * n_head_kv) * head_dim && wo.cols == n_head * head_dim;
+  return wqkv.rows + (wqkv_b ? wqkv_b->rows : 0) == (n_head + 2 * n_head_kv) * head_dim &&
+         wo.cols == n_head * head_dim;
 }
 
-void launch_attn_block(const DevWeight& wqkv, LayerGemv qg, int qrole, const DevWeight& wo, LayerGemv og,
-                       const AttnArgs& aa, const QKVArgs& qa, BlockSync bs, hipStream_t s) {
-  if (!attn_block_supported(wqkv, wo, aa.head_dim, aa.n_head, aa.n_head_kv))
+void launch_attn_block(const DevWeight& wqkv, const DevWeight* wqkv_b, LayerGemv qg, int qrole, const DevWeight& wo,
+                       LayerGemv og, const AttnArgs& aa, const QKVArgs& qa, BlockSync bs, hipStream_t s) {
+  if (!attn_block_supported(wqkv, wqkv_b, wo, aa.head_dim, aa.n_head, aa.n_head_kv))
     throw std::runtime_error("attention block: unsupported shapes");
   const int g = aa.n_head / aa.n_head_kv, hd = aa.head_dim;
-  const BlockCfg& c = *find_block_cfg(wqkv.cols / 32, wo.cols / 32, hd, g, qrole);
+  const BlockCfg& c = *find_block_cfg(wqkv.cols / 32, wo.cols / 32, hd, g, qrole, wt_of_w(&wqkv), wt_of_w(wqkv_b),
+                                      wt_of_w(&wo));
+  if (c.wto && !aa.q8k) throw std::runtime_error("attention block: a kq o projection reads Q8_K blocks");
   if (!bs.epoch || !bs.g_qkv || !bs.g_xo || !bs.err || !aa.q8 || !aa.partial || !aa.ticket || !qa.qkv ||
       qa.qkv != qg.out)
     throw std::runtime_error("attention block: missing buffers");
@@ -924,14 +967,22 @@ void launch_attn_block(const DevWeight& wqkv, LayerGemv qg, int qrole, const Dev
   if (og.xg != aa.q8 || !og.out) throw std::runtime_error("attention block: o projection must read the merged blocks");
   fill_gemv(wqkv, qg);
   fill_gemv(wo, og);
+  LayerGemv qgb = qg;
+  if (wqkv_b) {
+    fill_gemv(*wqkv_b, qgb);
+    qgb.out = qg.out + wqkv.rows;
+    qgb.resid_out = nullptr;
+    qgb.xn_out = nullptr;
+  }
   const int nbq = qg.nb, nbo = og.nb;
   // one pass group per lane (no MULTI) and enough prologue / x-copy slots
   auto passes = [](int nb, int R) { return (nb + 64 / R - 1) / (64 / R); };
   if (passes(nbq, c.QR) > c.QP || passes(nbo, c.OR) > c.OP) throw std::runtime_error("attention block: P too small");
   if (qrole == ROLE_PRO ? wqkv.cols > c.QE * 256 : 3 * nbq > c.QE * 256) throw std::runtime_error("attention block: qkv E");
   if (3 * nbo > c.OE * 256) throw std::runtime_error("attention block: o E");
-  const BlockGeom bg = block_geom(c, wqkv, wo, aa.n_head_kv, qrole);
-  c.fn(dim3(bg.nq + bg.na + bg.no), bg.lds, qg, og, aa, qa, bs, bg.nq, s);
+  const BlockGeom bg = block_geom(c, wqkv, wqkv_b, wo, aa.n_head_kv, qrole);
+  const int nqa = wqkv_b ? wqkv.rows / (4 * c.QR) : bg.nq;
+  c.fn(dim3(bg.nq + bg.na + bg.no), bg.lds, qg, og, aa, qa, bs, bg.nq, qgb, nqa, s);
   LLMI_HIP(hipGetLastError());
 }
 

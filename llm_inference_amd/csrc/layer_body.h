@@ -314,7 +314,7 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
   constexpr int L = RB ? 64 / R : 64;
   static_assert(PE == 0 || (RB && !MULTI && !EARLY && PE < P), "PE: single-chunk row-bound late roles");
   static_assert(!W8 || (RB && R <= 16), "W8: row-bound lanes");
-  static_assert(WT == 0 || (RB && R <= 8 && !MULTI && !HELP && !W8 && SYNC == 0), "kq: single-chunk row-bound lanes");
+  static_assert(WT == 0 || (RB && R <= 8 && !MULTI && !HELP && !W8), "kq: single-chunk row-bound lanes");
   LAYER_MARK(0);
   BLK_MARK(bs, 0);
   constexpr int EPT = E, X_LD = E;

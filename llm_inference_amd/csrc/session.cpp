@@ -552,7 +552,8 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
     bool blk = fuse_layers_ && !tp_ && dup_.empty() && getenv("LLMI_NO_BLOCK") == nullptr &&
                (grp == 1 || grp == 2 || grp == 4);
     for (const auto& l : L_)
-      blk = blk && l.fused && l.hd % 32 == 0 && attn_block_supported(l.qkv[0].w, l.o.w, l.hd, nh_, nkv_);
+      blk = blk && l.fused && l.hd % 32 == 0 &&
+            attn_block_supported(l.qkv[0].w, l.qkv.size() > 1 ? &l.qkv[1].w : nullptr, l.o.w, l.hd, nh_, nkv_);
     block_ = blk;
     // greedy token ids by screening (k_logits.hip): the fast F16 logits path
     // (a tensor-parallel rank screens its vocabulary shard; the keys meet in
@@ -923,7 +924,10 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
       LayerGemv g;
       int qrole = LAYER_PLAIN;
       if (l == 0) {
-        if (!x_q8) {
+        if (Ld.qkv[0].w.kq) {  // Q8_K quants in XBlocks for the kq qkv
+          launch_quantize_q8k_xblocks(xn_, E, act_.q8.xb, s);
+          kernels_per_token_++;
+        } else if (!x_q8) {
           launch_quantize_q8_0(xn_, E, act_.q8, s);
           kernels_per_token_++;
         }
@@ -952,7 +956,8 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
       bs.err = blk_err_;
       if (blk_trace_ && l == blk_trace_layer_) bs.trace = blk_trace_;
       if (trace_fn_ && qrole == LAYER_PRO) g.xn_out = xn_;
-      launch_attn_block(Ld.qkv[0].w, g, qrole, Ld.o.w, go, aa, qa, bs, s);
+      aa.q8k = Ld.o.w.kq ? 1 : 0;
+      launch_attn_block(Ld.qkv[0].w, Ld.qkv.size() > 1 ? &Ld.qkv[1].w : nullptr, g, qrole, Ld.o.w, go, aa, qa, bs, s);
       kernels_per_token_++;
       if (trace_fn_) {  // the launch's products: residual / norm (prologue), q|k|v and xo granules, attention, o
         if (qrole == LAYER_PRO) {
@@ -1477,7 +1482,9 @@ void Session::time_kernel(int which, int reps, double* us, double* bytes) {
                          bs.g_qkv = blk_gqkv_ + i * blk_gqkv_stride_;
                          bs.g_xo = blk_gxo_ + i * blk_gxo_stride_;
                          bs.err = blk_err_;
-                         launch_attn_block(Ld.qkv[0].w, q, LAYER_PRO, Ld.o.w, go, aa, qa, bs, stream_);
+                         aa.q8k = Ld.o.w.kq ? 1 : 0;
+                         launch_attn_block(Ld.qkv[0].w, Ld.qkv.size() > 1 ? &Ld.qkv[1].w : nullptr, q, LAYER_PRO,
+                                           Ld.o.w, go, aa, qa, bs, stream_);
                        },
                        (double)Ld.qkv[0].w.bytes + (double)Ld.o.w.bytes + kv});
     }
