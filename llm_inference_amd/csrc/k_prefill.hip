@@ -459,6 +459,119 @@ __global__ __launch_bounds__(256) void prefill_gemm3_kernel(PrefillGemm a) {
 }
 
 // ---------------------------------------------------------------------------
+// GEMM v4: v3's tile, ring and MFMA, with the scale epilogue cut to what the
+// per-block arithmetic needs (the kernel is VALU-bound: every 32x32x32 MFMA
+// of one 32-element block is followed by 16 conversions and 16 FMAs per lane).
+//  * the weight scales of a stage are converted f16 -> f32 ONCE per
+//    work-group into an f32 area of the stage (one thread per (block, row)),
+//    published by a second barrier, instead of 16 h2f per lane per MFMA;
+//  * s = d_w * d_x and acc = fma(s, (float)isum, acc) run as packed f32
+//    pairs (v_pk_mul_f32 / v_pk_fma_f32: per element the same IEEE ops).
+// Bit-identical to v1 / v3 (same fmaf(d_w * d_x, (float)isum, acc) in block
+// order per output).
+// ---------------------------------------------------------------------------
+constexpr int PG4_STAGE = PG3_STAGE + PG3_KB * PG3_M * 4;  // + f32 scales [4 blocks][64 rows]
+
+__global__ __launch_bounds__(256) void prefill_gemm4_kernel(PrefillGemm a) {
+  __shared__ __attribute__((aligned(16))) unsigned char s_ring[PG3_NS * PG4_STAGE];
+  const int t = threadIdx.x, lane = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6), r = lane & 31, h = lane >> 5;
+  const int wr = w & 1, wt = w >> 1;
+  const int nb = a.nb, n0 = blockIdx.x * PG3_M, tk0 = blockIdx.y * PG3_N;
+  const int nst = nb / PG3_KB;
+  auto st_wq = [&](int s) { return s_ring + s * PG4_STAGE; };
+  auto st_wd = [&](int s) { return s_ring + s * PG4_STAGE + PG3_KB * PG3_M * 16; };
+  auto st_x = [&](int s) { return s_ring + s * PG4_STAGE + PG3_KB * PG3_M * 16 + (PG3_KB / 2) * PG3_M * 4; };
+  auto st_wf = [&](int s) { return reinterpret_cast<float*>(s_ring + s * PG4_STAGE + PG3_STAGE); };
+  const XBlock* xrow = a.x + (size_t)min(tk0 + lane, a.T - 1) * a.xstride;
+  auto issue = [&](int c) {
+    const int s = c % PG3_NS, kb = c * PG3_KB;
+    glds16(a.qs + q4_block_index(a.slab, a.rows, nb, n0 + lane, kb + w), st_wq(s) + w * PG3_M * 16);
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+      const int sl = 3 * w + j, b = sl / 3, part = sl % 3;
+      glds16(reinterpret_cast<const uint4*>(xrow + kb + b) + part, st_x(s) + sl * PG3_N * 16);
+    }
+    if (w < 2) glds4(a.wd + q4_block_index(a.slab, a.rows, nb, n0 + lane, kb + 2 * w), st_wd(s) + w * PG3_M * 4);
+  };
+#define PG4_WAIT(AHEAD)                                                   \
+  do {                                                                    \
+    if ((AHEAD) >= 3) {                                                   \
+      if (w < 2) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");        \
+      else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");              \
+    } else if ((AHEAD) == 2) {                                            \
+      if (w < 2) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");        \
+      else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");               \
+    } else if ((AHEAD) == 1) {                                            \
+      if (w < 2) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");         \
+      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");               \
+    } else {                                                              \
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                    \
+    }                                                                     \
+  } while (0)
+  for (int c = 0; c < PG3_NS - 1 && c < nst; c++) issue(c);
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  f2 acc[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) acc[i] = (f2){0.0f, 0.0f};
+  const v16i zero = {};
+  for (int c = 0; c < nst; c++) {
+    const int ahead = min(PG3_NS - 2, nst - 1 - c);
+    PG4_WAIT(ahead);
+    __builtin_amdgcn_s_barrier();  // every wave's slices of stage c have landed; stage c - 1 is no longer read
+    if (c + PG3_NS - 1 < nst) issue(c + PG3_NS - 1);
+    const int s = c % PG3_NS;
+    {  // the stage's 4 x 64 weight scales -> f32, one per thread
+      const int b = t >> 6, row = t & 63;
+      const uint32_t pr = reinterpret_cast<const uint32_t*>(st_wd(s))[(b >> 1) * PG3_M + row];
+      st_wf(s)[b * PG3_M + row] = h2f((uint16_t)(pr >> ((b & 1) * 16)));
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // the f32 scales are in LDS (no vmcnt wait: the ring stays in flight)
+    const uint4* wq = reinterpret_cast<const uint4*>(st_wq(s));
+    const float* wf = st_wf(s);
+    const uint4* xs = reinterpret_cast<const uint4*>(st_x(s));
+#pragma unroll
+    for (int b = 0; b < PG3_KB; b++) {
+      const uint4 q = wq[b * PG3_M + 32 * wr + r];
+      const uint4 xq = xs[(3 * b + h) * PG3_N + 32 * wt + r];
+      const float dx = __uint_as_float(xs[(3 * b + 2) * PG3_N + 32 * wt + r].x);
+      v4i A, B;
+      A.x = q4_signed(h ? (q.x >> 4) & 0x0F0F0F0Fu : q.x & 0x0F0F0F0Fu);
+      A.y = q4_signed(h ? (q.y >> 4) & 0x0F0F0F0Fu : q.y & 0x0F0F0F0Fu);
+      A.z = q4_signed(h ? (q.z >> 4) & 0x0F0F0F0Fu : q.z & 0x0F0F0F0Fu);
+      A.w = q4_signed(h ? (q.w >> 4) & 0x0F0F0F0Fu : q.w & 0x0F0F0F0Fu);
+      B.x = (int)xq.x;
+      B.y = (int)xq.y;
+      B.z = (int)xq.z;
+      B.w = (int)xq.w;
+      const v16i D = __builtin_amdgcn_mfma_i32_32x32x32_i8(A, B, zero, 0, 0, 0);
+      const f2 dxx = {dx, dx};
+#pragma unroll
+      for (int g = 0; g < 4; g++) {  // rows 8g + 4h .. +3
+        const float4 w4 = *reinterpret_cast<const float4*>(&wf[b * PG3_M + 32 * wr + 8 * g + 4 * h]);
+        const f2 s01 = (f2){w4.x, w4.y} * dxx, s23 = (f2){w4.z, w4.w} * dxx;
+        const f2 d01 = {(float)D[4 * g + 0], (float)D[4 * g + 1]};
+        const f2 d23 = {(float)D[4 * g + 2], (float)D[4 * g + 3]};
+        acc[2 * g] = __builtin_elementwise_fma(s01, d01, acc[2 * g]);
+        acc[2 * g + 1] = __builtin_elementwise_fma(s23, d23, acc[2 * g + 1]);
+      }
+    }
+  }
+#undef PG4_WAIT
+  __builtin_amdgcn_s_barrier();
+  float* so = reinterpret_cast<float*>(s_ring) + (size_t)w * 32 * 33;
+#pragma unroll
+  for (int reg = 0; reg < 16; reg++) so[r * 33 + (reg & 3) + 8 * (reg >> 2) + 4 * h] = acc[reg >> 1][reg & 1];
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    const int idx = i * 64 + lane, tk = idx >> 5, row = idx & 31;
+    const int tok = tk0 + 32 * wt + tk;
+    if (tok < a.T) a.out[(size_t)tok * a.ostride + n0 + 32 * wr + row] = so[tk * 33 + row];
+  }
+}
+
+// ---------------------------------------------------------------------------
 // q/k norm + rope (+ q scale) and the K/V cache append, one wave per row
 // ---------------------------------------------------------------------------
 template <int HD>
@@ -700,9 +813,11 @@ void launch_prefill_gemm(const DevWeight& w, const XBlock* x, int xstride, int T
   a.T = T;
   a.out = out;
   a.ostride = ostride;
-  const char* ver = getenv("LLMI_PREFILL_GEMM");  // A/B: "1", "2"; default v3
-  const int v = ver ? atoi(ver) : 3;
-  if (v == 3 && w.rows % PG3_M == 0 && a.nb % PG3_KB == 0) {
+  const char* ver = getenv("LLMI_PREFILL_GEMM");  // A/B: "1", "2", "3"; default v4
+  const int v = ver ? atoi(ver) : 4;
+  if (v == 4 && w.rows % PG3_M == 0 && a.nb % PG3_KB == 0) {
+    hipLaunchKernelGGL(prefill_gemm4_kernel, dim3(w.rows / PG3_M, (T + PG3_N - 1) / PG3_N), dim3(256), 0, s, a);
+  } else if (v >= 3 && w.rows % PG3_M == 0 && a.nb % PG3_KB == 0) {
     hipLaunchKernelGGL(prefill_gemm3_kernel, dim3(w.rows / PG3_M, (T + PG3_N - 1) / PG3_N), dim3(256), 0, s, a);
   } else if (v >= 2 && w.rows % PG2_M == 0) {
     hipLaunchKernelGGL(prefill_gemm2_kernel, dim3(w.rows / PG2_M, (T + PG2_N - 1) / PG2_N), dim3(256), 0, s, a);

@@ -66,3 +66,20 @@ def test_prefill_chunking_is_exact(monkeypatch):
     m.forward(prompt[:100], 0)
     tail = m.forward(prompt[100:], 100)
     np.testing.assert_array_equal(tail, ref)
+
+
+def test_prefill_gemm_versions_bitwise(monkeypatch):
+    """The prefill GEMM variants (v1 register-staged 32-row tiles, v3 LDS-DMA
+    ring, v4 = v3 + f32 scale staging + packed f32 epilogue) compute every
+    output with the same fmaf(d_w * d_x, (float)isum, acc) in block order:
+    identical logits."""
+    from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
+    cfg = CONFIGS["mini-4b"]
+    g = build_gemma3_gguf(cfg, seed=23)
+    prompt = np.random.default_rng(2).integers(4, cfg.vocab, 200).astype(np.int32)
+    out = {}
+    for v in ("1", "3", "4"):
+        monkeypatch.setenv("LLMI_PREFILL_GEMM", v)
+        out[v] = _model(g, monkeypatch).forward(prompt, 0)
+    np.testing.assert_array_equal(out["4"], out["1"])
+    np.testing.assert_array_equal(out["3"], out["1"])
