@@ -572,6 +572,277 @@ __global__ __launch_bounds__(256) void prefill_gemm4_kernel(PrefillGemm a) {
 }
 
 // ---------------------------------------------------------------------------
+// GEMM v5 (default): eight waves per work-group in a WR x WT x WK grid -- WR
+// row groups of 32 weight rows, WT token groups of 32 NT tokens, WK groups that
+// split the blocks of K (block b goes to group b % WK) -- so the narrow and
+// long-K projections still put two work-groups on every CU (64 x 64 tiles
+// with K split 2, 32 x 64 with K split 4).
+//  * Each DMA piece of the LDS ring reads whole runs of memory: a row's 4
+//    consecutive Q4_0 blocks, a token's 4 consecutive XBlocks (v1-v4 and the
+//    first v5 took 16 B from a different 128-B line in every lane, so L2 moved
+//    8x the bytes); XOR-swizzled slots keep the fragment reads conflict-free.
+//  * Per block and 32 x 32 tile: one v_mfma_i32_32x32x32_i8 for the exact
+//    integer dots, and one v_mfma_f32_32x32x16_f16 for the 32 x 32 scale
+//    products d_w[row] * d_x[tok] (an outer product with k = 0 only, exact in
+//    f32), so the VALU does only (float)isum and the FMA per output; the VALU
+//    epilogue of block b - 1 runs while block b's MFMAs execute (ping-pong
+//    result registers, no copies).
+//  * Block id -> tile: the token tiles of one weight row tile get equal
+//    blockIdx % 8 (one XCD under round-robin placement: the row tile is
+//    fetched into one L2; speed only, never correctness).
+//  * Per output: acc_g = fmaf(d_w * d_x, (float)isum, acc_g) over the blocks of
+//    group g in order; out = ((acc_0 + acc_1) + acc_2) + ... in group order.
+//    WK = 1 is bit-identical to v1 / v3 / v4; every WK is independent of the
+//    chunking (a token's outputs do not depend on the other tokens).
+// Measured (4B, 512 tokens): qkv 39 -> 32, o 31 -> 25, gate_up 162 -> 133,
+// down 124 -> 96 us.  The compute alone (LLMI_PG5_NODMA build) is ~2/3 of it:
+// the VALU issue of ~55 instructions per block and tile (unpack, 16
+// conversions, 16 FMAs) at ~4 cycles each bounds this int8 design.
+// ---------------------------------------------------------------------------
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Stage image (KB = 4 blocks), every DMA piece reading whole runs of memory (v3/v4/first-cut v5 pieces took
+// 16 B from a different 128-B line in every lane -- row stride of the weights, token stride of the
+// activations -- so L2 moved 8x the bytes):
+//   wq [MR rows][4]    16-B quant blocks; lane i of a piece reads row i / 4's run of 4 blocks (64 B),
+//                      stored at slot b ^ sw(row), sw = (row >> 2) & 3 (conflict-free A reads)
+//   wd [2 pairs][MR]   u32 = f16 scales of blocks (2p, 2p + 1)
+//   xq [TN tok][4][3]  the token's 4 XBlocks (4 x 48 B contiguous) as 16-B parts, block slot
+//                      b ^ sw(tok): B fragment = part h, d_x = first dword of part 2
+template <int WR, int WT, int WK, int NT, int NS>
+struct PG5 {
+  static constexpr int KB = 4;
+  static constexpr int NW = WR * WT * WK, MR = 32 * WR, TN = 32 * NT * WT;
+  static constexpr int P_WQ = KB * MR / 64, P_WD = (KB / 2) * MR / 64, P_XQ = TN * KB * 3 / 64;
+  static constexpr int P = P_WQ + P_WD + P_XQ, PW = (P + NW - 1) / NW;
+  static constexpr int O_WD = KB * MR * 16, O_XQ = O_WD + (KB / 2) * MR * 4;
+  static constexpr int STAGE = O_XQ + TN * KB * 48;
+  static constexpr int EPI = NW * 32 * 33 * 4;  // one 32-token group of every wave, padded rows
+  static constexpr int LDS = STAGE * NS > EPI ? STAGE * NS : EPI;
+  static_assert(KB % WK == 0, "K groups");
+  static_assert(KB * MR % 64 == 0 && (KB / 2) * MR % 64 == 0 && TN * KB * 3 % 64 == 0, "pieces of 64 lanes");
+  static_assert(PW * (NS - 2) <= 63, "vmcnt range");
+};
+
+__device__ __forceinline__ int pg5_sw(int i) { return (i >> 2) & 3; }
+template <int N, int I = 0, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<N, I + 1>(f);
+  }
+}
+typedef _Float16 h2x8 __attribute__((ext_vector_type(8)));
+typedef float v16f __attribute__((ext_vector_type(16)));
+
+template <int WR, int WT, int WK, int NT, int NS>
+__global__ __launch_bounds__(512, (WK == 1 || NT > 1) ? 2 : 4) void prefill_gemm5_kernel(PrefillGemm a) {
+  using C = PG5<WR, WT, WK, NT, NS>;
+  constexpr int KB = C::KB;
+  __shared__ __attribute__((aligned(16))) unsigned char s_ring[C::LDS];
+  const int t = threadIdx.x, lane = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6), r = lane & 31, h = lane >> 5;
+  const int wr = w % WR, wt = (w / WR) % WT, kg = w / (WR * WT);
+  const int nb = a.nb, nst = nb / KB;
+  // tile of this work-group
+  const int n_rt = a.rows / C::MR, n_tt = (a.T + C::TN - 1) / C::TN;
+  const int bid = blockIdx.x;
+  int rt, tt;
+  if (n_rt % 8 == 0) {
+    const int j = bid >> 3;
+    rt = (j / n_tt) * 8 + (bid & 7);
+    tt = j % n_tt;
+  } else {
+    rt = bid / n_tt;
+    tt = bid % n_tt;
+  }
+  const int n0 = rt * C::MR, tk0 = tt * C::TN;
+  // this wave's DMA pieces (64 lanes each; wave w issues pieces w, w + NW, ... of every stage): per piece
+  // kind, lane pointer at chunk 0 and LDS offset within a stage, computed once; per chunk only a scalar
+  // offset is added (weights: kb blocks, or for the slab layout kb / 8 slabs + kb % 8)
+  const unsigned char* pb[C::PW];
+  int pk[C::PW], po[C::PW];
+#pragma unroll
+  for (int i = 0; i < C::PW; i++) {
+    const int p = (w + i * C::NW) % C::P;
+    if (p < C::P_WQ) {
+      const int u = p * 64 + lane, row = u / KB, b = (u % KB) ^ pg5_sw(row);
+      pk[i] = 0;
+      pb[i] = reinterpret_cast<const unsigned char*>(a.qs + q4_block_index(a.slab, a.rows, nb, n0 + row, b));
+      po[i] = p * 1024;
+    } else if (p < C::P_WQ + C::P_WD) {  // unit u: block pair u / MR, row u % MR
+      const int q = p - C::P_WQ, u = q * 64 + lane;
+      pk[i] = 1;
+      pb[i] = reinterpret_cast<const unsigned char*>(a.wd + q4_block_index(a.slab, a.rows, nb, n0 + u % C::MR, 2 * (u / C::MR)));
+      po[i] = C::O_WD + q * 256;
+    } else {  // unit u: (token, block slot, part)
+      const int q = p - C::P_WQ - C::P_WD, u = q * 64 + lane;
+      const int tok = u / (3 * KB), rem = u % (3 * KB), b = (rem / 3) ^ pg5_sw(tok);
+      pk[i] = 2;
+      pb[i] = reinterpret_cast<const unsigned char*>(a.x + (size_t)min(tk0 + tok, a.T - 1) * a.xstride + b) + 16 * (rem % 3);
+      po[i] = C::O_XQ + q * 1024;
+    }
+  }
+  auto issue = [&](int c) {
+#ifdef LLMI_PG5_NODMA  // development: compute floor (LDS never filled)
+    return;
+#endif
+    const int kb = c * KB;
+    const long wofs = a.slab ? (long)(kb >> 3) * a.rows * 8 + (kb & 7) : kb;  // weight block-index offset
+    unsigned char* st = s_ring + (c % NS) * C::STAGE;
+#pragma unroll
+    for (int i = 0; i < C::PW; i++) {
+      const int k = pk[i];
+      const long off = k == 0 ? wofs * 16 : k == 1 ? wofs * 2 : (long)kb * (long)sizeof(XBlock);
+      if (k == 1) glds4(pb[i] + off, st + po[i]);
+      else glds16(pb[i] + off, st + po[i]);
+    }
+  };
+  auto wait_ahead = [&](int ahead) {  // stages issued after the current one that may stay in flight
+    static_assert(NS >= 2 && NS <= 8, "NS");
+    static_for<NS - 1>([&](auto kc) {  // the first k with ahead >= NS - 2 - k waits for PW * (NS - 2 - k)
+      constexpr int k = decltype(kc)::value, n = NS - 2 - k;
+      if (ahead == n) vm_wait<C::PW * n>();
+    });
+  };
+  for (int c = 0; c < NS - 1 && c < nst; c++) issue(c);
+  float acc[NT][16];
+#pragma unroll
+  for (int j = 0; j < NT; j++)
+#pragma unroll
+    for (int i = 0; i < 16; i++) acc[j][i] = 0.0f;
+  const v16i zero = {};
+  const v16f zerof = {};
+  // per-lane LDS addresses (within a stage) of the A row and the B tokens, block slot 0; slots XOR-swizzled
+  const int arow = 32 * wr + r, a_sw = pg5_sw(arow);
+  int b_base[NT], b_sw[NT];
+#pragma unroll
+  for (int j = 0; j < NT; j++) {
+    const int tok = 32 * (wt * NT + j) + r;
+    b_base[j] = C::O_XQ + tok * KB * 48;
+    b_sw[j] = pg5_sw(tok);
+  }
+  // Software pipeline, one block deep, across stage boundaries: the MFMAs of block b are issued, then the
+  // VALU epilogue of block b - 1 runs on the matrix pipe's previous results while they execute; the LDS
+  // operands of block b + 1 are read before either.  (The carried results live in registers, so a stage's
+  // slot may be refilled once its MFMAs have read it.)  The scale products s[row][tok] = d_w[row] * d_x[tok]
+  // come from one f16 MFMA (k = 0 only: an outer product, exact in f32 -- 11-bit x 11-bit significands),
+  // so the VALU keeps only (float)isum and the FMA per output.
+  struct Ops {
+    v4i A;
+    h2x8 As;
+    v4i B[NT];
+    float dx[NT];
+  };
+  auto load_ops = [&](const unsigned char* st, int bb) {
+    Ops o;
+    const int b = bb * WK + kg;
+    const uint4 q = *reinterpret_cast<const uint4*>(st + (arow * KB + (b ^ a_sw)) * 16);
+    o.A.x = q4_signed(h ? (q.x >> 4) & 0x0F0F0F0Fu : q.x & 0x0F0F0F0Fu);
+    o.A.y = q4_signed(h ? (q.y >> 4) & 0x0F0F0F0Fu : q.y & 0x0F0F0F0Fu);
+    o.A.z = q4_signed(h ? (q.z >> 4) & 0x0F0F0F0Fu : q.z & 0x0F0F0F0Fu);
+    o.A.w = q4_signed(h ? (q.w >> 4) & 0x0F0F0F0Fu : q.w & 0x0F0F0F0Fu);
+    const int par = WK == 1 ? (bb & 1) : (kg & 1);  // the block's f16 in the scale pair
+    const uint32_t wp = reinterpret_cast<const uint32_t*>(st + C::O_WD)[(b >> 1) * C::MR + arow];
+    o.As = h2x8{};
+    o.As[0] = __builtin_bit_cast(_Float16, (uint16_t)(h ? 0u : (wp >> (16 * par)) & 0xFFFFu));
+#pragma unroll
+    for (int j = 0; j < NT; j++) {
+      const unsigned char* xb = st + b_base[j] + (b ^ b_sw[j]) * 48;
+      const uint4 xv = *reinterpret_cast<const uint4*>(xb + 16 * h);
+      o.dx[j] = *reinterpret_cast<const float*>(xb + 32);
+      o.B[j].x = (int)xv.x;
+      o.B[j].y = (int)xv.y;
+      o.B[j].z = (int)xv.z;
+      o.B[j].w = (int)xv.w;
+    }
+    return o;
+  };
+  // results of two blocks in flight, ping-pong by the block count's parity (compile-time indices: no copies)
+  v16i Dr[2][NT];
+  v16f Sr[2][NT];
+#pragma unroll
+  for (int j = 0; j < NT; j++) {
+    Dr[1][j] = zero;
+    Sr[1][j] = zerof;  // fmaf(+0, +0, acc) leaves acc unchanged
+  }
+  auto epi = [&](auto sl) {
+#pragma unroll
+    for (int j = 0; j < NT; j++)
+#pragma unroll
+      for (int reg = 0; reg < 16; reg++)
+        acc[j][reg] = fmaf(Sr[decltype(sl)::value][j][reg], (float)Dr[decltype(sl)::value][j][reg], acc[j][reg]);
+  };
+  constexpr int NB = KB / WK;  // blocks per stage and wave
+  auto stage = [&](int c, auto first) {  // first: slot of the stage's first block
+    wait_ahead(min(NS - 2, nst - 1 - c));
+    __builtin_amdgcn_s_barrier();  // every wave's pieces of stage c landed; stage c - 1 is no longer read
+    if (c + NS - 1 < nst) issue(c + NS - 1);
+#ifdef LLMI_PG5_NOCOMP  // development: DMA + barrier floor
+    if (c >= 0) return;
+#endif
+    const unsigned char* st = s_ring + (c % NS) * C::STAGE;
+    Ops o[2];
+    o[0] = load_ops(st, 0);
+    static_for<NB>([&](auto bbc) {
+      constexpr int bb = decltype(bbc)::value;
+      constexpr int sl = (decltype(first)::value + bb) & 1;
+      if constexpr (bb + 1 < NB) o[(bb + 1) & 1] = load_ops(st, bb + 1);
+#pragma unroll
+      for (int j = 0; j < NT; j++) {
+        Dr[sl][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(o[bb & 1].A, o[bb & 1].B[j], zero, 0, 0, 0);
+        h2x8 Bs = {};
+        Bs[0] = h ? (_Float16)0.0f : (_Float16)o[bb & 1].dx[j];  // d_x is an f16 value (q8 block scale): exact
+        Sr[sl][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(o[bb & 1].As, Bs, zerof, 0, 0, 0);
+      }
+      epi(std::integral_constant<int, sl ^ 1>{});  // the previous block's results
+    });
+  };
+  if constexpr (NB % 2 == 0) {
+    for (int c = 0; c < nst; c++) stage(c, std::integral_constant<int, 0>{});
+    epi(std::integral_constant<int, 1>{});
+  } else {
+    int c = 0;
+    for (; c + 1 < nst; c += 2) {
+      stage(c, std::integral_constant<int, 0>{});
+      stage(c + 1, std::integral_constant<int, 1>{});
+    }
+    if (c < nst) {
+      stage(c, std::integral_constant<int, 0>{});
+      epi(std::integral_constant<int, 0>{});
+    } else {
+      epi(std::integral_constant<int, 1>{});
+    }
+  }
+  // epilogue, one 32-token group at a time: every wave's tile (rows x 32 tokens) to LDS, then the K groups
+  // summed in group order and stored row-contiguous per token
+  float* ep = reinterpret_cast<float*>(s_ring);
+#pragma unroll
+  for (int j = 0; j < NT; j++) {
+    __builtin_amdgcn_s_barrier();  // the ring / the previous group's tiles are no longer read
+    float* mine = ep + (size_t)w * 32 * 33;
+#pragma unroll
+    for (int reg = 0; reg < 16; reg++) mine[r * 33 + (reg & 3) + 8 * (reg >> 2) + 4 * h] = acc[j][reg];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    for (int i = t; i < WT * C::MR * 32; i += 64 * C::NW) {
+      const int row = i % C::MR, tk = (i / C::MR) % 32, gt = i / (C::MR * 32);
+      const int tok = tk0 + 32 * (gt * NT + j) + tk;
+      float v = 0.0f;
+#pragma unroll
+      for (int g = 0; g < WK; g++) {
+        const int ww = (g * WT + gt) * WR + row / 32;  // wave (wr = row / 32, wt = gt, kg = g)
+        const float p = ep[(size_t)ww * 32 * 33 + tk * 33 + row % 32];
+        v = g ? v + p : p;
+      }
+      if (tok < a.T) a.out[(size_t)tok * a.ostride + n0 + row] = v;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // q/k norm + rope (+ q scale) and the K/V cache append, one wave per row
 // ---------------------------------------------------------------------------
 template <int HD>
@@ -799,6 +1070,30 @@ bool prefill_gemm_supported(const DevWeight& w) {
   return w.type == T_Q4_0 && w.rows % 32 == 0 && w.cols % 32 == 0 && (!w.slab || (w.cols / 32) % 8 == 0);
 }
 
+template <int WR, int WT, int WK, int NT, int NS>
+static bool try_gemm5(const PrefillGemm& a, hipStream_t s) {
+  using C = PG5<WR, WT, WK, NT, NS>;
+  if (a.rows % C::MR || a.nb % C::KB) return false;
+  const int n = (a.rows / C::MR) * ((a.T + C::TN - 1) / C::TN);
+  hipLaunchKernelGGL((prefill_gemm5_kernel<WR, WT, WK, NT, NS>), dim3(n), dim3(64 * C::NW), 0, s, a);
+  return true;
+}
+
+// v5 geometry (LLMI_PG5=<name> forces one for A/B; 4B 512-token prefill, us per GEMM qkv / o /
+// gate_up / down: mid 32.2 / 26.1 / 133.0 / 100.1, small 37.1 / 25.0 / 168.2 / 95.5, wide (128 x 64, no K
+// split) 32.2 / 25.3 / 145.8 / 103.7; a 6-stage ring, 64 tokens per wave or a 128 x 128 tile were slower):
+// 64 x 64 tiles with K split 2 (mid), or 32 x 64 with K split 4 (small) for the long-K GEMMs.  The K split
+// is chosen from K alone, so a tensor-parallel shard (fewer rows) sums every output in the same order as the
+// whole weight (tests/test_tp.py: bit-identical).
+static bool launch_gemm5(const PrefillGemm& a, hipStream_t s) {
+  const char* f = getenv("LLMI_PG5");
+  const std::string c = f ? f : a.nb >= 160 ? "small" : "mid";
+  if (c == "big" && try_gemm5<4, 2, 1, 2, 3>(a, s)) return true;
+  if (c == "wide" && try_gemm5<4, 2, 1, 1, 3>(a, s)) return true;
+  if (c == "small") return try_gemm5<1, 2, 4, 1, 4>(a, s);
+  return try_gemm5<2, 2, 2, 1, 4>(a, s) || try_gemm5<1, 4, 2, 1, 4>(a, s);  // K split 2, 64 or 32 rows
+}
+
 void launch_prefill_gemm(const DevWeight& w, const XBlock* x, int xstride, int T, float* out, int ostride,
                          hipStream_t s) {
   if (!prefill_gemm_supported(w)) throw std::runtime_error("prefill_gemm: unsupported weight");
@@ -813,9 +1108,10 @@ void launch_prefill_gemm(const DevWeight& w, const XBlock* x, int xstride, int T
   a.T = T;
   a.out = out;
   a.ostride = ostride;
-  const char* ver = getenv("LLMI_PREFILL_GEMM");  // A/B: "1", "2", "3"; default v4
-  const int v = ver ? atoi(ver) : 4;
-  if (v == 4 && w.rows % PG3_M == 0 && a.nb % PG3_KB == 0) {
+  const char* ver = getenv("LLMI_PREFILL_GEMM");  // A/B: "1", "2", "3", "4"; default v5
+  const int v = ver ? atoi(ver) : 5;
+  if (v == 5 && launch_gemm5(a, s)) {
+  } else if (v >= 4 && w.rows % PG3_M == 0 && a.nb % PG3_KB == 0) {
     hipLaunchKernelGGL(prefill_gemm4_kernel, dim3(w.rows / PG3_M, (T + PG3_N - 1) / PG3_N), dim3(256), 0, s, a);
   } else if (v >= 3 && w.rows % PG3_M == 0 && a.nb % PG3_KB == 0) {
     hipLaunchKernelGGL(prefill_gemm3_kernel, dim3(w.rows / PG3_M, (T + PG3_N - 1) / PG3_N), dim3(256), 0, s, a);

@@ -70,16 +70,31 @@ def test_prefill_chunking_is_exact(monkeypatch):
 
 def test_prefill_gemm_versions_bitwise(monkeypatch):
     """The prefill GEMM variants (v1 register-staged 32-row tiles, v3 LDS-DMA
-    ring, v4 = v3 + f32 scale staging + packed f32 epilogue) compute every
+    ring, v4 = v3 + f32 scale staging + packed f32 epilogue, v5 with one K
+    group per output = the 128 x 128 tile for every shape) compute every
     output with the same fmaf(d_w * d_x, (float)isum, acc) in block order:
-    identical logits."""
+    identical logits.  v5's default geometries split K over 2 or 4 wave groups
+    (per-group block-order chains, summed in group order): within the fast
+    budget of v1, and exact under re-chunking (test_prefill_chunking_is_exact
+    runs the default)."""
     from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
     cfg = CONFIGS["mini-4b"]
     g = build_gemma3_gguf(cfg, seed=23)
     prompt = np.random.default_rng(2).integers(4, cfg.vocab, 200).astype(np.int32)
     out = {}
-    for v in ("1", "3", "4"):
+    for v in ("1", "3", "4", "5"):
         monkeypatch.setenv("LLMI_PREFILL_GEMM", v)
+        if v == "5":
+            monkeypatch.setenv("LLMI_PG5", "big")
         out[v] = _model(g, monkeypatch).forward(prompt, 0)
     np.testing.assert_array_equal(out["4"], out["1"])
     np.testing.assert_array_equal(out["3"], out["1"])
+    np.testing.assert_array_equal(out["5"], out["1"])
+    for geo in ("mid", "small", "small4"):
+        monkeypatch.setenv("LLMI_PG5", geo)
+        got = _model(g, monkeypatch).forward(prompt, 0)
+        d = float(np.abs(got - out["1"]).max())
+        print(f"v5 {geo}: max|dlogit| vs v1 {d:.3g}")
+        assert d <= 1e-2
+    monkeypatch.delenv("LLMI_PG5")
+    monkeypatch.delenv("LLMI_PREFILL_GEMM")
