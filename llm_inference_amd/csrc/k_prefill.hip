@@ -109,6 +109,88 @@ __global__ __launch_bounds__(256) void prefill_norm_kernel(PrefillNorm a) {
   }
 }
 
+// residual mode, vectorized: a DPP quad of lanes per Q8_0 block (lane t & 3 owns elements 8 (t & 3) ..
+// + 7 of block t / 4 + 64 k), float4 loads, x quantized from registers (the decode layer prologue's scheme,
+// layer_body.h); EB = ceil(nb / 64) rounds.  Per token the same arithmetic whatever the chunk.
+template <int EB>
+__global__ __launch_bounds__(256) void prefill_norm_res_kernel(PrefillNorm a) {
+  __shared__ float s_red[4];
+  const int t = threadIdx.x, tok = blockIdx.x, n = a.n, nb = n / 32, sub = t & 3;
+  float* resid = a.resid + (size_t)tok * n;
+  const float* y = a.y + (size_t)tok * n;
+  float4 y4[EB][2], r4[EB][2];
+  auto in_row = [&](int k) { return t / 4 + 64 * k < nb; };
+#pragma unroll
+  for (int k = 0; k < EB; k++) {
+    const int e = (min(t / 4 + 64 * k, nb - 1) * 32 + sub * 8) / 4;
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      y4[k][h] = reinterpret_cast<const float4*>(y)[e + h];
+      r4[k][h] = reinterpret_cast<const float4*>(resid)[e + h];
+    }
+  }
+  float sc1 = 0.0f;
+  if (a.w_post) {
+    float ss = 0.0f;
+#pragma unroll
+    for (int k = 0; k < EB; k++)
+      if (in_row(k))
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+          ss = fmaf(y4[k][h].x, y4[k][h].x, ss);
+          ss = fmaf(y4[k][h].y, y4[k][h].y, ss);
+          ss = fmaf(y4[k][h].z, y4[k][h].z, ss);
+          ss = fmaf(y4[k][h].w, y4[k][h].w, ss);
+        }
+    sc1 = rms_scale_pf(block_sum<4>(ss, s_red), n, a.eps);
+  }
+  float ss2 = 0.0f;
+#pragma unroll
+  for (int k = 0; k < EB; k++) {
+    const int e = (min(t / 4 + 64 * k, nb - 1) * 32 + sub * 8) / 4;
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      float4& r = r4[k][h];
+      const float4 yv = y4[k][h];
+      if (a.w_post) {
+        const float4 wp = reinterpret_cast<const float4*>(a.w_post)[e + h];
+        r.x += (sc1 * yv.x) * wp.x;
+        r.y += (sc1 * yv.y) * wp.y;
+        r.z += (sc1 * yv.z) * wp.z;
+        r.w += (sc1 * yv.w) * wp.w;
+      } else {
+        r.x += yv.x;
+        r.y += yv.y;
+        r.z += yv.z;
+        r.w += yv.w;
+      }
+      if (in_row(k)) {
+        ss2 = fmaf(r.x, r.x, ss2);
+        ss2 = fmaf(r.y, r.y, ss2);
+        ss2 = fmaf(r.z, r.z, ss2);
+        ss2 = fmaf(r.w, r.w, ss2);
+        reinterpret_cast<float4*>(resid)[e + h] = r;
+      }
+    }
+  }
+  const float sc2 = rms_scale_pf(block_sum<4>(ss2, s_red), n, a.eps);
+  XBlock* xq = a.xq + (size_t)tok * a.xstride;
+#pragma unroll
+  for (int k = 0; k < EB; k++) {
+    const int b = min(t / 4 + 64 * k, nb - 1), e = (b * 32 + sub * 8) / 4;
+    float v[8];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const float4 r = r4[k][h], wn = reinterpret_cast<const float4*>(a.w_next)[e + h];
+      v[4 * h + 0] = (sc2 * r.x) * wn.x;
+      v[4 * h + 1] = (sc2 * r.y) * wn.y;
+      v[4 * h + 2] = (sc2 * r.z) * wn.z;
+      v[4 * h + 3] = (sc2 * r.w) * wn.w;
+    }
+    if (in_row(k)) q8_block_quad(v, sub, xq + b);  // whole quads in or out
+  }
+}
+
 // ---------------------------------------------------------------------------
 // GEMM: out[t][n] = sum_b d_w[n][b] d_x[t][b] * sum_k (q_w[n][b][k] - 8) q_x[t][b][k]
 // Work-group: 32 weight rows x 128 tokens, wave w: tokens [32 w, 32 w + 32).
@@ -1058,10 +1140,35 @@ __global__ __launch_bounds__(256) void prefill_gelu_kernel(const float* __restri
   q8_block_store(v, ok, xq + (size_t)tok * xstride + ic / 32, threadIdx.x & 31);
 }
 
+// GELU(gate) * up -> Q8_0, vectorized: a thread per 8 consecutive hidden units (one DPP quad per Q8_0 block),
+// float4 loads from the interleaved gate/up rows (H % 8 == 0: the 8 units sit in one H-group)
+__global__ __launch_bounds__(256) void prefill_gelu8_kernel(const float* __restrict__ gu, int F, int H,
+                                                            XBlock* __restrict__ xq, int xstride) {
+  const int tok = blockIdx.y, i = blockIdx.x * 256 + threadIdx.x;
+  if (i * 8 >= F) return;  // whole quads (F % 32 == 0)
+  const int u = 8 * i;
+  const float* g = gu + (size_t)tok * 2 * F + 2 * H * (u / H) + u % H;
+  const float4 g0 = reinterpret_cast<const float4*>(g)[0], g1 = reinterpret_cast<const float4*>(g)[1];
+  const float4 u0 = reinterpret_cast<const float4*>(g + H)[0], u1 = reinterpret_cast<const float4*>(g + H)[1];
+  const float v[8] = {gelu_mul1(g0.x, u0.x), gelu_mul1(g0.y, u0.y), gelu_mul1(g0.z, u0.z), gelu_mul1(g0.w, u0.w),
+                      gelu_mul1(g1.x, u1.x), gelu_mul1(g1.y, u1.y), gelu_mul1(g1.z, u1.z), gelu_mul1(g1.w, u1.w)};
+  q8_block_quad(v, i & 3, xq + (size_t)tok * xstride + i / 4);
+}
+
 }  // namespace
 
 void launch_prefill_norm(const PrefillNorm& a, int T, hipStream_t s) {
   if (a.n > 256 * PN_EPT || a.n % 32) throw std::runtime_error("prefill_norm: n_embd");
+  const int eb = (a.n / 32 + 63) / 64;
+  if (!a.table && eb <= 3 && !getenv("LLMI_PREFILL_NORM_V1")) {
+    switch (eb) {
+      case 1: hipLaunchKernelGGL(prefill_norm_res_kernel<1>, dim3(T), dim3(256), 0, s, a); break;
+      case 2: hipLaunchKernelGGL(prefill_norm_res_kernel<2>, dim3(T), dim3(256), 0, s, a); break;
+      default: hipLaunchKernelGGL(prefill_norm_res_kernel<3>, dim3(T), dim3(256), 0, s, a); break;
+    }
+    LLMI_HIP(hipGetLastError());
+    return;
+  }
   hipLaunchKernelGGL(prefill_norm_kernel, dim3(T), dim3(256), (size_t)a.n * 4, s, a);
   LLMI_HIP(hipGetLastError());
 }
@@ -1158,6 +1265,11 @@ void launch_prefill_attn(const PrefillAttn& a, int T, hipStream_t s) {
 
 void launch_prefill_gelu(const float* gu, int F, int H, XBlock* xq, int xstride, int T, hipStream_t s) {
   if (F % 32 || H <= 0 || F % H) throw std::runtime_error("prefill_gelu: shape");
+  if (H % 8 == 0 && !getenv("LLMI_PREFILL_GELU_V1")) {
+    hipLaunchKernelGGL(prefill_gelu8_kernel, dim3((F / 8 + 255) / 256, T), dim3(256), 0, s, gu, F, H, xq, xstride);
+    LLMI_HIP(hipGetLastError());
+    return;
+  }
   hipLaunchKernelGGL(prefill_gelu_kernel, dim3((F + 255) / 256, T), dim3(256), 0, s, gu, F, H, xq, xstride);
   LLMI_HIP(hipGetLastError());
 }
