@@ -1127,6 +1127,167 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(PrefillAttn a) {
 }
 
 // ---------------------------------------------------------------------------
+// causal attention on the matrix cores (default): one work-group per (kv head,
+// block of 32 query tokens), one wave per query head of the GQA group; 32-key
+// tiles of K and V stream into a double-buffered LDS image by LDS-DMA (rows of
+// the cache as they lie, 16-B units XOR-swizzled by key: conflict-free reads).
+//   S^T = K Q^T   (v_mfma_f32_32x32x16_f16 over head_dim; Q^T fragments held
+//                  in registers): a lane holds 16 keys' scores of its query
+//   online softmax per query in fp32 (the other 16 keys in lane ^ 32)
+//   O^T += V^T P^T  P^T from the score registers as is (f16), the MFMA's k
+//                  order permuted to the registers' key order; V^T by
+//                  ds_read_b64_tr_b16 (transposing LDS read) from the
+//                  row-major V image
+// Output heads as Q8_0 blocks (quantize_row_q8_0 arithmetic, the 32 values of
+// a block in lanes q and q + 32).  A query's result depends only on the cache
+// and its own q: exact under re-chunking.
+// ---------------------------------------------------------------------------
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef __fp16 fp16x4 __attribute__((__vector_size__(4 * sizeof(__fp16))));
+
+template <int HD, int G>
+__global__ __launch_bounds__(64 * G) void prefill_attn_mfma_kernel(PrefillAttn a, int T) {
+  constexpr int U = HD / 8;                // 16-B units per cache row
+  constexpr int SWM = U < 16 ? U - 1 : 15;  // swizzle mask (units)
+  constexpr int ROWB = HD * 2;              // bytes per cache row
+  constexpr int TILE = 32 * ROWB;           // bytes per K (or V) tile
+  constexpr int P = 2 * TILE / 1024;        // DMA pieces per tile (K then V)
+  static_assert(P % G == 0 && P / G <= 63, "pieces");
+  constexpr int RPP = 1024 / ROWB;          // cache rows per piece
+  __shared__ __attribute__((aligned(16))) unsigned char s_kv[2][2][TILE];
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), r = lane & 31, h = lane >> 5;
+  const int hk = blockIdx.x, tok0 = blockIdx.y * 32, hq = hk * G + w;
+  const int qtok = min(tok0 + r, T - 1);
+  const int qpos = a.pos0 + tok0 + r;                       // this lane's query position
+  const int last_pos = a.pos0 + min(tok0 + 32, T) - 1;     // the block's last query
+  const int first_pos = a.pos0 + tok0;
+  const int n_tiles = last_pos / 32 + 1;
+  const size_t cache0 = (size_t)hk * a.max_ctx;
+  // this wave's DMA pieces: lane -> (row, slot), source unit = slot ^ (row & SWM)
+  auto issue = [&](int t) {
+    unsigned char* dst = &s_kv[t & 1][0][0];
+#pragma unroll
+    for (int i = 0; i < P / G; i++) {
+      const int p = w + i * G, kind = p / (P / 2), pp = p % (P / 2);
+      const int row = pp * RPP + lane / U, slot = lane % U, u = slot ^ (row & SWM);
+      const int key = min(32 * t + row, a.max_ctx - 1);
+      const uint16_t* src = (kind ? a.v_cache : a.k_cache) + (cache0 + key) * HD + u * 8;
+      glds16(src, dst + kind * TILE + pp * 1024);
+    }
+  };
+  issue(0);
+  typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+  // Q^T fragments: lane (query r, h) holds q[d = 16 c + 8 h .. + 7]
+  f16x8 qf[HD / 16];
+  const uint4* qrow = reinterpret_cast<const uint4*>(a.q + ((size_t)qtok * a.n_head + hq) * HD);
+#pragma unroll
+  for (int c = 0; c < HD / 16; c++) qf[c] = __builtin_bit_cast(f16x8, qrow[2 * c + h]);
+  v16f o[HD / 32];
+#pragma unroll
+  for (int i = 0; i < HD / 32; i++) o[i] = v16f{};
+  float m_run = -INFINITY, l_run = 0.0f;
+  const int lg = lane >> 4, li = lane & 15, tq = li >> 2, tp = li & 3;  // tr_b16 group / position
+  for (int t = 0; t < n_tiles; t++) {
+    vm_wait<0>();
+    __builtin_amdgcn_s_barrier();  // tile t landed in every wave; tile t - 1's buffer is free
+    if (t + 1 < n_tiles) issue(t + 1);
+    const unsigned char* kt = &s_kv[t & 1][0][0];
+    const unsigned char* vt = &s_kv[t & 1][1][0];
+    // S^T: rows = keys (A from the K image), cols = queries
+    v16f sc = {};
+#pragma unroll
+    for (int c = 0; c < HD / 16; c++) {
+      const f16x8 kf = *reinterpret_cast<const f16x8*>(kt + r * ROWB + (((2 * c + h) ^ (r & SWM)) * 16));
+      sc = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[c], sc, 0, 0, 0);
+    }
+    // causal mask (select, never arithmetic on a masked score) + online softmax
+    const bool diag = 32 * t + 31 > first_pos;
+    float mt = -INFINITY;
+#pragma unroll
+    for (int reg = 0; reg < 16; reg++) {
+      const int key = 32 * t + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+      if (diag && key > qpos) sc[reg] = -INFINITY;
+      mt = fmaxf(mt, sc[reg]);
+    }
+    mt = fmaxf(mt, __shfl_xor(mt, 32));
+    const float m_new = fmaxf(m_run, mt);
+    const float alpha = expf(m_run - m_new);
+    float ps = 0.0f;
+    f16x8 pb[2];
+#pragma unroll
+    for (int reg = 0; reg < 16; reg++) {
+      const float pv = expf(sc[reg] - m_new);
+      ps += pv;
+      pb[reg >> 3][reg & 7] = (_Float16)pv;
+    }
+    ps += __shfl_xor(ps, 32);
+    l_run = l_run * alpha + ps;
+    m_run = m_new;
+#pragma unroll
+    for (int i = 0; i < HD / 32; i++) o[i] *= alpha;
+    // O^T += V^T P^T: MFMA kk (keys 16 kk ..) takes element j = key (j & 3) + 8 (j >> 2) + 4 h + 16 kk;
+    // V^T fragment by two transposing reads (rows = keys 16 kk + 4 h + {0, 8} + 0..3)
+#pragma unroll
+    for (int kk = 0; kk < 2; kk++) {
+#pragma unroll
+      for (int i = 0; i < HD / 32; i++) {
+        const int gh = lg >> 1;  // the h of this 16-lane group
+        const int col = 32 * i + 16 * (lg & 1) + 4 * tp;  // first of the 4 columns this lane addresses
+        // (the v4f16 form, joined by a shuffle: element-wise extraction from the v4i16 form was
+        // miscompiled into a splat of element 0 -- scripts/dev/pv_check.hip)
+        f16x4 vv[2];
+#pragma unroll
+        for (int e = 0; e < 2; e++) {
+          const int key = 16 * kk + 4 * gh + 8 * e + tq;
+          const int off = key * ROWB + (((col >> 3) ^ (key & SWM)) * 16) + (col & 7) * 2;
+          vv[e] = __builtin_bit_cast(f16x4, __builtin_amdgcn_ds_read_tr16_b64_v4f16(
+                                                 (__attribute__((address_space(3))) fp16x4*)(vt + off)));
+        }
+        const f16x8 vf = __builtin_shufflevector(vv[0], vv[1], 0, 1, 2, 3, 4, 5, 6, 7);
+        o[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf, pb[kk], o[i], 0, 0, 0);
+      }
+    }
+  }
+  // O = O^T / l -> Q8_0 blocks (32 head dims = one tile column; lanes q and q + 32 hold 16 each)
+  if (tok0 + r >= T) return;  // after the last LDS read: the partner lane of a live query is also out
+  const float inv_l = l_run;
+  XBlock* xo = a.xq + (size_t)(tok0 + r) * a.xstride + (size_t)hq * HD / 32;
+#pragma unroll
+  for (int i = 0; i < HD / 32; i++) {
+    float v[16];
+    float amax = 0.0f;
+#pragma unroll
+    for (int reg = 0; reg < 16; reg++) {
+      v[reg] = o[i][reg] / inv_l;
+      amax = fmaxf(amax, fabsf(v[reg]));
+    }
+    amax = fmaxf(amax, __shfl_xor(amax, 32));
+    const float dd = amax / 127.0f;
+    const float id = dd != 0.0f ? 1.0f / dd : 0.0f;
+    int sum = 0;
+    uint32_t wq[4];
+#pragma unroll
+    for (int g = 0; g < 4; g++) {
+      wq[g] = 0;
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        const int qv = nearest_int_fma(v[4 * g + e], id);
+        sum += qv;
+        wq[g] |= (uint32_t)(qv & 0xFF) << (8 * e);
+      }
+    }
+    sum += __shfl_xor(sum, 32);
+    uint32_t* qb = reinterpret_cast<uint32_t*>(xo + i);
+#pragma unroll
+    for (int g = 0; g < 4; g++) qb[2 * g + h] = wq[g];  // bytes 8 g + 4 h .. + 3
+    if (h == 0) {
+      xo[i].d = h2f(f2h_ggml(dd));
+      xo[i].nsum8 = -8 * sum;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // GELU(gate) * up from the interleaved gate/up GEMM rows -> Q8_0 (32 lanes a block)
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void prefill_gelu_kernel(const float* __restrict__ gu, int F, int H,
@@ -1244,8 +1405,18 @@ void launch_prefill_qk(const PrefillQK& a, int T, hipStream_t s) {
 
 template <int HD>
 static void attn_g(const PrefillAttn& a, int T, hipStream_t s) {
+  const int G = a.n_head / a.n_head_kv;
+  if (!getenv("LLMI_PREFILL_ATTN_V1") && HD >= 64) {
+    const dim3 grid(a.n_head_kv, (T + 31) / 32);
+    switch (G) {
+      case 1: hipLaunchKernelGGL((prefill_attn_mfma_kernel<HD, 1>), grid, dim3(64), 0, s, a, T); return;
+      case 2: hipLaunchKernelGGL((prefill_attn_mfma_kernel<HD, 2>), grid, dim3(128), 0, s, a, T); return;
+      case 4: hipLaunchKernelGGL((prefill_attn_mfma_kernel<HD, 4>), grid, dim3(256), 0, s, a, T); return;
+      default: break;
+    }
+  }
   const dim3 grid(a.n_head_kv, T);
-  switch (a.n_head / a.n_head_kv) {
+  switch (G) {
     case 1: hipLaunchKernelGGL((prefill_attn_kernel<HD, 1>), grid, dim3(256), 0, s, a); break;
     case 2: hipLaunchKernelGGL((prefill_attn_kernel<HD, 2>), grid, dim3(256), 0, s, a); break;
     case 4: hipLaunchKernelGGL((prefill_attn_kernel<HD, 4>), grid, dim3(256), 0, s, a); break;

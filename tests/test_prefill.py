@@ -98,3 +98,25 @@ def test_prefill_gemm_versions_bitwise(monkeypatch):
         assert d <= 1e-2
     monkeypatch.delenv("LLMI_PG5")
     monkeypatch.delenv("LLMI_PREFILL_GEMM")
+
+
+@pytest.mark.parametrize("cfg_name,n_prompt", [("mini-4b", 300), ("mini-1b", 77), ("mini-27b", 45)])
+def test_prefill_attention_mfma_vs_vector(cfg_name, n_prompt, monkeypatch):
+    """The causal prefill attention on the matrix cores (prefill_attn_mfma_kernel: S^T = K Q^T and
+    O^T = V^T P^T with P rounded to f16) against the fp32 vector kernel it replaced
+    (LLMI_PREFILL_ATTN_V1): same greedy token, logits within the fast budget (both are fp32-class
+    attentions; the 2-layer minis amplify a one-step change of a Q8_0 rounding, tests/test_hip_model.py;
+    op level the two kernels' Q8_0 outputs differ by about one quantization step:
+    scripts/dev/pattn_check.cpp)."""
+    from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
+    cfg = CONFIGS[cfg_name]
+    g = build_gemma3_gguf(cfg, seed=31)
+    prompt = np.random.default_rng(4).integers(4, cfg.vocab, n_prompt).astype(np.int32)
+    new = _model(g, monkeypatch).forward(prompt, 0)
+    monkeypatch.setenv("LLMI_PREFILL_ATTN_V1", "1")
+    old = _model(g, monkeypatch).forward(prompt, 0)
+    monkeypatch.delenv("LLMI_PREFILL_ATTN_V1")
+    d = float(np.abs(new - old).max())
+    print(f"{cfg_name} n={n_prompt}: max|mfma - vector attention| = {d:.3g}")
+    assert d <= FAST_VS_REF
+    assert int(np.argmax(new)) == int(np.argmax(old))
