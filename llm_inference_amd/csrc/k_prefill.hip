@@ -1145,34 +1145,40 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(PrefillAttn a) {
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef __fp16 fp16x4 __attribute__((__vector_size__(4 * sizeof(__fp16))));
 
-template <int HD, int G>
-__global__ __launch_bounds__(64 * G) void prefill_attn_mfma_kernel(PrefillAttn a, int T) {
+template <int HD, int G, int S>
+__global__ __launch_bounds__(64 * G * S) void prefill_attn_mfma_kernel(PrefillAttn a, int T) {
   constexpr int U = HD / 8;                // 16-B units per cache row
   constexpr int SWM = U < 16 ? U - 1 : 15;  // swizzle mask (units)
   constexpr int ROWB = HD * 2;              // bytes per cache row
   constexpr int TILE = 32 * ROWB;           // bytes per K (or V) tile
-  constexpr int P = 2 * TILE / 1024;        // DMA pieces per tile (K then V)
-  static_assert(P % G == 0 && P / G <= 63, "pieces");
+  constexpr int NW = G * S;                 // waves: head g = w % G, key split s = w / G
+  constexpr int P = S * 2 * TILE / 1024;    // DMA pieces per round (S tiles, K then V)
+  static_assert(P % NW == 0 && P / NW <= 63, "pieces");
   constexpr int RPP = 1024 / ROWB;          // cache rows per piece
-  __shared__ __attribute__((aligned(16))) unsigned char s_kv[2][2][TILE];
+  constexpr int RING = 2 * S * 2 * TILE;    // two rounds of S tiles
+  constexpr int MERGE = (S - 1) * G * 64 * (HD / 2 + 2) * 4;
+  __shared__ __attribute__((aligned(16))) unsigned char s_kv[RING > MERGE ? RING : MERGE];
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), r = lane & 31, h = lane >> 5;
-  const int hk = blockIdx.x, tok0 = blockIdx.y * 32, hq = hk * G + w;
+  const int g = w % G, sp = w / G;
+  // heaviest (last) query blocks first: dispatch order is a speed matter only
+  const int hk = blockIdx.x, tok0 = (gridDim.y - 1 - blockIdx.y) * 32, hq = hk * G + g;
   const int qtok = min(tok0 + r, T - 1);
   const int qpos = a.pos0 + tok0 + r;                       // this lane's query position
   const int last_pos = a.pos0 + min(tok0 + 32, T) - 1;     // the block's last query
   const int first_pos = a.pos0 + tok0;
-  const int n_tiles = last_pos / 32 + 1;
+  const int n_tiles = last_pos / 32 + 1, n_rounds = (n_tiles + S - 1) / S;
   const size_t cache0 = (size_t)hk * a.max_ctx;
-  // this wave's DMA pieces: lane -> (row, slot), source unit = slot ^ (row & SWM)
-  auto issue = [&](int t) {
-    unsigned char* dst = &s_kv[t & 1][0][0];
+  // round q: tiles S q .. S q + S - 1 into ring half q & 1; tile S q + j at slot j of the half
+  auto tile_ptr = [&](int round, int j) { return s_kv + ((round & 1) * S + j) * 2 * TILE; };
+  auto issue = [&](int round) {
 #pragma unroll
-    for (int i = 0; i < P / G; i++) {
-      const int p = w + i * G, kind = p / (P / 2), pp = p % (P / 2);
+    for (int i = 0; i < P / NW; i++) {
+      const int p = w + i * NW, j = p / (2 * TILE / 1024), q = p % (2 * TILE / 1024);
+      const int kind = q / (TILE / 1024), pp = q % (TILE / 1024);
       const int row = pp * RPP + lane / U, slot = lane % U, u = slot ^ (row & SWM);
-      const int key = min(32 * t + row, a.max_ctx - 1);
+      const int key = min(32 * (S * round + j) + row, a.max_ctx - 1);
       const uint16_t* src = (kind ? a.v_cache : a.k_cache) + (cache0 + key) * HD + u * 8;
-      glds16(src, dst + kind * TILE + pp * 1024);
+      glds16(src, tile_ptr(round, j) + kind * TILE + pp * 1024);
     }
   };
   issue(0);
@@ -1187,12 +1193,14 @@ __global__ __launch_bounds__(64 * G) void prefill_attn_mfma_kernel(PrefillAttn a
   for (int i = 0; i < HD / 32; i++) o[i] = v16f{};
   float m_run = -INFINITY, l_run = 0.0f;
   const int lg = lane >> 4, li = lane & 15, tq = li >> 2, tp = li & 3;  // tr_b16 group / position
-  for (int t = 0; t < n_tiles; t++) {
+  for (int round = 0; round < n_rounds; round++) {
     vm_wait<0>();
-    __builtin_amdgcn_s_barrier();  // tile t landed in every wave; tile t - 1's buffer is free
-    if (t + 1 < n_tiles) issue(t + 1);
-    const unsigned char* kt = &s_kv[t & 1][0][0];
-    const unsigned char* vt = &s_kv[t & 1][1][0];
+    __builtin_amdgcn_s_barrier();  // round landed in every wave; the previous round's half is free
+    if (round + 1 < n_rounds) issue(round + 1);
+    const int t = S * round + sp;  // this split's tile
+    if (t >= n_tiles) continue;    // wave-uniform; no cross-lane read is skipped by part of a wave
+    const unsigned char* kt = tile_ptr(round, sp);
+    const unsigned char* vt = kt + TILE;
     // S^T: rows = keys (A from the K image), cols = queries
     v16f sc = {};
 #pragma unroll
@@ -1211,12 +1219,13 @@ __global__ __launch_bounds__(64 * G) void prefill_attn_mfma_kernel(PrefillAttn a
     }
     mt = fmaxf(mt, __shfl_xor(mt, 32));
     const float m_new = fmaxf(m_run, mt);
-    const float alpha = expf(m_run - m_new);
+    // a split's first tile may be fully masked for some queries (m_new = -inf): keep its terms 0
+    const float alpha = m_new == -INFINITY ? 1.0f : expf(m_run - m_new);
     float ps = 0.0f;
     f16x8 pb[2];
 #pragma unroll
     for (int reg = 0; reg < 16; reg++) {
-      const float pv = expf(sc[reg] - m_new);
+      const float pv = m_new == -INFINITY ? 0.0f : expf(sc[reg] - m_new);
       ps += pv;
       pb[reg >> 3][reg & 7] = (_Float16)pv;
     }
@@ -1248,9 +1257,38 @@ __global__ __launch_bounds__(64 * G) void prefill_attn_mfma_kernel(PrefillAttn a
       }
     }
   }
+  // merge the key splits of each head through LDS (split 0 combines, in split order)
+  if constexpr (S > 1) {
+    vm_wait<0>();
+    __builtin_amdgcn_s_barrier();  // every wave is done with the ring
+    float* mg = reinterpret_cast<float*>(s_kv);
+    if (sp > 0) {
+      float* my = mg + (size_t)((sp - 1) * G + g) * 64 * (HD / 2 + 2);
+      my[lane] = m_run;
+      my[64 + lane] = l_run;
+#pragma unroll
+      for (int i = 0; i < HD / 32; i++)
+#pragma unroll
+        for (int reg = 0; reg < 16; reg++) my[128 + (i * 16 + reg) * 64 + lane] = o[i][reg];
+    }
+    __syncthreads();
+    if (sp > 0) return;
+#pragma unroll
+    for (int s2 = 1; s2 < S; s2++) {
+      const float* ot = mg + (size_t)((s2 - 1) * G + g) * 64 * (HD / 2 + 2);
+      const float m2 = ot[lane], l2 = ot[64 + lane];
+      const float mm = fmaxf(m_run, m2);
+      const float a1 = m_run == -INFINITY ? 0.0f : expf(m_run - mm), a2 = m2 == -INFINITY ? 0.0f : expf(m2 - mm);
+      l_run = l_run * a1 + l2 * a2;
+      m_run = mm;
+#pragma unroll
+      for (int i = 0; i < HD / 32; i++)
+#pragma unroll
+        for (int reg = 0; reg < 16; reg++) o[i][reg] = o[i][reg] * a1 + ot[128 + (i * 16 + reg) * 64 + lane] * a2;
+    }
+  }
   // O = O^T / l -> Q8_0 blocks (32 head dims = one tile column; lanes q and q + 32 hold 16 each)
   if (tok0 + r >= T) return;  // after the last LDS read: the partner lane of a live query is also out
-  const float inv_l = l_run;
   XBlock* xo = a.xq + (size_t)(tok0 + r) * a.xstride + (size_t)hq * HD / 32;
 #pragma unroll
   for (int i = 0; i < HD / 32; i++) {
@@ -1258,7 +1296,7 @@ __global__ __launch_bounds__(64 * G) void prefill_attn_mfma_kernel(PrefillAttn a
     float amax = 0.0f;
 #pragma unroll
     for (int reg = 0; reg < 16; reg++) {
-      v[reg] = o[i][reg] / inv_l;
+      v[reg] = o[i][reg] / l_run;
       amax = fmaxf(amax, fabsf(v[reg]));
     }
     amax = fmaxf(amax, __shfl_xor(amax, 32));
@@ -1267,19 +1305,19 @@ __global__ __launch_bounds__(64 * G) void prefill_attn_mfma_kernel(PrefillAttn a
     int sum = 0;
     uint32_t wq[4];
 #pragma unroll
-    for (int g = 0; g < 4; g++) {
-      wq[g] = 0;
+    for (int gq = 0; gq < 4; gq++) {
+      wq[gq] = 0;
 #pragma unroll
       for (int e = 0; e < 4; e++) {
-        const int qv = nearest_int_fma(v[4 * g + e], id);
+        const int qv = nearest_int_fma(v[4 * gq + e], id);
         sum += qv;
-        wq[g] |= (uint32_t)(qv & 0xFF) << (8 * e);
+        wq[gq] |= (uint32_t)(qv & 0xFF) << (8 * e);
       }
     }
     sum += __shfl_xor(sum, 32);
     uint32_t* qb = reinterpret_cast<uint32_t*>(xo + i);
 #pragma unroll
-    for (int g = 0; g < 4; g++) qb[2 * g + h] = wq[g];  // bytes 8 g + 4 h .. + 3
+    for (int gq = 0; gq < 4; gq++) qb[2 * gq + h] = wq[gq];  // bytes 8 gq + 4 h .. + 3
     if (h == 0) {
       xo[i].d = h2f(f2h_ggml(dd));
       xo[i].nsum8 = -8 * sum;
@@ -1408,10 +1446,15 @@ static void attn_g(const PrefillAttn& a, int T, hipStream_t s) {
   const int G = a.n_head / a.n_head_kv;
   if (!getenv("LLMI_PREFILL_ATTN_V1") && HD >= 64) {
     const dim3 grid(a.n_head_kv, (T + 31) / 32);
+    // key splits per work-group (LDS: two rounds of S tiles, and the merge)
+    constexpr int S4 = HD >= 256 ? 2 : 4;
     switch (G) {
-      case 1: hipLaunchKernelGGL((prefill_attn_mfma_kernel<HD, 1>), grid, dim3(64), 0, s, a, T); return;
-      case 2: hipLaunchKernelGGL((prefill_attn_mfma_kernel<HD, 2>), grid, dim3(128), 0, s, a, T); return;
-      case 4: hipLaunchKernelGGL((prefill_attn_mfma_kernel<HD, 4>), grid, dim3(256), 0, s, a, T); return;
+      // (head_dim 256 at G 1 or 4: one split -- more would spill the 128 O^T + 64 Q^T registers)
+      case 1: hipLaunchKernelGGL((prefill_attn_mfma_kernel<HD, 1, HD >= 256 ? 1 : 4>), grid, dim3(HD >= 256 ? 64 : 256), 0, s,
+                                 a, T); return;
+      case 2: hipLaunchKernelGGL((prefill_attn_mfma_kernel<HD, 2, S4>), grid, dim3(128 * S4), 0, s, a, T); return;
+      case 4: hipLaunchKernelGGL((prefill_attn_mfma_kernel<HD, 4, HD >= 256 ? 1 : 2>), grid, dim3(HD >= 256 ? 256 : 512), 0, s,
+                                 a, T); return;
       default: break;
     }
   }
