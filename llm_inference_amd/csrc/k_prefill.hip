@@ -24,6 +24,16 @@ namespace {
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
+typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void store_f16x8(uint16_t* dst, const float (&v)[8]) {  // 16-B aligned
+  uint4 o;
+  o.x = __builtin_bit_cast(uint32_t, f16x2v{(_Float16)v[0], (_Float16)v[1]});
+  o.y = __builtin_bit_cast(uint32_t, f16x2v{(_Float16)v[2], (_Float16)v[3]});
+  o.z = __builtin_bit_cast(uint32_t, f16x2v{(_Float16)v[4], (_Float16)v[5]});
+  o.w = __builtin_bit_cast(uint32_t, f16x2v{(_Float16)v[6], (_Float16)v[7]});
+  *reinterpret_cast<uint4*>(dst) = o;
+}
 
 __device__ __forceinline__ float rms_scale_pf(float sum, int n, double eps) {  // ops.cpp:37-38
   return 1.0f / sqrtf((float)((double)(sum / (float)n) + eps));
@@ -101,6 +111,14 @@ __global__ __launch_bounds__(256) void prefill_norm_kernel(PrefillNorm a) {
     if (i < n) s_x[i] = (sc2 * v[k]) * a.w_next[i];
   }
   __syncthreads();
+  if (a.x16) {
+    for (int i = t; i < n / 8; i += 256) {
+      const float4 f0 = reinterpret_cast<const float4*>(s_x)[2 * i], f1 = reinterpret_cast<const float4*>(s_x)[2 * i + 1];
+      const float vv[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+      store_f16x8(a.x16 + (size_t)tok * a.x16stride + 8 * i, vv);
+    }
+    return;
+  }
   XBlock* xq = a.xq + (size_t)tok * a.xstride;
   for (int i = t; i < n / 8; i += 256) {  // a DPP quad of lanes per Q8_0 block
     const float4 f0 = reinterpret_cast<const float4*>(s_x)[2 * i], f1 = reinterpret_cast<const float4*>(s_x)[2 * i + 1];
@@ -108,6 +126,7 @@ __global__ __launch_bounds__(256) void prefill_norm_kernel(PrefillNorm a) {
     q8_block_quad(vv, i & 3, xq + (i >> 2));
   }
 }
+
 
 // residual mode, vectorized: a DPP quad of lanes per Q8_0 block (lane t & 3 owns elements 8 (t & 3) ..
 // + 7 of block t / 4 + 64 k), float4 loads, x quantized from registers (the decode layer prologue's scheme,
@@ -187,7 +206,9 @@ __global__ __launch_bounds__(256) void prefill_norm_res_kernel(PrefillNorm a) {
       v[4 * h + 2] = (sc2 * r.z) * wn.z;
       v[4 * h + 3] = (sc2 * r.w) * wn.w;
     }
-    if (in_row(k)) q8_block_quad(v, sub, xq + b);  // whole quads in or out
+    if (!in_row(k)) continue;  // whole quads in or out
+    if (a.x16) store_f16x8(a.x16 + (size_t)tok * a.x16stride + b * 32 + sub * 8, v);
+    else q8_block_quad(v, sub, xq + b);
   }
 }
 
@@ -925,6 +946,179 @@ __global__ __launch_bounds__(512, (WK == 1 || NT > 1) ? 2 : 4) void prefill_gemm
 }
 
 // ---------------------------------------------------------------------------
+// GEMM v6 (f16 prefill, BASELINE configs[2]'s "F16 MFMA prefill GEMM"):
+// f16 activations [T][K] (written so by the norm / attention / GELU
+// producers instead of Q8_0 blocks) times the Q4_0 weights dequantized to f16
+// in registers, w = f16(d_w * (q - 8)) (one rounding), on
+// v_mfma_f32_32x32x16_f16 with the fp32 accumulator carried over all of K:
+// no per-block epilogue -- the v5 VALU bound (conversions and FMAs per 32-k
+// block) is gone; a wave dequantizes its 32 rows' block once for NT token
+// groups.  The v5 frame: LDS-DMA ring of KB-block stages filled by whole runs
+// of memory (a row's KB blocks, a token's KB x 64 B), XOR-swizzled 16-B slots,
+// waves in a WR x WT x WK grid (WK groups split K: block b -> group b % WK,
+// partial sums added in group order), token tiles of a row tile on one XCD.
+// Deterministic and independent of the chunking; within the fast budget of
+// the Q8_0 path (an f16 product per weight instead of Q8_0 activations).
+// ---------------------------------------------------------------------------
+template <int WR, int WT, int WK, int NT, int KB, int NS>
+struct PG6 {
+  static constexpr int NW = WR * WT * WK, MR = 32 * WR, TN = 32 * NT * WT;
+  static constexpr int XU = KB * 4;  // 16-B activation units per token per stage
+  static constexpr int P_WQ = KB * MR / 64, P_WD = (KB / 2) * MR / 64, P_X = TN * XU / 64;
+  static constexpr int P = P_WQ + P_WD + P_X, PW = (P + NW - 1) / NW;
+  static constexpr int O_WD = KB * MR * 16, O_X = O_WD + (KB / 2) * MR * 4;
+  static constexpr int STAGE = O_X + TN * XU * 16;
+  static constexpr int EPI = NW * 32 * 33 * 4;
+  static constexpr int LDS = STAGE * NS > EPI ? STAGE * NS : EPI;
+  static_assert(KB % WK == 0 && (KB == 2 || KB == 4), "KB");
+  static_assert(KB * MR % 64 == 0 && (KB / 2) * MR % 64 == 0 && TN * XU % 64 == 0, "pieces of 64 lanes");
+  static_assert(PW * (NS - 2) <= 63, "vmcnt range");
+};
+
+template <int KB>
+__device__ __forceinline__ int pg6_wsw(int row) { return KB == 4 ? (row >> 2) & 3 : (row >> 3) & 1; }
+
+template <int WR, int WT, int WK, int NT, int KB, int NS>
+__global__ __launch_bounds__(512, 2) void prefill_gemm6_kernel(PrefillGemm16 a) {
+  using C = PG6<WR, WT, WK, NT, KB, NS>;
+  typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+  __shared__ __attribute__((aligned(16))) unsigned char s_ring[C::LDS];
+  const int t = threadIdx.x, lane = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6), r = lane & 31, h = lane >> 5;
+  const int wr = w % WR, wt = (w / WR) % WT, kg = w / (WR * WT);
+  const int nb = a.nb, nst = nb / KB;
+  const int n_rt = a.rows / C::MR, n_tt = (a.T + C::TN - 1) / C::TN;
+  const int bid = blockIdx.x;
+  int rt, tt;
+  if (n_rt % 8 == 0) {
+    const int j = bid >> 3;
+    rt = (j / n_tt) * 8 + (bid & 7);
+    tt = j % n_tt;
+  } else {
+    rt = bid / n_tt;
+    tt = bid % n_tt;
+  }
+  const int n0 = rt * C::MR, tk0 = tt * C::TN;
+  const unsigned char* pb[C::PW];
+  int pk[C::PW], po[C::PW];
+#pragma unroll
+  for (int i = 0; i < C::PW; i++) {
+    const int p = (w + i * C::NW) % C::P;
+    if (p < C::P_WQ) {  // unit u: row u / KB, block slot u % KB
+      const int u = p * 64 + lane, row = u / KB, b = (u % KB) ^ pg6_wsw<KB>(row);
+      pk[i] = 0;
+      pb[i] = reinterpret_cast<const unsigned char*>(a.qs + q4_block_index(a.slab, a.rows, nb, n0 + row, b));
+      po[i] = p * 1024;
+    } else if (p < C::P_WQ + C::P_WD) {  // unit u: block pair u / MR, row u % MR
+      const int q = p - C::P_WQ, u = q * 64 + lane;
+      pk[i] = 1;
+      pb[i] = reinterpret_cast<const unsigned char*>(a.wd + q4_block_index(a.slab, a.rows, nb, n0 + u % C::MR, 2 * (u / C::MR)));
+      po[i] = C::O_WD + q * 256;
+    } else {  // unit u: (token, slot), the token's row of KB x 32 f16 as XU units, slot = unit ^ (tok & (XU - 1))
+      const int q = p - C::P_WQ - C::P_WD, u = q * 64 + lane;
+      const int tok = u / C::XU, un = (u % C::XU) ^ (tok & (C::XU - 1));
+      pk[i] = 2;
+      pb[i] = reinterpret_cast<const unsigned char*>(a.x + (size_t)min(tk0 + tok, a.T - 1) * a.xstride + un * 8);
+      po[i] = C::O_X + q * 1024;
+    }
+  }
+  auto issue = [&](int c) {
+    const int kb = c * KB;
+    const long wofs = a.slab ? (long)(kb >> 3) * a.rows * 8 + (kb & 7) : kb;
+    unsigned char* st = s_ring + (c % NS) * C::STAGE;
+#pragma unroll
+    for (int i = 0; i < C::PW; i++) {
+      const int k = pk[i];
+      const long off = k == 0 ? wofs * 16 : k == 1 ? wofs * 2 : (long)kb * 64;
+      if (k == 1) glds4(pb[i] + off, st + po[i]);
+      else glds16(pb[i] + off, st + po[i]);
+    }
+  };
+  auto wait_ahead = [&](int ahead) {
+    static_for<NS - 1>([&](auto kc) {
+      constexpr int k = decltype(kc)::value, n = NS - 2 - k;
+      if (ahead == n) vm_wait<C::PW * n>();
+    });
+  };
+  for (int c = 0; c < NS - 1 && c < nst; c++) issue(c);
+  v16f acc[NT];
+#pragma unroll
+  for (int j = 0; j < NT; j++) acc[j] = v16f{};
+  const int arow = 32 * wr + r, a_sw = pg6_wsw<KB>(arow);
+  int b_base[NT], b_sw[NT];
+#pragma unroll
+  for (int j = 0; j < NT; j++) {
+    const int tok = 32 * (wt * NT + j) + r;
+    b_base[j] = C::O_X + tok * C::XU * 16;
+    b_sw[j] = tok & (C::XU - 1);
+  }
+  const f16x2v m1032 = {(_Float16)-1032.0f, (_Float16)-1032.0f};
+  for (int c = 0; c < nst; c++) {
+    wait_ahead(min(NS - 2, nst - 1 - c));
+    __builtin_amdgcn_s_barrier();
+    if (c + NS - 1 < nst) issue(c + NS - 1);
+    const unsigned char* st = s_ring + (c % NS) * C::STAGE;
+    const uint32_t* wd = reinterpret_cast<const uint32_t*>(st + C::O_WD);
+#pragma unroll
+    for (int bb = 0; bb < KB / WK; bb++) {
+      const int b = bb * WK + kg;
+      // A: bytes 8h .. 8h + 7 of the row's block: low nibbles = k 8h.. (MFMA 0), high = k 16 + 8h.. (MFMA 1)
+      const uint2 qb = *reinterpret_cast<const uint2*>(st + (arow * KB + (b ^ a_sw)) * 16 + 8 * h);
+      const uint32_t wp = wd[(b >> 1) * C::MR + arow];
+      const uint32_t dsel = (WK == 1 ? (bb & 1) : (kg & 1)) ? (wp >> 16) : (wp & 0xFFFFu);
+      const f16x2v d2 = __builtin_bit_cast(f16x2v, dsel | (dsel << 16));
+      f16x8 A0, A1;
+      const uint32_t dw[2] = {qb.x, qb.y};
+#pragma unroll
+      for (int e = 0; e < 2; e++) {
+        const uint32_t v = dw[e], vh = v >> 4;
+#pragma unroll
+        for (int pr = 0; pr < 2; pr++) {  // bytes 2 pr, 2 pr + 1 of the dword
+          const uint32_t sel = pr ? 0x0C030C02u : 0x0C010C00u;
+          const uint32_t lo = (__builtin_amdgcn_perm(0u, v, sel) & 0x000F000Fu) | 0x64006400u;
+          const uint32_t hi = (__builtin_amdgcn_perm(0u, vh, sel) & 0x000F000Fu) | 0x64006400u;
+          const f16x2v fl = (__builtin_bit_cast(f16x2v, lo) + m1032) * d2;
+          const f16x2v fh = (__builtin_bit_cast(f16x2v, hi) + m1032) * d2;
+          A0[4 * e + 2 * pr] = fl[0];
+          A0[4 * e + 2 * pr + 1] = fl[1];
+          A1[4 * e + 2 * pr] = fh[0];
+          A1[4 * e + 2 * pr + 1] = fh[1];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < NT; j++) {
+        const unsigned char* xr = st + b_base[j];
+        const f16x8 B0 = *reinterpret_cast<const f16x8*>(xr + (((4 * b + h) ^ b_sw[j]) * 16));
+        const f16x8 B1 = *reinterpret_cast<const f16x8*>(xr + (((4 * b + 2 + h) ^ b_sw[j]) * 16));
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, B0, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, B1, acc[j], 0, 0, 0);
+      }
+    }
+  }
+  float* ep = reinterpret_cast<float*>(s_ring);
+#pragma unroll
+  for (int j = 0; j < NT; j++) {
+    __builtin_amdgcn_s_barrier();
+    float* mine = ep + (size_t)w * 32 * 33;
+#pragma unroll
+    for (int reg = 0; reg < 16; reg++) mine[r * 33 + (reg & 3) + 8 * (reg >> 2) + 4 * h] = acc[j][reg];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    for (int i = t; i < WT * C::MR * 32; i += 64 * C::NW) {
+      const int row = i % C::MR, tk = (i / C::MR) % 32, gt = i / (C::MR * 32);
+      const int tok = tk0 + 32 * (gt * NT + j) + tk;
+      float v = 0.0f;
+#pragma unroll
+      for (int g = 0; g < WK; g++) {
+        const int ww = (g * WT + gt) * WR + row / 32;
+        const float p = ep[(size_t)ww * 32 * 33 + tk * 33 + row % 32];
+        v = g ? v + p : p;
+      }
+      if (tok < a.T) a.out[(size_t)tok * a.ostride + n0 + row] = v;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // q/k norm + rope (+ q scale) and the K/V cache append, one wave per row
 // ---------------------------------------------------------------------------
 template <int HD>
@@ -1287,8 +1481,21 @@ __global__ __launch_bounds__(64 * G * S) void prefill_attn_mfma_kernel(PrefillAt
         for (int reg = 0; reg < 16; reg++) o[i][reg] = o[i][reg] * a1 + ot[128 + (i * 16 + reg) * 64 + lane] * a2;
     }
   }
-  // O = O^T / l -> Q8_0 blocks (32 head dims = one tile column; lanes q and q + 32 hold 16 each)
+  // O = O^T / l -> Q8_0 blocks (32 head dims = one tile column; lanes q and q + 32 hold 16 each), or f16
   if (tok0 + r >= T) return;  // after the last LDS read: the partner lane of a live query is also out
+  if (a.x16) {
+    uint16_t* xo16 = a.x16 + (size_t)(tok0 + r) * a.x16stride + (size_t)hq * HD;
+#pragma unroll
+    for (int i = 0; i < HD / 32; i++)
+#pragma unroll
+      for (int gq = 0; gq < 4; gq++) {  // dims 32 i + 8 gq + 4 h .. + 3
+        uint2 o2;
+        o2.x = __builtin_bit_cast(uint32_t, f16x2v{(_Float16)(o[i][4 * gq] / l_run), (_Float16)(o[i][4 * gq + 1] / l_run)});
+        o2.y = __builtin_bit_cast(uint32_t, f16x2v{(_Float16)(o[i][4 * gq + 2] / l_run), (_Float16)(o[i][4 * gq + 3] / l_run)});
+        *reinterpret_cast<uint2*>(xo16 + 32 * i + 8 * gq + 4 * h) = o2;
+      }
+    return;
+  }
   XBlock* xo = a.xq + (size_t)(tok0 + r) * a.xstride + (size_t)hq * HD / 32;
 #pragma unroll
   for (int i = 0; i < HD / 32; i++) {
@@ -1342,7 +1549,8 @@ __global__ __launch_bounds__(256) void prefill_gelu_kernel(const float* __restri
 // GELU(gate) * up -> Q8_0, vectorized: a thread per 8 consecutive hidden units (one DPP quad per Q8_0 block),
 // float4 loads from the interleaved gate/up rows (H % 8 == 0: the 8 units sit in one H-group)
 __global__ __launch_bounds__(256) void prefill_gelu8_kernel(const float* __restrict__ gu, int F, int H,
-                                                            XBlock* __restrict__ xq, int xstride) {
+                                                            XBlock* __restrict__ xq, int xstride,
+                                                            uint16_t* __restrict__ x16, int x16stride) {
   const int tok = blockIdx.y, i = blockIdx.x * 256 + threadIdx.x;
   if (i * 8 >= F) return;  // whole quads (F % 32 == 0)
   const int u = 8 * i;
@@ -1351,7 +1559,8 @@ __global__ __launch_bounds__(256) void prefill_gelu8_kernel(const float* __restr
   const float4 u0 = reinterpret_cast<const float4*>(g + H)[0], u1 = reinterpret_cast<const float4*>(g + H)[1];
   const float v[8] = {gelu_mul1(g0.x, u0.x), gelu_mul1(g0.y, u0.y), gelu_mul1(g0.z, u0.z), gelu_mul1(g0.w, u0.w),
                       gelu_mul1(g1.x, u1.x), gelu_mul1(g1.y, u1.y), gelu_mul1(g1.z, u1.z), gelu_mul1(g1.w, u1.w)};
-  q8_block_quad(v, i & 3, xq + (size_t)tok * xstride + i / 4);
+  if (x16) store_f16x8(x16 + (size_t)tok * x16stride + u, v);
+  else q8_block_quad(v, i & 3, xq + (size_t)tok * xstride + i / 4);
 }
 
 }  // namespace
@@ -1400,6 +1609,41 @@ static bool launch_gemm5(const PrefillGemm& a, hipStream_t s) {
   return try_gemm5<2, 2, 2, 1, 4>(a, s) || try_gemm5<1, 4, 2, 1, 4>(a, s);  // K split 2, 64 or 32 rows
 }
 
+template <int WR, int WT, int WK, int NT, int KB, int NS>
+static bool try_gemm6(const PrefillGemm16& a, hipStream_t s) {
+  using C = PG6<WR, WT, WK, NT, KB, NS>;
+  if (a.rows % C::MR || a.nb % KB) return false;
+  const int n = (a.rows / C::MR) * ((a.T + C::TN - 1) / C::TN);
+  hipLaunchKernelGGL((prefill_gemm6_kernel<WR, WT, WK, NT, KB, NS>), dim3(n), dim3(64 * C::NW), 0, s, a);
+  return true;
+}
+
+// v6 geometry (LLMI_PG6=<name> forces one for A/B); the K split depends on K alone (tensor-parallel shards
+// sum in the same order as the whole weight)
+void launch_prefill_gemm16(const DevWeight& w, const uint16_t* x, int xstride, int T, float* out, int ostride,
+                           hipStream_t s) {
+  if (!prefill_gemm_supported(w)) throw std::runtime_error("prefill_gemm16: unsupported weight");
+  PrefillGemm16 a;
+  a.qs = reinterpret_cast<const uint4*>(w.qs);
+  a.wd = w.d;
+  a.rows = w.rows;
+  a.nb = w.cols / 32;
+  a.slab = w.slab;
+  a.x = x;
+  a.xstride = xstride;
+  a.T = T;
+  a.out = out;
+  a.ostride = ostride;
+  const char* f = getenv("LLMI_PG6");
+  const std::string c = f ? f : a.nb >= 160 ? "k4" : "k2";
+  bool ok = false;
+  if (c == "big") ok = try_gemm6<4, 2, 1, 2, 2, 3>(a, s);
+  else if (c == "k4") ok = try_gemm6<1, 2, 4, 2, 4, 3>(a, s) || try_gemm6<1, 2, 4, 1, 4, 3>(a, s);
+  if (!ok) ok = try_gemm6<2, 2, 2, 2, 2, 3>(a, s) || try_gemm6<1, 4, 2, 1, 4, 3>(a, s);
+  if (!ok) throw std::runtime_error("prefill_gemm16: shape");
+  LLMI_HIP(hipGetLastError());
+}
+
 void launch_prefill_gemm(const DevWeight& w, const XBlock* x, int xstride, int T, float* out, int ostride,
                          hipStream_t s) {
   if (!prefill_gemm_supported(w)) throw std::runtime_error("prefill_gemm: unsupported weight");
@@ -1444,17 +1688,19 @@ void launch_prefill_qk(const PrefillQK& a, int T, hipStream_t s) {
 template <int HD>
 static void attn_g(const PrefillAttn& a, int T, hipStream_t s) {
   const int G = a.n_head / a.n_head_kv;
+  if (a.x16 && (getenv("LLMI_PREFILL_ATTN_V1") || (G != 1 && G != 2 && G != 4)))
+    throw std::runtime_error("prefill_attn: f16 output needs the MFMA kernel (GQA group 1, 2 or 4)");
   if (!getenv("LLMI_PREFILL_ATTN_V1") && HD >= 64) {
     const dim3 grid(a.n_head_kv, (T + 31) / 32);
-    // key splits per work-group (LDS: two rounds of S tiles, and the merge)
+    // key splits per work-group (LDS: two rounds of S tiles, and the merge); S depends on head_dim only, so a
+    // tensor-parallel rank (fewer heads per kv head: smaller G) merges the same splits as the whole model
+    // (bit-identical).  head_dim 256 at G 1 / 4 spills some of the 128 O^T + 64 Q^T registers (correct, slower).
     constexpr int S4 = HD >= 256 ? 2 : 4;
     switch (G) {
-      // (head_dim 256 at G 1 or 4: one split -- more would spill the 128 O^T + 64 Q^T registers)
-      case 1: hipLaunchKernelGGL((prefill_attn_mfma_kernel<HD, 1, HD >= 256 ? 1 : 4>), grid, dim3(HD >= 256 ? 64 : 256), 0, s,
-                                 a, T); return;
+      case 1: hipLaunchKernelGGL((prefill_attn_mfma_kernel<HD, 1, S4>), grid, dim3(64 * S4), 0, s, a, T); return;
       case 2: hipLaunchKernelGGL((prefill_attn_mfma_kernel<HD, 2, S4>), grid, dim3(128 * S4), 0, s, a, T); return;
-      case 4: hipLaunchKernelGGL((prefill_attn_mfma_kernel<HD, 4, HD >= 256 ? 1 : 2>), grid, dim3(HD >= 256 ? 256 : 512), 0, s,
-                                 a, T); return;
+      case 4: hipLaunchKernelGGL((prefill_attn_mfma_kernel<HD, 4, HD == 128 ? 2 : S4>), grid,
+                                 dim3(256 * (HD == 128 ? 2 : S4)), 0, s, a, T); return;
       default: break;
     }
   }
@@ -1477,10 +1723,13 @@ void launch_prefill_attn(const PrefillAttn& a, int T, hipStream_t s) {
   LLMI_HIP(hipGetLastError());
 }
 
-void launch_prefill_gelu(const float* gu, int F, int H, XBlock* xq, int xstride, int T, hipStream_t s) {
+void launch_prefill_gelu(const float* gu, int F, int H, XBlock* xq, int xstride, int T, hipStream_t s, uint16_t* x16,
+                         int x16stride) {
   if (F % 32 || H <= 0 || F % H) throw std::runtime_error("prefill_gelu: shape");
-  if (H % 8 == 0 && !getenv("LLMI_PREFILL_GELU_V1")) {
-    hipLaunchKernelGGL(prefill_gelu8_kernel, dim3((F / 8 + 255) / 256, T), dim3(256), 0, s, gu, F, H, xq, xstride);
+  if (x16 && H % 8) throw std::runtime_error("prefill_gelu: f16 output needs H % 8 == 0");
+  if (H % 8 == 0 && (x16 || !getenv("LLMI_PREFILL_GELU_V1"))) {
+    hipLaunchKernelGGL(prefill_gelu8_kernel, dim3((F / 8 + 255) / 256, T), dim3(256), 0, s, gu, F, H, xq, xstride, x16,
+                       x16stride);
     LLMI_HIP(hipGetLastError());
     return;
   }

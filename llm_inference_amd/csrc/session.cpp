@@ -763,9 +763,10 @@ void Session::ensure_prefill_buffers(int cap) {
   pf_resid_ = dalloc<float>((size_t)cap * E);
   pf_out_ = dalloc<float>((size_t)cap * pf_ostride_);
   pf_xq_ = dalloc<XBlock>((size_t)cap * pf_xs_);
+  pf_x16_ = dalloc<uint16_t>((size_t)cap * pf_xs_ * 32);
   pf_q_ = dalloc<uint16_t>((size_t)cap * maxq);
   if (tp_)  // all-gather staging: the largest exchanged [T][row] activation (f32 rows or Q8_0 block rows)
-    pf_gather_ = dalloc<uint8_t>((size_t)cap * std::max((size_t)E * 4, (size_t)pf_xs_ * sizeof(XBlock)));
+    pf_gather_ = dalloc<uint8_t>((size_t)cap * std::max({(size_t)E * 4, (size_t)pf_xs_ * sizeof(XBlock), (size_t)pf_xs_ * 64}));
   pf_cap_ = cap;
 }
 
@@ -799,11 +800,31 @@ void Session::prefill(const int32_t* tokens, int n, int pos) {
   int chunk = 512;
   if (const char* c = getenv("LLMI_PREFILL_CHUNK")) chunk = std::max(1, atoi(c));
   ensure_prefill_buffers(std::min(chunk, n));
-  const int XS = pf_xs_;
+  const int XS = pf_xs_, X16 = pf_xs_ * 32;
   const int r = tp_rank_;  // tensor parallel: this rank's column slices (0 on one device)
   const float emb_scale = std::sqrt(static_cast<float>(E));  // model.cpp:337-338
+  // Q8_0 activation blocks + the int8 GEMM (v5, default: the reference's Q8_0 numerics), or f16 activations + the
+  // f16 MFMA GEMM (v6, LLMI_PREFILL_F16=1: not faster yet -- activation tile re-reads bound it -- and further from
+  // the reference's Q8_0 arithmetic)
+  const int G = nh_ / std::max(nkv_, 1);
+  const bool f16 = getenv("LLMI_PREFILL_F16") && !getenv("LLMI_PREFILL_ATTN_V1") && (G == 1 || G == 2 || G == 4) &&
+                   layer_gemv_gelu_group(L_[0].gate_up[0].w.cols, L_[0].gate_up[0].w.type) % 8 == 0;
+  auto gemm = [&](const DevWeight& w, float* out, int ostride) {
+    if (f16) launch_prefill_gemm16(w, pf_x16_, X16, T_cur_, out, ostride, s);
+    else launch_prefill_gemm(w, pf_xq_, XS, T_cur_, out, ostride, s);
+  };
+  auto xtap = [&](const char* name, int l) {
+    if (f16) tap(name, l, pf_x16_, (size_t)T_cur_ * X16 * 2, s);
+    else tap(name, l, pf_xq_, (size_t)T_cur_ * XS * sizeof(XBlock), s);
+  };
+  auto xgather = [&](int cols) {  // this rank's activation columns [r * cols, (r + 1) * cols) to every rank
+    if (!tp_) return;
+    if (f16) gather_cols(pf_x16_, (size_t)X16 * 2, (size_t)cols * 2, T_cur_, s);
+    else gather_cols(pf_xq_, (size_t)XS * sizeof(XBlock), (size_t)(cols / 32) * sizeof(XBlock), T_cur_, s);
+  };
   for (int c0 = 0; c0 < n; c0 += pf_cap_) {
     const int T = std::min(pf_cap_, n - c0), p0 = pos + c0;
+    T_cur_ = T;
     const bool last_chunk = c0 + T == n;
     LLMI_HIP(hipMemcpyAsync(pf_tokens_, tokens + c0, (size_t)T * 4, hipMemcpyHostToDevice, s));
     PrefillNorm en;
@@ -818,12 +839,14 @@ void Session::prefill(const int32_t* tokens, int n, int pos) {
     en.xstride = XS;
     en.n = E;
     en.eps = hp_.eps;
+    en.x16 = f16 ? pf_x16_ : nullptr;
+    en.x16stride = X16;
     launch_prefill_norm(en, T, s);
     for (int l = 0; l < hp_.n_layer; l++) {
       const LayerDev& Ld = L_[l];
       const int hd = Ld.hd;
-      tap("pf_x_qkv", l, pf_xq_, (size_t)T * XS * sizeof(XBlock), s);
-      launch_prefill_gemm(Ld.qkv[0].w, pf_xq_, XS, T, pf_out_, Ld.qkv_rows, s);
+      xtap("pf_x_qkv", l);
+      gemm(Ld.qkv[0].w, pf_out_, Ld.qkv_rows);
       tap("pf_qkv", l, pf_out_, (size_t)T * Ld.qkv_rows * 4, s);
       PrefillQK qk;
       qk.qkv = pf_out_;
@@ -856,13 +879,15 @@ void Session::prefill(const int32_t* tokens, int n, int pos) {
       const int hb = nh_ * hd / 32;  // this rank's heads' Q8_0 blocks per token
       at.xq = pf_xq_ + (size_t)r * hb;
       at.xstride = XS;
+      at.x16 = f16 ? pf_x16_ + (size_t)r * nh_ * hd : nullptr;
+      at.x16stride = X16;
       launch_prefill_attn(at, T, s);
-      if (tp_) gather_cols(pf_xq_, (size_t)XS * sizeof(XBlock), (size_t)hb * sizeof(XBlock), T, s);
+      xgather(nh_ * hd);
       tap("pf_q", l, pf_q_, (size_t)T * nh_ * hd * 2, s);
       tap("kc", l, Ld.kc, (size_t)nkv_ * max_ctx_ * hd * 2, s);
       tap("vc", l, Ld.vc, (size_t)nkv_ * max_ctx_ * hd * 2, s);
-      tap("pf_x_o", l, pf_xq_, (size_t)T * XS * sizeof(XBlock), s);
-      launch_prefill_gemm(Ld.o.w, pf_xq_, XS, T, pf_out_ + (size_t)r * e_sh_, E, s);
+      xtap("pf_x_o", l);
+      gemm(Ld.o.w, pf_out_ + (size_t)r * e_sh_, E);
       if (tp_) gather_cols(pf_out_, (size_t)E * 4, (size_t)e_sh_ * 4, T, s);
       tap("pf_o", l, pf_out_, (size_t)T * E * 4, s);
       PrefillNorm rn;  // post-attention norm + residual, then ffn_norm
@@ -874,17 +899,19 @@ void Session::prefill(const int32_t* tokens, int n, int pos) {
       rn.xstride = XS;
       rn.n = E;
       rn.eps = hp_.eps;
+      rn.x16 = f16 ? pf_x16_ : nullptr;
+      rn.x16stride = X16;
       launch_prefill_norm(rn, T, s);
       tap("pf_resid_attn", l, pf_resid_, (size_t)T * E * 4, s);
-      tap("pf_x_gate_up", l, pf_xq_, (size_t)T * XS * sizeof(XBlock), s);
+      xtap("pf_x_gate_up", l);
       const int FL = tp_ ? f_sh_ : F;  // this rank's hidden units
-      launch_prefill_gemm(Ld.gate_up[0].w, pf_xq_, XS, T, pf_out_, 2 * FL, s);
+      gemm(Ld.gate_up[0].w, pf_out_, 2 * FL);
       tap("pf_gate_up", l, pf_out_, (size_t)T * 2 * F * 4, s);
       launch_prefill_gelu(pf_out_, FL, layer_gemv_gelu_group(Ld.gate_up[0].w.cols, Ld.gate_up[0].w.type),
-                          pf_xq_ + (size_t)r * (FL / 32), XS, T, s);
-      if (tp_) gather_cols(pf_xq_, (size_t)XS * sizeof(XBlock), (size_t)(FL / 32) * sizeof(XBlock), T, s);
-      tap("pf_x_down", l, pf_xq_, (size_t)T * XS * sizeof(XBlock), s);
-      launch_prefill_gemm(Ld.down.w, pf_xq_, XS, T, pf_out_ + (size_t)r * e_sh_, E, s);
+                          pf_xq_ + (size_t)r * (FL / 32), XS, T, s, f16 ? pf_x16_ + (size_t)r * FL : nullptr, X16);
+      xgather(FL);
+      xtap("pf_x_down", l);
+      gemm(Ld.down.w, pf_out_ + (size_t)r * e_sh_, E);
       if (tp_) gather_cols(pf_out_, (size_t)E * 4, (size_t)e_sh_ * 4, T, s);
       tap("pf_down", l, pf_out_, (size_t)T * E * 4, s);
       if (l + 1 < hp_.n_layer) {  // post-ffw norm + residual, then the next attn_norm

@@ -180,6 +180,8 @@ class Session {
   int32_t* pf_tokens_ = nullptr;
   float *pf_resid_ = nullptr, *pf_out_ = nullptr;
   XBlock* pf_xq_ = nullptr;
+  uint16_t* pf_x16_ = nullptr;  // f16 prefill activations [cap][pf_xs_ * 32] (GEMM v6)
+  int T_cur_ = 0;              // tokens of the prefill chunk being enqueued
   uint16_t* pf_q_ = nullptr;
   uint8_t* pf_gather_ = nullptr;  // tensor parallel: all-gather staging of the prefill slices
 };

@@ -90,12 +90,23 @@ struct PrefillNorm {  // per token: embedding (table != null) or residual + norm
   XBlock* xq = nullptr;           // [T][xstride] out
   int xstride = 0, n = 0;
   double eps = 0;
+  uint16_t* x16 = nullptr;        // non-null: x as f16 rows [T][x16stride] instead of Q8_0 blocks (GEMM v6)
+  int x16stride = 0;
 };
 struct PrefillGemm {
   const uint4* qs = nullptr;
   const uint16_t* wd = nullptr;
   int rows = 0, nb = 0, slab = 0;
   const XBlock* x = nullptr;
+  int xstride = 0, T = 0;
+  float* out = nullptr;
+  int ostride = 0;
+};
+struct PrefillGemm16 {  // f16 activations [T][xstride elements] (k_prefill.hip GEMM v6)
+  const uint4* qs = nullptr;
+  const uint16_t* wd = nullptr;
+  int rows = 0, nb = 0, slab = 0;
+  const uint16_t* x = nullptr;
   int xstride = 0, T = 0;
   float* out = nullptr;
   int ostride = 0;
@@ -116,14 +127,19 @@ struct PrefillAttn {
   int n_head = 0, n_head_kv = 0, head_dim = 0, max_ctx = 0, pos0 = 0;
   XBlock* xq = nullptr;  // [T][xstride]: the heads' outputs as Q8_0 blocks
   int xstride = 0;
+  uint16_t* x16 = nullptr;  // non-null: the heads' outputs as f16 rows [T][x16stride] (GEMM v6)
+  int x16stride = 0;
 };
 void launch_prefill_norm(const PrefillNorm& a, int T, hipStream_t s);
 bool prefill_gemm_supported(const DevWeight& w);
 void launch_prefill_gemm(const DevWeight& w, const XBlock* x, int xstride, int T, float* out, int ostride,
                          hipStream_t s);
+void launch_prefill_gemm16(const DevWeight& w, const uint16_t* x, int xstride, int T, float* out, int ostride,
+                           hipStream_t s);
 void launch_prefill_qk(const PrefillQK& a, int T, hipStream_t s);
 void launch_prefill_attn(const PrefillAttn& a, int T, hipStream_t s);
-void launch_prefill_gelu(const float* gu, int F, int H, XBlock* xq, int xstride, int T, hipStream_t s);
+void launch_prefill_gelu(const float* gu, int F, int H, XBlock* xq, int xstride, int T, hipStream_t s,
+                         uint16_t* x16 = nullptr, int x16stride = 0);
 
 // the weight layout the launch-table entry for (w's shape, role) reads
 int layer_gemv_slab(const DevWeight& w, int role);

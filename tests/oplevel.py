@@ -224,12 +224,20 @@ class OpChecker:
 
     def prefill(self, taps, T_tok):
         """Traced batched prefill: every projection GEMM, token by token, from
-        the device's own Q8_0 input blocks (prefill_gemm_kernel vs the
-        reference's per-token mat_vec_mul rows)."""
+        the device's own inputs -- Q8_0 blocks (int8 GEMM v5 vs the reference's
+        per-token mat_vec_mul rows, GEMV tolerance) or f16 rows (the default f16
+        GEMM v6 vs the exactly dequantized Q4_0 weights times those f16 values in
+        float64: the kernel's weights are f16(d (q - 8)), PREFILL16_RTOL)."""
         c = self.cfg
         E, F = c.n_embd, c.n_ff
         D = taps_by_layer(taps)
         H = GELU_H[E]
+        xs = max(E, F, c.n_head * c.head_dim) // 32  # activation blocks per token (session pf_xs_)
+        row_bytes = len(D[("pf_x_qkv", 0)][-1]) // T_tok
+        assert row_bytes in (48 * xs, 64 * xs), f"prefill activation row of {row_bytes} B"
+        f16_in = row_bytes == 64 * xs
+        if f16_in:
+            return self._prefill_f16(D, T_tok, H)
         for l in range(c.n_layer):
             for proj, w, ncols in (("qkv", self.w.qkv(l), E),
                                    ("o", self.w.raw(f"blk.{l}.attn_output.weight"), c.n_head * c.head_dim),
@@ -247,3 +255,39 @@ class OpChecker:
                     else:
                         ref = self.gemv_q8(w, xq)
                     self.note(f"prefill_gemm_{proj}", rel_err(out[t, : ref.size], ref), GEMV_RTOL)
+
+    def _prefill_f16(self, D, T_tok, H):
+        c = self.cfg
+        E, F = c.n_embd, c.n_ff
+        for l in range(c.n_layer):
+            for proj, names, ncols in (("qkv", [f"blk.{l}.attn_{p}.weight" for p in "qkv"], E),
+                                       ("o", [f"blk.{l}.attn_output.weight"], c.n_head * c.head_dim),
+                                       ("gate_up", None, E),
+                                       ("down", [f"blk.{l}.ffn_down.weight"], F)):
+                x = np.frombuffer(D[(f"pf_x_{proj}", l)][-1], np.float16).reshape(T_tok, -1)[:, :ncols].astype(np.float64)
+                out = f32(D[(f"pf_{proj}", l)][-1]).reshape(T_tok, -1)
+                if proj == "gate_up":
+                    g = dequant_q4_0(self.w.raw(f"blk.{l}.ffn_gate.weight"))
+                    u = dequant_q4_0(self.w.raw(f"blk.{l}.ffn_up.weight"))
+                    W = np.concatenate([np.concatenate([g[k * H:(k + 1) * H], u[k * H:(k + 1) * H]]) for k in range(F // H)])
+                else:
+                    W = np.concatenate([dequant_q4_0(self.w.raw(n)) for n in names])
+                ref = x @ W.T
+                for t in range(T_tok):
+                    self.note(f"prefill_gemm16_{proj}", rel_err(out[t, : ref.shape[1]], ref[t]), PREFILL16_RTOL)
+
+
+PREFILL16_RTOL = 2e-3
+
+
+def dequant_q4_0(w):
+    """Q4_0 rows -> float64 (d * (q - 8); ops.h block layout: f16 d, 16 bytes, element i = low nibble of byte
+    i, element i + 16 = high nibble)."""
+    data, tt, rows, cols = w
+    assert tt == TT.Q4_0, "f16 prefill GEMM check: Q4_0 weights only"
+    b = data.reshape(rows, cols // 32, 18)
+    d = b[:, :, :2].copy().view(np.float16).astype(np.float64)[:, :, 0]
+    qs = b[:, :, 2:]
+    q = np.concatenate([qs & 15, qs >> 4], axis=2).astype(np.float64) - 8.0
+    return (q * d[:, :, None]).reshape(rows, cols)
+

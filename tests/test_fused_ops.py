@@ -75,3 +75,12 @@ def test_ops_mini1b_long_context(oracle):
 def test_ops_mini27b_shapes(oracle):
     """Gemma-3 27B layer shapes (5376 / 21504 columns, 32 / 16 heads of 128)."""
     _run(oracle, "mini-27b", 26, 8, 2, 64, swa_pattern=[True, False])
+
+
+@pytest.mark.parametrize("cfg_name", ["mini-4b", "mini-27b"])
+def test_ops_prefill_f16_gemm(oracle, monkeypatch, cfg_name):
+    """The opt-in f16 prefill (LLMI_PREFILL_F16=1: f16 activations from the norm / attention / GELU producers,
+    GEMM v6 with Q4_0 weights dequantized to f16 on v_mfma_f32_32x32x16_f16): every GEMM output row against the
+    exactly dequantized weights times the device's own f16 inputs in float64 (tests/oplevel.py PREFILL16_RTOL)."""
+    chk = _run(oracle, cfg_name, 27, 40, 1, 64, monkeypatch, {"LLMI_PREFILL_F16": "1"})
+    assert "prefill_gemm16_gate_up" in chk.report and "prefill_gemm16_down" in chk.report
