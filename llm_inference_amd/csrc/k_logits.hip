@@ -153,7 +153,7 @@ __global__ __launch_bounds__(256) void screen_prep_kernel(const uint16_t* __rest
 // pairs with the next pair's loads in flight (as gemv_f16_rows_pipe).
 // CPL: 16-B chunks per lane, ceil(2 nb / 32) (5 for 2560 columns; chunks
 // past the row's 2 nb contribute nothing).
-template <int CPL>
+template <int CPL, int AHEAD>
 __global__ __launch_bounds__(256) void screen_gemv_kernel(const uint4* __restrict__ qs, const uint16_t* __restrict__ d,
                                                           int rows, int nb, const ScreenX* __restrict__ xs,
                                                           float* __restrict__ hi, unsigned* __restrict__ m_key) {
@@ -188,10 +188,14 @@ __global__ __launch_bounds__(256) void screen_gemv_kernel(const uint4* __restric
   uint4 cq[CPL];
   uint16_t cs[CPL];
   load(cq, cs, min(row, rows - 1));
+  // AHEAD = 2: a second row pair in flight (bytes in flight per CU: MI355X_MICROARCH HBM latency x rate)
+  uint4 mq[AHEAD > 1 ? CPL : 1];
+  uint16_t ms[AHEAD > 1 ? CPL : 1];
+  if constexpr (AHEAD > 1) load(mq, ms, min(row + 2 * npairs, rows - 1));
   for (; 2 * pair < rows; pair += npairs, row += 2 * npairs) {
     uint4 nq[CPL];
     uint16_t ns[CPL];
-    load(nq, ns, min(row + 2 * npairs, rows - 1));
+    load(nq, ns, min(row + 2 * AHEAD * npairs, rows - 1));
     float ap = 0.0f, bp = 0.0f;
 #pragma unroll
     for (int p = 0; p < CPL; p++) {
@@ -212,8 +216,15 @@ __global__ __launch_bounds__(256) void screen_gemv_kernel(const uint4* __restric
     }
 #pragma unroll
     for (int p = 0; p < CPL; p++) {
-      cq[p] = nq[p];
-      cs[p] = ns[p];
+      if constexpr (AHEAD > 1) {
+        cq[p] = mq[p];
+        cs[p] = ms[p];
+        mq[p] = nq[p];
+        ms[p] = ns[p];
+      } else {
+        cq[p] = nq[p];
+        cs[p] = ns[p];
+      }
     }
   }
   mloc = wave_max(mloc);
@@ -310,12 +321,18 @@ void launch_screen_argmax(const DevWeight& table, const ScreenTable& st, const u
   const int cpl = (2 * nb + 31) / 32;
   const int rows = table.rows;
   static const int wpc = getenv("LLMI_SCREEN_WPC") ? atoi(getenv("LLMI_SCREEN_WPC")) : 8;  // waves per CU (A/B)
+  // row pairs in flight per half-wave (A/B on the 4B bench: 1 -> 2 = 132.8 -> 127.7 us; 4 or 12 waves per CU slower)
+  static const int ahead = getenv("LLMI_SCREEN_AHEAD") ? atoi(getenv("LLMI_SCREEN_AHEAD")) : 2;
   const dim3 grid((std::min((rows + 1) / 2, 256 * wpc) + 3) / 4);
   switch (cpl) {
 #define LLMI_SCR(C)                                                                                               \
   case C:                                                                                                         \
-    hipLaunchKernelGGL(screen_gemv_kernel<C>, grid, dim3(256), 0, s, reinterpret_cast<const uint4*>(st.qs), st.d, \
-                       rows, nb, st.xs, st.hi, st.m_key);                                                         \
+    if (ahead > 1)                                                                                                \
+      hipLaunchKernelGGL((screen_gemv_kernel<C, 2>), grid, dim3(256), 0, s, reinterpret_cast<const uint4*>(st.qs), \
+                         st.d, rows, nb, st.xs, st.hi, st.m_key);                                                 \
+    else                                                                                                          \
+      hipLaunchKernelGGL((screen_gemv_kernel<C, 1>), grid, dim3(256), 0, s, reinterpret_cast<const uint4*>(st.qs), \
+                         st.d, rows, nb, st.xs, st.hi, st.m_key);                                                 \
     break;
     LLMI_SCR(1) LLMI_SCR(2) LLMI_SCR(3) LLMI_SCR(4) LLMI_SCR(5) LLMI_SCR(6) LLMI_SCR(7) LLMI_SCR(8) LLMI_SCR(9)
     LLMI_SCR(10) LLMI_SCR(11) LLMI_SCR(12)
