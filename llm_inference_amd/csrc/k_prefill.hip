@@ -960,32 +960,38 @@ __global__ __launch_bounds__(512, (WK == 1 || NT > 1) ? 2 : 4) void prefill_gemm
 // Deterministic and independent of the chunking; within the fast budget of
 // the Q8_0 path (an f16 product per weight instead of Q8_0 activations).
 // ---------------------------------------------------------------------------
-template <int WR, int WT, int WK, int NT, int KB, int NS>
+// Weight types (WQ): 0 Q4_0 (d_w per block), 1 Q4_K and 2 Q6_K in the kq layout (kernels.h: per 32-element
+// sub-block 16 B of nibbles in the Q4_0 order and a u16 scale word, per 256-element super-block a u32 of
+// d (| dmin), Q6_K also 8 B of high bits) -- w = f16(d sc q - dmin m) (Q4_K) or f16(d sc (q6 - 32)) (Q6_K),
+// the K-quant prefill (the reference runs it as a token loop of mat_vec_mul_q4_k / _q6_k, ops.cpp:614-785).
+template <int WR, int WT, int WK, int NT, int KB, int NS, int WQ>
 struct PG6 {
   static constexpr int NW = WR * WT * WK, MR = 32 * WR, TN = 32 * NT * WT;
   static constexpr int XU = KB * 4;  // 16-B activation units per token per stage
-  static constexpr int P_WQ = KB * MR / 64, P_WD = (KB / 2) * MR / 64, P_X = TN * XU / 64;
-  static constexpr int P = P_WQ + P_WD + P_X, PW = (P + NW - 1) / NW;
-  static constexpr int O_WD = KB * MR * 16, O_X = O_WD + (KB / 2) * MR * 4;
+  static constexpr int P_WQ = KB * MR / 64, P_WD = (KB / 2) * MR / 64, P_DD = WQ ? MR / 64 : 0,
+                       P_QH = WQ == 2 ? (KB / 2) * MR / 64 : 0, P_X = TN * XU / 64;
+  static constexpr int P = P_WQ + P_WD + P_DD + P_QH + P_X, PW = (P + NW - 1) / NW;
+  static constexpr int O_WD = KB * MR * 16, O_DD = O_WD + (KB / 2) * MR * 4, O_QH = O_DD + (WQ ? MR * 4 : 0),
+                       O_X = O_QH + (WQ == 2 ? MR * KB * 8 : 0);
   static constexpr int STAGE = O_X + TN * XU * 16;
   static constexpr int EPI = NW * 32 * 33 * 4;
   static constexpr int LDS = STAGE * NS > EPI ? STAGE * NS : EPI;
   static_assert(KB % WK == 0 && (KB == 2 || KB == 4), "KB");
-  static_assert(KB * MR % 64 == 0 && (KB / 2) * MR % 64 == 0 && TN * XU % 64 == 0, "pieces of 64 lanes");
+  static_assert(KB * MR % 64 == 0 && (KB / 2) * MR % 64 == 0 && TN * XU % 64 == 0 && MR % 64 == 0, "pieces of 64 lanes");
   static_assert(PW * (NS - 2) <= 63, "vmcnt range");
 };
 
 template <int KB>
 __device__ __forceinline__ int pg6_wsw(int row) { return KB == 4 ? (row >> 2) & 3 : (row >> 3) & 1; }
 
-template <int WR, int WT, int WK, int NT, int KB, int NS>
+template <int WR, int WT, int WK, int NT, int KB, int NS, int WQ>
 __global__ __launch_bounds__(512, 2) void prefill_gemm6_kernel(PrefillGemm16 a) {
-  using C = PG6<WR, WT, WK, NT, KB, NS>;
+  using C = PG6<WR, WT, WK, NT, KB, NS, WQ>;
   typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
   __shared__ __attribute__((aligned(16))) unsigned char s_ring[C::LDS];
   const int t = threadIdx.x, lane = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6), r = lane & 31, h = lane >> 5;
   const int wr = w % WR, wt = (w / WR) % WT, kg = w / (WR * WT);
-  const int nb = a.nb, nst = nb / KB;
+  const int nb = a.nb, nst = nb / KB, nsb = nb / 8;
   const int n_rt = a.rows / C::MR, n_tt = (a.T + C::TN - 1) / C::TN;
   const int bid = blockIdx.x;
   int rt, tt;
@@ -1002,23 +1008,45 @@ __global__ __launch_bounds__(512, 2) void prefill_gemm6_kernel(PrefillGemm16 a) 
   int pk[C::PW], po[C::PW];
 #pragma unroll
   for (int i = 0; i < C::PW; i++) {
-    const int p = (w + i * C::NW) % C::P;
+    int p = (w + i * C::NW) % C::P;
     if (p < C::P_WQ) {  // unit u: row u / KB, block slot u % KB
       const int u = p * 64 + lane, row = u / KB, b = (u % KB) ^ pg6_wsw<KB>(row);
       pk[i] = 0;
       pb[i] = reinterpret_cast<const unsigned char*>(a.qs + q4_block_index(a.slab, a.rows, nb, n0 + row, b));
       po[i] = p * 1024;
-    } else if (p < C::P_WQ + C::P_WD) {  // unit u: block pair u / MR, row u % MR
-      const int q = p - C::P_WQ, u = q * 64 + lane;
+      continue;
+    }
+    p -= C::P_WQ;
+    if (p < C::P_WD) {  // unit u: block pair u / MR, row u % MR (f16 scales / kq scale words)
+      const int u = p * 64 + lane;
       pk[i] = 1;
       pb[i] = reinterpret_cast<const unsigned char*>(a.wd + q4_block_index(a.slab, a.rows, nb, n0 + u % C::MR, 2 * (u / C::MR)));
-      po[i] = C::O_WD + q * 256;
-    } else {  // unit u: (token, slot), the token's row of KB x 32 f16 as XU units, slot = unit ^ (tok & (XU - 1))
-      const int q = p - C::P_WQ - C::P_WD, u = q * 64 + lane;
+      po[i] = C::O_WD + p * 256;
+      continue;
+    }
+    p -= C::P_WD;
+    if (p < C::P_DD) {  // unit u: row u, the super-block word of the stage
+      const int u = p * 64 + lane;
+      pk[i] = 3;
+      pb[i] = reinterpret_cast<const unsigned char*>(a.kdd + (size_t)(n0 + u) * nsb);
+      po[i] = C::O_DD + p * 256;
+      continue;
+    }
+    p -= C::P_DD;
+    if (p < C::P_QH) {  // unit u: row u / (KB / 2), sub-block pair u % (KB / 2): 16 B of high bits
+      const int u = p * 64 + lane, row = u / (KB / 2), pr = u % (KB / 2);
+      pk[i] = 4;
+      pb[i] = reinterpret_cast<const unsigned char*>(a.kqh + (size_t)(n0 + row) * nb + 2 * pr);
+      po[i] = C::O_QH + p * 1024;
+      continue;
+    }
+    p -= C::P_QH;
+    {  // unit u: (token, slot), the token's row of KB x 32 f16 as XU units, slot = unit ^ (tok & (XU - 1))
+      const int u = p * 64 + lane;
       const int tok = u / C::XU, un = (u % C::XU) ^ (tok & (C::XU - 1));
       pk[i] = 2;
       pb[i] = reinterpret_cast<const unsigned char*>(a.x + (size_t)min(tk0 + tok, a.T - 1) * a.xstride + un * 8);
-      po[i] = C::O_X + q * 1024;
+      po[i] = C::O_X + p * 1024;
     }
   }
   auto issue = [&](int c) {
@@ -1028,8 +1056,9 @@ __global__ __launch_bounds__(512, 2) void prefill_gemm6_kernel(PrefillGemm16 a) 
 #pragma unroll
     for (int i = 0; i < C::PW; i++) {
       const int k = pk[i];
-      const long off = k == 0 ? wofs * 16 : k == 1 ? wofs * 2 : (long)kb * 64;
-      if (k == 1) glds4(pb[i] + off, st + po[i]);
+      const long off = k == 0 ? wofs * 16 : k == 1 ? wofs * 2 : k == 2 ? (long)kb * 64 : k == 3 ? (long)(kb >> 3) * 4
+                                                                                                 : (long)kb * 8;
+      if (k == 1 || k == 3) glds4(pb[i] + off, st + po[i]);
       else glds16(pb[i] + off, st + po[i]);
     }
   };
@@ -1051,7 +1080,9 @@ __global__ __launch_bounds__(512, 2) void prefill_gemm6_kernel(PrefillGemm16 a) 
     b_base[j] = C::O_X + tok * C::XU * 16;
     b_sw[j] = tok & (C::XU - 1);
   }
+  const f16x2v m1024 = {(_Float16)-1024.0f, (_Float16)-1024.0f};
   const f16x2v m1032 = {(_Float16)-1032.0f, (_Float16)-1032.0f};
+  const f16x2v m1056 = {(_Float16)-1056.0f, (_Float16)-1056.0f};
   for (int c = 0; c < nst; c++) {
     wait_ahead(min(NS - 2, nst - 1 - c));
     __builtin_amdgcn_s_barrier();
@@ -1064,20 +1095,57 @@ __global__ __launch_bounds__(512, 2) void prefill_gemm6_kernel(PrefillGemm16 a) 
       // A: bytes 8h .. 8h + 7 of the row's block: low nibbles = k 8h.. (MFMA 0), high = k 16 + 8h.. (MFMA 1)
       const uint2 qb = *reinterpret_cast<const uint2*>(st + (arow * KB + (b ^ a_sw)) * 16 + 8 * h);
       const uint32_t wp = wd[(b >> 1) * C::MR + arow];
-      const uint32_t dsel = (WK == 1 ? (bb & 1) : (kg & 1)) ? (wp >> 16) : (wp & 0xFFFFu);
-      const f16x2v d2 = __builtin_bit_cast(f16x2v, dsel | (dsel << 16));
+      const uint32_t sw16 = (WK == 1 ? (bb & 1) : (kg & 1)) ? (wp >> 16) : (wp & 0xFFFFu);
+      f16x2v s0, s1, o0 = {}, o1 = {};  // MFMA 0 / 1: w = q * s + o, q the stored integer
+      if constexpr (WQ == 0) {
+        s0 = s1 = __builtin_bit_cast(f16x2v, sw16 | (sw16 << 16));
+      } else {
+        const uint32_t ddw = reinterpret_cast<const uint32_t*>(st + C::O_DD)[arow];
+        const float d = h2f((uint16_t)(ddw & 0xFFFF));
+        if constexpr (WQ == 1) {  // d sc q - dmin m
+          const float sc = d * (float)(sw16 & 0xFF), mn = h2f((uint16_t)(ddw >> 16)) * (float)(sw16 >> 8);
+          const _Float16 sh = (_Float16)sc, mh = (_Float16)(-mn);
+          s0 = s1 = f16x2v{sh, sh};
+          o0 = o1 = f16x2v{mh, mh};
+        } else {  // d sc_g (q6 - 32), sc_g: int8 per 16 elements
+          const _Float16 a0 = (_Float16)(d * (float)(int)(int8_t)(sw16 & 0xFF));
+          const _Float16 a1 = (_Float16)(d * (float)(int)(int8_t)(sw16 >> 8));
+          s0 = f16x2v{a0, a0};
+          s1 = f16x2v{a1, a1};
+        }
+      }
+      uint2 qh2 = {};
+      if constexpr (WQ == 2) qh2 = *reinterpret_cast<const uint2*>(st + C::O_QH + (arow * KB + b) * 8);
       f16x8 A0, A1;
       const uint32_t dw[2] = {qb.x, qb.y};
 #pragma unroll
       for (int e = 0; e < 2; e++) {
         const uint32_t v = dw[e], vh = v >> 4;
 #pragma unroll
-        for (int pr = 0; pr < 2; pr++) {  // bytes 2 pr, 2 pr + 1 of the dword
+        for (int pr = 0; pr < 2; pr++) {  // bytes 2 pr, 2 pr + 1 of the dword = elements 8h + 4e + 2pr, +1
           const uint32_t sel = pr ? 0x0C030C02u : 0x0C010C00u;
-          const uint32_t lo = (__builtin_amdgcn_perm(0u, v, sel) & 0x000F000Fu) | 0x64006400u;
-          const uint32_t hi = (__builtin_amdgcn_perm(0u, vh, sel) & 0x000F000Fu) | 0x64006400u;
-          const f16x2v fl = (__builtin_bit_cast(f16x2v, lo) + m1032) * d2;
-          const f16x2v fh = (__builtin_bit_cast(f16x2v, hi) + m1032) * d2;
+          uint32_t lo = __builtin_amdgcn_perm(0u, v, sel) & 0x000F000Fu;
+          uint32_t hi = __builtin_amdgcn_perm(0u, vh, sel) & 0x000F000Fu;
+          if constexpr (WQ == 2) {  // high bits: element 4k + i at bits 2k.. of byte i (k = 2h + e, i = 2pr, 2pr + 1)
+            const int k = 2 * h + e;
+            const uint32_t hl = __builtin_amdgcn_perm(0u, (qh2.x >> (2 * k)) & 0x03030303u, sel);
+            const uint32_t hh = __builtin_amdgcn_perm(0u, (qh2.y >> (2 * k)) & 0x03030303u, sel);
+            lo |= hl << 4;
+            hi |= hh << 4;
+          }
+          const f16x2v bl = __builtin_bit_cast(f16x2v, lo | 0x64006400u);  // 1024 + q
+          const f16x2v bh = __builtin_bit_cast(f16x2v, hi | 0x64006400u);
+          f16x2v fl, fh;
+          if constexpr (WQ == 0) {
+            fl = (bl + m1032) * s0;
+            fh = (bh + m1032) * s1;
+          } else if constexpr (WQ == 1) {
+            fl = __builtin_elementwise_fma(bl + m1024, s0, o0);
+            fh = __builtin_elementwise_fma(bh + m1024, s1, o1);
+          } else {
+            fl = (bl + m1056) * s0;
+            fh = (bh + m1056) * s1;
+          }
           A0[4 * e + 2 * pr] = fl[0];
           A0[4 * e + 2 * pr + 1] = fl[1];
           A1[4 * e + 2 * pr] = fh[0];
@@ -1609,23 +1677,39 @@ static bool launch_gemm5(const PrefillGemm& a, hipStream_t s) {
   return try_gemm5<2, 2, 2, 1, 4>(a, s) || try_gemm5<1, 4, 2, 1, 4>(a, s);  // K split 2, 64 or 32 rows
 }
 
-template <int WR, int WT, int WK, int NT, int KB, int NS>
+template <int WR, int WT, int WK, int NT, int KB, int NS, int WQ>
 static bool try_gemm6(const PrefillGemm16& a, hipStream_t s) {
-  using C = PG6<WR, WT, WK, NT, KB, NS>;
+  using C = PG6<WR, WT, WK, NT, KB, NS, WQ>;
   if (a.rows % C::MR || a.nb % KB) return false;
   const int n = (a.rows / C::MR) * ((a.T + C::TN - 1) / C::TN);
-  hipLaunchKernelGGL((prefill_gemm6_kernel<WR, WT, WK, NT, KB, NS>), dim3(n), dim3(64 * C::NW), 0, s, a);
+  hipLaunchKernelGGL((prefill_gemm6_kernel<WR, WT, WK, NT, KB, NS, WQ>), dim3(n), dim3(64 * C::NW), 0, s, a);
   return true;
+}
+
+template <int WQ>
+static bool gemm6_geometry(const PrefillGemm16& a, hipStream_t s) {
+  const char* f = getenv("LLMI_PG6");
+  const std::string c = f ? f : a.nb >= 160 ? "k4" : "k2";
+  if (c == "big" && try_gemm6<4, 2, 1, 2, 2, 3, WQ>(a, s)) return true;
+  if (c == "k4" && try_gemm6<2, 1, 4, 2, 4, 3, WQ>(a, s)) return true;
+  return try_gemm6<2, 2, 2, 2, 2, 3, WQ>(a, s);
+}
+
+bool prefill_gemm16_supported(const DevWeight& w) {
+  if (w.type == T_Q4_0) return prefill_gemm_supported(w) && w.rows % 64 == 0 && (w.cols / 32) % 4 == 0;
+  return (w.type == T_Q4_K || w.type == T_Q6_K) && w.kq && w.rows % 64 == 0 && w.cols % 256 == 0;
 }
 
 // v6 geometry (LLMI_PG6=<name> forces one for A/B); the K split depends on K alone (tensor-parallel shards
 // sum in the same order as the whole weight)
 void launch_prefill_gemm16(const DevWeight& w, const uint16_t* x, int xstride, int T, float* out, int ostride,
                            hipStream_t s) {
-  if (!prefill_gemm_supported(w)) throw std::runtime_error("prefill_gemm16: unsupported weight");
+  if (!prefill_gemm16_supported(w)) throw std::runtime_error("prefill_gemm16: unsupported weight");
   PrefillGemm16 a;
   a.qs = reinterpret_cast<const uint4*>(w.qs);
   a.wd = w.d;
+  a.kdd = w.kdd;
+  a.kqh = w.kqh;
   a.rows = w.rows;
   a.nb = w.cols / 32;
   a.slab = w.slab;
@@ -1634,12 +1718,8 @@ void launch_prefill_gemm16(const DevWeight& w, const uint16_t* x, int xstride, i
   a.T = T;
   a.out = out;
   a.ostride = ostride;
-  const char* f = getenv("LLMI_PG6");
-  const std::string c = f ? f : a.nb >= 160 ? "k4" : "k2";
-  bool ok = false;
-  if (c == "big") ok = try_gemm6<4, 2, 1, 2, 2, 3>(a, s);
-  else if (c == "k4") ok = try_gemm6<1, 2, 4, 2, 4, 3>(a, s) || try_gemm6<1, 2, 4, 1, 4, 3>(a, s);
-  if (!ok) ok = try_gemm6<2, 2, 2, 2, 2, 3>(a, s) || try_gemm6<1, 4, 2, 1, 4, 3>(a, s);
+  const bool ok = w.type == T_Q4_0 ? gemm6_geometry<0>(a, s) : w.type == T_Q4_K ? gemm6_geometry<1>(a, s)
+                                                                                : gemm6_geometry<2>(a, s);
   if (!ok) throw std::runtime_error("prefill_gemm16: shape");
   LLMI_HIP(hipGetLastError());
 }

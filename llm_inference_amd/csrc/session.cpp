@@ -540,10 +540,25 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
     // projection; Q8_0 block slices need 32-aligned head and hidden shards)
     bool pf = fuse_layers_ && (embd_.type == T_F16 || embd_.type == T_Q8_0) && hp_.n_embd <= 8192 &&
               hp_.n_embd % 32 == 0 && hp_.n_ff % 32 == 0 && (!tp_ || (f_sh_ % 32 == 0 && coll_));
-    for (const auto& l : L_)
-      pf = pf && l.fused && (l.hd == 64 || l.hd == 128 || l.hd == 256) && prefill_gemm_supported(l.qkv[0].w) &&
-           prefill_gemm_supported(l.o.w) && prefill_gemm_supported(l.gate_up[0].w) &&
-           prefill_gemm_supported(l.down.w);
+    // Q4_0 layers: the int8 GEMM (v5) or the f16 one (v6, LLMI_PREFILL_F16); K-quant (kq) layers: the f16 GEMM
+    auto gemm_ok = [&](const DevWeight& w) {
+      return w.type == T_Q4_0 ? prefill_gemm_supported(w) : prefill_gemm16_supported(w);
+    };
+    for (const auto& l : L_) {
+      bool ok = l.fused && (l.hd == 64 || l.hd == 128 || l.hd == 256) && gemm_ok(l.o.w) && gemm_ok(l.gate_up[0].w) &&
+                gemm_ok(l.down.w) && !l.qkv.empty();
+      for (const auto& part : l.qkv) ok = ok && gemm_ok(part.w);
+      bool kq = l.o.w.type != T_Q4_0 || l.gate_up[0].w.type != T_Q4_0 || l.down.w.type != T_Q4_0;
+      for (const auto& part : l.qkv) kq = kq || part.w.type != T_Q4_0;
+      if (ok && kq)  // f16 path: GELU group must allow the 8-unit f16 writes
+        ok = layer_gemv_gelu_group(l.gate_up[0].w.cols, l.gate_up[0].w.type) % 8 == 0;
+      pf = pf && ok;
+      pf_kq_ = pf_kq_ || kq;
+    }
+    // K-quant layers: the batched prefill (f16 path) is opt-in (LLMI_PREFILL_KQ=1) -- its f16 activations
+    // are further from the reference's Q8_K arithmetic than the fast-mode budget;
+    // the default is the decode token loop
+    if (pf_kq_ && !getenv("LLMI_PREFILL_KQ")) pf = false;
     const int grp = nkv_ > 0 ? nh_ / nkv_ : 0;
     prefill_ok_ = pf && (grp == 1 || grp == 2 || grp == 4);
     // attention block (qkv + attention + o in one launch): the fused fast
@@ -807,8 +822,9 @@ void Session::prefill(const int32_t* tokens, int n, int pos) {
   // f16 MFMA GEMM (v6, LLMI_PREFILL_F16=1: not faster yet -- activation tile re-reads bound it -- and further from
   // the reference's Q8_0 arithmetic)
   const int G = nh_ / std::max(nkv_, 1);
-  const bool f16 = getenv("LLMI_PREFILL_F16") && !getenv("LLMI_PREFILL_ATTN_V1") && (G == 1 || G == 2 || G == 4) &&
+  const bool f16 = (pf_kq_ || getenv("LLMI_PREFILL_F16")) && !getenv("LLMI_PREFILL_ATTN_V1") && (G == 1 || G == 2 || G == 4) &&
                    layer_gemv_gelu_group(L_[0].gate_up[0].w.cols, L_[0].gate_up[0].w.type) % 8 == 0;
+  if (pf_kq_ && !f16) throw status_error(LLMI_E_ARG, "prefill: K-quant layers need the f16 prefill path");
   auto gemm = [&](const DevWeight& w, float* out, int ostride) {
     if (f16) launch_prefill_gemm16(w, pf_x16_, X16, T_cur_, out, ostride, s);
     else launch_prefill_gemm(w, pf_xq_, XS, T_cur_, out, ostride, s);
@@ -846,7 +862,8 @@ void Session::prefill(const int32_t* tokens, int n, int pos) {
       const LayerDev& Ld = L_[l];
       const int hd = Ld.hd;
       xtap("pf_x_qkv", l);
-      gemm(Ld.qkv[0].w, pf_out_, Ld.qkv_rows);
+      for (size_t pi = 0, r0 = 0; pi < Ld.qkv.size(); r0 += Ld.qkv[pi].w.rows, pi++)  // q|k|v, or q|k and v (kq)
+        gemm(Ld.qkv[pi].w, pf_out_ + r0, Ld.qkv_rows);
       tap("pf_qkv", l, pf_out_, (size_t)T * Ld.qkv_rows * 4, s);
       PrefillQK qk;
       qk.qkv = pf_out_;

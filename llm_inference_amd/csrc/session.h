@@ -182,6 +182,7 @@ class Session {
   XBlock* pf_xq_ = nullptr;
   uint16_t* pf_x16_ = nullptr;  // f16 prefill activations [cap][pf_xs_ * 32] (GEMM v6)
   int T_cur_ = 0;              // tokens of the prefill chunk being enqueued
+  bool pf_kq_ = false;         // K-quant layers: the batched prefill runs the f16 path
   uint16_t* pf_q_ = nullptr;
   uint8_t* pf_gather_ = nullptr;  // tensor parallel: all-gather staging of the prefill slices
 };

@@ -104,7 +104,9 @@ struct PrefillGemm {
 };
 struct PrefillGemm16 {  // f16 activations [T][xstride elements] (k_prefill.hip GEMM v6)
   const uint4* qs = nullptr;
-  const uint16_t* wd = nullptr;
+  const uint16_t* wd = nullptr;   // Q4_0: f16 d per block; kq: the u16 scale word per sub-block
+  const uint32_t* kdd = nullptr;  // kq: per super-block d (| dmin)
+  const uint2* kqh = nullptr;     // Q6_K kq: high bits per sub-block
   int rows = 0, nb = 0, slab = 0;
   const uint16_t* x = nullptr;
   int xstride = 0, T = 0;
@@ -134,6 +136,7 @@ void launch_prefill_norm(const PrefillNorm& a, int T, hipStream_t s);
 bool prefill_gemm_supported(const DevWeight& w);
 void launch_prefill_gemm(const DevWeight& w, const XBlock* x, int xstride, int T, float* out, int ostride,
                          hipStream_t s);
+bool prefill_gemm16_supported(const DevWeight& w);
 void launch_prefill_gemm16(const DevWeight& w, const uint16_t* x, int xstride, int T, float* out, int ostride,
                            hipStream_t s);
 void launch_prefill_qk(const PrefillQK& a, int T, hipStream_t s);

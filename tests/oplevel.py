@@ -267,14 +267,24 @@ class OpChecker:
                 x = np.frombuffer(D[(f"pf_x_{proj}", l)][-1], np.float16).reshape(T_tok, -1)[:, :ncols].astype(np.float64)
                 out = f32(D[(f"pf_{proj}", l)][-1]).reshape(T_tok, -1)
                 if proj == "gate_up":
-                    g = dequant_q4_0(self.w.raw(f"blk.{l}.ffn_gate.weight"))
-                    u = dequant_q4_0(self.w.raw(f"blk.{l}.ffn_up.weight"))
+                    g = self.dequant(self.w.raw(f"blk.{l}.ffn_gate.weight"))
+                    u = self.dequant(self.w.raw(f"blk.{l}.ffn_up.weight"))
                     W = np.concatenate([np.concatenate([g[k * H:(k + 1) * H], u[k * H:(k + 1) * H]]) for k in range(F // H)])
                 else:
-                    W = np.concatenate([dequant_q4_0(self.w.raw(n)) for n in names])
+                    W = np.concatenate([self.dequant(self.w.raw(n)) for n in names])
                 ref = x @ W.T
                 for t in range(T_tok):
                     self.note(f"prefill_gemm16_{proj}", rel_err(out[t, : ref.shape[1]], ref[t]), PREFILL16_RTOL)
+
+
+    def dequant(self, w):
+        """Weight rows -> float64: Q4_0 in numpy, other types through the oracle's dequantize_row."""
+        data, tt, rows, cols = w
+        if tt == TT.Q4_0:
+            return dequant_q4_0(w)
+        rb = data.size // rows
+        return np.stack([np.asarray(self.orc.dequantize_row(tt, data[i * rb:(i + 1) * rb], cols), np.float64)
+                         for i in range(rows)])
 
 
 PREFILL16_RTOL = 2e-3

@@ -30,6 +30,10 @@ def _run(oracle, cfg_name, seed, n_prompt, n_decode, max_ctx, monkeypatch=None, 
     taps = m.trace(prompt, 0)
     if check_prefill and m.info.batched_prefill:
         chk.prefill(taps, n_prompt)
+    if n_decode < 0:  # prefill GEMMs only (the decode op checks assume Q8_0 activations)
+        print(cfg_name, env or "", {k: f"{v:.2e}" for k, v in sorted(chk.report.items())})
+        m.close()
+        return chk
     tok = int(np.frombuffer([b for n, l, b in taps if n == "token"][-1], np.int32)[0])
     pos = n_prompt
     for _ in range(n_decode):
@@ -84,3 +88,13 @@ def test_ops_prefill_f16_gemm(oracle, monkeypatch, cfg_name):
     exactly dequantized weights times the device's own f16 inputs in float64 (tests/oplevel.py PREFILL16_RTOL)."""
     chk = _run(oracle, cfg_name, 27, 40, 1, 64, monkeypatch, {"LLMI_PREFILL_F16": "1"})
     assert "prefill_gemm16_gate_up" in chk.report and "prefill_gemm16_down" in chk.report
+
+
+def test_ops_prefill_kquant_gemm(oracle, monkeypatch):
+    """Gemma-3 4B Q4_K_M layer shapes (q, k, o, gate, up Q4_K; v, down Q6_K in the kq layout): the opt-in
+    batched prefill (LLMI_PREFILL_KQ=1) runs the f16 path, GEMM v6 dequantizing the K-quant sub-blocks to f16 -- every output row against
+    the reference's dequantize_row weights times the device's own f16 inputs in float64."""
+    from llm_inference_amd.gguf import TensorType as TT
+    chk = _run(oracle, "mini-4b", 29, 24, -1, 64, monkeypatch, {"LLMI_PREFILL_KQ": "1"}, wtype=TT.Q4_K,
+               wtypes={"v": TT.Q6_K, "down": TT.Q6_K})
+    assert "prefill_gemm16_qkv" in chk.report and "prefill_gemm16_down" in chk.report

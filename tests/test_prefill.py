@@ -120,3 +120,28 @@ def test_prefill_attention_mfma_vs_vector(cfg_name, n_prompt, monkeypatch):
     print(f"{cfg_name} n={n_prompt}: max|mfma - vector attention| = {d:.3g}")
     assert d <= FAST_VS_REF
     assert int(np.argmax(new)) == int(np.argmax(old))
+
+
+def test_kquant_batched_prefill(monkeypatch):
+    """Q4_K_M layer shapes (BASELINE configs[3]) through the opt-in batched prefill (LLMI_PREFILL_KQ=1: f16
+    activations, GEMM v6 on the kq weights) instead of the token loop: the same greedy continuation and exact
+    under re-chunking; the logit gap to the token loop (f16 activations there, Q8_K blocks in the loop) is
+    reported, not bounded by the Q8 fast budget."""
+    monkeypatch.setenv("LLMI_PREFILL_KQ", "1")
+    from llm_inference_amd.gguf import TensorType as TT
+    from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
+    cfg = CONFIGS["mini-4b"]
+    g = build_gemma3_gguf(cfg, seed=33, wtype=TT.Q4_K, wtypes={"v": TT.Q6_K, "down": TT.Q6_K})
+    prompt = np.random.default_rng(6).integers(4, cfg.vocab, 150).astype(np.int32)
+    mp = _model(g, monkeypatch)
+    assert mp.get_info().batched_prefill == 1
+    lp = mp.forward(prompt, 0)
+    ids_p = mp.generate(int(np.argmax(lp)), len(prompt), 8)
+    ml = _model(g, monkeypatch, no_prefill=True)
+    ll = ml.forward(prompt, 0)
+    ids_l = ml.generate(int(np.argmax(ll)), len(prompt), 8)
+    d = float(np.abs(lp - ll).max())
+    print(f"mini-4b Q4_K_M n={len(prompt)}: max|f16 batched prefill - token loop| = {d:.3g}")
+    assert int(np.argmax(lp)) == int(np.argmax(ll))
+    assert ids_p.tolist() == ids_l.tolist()
+    np.testing.assert_array_equal(_model(g, monkeypatch, chunk=41).forward(prompt, 0), lp)
