@@ -136,6 +136,21 @@ static std::vector<GemvPart> make_parts(const GGUFView& g, const std::vector<Row
 // mapping head / (n_head / n_head_kv), model.cpp:478-550, requires).
 void Session::setup_tp() {
   const int G = tp_size_, r = tp_rank_;
+  if (hp_.n_embd % G || hp_.n_ff % G)
+    throw status_error(LLMI_E_ARG, "tensor parallel: embedding_length / feed_forward_length % tp_size != 0");
+  e_sh_ = hp_.n_embd / G;
+  f_sh_ = hp_.n_ff / G;
+  // default: the q|k|v projection and the attention replicated on every rank (all heads, the whole KV
+  // cache), o / gate_up / down row-sharded -- three all-gathers per layer instead of four, and the
+  // attention block (qkv + attention + the rank's o rows in one launch) on the ranks; LLMI_TP_HEAD_SHARD=1
+  // shards the heads as well (an all-gather of the heads' outputs before o)
+  tp_rep_attn_ = getenv("LLMI_TP_HEAD_SHARD") == nullptr;
+  if (tp_rep_attn_) {
+    nh_ = hp_.n_head;
+    nkv_ = hp_.n_head_kv;
+    kv0_ = 0;
+    return;
+  }
   if (hp_.n_head % G) throw status_error(LLMI_E_ARG, "tensor parallel: head_count % tp_size != 0");
   nh_ = hp_.n_head / G;
   const int grp = hp_.n_head / hp_.n_head_kv;
@@ -148,10 +163,6 @@ void Session::setup_tp() {
   } else {
     throw status_error(LLMI_E_ARG, "tensor parallel: q heads of a rank span several kv heads");
   }
-  if (hp_.n_embd % G || hp_.n_ff % G)
-    throw status_error(LLMI_E_ARG, "tensor parallel: embedding_length / feed_forward_length % tp_size != 0");
-  e_sh_ = hp_.n_embd / G;
-  f_sh_ = hp_.n_ff / G;
 }
 
 void Session::upload(const GGUFView& g) {  // model.cpp:169-238 tensor map
@@ -246,7 +257,7 @@ void Session::upload(const GGUFView& g) {  // model.cpp:169-238 tensor map
     const int hd = Ld.hd, r = tp_rank_;
     const std::vector<RowSlice> qkv_rows =
         !Ld.has_kv ? std::vector<RowSlice>{all_rows(q)}
-        : tp_ ? std::vector<RowSlice>{{q, r * nh_ * hd, nh_ * hd}, {k, kv0_ * hd, nkv_ * hd}, {v, kv0_ * hd, nkv_ * hd}}
+        : tp_ && !tp_rep_attn_ ? std::vector<RowSlice>{{q, r * nh_ * hd, nh_ * hd}, {k, kv0_ * hd, nkv_ * hd}, {v, kv0_ * hd, nkv_ * hd}}
               : std::vector<RowSlice>{all_rows(q), all_rows(k), all_rows(v)};
     Ld.qkv = make_parts(g, qkv_rows, stream_, weight_bytes_);
     Ld.k_off = qkv_rows[0].n;
@@ -564,7 +575,7 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
     // attention block (qkv + attention + o in one launch): the fused fast
     // path on one device, shapes in k_attn.hip's table; LLMI_NO_BLOCK=1 keeps
     // the three launches (A/B)
-    bool blk = fuse_layers_ && !tp_ && dup_.empty() && getenv("LLMI_NO_BLOCK") == nullptr &&
+    bool blk = fuse_layers_ && (!tp_ || tp_rep_attn_) && dup_.empty() && getenv("LLMI_NO_BLOCK") == nullptr &&
                (grp == 1 || grp == 2 || grp == 4);
     for (const auto& l : L_)
       blk = blk && l.fused && l.hd % 32 == 0 &&
@@ -894,12 +905,13 @@ void Session::prefill(const int32_t* tokens, int n, int pos) {
       at.max_ctx = max_ctx_;
       at.pos0 = p0;
       const int hb = nh_ * hd / 32;  // this rank's heads' Q8_0 blocks per token
-      at.xq = pf_xq_ + (size_t)r * hb;
+      const int hr = tp_rep_attn_ ? 0 : r;  // replicated attention: every rank has all heads
+      at.xq = pf_xq_ + (size_t)hr * hb;
       at.xstride = XS;
-      at.x16 = f16 ? pf_x16_ + (size_t)r * nh_ * hd : nullptr;
+      at.x16 = f16 ? pf_x16_ + (size_t)hr * nh_ * hd : nullptr;
       at.x16stride = X16;
       launch_prefill_attn(at, T, s);
-      xgather(nh_ * hd);
+      if (!tp_rep_attn_) xgather(nh_ * hd);
       tap("pf_q", l, pf_q_, (size_t)T * nh_ * hd * 2, s);
       tap("kc", l, Ld.kc, (size_t)nkv_ * max_ctx_ * hd * 2, s);
       tap("vc", l, Ld.vc, (size_t)nkv_ * max_ctx_ * hd * 2, s);
@@ -992,7 +1004,7 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
       AttnArgs aa{q_, Ld.kc, Ld.vc, nh_, nkv_, hd, max_ctx_, d_pos_, part_, attn_, ticket_, blk_xo_};
       LayerGemv go;
       go.xg = blk_xo_;
-      go.out = o_out_;
+      go.out = o_out_ + (size_t)tp_rank_ * e_sh_;  // this rank's o rows (all of them on one device)
       BlockSync bs;
       bs.epoch = epoch;
       bs.g_qkv = blk_gqkv_ + (size_t)l * blk_gqkv_stride_;
@@ -1060,8 +1072,9 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
       const bool q8_in_combine = hd % 32 == 0;
       if (tp_ && !q8_in_combine) throw status_error(LLMI_E_ARG, "tensor parallel: head_dim % 32 != 0");
       const int hb = nh_ * hd / 32;  // Q8_0 blocks of this rank's heads
+      const int hr = tp_rep_attn_ ? 0 : tp_rank_;  // the heads' place in the all-heads vector
       AttnArgs aa{q_, Ld.kc, Ld.vc, nh_, nkv_, hd, max_ctx_, d_pos_, part_, attn_,
-                  ticket_, q8_in_combine ? act_.q8.xb + (size_t)tp_rank_ * hb : nullptr};
+                  ticket_, q8_in_combine ? act_.q8.xb + (size_t)hr * hb : nullptr};
       aa.q8k = Ld.o.w.kq ? 1 : 0;  // the kq o projection reads Q8_K quants
       for (int r = 0; r < dup("attn"); r++) launch_attention(aa, false, s, &qa);
       kernels_per_token_++;
@@ -1073,7 +1086,7 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
         launch_quantize_q8_0(attn_, hp_.n_head * hd, act_.q8, s);
         kernels_per_token_++;
       }
-      if (tp_) coll_->all_gather(act_.q8.xb, (size_t)hb * sizeof(XBlock), s);
+      if (tp_ && !tp_rep_attn_) coll_->all_gather(act_.q8.xb, (size_t)hb * sizeof(XBlock), s);
       LayerGemv go;
       go.xg = act_.q8.xb;
       go.out = o_out_ + (size_t)tp_rank_ * e_sh_;

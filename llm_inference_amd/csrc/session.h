@@ -172,6 +172,7 @@ class Session {
   int tp_rank_ = 0, tp_size_ = 1;
   std::unique_ptr<Collective> coll_;
   int nh_ = 0, nkv_ = 0, kv0_ = 0, e_sh_ = 0, f_sh_ = 0, v_sh_ = 0, v_rows_ = 0;
+  bool tp_rep_attn_ = false;  // tensor parallel: qkv + attention replicated on every rank (setup_tp)
   DevWeight logits_w_;  // the logits GEMV's rows: embd_ itself, or this rank's slice
   bool own_logits_w_ = false;
   // batched prefill (fast fused path, one device): chunk buffers

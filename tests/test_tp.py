@@ -46,13 +46,25 @@ def _run_ranks(g, tp, prompt, n_gen, max_ctx=64):
     return out
 
 
-@pytest.mark.parametrize("cfg_name,tp", [("mini-1b", 2), ("mini-1b", 4), ("mini-4b", 2), ("mini-4b", 4),
-                                         ("mini-4b", 8)])
-def test_sharded_matches_whole_model(cfg_name, tp, monkeypatch):
+def _qkv_bytes(g):
+    """Bytes of every layer's q, k and v weights (replicated on every rank by default)."""
+    from llm_inference_amd.gguf import GGUFFile
+    f = GGUFFile(g)
+    return sum(t.nbytes for t in f.tensor_infos if t.name.split(".")[-2] in ("attn_q", "attn_k", "attn_v"))
+
+
+@pytest.mark.parametrize("cfg_name,tp,mode", [("mini-1b", 2, "rep"), ("mini-1b", 4, "rep"), ("mini-4b", 2, "rep"),
+                                              ("mini-4b", 4, "rep"), ("mini-4b", 8, "rep"), ("mini-1b", 4, "shard"),
+                                              ("mini-4b", 8, "shard")])
+def test_sharded_matches_whole_model(cfg_name, tp, mode, monkeypatch):
+    """mode rep (default): q|k|v and the attention replicated on every rank, o / gate_up / down row-sharded;
+    shard (LLMI_TP_HEAD_SHARD=1): the heads sharded too (one more all-gather per layer)."""
     from llm_inference_amd.model import Model
     from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
     cfg = CONFIGS[cfg_name]
     g = build_gemma3_gguf(cfg, seed=3)
+    if mode == "shard":
+        monkeypatch.setenv("LLMI_TP_HEAD_SHARD", "1")
     prompt = np.random.default_rng(5).integers(4, cfg.vocab, 12).astype(np.int32)
     # sharded sessions run the prompt through the decode kernels (the batched
     # prefill is single-device): compare with the whole model doing the same
@@ -72,8 +84,9 @@ def test_sharded_matches_whole_model(cfg_name, tp, monkeypatch):
         np.testing.assert_array_equal(lg, ref)
         assert toks.tolist() == ref_toks.tolist()
         assert info.tp_rank == r and info.tp_size == tp
-        # each rank streams about 1/tp of the projection + logits bytes
-        assert info.bytes_per_token < full_bytes / tp * 1.2
+        # each rank streams about 1/tp of the projection + logits bytes (+ the replicated q|k|v)
+        rep = _qkv_bytes(g) if mode == "rep" else 0
+        assert info.bytes_per_token < (full_bytes - rep) / tp * 1.2 + rep
     # every rank ends with the same gathered logits
     for lg, _, _ in out[1:]:
         assert np.array_equal(lg, out[0][0])
@@ -104,6 +117,28 @@ def test_sharded_batched_prefill(cfg_name, tp, monkeypatch):
         assert toks.tolist() == ref_toks.tolist()
 
 
+@pytest.mark.parametrize("cfg_name,tp", [("mini-4b", 2), ("mini-4b", 8), ("mini-1b", 2)])
+def test_sharded_attention_block(cfg_name, tp, monkeypatch):
+    """Replicated attention on the ranks runs the single-device attention block (q|k|v + attention + the
+    rank's o rows in one launch) and the batched prefill: logits and greedy ids bit-identical to the whole
+    model with its block, fewer kernels per token than the per-projection shard path."""
+    from llm_inference_amd.model import Model
+    from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
+    cfg = CONFIGS[cfg_name]
+    g = build_gemma3_gguf(cfg, seed=17)
+    prompt = np.random.default_rng(19).integers(4, cfg.vocab, 40).astype(np.int32)
+    whole = Model(g, exact=False, max_ctx=64)
+    ref = whole.forward(prompt, 0)
+    ref_toks = whole.generate(int(np.argmax(ref)), len(prompt), 8)
+    whole.close()
+    out = _run_ranks(g, tp, prompt, 8)
+    for r, (lg, toks, info) in enumerate(out):
+        print(f"{cfg_name} tp{tp} rank {r}: kernels/token {info.kernels_per_token}, max|dlogit| {float(np.abs(lg - ref).max()):.3g}")
+        np.testing.assert_array_equal(lg, ref)
+        assert toks.tolist() == ref_toks.tolist()
+        assert info.batched_prefill == 1
+
+
 def test_rccl_single_rank_in_graph(monkeypatch):
     """ncclAllGather captured into the per-token hipGraph (one-rank
     communicator): identical to the whole-model session."""
@@ -129,9 +164,12 @@ def test_tp_argument_errors():
     from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
     g = build_gemma3_gguf(CONFIGS["mini-1b"], seed=1)
     grp = TPGroup(3)
-    with pytest.raises(LLMIError) as ei:  # 4 heads over 3 ranks
+    monkeypatch_env = pytest.MonkeyPatch()
+    monkeypatch_env.setenv("LLMI_TP_HEAD_SHARD", "1")
+    with pytest.raises(LLMIError) as ei:  # 4 heads over 3 ranks (head-sharded mode)
         Model(g, tp_rank=0, tp_size=3, tp_group=grp)
     assert ei.value.status == "E_ARG"
+    monkeypatch_env.undo()
     with pytest.raises(LLMIError) as ei:  # sharding needs the fast fused kernels
         Model(g, exact=True, tp_rank=0, tp_size=3, tp_group=grp)
     assert ei.value.status == "E_ARG"
