@@ -109,11 +109,12 @@ struct LayerCfg {
   {NB, ROLE, R, NW, P, E, false, SLAB, false, launch_cfg<R, NW, P, E, ROLE, false, false, PE>}
 // Q8_0 weights: row-major, single chunk (P passes of 16-B half blocks)
 // kq entries, one per weight type (+ the q|k Q4_K, v Q6_K launch for qkv roles)
-#define LLMI_LCFGK1(NB, ROLE, R, NW, P, E, EARLY, PE, WT)                                          \
-  {NB, ROLE, R, NW, P, E, false, 0, false, launch_cfg<R, NW, P, E, ROLE, false, EARLY, PE, false, WT>, false, WT, \
+#define LLMI_LCFGK1(NB, ROLE, R, NW, P, E, EARLY, PE, WT, SLAB)                                        \
+  {NB, ROLE, R, NW, P, E, false, SLAB, false, launch_cfg<R, NW, P, E, ROLE, false, EARLY, PE, false, WT>, false, WT, \
    fn2_of<R, NW, P, E, ROLE, EARLY, PE, WT>()}
-#define LLMI_LCFGK(NB, ROLE, R, NW, P, E, EARLY, PE)              \
-  LLMI_LCFGK1(NB, ROLE, R, NW, P, E, EARLY, PE, WT_Q4_K), LLMI_LCFGK1(NB, ROLE, R, NW, P, E, EARLY, PE, WT_Q6_K)
+#define LLMI_LCFGK(NB, ROLE, R, NW, P, E, EARLY, PE, SLAB)                                     \
+  LLMI_LCFGK1(NB, ROLE, R, NW, P, E, EARLY, PE, WT_Q4_K, SLAB), \
+      LLMI_LCFGK1(NB, ROLE, R, NW, P, E, EARLY, PE, WT_Q6_K, SLAB)
 #define LLMI_LCFG8(NB, ROLE, R, NW, P, E, EARLY) \
   {NB, ROLE, R, NW, P, E, false, 0, false, launch_cfg<R, NW, P, E, ROLE, false, EARLY, 0, true>, true}
 // PRO / GELU entries with NH helper waves (template role ROLE_PRO_H / ROLE_GELU_H)
@@ -125,6 +126,9 @@ struct LayerCfg {
 // 4B down 5.8 -> 5.4 us with PE3 (of 5) instead of EARLY; 27B
 // gate_up 35.8 -> 26.3 us with R8 NW8 P4 slab, qkv 10.4 -> 10.0 us, down
 // 24 -> 17-19.5 us issuing the weights after the quantized x is in LDS)
+#ifndef KQ_GU_SLAB
+#define KQ_GU_SLAB 1
+#endif
 const LayerCfg kLayerCfgs[] = {
     // PLAIN: x blocks copied to LDS
     LLMI_LCFG(32, ROLE_PLAIN, 2, 2, 1, 1, false, true, 0),     // 1B o        1152 rows -> 288 WGs
@@ -157,11 +161,11 @@ const LayerCfg kLayerCfgs[] = {
     LLMI_LCFG8(216, ROLE_QUANT, 1, 4, 7, 4, true),    // 1B down     1152 rows -> 288 WGs
     // K-quant weights in the kq layout (Gemma-3 4B Q4_K_M, BASELINE configs[3]): the Q4_0 4B
     // geometry (a 32-element sub-block per 16-B unit, as a Q4_0 block), row-major
-    LLMI_LCFGK(80, ROLE_PLAIN, 4, 4, 5, 1, true, 0),      // 4B qkv l0   4096 rows -> 256 WGs
-    LLMI_LCFGK(80, ROLE_PRO, 4, 4, 5, 10, true, 0),       // 4B qkv      256 WGs
-    LLMI_LCFGK(64, ROLE_PLAIN, 1, 10, 1, 1, true, 0),     // 4B o        2560 rows -> 256 WGs
-    LLMI_LCFGK(80, ROLE_GELU, 8, 10, 10, 4, false, 7),    // 4B gate_up  20480 rows, H 40 -> 256 WGs
-    LLMI_LCFGK(320, ROLE_QUANT, 1, 10, 5, 2, false, 3),   // 4B down     2560 rows -> 256 WGs
+    LLMI_LCFGK(80, ROLE_PLAIN, 4, 4, 5, 1, true, 0, 0),      // 4B qkv l0   4096 rows -> 256 WGs
+    LLMI_LCFGK(80, ROLE_PRO, 4, 4, 5, 10, true, 0, 0),       // 4B qkv      256 WGs
+    LLMI_LCFGK(64, ROLE_PLAIN, 1, 10, 1, 1, true, 0, 0),     // 4B o        2560 rows -> 256 WGs
+    LLMI_LCFGK(80, ROLE_GELU, 8, 10, 10, 4, false, 7, KQ_GU_SLAB),  // 4B gate_up  20480 rows, H 40 -> 256 WGs
+    LLMI_LCFGK(320, ROLE_QUANT, 1, 10, 5, 2, false, 3, 0),   // 4B down     2560 rows -> 256 WGs
 };
 #undef LLMI_LCFG
 

@@ -1028,7 +1028,7 @@ __global__ __launch_bounds__(512, 2) void prefill_gemm6_kernel(PrefillGemm16 a) 
     if (p < C::P_DD) {  // unit u: row u, the super-block word of the stage
       const int u = p * 64 + lane;
       pk[i] = 3;
-      pb[i] = reinterpret_cast<const unsigned char*>(a.kdd + (size_t)(n0 + u) * nsb);
+      pb[i] = reinterpret_cast<const unsigned char*>(a.kdd + (size_t)(n0 + u) * (a.slab ? 1 : nsb));
       po[i] = C::O_DD + p * 256;
       continue;
     }
@@ -1036,7 +1036,7 @@ __global__ __launch_bounds__(512, 2) void prefill_gemm6_kernel(PrefillGemm16 a) 
     if (p < C::P_QH) {  // unit u: row u / (KB / 2), sub-block pair u % (KB / 2): 16 B of high bits
       const int u = p * 64 + lane, row = u / (KB / 2), pr = u % (KB / 2);
       pk[i] = 4;
-      pb[i] = reinterpret_cast<const unsigned char*>(a.kqh + (size_t)(n0 + row) * nb + 2 * pr);
+      pb[i] = reinterpret_cast<const unsigned char*>(a.kqh + q4_block_index(a.slab, a.rows, nb, n0 + row, 2 * pr));
       po[i] = C::O_QH + p * 1024;
       continue;
     }
@@ -1056,8 +1056,11 @@ __global__ __launch_bounds__(512, 2) void prefill_gemm6_kernel(PrefillGemm16 a) 
 #pragma unroll
     for (int i = 0; i < C::PW; i++) {
       const int k = pk[i];
-      const long off = k == 0 ? wofs * 16 : k == 1 ? wofs * 2 : k == 2 ? (long)kb * 64 : k == 3 ? (long)(kb >> 3) * 4
-                                                                                                 : (long)kb * 8;
+      const long off = k == 0   ? wofs * 16
+                       : k == 1 ? wofs * 2
+                       : k == 2 ? (long)kb * 64
+                       : k == 3 ? (long)(kb >> 3) * (a.slab ? a.rows : 1) * 4
+                                : wofs * 8;
       if (k == 1 || k == 3) glds4(pb[i] + off, st + po[i]);
       else glds16(pb[i] + off, st + po[i]);
     }

@@ -151,12 +151,19 @@ __device__ __forceinline__ void kq_scale_min(int j, const uint8_t* q, int& d, in
   }
 }
 
+// destination of source super-block sbk (row-major: row * nsb + s): itself, or
+// slab-major (s * rows + row: super-block s of every row together)
+__device__ __forceinline__ size_t kq_dst(size_t sbk, int rows, int nsb) {
+  if (!rows) return sbk;
+  return (sbk % nsb) * rows + sbk / nsb;
+}
+
 __global__ void repack_q4_k_kernel(const uint8_t* __restrict__ src, size_t n_sub, uint4* __restrict__ qs,
-                                   uint16_t* __restrict__ sc, uint32_t* __restrict__ dd) {
-  const size_t u = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // sub-block (row-major: row * nsub + j)
-  if (u >= n_sub) return;
-  const size_t sbk = u / 8;
-  const int j = (int)(u % 8);
+                                   uint16_t* __restrict__ sc, uint32_t* __restrict__ dd, int slab_rows, int nsb) {
+  const size_t u0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // sub-block (row-major: row * nsub + j)
+  if (u0 >= n_sub) return;
+  const size_t sbk = u0 / 8, dsb = kq_dst(sbk, slab_rows, nsb), u = dsb * 8 + u0 % 8;
+  const int j = (int)(u0 % 8);
   const uint8_t* b = src + sbk * 144;
   const uint8_t* q = b + 16 + 32 * (j / 2);
   const int sh = (j & 1) * 4;
@@ -173,15 +180,16 @@ __global__ void repack_q4_k_kernel(const uint8_t* __restrict__ src, size_t n_sub
   int d6, m6;
   kq_scale_min(j, b + 4, d6, m6);
   sc[u] = (uint16_t)(d6 | (m6 << 8));
-  if (j == 0) dd[sbk] = (uint32_t)b[0] | ((uint32_t)b[1] << 8) | ((uint32_t)b[2] << 16) | ((uint32_t)b[3] << 24);
+  if (j == 0) dd[dsb] = (uint32_t)b[0] | ((uint32_t)b[1] << 8) | ((uint32_t)b[2] << 16) | ((uint32_t)b[3] << 24);
 }
 
 __global__ void repack_q6_k_kernel(const uint8_t* __restrict__ src, size_t n_sub, uint4* __restrict__ qs,
-                                   uint16_t* __restrict__ sc, uint32_t* __restrict__ dd, uint2* __restrict__ qh) {
-  const size_t u = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (u >= n_sub) return;
-  const size_t sbk = u / 8;
-  const int m = (int)(u % 8), n = m / 4, jq = m % 4;
+                                   uint16_t* __restrict__ sc, uint32_t* __restrict__ dd, uint2* __restrict__ qh,
+                                   int slab_rows, int nsb) {
+  const size_t u0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u0 >= n_sub) return;
+  const size_t sbk = u0 / 8, dsb = kq_dst(sbk, slab_rows, nsb), u = dsb * 8 + u0 % 8;
+  const int m = (int)(u0 % 8), n = m / 4, jq = m % 4;
   const uint8_t* b = src + sbk * 210;
   const uint8_t* ql = b + 64 * n + 32 * (jq & 1);
   const uint8_t* qhb = b + 128 + 32 * n;
@@ -205,12 +213,13 @@ __global__ void repack_q6_k_kernel(const uint8_t* __restrict__ src, size_t n_sub
   qh[u] = make_uint2(h[0], h[1]);
   const uint8_t* scb = b + 192 + 8 * n + 2 * jq;
   sc[u] = (uint16_t)(scb[0] | (scb[1] << 8));
-  if (m == 0) dd[sbk] = (uint32_t)b[208] | ((uint32_t)b[209] << 8);
+  if (m == 0) dd[dsb] = (uint32_t)b[208] | ((uint32_t)b[209] << 8);
 }
 
-void to_kq_layout(DevWeight& w, hipStream_t s) {
+void to_kq_layout(DevWeight& w, hipStream_t s, int slab) {
   if ((w.type != T_Q4_K && w.type != T_Q6_K) || w.kq || w.cols % 256) throw std::runtime_error("to_kq_layout: weight");
   const size_t nsb = (size_t)w.rows * (w.cols / 256), nsub = nsb * 8;
+  const int srows = slab ? w.rows : 0, rsb = w.cols / 256;
   uint4* qs;
   uint16_t* sc;
   uint32_t* dd;
@@ -220,10 +229,10 @@ void to_kq_layout(DevWeight& w, hipStream_t s) {
   LLMI_HIP(hipMalloc(&dd, nsb * 4 + 64));
   const dim3 grid((unsigned)((nsub + 255) / 256));
   if (w.type == T_Q4_K) {
-    hipLaunchKernelGGL(repack_q4_k_kernel, grid, dim3(256), 0, s, (const uint8_t*)w.qs, nsub, qs, sc, dd);
+    hipLaunchKernelGGL(repack_q4_k_kernel, grid, dim3(256), 0, s, (const uint8_t*)w.qs, nsub, qs, sc, dd, srows, rsb);
   } else {
     LLMI_HIP(hipMalloc(&qh, nsub * 8 + 64));
-    hipLaunchKernelGGL(repack_q6_k_kernel, grid, dim3(256), 0, s, (const uint8_t*)w.qs, nsub, qs, sc, dd, qh);
+    hipLaunchKernelGGL(repack_q6_k_kernel, grid, dim3(256), 0, s, (const uint8_t*)w.qs, nsub, qs, sc, dd, qh, srows, rsb);
   }
   LLMI_HIP(hipGetLastError());
   LLMI_HIP(hipStreamSynchronize(s));
@@ -233,6 +242,7 @@ void to_kq_layout(DevWeight& w, hipStream_t s) {
   w.kdd = dd;
   w.kqh = qh;
   w.kq = 1;
+  w.slab = slab ? 1 : 0;
 }
 
 // ---------------------------------------------------------------------------

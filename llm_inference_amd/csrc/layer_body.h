@@ -351,7 +351,23 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
   __amdgpu_buffer_rsrc_t rq, rd;
   int voq, vod, sq, sd;
   KqOff kq{};
-  if constexpr (WT != 0) {  // kq layout: row-major sub-blocks, super-block words, Q6_K high bits
+  if (WT != 0 && a.slab) {  // kq slab-major: super-block s of row r at (s rows + r), its 8 sub-blocks contiguous
+    const int r = wrow0 + rk, sl = rj >> 3, j8 = rj & 7, ps = (L / 8) * a.rows;
+    rq = buf_rsrc(a.qs, (uint32_t)a.rows * nb * 16);
+    rd = buf_rsrc(a.wd, (uint32_t)a.rows * nb * 2);
+    voq = (sl * a.rows + r) * 128 + j8 * 16;
+    vod = (sl * a.rows + r) * 16 + j8 * 2;
+    sq = ps * 128;
+    sd = ps * 16;
+    kq.rdd = buf_rsrc(a.kdd, (uint32_t)a.rows * (nb / 8) * 4);
+    kq.vdd = (sl * a.rows + r) * 4;
+    kq.sdd = ps * 4;
+    if constexpr (WT == WT_Q6_K) {
+      kq.rqh = buf_rsrc(a.kqh, (uint32_t)a.rows * nb * 8);
+      kq.vqh = (sl * a.rows + r) * 64 + j8 * 8;
+      kq.sqh = ps * 64;
+    }
+  } else if constexpr (WT != 0) {  // kq layout: row-major sub-blocks, super-block words, Q6_K high bits
     const int nsb = nb / 8;
     rq = buf_rsrc(a.qs + (size_t)min(wrow0, a.rows) * nb, (uint32_t)wrows * nb * 16);
     rd = buf_rsrc(a.wd + (size_t)min(wrow0, a.rows) * nb, (uint32_t)wrows * nb * 2);

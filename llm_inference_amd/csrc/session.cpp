@@ -406,7 +406,7 @@ void Session::upload(const GGUFView& g) {  // model.cpp:169-238 tensor map
   }
   if (all_fused) {  // the weight layouts the fused launch-table entries read
     auto relayout = [&](DevWeight& w, int role) {
-      if (w.type == T_Q4_K || w.type == T_Q6_K) to_kq_layout(w, stream_);
+      if (w.type == T_Q4_K || w.type == T_Q6_K) to_kq_layout(w, stream_, layer_gemv_slab(w, role));
       else if (layer_gemv_slab(w, role)) to_slab_layout(w, stream_);
     };
     for (auto& Ld : L_) {

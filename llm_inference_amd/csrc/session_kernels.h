@@ -15,7 +15,7 @@ void free_weight(DevWeight& w);
 // 8 blocks x all rows, block b of row r at (b / 8) rows 8 + r 8 + b % 8.
 void to_slab_layout(DevWeight& w, hipStream_t s);
 // Q4_K / Q6_K GGUF rows -> the kq sub-block layout of the fused layer kernels (kernels.h)
-void to_kq_layout(DevWeight& w, hipStream_t s);
+void to_kq_layout(DevWeight& w, hipStream_t s, int slab = 0);
 
 // outputs of a norm that feeds a GEMV: xn (always), plus optionally the Q8_0
 // blocks and/or the f16-rounded copy the next GEMV consumes
