@@ -715,13 +715,15 @@ __device__ __forceinline__ void vm_wait() {
 //   wd [2 pairs][MR]   u32 = f16 scales of blocks (2p, 2p + 1)
 //   xq [TN tok][4][3]  the token's 4 XBlocks (4 x 48 B contiguous) as 16-B parts, block slot
 //                      b ^ sw(tok): B fragment = part h, d_x = first dword of part 2
-template <int WR, int WT, int WK, int NT, int NS>
+//   (W8: Q8_0 weights -- wq [MR rows][2 KB] 16-B halves of the 32-B blocks, lane i of a piece reading row
+//   i / 8's 128-B run, half slot s ^ (row & 7): the A fragment is half h of the block as it lies, no unpack)
+template <int WR, int WT, int WK, int NT, int NS, bool W8 = false>
 struct PG5 {
-  static constexpr int KB = 4;
+  static constexpr int KB = 4, WB = W8 ? 32 : 16;  // weight bytes per block
   static constexpr int NW = WR * WT * WK, MR = 32 * WR, TN = 32 * NT * WT;
-  static constexpr int P_WQ = KB * MR / 64, P_WD = (KB / 2) * MR / 64, P_XQ = TN * KB * 3 / 64;
+  static constexpr int P_WQ = KB * MR * (WB / 16) / 64, P_WD = (KB / 2) * MR / 64, P_XQ = TN * KB * 3 / 64;
   static constexpr int P = P_WQ + P_WD + P_XQ, PW = (P + NW - 1) / NW;
-  static constexpr int O_WD = KB * MR * 16, O_XQ = O_WD + (KB / 2) * MR * 4;
+  static constexpr int O_WD = KB * MR * WB, O_XQ = O_WD + (KB / 2) * MR * 4;
   static constexpr int STAGE = O_XQ + TN * KB * 48;
   static constexpr int EPI = NW * 32 * 33 * 4;  // one 32-token group of every wave, padded rows
   static constexpr int LDS = STAGE * NS > EPI ? STAGE * NS : EPI;
@@ -741,9 +743,9 @@ __device__ __forceinline__ void static_for(F&& f) {
 typedef _Float16 h2x8 __attribute__((ext_vector_type(8)));
 typedef float v16f __attribute__((ext_vector_type(16)));
 
-template <int WR, int WT, int WK, int NT, int NS>
+template <int WR, int WT, int WK, int NT, int NS, bool W8>
 __global__ __launch_bounds__(512, (WK == 1 || NT > 1) ? 2 : 4) void prefill_gemm5_kernel(PrefillGemm a) {
-  using C = PG5<WR, WT, WK, NT, NS>;
+  using C = PG5<WR, WT, WK, NT, NS, W8>;
   constexpr int KB = C::KB;
   __shared__ __attribute__((aligned(16))) unsigned char s_ring[C::LDS];
   const int t = threadIdx.x, lane = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6), r = lane & 31, h = lane >> 5;
@@ -770,7 +772,12 @@ __global__ __launch_bounds__(512, (WK == 1 || NT > 1) ? 2 : 4) void prefill_gemm
 #pragma unroll
   for (int i = 0; i < C::PW; i++) {
     const int p = (w + i * C::NW) % C::P;
-    if (p < C::P_WQ) {
+    if (p < C::P_WQ && W8) {  // unit u: row u / 2KB, half slot u % 2KB (row-major Q8_0 blocks)
+      const int u = p * 64 + lane, row = u / (2 * KB), hs = (u % (2 * KB)) ^ (row & 7);
+      pk[i] = 0;
+      pb[i] = reinterpret_cast<const unsigned char*>(a.qs) + ((size_t)(n0 + row) * nb + (hs >> 1)) * 32 + (hs & 1) * 16;
+      po[i] = p * 1024;
+    } else if (p < C::P_WQ) {
       const int u = p * 64 + lane, row = u / KB, b = (u % KB) ^ pg5_sw(row);
       pk[i] = 0;
       pb[i] = reinterpret_cast<const unsigned char*>(a.qs + q4_block_index(a.slab, a.rows, nb, n0 + row, b));
@@ -798,7 +805,7 @@ __global__ __launch_bounds__(512, (WK == 1 || NT > 1) ? 2 : 4) void prefill_gemm
 #pragma unroll
     for (int i = 0; i < C::PW; i++) {
       const int k = pk[i];
-      const long off = k == 0 ? wofs * 16 : k == 1 ? wofs * 2 : (long)kb * (long)sizeof(XBlock);
+      const long off = k == 0 ? wofs * C::WB : k == 1 ? wofs * 2 : (long)kb * (long)sizeof(XBlock);
       if (k == 1) glds4(pb[i] + off, st + po[i]);
       else glds16(pb[i] + off, st + po[i]);
     }
@@ -842,11 +849,19 @@ __global__ __launch_bounds__(512, (WK == 1 || NT > 1) ? 2 : 4) void prefill_gemm
   auto load_ops = [&](const unsigned char* st, int bb) {
     Ops o;
     const int b = bb * WK + kg;
-    const uint4 q = *reinterpret_cast<const uint4*>(st + (arow * KB + (b ^ a_sw)) * 16);
-    o.A.x = q4_signed(h ? (q.x >> 4) & 0x0F0F0F0Fu : q.x & 0x0F0F0F0Fu);
-    o.A.y = q4_signed(h ? (q.y >> 4) & 0x0F0F0F0Fu : q.y & 0x0F0F0F0Fu);
-    o.A.z = q4_signed(h ? (q.z >> 4) & 0x0F0F0F0Fu : q.z & 0x0F0F0F0Fu);
-    o.A.w = q4_signed(h ? (q.w >> 4) & 0x0F0F0F0Fu : q.w & 0x0F0F0F0Fu);
+    if constexpr (W8) {
+      const uint4 q = *reinterpret_cast<const uint4*>(st + (arow * 2 * KB + ((2 * b + h) ^ (arow & 7))) * 16);
+      o.A.x = (int)q.x;
+      o.A.y = (int)q.y;
+      o.A.z = (int)q.z;
+      o.A.w = (int)q.w;
+    } else {
+      const uint4 q = *reinterpret_cast<const uint4*>(st + (arow * KB + (b ^ a_sw)) * 16);
+      o.A.x = q4_signed(h ? (q.x >> 4) & 0x0F0F0F0Fu : q.x & 0x0F0F0F0Fu);
+      o.A.y = q4_signed(h ? (q.y >> 4) & 0x0F0F0F0Fu : q.y & 0x0F0F0F0Fu);
+      o.A.z = q4_signed(h ? (q.z >> 4) & 0x0F0F0F0Fu : q.z & 0x0F0F0F0Fu);
+      o.A.w = q4_signed(h ? (q.w >> 4) & 0x0F0F0F0Fu : q.w & 0x0F0F0F0Fu);
+    }
     const int par = WK == 1 ? (bb & 1) : (kg & 1);  // the block's f16 in the scale pair
     const uint32_t wp = reinterpret_cast<const uint32_t*>(st + C::O_WD)[(b >> 1) * C::MR + arow];
     o.As = h2x8{};
@@ -1653,6 +1668,7 @@ void launch_prefill_norm(const PrefillNorm& a, int T, hipStream_t s) {
 }
 
 bool prefill_gemm_supported(const DevWeight& w) {
+  if (w.type == T_Q8_0) return w.rows % 32 == 0 && w.cols % 128 == 0 && !w.slab;  // v5 only
   return w.type == T_Q4_0 && w.rows % 32 == 0 && w.cols % 32 == 0 && (!w.slab || (w.cols / 32) % 8 == 0);
 }
 
@@ -1661,7 +1677,10 @@ static bool try_gemm5(const PrefillGemm& a, hipStream_t s) {
   using C = PG5<WR, WT, WK, NT, NS>;
   if (a.rows % C::MR || a.nb % C::KB) return false;
   const int n = (a.rows / C::MR) * ((a.T + C::TN - 1) / C::TN);
-  hipLaunchKernelGGL((prefill_gemm5_kernel<WR, WT, WK, NT, NS>), dim3(n), dim3(64 * C::NW), 0, s, a);
+  if (a.w8)
+    hipLaunchKernelGGL((prefill_gemm5_kernel<WR, WT, WK, NT, NS, true>), dim3(n), dim3(64 * C::NW), 0, s, a);
+  else
+    hipLaunchKernelGGL((prefill_gemm5_kernel<WR, WT, WK, NT, NS, false>), dim3(n), dim3(64 * C::NW), 0, s, a);
   return true;
 }
 
@@ -1736,6 +1755,7 @@ void launch_prefill_gemm(const DevWeight& w, const XBlock* x, int xstride, int T
   a.rows = w.rows;
   a.nb = w.cols / 32;
   a.slab = w.slab;
+  a.w8 = w.type == T_Q8_0;
   a.x = x;
   a.xstride = xstride;
   a.T = T;
@@ -1743,7 +1763,9 @@ void launch_prefill_gemm(const DevWeight& w, const XBlock* x, int xstride, int T
   a.ostride = ostride;
   const char* ver = getenv("LLMI_PREFILL_GEMM");  // A/B: "1", "2", "3", "4"; default v5
   const int v = ver ? atoi(ver) : 5;
-  if (v == 5 && launch_gemm5(a, s)) {
+  if (a.w8) {  // Q8_0 weights: v5 only
+    if (!launch_gemm5(a, s)) throw std::runtime_error("prefill_gemm: Q8_0 shape");
+  } else if (v == 5 && launch_gemm5(a, s)) {
   } else if (v >= 4 && w.rows % PG3_M == 0 && a.nb % PG3_KB == 0) {
     hipLaunchKernelGGL(prefill_gemm4_kernel, dim3(w.rows / PG3_M, (T + PG3_N - 1) / PG3_N), dim3(256), 0, s, a);
   } else if (v >= 3 && w.rows % PG3_M == 0 && a.nb % PG3_KB == 0) {

@@ -551,16 +551,18 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
     // projection; Q8_0 block slices need 32-aligned head and hidden shards)
     bool pf = fuse_layers_ && (embd_.type == T_F16 || embd_.type == T_Q8_0) && hp_.n_embd <= 8192 &&
               hp_.n_embd % 32 == 0 && hp_.n_ff % 32 == 0 && (!tp_ || (f_sh_ % 32 == 0 && coll_));
-    // Q4_0 layers: the int8 GEMM (v5) or the f16 one (v6, LLMI_PREFILL_F16); K-quant (kq) layers: the f16 GEMM
+    // Q4_0 layers: the int8 GEMM (v5) or the f16 one (v6, LLMI_PREFILL_F16); Q8_0 layers: v5; K-quant (kq)
+    // layers: the f16 GEMM
+    auto q40 = [](const DevWeight& w) { return w.type == T_Q4_0 || w.type == T_Q8_0; };
     auto gemm_ok = [&](const DevWeight& w) {
-      return w.type == T_Q4_0 ? prefill_gemm_supported(w) : prefill_gemm16_supported(w);
+      return q40(w) ? prefill_gemm_supported(w) : prefill_gemm16_supported(w);
     };
     for (const auto& l : L_) {
       bool ok = l.fused && (l.hd == 64 || l.hd == 128 || l.hd == 256) && gemm_ok(l.o.w) && gemm_ok(l.gate_up[0].w) &&
                 gemm_ok(l.down.w) && !l.qkv.empty();
       for (const auto& part : l.qkv) ok = ok && gemm_ok(part.w);
-      bool kq = l.o.w.type != T_Q4_0 || l.gate_up[0].w.type != T_Q4_0 || l.down.w.type != T_Q4_0;
-      for (const auto& part : l.qkv) kq = kq || part.w.type != T_Q4_0;
+      bool kq = !q40(l.o.w) || !q40(l.gate_up[0].w) || !q40(l.down.w);
+      for (const auto& part : l.qkv) kq = kq || !q40(part.w);
       if (ok && kq)  // f16 path: GELU group must allow the 8-unit f16 writes
         ok = layer_gemv_gelu_group(l.gate_up[0].w.cols, l.gate_up[0].w.type) % 8 == 0;
       pf = pf && ok;
@@ -833,7 +835,8 @@ void Session::prefill(const int32_t* tokens, int n, int pos) {
   // f16 MFMA GEMM (v6, LLMI_PREFILL_F16=1: not faster yet -- activation tile re-reads bound it -- and further from
   // the reference's Q8_0 arithmetic)
   const int G = nh_ / std::max(nkv_, 1);
-  const bool f16 = (pf_kq_ || getenv("LLMI_PREFILL_F16")) && !getenv("LLMI_PREFILL_ATTN_V1") && (G == 1 || G == 2 || G == 4) &&
+  const bool f16 = (pf_kq_ || (getenv("LLMI_PREFILL_F16") && L_[0].o.w.type == T_Q4_0)) && !getenv("LLMI_PREFILL_ATTN_V1") &&
+                   (G == 1 || G == 2 || G == 4) &&
                    layer_gemv_gelu_group(L_[0].gate_up[0].w.cols, L_[0].gate_up[0].w.type) % 8 == 0;
   if (pf_kq_ && !f16) throw status_error(LLMI_E_ARG, "prefill: K-quant layers need the f16 prefill path");
   auto gemm = [&](const DevWeight& w, float* out, int ostride) {

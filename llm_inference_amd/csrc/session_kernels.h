@@ -96,7 +96,7 @@ struct PrefillNorm {  // per token: embedding (table != null) or residual + norm
 struct PrefillGemm {
   const uint4* qs = nullptr;
   const uint16_t* wd = nullptr;
-  int rows = 0, nb = 0, slab = 0;
+  int rows = 0, nb = 0, slab = 0, w8 = 0;  // w8: Q8_0 weights (qs [rows][nb][32 B])
   const XBlock* x = nullptr;
   int xstride = 0, T = 0;
   float* out = nullptr;

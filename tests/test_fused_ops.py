@@ -65,9 +65,11 @@ def test_ops_mini1b_block(oracle):
 
 
 def test_ops_mini1b_q8_0_fused(oracle):
-    """Q8_0 weights in the fused layer launch table (W8 entries)."""
+    """Q8_0 weights in the fused layer launch table (W8 entries) and in the batched prefill (GEMM v5 with the
+    Q8_0 blocks as the int8 A operand): every prefill GEMM row against the reference's Q8_0 x Q8_0 rows."""
     from llm_inference_amd.gguf import TensorType as TT
-    _run(oracle, "mini-1b", 24, 10, 2, 64, wtype=TT.Q8_0, check_prefill=False)
+    chk = _run(oracle, "mini-1b", 24, 10, 2, 64, wtype=TT.Q8_0)
+    assert "prefill_gemm_qkv" in chk.report and "prefill_gemm_down" in chk.report
 
 
 def test_ops_mini1b_long_context(oracle):

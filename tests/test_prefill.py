@@ -52,6 +52,29 @@ def test_prefill_vs_token_loop(cfg_name, n_prompt, monkeypatch):
     assert ids_p.tolist() == ids_l.tolist()
 
 
+@pytest.mark.parametrize("cfg_name,n_prompt", [("mini-1b", 70), ("mini-1b", 300)])  # Q8_0 fused entries: 1B shapes
+def test_q8_0_batched_prefill(cfg_name, n_prompt, monkeypatch):
+    """Q8_0 weights (BASELINE configs[3]'s 1B Q8_0) through the batched prefill (GEMM v5, the weight blocks as
+    the int8 A operand) against the token loop: fast budget, same greedy ids, exact under re-chunking."""
+    from llm_inference_amd.gguf import TensorType as TT
+    from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
+    cfg = CONFIGS[cfg_name]
+    g = build_gemma3_gguf(cfg, seed=35, wtype=TT.Q8_0)
+    prompt = np.random.default_rng(8).integers(4, cfg.vocab, n_prompt).astype(np.int32)
+    mp = _model(g, monkeypatch)
+    assert mp.get_info().batched_prefill == 1
+    lp = mp.forward(prompt, 0)
+    ids_p = mp.generate(int(np.argmax(lp)), n_prompt, 8)
+    ml = _model(g, monkeypatch, no_prefill=True)
+    ll = ml.forward(prompt, 0)
+    ids_l = ml.generate(int(np.argmax(ll)), n_prompt, 8)
+    d = float(np.abs(lp - ll).max())
+    print(f"{cfg_name} Q8_0 n={n_prompt}: max|prefill - token loop| = {d:.3g}")
+    assert d <= FAST_VS_REF
+    assert ids_p.tolist() == ids_l.tolist()
+    np.testing.assert_array_equal(_model(g, monkeypatch, chunk=33).forward(prompt, 0), lp)
+
+
 def test_prefill_chunking_is_exact(monkeypatch):
     from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
     cfg = CONFIGS["mini-4b"]
