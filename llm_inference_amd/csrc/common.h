@@ -406,17 +406,23 @@ __device__ __forceinline__ void q8_block_quad(const float (&v)[8], int sub, XBlo
 // Every lane of the half-wave must execute it.
 __device__ __forceinline__ void q8k_block_quad(const float (&v)[8], int sub, XBlock* __restrict__ blk) {
   const int e0 = ((int)(threadIdx.x >> 2) & 7) * 32 + sub * 8;
-  float ax = -1.0f, sv = 0.0f;
-  int ix = 0;
+  // the super-block's max |x| (DPP within each 16-lane row, one swizzle across the two rows), then the first
+  // element attaining it and its sign as the min of (index << 1 | sign) -- the reference's first maximal |x|
+  float ax = 0.0f;
 #pragma unroll
-  for (int k = 0; k < 8; k++)
-    if (fabsf(v[k]) > ax) { ax = fabsf(v[k]); ix = e0 + k; sv = v[k]; }
+  for (int k = 0; k < 8; k++) ax = fmaxf(ax, fabsf(v[k]));
+  ax = row16_max(ax);
+  ax = fmaxf(ax, __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(ax), 0x401F)));  // lane ^ 16
+  int key = 0x7FFFFFFF;
 #pragma unroll
-  for (int o = 1; o < 32; o <<= 1) {
-    const float oa = __shfl_xor(ax, o), os = __shfl_xor(sv, o);
-    const int oi = __shfl_xor(ix, o);
-    if (oa > ax || (oa == ax && oi < ix)) { ax = oa; ix = oi; sv = os; }
-  }
+  for (int k = 7; k >= 0; k--)
+    if (fabsf(v[k]) == ax) key = ((e0 + k) << 1) | (v[k] < 0.0f ? 1 : 0);
+  key = min(key, dpp_i<DPP_QUAD_1032>(key));
+  key = min(key, dpp_i<DPP_QUAD_2301>(key));
+  key = min(key, dpp_i<DPP_ROW_MIRROR>(key));
+  key = min(key, dpp_i<DPP_ROW_HALF_MIRROR>(key));
+  key = min(key, __builtin_amdgcn_ds_swizzle(key, 0x401F));
+  const float sv = (key & 1) ? -ax : ax;
   uint32_t w0 = 0, w1 = 0;
   int s = 0;
   float d = 0.0f;
