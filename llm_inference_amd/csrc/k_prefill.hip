@@ -120,10 +120,11 @@ __global__ __launch_bounds__(256) void prefill_norm_kernel(PrefillNorm a) {
     return;
   }
   XBlock* xq = a.xq + (size_t)tok * a.xstride;
-  for (int i = t; i < n / 8; i += 256) {  // a DPP quad of lanes per Q8_0 block
+  for (int i = t; i < n / 8; i += 256) {  // a DPP quad of lanes per Q8_0 block (Q8_K: a half-wave per super-block)
     const float4 f0 = reinterpret_cast<const float4*>(s_x)[2 * i], f1 = reinterpret_cast<const float4*>(s_x)[2 * i + 1];
     const float vv[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
-    q8_block_quad(vv, i & 3, xq + (i >> 2));
+    if (a.q8k) q8k_block_quad(vv, i & 3, xq + (i >> 2));
+    else q8_block_quad(vv, i & 3, xq + (i >> 2));
   }
 }
 
@@ -208,6 +209,7 @@ __global__ __launch_bounds__(256) void prefill_norm_res_kernel(PrefillNorm a) {
     }
     if (!in_row(k)) continue;  // whole quads in or out
     if (a.x16) store_f16x8(a.x16 + (size_t)tok * a.x16stride + b * 32 + sub * 8, v);
+    else if (a.q8k) q8k_block_quad(v, sub, xq + b);  // half-waves = super-blocks (blocks t / 4 + 64 k)
     else q8_block_quad(v, sub, xq + b);
   }
 }
@@ -717,13 +719,18 @@ __device__ __forceinline__ void vm_wait() {
 //                      b ^ sw(tok): B fragment = part h, d_x = first dword of part 2
 //   (W8: Q8_0 weights -- wq [MR rows][2 KB] 16-B halves of the 32-B blocks, lane i of a piece reading row
 //   i / 8's 128-B run, half slot s ^ (row & 7): the A fragment is half h of the block as it lies, no unpack)
-template <int WR, int WT, int WK, int NT, int NS, bool W8 = false>
+//   (KQ: Q4_K (1) / Q6_K (2) weights in the kq layout -- wq / wd hold the 16-B nibble sub-blocks and their u16
+//   scale words as Q4_0's blocks and scales; dd [64] the rows' u32 super-block word (d | dmin) of the stage;
+//   Q6_K qh [MR][4] the sub-blocks' 8 B of high bits; the activation blocks hold Q8_K quants)
+template <int WR, int WT, int WK, int NT, int NS, bool W8 = false, int KQ = 0>
 struct PG5 {
   static constexpr int KB = 4, WB = W8 ? 32 : 16;  // weight bytes per block
   static constexpr int NW = WR * WT * WK, MR = 32 * WR, TN = 32 * NT * WT;
   static constexpr int P_WQ = KB * MR * (WB / 16) / 64, P_WD = (KB / 2) * MR / 64, P_XQ = TN * KB * 3 / 64;
-  static constexpr int P = P_WQ + P_WD + P_XQ, PW = (P + NW - 1) / NW;
-  static constexpr int O_WD = KB * MR * WB, O_XQ = O_WD + (KB / 2) * MR * 4;
+  static constexpr int P_DD = KQ ? (MR + 63) / 64 : 0, P_QH = KQ == 2 ? MR / 32 : 0;
+  static constexpr int P = P_WQ + P_WD + P_DD + P_QH + P_XQ, PW = (P + NW - 1) / NW;
+  static constexpr int O_WD = KB * MR * WB, O_DD = O_WD + (KB / 2) * MR * 4, O_QH = O_DD + P_DD * 256;
+  static constexpr int O_XQ = O_QH + P_QH * 1024;
   static constexpr int STAGE = O_XQ + TN * KB * 48;
   static constexpr int EPI = NW * 32 * 33 * 4;  // one 32-token group of every wave, padded rows
   static constexpr int LDS = STAGE * NS > EPI ? STAGE * NS : EPI;
@@ -743,9 +750,14 @@ __device__ __forceinline__ void static_for(F&& f) {
 typedef _Float16 h2x8 __attribute__((ext_vector_type(8)));
 typedef float v16f __attribute__((ext_vector_type(16)));
 
-template <int WR, int WT, int WK, int NT, int NS, bool W8>
-__global__ __launch_bounds__(512, (WK == 1 || NT > 1) ? 2 : 4) void prefill_gemm5_kernel(PrefillGemm a) {
-  using C = PG5<WR, WT, WK, NT, NS, W8>;
+__device__ __forceinline__ int pg_q6_bytes(uint32_t nib4, uint32_t hb, int k) {  // 4 six-bit values - 32 (int8)
+  const uint32_t v = nib4 | (((hb >> (2 * k)) & 0x03030303u) << 4);
+  return (int)((v + 0x60606060u) ^ 0x80808080u);
+}
+
+template <int WR, int WT, int WK, int NT, int NS, bool W8, int KQ = 0>
+__global__ __launch_bounds__(512, KQ == 2 ? 1 : (WK == 1 || NT > 1) ? 2 : 4) void prefill_gemm5_kernel(PrefillGemm a) {
+  using C = PG5<WR, WT, WK, NT, NS, W8, KQ>;
   constexpr int KB = C::KB;
   __shared__ __attribute__((aligned(16))) unsigned char s_ring[C::LDS];
   const int t = threadIdx.x, lane = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6), r = lane & 31, h = lane >> 5;
@@ -787,8 +799,18 @@ __global__ __launch_bounds__(512, (WK == 1 || NT > 1) ? 2 : 4) void prefill_gemm
       pk[i] = 1;
       pb[i] = reinterpret_cast<const unsigned char*>(a.wd + q4_block_index(a.slab, a.rows, nb, n0 + u % C::MR, 2 * (u / C::MR)));
       po[i] = C::O_WD + q * 256;
+    } else if (p < C::P_WQ + C::P_WD + C::P_DD) {  // unit u: row u % MR, the stage's super-block word
+      const int q = p - C::P_WQ - C::P_WD, u = (q * 64 + lane) % C::MR;
+      pk[i] = 3;
+      pb[i] = reinterpret_cast<const unsigned char*>(a.kdd + (size_t)(n0 + u) * (a.slab ? 1 : nb / 8));
+      po[i] = C::O_DD + q * 256;
+    } else if (p < C::P_WQ + C::P_WD + C::P_DD + C::P_QH) {  // unit u: row u / 2, sub-blocks 2 (u % 2) .. + 1
+      const int q = p - C::P_WQ - C::P_WD - C::P_DD, u = q * 64 + lane;
+      pk[i] = 4;
+      pb[i] = reinterpret_cast<const unsigned char*>(a.kqh + q4_block_index(a.slab, a.rows, nb, n0 + u / 2, 2 * (u % 2)));
+      po[i] = C::O_QH + q * 1024;
     } else {  // unit u: (token, block slot, part)
-      const int q = p - C::P_WQ - C::P_WD, u = q * 64 + lane;
+      const int q = p - C::P_WQ - C::P_WD - C::P_DD - C::P_QH, u = q * 64 + lane;
       const int tok = u / (3 * KB), rem = u % (3 * KB), b = (rem / 3) ^ pg5_sw(tok);
       pk[i] = 2;
       pb[i] = reinterpret_cast<const unsigned char*>(a.x + (size_t)min(tk0 + tok, a.T - 1) * a.xstride + b) + 16 * (rem % 3);
@@ -805,8 +827,12 @@ __global__ __launch_bounds__(512, (WK == 1 || NT > 1) ? 2 : 4) void prefill_gemm
 #pragma unroll
     for (int i = 0; i < C::PW; i++) {
       const int k = pk[i];
-      const long off = k == 0 ? wofs * C::WB : k == 1 ? wofs * 2 : (long)kb * (long)sizeof(XBlock);
-      if (k == 1) glds4(pb[i] + off, st + po[i]);
+      const long off = k == 0   ? wofs * C::WB
+                       : k == 1 ? wofs * 2
+                       : k == 3 ? (long)(kb >> 3) * (a.slab ? a.rows : 1) * 4
+                       : k == 4 ? wofs * 8
+                                : (long)kb * (long)sizeof(XBlock);
+      if (k == 1 || k == 3) glds4(pb[i] + off, st + po[i]);
       else glds16(pb[i] + off, st + po[i]);
     }
   };
@@ -840,16 +866,52 @@ __global__ __launch_bounds__(512, (WK == 1 || NT > 1) ? 2 : 4) void prefill_gemm
   // slot may be refilled once its MFMAs have read it.)  The scale products s[row][tok] = d_w[row] * d_x[tok]
   // come from one f16 MFMA (k = 0 only: an outer product, exact in f32 -- 11-bit x 11-bit significands),
   // so the VALU keeps only (float)isum and the FMA per output.
+  // KQ: the scale products s[row][tok] = (d sc)[row] d_x[tok] (d_x: the Q8_K super-block's f32 d) from an f32
+  // MFMA (k = 0 only, one rounding); Q4_K's min term sum_b (dmin m)[row][b] (d_x bsum)[tok][b] accumulates on
+  // the matrix pipe (Macc, subtracted at the end: t = fma(d sc, isum, -(dmin m) d_x bsum), ops.cpp:614-706);
+  // Q6_K's two 16-element scales split the i8 product by lane half (A zeroed on the other half: i0, i1) and
+  // take two scale products (ops.cpp:708-785)
   struct Ops {
-    v4i A;
+    v4i A, A1;
     h2x8 As;
+    float aS, aS1, aM;
     v4i B[NT];
     float dx[NT];
+    int ns[NT];
   };
   auto load_ops = [&](const unsigned char* st, int bb) {
     Ops o;
     const int b = bb * WK + kg;
-    if constexpr (W8) {
+    if constexpr (KQ != 0) {
+      const uint4 q = *reinterpret_cast<const uint4*>(st + (arow * KB + (b ^ a_sw)) * 16);
+      const uint32_t wp = reinterpret_cast<const uint32_t*>(st + C::O_WD)[(b >> 1) * C::MR + arow];
+      const uint32_t sw = (wp >> (16 * (b & 1))) & 0xFFFFu;
+      const uint32_t dd = reinterpret_cast<const uint32_t*>(st + C::O_DD)[arow];
+      const float d = h2f((uint16_t)(dd & 0xFFFFu));
+      const uint32_t n0_ = h ? (q.x >> 4) & 0x0F0F0F0Fu : q.x & 0x0F0F0F0Fu, n1_ = h ? (q.y >> 4) & 0x0F0F0F0Fu : q.y & 0x0F0F0F0Fu;
+      const uint32_t n2_ = h ? (q.z >> 4) & 0x0F0F0F0Fu : q.z & 0x0F0F0F0Fu, n3_ = h ? (q.w >> 4) & 0x0F0F0F0Fu : q.w & 0x0F0F0F0Fu;
+      if constexpr (KQ == 1) {
+        o.A.x = (int)n0_;
+        o.A.y = (int)n1_;
+        o.A.z = (int)n2_;
+        o.A.w = (int)n3_;
+        o.aS = h ? 0.0f : d * (float)(sw & 0xFFu);
+        o.aM = h ? 0.0f : h2f((uint16_t)(dd >> 16)) * (float)(sw >> 8);
+      } else {
+        const uint2 hb = *reinterpret_cast<const uint2*>(st + C::O_QH + arow * 32 + b * 8);
+        const uint32_t hw = h ? hb.y : hb.x;
+        v4i A6;
+        A6.x = pg_q6_bytes(n0_, hw, 0);
+        A6.y = pg_q6_bytes(n1_, hw, 1);
+        A6.z = pg_q6_bytes(n2_, hw, 2);
+        A6.w = pg_q6_bytes(n3_, hw, 3);
+        const v4i z4 = {};
+        o.A = h ? z4 : A6;
+        o.A1 = h ? A6 : z4;
+        o.aS = h ? 0.0f : d * (float)(int8_t)(sw & 0xFFu);
+        o.aS1 = h ? 0.0f : d * (float)(int8_t)(sw >> 8);
+      }
+    } else if constexpr (W8) {
       const uint4 q = *reinterpret_cast<const uint4*>(st + (arow * 2 * KB + ((2 * b + h) ^ (arow & 7))) * 16);
       o.A.x = (int)q.x;
       o.A.y = (int)q.y;
@@ -862,15 +924,18 @@ __global__ __launch_bounds__(512, (WK == 1 || NT > 1) ? 2 : 4) void prefill_gemm
       o.A.z = q4_signed(h ? (q.z >> 4) & 0x0F0F0F0Fu : q.z & 0x0F0F0F0Fu);
       o.A.w = q4_signed(h ? (q.w >> 4) & 0x0F0F0F0Fu : q.w & 0x0F0F0F0Fu);
     }
-    const int par = WK == 1 ? (bb & 1) : (kg & 1);  // the block's f16 in the scale pair
-    const uint32_t wp = reinterpret_cast<const uint32_t*>(st + C::O_WD)[(b >> 1) * C::MR + arow];
-    o.As = h2x8{};
-    o.As[0] = __builtin_bit_cast(_Float16, (uint16_t)(h ? 0u : (wp >> (16 * par)) & 0xFFFFu));
+    if constexpr (KQ == 0) {
+      const int par = WK == 1 ? (bb & 1) : (kg & 1);  // the block's f16 in the scale pair
+      const uint32_t wp = reinterpret_cast<const uint32_t*>(st + C::O_WD)[(b >> 1) * C::MR + arow];
+      o.As = h2x8{};
+      o.As[0] = __builtin_bit_cast(_Float16, (uint16_t)(h ? 0u : (wp >> (16 * par)) & 0xFFFFu));
+    }
 #pragma unroll
     for (int j = 0; j < NT; j++) {
       const unsigned char* xb = st + b_base[j] + (b ^ b_sw[j]) * 48;
       const uint4 xv = *reinterpret_cast<const uint4*>(xb + 16 * h);
       o.dx[j] = *reinterpret_cast<const float*>(xb + 32);
+      if constexpr (KQ == 1) o.ns[j] = *reinterpret_cast<const int*>(xb + 36);
       o.B[j].x = (int)xv.x;
       o.B[j].y = (int)xv.y;
       o.B[j].z = (int)xv.z;
@@ -881,17 +946,28 @@ __global__ __launch_bounds__(512, (WK == 1 || NT > 1) ? 2 : 4) void prefill_gemm
   // results of two blocks in flight, ping-pong by the block count's parity (compile-time indices: no copies)
   v16i Dr[2][NT];
   v16f Sr[2][NT];
+  v16i Dr2[KQ == 2 ? 2 : 1][NT];
+  v16f Sr2[KQ == 2 ? 2 : 1][NT];
+  v16f Macc[KQ == 1 ? NT : 1];
 #pragma unroll
   for (int j = 0; j < NT; j++) {
     Dr[1][j] = zero;
     Sr[1][j] = zerof;  // fmaf(+0, +0, acc) leaves acc unchanged
+    if constexpr (KQ == 2) {
+      Dr2[1][j] = zero;
+      Sr2[1][j] = zerof;
+    }
+    if constexpr (KQ == 1) Macc[j] = zerof;
   }
   auto epi = [&](auto sl) {
+    constexpr int S = decltype(sl)::value;
 #pragma unroll
     for (int j = 0; j < NT; j++)
 #pragma unroll
-      for (int reg = 0; reg < 16; reg++)
-        acc[j][reg] = fmaf(Sr[decltype(sl)::value][j][reg], (float)Dr[decltype(sl)::value][j][reg], acc[j][reg]);
+      for (int reg = 0; reg < 16; reg++) {
+        acc[j][reg] = fmaf(Sr[S][j][reg], (float)Dr[S][j][reg], acc[j][reg]);
+        if constexpr (KQ == 2) acc[j][reg] = fmaf(Sr2[S][j][reg], (float)Dr2[S][j][reg], acc[j][reg]);
+      }
   };
   constexpr int NB = KB / WK;  // blocks per stage and wave
   auto stage = [&](int c, auto first) {  // first: slot of the stage's first block
@@ -910,10 +986,22 @@ __global__ __launch_bounds__(512, (WK == 1 || NT > 1) ? 2 : 4) void prefill_gemm
       if constexpr (bb + 1 < NB) o[(bb + 1) & 1] = load_ops(st, bb + 1);
 #pragma unroll
       for (int j = 0; j < NT; j++) {
-        Dr[sl][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(o[bb & 1].A, o[bb & 1].B[j], zero, 0, 0, 0);
-        h2x8 Bs = {};
-        Bs[0] = h ? (_Float16)0.0f : (_Float16)o[bb & 1].dx[j];  // d_x is an f16 value (q8 block scale): exact
-        Sr[sl][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(o[bb & 1].As, Bs, zerof, 0, 0, 0);
+        const Ops& op = o[bb & 1];
+        Dr[sl][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(op.A, op.B[j], zero, 0, 0, 0);
+        if constexpr (KQ != 0) {
+          const float bS = h ? 0.0f : op.dx[j];
+          Sr[sl][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(op.aS, bS, zerof, 0, 0, 0);
+          if constexpr (KQ == 1)
+            Macc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(op.aM, h ? 0.0f : op.dx[j] * (float)op.ns[j], Macc[j], 0, 0, 0);
+          if constexpr (KQ == 2) {
+            Dr2[sl][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(op.A1, op.B[j], zero, 0, 0, 0);
+            Sr2[sl][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(op.aS1, bS, zerof, 0, 0, 0);
+          }
+        } else {
+          h2x8 Bs = {};
+          Bs[0] = h ? (_Float16)0.0f : (_Float16)op.dx[j];  // d_x is an f16 value (q8 block scale): exact
+          Sr[sl][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(op.As, Bs, zerof, 0, 0, 0);
+        }
       }
       epi(std::integral_constant<int, sl ^ 1>{});  // the previous block's results
     });
@@ -933,6 +1021,12 @@ __global__ __launch_bounds__(512, (WK == 1 || NT > 1) ? 2 : 4) void prefill_gemm
     } else {
       epi(std::integral_constant<int, 1>{});
     }
+  }
+  if constexpr (KQ == 1) {  // the Q4_K min terms
+#pragma unroll
+    for (int j = 0; j < NT; j++)
+#pragma unroll
+      for (int reg = 0; reg < 16; reg++) acc[j][reg] -= Macc[j][reg];
   }
   // epilogue, one 32-token group at a time: every wave's tile (rows x 32 tokens) to LDS, then the K groups
   // summed in group order and stored row-contiguous per token
@@ -1583,6 +1677,52 @@ __global__ __launch_bounds__(64 * G * S) void prefill_attn_mfma_kernel(PrefillAt
     return;
   }
   XBlock* xo = a.xq + (size_t)(tok0 + r) * a.xstride + (size_t)hq * HD / 32;
+  if constexpr (HD == 256) {
+    if (a.q8k) {  // Q8_K (ops.cpp:142-178): the head's 256 dims are one super-block, lanes r and r + 32
+      float ax = 0.0f;
+#pragma unroll
+      for (int i = 0; i < HD / 32; i++)
+#pragma unroll
+        for (int reg = 0; reg < 16; reg++) ax = fmaxf(ax, fabsf(o[i][reg] / l_run));
+      ax = fmaxf(ax, __shfl_xor(ax, 32));
+      int key = 0x7FFFFFFF;  // the first dim attaining max |x|, with its sign
+#pragma unroll
+      for (int i = 0; i < HD / 32; i++)
+#pragma unroll
+        for (int reg = 0; reg < 16; reg++) {
+          const float v = o[i][reg] / l_run;
+          const int dim = 32 * i + 8 * (reg >> 2) + 4 * h + (reg & 3);
+          if (fabsf(v) == ax) key = min(key, (dim << 1) | (v < 0.0f ? 1 : 0));
+        }
+      key = min(key, __shfl_xor(key, 32));
+      const float iscale = ax != 0.0f ? -127.f / ((key & 1) ? -ax : ax) : 0.0f;
+#pragma unroll
+      for (int i = 0; i < HD / 32; i++) {
+        int sum = 0;
+        uint32_t wq[4];
+#pragma unroll
+        for (int gq = 0; gq < 4; gq++) {
+          wq[gq] = 0;
+#pragma unroll
+          for (int e = 0; e < 4; e++) {
+            int qv = ax != 0.0f ? nearest_int_fma(iscale, o[i][4 * gq + e] / l_run) : 0;
+            qv = qv < -128 ? -128 : (qv > 127 ? 127 : qv);
+            sum += qv;
+            wq[gq] |= (uint32_t)(qv & 0xFF) << (8 * e);
+          }
+        }
+        sum += __shfl_xor(sum, 32);
+        uint32_t* qb = reinterpret_cast<uint32_t*>(xo + i);
+#pragma unroll
+        for (int gq = 0; gq < 4; gq++) qb[2 * gq + h] = wq[gq];
+        if (h == 0) {
+          xo[i].d = ax != 0.0f ? 1.0f / iscale : 0.0f;
+          xo[i].nsum8 = sum;
+        }
+      }
+      return;
+    }
+  }
 #pragma unroll
   for (int i = 0; i < HD / 32; i++) {
     float v[16];
@@ -1636,9 +1776,9 @@ __global__ __launch_bounds__(256) void prefill_gelu_kernel(const float* __restri
 // float4 loads from the interleaved gate/up rows (H % 8 == 0: the 8 units sit in one H-group)
 __global__ __launch_bounds__(256) void prefill_gelu8_kernel(const float* __restrict__ gu, int F, int H,
                                                             XBlock* __restrict__ xq, int xstride,
-                                                            uint16_t* __restrict__ x16, int x16stride) {
+                                                            uint16_t* __restrict__ x16, int x16stride, int q8k) {
   const int tok = blockIdx.y, i = blockIdx.x * 256 + threadIdx.x;
-  if (i * 8 >= F) return;  // whole quads (F % 32 == 0)
+  if (i * 8 >= F) return;  // whole quads (F % 32 == 0); Q8_K: whole half-waves (F % 256 == 0)
   const int u = 8 * i;
   const float* g = gu + (size_t)tok * 2 * F + 2 * H * (u / H) + u % H;
   const float4 g0 = reinterpret_cast<const float4*>(g)[0], g1 = reinterpret_cast<const float4*>(g)[1];
@@ -1646,6 +1786,7 @@ __global__ __launch_bounds__(256) void prefill_gelu8_kernel(const float* __restr
   const float v[8] = {gelu_mul1(g0.x, u0.x), gelu_mul1(g0.y, u0.y), gelu_mul1(g0.z, u0.z), gelu_mul1(g0.w, u0.w),
                       gelu_mul1(g1.x, u1.x), gelu_mul1(g1.y, u1.y), gelu_mul1(g1.z, u1.z), gelu_mul1(g1.w, u1.w)};
   if (x16) store_f16x8(x16 + (size_t)tok * x16stride + u, v);
+  else if (q8k) q8k_block_quad(v, i & 3, xq + (size_t)tok * xstride + i / 4);
   else q8_block_quad(v, i & 3, xq + (size_t)tok * xstride + i / 4);
 }
 
@@ -1653,6 +1794,7 @@ __global__ __launch_bounds__(256) void prefill_gelu8_kernel(const float* __restr
 
 void launch_prefill_norm(const PrefillNorm& a, int T, hipStream_t s) {
   if (a.n > 256 * PN_EPT || a.n % 32) throw std::runtime_error("prefill_norm: n_embd");
+  if (a.q8k && (a.n % 256 || a.x16)) throw std::runtime_error("prefill_norm: Q8_K blocks need n % 256 == 0");
   const int eb = (a.n / 32 + 63) / 64;
   if (!a.table && eb <= 3 && !getenv("LLMI_PREFILL_NORM_V1")) {
     switch (eb) {
@@ -1669,6 +1811,7 @@ void launch_prefill_norm(const PrefillNorm& a, int T, hipStream_t s) {
 
 bool prefill_gemm_supported(const DevWeight& w) {
   if (w.type == T_Q8_0) return w.rows % 32 == 0 && w.cols % 128 == 0 && !w.slab;  // v5 only
+  if (w.type == T_Q4_K || w.type == T_Q6_K) return w.kq && w.rows % 32 == 0 && w.cols % 256 == 0;  // v5, Q8_K x
   return w.type == T_Q4_0 && w.rows % 32 == 0 && w.cols % 32 == 0 && (!w.slab || (w.cols / 32) % 8 == 0);
 }
 
@@ -1677,7 +1820,11 @@ static bool try_gemm5(const PrefillGemm& a, hipStream_t s) {
   using C = PG5<WR, WT, WK, NT, NS>;
   if (a.rows % C::MR || a.nb % C::KB) return false;
   const int n = (a.rows / C::MR) * ((a.T + C::TN - 1) / C::TN);
-  if (a.w8)
+  if (a.kq == 1)
+    hipLaunchKernelGGL((prefill_gemm5_kernel<WR, WT, WK, NT, NS, false, 1>), dim3(n), dim3(64 * C::NW), 0, s, a);
+  else if (a.kq == 2)
+    hipLaunchKernelGGL((prefill_gemm5_kernel<WR, WT, WK, NT, NS, false, 2>), dim3(n), dim3(64 * C::NW), 0, s, a);
+  else if (a.w8)
     hipLaunchKernelGGL((prefill_gemm5_kernel<WR, WT, WK, NT, NS, true>), dim3(n), dim3(64 * C::NW), 0, s, a);
   else
     hipLaunchKernelGGL((prefill_gemm5_kernel<WR, WT, WK, NT, NS, false>), dim3(n), dim3(64 * C::NW), 0, s, a);
@@ -1756,6 +1903,9 @@ void launch_prefill_gemm(const DevWeight& w, const XBlock* x, int xstride, int T
   a.nb = w.cols / 32;
   a.slab = w.slab;
   a.w8 = w.type == T_Q8_0;
+  a.kq = w.type == T_Q4_K ? 1 : w.type == T_Q6_K ? 2 : 0;
+  a.kdd = w.kdd;
+  a.kqh = w.kqh;
   a.x = x;
   a.xstride = xstride;
   a.T = T;
@@ -1763,8 +1913,8 @@ void launch_prefill_gemm(const DevWeight& w, const XBlock* x, int xstride, int T
   a.ostride = ostride;
   const char* ver = getenv("LLMI_PREFILL_GEMM");  // A/B: "1", "2", "3", "4"; default v5
   const int v = ver ? atoi(ver) : 5;
-  if (a.w8) {  // Q8_0 weights: v5 only
-    if (!launch_gemm5(a, s)) throw std::runtime_error("prefill_gemm: Q8_0 shape");
+  if (a.w8 || a.kq) {  // Q8_0 / kq weights: v5 only
+    if (!launch_gemm5(a, s)) throw std::runtime_error("prefill_gemm: Q8_0 / K-quant shape");
   } else if (v == 5 && launch_gemm5(a, s)) {
   } else if (v >= 4 && w.rows % PG3_M == 0 && a.nb % PG3_KB == 0) {
     hipLaunchKernelGGL(prefill_gemm4_kernel, dim3(w.rows / PG3_M, (T + PG3_N - 1) / PG3_N), dim3(256), 0, s, a);
@@ -1793,8 +1943,9 @@ void launch_prefill_qk(const PrefillQK& a, int T, hipStream_t s) {
 template <int HD>
 static void attn_g(const PrefillAttn& a, int T, hipStream_t s) {
   const int G = a.n_head / a.n_head_kv;
-  if (a.x16 && (getenv("LLMI_PREFILL_ATTN_V1") || (G != 1 && G != 2 && G != 4)))
-    throw std::runtime_error("prefill_attn: f16 output needs the MFMA kernel (GQA group 1, 2 or 4)");
+  if ((a.x16 || a.q8k) && (getenv("LLMI_PREFILL_ATTN_V1") || (G != 1 && G != 2 && G != 4)))
+    throw std::runtime_error("prefill_attn: f16 / Q8_K output needs the MFMA kernel (GQA group 1, 2 or 4)");
+  if (a.q8k && (HD != 256 || a.x16)) throw std::runtime_error("prefill_attn: Q8_K output needs head_dim 256");
   if (!getenv("LLMI_PREFILL_ATTN_V1") && HD >= 64) {
     const dim3 grid(a.n_head_kv, (T + 31) / 32);
     // key splits per work-group (LDS: two rounds of S tiles, and the merge); S depends on head_dim only, so a
@@ -1829,12 +1980,13 @@ void launch_prefill_attn(const PrefillAttn& a, int T, hipStream_t s) {
 }
 
 void launch_prefill_gelu(const float* gu, int F, int H, XBlock* xq, int xstride, int T, hipStream_t s, uint16_t* x16,
-                         int x16stride) {
+                         int x16stride, int q8k) {
+  if (q8k && (H % 8 || F % 256)) throw std::runtime_error("prefill_gelu: Q8_K output needs H % 8 == 0, F % 256 == 0");
   if (F % 32 || H <= 0 || F % H) throw std::runtime_error("prefill_gelu: shape");
   if (x16 && H % 8) throw std::runtime_error("prefill_gelu: f16 output needs H % 8 == 0");
-  if (H % 8 == 0 && (x16 || !getenv("LLMI_PREFILL_GELU_V1"))) {
+  if (H % 8 == 0 && (x16 || q8k || !getenv("LLMI_PREFILL_GELU_V1"))) {
     hipLaunchKernelGGL(prefill_gelu8_kernel, dim3((F / 8 + 255) / 256, T), dim3(256), 0, s, gu, F, H, xq, xstride, x16,
-                       x16stride);
+                       x16stride, q8k);
     LLMI_HIP(hipGetLastError());
     return;
   }

@@ -555,7 +555,7 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
     // layers: the f16 GEMM
     auto q40 = [](const DevWeight& w) { return w.type == T_Q4_0 || w.type == T_Q8_0; };
     auto gemm_ok = [&](const DevWeight& w) {
-      return q40(w) ? prefill_gemm_supported(w) : prefill_gemm16_supported(w);
+      return prefill_gemm_supported(w) || (!q40(w) && getenv("LLMI_PREFILL_F16") && prefill_gemm16_supported(w));
     };
     for (const auto& l : L_) {
       bool ok = l.fused && (l.hd == 64 || l.hd == 128 || l.hd == 256) && gemm_ok(l.o.w) && gemm_ok(l.gate_up[0].w) &&
@@ -563,15 +563,16 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
       for (const auto& part : l.qkv) ok = ok && gemm_ok(part.w);
       bool kq = !q40(l.o.w) || !q40(l.gate_up[0].w) || !q40(l.down.w);
       for (const auto& part : l.qkv) kq = kq || !q40(part.w);
-      if (ok && kq)  // f16 path: GELU group must allow the 8-unit f16 writes
-        ok = layer_gemv_gelu_group(l.gate_up[0].w.cols, l.gate_up[0].w.type) % 8 == 0;
+      if (ok && kq)  // 8-unit GELU writes; Q8_K blocks: whole super-blocks (a head of 256, 256-aligned rank slices)
+        ok = layer_gemv_gelu_group(l.gate_up[0].w.cols, l.gate_up[0].w.type) % 8 == 0 &&
+             (getenv("LLMI_PREFILL_F16") ||
+              (l.hd == 256 && hp_.n_embd % 256 == 0 && hp_.n_ff % 256 == 0 && (!tp_ || f_sh_ % 256 == 0)));
       pf = pf && ok;
       pf_kq_ = pf_kq_ || kq;
     }
-    // K-quant layers: the batched prefill (f16 path) is opt-in (LLMI_PREFILL_KQ=1) -- its f16 activations
-    // are further from the reference's Q8_K arithmetic than the fast-mode budget;
-    // the default is the decode token loop
-    if (pf_kq_ && !getenv("LLMI_PREFILL_KQ")) pf = false;
+    // K-quant layers: the int8 GEMM on Q8_K activation blocks (the decode's quantization); the f16 path
+    // (LLMI_PREFILL_F16=1) is opt-in -- its f16 activations are further from the reference's Q8_K arithmetic
+    // than the fast-mode budget
     const int grp = nkv_ > 0 ? nh_ / nkv_ : 0;
     prefill_ok_ = pf && (grp == 1 || grp == 2 || grp == 4);
     // attention block (qkv + attention + o in one launch): the fused fast
@@ -835,10 +836,12 @@ void Session::prefill(const int32_t* tokens, int n, int pos) {
   // f16 MFMA GEMM (v6, LLMI_PREFILL_F16=1: not faster yet -- activation tile re-reads bound it -- and further from
   // the reference's Q8_0 arithmetic)
   const int G = nh_ / std::max(nkv_, 1);
-  const bool f16 = (pf_kq_ || (getenv("LLMI_PREFILL_F16") && L_[0].o.w.type == T_Q4_0)) && !getenv("LLMI_PREFILL_ATTN_V1") &&
-                   (G == 1 || G == 2 || G == 4) &&
+  // K-quant (kq) layers: Q8_K activation blocks from the same producers (the decode's quantization) and the int8
+  // GEMM's K-quant variant, or the opt-in f16 path
+  const bool f16 = getenv("LLMI_PREFILL_F16") && (pf_kq_ || L_[0].o.w.type == T_Q4_0) &&
+                   !getenv("LLMI_PREFILL_ATTN_V1") && (G == 1 || G == 2 || G == 4) &&
                    layer_gemv_gelu_group(L_[0].gate_up[0].w.cols, L_[0].gate_up[0].w.type) % 8 == 0;
-  if (pf_kq_ && !f16) throw status_error(LLMI_E_ARG, "prefill: K-quant layers need the f16 prefill path");
+  const int q8k = pf_kq_ && !f16 ? 1 : 0;
   auto gemm = [&](const DevWeight& w, float* out, int ostride) {
     if (f16) launch_prefill_gemm16(w, pf_x16_, X16, T_cur_, out, ostride, s);
     else launch_prefill_gemm(w, pf_xq_, XS, T_cur_, out, ostride, s);
@@ -871,6 +874,7 @@ void Session::prefill(const int32_t* tokens, int n, int pos) {
     en.eps = hp_.eps;
     en.x16 = f16 ? pf_x16_ : nullptr;
     en.x16stride = X16;
+    en.q8k = q8k;
     launch_prefill_norm(en, T, s);
     for (int l = 0; l < hp_.n_layer; l++) {
       const LayerDev& Ld = L_[l];
@@ -913,6 +917,7 @@ void Session::prefill(const int32_t* tokens, int n, int pos) {
       at.xstride = XS;
       at.x16 = f16 ? pf_x16_ + (size_t)hr * nh_ * hd : nullptr;
       at.x16stride = X16;
+      at.q8k = q8k;
       launch_prefill_attn(at, T, s);
       if (!tp_rep_attn_) xgather(nh_ * hd);
       tap("pf_q", l, pf_q_, (size_t)T * nh_ * hd * 2, s);
@@ -933,6 +938,7 @@ void Session::prefill(const int32_t* tokens, int n, int pos) {
       rn.eps = hp_.eps;
       rn.x16 = f16 ? pf_x16_ : nullptr;
       rn.x16stride = X16;
+      rn.q8k = q8k;
       launch_prefill_norm(rn, T, s);
       tap("pf_resid_attn", l, pf_resid_, (size_t)T * E * 4, s);
       xtap("pf_x_gate_up", l);
@@ -940,7 +946,7 @@ void Session::prefill(const int32_t* tokens, int n, int pos) {
       gemm(Ld.gate_up[0].w, pf_out_, 2 * FL);
       tap("pf_gate_up", l, pf_out_, (size_t)T * 2 * F * 4, s);
       launch_prefill_gelu(pf_out_, FL, layer_gemv_gelu_group(Ld.gate_up[0].w.cols, Ld.gate_up[0].w.type),
-                          pf_xq_ + (size_t)r * (FL / 32), XS, T, s, f16 ? pf_x16_ + (size_t)r * FL : nullptr, X16);
+                          pf_xq_ + (size_t)r * (FL / 32), XS, T, s, f16 ? pf_x16_ + (size_t)r * FL : nullptr, X16, q8k);
       xgather(FL);
       xtap("pf_x_down", l);
       gemm(Ld.down.w, pf_out_ + (size_t)r * e_sh_, E);

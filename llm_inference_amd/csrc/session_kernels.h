@@ -92,11 +92,15 @@ struct PrefillNorm {  // per token: embedding (table != null) or residual + norm
   double eps = 0;
   uint16_t* x16 = nullptr;        // non-null: x as f16 rows [T][x16stride] instead of Q8_0 blocks (GEMM v6)
   int x16stride = 0;
+  int q8k = 0;                    // 1: Q8_K quants in the blocks (super-block d, block sums; n % 256 == 0)
 };
 struct PrefillGemm {
   const uint4* qs = nullptr;
   const uint16_t* wd = nullptr;
   int rows = 0, nb = 0, slab = 0, w8 = 0;  // w8: Q8_0 weights (qs [rows][nb][32 B])
+  int kq = 0;                              // 1 / 2: Q4_K / Q6_K weights in the kq layout (x: Q8_K blocks)
+  const uint32_t* kdd = nullptr;
+  const uint2* kqh = nullptr;
   const XBlock* x = nullptr;
   int xstride = 0, T = 0;
   float* out = nullptr;
@@ -131,6 +135,7 @@ struct PrefillAttn {
   int xstride = 0;
   uint16_t* x16 = nullptr;  // non-null: the heads' outputs as f16 rows [T][x16stride] (GEMM v6)
   int x16stride = 0;
+  int q8k = 0;              // 1: Q8_K quants (one super-block per head: head_dim 256)
 };
 void launch_prefill_norm(const PrefillNorm& a, int T, hipStream_t s);
 bool prefill_gemm_supported(const DevWeight& w);
@@ -142,7 +147,7 @@ void launch_prefill_gemm16(const DevWeight& w, const uint16_t* x, int xstride, i
 void launch_prefill_qk(const PrefillQK& a, int T, hipStream_t s);
 void launch_prefill_attn(const PrefillAttn& a, int T, hipStream_t s);
 void launch_prefill_gelu(const float* gu, int F, int H, XBlock* xq, int xstride, int T, hipStream_t s,
-                         uint16_t* x16 = nullptr, int x16stride = 0);
+                         uint16_t* x16 = nullptr, int x16stride = 0, int q8k = 0);
 
 // the weight layout the launch-table entry for (w's shape, role) reads
 int layer_gemv_slab(const DevWeight& w, int role);

@@ -69,6 +69,20 @@ def xblocks_to_q8_0(words: np.ndarray) -> np.ndarray:
     return out.reshape(-1)
 
 
+def xblocks_q8k_to_f32(words: np.ndarray) -> np.ndarray:
+    """Device XBlock rows holding Q8_K quants (q8k_block_quad: d = the super-block's f32 d, nsum8 = the
+    block's sum of q) -> x' = d q in f32; the reference's quantize_row_q8_k (ops.cpp:142-178) of x' gives back
+    the same quants (its max element is d * (+-127)), so mat_vec_mul(w, x') is the reference's row dot on
+    these blocks (to one ulp of d)."""
+    w = np.ascontiguousarray(words, np.uint32).reshape(-1, 12)
+    q = w[:, :8].copy().view(np.int8).reshape(-1, 32)
+    d = w[:, 8].copy().view(np.float32)
+    assert np.array_equal(w[:, 9].view(np.int32), q.astype(np.int32).sum(1)), "XBlock nsum8 != sum(q)"
+    assert np.array_equal(d.reshape(-1, 8), np.repeat(d.reshape(-1, 8)[:, :1], 8, 1)), "Q8_K d differs in a super-block"
+    assert np.abs(q.reshape(-1, 256)).max(1).min() >= 127 or not d.any(), "Q8_K super-block without a +-127 quant"
+    return (d[:, None] * q.astype(np.float32)).astype(np.float32).reshape(-1)
+
+
 def rel_err(got, ref):
     return float(np.abs(np.asarray(got, np.float64) - ref).max() / max(float(np.abs(ref).max()), 1e-30))
 
@@ -238,22 +252,29 @@ class OpChecker:
         f16_in = row_bytes == 64 * xs
         if f16_in:
             return self._prefill_f16(D, T_tok, H)
+        kq_types = (TT.Q4_K, TT.Q6_K)
         for l in range(c.n_layer):
-            for proj, w, ncols in (("qkv", self.w.qkv(l), E),
-                                   ("o", self.w.raw(f"blk.{l}.attn_output.weight"), c.n_head * c.head_dim),
-                                   ("gate_up", None, E),
-                                   ("down", self.w.raw(f"blk.{l}.ffn_down.weight"), F)):
+            for proj, names, ncols in (("qkv", [f"blk.{l}.attn_{p}.weight" for p in "qkv"], E),
+                                       ("o", [f"blk.{l}.attn_output.weight"], c.n_head * c.head_dim),
+                                       ("gate_up", None, E),
+                                       ("down", [f"blk.{l}.ffn_down.weight"], F)):
                 xs = np.frombuffer(D[(f"pf_x_{proj}", l)][-1], np.uint32).reshape(T_tok, -1, 12)
                 out = f32(D[(f"pf_{proj}", l)][-1]).reshape(T_tok, -1)
+                ws = [self.w.raw(n) for n in (names or [f"blk.{l}.ffn_gate.weight", f"blk.{l}.ffn_up.weight"])]
+                kq = ws[0][1] in kq_types  # Q8_K activation blocks (K-quant layers), else Q8_0
                 for t in range(T_tok):
-                    xq = xblocks_to_q8_0(xs[t, : ncols // 32])
+                    if kq:
+                        xf = xblocks_q8k_to_f32(xs[t, : ncols // 32])
+                        dot = lambda w: self.gemv(w, xf)  # noqa: E731
+                    else:
+                        xq = xblocks_to_q8_0(xs[t, : ncols // 32])
+                        dot = lambda w: self.gemv_q8(w, xq)  # noqa: E731
                     if proj == "gate_up":
-                        g = self.gemv_q8(self.w.raw(f"blk.{l}.ffn_gate.weight"), xq)
-                        u = self.gemv_q8(self.w.raw(f"blk.{l}.ffn_up.weight"), xq)
+                        g, u = dot(ws[0]), dot(ws[1])
                         ref = np.concatenate([np.concatenate([g[k * H:(k + 1) * H], u[k * H:(k + 1) * H]])
                                               for k in range(F // H)])
                     else:
-                        ref = self.gemv_q8(w, xq)
+                        ref = np.concatenate([dot(w) for w in ws])
                     self.note(f"prefill_gemm_{proj}", rel_err(out[t, : ref.size], ref), GEMV_RTOL)
 
     def _prefill_f16(self, D, T_tok, H):

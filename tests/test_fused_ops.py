@@ -94,9 +94,22 @@ def test_ops_prefill_f16_gemm(oracle, monkeypatch, cfg_name):
 
 def test_ops_prefill_kquant_gemm(oracle, monkeypatch):
     """Gemma-3 4B Q4_K_M layer shapes (q, k, o, gate, up Q4_K; v, down Q6_K in the kq layout): the opt-in
-    batched prefill (LLMI_PREFILL_KQ=1) runs the f16 path, GEMM v6 dequantizing the K-quant sub-blocks to f16 -- every output row against
-    the reference's dequantize_row weights times the device's own f16 inputs in float64."""
+    f16 batched prefill (LLMI_PREFILL_F16=1), GEMM v6 dequantizing the K-quant sub-blocks to f16 -- every output
+    row against the reference's dequantize_row weights times the device's own f16 inputs in float64."""
     from llm_inference_amd.gguf import TensorType as TT
-    chk = _run(oracle, "mini-4b", 29, 24, -1, 64, monkeypatch, {"LLMI_PREFILL_KQ": "1"}, wtype=TT.Q4_K,
+    chk = _run(oracle, "mini-4b", 29, 24, -1, 64, monkeypatch, {"LLMI_PREFILL_F16": "1"}, wtype=TT.Q4_K,
                wtypes={"v": TT.Q6_K, "down": TT.Q6_K})
     assert "prefill_gemm16_qkv" in chk.report and "prefill_gemm16_down" in chk.report
+
+
+@pytest.mark.parametrize("vtype", ["q6_k", "q4_k"])
+def test_ops_prefill_kquant_int8(oracle, vtype):
+    """The default K-quant batched prefill: Q8_K activation blocks from the norm / attention / GELU producers
+    (the reference's quantize_row_q8_k, checked block by block: one f32 d per super-block, a +-127 quant in
+    each, block sums) and the int8 GEMM's Q4_K / Q6_K variant (i8 MFMA per sub-block, the d sc / dmin m
+    scale products on f32 MFMAs) -- every output row against the reference's mat_vec_mul_q4_k / _q6_k of
+    those blocks (GEMV tolerance); then decode steps op by op."""
+    from llm_inference_amd.gguf import TensorType as TT
+    vt = TT.Q6_K if vtype == "q6_k" else TT.Q4_K
+    chk = _run(oracle, "mini-4b", 30, 20, -1, 64, wtype=TT.Q4_K, wtypes={"v": vt, "down": vt})
+    assert "prefill_gemm_qkv" in chk.report and "prefill_gemm_down" in chk.report

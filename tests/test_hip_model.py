@@ -189,6 +189,7 @@ def test_q8_0_fused_matches_unfused(oracle, monkeypatch):
     from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
     cfg = CONFIGS["mini-1b"]
     g = build_gemma3_gguf(cfg, seed=12, wtype=TT.Q8_0)
+    monkeypatch.setenv("LLMI_NO_PREFILL", "1")  # the decode launches on both sides (prefill: tests/test_prefill.py)
     prompt = np.random.default_rng(5).integers(4, cfg.vocab, 9).astype(np.int32)
     fused = Model(g, exact=False, max_ctx=64)
     lf = fused.forward(prompt, 0)
@@ -249,6 +250,7 @@ def test_kquant_fused_matches_unfused(oracle, monkeypatch, vtype):
     cfg = CONFIGS["mini-4b"]
     vt = TT.Q6_K if vtype == "q6_k" else TT.Q4_K
     g = build_gemma3_gguf(cfg, seed=17, wtype=TT.Q4_K, wtypes={"v": vt, "down": vt})
+    monkeypatch.setenv("LLMI_NO_PREFILL", "1")  # the decode launches on both sides (prefill: tests/test_prefill.py)
     prompt = np.random.default_rng(6).integers(4, cfg.vocab, 9).astype(np.int32)
     fused = Model(g, exact=False, max_ctx=64)
     lf = fused.forward(prompt, 0)
