@@ -148,6 +148,11 @@ const LayerCfg kLayerCfgs[] = {
     LLMI_LCFGP(80, ROLE_GELU, 8, 10, 10, 4, 1, 7),            // 4B  20480 rows, H 40 -> 256 WGs (PE7: 8.4 -> 7.8 us)
     LLMI_LCFG(120, ROLE_GELU, 8, 8, 8, 8, true, false, 0),     // 12B 30720 rows, H 32 -> 480 WGs
     LLMI_LCFG(168, ROLE_GELU, 8, 8, 4, 11, true, false, 1),    // 27B 43008 rows, H 32 -> 672 WGs
+    // PLAIN down: the GELU launch (32 units per work-group) wrote the Q8_0 blocks (LayerGemv::hq), so the down
+    // launch copies 24-42 KB of blocks instead of quantizing the whole f32 hid in every work-group
+    // (scripts/gemv_sweep 27b.down: plain R1 NW8 P6 15.0 us vs quant 19.5 us)
+    LLMI_LCFG(216, ROLE_PLAIN, 1, 4, 4, 3, false, true, 0),    // 1B down     1152 rows -> 288 WGs
+    LLMI_LCFG(672, ROLE_PLAIN, 1, 8, 6, 4, true, true, 0),     // 27B down    5376 rows -> 672 WGs
     // QUANT: f32 activation quantized into LDS (down projection)
     LLMI_LCFG(216, ROLE_QUANT, 1, 4, 4, 4, false, true, 0),    // 1B down     1152 rows -> 288 WGs (6.5 -> 5.0 us)
     LLMI_LCFGP(320, ROLE_QUANT, 1, 10, 5, 2, 0, 3),           // 4B down     2560 rows -> 256 WGs (PE3: 5.8 -> 5.4 us)
@@ -159,6 +164,7 @@ const LayerCfg kLayerCfgs[] = {
     LLMI_LCFG8(32, ROLE_PLAIN, 1, 4, 1, 1, true),     // 1B o        1152 rows -> 288 WGs
     LLMI_LCFG8(36, ROLE_GELU, 8, 8, 9, 3, false),     // 1B gate_up  13824 rows, H 32 -> 216 WGs
     LLMI_LCFG8(216, ROLE_QUANT, 1, 4, 7, 4, true),    // 1B down     1152 rows -> 288 WGs
+    LLMI_LCFG8(216, ROLE_PLAIN, 1, 4, 7, 3, true),    // 1B down from the GELU launch's blocks
     // K-quant weights in the kq layout (Gemma-3 4B Q4_K_M, BASELINE configs[3]): the Q4_0 4B
     // geometry (a 32-element sub-block per 16-B unit, as a Q4_0 block), row-major
     LLMI_LCFGK(80, ROLE_PLAIN, 4, 4, 5, 1, true, 0, 0),      // 4B qkv l0   4096 rows -> 256 WGs

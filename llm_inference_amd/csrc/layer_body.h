@@ -270,6 +270,18 @@ __device__ unsigned long long* g_layer_trace = nullptr;
   } while (0)
 #endif
 
+// GELU(gate) * up of a work-group's H hidden units -> hid; with H = 32 (one Q8_0 block per work-group) and
+// a.hq also the block (quantize_row_q8_0, ops.cpp:116-139, of the same f32 values, 32 lanes), so the down
+// launch reads blocks (PLAIN) instead of quantizing the whole hid in every work-group (QUANT)
+template <int H>
+__device__ __forceinline__ void gelu_out(const LayerGemv& a, int bid, const float* s_rows, int t) {
+  if (t >= H) return;
+  const float g = gelu_mul1(s_rows[t], s_rows[H + t]);
+  a.hid[bid * H + t] = g;
+  if constexpr (H == 32)
+    if (a.hq) q8_block_store(g, true, a.hq + bid, t);
+}
+
 enum { SYNC_SIG = 1, SYNC_WAIT = 2 };
 enum { ROLE_PLAIN = LAYER_PLAIN, ROLE_PRO = LAYER_PRO, ROLE_GELU = LAYER_GELU, ROLE_QUANT = LAYER_QUANT,
        // PRO / GELU with E extra HELPER waves that do the prologue while the
@@ -724,7 +736,7 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
       }
       __syncthreads();
       constexpr int H = NW * R / 2;  // hidden units of this work-group
-      if (t < H) a.hid[bid * H + t] = gelu_mul1(s_rows[t], s_rows[H + t]);
+      gelu_out<H>(a, bid, s_rows, t);
     } else if (!helper) {
       if constexpr (R <= 2) {
         if (lane == 0)
@@ -765,7 +777,7 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
     }
     __syncthreads();
     constexpr int H = NW * R / 2;  // hidden units of this work-group
-    if (t < H) a.hid[bid * H + t] = gelu_mul1(s_rows[t], s_rows[H + t]);
+    gelu_out<H>(a, bid, s_rows, t);
   } else {
 #pragma unroll
     for (int k = 0; k < R; k++) {

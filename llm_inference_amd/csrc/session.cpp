@@ -458,6 +458,7 @@ void Session::alloc_buffers() {
   o_out_ = dalloc<float>(E);
   gu_ = dalloc<float>(2 * (size_t)F);
   hid_ = dalloc<float>(F);
+  hq_ = dalloc<XBlock>(F / 32 + 1);
   d_out_ = dalloc<float>(E);
   logits_ = dalloc<float>((size_t)tp_size_ * v_sh_);
   act_.q8.xb = dalloc<XBlock>(maxcols / 32 + 1);
@@ -683,6 +684,16 @@ void Session::gemv_parts(const std::vector<GemvPart>& parts, const float* x, int
 }
 
 // One decode token.  Reads *d_token_/*d_pos_, ends with the token feedback.
+// the down projection as a PLAIN launch on the GELU launch's Q8_0 blocks: one device (a rank's hid slice is
+// all-gathered as f32), 32 hidden units per GELU work-group, a PLAIN table entry for the shape
+// (LLMI_DOWN_QUANT=1 keeps the QUANT launch, A/B)
+bool Session::down_plain(const LayerDev& Ld) const {
+  static const bool off = getenv("LLMI_DOWN_QUANT") != nullptr;
+  const DevWeight& g = Ld.gate_up[0].w;
+  return !off && !tp_ && (Ld.down.w.type == T_Q4_0 || Ld.down.w.type == T_Q8_0) &&
+         layer_gemv_gelu_group(g.cols, g.type) == 32 && layer_gemv_supported(Ld.down.w, LAYER_PLAIN);
+}
+
 void Session::record_step(hipStream_t s, bool gen) {
   kernels_per_token_ = 0;
   const int E = hp_.n_embd;
@@ -1113,6 +1124,8 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
     gg.w_next = Ld.ffn_norm;
     gg.eps = hp_.eps;
     gg.hid = hid_ + (size_t)tp_rank_ * f_sh_;
+    const bool dplain = down_plain(Ld);
+    if (dplain) gg.hq = hq_;
     gg.epoch = epoch;  // advances the attention block's granule tag of this layer
     if (dump_ || trace_fn_) gg.xn_out = xn_;
     for (int r = 0; r < dup("gate_up"); r++) launch_layer_gemv(Ld.gate_up[0].w, gg, LAYER_GELU, s);
@@ -1126,8 +1139,9 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
     if (tp_) coll_->all_gather(hid_, (size_t)f_sh_ * sizeof(float), s);
     LayerGemv gd;
     gd.y = hid_;  // QUANT: GELU output quantized per block in the down launch
+    gd.xg = hq_;  // PLAIN: the blocks the GELU launch wrote
     gd.out = d_out_ + (size_t)tp_rank_ * e_sh_;
-    for (int r = 0; r < dup("down"); r++) launch_layer_gemv(Ld.down.w, gd, LAYER_QUANT, s);
+    for (int r = 0; r < dup("down"); r++) launch_layer_gemv(Ld.down.w, gd, dplain ? LAYER_PLAIN : LAYER_QUANT, s);
     tap("down", l, d_out_, (size_t)E * 4, s);
     if (tp_) coll_->all_gather(d_out_, (size_t)e_sh_ * sizeof(float), s);
     dump("ffn_out-" + L, d_out_, E, s);
@@ -1567,14 +1581,17 @@ void Session::time_kernel(int which, int reps, double* us, double* bytes) {
       gu.w_next = Ld.ffn_norm;
       gu.out = nullptr;
       gu.hid = hid_;
+      if (down_plain(Ld)) gu.hq = hq_;
       items.push_back({[this, &Ld, gu]() { launch_layer_gemv(Ld.gate_up[0].w, gu, LAYER_GELU, stream_); },
                        (double)Ld.gate_up[0].w.bytes});
     }
     if (which == 4 || which == 5) {
       LayerGemv d;
       d.y = hid_;
+      d.xg = hq_;
       d.out = d_out_;
-      items.push_back({[this, &Ld, d]() { launch_layer_gemv(Ld.down.w, d, LAYER_QUANT, stream_); },
+      const int drole = down_plain(Ld) ? LAYER_PLAIN : LAYER_QUANT;
+      items.push_back({[this, &Ld, d, drole]() { launch_layer_gemv(Ld.down.w, d, drole, stream_); },
                        (double)Ld.down.w.bytes});
     }
   }

@@ -84,6 +84,7 @@ class Session {
   void build_rope_tables();
   // gen: the decode loop's step (token id only: screened logits when screen_)
   void record_step(hipStream_t s, bool gen = false);
+  bool down_plain(const LayerDev& Ld) const;
   void record_logits(hipStream_t s, bool gen = false);  // xn_ / act_.x16 -> logits, argmax key, token feedback
   void prefill(const int32_t* tokens, int n, int pos);  // batched (k_prefill.hip)
   void gather_cols(void* buf, size_t pitch_b, size_t slice_b, int T, hipStream_t s);
@@ -133,6 +134,7 @@ class Session {
   int* blk_err_ = nullptr;       // set by a bounded wait that gave up
   unsigned long long* blk_trace_ = nullptr;  // LLMI_BLOCK_TRACE (development)
   int blk_trace_layer_ = -1;
+  XBlock* hq_ = nullptr;         // the GELU launch's Q8_0 blocks of hid (down as a PLAIN launch, 32-unit groups)
   XBlock* blk_xo_ = nullptr;     // attention output Q8_0 blocks (layer 0's qkv still reads act_.q8 in the launch)
   void check_device_error();
   bool ex_gemv_ = false, ex_norm_ = false, ex_attn_ = false, ex_logits_ = false;  // per kernel family

@@ -61,6 +61,7 @@ struct LayerGemv {
   double eps = 0;
   float* out = nullptr;     // PLAIN / PRO / QUANT: [rows]
   float* hid = nullptr;     // GELU: [rows / 2] = GELU(gate) * up
+  XBlock* hq = nullptr;     // GELU with 32 units per work-group: also their Q8_0 block (the down launch's x)
   unsigned* epoch = nullptr;  // optional: work-group 0 advances *epoch (the attention block's granule tag)
   const uint32_t* kdd = nullptr;  // kq weights (Q4_K / Q6_K): super-block d words, Q6_K high bits
   const uint2* kqh = nullptr;
