@@ -55,7 +55,7 @@ def test_model_test_gguf(oracle, golden_models, exact):
     check(l1, golden_models["model_test__l1"], ideal.forward([1], 0), exact)
     if exact:
         for i, v in [(0, 2.9909527), (1, -0.216222), (8, 1.6922607), (9, -2.588623)]:  # model_test.cpp:426-432
-            assert abs(l1[i] - v) < 0.003 + 2e-3
+            assert abs(l1[i] - v) < 0.003  # ModelTest's own tolerance (model_test.cpp:422)
     nt = int(np.argmax(golden_models["model_test__l1"]))
     assert m.last_argmax == nt
     l2 = m.forward([nt], 1)
