@@ -180,3 +180,52 @@ def test_mini4b_configs2_length(oracle):
     for i in range(64):
         o2.append(int(np.argmax(om2.forward([o2[-1]], 512 + i))))
     assert ex_run == o2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("quant", ["q4_k_m", "q8_0"])
+def test_full_size_quant_batched_prefill(oracle, monkeypatch, quant):
+    """BASELINE configs[3] at full depth and vocabulary -- Gemma-3 4B Q4_K_M (34 layers, Q4_K projections,
+    Q6_K v / down, 262,208 logits rows; batched prefill on Q8_K blocks, the int8 GEMM's K-quant variant, fused
+    kq decode launches) and 1B Q8_0 (26 layers; GEMM v5 on the Q8_0 weight blocks, W8 decode launches) --
+    against the oracle teacher-forced on the device's ids: each step's oracle argmax equals the device's
+    wherever the oracle's top-2 margin exceeds 4x the prompt step's measured logit error; the token loop
+    (LLMI_NO_PREFILL=1) gives the same first id."""
+    from llm_inference_amd.gguf import TensorType as TT
+    from llm_inference_amd.model import Model
+    from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
+    if quant == "q4_k_m":
+        cfg = CONFIGS["gemma-3-4b"]
+        g = build_gemma3_gguf(cfg, seed=77, centered=True, wtype=TT.Q4_K, wtypes={"v": TT.Q6_K, "down": TT.Q6_K})
+    else:
+        cfg = CONFIGS["gemma-3-1b"]
+        g = build_gemma3_gguf(cfg, seed=78, centered=True, wtype=TT.Q8_0)
+    prompt = np.concatenate([[2], np.random.default_rng(77).integers(4, cfg.vocab, 23)]).astype(np.int32)
+    n = 4
+    m = Model(g, max_ctx=64)
+    assert m.info.batched_prefill == 1
+    lg = m.forward(prompt, 0)
+    run = [int(np.argmax(lg))] + m.generate(int(np.argmax(lg)), len(prompt), n).tolist()
+    om = oracle.model(g, n_threads=16, max_ctx=64)
+    ol = [om.forward(prompt, 0)]
+    for i in range(n):
+        ol.append(om.forward([run[i]], len(prompt) + i))
+    ol = np.stack(ol)
+    err0 = float(np.abs(lg - ol[0]).max())
+    srt = np.sort(ol, 1)
+    margin = srt[:, -1] - srt[:, -2]
+    decided = margin > 4.0 * err0
+    agree = ol.argmax(1) == np.array(run)
+    print(f"{quant} full size: prefill-step |logits - oracle| {err0:.3g} (max |logit| "
+          f"{float(np.abs(ol[0]).max()):.3g}); margins {np.round(margin, 3).tolist()}; "
+          f"decided {int(decided.sum())}/{n + 1}, agreement {int(agree.sum())}/{n + 1}")
+    assert agree[decided].all()
+    assert err0 < 0.05 * float(np.abs(ol[0]).max())
+    m.close()
+    monkeypatch.setenv("LLMI_NO_PREFILL", "1")
+    ml = Model(g, max_ctx=64)
+    ll = ml.forward(prompt, 0)
+    print(f"{quant} full size: |batched prefill - token loop| {float(np.abs(ll - lg).max()):.3g}")
+    if margin[0] > 4.0 * err0:
+        assert int(np.argmax(ll)) == run[0]
+    ml.close()
