@@ -386,7 +386,7 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, const QKVArgs
   const int n_keys = pos + 1;
   const bool own_new = FUSED && (pos / TK) % NS == c;
   const int hkc = hkv / KVD;  // cache head
-  static_assert(KVD == 1 || !FUSED, "virtual kv heads: the KV append runs in its own launch");
+  static_assert(KVD == 1 || !FUSED || BLK, "virtual kv heads: the KV append runs in its own launch (or the block)");
   const uint4* kb = reinterpret_cast<const uint4*>(a.k_cache + (size_t)hkc * a.max_ctx * HD);
   const uint4* vb = reinterpret_cast<const uint4*>(a.v_cache + (size_t)hkc * a.max_ctx * HD);
   uint4 kr[NLD], vr[NLD];
@@ -417,9 +417,9 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, const QKVArgs
   float vrow[DPL];
   if (FUSED && !BLK) {
     if (w < G) row_load<HD>(rq, qa.qkv + (size_t)(hkv * G + w) * HD, qa.q_norm_w, cs);
-    if (w == (G & 3)) row_load<HD>(rk, qa.qkv + qa.k_off + (size_t)hkv * HD, qa.k_norm_w, cs);
+    if (w == (G & 3)) row_load<HD>(rk, qa.qkv + qa.k_off + (size_t)hkc * HD, qa.k_norm_w, cs);
     if (w == ((G + 1) & 3)) {
-      ld_vec<DPL>(vrow, qa.qkv + qa.v_off + (size_t)hkv * HD + min(lane, HD / DPL - 1) * DPL);
+      ld_vec<DPL>(vrow, qa.qkv + qa.v_off + (size_t)hkc * HD + min(lane, HD / DPL - 1) * DPL);
     }
   }
   int tile = c;
@@ -427,10 +427,10 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, const QKVArgs
   if constexpr (BLK) {  // the history tile is in flight; now this token's rows, from their granules
     const uint32_t tag = btag;
     if (w < G) row_load_gr<HD>(rq, bs.g_qkv + (size_t)(hkv * G + w) * HD, qa.q_norm_w, cs, tag, bs.err);
-    if (w == (G & 3)) row_load_gr<HD>(rk, bs.g_qkv + qa.k_off + (size_t)hkv * HD, qa.k_norm_w, cs, tag, bs.err);
+    if (w == (G & 3)) row_load_gr<HD>(rk, bs.g_qkv + qa.k_off + (size_t)hkc * HD, qa.k_norm_w, cs, tag, bs.err);
     if (w == ((G + 1) & 3)) {
       uint32_t u[DPL];
-      ld_granules<DPL>(u, bs.g_qkv + qa.v_off + (size_t)hkv * HD, min(lane, HD / DPL - 1) * DPL, tag, bs.err);
+      ld_granules<DPL>(u, bs.g_qkv + qa.v_off + (size_t)hkc * HD, min(lane, HD / DPL - 1) * DPL, tag, bs.err);
 #pragma unroll
       for (int d = 0; d < DPL; d++) vrow[d] = __uint_as_float(u[d]);
     }
@@ -452,7 +452,7 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, const QKVArgs
       for (int d = 0; d < DPL; d++) {
         const uint16_t k16 = f2h_ggml(kn[d]);
         if (ok) s_new[0][lane * DPL + d] = k16;
-        if (ok && own_new) qa.k_cache[((size_t)hkv * a.max_ctx + pos) * HD + lane * DPL + d] = k16;
+        if (ok && own_new && hkv % KVD == 0) qa.k_cache[((size_t)hkc * a.max_ctx + pos) * HD + lane * DPL + d] = k16;
       }
     }
     if (w == ((G + 1) & 3)) {
@@ -460,7 +460,7 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, const QKVArgs
       for (int d = 0; d < DPL; d++) {
         const uint16_t v16 = f2h_ggml(vrow[d]);
         if (ok) s_new[FUSED ? 1 : 0][lane * DPL + d] = v16;
-        if (ok && own_new) qa.v_cache[((size_t)hkv * a.max_ctx + pos) * HD + lane * DPL + d] = v16;
+        if (ok && own_new && hkv % KVD == 0) qa.v_cache[((size_t)hkc * a.max_ctx + pos) * HD + lane * DPL + d] = v16;
       }
     }
   } else {
@@ -776,7 +776,7 @@ constexpr size_t block_attn_lds() {  // s_k + s_v (32-key tiles) + s_red
 // of that format (Q4_K_M: q|k Q4_K, v Q6_K), granules and outputs continuing
 // after the first weight's rows
 template <int HD, int G, int QR, int QP, int QE, int QROLE, int OR, int OP, int OE, int WTQ = 0, int WTQB = 0,
-          int WTO = 0>
+          int WTO = 0, int KVD = 1>
 __global__ __launch_bounds__(256) void attn_block_kernel(LayerGemv qg, LayerGemv og, AttnArgs aa, QKVArgs qa,
                                                         BlockSync bs, int nq, LayerGemv qgb, int nqa) {
   extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
@@ -800,7 +800,8 @@ __global__ __launch_bounds__(256) void attn_block_kernel(LayerGemv qg, LayerGemv
     uint16_t* s_k = reinterpret_cast<uint16_t*>(s_dyn);
     uint16_t* s_v = s_k + 32 * KS;
     float* s_red = reinterpret_cast<float*>(s_v + 32 * HD);
-    attn_split_body<HD, G, true, 32, true>(aa, qa, s_k, s_v, s_red, b % aa.n_head_kv, b / aa.n_head_kv, bs);
+    // KVD > 1: aa.n_head_kv counts virtual kv heads (G q heads each, KVD per cache head)
+    attn_split_body<HD, G, true, 32, true, KVD>(aa, qa, s_k, s_v, s_red, b % aa.n_head_kv, b / aa.n_head_kv, bs);
     return;
   }
   b -= na;
@@ -810,17 +811,18 @@ __global__ __launch_bounds__(256) void attn_block_kernel(LayerGemv qg, LayerGemv
 using BlockFn = void (*)(dim3, size_t, const LayerGemv&, const LayerGemv&, const AttnArgs&, const QKVArgs&,
                          const BlockSync&, int, const LayerGemv&, int, hipStream_t);
 
-template <int HD, int G, int QR, int QP, int QE, int QROLE, int OR, int OP, int OE, int WTQ, int WTQB, int WTO>
+template <int HD, int G, int QR, int QP, int QE, int QROLE, int OR, int OP, int OE, int WTQ, int WTQB, int WTO,
+          int KVD = 1>
 void block_launch(dim3 grid, size_t lds, const LayerGemv& qg, const LayerGemv& og, const AttnArgs& aa,
                   const QKVArgs& qa, const BlockSync& bs, int nq, const LayerGemv& qgb, int nqa, hipStream_t s) {
   KernelTiming& kt = kernel_timing();
   if (kt.start) {  // bench: events signalled by this dispatch itself (its duration as rocprofv3 reports it)
-    hipExtLaunchKernelGGL((attn_block_kernel<HD, G, QR, QP, QE, QROLE, OR, OP, OE, WTQ, WTQB, WTO>), grid, dim3(256),
+    hipExtLaunchKernelGGL((attn_block_kernel<HD, G, QR, QP, QE, QROLE, OR, OP, OE, WTQ, WTQB, WTO, KVD>), grid, dim3(256),
                           (uint32_t)lds, s, kt.start, kt.stop, 0u, qg, og, aa, qa, bs, nq, qgb, nqa);
     kt = KernelTiming{};
     return;
   }
-  hipLaunchKernelGGL((attn_block_kernel<HD, G, QR, QP, QE, QROLE, OR, OP, OE, WTQ, WTQB, WTO>), grid, dim3(256), lds, s,
+  hipLaunchKernelGGL((attn_block_kernel<HD, G, QR, QP, QE, QROLE, OR, OP, OE, WTQ, WTQB, WTO, KVD>), grid, dim3(256), lds, s,
                      qg, og, aa, qa, bs, nq, qgb, nqa);
 }
 
@@ -831,12 +833,19 @@ struct BlockCfg {
   BlockFn fn;
   const void* kern;  // the kernel (occupancy query)
   int wtq, wtqb, wto;  // weight formats (layer_body WT): qkv, second qkv weight (0: none), o
+  int kvd;             // virtual kv heads per cache head (attention work-groups of g / kvd q heads)
 };
 #define LLMI_BCFGW(NBQ, NBO, HD, G, QROLE, QR, QP, QE, OR, OP, OE, WTQ, WTQB, WTO)                          \
   {NBQ, NBO, HD, G, QROLE, QR, QP, QE, OR, OP, OE, block_attn_lds<HD, G>(),                                  \
    block_launch<HD, G, QR, QP, QE, QROLE, OR, OP, OE, WTQ, WTQB, WTO>,                                        \
    reinterpret_cast<const void*>(&attn_block_kernel<HD, G, QR, QP, QE, QROLE, OR, OP, OE, WTQ, WTQB, WTO>), WTQ, \
-   WTQB, WTO}
+   WTQB, WTO, 1}
+// GQA group GM split over KVD virtual kv heads (G = GM / KVD q heads per attention work-group)
+#define LLMI_BCFGV(NBQ, NBO, HD, GM, KVD, QROLE, QR, QP, QE, OR, OP, OE)                                         \
+  {NBQ, NBO, HD, GM, QROLE, QR, QP, QE, OR, OP, OE, block_attn_lds<HD, GM / KVD>(),                               \
+   block_launch<HD, GM / KVD, QR, QP, QE, QROLE, OR, OP, OE, 0, 0, 0, KVD>,                                       \
+   reinterpret_cast<const void*>(&attn_block_kernel<HD, GM / KVD, QR, QP, QE, QROLE, OR, OP, OE, 0, 0, 0, KVD>), 0, \
+   0, 0, KVD}
 #define LLMI_BCFG(NBQ, NBO, HD, G, QROLE, QR, QP, QE, OR, OP, OE) \
   LLMI_BCFGW(NBQ, NBO, HD, G, QROLE, QR, QP, QE, OR, OP, OE, 0, 0, 0)
 // qkv: 4 waves x QR rows per work-group (rows per work-group must divide
@@ -847,6 +856,9 @@ const BlockCfg kBlockCfgs[] = {
     // rows per wave (160 WGs), 902 with 2 (320 WGs))
     LLMI_BCFG(80, 64, 256, 2, ROLE_PRO, 4, 5, 10, 8, 8, 1),
     LLMI_BCFG(80, 64, 256, 2, ROLE_PLAIN, 4, 5, 1, 8, 8, 1),   // 4B layer 0
+    // 1B: GQA group 4 as two virtual kv heads of 2 (64 attention WGs, two merges of 2 heads)
+    LLMI_BCFGV(36, 32, 256, 4, 2, ROLE_PRO, 4, 3, 5, 4, 2, 1),
+    LLMI_BCFGV(36, 32, 256, 4, 2, ROLE_PLAIN, 4, 3, 1, 4, 2, 1),
     LLMI_BCFG(36, 32, 256, 4, ROLE_PRO, 4, 3, 5, 4, 2, 1),     // 1B:  qkv 1536 rows -> 96 WGs, o 1152 -> 72
     LLMI_BCFG(36, 32, 256, 4, ROLE_PLAIN, 4, 3, 1, 4, 2, 1),   // 1B layer 0
     // 4B Q4_K_M (kq weights): q|k Q4_K + v Q6_K, or all Q4_K; o Q4_K; the Q4_0 geometry
@@ -865,9 +877,10 @@ int wt_of_w(const DevWeight* w) {
 
 const BlockCfg* find_block_cfg(int nb_qkv, int nb_o, int hd, int g, int qrole, int wtq = 0, int wtqb = 0,
                                int wto = 0) {
+  static const bool no_kvd = getenv("LLMI_BLOCK_NO_KVD") != nullptr;  // A/B: whole GQA groups per work-group
   for (const auto& c : kBlockCfgs)
     if (c.nb_qkv == nb_qkv && c.nb_o == nb_o && c.hd == hd && c.g == g && c.qrole == qrole && c.wtq == wtq &&
-        c.wtqb == wtqb && c.wto == wto)
+        c.wtqb == wtqb && c.wto == wto && !(no_kvd && c.kvd > 1))
       return &c;
   return nullptr;
 }
@@ -901,7 +914,7 @@ static BlockGeom block_geom(const BlockCfg& c, const DevWeight& wqkv, const DevW
                             int n_head_kv, int qrole) {
   BlockGeom g;
   g.nq = (wqkv.rows + (wqkv_b ? wqkv_b->rows : 0) + 4 * c.QR - 1) / (4 * c.QR);
-  g.na = n_head_kv * ATTN_NSPLIT;
+  g.na = n_head_kv * c.kvd * ATTN_NSPLIT;
   g.no = (wo.rows + 4 * c.OR - 1) / (4 * c.OR);
   const size_t lds_q = (size_t)(wqkv.cols / 32) * sizeof(XBlock) + 16 + (qrole == ROLE_PRO ? (size_t)wqkv.cols * 4 : 0);
   const size_t lds_o = (size_t)(wo.cols / 32) * sizeof(XBlock) + 16;
@@ -982,7 +995,9 @@ void launch_attn_block(const DevWeight& wqkv, const DevWeight* wqkv_b, LayerGemv
   if (3 * nbo > c.OE * 256) throw std::runtime_error("attention block: o E");
   const BlockGeom bg = block_geom(c, wqkv, wqkv_b, wo, aa.n_head_kv, qrole);
   const int nqa = wqkv_b ? wqkv.rows / (4 * c.QR) : bg.nq;
-  c.fn(dim3(bg.nq + bg.na + bg.no), bg.lds, qg, og, aa, qa, bs, bg.nq, qgb, nqa, s);
+  AttnArgs av = aa;  // virtual kv heads: the attention role's head count
+  av.n_head_kv *= c.kvd;
+  c.fn(dim3(bg.nq + bg.na + bg.no), bg.lds, qg, og, av, qa, bs, bg.nq, qgb, nqa, s);
   LLMI_HIP(hipGetLastError());
 }
 
