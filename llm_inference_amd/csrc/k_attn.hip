@@ -775,6 +775,8 @@ constexpr size_t block_attn_lds() {  // s_k + s_v (32-key tiles) + s_red
 // Q6_K); WTQB != 0: the qkv rows from nqa work-groups on are a second weight
 // of that format (Q4_K_M: q|k Q4_K, v Q6_K), granules and outputs continuing
 // after the first weight's rows
+constexpr int WT_W8 = 3;  // Q8_0 weights in the block (layer_body W8), beside the kq formats WT_Q4_K / WT_Q6_K
+
 template <int HD, int G, int QR, int QP, int QE, int QROLE, int OR, int OP, int OE, int WTQ = 0, int WTQB = 0,
           int WTO = 0, int KVD = 1>
 __global__ __launch_bounds__(256) void attn_block_kernel(LayerGemv qg, LayerGemv og, AttnArgs aa, QKVArgs qa,
@@ -786,11 +788,11 @@ __global__ __launch_bounds__(256) void attn_block_kernel(LayerGemv qg, LayerGemv
       if (b >= nqa) {
         BlockSync bsb = bs;
         bsb.g_qkv += qg.rows;
-        layer_body<QR, 4, QP, QE, QROLE, false, true, SYNC_SIG, 0, false, WTQB>(qgb, b - nqa, s_dyn, bsb);
+        layer_body<QR, 4, QP, QE, QROLE, false, true, SYNC_SIG, 0, false, WTQB == WT_W8 ? 0 : WTQB>(qgb, b - nqa, s_dyn, bsb);
         return;
       }
     }
-    layer_body<QR, 4, QP, QE, QROLE, false, true, SYNC_SIG, 0, false, WTQ>(qg, b, s_dyn, bs);
+    layer_body<QR, 4, QP, QE, QROLE, false, true, SYNC_SIG, 0, WTQ == WT_W8, WTQ == WT_W8 ? 0 : WTQ>(qg, b, s_dyn, bs);
     return;
   }
   b -= nq;
@@ -805,7 +807,7 @@ __global__ __launch_bounds__(256) void attn_block_kernel(LayerGemv qg, LayerGemv
     return;
   }
   b -= na;
-  layer_body<OR, 4, OP, OE, ROLE_PLAIN, false, true, SYNC_WAIT, 0, false, WTO>(og, b, s_dyn, bs);
+  layer_body<OR, 4, OP, OE, ROLE_PLAIN, false, true, SYNC_WAIT, 0, WTO == WT_W8, WTO == WT_W8 ? 0 : WTO>(og, b, s_dyn, bs);
 }
 
 using BlockFn = void (*)(dim3, size_t, const LayerGemv&, const LayerGemv&, const AttnArgs&, const QKVArgs&,
@@ -840,12 +842,15 @@ struct BlockCfg {
    block_launch<HD, G, QR, QP, QE, QROLE, OR, OP, OE, WTQ, WTQB, WTO>,                                        \
    reinterpret_cast<const void*>(&attn_block_kernel<HD, G, QR, QP, QE, QROLE, OR, OP, OE, WTQ, WTQB, WTO>), WTQ, \
    WTQB, WTO, 1}
-// GQA group GM split over KVD virtual kv heads (G = GM / KVD q heads per attention work-group)
-#define LLMI_BCFGV(NBQ, NBO, HD, GM, KVD, QROLE, QR, QP, QE, OR, OP, OE)                                         \
-  {NBQ, NBO, HD, GM, QROLE, QR, QP, QE, OR, OP, OE, block_attn_lds<HD, GM / KVD>(),                               \
-   block_launch<HD, GM / KVD, QR, QP, QE, QROLE, OR, OP, OE, 0, 0, 0, KVD>,                                       \
-   reinterpret_cast<const void*>(&attn_block_kernel<HD, GM / KVD, QR, QP, QE, QROLE, OR, OP, OE, 0, 0, 0, KVD>), 0, \
-   0, 0, KVD}
+// GQA group GM split over KVD virtual kv heads (G = GM / KVD q heads per attention work-group); WT: the
+// weight format of qkv and o (0 Q4_0, WT_W8 Q8_0: P counts 16-B half-block passes)
+#define LLMI_BCFGVW(NBQ, NBO, HD, GM, KVD, QROLE, QR, QP, QE, OR, OP, OE, WT)                                       \
+  {NBQ, NBO, HD, GM, QROLE, QR, QP, QE, OR, OP, OE, block_attn_lds<HD, GM / KVD>(),                                 \
+   block_launch<HD, GM / KVD, QR, QP, QE, QROLE, OR, OP, OE, WT, 0, WT, KVD>,                                       \
+   reinterpret_cast<const void*>(&attn_block_kernel<HD, GM / KVD, QR, QP, QE, QROLE, OR, OP, OE, WT, 0, WT, KVD>), WT, \
+   0, WT, KVD}
+#define LLMI_BCFGV(NBQ, NBO, HD, GM, KVD, QROLE, QR, QP, QE, OR, OP, OE) \
+  LLMI_BCFGVW(NBQ, NBO, HD, GM, KVD, QROLE, QR, QP, QE, OR, OP, OE, 0)
 #define LLMI_BCFG(NBQ, NBO, HD, G, QROLE, QR, QP, QE, OR, OP, OE) \
   LLMI_BCFGW(NBQ, NBO, HD, G, QROLE, QR, QP, QE, OR, OP, OE, 0, 0, 0)
 // qkv: 4 waves x QR rows per work-group (rows per work-group must divide
@@ -861,6 +866,9 @@ const BlockCfg kBlockCfgs[] = {
     LLMI_BCFGV(36, 32, 256, 4, 2, ROLE_PLAIN, 4, 3, 1, 4, 2, 1),
     LLMI_BCFG(36, 32, 256, 4, ROLE_PRO, 4, 3, 5, 4, 2, 1),     // 1B:  qkv 1536 rows -> 96 WGs, o 1152 -> 72
     LLMI_BCFG(36, 32, 256, 4, ROLE_PLAIN, 4, 3, 1, 4, 2, 1),   // 1B layer 0
+    // 1B Q8_0 (BASELINE configs[3]): the same, Q8_0 weights (72 / 64 half-block units per qkv / o row)
+    LLMI_BCFGVW(36, 32, 256, 4, 2, ROLE_PRO, 4, 5, 5, 4, 4, 1, WT_W8),
+    LLMI_BCFGVW(36, 32, 256, 4, 2, ROLE_PLAIN, 4, 5, 1, 4, 4, 1, WT_W8),
     // 4B Q4_K_M (kq weights): q|k Q4_K + v Q6_K, or all Q4_K; o Q4_K; the Q4_0 geometry
     LLMI_BCFGW(80, 64, 256, 2, ROLE_PRO, 4, 5, 10, 8, 8, 1, WT_Q4_K, WT_Q6_K, WT_Q4_K),
     LLMI_BCFGW(80, 64, 256, 2, ROLE_PLAIN, 4, 5, 1, 8, 8, 1, WT_Q4_K, WT_Q6_K, WT_Q4_K),
@@ -872,7 +880,7 @@ const BlockCfg kBlockCfgs[] = {
 
 int wt_of_w(const DevWeight* w) {
   if (!w) return 0;
-  return w->type == T_Q4_K ? WT_Q4_K : w->type == T_Q6_K ? WT_Q6_K : 0;
+  return w->type == T_Q4_K ? WT_Q4_K : w->type == T_Q6_K ? WT_Q6_K : w->type == T_Q8_0 ? WT_W8 : 0;
 }
 
 const BlockCfg* find_block_cfg(int nb_qkv, int nb_o, int hd, int g, int qrole, int wtq = 0, int wtqb = 0,
@@ -947,7 +955,8 @@ static bool block_co_resident(const BlockCfg& c, const BlockGeom& g) {
 
 bool attn_block_supported(const DevWeight& wqkv, const DevWeight* wqkv_b, const DevWeight& wo, int head_dim,
                           int n_head, int n_head_kv) {
-  const bool q40 = wqkv.type == T_Q4_0 && wo.type == T_Q4_0 && !wqkv_b && !wqkv.slab && !wo.slab;
+  const bool q40 = (wqkv.type == T_Q4_0 || wqkv.type == T_Q8_0) && wo.type == wqkv.type && !wqkv_b && !wqkv.slab &&
+                   !wo.slab;
   const bool kq = wqkv.kq && wo.kq && (!wqkv_b || (wqkv_b->kq && wqkv_b->cols == wqkv.cols));
   if (!q40 && !kq) return false;
   if (wqkv.cols % 32 || wo.cols % 32 || n_head_kv <= 0 || n_head % n_head_kv) return false;
@@ -970,7 +979,8 @@ void launch_attn_block(const DevWeight& wqkv, const DevWeight* wqkv_b, LayerGemv
   const int g = aa.n_head / aa.n_head_kv, hd = aa.head_dim;
   const BlockCfg& c = *find_block_cfg(wqkv.cols / 32, wo.cols / 32, hd, g, qrole, wt_of_w(&wqkv), wt_of_w(wqkv_b),
                                       wt_of_w(&wo));
-  if (c.wto && !aa.q8k) throw std::runtime_error("attention block: a kq o projection reads Q8_K blocks");
+  if ((c.wto == WT_Q4_K || c.wto == WT_Q6_K) != (aa.q8k != 0))
+    throw std::runtime_error("attention block: a kq o projection reads Q8_K blocks (and only it)");
   if (!bs.epoch || !bs.g_qkv || !bs.g_xo || !bs.err || !aa.q8 || !aa.partial || !aa.ticket || !qa.qkv ||
       qa.qkv != qg.out)
     throw std::runtime_error("attention block: missing buffers");
@@ -990,7 +1000,8 @@ void launch_attn_block(const DevWeight& wqkv, const DevWeight* wqkv_b, LayerGemv
   const int nbq = qg.nb, nbo = og.nb;
   // one pass group per lane (no MULTI) and enough prologue / x-copy slots
   auto passes = [](int nb, int R) { return (nb + 64 / R - 1) / (64 / R); };
-  if (passes(nbq, c.QR) > c.QP || passes(nbo, c.OR) > c.OP) throw std::runtime_error("attention block: P too small");
+  const int uq = c.wtq == WT_W8 ? 2 * nbq : nbq, uo = c.wto == WT_W8 ? 2 * nbo : nbo;  // 16-B units per row
+  if (passes(uq, c.QR) > c.QP || passes(uo, c.OR) > c.OP) throw std::runtime_error("attention block: P too small");
   if (qrole == ROLE_PRO ? wqkv.cols > c.QE * 256 : 3 * nbq > c.QE * 256) throw std::runtime_error("attention block: qkv E");
   if (3 * nbo > c.OE * 256) throw std::runtime_error("attention block: o E");
   const BlockGeom bg = block_geom(c, wqkv, wqkv_b, wo, aa.n_head_kv, qrole);
