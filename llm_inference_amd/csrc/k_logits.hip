@@ -153,19 +153,23 @@ __global__ __launch_bounds__(256) void screen_prep_kernel(const uint16_t* __rest
 // pairs with the next pair's loads in flight (as gemv_f16_rows_pipe).
 // CPL: 16-B chunks per lane, ceil(2 nb / 32) (5 for 2560 columns; chunks
 // past the row's 2 nb contribute nothing).
-template <int CPL, int AHEAD>
+template <int CPL, int AHEAD, int LPR = 32>
 __global__ __launch_bounds__(256) void screen_gemv_kernel(const uint4* __restrict__ qs, const uint16_t* __restrict__ d,
                                                           int rows, int nb, const ScreenX* __restrict__ xs,
                                                           float* __restrict__ hi, unsigned* __restrict__ m_key) {
+  // LPR lanes per row (32: half a wave; 16: a quarter, for short rows -- 1B's 72 chunks fill 5 of 16 lanes'
+  // passes instead of 3 of 32 lanes' at 75 %), RPW rows per wave
+  static_assert(LPR == 32 || LPR == 16, "lanes per row");
+  constexpr int RPW = 64 / LPR;
   const int NC = 2 * nb;  // 16-B chunks per row
-  const int lane = threadIdx.x & 63, j = lane & 31, half = lane >> 5;
-  int pair = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int npairs = gridDim.x * 4;
+  const int lane = threadIdx.x & 63, j = lane % LPR, sub = lane / LPR;
+  int grp = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int ngrp = gridDim.x * 4;
   int4 xq[CPL];
   float xd[CPL], xc[CPL];
 #pragma unroll
   for (int p = 0; p < CPL; p++) {
-    const int c = p * 32 + j, b = min(c, NC - 1) >> 1;
+    const int c = p * LPR + j, b = min(c, NC - 1) >> 1;
     const bool ok = c < NC;
     const int4* xb = reinterpret_cast<const int4*>(xs + b);
     xq[p] = ok ? ((c & 1) ? xb[1] : xb[0]) : make_int4(0, 0, 0, 0);
@@ -179,23 +183,24 @@ __global__ __launch_bounds__(256) void screen_gemv_kernel(const uint4* __restric
     const uint16_t* dr = d + (size_t)r * nb;
 #pragma unroll
     for (int p = 0; p < CPL; p++) {
-      const int c = min(p * 32 + j, NC - 1);  // clamped (masked by x = 0)
+      const int c = min(p * LPR + j, NC - 1);  // clamped (masked by x = 0)
       q[p] = ld_nt(qr + c);
       s[p] = dr[c >> 1];
     }
   };
-  int row = 2 * pair + half;
+  auto row_sum = [](float v) { return LPR == 32 ? half_sum(v) : row16_sum(v); };
+  int row = RPW * grp + sub;
   uint4 cq[CPL];
   uint16_t cs[CPL];
   load(cq, cs, min(row, rows - 1));
-  // AHEAD = 2: a second row pair in flight (bytes in flight per CU: MI355X_MICROARCH HBM latency x rate)
+  // AHEAD = 2: a second row group in flight (bytes in flight per CU: MI355X_MICROARCH HBM latency x rate)
   uint4 mq[AHEAD > 1 ? CPL : 1];
   uint16_t ms[AHEAD > 1 ? CPL : 1];
-  if constexpr (AHEAD > 1) load(mq, ms, min(row + 2 * npairs, rows - 1));
-  for (; 2 * pair < rows; pair += npairs, row += 2 * npairs) {
+  if constexpr (AHEAD > 1) load(mq, ms, min(row + RPW * ngrp, rows - 1));
+  for (; RPW * grp < rows; grp += ngrp, row += RPW * ngrp) {
     uint4 nq[CPL];
     uint16_t ns[CPL];
-    load(nq, ns, min(row + 2 * AHEAD * npairs, rows - 1));
+    load(nq, ns, min(row + RPW * AHEAD * ngrp, rows - 1));
     float ap = 0.0f, bp = 0.0f;
 #pragma unroll
     for (int p = 0; p < CPL; p++) {
@@ -208,8 +213,8 @@ __global__ __launch_bounds__(256) void screen_gemv_kernel(const uint4* __restric
       ap += dw * (xd[p] * (float)is);
       bp += dw * xc[p];
     }
-    ap = half_sum(ap);
-    bp = half_sum(bp) * (1.0f + 0x1p-10f);
+    ap = row_sum(ap);
+    bp = row_sum(bp) * (1.0f + 0x1p-10f);
     if (j == 0 && row < rows) {
       hi[row] = (ap + bp) + A;
       mloc = fmaxf(mloc, (ap - bp) - A);
@@ -318,21 +323,24 @@ void launch_screen_argmax(const DevWeight& table, const ScreenTable& st, const u
   if (!screen_supported(table)) throw std::runtime_error("screen: unsupported logits table");
   const int n = table.cols, nb = n / 32;
   hipLaunchKernelGGL(screen_prep_kernel, dim3(1), dim3(256), 0, s, x16, n, st.xs, st.m_key);
-  const int cpl = (2 * nb + 31) / 32;
   const int rows = table.rows;
   static const int wpc = getenv("LLMI_SCREEN_WPC") ? atoi(getenv("LLMI_SCREEN_WPC")) : 8;  // waves per CU (A/B)
-  // row pairs in flight per half-wave (A/B on the 4B bench: 1 -> 2 = 132.8 -> 127.7 us; 4 or 12 waves per CU slower)
+  // row groups in flight per lane group (A/B on the 4B bench: 1 -> 2 = 132.8 -> 127.7 us; 4 or 12 waves per CU slower)
   static const int ahead = getenv("LLMI_SCREEN_AHEAD") ? atoi(getenv("LLMI_SCREEN_AHEAD")) : 2;
-  const dim3 grid((std::min((rows + 1) / 2, 256 * wpc) + 3) / 4);
+  // lanes per row: a quarter wave for short rows (<= 80 chunks: the 1B table's 72), else half a wave
+  static const int lpr_env = getenv("LLMI_SCREEN_LPR") ? atoi(getenv("LLMI_SCREEN_LPR")) : 0;
+  const int lpr = lpr_env == 16 || lpr_env == 32 ? lpr_env : (2 * nb <= 80 ? 16 : 32);
+  const int cpl = (2 * nb + lpr - 1) / lpr, rpw = 64 / lpr;
+  const dim3 grid((std::min((rows + rpw - 1) / rpw, 256 * wpc) + 3) / 4);
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, reinterpret_cast<const uint4*>(st.qs), st.d, rows, nb, st.xs, st.hi,
+                       st.m_key);
+  };
   switch (cpl) {
-#define LLMI_SCR(C)                                                                                               \
-  case C:                                                                                                         \
-    if (ahead > 1)                                                                                                \
-      hipLaunchKernelGGL((screen_gemv_kernel<C, 2>), grid, dim3(256), 0, s, reinterpret_cast<const uint4*>(st.qs), \
-                         st.d, rows, nb, st.xs, st.hi, st.m_key);                                                 \
-    else                                                                                                          \
-      hipLaunchKernelGGL((screen_gemv_kernel<C, 1>), grid, dim3(256), 0, s, reinterpret_cast<const uint4*>(st.qs), \
-                         st.d, rows, nb, st.xs, st.hi, st.m_key);                                                 \
+#define LLMI_SCR(C)                                                       \
+  case C:                                                                 \
+    if (lpr == 16) go(ahead > 1 ? screen_gemv_kernel<C, 2, 16> : screen_gemv_kernel<C, 1, 16>); \
+    else go(ahead > 1 ? screen_gemv_kernel<C, 2, 32> : screen_gemv_kernel<C, 1, 32>);           \
     break;
     LLMI_SCR(1) LLMI_SCR(2) LLMI_SCR(3) LLMI_SCR(4) LLMI_SCR(5) LLMI_SCR(6) LLMI_SCR(7) LLMI_SCR(8) LLMI_SCR(9)
     LLMI_SCR(10) LLMI_SCR(11) LLMI_SCR(12)
