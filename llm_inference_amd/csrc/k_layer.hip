@@ -117,6 +117,12 @@ struct LayerCfg {
       LLMI_LCFGK1(NB, ROLE, R, NW, P, E, EARLY, PE, WT_Q6_K, SLAB)
 #define LLMI_LCFG8(NB, ROLE, R, NW, P, E, EARLY) \
   {NB, ROLE, R, NW, P, E, false, 0, false, launch_cfg<R, NW, P, E, ROLE, false, EARLY, 0, true>, true}
+// late W8 roles with the first PE passes issued right after the prologue's loads
+#define LLMI_LCFG8P(NB, ROLE, R, NW, P, E, PE) \
+  {NB, ROLE, R, NW, P, E, false, 0, false, launch_cfg<R, NW, P, E, ROLE, false, false, PE, true>, true}
+#ifndef LLMI_W8_GELU_PE
+#define LLMI_W8_GELU_PE 7  // 1B Q8_0 gate_up: PE 0 / 3 / 5 / 7 / 8 = 6.71 / 6.39 / 6.23 / 5.68 / 6.24 us
+#endif
 // PRO / GELU entries with NH helper waves (template role ROLE_PRO_H / ROLE_GELU_H)
 #define LLMI_LCFGH(NB, ROLE, R, NW, P, NH, MULTI, SLAB) \
   {NB, ROLE, R, NW, P, NH, MULTI, SLAB, true,          \
@@ -162,7 +168,7 @@ const LayerCfg kLayerCfgs[] = {
     LLMI_LCFG8(36, ROLE_PLAIN, 4, 2, 5, 1, true),     // 1B qkv l0   1536 rows -> 192 WGs
     LLMI_LCFG8(36, ROLE_PRO, 4, 4, 5, 5, true),       // 1B qkv      96 WGs
     LLMI_LCFG8(32, ROLE_PLAIN, 1, 4, 1, 1, true),     // 1B o        1152 rows -> 288 WGs
-    LLMI_LCFG8(36, ROLE_GELU, 8, 8, 9, 3, false),     // 1B gate_up  13824 rows, H 32 -> 216 WGs
+    LLMI_LCFG8P(36, ROLE_GELU, 8, 8, 9, 3, LLMI_W8_GELU_PE),  // 1B gate_up  13824 rows, H 32 -> 216 WGs
     LLMI_LCFG8(216, ROLE_QUANT, 1, 4, 7, 4, true),    // 1B down     1152 rows -> 288 WGs
     LLMI_LCFG8(216, ROLE_PLAIN, 1, 4, 7, 3, true),    // 1B down from the GELU launch's blocks
     // K-quant weights in the kq layout (Gemma-3 4B Q4_K_M, BASELINE configs[3]): the Q4_0 4B
