@@ -386,7 +386,8 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, const QKVArgs
   const int n_keys = pos + 1;
   const bool own_new = FUSED && (pos / TK) % NS == c;
   const int hkc = hkv / KVD;  // cache head
-  static_assert(KVD == 1 || !FUSED || BLK, "virtual kv heads: the KV append runs in its own launch (or the block)");
+  // KVD > 1 with FUSED: the even virtual head appends the cache head's new K/V row (below); every virtual head's
+  // own_new work-group takes the new row from LDS (s_new), never from the cache
   const uint4* kb = reinterpret_cast<const uint4*>(a.k_cache + (size_t)hkc * a.max_ctx * HD);
   const uint4* vb = reinterpret_cast<const uint4*>(a.v_cache + (size_t)hkc * a.max_ctx * HD);
   uint4 kr[NLD], vr[NLD];
@@ -693,6 +694,18 @@ __global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa)
 
 template <int HD, int G>
 static void launch_split_g(const AttnArgs& a, const QKVArgs* fused, hipStream_t s) {
+  // LLMI_ATTN_KVD=2 (A/B): GQA pairs as two virtual kv heads of one q head (twice the work-groups, two merges)
+  static const int kvd_env = getenv("LLMI_ATTN_KVD") ? atoi(getenv("LLMI_ATTN_KVD")) : 1;
+  if constexpr (G == 2) {
+    if (kvd_env == 2 && (!a.q8k || HD % 256 == 0)) {
+      const dim3 grid(a.n_head_kv * 2, ATTN_NSPLIT);
+      if (fused)
+        hipLaunchKernelGGL((attn_split_kernel<HD, 1, true, 2>), grid, dim3(256), 0, s, a, *fused);
+      else
+        hipLaunchKernelGGL((attn_split_kernel<HD, 1, false, 2>), grid, dim3(256), 0, s, a, QKVArgs{});
+      return;
+    }
+  }
   const dim3 grid(a.n_head_kv, ATTN_NSPLIT);
   if (fused)
     hipLaunchKernelGGL((attn_split_kernel<HD, G, true>), grid, dim3(256), 0, s, a, *fused);
