@@ -572,6 +572,93 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, const QKVArgs
   ATTN_MARK(3);
   // ---- publish the partial, take a ticket --------------------------------
   float* part0 = a.partial + (size_t)hkv * G * NS * (HD + 2);  // [G][NS][HD + 2]
+  // reset: this work-group puts the ticket back to 0 for the next launch (the one that reads it last)
+  auto merge_heads = [&](auto gmc, int g0, bool reset) {
+    constexpr int GM = decltype(gmc)::value;
+  // ---- merge the NS partials of GM heads from head g0 (the last work-group: all G; DUAL: one each) ----
+  // One batch of loads: the (m, l) pairs first (the weights are reduced while
+  // the rest lands), then every thread's partial accumulators for its (g, d)
+  // outputs.  w_c = l_c ? exp(m_c - M) : 0, L = sum_c l_c w_c (half-wave
+  // tree), o = sum_c fma(v_c, w_c) in split order, out = o / L.
+  // per (head g, split cc) weight w = l ? exp(m - M_g) : 0 and L_g = sum l w,
+  // by half-wave reductions: lane t holds split t % NS of head t / NS (NS = 32)
+  static_assert(NS == 32, "merge reductions are half-wave wide");
+  float* pg0 = part0 + (size_t)g0 * NS * (HD + 2);  // head g0's partials
+  float mv = -INFINITY, lv = 0.0f;
+  if (t < GM * NS) {
+    const float* pm = pg0 + ((size_t)(t / NS) * NS + t % NS) * (HD + 2) + HD;
+    mv = ld_sc1(pm);
+    lv = ld_sc1(pm + 1);
+  }
+  constexpr int PAIRS = (GM * HD + 255) / 256;
+  float v[PAIRS][NS];
+  // splits that own no key (c TK >= n_keys: m = -inf, l = 0, zero
+  // accumulator, weight 0) are read out of bounds -- 0 without memory
+  // traffic, and the loads stay unconditional (8-15 of 32 at pos 512-768)
+  const int n_act = min(NS, (n_keys + TK - 1) / TK);
+  const __amdgpu_buffer_rsrc_t rpart = buf_rsrc(pg0, (uint32_t)(GM * NS * (HD + 2) * 4));
+#pragma unroll
+  for (int p = 0; p < PAIRS; p++) {
+    const int idx = min(t + p * 256, GM * HD - 1);
+    const int eg = (idx / HD) * NS * (HD + 2) + idx % HD;
+#pragma unroll
+    for (int cc = 0; cc < NS; cc++)
+      v[p][cc] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+          rpart, cc < n_act ? (eg + cc * (HD + 2)) * 4 : (1 << 30), 0, BUF_SC1));
+  }
+  __shared__ float s_wt[G][NS];  // [GM] used
+  __shared__ float s_L[G];
+  ATTN_MARK(6);
+  if (w < (GM * NS + 63) / 64) {  // whole waves
+    const float M = half_max(mv);
+    const float wt = lv == 0.0f ? 0.0f : expf(mv - M);
+    const float L = half_sum(lv * wt);
+    if (t < GM * NS) {
+      s_wt[t / NS][t % NS] = wt;
+      if (t % NS == 0) s_L[t / NS] = L;
+    }
+  }
+  __syncthreads();
+  float* s_out = TK * KS * 2 >= G * HD * 4 ? reinterpret_cast<float*>(s_k) : s_outbuf;  // [GM][HD]
+#pragma unroll
+  for (int p = 0; p < PAIRS; p++) {
+    const int idx = t + p * 256;
+    if (idx < GM * HD) {
+      const int g = idx / HD;
+      float o = 0.0f;
+#pragma unroll
+      for (int cc = 0; cc < NS; cc++) o = fmaf(v[p][cc], s_wt[g][cc], o);
+      const float val = o / s_L[g];
+      a.out[((size_t)hkv * G + g0) * HD + idx] = val;
+      s_out[idx] = val;
+    }
+  }
+  ATTN_MARK(7);
+  if (a.q8 != nullptr && HD % 32 == 0) {  // Q8_0 blocks of the heads' outputs (ops.cpp:116-139), 4 lanes per block
+    __syncthreads();
+    constexpr int NBK = HD % 32 == 0 ? G * HD / 32 : 1, NBM = HD % 32 == 0 ? GM * HD / 32 : 1;
+    __shared__ __attribute__((aligned(16))) XBlock s_q8[BLK ? NBK : 1];
+    for (int i = t; i < GM * HD / 8; i += 256) {
+      const float4 f0 = reinterpret_cast<const float4*>(s_out)[2 * i], f1 = reinterpret_cast<const float4*>(s_out)[2 * i + 1];
+      const float vv[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+      XBlock* xb = BLK ? s_q8 + (i >> 2) : a.q8 + ((size_t)hkv * G + g0) * HD / 32 + (i >> 2);
+      if (a.q8k) q8k_block_quad(vv, i & 3, xb);
+      else q8_block_quad(vv, i & 3, xb);
+    }
+    if constexpr (BLK) {  // the blocks' words as granules for the o projection
+      __syncthreads();
+      const uint32_t tag = btag;
+      uint2* dst = bs.g_xo + ((size_t)hkv * NBK + (size_t)g0 * HD / 32) * 12;
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(s_q8);
+      for (int i = t; i < NBM * 12; i += 256) st_granule(dst + i, src[i], tag);
+      BLK_MARK(bs, 4);
+    }
+  }
+  ATTN_MARK(5);
+  if (reset && t == 0) __hip_atomic_store(a.ticket + hkv, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+  };
+
+
   if (kp == 0) {
 #pragma unroll
     for (int g = 0; g < G; g++)
@@ -584,93 +671,35 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, const QKVArgs
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (t == 0)
-    s_last = __hip_atomic_fetch_add(a.ticket + hkv, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == NS - 1;
+  // DUAL (the block with G = 2): the last split merges head 1 and the second-to-last, once the last ticket is
+  // in, merges head 0 -- the two merges run in parallel instead of one work-group reading both heads' partials
+  constexpr bool DUAL = BLK && G == 2;
+  if (t == 0) {
+    const unsigned old = __hip_atomic_fetch_add(a.ticket + hkv, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = old == NS - 1 ? 1 : (DUAL && old == NS - 2) ? 2 : 0;
+  }
   __syncthreads();
   ATTN_MARK(4);
   BLK_MARK(bs, 3);
-  if (!s_last) return;
-
-  // ---- last work-group: merge the NS partials of the G heads -------------
-  // One batch of loads: the (m, l) pairs first (the weights are reduced while
-  // the rest lands), then every thread's partial accumulators for its (g, d)
-  // outputs.  w_c = l_c ? exp(m_c - M) : 0, L = sum_c l_c w_c (half-wave
-  // tree), o = sum_c fma(v_c, w_c) in split order, out = o / L.
-  // per (head g, split cc) weight w = l ? exp(m - M_g) : 0 and L_g = sum l w,
-  // by half-wave reductions: lane t holds split t % NS of head t / NS (NS = 32)
-  static_assert(NS == 32, "merge reductions are half-wave wide");
-  float mv = -INFINITY, lv = 0.0f;
-  if (t < G * NS) {
-    const float* pm = part0 + ((size_t)(t / NS) * NS + t % NS) * (HD + 2) + HD;
-    mv = ld_sc1(pm);
-    lv = ld_sc1(pm + 1);
-  }
-  constexpr int PAIRS = (G * HD + 255) / 256;
-  float v[PAIRS][NS];
-  // splits that own no key (c TK >= n_keys: m = -inf, l = 0, zero
-  // accumulator, weight 0) are read out of bounds -- 0 without memory
-  // traffic, and the loads stay unconditional (8-15 of 32 at pos 512-768)
-  const int n_act = min(NS, (n_keys + TK - 1) / TK);
-  const __amdgpu_buffer_rsrc_t rpart = buf_rsrc(part0, (uint32_t)(G * NS * (HD + 2) * 4));
-#pragma unroll
-  for (int p = 0; p < PAIRS; p++) {
-    const int idx = min(t + p * 256, G * HD - 1);
-    const int eg = (idx / HD) * NS * (HD + 2) + idx % HD;
-#pragma unroll
-    for (int cc = 0; cc < NS; cc++)
-      v[p][cc] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-          rpart, cc < n_act ? (eg + cc * (HD + 2)) * 4 : (1 << 30), 0, BUF_SC1));
-  }
-  __shared__ float s_wt[G][NS];
-  __shared__ float s_L[G];
-  ATTN_MARK(6);
-  if (w < (G * NS + 63) / 64) {  // whole waves
-    const float M = half_max(mv);
-    const float wt = lv == 0.0f ? 0.0f : expf(mv - M);
-    const float L = half_sum(lv * wt);
-    if (t < G * NS) {
-      s_wt[t / NS][t % NS] = wt;
-      if (t % NS == 0) s_L[t / NS] = L;
-    }
-  }
-  __syncthreads();
-  float* s_out = TK * KS * 2 >= G * HD * 4 ? reinterpret_cast<float*>(s_k) : s_outbuf;  // [G][HD]
-#pragma unroll
-  for (int p = 0; p < PAIRS; p++) {
-    const int idx = t + p * 256;
-    if (idx < G * HD) {
-      const int g = idx / HD;
-      float o = 0.0f;
-#pragma unroll
-      for (int cc = 0; cc < NS; cc++) o = fmaf(v[p][cc], s_wt[g][cc], o);
-      const float val = o / s_L[g];
-      a.out[(size_t)hkv * G * HD + idx] = val;
-      s_out[idx] = val;
-    }
-  }
-  ATTN_MARK(7);
-  if (a.q8 != nullptr && HD % 32 == 0) {  // Q8_0 blocks of the heads' outputs (ops.cpp:116-139), 4 lanes per block
-    __syncthreads();
-    constexpr int NBK = HD % 32 == 0 ? G * HD / 32 : 1;
-    __shared__ __attribute__((aligned(16))) XBlock s_q8[BLK ? NBK : 1];
-    for (int i = t; i < G * HD / 8; i += 256) {
-      const float4 f0 = reinterpret_cast<const float4*>(s_out)[2 * i], f1 = reinterpret_cast<const float4*>(s_out)[2 * i + 1];
-      const float vv[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
-      XBlock* xb = BLK ? s_q8 + (i >> 2) : a.q8 + (size_t)hkv * G * HD / 32 + (i >> 2);
-      if (a.q8k) q8k_block_quad(vv, i & 3, xb);
-      else q8_block_quad(vv, i & 3, xb);
-    }
-    if constexpr (BLK) {  // the blocks' words as granules for the o projection
+  const int role = s_last;
+  if (role == 0) return;
+  if constexpr (DUAL) {
+    if (role == 2) {  // every partial is published once the ticket reaches NS (bounded wait)
+      if (t == 0) {
+        int n = 0;
+        while (__hip_atomic_load(a.ticket + hkv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)NS) {
+          if (++n >= BLOCK_SPIN_LIMIT) {
+            __hip_atomic_store(bs.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+        }
+      }
       __syncthreads();
-      const uint32_t tag = btag;
-      uint2* dst = bs.g_xo + (size_t)hkv * NBK * 12;
-      const uint32_t* src = reinterpret_cast<const uint32_t*>(s_q8);
-      for (int i = t; i < NBK * 12; i += 256) st_granule(dst + i, src[i], tag);
-      BLK_MARK(bs, 4);
     }
+    merge_heads(std::integral_constant<int, 1>{}, role == 1 ? 1 : 0, role == 2);
+  } else {
+    merge_heads(std::integral_constant<int, G>{}, 0, true);
   }
-  ATTN_MARK(5);
-  if (t == 0) __hip_atomic_store(a.ticket + hkv, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
 }
 
 // Key tiles of 32 keys while every split owns at most one tile (short
