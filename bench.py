@@ -54,18 +54,30 @@ def parse():
     return p.parse_args()
 
 
-def pmc_traffic(kernel_substr: str):
+def pmc_key(a) -> str:
+    """The workload a PMC pass must have run to be quoted for this bench line:
+    model, weight types, prefill and decode lengths (the attention kernels'
+    bytes depend on the position they are timed at)."""
+    return f"{a.config}/{a.quant}/prefill{a.prefill}/warmup{a.warmup}/steps{a.steps}/reps{a.kernel_reps}"
+
+
+def pmc_traffic(kernel_substr: str, key: str):
     """HBM bytes per launch of the kernel whose name contains kernel_substr,
     from the newest committed rocprofv3 --pmc FETCH_SIZE pass (profiles/,
-    x2 gfx950 correction: scripts/pmc_summary.py); (None, None) when absent."""
+    x2 gfx950 correction: scripts/pmc_summary.py) OF THE SAME WORKLOAD (`key`,
+    pmc_key), over that pass's last dispatches of the kernel -- the ones the
+    bench's roofline timing (Model.time_kernel, after the decode loop) made, at
+    the position it reports; (None, None) when no such pass is committed."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_fetch*.json")))
     for f in reversed(files):
-        ks = json.load(open(f)).get("kernels", {})
-        hits = [v for k, v in ks.items() if kernel_substr in k]
+        d = json.load(open(f))
+        if d.get("config") != key:
+            continue
+        hits = [v for k, v in d.get("kernels", {}).items() if kernel_substr in k]
         if hits:
             v = max(hits, key=lambda h: h["dispatches"])
-            return round(v["hbm_bytes_mean"]), os.path.relpath(f, ROOT)
+            return round(v.get("hbm_bytes_tail_mean", v["hbm_bytes_mean"])), os.path.relpath(f, ROOT)
     return None, None
 
 
@@ -172,7 +184,9 @@ def cpu_baseline(g, cfg, n_decode: int, gpu_ids=None, mean_ctx=None):
     out.update({
         "value": round(len(per) / per.sum(), 3), "unit": "tokens/s", "kind": kind,
         "sample": f"{cfg.name} synthetic GGUF, {len(prompt)}-token prompt then {len(per)} greedy decode tokens "
-                  f"(pos {len(prompt)}-{len(prompt) + len(per) - 1}) via Model::forward on {threads} threads",
+                  f"(pos {len(prompt)}-{len(prompt) + len(per) - 1}) via Model::forward on {threads} threads; "
+                  f"a SHORT-CONTEXT sample: the reference's single-threaded attention grows with the position, "
+                  f"so its rate at the GPU line's mean context is lower (estimated_at_gpu_mean_context)",
         "half_threads": {"threads": max(1, threads // 2),
                          "value": round(len(runs[max(1, threads // 2)][1]) / sum(runs[max(1, threads // 2)][1]), 3)},
         "attention_s_per_position": float(max(slope, 0.0)),
@@ -299,8 +313,14 @@ def main():
     dom = fams.get(dom_name, {})
     kpat = {"attention_block": "attn_block_kernel", "gate_up": "gemv_q4_0_layer<8, 10, 10",
             "down": "gemv_q4_0_layer<1, 10, 5", "token_selection": "screen_gemv_kernel"}.get(dom_name, "-")
-    traffic, traffic_src = pmc_traffic(kpat)
-    mean_ctx = pos - a.steps / 2
+    traffic, traffic_src = pmc_traffic(kpat, pmc_key(a))
+    # the timed steps decode positions pos .. pos + steps - 1; the step at
+    # position p attends to p + 1 keys, so the mean KV history read is
+    # pos + (steps + 1) / 2 keys per layer
+    mean_ctx = pos + (a.steps + 1) / 2
+    # time_kernel runs after the loop: the device position is then pos + steps
+    # (the attention block attends to pos + steps + 1 keys there)
+    pos_end = pos + a.steps
     tok_bytes = info.bytes_per_token + info.kv_bytes_per_pos * mean_ctx
     if info.screened_logits:  # the decode loop streams the int8 screening table instead of the F16 one
         tok_bytes += info.screen_bytes - info.vocab * info.n_embd * 2
@@ -355,7 +375,7 @@ def main():
             "frac": dom["frac"], "traffic": traffic, "traffic_unit": "HBM bytes per launch (FETCH_SIZE x2)",
             "traffic_source": traffic_src,
             "us_per_launch": dom["us_per_launch"], "bytes_per_launch": dom["bytes_per_launch"],
-            "position": pos,
+            "position": pos_end, "keys_attended": pos_end + 1, "pmc_key": pmc_key(a),
         } if dom else None),
         "kernel_families": fams,
         "logits_gemv": {"us": round(us_l, 2), "GBps": round(by_l / (us_l * 1e-6) / 1e9, 1)},

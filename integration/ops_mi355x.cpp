@@ -53,19 +53,44 @@ struct WeightKeyHash {
   }
 };
 
-// Sampled content fingerprint of a weight's bytes (FNV-1a over 64 evenly
-// spaced 64-byte windows and the length): a buffer freed and reallocated at
+// Content fingerprint of a weight's bytes: a buffer freed and reallocated at
 // the same address with other contents (model_test.cpp:394/410/463 builds
 // several Models from heap vectors in one process) gets a new upload instead
-// of the previous tensor's device copy.
+// of the previous tensor's device copy.  Buffers up to FULL_HASH_BYTES are
+// hashed WHOLE (every byte: an edit anywhere is seen); larger ones (the
+// reference mmaps them read-only, gguf.cpp:130-149, so they cannot change in
+// place) are hashed over 4096 evenly spaced 64-byte windows plus the length --
+// callers that rewrite a large weight in place must call
+// llmi_ops_flush_weights().
+constexpr size_t FULL_HASH_BYTES = (size_t)64 << 20;
+
+uint64_t hash_words(const uint8_t* p, size_t n, uint64_t h) {  // 4 independent lanes, 8-byte words
+  uint64_t a = h, b = h ^ 0x9E3779B97F4A7C15ull, c = h ^ 0xC2B2AE3D27D4EB4Full, d = h ^ 0x165667B19E3779F9ull;
+  size_t i = 0;
+  auto mix = [](uint64_t x, uint64_t w) {
+    x ^= w * 0x87C37B91114253D5ull;
+    x = (x << 31) | (x >> 33);
+    return x * 0x4CF5AD432745937Full;
+  };
+  for (; i + 32 <= n; i += 32) {
+    uint64_t w[4];
+    std::memcpy(w, p + i, 32);
+    a = mix(a, w[0]);
+    b = mix(b, w[1]);
+    c = mix(c, w[2]);
+    d = mix(d, w[3]);
+  }
+  for (; i < n; i++) a = mix(a, p[i]);
+  return mix(mix(mix(a, b), c), d);
+}
+
 uint64_t fingerprint(const void* data, size_t bytes) {
   const uint8_t* p = static_cast<const uint8_t*>(data);
-  uint64_t h = 1469598103934665603ull ^ bytes;
-  const size_t win = 64, n = bytes < win ? 1 : 64;
-  for (size_t i = 0; i < n; i++) {
-    const size_t off = bytes <= win ? 0 : (bytes - win) * i / (n - 1 ? n - 1 : 1);
-    for (size_t j = 0; j < win && off + j < bytes; j++) h = (h ^ p[off + j]) * 1099511628211ull;
-  }
+  const uint64_t h0 = 1469598103934665603ull ^ bytes;
+  if (bytes <= FULL_HASH_BYTES) return hash_words(p, bytes, h0);
+  constexpr size_t win = 64, n = 4096;
+  uint64_t h = h0;
+  for (size_t i = 0; i < n; i++) h = hash_words(p + (bytes - win) * i / (n - 1), win, h);
   return h;
 }
 

@@ -685,16 +685,23 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, const QKVArgs
   if (role == 0) return;
   if constexpr (DUAL) {
     if (role == 2) {  // every partial is published once the ticket reaches NS (bounded wait)
+      __shared__ int s_ok;
       if (t == 0) {
         int n = 0;
+        s_ok = 1;
         while (__hip_atomic_load(a.ticket + hkv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)NS) {
           if (++n >= BLOCK_SPIN_LIMIT) {
             __hip_atomic_store(bs.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_ok = 0;
             break;
           }
         }
       }
       __syncthreads();
+      // timed out: no merge from incomplete partials and no ticket reset (the
+      // slow split still adds to it); the host zeroes every ticket when it
+      // reports the error (Session::check_device_error)
+      if (s_ok == 0) return;
     }
     merge_heads(std::integral_constant<int, 1>{}, role == 1 ? 1 : 0, role == 2);
   } else {

@@ -48,6 +48,10 @@ void Session::load_hparams(const GGUFView& g) {  // model.cpp:58-167
     for (const auto& v : sw->arr) hp_.swa_layers.push_back((v.u32 & 0xFF) != 0);
   if (const GValue* v = g.find(p + "attention.logit_softcapping"))
     if (v->f32() > 0.0f) throw status_error(LLMI_E_GGUF, "unsupported: " + p + "attention.logit_softcapping");
+  // ALiBi (model.cpp:125-128, 492-518): no Gemma file sets it, and the reference's bias term
+  // slope * (t_k - (pos + t)) is evaluated in uint32_t (a wrapped, huge positive bias); refused, never ignored
+  if (const GValue* v = g.find(p + "attention.max_alibi_bias"))
+    if (v->f32() > 0.0f) throw status_error(LLMI_E_GGUF, "unsupported: " + p + "attention.max_alibi_bias");
   if (const GValue* v = g.find(p + "attention.final_logit_softcapping")) hp_.final_softcap = v->f32();
   // Gemma-4 (model.cpp:119-122, 148-166): attention scale 1, per-layer
   // embedding width, the first layer that reads an earlier layer's cache
@@ -830,7 +834,26 @@ void Session::gather_cols(void* buf, size_t pitch_b, size_t slice_b, int T, hipS
       LLMI_HIP(hipMemcpy2DAsync(b + r * slice_b, pitch_b, g + r * blk, slice_b, slice_b, T, hipMemcpyDeviceToDevice, s));
 }
 
+// The opt-in f16 path (LLMI_PREFILL_F16) writes its activations as f16: a value past 65504 becomes inf and the
+// GEMMs then produce non-finite rows.  Such a row reaches the last token's final norm through the residual stream
+// or, via the KV cache, through attention (a non-last token's row can escape only in the last layer's FFN, whose
+// output feeds nothing but that token's own residual).  So a finite final norm row proves no f16 activation that
+// matters overflowed; otherwise the prefill is recomputed on the int8 path (the reference's Q8 numerics), which
+// overwrites the same KV rows -- never a non-finite result.
 void Session::prefill(const int32_t* tokens, int n, int pos) {
+  if (!prefill_run(tokens, n, pos, true)) return;
+  std::vector<float> h((size_t)hp_.n_embd);
+  LLMI_HIP(hipMemcpyAsync(h.data(), xn_, h.size() * 4, hipMemcpyDeviceToHost, stream_));
+  LLMI_HIP(hipStreamSynchronize(stream_));
+  for (float v : h)
+    if (!std::isfinite(v)) {
+      pf_f16_redo_++;
+      prefill_run(tokens, n, pos, false);
+      return;
+    }
+}
+
+bool Session::prefill_run(const int32_t* tokens, int n, int pos, bool allow_f16) {
   hipStream_t s = stream_;
   const int E = hp_.n_embd, F = hp_.n_ff;
   // 512 tokens per chunk: the prefill GEMMs' weight tiles are re-read once per
@@ -849,7 +872,7 @@ void Session::prefill(const int32_t* tokens, int n, int pos) {
   const int G = nh_ / std::max(nkv_, 1);
   // K-quant (kq) layers: Q8_K activation blocks from the same producers (the decode's quantization) and the int8
   // GEMM's K-quant variant, or the opt-in f16 path
-  const bool f16 = getenv("LLMI_PREFILL_F16") && (pf_kq_ || L_[0].o.w.type == T_Q4_0) &&
+  const bool f16 = allow_f16 && getenv("LLMI_PREFILL_F16") && (pf_kq_ || L_[0].o.w.type == T_Q4_0) &&
                    !getenv("LLMI_PREFILL_ATTN_V1") && (G == 1 || G == 2 || G == 4) &&
                    layer_gemv_gelu_group(L_[0].gate_up[0].w.cols, L_[0].gate_up[0].w.type) % 8 == 0;
   const int q8k = pf_kq_ && !f16 ? 1 : 0;
@@ -980,6 +1003,7 @@ void Session::prefill(const int32_t* tokens, int n, int pos) {
       record_logits(s);
     }
   }
+  return f16;
 }
 
 // Fast path with every projection a gemv_q4_0_layer launch: 5 launches per
@@ -1428,8 +1452,9 @@ void Session::check_device_error() {
   if (!blk_err_) return;
   int e = 0;
   LLMI_HIP(hipMemcpy(&e, blk_err_, sizeof(e), hipMemcpyDeviceToHost));
-  if (e) {  // reported once: the flag is cleared so the session's next call starts clean
+  if (e) {  // reported once: the flag and every attention ticket are cleared so the session's next call starts clean
     LLMI_HIP(hipMemset(blk_err_, 0, sizeof(int)));
+    LLMI_HIP(hipMemset(ticket_, 0, sizeof(unsigned) * (size_t)hp_.n_head));
     throw status_error(LLMI_E_HIP, "attention block: a cross-work-group wait timed out (device results invalid)");
   }
 }

@@ -126,9 +126,10 @@ def random_tensor(ttype: int, n_rows: int, n_cols: int, seed: int = 0, **kw) -> 
 def build_gemma3_gguf(cfg: Gemma3Config, seed: int = 0, wtype: int = TensorType.Q4_0,
                       embd_type: int = TensorType.F16, wtypes: Optional[Dict[str, int]] = None,
                       swa_pattern: Optional[list] = None, centered: bool = False,
-                      pieces: Optional[list] = None) -> np.ndarray:
+                      pieces: Optional[list] = None, extra_meta: Optional[Dict[str, object]] = None) -> np.ndarray:
     """Random-init Gemma-3 GGUF with the tensor names/shapes model.cpp maps
-    (model.cpp:169-238).  Returns the whole file as a uint8 numpy array."""
+    (model.cpp:169-238).  Returns the whole file as a uint8 numpy array.
+    extra_meta: more metadata keys (without the "gemma3." prefix)."""
     rng = np.random.default_rng(seed)
     b = GGUFBuilder(align_tensors=True)
     a = "gemma3"
@@ -144,6 +145,8 @@ def build_gemma3_gguf(cfg: Gemma3Config, seed: int = 0, wtype: int = TensorType.
     b.add_meta(f"{a}.rope.freq_base", float(cfg.rope_base))
     if swa_pattern is not None:
         b.add_meta(f"{a}.attention.sliding_window_pattern", [bool(x) for x in swa_pattern])
+    for k, v in (extra_meta or {}).items():
+        b.add_meta(f"{a}.{k}", v)
     toks = ["<pad>", "<eos>", "<bos>", "<unk>"] + [f"t{i}" for i in range(4, cfg.vocab)]
     for i, p in enumerate(pieces or []):  # real vocabulary pieces at ids 4.. (the tokenizer's greedy longest match)
         toks[4 + i] = p

@@ -81,3 +81,38 @@ def test_dropin_two_models_one_process(oracle, tmp_path):
         _, a, l0 = rows[3 * mi]
         assert a == int(np.argmax(lg))
         np.testing.assert_allclose(l0, lg[:16], atol=1e-5, rtol=0)
+
+
+def test_dropin_same_shape_one_block_edited(oracle, tmp_path):
+    """Two GGUFs identical except ONE Q4_0 block in the middle of a weight
+    (bytes the round-2 sampled fingerprint never read: 64 windows of 64 B).
+    Run back to back in one process, the second file's mmap may land at the
+    first's address with the same tensor shapes: the compat layer's weight
+    cache must see the edit (ops_mi355x.cpp hashes buffers up to 64 MiB
+    whole) -- each model's logits equal the oracle's for its own bytes."""
+    from llm_inference_amd.gguf import GGUFFile
+    from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
+    g = np.array(build_gemma3_gguf(CONFIGS["tiny"], seed=7, swa_pattern=[True, False, True]), np.uint8)
+    f = GGUFFile(g)
+    t = f.tensor("blk.0.ffn_up.weight")
+    start = f.data_section_start + t.tensor_offset
+    mid = start + (t.nbytes // 2 // 18) * 18 + 37 * 18  # a block boundary off the 64 sampled windows
+    g2 = g.copy()
+    g2[mid + 2:mid + 18] ^= 0x5A  # the block's nibbles (its f16 scale kept)
+    assert not np.array_equal(g, g2)
+    paths = []
+    for i, gg in enumerate((g, g2)):
+        p = tmp_path / f"e{i}.gguf"
+        p.write_bytes(gg.tobytes())
+        paths.append(str(p))
+    prompt = [2, 17, 301, 44, 9]
+    rows = run(",".join(paths), 1, prompt)
+    assert len(rows) == 2 * 2
+    outs = []
+    for mi, gg in enumerate((g, g2)):
+        lg = oracle.model(gg, n_threads=4, max_ctx=64).forward(prompt, 0)
+        _, a, l0 = rows[2 * mi]
+        assert a == int(np.argmax(lg))
+        np.testing.assert_allclose(l0, lg[:16], atol=1e-5, rtol=0)
+        outs.append(lg)
+    assert np.abs(outs[0][:16] - outs[1][:16]).max() > 1e-3, "the edit must change the compared logits"

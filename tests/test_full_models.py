@@ -229,3 +229,15 @@ def test_full_size_quant_batched_prefill(oracle, monkeypatch, quant):
     if margin[0] > 4.0 * err0:
         assert int(np.argmax(ll)) == run[0]
     ml.close()
+    # the opt-in f16 prefill (LLMI_PREFILL_F16=1): at this depth its f16 activations overflowed (round 2: a
+    # non-finite argmax); the session must detect it and recompute on the int8 path -- finite logits, and the
+    # batched int8 prefill's result
+    monkeypatch.delenv("LLMI_NO_PREFILL")
+    monkeypatch.setenv("LLMI_PREFILL_F16", "1")
+    mf = Model(g, max_ctx=64)
+    lf = mf.forward(prompt, 0)
+    assert np.isfinite(lf).all(), "f16 prefill returned non-finite logits"
+    print(f"{quant} full size: |f16-path prefill - int8 prefill| {float(np.abs(lf - lg).max()):.3g}")
+    if margin[0] > 4.0 * err0:
+        assert int(np.argmax(lf)) == run[0]
+    mf.close()

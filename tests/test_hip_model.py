@@ -124,6 +124,14 @@ def test_session_errors():
     assert ei.value.status == "E_RANGE"
     with pytest.raises(LLMIError):
         m.forward([10], 0)  # vocab is 10
+    # attention features no Gemma-3 file sets are refused at load, never silently ignored
+    # (model.cpp:125-133, 492-518): ALiBi and the attention logit soft-cap
+    from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
+    for key in ("attention.max_alibi_bias", "attention.logit_softcapping"):
+        with pytest.raises(LLMIError) as ei:
+            Model(build_gemma3_gguf(CONFIGS["tiny"], seed=1, extra_meta={key: 8.0}), max_ctx=16)
+        assert ei.value.status == "E_GGUF" and key in str(ei.value)
+    Model(build_gemma3_gguf(CONFIGS["tiny"], seed=1, extra_meta={"attention.max_alibi_bias": 0.0}), max_ctx=16).close()
 
 
 def test_unfused_fast_path_matches_fused(oracle, monkeypatch):
