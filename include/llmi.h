@@ -191,6 +191,8 @@ typedef struct {
   int screened_logits;        /* 1: llmi_session_enqueue/generate pick each greedy token by int8 screening +
                                  exact f16 rescoring (same ids as the full F16 logits GEMV; forward keeps it) */
   size_t screen_bytes;        /* bytes of the int8 screening table streamed per decode-loop token */
+  int prefill_f16_redo;       /* opt-in f16 prefills (LLMI_PREFILL_F16) whose f16 activations overflowed and were
+                                 recomputed on the int8 path (never a non-finite result) */
 } llmi_session_info;
 int llmi_session_get_info(const llmi_session* s, llmi_session_info* info);
 

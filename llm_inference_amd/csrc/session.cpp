@@ -144,11 +144,19 @@ void Session::setup_tp() {
     throw status_error(LLMI_E_ARG, "tensor parallel: embedding_length / feed_forward_length % tp_size != 0");
   e_sh_ = hp_.n_embd / G;
   f_sh_ = hp_.n_ff / G;
-  // default: the q|k|v projection and the attention replicated on every rank (all heads, the whole KV
-  // cache), o / gate_up / down row-sharded -- three all-gathers per layer instead of four, and the
-  // attention block (qkv + attention + the rank's o rows in one launch) on the ranks; LLMI_TP_HEAD_SHARD=1
-  // shards the heads as well (an all-gather of the heads' outputs before o)
-  tp_rep_attn_ = getenv("LLMI_TP_HEAD_SHARD") == nullptr;
+  // Two modes, chosen per model (LLMI_TP_HEAD_SHARD=0 / 1 forces one):
+  //  replicated: the q|k|v projection and the attention on every rank (all heads, the whole KV cache),
+  //    o / gate_up / down row-sharded -- three all-gathers per layer instead of four, and the attention
+  //    block (qkv + attention + the rank's o rows in one launch) on the ranks;
+  //  head-sharded: the heads split as well (an all-gather of the heads' outputs before o).
+  // Replicating costs every rank the whole q|k|v weight per layer.  Measured per-rank kernel time without the
+  // exchange (profiles/r02_tp_solo.jsonl): 4B (n_embd 2560) replicated 0.97 / 0.93 / 0.91 ms vs head-sharded
+  // 1.01 / 0.97 / 0.92 at tp 2 / 4 / 8; 27B (n_embd 5376, 24.8 MB of q|k|v per layer) 3.66 / 2.90 / 2.79 vs
+  // 3.37 / 2.45 / 2.32.  So the heads are sharded by default for the wide models whose kv heads divide
+  // evenly over the ranks (n_embd >= 4096: 12B, 27B), replicated otherwise.
+  const char* hs = getenv("LLMI_TP_HEAD_SHARD");
+  const bool wide = hp_.n_embd >= 4096 && hp_.n_head % G == 0 && hp_.n_head_kv % G == 0;
+  tp_rep_attn_ = hs ? atoi(hs) == 0 : !wide;
   if (tp_rep_attn_) {
     nh_ = hp_.n_head;
     nkv_ = hp_.n_head_kv;
@@ -718,11 +726,13 @@ void Session::record_step(hipStream_t s, bool gen) {
     return o;
   };
   bool x_q8 = false;  // xn_'s Q8_0 blocks are already in act_
+  const void* x_blocks = nullptr;  // where they are (Q8_0: act_.q8.xb, Q8_K: act_.q8k)
   if (embd_.type == T_F16 || embd_.type == T_Q8_0) {
     const NormOut o = nout(L_[0].qkv);
     launch_embed_norm(embd_.type, embd_raw_, embd_row_bytes_, d_token_, emb_scale, resid_, L_[0].attn_norm, o, E,
                       hp_.eps, ex_norm_, s);
     x_q8 = o.q8 != nullptr || o.q8k != nullptr;
+    x_blocks = o.q8k ? (const void*)o.q8k : (const void*)o.q8;
     kernels_per_token_++;
   } else {
     launch_dequantize_rows(embd_.type, embd_raw_, embd_row_bytes_, d_token_, 1, E, emb_scale, resid_, s);
@@ -746,7 +756,8 @@ void Session::record_step(hipStream_t s, bool gen) {
   dump("attn_norm-0", xn_, E, s);
   tap("inp_scaled", -1, resid_, (size_t)E * 4, s);
   tap("attn_norm", 0, xn_, (size_t)E * 4, s);
-  if (x_q8) tap("xq", 0, act_.q8.xb, (size_t)(E / 32) * sizeof(XBlock), s);
+  // Q8_0: XBlocks; Q8_K: the reference's 292-B block_q8_K (norm_outputs, k_session.hip)
+  if (x_q8) tap("xq", 0, x_blocks, x_blocks == (const void*)act_.q8k ? (size_t)(E / 256) * 292 : (size_t)(E / 32) * sizeof(XBlock), s);
   bool fused = fuse_layers_;
   for (const auto& l : L_) fused &= l.fused;
   if (tp_ && !fused) throw status_error(LLMI_E_ARG, "tensor parallel needs the fused layer path");
@@ -1474,6 +1485,7 @@ void Session::info(llmi_session_info* o) const {
   o->batched_prefill = prefill_ok_ ? 1 : 0;
   o->screened_logits = screen_ ? 1 : 0;
   o->screen_bytes = screen_ ? scr_.bytes : 0;
+  o->prefill_f16_redo = pf_f16_redo_;
   size_t b = logits_w_.bytes;  // this rank's bytes
   for (const auto& l : L_) {
     for (const auto& p : l.qkv) b += p.w.bytes;

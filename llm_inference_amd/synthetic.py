@@ -86,6 +86,22 @@ def fill_random(out: np.ndarray, ttype: int, n_rows: int, n_cols: int, rng: np.r
         blk = out.reshape(-1, 22)
         blk[:, 2:] = rng.integers(0, 256, size=(blk.shape[0], 20), dtype=np.uint8)
         blk[:, 0:2] = _f16_bits(rng.uniform(scale_lo, scale_hi, blk.shape[0]) / 2).view(np.uint8).reshape(-1, 2)
+    elif ttype == TensorType.Q4_K and centered:
+        # w = d sc q - dmin m (ops.cpp:633-641 get_scale_min_k4) with m = sc and dmin = 7.5 d: w = d sc (q - 7.5),
+        # zero mean like trained weights (random mins make every projection's output one-signed: a dead FFN)
+        blk = out.reshape(-1, 144)
+        nb = blk.shape[0]
+        blk[:, 16:] = rng.integers(0, 256, size=(nb, 128), dtype=np.uint8)
+        sc = rng.integers(1, 64, size=(nb, 8), dtype=np.uint8)
+        sb = np.zeros((nb, 12), np.uint8)
+        sb[:, 0:4] = sc[:, 0:4] | ((sc[:, 4:8] >> 4) << 6)
+        sb[:, 4:8] = sc[:, 0:4] | ((sc[:, 4:8] >> 4) << 6)
+        sb[:, 8:12] = (sc[:, 4:8] & 15) | ((sc[:, 4:8] & 15) << 4)
+        blk[:, 4:16] = sb
+        d = rng.uniform(scale_lo, scale_hi, nb).astype(np.float32) / 64  # d sc ~ Q4_0 scale range
+        d16 = d.astype(np.float16)
+        blk[:, 0:2] = d16.view(np.uint16).view(np.uint8).reshape(-1, 2)
+        blk[:, 2:4] = _f16_bits(d16.astype(np.float32) * 7.5).view(np.uint8).reshape(-1, 2)
     elif ttype == TensorType.Q4_K:
         blk = out.reshape(-1, 144)
         blk[:, 4:] = rng.integers(0, 256, size=(blk.shape[0], 140), dtype=np.uint8)

@@ -79,8 +79,24 @@ def xblocks_q8k_to_f32(words: np.ndarray) -> np.ndarray:
     d = w[:, 8].copy().view(np.float32)
     assert np.array_equal(w[:, 9].view(np.int32), q.astype(np.int32).sum(1)), "XBlock nsum8 != sum(q)"
     assert np.array_equal(d.reshape(-1, 8), np.repeat(d.reshape(-1, 8)[:, :1], 8, 1)), "Q8_K d differs in a super-block"
-    assert np.abs(q.reshape(-1, 256)).max(1).min() >= 127 or not d.any(), "Q8_K super-block without a +-127 quant"
+    mx, dsb = np.abs(q.reshape(-1, 256)).max(1), d.reshape(-1, 8)[:, 0]
+    bad = np.nonzero((mx < 127) & ((dsb != 0) | (mx != 0)))[0]  # an all-zero x gives d = 0 and zero quants
+    assert bad.size == 0, f"Q8_K super-blocks {bad[:8].tolist()} without a +-127 quant (max |q| {mx[bad[:8]].tolist()}, d {dsb[bad[:8]].tolist()})"
     return (d[:, None] * q.astype(np.float32)).astype(np.float32).reshape(-1)
+
+
+def score_sensitivity(q, kc, vc):
+    """First-order bound on the relative change of one head's exact attention output when every score carries
+    an fp32-sized error e_t = 2 sqrt(hd) 2^-24 sum_i |q16_i k_ti|: max_i sum_t p_t e_t |v_ti - o_i| / max |o|."""
+    q16 = np.asarray(q, np.float32).astype(np.float16).astype(np.float64)
+    K = np.asarray(kc).view(np.float16).astype(np.float64)
+    V = np.asarray(vc).view(np.float16).astype(np.float64)
+    sc = K @ q16
+    p = np.exp(sc - sc.max())
+    p /= p.sum()
+    o = p @ V
+    e = 2.0 * math.sqrt(q16.size) * 2.0 ** -24 * (np.abs(K) @ np.abs(q16))
+    return float(((p * e)[:, None] * np.abs(V - o[None, :])).sum(0).max() / max(float(np.abs(o).max()), 1e-30))
 
 
 def rel_err(got, ref):
@@ -159,8 +175,12 @@ class OpChecker:
         got = attn_dev.reshape(nh, hd)
         ref64 = np.stack([self.orc.attn_head_f64(qr[h], kc[h // g, : pos + 1], vc[h // g, : pos + 1]) for h in range(nh)])
         refr = np.stack([self.orc.attn_head(qr[h], kc[h // g, : pos + 1], vc[h // g, : pos + 1]) for h in range(nh)])
-        # fp32 split-K sums: rounding grows like sqrt(keys) (2e-5 up to 256 keys)
-        self.note("attention_vs_f64", rel_err(got, ref64), ATTN_F64_RTOL * math.sqrt(max(1.0, (pos + 1) / 256.0)))
+        # fp32 split-K sums: rounding grows like sqrt(keys) (2e-5 up to 256 keys); plus the first-order effect of
+        # fp32 scores (an error of ~2 sqrt(hd) 2^-24 sum_i |q_i k_i| per key, through p_t |v_t - o|): large
+        # scores (centered K-quant weights) make the exact softmax itself that sensitive
+        sens = max(score_sensitivity(qr[h], kc[h // g, : pos + 1], vc[h // g, : pos + 1]) for h in range(nh))
+        self.report["attention_score_sensitivity"] = max(self.report["attention_score_sensitivity"], sens)
+        self.note("attention_vs_f64", rel_err(got, ref64), ATTN_F64_RTOL * math.sqrt(max(1.0, (pos + 1) / 256.0)) + sens)
         # the reference's own f16 V accumulator drifts from exact math with the
         # key count (~1e-3 at 256 keys, ~7e-3 at 1100): the fast path may differ
         # from it by that drift plus its own distance to exact math
@@ -168,13 +188,28 @@ class OpChecker:
         self.report["reference_attention_drift"] = max(self.report["reference_attention_drift"], ref_drift)
         self.note("attention_vs_reference", rel_err(got, refr), ref_drift * 1.01 + 2 * ATTN_F64_RTOL)
 
+    def q8k_blocks(self, words, x, what):
+        """Device XBlocks holding Q8_K quants vs the reference's quantize_row_q8_k of x (ops.cpp:142-178),
+        bit for bit: per 256-element super-block the f32 d and the 256 quants; returns x' = d q (f32)."""
+        xf = xblocks_q8k_to_f32(words)
+        w = np.ascontiguousarray(words, np.uint32).reshape(-1, 12)
+        ref = np.frombuffer(self.orc.quantize_q8_k(x), np.uint8).reshape(-1, 292)
+        assert np.array_equal(w[:, :8].copy().view(np.int8).reshape(-1, 256), ref[:, 4:260].view(np.int8)), \
+            f"{what}: Q8_K quants"
+        assert np.array_equal(w[:, 8].copy().view(np.float32).reshape(-1, 8)[:, 0], ref[:, :4].copy().view(np.float32)[:, 0]), \
+            f"{what}: Q8_K d"
+        return xf
+
     def decode_step(self, taps, pos, gen, token=None):
-        """One traced decode step (llmi_session_trace, n_tokens = 1)."""
+        """One traced decode step (llmi_session_trace, n_tokens = 1).  Q4_0 / Q8_0 layers read Q8_0 activation
+        blocks; K-quant layers (Q4_K / Q6_K in the kq layout) read Q8_K blocks, checked against the reference's
+        quantize_row_q8_k and dotted through the reference's mat_vec_mul_q4_k / _q6_k."""
         c = self.cfg
         E, F = c.n_embd, c.n_ff
         T = taps_by_layer(taps)
         one = lambda n, l: T[(n, l)][-1]
         block = ("qkv_g", 0) in T
+        kq = self.w.raw("blk.0.attn_q.weight")[1] in (TT.Q4_K, TT.Q6_K)
         for l in range(c.n_layer):
             x = f32(one("attn_norm", l))
             if l == 0:
@@ -193,7 +228,15 @@ class OpChecker:
                 self.note("norm", rel_err(x, self.norm(got_r, f"blk.{l}.attn_norm.weight")), NORM_RTOL)
             wqkv = self.w.qkv(l)
             qkv = granule_values(one("qkv_g", l)) if block else f32(one("qkv", l))
-            if l == 0 and ("xq", 0) in T:  # layer 0 reads embed_norm's Q8_0 blocks
+            if kq:  # q, k, v per tensor (Q4_K_M: q|k Q4_K, v Q6_K); every row's dot is independent of the stacking
+                xin = x
+                if l == 0 and ("xq", 0) in T:  # layer 0 reads embed_norm's block_q8_K rows (292 B, ops.h:18-23)
+                    b = np.frombuffer(one("xq", 0), np.uint8)
+                    assert b.size == E // 256 * 292 and np.array_equal(b, self.orc.quantize_q8_k(x)), "embed_norm Q8_K blocks"
+                    sb = b.reshape(-1, 292)
+                    xin = (sb[:, :4].copy().view(np.float32) * sb[:, 4:260].view(np.int8).astype(np.float32)).reshape(-1)
+                ref = np.concatenate([self.gemv(self.w.raw(f"blk.{l}.attn_{p}.weight"), xin) for p in "qkv"])
+            elif l == 0 and ("xq", 0) in T:  # layer 0 reads embed_norm's Q8_0 blocks
                 xq = xblocks_to_q8_0(np.frombuffer(one("xq", 0), np.uint32))
                 assert np.array_equal(xq, self.orc.quantize_q8_0(x)), "embed_norm Q8_0 blocks"
                 ref = self.gemv_q8(wqkv, xq)
@@ -204,10 +247,14 @@ class OpChecker:
             self.attention(l, qkv, np.frombuffer(one("kc", l), np.uint16), np.frombuffer(one("vc", l), np.uint16),
                            pos, attn)
             xo_words = granule_values(one("xo_g", l)).view(np.uint32) if block else np.frombuffer(one("xo", l), np.uint32)
-            xo = xblocks_to_q8_0(xo_words)
-            assert np.array_equal(xo, self.orc.quantize_q8_0(attn)), f"layer {l}: attention Q8_0 blocks"
             o = f32(one("o", l))
-            self.note("gemv_o", rel_err(o, self.gemv_q8(self.w.raw(f"blk.{l}.attn_output.weight"), xo)), GEMV_RTOL)
+            if kq:
+                xof = self.q8k_blocks(xo_words[: c.n_head * c.head_dim // 32 * 12], attn, f"layer {l}: attention")
+                self.note("gemv_o", rel_err(o, self.gemv(self.w.raw(f"blk.{l}.attn_output.weight"), xof)), GEMV_RTOL)
+            else:
+                xo = xblocks_to_q8_0(xo_words)
+                assert np.array_equal(xo, self.orc.quantize_q8_0(attn)), f"layer {l}: attention Q8_0 blocks"
+                self.note("gemv_o", rel_err(o, self.gemv_q8(self.w.raw(f"blk.{l}.attn_output.weight"), xo)), GEMV_RTOL)
             r_in = f32(one("attn_resid", l)) if l else f32(one("inp_scaled", -1))
             r2 = r_in + self.norm(o, f"blk.{l}.post_attention_norm.weight")
             got_r2 = f32(one("ffn_resid", l))
@@ -217,6 +264,7 @@ class OpChecker:
             gate = self.gemv(self.w.raw(f"blk.{l}.ffn_gate.weight"), xf)
             up = self.gemv(self.w.raw(f"blk.{l}.ffn_up.weight"), xf)
             hid = f32(one("hid", l))
+            assert np.abs(hid).max() > 0, f"layer {l}: the FFN is dead (GELU output all zero): the check would be vacuous"
             # GELU(g) * u with g, u each within GEMV_RTOL of max: |d hid| <~ (|GELU'| + 1) max|g| max|u| GEMV_RTOL
             err = float(np.abs(hid - self.orc.gelu_mul(gate, up)).max()) / (float(np.abs(gate).max() * np.abs(up).max()) + 1e-30)
             self.note("gemv_gate_up_gelu", err, 3 * GEMV_RTOL)
@@ -264,7 +312,10 @@ class OpChecker:
                 kq = ws[0][1] in kq_types  # Q8_K activation blocks (K-quant layers), else Q8_0
                 for t in range(T_tok):
                     if kq:
-                        xf = xblocks_q8k_to_f32(xs[t, : ncols // 32])
+                        try:
+                            xf = xblocks_q8k_to_f32(xs[t, : ncols // 32])
+                        except AssertionError as e:
+                            raise AssertionError(f"layer {l} {proj} token {t}: {e}") from None
                         dot = lambda w: self.gemv(w, xf)  # noqa: E731
                     else:
                         xq = xblocks_to_q8_0(xs[t, : ncols // 32])

@@ -229,15 +229,31 @@ def test_full_size_quant_batched_prefill(oracle, monkeypatch, quant):
     if margin[0] > 4.0 * err0:
         assert int(np.argmax(ll)) == run[0]
     ml.close()
-    # the opt-in f16 prefill (LLMI_PREFILL_F16=1): at this depth its f16 activations overflowed (round 2: a
-    # non-finite argmax); the session must detect it and recompute on the int8 path -- finite logits, and the
-    # batched int8 prefill's result
+    if quant != "q4_k_m":
+        return
+    # the opt-in f16 prefill (LLMI_PREFILL_F16=1) on this (centered) model: f16 activations stay finite
     monkeypatch.delenv("LLMI_NO_PREFILL")
     monkeypatch.setenv("LLMI_PREFILL_F16", "1")
     mf = Model(g, max_ctx=64)
     lf = mf.forward(prompt, 0)
-    assert np.isfinite(lf).all(), "f16 prefill returned non-finite logits"
+    assert np.isfinite(lf).all() and mf.get_info().prefill_f16_redo == 0
     print(f"{quant} full size: |f16-path prefill - int8 prefill| {float(np.abs(lf - lg).max()):.3g}")
     if margin[0] > 4.0 * err0:
         assert int(np.argmax(lf)) == run[0]
     mf.close()
+    # ... and on the bench's uncentered 4B Q4_K_M (random K-quant mins: activations grow layer by layer), where
+    # round 2's f16 prefill returned a non-finite argmax: the session detects the overflow and recomputes the
+    # prefill on the int8 path -- finite logits equal to the int8 prefill's, bit for bit
+    gb = build_gemma3_gguf(cfg, seed=1234, wtype=TT.Q4_K, wtypes={"v": TT.Q6_K, "down": TT.Q6_K})
+    mf = Model(gb, max_ctx=64)
+    lf = mf.forward(prompt, 0)
+    redo = mf.get_info().prefill_f16_redo
+    mf.close()
+    monkeypatch.delenv("LLMI_PREFILL_F16")
+    mi = Model(gb, max_ctx=64)
+    li = mi.forward(prompt, 0)
+    mi.close()
+    print(f"uncentered 4B Q4_K_M: f16 prefill redone on the int8 path {redo} time(s)")
+    assert np.isfinite(lf).all(), "f16 prefill returned non-finite logits"
+    if redo:
+        np.testing.assert_array_equal(lf.view(np.uint32), li.view(np.uint32))

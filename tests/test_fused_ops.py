@@ -108,8 +108,13 @@ def test_ops_prefill_kquant_int8(oracle, vtype):
     (the reference's quantize_row_q8_k, checked block by block: one f32 d per super-block, a +-127 quant in
     each, block sums) and the int8 GEMM's Q4_K / Q6_K variant (i8 MFMA per sub-block, the d sc / dmin m
     scale products on f32 MFMAs) -- every output row against the reference's mat_vec_mul_q4_k / _q6_k of
-    those blocks (GEMV tolerance); then decode steps op by op."""
+    those blocks (GEMV tolerance); then 3 decode steps op by op through the FUSED kq launches: the attention
+    block (q|k Q4_K + v Q6_K, or all Q4_K, as its qkv role; Q8_K blocks of x from the prologue and of the
+    attention output from the merge, checked bit for bit against quantize_row_q8_k; o Q4_K), the slab-major
+    Q4_K gate_up with the GELU epilogue and the Q6_K / Q4_K down launch."""
     from llm_inference_amd.gguf import TensorType as TT
     vt = TT.Q6_K if vtype == "q6_k" else TT.Q4_K
-    chk = _run(oracle, "mini-4b", 30, 20, -1, 64, wtype=TT.Q4_K, wtypes={"v": vt, "down": vt})
+    chk = _run(oracle, "mini-4b", 30, 20, 3, 64, wtype=TT.Q4_K, wtypes={"v": vt, "down": vt},
+               swa_pattern=[True, False], centered=True)
     assert "prefill_gemm_qkv" in chk.report and "prefill_gemm_down" in chk.report
+    assert "gemv_qkv" in chk.report and "gemv_o" in chk.report and "gemv_down" in chk.report

@@ -146,18 +146,24 @@ def test_prefill_attention_mfma_vs_vector(cfg_name, n_prompt, monkeypatch):
 
 
 @pytest.mark.parametrize("mode", ["int8", "f16"])
-def test_kquant_batched_prefill(monkeypatch, mode):
-    """Q4_K_M layer shapes (BASELINE configs[3]) through the batched prefill instead of the token loop.
-    int8 (default): Q8_K activation blocks (the decode's quantization) and the int8 GEMM's K-quant variant --
-    the fast budget vs the token loop, the same greedy continuation, exact under re-chunking.  f16 (opt-in,
-    LLMI_PREFILL_F16=1: f16 activations, GEMM v6 on the kq weights): the same ids and chunk-exactness; its gap
-    to the token loop (f16 activations there, Q8_K blocks in the loop) is reported, not bounded by the Q8
-    budget.  The K-quant minis are more sensitive than the Q4_0 ones (logits ~100):
-    over seeds 33 / 35 / 36 and 32-200 tokens the int8 gap is 0.01-0.1, next to the token loop's own
-    per-projection layout (LLMI_NO_FUSE) at 0.003-0.08 on the same inputs, with one outlier (seed 33, 150
-    tokens: 0.53, control 0.08) -- scripts/dev/kqp_diag3.py; op by op the path is exact
-    (tests/test_fused_ops.py::test_ops_prefill_kquant_int8)."""
-    n_prompt = 100 if mode == "int8" else 150
+def test_kquant_batched_prefill(monkeypatch, oracle, mode):
+    """Q4_K_M layer shapes (BASELINE configs[3]) through the batched prefill instead of the token loop, at the
+    case round 2 shortened the test to hide (seed 33, 150 tokens: 0.53 between the two paths).
+
+    Root cause (scripts/dev/kqp_root.py, gpurun_out record in DESIGN.md section 5): this input is
+    ILL-CONDITIONED for attention rounding.  The reference's own arithmetic (the oracle: f16 V accumulator
+    rounded at every key, model.cpp:481-547) and the same arithmetic with exact (f64) attention differ by 0.567
+    in logits of magnitude ~100.  Both device paths are fp32-class attentions (the batched prefill's P.V on
+    f16 MFMA inputs, the token loop's fp32 split-K), so they land within that spread of the reference: batched
+    0.149 from the oracle, token loop 0.417 -- the 0.53 between them is the input's attention sensitivity, not
+    a defect of either path.  Over other seeds / lengths (the same script) that sensitivity is 0.04-0.12 and
+    every path is within 0.16 of the oracle.
+
+    Stated bound (the fast budget of tests/test_hip_model.py widened by the input's measured conditioning):
+    |device - reference| <= FAST_VS_REF + |reference - reference with f64 attention| for each path, the same
+    argmax, the same greedy continuation; chunk-exact.  f16 (opt-in LLMI_PREFILL_F16=1: f16 activations,
+    GEMM v6 on the kq weights): the same ids and chunk-exactness; its gap is reported."""
+    n_prompt = 150
     if mode == "f16":
         monkeypatch.setenv("LLMI_PREFILL_F16", "1")
     from llm_inference_amd.gguf import TensorType as TT
@@ -172,10 +178,16 @@ def test_kquant_batched_prefill(monkeypatch, mode):
     ml = _model(g, monkeypatch, no_prefill=True)
     ll = ml.forward(prompt, 0)
     ids_l = ml.generate(int(np.argmax(ll)), len(prompt), 8)
+    ref = oracle.model(g, n_threads=16, max_ctx=256).forward(prompt, 0)
+    ref64 = oracle.model(g, n_threads=16, max_ctx=256, attn_f64=True).forward(prompt, 0)
+    cond = float(np.abs(ref - ref64).max())
     d = float(np.abs(lp - ll).max())
-    print(f"mini-4b Q4_K_M n={len(prompt)}: max|{mode} batched prefill - token loop| = {d:.3g}")
+    dp, dl = float(np.abs(lp - ref).max()), float(np.abs(ll - ref).max())
+    print(f"mini-4b Q4_K_M n={len(prompt)}: |reference - f64-attention reference| {cond:.3g}; |{mode} batched "
+          f"prefill - reference| {dp:.3g}; |token loop - reference| {dl:.3g}; |batched - token loop| {d:.3g}")
+    assert dl <= FAST_VS_REF + cond
     if mode == "int8":
-        assert d <= FAST_VS_REF
-    assert int(np.argmax(lp)) == int(np.argmax(ll))
+        assert dp <= FAST_VS_REF + cond
+    assert int(np.argmax(lp)) == int(np.argmax(ll)) == int(np.argmax(ref))
     assert ids_p.tolist() == ids_l.tolist()
     np.testing.assert_array_equal(_model(g, monkeypatch, chunk=41).forward(prompt, 0), lp)
