@@ -193,6 +193,8 @@ typedef struct {
   size_t screen_bytes;        /* bytes of the int8 screening table streamed per decode-loop token */
   int prefill_f16_redo;       /* opt-in f16 prefills (LLMI_PREFILL_F16) whose f16 activations overflowed and were
                                  recomputed on the int8 path (never a non-finite result) */
+  int layer_engine;           /* 1: each decode layer is ONE launch of the layer engine (one 1024-thread work-group
+                                 per CU, the layer's weights issued at launch start: DESIGN.md section 4.3) */
 } llmi_session_info;
 int llmi_session_get_info(const llmi_session* s, llmi_session_info* info);
 
@@ -203,7 +205,8 @@ int llmi_session_get_info(const llmi_session* s, llmi_session_info* info);
  *       history read at the session's current position),
  *   1 = F16 logits GEMV, 2 = the decode loop's screened token selection,
  *   3 = gate_up (+ norm prologue + GELU), 4 = down (+ Q8_0 prologue),
- *   5 = qkv / o / gate_up / down as standalone layer GEMVs (round-1 family).
+ *   5 = qkv / o / gate_up / down as standalone layer GEMVs (round-1 family),
+ *   6 = the layer engine (one launch per decode layer: qkv + attention + o + gate_up + down).
  * Returns the mean microseconds and the mean algorithmic bytes per launch
  * (0 / 0 when the family does not exist on this session). */
 int llmi_session_time_kernel(llmi_session* s, int which, int reps, double* us_per_launch, double* bytes_per_launch);

@@ -82,7 +82,7 @@ void upload_rows(DevWeight& w, int dst_row0, const void* host, int rows, hipStre
   }
 }
 
-DevWeight alloc_weight(uint32_t type, int rows, int cols) {
+DevWeight alloc_weight(uint32_t type, int rows, int cols, size_t slack) {
   if (!gemv_type_supported(type))
     throw std::runtime_error("mat_vec_mul: unsupported tensor type " + std::to_string(type));
   DevWeight w;
@@ -92,10 +92,10 @@ DevWeight alloc_weight(uint32_t type, int rows, int cols) {
   w.bytes = gguf_bytes(type, rows, cols);
   if (type == T_Q4_0 || type == T_Q8_0) {
     const size_t nblk = (size_t)rows * (cols / 32);
-    LLMI_HIP(hipMalloc(&w.qs, nblk * (type == T_Q4_0 ? 16 : 32) + 64));
-    LLMI_HIP(hipMalloc((void**)&w.d, nblk * 2 + 64));
+    LLMI_HIP(hipMalloc(&w.qs, nblk * (type == T_Q4_0 ? 16 : 32) + slack));
+    LLMI_HIP(hipMalloc((void**)&w.d, nblk * 2 + slack));
   } else {
-    LLMI_HIP(hipMalloc(&w.qs, w.bytes + 64));
+    LLMI_HIP(hipMalloc(&w.qs, w.bytes + slack));
   }
   return w;
 }

@@ -71,7 +71,7 @@ float* Session::dev_f32_copy(const GGUFView& g, const GTensor* t, int n) {
   if (!t) return nullptr;
   if (t->type != T_F32) throw status_error(LLMI_E_TYPE, "norm weight " + t->name + " is not F32");
   if ((int)t->shape[0] < n) throw status_error(LLMI_E_SIZE, "norm weight " + t->name + " too short");
-  float* d = dalloc<float>(t->shape[0]);
+  float* d = dalloc<float>(t->shape[0] + 256);  // + 1 KB: the layer engine copies norm vectors in whole 1-KB pieces
   LLMI_HIP(hipMemcpy(d, g.tensor_data(*t), t->shape[0] * 4, hipMemcpyHostToDevice));
   return d;
 }
@@ -624,6 +624,7 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
       for (const auto& l : L_) maxhd = std::max(maxhd, l.hd);
       blk_xo_ = dalloc<XBlock>((size_t)nh_ * maxhd / 32 + 1);
     }
+    setup_engine(g);
   } catch (const gguf_error& e) {
     release();
     throw status_error(LLMI_E_GGUF, e.what());
@@ -655,6 +656,13 @@ void Session::release() {
     free_weight(l.ple_proj.w);
   }
   L_.clear();
+  for (auto& e : eng_w_) {
+    free_weight(e.q);
+    free_weight(e.o);
+    free_weight(e.g);
+    free_weight(e.d);
+  }
+  eng_w_.clear();
   for (auto& p : ple_model_proj_) free_weight(p.w);
   ple_model_proj_.clear();
   ple_table_ = DevWeight{};  // its bytes are an allocs_ entry
@@ -761,7 +769,9 @@ void Session::record_step(hipStream_t s, bool gen) {
   bool fused = fuse_layers_;
   for (const auto& l : L_) fused &= l.fused;
   if (tp_ && !fused) throw status_error(LLMI_E_ARG, "tensor parallel needs the fused layer path");
-  if (fused) {
+  if (fused && engine_ && !dump_ && !trace_fn_) {
+    record_layers_engine(s, x_q8);
+  } else if (fused) {
     record_layers_fused(s, x_q8);
   } else {
     record_layers(s, x_q8);
@@ -1022,6 +1032,140 @@ bool Session::prefill_run(const int32_t* tokens, int n, int pos, bool allow_f16)
 // GELU epilogue], down [+ Q8_0 of the GELU output]).  The residual stream
 // ping-pongs between resid_ and resid2_ (a prologue's work-group 0 writes the
 // buffer its sibling work-groups are not reading).
+// The layer engine (k_engine.hip): Gemma-3 layers whose four projections are Q4_0,
+// head_dim 256, two q heads per (virtual) kv head, on one device.  Opt-in (LLMI_ENGINE=1): measured slower than
+// the three launches per layer (attention block, gate_up, down) -- 38 vs 29 us per 4B layer; the layer's weight
+// stream, issued at launch start, queues every cross-CU hand-off behind it (profiles/r03_engine_trace.txt).
+// Dumps and op-level traces always use the three launches.
+void Session::setup_engine(const GGUFView& g) {
+  engine_ = false;
+  const char* on = getenv("LLMI_ENGINE");
+  if (!on || atoi(on) == 0) return;
+  if (!fuse_layers_ || tp_ || !dup_.empty() || ple_table_.qs || hp_.gemma4) return;
+  if (embd_.type != T_F16 && embd_.type != T_Q8_0) return;
+  for (const auto& l : L_) {
+    const bool q40 = l.qkv.size() == 1 && l.qkv[0].w.type == T_Q4_0 && l.o.w.type == T_Q4_0 &&
+                     l.gate_up.size() == 1 && l.gate_up[0].w.type == T_Q4_0 && l.down.w.type == T_Q4_0;
+    if (!l.fused || !q40 || !l.has_kv || l.hd != 256 || l.out_scale != 1.0f || l.qkv_rows != L_[0].qkv_rows ||
+        !l.post_ffw_norm || !l.post_attn_norm || !l.ffn_norm || !l.attn_norm || !l.q_norm || !l.k_norm)
+      return;
+  }
+  EngineLayer plan;
+  if (!engine_plan(hp_.n_embd, hp_.n_ff, nh_, nkv_, 256, L_[0].qkv_rows, plan)) return;
+  const int E = hp_.n_embd, F = hp_.n_ff, H = plan.ru;
+  constexpr size_t kSlack = 8192;  // the down rows are read in whole 1-KB LDS-DMA pieces
+  eng_w_.resize(hp_.n_layer);
+  for (int l = 0; l < hp_.n_layer; l++) {
+    const std::string b = "blk." + std::to_string(l) + ".";
+    const GTensor *q = g.tensor(b + "attn_q.weight"), *k = g.tensor(b + "attn_k.weight"), *v = g.tensor(b + "attn_v.weight");
+    const GTensor *o = g.tensor(b + "attn_output.weight"), *gt = g.tensor(b + "ffn_gate.weight");
+    const GTensor *up = g.tensor(b + "ffn_up.weight"), *dn = g.tensor(b + "ffn_down.weight");
+    EngWeights& w = eng_w_[l];
+    w.q = alloc_weight(T_Q4_0, L_[l].qkv_rows, E, kSlack);
+    int r0 = 0;
+    for (const GTensor* t : {q, k, v}) {
+      const int n = (int)t->shape[1];
+      upload_rows(w.q, r0, g.tensor_data(*t), n, stream_);
+      r0 += n;
+    }
+    w.o = alloc_weight(T_Q4_0, E, (int)o->shape[0], kSlack);
+    upload_rows(w.o, 0, g.tensor_data(*o), E, stream_);
+    // gate / up interleaved in groups of H = n_ff / CUs: CU c's 2H rows are one contiguous run
+    const size_t rb = gguf_bytes(T_Q4_0, 1, E);
+    std::vector<uint8_t> il((size_t)2 * F * rb);
+    const uint8_t *sg = (const uint8_t*)g.tensor_data(*gt), *su = (const uint8_t*)g.tensor_data(*up);
+    for (int c = 0; c < F / H; c++) {
+      std::memcpy(&il[(size_t)(2 * H * c) * rb], sg + (size_t)(H * c) * rb, H * rb);
+      std::memcpy(&il[(size_t)(2 * H * c + H) * rb], su + (size_t)(H * c) * rb, H * rb);
+    }
+    w.g = alloc_weight(T_Q4_0, 2 * F, E, kSlack);
+    upload_rows(w.g, 0, il.data(), 2 * F, stream_);
+    w.d = alloc_weight(T_Q4_0, E, F, kSlack);
+    upload_rows(w.d, 0, g.tensor_data(*dn), E, stream_);
+  }
+  eng_ = plan;
+  eng_epoch_ = dalloc<unsigned>(1);
+  eng_gqkv_ = dalloc<uint2>(L_[0].qkv_rows);
+  eng_gxo_ = dalloc<uint2>((size_t)nh_ * 256 / 32 * 12);
+  eng_go_ = dalloc<uint2>(E);
+  eng_ghid_ = dalloc<uint2>(F);
+  eng_zero_ = dalloc<uint4>(256);
+  if (!blk_err_) blk_err_ = dalloc<int>(2);
+  if (!blk_trace_)
+    if (const char* tr = getenv("LLMI_BLOCK_TRACE")) {  // development: per-CU phase clocks of one layer
+      blk_trace_layer_ = atoi(tr);
+      blk_trace_ = dalloc<unsigned long long>(4096 * 8);
+    }
+  engine_ = true;
+}
+
+EngineLayer Session::engine_args(int l, float* resid_in, float* resid_out) const {
+  const LayerDev& Ld = L_[l];
+  const EngWeights& w = eng_w_[l];
+  EngineLayer a = eng_;
+  a.q_qs = (const uint4*)w.q.qs;
+  a.q_d = w.q.d;
+  a.o_qs = (const uint4*)w.o.qs;
+  a.o_d = w.o.d;
+  a.g_qs = (const uint4*)w.g.qs;
+  a.g_d = w.g.d;
+  a.d_qs = (const uint4*)w.d.qs;
+  a.d_d = w.d.d;
+  a.k_off = Ld.k_off;
+  a.v_off = Ld.v_off;
+  a.w_post = l > 0 ? L_[l - 1].post_ffw_norm : Ld.post_ffw_norm;  // (layer 0 reads x0 instead)
+  a.attn_norm = Ld.attn_norm;
+  a.q_norm = Ld.q_norm;
+  a.k_norm = Ld.k_norm;
+  a.post_attn_norm = Ld.post_attn_norm;
+  a.ffn_norm = Ld.ffn_norm;
+  a.y_in = d_out_;  // every CU reads it before any CU writes this layer's rows (those follow the GELU exchange)
+  a.x0 = act_.q8.xb;
+  a.resid_in = resid_in;
+  a.resid_out = resid_out;
+  a.y_out = d_out_;
+  a.rope_cs = Ld.is_swa ? rope_swa_ : rope_glb_;
+  a.attn_scale = hp_.attn_scale;
+  a.eps = hp_.eps;
+  a.k_cache = Ld.kc;
+  a.v_cache = Ld.vc;
+  a.max_ctx = max_ctx_;
+  a.d_pos = d_pos_;
+  a.partial = part_;
+  a.ticket = ticket_;
+  a.zero = eng_zero_;
+  a.epoch = eng_epoch_;
+  a.g_qkv = eng_gqkv_;
+  a.g_xo = eng_gxo_;
+  a.g_o = eng_go_;
+  a.g_hid = eng_ghid_;
+  a.err = blk_err_;
+  return a;
+}
+
+void Session::record_layers_engine(hipStream_t s, bool x_q8) {
+  const int E = hp_.n_embd;
+  if (!x_q8) {  // layer 0 reads the Q8_0 blocks of attn_norm(embedding)
+    launch_quantize_q8_0(xn_, E, act_.q8, s);
+    kernels_per_token_++;
+  }
+  float* cur = resid_;
+  float* other = resid2_;
+  for (int l = 0; l < hp_.n_layer; l++) {
+    EngineLayer a = engine_args(l, cur, other);
+    if (blk_trace_ && l == blk_trace_layer_) a.trace = blk_trace_;
+    launch_layer_engine(a, l == 0, s);
+    kernels_per_token_++;
+    std::swap(cur, other);
+  }
+  // final residual + output_norm (-> xn_, and f16 x for an F16 logits table)
+  NormOut o2;
+  o2.xn = xn_;
+  if (embd_.type == T_F16) o2.x16 = act_.x16;
+  launch_residual_norm(d_out_, L_.back().post_ffw_norm, cur, out_norm_, o2, E, hp_.eps, false, s);
+  kernels_per_token_++;
+}
+
 void Session::record_layers_fused(hipStream_t s, bool x_q8) {
   const int E = hp_.n_embd;
   float* cur = resid_;
@@ -1486,6 +1630,7 @@ void Session::info(llmi_session_info* o) const {
   o->screened_logits = screen_ ? 1 : 0;
   o->screen_bytes = screen_ ? scr_.bytes : 0;
   o->prefill_f16_redo = pf_f16_redo_;
+  o->layer_engine = engine_ ? 1 : 0;
   size_t b = logits_w_.bytes;  // this rank's bytes
   for (const auto& l : L_) {
     for (const auto& p : l.qkv) b += p.w.bytes;
@@ -1561,7 +1706,7 @@ void Session::time_kernel(int which, int reps, double* us, double* bytes) {
   //   5: the r01 family: qkv PRO, o PLAIN, gate_up, down as standalone launches
   bool fused = fuse_layers_;
   for (const auto& l : L_) fused &= l.fused;
-  if (!fused || (which == 0 && !block_) || which < 0 || which > 5 || reps <= 0) {
+  if (!fused || (which == 0 && !block_) || (which == 6 && !engine_) || which < 0 || which > 6 || reps <= 0) {
     *us = *bytes = 0.0;
     return;
   }
@@ -1604,6 +1749,12 @@ void Session::time_kernel(int which, int reps, double* us, double* bytes) {
                                            Ld.o.w, go, aa, qa, bs, stream_);
                        },
                        (double)Ld.qkv[0].w.bytes + (double)Ld.o.w.bytes + kv});
+    }
+    if (which == 6) {  // the layer engine: the whole layer, its own weights, the KV history at the current pos
+      const double kv = 2.0 * nkv_ * hd * 2.0 * (pos + 1);
+      const EngineLayer ea = engine_args((int)i, resid_, resid_scratch_);
+      items.push_back({[this, ea]() { launch_layer_engine(ea, false, stream_); },
+                       (double)(Ld.qkv[0].w.bytes + Ld.o.w.bytes + Ld.gate_up[0].w.bytes + Ld.down.w.bytes) + kv});
     }
     if (which == 5) {
       items.push_back({[this, &Ld, q]() { launch_layer_gemv(Ld.qkv[0].w, q, LAYER_PRO, stream_); },

@@ -92,6 +92,9 @@ class Session {
   void ensure_prefill_buffers(int cap);
   void record_layers(hipStream_t s, bool x_q8);
   void record_layers_fused(hipStream_t s, bool x_q8);
+  void setup_engine(const GGUFView& g);
+  void record_layers_engine(hipStream_t s, bool x_q8);
+  EngineLayer engine_args(int l, float* resid_in, float* resid_out) const;
   void prepare_act(uint32_t wtype, const float* x, int n, ActBuf& act, hipStream_t s);
   void gemv_parts(const std::vector<GemvPart>& parts, const float* x, int n_in, float* out, hipStream_t s,
                   bool x_ready);
@@ -122,6 +125,15 @@ class Session {
   bool exact_ = false, use_graph_ = true;
   bool fuse_layers_ = false;  // fast path: norms / GELU folded into the Q4_0 GEMVs
   bool block_ = false;        // fast path: qkv + attention + o as one launch per layer (k_attn.hip)
+  // the layer engine (k_engine.hip): a whole decode layer per launch, one 1024-thread work-group per CU;
+  // its own row-major copies of the four projections (gate/up interleaved in groups of eng_.ru)
+  bool engine_ = false;
+  EngineLayer eng_{};                     // the per-CU split (engine_plan)
+  struct EngWeights { DevWeight q, o, g, d; };
+  std::vector<EngWeights> eng_w_;
+  unsigned* eng_epoch_ = nullptr;
+  uint2 *eng_gqkv_ = nullptr, *eng_gxo_ = nullptr, *eng_go_ = nullptr, *eng_ghid_ = nullptr;
+  uint4* eng_zero_ = nullptr;
   unsigned* blk_epoch_ = nullptr;  // [n_layer] attention-block launch counts (granule tags)
   uint2* blk_gqkv_ = nullptr;      // [n_layer][qkv rows] granules
   // Gemma-4 per-layer inputs (model.cpp:568-704)

@@ -8,7 +8,7 @@ namespace llmi {
 
 size_t gguf_bytes(uint32_t type, size_t rows, size_t cols);
 bool gemv_type_supported(uint32_t type);
-DevWeight alloc_weight(uint32_t type, int rows, int cols);
+DevWeight alloc_weight(uint32_t type, int rows, int cols, size_t slack = 64);  // slack: bytes allocated past qs / d
 void upload_rows(DevWeight& w, int dst_row0, const void* host, int rows, hipStream_t s);
 void free_weight(DevWeight& w);
 // Q4_0 row-major blocks -> slab-major (k_layer.hip's a.slab layout): slabs of
@@ -76,6 +76,41 @@ struct BlockSync {
   int* err = nullptr;               // set when a bounded wait gives up (the step's results are invalid)
   unsigned long long* trace = nullptr;  // development: [work-group][8] wall clocks (LLMI_BLOCK_TRACE)
 };
+// The layer engine (k_engine.hip): one Gemma-3 decode layer, Q4_0 weights, as one
+// persistent launch of one 1024-thread work-group per CU.
+struct EngineLayer {
+  // row-major Q4_0 weights (qs [rows][nb] 16-B blocks, d [rows][nb] f16), each
+  // allocated with >= 4 KB of slack (the down rows are copied in whole 1-KB pieces)
+  const uint4 *q_qs = nullptr, *o_qs = nullptr, *g_qs = nullptr, *d_qs = nullptr;
+  const uint16_t *q_d = nullptr, *o_d = nullptr, *g_d = nullptr, *d_d = nullptr;
+  int E = 0, Fu = 0;              // n_embd, n_ff
+  int nq = 0, k_off = 0, v_off = 0;  // qkv rows (q | k | v) and the k / v offsets
+  int n_head = 0, n_kv = 0, kvd = 1;  // kvd: virtual kv heads (2 q heads each) per cache head
+  int rq = 0, ro = 0, ru = 0, rd = 0;  // per CU: qkv rows, o rows, gate/up units (gate_up interleaved in groups of ru), down rows
+  const float *w_post = nullptr, *attn_norm = nullptr, *q_norm = nullptr, *k_norm = nullptr;
+  const float *post_attn_norm = nullptr, *ffn_norm = nullptr;
+  const float* y_in = nullptr;    // previous layer's down output (layer > 0)
+  const XBlock* x0 = nullptr;     // layer 0: the Q8_0 blocks of attn_norm(embedding)
+  const float* resid_in = nullptr;
+  float* resid_out = nullptr;
+  float* y_out = nullptr;
+  const float* rope_cs = nullptr;
+  float attn_scale = 1.0f;
+  double eps = 0;
+  uint16_t *k_cache = nullptr, *v_cache = nullptr;
+  int max_ctx = 0;
+  const int* d_pos = nullptr;
+  float* partial = nullptr;   // [n_head][ATTN_NSPLIT][head_dim + 2]
+  unsigned* ticket = nullptr;  // [n_kv kvd], zeroed, reset by the merging work-group
+  const uint4* zero = nullptr;  // >= 512 B of zeros (K / V rows past the context)
+  unsigned* epoch = nullptr;    // launch count: granule tag = *epoch + 1
+  uint2 *g_qkv = nullptr, *g_xo = nullptr, *g_o = nullptr, *g_hid = nullptr;
+  int* err = nullptr;
+  unsigned long long* trace = nullptr;  // development: [CU][16] phase clocks (LLMI_BLOCK_TRACE builds)
+};
+// fills the per-CU split of `a` and checks the launch fits (shapes, LDS, occupancy)
+bool engine_plan(int E, int F, int n_head, int n_kv, int hd, int qkv_rows, EngineLayer& a);
+void launch_layer_engine(const EngineLayer& a, bool first, hipStream_t s);
 bool layer_gemv_supported(const DevWeight& w, int role);
 // ---- batched prefill (k_prefill.hip) ----
 struct PrefillNorm {  // per token: embedding (table != null) or residual + norm, then x -> Q8_0
