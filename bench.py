@@ -297,14 +297,16 @@ def main():
     fams = {}
     # (with the layer engine the whole layer is ONE launch: info.layer_engine, family 6)
     engine = bool(getattr(info, "layer_engine", 0))
+    ffn = bool(getattr(info, "ffn_engine", 0))
+    in_graph = {6: engine, 0: not engine, 7: ffn and not engine, 3: not (engine or ffn), 4: not (engine or ffn),
+                2: bool(info.screened_logits)}
     for name, which, per_tok, kern in (("layer_engine", 6, L, "layer_engine_kernel"),
                                        ("attention_block", 0, L, "attn_block_kernel"),
+                                       ("ffn_engine", 7, L, "ffn_engine_kernel"),
                                        ("gate_up", 3, L, "gemv_q4_0_layer"),
                                        ("down", 4, L, "gemv_q4_0_layer"),
                                        ("token_selection", 2, 1, "screen_gemv_kernel")):
-        if which == 2 and not info.screened_logits:
-            continue
-        if (which == 6) != engine and which != 2:  # only the families the timed graph launches
+        if not in_graph[which]:  # only the families the timed graph launches
             continue
         us_f, by_f = m.time_kernel(which, a.kernel_reps if which != 2 else 8)
         if us_f <= 0:
@@ -316,7 +318,7 @@ def main():
     us_l, by_l = m.time_kernel(1, 2)
     dom_name = max(fams, key=lambda k: fams[k]["us_per_token"]) if fams else None
     dom = fams.get(dom_name, {})
-    kpat = {"layer_engine": "layer_engine_kernel", "attention_block": "attn_block_kernel", "gate_up": "gemv_q4_0_layer<8, 10, 10",
+    kpat = {"layer_engine": "layer_engine_kernel", "ffn_engine": "ffn_engine_kernel", "attention_block": "attn_block_kernel", "gate_up": "gemv_q4_0_layer<8, 10, 10",
             "down": "gemv_q4_0_layer<1, 10, 5", "token_selection": "screen_gemv_kernel"}.get(dom_name, "-")
     traffic, traffic_src = pmc_traffic(kpat, pmc_key(a))
     # the timed steps decode positions pos .. pos + steps - 1; the step at

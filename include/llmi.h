@@ -195,6 +195,7 @@ typedef struct {
                                  recomputed on the int8 path (never a non-finite result) */
   int layer_engine;           /* 1: each decode layer is ONE launch of the layer engine (one 1024-thread work-group
                                  per CU, the layer's weights issued at launch start: DESIGN.md section 4.3) */
+  int ffn_engine;             /* 1: gate_up + GELU + down of each layer are ONE launch (the FFN engine) */
 } llmi_session_info;
 int llmi_session_get_info(const llmi_session* s, llmi_session_info* info);
 
@@ -206,7 +207,8 @@ int llmi_session_get_info(const llmi_session* s, llmi_session_info* info);
  *   1 = F16 logits GEMV, 2 = the decode loop's screened token selection,
  *   3 = gate_up (+ norm prologue + GELU), 4 = down (+ Q8_0 prologue),
  *   5 = qkv / o / gate_up / down as standalone layer GEMVs (round-1 family),
- *   6 = the layer engine (one launch per decode layer: qkv + attention + o + gate_up + down).
+ *   6 = the layer engine (one launch per decode layer: qkv + attention + o + gate_up + down),
+ *   7 = the FFN engine (gate_up + GELU + down, one launch per layer).
  * Returns the mean microseconds and the mean algorithmic bytes per launch
  * (0 / 0 when the family does not exist on this session). */
 int llmi_session_time_kernel(llmi_session* s, int which, int reps, double* us_per_launch, double* bytes_per_launch);

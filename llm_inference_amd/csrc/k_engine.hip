@@ -245,15 +245,67 @@ __host__ __device__ inline EngLds eng_lds(const EngineLayer& a, int hd, int g) {
   return L;
 }
 
+// the FFN engine's carve-up: down rows, the gate_up products / GELU blocks + down products, x2
+__host__ __device__ inline EngLds eng_ffn_lds(const EngineLayer& a) {
+  const int nbE = a.E / 32, nbF = a.Fu / 32, ud = a.rd * nbF;
+  EngLds L{};
+  int o = 0;
+  L.dq = o;
+  o += eng_align(ud * 16);
+  L.dd = o;
+  o += eng_align(ud * 2);
+  const int kv_g = 2 * a.ru * nbE * 4, kv_d = eng_align(nbF * (int)sizeof(XBlock)) + ud * 4;
+  L.kv = o;
+  o += eng_align(kv_g > kv_d ? kv_g : kv_d);
+  L.x = o;
+  o += eng_align(nbE * (int)sizeof(XBlock));
+  L.total = o;
+  return L;
+}
+
 namespace {
+
+// barrier of the four comm waves only (the worker waves are streaming weights meanwhile): an LDS arrival
+// counter; n counts this thread's barriers x ENG_CW (uniform over the comm waves)
+__device__ __forceinline__ void eng_cbar(unsigned* c, unsigned& n) {
+  n += ENG_CW;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's LDS writes are done before it arrives
+  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  while (__hip_atomic_load(c, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < n) __builtin_amdgcn_s_sleep(0);
+  asm volatile("" ::: "memory");
+}
+
+// sum over the comm waves (fixed order); red: ENG_CW floats not in use by another sum
+__device__ __forceinline__ float eng_csum(float v, float* red, unsigned* c, unsigned& n) {
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  eng_cbar(c, n);
+  return (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// row sums by NWV waves (rows w, w + NWV, ...; out(r, sum) by lane 0)
+template <int NWV, class F>
+__device__ __forceinline__ void eng_row_sums_n(const float* sv, int nrows, int nb, F&& out) {
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane = threadIdx.x & 63;
+  for (int r = w; r < nrows; r += NWV) {
+    float s = 0.0f;
+    for (int j = lane; j < nb; j += 64) s += sv[r * nb + j];
+    s = wave_sum(s);
+    if (lane == 0) out(r, s);
+  }
+}
 
 template <int HD, int G, int PQ, int PO, int PG, bool FIRST>
 __global__ __launch_bounds__(ENG_T) void layer_engine_kernel(EngineLayer a) {
   extern __shared__ __attribute__((aligned(1024))) unsigned char s_dyn[];
   constexpr int NS = ATTN_NSPLIT, TK = ENG_TK, CH = HD / 8, DPL = HD / 64;
   static_assert(HD == 256 && G == 2, "engine attention: head_dim 256, 2 q heads per (virtual) kv head");
-  static_assert(G * TK * 16 == ENG_T, "scores: 16 lanes per (head, key) pair");
+  constexpr int CT = ENG_CW * 64;  // comm threads
+  static_assert(CT % (G * TK) == 0, "scores: whole lane groups per (head, key) pair");
+  constexpr int LPP = CT / (G * TK);  // lanes per (head, key) pair
   __shared__ float s_red[2][ENG_NW];
+  __shared__ float s_cred[2][ENG_CW];
+  __shared__ unsigned s_cbar;
   __shared__ __attribute__((aligned(16))) float s_raw[(G + 2) * HD];
   __shared__ __attribute__((aligned(16))) uint16_t s_q[G][HD];
   __shared__ __attribute__((aligned(16))) uint16_t s_new[2][HD];
@@ -269,7 +321,7 @@ __global__ __launch_bounds__(ENG_T) void layer_engine_kernel(EngineLayer a) {
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const bool cw = w < ENG_CW;
-  const int wl = t - ENG_CW * 64;  // worker lane (waves 4-15)
+  const int wl = t - CT;  // worker lane (waves 4-15)
   const int cu = blockIdx.x;
   const int E = a.E, nbE = E / 32, nbO = a.n_head * HD / 32, nbF = a.Fu / 32;
   const EngLds L = eng_lds(a, HD, G);
@@ -289,14 +341,13 @@ __global__ __launch_bounds__(ENG_T) void layer_engine_kernel(EngineLayer a) {
   const int pos = *a.d_pos;
   const int n4 = E / 4;
   const bool pt = t < n4;  // prologue threads: elements 4t .. 4t + 3 (whole octets: E % 32 == 0)
+  if (t == 0) s_cbar = 0;
 
-  // ---- P0: loads, issued in the order they are needed ----------------------
-  // Loads leave each CU roughly in issue order, so a latency-critical load issued behind the layer's
-  // weight slices waits for them (phase trace: the prologue operands behind 207 KB per CU took 10 us).
-  // Raw barriers (no memory wait) put every wave's prologue operands, then every wave's qkv rows,
-  // ahead of the bulk; the gate_up rows are issued after the qkv GEMV, the down rows after the attention.
-  // Unconditional loads (threads past E / 4 re-read the last float4, masked below): no phi copies, so
-  // no wait before the weights are issued.
+  // ---- P0: the prologue's operands, then the qkv rows (raw barriers order the issue) ----
+  // Memory queues are first-come-first-served across the chip, so a latency-critical load issued while a
+  // bulk stream is in flight waits for its backlog (profiles/r03_engine_trace.txt).  Here only the qkv rows
+  // are issued with the prologue; the gate_up and down rows are streamed by the worker waves at a bounded
+  // depth while the comm waves run the attention and the o projection (P3-P5).
   const int ti = min(t, n4 - 1);
   const float4 r4i = reinterpret_cast<const float4*>(a.resid_in)[ti];
   float4 y4 = make_float4(0.f, 0.f, 0.f, 0.f), p4 = y4, nw4 = y4;
@@ -309,14 +360,11 @@ __global__ __launch_bounds__(ENG_T) void layer_engine_kernel(EngineLayer a) {
     for (int i = t; i < nbE * 3; i += ENG_T) reinterpret_cast<uint4*>(s_x)[i] = reinterpret_cast<const uint4*>(a.x0)[i];
   }
   __builtin_amdgcn_s_barrier();
-  // attention unit of this CU: (virtual kv head, key split), as the attention block's b % n, b / n
   const int nvh = a.n_kv * a.kvd;
   const bool attn_cu = cu < nvh * NS;
   const int hkv = attn_cu ? cu % nvh : 0, split = attn_cu ? cu / nvh : 0, hkc = hkv / a.kvd;
   const int n_keys = pos + 1;
-  // K / V tile `tile` -> s_k / s_v ([TK][HD] f16, rows contiguous) by LDS-DMA, 2 rows per wave
-  // instruction; keys past the context read zeros (the cache beyond pos may hold stale or NaN bits)
-  auto dma_tile = [&](int tile) {
+  auto dma_tile = [&](int tile) {  // comm waves: K / V tile -> s_k / s_v, 2 rows per wave instruction
     for (int i = w; i < TK; i += ENG_CW) {
       const bool isv = i >= TK / 2;
       const int ii = isv ? i - TK / 2 : i;
@@ -327,20 +375,18 @@ __global__ __launch_bounds__(ENG_T) void layer_engine_kernel(EngineLayer a) {
       eng_glds16(src, (isv ? s_v : s_k) + ii * 2 * HD);
     }
   };
-  // Worker weight slices (rows [c R, c R + R) of a row-major Q4_0 matrix are one contiguous run).  Unit
-  // u = p LW + j (j < LW, LW = (768 / nb) nb) is block j % nb of row u / nb, so a lane's activation block
-  // is the same in every pass (read from LDS once).  Every wave issues the same loads -- the comm waves'
-  // descriptors are empty (out of bounds: zeros, no traffic) -- so hipcc's s_waitcnt counts agree on
-  // every path.
-  const int lwq = (ENG_LW / nbE) * nbE, lwo = (ENG_LW / nbO) * nbO;
+  // worker slices: unit u = p LW + j (j < LW = (768 / nb) nb) is block j % nb of row u / nb, so a lane's
+  // activation block is fixed across passes; every wave issues the same loads (empty descriptors for the
+  // comm waves), so hipcc's s_waitcnt counts agree on every path
+  const int lwq = (ENG_LW / nbE) * nbE, lwo = (CT / nbO) * nbO;
   const int nrq = max(0, min(a.nq - cu * a.rq, a.rq)), nro = max(0, min(E - cu * a.ro, a.ro));
   const int nrd = max(0, min(E - cu * a.rd, a.rd));
   const int Uq = nrq * nbE, Uo = nro * nbO, Ug = 2 * a.ru * nbE, Ud = nrd * nbF;
   const uint32_t on = cw ? 0u : 1u;
-  const int jq = cw ? lwq : wl, jo = cw ? lwo : wl;  // comm waves and idle worker lanes: out of bounds
-  const bool okq = jq < lwq, oko = jo < lwo;
-  uint4 wq[PQ], wo[PO], wg[PG];
-  uint16_t sq[PQ], so[PO], sg[PG];
+  const int jq = cw ? lwq : wl;
+  const bool okq = jq < lwq;
+  uint4 wq[PQ], wg[PG];
+  uint16_t sq[PQ], sg[PG];
   {
     const __amdgpu_buffer_rsrc_t rq = buf_rsrc(a.q_qs + (size_t)cu * a.rq * nbE, on * Uq * 16),
                                  rqd = buf_rsrc(a.q_d + (size_t)cu * a.rq * nbE, on * Uq * 2);
@@ -351,30 +397,8 @@ __global__ __launch_bounds__(ENG_T) void layer_engine_kernel(EngineLayer a) {
       sq[p] = buf_ld2(rqd, u * 2, 0);
     }
   }
-  __builtin_amdgcn_s_barrier();
-  if (cw) {
-    if (attn_cu) dma_tile(split);
-    // P5's norm weights into LDS (whole 1-KB pieces: the session's norm vectors have >= 1 KB of slack)
-    const int nk = (E * 4 + 1023) / 1024;
-    for (int i = w; i < 2 * nk; i += ENG_CW) {
-      const bool f = i >= nk;
-      const int ii = f ? i - nk : i;
-      eng_glds16(reinterpret_cast<const unsigned char*>(f ? a.ffn_norm : a.post_attn_norm) + ii * 1024 + lane * 16,
-                 s_dyn + (f ? L.fn : L.pn) + ii * 1024);
-    }
-  }
-  {
-    const __amdgpu_buffer_rsrc_t ro = buf_rsrc(a.o_qs + (size_t)cu * a.ro * nbO, on * Uo * 16),
-                                 rod = buf_rsrc(a.o_d + (size_t)cu * a.ro * nbO, on * Uo * 2);
-#pragma unroll
-    for (int p = 0; p < PO; p++) {
-      const int u = oko ? p * lwo + jo : (1 << 24);
-      wo[p] = buf_ld16(ro, u * 16, 0);
-      so[p] = buf_ld2(rod, u * 2, 0);
-    }
-  }
 
-  // ---- P1: residual + post_ffw norm + attn_norm -> Q8_0 x -----------------
+  // ---- P1: residual + post_ffw norm + attn_norm -> Q8_0 x (all waves) ------
   float4 r4 = r4i;
   if constexpr (!FIRST) {
     if (!pt) y4 = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -406,7 +430,7 @@ __global__ __launch_bounds__(ENG_T) void layer_engine_kernel(EngineLayer a) {
   __syncthreads();
   ENG_MARK(1);
 
-  // ---- P2: qkv rows -> granules --------------------------------------------
+  // ---- P2: qkv rows -> granules (all waves) --------------------------------
   if (!cw && okq) {
     const XBlock* xb = s_x + jq % nbE;
 #pragma unroll
@@ -417,8 +441,14 @@ __global__ __launch_bounds__(ENG_T) void layer_engine_kernel(EngineLayer a) {
   }
   __syncthreads();
   ENG_MARK(12);
-  // the gate_up rows, now that the qkv rows are consumed (issued after the barrier: not hoisted above the qkv dots)
-  {
+  eng_row_sums(s_vq, nrq, nbE, [&](int r, float v) { st_granule(a.g_qkv + cu * a.rq + r, __float_as_uint(v), tag); });
+  ENG_MARK(2);
+
+  if (!cw) {
+    // ---- worker waves: the gate_up rows (registers), then the down rows (LDS-DMA), at most DEPTH passes
+    // of 1 KB per wave in flight (12 waves x DEPTH KB per CU, a few MB chip-wide), so the comm waves' hand-offs
+    // do not queue behind the layer's 44 MB ----
+    constexpr int DEPTH = 3;
     const __amdgpu_buffer_rsrc_t rg = buf_rsrc(a.g_qs + (size_t)cu * 2 * a.ru * nbE, on * Ug * 16),
                                  rgd = buf_rsrc(a.g_d + (size_t)cu * 2 * a.ru * nbE, on * Ug * 2);
 #pragma unroll
@@ -426,136 +456,162 @@ __global__ __launch_bounds__(ENG_T) void layer_engine_kernel(EngineLayer a) {
       const int u = okq ? p * lwq + jq : (1 << 24);
       wg[p] = buf_ld16(rg, u * 16, 0);
       sg[p] = buf_ld2(rgd, u * 2, 0);
+      if (p >= DEPTH) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * DEPTH) : "memory");
     }
-  }
-  eng_row_sums(s_vq, nrq, nbE, [&](int r, float v) { st_granule(a.g_qkv + cu * a.rq + r, __float_as_uint(v), tag); });
-  ENG_MARK(2);
-
-  // ---- P3: attention (one (virtual kv head, split) per CU c < n_kv kvd NSPLIT) ----
-  if (attn_cu) {
-    const int own_tile = pos / TK;
-    const bool own_new = own_tile % NS == split;
-    if (cw) {  // this head group's q rows, the k row and the v row from their granules
-      constexpr int K = ((G + 2) * HD / 4 + ENG_CW * 64 - 1) / (ENG_CW * 64);
-      int off[K];
-      bool act[K];
-      uint32_t u[K][4];
-#pragma unroll
-      for (int k = 0; k < K; k++) {
-        const int e = (k * ENG_CW * 64 + t) * 4;
-        act[k] = e < (G + 2) * HD;
-        off[k] = e < G * HD         ? hkv * G * HD + e
-                 : e < (G + 1) * HD ? a.k_off + hkc * HD + (e - G * HD)
-                                    : a.v_off + hkc * HD + (e - (G + 1) * HD);
+    const unsigned char* dq = reinterpret_cast<const unsigned char*>(a.d_qs + (size_t)cu * a.rd * nbF);
+    const unsigned char* dd = reinterpret_cast<const unsigned char*>(a.d_d + (size_t)cu * a.rd * nbF);
+    const int nqi = (Ud * 16 + 1023) / 1024, ndi = (Ud * 2 + 1023) / 1024;
+    for (int i = w - ENG_CW; i < nqi + ndi; i += ENG_NW - ENG_CW) {
+      if (i < nqi) eng_glds16(dq + i * 1024 + lane * 16, s_dyn + L.dq + i * 1024);
+      else eng_glds16(dd + (i - nqi) * 1024 + lane * 16, s_dyn + L.dd + (i - nqi) * 1024);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DEPTH) : "memory");
+    }
+  } else {
+    // ---- comm waves: P3 attention, P4 o projection, P5 residual + norms (comm-wave barriers only) ----
+    unsigned nb_c = 0;
+    uint4 wo[PO];
+    uint16_t so[PO];
+    const int jo = t, oko = jo < lwo;
+    {  // the o rows (comm registers), the K / V tile and the FFN norm weights
+      if (attn_cu) dma_tile(split);
+      const int nk = (E * 4 + 1023) / 1024;
+      for (int i = w; i < 2 * nk; i += ENG_CW) {
+        const bool f = i >= nk;
+        const int ii = f ? i - nk : i;
+        eng_glds16(reinterpret_cast<const unsigned char*>(f ? a.ffn_norm : a.post_attn_norm) + ii * 1024 + lane * 16,
+                   s_dyn + (f ? L.fn : L.pn) + ii * 1024);
       }
-      eng_sweep<K>(u, a.g_qkv, off, act, tag, a.err);
+      const __amdgpu_buffer_rsrc_t ro = buf_rsrc(a.o_qs + (size_t)cu * a.ro * nbO, (uint32_t)Uo * 16),
+                                   rod = buf_rsrc(a.o_d + (size_t)cu * a.ro * nbO, (uint32_t)Uo * 2);
 #pragma unroll
-      for (int k = 0; k < K; k++)
-        if (act[k]) *reinterpret_cast<float4*>(s_raw + (k * ENG_CW * 64 + t) * 4) = u4f(u[k]);
+      for (int p = 0; p < PO; p++) {
+        const int u = oko ? p * lwo + jo : (1 << 24);
+        wo[p] = buf_ld16(ro, u * 16, 0);
+        so[p] = buf_ld2(rod, u * 2, 0);
+      }
     }
-    __syncthreads();
-    ENG_MARK(3);
-    if (w < G + 2) {  // per-row norm + NEOX rope (model.cpp:762-767, 792-794): waves 0..G-1 q heads, G the k row, G+1 v
-      const int i0 = lane * DPL;
-      float v[DPL];
+    // ---- P3: attention (one (virtual kv head, split) per CU c < n_kv kvd NSPLIT) ----
+    if (attn_cu) {
+      const int own_tile = pos / TK;
+      const bool own_new = own_tile % NS == split;
+      {  // this head group's q rows, the k row and the v row from their granules
+        constexpr int K = ((G + 2) * HD / 4 + CT - 1) / CT;
+        int off[K];
+        bool act[K];
+        uint32_t u[K][4];
 #pragma unroll
-      for (int d = 0; d < DPL; d++) v[d] = s_raw[w * HD + i0 + d];
-      if (w <= G) {
-        const float* nwp = (w < G ? a.q_norm : a.k_norm) + i0;
-        const int j0 = i0 < HD / 2 ? i0 : i0 - HD / 2;
-        const float* cs = a.rope_cs + (size_t)pos * (HD / 2) * 2 + 2 * j0;
-        float nw[DPL], c[DPL], sn[DPL];
-#pragma unroll
-        for (int d = 0; d < DPL; d++) {
-          nw[d] = nwp[d];
-          c[d] = cs[2 * d];
-          sn[d] = cs[2 * d + 1];
+        for (int k = 0; k < K; k++) {
+          const int e = (k * CT + t) * 4;
+          act[k] = e < (G + 2) * HD;
+          off[k] = e < G * HD         ? hkv * G * HD + e
+                   : e < (G + 1) * HD ? a.k_off + hkc * HD + (e - G * HD)
+                                      : a.v_off + hkc * HD + (e - (G + 1) * HD);
         }
-        float ss = 0.0f;
+        eng_sweep<K>(u, a.g_qkv, off, act, tag, a.err);
 #pragma unroll
-        for (int d = 0; d < DPL; d++) ss = fmaf(v[d], v[d], ss);
-        ss = wave_sum(ss);
-        const float sc = 1.0f / sqrtf((float)((double)(ss / (float)HD) + a.eps));
+        for (int k = 0; k < K; k++)
+          if (act[k]) *reinterpret_cast<float4*>(s_raw + (k * CT + t) * 4) = u4f(u[k]);
+      }
+      eng_cbar(&s_cbar, nb_c);
+      ENG_MARK(3);
+      if (w < G + 2) {  // per-row norm + NEOX rope (model.cpp:762-767, 792-794): waves 0..G-1 q heads, G the k row, G+1 v
+        const int i0 = lane * DPL;
+        float v[DPL];
 #pragma unroll
-        for (int d = 0; d < DPL; d++) {
-          const int i = i0 + d;
-          const float n = (sc * v[d]) * nw[d];
-          const float pn = __shfl_xor(n, 32);
-          const float r = i < HD / 2 ? fmaf(n, c[d], -(pn * sn[d])) : fmaf(pn, sn[d], n * c[d]);
-          if (w < G) {
-            s_q[w][i] = f2h_ggml(r * a.attn_scale);
-          } else {
-            const uint16_t k16 = f2h_ggml(r);
-            s_new[0][i] = k16;
-            if (own_new && hkv % a.kvd == 0) a.k_cache[((size_t)hkc * a.max_ctx + pos) * HD + i] = k16;
+        for (int d = 0; d < DPL; d++) v[d] = s_raw[w * HD + i0 + d];
+        if (w <= G) {
+          const float* nwp = (w < G ? a.q_norm : a.k_norm) + i0;
+          const int j0 = i0 < HD / 2 ? i0 : i0 - HD / 2;
+          const float* cs = a.rope_cs + (size_t)pos * (HD / 2) * 2 + 2 * j0;
+          float nw[DPL], c[DPL], sn[DPL];
+#pragma unroll
+          for (int d = 0; d < DPL; d++) {
+            nw[d] = nwp[d];
+            c[d] = cs[2 * d];
+            sn[d] = cs[2 * d + 1];
+          }
+          float ss = 0.0f;
+#pragma unroll
+          for (int d = 0; d < DPL; d++) ss = fmaf(v[d], v[d], ss);
+          ss = wave_sum(ss);
+          const float sc = 1.0f / sqrtf((float)((double)(ss / (float)HD) + a.eps));
+#pragma unroll
+          for (int d = 0; d < DPL; d++) {
+            const int i = i0 + d;
+            const float n = (sc * v[d]) * nw[d];
+            const float pn = __shfl_xor(n, 32);
+            const float r = i < HD / 2 ? fmaf(n, c[d], -(pn * sn[d])) : fmaf(pn, sn[d], n * c[d]);
+            if (w < G) {
+              s_q[w][i] = f2h_ggml(r * a.attn_scale);
+            } else {
+              const uint16_t k16 = f2h_ggml(r);
+              s_new[0][i] = k16;
+              if (own_new && hkv % a.kvd == 0) a.k_cache[((size_t)hkc * a.max_ctx + pos) * HD + i] = k16;
+            }
+          }
+        } else {
+#pragma unroll
+          for (int d = 0; d < DPL; d++) {
+            const uint16_t v16 = f2h_ggml(v[d]);
+            s_new[1][i0 + d] = v16;
+            if (own_new && hkv % a.kvd == 0) a.v_cache[((size_t)hkc * a.max_ctx + pos) * HD + i0 + d] = v16;
           }
         }
-      } else {
-#pragma unroll
-        for (int d = 0; d < DPL; d++) {
-          const uint16_t v16 = f2h_ggml(v[d]);
-          s_new[1][i0 + d] = v16;
-          if (own_new && hkv % a.kvd == 0) a.v_cache[((size_t)hkc * a.max_ctx + pos) * HD + i0 + d] = v16;
-        }
       }
-    }
-    if (cw) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the first tile's LDS-DMA
-    __syncthreads();
-    float m_run = -INFINITY, l_run = 0.0f;  // head w's running max / sum (waves w < G)
-    float acc[G][4];
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the first tile's LDS-DMA (landed long ago: the polls waited)
+      eng_cbar(&s_cbar, nb_c);
+      float m_run = -INFINITY, l_run = 0.0f;  // head w's running max / sum (waves w < G)
+      float acc[G][4];
 #pragma unroll
-    for (int g = 0; g < G; g++)
+      for (int g = 0; g < G; g++)
 #pragma unroll
-      for (int e = 0; e < 4; e++) acc[g][e] = 0.0f;
-    const int d_own = 4 * lane, kp = w;  // PV (comm threads): 4 head dims, key class w
-    typedef _Float16 h2t __attribute__((ext_vector_type(2)));
-    for (int tile = split; tile * TK < n_keys; tile += NS) {
-      if (tile != split) {  // later tiles (contexts past NSPLIT * TK keys): loaded here
-        if (cw) {
+        for (int e = 0; e < 4; e++) acc[g][e] = 0.0f;
+      const int d_own = 4 * lane, kp = w;  // PV: 4 head dims, key class w
+      typedef _Float16 h2t __attribute__((ext_vector_type(2)));
+      for (int tile = split; tile * TK < n_keys; tile += NS) {
+        if (tile != split) {  // later tiles (contexts past NSPLIT * TK keys): loaded here
           dma_tile(tile);
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          eng_cbar(&s_cbar, nb_c);
         }
-        __syncthreads();
-      }
-      if (tile == own_tile) {  // this token's k / v row, written in this launch
-        const int j = pos % TK;
-        if (t < CH) reinterpret_cast<uint4*>(s_k + j * HD)[t] = reinterpret_cast<const uint4*>(s_new[0])[t];
-        else if (t < 2 * CH) reinterpret_cast<uint4*>(s_v + j * HD)[t - CH] = reinterpret_cast<const uint4*>(s_new[1])[t - CH];
-        __syncthreads();
-      }
-      {  // scores: 16 lanes per (head, key), chunks part and part + 16 of the 32 16-B chunks
-        const int pr = t >> 4, part = t & 15, g = pr / TK, j = pr % TK;
-        const uint4* krow = reinterpret_cast<const uint4*>(s_k + j * HD);
-        const uint4* qrow = reinterpret_cast<const uint4*>(s_q[g]);
-        float s0 = 0.0f, s1 = 0.0f;
+        if (tile == own_tile) {  // this token's k / v row, written in this launch
+          const int j = pos % TK;
+          if (t < CH) reinterpret_cast<uint4*>(s_k + j * HD)[t] = reinterpret_cast<const uint4*>(s_new[0])[t];
+          else if (t < 2 * CH) reinterpret_cast<uint4*>(s_v + j * HD)[t - CH] = reinterpret_cast<const uint4*>(s_new[1])[t - CH];
+          eng_cbar(&s_cbar, nb_c);
+        }
+        {  // scores: LPP lanes per (head, key); each lane 32 / LPP chunks, the chunk order rotated by the key
+           // (conflict-free LDS reads of unpadded rows)
+          const int pr = t / LPP, part = t % LPP, g = pr / TK, j = pr % TK;
+          const uint4* krow = reinterpret_cast<const uint4*>(s_k + j * HD);
+          const uint4* qrow = reinterpret_cast<const uint4*>(s_q[g]);
+          float s0 = 0.0f, s1 = 0.0f;
 #pragma unroll
-        for (int i = 0; i < 2; i++) {
-          const uint4 kk = krow[part + 16 * i], qq = qrow[part + 16 * i];
-          s0 = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2t, kk.x), __builtin_bit_cast(h2t, qq.x), s0, false);
-          s1 = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2t, kk.y), __builtin_bit_cast(h2t, qq.y), s1, false);
-          s0 = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2t, kk.z), __builtin_bit_cast(h2t, qq.z), s0, false);
-          s1 = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2t, kk.w), __builtin_bit_cast(h2t, qq.w), s1, false);
+          for (int i = 0; i < CH / LPP; i++) {
+            const int c = (part + LPP * i + LPP * j) & (CH - 1);
+            const uint4 kk = krow[c], qq = qrow[c];
+            s0 = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2t, kk.x), __builtin_bit_cast(h2t, qq.x), s0, false);
+            s1 = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2t, kk.y), __builtin_bit_cast(h2t, qq.y), s1, false);
+            s0 = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2t, kk.z), __builtin_bit_cast(h2t, qq.z), s0, false);
+            s1 = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2t, kk.w), __builtin_bit_cast(h2t, qq.w), s1, false);
+          }
+          float sc = s0 + s1;
+#pragma unroll
+          for (int o = 1; o < LPP; o <<= 1) sc += __shfl_xor(sc, o);
+          if (part == 0) s_p[g][j] = tile * TK + j < n_keys ? sc : -INFINITY;
         }
-        float sc = s0 + s1;
-        sc += __shfl_xor(sc, 8);
-        sc += __shfl_xor(sc, 4);
-        sc += __shfl_xor(sc, 2);
-        sc += __shfl_xor(sc, 1);
-        if (part == 0) s_p[g][j] = tile * TK + j < n_keys ? sc : -INFINITY;
-      }
-      __syncthreads();
-      if (w < G) {
-        const float sc = lane < TK ? s_p[w][lane] : -INFINITY;
-        const float m_new = fmaxf(m_run, wave_max(sc));
-        const float p = expf(sc - m_new);          // masked keys: exp(-inf) = 0
-        const float alpha = expf(m_run - m_new);   // first tile: exp(-inf) = 0
-        l_run = l_run * alpha + wave_sum(p);
-        m_run = m_new;
-        if (lane < TK) s_p[w][lane] = p;
-        if (lane == 0) s_alpha[w] = alpha;
-      }
-      __syncthreads();
-      if (cw) {
+        eng_cbar(&s_cbar, nb_c);
+        if (w < G) {
+          const float sc = lane < TK ? s_p[w][lane] : -INFINITY;
+          const float m_new = fmaxf(m_run, wave_max(sc));
+          const float p = expf(sc - m_new);          // masked keys: exp(-inf) = 0
+          const float alpha = expf(m_run - m_new);   // first tile: exp(-inf) = 0
+          l_run = l_run * alpha + wave_sum(p);
+          m_run = m_new;
+          if (lane < TK) s_p[w][lane] = p;
+          if (lane == 0) s_alpha[w] = alpha;
+        }
+        eng_cbar(&s_cbar, nb_c);
 #pragma unroll
         for (int g = 0; g < G; g++) {
           const float al = s_alpha[g];
@@ -576,184 +632,182 @@ __global__ __launch_bounds__(ENG_T) void layer_engine_kernel(EngineLayer a) {
             acc[g][3] = fmaf(p, v3, acc[g][3]);
           }
         }
+        eng_cbar(&s_cbar, nb_c);  // the tile's LDS is reused by the next one
       }
-      __syncthreads();  // the tile's LDS is reused by the next one
-    }
-    // the 4 key classes -> the split's partial (sc1 stores), then the head's ticket
-    if (cw && kp > 0) {
+      // the 4 key classes -> the split's partial (sc1 stores), then the head's ticket
+      if (kp > 0) {
 #pragma unroll
-      for (int g = 0; g < G; g++)
-        *reinterpret_cast<float4*>(s_pv + ((kp * G + g) * HD + d_own)) = make_float4(acc[g][0], acc[g][1], acc[g][2], acc[g][3]);
-    }
-    __syncthreads();
-    float* part0 = a.partial + (size_t)hkv * G * NS * (HD + 2);  // [G][NS][HD + 2]
-    if (w == 0) {
+        for (int g = 0; g < G; g++)
+          *reinterpret_cast<float4*>(s_pv + ((kp * G + g) * HD + d_own)) = make_float4(acc[g][0], acc[g][1], acc[g][2], acc[g][3]);
+      }
+      eng_cbar(&s_cbar, nb_c);
+      float* part0 = a.partial + (size_t)hkv * G * NS * (HD + 2);  // [G][NS][HD + 2]
+      if (w == 0) {
 #pragma unroll
-      for (int g = 0; g < G; g++) {
-        for (int r = 1; r < ENG_CW; r++) {
-          const float4 o = *reinterpret_cast<const float4*>(s_pv + ((r * G + g) * HD + d_own));
-          acc[g][0] += o.x;
-          acc[g][1] += o.y;
-          acc[g][2] += o.z;
-          acc[g][3] += o.w;
+        for (int g = 0; g < G; g++) {
+          for (int r = 1; r < ENG_CW; r++) {
+            const float4 o = *reinterpret_cast<const float4*>(s_pv + ((r * G + g) * HD + d_own));
+            acc[g][0] += o.x;
+            acc[g][1] += o.y;
+            acc[g][2] += o.z;
+            acc[g][3] += o.w;
+          }
+#pragma unroll
+          for (int e = 0; e < 4; e++) st_sc1(part0 + ((size_t)g * NS + split) * (HD + 2) + d_own + e, acc[g][e]);
         }
-#pragma unroll
-        for (int e = 0; e < 4; e++) st_sc1(part0 + ((size_t)g * NS + split) * (HD + 2) + d_own + e, acc[g][e]);
       }
-    }
-    if (w < G && lane == 0) {
-      st_sc1(part0 + ((size_t)w * NS + split) * (HD + 2) + HD, m_run);
-      st_sc1(part0 + ((size_t)w * NS + split) * (HD + 2) + HD + 1, l_run);
-    }
-    if (cw) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t == 0) {
-      const unsigned old = __hip_atomic_fetch_add(a.ticket + hkv, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_flag = old == NS - 1 ? 1 : old == NS - 2 ? 2 : 0;
-    }
-    __syncthreads();
-    int role = s_flag;
-    if (role == 2) {  // second-to-last: merges head 0 once the last ticket is in (bounded wait)
-      __syncthreads();  // every thread has read s_flag
+      if (w < G && lane == 0) {
+        st_sc1(part0 + ((size_t)w * NS + split) * (HD + 2) + HD, m_run);
+        st_sc1(part0 + ((size_t)w * NS + split) * (HD + 2) + HD + 1, l_run);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      eng_cbar(&s_cbar, nb_c);
       if (t == 0) {
-        int n = 0;
-        s_flag = 2;
-        while (__hip_atomic_load(a.ticket + hkv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)NS) {
-          if (++n >= BLOCK_SPIN_LIMIT) {
-            __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_flag = 0;  // no merge from incomplete partials, no ticket reset (the host zeroes the tickets)
-            break;
+        const unsigned old = __hip_atomic_fetch_add(a.ticket + hkv, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_flag = old == NS - 1 ? 1 : old == NS - 2 ? 2 : 0;
+      }
+      eng_cbar(&s_cbar, nb_c);
+      int role = s_flag;
+      if (role == 2) {  // second-to-last: merges head 0 once the last ticket is in (bounded wait)
+        eng_cbar(&s_cbar, nb_c);  // every thread has read s_flag
+        if (t == 0) {
+          int n = 0;
+          s_flag = 2;
+          while (__hip_atomic_load(a.ticket + hkv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)NS) {
+            if (++n >= BLOCK_SPIN_LIMIT) {
+              __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              s_flag = 0;  // no merge from incomplete partials, no ticket reset (the host zeroes the tickets)
+              break;
+            }
           }
         }
+        eng_cbar(&s_cbar, nb_c);
+        role = s_flag;
       }
-      __syncthreads();
-      role = s_flag;
-    }
-    if (role != 0) {
-      const int g0 = role == 1 ? 1 : 0;
-      const float* pg = part0 + (size_t)g0 * NS * (HD + 2);
-      const int n_act = min(NS, (n_keys + TK - 1) / TK);
-      float mv = -INFINITY, lv = 0.0f;
-      float v[NS];
-      if (cw) {
+      if (role != 0) {
+        const int g0 = role == 1 ? 1 : 0;
+        const float* pg = part0 + (size_t)g0 * NS * (HD + 2);
+        const int n_act = min(NS, (n_keys + TK - 1) / TK);
+        float mv = -INFINITY, lv = 0.0f;
+        float v[NS];
         if (t < NS) {
           mv = ld_sc1(pg + t * (HD + 2) + HD);
           lv = ld_sc1(pg + t * (HD + 2) + HD + 1);
         }
-        // splits without keys (c TK >= n_keys: weight 0) are read out of bounds: 0, no traffic
         const __amdgpu_buffer_rsrc_t rp = buf_rsrc(pg, (uint32_t)(NS * (HD + 2) * 4));
 #pragma unroll
         for (int cc = 0; cc < NS; cc++)
           v[cc] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rp, cc < n_act ? (cc * (HD + 2) + t) * 4 : (1 << 30), 0, BUF_SC1));
-        if (w == 0) {  // lanes 0-31: the splits' (m, l); the half-wave reductions of k_attn.hip's merge
+        if (w == 0) {  // lanes 0-31: the splits' (m, l)
           const float M = half_max(mv);
           const float wt = lv == 0.0f ? 0.0f : expf(mv - M);
           const float Ls = half_sum(lv * wt);
           if (t < NS) s_wt[t] = wt;
           if (t == 0) s_L = Ls;
         }
-      }
-      __syncthreads();
-      if (cw) {
+        eng_cbar(&s_cbar, nb_c);
         float o = 0.0f;
 #pragma unroll
         for (int cc = 0; cc < NS; cc++) o = fmaf(v[cc], s_wt[cc], o);
         s_mo[t] = o / s_L;
+        eng_cbar(&s_cbar, nb_c);
+        if (t < HD / 4) q8_block_oct(reinterpret_cast<const float4*>(s_mo)[t], t & 7, s_mq + (t >> 3));
+        eng_cbar(&s_cbar, nb_c);
+        if (t < HD / 32 * 12)
+          st_granule(a.g_xo + ((size_t)(hkv * G + g0) * HD / 32) * 12 + t, reinterpret_cast<const uint32_t*>(s_mq)[t], tag);
+        if (role == 2 && t == 0) __hip_atomic_store(a.ticket + hkv, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      __syncthreads();
-      if (t < HD / 4) q8_block_oct(reinterpret_cast<const float4*>(s_mo)[t], t & 7, s_mq + (t >> 3));
-      __syncthreads();
-      if (t < HD / 32 * 12)
-        st_granule(a.g_xo + ((size_t)(hkv * G + g0) * HD / 32) * 12 + t, reinterpret_cast<const uint32_t*>(s_mq)[t], tag);
-      if (role == 2 && t == 0) __hip_atomic_store(a.ticket + hkv, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-  }
-  // the down rows by LDS-DMA, after the attention (the session allocates >= 8 KB past every engine
-  // weight: whole 1-KB pieces)
-  if (!cw) {
-    const unsigned char* dq = reinterpret_cast<const unsigned char*>(a.d_qs + (size_t)cu * a.rd * nbF);
-    const unsigned char* dd = reinterpret_cast<const unsigned char*>(a.d_d + (size_t)cu * a.rd * nbF);
-    const int nqi = (Ud * 16 + 1023) / 1024, ndi = (Ud * 2 + 1023) / 1024;
-    for (int i = w - ENG_CW; i < nqi + ndi; i += ENG_NW - ENG_CW) {
-      if (i < nqi) eng_glds16(dq + i * 1024 + lane * 16, s_dyn + L.dq + i * 1024);
-      else eng_glds16(dd + (i - nqi) * 1024 + lane * 16, s_dyn + L.dd + (i - nqi) * 1024);
-    }
-  }
-  ENG_MARK(4);
-
-  // ---- P4: o rows from the merged blocks -> granules g_o ------------------
-  if (cw) {  // 12 words per block, 4 granules per set
-    for (int i = t; i < nbO * 3; i += ENG_CW * 64) {
+    ENG_MARK(4);
+    // ---- P4: o rows from the merged blocks -> granules g_o (comm waves) ----
+    for (int i = t; i < nbO * 3; i += CT) {  // 12 words per block, 4 granules per set
       int off[1] = {4 * i};
       bool act[1] = {true};
       uint32_t u[1][4];
       eng_sweep<1>(u, a.g_xo, off, act, tag, a.err);
       reinterpret_cast<uint4*>(s_xo)[i] = make_uint4(u[0][0], u[0][1], u[0][2], u[0][3]);
     }
-  }
-  __syncthreads();
-  ENG_MARK(5);
-  if (!cw && oko) {
-    const XBlock* xb = s_xo + jo % nbO;
+    eng_cbar(&s_cbar, nb_c);
+    ENG_MARK(5);
+    if (oko) {
+      const XBlock* xb = s_xo + jo % nbO;
 #pragma unroll
-    for (int p = 0; p < PO; p++) {
-      const int u = p * lwo + jo;
-      if (u < Uo) s_kvf[u] = eng_dot(wo[p], so[p], xb);
-    }
-  }
-  __syncthreads();
-  eng_row_sums(s_kvf, nro, nbO, [&](int r, float v) { st_granule(a.g_o + cu * a.ro + r, __float_as_uint(v), tag); });
-  ENG_MARK(6);
-
-  // ---- P5: residual + post_attn norm + ffn_norm -> Q8_0 x2 ----------------
-  float* s_of = s_kvf + eng_align(E * 4) / 4;  // o, f32 [E] (past the o products still being read)
-  if (cw) {
-    constexpr int K = 3;  // sets per lane in flight per round (the gate_up rows are still in registers)
-    for (int i0 = 0; i0 < n4; i0 += K * ENG_CW * 64) {
-      int off[K];
-      bool act[K];
-      uint32_t u[K][4];
-#pragma unroll
-      for (int k = 0; k < K; k++) {
-        off[k] = 4 * (i0 + k * ENG_CW * 64 + t);
-        act[k] = i0 + k * ENG_CW * 64 + t < n4;
+      for (int p = 0; p < PO; p++) {
+        const int u = p * lwo + jo;
+        if (u < Uo) s_kvf[u] = eng_dot(wo[p], so[p], xb);
       }
-      eng_sweep<K>(u, a.g_o, off, act, tag, a.err);
+    }
+    eng_cbar(&s_cbar, nb_c);
+    eng_row_sums_n<ENG_CW>(s_kvf, nro, nbO, [&](int r, float v) { st_granule(a.g_o + cu * a.ro + r, __float_as_uint(v), tag); });
+    ENG_MARK(6);
+    // ---- P5: residual + post_attn norm + ffn_norm -> Q8_0 x2 (comm waves) ----
+    float* s_of = s_kvf + eng_align(E * 4) / 4;  // o, f32 [E] (past the o products still being read)
+    {
+      constexpr int K = 3;
+      for (int i0 = 0; i0 < n4; i0 += K * CT) {
+        int off[K];
+        bool act[K];
+        uint32_t u[K][4];
 #pragma unroll
-      for (int k = 0; k < K; k++)
-        if (act[k]) reinterpret_cast<float4*>(s_of)[i0 + k * ENG_CW * 64 + t] = u4f(u[k]);
+        for (int k = 0; k < K; k++) {
+          off[k] = 4 * (i0 + k * CT + t);
+          act[k] = i0 + k * CT + t < n4;
+        }
+        eng_sweep<K>(u, a.g_o, off, act, tag, a.err);
+#pragma unroll
+        for (int k = 0; k < K; k++)
+          if (act[k]) reinterpret_cast<float4*>(s_of)[i0 + k * CT + t] = u4f(u[k]);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the norm weights' LDS-DMA
+    eng_cbar(&s_cbar, nb_c);
+    ENG_MARK(13);
+    {
+      constexpr int KE = 4;  // float4 groups per comm thread: E / 4 <= 4 x 256
+      const float4* pn = reinterpret_cast<const float4*>(s_dyn + L.pn);
+      const float4* fn = reinterpret_cast<const float4*>(s_dyn + L.fn);
+      float4 o4[KE], h[KE];
+      float ss = 0.0f;
+#pragma unroll
+      for (int k = 0; k < KE; k++) {
+        const int i = k * CT + t;
+        o4[k] = i < n4 ? reinterpret_cast<const float4*>(s_of)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+        ss = fmaf(o4[k].x, o4[k].x, ss);
+        ss = fmaf(o4[k].y, o4[k].y, ss);
+        ss = fmaf(o4[k].z, o4[k].z, ss);
+        ss = fmaf(o4[k].w, o4[k].w, ss);
+      }
+      const float sc1 = 1.0f / sqrtf((float)((double)(eng_csum(ss, s_cred[0], &s_cbar, nb_c) / (float)E) + a.eps));
+      float ss2 = 0.0f;
+#pragma unroll
+      for (int k = 0; k < KE; k++) {
+        const int i = k * CT + t;
+        if (i < n4) {
+          const float4 r = s_resid[i], p = pn[i];
+          h[k] = make_float4(r.x + (sc1 * o4[k].x) * p.x, r.y + (sc1 * o4[k].y) * p.y, r.z + (sc1 * o4[k].z) * p.z,
+                             r.w + (sc1 * o4[k].w) * p.w);
+          ss2 = fmaf(h[k].x, h[k].x, ss2);
+          ss2 = fmaf(h[k].y, h[k].y, ss2);
+          ss2 = fmaf(h[k].z, h[k].z, ss2);
+          ss2 = fmaf(h[k].w, h[k].w, ss2);
+          if (cu == 0) reinterpret_cast<float4*>(a.resid_out)[i] = h[k];
+        } else {
+          h[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
+      const float sc2 = 1.0f / sqrtf((float)((double)(eng_csum(ss2, s_cred[1], &s_cbar, nb_c) / (float)E) + a.eps));
+#pragma unroll
+      for (int k = 0; k < KE; k++) {
+        const int i = k * CT + t;
+        if (k * CT < n4 && i < n4) {  // whole octets (n4 % 8 == 0)
+          const float4 f = fn[i];
+          q8_block_oct(make_float4((sc2 * h[k].x) * f.x, (sc2 * h[k].y) * f.y, (sc2 * h[k].z) * f.z, (sc2 * h[k].w) * f.w),
+                       i & 7, s_x + (i >> 3));
+        }
+      }
     }
   }
-  __syncthreads();
-  ENG_MARK(13);
-  {
-    const float4 o4 = pt ? reinterpret_cast<const float4*>(s_of)[t] : make_float4(0.f, 0.f, 0.f, 0.f);
-    float ss = 0.0f;
-    ss = fmaf(o4.x, o4.x, ss);
-    ss = fmaf(o4.y, o4.y, ss);
-    ss = fmaf(o4.z, o4.z, ss);
-    ss = fmaf(o4.w, o4.w, ss);
-    const float sc1 = 1.0f / sqrtf((float)((double)(eng_block_sum(ss, s_red[0]) / (float)E) + a.eps));
-    float4 h = make_float4(0.f, 0.f, 0.f, 0.f);
-    float ss2 = 0.0f;
-    if (pt) {
-      const float4 r = s_resid[t], pn = reinterpret_cast<const float4*>(s_dyn + L.pn)[t];
-      h = make_float4(r.x + (sc1 * o4.x) * pn.x, r.y + (sc1 * o4.y) * pn.y, r.z + (sc1 * o4.z) * pn.z,
-                      r.w + (sc1 * o4.w) * pn.w);
-      ss2 = fmaf(h.x, h.x, ss2);
-      ss2 = fmaf(h.y, h.y, ss2);
-      ss2 = fmaf(h.z, h.z, ss2);
-      ss2 = fmaf(h.w, h.w, ss2);
-      if (cu == 0) reinterpret_cast<float4*>(a.resid_out)[t] = h;
-    }
-    const float sc2 = 1.0f / sqrtf((float)((double)(eng_block_sum(ss2, s_red[1]) / (float)E) + a.eps));
-    if (pt) {
-      const float4 fn = reinterpret_cast<const float4*>(s_dyn + L.fn)[t];
-      q8_block_oct(make_float4((sc2 * h.x) * fn.x, (sc2 * h.y) * fn.y, (sc2 * h.z) * fn.z, (sc2 * h.w) * fn.w), t & 7,
-                   s_x + (t >> 3));
-    }
-  }
-  __syncthreads();
+  __syncthreads();  // P6: the comm waves' x2 and the workers' slices meet
   ENG_MARK(7);
 
   // ---- P6: gate_up + GELU -> granules g_hid --------------------------------
@@ -776,29 +830,27 @@ __global__ __launch_bounds__(ENG_T) void layer_engine_kernel(EngineLayer a) {
   }
   ENG_MARK(8);
 
-  // ---- P7: the whole GELU output -> Q8_0 blocks in LDS ---------------------
-  // comm waves: set i = 4 consecutive elements, octets of lanes = one 32-element block (i & 7 = lane & 7);
-  // 5 sets per lane in flight per round
+  // ---- P7: the whole GELU output -> Q8_0 blocks in LDS (comm waves sweep) ----
   XBlock* s_hx = reinterpret_cast<XBlock*>(s_dyn + L.kv);
   float* s_vd = reinterpret_cast<float*>(s_dyn + L.kv + eng_align(nbF * (int)sizeof(XBlock)));
   if (cw) {
     constexpr int K = 5;
     const int nsets = a.Fu / 4;
-    for (int i0 = 0; i0 < nsets; i0 += K * ENG_CW * 64) {  // uniform trip count over the comm waves
+    for (int i0 = 0; i0 < nsets; i0 += K * CT) {
       int off[K];
       bool act[K];
       uint32_t u[K][4];
 #pragma unroll
       for (int k = 0; k < K; k++) {
-        const int i = i0 + k * ENG_CW * 64 + t;
+        const int i = i0 + k * CT + t;
         off[k] = 4 * i;
         act[k] = i < nsets;
       }
       eng_sweep<K>(u, a.g_hid, off, act, tag, a.err);
 #pragma unroll
       for (int k = 0; k < K; k++) {
-        const int i = i0 + k * ENG_CW * 64 + t;
-        if (i0 + k * ENG_CW * 64 < nsets)  // whole octets (nsets % 8 == 0)
+        const int i = i0 + k * CT + t;
+        if (i0 + k * CT < nsets)  // whole octets (nsets % 8 == 0)
           if (i < nsets) q8_block_oct(u4f(u[k]), i & 7, s_hx + (i >> 3));
       }
     }
@@ -819,6 +871,172 @@ __global__ __launch_bounds__(ENG_T) void layer_engine_kernel(EngineLayer a) {
   eng_row_sums(s_vd, nrd, nbF, [&](int r, float v) { a.y_out[cu * a.rd + r] = v; });
   ENG_MARK(10);
   if (cu == 0 && t == 0) *a.epoch = tag;  // every CU read the epoch before any CU got past P7
+}
+
+// ---------------------------------------------------------------------------
+// FFN engine: gate_up + GELU + down of one layer as ONE launch of one 1024-thread work-group per CU, after
+// the attention block (k_attn.hip).  The down rows (LDS-DMA) and the gate_up rows (worker registers) are
+// issued at launch start, behind the prologue operands; the GELU output crosses CUs once (granules, comm-wave
+// sweep) instead of through a launch boundary plus a re-read of the FFN weights' stream start.
+//   P5  every CU: residual + post_attn norm + ffn_norm of o (the block's output) -> Q8_0 x2
+//   P6  gate_up: ru hidden units per CU, GELU(gate) * up -> granules g_hid
+//   P7  every CU: the whole GELU output -> Q8_0 blocks in LDS
+//   P8  down rows [c rd, ..) -> y_out; work-group 0 advances the attention block's epoch (blk_epoch)
+// ---------------------------------------------------------------------------
+template <int PG>
+__global__ __launch_bounds__(ENG_T) void ffn_engine_kernel(EngineLayer a) {
+  extern __shared__ __attribute__((aligned(1024))) unsigned char s_dyn[];
+  __shared__ float s_red[2][ENG_NW];
+  __shared__ float s_gu[256];
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const bool cw = w < ENG_CW;
+  const int wl = t - ENG_CW * 64;
+  const int cu = blockIdx.x;
+  const int E = a.E, nbE = E / 32, nbF = a.Fu / 32;
+  const EngLds L = eng_ffn_lds(a);
+  const uint4* s_dq = reinterpret_cast<const uint4*>(s_dyn + L.dq);
+  const uint16_t* s_dd = reinterpret_cast<const uint16_t*>(s_dyn + L.dd);
+  float* s_kvf = reinterpret_cast<float*>(s_dyn + L.kv);
+  XBlock* s_x = reinterpret_cast<XBlock*>(s_dyn + L.x);
+  ENG_MARK(0);
+  const uint32_t tag = *a.epoch + 1u;
+  const int n4 = E / 4;
+  const bool pt = t < n4;
+  // P0: the prologue operands (unconditional loads, masked below), then the weight slices
+  const int ti = min(t, n4 - 1);
+  const float4 o4i = reinterpret_cast<const float4*>(a.y_in)[ti];
+  const float4 r4 = reinterpret_cast<const float4*>(a.resid_in)[ti];
+  const float4 pn = reinterpret_cast<const float4*>(a.post_attn_norm)[ti];
+  const float4 fn = reinterpret_cast<const float4*>(a.ffn_norm)[ti];
+  __builtin_amdgcn_s_barrier();
+  const int lwq = (ENG_LW / nbE) * nbE;
+  const int nrd = max(0, min(E - cu * a.rd, a.rd));
+  const int Ug = 2 * a.ru * nbE, Ud = nrd * nbF;
+  const uint32_t on = cw ? 0u : 1u;
+  const int jq = cw ? lwq : wl;
+  const bool okq = jq < lwq;
+  uint4 wg[PG];
+  uint16_t sg[PG];
+  {
+    const __amdgpu_buffer_rsrc_t rg = buf_rsrc(a.g_qs + (size_t)cu * 2 * a.ru * nbE, on * Ug * 16),
+                                 rgd = buf_rsrc(a.g_d + (size_t)cu * 2 * a.ru * nbE, on * Ug * 2);
+#pragma unroll
+    for (int p = 0; p < PG; p++) {
+      const int u = okq ? p * lwq + jq : (1 << 24);
+      wg[p] = buf_ld16(rg, u * 16, 0);
+      sg[p] = buf_ld2(rgd, u * 2, 0);
+    }
+  }
+  __builtin_amdgcn_s_barrier();
+  if (!cw) {  // the down rows by LDS-DMA (>= 8 KB of allocation slack: whole 1-KB pieces)
+    const unsigned char* dq = reinterpret_cast<const unsigned char*>(a.d_qs + (size_t)cu * a.rd * nbF);
+    const unsigned char* dd = reinterpret_cast<const unsigned char*>(a.d_d + (size_t)cu * a.rd * nbF);
+    const int nqi = (Ud * 16 + 1023) / 1024, ndi = (Ud * 2 + 1023) / 1024;
+    for (int i = w - ENG_CW; i < nqi + ndi; i += ENG_NW - ENG_CW) {
+      if (i < nqi) eng_glds16(dq + i * 1024 + lane * 16, s_dyn + L.dq + i * 1024);
+      else eng_glds16(dd + (i - nqi) * 1024 + lane * 16, s_dyn + L.dd + (i - nqi) * 1024);
+    }
+  }
+  // P5: residual + post_attn norm + ffn_norm -> Q8_0 x2 (model.cpp:843-858, 915-924 + run_norm)
+  {
+    const float4 o4 = pt ? o4i : make_float4(0.f, 0.f, 0.f, 0.f);
+    float ss = 0.0f;
+    ss = fmaf(o4.x, o4.x, ss);
+    ss = fmaf(o4.y, o4.y, ss);
+    ss = fmaf(o4.z, o4.z, ss);
+    ss = fmaf(o4.w, o4.w, ss);
+    const float sc1 = 1.0f / sqrtf((float)((double)(eng_block_sum(ss, s_red[0]) / (float)E) + a.eps));
+    const float4 h = make_float4(r4.x + (sc1 * o4.x) * pn.x, r4.y + (sc1 * o4.y) * pn.y, r4.z + (sc1 * o4.z) * pn.z,
+                                 r4.w + (sc1 * o4.w) * pn.w);
+    float ss2 = 0.0f;
+    if (pt) {
+      ss2 = fmaf(h.x, h.x, ss2);
+      ss2 = fmaf(h.y, h.y, ss2);
+      ss2 = fmaf(h.z, h.z, ss2);
+      ss2 = fmaf(h.w, h.w, ss2);
+      if (cu == 0) reinterpret_cast<float4*>(a.resid_out)[t] = h;
+    }
+    const float sc2 = 1.0f / sqrtf((float)((double)(eng_block_sum(ss2, s_red[1]) / (float)E) + a.eps));
+    if (pt)
+      q8_block_oct(make_float4((sc2 * h.x) * fn.x, (sc2 * h.y) * fn.y, (sc2 * h.z) * fn.z, (sc2 * h.w) * fn.w), t & 7,
+                   s_x + (t >> 3));
+  }
+  __syncthreads();
+  ENG_MARK(7);
+  // P6: gate_up + GELU -> granules g_hid
+  if (!cw && okq) {
+    const XBlock* xb = s_x + jq % nbE;
+#pragma unroll
+    for (int p = 0; p < PG; p++) {
+      const int u = p * lwq + jq;
+      if (u < Ug) s_kvf[u] = eng_dot(wg[p], sg[p], xb);
+    }
+  }
+  __syncthreads();
+  ENG_MARK(14);
+  eng_row_sums(s_kvf, 2 * a.ru, nbE, [&](int r, float v) { s_gu[r] = v; });
+  __syncthreads();
+  ENG_MARK(15);
+  if (t < a.ru) {  // model.cpp:892-899
+    const float hv = gelu_mul1(s_gu[t], s_gu[a.ru + t]);
+    st_granule(a.g_hid + cu * a.ru + t, __float_as_uint(hv), tag);
+  }
+  ENG_MARK(8);
+  // P7: the whole GELU output -> Q8_0 blocks in LDS (comm waves; 5 sets of 4 granules per lane in flight)
+  XBlock* s_hx = reinterpret_cast<XBlock*>(s_dyn + L.kv);
+  float* s_vd = reinterpret_cast<float*>(s_dyn + L.kv + eng_align(nbF * (int)sizeof(XBlock)));
+  if (cw) {
+    constexpr int K = 5;
+    const int nsets = a.Fu / 4;
+    for (int i0 = 0; i0 < nsets; i0 += K * ENG_CW * 64) {
+      int off[K];
+      bool act[K];
+      uint32_t u[K][4];
+#pragma unroll
+      for (int k = 0; k < K; k++) {
+        const int i = i0 + k * ENG_CW * 64 + t;
+        off[k] = 4 * i;
+        act[k] = i < nsets;
+      }
+      eng_sweep<K>(u, a.g_hid, off, act, tag, a.err);
+#pragma unroll
+      for (int k = 0; k < K; k++) {
+        const int i = i0 + k * ENG_CW * 64 + t;
+        if (i0 + k * ENG_CW * 64 < nsets)
+          if (i < nsets) q8_block_oct(u4f(u[k]), i & 7, s_hx + (i >> 3));
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the down rows' LDS-DMA (worker waves)
+  __syncthreads();
+  ENG_MARK(9);
+  // P8: down rows -> y_out
+  {
+    const int lwd = (ENG_T / nbF) * nbF;
+    if (t < lwd) {
+      const XBlock* xb = s_hx + t % nbF;
+      for (int u = t; u < Ud; u += lwd) s_vd[u] = eng_dot(s_dq[u], s_dd[u], xb);
+    }
+  }
+  __syncthreads();
+  eng_row_sums(s_vd, nrd, nbF, [&](int r, float v) { a.y_out[cu * a.rd + r] = v; });
+  ENG_MARK(10);
+  if (cu == 0 && t == 0) {
+    *a.epoch = tag;                     // every CU read the epoch before any CU got past P7
+    if (a.blk_epoch) *a.blk_epoch += 1u;  // the attention block's granule tag of this layer (gate_up's job before)
+  }
+}
+
+template <int PG>
+void ffn_launch(int grid, size_t lds, const EngineLayer& a, hipStream_t s) {
+  KernelTiming& kt = kernel_timing();
+  if (kt.start) {
+    hipExtLaunchKernelGGL((ffn_engine_kernel<PG>), dim3(grid), dim3(ENG_T), (uint32_t)lds, s, kt.start, kt.stop, 0u, a);
+    kt = KernelTiming{};
+    return;
+  }
+  hipLaunchKernelGGL((ffn_engine_kernel<PG>), dim3(grid), dim3(ENG_T), lds, s, a);
 }
 
 struct EngCfg {
@@ -845,7 +1063,7 @@ void eng_launch(int grid, size_t lds, const EngineLayer& a, hipStream_t s) {
     reinterpret_cast<const void*>(&layer_engine_kernel<HD, G, PQ, PO, PG, true>)},                     \
    {eng_launch<HD, G, PQ, PO, PG, false>, eng_launch<HD, G, PQ, PO, PG, true>}}
 const EngCfg kEngCfgs[] = {
-    LLMI_ECFG(256, 2, 2, 1, 9),  // 4B: qkv 16 rows x 80 blocks, o 10 x 64, gate_up 80 x 80 (down 10 x 320 in LDS)
+    LLMI_ECFG(256, 2, 2, 3, 9),  // 4B: qkv 16 rows x 80 blocks, o 10 x 64 (comm lanes), gate_up 80 x 80 (down 10 x 320 in LDS)
     LLMI_ECFG(256, 2, 1, 1, 3),  // 1B (virtual kv heads of 2): qkv 6 x 36, o 5 x 32, gate_up 54 x 36 (down 5 x 216)
 };
 #undef LLMI_ECFG
@@ -862,12 +1080,12 @@ int eng_n_cu() {
 
 const EngCfg* eng_find(const EngineLayer& a, int hd, int g) {
   // worker lanes per pass: a whole number of rows' blocks (each lane keeps one activation block)
-  auto passes = [](int units, int nb) { const int lw = (ENG_LW / nb) * nb; return (units + lw - 1) / lw; };
+  auto passes = [](int units, int nb, int lanes) { const int lw = (lanes / nb) * nb; return (units + lw - 1) / lw; };
   const int nbE = a.E / 32, nbO = a.n_head * hd / 32;
-  if (nbE > ENG_LW || nbO > ENG_LW || a.Fu / 32 > ENG_T) return nullptr;
-  for (const auto& c : kEngCfgs)
-    if (c.hd == hd && c.g == g && c.pq == passes(a.rq * nbE, nbE) && c.po == passes(a.ro * nbO, nbO) &&
-        c.pg == passes(2 * a.ru * nbE, nbE))
+  if (nbE > ENG_LW || nbO > ENG_CW * 64 || a.Fu / 32 > ENG_T) return nullptr;
+  for (const auto& c : kEngCfgs)  // qkv / gate_up on the worker lanes, o on the comm lanes
+    if (c.hd == hd && c.g == g && c.pq == passes(a.rq * nbE, nbE, ENG_LW) &&
+        c.po == passes(a.ro * nbO, nbO, ENG_CW * 64) && c.pg == passes(2 * a.ru * nbE, nbE, ENG_LW))
       return &c;
   return nullptr;
 }
@@ -915,6 +1133,55 @@ void launch_layer_engine(const EngineLayer& a, bool first, hipStream_t s) {
     throw std::runtime_error("layer engine: missing buffers");
   const EngLds L = eng_lds(a, 256, 2);
   c->fn[first ? 1 : 0](eng_n_cu(), (size_t)L.total, a, s);
+  LLMI_HIP(hipGetLastError());
+}
+
+
+// ---- FFN engine ----
+namespace {
+struct FfnCfg {
+  int pg;
+  const void* kern;
+  void (*fn)(int, size_t, const EngineLayer&, hipStream_t);
+};
+#define LLMI_FCFG(PG) {PG, reinterpret_cast<const void*>(&ffn_engine_kernel<PG>), ffn_launch<PG>}
+const FfnCfg kFfnCfgs[] = {LLMI_FCFG(9), LLMI_FCFG(3), LLMI_FCFG(11)};  // 4B (80 rows x 80 blocks), 1B, 12B-like
+#undef LLMI_FCFG
+const FfnCfg* ffn_find(const EngineLayer& a) {
+  const int nbE = a.E / 32;
+  if (nbE > ENG_LW || a.Fu / 32 > ENG_T) return nullptr;
+  const int lw = (ENG_LW / nbE) * nbE, pg = (2 * a.ru * nbE + lw - 1) / lw;
+  for (const auto& c : kFfnCfgs)
+    if (c.pg == pg) return &c;
+  return nullptr;
+}
+}  // namespace
+
+bool ffn_engine_plan(int E, int F, EngineLayer& a) {
+  const int ncu = eng_n_cu();
+  if (ncu <= 0 || E % 32 || F % 32 || E / 4 > ENG_T || F % ncu || (F / 4) % 8 || 2 * (F / ncu) > 256) return false;
+  a.E = E;
+  a.Fu = F;
+  a.ro = a.rd = (E + ncu - 1) / ncu;
+  a.ru = F / ncu;
+  const FfnCfg* c = ffn_find(a);
+  if (!c) return false;
+  const EngLds L = eng_ffn_lds(a);
+  if (L.total > 150 * 1024) return false;
+  int per_cu = 0;
+  if (hipFuncSetAttribute(c->kern, hipFuncAttributeMaxDynamicSharedMemorySize, L.total) != hipSuccess) return false;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, c->kern, ENG_T, L.total) != hipSuccess || per_cu < 1)
+    return false;
+  return true;
+}
+
+void launch_ffn_engine(const EngineLayer& a, hipStream_t s) {
+  const FfnCfg* c = ffn_find(a);
+  if (!c) throw std::runtime_error("FFN engine: no launch configuration for the shapes");
+  if (!a.g_qs || !a.d_qs || !a.epoch || !a.g_hid || !a.err || !a.y_in || !a.y_out || !a.resid_in || !a.resid_out ||
+      a.resid_in == a.resid_out || !a.post_attn_norm || !a.ffn_norm)
+    throw std::runtime_error("FFN engine: missing buffers");
+  c->fn(eng_n_cu(), (size_t)eng_ffn_lds(a).total, a, s);
   LLMI_HIP(hipGetLastError());
 }
 

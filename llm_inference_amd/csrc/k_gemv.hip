@@ -560,6 +560,61 @@ __global__ __launch_bounds__(256) void gemv_q5_0_exact(const uint8_t* __restrict
   out[row] = sum;
 }
 
+// fast Q5_0 (ops.cpp:840-893 arithmetic, f32 x: d * (q - 16) * x per element): R rows per wave as a
+// flat (row, block) item list like the Q8_0 kernel, one 22-B GGUF block per lane per pass (eleven 2-B
+// loads: the blocks are 2-B aligned), the block's 32 products summed in the lane in element order, then
+// the fp32 sums across blocks and lanes reassociated (fast mode)
+template <int R, int P>
+__global__ __launch_bounds__(256) void gemv_q5_0_fast(const uint16_t* __restrict__ wq, int rows, int nb, uint32_t magic,
+                                                      const float* __restrict__ x, float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * R;
+  if (row0 >= rows) return;
+  const int nrows = min(R, rows - row0);
+  const int total = nrows * nb;
+  const uint16_t* qw = wq + (size_t)row0 * nb * 11;
+  float acc[R];
+#pragma unroll
+  for (int k = 0; k < R; k++) acc[k] = 0.0f;
+  for (int c0 = 0; c0 < total; c0 += 64 * P) {
+    uint16_t blk[P][11];
+    int rr[P], bb[P];
+#pragma unroll
+    for (int p = 0; p < P; p++) {
+      const int f = c0 + p * 64 + lane;
+      const int fc = f < total ? f : 0;
+      const int r = div_by_magic(fc, magic);
+      rr[p] = f < total ? r : R;
+      bb[p] = fc - r * nb;
+#pragma unroll
+      for (int k = 0; k < 11; k++) blk[p][k] = __builtin_nontemporal_load(qw + (size_t)fc * 11 + k);
+    }
+#pragma unroll
+    for (int p = 0; p < P; p++) {
+      const float d = h2f(blk[p][0]);
+      const uint32_t qh = (uint32_t)blk[p][1] | ((uint32_t)blk[p][2] << 16);
+      const float4* xv = reinterpret_cast<const float4*>(x + bb[p] * 32);
+      float s = 0.0f;
+#pragma unroll
+      for (int i4 = 0; i4 < 4; i4++) {  // elements 4 i4 .. 4 i4 + 3 and 16 + the same
+        const float4 xl = xv[i4], xh = xv[4 + i4];
+        const float xa[4] = {xl.x, xl.y, xl.z, xl.w}, xb[4] = {xh.x, xh.y, xh.z, xh.w};
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+          const int i = 4 * i4 + e;
+          const uint32_t qb = (blk[p][3 + (i >> 1)] >> (8 * (i & 1))) & 0xFF;  // byte i of the nibbles
+          const int q0 = (int)(qb & 0x0F) | (int)(((qh >> i) & 1) << 4);
+          const int q1 = (int)(qb >> 4) | (int)(((qh >> (i + 16)) & 1) << 4);
+          s = fmaf(d * (float)(q0 - 16), xa[e], s);
+          s = fmaf(d * (float)(q1 - 16), xb[e], s);
+        }
+      }
+      acc_add<R>(acc, rr[p], s);
+    }
+  }
+  rows_out<R>(acc, lane, row0, nrows, out);
+}
+
 __global__ __launch_bounds__(256) void gemv_bf16_exact(const uint16_t* __restrict__ w, int rows, int cols,
                                                        const float* __restrict__ x, float* __restrict__ out) {
   const int row = blockIdx.x * blockDim.x + threadIdx.x;
@@ -704,10 +759,26 @@ void launch_gemv(const DevWeight& w, const ActBuf& x, float* o, GemvMode mode, h
 #undef LLMI_KQ
       break;
     }
-    case T_Q5_0:
-      hipLaunchKernelGGL(gemv_q5_0_exact, dim3((rows + 255) / 256), dim3(256), 0, s, (const uint8_t*)w.qs, rows,
-                         w.cols / 32, x.xf, o);
+    case T_Q5_0: {
+      const int nb = w.cols / 32;
+      if (mode == GEMV_EXACT) {
+        hipLaunchKernelGGL(gemv_q5_0_exact, dim3((rows + 255) / 256), dim3(256), 0, s, (const uint8_t*)w.qs, rows, nb,
+                           x.xf, o);
+      } else {
+        const int R = rows_per_wave(nb, rows), P = std::min(4, passes_per_chunk(R, nb));  // 11 VGPRs per pass
+        const dim3 grid((rows + 4 * R - 1) / (4 * R));
+        switch (R * 16 + P) {
+#define LLMI_Q5(RR, PP) \
+  case RR * 16 + PP: hipLaunchKernelGGL((gemv_q5_0_fast<RR, PP>), grid, dim3(256), 0, s, (const uint16_t*)w.qs, rows, nb, div_magic(nb), x.xf, o); break;
+#define LLMI_Q5R(RR) LLMI_Q5(RR, 1) LLMI_Q5(RR, 2) LLMI_Q5(RR, 4)
+          LLMI_Q5R(1) LLMI_Q5R(2) LLMI_Q5R(4) LLMI_Q5R(8)
+#undef LLMI_Q5R
+#undef LLMI_Q5
+          default: throw std::runtime_error("gemv: no Q5_0 kernel for R/P");
+        }
+      }
       break;
+    }
     case T_BF16:
       hipLaunchKernelGGL(gemv_bf16_exact, dim3((rows + 255) / 256), dim3(256), 0, s, (const uint16_t*)w.qs, rows,
                          w.cols, x.xf, o);

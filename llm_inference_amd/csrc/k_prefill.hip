@@ -216,13 +216,13 @@ __global__ __launch_bounds__(256) void prefill_norm_res_kernel(PrefillNorm a) {
 
 // ---------------------------------------------------------------------------
 // GEMM: out[t][n] = sum_b d_w[n][b] d_x[t][b] * sum_k (q_w[n][b][k] - 8) q_x[t][b][k]
-// Work-group: 32 weight rows x 128 tokens, wave w: tokens [32 w, 32 w + 32).
 // MFMA lane maps (scripts/dev/mfma_i8_check): lane (r = l & 31, h = l >> 5)
 // holds A[row r][k 16h..16h+15] (the low (h 0) or high (h 1) nibbles of the
 // row's 16 quant bytes, in k order) and B[k 16h..][token r] (the token's
 // Q8_0 q[16h..16h+15]); D[row (reg & 3) + 8 (reg >> 2) + 4 h][token r].
+// (GEMMs v1-v4 were retired in round 3: v5 with one K group per output computes
+// v1's fmaf chain bit for bit; tests/golden/prefill_v1_ref.npz pins it.)
 // ---------------------------------------------------------------------------
-constexpr int PG_TOK = 128;
 
 __device__ __forceinline__ size_t q4_block_index(int slab, int rows, int nb, int n, int b) {
   return slab ? ((size_t)(b >> 3) * rows + n) * 8 + (b & 7) : (size_t)n * nb + b;
@@ -231,218 +231,6 @@ __device__ __forceinline__ size_t q4_block_index(int slab, int rows, int nb, int
 __device__ __forceinline__ int q4_signed(uint32_t w) {  // 4 nibbles (bytes 0..15) -> int8 (n - 8)
   return (int)((w + 0x78787878u) ^ 0x80808080u);
 }
-
-__global__ __launch_bounds__(256) void prefill_gemm_kernel(PrefillGemm a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
-  uint16_t* s_dw = reinterpret_cast<uint16_t*>(s_dyn);                                   // [nb][32]
-  float* s_o = reinterpret_cast<float*>(s_dyn + (((size_t)a.nb * 64 + 15) & ~(size_t)15));  // [4][32][33]
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6, r = lane & 31, h = lane >> 5;
-  const int nb = a.nb, n0 = blockIdx.x * 32;
-  const int tok0 = blockIdx.y * PG_TOK + w * 32;
-  for (int i = t; i < 32 * nb; i += 256) {  // the tile's block scales, transposed
-    const int row = i / nb, b = i % nb;
-    s_dw[b * 32 + row] = a.wd[q4_block_index(a.slab, a.rows, nb, n0 + row, b)];
-  }
-  __syncthreads();
-  const XBlock* xr = a.x + (size_t)min(tok0 + r, a.T - 1) * a.xstride;
-  float acc[16];
-#pragma unroll
-  for (int i = 0; i < 16; i++) acc[i] = 0.0f;
-  const v16i zero = {};
-  uint4 wq = a.qs[q4_block_index(a.slab, a.rows, nb, n0 + r, 0)];
-  int4 xq = h ? xr[0].hi : xr[0].lo;
-  float dx = xr[0].d;
-  for (int b = 0; b < nb; b++) {
-    // next block in flight while this one is multiplied
-    const int bn = min(b + 1, nb - 1);
-    const uint4 wq_n = a.qs[q4_block_index(a.slab, a.rows, nb, n0 + r, bn)];
-    const int4 xq_n = h ? xr[bn].hi : xr[bn].lo;
-    const float dx_n = xr[bn].d;
-    v4i A, B;
-    A.x = q4_signed(h ? (wq.x >> 4) & 0x0F0F0F0Fu : wq.x & 0x0F0F0F0Fu);
-    A.y = q4_signed(h ? (wq.y >> 4) & 0x0F0F0F0Fu : wq.y & 0x0F0F0F0Fu);
-    A.z = q4_signed(h ? (wq.z >> 4) & 0x0F0F0F0Fu : wq.z & 0x0F0F0F0Fu);
-    A.w = q4_signed(h ? (wq.w >> 4) & 0x0F0F0F0Fu : wq.w & 0x0F0F0F0Fu);
-    B.x = xq.x;
-    B.y = xq.y;
-    B.z = xq.z;
-    B.w = xq.w;
-    const v16i D = __builtin_amdgcn_mfma_i32_32x32x32_i8(A, B, zero, 0, 0, 0);
-#pragma unroll
-    for (int g = 0; g < 4; g++) {  // rows 8g + 4h .. +3: one 8-B read of 4 scales
-      const uint2 d4 = *reinterpret_cast<const uint2*>(&s_dw[b * 32 + 8 * g + 4 * h]);
-      const float s0 = h2f((uint16_t)(d4.x & 0xFFFF)) * dx, s1 = h2f((uint16_t)(d4.x >> 16)) * dx;
-      const float s2 = h2f((uint16_t)(d4.y & 0xFFFF)) * dx, s3 = h2f((uint16_t)(d4.y >> 16)) * dx;
-      acc[4 * g + 0] = fmaf(s0, (float)D[4 * g + 0], acc[4 * g + 0]);
-      acc[4 * g + 1] = fmaf(s1, (float)D[4 * g + 1], acc[4 * g + 1]);
-      acc[4 * g + 2] = fmaf(s2, (float)D[4 * g + 2], acc[4 * g + 2]);
-      acc[4 * g + 3] = fmaf(s3, (float)D[4 * g + 3], acc[4 * g + 3]);
-    }
-    wq = wq_n;
-    xq = xq_n;
-    dx = dx_n;
-  }
-  // transpose through LDS so each token's 32 outputs are one 128-B store
-  float* so = s_o + (size_t)w * 32 * 33;
-#pragma unroll
-  for (int reg = 0; reg < 16; reg++) so[r * 33 + (reg & 3) + 8 * (reg >> 2) + 4 * h] = acc[reg];
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's LDS writes done (wave-local hand-off)
-#pragma unroll
-  for (int i = 0; i < 16; i++) {
-    const int idx = i * 64 + lane, tk = idx >> 5, row = idx & 31;
-    if (tok0 + tk < a.T) a.out[(size_t)(tok0 + tk) * a.ostride + n0 + row] = so[tk * 33 + row];
-  }
-}
-
-// ---------------------------------------------------------------------------
-// GEMM v2 (the prefill's default): a 64-row x 128-token tile per work-group;
-// wave (wr, wt) computes rows 32 wr.. x tokens 64 wt.. as TWO
-// v_mfma_i32_32x32x32_i8 per Q4_0 block (32 tokens each) that share the A
-// operand and the row scales.  The K loop walks chunks of 4 blocks: every
-// thread loads its share of the NEXT chunk into registers (weights 16 B,
-// scales 2 B, activations 6 x 16 B) while the waves multiply the CURRENT
-// chunk out of LDS, so global latency hides under the chunk's MFMAs and
-// epilogues, and the 4 waves share one copy of the tiles (v1 re-read every
-// block from global, one block ahead, per wave).  At staging the Q4_0 nibbles
-// are unpacked once to signed int8 (the MFMA A operand as is) and the block
-// scales widened to f32.  The epilogue -- the bulk of the work: per output
-// and block one int->float conversion, the scale product and the accumulate
-// -- runs on packed 2 x f32 VALU ops.  Per output the block terms are added
-// in block order as fmaf(d_w * d_x, (float)isum, acc), like v1: bit-identical.
-// ---------------------------------------------------------------------------
-constexpr int PG2_M = 64, PG2_N = 128, PG2_KB = 4;
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-
-__global__ __launch_bounds__(256) void prefill_gemm2_kernel(PrefillGemm a) {
-  // one LDS image: the chunk's tiles, reused for the output transpose (16.9 KB)
-  __shared__ __attribute__((aligned(16))) unsigned char s_raw[PG2_KB * PG2_M * 32 + PG2_KB * PG2_M * 4 +
-                                                              PG2_KB * PG2_N * 32 + PG2_KB * PG2_N * 4];
-  auto s_w = reinterpret_cast<uint4(*)[PG2_M][2]>(s_raw);                                   // signed int8 lo|hi, 8 KB
-  auto s_dw = reinterpret_cast<float(*)[PG2_M]>(s_raw + PG2_KB * PG2_M * 32);               // 1 KB
-  auto s_xq = reinterpret_cast<uint4(*)[PG2_N][2]>(s_raw + PG2_KB * PG2_M * 36);            // 16 KB
-  auto s_dx = reinterpret_cast<float(*)[PG2_N]>(s_raw + PG2_KB * PG2_M * 36 + PG2_KB * PG2_N * 32);  // 2 KB
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6, r = lane & 31, h = lane >> 5;
-  const int wr = w & 1, wt = w >> 1;
-  const int nb = a.nb, n0 = blockIdx.x * PG2_M, tk0 = blockIdx.y * PG2_N;
-  // staging roles -- weights: row t & 63, block t >> 6 of the chunk; activations:
-  // token t >> 1, blocks 2 (t & 1), +1
-  const int srow = t & 63, swb = t >> 6;
-  const int stk = t >> 1, sxb = 2 * (t & 1);
-  const XBlock* xrow = a.x + (size_t)min(tk0 + stk, a.T - 1) * a.xstride;
-  uint4 rw, rx0, rx1, rx2, rx3, rx4, rx5;
-  uint16_t rd;
-#define PG2_FETCH(KB)                                                                             \
-  do {                                                                                            \
-    const int bw_ = min((KB) + swb, nb - 1);                                                     \
-    rw = a.qs[q4_block_index(a.slab, a.rows, nb, n0 + srow, bw_)];                               \
-    rd = a.wd[q4_block_index(a.slab, a.rows, nb, n0 + srow, bw_)];                               \
-    const int b0_ = (KB) + sxb, b1_ = b0_ + 1;                                                   \
-    const uint4* x0_ = reinterpret_cast<const uint4*>(xrow + min(b0_, nb - 1));                  \
-    const uint4* x1_ = reinterpret_cast<const uint4*>(xrow + min(b1_, nb - 1));                  \
-    rx0 = x0_[0]; rx1 = x0_[1]; rx2 = x0_[2];                                                     \
-    rx3 = x1_[0]; rx4 = x1_[1]; rx5 = x1_[2];                                                     \
-    if (b0_ >= nb) rx2.x = 0; /* padded blocks: d_x = 0, they add 0 */                           \
-    if (b1_ >= nb) rx5.x = 0;                                                                     \
-  } while (0)
-  f32x2 acc[2][8];
-#pragma unroll
-  for (int u = 0; u < 2; u++)
-#pragma unroll
-    for (int i = 0; i < 8; i++) acc[u][i] = f32x2{0.0f, 0.0f};
-  const v16i zero = {};
-  PG2_FETCH(0);
-  for (int kb = 0; kb < nb; kb += PG2_KB) {
-    __syncthreads();  // every wave is done reading the previous chunk
-    {  // registers -> LDS: nibbles unpacked to signed int8, f16 scales widened
-      uint4 lo, hi;
-      lo.x = (uint32_t)q4_signed(rw.x & 0x0F0F0F0Fu); hi.x = (uint32_t)q4_signed((rw.x >> 4) & 0x0F0F0F0Fu);
-      lo.y = (uint32_t)q4_signed(rw.y & 0x0F0F0F0Fu); hi.y = (uint32_t)q4_signed((rw.y >> 4) & 0x0F0F0F0Fu);
-      lo.z = (uint32_t)q4_signed(rw.z & 0x0F0F0F0Fu); hi.z = (uint32_t)q4_signed((rw.z >> 4) & 0x0F0F0F0Fu);
-      lo.w = (uint32_t)q4_signed(rw.w & 0x0F0F0F0Fu); hi.w = (uint32_t)q4_signed((rw.w >> 4) & 0x0F0F0F0Fu);
-      s_w[swb][srow][0] = lo;
-      s_w[swb][srow][1] = hi;
-      s_dw[swb][srow] = h2f(rd);
-      s_xq[sxb][stk][0] = rx0;
-      s_xq[sxb][stk][1] = rx1;
-      s_dx[sxb][stk] = __uint_as_float(rx2.x);
-      s_xq[sxb + 1][stk][0] = rx3;
-      s_xq[sxb + 1][stk][1] = rx4;
-      s_dx[sxb + 1][stk] = __uint_as_float(rx5.x);
-    }
-    __syncthreads();
-    if (kb + PG2_KB < nb) PG2_FETCH(kb + PG2_KB);  // the next chunk streams during this one's MFMAs
-    const int kn = min(PG2_KB, nb - kb);
-    for (int b = 0; b < kn; b++) {
-      const uint4 wq = s_w[b][32 * wr + r][h];
-      v4i A;
-      A.x = (int)wq.x;
-      A.y = (int)wq.y;
-      A.z = (int)wq.z;
-      A.w = (int)wq.w;
-      v16i D[2];
-      float dx[2];
-#pragma unroll
-      for (int u = 0; u < 2; u++) {
-        const uint4 xq = s_xq[b][64 * wt + 32 * u + r][h];
-        dx[u] = s_dx[b][64 * wt + 32 * u + r];
-        v4i B;
-        B.x = (int)xq.x;
-        B.y = (int)xq.y;
-        B.z = (int)xq.z;
-        B.w = (int)xq.w;
-        D[u] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A, B, zero, 0, 0, 0);
-      }
-#pragma unroll
-      for (int g = 0; g < 4; g++) {  // rows 8g + 4h .. +3 of the wave's 32: one 16-B read of 4 scales
-        const float4 d4 = *reinterpret_cast<const float4*>(&s_dw[b][32 * wr + 8 * g + 4 * h]);
-        const f32x2 dlo = {d4.x, d4.y}, dhi = {d4.z, d4.w};
-#pragma unroll
-        for (int u = 0; u < 2; u++) {
-          const f32x2 x2 = {dx[u], dx[u]};
-          const f32x2 i01 = {(float)D[u][4 * g + 0], (float)D[u][4 * g + 1]};
-          const f32x2 i23 = {(float)D[u][4 * g + 2], (float)D[u][4 * g + 3]};
-          acc[u][2 * g + 0] = __builtin_elementwise_fma(dlo * x2, i01, acc[u][2 * g + 0]);
-          acc[u][2 * g + 1] = __builtin_elementwise_fma(dhi * x2, i23, acc[u][2 * g + 1]);
-        }
-      }
-    }
-  }
-#undef PG2_FETCH
-  // transpose through LDS (one 32-token half at a time: 4 waves x 32 x 33 floats) so each
-  // token's 32 outputs are one 128-B store
-  static_assert(4 * 32 * 33 * 4 <= sizeof(s_raw), "transpose fits the tile image");
-  float* so = reinterpret_cast<float*>(s_raw) + (size_t)w * 32 * 33;
-#pragma unroll
-  for (int u = 0; u < 2; u++) {
-    __syncthreads();
-#pragma unroll
-    for (int reg = 0; reg < 16; reg++)
-      so[r * 33 + (reg & 3) + 8 * (reg >> 2) + 4 * h] = acc[u][reg >> 1][reg & 1];
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-local hand-off
-#pragma unroll
-    for (int i = 0; i < 16; i++) {
-      const int idx = i * 64 + lane, tk = idx >> 5, row = idx & 31;
-      const int tok = tk0 + 64 * wt + 32 * u + tk;
-      if (tok < a.T) a.out[(size_t)tok * a.ostride + n0 + 32 * wr + row] = so[tk * 33 + row];
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// GEMM v3: the same 64-row x 64-token tile and per-block MFMA as v1/v2, fed
-// by an LDS-DMA ring (global_load_lds_dwordx4 straight into LDS, no staging
-// registers) PG3_NS stages deep, so PG3_NS - 1 chunks of 4 blocks stream
-// while one is multiplied (v2's one-chunk register prefetch left every chunk
-// waiting out a full HBM round trip).  Per stage and wave: the weight quants
-// of one block (64 rows x 16 B), a third of the activation parts (3 of the
-// 12 (block, 16-B part) slices of 64 tokens), and for waves 0-1 one pair of
-// block scales (64 rows x 4 B).  Raw s_barrier + counted vmcnt keep the later
-// stages in flight across the barriers (cdna_hip_programming.md section 5,
-// 'Pipelining across barriers').  The epilogue is v1's fmaf(d_w * d_x,
-// (float)isum, acc) in block order: bit-identical to v1.
-// ---------------------------------------------------------------------------
-constexpr int PG3_M = 64, PG3_N = 64, PG3_KB = 4, PG3_NS = 4;
-constexpr int PG3_STAGE = PG3_KB * PG3_M * 16 + (PG3_KB / 2) * PG3_M * 4 + PG3_KB * 3 * PG3_N * 16;  // 16.5 KB
 
 // LDS-DMA issue as inline asm: hipcc's own glds builtin makes it wait vmcnt(0)
 // before every later LDS read (it cannot tell which stage a ds_read touches),
@@ -467,215 +255,6 @@ __device__ __forceinline__ void glds4(const void* g, unsigned char* lds_wave_bas
                : "memory");
 }
 
-__global__ __launch_bounds__(256) void prefill_gemm3_kernel(PrefillGemm a) {
-  __shared__ __attribute__((aligned(16))) unsigned char s_ring[PG3_NS * PG3_STAGE];
-  const int t = threadIdx.x, lane = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6), r = lane & 31, h = lane >> 5;
-  const int wr = w & 1, wt = w >> 1;
-  const int nb = a.nb, n0 = blockIdx.x * PG3_M, tk0 = blockIdx.y * PG3_N;
-  const int nst = nb / PG3_KB;  // host-checked: nb % 4 == 0
-  // stage layout: wq[4][64] uint4 | wd[2][64] u32 (f16 pairs) | x[4][3][64] uint4
-  auto st_wq = [&](int s) { return s_ring + s * PG3_STAGE; };
-  auto st_wd = [&](int s) { return s_ring + s * PG3_STAGE + PG3_KB * PG3_M * 16; };
-  auto st_x = [&](int s) { return s_ring + s * PG3_STAGE + PG3_KB * PG3_M * 16 + (PG3_KB / 2) * PG3_M * 4; };
-  const XBlock* xrow = a.x + (size_t)min(tk0 + lane, a.T - 1) * a.xstride;
-  // wave w issues for stage s (chunk c): wq block w; x slices 3w..3w+2; waves 0-1: wd pair w
-  auto issue = [&](int c) {
-    const int s = c % PG3_NS, kb = c * PG3_KB;
-    glds16(a.qs + q4_block_index(a.slab, a.rows, nb, n0 + lane, kb + w), st_wq(s) + w * PG3_M * 16);
-#pragma unroll
-    for (int j = 0; j < 3; j++) {
-      const int sl = 3 * w + j, b = sl / 3, part = sl % 3;
-      glds16(reinterpret_cast<const uint4*>(xrow + kb + b) + part, st_x(s) + sl * PG3_N * 16);
-    }
-    if (w < 2) glds4(a.wd + q4_block_index(a.slab, a.rows, nb, n0 + lane, kb + 2 * w), st_wd(s) + w * PG3_M * 4);
-  };
-  // stage c is complete for this wave once only the issues of the stages after it remain
-#define PG3_WAIT(AHEAD)                                                   \
-  do {                                                                    \
-    if ((AHEAD) >= 3) {                                                   \
-      if (w < 2) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");        \
-      else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");              \
-    } else if ((AHEAD) == 2) {                                            \
-      if (w < 2) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");        \
-      else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");               \
-    } else if ((AHEAD) == 1) {                                            \
-      if (w < 2) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");         \
-      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");               \
-    } else {                                                              \
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                    \
-    }                                                                     \
-  } while (0)
-  static_assert(PG3_NS == 4, "PG3_WAIT counts are written for 3 stages ahead");
-  for (int c = 0; c < PG3_NS - 1 && c < nst; c++) issue(c);
-  float acc[16];
-#pragma unroll
-  for (int i = 0; i < 16; i++) acc[i] = 0.0f;
-  const v16i zero = {};
-  for (int c = 0; c < nst; c++) {
-    const int ahead = min(PG3_NS - 2, nst - 1 - c);  // stages issued after c that may stay in flight
-    PG3_WAIT(ahead);
-    __builtin_amdgcn_s_barrier();  // every wave's slices of stage c have landed; stage c - 1 is no longer read
-    if (c + PG3_NS - 1 < nst) issue(c + PG3_NS - 1);  // refills the slot stage c - 1 used
-    const int s = c % PG3_NS;
-    const uint4* wq = reinterpret_cast<const uint4*>(st_wq(s));
-    const uint32_t* wd = reinterpret_cast<const uint32_t*>(st_wd(s));
-    const uint4* xs = reinterpret_cast<const uint4*>(st_x(s));
-#pragma unroll
-    for (int b = 0; b < PG3_KB; b++) {
-      const uint4 q = wq[b * PG3_M + 32 * wr + r];
-      const uint4 xq = xs[(3 * b + h) * PG3_N + 32 * wt + r];
-      const float dx = __uint_as_float(xs[(3 * b + 2) * PG3_N + 32 * wt + r].x);
-      v4i A, B;
-      A.x = q4_signed(h ? (q.x >> 4) & 0x0F0F0F0Fu : q.x & 0x0F0F0F0Fu);
-      A.y = q4_signed(h ? (q.y >> 4) & 0x0F0F0F0Fu : q.y & 0x0F0F0F0Fu);
-      A.z = q4_signed(h ? (q.z >> 4) & 0x0F0F0F0Fu : q.z & 0x0F0F0F0Fu);
-      A.w = q4_signed(h ? (q.w >> 4) & 0x0F0F0F0Fu : q.w & 0x0F0F0F0Fu);
-      B.x = (int)xq.x;
-      B.y = (int)xq.y;
-      B.z = (int)xq.z;
-      B.w = (int)xq.w;
-      const v16i D = __builtin_amdgcn_mfma_i32_32x32x32_i8(A, B, zero, 0, 0, 0);
-#pragma unroll
-      for (int g = 0; g < 4; g++) {  // rows 8g + 4h .. +3: 4 scale pairs in one 16-B read
-        const uint4 d4 = *reinterpret_cast<const uint4*>(&wd[(b >> 1) * PG3_M + 32 * wr + 8 * g + 4 * h]);
-        const int sh = (b & 1) * 16;
-        const float s0 = h2f((uint16_t)(d4.x >> sh)) * dx, s1 = h2f((uint16_t)(d4.y >> sh)) * dx;
-        const float s2 = h2f((uint16_t)(d4.z >> sh)) * dx, s3 = h2f((uint16_t)(d4.w >> sh)) * dx;
-        acc[4 * g + 0] = fmaf(s0, (float)D[4 * g + 0], acc[4 * g + 0]);
-        acc[4 * g + 1] = fmaf(s1, (float)D[4 * g + 1], acc[4 * g + 1]);
-        acc[4 * g + 2] = fmaf(s2, (float)D[4 * g + 2], acc[4 * g + 2]);
-        acc[4 * g + 3] = fmaf(s3, (float)D[4 * g + 3], acc[4 * g + 3]);
-      }
-    }
-  }
-#undef PG3_WAIT
-  // transpose through LDS (the ring; every DMA has landed: the last wait was vmcnt(0))
-  __builtin_amdgcn_s_barrier();
-  float* so = reinterpret_cast<float*>(s_ring) + (size_t)w * 32 * 33;
-#pragma unroll
-  for (int reg = 0; reg < 16; reg++) so[r * 33 + (reg & 3) + 8 * (reg >> 2) + 4 * h] = acc[reg];
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-local hand-off
-#pragma unroll
-  for (int i = 0; i < 16; i++) {
-    const int idx = i * 64 + lane, tk = idx >> 5, row = idx & 31;
-    const int tok = tk0 + 32 * wt + tk;
-    if (tok < a.T) a.out[(size_t)tok * a.ostride + n0 + 32 * wr + row] = so[tk * 33 + row];
-  }
-}
-
-// ---------------------------------------------------------------------------
-// GEMM v4: v3's tile, ring and MFMA, with the scale epilogue cut to what the
-// per-block arithmetic needs (the kernel is VALU-bound: every 32x32x32 MFMA
-// of one 32-element block is followed by 16 conversions and 16 FMAs per lane).
-//  * the weight scales of a stage are converted f16 -> f32 ONCE per
-//    work-group into an f32 area of the stage (one thread per (block, row)),
-//    published by a second barrier, instead of 16 h2f per lane per MFMA;
-//  * s = d_w * d_x and acc = fma(s, (float)isum, acc) run as packed f32
-//    pairs (v_pk_mul_f32 / v_pk_fma_f32: per element the same IEEE ops).
-// Bit-identical to v1 / v3 (same fmaf(d_w * d_x, (float)isum, acc) in block
-// order per output).
-// ---------------------------------------------------------------------------
-constexpr int PG4_STAGE = PG3_STAGE + PG3_KB * PG3_M * 4;  // + f32 scales [4 blocks][64 rows]
-
-__global__ __launch_bounds__(256) void prefill_gemm4_kernel(PrefillGemm a) {
-  __shared__ __attribute__((aligned(16))) unsigned char s_ring[PG3_NS * PG4_STAGE];
-  const int t = threadIdx.x, lane = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6), r = lane & 31, h = lane >> 5;
-  const int wr = w & 1, wt = w >> 1;
-  const int nb = a.nb, n0 = blockIdx.x * PG3_M, tk0 = blockIdx.y * PG3_N;
-  const int nst = nb / PG3_KB;
-  auto st_wq = [&](int s) { return s_ring + s * PG4_STAGE; };
-  auto st_wd = [&](int s) { return s_ring + s * PG4_STAGE + PG3_KB * PG3_M * 16; };
-  auto st_x = [&](int s) { return s_ring + s * PG4_STAGE + PG3_KB * PG3_M * 16 + (PG3_KB / 2) * PG3_M * 4; };
-  auto st_wf = [&](int s) { return reinterpret_cast<float*>(s_ring + s * PG4_STAGE + PG3_STAGE); };
-  const XBlock* xrow = a.x + (size_t)min(tk0 + lane, a.T - 1) * a.xstride;
-  auto issue = [&](int c) {
-    const int s = c % PG3_NS, kb = c * PG3_KB;
-    glds16(a.qs + q4_block_index(a.slab, a.rows, nb, n0 + lane, kb + w), st_wq(s) + w * PG3_M * 16);
-#pragma unroll
-    for (int j = 0; j < 3; j++) {
-      const int sl = 3 * w + j, b = sl / 3, part = sl % 3;
-      glds16(reinterpret_cast<const uint4*>(xrow + kb + b) + part, st_x(s) + sl * PG3_N * 16);
-    }
-    if (w < 2) glds4(a.wd + q4_block_index(a.slab, a.rows, nb, n0 + lane, kb + 2 * w), st_wd(s) + w * PG3_M * 4);
-  };
-#define PG4_WAIT(AHEAD)                                                   \
-  do {                                                                    \
-    if ((AHEAD) >= 3) {                                                   \
-      if (w < 2) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");        \
-      else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");              \
-    } else if ((AHEAD) == 2) {                                            \
-      if (w < 2) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");        \
-      else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");               \
-    } else if ((AHEAD) == 1) {                                            \
-      if (w < 2) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");         \
-      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");               \
-    } else {                                                              \
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                    \
-    }                                                                     \
-  } while (0)
-  for (int c = 0; c < PG3_NS - 1 && c < nst; c++) issue(c);
-  typedef float f2 __attribute__((ext_vector_type(2)));
-  f2 acc[8];
-#pragma unroll
-  for (int i = 0; i < 8; i++) acc[i] = (f2){0.0f, 0.0f};
-  const v16i zero = {};
-  for (int c = 0; c < nst; c++) {
-    const int ahead = min(PG3_NS - 2, nst - 1 - c);
-    PG4_WAIT(ahead);
-    __builtin_amdgcn_s_barrier();  // every wave's slices of stage c have landed; stage c - 1 is no longer read
-    if (c + PG3_NS - 1 < nst) issue(c + PG3_NS - 1);
-    const int s = c % PG3_NS;
-    {  // the stage's 4 x 64 weight scales -> f32, one per thread
-      const int b = t >> 6, row = t & 63;
-      const uint32_t pr = reinterpret_cast<const uint32_t*>(st_wd(s))[(b >> 1) * PG3_M + row];
-      st_wf(s)[b * PG3_M + row] = h2f((uint16_t)(pr >> ((b & 1) * 16)));
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // the f32 scales are in LDS (no vmcnt wait: the ring stays in flight)
-    const uint4* wq = reinterpret_cast<const uint4*>(st_wq(s));
-    const float* wf = st_wf(s);
-    const uint4* xs = reinterpret_cast<const uint4*>(st_x(s));
-#pragma unroll
-    for (int b = 0; b < PG3_KB; b++) {
-      const uint4 q = wq[b * PG3_M + 32 * wr + r];
-      const uint4 xq = xs[(3 * b + h) * PG3_N + 32 * wt + r];
-      const float dx = __uint_as_float(xs[(3 * b + 2) * PG3_N + 32 * wt + r].x);
-      v4i A, B;
-      A.x = q4_signed(h ? (q.x >> 4) & 0x0F0F0F0Fu : q.x & 0x0F0F0F0Fu);
-      A.y = q4_signed(h ? (q.y >> 4) & 0x0F0F0F0Fu : q.y & 0x0F0F0F0Fu);
-      A.z = q4_signed(h ? (q.z >> 4) & 0x0F0F0F0Fu : q.z & 0x0F0F0F0Fu);
-      A.w = q4_signed(h ? (q.w >> 4) & 0x0F0F0F0Fu : q.w & 0x0F0F0F0Fu);
-      B.x = (int)xq.x;
-      B.y = (int)xq.y;
-      B.z = (int)xq.z;
-      B.w = (int)xq.w;
-      const v16i D = __builtin_amdgcn_mfma_i32_32x32x32_i8(A, B, zero, 0, 0, 0);
-      const f2 dxx = {dx, dx};
-#pragma unroll
-      for (int g = 0; g < 4; g++) {  // rows 8g + 4h .. +3
-        const float4 w4 = *reinterpret_cast<const float4*>(&wf[b * PG3_M + 32 * wr + 8 * g + 4 * h]);
-        const f2 s01 = (f2){w4.x, w4.y} * dxx, s23 = (f2){w4.z, w4.w} * dxx;
-        const f2 d01 = {(float)D[4 * g + 0], (float)D[4 * g + 1]};
-        const f2 d23 = {(float)D[4 * g + 2], (float)D[4 * g + 3]};
-        acc[2 * g] = __builtin_elementwise_fma(s01, d01, acc[2 * g]);
-        acc[2 * g + 1] = __builtin_elementwise_fma(s23, d23, acc[2 * g + 1]);
-      }
-    }
-  }
-#undef PG4_WAIT
-  __builtin_amdgcn_s_barrier();
-  float* so = reinterpret_cast<float*>(s_ring) + (size_t)w * 32 * 33;
-#pragma unroll
-  for (int reg = 0; reg < 16; reg++) so[r * 33 + (reg & 3) + 8 * (reg >> 2) + 4 * h] = acc[reg >> 1][reg & 1];
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-  for (int i = 0; i < 16; i++) {
-    const int idx = i * 64 + lane, tk = idx >> 5, row = idx & 31;
-    const int tok = tk0 + 32 * wt + tk;
-    if (tok < a.T) a.out[(size_t)tok * a.ostride + n0 + 32 * wr + row] = so[tk * 33 + row];
-  }
-}
-
 // ---------------------------------------------------------------------------
 // GEMM v5 (default): eight waves per work-group in a WR x WT x WK grid -- WR
 // row groups of 32 weight rows, WT token groups of 32 NT tokens, WK groups that
@@ -697,7 +276,7 @@ __global__ __launch_bounds__(256) void prefill_gemm4_kernel(PrefillGemm a) {
 //    fetched into one L2; speed only, never correctness).
 //  * Per output: acc_g = fmaf(d_w * d_x, (float)isum, acc_g) over the blocks of
 //    group g in order; out = ((acc_0 + acc_1) + acc_2) + ... in group order.
-//    WK = 1 is bit-identical to v1 / v3 / v4; every WK is independent of the
+//    WK = 1 is bit-identical to v1 / v3 / v4 (retired); every WK is independent of the
 //    chunking (a token's outputs do not depend on the other tokens).
 // Measured (4B, 512 tokens): qkv 39 -> 32, o 31 -> 25, gate_up 162 -> 133,
 // down 124 -> 96 us.  The compute alone (LLMI_PG5_NODMA build) is ~2/3 of it:
@@ -1809,10 +1388,10 @@ void launch_prefill_norm(const PrefillNorm& a, int T, hipStream_t s) {
   LLMI_HIP(hipGetLastError());
 }
 
-bool prefill_gemm_supported(const DevWeight& w) {
-  if (w.type == T_Q8_0) return w.rows % 32 == 0 && w.cols % 128 == 0 && !w.slab;  // v5 only
-  if (w.type == T_Q4_K || w.type == T_Q6_K) return w.kq && w.rows % 32 == 0 && w.cols % 256 == 0;  // v5, Q8_K x
-  return w.type == T_Q4_0 && w.rows % 32 == 0 && w.cols % 32 == 0 && (!w.slab || (w.cols / 32) % 8 == 0);
+bool prefill_gemm_supported(const DevWeight& w) {  // GEMM v5: 32-row tiles, 4-block K steps
+  if (w.type == T_Q8_0) return w.rows % 32 == 0 && w.cols % 128 == 0 && !w.slab;
+  if (w.type == T_Q4_K || w.type == T_Q6_K) return w.kq && w.rows % 32 == 0 && w.cols % 256 == 0;  // Q8_K x
+  return w.type == T_Q4_0 && w.rows % 32 == 0 && w.cols % 128 == 0 && (!w.slab || (w.cols / 32) % 8 == 0);
 }
 
 template <int WR, int WT, int WK, int NT, int NS>
@@ -1911,21 +1490,7 @@ void launch_prefill_gemm(const DevWeight& w, const XBlock* x, int xstride, int T
   a.T = T;
   a.out = out;
   a.ostride = ostride;
-  const char* ver = getenv("LLMI_PREFILL_GEMM");  // A/B: "1", "2", "3", "4"; default v5
-  const int v = ver ? atoi(ver) : 5;
-  if (a.w8 || a.kq) {  // Q8_0 / kq weights: v5 only
-    if (!launch_gemm5(a, s)) throw std::runtime_error("prefill_gemm: Q8_0 / K-quant shape");
-  } else if (v == 5 && launch_gemm5(a, s)) {
-  } else if (v >= 4 && w.rows % PG3_M == 0 && a.nb % PG3_KB == 0) {
-    hipLaunchKernelGGL(prefill_gemm4_kernel, dim3(w.rows / PG3_M, (T + PG3_N - 1) / PG3_N), dim3(256), 0, s, a);
-  } else if (v >= 3 && w.rows % PG3_M == 0 && a.nb % PG3_KB == 0) {
-    hipLaunchKernelGGL(prefill_gemm3_kernel, dim3(w.rows / PG3_M, (T + PG3_N - 1) / PG3_N), dim3(256), 0, s, a);
-  } else if (v >= 2 && w.rows % PG2_M == 0) {
-    hipLaunchKernelGGL(prefill_gemm2_kernel, dim3(w.rows / PG2_M, (T + PG2_N - 1) / PG2_N), dim3(256), 0, s, a);
-  } else {  // v1: any multiple of 32 rows (LLMI_PREFILL_GEMM=1 selects it for A/B)
-    const size_t lds = (((size_t)a.nb * 64 + 15) & ~(size_t)15) + 4 * 32 * 33 * 4;
-    hipLaunchKernelGGL(prefill_gemm_kernel, dim3(w.rows / 32, (T + PG_TOK - 1) / PG_TOK), dim3(256), lds, s, a);
-  }
+  if (!launch_gemm5(a, s)) throw std::runtime_error("prefill_gemm: shape outside the v5 geometries");
   LLMI_HIP(hipGetLastError());
 }
 

@@ -612,6 +612,19 @@ void launch_finalize_token(unsigned long long* keys, int n_keys, int shard, int3
   LLMI_HIP(hipGetLastError());
 }
 
+// the token loop's per-token inputs as kernel arguments (no host staging buffer, so no stream sync and no
+// pinned-memory copy between the step-graph replays)
+__global__ void set_token_pos_kernel(int32_t* d_token, int32_t* d_pos, int32_t* ring_idx, int token, int pos, int reset) {
+  *d_token = token;
+  *d_pos = pos;
+  if (reset) *ring_idx = 0;
+}
+void launch_set_token_pos(int32_t* d_token, int32_t* d_pos, int32_t* ring_idx, int token, int pos, bool reset,
+                          hipStream_t s) {
+  hipLaunchKernelGGL(set_token_pos_kernel, dim3(1), dim3(1), 0, s, d_token, d_pos, ring_idx, token, pos, reset ? 1 : 0);
+  LLMI_HIP(hipGetLastError());
+}
+
 // ---------------------------------------------------------------------------
 // embedding lookup + scale + first attn_norm, in one block
 // ---------------------------------------------------------------------------

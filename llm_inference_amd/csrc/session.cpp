@@ -625,6 +625,7 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
       blk_xo_ = dalloc<XBlock>((size_t)nh_ * maxhd / 32 + 1);
     }
     setup_engine(g);
+    if (!engine_) setup_ffn_engine(g);
   } catch (const gguf_error& e) {
     release();
     throw status_error(LLMI_E_GGUF, e.what());
@@ -1099,6 +1100,53 @@ void Session::setup_engine(const GGUFView& g) {
   engine_ = true;
 }
 
+// The FFN engine (k_engine.hip): gate_up + GELU + down of a Q4_0 layer as one launch of one 1024-thread
+// work-group per CU, both weights issued at launch start.  Opt-in (LLMI_FFN_ENGINE=1): measured slower than the
+// two launches (747 vs 926 tok/s on 4B: the prologue's operands and the GELU exchange queue behind the 44 MB
+// weight stream; profiles/r03_engine_trace.txt).
+void Session::setup_ffn_engine(const GGUFView& g) {
+  ffn_engine_ = false;
+  const char* on = getenv("LLMI_FFN_ENGINE");
+  if (!on || atoi(on) == 0) return;
+  if (!fuse_layers_ || tp_ || !dup_.empty() || ple_table_.qs || hp_.gemma4) return;
+  for (const auto& l : L_)
+    if (!l.fused || l.gate_up.size() != 1 || l.gate_up[0].w.type != T_Q4_0 || l.down.w.type != T_Q4_0 ||
+        l.out_scale != 1.0f || !l.post_attn_norm || !l.ffn_norm)
+      return;
+  EngineLayer plan;
+  if (!ffn_engine_plan(hp_.n_embd, hp_.n_ff, plan)) return;
+  const int E = hp_.n_embd, F = hp_.n_ff, H = plan.ru;
+  constexpr size_t kSlack = 8192;  // the down rows are read in whole 1-KB LDS-DMA pieces
+  eng_w_.resize(hp_.n_layer);
+  for (int l = 0; l < hp_.n_layer; l++) {
+    const std::string b = "blk." + std::to_string(l) + ".";
+    const GTensor *gt = g.tensor(b + "ffn_gate.weight"), *up = g.tensor(b + "ffn_up.weight");
+    const GTensor* dn = g.tensor(b + "ffn_down.weight");
+    EngWeights& w = eng_w_[l];
+    const size_t rb = gguf_bytes(T_Q4_0, 1, E);
+    std::vector<uint8_t> il((size_t)2 * F * rb);
+    const uint8_t *sg = (const uint8_t*)g.tensor_data(*gt), *su = (const uint8_t*)g.tensor_data(*up);
+    for (int c = 0; c < F / H; c++) {
+      std::memcpy(&il[(size_t)(2 * H * c) * rb], sg + (size_t)(H * c) * rb, H * rb);
+      std::memcpy(&il[(size_t)(2 * H * c + H) * rb], su + (size_t)(H * c) * rb, H * rb);
+    }
+    w.g = alloc_weight(T_Q4_0, 2 * F, E, kSlack);
+    upload_rows(w.g, 0, il.data(), 2 * F, stream_);
+    w.d = alloc_weight(T_Q4_0, E, F, kSlack);
+    upload_rows(w.d, 0, g.tensor_data(*dn), E, stream_);
+  }
+  eng_ = plan;
+  eng_epoch_ = dalloc<unsigned>(1);
+  eng_ghid_ = dalloc<uint2>(F);
+  if (!blk_err_) blk_err_ = dalloc<int>(2);
+  if (!blk_trace_)
+    if (const char* tr = getenv("LLMI_BLOCK_TRACE")) {
+      blk_trace_layer_ = atoi(tr);
+      blk_trace_ = dalloc<unsigned long long>(4096 * 8);
+    }
+  ffn_engine_ = true;
+}
+
 EngineLayer Session::engine_args(int l, float* resid_in, float* resid_out) const {
   const LayerDev& Ld = L_[l];
   const EngWeights& w = eng_w_[l];
@@ -1295,6 +1343,29 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
       dump("attention results (node_30 for MUL_MAT)-" + L, o_out_, E, s);
     }
     if (tp_) coll_->all_gather(o_out_, (size_t)e_sh_ * sizeof(float), s);
+    if (ffn_engine_ && !dump_ && !trace_fn_) {  // gate_up + GELU + down: one launch
+      EngineLayer a = eng_;
+      a.g_qs = (const uint4*)eng_w_[l].g.qs;
+      a.g_d = eng_w_[l].g.d;
+      a.d_qs = (const uint4*)eng_w_[l].d.qs;
+      a.d_d = eng_w_[l].d.d;
+      a.post_attn_norm = Ld.post_attn_norm;
+      a.ffn_norm = Ld.ffn_norm;
+      a.y_in = o_out_;
+      a.resid_in = cur;
+      a.resid_out = other;
+      a.y_out = d_out_;
+      a.eps = hp_.eps;
+      a.epoch = eng_epoch_;
+      a.g_hid = eng_ghid_;
+      a.err = blk_err_;
+      a.blk_epoch = epoch;  // the attention block's granule tag of this layer (the gate_up launch's job before)
+      if (blk_trace_ && l == blk_trace_layer_) a.trace = blk_trace_;
+      launch_ffn_engine(a, s);
+      std::swap(cur, other);
+      kernels_per_token_ += block_ ? 1 : 2;
+      continue;
+    }
     LayerGemv gg;
     gg.y = o_out_;
     gg.w_post = Ld.post_attn_norm;
@@ -1450,14 +1521,12 @@ void Session::run_step(bool gen) {
   }
 }
 
+// The token and position travel as kernel arguments of a one-thread launch in stream order.  (Round 2 staged
+// them in a pinned buffer: a hipStreamSynchronize + two 4-byte H2D copies before every step-graph replay of the
+// token loop; under rocprofv3 --kernel-trace that sequence aborted after ~33 replays with
+// HSA_STATUS_ERROR_INVALID_PACKET_FORMAT, while the decode loop -- replays only -- profiled clean.)
 void Session::set_token_pos(int32_t token, int pos, bool reset_ring) {
-  LLMI_HIP(hipStreamSynchronize(stream_));  // h_stage_ reuse
-  h_stage_[0] = token;
-  h_stage_[1] = pos;
-  h_stage_[2] = 0;
-  LLMI_HIP(hipMemcpyAsync(d_token_, &h_stage_[0], 4, hipMemcpyHostToDevice, stream_));
-  LLMI_HIP(hipMemcpyAsync(d_pos_, &h_stage_[1], 4, hipMemcpyHostToDevice, stream_));
-  if (reset_ring) LLMI_HIP(hipMemcpyAsync(ring_idx_, &h_stage_[2], 4, hipMemcpyHostToDevice, stream_));
+  launch_set_token_pos(d_token_, d_pos_, ring_idx_, token, pos, reset_ring, stream_);
 }
 
 void Session::forward(const int32_t* tokens, int n, int pos, float* logits, int32_t* argmax) {
@@ -1631,6 +1700,7 @@ void Session::info(llmi_session_info* o) const {
   o->screen_bytes = screen_ ? scr_.bytes : 0;
   o->prefill_f16_redo = pf_f16_redo_;
   o->layer_engine = engine_ ? 1 : 0;
+  o->ffn_engine = ffn_engine_ ? 1 : 0;
   size_t b = logits_w_.bytes;  // this rank's bytes
   for (const auto& l : L_) {
     for (const auto& p : l.qkv) b += p.w.bytes;
@@ -1706,7 +1776,8 @@ void Session::time_kernel(int which, int reps, double* us, double* bytes) {
   //   5: the r01 family: qkv PRO, o PLAIN, gate_up, down as standalone launches
   bool fused = fuse_layers_;
   for (const auto& l : L_) fused &= l.fused;
-  if (!fused || (which == 0 && !block_) || (which == 6 && !engine_) || which < 0 || which > 6 || reps <= 0) {
+  if (!fused || (which == 0 && !block_) || (which == 6 && !engine_) || (which == 7 && !ffn_engine_) || which < 0 ||
+      which > 7 || reps <= 0) {
     *us = *bytes = 0.0;
     return;
   }
@@ -1755,6 +1826,25 @@ void Session::time_kernel(int which, int reps, double* us, double* bytes) {
       const EngineLayer ea = engine_args((int)i, resid_, resid_scratch_);
       items.push_back({[this, ea]() { launch_layer_engine(ea, false, stream_); },
                        (double)(Ld.qkv[0].w.bytes + Ld.o.w.bytes + Ld.gate_up[0].w.bytes + Ld.down.w.bytes) + kv});
+    }
+    if (which == 7) {  // the FFN engine: gate_up + GELU + down, its own weights
+      EngineLayer ea = eng_;
+      ea.g_qs = (const uint4*)eng_w_[i].g.qs;
+      ea.g_d = eng_w_[i].g.d;
+      ea.d_qs = (const uint4*)eng_w_[i].d.qs;
+      ea.d_d = eng_w_[i].d.d;
+      ea.post_attn_norm = Ld.post_attn_norm;
+      ea.ffn_norm = Ld.ffn_norm;
+      ea.y_in = o_out_;
+      ea.resid_in = resid_;
+      ea.resid_out = resid_scratch_;
+      ea.y_out = d_out_;
+      ea.eps = hp_.eps;
+      ea.epoch = eng_epoch_;
+      ea.g_hid = eng_ghid_;
+      ea.err = blk_err_;
+      items.push_back({[this, ea]() { launch_ffn_engine(ea, stream_); },
+                       (double)(Ld.gate_up[0].w.bytes + Ld.down.w.bytes)});
     }
     if (which == 5) {
       items.push_back({[this, &Ld, q]() { launch_layer_gemv(Ld.qkv[0].w, q, LAYER_PRO, stream_); },

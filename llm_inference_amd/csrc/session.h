@@ -93,6 +93,7 @@ class Session {
   void record_layers(hipStream_t s, bool x_q8);
   void record_layers_fused(hipStream_t s, bool x_q8);
   void setup_engine(const GGUFView& g);
+  void setup_ffn_engine(const GGUFView& g);
   void record_layers_engine(hipStream_t s, bool x_q8);
   EngineLayer engine_args(int l, float* resid_in, float* resid_out) const;
   void prepare_act(uint32_t wtype, const float* x, int n, ActBuf& act, hipStream_t s);
@@ -128,7 +129,8 @@ class Session {
   // the layer engine (k_engine.hip): a whole decode layer per launch, one 1024-thread work-group per CU;
   // its own row-major copies of the four projections (gate/up interleaved in groups of eng_.ru)
   bool engine_ = false;
-  EngineLayer eng_{};                     // the per-CU split (engine_plan)
+  bool ffn_engine_ = false;               // gate_up + down of each layer as one launch (k_engine.hip FFN engine)
+  EngineLayer eng_{};                     // the per-CU split (engine_plan / ffn_engine_plan)
   struct EngWeights { DevWeight q, o, g, d; };
   std::vector<EngWeights> eng_w_;
   unsigned* eng_epoch_ = nullptr;

@@ -107,10 +107,15 @@ struct EngineLayer {
   uint2 *g_qkv = nullptr, *g_xo = nullptr, *g_o = nullptr, *g_hid = nullptr;
   int* err = nullptr;
   unsigned long long* trace = nullptr;  // development: [CU][16] phase clocks (LLMI_BLOCK_TRACE builds)
+  unsigned* blk_epoch = nullptr;        // FFN engine: the attention block's per-layer epoch, advanced at the end
 };
 // fills the per-CU split of `a` and checks the launch fits (shapes, LDS, occupancy)
 bool engine_plan(int E, int F, int n_head, int n_kv, int hd, int qkv_rows, EngineLayer& a);
 void launch_layer_engine(const EngineLayer& a, bool first, hipStream_t s);
+// The FFN engine: gate_up + GELU + down of one layer in one launch after the attention block (y_in = the
+// block's o output; gate_up interleaved in groups of ru, row-major; the down rows with >= 8 KB of slack)
+bool ffn_engine_plan(int E, int F, EngineLayer& a);
+void launch_ffn_engine(const EngineLayer& a, hipStream_t s);
 bool layer_gemv_supported(const DevWeight& w, int role);
 // ---- batched prefill (k_prefill.hip) ----
 struct PrefillNorm {  // per token: embedding (table != null) or residual + norm, then x -> Q8_0
@@ -220,5 +225,8 @@ void launch_screen_argmax(const DevWeight& table, const ScreenTable& st, const u
                           unsigned long long* amax_key, hipStream_t s);
 void launch_finalize_token(unsigned long long* keys, int n_keys, int shard, int32_t* d_token, int32_t* d_pos,
                            int32_t* ring, int32_t* ring_idx, int ring_cap, hipStream_t s);
+// d_token = token, d_pos = pos (and ring_idx = 0 when reset): the token loop's inputs, in stream order
+void launch_set_token_pos(int32_t* d_token, int32_t* d_pos, int32_t* ring_idx, int token, int pos, bool reset,
+                          hipStream_t s);
 
 }  // namespace llmi

@@ -183,3 +183,17 @@ def test_f16_logits_widths(ops, rows, cols):
     o = ops.mat_vec_mul_raw(T.F16, w.view(np.uint16), rows, cols, x, exact=False)
     ref = w.astype(np.float64) @ x.astype(np.float16).astype(np.float64)
     assert np.abs(o - ref).max() <= 1e-4 * np.abs(ref).max() + 1e-6
+
+
+@pytest.mark.parametrize("rows,cols", [(40, 6912), (37, 1152), (3, 32), (260, 2560)])
+def test_gemv_q5_0_fast_vs_oracle(ops, oracle, rows, cols):
+    """Fast Q5_0 GEMV (k_gemv.hip gemv_q5_0_fast: the Q4_K_M files' fallback type for 1152-wide tensors,
+    ops.cpp:840-893) vs the oracle restatement at ragged shapes: the module's fast-GEMV tolerance; the exact
+    kernel stays bit-identical."""
+    from llm_inference_amd.synthetic import random_tensor
+    w = random_tensor(T.Q5_0, rows, cols, seed=rows + cols)
+    x = np.random.default_rng(cols).standard_normal(cols).astype(np.float32)
+    ref = oracle.mat_vec_mul(T.Q5_0, w, rows, cols, x)
+    np.testing.assert_array_equal(bits(ops.mat_vec_mul_raw(T.Q5_0, w, rows, cols, x, exact=True)), bits(ref))
+    o = ops.mat_vec_mul_raw(T.Q5_0, w, rows, cols, x, exact=False)
+    assert np.abs(o - ref).max() <= 1e-4 * np.abs(ref).max() + 1e-6

@@ -91,36 +91,32 @@ def test_prefill_chunking_is_exact(monkeypatch):
     np.testing.assert_array_equal(tail, ref)
 
 
-def test_prefill_gemm_versions_bitwise(monkeypatch):
-    """The prefill GEMM variants (v1 register-staged 32-row tiles, v3 LDS-DMA
-    ring, v4 = v3 + f32 scale staging + packed f32 epilogue, v5 with one K
-    group per output = the 128 x 128 tile for every shape) compute every
-    output with the same fmaf(d_w * d_x, (float)isum, acc) in block order:
-    identical logits.  v5's default geometries split K over 2 or 4 wave groups
-    (per-group block-order chains, summed in group order): within the fast
-    budget of v1, and exact under re-chunking (test_prefill_chunking_is_exact
-    runs the default)."""
-    from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
-    cfg = CONFIGS["mini-4b"]
-    g = build_gemma3_gguf(cfg, seed=23)
-    prompt = np.random.default_rng(2).integers(4, cfg.vocab, 200).astype(np.int32)
-    out = {}
-    for v in ("1", "3", "4", "5"):
-        monkeypatch.setenv("LLMI_PREFILL_GEMM", v)
-        if v == "5":
-            monkeypatch.setenv("LLMI_PG5", "big")
-        out[v] = _model(g, monkeypatch).forward(prompt, 0)
-    np.testing.assert_array_equal(out["4"], out["1"])
-    np.testing.assert_array_equal(out["3"], out["1"])
-    np.testing.assert_array_equal(out["5"], out["1"])
+def test_prefill_gemm_v5_matches_pinned_v1(monkeypatch):
+    """The retired prefill GEMM v1 (register-staged 32-row tiles; v1-v4 left the library in round 3) computed
+    every output as one fmaf(d_w * d_x, (float)isum, acc) chain in block order.  v5 with one K group per
+    output (LLMI_PG5=big: 128 x 128 tiles) computes the same chain: its logits equal v1's pinned bits
+    (tests/golden/prefill_v1_ref.npz, made by tests/golden/gen_prefill_v1.py on the GPU with v1 still in the
+    library).  v5's default geometries split K over 2 or 4 wave groups (per-group block-order chains, summed
+    in group order): within 1e-2 of v1's logits, and exact under re-chunking
+    (test_prefill_chunking_is_exact runs the default)."""
+    import os
+    sys_path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    import sys
+    sys.path.insert(0, sys_path)
+    import gen_prefill_v1
+    pin = np.load(os.path.join(sys_path, "prefill_v1_ref.npz"))
+    g, prompt = gen_prefill_v1.case()
+    assert np.array_equal(pin["prompt"], prompt)
+    monkeypatch.setenv("LLMI_PG5", "big")
+    big = _model(g, monkeypatch, max_ctx=256).forward(prompt, 0)  # the pin's session geometry
+    np.testing.assert_array_equal(big.view(np.uint32), pin["logits"].view(np.uint32))
     for geo in ("mid", "small", "small4"):
         monkeypatch.setenv("LLMI_PG5", geo)
-        got = _model(g, monkeypatch).forward(prompt, 0)
-        d = float(np.abs(got - out["1"]).max())
+        got = _model(g, monkeypatch, max_ctx=256).forward(prompt, 0)
+        d = float(np.abs(got - pin["logits"]).max())
         print(f"v5 {geo}: max|dlogit| vs v1 {d:.3g}")
         assert d <= 1e-2
     monkeypatch.delenv("LLMI_PG5")
-    monkeypatch.delenv("LLMI_PREFILL_GEMM")
 
 
 @pytest.mark.parametrize("cfg_name,n_prompt", [("mini-4b", 300), ("mini-1b", 77), ("mini-27b", 45)])
