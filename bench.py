@@ -47,6 +47,8 @@ def parse():
     p.add_argument("--cpu-decode", type=int, default=32, help="decode tokens in the CPU baseline sample")
     p.add_argument("--kernel-reps", type=int, default=2)
     p.add_argument("--no-graph", action="store_true", help="eager launches (for kernel tracers)")
+    p.add_argument("--exchange", choices=["push", "rccl"], default="push",
+                   help="tp: the one-shot push all-gather over IPC-mapped mailboxes (k_exchange.hip) or RCCL")
     p.add_argument("--mode", choices=["tp", "replicas"], default="tp",
                    help="N>1: row-sharded tensor parallel (one stream) or independent replicas")
     p.add_argument("--quant", choices=["q4_0", "q4_k_m", "q8_0"], default="q4_0",
@@ -103,6 +105,14 @@ class Dist:
         box = [obj]
         self.dist.broadcast_object_list(box, src=0)
         return box[0]
+
+    def all_gather(self, obj) -> list:
+        """Every rank's object, in rank order (the push exchange's mailbox handles)."""
+        if self.world == 1:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
 
     def max(self, v: float) -> float:
         if self.world == 1:
@@ -259,11 +269,33 @@ def main():
     g = build_gemma3_gguf(cfg, seed=1234, **qkw)
     t_build = time.time() - t0
     max_ctx = a.prefill + a.warmup + a.steps + 8
-    tp_kw = {}
-    if tp:  # one RCCL communicator over the node's GPUs
-        tp_kw = dict(tp_rank=d.rank, tp_size=d.world, tp_id=d.broadcast(tp_unique_id() if d.rank == 0 else None))
-    m = Model(g, device=d.local if a.gpus > 1 else 0, exact=a.exact, max_ctx=max_ctx, use_graph=not a.no_graph,
-              **tp_kw)
+    # LLMI_BENCH_ONE_DEVICE=1 (development): every rank on device 0 -- the tp path rehearsed on a one-GPU box
+    dev = d.local if a.gpus > 1 and not os.environ.get("LLMI_BENCH_ONE_DEVICE") else 0
+
+    def rccl_model():  # one RCCL communicator over the node's GPUs
+        tid = d.broadcast(tp_unique_id() if d.rank == 0 else None)
+        return Model(g, device=dev, exact=a.exact, max_ctx=max_ctx, use_graph=not a.no_graph, tp_rank=d.rank,
+                     tp_size=d.world, tp_id=tid)
+
+    exchange = a.exchange if tp else None
+    if not tp:
+        m = Model(g, device=dev, exact=a.exact, max_ctx=max_ctx, use_graph=not a.no_graph)
+    elif exchange == "rccl":
+        m = rccl_model()
+    else:  # push: every rank's mailbox handle to every rank; if any rank cannot map them, all fall back to RCCL
+        m = Model(g, device=dev, exact=a.exact, max_ctx=max_ctx, use_graph=not a.no_graph, tp_rank=d.rank,
+                  tp_size=d.world, tp_peer=True)
+        err = None
+        try:
+            handles = d.all_gather(m.peer_handle())
+            m.peer_connect(handles)
+        except Exception as e:  # noqa: BLE001 -- reported, then the RCCL exchange
+            err = e
+        if d.max(1.0 if err is not None else 0.0) > 0:
+            print(f"[bench] rank {d.rank}: push exchange unavailable ({err!r}); RCCL instead", file=sys.stderr)
+            m.close()
+            exchange = "rccl"
+            m = rccl_model()
     info = m.info
     rng = np.random.default_rng(99 + (0 if tp else d.rank))  # tensor-parallel ranks decode the same stream
     prompt = np.concatenate([[2], rng.integers(4, cfg.vocab, a.prefill - 1)]).astype(np.int32)
@@ -362,7 +394,9 @@ def main():
             "workload": f"{cfg.name}-{a.quant} greedy decode after a {a.prefill}-token prefill "
                         f"(BASELINE {base_cfg})",
             "prefill_tokens": a.prefill, "decode_tokens": a.steps, "mode": "exact" if a.exact else "fast",
-            "parallelism": (f"tp{d.world} (row-sharded, RCCL all-gather)" if tp else f"replicas{d.world}")
+            "parallelism": (f"tp{d.world} (row-sharded, " + ("one-shot push all-gather over IPC-mapped mailboxes"
+                                                              if exchange == "push" else "RCCL all-gather") + ")"
+                            if tp else f"replicas{d.world}")
                            if d.world > 1 else "single",
             "kernels_per_token": info.kernels_per_token,
         },

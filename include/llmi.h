@@ -47,6 +47,8 @@ typedef enum {
 /* flags */
 #define LLMI_EXACT 1u      /* bit-exact AVX2-order kernels */
 #define LLMI_NO_GRAPH 2u   /* session: launch kernels eagerly instead of one hipGraph per token */
+#define LLMI_TP_PEER 4u    /* session: tensor-parallel rank of tp_size processes (one per GPU) exchanging by
+                              one-shot peer push (llmi_session_peer_connect) instead of RCCL */
 
 const char* llmi_last_error(void);
 int llmi_version(void);
@@ -120,14 +122,26 @@ typedef struct {
   int tp_rank, tp_size;
   const void* tp_id;        /* LLMI_TP_ID_BYTES from llmi_tp_unique_id on one rank: RCCL over xGMI */
   llmi_tp_group* tp_group;  /* or: ranks on one device in one process (tests; one host thread per rank) */
+  /* or (both NULL, flags LLMI_TP_PEER): the one-shot push exchange between processes, below */
 } llmi_session_opts;
 
 #define LLMI_TP_ID_BYTES 128
 /* new RCCL communicator id (ncclGetUniqueId); distribute it to every rank */
 int llmi_tp_unique_id(void* out);
-/* single-device group of `size` ranks: device-to-device slice copies */
+/* single-device group of `size` ranks: the push exchange split around a host barrier (LLMI_TP_EXCHANGE=copy:
+ * device-to-device slice copies) */
 int llmi_tp_group_create(int size, llmi_tp_group** out);
 void llmi_tp_group_destroy(llmi_tp_group* g);
+
+/* One-shot push exchange (replaces ncclAllGather, the exchange of ops.cpp:439-450's row split
+ * across devices): every rank writes its slice of each all-gather as data-tagged 8-byte granules {word, tag}
+ * straight into every peer's mailbox through xGMI peer mappings, then polls its own mailbox -- one kernel per
+ * exchange, captured in the token's hipGraph.  A LLMI_TP_PEER session: after creation, every rank publishes
+ * its mailbox handle, and before its first forward connects to all of them (rank order, tp_size x
+ * LLMI_PEER_HANDLE_BYTES); the handles travel by any host channel (bench.py: torch.distributed). */
+#define LLMI_PEER_HANDLE_BYTES 64
+int llmi_session_peer_handle(const llmi_session* s, void* out);
+int llmi_session_peer_connect(llmi_session* s, const void* handles);
 
 /* Parses the GGUF (format of gguf.cpp:274-304, hparams of model.cpp:58-167)
  * and uploads every weight.  The bytes are only read during the call. */
@@ -196,6 +210,7 @@ typedef struct {
   int layer_engine;           /* 1: each decode layer is ONE launch of the layer engine (one 1024-thread work-group
                                  per CU, the layer's weights issued at launch start: DESIGN.md section 4.3) */
   int ffn_engine;             /* 1: gate_up + GELU + down of each layer are ONE launch (the FFN engine) */
+  int tp_exchange;            /* tensor-parallel exchange: 0 none, 1 RCCL, 2 device copies, 3 one-shot push */
 } llmi_session_info;
 int llmi_session_get_info(const llmi_session* s, llmi_session_info* info);
 

@@ -17,6 +17,8 @@ LIB_PATH = os.environ.get("LLMI_LIB") or os.path.join(HERE, "libllmi.so")
 
 LLMI_EXACT = 1
 LLMI_NO_GRAPH = 2
+LLMI_TP_PEER = 4
+PEER_HANDLE_BYTES = 64
 
 STATUS = {0: "OK", 1: "E_SIZE", 2: "E_TYPE", 3: "E_ARG", 4: "E_HIP", 5: "E_GGUF", 6: "E_NODEV", 7: "E_RANGE"}
 
@@ -48,7 +50,7 @@ class SessionInfo(C.Structure):
                 ("kv_bytes_per_pos", C.c_size_t), ("kernels_per_token", C.c_int),
                 ("tp_rank", C.c_int), ("tp_size", C.c_int), ("batched_prefill", C.c_int),
                 ("screened_logits", C.c_int), ("screen_bytes", C.c_size_t), ("prefill_f16_redo", C.c_int),
-                ("layer_engine", C.c_int), ("ffn_engine", C.c_int)]
+                ("layer_engine", C.c_int), ("ffn_engine", C.c_int), ("tp_exchange", C.c_int)]
 
 
 _lib = None
@@ -79,6 +81,8 @@ _SIGS = {
     "llmi_tp_unique_id": (C.c_int, [_vp]),
     "llmi_tp_group_create": (C.c_int, [C.c_int, C.POINTER(_vp)]),
     "llmi_tp_group_destroy": (None, [_vp]),
+    "llmi_session_peer_handle": (C.c_int, [_vp, _vp]),
+    "llmi_session_peer_connect": (C.c_int, [_vp, _vp]),
     "llmi_session_forward": (C.c_int, [_vp, _vp, C.c_int, C.c_int, _vp, _vp]),
     "llmi_session_generate": (C.c_int, [_vp, _i32, C.c_int, C.c_int, _vp]),
     "llmi_session_dump": (C.c_int, [_vp, _vp, C.c_int, C.c_int, C.c_char_p]),

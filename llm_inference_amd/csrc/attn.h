@@ -52,10 +52,12 @@ void launch_qk_norm_rope_kv(const QKVArgs& a, bool exact, hipStream_t s);
 void launch_attention(const AttnArgs& a, bool exact, hipStream_t s, const QKVArgs* fused = nullptr);
 // qkv GEMV (qrole LAYER_PLAIN / LAYER_PRO) + fused attention + o GEMV in one
 // launch (k_attn.hip, attention block); qg.out must be qa.qkv, og.xg must be
-// aa.q8.  attn_block_supported: a launch-table entry exists for the shapes.
+// aa.q8.  attn_block_supported: a launch-table entry exists for the shapes and
+// the qkv role (LAYER_PLAIN: x blocks given; LAYER_PRO: residual + norms in the
+// launch's prologue), and its grid is co-resident.
 // wqkv_b: the second qkv weight of a q|k Q4_K + v Q6_K layer (kq layout), or null
 bool attn_block_supported(const DevWeight& wqkv, const DevWeight* wqkv_b, const DevWeight& wo, int head_dim,
-                          int n_head, int n_head_kv);
+                          int n_head, int n_head_kv, int qrole);
 void launch_attn_block(const DevWeight& wqkv, const DevWeight* wqkv_b, LayerGemv qg, int qrole, const DevWeight& wo,
                        LayerGemv og,
                        const AttnArgs& aa, const QKVArgs& qa, BlockSync bs, hipStream_t s);

@@ -472,6 +472,22 @@ int llmi_tp_group_create(int size, llmi_tp_group** out) {
 
 void llmi_tp_group_destroy(llmi_tp_group* g) { delete reinterpret_cast<LocalGroup*>(g); }
 
+static_assert(LLMI_PEER_HANDLE_BYTES == PEER_HANDLE_BYTES, "peer handle size");
+
+int llmi_session_peer_handle(const llmi_session* s, void* out) {
+  return guard([&] {
+    if (!s || !out) throw status_error(LLMI_E_ARG, "peer handle: null argument");
+    s->s->peer_handle(out);
+  });
+}
+
+int llmi_session_peer_connect(llmi_session* s, const void* handles) {
+  return guard([&] {
+    if (!s) throw status_error(LLMI_E_ARG, "peer connect: null session");
+    s->s->peer_connect(handles);
+  });
+}
+
 int llmi_session_get_info(const llmi_session* s, llmi_session_info* info) {
   return guard([&] { s->s->info(info); });
 }

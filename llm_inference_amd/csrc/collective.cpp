@@ -3,7 +3,9 @@
 
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -18,6 +20,9 @@ namespace llmi {
     if (r_ != ncclSuccess) throw hip_error(std::string(#call) + ": " + ncclGetErrorString(r_)); \
   } while (0)
 
+void Collective::peer_handle(void*) const { throw std::runtime_error("peer handle: not a push-exchange (LLMI_TP_PEER) session"); }
+void Collective::peer_connect(const void*) { throw std::runtime_error("peer connect: not a push-exchange (LLMI_TP_PEER) session"); }
+
 void rccl_unique_id(void* out128) {
   static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
   ncclUniqueId id;
@@ -26,6 +31,111 @@ void rccl_unique_id(void* out128) {
 }
 
 namespace {
+
+// One rank's side of the push exchange (k_exchange.hip): its mailbox of [2 halves][G slots][kCap] granules,
+// the peers' mailboxes as mapped into this process, and the exchange counter.  Messages longer than kCap words
+// per rank go as consecutive exchanges of kCap-word chunks.
+class Mailbox {
+ public:
+  static constexpr int kCap = 1 << 18;  // words per rank slot (1 MB of payload): every decode exchange in one
+  Mailbox(int rank, int G, bool ipc) : rank_(rank), G_(G) {
+    if (G < 1 || G > PX_MAX_RANKS) throw std::runtime_error("push exchange: 1-16 ranks");
+    const size_t bytes = (size_t)2 * G * kCap * sizeof(uint2);
+    // uncached (fine-grained) memory for the cross-process case: peers' stores land in HBM and this rank's
+    // system-scope loads read HBM (the same-process group shares one device's L2 and takes plain memory)
+    if (ipc) LLMI_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&mine_), bytes, hipDeviceMallocUncached));
+    else LLMI_HIP(hipMalloc(&mine_, bytes));
+    LLMI_HIP(hipMemset(mine_, 0, bytes));  // tag 0: nothing published (the first exchange's tag is 1)
+    LLMI_HIP(hipMalloc(&ctl_, 4 * sizeof(unsigned)));
+    LLMI_HIP(hipMemset(ctl_, 0, 4 * sizeof(unsigned)));
+    LLMI_HIP(hipDeviceSynchronize());
+    peers_.assign(G, nullptr);
+    peers_[rank] = mine_;
+  }
+  ~Mailbox() {
+    for (int q = 0; q < G_; q++)
+      if (q != rank_ && opened_ && peers_[q]) (void)hipIpcCloseMemHandle(peers_[q]);
+    (void)hipFree(mine_);
+    (void)hipFree(ctl_);
+  }
+  uint2* mine() const { return mine_; }
+  void set_peer(int q, uint2* p) { peers_[q] = p; }
+  bool connected() const {
+    for (uint2* p : peers_)
+      if (!p) return false;
+    return true;
+  }
+  void handle(void* out) const {
+    static_assert(sizeof(hipIpcMemHandle_t) <= PEER_HANDLE_BYTES, "IPC handle size");
+    hipIpcMemHandle_t h;
+    LLMI_HIP(hipIpcGetMemHandle(&h, mine_));
+    std::memset(out, 0, PEER_HANDLE_BYTES);
+    std::memcpy(out, &h, sizeof(h));
+  }
+  void open(const void* handles) {
+    for (int q = 0; q < G_; q++) {
+      if (q == rank_) continue;
+      hipIpcMemHandle_t h;
+      std::memcpy(&h, static_cast<const char*>(handles) + (size_t)q * PEER_HANDLE_BYTES, sizeof(h));
+      void* p = nullptr;
+      LLMI_HIP(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+      peers_[q] = static_cast<uint2*>(p);
+    }
+    opened_ = true;
+  }
+  // the all-gather of `bytes` per rank at buf (rank q's slice at buf + q bytes), as `phase` launches
+  void run(void* buf, size_t bytes, int phase, hipStream_t s) {
+    for (size_t c = 0; c < chunks(bytes); c++) run_chunk(buf, bytes, c, phase, s);
+  }
+  // a chunked message is a sequence of exchanges: the split (push / gather) caller needs them one at a time
+  static size_t chunks(size_t bytes) { return (bytes / 4 + kCap - 1) / kCap; }
+  void run_chunk(void* buf, size_t bytes, size_t c, int phase, hipStream_t s) {
+    if (!connected()) throw std::runtime_error("push exchange: peers not connected (llmi_session_peer_connect)");
+    if (bytes % 4) throw std::runtime_error("push exchange: slice bytes % 4 != 0");
+    const size_t words = bytes / 4, off = c * kCap;
+    PushArgs a{};
+    for (int q = 0; q < G_; q++) a.mail[q] = peers_[q];
+    a.buf = static_cast<uint32_t*>(buf) + off;
+    a.stride = words;
+    a.words = (int)std::min<size_t>(kCap, words - off);
+    a.rank = rank_;
+    a.G = G_;
+    a.cap = kCap;
+    a.phase = phase;
+    a.epoch = ctl_;
+    a.ticket = ctl_ + 1;
+    a.err = reinterpret_cast<int*>(ctl_ + 2);
+    launch_push_exchange(a, s);
+  }
+  bool failed() {  // reads and clears the device flag (callers have synchronised the stream)
+    int e = 0;
+    LLMI_HIP(hipMemcpy(&e, ctl_ + 2, sizeof(int), hipMemcpyDeviceToHost));
+    if (e) LLMI_HIP(hipMemset(ctl_ + 2, 0, sizeof(int)));
+    return e != 0;
+  }
+
+ private:
+  int rank_, G_;
+  uint2* mine_ = nullptr;
+  unsigned* ctl_ = nullptr;  // [0] exchange count, [1] ticket, [2] error flag
+  std::vector<uint2*> peers_;
+  bool opened_ = false;
+};
+
+// one process per GPU, the push exchange through IPC-mapped mailboxes
+class PeerCollective : public Collective {
+ public:
+  PeerCollective(int rank, int size) : Collective(rank, size), mb_(rank, size, true) {}
+  bool graph_safe() const override { return true; }
+  int kind() const override { return EX_PUSH; }
+  void all_gather(void* buf, size_t bytes, hipStream_t s) override { mb_.run(buf, bytes, PX_PUSH | PX_GATHER, s); }
+  bool failed() override { return mb_.failed(); }
+  void peer_handle(void* out) const override { mb_.handle(out); }
+  void peer_connect(const void* handles) override { mb_.open(handles); }
+
+ private:
+  Mailbox mb_;
+};
 
 class RcclCollective : public Collective {
  public:
@@ -38,6 +148,7 @@ class RcclCollective : public Collective {
     if (comm_) (void)ncclCommDestroy(comm_);
   }
   bool graph_safe() const override { return true; }
+  int kind() const override { return EX_RCCL; }
   void all_gather(void* buf, size_t bytes, hipStream_t s) override {
     char* b = static_cast<char*>(buf);
     LLMI_NCCL(ncclAllGather(b + (size_t)rank_ * bytes, b, bytes, ncclUint8, comm_, s));
@@ -50,21 +161,29 @@ class RcclCollective : public Collective {
 class LocalCollective : public Collective {
  public:
   LocalCollective(LocalGroup* g, int rank) : Collective(rank, g->n), g_(g) {
+    const char* ex = getenv("LLMI_TP_EXCHANGE");
+    push_ = !(ex && std::string(ex) == "copy");
+    if (push_) mb_.reset(new Mailbox(rank, g->n, false));
     std::lock_guard<std::mutex> lk(g->mu);
     if (rank < 0 || rank >= g->n || g->joined[rank]) throw std::runtime_error("local group: bad or duplicate rank");
     g->joined[rank] = true;
+    if (push_) g->mail[rank] = mb_->mine();
     LLMI_HIP(hipEventCreateWithFlags(&g->ready[rank], hipEventDisableTiming));
     LLMI_HIP(hipEventCreateWithFlags(&g->done[rank], hipEventDisableTiming));
   }
   ~LocalCollective() override {
     std::lock_guard<std::mutex> lk(g_->mu);
     g_->joined[rank_] = false;
+    g_->mail[rank_] = nullptr;
     (void)hipEventDestroy(g_->ready[rank_]);
     (void)hipEventDestroy(g_->done[rank_]);
     g_->ready[rank_] = g_->done[rank_] = nullptr;
   }
   bool graph_safe() const override { return false; }
+  int kind() const override { return push_ ? EX_PUSH : EX_COPY; }
+  bool failed() override { return push_ && mb_->failed(); }
   void all_gather(void* buf, size_t bytes, hipStream_t s) override {
+    if (push_) return push_gather(buf, bytes, s);
     LocalGroup& g = *g_;
     char* b = static_cast<char*>(buf);
     // 1. publish this rank's buffer once its slice is written
@@ -86,7 +205,28 @@ class LocalCollective : public Collective {
   }
 
  private:
+  // push launch, host barrier, then the gather launch once every peer's push has run (the ranks' streams
+  // share this process's hardware queues: a gather spinning ahead of a peer's push could block it)
+  void push_gather(void* buf, size_t bytes, hipStream_t s) {
+    LocalGroup& g = *g_;
+    if (!mb_->connected()) {  // first exchange: every rank has registered its mailbox
+      g.barrier();
+      for (int q = 0; q < size_; q++) mb_->set_peer(q, g.mail[q]);
+    }
+    for (size_t c = 0; c < Mailbox::chunks(bytes); c++) {
+      mb_->run_chunk(buf, bytes, c, PX_PUSH, s);
+      LLMI_HIP(hipEventRecord(g.ready[rank_], s));
+      g.barrier();
+      for (int q = 0; q < size_; q++)
+        if (q != rank_) LLMI_HIP(hipStreamWaitEvent(s, g.ready[q], 0));
+      mb_->run_chunk(buf, bytes, c, PX_GATHER, s);
+      g.barrier();  // nobody records its next push event before every peer has waited on this one
+    }
+  }
+
   LocalGroup* g_;
+  bool push_ = true;
+  std::unique_ptr<Mailbox> mb_;
 };
 
 // diagnostics (LLMI_TP_SOLO): one rank of a sharded group with the exchange
@@ -95,6 +235,7 @@ class NullCollective : public Collective {
  public:
   using Collective::Collective;
   bool graph_safe() const override { return true; }
+  int kind() const override { return EX_NONE; }
   void all_gather(void*, size_t, hipStream_t) override {}
 };
 
@@ -104,7 +245,8 @@ std::unique_ptr<Collective> make_null(int rank, int size) {
   return std::unique_ptr<Collective>(new NullCollective(rank, size));
 }
 
-LocalGroup::LocalGroup(int n_) : n(n_), joined(n_, false), bufs(n_, nullptr), ready(n_, nullptr), done(n_, nullptr) {
+LocalGroup::LocalGroup(int n_)
+    : n(n_), joined(n_, false), bufs(n_, nullptr), ready(n_, nullptr), done(n_, nullptr), mail(n_, nullptr) {
   if (n_ < 1) throw std::runtime_error("local group: size < 1");
 }
 
@@ -129,6 +271,10 @@ std::unique_ptr<Collective> make_rccl(int rank, int size, const void* id128) {
 
 std::unique_ptr<Collective> make_local(LocalGroup* g, int rank) {
   return std::unique_ptr<Collective>(new LocalCollective(g, rank));
+}
+
+std::unique_ptr<Collective> make_peer(int rank, int size) {
+  return std::unique_ptr<Collective>(new PeerCollective(rank, size));
 }
 
 }  // namespace llmi

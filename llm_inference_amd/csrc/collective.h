@@ -9,10 +9,18 @@
 //
 //  * RcclCollective: one process per GPU, ncclAllGather over xGMI; capturable
 //    into the session's per-token hipGraph.
-//  * LocalCollective: G sessions on ONE device driven from G host threads,
-//    exchanging slices with device-to-device copies.  Not capturable (it
-//    synchronises the host threads at every call); it exists so the sharding
-//    itself is testable on a single GPU (RCCL refuses two ranks per device).
+//  * PeerCollective: one process per GPU, the one-shot push exchange of
+//    k_exchange.hip (every rank writes its slice as data-tagged granules into
+//    every peer's mailbox through xGMI peer mappings, then polls its own: one
+//    kernel per all-gather, no RCCL call); the mailboxes' IPC handles are
+//    swapped by the caller (llmi_session_peer_handle / _connect).  Capturable.
+//  * LocalCollective: G sessions on ONE device driven from G host threads.
+//    Default: the same push kernel, split into push and gather launches around
+//    a host barrier (one process's ranks share its hardware queues, so a
+//    waiting gather must not be able to block a peer's push); LLMI_TP_EXCHANGE=
+//    copy: device-to-device slice copies.  Not capturable (it synchronises the
+//    host threads at every call); it exists so the sharding and the exchange
+//    are testable on a single GPU (RCCL refuses two ranks per device).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -25,6 +33,9 @@
 
 namespace llmi {
 
+// exchange kinds (llmi_session_info.tp_exchange)
+enum { EX_NONE = 0, EX_RCCL = 1, EX_COPY = 2, EX_PUSH = 3 };
+
 class Collective {
  public:
   Collective(int rank, int size) : rank_(rank), size_(size) {}
@@ -32,12 +43,34 @@ class Collective {
   int rank() const { return rank_; }
   int size() const { return size_; }
   virtual bool graph_safe() const = 0;
+  virtual int kind() const = 0;
   // in place: this rank's slice is already at buf + rank * bytes
   virtual void all_gather(void* buf, size_t bytes, hipStream_t s) = 0;
+  // a bounded device-side wait of the exchange timed out since the last call (flag cleared)
+  virtual bool failed() { return false; }
+  // push exchange between processes: this rank's mailbox handle, then every rank's (rank order)
+  virtual void peer_handle(void* out) const;
+  virtual void peer_connect(const void* handles);
 
  protected:
   int rank_, size_;
 };
+
+// ---- the one-shot push all-gather (k_exchange.hip) ----
+constexpr int PX_MAX_RANKS = 16;
+constexpr int PX_PUSH = 1, PX_GATHER = 2;
+struct PushArgs {
+  uint2* mail[PX_MAX_RANKS];  // every rank's mailbox [2][G][cap] granules (this process's mapping of it)
+  uint32_t* buf;              // rank q's slice of this exchange at buf + q * stride (words)
+  size_t stride;
+  int words;                  // per rank, <= cap
+  int rank, G, cap, phase;    // phase: PX_PUSH | PX_GATHER
+  unsigned* epoch;            // exchanges completed (tag = epoch + 1)
+  unsigned* ticket;           // work-groups done with the gather (the last one advances epoch)
+  int* err;                   // set when a wait times out
+};
+void launch_push_exchange(const PushArgs& a, hipStream_t s);
+constexpr int PEER_HANDLE_BYTES = 64;
 
 // unique id for a new RCCL communicator (rank 0 makes it, the caller
 // distributes it, every rank passes it to make_rccl)
@@ -59,9 +92,12 @@ struct LocalGroup {
   std::vector<bool> joined;
   std::vector<void*> bufs;
   std::vector<hipEvent_t> ready, done;
+  std::vector<uint2*> mail;  // push exchange: every rank's mailbox (same process, same device)
 };
 
 std::unique_ptr<Collective> make_local(LocalGroup* g, int rank);
+// one process per GPU, push exchange; all_gather throws until peer_connect
+std::unique_ptr<Collective> make_peer(int rank, int size);
 // no exchange at all (diagnostics only: per-rank kernel time of a shard)
 std::unique_ptr<Collective> make_null(int rank, int size);
 

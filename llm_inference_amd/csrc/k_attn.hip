@@ -356,14 +356,15 @@ constexpr int attn_kp() {  // PV key residue classes
 // KVD: virtual kv heads per cache head (GQA groups of 8 run as two work-group
 // sets of 4 q heads over the same cache head: hkv indexes the q-head group,
 // hkv / KVD the cache)
-template <int HD, int G, bool FUSED, int TK, bool BLK = false, int KVD = 1>
+// NS: key-range splits per kv head (ATTN_NSPLIT; 16 in the 27B attention block, whose grid must stay co-resident)
+template <int HD, int G, bool FUSED, int TK, bool BLK = false, int KVD = 1, int NS = ATTN_NSPLIT>
 __device__ __forceinline__ void attn_split_body(const AttnArgs& a, const QKVArgs& qa, uint16_t* __restrict__ s_k,
                                                 uint16_t* __restrict__ s_v, float* __restrict__ s_red,
                                                 const int hkv, const int c, const BlockSync& bs) {
   static_assert(!BLK || FUSED, "BLK implies FUSED");
   const uint32_t btag = BLK ? *bs.epoch + 1u : 0u;  // granule tag, loaded up front
   BLK_MARK(bs, 0);
-  constexpr int NS = ATTN_NSPLIT;
+  static_assert(NS == 32 || NS == 16, "merge reductions are half-wave or row wide");
   static_assert(TK == 32 || TK == 64, "key tile: 32 or 64 keys");
   constexpr int CH = HD / 8;                         // 16-byte chunks per row
   constexpr int TP0 = 4 / G;                         // threads per (head, key) pair
@@ -581,8 +582,7 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, const QKVArgs
   // outputs.  w_c = l_c ? exp(m_c - M) : 0, L = sum_c l_c w_c (half-wave
   // tree), o = sum_c fma(v_c, w_c) in split order, out = o / L.
   // per (head g, split cc) weight w = l ? exp(m - M_g) : 0 and L_g = sum l w,
-  // by half-wave reductions: lane t holds split t % NS of head t / NS (NS = 32)
-  static_assert(NS == 32, "merge reductions are half-wave wide");
+  // by half-wave (NS = 32) or 16-lane row (NS = 16) reductions: lane t holds split t % NS of head t / NS
   float* pg0 = part0 + (size_t)g0 * NS * (HD + 2);  // head g0's partials
   float mv = -INFINITY, lv = 0.0f;
   if (t < GM * NS) {
@@ -610,9 +610,9 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, const QKVArgs
   __shared__ float s_L[G];
   ATTN_MARK(6);
   if (w < (GM * NS + 63) / 64) {  // whole waves
-    const float M = half_max(mv);
+    const float M = NS == 32 ? half_max(mv) : row16_max(mv);
     const float wt = lv == 0.0f ? 0.0f : expf(mv - M);
-    const float L = half_sum(lv * wt);
+    const float L = NS == 32 ? half_sum(lv * wt) : row16_sum(lv * wt);
     if (t < GM * NS) {
       s_wt[t / NS][t % NS] = wt;
       if (t % NS == 0) s_L[t / NS] = L;
@@ -827,7 +827,7 @@ constexpr size_t block_attn_lds() {  // s_k + s_v (32-key tiles) + s_red
 constexpr int WT_W8 = 3;  // Q8_0 weights in the block (layer_body W8), beside the kq formats WT_Q4_K / WT_Q6_K
 
 template <int HD, int G, int QR, int QP, int QE, int QROLE, int OR, int OP, int OE, int WTQ = 0, int WTQB = 0,
-          int WTO = 0, int KVD = 1>
+          int WTO = 0, int KVD = 1, int NS = ATTN_NSPLIT>
 __global__ __launch_bounds__(256) void attn_block_kernel(LayerGemv qg, LayerGemv og, AttnArgs aa, QKVArgs qa,
                                                         BlockSync bs, int nq, LayerGemv qgb, int nqa) {
   extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
@@ -845,14 +845,14 @@ __global__ __launch_bounds__(256) void attn_block_kernel(LayerGemv qg, LayerGemv
     return;
   }
   b -= nq;
-  const int na = aa.n_head_kv * ATTN_NSPLIT;
+  const int na = aa.n_head_kv * NS;
   if (b < na) {
     constexpr int KS = attn_ks<HD, G>();
     uint16_t* s_k = reinterpret_cast<uint16_t*>(s_dyn);
     uint16_t* s_v = s_k + 32 * KS;
     float* s_red = reinterpret_cast<float*>(s_v + 32 * HD);
     // KVD > 1: aa.n_head_kv counts virtual kv heads (G q heads each, KVD per cache head)
-    attn_split_body<HD, G, true, 32, true, KVD>(aa, qa, s_k, s_v, s_red, b % aa.n_head_kv, b / aa.n_head_kv, bs);
+    attn_split_body<HD, G, true, 32, true, KVD, NS>(aa, qa, s_k, s_v, s_red, b % aa.n_head_kv, b / aa.n_head_kv, bs);
     return;
   }
   b -= na;
@@ -863,17 +863,17 @@ using BlockFn = void (*)(dim3, size_t, const LayerGemv&, const LayerGemv&, const
                          const BlockSync&, int, const LayerGemv&, int, hipStream_t);
 
 template <int HD, int G, int QR, int QP, int QE, int QROLE, int OR, int OP, int OE, int WTQ, int WTQB, int WTO,
-          int KVD = 1>
+          int KVD = 1, int NS = ATTN_NSPLIT>
 void block_launch(dim3 grid, size_t lds, const LayerGemv& qg, const LayerGemv& og, const AttnArgs& aa,
                   const QKVArgs& qa, const BlockSync& bs, int nq, const LayerGemv& qgb, int nqa, hipStream_t s) {
   KernelTiming& kt = kernel_timing();
   if (kt.start) {  // bench: events signalled by this dispatch itself (its duration as rocprofv3 reports it)
-    hipExtLaunchKernelGGL((attn_block_kernel<HD, G, QR, QP, QE, QROLE, OR, OP, OE, WTQ, WTQB, WTO, KVD>), grid, dim3(256),
+    hipExtLaunchKernelGGL((attn_block_kernel<HD, G, QR, QP, QE, QROLE, OR, OP, OE, WTQ, WTQB, WTO, KVD, NS>), grid, dim3(256),
                           (uint32_t)lds, s, kt.start, kt.stop, 0u, qg, og, aa, qa, bs, nq, qgb, nqa);
     kt = KernelTiming{};
     return;
   }
-  hipLaunchKernelGGL((attn_block_kernel<HD, G, QR, QP, QE, QROLE, OR, OP, OE, WTQ, WTQB, WTO, KVD>), grid, dim3(256), lds, s,
+  hipLaunchKernelGGL((attn_block_kernel<HD, G, QR, QP, QE, QROLE, OR, OP, OE, WTQ, WTQB, WTO, KVD, NS>), grid, dim3(256), lds, s,
                      qg, og, aa, qa, bs, nq, qgb, nqa);
 }
 
@@ -885,6 +885,7 @@ struct BlockCfg {
   const void* kern;  // the kernel (occupancy query)
   int wtq, wtqb, wto;  // weight formats (layer_body WT): qkv, second qkv weight (0: none), o
   int kvd;             // virtual kv heads per cache head (attention work-groups of g / kvd q heads)
+  int ns = ATTN_NSPLIT;  // key-range splits per kv head
 };
 #define LLMI_BCFGW(NBQ, NBO, HD, G, QROLE, QR, QP, QE, OR, OP, OE, WTQ, WTQB, WTO)                          \
   {NBQ, NBO, HD, G, QROLE, QR, QP, QE, OR, OP, OE, block_attn_lds<HD, G>(),                                  \
@@ -902,6 +903,11 @@ struct BlockCfg {
   LLMI_BCFGVW(NBQ, NBO, HD, GM, KVD, QROLE, QR, QP, QE, OR, OP, OE, 0)
 #define LLMI_BCFG(NBQ, NBO, HD, G, QROLE, QR, QP, QE, OR, OP, OE) \
   LLMI_BCFGW(NBQ, NBO, HD, G, QROLE, QR, QP, QE, OR, OP, OE, 0, 0, 0)
+// NS key-range splits per kv head instead of ATTN_NSPLIT (Q4_0)
+#define LLMI_BCFGS(NBQ, NBO, HD, G, QROLE, QR, QP, QE, OR, OP, OE, NS)                                            \
+  {NBQ, NBO, HD, G, QROLE, QR, QP, QE, OR, OP, OE, block_attn_lds<HD, G>(),                                        \
+   block_launch<HD, G, QR, QP, QE, QROLE, OR, OP, OE, 0, 0, 0, 1, NS>,                                             \
+   reinterpret_cast<const void*>(&attn_block_kernel<HD, G, QR, QP, QE, QROLE, OR, OP, OE, 0, 0, 0, 1, NS>), 0, 0, 0, 1, NS}
 // qkv: 4 waves x QR rows per work-group (rows per work-group must divide
 // head_dim); o: 4 waves x OR rows.  E as in k_layer.hip's table.
 const BlockCfg kBlockCfgs[] = {
@@ -923,6 +929,10 @@ const BlockCfg kBlockCfgs[] = {
     LLMI_BCFGW(80, 64, 256, 2, ROLE_PLAIN, 4, 5, 1, 8, 8, 1, WT_Q4_K, WT_Q6_K, WT_Q4_K),
     LLMI_BCFGW(80, 64, 256, 2, ROLE_PRO, 4, 5, 10, 8, 8, 1, WT_Q4_K, 0, WT_Q4_K),
     LLMI_BCFGW(80, 64, 256, 2, ROLE_PLAIN, 4, 5, 1, 8, 8, 1, WT_Q4_K, 0, WT_Q4_K),
+    // 27B (PLAIN only: the residual + norms run as their own launch, whose 5376-wide prologue would not fit the
+    // registers): qkv 8192 rows -> 256 WGs, 16 kv heads x 16 splits -> 256 attention WGs, o 5376 -> 168 WGs
+    // (680 in all; with 32 splits and 4 rows per wave, 1192, the grid is not co-resident)
+    LLMI_BCFGS(168, 128, 128, 2, ROLE_PLAIN, 8, 21, 2, 8, 16, 2, 16),
 };
 #undef LLMI_BCFG
 #undef LLMI_BCFGW
@@ -971,7 +981,7 @@ static BlockGeom block_geom(const BlockCfg& c, const DevWeight& wqkv, const DevW
                             int n_head_kv, int qrole) {
   BlockGeom g;
   g.nq = (wqkv.rows + (wqkv_b ? wqkv_b->rows : 0) + 4 * c.QR - 1) / (4 * c.QR);
-  g.na = n_head_kv * c.kvd * ATTN_NSPLIT;
+  g.na = n_head_kv * c.kvd * c.ns;
   g.no = (wo.rows + 4 * c.OR - 1) / (4 * c.OR);
   const size_t lds_q = (size_t)(wqkv.cols / 32) * sizeof(XBlock) + 16 + (qrole == ROLE_PRO ? (size_t)wqkv.cols * 4 : 0);
   const size_t lds_o = (size_t)(wo.cols / 32) * sizeof(XBlock) + 16;
@@ -1003,14 +1013,14 @@ static bool block_co_resident(const BlockCfg& c, const BlockGeom& g) {
 }
 
 bool attn_block_supported(const DevWeight& wqkv, const DevWeight* wqkv_b, const DevWeight& wo, int head_dim,
-                          int n_head, int n_head_kv) {
+                          int n_head, int n_head_kv, int qrole) {
   const bool q40 = (wqkv.type == T_Q4_0 || wqkv.type == T_Q8_0) && wo.type == wqkv.type && !wqkv_b && !wqkv.slab &&
                    !wo.slab;
   const bool kq = wqkv.kq && wo.kq && (!wqkv_b || (wqkv_b->kq && wqkv_b->cols == wqkv.cols));
   if (!q40 && !kq) return false;
   if (wqkv.cols % 32 || wo.cols % 32 || n_head_kv <= 0 || n_head % n_head_kv) return false;
   const int g = n_head / n_head_kv;
-  for (int role : {(int)ROLE_PLAIN, (int)ROLE_PRO}) {
+  for (int role : {qrole}) {
     const BlockCfg* c = find_block_cfg(wqkv.cols / 32, wo.cols / 32, head_dim, g, role, wt_of_w(&wqkv),
                                        wt_of_w(wqkv_b), wt_of_w(&wo));
     if (!c || head_dim % (4 * c->QR) != 0) return false;
@@ -1023,7 +1033,7 @@ bool attn_block_supported(const DevWeight& wqkv, const DevWeight* wqkv_b, const 
 
 void launch_attn_block(const DevWeight& wqkv, const DevWeight* wqkv_b, LayerGemv qg, int qrole, const DevWeight& wo,
                        LayerGemv og, const AttnArgs& aa, const QKVArgs& qa, BlockSync bs, hipStream_t s) {
-  if (!attn_block_supported(wqkv, wqkv_b, wo, aa.head_dim, aa.n_head, aa.n_head_kv))
+  if (!attn_block_supported(wqkv, wqkv_b, wo, aa.head_dim, aa.n_head, aa.n_head_kv, qrole))
     throw std::runtime_error("attention block: unsupported shapes");
   const int g = aa.n_head / aa.n_head_kv, hd = aa.head_dim;
   const BlockCfg& c = *find_block_cfg(wqkv.cols / 32, wo.cols / 32, hd, g, qrole, wt_of_w(&wqkv), wt_of_w(wqkv_b),

@@ -1,0 +1,133 @@
+// k_exchange.hip -- the one-shot push all-gather of the row-sharded decode
+// ("a one-shot P2P push over xGMI (fully connected 8 GPUs)
+// with flag signaling"), the exchange behind collective.h's push variants.
+//
+// Every rank owns a mailbox on its own device: [2 halves][G sender slots][cap]
+// granules of 8 B = {32-bit word, 32-bit tag} (common.h's data-tagged
+// granule, here across devices).  An all-gather of `words` per rank:
+//   push   -- the rank writes each word of its slice, tagged, into slot
+//             [half][rank] of EVERY rank's mailbox (peers' through xGMI peer
+//             mappings), one 8-byte system-scope store per word and peer: the
+//             word and its flag arrive together, no fence, no flag word;
+//   gather -- the rank re-loads its own mailbox's other slots until every
+//             granule carries this exchange's tag and writes the words into
+//             the destination buffer.
+// tag = the rank's exchange count + 1 (a device counter the last gathering
+// work-group advances, so it lives inside the token's hipGraph); every rank
+// makes the same exchanges in the same order, so the counts agree.  Halves
+// alternate with the tag's parity: a rank can push exchange n + 1 while a
+// slower peer still reads exchange n (other half), but not n + 2 -- that needs
+// the slow peer's own n + 1 push, which comes after its n gather.
+// The waits are bounded by wall-clock time (a rank that stopped sets *err; the
+// session reports it at the next sync).
+#include "collective.h"
+#include "common.h"
+
+namespace llmi {
+
+namespace {
+
+constexpr int PX_T = 256;                          // threads per work-group
+constexpr int PX_B = 4;                            // granules per thread per gather batch
+constexpr uint64_t PX_TIMEOUT = 1000000000ull;     // 10 s of the 100 MHz wall clock (a peer's host may lag)
+
+__device__ __forceinline__ void px_store(uint2* g, uint32_t v, uint32_t tag) {
+  __hip_atomic_store(reinterpret_cast<uint64_t*>(g), ((uint64_t)tag << 32) | v, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint64_t px_load(const uint2* g) {
+  return __hip_atomic_load(reinterpret_cast<const uint64_t*>(g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// work-group b handles words [b per, (b + 1) per) of every rank's slice
+__global__ __launch_bounds__(PX_T) void push_exchange_kernel(PushArgs a) {
+  __shared__ uint32_t s_tag;
+  const int t = threadIdx.x;
+  if (t == 0) s_tag = __hip_atomic_load(a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  __syncthreads();
+  const uint32_t tag = s_tag;
+  const size_t half = tag & 1u;
+  const int per = (a.words + gridDim.x - 1) / gridDim.x;
+  const int w0 = blockIdx.x * per, n = max(0, min(a.words, w0 + per) - w0);
+  if (a.phase & PX_PUSH) {
+    const uint32_t* src = a.buf + (size_t)a.rank * a.stride;
+    const size_t slot = (half * a.G + a.rank) * (size_t)a.cap;
+    for (int i = t; i < n; i += PX_T) {
+      const uint32_t v = src[w0 + i];
+#pragma unroll 4
+      for (int q = 0; q < a.G; q++) px_store(a.mail[q] + slot + w0 + i, v, tag);
+    }
+  }
+  if (a.phase & PX_GATHER) {
+    // items (peer q != rank, word i) in batches of PX_B per thread: every load of a batch is issued before any
+    // tag is checked, and only the granules still missing are re-loaded
+    const int nq = a.G - 1, items = nq * n;
+    const uint2* mine = a.mail[a.rank];
+    const uint64_t t0 = wall_clock64();
+    bool late = false;
+    for (int j0 = t; j0 < items; j0 += PX_T * PX_B) {
+      int dst[PX_B];
+      const uint2* src[PX_B];
+      uint64_t g[PX_B];
+      bool ok[PX_B];
+#pragma unroll
+      for (int k = 0; k < PX_B; k++) {
+        const int j = min(j0 + k * PX_T, items - 1);  // clamped: the tail repeats the last item
+        const int qi = j / n, i = j % n, q = qi + (qi >= a.rank ? 1 : 0);
+        src[k] = mine + (half * a.G + q) * (size_t)a.cap + w0 + i;
+        dst[k] = (int)((size_t)q * a.stride) + w0 + i;
+        g[k] = px_load(src[k]);
+      }
+      for (;;) {
+        bool all = true;
+#pragma unroll
+        for (int k = 0; k < PX_B; k++) {
+          ok[k] = (uint32_t)(g[k] >> 32) == tag;
+          all = all && ok[k];
+        }
+        if (all || late) break;
+        if (wall_clock64() - t0 > PX_TIMEOUT) {
+          late = true;
+          __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+        for (int k = 0; k < PX_B; k++)
+          if (!ok[k]) g[k] = px_load(src[k]);
+      }
+#pragma unroll
+      for (int k = 0; k < PX_B; k++)
+        if (j0 + k * PX_T < items) a.buf[dst[k]] = (uint32_t)g[k];
+    }
+    // the last work-group to finish advances the exchange count (the next exchange's tag)
+    __syncthreads();
+    if (t == 0) {
+      if (gridDim.x == 1) {
+        __hip_atomic_store(a.epoch, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        const unsigned k = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (k == gridDim.x - 1) {
+          __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(a.epoch, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    }
+  }
+}
+
+}  // namespace
+
+void launch_push_exchange(const PushArgs& a, hipStream_t s) {
+  if (a.G < 1 || a.G > PX_MAX_RANKS || a.rank < 0 || a.rank >= a.G || a.words < 0 || a.words > a.cap ||
+      (size_t)a.words > a.stride)
+    throw std::runtime_error("push exchange: bad arguments");
+  if (a.words == 0) return;
+  // one work-group per 256 words up to 64 (a 1 MB prefill chunk: 4096 words each) -- a few CUs' worth of
+  // spinning waves, whatever the peers are running
+  const int nwg = std::max(1, std::min(64, (a.words + PX_T - 1) / PX_T));
+  hipLaunchKernelGGL(push_exchange_kernel, dim3(nwg), dim3(PX_T), 0, s, a);
+  LLMI_HIP(hipGetLastError());
+}
+
+}  // namespace llmi

@@ -143,12 +143,13 @@ const LayerCfg kLayerCfgs[] = {
     LLMI_LCFG(80, ROLE_PLAIN, 4, 4, 5, 1, false, true, 0),     // 4B qkv l0   4096 rows -> 256 WGs
     LLMI_LCFG(120, ROLE_PLAIN, 8, 4, 8, 2, true, true, 0),     // 12B qkv l0  8192 rows -> 256 WGs
     LLMI_LCFG(128, ROLE_PLAIN, 1, 8, 2, 1, false, true, 0),    // 12B/27B o   3840/5376 rows -> 480/672 WGs
-    LLMI_LCFG(168, ROLE_PLAIN, 8, 4, 7, 2, true, true, 1),     // 27B qkv l0  8192 rows -> 256 WGs
+    // (27B qkv row-major: the attention block reads it so; slab-major was 10.0 vs 10.4 us standalone)
+    LLMI_LCFG(168, ROLE_PLAIN, 8, 4, 7, 2, true, true, 0),     // 27B qkv l0  8192 rows -> 256 WGs
     // PRO: residual + norm prologue
     LLMI_LCFG(36, ROLE_PRO, 8, 2, 5, 9, false, true, 0),       // 1B qkv      96 WGs
     LLMI_LCFG(80, ROLE_PRO, 4, 4, 5, 10, false, true, 0),      // 4B qkv      256 WGs
     LLMI_LCFG(120, ROLE_PRO, 8, 4, 8, 15, true, true, 0),      // 12B qkv     256 WGs
-    LLMI_LCFG(168, ROLE_PRO, 4, 8, 6, 11, true, true, 1),      // 27B qkv     256 WGs
+    LLMI_LCFG(168, ROLE_PRO, 4, 8, 6, 11, true, true, 0),      // 27B qkv     256 WGs
     // GELU: prologue + GELU epilogue, 2H = R NW interleaved gate/up rows per WG
     LLMI_LCFGP(36, ROLE_GELU, 8, 8, 5, 3, 0, 3),              // 1B  13824 rows, H 32 -> 216 WGs (PE3: 5.9 -> 5.1 us)
     LLMI_LCFGP(80, ROLE_GELU, 8, 10, 10, 4, 1, 7),            // 4B  20480 rows, H 40 -> 256 WGs (PE7: 8.4 -> 7.8 us)

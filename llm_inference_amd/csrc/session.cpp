@@ -534,7 +534,8 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
     throw status_error(LLMI_E_ARG, "attn_split must be 0 or " + std::to_string(ATTN_NSPLIT));
   // LLMI_TP_SOLO (diagnostics): rank tp_rank of tp_size alone, no exchange
   const bool tp_solo = getenv("LLMI_TP_SOLO") != nullptr && opts.tp_size > 1 && !opts.tp_id && !opts.tp_group;
-  tp_ = opts.tp_id != nullptr || opts.tp_group != nullptr || tp_solo;
+  const bool tp_peer = (opts.flags & LLMI_TP_PEER) != 0 && !opts.tp_id && !opts.tp_group && !tp_solo;
+  tp_ = opts.tp_id != nullptr || opts.tp_group != nullptr || tp_solo || tp_peer;
   if (tp_) {
     tp_rank_ = opts.tp_rank;
     tp_size_ = opts.tp_size;
@@ -549,6 +550,7 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
     if (tp_) {
       coll_ = tp_solo         ? make_null(tp_rank_, tp_size_)
               : opts.tp_group ? make_local(reinterpret_cast<LocalGroup*>(opts.tp_group), tp_rank_)
+              : tp_peer       ? make_peer(tp_rank_, tp_size_)
                               : make_rccl(tp_rank_, tp_size_, opts.tp_id);
       if (!coll_->graph_safe()) use_graph_ = false;
     }
@@ -593,10 +595,16 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
     // the three launches (A/B)
     bool blk = fuse_layers_ && (!tp_ || tp_rep_attn_) && dup_.empty() && getenv("LLMI_NO_BLOCK") == nullptr &&
                (grp == 1 || grp == 2 || grp == 4);
-    for (const auto& l : L_)
-      blk = blk && l.fused && l.hd % 32 == 0 &&
-            attn_block_supported(l.qkv[0].w, l.qkv.size() > 1 ? &l.qkv[1].w : nullptr, l.o.w, l.hd, nh_, nkv_);
+    bool pro = true;
+    for (const auto& l : L_) {
+      const DevWeight* wb = l.qkv.size() > 1 ? &l.qkv[1].w : nullptr;
+      blk = blk && l.fused && l.hd % 32 == 0 && attn_block_supported(l.qkv[0].w, wb, l.o.w, l.hd, nh_, nkv_, LAYER_PLAIN);
+      pro = pro && attn_block_supported(l.qkv[0].w, wb, l.o.w, l.hd, nh_, nkv_, LAYER_PRO);
+    }
     block_ = blk;
+    // 27B: the 5376-wide residual/norm prologue does not fit the block's registers at a co-resident grid, so
+    // launch_residual_norm runs first and the block's qkv role reads the Q8_0 blocks it wrote
+    block_pro_ = blk && pro;
     // greedy token ids by screening (k_logits.hip): the fast F16 logits path
     // (a tensor-parallel rank screens its vocabulary shard; the keys meet in
     // finalize as before); LLMI_FULL_LOGITS=1 keeps the full GEMV in the loop
@@ -1235,7 +1243,7 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
           kernels_per_token_++;
         }
         g.xg = act_.q8.xb;
-      } else {
+      } else if (block_pro_) {
         qrole = LAYER_PRO;
         g.y = d_out_;
         g.w_post = L_[l - 1].post_ffw_norm;
@@ -1244,6 +1252,15 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
         g.w_next = Ld.attn_norm;
         g.eps = hp_.eps;
         std::swap(cur, other);
+      } else {  // model.cpp:722-756: residual + post-FFN norm, attention norm, Q8_0 blocks; the block reads them
+        NormOut on;
+        on.xn = xn_;
+        on.q8 = act_.q8.xb;
+        launch_residual_norm(d_out_, L_[l - 1].post_ffw_norm, cur, Ld.attn_norm, on, E, hp_.eps, false, s);
+        kernels_per_token_++;
+        tap("attn_resid", l, cur, (size_t)E * 4, s);
+        tap("attn_norm", l, xn_, (size_t)E * 4, s);
+        g.xg = act_.q8.xb;
       }
       g.out = qkv_;
       QKVArgs qa{qkv_, Ld.k_off, Ld.v_off, nh_, nkv_, hd, Ld.q_norm, Ld.k_norm,
@@ -1663,7 +1680,20 @@ void Session::sync(int32_t* out, int n) {
 
 // a bounded in-kernel wait that gave up (k_attn.hip attention block): the
 // results since the last check are invalid -- report it, never return them
+void Session::peer_handle(void* out) const {
+  if (!coll_) throw status_error(LLMI_E_ARG, "peer handle: not a tensor-parallel session");
+  coll_->peer_handle(out);
+}
+
+void Session::peer_connect(const void* handles) {
+  if (!coll_) throw status_error(LLMI_E_ARG, "peer connect: not a tensor-parallel session");
+  if (!handles) throw status_error(LLMI_E_ARG, "peer connect: no handles");
+  coll_->peer_connect(handles);
+}
+
 void Session::check_device_error() {
+  if (coll_ && coll_->failed())  // a push exchange waited past its bound for a peer's slice
+    throw status_error(LLMI_E_HIP, "tensor-parallel push exchange: a peer's slice did not arrive (device results invalid)");
   if (blk_trace_) {  // development: append the last traced launch (work-group x 8 clocks) to LLMI_BLOCK_TRACE_OUT
     std::vector<unsigned long long> h(4096 * 8);
     LLMI_HIP(hipMemcpy(h.data(), blk_trace_, h.size() * 8, hipMemcpyDeviceToHost));
@@ -1701,6 +1731,7 @@ void Session::info(llmi_session_info* o) const {
   o->prefill_f16_redo = pf_f16_redo_;
   o->layer_engine = engine_ ? 1 : 0;
   o->ffn_engine = ffn_engine_ ? 1 : 0;
+  o->tp_exchange = coll_ ? coll_->kind() : 0;
   size_t b = logits_w_.bytes;  // this rank's bytes
   for (const auto& l : L_) {
     for (const auto& p : l.qkv) b += p.w.bytes;
@@ -1816,8 +1847,10 @@ void Session::time_kernel(int which, int reps, double* us, double* bytes) {
                          bs.g_xo = blk_gxo_ + i * blk_gxo_stride_;
                          bs.err = blk_err_;
                          aa.q8k = Ld.o.w.kq ? 1 : 0;
-                         launch_attn_block(Ld.qkv[0].w, Ld.qkv.size() > 1 ? &Ld.qkv[1].w : nullptr, q, LAYER_PRO,
-                                           Ld.o.w, go, aa, qa, bs, stream_);
+                         LayerGemv qq = q;  // PLAIN block (27B): the x blocks of the last norm launch
+                         if (!block_pro_) qq.xg = act_.q8.xb;
+                         launch_attn_block(Ld.qkv[0].w, Ld.qkv.size() > 1 ? &Ld.qkv[1].w : nullptr, qq,
+                                           block_pro_ ? LAYER_PRO : LAYER_PLAIN, Ld.o.w, go, aa, qa, bs, stream_);
                        },
                        (double)Ld.qkv[0].w.bytes + (double)Ld.o.w.bytes + kv});
     }

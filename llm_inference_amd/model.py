@@ -12,7 +12,8 @@ from typing import Optional, Sequence
 
 import numpy as np
 
-from ._lib import LLMI_EXACT, LLMI_NO_GRAPH, TP_ID_BYTES, TRACE_FN, SessionInfo, SessionOpts, check, lib, ptr
+from ._lib import (LLMI_EXACT, LLMI_NO_GRAPH, LLMI_TP_PEER, PEER_HANDLE_BYTES, TP_ID_BYTES, TRACE_FN, SessionInfo,
+                   SessionOpts, check, lib, ptr)
 from .gguf import GGUFFile
 
 
@@ -46,9 +47,11 @@ class TPGroup:
 class Model:
     def __init__(self, gguf, device: int = 0, exact: bool = False, max_ctx: int = 4096,
                  use_graph: bool = True, attn_split: int = 0, tp_rank: int = 0, tp_size: int = 1,
-                 tp_id: Optional[bytes] = None, tp_group: Optional["TPGroup"] = None):
-        """tp_id (RCCL, one process per GPU) or tp_group (ranks on one device,
-        one host thread each) makes this session rank tp_rank of a row-sharded
+                 tp_id: Optional[bytes] = None, tp_group: Optional["TPGroup"] = None, tp_peer: bool = False):
+        """tp_id (RCCL, one process per GPU), tp_group (ranks on one device,
+        one host thread each) or tp_peer (one process per GPU, the one-shot
+        push exchange: peer_handle() / peer_connect() before the first
+        forward) makes this session rank tp_rank of a row-sharded
         tensor-parallel group of tp_size (include/llmi.h)."""
         buf = gguf if isinstance(gguf, np.ndarray) else np.frombuffer(gguf, np.uint8)
         buf = np.ascontiguousarray(buf)
@@ -56,7 +59,8 @@ class Model:
         if tp_id is not None and len(tp_id) != TP_ID_BYTES:
             raise ValueError(f"tp_id must be {TP_ID_BYTES} bytes")
         self._tp_group = tp_group  # keep the group alive as long as the session
-        opts = SessionOpts(device, (LLMI_EXACT if exact else 0) | (0 if use_graph else LLMI_NO_GRAPH),
+        flags = (LLMI_EXACT if exact else 0) | (0 if use_graph else LLMI_NO_GRAPH) | (LLMI_TP_PEER if tp_peer else 0)
+        opts = SessionOpts(device, flags,
                            max_ctx, attn_split, tp_rank, tp_size,
                            C.cast(self._tp_id, C.c_void_p) if self._tp_id is not None else None,
                            tp_group.h.value if tp_group is not None else None)
@@ -113,6 +117,19 @@ class Model:
         out = np.zeros(max(n, 1), np.int32)
         check(lib().llmi_session_sync(self.h, ptr(out) if n else None, n))
         return out[:n] if n else None
+
+    def peer_handle(self) -> bytes:
+        """This rank's push-exchange mailbox handle (LLMI_PEER_HANDLE_BYTES)."""
+        b = C.create_string_buffer(PEER_HANDLE_BYTES)
+        check(lib().llmi_session_peer_handle(self.h, b))
+        return b.raw
+
+    def peer_connect(self, handles: Sequence[bytes]) -> None:
+        """Every rank's peer_handle(), in rank order."""
+        if len(handles) != self.info.tp_size or any(len(h) != PEER_HANDLE_BYTES for h in handles):
+            raise ValueError(f"need {self.info.tp_size} handles of {PEER_HANDLE_BYTES} bytes")
+        b = C.create_string_buffer(b"".join(handles), PEER_HANDLE_BYTES * len(handles))
+        check(lib().llmi_session_peer_connect(self.h, b))
 
     def time_kernel(self, which: int, reps: int):
         us, by = C.c_double(), C.c_double()

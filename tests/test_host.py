@@ -59,7 +59,9 @@ def _dist_worker(rank, world, port, q):
     d.barrier()
     # the RCCL unique id travels from rank 0 to every rank (bench.py --mode tp)
     tid = d.broadcast(bytes(range(128)) if rank == 0 else None)
-    q.put((rank, (d.max(1.5 + rank), tid == bytes(range(128)))))
+    # the push exchange's mailbox handles: every rank's, in rank order
+    hs = d.all_gather(bytes([rank]) * 64)
+    q.put((rank, (d.max(1.5 + rank), tid == bytes(range(128)) and hs == [bytes([0]) * 64, bytes([1]) * 64])))
     d.dist.destroy_process_group()
 
 

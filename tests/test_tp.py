@@ -9,9 +9,13 @@ rank's smaller GQA group selects another instantiation) and the replicated
 residual/norm prologues are unchanged by sharding.
 
 RCCL refuses two ranks on one GPU, so the multi-rank cases run the ranks as
-host threads on one device with device-to-device slice copies (TPGroup); the
-RCCL path itself is exercised with a one-rank communicator, captured in the
-decode hipGraph like the multi-GPU run.
+host threads on one device (TPGroup) exchanging through the one-shot push
+all-gather of csrc/k_exchange.hip (mailboxes of data-tagged granules, the push
+and the gather launches split around a host barrier; LLMI_TP_EXCHANGE=copy
+keeps device-to-device slice copies as the A/B); the same kernel between
+processes (LLMI_TP_PEER, IPC-mapped mailboxes) is tests/test_tp_peer.py; the
+RCCL path is exercised with a one-rank communicator, captured in the decode
+hipGraph like the multi-GPU run.
 """
 import threading
 
@@ -84,6 +88,7 @@ def test_sharded_matches_whole_model(cfg_name, tp, mode, monkeypatch):
         np.testing.assert_array_equal(lg, ref)
         assert toks.tolist() == ref_toks.tolist()
         assert info.tp_rank == r and info.tp_size == tp
+        assert info.tp_exchange == 3  # the push exchange (the default)
         # each rank streams about 1/tp of the projection + logits bytes (+ the replicated q|k|v)
         rep = _qkv_bytes(g) if mode == "rep" else 0
         assert info.bytes_per_token < (full_bytes - rep) / tp * 1.2 + rep
@@ -137,6 +142,29 @@ def test_sharded_attention_block(cfg_name, tp, monkeypatch):
         np.testing.assert_array_equal(lg, ref)
         assert toks.tolist() == ref_toks.tolist()
         assert info.batched_prefill == 1
+
+
+@pytest.mark.parametrize("exchange", ["copy", "push"])
+def test_exchange_ab_and_chunked_messages(exchange, monkeypatch):
+    """The two single-device exchanges give the same bits: 4B layer shapes at tp 2 with a 300-token batched
+    prefill, whose GELU-block all-gather (300 tokens x 5.8 KB per rank) exceeds the push mailbox's 1 MB slot
+    and goes as two consecutive exchanges (tags 2 apart: both halves of the mailbox reused)."""
+    from llm_inference_amd.model import Model
+    from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
+    cfg = CONFIGS["mini-4b"]
+    g = build_gemma3_gguf(cfg, seed=23)
+    prompt = np.random.default_rng(29).integers(4, cfg.vocab, 300).astype(np.int32)
+    monkeypatch.setenv("LLMI_NO_BLOCK", "1")
+    whole = Model(g, exact=False, max_ctx=384)
+    ref = whole.forward(prompt, 0)
+    ref_toks = whole.generate(int(np.argmax(ref)), len(prompt), 5)
+    whole.close()
+    monkeypatch.setenv("LLMI_TP_EXCHANGE", exchange)
+    out = _run_ranks(g, 2, prompt, 5, max_ctx=384)
+    for r, (lg, toks, info) in enumerate(out):
+        assert info.tp_exchange == (3 if exchange == "push" else 2)
+        np.testing.assert_array_equal(lg, ref)
+        assert toks.tolist() == ref_toks.tolist()
 
 
 def test_rccl_single_rank_in_graph(monkeypatch):
