@@ -100,10 +100,19 @@ struct LayerCfg {
   bool w8 = false;  // Q8_0 weights (P counts half-block passes)
   int wt = 0;       // kq weights: WT_Q4_K / WT_Q6_K
   Launch2Fn fn2 = nullptr;  // kq: q|k Q4_K + v Q6_K in one launch (PRO / PLAIN qkv entries)
+  int rows_max = 0;  // > 0: a tensor-parallel shard entry, for weights of at most this many rows
 };
 
 #define LLMI_LCFG(NB, ROLE, R, NW, P, E, MULTI, EARLY, SLAB) \
   {NB, ROLE, R, NW, P, E, MULTI, SLAB, false, launch_cfg<R, NW, P, E, ROLE, MULTI, EARLY>}
+// shard entries (tensor-parallel ranks' row slices, at most RMAX rows): the whole matrix's entry with fewer waves
+// per work-group, so a slice still puts work-groups on most CUs.  Only roles whose per-row arithmetic does not
+// depend on NW (PLAIN: x blocks copied; QUANT: per-block quantization) and with the whole entry's R and P (a
+// row's lane split and pass order): a rank's rows stay bit-identical to the one-device session's
+#define LLMI_LCFGR(NB, ROLE, R, NW, P, E, MULTI, EARLY, SLAB, RMAX) \
+  {NB, ROLE, R, NW, P, E, MULTI, SLAB, false, launch_cfg<R, NW, P, E, ROLE, MULTI, EARLY>, false, 0, nullptr, RMAX}
+#define LLMI_LCFGPR(NB, ROLE, R, NW, P, E, SLAB, PE, RMAX) \
+  {NB, ROLE, R, NW, P, E, false, SLAB, false, launch_cfg<R, NW, P, E, ROLE, false, false, PE>, false, 0, nullptr, RMAX}
 // late roles with the first PE passes issued right after the prologue's loads
 #define LLMI_LCFGP(NB, ROLE, R, NW, P, E, SLAB, PE) \
   {NB, ROLE, R, NW, P, E, false, SLAB, false, launch_cfg<R, NW, P, E, ROLE, false, false, PE>}
@@ -139,9 +148,11 @@ const LayerCfg kLayerCfgs[] = {
     // PLAIN: x blocks copied to LDS
     LLMI_LCFG(32, ROLE_PLAIN, 2, 2, 1, 1, false, true, 0),     // 1B o        1152 rows -> 288 WGs
     LLMI_LCFG(36, ROLE_PLAIN, 8, 1, 5, 2, false, true, 0),     // 1B qkv l0   1536 rows -> 192 WGs
+    LLMI_LCFGR(64, ROLE_PLAIN, 1, 2, 1, 2, false, true, 0, 1280),  // 4B o shard  320-1280 rows -> 160-640 WGs
     LLMI_LCFG(64, ROLE_PLAIN, 1, 10, 1, 1, false, true, 0),    // 4B o        2560 rows -> 256 WGs
     LLMI_LCFG(80, ROLE_PLAIN, 4, 4, 5, 1, false, true, 0),     // 4B qkv l0   4096 rows -> 256 WGs
     LLMI_LCFG(120, ROLE_PLAIN, 8, 4, 8, 2, true, true, 0),     // 12B qkv l0  8192 rows -> 256 WGs
+    LLMI_LCFGR(128, ROLE_PLAIN, 1, 2, 2, 3, false, true, 0, 2688),  // 12B/27B o shard (tp 2-8) -> 240-1344 WGs
     LLMI_LCFG(128, ROLE_PLAIN, 1, 8, 2, 1, false, true, 0),    // 12B/27B o   3840/5376 rows -> 480/672 WGs
     // (27B qkv row-major: the attention block reads it so; slab-major was 10.0 vs 10.4 us standalone)
     LLMI_LCFG(168, ROLE_PLAIN, 8, 4, 7, 2, true, true, 0),     // 27B qkv l0  8192 rows -> 256 WGs
@@ -159,9 +170,12 @@ const LayerCfg kLayerCfgs[] = {
     // launch copies 24-42 KB of blocks instead of quantizing the whole f32 hid in every work-group
     // (scripts/gemv_sweep 27b.down: plain R1 NW8 P6 15.0 us vs quant 19.5 us)
     LLMI_LCFG(216, ROLE_PLAIN, 1, 4, 4, 3, false, true, 0),    // 1B down     1152 rows -> 288 WGs
+    LLMI_LCFGR(672, ROLE_PLAIN, 1, 4, 6, 8, true, true, 0, 2688),  // 27B down shard (tp 2-8) -> 168-672 WGs
     LLMI_LCFG(672, ROLE_PLAIN, 1, 8, 6, 4, true, true, 0),     // 27B down    5376 rows -> 672 WGs
     // QUANT: f32 activation quantized into LDS (down projection)
     LLMI_LCFG(216, ROLE_QUANT, 1, 4, 4, 4, false, true, 0),    // 1B down     1152 rows -> 288 WGs (6.5 -> 5.0 us)
+    // (a 4B QUANT shard entry, NW 2: 0.948 vs 0.907 ms per tp-8 rank -- 160 work-groups each quantizing the
+    // whole 40 KB hid; not kept)
     LLMI_LCFGP(320, ROLE_QUANT, 1, 10, 5, 2, 0, 3),           // 4B down     2560 rows -> 256 WGs (PE3: 5.8 -> 5.4 us)
     LLMI_LCFG(480, ROLE_QUANT, 1, 8, 8, 4, false, true, 0),    // 12B down    3840 rows -> 480 WGs
     LLMI_LCFG(672, ROLE_QUANT, 1, 8, 6, 6, true, false, 0),    // 27B down    5376 rows -> 672 WGs
@@ -184,10 +198,14 @@ const LayerCfg kLayerCfgs[] = {
 
 int wt_of(uint32_t type) { return type == T_Q4_K ? WT_Q4_K : type == T_Q6_K ? WT_Q6_K : 0; }
 
-const LayerCfg* find_cfg(int nb, int role, uint32_t type = T_Q4_0) {
+// rows: the weight's row count (0: unknown -- only whole-matrix entries); shard entries come first in the table
+const LayerCfg* find_cfg(int nb, int role, uint32_t type = T_Q4_0, int rows = 0) {
   if (type != T_Q4_0 && type != T_Q8_0 && type != T_Q4_K && type != T_Q6_K) return nullptr;
-  for (const auto& c : kLayerCfgs)
+  static const bool no_shard = getenv("LLMI_NO_SHARD_CFG") != nullptr;  // A/B: whole-matrix entries only
+  for (const auto& c : kLayerCfgs) {
+    if (c.rows_max > 0 && (no_shard || rows <= 0 || rows > c.rows_max)) continue;
     if (c.nb == nb && c.role == role && c.w8 == (type == T_Q8_0) && c.wt == wt_of(type)) return &c;
+  }
   return nullptr;
 }
 
@@ -205,7 +223,7 @@ KernelTiming& kernel_timing() {
 bool layer_gemv_supported(const DevWeight& w, int role) {
   const bool k = w.type == T_Q4_K || w.type == T_Q6_K;
   if ((w.type != T_Q4_0 && w.type != T_Q8_0 && !k) || w.cols % (k ? 256 : 32) != 0 || w.rows <= 0) return false;
-  const LayerCfg* c = find_cfg(w.cols / 32, role, w.type);
+  const LayerCfg* c = find_cfg(w.cols / 32, role, w.type, w.rows);
   if (!c) return false;
   if (role == LAYER_GELU && w.rows % (c->R * c->NW) != 0) return false;
   return true;
@@ -229,7 +247,7 @@ void launch_layer_gemv(const DevWeight& w, LayerGemv a, int role, hipStream_t s)
   if (role == LAYER_PLAIN && !a.xg) throw std::runtime_error("layer gemv: missing activation blocks");
   if (role == LAYER_QUANT && !a.y) throw std::runtime_error("layer gemv: missing activation");
   if (role == LAYER_GELU ? !a.hid : !a.out) throw std::runtime_error("layer gemv: missing output");
-  const LayerCfg& c = *find_cfg(w.cols / 32, role, w.type);
+  const LayerCfg& c = *find_cfg(w.cols / 32, role, w.type, w.rows);
   const int nb = w.cols / 32, nu = c.w8 ? 2 * nb : nb;  // 16-B units per row
   const bool rb = c.R == 1 || c.R == 2 || c.R == 4 || c.R == 8 || c.R == 16;
   if (!c.multi && (rb ? (nu + 64 / c.R - 1) / (64 / c.R) > c.P : c.R * nb > 64 * c.P))

@@ -719,7 +719,8 @@ void Session::gemv_parts(const std::vector<GemvPart>& parts, const float* x, int
 bool Session::down_plain(const LayerDev& Ld) const {
   static const bool off = getenv("LLMI_DOWN_QUANT") != nullptr;
   const DevWeight& g = Ld.gate_up[0].w;
-  return !off && !tp_ && (Ld.down.w.type == T_Q4_0 || Ld.down.w.type == T_Q8_0) &&
+  // a tensor-parallel rank: its GELU blocks are all-gathered instead of its f32 hid (whole blocks per rank)
+  return !off && (!tp_ || f_sh_ % 32 == 0) && (Ld.down.w.type == T_Q4_0 || Ld.down.w.type == T_Q8_0) &&
          layer_gemv_gelu_group(g.cols, g.type) == 32 && layer_gemv_supported(Ld.down.w, LAYER_PLAIN);
 }
 
@@ -1392,7 +1393,7 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
     gg.eps = hp_.eps;
     gg.hid = hid_ + (size_t)tp_rank_ * f_sh_;
     const bool dplain = down_plain(Ld);
-    if (dplain) gg.hq = hq_;
+    if (dplain) gg.hq = hq_ + (size_t)tp_rank_ * (f_sh_ / 32);
     gg.epoch = epoch;  // advances the attention block's granule tag of this layer
     if (dump_ || trace_fn_) gg.xn_out = xn_;
     for (int r = 0; r < dup("gate_up"); r++) launch_layer_gemv(Ld.gate_up[0].w, gg, LAYER_GELU, s);
@@ -1403,7 +1404,8 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
     dump("ffn_norm-" + L, xn_, E, s);
     dump("ffn_geglu-" + L, hid_, hp_.n_ff, s);
     std::swap(cur, other);
-    if (tp_) coll_->all_gather(hid_, (size_t)f_sh_ * sizeof(float), s);
+    if (tp_ && dplain) coll_->all_gather(hq_, (size_t)(f_sh_ / 32) * sizeof(XBlock), s);
+    else if (tp_) coll_->all_gather(hid_, (size_t)f_sh_ * sizeof(float), s);
     LayerGemv gd;
     gd.y = hid_;  // QUANT: GELU output quantized per block in the down launch
     gd.xg = hq_;  // PLAIN: the blocks the GELU launch wrote
