@@ -31,12 +31,13 @@ namespace llmi {
 
 namespace {
 
-template <int R, int NW, int P, int E, int ROLE, bool MULTI, bool EARLY, int PE = 0, bool W8 = false, int WT = 0>
+template <int R, int NW, int P, int E, int ROLE, bool MULTI, bool EARLY, int PE = 0, bool W8 = false, int WT = 0,
+          int RW = 0>
 __global__ __launch_bounds__(NW * 64 + (role_help(ROLE) ? E * 64 : 0)) void gemv_q4_0_layer(LayerGemv a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
   // the attention block's granule tag of this layer, for its next launch
   if (a.epoch && blockIdx.x == 0 && threadIdx.x == 0) *a.epoch += 1u;
-  layer_body<R, NW, P, E, ROLE, MULTI, EARLY, 0, PE, W8, WT>(a, blockIdx.x, s_dyn, BlockSync{});
+  layer_body<R, NW, P, E, ROLE, MULTI, EARLY, 0, PE, W8, WT, RW>(a, blockIdx.x, s_dyn, BlockSync{});
 }
 
 // K-quant q|k|v of two weight types in one launch (Q4_K_M: q, k Q4_K, v Q6_K):
@@ -65,17 +66,18 @@ __global__ __launch_bounds__(NW * 64) void gemv_kq2_layer(LayerGemv a, LayerGemv
 using LaunchFn = void (*)(dim3, size_t, const LayerGemv&, hipStream_t);
 using Launch2Fn = void (*)(dim3, size_t, const LayerGemv&, const LayerGemv&, int, hipStream_t);
 
-template <int R, int NW, int P, int E, int ROLE, bool MULTI, bool EARLY, int PE = 0, bool W8 = false, int WT = 0>
+template <int R, int NW, int P, int E, int ROLE, bool MULTI, bool EARLY, int PE = 0, bool W8 = false, int WT = 0,
+          int RW = 0>
 void launch_cfg(dim3 grid, size_t lds, const LayerGemv& a, hipStream_t s) {
   const dim3 block(NW * 64 + (role_help(ROLE) ? E * 64 : 0));
   KernelTiming& kt = kernel_timing();
   if (kt.start) {
-    hipExtLaunchKernelGGL((gemv_q4_0_layer<R, NW, P, E, ROLE, MULTI, EARLY, PE, W8, WT>), grid, block, (uint32_t)lds,
+    hipExtLaunchKernelGGL((gemv_q4_0_layer<R, NW, P, E, ROLE, MULTI, EARLY, PE, W8, WT, RW>), grid, block, (uint32_t)lds,
                           s, kt.start, kt.stop, 0u, a);
     kt = KernelTiming{};
     return;
   }
-  hipLaunchKernelGGL((gemv_q4_0_layer<R, NW, P, E, ROLE, MULTI, EARLY, PE, W8, WT>), grid, block, lds, s, a);
+  hipLaunchKernelGGL((gemv_q4_0_layer<R, NW, P, E, ROLE, MULTI, EARLY, PE, W8, WT, RW>), grid, block, lds, s, a);
 }
 
 template <int R, int NW, int P, int E, int ROLE, bool EARLY, int PE, int WTA, int WTB>
@@ -101,6 +103,7 @@ struct LayerCfg {
   int wt = 0;       // kq weights: WT_Q4_K / WT_Q6_K
   Launch2Fn fn2 = nullptr;  // kq: q|k Q4_K + v Q6_K in one launch (PRO / PLAIN qkv entries)
   int rows_max = 0;  // > 0: a tensor-parallel shard entry, for weights of at most this many rows
+  int rw = 0;        // > 0: waves carrying rows (layer_body RW), the others only share the prologue
 };
 
 #define LLMI_LCFG(NB, ROLE, R, NW, P, E, MULTI, EARLY, SLAB) \
@@ -111,6 +114,10 @@ struct LayerCfg {
 // row's lane split and pass order): a rank's rows stay bit-identical to the one-device session's
 #define LLMI_LCFGR(NB, ROLE, R, NW, P, E, MULTI, EARLY, SLAB, RMAX) \
   {NB, ROLE, R, NW, P, E, MULTI, SLAB, false, launch_cfg<R, NW, P, E, ROLE, MULTI, EARLY>, false, 0, nullptr, RMAX}
+// PRO / GELU shards: all NW waves run the prologue (its reductions unchanged), RW of them carry rows
+#define LLMI_LCFGW(NB, ROLE, R, NW, P, E, MULTI, EARLY, RW, RMAX)                                                  \
+  {NB, ROLE, R, NW, P, E, MULTI, 0, false, launch_cfg<R, NW, P, E, ROLE, MULTI, EARLY, 0, false, 0, RW>, false, 0, \
+   nullptr, RMAX, RW}
 #define LLMI_LCFGPR(NB, ROLE, R, NW, P, E, SLAB, PE, RMAX) \
   {NB, ROLE, R, NW, P, E, false, SLAB, false, launch_cfg<R, NW, P, E, ROLE, false, false, PE>, false, 0, nullptr, RMAX}
 // late roles with the first PE passes issued right after the prologue's loads
@@ -160,6 +167,8 @@ const LayerCfg kLayerCfgs[] = {
     LLMI_LCFG(36, ROLE_PRO, 8, 2, 5, 9, false, true, 0),       // 1B qkv      96 WGs
     LLMI_LCFG(80, ROLE_PRO, 4, 4, 5, 10, false, true, 0),      // 4B qkv      256 WGs
     LLMI_LCFG(120, ROLE_PRO, 8, 4, 8, 15, true, true, 0),      // 12B qkv     256 WGs
+    LLMI_LCFGW(168, ROLE_PRO, 4, 8, 6, 11, true, true, 1, 1024),  // 27B qkv shard (tp 8): 1 row wave -> 256 WGs
+    LLMI_LCFGW(168, ROLE_PRO, 4, 8, 6, 11, true, true, 2, 2048),  // 27B qkv shard (tp 4): 2 row waves -> 256 WGs
     LLMI_LCFG(168, ROLE_PRO, 4, 8, 6, 11, true, true, 0),      // 27B qkv     256 WGs
     // GELU: prologue + GELU epilogue, 2H = R NW interleaved gate/up rows per WG
     LLMI_LCFGP(36, ROLE_GELU, 8, 8, 5, 3, 0, 3),              // 1B  13824 rows, H 32 -> 216 WGs (PE3: 5.9 -> 5.1 us)
@@ -225,7 +234,7 @@ bool layer_gemv_supported(const DevWeight& w, int role) {
   if ((w.type != T_Q4_0 && w.type != T_Q8_0 && !k) || w.cols % (k ? 256 : 32) != 0 || w.rows <= 0) return false;
   const LayerCfg* c = find_cfg(w.cols / 32, role, w.type, w.rows);
   if (!c) return false;
-  if (role == LAYER_GELU && w.rows % (c->R * c->NW) != 0) return false;
+  if (role == LAYER_GELU && w.rows % (c->R * (c->rw ? c->rw : c->NW)) != 0) return false;
   return true;
 }
 
@@ -236,7 +245,7 @@ int layer_gemv_slab(const DevWeight& w, int role) {
 
 int layer_gemv_gelu_group(int cols, uint32_t type) {
   const LayerCfg* c = cols % 32 == 0 ? find_cfg(cols / 32, LAYER_GELU, type) : nullptr;
-  return c ? c->R * c->NW / 2 : 0;
+  return c ? c->R * (c->rw ? c->rw : c->NW) / 2 : 0;
 }
 
 void launch_layer_gemv(const DevWeight& w, LayerGemv a, int role, hipStream_t s) {
@@ -259,6 +268,7 @@ void launch_layer_gemv(const DevWeight& w, LayerGemv a, int role, hipStream_t s)
   if (role == LAYER_QUANT && 4 * nb > c.E * c.NW * 64) throw std::runtime_error("layer gemv: quant E too small");
   if (w.slab != c.slab) throw std::runtime_error("layer gemv: weight layout does not match the launch table");
   if (c.wt && !w.kq) throw std::runtime_error("layer gemv: K-quant weight not in the kq layout");
+  if (c.rw && (w.slab || c.help || c.w8 || c.wt)) throw std::runtime_error("layer gemv: RW entries are row-major Q4_0");
   a.qs = reinterpret_cast<const uint4*>(w.qs);
   a.wd = w.d;
   a.kdd = w.kdd;
@@ -270,7 +280,7 @@ void launch_layer_gemv(const DevWeight& w, LayerGemv a, int role, hipStream_t s)
   a.n = w.cols;
   // x blocks + pad slot of the x copy (+ the f32 x staging of the prologue)
   const size_t lds = (size_t)nb * sizeof(XBlock) + 16 + (pro ? (size_t)w.cols * 4 : 0);
-  const int rows_per_wg = c.NW * c.R;
+  const int rows_per_wg = (c.rw ? c.rw : c.NW) * c.R;
   c.fn(dim3((w.rows + rows_per_wg - 1) / rows_per_wg), lds, a, s);
   LLMI_HIP(hipGetLastError());
 }

@@ -314,8 +314,13 @@ constexpr int HELP_K4 = 6;  // float4 per helper lane and operand: n <= E * 256 
 // W8: Q8_0 weights (qs [rows][nb][32 B], row-major) instead of Q4_0.
 // WT: K-quant weights in the kq layout (WT_Q4_K / WT_Q6_K; row-major, single
 // chunk, R <= 8): the activation blocks hold Q8_K quants (q8k_block_quad).
+// RW (0: NW): only waves [0, RW) carry rows; all NW waves run the prologue, so
+// its reductions -- and every row's arithmetic -- are those of the RW = NW
+// launch while a work-group owns fewer rows (tensor-parallel shard entries:
+// more work-groups for a rank's slice, rows bit-identical to one device's;
+// row-major weights only).
 template <int R, int NW, int P, int E, int ROLE, bool MULTI, bool EARLY, int SYNC = 0, int PE = 0, bool W8 = false,
-          int WT = 0>
+          int WT = 0, int RW0 = 0>
 __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, unsigned char* s_dyn,
                                            const BlockSync& bs) {
   constexpr bool HELP = role_help(ROLE);
@@ -336,7 +341,10 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
   constexpr int T = NW * 64;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int nb = a.nb;
-  const int row0 = (bid * NW + w) * R;
+  constexpr int RW = RW0 > 0 ? RW0 : NW;
+  static_assert(RW <= NW && (RW == NW || R == 1 || R == 2 || R == 4 || R == 8 || R == 16), "RW: row-bound lanes");
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const int row0 = (bid * RW + w) * R;
   static_assert(SYNC != SYNC_SIG || ROLE == ROLE_PLAIN || ROLE == ROLE_PRO, "SIG: qkv roles (-> g_qkv)");
   static_assert(SYNC != SYNC_WAIT || ROLE == ROLE_PLAIN, "WAIT: the o projection (<- g_xo)");
   // this launch's granule tag, loaded up front (its latency hides under the prologue)
@@ -347,7 +355,7 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
     if constexpr (SYNC == SYNC_SIG) st_granule(bs.g_qkv + (p - a.out), __float_as_uint(v), btag);
     else *p = v;
   };
-  const int nrows = max(0, min(R, a.rows - row0));
+  const int nrows = wu < RW ? max(0, min(R, a.rows - row0)) : 0;
   const int total = nrows * nb;
   const uint4* qw = a.qs + (size_t)min(row0, a.rows - 1) * nb;
   const uint16_t* dw = a.wd + (size_t)min(row0, a.rows - 1) * nb;
@@ -358,8 +366,8 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
   // wave reads inside the same slab and the chip sweeps memory in order.
   const int rk = lane / L, rj = lane % L;
   const bool row_ok = rk < nrows;
-  const int wrow0 = (bid * NW + __builtin_amdgcn_readfirstlane(w)) * R;
-  const int wrows = max(0, a.rows - wrow0);
+  const int wrow0 = (bid * RW + wu) * R;
+  const int wrows = wu < RW ? max(0, a.rows - wrow0) : 0;  // no rows: every weight load out of bounds (no traffic)
   __amdgpu_buffer_rsrc_t rq, rd;
   int voq, vod, sq, sd;
   KqOff kq{};
@@ -735,7 +743,7 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
         }
       }
       __syncthreads();
-      constexpr int H = NW * R / 2;  // hidden units of this work-group
+      constexpr int H = RW * R / 2;  // hidden units of this work-group
       gelu_out<H>(a, bid, s_rows, t);
     } else if (!helper) {
       if constexpr (R <= 2) {
@@ -776,7 +784,7 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
       if (lane == 0) s_rows[w * R + k] = s;
     }
     __syncthreads();
-    constexpr int H = NW * R / 2;  // hidden units of this work-group
+    constexpr int H = RW * R / 2;  // hidden units of this work-group
     gelu_out<H>(a, bid, s_rows, t);
   } else {
 #pragma unroll
