@@ -424,7 +424,10 @@ def main():
                                  if info.screened_logits else "full F16 logits GEMV + argmax"),
         "timing_detail": {"synthetic_build_s": round(t_build, 1), "prefill_s": round(t_prefill, 4),
                           "prefill_tokens_per_s": round(a.prefill / t_prefill, 1),
-                          "prefill_mode": "batched int8-MFMA" if info.batched_prefill else "token loop"},
+                          "prefill_mode": "batched int8-MFMA" if info.batched_prefill else "token loop",
+                          # attention-block hand-off waits (per wave) over 20 us since the session was created
+                          # (prefill tail, warmup, timed steps, kernel timing): the spin-wait outlier check
+                          "block_slow_waits": m.get_info().block_slow_waits},
     }
     gpu_ids = None
     if d.rank == 0 and d.world == 1 and not a.no_cpu_baseline:

@@ -211,6 +211,7 @@ typedef struct {
                                  per CU, the layer's weights issued at launch start: DESIGN.md section 4.3) */
   int ffn_engine;             /* 1: gate_up + GELU + down of each layer are ONE launch (the FFN engine) */
   int tp_exchange;            /* tensor-parallel exchange: 0 none, 1 RCCL, 2 device copies, 3 one-shot push */
+  long long block_slow_waits; /* attention-block hand-off waits (per wave) that took over 20 us, since creation */
 } llmi_session_info;
 int llmi_session_get_info(const llmi_session* s, llmi_session_info* info);
 

@@ -689,6 +689,7 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, const QKVArgs
       if (t == 0) {
         int n = 0;
         s_ok = 1;
+        const uint64_t t0 = wall_clock64();
         while (__hip_atomic_load(a.ticket + hkv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)NS) {
           if (++n >= BLOCK_SPIN_LIMIT) {
             __hip_atomic_store(bs.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -696,6 +697,8 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, const QKVArgs
             break;
           }
         }
+        if (wall_clock64() - t0 > BLOCK_SLOW_TICKS)
+          __hip_atomic_fetch_add(bs.err + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       __syncthreads();
       // timed out: no merge from incomplete partials and no ticket reset (the

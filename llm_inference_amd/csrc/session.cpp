@@ -1706,8 +1706,13 @@ void Session::check_device_error() {
       }
   }
   if (!blk_err_) return;
-  int e = 0;
-  LLMI_HIP(hipMemcpy(&e, blk_err_, sizeof(e), hipMemcpyDeviceToHost));
+  int ev[2] = {0, 0};
+  LLMI_HIP(hipMemcpy(ev, blk_err_, sizeof(ev), hipMemcpyDeviceToHost));
+  const int e = ev[0];
+  if (ev[1]) {
+    slow_waits_ += ev[1];
+    LLMI_HIP(hipMemset(blk_err_ + 1, 0, sizeof(int)));
+  }
   if (e) {  // reported once: the flag and every attention ticket are cleared so the session's next call starts clean
     LLMI_HIP(hipMemset(blk_err_, 0, sizeof(int)));
     LLMI_HIP(hipMemset(ticket_, 0, sizeof(unsigned) * (size_t)hp_.n_head));
@@ -1734,6 +1739,7 @@ void Session::info(llmi_session_info* o) const {
   o->layer_engine = engine_ ? 1 : 0;
   o->ffn_engine = ffn_engine_ ? 1 : 0;
   o->tp_exchange = coll_ ? coll_->kind() : 0;
+  o->block_slow_waits = slow_waits_;
   size_t b = logits_w_.bytes;  // this rank's bytes
   for (const auto& l : L_) {
     for (const auto& p : l.qkv) b += p.w.bytes;

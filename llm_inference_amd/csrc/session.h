@@ -128,7 +128,8 @@ class Session {
   bool exact_ = false, use_graph_ = true;
   bool fuse_layers_ = false;  // fast path: norms / GELU folded into the Q4_0 GEMVs
   bool block_ = false;        // fast path: qkv + attention + o as one launch per layer (k_attn.hip)
-  bool block_pro_ = false;    // ... with the residual + norms in its prologue (else their own launch first: 27B)
+  bool block_pro_ = false;
+  long long slow_waits_ = 0;  // block hand-off waits over 20 us (blk_err_[1], accumulated at every sync)    // ... with the residual + norms in its prologue (else their own launch first: 27B)
   // the layer engine (k_engine.hip): a whole decode layer per launch, one 1024-thread work-group per CU;
   // its own row-major copies of the four projections (gate/up interleaved in groups of eng_.ru)
   bool engine_ = false;
