@@ -158,8 +158,10 @@ __device__ __forceinline__ uint64_t ld_sc1(const uint64_t* p) {
 // producer's epoch + 1, the epoch advancing once per launch), and the
 // buffers start zeroed (epoch 0 -> tag 1).
 constexpr int BLOCK_SPIN_LIMIT = 1 << 21;  // ~0.1-0.3 s of polls: a wait that never ends is a bug
-// a wait that took longer than this (wall clock, 100 MHz) adds 1 to err[1] once per wave: how often a hand-off
-// stalls, reported by the session (llmi_session_info.block_slow_waits); costs nothing on the first-try path
+// a wait that took longer than this (wall clock, 100 MHz ticks) adds 1 to err[1]: how often a hand-off stalls,
+// reported by the session (llmi_session_info.block_slow_waits).  Product builds count the merge's ticket wait
+// (one thread per merging work-group); the granule loads count only in LLMI_SLOW_WAITS diagnostic builds
+// (once per wave) -- any count there reshuffled the attention block's registers and cost it 0.5 %
 constexpr uint64_t BLOCK_SLOW_TICKS = 2000;  // 20 us
 __device__ __forceinline__ void count_slow_wait(bool slow, int* err) {
   const unsigned long long m = __ballot(slow);
@@ -176,7 +178,9 @@ template <int N>
 __device__ __forceinline__ void ld_granules(uint32_t (&v)[N], const uint2* g, int off, uint32_t tag, int* err) {
   const __amdgpu_buffer_rsrc_t r = buf_rsrc(g, 1u << 30);
   int n = 0;
+#ifdef LLMI_SLOW_WAITS
   uint64_t t0 = 0;
+#endif
   for (;;) {
     bool ok;
     if constexpr (N == 4) {
@@ -193,7 +197,9 @@ __device__ __forceinline__ void ld_granules(uint32_t (&v)[N], const uint2* g, in
       ok = (uint32_t)(a >> 32) == tag;
     }
     if (ok) break;
+#ifdef LLMI_SLOW_WAITS
     if (n == 0) t0 = wall_clock64();
+#endif
     if (++n >= BLOCK_SPIN_LIMIT) {
       __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       break;
@@ -201,7 +207,9 @@ __device__ __forceinline__ void ld_granules(uint32_t (&v)[N], const uint2* g, in
     __builtin_amdgcn_s_sleep(1);
     asm volatile("" ::: "memory");  // re-load every time
   }
+#ifdef LLMI_SLOW_WAITS  // diagnostic builds only: any count here reshuffles the attention block's registers (-0.5 %)
   count_slow_wait(n > 0 && wall_clock64() - t0 > BLOCK_SLOW_TICKS, err);
+#endif
 }
 
 // development trace of the block kernels (builds with -DLLMI_BLOCK_TRACE

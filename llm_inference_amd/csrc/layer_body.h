@@ -343,7 +343,6 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
   const int nb = a.nb;
   constexpr int RW = RW0 > 0 ? RW0 : NW;
   static_assert(RW <= NW && (RW == NW || R == 1 || R == 2 || R == 4 || R == 8 || R == 16), "RW: row-bound lanes");
-  const int wu = __builtin_amdgcn_readfirstlane(w);
   const int row0 = (bid * RW + w) * R;
   static_assert(SYNC != SYNC_SIG || ROLE == ROLE_PLAIN || ROLE == ROLE_PRO, "SIG: qkv roles (-> g_qkv)");
   static_assert(SYNC != SYNC_WAIT || ROLE == ROLE_PLAIN, "WAIT: the o projection (<- g_xo)");
@@ -355,7 +354,9 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
     if constexpr (SYNC == SYNC_SIG) st_granule(bs.g_qkv + (p - a.out), __float_as_uint(v), btag);
     else *p = v;
   };
-  const int nrows = wu < RW ? max(0, min(R, a.rows - row0)) : 0;
+  // (RW0 == 0: the expressions of the all-waves launch exactly -- a select the compiler cannot fold away
+  // reshuffled the attention block's registers and cost it 1 %)
+  const int nrows = RW0 == 0 ? max(0, min(R, a.rows - row0)) : w < RW ? max(0, min(R, a.rows - row0)) : 0;
   const int total = nrows * nb;
   const uint4* qw = a.qs + (size_t)min(row0, a.rows - 1) * nb;
   const uint16_t* dw = a.wd + (size_t)min(row0, a.rows - 1) * nb;
@@ -366,8 +367,10 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
   // wave reads inside the same slab and the chip sweeps memory in order.
   const int rk = lane / L, rj = lane % L;
   const bool row_ok = rk < nrows;
+  const int wu = __builtin_amdgcn_readfirstlane(w);
   const int wrow0 = (bid * RW + wu) * R;
-  const int wrows = wu < RW ? max(0, a.rows - wrow0) : 0;  // no rows: every weight load out of bounds (no traffic)
+  // no rows: every weight load out of bounds (no traffic)
+  const int wrows = RW0 == 0 ? max(0, a.rows - wrow0) : wu < RW ? max(0, a.rows - wrow0) : 0;
   __amdgpu_buffer_rsrc_t rq, rd;
   int voq, vod, sq, sd;
   KqOff kq{};
