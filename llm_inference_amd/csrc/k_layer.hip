@@ -175,6 +175,7 @@ const LayerCfg kLayerCfgs[] = {
     LLMI_LCFGP(80, ROLE_GELU, 8, 10, 10, 4, 1, 7),            // 4B  20480 rows, H 40 -> 256 WGs (PE7: 8.4 -> 7.8 us)
     LLMI_LCFG(120, ROLE_GELU, 8, 8, 8, 8, true, false, 0),     // 12B 30720 rows, H 32 -> 480 WGs
     LLMI_LCFG(168, ROLE_GELU, 8, 8, 4, 11, true, false, 1),    // 27B 43008 rows, H 32 -> 672 WGs
+    LLMI_LCFG(168, ROLE_GELU_X, 8, 8, 4, 1, true, false, 1),   // 27B gate_up on the norm launch's x blocks
     // PLAIN down: the GELU launch (32 units per work-group) wrote the Q8_0 blocks (LayerGemv::hq), so the down
     // launch copies 24-42 KB of blocks instead of quantizing the whole f32 hid in every work-group
     // (scripts/gemv_sweep 27b.down: plain R1 NW8 P6 15.0 us vs quant 19.5 us)
@@ -234,7 +235,7 @@ bool layer_gemv_supported(const DevWeight& w, int role) {
   if ((w.type != T_Q4_0 && w.type != T_Q8_0 && !k) || w.cols % (k ? 256 : 32) != 0 || w.rows <= 0) return false;
   const LayerCfg* c = find_cfg(w.cols / 32, role, w.type, w.rows);
   if (!c) return false;
-  if (role == LAYER_GELU && w.rows % (c->R * (c->rw ? c->rw : c->NW)) != 0) return false;
+  if ((role == LAYER_GELU || role == LAYER_GELU_X) && w.rows % (c->R * (c->rw ? c->rw : c->NW)) != 0) return false;
   return true;
 }
 
@@ -253,9 +254,10 @@ void launch_layer_gemv(const DevWeight& w, LayerGemv a, int role, hipStream_t s)
   const bool pro = role == LAYER_PRO || role == LAYER_GELU;
   if (pro && (!a.y || !a.resid_in || !a.resid_out || !a.w_next || a.resid_in == a.resid_out))
     throw std::runtime_error("layer gemv: missing prologue operand");
-  if (role == LAYER_PLAIN && !a.xg) throw std::runtime_error("layer gemv: missing activation blocks");
+  const bool xin = role == LAYER_PLAIN || role == LAYER_GELU_X;  // x blocks copied to LDS
+  if (xin && !a.xg) throw std::runtime_error("layer gemv: missing activation blocks");
   if (role == LAYER_QUANT && !a.y) throw std::runtime_error("layer gemv: missing activation");
-  if (role == LAYER_GELU ? !a.hid : !a.out) throw std::runtime_error("layer gemv: missing output");
+  if (role == LAYER_GELU || role == LAYER_GELU_X ? !a.hid : !a.out) throw std::runtime_error("layer gemv: missing output");
   const LayerCfg& c = *find_cfg(w.cols / 32, role, w.type, w.rows);
   const int nb = w.cols / 32, nu = c.w8 ? 2 * nb : nb;  // 16-B units per row
   const bool rb = c.R == 1 || c.R == 2 || c.R == 4 || c.R == 8 || c.R == 16;
@@ -264,7 +266,7 @@ void launch_layer_gemv(const DevWeight& w, LayerGemv a, int role, hipStream_t s)
   if (pro && !c.help && w.cols > c.E * c.NW * 64) throw std::runtime_error("layer gemv: prologue E too small");
   if (pro && c.help && (w.cols % (c.E * 32) != 0 || w.cols > c.E * 256 * HELP_K4))
     throw std::runtime_error("layer gemv: helper segments must be whole Q8_0 blocks within HELP_K4");
-  if (role == LAYER_PLAIN && 3 * nb > c.E * c.NW * 64) throw std::runtime_error("layer gemv: x copy E too small");
+  if (xin && 3 * nb > c.E * c.NW * 64) throw std::runtime_error("layer gemv: x copy E too small");
   if (role == LAYER_QUANT && 4 * nb > c.E * c.NW * 64) throw std::runtime_error("layer gemv: quant E too small");
   if (w.slab != c.slab) throw std::runtime_error("layer gemv: weight layout does not match the launch table");
   if (c.wt && !w.kq) throw std::runtime_error("layer gemv: K-quant weight not in the kq layout");

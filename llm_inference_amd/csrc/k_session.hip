@@ -335,7 +335,8 @@ __device__ void q8k_group(const float* xs, bool active, uint8_t* blk, float* s_a
 }
 
 // s_h: n floats of LDS (free again: callers are past their last use of it).
-// Q8_0 blocks: x staged in LDS, one thread per block (q8_block_serial).
+// Q8_0 blocks: x staged in LDS, one DPP quad per block (q8_block_quad, bit-identical to the one-thread
+// q8_block_serial this used: 27B's 168 blocks as serial 32-element chains made the launch 5.8 us)
 __device__ __forceinline__ void norm_outputs(const float (&xv)[NORM_EPT], int n, const NormOut& out, float* s_h) {
   const int t = threadIdx.x;
   __syncthreads();  // s_h reuse
@@ -350,10 +351,12 @@ __device__ __forceinline__ void norm_outputs(const float (&xv)[NORM_EPT], int n,
   }
   if (out.q8) {
     __syncthreads();
-    for (int b = t; b < n / 32; b += 1024) {
-      XBlock blk;
-      q8_block_serial(s_h + 32 * b, &blk);
-      out.q8[b] = blk;
+    const int sub = t & 3;
+    for (int b = t >> 2; b < n / 32; b += 256) {  // whole quads in or out together
+      const float4 f0 = reinterpret_cast<const float4*>(s_h + 32 * b + 8 * sub)[0];
+      const float4 f1 = reinterpret_cast<const float4*>(s_h + 32 * b + 8 * sub)[1];
+      const float v[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+      q8_block_quad(v, sub, out.q8 + b);
     }
   }
   if (out.q8k) {  // one wave per Q8_K super-block (n % 256 == 0: host-checked), no block barriers

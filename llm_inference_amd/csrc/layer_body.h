@@ -286,7 +286,7 @@ enum { SYNC_SIG = 1, SYNC_WAIT = 2 };
 enum { ROLE_PLAIN = LAYER_PLAIN, ROLE_PRO = LAYER_PRO, ROLE_GELU = LAYER_GELU, ROLE_QUANT = LAYER_QUANT,
        // PRO / GELU with E extra HELPER waves that do the prologue while the
        // NW streaming waves' weight loads are already in flight
-       ROLE_PRO_H = 4, ROLE_GELU_H = 5 };
+       ROLE_PRO_H = 4, ROLE_GELU_H = 5, ROLE_GELU_X = LAYER_GELU_X };
 constexpr bool role_help(int r) { return r == ROLE_PRO_H || r == ROLE_GELU_H; }
 constexpr int HELP_K4 = 6;  // float4 per helper lane and operand: n <= E * 256 * HELP_K4
 
@@ -325,7 +325,7 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
                                            const BlockSync& bs) {
   constexpr bool HELP = role_help(ROLE);
   constexpr bool PRO = ROLE == ROLE_PRO || ROLE == ROLE_GELU || HELP;
-  constexpr bool GELU = ROLE == ROLE_GELU || ROLE == ROLE_GELU_H;
+  constexpr bool GELU = ROLE == ROLE_GELU || ROLE == ROLE_GELU_H || ROLE == ROLE_GELU_X;
   constexpr bool RB = R == 1 || R == 2 || R == 4 || R == 8 || R == 16;  // row-bound lanes, else flat items
   static_assert(!HELP || RB, "helper roles use the row-bound stream");
   constexpr int L = RB ? 64 / R : 64;

@@ -1385,6 +1385,21 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
       continue;
     }
     LayerGemv gg;
+    // LLMI_GELU_X=1 (27B, the block without its in-launch prologue; opt-in, measured even): the post-attention
+    // residual + FFN norm as their own launch too, and gate_up on its x blocks -- gate_up 29.4 -> 24.6 us (672
+    // work-groups no longer re-read 86 KB of prologue operands each), but the one-work-group norm launch takes
+    // 5.7 us: 214.8 vs 214.9 tok/s
+    static const bool gelu_x_env = getenv("LLMI_GELU_X") != nullptr;
+    const bool gelu_x = gelu_x_env && block_ && !block_pro_ && !dump_ &&
+                        layer_gemv_supported(Ld.gate_up[0].w, LAYER_GELU_X);
+    if (gelu_x) {
+      NormOut on;
+      on.xn = xn_;
+      on.q8 = act_.q8.xb;
+      launch_residual_norm(o_out_, Ld.post_attn_norm, cur, Ld.ffn_norm, on, E, hp_.eps, false, s);
+      kernels_per_token_++;
+      gg.xg = act_.q8.xb;
+    }
     gg.y = o_out_;
     gg.w_post = Ld.post_attn_norm;
     gg.resid_in = cur;
@@ -1396,14 +1411,14 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
     if (dplain) gg.hq = hq_ + (size_t)tp_rank_ * (f_sh_ / 32);
     gg.epoch = epoch;  // advances the attention block's granule tag of this layer
     if (dump_ || trace_fn_) gg.xn_out = xn_;
-    for (int r = 0; r < dup("gate_up"); r++) launch_layer_gemv(Ld.gate_up[0].w, gg, LAYER_GELU, s);
-    tap("ffn_resid", l, other, (size_t)E * 4, s);
+    for (int r = 0; r < dup("gate_up"); r++) launch_layer_gemv(Ld.gate_up[0].w, gg, gelu_x ? LAYER_GELU_X : LAYER_GELU, s);
+    tap("ffn_resid", l, gelu_x ? cur : other, (size_t)E * 4, s);
     tap("ffn_norm", l, xn_, (size_t)E * 4, s);
     tap("hid", l, hid_, (size_t)hp_.n_ff * 4, s);
     dump("sa_out-" + L, other, E, s);
     dump("ffn_norm-" + L, xn_, E, s);
     dump("ffn_geglu-" + L, hid_, hp_.n_ff, s);
-    std::swap(cur, other);
+    if (!gelu_x) std::swap(cur, other);  // (the norm launch updated cur in place)
     if (tp_ && dplain) coll_->all_gather(hq_, (size_t)(f_sh_ / 32) * sizeof(XBlock), s);
     else if (tp_) coll_->all_gather(hid_, (size_t)f_sh_ * sizeof(float), s);
     LayerGemv gd;

@@ -41,7 +41,9 @@ void launch_embed_norm(uint32_t type, const uint8_t* table, size_t row_bytes, co
 // q8k (n % 256 == 0): the GELU output's Q8_K super-blocks for a Q4_K / Q6_K down projection
 void launch_gelu_quant(const float* gu, int n, float* hid, const Q8Act* q8, hipStream_t s, uint8_t* q8k = nullptr);
 // Q4_0 GEMV with the decode step's neighbours fused in (k_layer.hip)
-enum LayerRole { LAYER_PLAIN = 0, LAYER_PRO = 1, LAYER_GELU = 2, LAYER_QUANT = 3 };
+// LAYER_GELU_X: the GELU epilogue on x blocks given (a residual/norm launch wrote them: 27B, where the GELU
+// prologue's per-work-group residual/norm costs more than a launch of its own)
+enum LayerRole { LAYER_PLAIN = 0, LAYER_PRO = 1, LAYER_GELU = 2, LAYER_QUANT = 3, LAYER_GELU_X = 6 };
 struct LayerGemv {
   const uint4* qs = nullptr;  // set by launch_layer_gemv from the weight
   const uint16_t* wd = nullptr;
