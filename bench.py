@@ -58,9 +58,12 @@ def parse():
 
 def pmc_key(a) -> str:
     """The workload a PMC pass must have run to be quoted for this bench line:
-    model, weight types, prefill and decode lengths (the attention kernels'
-    bytes depend on the position they are timed at)."""
-    return f"{a.config}/{a.quant}/prefill{a.prefill}/warmup{a.warmup}/steps{a.steps}/reps{a.kernel_reps}"
+    model, weight types, the position the roofline kernels are timed at
+    (prefill + warmup + steps: the attention kernels' KV bytes depend on it)
+    and the timing reps (the pass's tail dispatches).  A short pass that ends
+    at the same position (e.g. --prefill 768 --warmup 2 --steps 14 for the
+    default 512 + 16 + 256) measures the same launches."""
+    return f"{a.config}/{a.quant}/pos{a.prefill + a.warmup + a.steps}/reps{a.kernel_reps}"
 
 
 def pmc_traffic(kernel_substr: str, key: str):

@@ -30,10 +30,10 @@ if want prof; then  # the timed decode graph itself (hipGraph replay), after a 5
   run rocprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- \
     python3 bench.py --steps 64 --warmup 4 --prefill 512 --no-cpu-baseline
 fi
-if want pmc; then
+if want pmc; then  # FETCH_SIZE of the launches the default bench line times: position 784 (512 + 16 + 256), 2 reps
   run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- \
-    python3 bench.py --steps 16 --warmup 2 --prefill 512 --no-cpu-baseline --kernel-reps 1
+    python3 bench.py --prefill 768 --warmup 2 --steps 14 --no-cpu-baseline
   python3 scripts/pmc_summary.py gpurun_out/pmc_fetch/run_counter_collection.csv gpurun_out/pmc_fetch_summary.json \
-    > gpurun_out/pmc_summary.log 2>&1
+    gemma-3-4b/q4_0/pos784/reps2 68 > gpurun_out/pmc_summary.log 2>&1
 fi
 echo "== done"
