@@ -155,11 +155,10 @@ const LayerCfg kLayerCfgs[] = {
     // PLAIN: x blocks copied to LDS
     LLMI_LCFG(32, ROLE_PLAIN, 2, 2, 1, 1, false, true, 0),     // 1B o        1152 rows -> 288 WGs
     LLMI_LCFG(36, ROLE_PLAIN, 8, 1, 5, 2, false, true, 0),     // 1B qkv l0   1536 rows -> 192 WGs
-    LLMI_LCFGR(64, ROLE_PLAIN, 1, 2, 1, 2, false, true, 0, 1280),  // 4B o shard  320-1280 rows -> 160-640 WGs
     LLMI_LCFG(64, ROLE_PLAIN, 1, 10, 1, 1, false, true, 0),    // 4B o        2560 rows -> 256 WGs
     LLMI_LCFG(80, ROLE_PLAIN, 4, 4, 5, 1, false, true, 0),     // 4B qkv l0   4096 rows -> 256 WGs
     LLMI_LCFG(120, ROLE_PLAIN, 8, 4, 8, 2, true, true, 0),     // 12B qkv l0  8192 rows -> 256 WGs
-    LLMI_LCFGR(128, ROLE_PLAIN, 1, 2, 2, 3, false, true, 0, 2688),  // 12B/27B o shard (tp 2-8) -> 240-1344 WGs
+    // (an o shard entry, NW 2: 4.60 vs 3.98 us per 27B tp-8 rank launch -- the x copy of 336 work-groups; dropped)
     LLMI_LCFG(128, ROLE_PLAIN, 1, 8, 2, 1, false, true, 0),    // 12B/27B o   3840/5376 rows -> 480/672 WGs
     // (27B qkv row-major: the attention block reads it so; slab-major was 10.0 vs 10.4 us standalone)
     LLMI_LCFG(168, ROLE_PLAIN, 8, 4, 7, 2, true, true, 0),     // 27B qkv l0  8192 rows -> 256 WGs
@@ -174,6 +173,9 @@ const LayerCfg kLayerCfgs[] = {
     LLMI_LCFGP(36, ROLE_GELU, 8, 8, 5, 3, 0, 3),              // 1B  13824 rows, H 32 -> 216 WGs (PE3: 5.9 -> 5.1 us)
     LLMI_LCFGP(80, ROLE_GELU, 8, 10, 10, 4, 1, 7),            // 4B  20480 rows, H 40 -> 256 WGs (PE7: 8.4 -> 7.8 us)
     LLMI_LCFG(120, ROLE_GELU, 8, 8, 8, 8, true, false, 0),     // 12B 30720 rows, H 32 -> 480 WGs
+    // (a 27B gate_up shard entry with longer weight chunks -- P 7 or 11 instead of 4, more bytes in flight per
+    // work-group of the tp-8 rank's 84; P does not change a row's pass order: 2.12-2.13 vs 2.08 ms per rank token,
+    // and the 2-row-wave qkv shard 2.13; not kept)
     LLMI_LCFG(168, ROLE_GELU, 8, 8, 4, 11, true, false, 1),    // 27B 43008 rows, H 32 -> 672 WGs
     LLMI_LCFG(168, ROLE_GELU_X, 8, 8, 4, 1, true, false, 1),   // 27B gate_up on the norm launch's x blocks
     // PLAIN down: the GELU launch (32 units per work-group) wrote the Q8_0 blocks (LayerGemv::hq), so the down
