@@ -335,12 +335,13 @@ __device__ __forceinline__ int pg_q6_bytes(uint32_t nib4, uint32_t hb, int k) { 
 }
 
 template <int WR, int WT, int WK, int NT, int NS, bool W8, int KQ = 0>
-__global__ __launch_bounds__(512, KQ == 2 ? 1 : (WK == 1 || NT > 1) ? 2 : 4) void prefill_gemm5_kernel(PrefillGemm a) {
+__global__ __launch_bounds__(64 * WR * WT * WK, KQ == 2 ? 1 : (WK == 1 || NT > 1) ? 2 : 4) void prefill_gemm5_kernel(PrefillGemm a) {
   using C = PG5<WR, WT, WK, NT, NS, W8, KQ>;
   constexpr int KB = C::KB;
   __shared__ __attribute__((aligned(16))) unsigned char s_ring[C::LDS];
   const int t = threadIdx.x, lane = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6), r = lane & 31, h = lane >> 5;
   const int wr = w % WR, wt = (w / WR) % WT, kg = w / (WR * WT);
+  const uint32_t nsh = 4u * h;  // the lane half's nibble (low: k 0-15, high: k 16-31): one variable shift
   const int nb = a.nb, nst = nb / KB;
   // tile of this work-group
   const int n_rt = a.rows / C::MR, n_tt = (a.T + C::TN - 1) / C::TN;
@@ -360,6 +361,11 @@ __global__ __launch_bounds__(512, KQ == 2 ? 1 : (WK == 1 || NT > 1) ? 2 : 4) voi
   // offset is added (weights: kb blocks, or for the slab layout kb / 8 slabs + kb % 8)
   const unsigned char* pb[C::PW];
   int pk[C::PW], po[C::PW];
+#ifdef LLMI_PG5_DUP  // development A/B: every wave issues PW pieces (the surplus ones duplicate others)
+  const bool full_last = true;
+#else
+  const bool full_last = w + (C::PW - 1) * C::NW < C::P;  // wave-uniform: P not a multiple of NW
+#endif
 #pragma unroll
   for (int i = 0; i < C::PW; i++) {
     const int p = (w + i * C::NW) % C::P;
@@ -405,6 +411,7 @@ __global__ __launch_bounds__(512, KQ == 2 ? 1 : (WK == 1 || NT > 1) ? 2 : 4) voi
     unsigned char* st = s_ring + (c % NS) * C::STAGE;
 #pragma unroll
     for (int i = 0; i < C::PW; i++) {
+      if (i == C::PW - 1 && !full_last) break;  // P not a multiple of NW: this wave has PW - 1 pieces
       const int k = pk[i];
       const long off = k == 0   ? wofs * C::WB
                        : k == 1 ? wofs * 2
@@ -419,7 +426,10 @@ __global__ __launch_bounds__(512, KQ == 2 ? 1 : (WK == 1 || NT > 1) ? 2 : 4) voi
     static_assert(NS >= 2 && NS <= 8, "NS");
     static_for<NS - 1>([&](auto kc) {  // the first k with ahead >= NS - 2 - k waits for PW * (NS - 2 - k)
       constexpr int k = decltype(kc)::value, n = NS - 2 - k;
-      if (ahead == n) vm_wait<C::PW * n>();
+      if (ahead == n) {
+        if (full_last) vm_wait<C::PW * n>();
+        else vm_wait<(C::PW - 1) * n>();
+      }
     });
   };
   for (int c = 0; c < NS - 1 && c < nst; c++) issue(c);
@@ -467,8 +477,8 @@ __global__ __launch_bounds__(512, KQ == 2 ? 1 : (WK == 1 || NT > 1) ? 2 : 4) voi
       const uint32_t sw = (wp >> (16 * (b & 1))) & 0xFFFFu;
       const uint32_t dd = reinterpret_cast<const uint32_t*>(st + C::O_DD)[arow];
       const float d = h2f((uint16_t)(dd & 0xFFFFu));
-      const uint32_t n0_ = h ? (q.x >> 4) & 0x0F0F0F0Fu : q.x & 0x0F0F0F0Fu, n1_ = h ? (q.y >> 4) & 0x0F0F0F0Fu : q.y & 0x0F0F0F0Fu;
-      const uint32_t n2_ = h ? (q.z >> 4) & 0x0F0F0F0Fu : q.z & 0x0F0F0F0Fu, n3_ = h ? (q.w >> 4) & 0x0F0F0F0Fu : q.w & 0x0F0F0F0Fu;
+      const uint32_t n0_ = (q.x >> nsh) & 0x0F0F0F0Fu, n1_ = (q.y >> nsh) & 0x0F0F0F0Fu;
+      const uint32_t n2_ = (q.z >> nsh) & 0x0F0F0F0Fu, n3_ = (q.w >> nsh) & 0x0F0F0F0Fu;
       if constexpr (KQ == 1) {
         o.A.x = (int)n0_;
         o.A.y = (int)n1_;
@@ -498,10 +508,10 @@ __global__ __launch_bounds__(512, KQ == 2 ? 1 : (WK == 1 || NT > 1) ? 2 : 4) voi
       o.A.w = (int)q.w;
     } else {
       const uint4 q = *reinterpret_cast<const uint4*>(st + (arow * KB + (b ^ a_sw)) * 16);
-      o.A.x = q4_signed(h ? (q.x >> 4) & 0x0F0F0F0Fu : q.x & 0x0F0F0F0Fu);
-      o.A.y = q4_signed(h ? (q.y >> 4) & 0x0F0F0F0Fu : q.y & 0x0F0F0F0Fu);
-      o.A.z = q4_signed(h ? (q.z >> 4) & 0x0F0F0F0Fu : q.z & 0x0F0F0F0Fu);
-      o.A.w = q4_signed(h ? (q.w >> 4) & 0x0F0F0F0Fu : q.w & 0x0F0F0F0Fu);
+      o.A.x = q4_signed((q.x >> nsh) & 0x0F0F0F0Fu);
+      o.A.y = q4_signed((q.y >> nsh) & 0x0F0F0F0Fu);
+      o.A.z = q4_signed((q.z >> nsh) & 0x0F0F0F0Fu);
+      o.A.w = q4_signed((q.w >> nsh) & 0x0F0F0F0Fu);
     }
     if constexpr (KQ == 0) {
       const int par = WK == 1 ? (bb & 1) : (kg & 1);  // the block's f16 in the scale pair
@@ -694,6 +704,11 @@ __global__ __launch_bounds__(512, 2) void prefill_gemm6_kernel(PrefillGemm16 a) 
   const int n0 = rt * C::MR, tk0 = tt * C::TN;
   const unsigned char* pb[C::PW];
   int pk[C::PW], po[C::PW];
+#ifdef LLMI_PG5_DUP  // development A/B: every wave issues PW pieces (the surplus ones duplicate others)
+  const bool full_last = true;
+#else
+  const bool full_last = w + (C::PW - 1) * C::NW < C::P;  // wave-uniform: P not a multiple of NW
+#endif
 #pragma unroll
   for (int i = 0; i < C::PW; i++) {
     int p = (w + i * C::NW) % C::P;
@@ -743,6 +758,7 @@ __global__ __launch_bounds__(512, 2) void prefill_gemm6_kernel(PrefillGemm16 a) 
     unsigned char* st = s_ring + (c % NS) * C::STAGE;
 #pragma unroll
     for (int i = 0; i < C::PW; i++) {
+      if (i == C::PW - 1 && !full_last) break;  // P not a multiple of NW: this wave has PW - 1 pieces
       const int k = pk[i];
       const long off = k == 0   ? wofs * 16
                        : k == 1 ? wofs * 2
@@ -1415,12 +1431,16 @@ static bool try_gemm5(const PrefillGemm& a, hipStream_t s) {
 // split) 32.2 / 25.3 / 145.8 / 103.7; a 6-stage ring, 64 tokens per wave or a 128 x 128 tile were slower):
 // 64 x 64 tiles with K split 2 (mid), or 32 x 64 with K split 4 (small) for the long-K GEMMs.  The K split
 // is chosen from K alone, so a tensor-parallel shard (fewer rows) sums every output in the same order as the
-// whole weight (tests/test_tp.py: bit-identical).
+// whole weight (tests/test_tp.py: bit-identical).  Round 3: sixteen-wave work-groups (x16: 128 x 64 tiles, and
+// 64 x 64 with K split 4 for down; y16: 64 x 128 / 128 x 32) cut the L2 -> LDS bytes by a third yet ran
+// 130 / 118 and 134 / 113 us (gate_up / down) against 128 / 99: not the bound.
 static bool launch_gemm5(const PrefillGemm& a, hipStream_t s) {
   const char* f = getenv("LLMI_PG5");
   const std::string c = f ? f : a.nb >= 160 ? "small" : "mid";
   if (c == "big" && try_gemm5<4, 2, 1, 2, 3>(a, s)) return true;
   if (c == "wide" && try_gemm5<4, 2, 1, 1, 3>(a, s)) return true;
+  if (c == "x16") return a.nb >= 160 ? try_gemm5<2, 2, 4, 1, 4>(a, s) : try_gemm5<4, 2, 2, 1, 4>(a, s);
+  if (c == "y16") return a.nb >= 160 ? try_gemm5<4, 1, 4, 1, 4>(a, s) : try_gemm5<2, 4, 2, 1, 4>(a, s);
   if (c == "small") return try_gemm5<1, 2, 4, 1, 4>(a, s);
   return try_gemm5<2, 2, 2, 1, 4>(a, s) || try_gemm5<1, 4, 2, 1, 4>(a, s);  // K split 2, 64 or 32 rows
 }
