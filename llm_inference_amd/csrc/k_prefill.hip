@@ -1130,16 +1130,23 @@ __global__ __launch_bounds__(64 * G * S) void prefill_attn_mfma_kernel(PrefillAt
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), r = lane & 31, h = lane >> 5;
   const int g = w % G, sp = w / G;
   // heaviest (last) query blocks first: dispatch order is a speed matter only
-  const int hk = blockIdx.x, tok0 = (gridDim.y - 1 - blockIdx.y) * 32, hq = hk * G + g;
+  const int hk = blockIdx.x, qb = gridDim.y - 1 - blockIdx.y, tok0 = qb * 32, hq = hk * G + g;
   const int qtok = min(tok0 + r, T - 1);
   const int qpos = a.pos0 + tok0 + r;                       // this lane's query position
   const int last_pos = a.pos0 + min(tok0 + 32, T) - 1;     // the block's last query
   const int first_pos = a.pos0 + tok0;
   const int n_tiles = last_pos / 32 + 1, n_rounds = (n_tiles + S - 1) / S;
+  // key splits across work-groups: round q (tiles S q .. S q + S - 1) is work-group q % KS's (blockIdx.z) -- a
+  // function of the key position only, so chunk-exact and the same on tensor-parallel ranks; a query block with
+  // fewer rounds than KS uses its first n_rounds work-groups
+  const int KS = a.ks, ks = blockIdx.z, nks = min(KS, n_rounds);
+  if (ks >= nks) return;  // whole work-group, before any barrier
+  const int my_rounds = (n_rounds - ks + KS - 1) / KS;
   const size_t cache0 = (size_t)hk * a.max_ctx;
-  // round q: tiles S q .. S q + S - 1 into ring half q & 1; tile S q + j at slot j of the half
-  auto tile_ptr = [&](int round, int j) { return s_kv + ((round & 1) * S + j) * 2 * TILE; };
-  auto issue = [&](int round) {
+  // local round lr (global round ks + lr KS): its tiles into ring half lr & 1; tile S q + j at slot j of the half
+  auto tile_ptr = [&](int lr, int j) { return s_kv + ((lr & 1) * S + j) * 2 * TILE; };
+  auto issue = [&](int lr) {
+    const int round = ks + lr * KS;
 #pragma unroll
     for (int i = 0; i < P / NW; i++) {
       const int p = w + i * NW, j = p / (2 * TILE / 1024), q = p % (2 * TILE / 1024);
@@ -1147,7 +1154,7 @@ __global__ __launch_bounds__(64 * G * S) void prefill_attn_mfma_kernel(PrefillAt
       const int row = pp * RPP + lane / U, slot = lane % U, u = slot ^ (row & SWM);
       const int key = min(32 * (S * round + j) + row, a.max_ctx - 1);
       const uint16_t* src = (kind ? a.v_cache : a.k_cache) + (cache0 + key) * HD + u * 8;
-      glds16(src, tile_ptr(round, j) + kind * TILE + pp * 1024);
+      glds16(src, tile_ptr(lr, j) + kind * TILE + pp * 1024);
     }
   };
   issue(0);
@@ -1162,13 +1169,13 @@ __global__ __launch_bounds__(64 * G * S) void prefill_attn_mfma_kernel(PrefillAt
   for (int i = 0; i < HD / 32; i++) o[i] = v16f{};
   float m_run = -INFINITY, l_run = 0.0f;
   const int lg = lane >> 4, li = lane & 15, tq = li >> 2, tp = li & 3;  // tr_b16 group / position
-  for (int round = 0; round < n_rounds; round++) {
+  for (int lr = 0; lr < my_rounds; lr++) {
     vm_wait<0>();
     __builtin_amdgcn_s_barrier();  // round landed in every wave; the previous round's half is free
-    if (round + 1 < n_rounds) issue(round + 1);
-    const int t = S * round + sp;  // this split's tile
-    if (t >= n_tiles) continue;    // wave-uniform; no cross-lane read is skipped by part of a wave
-    const unsigned char* kt = tile_ptr(round, sp);
+    if (lr + 1 < my_rounds) issue(lr + 1);
+    const int t = S * (ks + lr * KS) + sp;  // this split's tile
+    if (t >= n_tiles) continue;             // wave-uniform; no cross-lane read is skipped by part of a wave
+    const unsigned char* kt = tile_ptr(lr, sp);
     const unsigned char* vt = kt + TILE;
     // S^T: rows = keys (A from the K image), cols = queries
     v16f sc = {};
@@ -1254,6 +1261,50 @@ __global__ __launch_bounds__(64 * G * S) void prefill_attn_mfma_kernel(PrefillAt
       for (int i = 0; i < HD / 32; i++)
 #pragma unroll
         for (int reg = 0; reg < 16; reg++) o[i][reg] = o[i][reg] * a1 + ot[128 + (i * 16 + reg) * 64 + lane] * a2;
+    }
+  }
+  // key splits across work-groups: every work-group's (m, l, O^T) to the scratch (write-through), and the last
+  // of the query block's work-groups to count in (a per-head counter; MI355X_MICROARCH hand-off counter form)
+  // merges them all in split order -- whichever work-group that is, the same arithmetic
+  if (nks > 1) {
+    constexpr int SLAB = 64 * (HD / 2 + 2);  // floats: m[64], l[64], then O^T quads [HD / 8][64][4]
+    const size_t hb = (size_t)hq * gridDim.y + qb;
+    const __amdgpu_buffer_rsrc_t pr = buf_rsrc(a.part + hb * KS * SLAB, (uint32_t)(KS * SLAB * 4));
+    const int mine = ks * SLAB * 4;
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(m_run), pr, mine + lane * 4, 0, BUF_SC1);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(l_run), pr, mine + 256 + lane * 4, 0, BUF_SC1);
+#pragma unroll
+    for (int i = 0; i < HD / 32; i++)
+#pragma unroll
+      for (int q4 = 0; q4 < 4; q4++) {
+        const u32x4_t v = {__float_as_uint(o[i][4 * q4]), __float_as_uint(o[i][4 * q4 + 1]),
+                           __float_as_uint(o[i][4 * q4 + 2]), __float_as_uint(o[i][4 * q4 + 3])};
+        __builtin_amdgcn_raw_buffer_store_b128(v, pr, mine + 512 + ((i * 4 + q4) * 64 + lane) * 16, 0, BUF_SC1);
+      }
+    vm_wait<0>();  // drained: the partial is in memory before the count
+    int prev = 0;
+    if (lane == 0) prev = __hip_atomic_fetch_add(a.cnt + hb, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    prev = __shfl(prev, 0);
+    if (prev != nks - 1) return;  // wave-uniform
+    if (lane == 0) __hip_atomic_store(a.cnt + hb, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int k2 = 0; k2 < nks; k2++) {
+      const int off = k2 * SLAB * 4;
+      const float m2 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(pr, off + lane * 4, 0, BUF_SC1));
+      const float l2 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(pr, off + 256 + lane * 4, 0, BUF_SC1));
+      const float mm = k2 ? fmaxf(m_run, m2) : m2;
+      const float a1 = k2 == 0 || m_run == -INFINITY ? 0.0f : expf(m_run - mm);
+      const float a2 = m2 == -INFINITY ? 0.0f : expf(m2 - mm);
+      l_run = k2 ? l_run * a1 + l2 * a2 : l2;
+      m_run = mm;
+#pragma unroll
+      for (int i = 0; i < HD / 32; i++)
+#pragma unroll
+        for (int q4 = 0; q4 < 4; q4++) {
+          const uint4 v = buf_ld16_sc1(pr, off + 512 + ((i * 4 + q4) * 64 + lane) * 16);
+          const float vv[4] = {__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w)};
+#pragma unroll
+          for (int e = 0; e < 4; e++) o[i][4 * q4 + e] = k2 ? o[i][4 * q4 + e] * a1 + vv[e] * a2 : vv[e];
+        }
     }
   }
   // O = O^T / l -> Q8_0 blocks (32 head dims = one tile column; lanes q and q + 32 hold 16 each), or f16
@@ -1532,7 +1583,9 @@ static void attn_g(const PrefillAttn& a, int T, hipStream_t s) {
     throw std::runtime_error("prefill_attn: f16 / Q8_K output needs the MFMA kernel (GQA group 1, 2 or 4)");
   if (a.q8k && (HD != 256 || a.x16)) throw std::runtime_error("prefill_attn: Q8_K output needs head_dim 256");
   if (!getenv("LLMI_PREFILL_ATTN_V1") && HD >= 64) {
-    const dim3 grid(a.n_head_kv, (T + 31) / 32);
+    if (a.ks > 1 && (!a.part || !a.cnt || a.ks > PREFILL_ATTN_KS_MAX))
+      throw std::runtime_error("prefill_attn: key splits need the partial scratch");
+    const dim3 grid(a.n_head_kv, (T + 31) / 32, std::max(1, a.ks));
     // key splits per work-group (LDS: two rounds of S tiles, and the merge); S depends on head_dim only, so a
     // tensor-parallel rank (fewer heads per kv head: smaller G) merges the same splits as the whole model
     // (bit-identical).  head_dim 256 at G 1 / 4 spills some of the 128 O^T + 64 Q^T registers (correct, slower).

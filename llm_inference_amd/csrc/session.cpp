@@ -840,6 +840,11 @@ void Session::ensure_prefill_buffers(int cap) {
   pf_xq_ = dalloc<XBlock>((size_t)cap * pf_xs_);
   pf_x16_ = dalloc<uint16_t>((size_t)cap * pf_xs_ * 32);
   pf_q_ = dalloc<uint16_t>((size_t)cap * maxq);
+  int maxhd = 0;
+  for (const auto& l : L_) maxhd = std::max(maxhd, l.hd);
+  const size_t nqb = (size_t)(cap + 31) / 32;
+  pf_apart_ = dalloc<float>((size_t)nh_ * nqb * PREFILL_ATTN_KS_MAX * 64 * (maxhd / 2 + 2));
+  pf_acnt_ = dalloc<int>((size_t)nh_ * nqb);
   if (tp_)  // all-gather staging: the largest exchanged [T][row] activation (f32 rows or Q8_0 block rows)
     pf_gather_ = dalloc<uint8_t>((size_t)cap * std::max({(size_t)E * 4, (size_t)pf_xs_ * sizeof(XBlock), (size_t)pf_xs_ * 64}));
   pf_cap_ = cap;
@@ -893,6 +898,10 @@ bool Session::prefill_run(const int32_t* tokens, int n, int pos, bool allow_f16)
   // at 256-token chunks, 17.4 ms at 512)
   int chunk = 512;
   if (const char* c = getenv("LLMI_PREFILL_CHUNK")) chunk = std::max(1, atoi(c));
+  // attention key splits across work-groups: a constant (never a function of the heads per rank), so tensor-
+  // parallel ranks merge the same partials in the same order as one device
+  pf_attn_ks_ = 4;
+  if (const char* c = getenv("LLMI_PREFILL_ATTN_KS")) pf_attn_ks_ = std::min(std::max(1, atoi(c)), PREFILL_ATTN_KS_MAX);
   ensure_prefill_buffers(std::min(chunk, n));
   const int XS = pf_xs_, X16 = pf_xs_ * 32;
   const int r = tp_rank_;  // tensor parallel: this rank's column slices (0 on one device)
@@ -983,6 +992,9 @@ bool Session::prefill_run(const int32_t* tokens, int n, int pos, bool allow_f16)
       at.x16 = f16 ? pf_x16_ + (size_t)hr * nh_ * hd : nullptr;
       at.x16stride = X16;
       at.q8k = q8k;
+      at.ks = pf_attn_ks_;
+      at.part = pf_apart_;
+      at.cnt = pf_acnt_;
       launch_prefill_attn(at, T, s);
       if (!tp_rep_attn_) xgather(nh_ * hd);
       tap("pf_q", l, pf_q_, (size_t)T * nh_ * hd * 2, s);

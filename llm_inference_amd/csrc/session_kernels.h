@@ -179,7 +179,14 @@ struct PrefillAttn {
   uint16_t* x16 = nullptr;  // non-null: the heads' outputs as f16 rows [T][x16stride] (GEMM v6)
   int x16stride = 0;
   int q8k = 0;              // 1: Q8_K quants (one super-block per head: head_dim 256)
+  // key splits across work-groups (MFMA kernel): round q of a query block's key tiles goes to work-group q % ks;
+  // partials [head][query block][ks] (64 (head_dim / 2 + 2) floats each) and a counter per (head, query block)
+  // (zeroed; the merging work-group re-zeroes it)
+  int ks = 1;
+  float* part = nullptr;
+  int* cnt = nullptr;
 };
+constexpr int PREFILL_ATTN_KS_MAX = 8;
 void launch_prefill_norm(const PrefillNorm& a, int T, hipStream_t s);
 bool prefill_gemm_supported(const DevWeight& w);
 void launch_prefill_gemm(const DevWeight& w, const XBlock* x, int xstride, int T, float* out, int ostride,

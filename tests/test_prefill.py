@@ -107,6 +107,9 @@ def test_prefill_gemm_v5_matches_pinned_v1(monkeypatch):
     pin = np.load(os.path.join(sys_path, "prefill_v1_ref.npz"))
     g, prompt = gen_prefill_v1.case()
     assert np.array_equal(pin["prompt"], prompt)
+    # the pin predates the attention's key splits across work-groups (another merge order of the same softmax
+    # partials): one work-group per query block, as when the pin was made
+    monkeypatch.setenv("LLMI_PREFILL_ATTN_KS", "1")
     monkeypatch.setenv("LLMI_PG5", "big")
     big = _model(g, monkeypatch, max_ctx=256).forward(prompt, 0)  # the pin's session geometry
     np.testing.assert_array_equal(big.view(np.uint32), pin["logits"].view(np.uint32))
