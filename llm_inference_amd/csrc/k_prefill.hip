@@ -1114,6 +1114,106 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(PrefillAttn a) {
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef __fp16 fp16x4 __attribute__((__vector_size__(4 * sizeof(__fp16))));
 
+// The attention's outputs for one query (lanes r and r + 32 of a wave hold 16 of every 32 head dims): O^T / l as
+// f16 rows, Q8_K (head_dim 256: the head is one super-block, NI = 8) or Q8_0 blocks i0 .. i0 + NI - 1
+template <int HD, int NI>
+__device__ __forceinline__ void attn_emit(const PrefillAttn& a, const v16f (&o)[NI], float l_run, int i0, int tok,
+                                          int hq, int h) {
+  if (a.x16) {
+    uint16_t* xo16 = a.x16 + (size_t)tok * a.x16stride + (size_t)hq * HD + 32 * i0;
+#pragma unroll
+    for (int i = 0; i < NI; i++)
+#pragma unroll
+      for (int gq = 0; gq < 4; gq++) {  // dims 32 i + 8 gq + 4 h .. + 3
+        uint2 o2;
+        o2.x = __builtin_bit_cast(uint32_t, f16x2v{(_Float16)(o[i][4 * gq] / l_run), (_Float16)(o[i][4 * gq + 1] / l_run)});
+        o2.y = __builtin_bit_cast(uint32_t, f16x2v{(_Float16)(o[i][4 * gq + 2] / l_run), (_Float16)(o[i][4 * gq + 3] / l_run)});
+        *reinterpret_cast<uint2*>(xo16 + 32 * i + 8 * gq + 4 * h) = o2;
+      }
+    return;
+  }
+  XBlock* xo = a.xq + (size_t)tok * a.xstride + (size_t)hq * HD / 32 + i0;
+  if constexpr (HD == 256 && NI == HD / 32) {
+    if (a.q8k) {  // Q8_K (ops.cpp:142-178): the head's 256 dims are one super-block, lanes r and r + 32
+      float ax = 0.0f;
+#pragma unroll
+      for (int i = 0; i < HD / 32; i++)
+#pragma unroll
+        for (int reg = 0; reg < 16; reg++) ax = fmaxf(ax, fabsf(o[i][reg] / l_run));
+      ax = fmaxf(ax, __shfl_xor(ax, 32));
+      int key = 0x7FFFFFFF;  // the first dim attaining max |x|, with its sign
+#pragma unroll
+      for (int i = 0; i < HD / 32; i++)
+#pragma unroll
+        for (int reg = 0; reg < 16; reg++) {
+          const float v = o[i][reg] / l_run;
+          const int dim = 32 * i + 8 * (reg >> 2) + 4 * h + (reg & 3);
+          if (fabsf(v) == ax) key = min(key, (dim << 1) | (v < 0.0f ? 1 : 0));
+        }
+      key = min(key, __shfl_xor(key, 32));
+      const float iscale = ax != 0.0f ? -127.f / ((key & 1) ? -ax : ax) : 0.0f;
+#pragma unroll
+      for (int i = 0; i < HD / 32; i++) {
+        int sum = 0;
+        uint32_t wq[4];
+#pragma unroll
+        for (int gq = 0; gq < 4; gq++) {
+          wq[gq] = 0;
+#pragma unroll
+          for (int e = 0; e < 4; e++) {
+            int qv = ax != 0.0f ? nearest_int_fma(iscale, o[i][4 * gq + e] / l_run) : 0;
+            qv = qv < -128 ? -128 : (qv > 127 ? 127 : qv);
+            sum += qv;
+            wq[gq] |= (uint32_t)(qv & 0xFF) << (8 * e);
+          }
+        }
+        sum += __shfl_xor(sum, 32);
+        uint32_t* qb = reinterpret_cast<uint32_t*>(xo + i);
+#pragma unroll
+        for (int gq = 0; gq < 4; gq++) qb[2 * gq + h] = wq[gq];
+        if (h == 0) {
+          xo[i].d = ax != 0.0f ? 1.0f / iscale : 0.0f;
+          xo[i].nsum8 = sum;
+        }
+      }
+      return;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NI; i++) {
+    float v[16];
+    float amax = 0.0f;
+#pragma unroll
+    for (int reg = 0; reg < 16; reg++) {
+      v[reg] = o[i][reg] / l_run;
+      amax = fmaxf(amax, fabsf(v[reg]));
+    }
+    amax = fmaxf(amax, __shfl_xor(amax, 32));
+    const float dd = amax / 127.0f;
+    const float id = dd != 0.0f ? 1.0f / dd : 0.0f;
+    int sum = 0;
+    uint32_t wq[4];
+#pragma unroll
+    for (int gq = 0; gq < 4; gq++) {
+      wq[gq] = 0;
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        const int qv = nearest_int_fma(v[4 * gq + e], id);
+        sum += qv;
+        wq[gq] |= (uint32_t)(qv & 0xFF) << (8 * e);
+      }
+    }
+    sum += __shfl_xor(sum, 32);
+    uint32_t* qb = reinterpret_cast<uint32_t*>(xo + i);
+#pragma unroll
+    for (int gq = 0; gq < 4; gq++) qb[2 * gq + h] = wq[gq];  // bytes 8 gq + 4 h .. + 3
+    if (h == 0) {
+      xo[i].d = h2f(f2h_ggml(dd));
+      xo[i].nsum8 = -8 * sum;
+    }
+  }
+}
+
 template <int HD, int G, int S>
 __global__ __launch_bounds__(64 * G * S) void prefill_attn_mfma_kernel(PrefillAttn a, int T) {
   constexpr int U = HD / 8;                // 16-B units per cache row
@@ -1263,145 +1363,84 @@ __global__ __launch_bounds__(64 * G * S) void prefill_attn_mfma_kernel(PrefillAt
         for (int reg = 0; reg < 16; reg++) o[i][reg] = o[i][reg] * a1 + ot[128 + (i * 16 + reg) * 64 + lane] * a2;
     }
   }
-  // key splits across work-groups: every work-group's (m, l, O^T) to the scratch (write-through), and the last
-  // of the query block's work-groups to count in (a per-head counter; MI355X_MICROARCH hand-off counter form)
-  // merges them all in split order -- whichever work-group that is, the same arithmetic
-  if (nks > 1) {
-    constexpr int SLAB = 64 * (HD / 2 + 2);  // floats: m[64], l[64], then O^T quads [HD / 8][64][4]
-    const size_t hb = (size_t)hq * gridDim.y + qb;
-    const __amdgpu_buffer_rsrc_t pr = buf_rsrc(a.part + hb * KS * SLAB, (uint32_t)(KS * SLAB * 4));
-    const int mine = ks * SLAB * 4;
-    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(m_run), pr, mine + lane * 4, 0, BUF_SC1);
-    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(l_run), pr, mine + 256 + lane * 4, 0, BUF_SC1);
+  if (nks > 1) {  // this work-group's partial (m, l, O^T); prefill_attn_merge_kernel combines them
+    float* pp = a.part + (((size_t)hq * gridDim.y + qb) * KS + ks) * (64 * (HD / 2 + 2));
+    pp[lane] = m_run;
+    pp[64 + lane] = l_run;
 #pragma unroll
     for (int i = 0; i < HD / 32; i++)
 #pragma unroll
-      for (int q4 = 0; q4 < 4; q4++) {
-        const u32x4_t v = {__float_as_uint(o[i][4 * q4]), __float_as_uint(o[i][4 * q4 + 1]),
-                           __float_as_uint(o[i][4 * q4 + 2]), __float_as_uint(o[i][4 * q4 + 3])};
-        __builtin_amdgcn_raw_buffer_store_b128(v, pr, mine + 512 + ((i * 4 + q4) * 64 + lane) * 16, 0, BUF_SC1);
-      }
-    vm_wait<0>();  // drained: the partial is in memory before the count
-    int prev = 0;
-    if (lane == 0) prev = __hip_atomic_fetch_add(a.cnt + hb, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    prev = __shfl(prev, 0);
-    if (prev != nks - 1) return;  // wave-uniform
-    if (lane == 0) __hip_atomic_store(a.cnt + hb, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (int k2 = 0; k2 < nks; k2++) {
-      const int off = k2 * SLAB * 4;
-      const float m2 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(pr, off + lane * 4, 0, BUF_SC1));
-      const float l2 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(pr, off + 256 + lane * 4, 0, BUF_SC1));
-      const float mm = k2 ? fmaxf(m_run, m2) : m2;
-      const float a1 = k2 == 0 || m_run == -INFINITY ? 0.0f : expf(m_run - mm);
-      const float a2 = m2 == -INFINITY ? 0.0f : expf(m2 - mm);
-      l_run = k2 ? l_run * a1 + l2 * a2 : l2;
-      m_run = mm;
-#pragma unroll
-      for (int i = 0; i < HD / 32; i++)
-#pragma unroll
-        for (int q4 = 0; q4 < 4; q4++) {
-          const uint4 v = buf_ld16_sc1(pr, off + 512 + ((i * 4 + q4) * 64 + lane) * 16);
-          const float vv[4] = {__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w)};
-#pragma unroll
-          for (int e = 0; e < 4; e++) o[i][4 * q4 + e] = k2 ? o[i][4 * q4 + e] * a1 + vv[e] * a2 : vv[e];
-        }
-    }
+      for (int q4 = 0; q4 < 4; q4++)
+        reinterpret_cast<float4*>(pp + 128)[(i * 4 + q4) * 64 + lane] =
+            make_float4(o[i][4 * q4], o[i][4 * q4 + 1], o[i][4 * q4 + 2], o[i][4 * q4 + 3]);
+    return;
   }
   // O = O^T / l -> Q8_0 blocks (32 head dims = one tile column; lanes q and q + 32 hold 16 each), or f16
   if (tok0 + r >= T) return;  // after the last LDS read: the partner lane of a live query is also out
-  if (a.x16) {
-    uint16_t* xo16 = a.x16 + (size_t)(tok0 + r) * a.x16stride + (size_t)hq * HD;
+  attn_emit<HD, HD / 32>(a, o, l_run, 0, tok0 + r, hq, h);
+}
+
+// Key-split partials of the query blocks that have more than one (prefill_attn_mfma_kernel, a.ks > 1): one wave
+// per (head, query block, 32 head dims) -- or per (head, query block) for Q8_K output (one super-block per
+// head) -- rescales every partial against their maximum and sums them in split order, then writes the outputs
+// as the attention kernel does.  Spread over the chip: the partials of one query block are read by HD / 32
+// work-groups at once rather than by the one work-group that counted in last (round 3, first cut: 26.8 us).
+template <int HD, int NI>
+__global__ __launch_bounds__(64) void prefill_attn_merge_kernel(PrefillAttn a, int T, int S) {
+  const int lane = threadIdx.x, r = lane & 31, h = lane >> 5;
+  const int hq = blockIdx.x, nqb = gridDim.y, qb = nqb - 1 - blockIdx.y, tok0 = qb * 32, i0 = blockIdx.z * NI;
+  const int last_pos = a.pos0 + min(tok0 + 32, T) - 1;
+  const int n_rounds = (last_pos / 32 + 1 + S - 1) / S, KS = a.ks, nks = min(KS, n_rounds);
+  if (nks <= 1) return;  // written by the attention kernel
+  constexpr int SLAB = 64 * (HD / 2 + 2);
+  const float* pp = a.part + ((size_t)hq * nqb + qb) * KS * SLAB;
+  float wk[PREFILL_ATTN_KS_MAX];
+  float m = -INFINITY;
 #pragma unroll
-    for (int i = 0; i < HD / 32; i++)
-#pragma unroll
-      for (int gq = 0; gq < 4; gq++) {  // dims 32 i + 8 gq + 4 h .. + 3
-        uint2 o2;
-        o2.x = __builtin_bit_cast(uint32_t, f16x2v{(_Float16)(o[i][4 * gq] / l_run), (_Float16)(o[i][4 * gq + 1] / l_run)});
-        o2.y = __builtin_bit_cast(uint32_t, f16x2v{(_Float16)(o[i][4 * gq + 2] / l_run), (_Float16)(o[i][4 * gq + 3] / l_run)});
-        *reinterpret_cast<uint2*>(xo16 + 32 * i + 8 * gq + 4 * h) = o2;
-      }
-    return;
+  for (int k = 0; k < PREFILL_ATTN_KS_MAX; k++) {
+    wk[k] = k < nks ? pp[k * SLAB + lane] : -INFINITY;
+    m = fmaxf(m, wk[k]);
   }
-  XBlock* xo = a.xq + (size_t)(tok0 + r) * a.xstride + (size_t)hq * HD / 32;
-  if constexpr (HD == 256) {
-    if (a.q8k) {  // Q8_K (ops.cpp:142-178): the head's 256 dims are one super-block, lanes r and r + 32
-      float ax = 0.0f;
+  float l = 0.0f;
 #pragma unroll
-      for (int i = 0; i < HD / 32; i++)
+  for (int k = 0; k < PREFILL_ATTN_KS_MAX; k++)
+    if (k < nks) {  // m finite: partial 0 holds key 0
+      wk[k] = wk[k] == -INFINITY ? 0.0f : expf(wk[k] - m);
+      l = k ? l + wk[k] * pp[k * SLAB + 64 + lane] : wk[k] * pp[k * SLAB + 64 + lane];
+    }
+  v16f o[NI];
+  if constexpr (NI > 1) {  // the whole head (Q8_K): partial by partial, every quad's loads in flight
+    for (int k = 0; k < nks; k++) {
+      const float4* src = reinterpret_cast<const float4*>(pp + k * SLAB + 128);
 #pragma unroll
-        for (int reg = 0; reg < 16; reg++) ax = fmaxf(ax, fabsf(o[i][reg] / l_run));
-      ax = fmaxf(ax, __shfl_xor(ax, 32));
-      int key = 0x7FFFFFFF;  // the first dim attaining max |x|, with its sign
+      for (int i = 0; i < NI; i++)
 #pragma unroll
-      for (int i = 0; i < HD / 32; i++)
+        for (int q4 = 0; q4 < 4; q4++) {
+          const float4 v = src[((i0 + i) * 4 + q4) * 64 + lane];
+          const float vv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-        for (int reg = 0; reg < 16; reg++) {
-          const float v = o[i][reg] / l_run;
-          const int dim = 32 * i + 8 * (reg >> 2) + 4 * h + (reg & 3);
-          if (fabsf(v) == ax) key = min(key, (dim << 1) | (v < 0.0f ? 1 : 0));
+          for (int e = 0; e < 4; e++) o[i][4 * q4 + e] = k ? o[i][4 * q4 + e] + wk[k] * vv[e] : wk[k] * vv[e];
         }
-      key = min(key, __shfl_xor(key, 32));
-      const float iscale = ax != 0.0f ? -127.f / ((key & 1) ? -ax : ax) : 0.0f;
+    }
+  } else
 #pragma unroll
-      for (int i = 0; i < HD / 32; i++) {
-        int sum = 0;
-        uint32_t wq[4];
+  for (int i = 0; i < NI; i++)
 #pragma unroll
-        for (int gq = 0; gq < 4; gq++) {
-          wq[gq] = 0;
+    for (int q4 = 0; q4 < 4; q4++) {
+      float4 v[PREFILL_ATTN_KS_MAX];
 #pragma unroll
-          for (int e = 0; e < 4; e++) {
-            int qv = ax != 0.0f ? nearest_int_fma(iscale, o[i][4 * gq + e] / l_run) : 0;
-            qv = qv < -128 ? -128 : (qv > 127 ? 127 : qv);
-            sum += qv;
-            wq[gq] |= (uint32_t)(qv & 0xFF) << (8 * e);
-          }
+      for (int k = 0; k < PREFILL_ATTN_KS_MAX; k++)
+        if (k < nks) v[k] = reinterpret_cast<const float4*>(pp + k * SLAB + 128)[((i0 + i) * 4 + q4) * 64 + lane];
+#pragma unroll
+      for (int k = 0; k < PREFILL_ATTN_KS_MAX; k++)
+        if (k < nks) {
+          const float vv[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+          for (int e = 0; e < 4; e++) o[i][4 * q4 + e] = k ? o[i][4 * q4 + e] + wk[k] * vv[e] : wk[k] * vv[e];
         }
-        sum += __shfl_xor(sum, 32);
-        uint32_t* qb = reinterpret_cast<uint32_t*>(xo + i);
-#pragma unroll
-        for (int gq = 0; gq < 4; gq++) qb[2 * gq + h] = wq[gq];
-        if (h == 0) {
-          xo[i].d = ax != 0.0f ? 1.0f / iscale : 0.0f;
-          xo[i].nsum8 = sum;
-        }
-      }
-      return;
     }
-  }
-#pragma unroll
-  for (int i = 0; i < HD / 32; i++) {
-    float v[16];
-    float amax = 0.0f;
-#pragma unroll
-    for (int reg = 0; reg < 16; reg++) {
-      v[reg] = o[i][reg] / l_run;
-      amax = fmaxf(amax, fabsf(v[reg]));
-    }
-    amax = fmaxf(amax, __shfl_xor(amax, 32));
-    const float dd = amax / 127.0f;
-    const float id = dd != 0.0f ? 1.0f / dd : 0.0f;
-    int sum = 0;
-    uint32_t wq[4];
-#pragma unroll
-    for (int gq = 0; gq < 4; gq++) {
-      wq[gq] = 0;
-#pragma unroll
-      for (int e = 0; e < 4; e++) {
-        const int qv = nearest_int_fma(v[4 * gq + e], id);
-        sum += qv;
-        wq[gq] |= (uint32_t)(qv & 0xFF) << (8 * e);
-      }
-    }
-    sum += __shfl_xor(sum, 32);
-    uint32_t* qb = reinterpret_cast<uint32_t*>(xo + i);
-#pragma unroll
-    for (int gq = 0; gq < 4; gq++) qb[2 * gq + h] = wq[gq];  // bytes 8 gq + 4 h .. + 3
-    if (h == 0) {
-      xo[i].d = h2f(f2h_ggml(dd));
-      xo[i].nsum8 = -8 * sum;
-    }
-  }
+  if (tok0 + r >= T) return;
+  attn_emit<HD, NI>(a, o, l, i0, tok0 + r, hq, h);
 }
 
 // ---------------------------------------------------------------------------
@@ -1583,19 +1622,36 @@ static void attn_g(const PrefillAttn& a, int T, hipStream_t s) {
     throw std::runtime_error("prefill_attn: f16 / Q8_K output needs the MFMA kernel (GQA group 1, 2 or 4)");
   if (a.q8k && (HD != 256 || a.x16)) throw std::runtime_error("prefill_attn: Q8_K output needs head_dim 256");
   if (!getenv("LLMI_PREFILL_ATTN_V1") && HD >= 64) {
-    if (a.ks > 1 && (!a.part || !a.cnt || a.ks > PREFILL_ATTN_KS_MAX))
+    if (a.ks > 1 && (!a.part || a.ks > PREFILL_ATTN_KS_MAX))
       throw std::runtime_error("prefill_attn: key splits need the partial scratch");
     const dim3 grid(a.n_head_kv, (T + 31) / 32, std::max(1, a.ks));
     // key splits per work-group (LDS: two rounds of S tiles, and the merge); S depends on head_dim only, so a
     // tensor-parallel rank (fewer heads per kv head: smaller G) merges the same splits as the whole model
     // (bit-identical).  head_dim 256 at G 1 / 4 spills some of the 128 O^T + 64 Q^T registers (correct, slower).
     constexpr int S4 = HD >= 256 ? 2 : 4;
+    int S = 0;
     switch (G) {
-      case 1: hipLaunchKernelGGL((prefill_attn_mfma_kernel<HD, 1, S4>), grid, dim3(64 * S4), 0, s, a, T); return;
-      case 2: hipLaunchKernelGGL((prefill_attn_mfma_kernel<HD, 2, S4>), grid, dim3(128 * S4), 0, s, a, T); return;
-      case 4: hipLaunchKernelGGL((prefill_attn_mfma_kernel<HD, 4, HD == 128 ? 2 : S4>), grid,
-                                 dim3(256 * (HD == 128 ? 2 : S4)), 0, s, a, T); return;
+      case 1: hipLaunchKernelGGL((prefill_attn_mfma_kernel<HD, 1, S4>), grid, dim3(64 * S4), 0, s, a, T); S = S4; break;
+      case 2: hipLaunchKernelGGL((prefill_attn_mfma_kernel<HD, 2, S4>), grid, dim3(128 * S4), 0, s, a, T); S = S4; break;
+      case 4:
+        hipLaunchKernelGGL((prefill_attn_mfma_kernel<HD, 4, HD == 128 ? 2 : S4>), grid, dim3(256 * (HD == 128 ? 2 : S4)),
+                           0, s, a, T);
+        S = HD == 128 ? 2 : S4;
+        break;
       default: break;
+    }
+    if (S) {
+      const int nqb = (T + 31) / 32;
+      if (a.ks > 1 && (a.pos0 + T - 1) / 32 + 1 > S) {  // some query block has more than one partial
+        if constexpr (HD == 256) {
+          if (a.q8k) {
+            hipLaunchKernelGGL((prefill_attn_merge_kernel<HD, HD / 32>), dim3(a.n_head, nqb, 1), dim3(64), 0, s, a, T, S);
+            return;
+          }
+        }
+        hipLaunchKernelGGL((prefill_attn_merge_kernel<HD, 1>), dim3(a.n_head, nqb, HD / 32), dim3(64), 0, s, a, T, S);
+      }
+      return;
     }
   }
   const dim3 grid(a.n_head_kv, T);

@@ -844,7 +844,6 @@ void Session::ensure_prefill_buffers(int cap) {
   for (const auto& l : L_) maxhd = std::max(maxhd, l.hd);
   const size_t nqb = (size_t)(cap + 31) / 32;
   pf_apart_ = dalloc<float>((size_t)nh_ * nqb * PREFILL_ATTN_KS_MAX * 64 * (maxhd / 2 + 2));
-  pf_acnt_ = dalloc<int>((size_t)nh_ * nqb);
   if (tp_)  // all-gather staging: the largest exchanged [T][row] activation (f32 rows or Q8_0 block rows)
     pf_gather_ = dalloc<uint8_t>((size_t)cap * std::max({(size_t)E * 4, (size_t)pf_xs_ * sizeof(XBlock), (size_t)pf_xs_ * 64}));
   pf_cap_ = cap;
@@ -994,7 +993,6 @@ bool Session::prefill_run(const int32_t* tokens, int n, int pos, bool allow_f16)
       at.q8k = q8k;
       at.ks = pf_attn_ks_;
       at.part = pf_apart_;
-      at.cnt = pf_acnt_;
       launch_prefill_attn(at, T, s);
       if (!tp_rep_attn_) xgather(nh_ * hd);
       tap("pf_q", l, pf_q_, (size_t)T * nh_ * hd * 2, s);

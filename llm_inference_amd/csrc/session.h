@@ -207,8 +207,7 @@ class Session {
   int pf_f16_redo_ = 0;        // f16 prefills whose activations overflowed f16 and were recomputed on the int8 path
   bool pf_kq_ = false;         // K-quant layers: the batched prefill runs the f16 path
   uint16_t* pf_q_ = nullptr;
-  float* pf_apart_ = nullptr;  // prefill attention: key-split partials and counters
-  int* pf_acnt_ = nullptr;
+  float* pf_apart_ = nullptr;  // prefill attention: key-split partials
   int pf_attn_ks_ = 4;
   uint8_t* pf_gather_ = nullptr;  // tensor parallel: all-gather staging of the prefill slices
 };

@@ -180,11 +180,9 @@ struct PrefillAttn {
   int x16stride = 0;
   int q8k = 0;              // 1: Q8_K quants (one super-block per head: head_dim 256)
   // key splits across work-groups (MFMA kernel): round q of a query block's key tiles goes to work-group q % ks;
-  // partials [head][query block][ks] (64 (head_dim / 2 + 2) floats each) and a counter per (head, query block)
-  // (zeroed; the merging work-group re-zeroes it)
+  // partials [head][query block][ks] (64 (head_dim / 2 + 2) floats each), combined by a merge launch
   int ks = 1;
   float* part = nullptr;
-  int* cnt = nullptr;
 };
 constexpr int PREFILL_ATTN_KS_MAX = 8;
 void launch_prefill_norm(const PrefillNorm& a, int T, hipStream_t s);
