@@ -1524,7 +1524,9 @@ static bool try_gemm5(const PrefillGemm& a, hipStream_t s) {
 // is chosen from K alone, so a tensor-parallel shard (fewer rows) sums every output in the same order as the
 // whole weight (tests/test_tp.py: bit-identical).  Round 3: sixteen-wave work-groups (x16: 128 x 64 tiles, and
 // 64 x 64 with K split 4 for down; y16: 64 x 128 / 128 x 32) cut the L2 -> LDS bytes by a third yet ran
-// 130 / 118 and 134 / 113 us (gate_up / down) against 128 / 99: not the bound.
+// 130 / 118 and 134 / 113 us (gate_up / down) against 128 / 99: not the bound.  Two token tiles per wave (NT 2,
+// 3 stages: 128 x 64 / 64 x 64 K split 4, or 64 x 128 / 32 x 128): 130 / 115 and 141 / 130 against 124 / 97 --
+// the unpack and weight-scale work they share is not worth the registers (occupancy 2).
 static bool launch_gemm5(const PrefillGemm& a, hipStream_t s) {
   const char* f = getenv("LLMI_PG5");
   const std::string c = f ? f : a.nb >= 160 ? "small" : "mid";
