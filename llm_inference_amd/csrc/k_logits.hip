@@ -36,8 +36,6 @@ namespace llmi {
 
 namespace {
 
-constexpr float SCREEN_DENORM = 6.103515625e-05f;  // 2^-14: smallest normal f16
-
 __device__ __forceinline__ float dot8_h(uint4 w, uint4 x, float acc) {  // = k_gemv.hip dot8_f16
   typedef _Float16 h2t __attribute__((ext_vector_type(2)));
   acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2t, w.x), __builtin_bit_cast(h2t, x.x), acc, false);
@@ -99,53 +97,24 @@ __global__ void quantize_table_q8_kernel(const uint16_t* __restrict__ w, size_t 
 }
 
 // ---- per token --------------------------------------------------------------
-// one work-group: thread b < nb quantizes block b of x16 and computes c_b in
-// f64; thread 0 resets M.  xs[b] = {qx[32], dx, c_b / 2, A, pad}.
-__global__ __launch_bounds__(256) void screen_prep_kernel(const uint16_t* __restrict__ x16, int n, ScreenX* __restrict__ xs,
-                                                          unsigned* __restrict__ m_key) {
+// one work-group of 1024 threads: DPP quad b < nb quantizes block b of x16 and
+// computes c_b in f64 (screen_prep_quad, session_kernels.h); wave 0 sums A and
+// resets M.  xs[b] = {qx[32], dx, c_b / 2, 0, 0}, xs[nb].a = A.  The decode
+// loop's final norm runs the same two functions on its own x (NormOut::scr),
+// so this launch serves only the other callers (time_kernel, unfolded norms).
+__global__ __launch_bounds__(1024) void screen_prep_kernel(const uint16_t* __restrict__ x16, int n, ScreenX* __restrict__ xs,
+                                                           unsigned* __restrict__ m_key) {
   __shared__ double s_l1[256];
-  const int b = threadIdx.x, nb = n / 32;
-  double l1 = 0.0;
-  if (b < nb) {
-    float v[32];
-    float amax = 0.0f;
+  const int t = threadIdx.x, b = t >> 2, sub = t & 3, nb = n / 32;
+  if (b < nb) {  // whole quads in or out together
+    float v[8];
 #pragma unroll
-    for (int i = 0; i < 32; i++) {
-      v[i] = h2f(x16[b * 32 + i]);
-      amax = fmaxf(amax, fabsf(v[i]));
-    }
-    const float dx = amax / 127.0f;
-    double e = 0.0, den = 0.0;
-    uint32_t packed[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-    for (int i = 0; i < 32; i++) {
-      const int q = dx > 0.0f ? (int)fminf(127.0f, fmaxf(-127.0f, rintf(v[i] / dx))) : 0;
-      packed[i / 4] |= (uint32_t)(q & 0xFF) << (8 * (i % 4));
-      l1 += fabs((double)v[i]);
-      e += fabs((double)v[i] - (double)dx * (double)q);
-      if (fabsf(v[i]) < SCREEN_DENORM) den += fabs((double)v[i]);
-    }
-    const double k_u = (double)(n + 32) * 0x1p-24;
-    double c = 0.5 * l1 + 127.5 * e + 127.5 * k_u * (l1 + e) + 127.5 * den;
-    c *= 1.0 + 0x1p-10;
-    ScreenX o;
-    o.lo = make_int4((int)packed[0], (int)packed[1], (int)packed[2], (int)packed[3]);
-    o.hi = make_int4((int)packed[4], (int)packed[5], (int)packed[6], (int)packed[7]);
-    o.dx = dx;
-    o.c_half = __double2float_ru(0.5 * c);
-    o.a = 0.0f;
-    o.pad = 0.0f;
-    xs[b] = o;
+    for (int i = 0; i < 8; i++) v[i] = h2f(x16[b * 32 + sub * 8 + i]);
+    const double l1 = screen_prep_quad(v, sub, n, xs + b);
+    if (sub == 0) s_l1[b] = l1;
   }
-  s_l1[b] = l1;
   __syncthreads();
-  if (b == 0) {
-    double tot = 0.0;
-    for (int i = 0; i < nb; i++) tot += s_l1[i];
-    // A: denormal flushing of the table's f16 values (2^-14 per |x|), doubled
-    xs[nb].a = __double2float_ru(2.0 * (double)SCREEN_DENORM * tot * (1.0 + 0x1p-10));
-    *m_key = 0u;
-  }
+  if (t < 64) screen_prep_total(s_l1, nb, xs, m_key);
 }
 
 // Screening GEMV: half a wave per row (lane j of a half owns 16-B chunks j,
@@ -318,11 +287,12 @@ void free_screen_table(ScreenTable& st) {
 }
 
 void launch_screen_argmax(const DevWeight& table, const ScreenTable& st, const uint16_t* x16,
-                          unsigned long long* amax_key, hipStream_t s) {
+                          unsigned long long* amax_key, hipStream_t s, bool prepped) {
   if (table.rows != st.rows || table.cols != st.cols) throw std::runtime_error("screen: table mismatch");
   if (!screen_supported(table)) throw std::runtime_error("screen: unsupported logits table");
   const int n = table.cols, nb = n / 32;
-  hipLaunchKernelGGL(screen_prep_kernel, dim3(1), dim3(256), 0, s, x16, n, st.xs, st.m_key);
+  if (nb > 256) throw std::runtime_error("screen: n_embd > 8192");
+  if (!prepped) hipLaunchKernelGGL(screen_prep_kernel, dim3(1), dim3(1024), 0, s, x16, n, st.xs, st.m_key);
   const int rows = table.rows;
   static const int wpc = getenv("LLMI_SCREEN_WPC") ? atoi(getenv("LLMI_SCREEN_WPC")) : 8;  // waves per CU (A/B)
   // row groups in flight per lane group (A/B on the 4B bench: 1 -> 2 = 132.8 -> 127.7 us; 4 or 12 waves per CU slower)

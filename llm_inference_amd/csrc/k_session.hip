@@ -404,6 +404,20 @@ __device__ __forceinline__ void norm_outputs(const float (&xv)[NORM_EPT], int n,
       if (lane == 0) *reinterpret_cast<float*>(blk) = 1.0f / iscale;
     }
   }
+  if (out.scr) {  // the screening's x16 blocks from the same f16 roundings (screen_prep_kernel's arithmetic)
+    __shared__ double s_l1[256];  // n <= 8192: at most 256 blocks, one quad each
+    __syncthreads();  // s_h holds xv
+    const int b = t >> 2, sub = t & 3;
+    if (b < n / 32) {
+      float v[8];
+#pragma unroll
+      for (int i = 0; i < 8; i++) v[i] = h2f(f2h_ggml(s_h[32 * b + 8 * sub + i]));
+      const double l1 = screen_prep_quad(v, sub, n, out.scr + b);
+      if (sub == 0) s_l1[b] = l1;
+    }
+    __syncthreads();
+    if (t < 64) screen_prep_total(s_l1, n / 32, out.scr, out.scr_mkey);
+  }
 }
 
 template <bool EXACT>
@@ -588,9 +602,13 @@ void launch_argmax(const float* x, int n, unsigned long long* key, hipStream_t s
 // row-sharded logits key q holds the best of vocabulary
 // rows [q * shard, (q + 1) * shard) by local index; the winner is re-keyed by
 // global index so ties resolve to the lowest id, as the whole-vocab argmax.
-__global__ void finalize_token_kernel(unsigned long long* keys, int n_keys, int shard, int32_t* d_token,
-                                      int32_t* d_pos, int32_t* ring, int32_t* ring_idx, int ring_cap) {
+// The buffers are distinct (__restrict__) and every load is issued before the first store: one memory
+// round trip instead of three dependent ones (the single thread's launch was ~4.2 us).
+__global__ void finalize_token_kernel(unsigned long long* __restrict__ keys, int n_keys, int shard,
+                                      int32_t* __restrict__ d_token, int32_t* __restrict__ d_pos,
+                                      int32_t* __restrict__ ring, int32_t* __restrict__ ring_idx, int ring_cap) {
   unsigned long long best = keys[0];
+  const int pos = *d_pos, i = *ring_idx;
   keys[0] = 0;
   for (int q = 1; q < n_keys; q++) {
     const unsigned long long k = keys[q];
@@ -602,8 +620,7 @@ __global__ void finalize_token_kernel(unsigned long long* keys, int n_keys, int 
   }
   const uint32_t tok = argmax_key_index(best);
   *d_token = (int32_t)tok;
-  *d_pos = *d_pos + 1;
-  const int i = *ring_idx;
+  *d_pos = pos + 1;
   if (i < ring_cap) ring[i] = (int32_t)tok;
   *ring_idx = i + 1;
 }
@@ -669,6 +686,75 @@ __device__ float deq_embed(uint32_t type, const uint8_t* row, int i) {
     }
     default: return 0.0f;  // Q6_K/Q4_K/Q5_0 tables use launch_dequantize_rows + rms_norm
   }
+}
+
+// The decode loop's token feedback and the next step's embed_norm in one launch (the step graph then starts at
+// layer 0): thread 0 runs finalize_token_kernel's selection and bookkeeping, the token reaches the work-group
+// through LDS, and the embedding row + scale + first attn_norm follow as embed_norm_kernel computes them.
+template <bool EXACT>
+__global__ __launch_bounds__(1024) void finalize_embed_norm_kernel(
+    unsigned long long* __restrict__ keys, int n_keys, int shard, int32_t* __restrict__ d_token,
+    int32_t* __restrict__ d_pos, int32_t* __restrict__ ring, int32_t* __restrict__ ring_idx, int ring_cap,
+    uint32_t type, const uint8_t* __restrict__ table, size_t row_bytes, float emb_scale, float* __restrict__ resid,
+    const float* __restrict__ w, NormOut out, int n, double eps) {
+  extern __shared__ float s_h[];
+  __shared__ float sh[16];
+  __shared__ int s_tok;
+  const int t = threadIdx.x;
+  float wv[NORM_EPT];
+#pragma unroll
+  for (int k = 0; k < NORM_EPT; k++) wv[k] = t + k * 1024 < n ? w[t + k * 1024] : 0.0f;
+  if (t == 0) {
+    unsigned long long best = keys[0];
+    const int pos = *d_pos, i = *ring_idx;
+    keys[0] = 0;
+    for (int q = 1; q < n_keys; q++) {
+      const unsigned long long k = keys[q];
+      keys[q] = 0;
+      if (k == 0) continue;
+      const uint32_t gi = (uint32_t)q * (uint32_t)shard + argmax_key_index(k);
+      const unsigned long long kg = (k & 0xFFFFFFFF00000000ull) | (0xFFFFFFFFu - gi);
+      if (kg > best) best = kg;
+    }
+    const uint32_t tok = argmax_key_index(best);
+    *d_token = (int32_t)tok;
+    *d_pos = pos + 1;
+    if (i < ring_cap) ring[i] = (int32_t)tok;
+    *ring_idx = i + 1;
+    s_tok = (int)tok;
+  }
+  __syncthreads();
+  const uint8_t* row = table + (size_t)s_tok * row_bytes;
+  float ev[NORM_EPT];
+#pragma unroll
+  for (int k = 0; k < NORM_EPT; k++) {
+    const int i = t + k * 1024;
+    const bool ok = i < n;
+    ev[k] = ok ? deq_embed(type, row, i) * emb_scale : 0.0f;
+    if (ok) resid[i] = ev[k];
+  }
+  const float sc = rms_scale(sumsq_regs<EXACT>(ev, n, s_h, sh), n, eps);
+  float xv[NORM_EPT];
+#pragma unroll
+  for (int k = 0; k < NORM_EPT; k++) xv[k] = (sc * ev[k]) * wv[k];
+  norm_outputs(xv, n, out, s_h);
+}
+
+void launch_finalize_embed_norm(unsigned long long* keys, int n_keys, int shard, int32_t* d_token, int32_t* d_pos,
+                                int32_t* ring, int32_t* ring_idx, int ring_cap, uint32_t type, const uint8_t* table,
+                                size_t row_bytes, float emb_scale, float* resid, const float* w, const NormOut& out,
+                                int n, double eps, bool exact, hipStream_t s) {
+  if (n > 1024 * NORM_EPT) throw std::runtime_error("embed_norm: n_embd > 8192");
+  if (type != T_F16 && type != T_F32 && type != T_Q8_0) throw std::runtime_error("finalize_embed_norm: table type");
+  if (exact)
+    hipLaunchKernelGGL(finalize_embed_norm_kernel<true>, dim3(1), dim3(1024), (size_t)n * 4, s, keys, n_keys, shard,
+                       d_token, d_pos, ring, ring_idx, ring_cap, type, table, row_bytes, emb_scale, resid, w, out, n,
+                       eps);
+  else
+    hipLaunchKernelGGL(finalize_embed_norm_kernel<false>, dim3(1), dim3(1024), (size_t)n * 4, s, keys, n_keys, shard,
+                       d_token, d_pos, ring, ring_idx, ring_cap, type, table, row_bytes, emb_scale, resid, w, out, n,
+                       eps);
+  LLMI_HIP(hipGetLastError());
 }
 
 void launch_embed_norm(uint32_t type, const uint8_t* table, size_t row_bytes, const int32_t* d_token,

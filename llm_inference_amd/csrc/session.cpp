@@ -724,34 +724,60 @@ bool Session::down_plain(const LayerDev& Ld) const {
          layer_gemv_gelu_group(g.cols, g.type) == 32 && layer_gemv_supported(Ld.down.w, LAYER_PLAIN);
 }
 
-void Session::record_step(hipStream_t s, bool gen) {
+// the screened token selection's step 1 (k_logits.hip screen_prep) in the final norm's launch: its x16 blocks,
+// A and the M reset from the same f16 roundings (LLMI_SCREEN_PREP=1 keeps the separate launch, A/B)
+void Session::screen_norm(NormOut& o) {
+  static const bool sep = getenv("LLMI_SCREEN_PREP") != nullptr;
+  if (sep || !rec_gen_ || !screen_ || o.x16 != act_.x16 || hp_.n_embd > 8192) return;
+  o.scr = scr_.xs;
+  o.scr_mkey = scr_.m_key;
+  scr_prepped_ = true;
+}
+
+// a norm feeding GEMV parts also writes their Q8_0 activation when every
+// part consumes Q8_0 (one fewer launch); Q8_K blocks for K-quant parts
+static NormOut norm_out_for(const std::vector<GemvPart>& consumer, float* xn, const ActBuf& act, bool ex_norm) {
+  auto is_q8 = [](uint32_t t) { return t == T_Q4_0 || t == T_Q8_0; };
+  NormOut o;
+  o.xn = xn;
+  bool q8 = !consumer.empty(), q8k = !consumer.empty();
+  for (const auto& p : consumer) {
+    q8 &= is_q8(p.w.type);
+    q8k &= (p.w.type == T_Q4_K || p.w.type == T_Q6_K) && p.w.cols % 256 == 0;
+  }
+  if (q8) o.q8 = act.q8.xb;
+  if (q8k && !ex_norm) o.q8k = act.q8k;  // exact mode keeps the reference's separate quantize launch
+  return o;
+}
+
+NormOut Session::embed_out() const { return norm_out_for(L_[0].qkv, xn_, act_, ex_norm_); }
+
+// the decode-loop graph may end with the next token's embed_norm (launch_finalize_embed_norm): one launch fewer
+// per token (LLMI_NO_EMBED_FOLD=1 keeps finalize_token + embed_norm, A/B)
+bool Session::embed_fold_ok() const {
+  static const bool off = getenv("LLMI_NO_EMBED_FOLD") != nullptr;
+  return !off && use_graph_ && screen_ && (embd_.type == T_F16 || embd_.type == T_Q8_0) && !ple_table_.qs;
+}
+
+void Session::record_step(hipStream_t s, bool gen, bool fold_embed) {
   kernels_per_token_ = 0;
+  rec_gen_ = gen;
+  scr_prepped_ = false;
+  rec_fold_ = fold_embed && gen && embed_fold_ok() && !dump_ && !trace_fn_;
   const int E = hp_.n_embd;
   const float emb_scale = std::sqrt(static_cast<float>(E));  // model.cpp:337-338
-  auto is_q8 = [](uint32_t t) { return t == T_Q4_0 || t == T_Q8_0; };
-  // a norm feeding GEMV parts also writes their Q8_0 activation when every
-  // part consumes Q8_0 (one fewer launch); x16 for the F16 logits GEMV
-  auto nout = [&](const std::vector<GemvPart>& consumer) {
-    NormOut o;
-    o.xn = xn_;
-    bool q8 = !consumer.empty(), q8k = !consumer.empty();
-    for (const auto& p : consumer) {
-      q8 &= is_q8(p.w.type);
-      q8k &= (p.w.type == T_Q4_K || p.w.type == T_Q6_K) && p.w.cols % 256 == 0;
-    }
-    if (q8) o.q8 = act_.q8.xb;
-    if (q8k && !ex_norm_) o.q8k = act_.q8k;  // exact mode keeps the reference's separate quantize launch
-    return o;
-  };
+  auto nout = [&](const std::vector<GemvPart>& consumer) { return norm_out_for(consumer, xn_, act_, ex_norm_); };
   bool x_q8 = false;  // xn_'s Q8_0 blocks are already in act_
   const void* x_blocks = nullptr;  // where they are (Q8_0: act_.q8.xb, Q8_K: act_.q8k)
   if (embd_.type == T_F16 || embd_.type == T_Q8_0) {
     const NormOut o = nout(L_[0].qkv);
-    launch_embed_norm(embd_.type, embd_raw_, embd_row_bytes_, d_token_, emb_scale, resid_, L_[0].attn_norm, o, E,
-                      hp_.eps, ex_norm_, s);
+    if (!rec_fold_) {  // folded: the previous step's token feedback launch (or enqueue) ran it
+      launch_embed_norm(embd_.type, embd_raw_, embd_row_bytes_, d_token_, emb_scale, resid_, L_[0].attn_norm, o, E,
+                        hp_.eps, ex_norm_, s);
+      kernels_per_token_++;
+    }
     x_q8 = o.q8 != nullptr || o.q8k != nullptr;
     x_blocks = o.q8k ? (const void*)o.q8k : (const void*)o.q8;
-    kernels_per_token_++;
   } else {
     launch_dequantize_rows(embd_.type, embd_raw_, embd_row_bytes_, d_token_, 1, E, emb_scale, resid_, s);
     launch_rms_norm(resid_, L_[0].attn_norm, xn_, E, 1, hp_.eps, ex_norm_, s);
@@ -787,6 +813,7 @@ void Session::record_step(hipStream_t s, bool gen) {
     record_layers(s, x_q8);
   }
   record_logits(s, gen);
+  rec_gen_ = scr_prepped_ = rec_fold_ = false;
 }
 
 void Session::record_logits(hipStream_t s, bool gen) {
@@ -799,8 +826,8 @@ void Session::record_logits(hipStream_t s, bool gen) {
   float* lg = logits_ + (size_t)tp_rank_ * v_sh_;
   unsigned long long* key = amax_key_ + tp_rank_;
   if (gen && screen_) {  // token id only: int8 screening + exact rescoring of the candidates
-    launch_screen_argmax(logits_w_, scr_, act_.x16, key, s);
-    kernels_per_token_ += 3;
+    launch_screen_argmax(logits_w_, scr_, act_.x16, key, s, scr_prepped_);
+    kernels_per_token_ += scr_prepped_ ? 2 : 3;
     tap("x16", -1, act_.x16, (size_t)E * 2, s);
   } else {
     for (int r = 0; r < dup("logits"); r++)
@@ -818,7 +845,12 @@ void Session::record_logits(hipStream_t s, bool gen) {
     kernels_per_token_++;
   }
   if (tp_) coll_->all_gather(amax_key_, sizeof(unsigned long long), s);
-  launch_finalize_token(amax_key_, tp_size_, v_sh_, d_token_, d_pos_, ring_, ring_idx_, max_ctx_, s);
+  if (rec_fold_)
+    launch_finalize_embed_norm(amax_key_, tp_size_, v_sh_, d_token_, d_pos_, ring_, ring_idx_, max_ctx_, embd_.type,
+                               embd_raw_, embd_row_bytes_, std::sqrt(static_cast<float>(E)), resid_, L_[0].attn_norm,
+                               embed_out(), E, hp_.eps, ex_norm_, s);
+  else
+    launch_finalize_token(amax_key_, tp_size_, v_sh_, d_token_, d_pos_, ring_, ring_idx_, max_ctx_, s);
   kernels_per_token_++;
   tap("token", -1, d_token_, 4, s);
 }
@@ -1229,6 +1261,7 @@ void Session::record_layers_engine(hipStream_t s, bool x_q8) {
   NormOut o2;
   o2.xn = xn_;
   if (embd_.type == T_F16) o2.x16 = act_.x16;
+  screen_norm(o2);
   launch_residual_norm(d_out_, L_.back().post_ffw_norm, cur, out_norm_, o2, E, hp_.eps, false, s);
   kernels_per_token_++;
 }
@@ -1445,6 +1478,7 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
   NormOut o2;
   o2.xn = xn_;
   if (embd_.type == T_F16) o2.x16 = act_.x16;
+  screen_norm(o2);
   launch_residual_norm(d_out_, L_.back().post_ffw_norm, cur, out_norm_, o2, E, hp_.eps, false, s);
   kernels_per_token_++;
   tap("final_resid", -1, cur, (size_t)E * 4, s);
@@ -1519,6 +1553,7 @@ void Session::record_layers(hipStream_t s, bool x_q8) {
     NormOut o2 = last ? NormOut{} : nout(L_[l + 1].qkv);
     o2.xn = xn_;
     if (last && embd_.type == T_F16) o2.x16 = act_.x16;  // logits input, ops.cpp:542-551
+    if (last) screen_norm(o2);
     if (ple_table_.qs) {  // Gemma-4 per-layer embedding step (model.cpp:926-966), then the output scale
       const int EP = hp_.n_epl;
       launch_residual_norm(d_out_, Ld.post_ffw_norm, resid_, w_next, NormOut{xn_}, E, hp_.eps, ex_norm_, s);
@@ -1543,7 +1578,7 @@ void Session::ensure_graph(bool gen) {
   if (!use_graph_ || ge) return;
   LLMI_HIP(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
   try {
-    record_step(stream_, gen);
+    record_step(stream_, gen, gen);
   } catch (...) {
     hipGraph_t gg;
     (void)hipStreamEndCapture(stream_, &gg);
@@ -1696,6 +1731,11 @@ void Session::enqueue(int32_t first, int pos, int n_steps) {
   if (first < 0 || first >= vocab_) throw status_error(LLMI_E_RANGE, "token id out of range");
   if (pos < 0 || pos + n_steps > max_ctx_) throw status_error(LLMI_E_RANGE, "generate: context overflow");
   set_token_pos(first, pos, true);
+  if (n_steps > 0 && screen_ && embed_fold_ok()) {  // the folded step graph starts at layer 0: the first embedding here
+    const int E = hp_.n_embd;
+    launch_embed_norm(embd_.type, embd_raw_, embd_row_bytes_, d_token_, std::sqrt(static_cast<float>(E)), resid_,
+                      L_[0].attn_norm, embed_out(), E, hp_.eps, ex_norm_, stream_);
+  }
   for (int i = 0; i < n_steps; i++) run_step(true);
 }
 

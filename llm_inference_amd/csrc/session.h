@@ -85,7 +85,11 @@ class Session {
   void alloc_buffers();
   void build_rope_tables();
   // gen: the decode loop's step (token id only: screened logits when screen_)
-  void record_step(hipStream_t s, bool gen = false);
+  // fold_embed: the step ends with the NEXT step's embed_norm inside the token feedback launch and starts at
+  // layer 0 (the decode-loop graph; enqueue launches the first embed_norm itself)
+  void record_step(hipStream_t s, bool gen = false, bool fold_embed = false);
+  bool embed_fold_ok() const;
+  NormOut embed_out() const;
   bool down_plain(const LayerDev& Ld) const;
   void record_logits(hipStream_t s, bool gen = false);  // xn_ / act_.x16 -> logits, argmax key, token feedback
   void prefill(const int32_t* tokens, int n, int pos);  // batched (k_prefill.hip)
@@ -182,6 +186,10 @@ class Session {
   hipGraphExec_t graph_gen_exec_ = nullptr;
   bool screen_ = false;                     // k_logits.hip: token ids by screening + exact rescoring
   ScreenTable scr_;
+  bool rec_gen_ = false;       // record_step: this step ends with the screened token selection
+  bool scr_prepped_ = false;   // the final norm wrote scr_.xs (no screen_prep launch)
+  bool rec_fold_ = false;      // record_step(fold_embed): record_logits ends with finalize + embed_norm
+  void screen_norm(NormOut& o);  // the final norm also writes the screening's x16 blocks where they will be used
   int kernels_per_token_ = 0;
   std::string dup_;
   size_t weight_bytes_ = 0;

@@ -19,11 +19,16 @@ void to_kq_layout(DevWeight& w, hipStream_t s, int slab = 0);
 
 // outputs of a norm that feeds a GEMV: xn (always), plus optionally the Q8_0
 // blocks and/or the f16-rounded copy the next GEMV consumes
+struct ScreenX;
 struct NormOut {
   float* xn = nullptr;
   XBlock* q8 = nullptr;
   uint16_t* x16 = nullptr;
   uint8_t* q8k = nullptr;  // Q8_K super-blocks (292 B, quantize_row_q8_k) for Q4_K / Q6_K consumers
+  // the screened token selection's per-token x16 blocks (k_logits.hip step 1), written by the final norm so
+  // the decode loop needs no screen_prep launch; scr_mkey: M, reset here
+  ScreenX* scr = nullptr;
+  unsigned* scr_mkey = nullptr;
 };
 // resid = (resid + rms(y) * w_post) * post_scale (y itself when w_post is null;
 // post_scale: Gemma-4 layer output scale, 1 = none); outputs rms(resid) * w_next
@@ -38,6 +43,11 @@ void launch_softcap(float* x, int n, float cap, hipStream_t s);
 void launch_embed_norm(uint32_t type, const uint8_t* table, size_t row_bytes, const int32_t* d_token,
                        float emb_scale, float* resid, const float* w, const NormOut& out, int n, double eps,
                        bool exact, hipStream_t s);
+// the decode loop's token feedback (launch_finalize_token) + the next step's embed_norm, one launch
+void launch_finalize_embed_norm(unsigned long long* keys, int n_keys, int shard, int32_t* d_token, int32_t* d_pos,
+                                int32_t* ring, int32_t* ring_idx, int ring_cap, uint32_t type, const uint8_t* table,
+                                size_t row_bytes, float emb_scale, float* resid, const float* w, const NormOut& out,
+                                int n, double eps, bool exact, hipStream_t s);
 // q8k (n % 256 == 0): the GELU output's Q8_K super-blocks for a Q4_K / Q6_K down projection
 void launch_gelu_quant(const float* gu, int n, float* hid, const Q8Act* q8, hipStream_t s, uint8_t* q8k = nullptr);
 // Q4_0 GEMV with the decode step's neighbours fused in (k_layer.hip)
@@ -228,8 +238,64 @@ struct ScreenTable {
 bool screen_supported(const DevWeight& table);
 void alloc_screen_table(const DevWeight& table, ScreenTable& st, hipStream_t s);
 void free_screen_table(ScreenTable& st);
+// prepped: st.xs / st.m_key already hold this token's x16 blocks (a norm with NormOut::scr wrote them)
 void launch_screen_argmax(const DevWeight& table, const ScreenTable& st, const uint16_t* x16,
-                          unsigned long long* amax_key, hipStream_t s);
+                          unsigned long long* amax_key, hipStream_t s, bool prepped = false);
+
+// ---- the screening's x16 blocks (k_logits.hip step 1), shared by screen_prep_kernel and norm_outputs ----
+constexpr float SCREEN_DENORM = 6.103515625e-05f;  // 2^-14: smallest normal f16
+// one DPP quad per 32-block b (sub = lane & 3 holds v = elements 8 sub .. 8 sub + 7 of the f16-rounded x):
+// qx = rint(x / dx), dx = amax / 127, c_b (k_logits.hip header) into *o, entry .a = 0; returns |x_b|_1 (f64,
+// quad total).  Quad sums are in a different order than a serial chain: c_b and A are bounds widened by 2^-10
+// and rounded up, so any order is valid (the f64 rounding is ~2^-47 relative).
+__device__ __forceinline__ double screen_prep_quad(const float (&v)[8], int sub, int n, ScreenX* __restrict__ o) {
+  float amax = 0.0f;
+#pragma unroll
+  for (int i = 0; i < 8; i++) amax = fmaxf(amax, fabsf(v[i]));
+  amax = fmaxf(amax, __shfl_xor(amax, 1));
+  amax = fmaxf(amax, __shfl_xor(amax, 2));
+  const float dx = amax / 127.0f;
+  double l1 = 0.0, e = 0.0, den = 0.0;
+  uint32_t packed[2] = {0, 0};
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const int q = dx > 0.0f ? (int)fminf(127.0f, fmaxf(-127.0f, rintf(v[i] / dx))) : 0;
+    packed[i / 4] |= (uint32_t)(q & 0xFF) << (8 * (i % 4));
+    l1 += fabs((double)v[i]);
+    e += fabs((double)v[i] - (double)dx * (double)q);
+    if (fabsf(v[i]) < SCREEN_DENORM) den += fabs((double)v[i]);
+  }
+#pragma unroll
+  for (int m = 1; m <= 2; m <<= 1) {
+    l1 += __shfl_xor(l1, m);
+    e += __shfl_xor(e, m);
+    den += __shfl_xor(den, m);
+  }
+  int* words = reinterpret_cast<int*>(o);  // lo = qx words 0..3, hi = 4..7: this lane's 8 quants are words 2 sub, 2 sub + 1
+  words[2 * sub] = (int)packed[0];
+  words[2 * sub + 1] = (int)packed[1];
+  if (sub == 0) {
+    const double k_u = (double)(n + 32) * 0x1p-24;
+    double c = 0.5 * l1 + 127.5 * e + 127.5 * k_u * (l1 + e) + 127.5 * den;
+    c *= 1.0 + 0x1p-10;
+    reinterpret_cast<float4*>(o)[2] = make_float4(dx, __double2float_ru(0.5 * c), 0.0f, 0.0f);
+  }
+  return l1;
+}
+// all nb blocks' l1 in s_l1 (visible to the caller's first wave): A into xs[nb].a, M reset -- wave 0 only
+__device__ __forceinline__ void screen_prep_total(const double* s_l1, int nb, ScreenX* __restrict__ xs,
+                                                  unsigned* __restrict__ m_key) {
+  const int lane = threadIdx.x & 63;
+  double tot = 0.0;
+  for (int b = lane; b < nb; b += 64) tot += s_l1[b];
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) tot += __shfl_xor(tot, m);
+  if (lane == 0) {
+    // A: denormal flushing of the table's f16 values (2^-14 per |x|), doubled
+    xs[nb].a = __double2float_ru(2.0 * (double)SCREEN_DENORM * tot * (1.0 + 0x1p-10));
+    *m_key = 0u;
+  }
+}
 void launch_finalize_token(unsigned long long* keys, int n_keys, int shard, int32_t* d_token, int32_t* d_pos,
                            int32_t* ring, int32_t* ring_idx, int ring_cap, hipStream_t s);
 // d_token = token, d_pos = pos (and ring_idx = 0 when reset): the token loop's inputs, in stream order
