@@ -147,36 +147,28 @@ __global__ __launch_bounds__(256) void screen_gemv_kernel(const uint4* __restric
   }
   const float A = xs[nb].a;
   float mloc = -INFINITY;
-  // scales: the row's nb f16 d as nb / 2 dwords, lane j loading dwords j, j + LPR, ... (SPL loads instead of
-  // CPL 2-byte loads); chunk c's scale (block c / 2, dword c / 4) comes from lane (c / 4) % LPR of load
-  // c / (4 LPR) by a lane shuffle, its half (c / 2) & 1 = (j / 2) & 1 is fixed per lane.  Clamped dwords stay
-  // finite scales for the chunks past the row (their x is 0).
-  constexpr int SPL = (CPL + 3) / 4;
-  const int ND = nb / 2;  // nb even: host-checked
-  const int hsh = 16 * ((j >> 1) & 1);
-  auto load = [&](uint4 (&q)[CPL], uint32_t (&s)[SPL], int r) {
+  auto load = [&](uint4 (&q)[CPL], uint16_t (&s)[CPL], int r) {
     const uint4* qr = qs + (size_t)r * NC;
-    const uint32_t* dr = reinterpret_cast<const uint32_t*>(d + (size_t)r * nb);
+    const uint16_t* dr = d + (size_t)r * nb;
 #pragma unroll
     for (int p = 0; p < CPL; p++) {
       const int c = min(p * LPR + j, NC - 1);  // clamped (masked by x = 0)
       q[p] = ld_nt(qr + c);
+      s[p] = dr[c >> 1];
     }
-#pragma unroll
-    for (int k = 0; k < SPL; k++) s[k] = dr[min(k * LPR + j, ND - 1)];
   };
   auto row_sum = [](float v) { return LPR == 32 ? half_sum(v) : row16_sum(v); };
   int row = RPW * grp + sub;
   uint4 cq[CPL];
-  uint32_t cs[SPL];
+  uint16_t cs[CPL];
   load(cq, cs, min(row, rows - 1));
   // AHEAD = 2: a second row group in flight (bytes in flight per CU: MI355X_MICROARCH HBM latency x rate)
   uint4 mq[AHEAD > 1 ? CPL : 1];
-  uint32_t ms[AHEAD > 1 ? SPL : 1];
+  uint16_t ms[AHEAD > 1 ? CPL : 1];
   if constexpr (AHEAD > 1) load(mq, ms, min(row + RPW * ngrp, rows - 1));
   for (; RPW * grp < rows; grp += ngrp, row += RPW * ngrp) {
     uint4 nq[CPL];
-    uint32_t ns[SPL];
+    uint16_t ns[CPL];
     load(nq, ns, min(row + RPW * AHEAD * ngrp, rows - 1));
     float ap = 0.0f, bp = 0.0f;
 #pragma unroll
@@ -186,9 +178,7 @@ __global__ __launch_bounds__(256) void screen_gemv_kernel(const uint4* __restric
       is = sdot4((int)cq[p].y, xq[p].y, is);
       is = sdot4((int)cq[p].z, xq[p].z, is);
       is = sdot4((int)cq[p].w, xq[p].w, is);
-      const int src = sub * LPR + (p % 4) * (LPR / 4) + (j >> 2);
-      const uint32_t sw = (uint32_t)__shfl((int)cs[p / 4], src);
-      const float dw = h2f((uint16_t)(sw >> hsh));
+      const float dw = h2f(cs[p]);
       ap += dw * (xd[p] * (float)is);
       bp += dw * xc[p];
     }
@@ -202,18 +192,12 @@ __global__ __launch_bounds__(256) void screen_gemv_kernel(const uint4* __restric
     for (int p = 0; p < CPL; p++) {
       if constexpr (AHEAD > 1) {
         cq[p] = mq[p];
+        cs[p] = ms[p];
         mq[p] = nq[p];
+        ms[p] = ns[p];
       } else {
         cq[p] = nq[p];
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < SPL; k++) {
-      if constexpr (AHEAD > 1) {
-        cs[k] = ms[k];
-        ms[k] = ns[k];
-      } else {
-        cs[k] = ns[k];
+        cs[p] = ns[p];
       }
     }
   }
@@ -307,7 +291,7 @@ void launch_screen_argmax(const DevWeight& table, const ScreenTable& st, const u
   if (table.rows != st.rows || table.cols != st.cols) throw std::runtime_error("screen: table mismatch");
   if (!screen_supported(table)) throw std::runtime_error("screen: unsupported logits table");
   const int n = table.cols, nb = n / 32;
-  if (nb > 256 || nb % 2) throw std::runtime_error("screen: n_embd > 8192 or not a multiple of 64");
+  if (nb > 256) throw std::runtime_error("screen: n_embd > 8192");
   if (!prepped) hipLaunchKernelGGL(screen_prep_kernel, dim3(1), dim3(1024), 0, s, x16, n, st.xs, st.m_key);
   const int rows = table.rows;
   static const int wpc = getenv("LLMI_SCREEN_WPC") ? atoi(getenv("LLMI_SCREEN_WPC")) : 8;  // waves per CU (A/B)
