@@ -4,7 +4,9 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <random>
 #include <cstdlib>
 #include <cstring>
 #include <stdexcept>
@@ -32,20 +34,41 @@ void rccl_unique_id(void* out128) {
 
 namespace {
 
-// One rank's side of the push exchange (k_exchange.hip): its mailbox of [2 halves][G slots][kCap] granules,
-// the peers' mailboxes as mapped into this process, and the exchange counter.  Messages longer than kCap words
-// per rank go as consecutive exchanges of kCap-word chunks.
+// The first tag of a push-exchange group's lifetime, in [1, 2^31): tags run seed, seed + 1, ... so a new group
+// never matches granules an earlier group left at the same addresses (its memory may be a freed mailbox's, and
+// round 3's one recorded wrong-logits failure of an 8-rank group on one GPU was consistent with exactly that: tags
+// restarted at 1 for every group, so a stale line of the previous group's exchange n carried the new group's tag
+// n).  Every rank of a group must use the same seed: a LocalGroup draws one; peer processes derive it from the
+// exchanged handles (the same bytes on every rank).
+uint32_t seed_from(uint64_t h) {
+  h ^= h >> 33;
+  h *= 0xff51afd7ed558ccdull;
+  h ^= h >> 33;
+  return 1u + (uint32_t)(h % ((1ull << 31) - 1));
+}
+
+uint64_t px_timeout_ticks() {  // LLMI_PX_TIMEOUT_MS (default 10 s): the bound of every device-side wait
+  double ms = 10000.0;
+  if (const char* e = getenv("LLMI_PX_TIMEOUT_MS")) ms = std::max(1.0, atof(e));
+  return (uint64_t)(ms * 1e5);  // 100 MHz wall clock
+}
+
+// One rank's side of the push exchange (k_exchange.hip): its mailbox of [2 halves][G slots][kCap + PX_MAX_WG]
+// granules (words, then the per-work-group checksums), the peers' mailboxes as mapped into this process, and the
+// exchange counter.  Messages longer than kCap words per rank go as consecutive exchanges of kCap-word chunks.
+// The memory is uncached (fine-grained): the pushers' stores land in HBM and the gatherer's loads read HBM, whichever
+// XCD (and so whichever L2) each work-group runs on -- the 8 XCDs' L2s are not coherent with each other, also
+// inside one process on one device.
 class Mailbox {
  public:
   static constexpr int kCap = 1 << 18;  // words per rank slot (1 MB of payload): every decode exchange in one
-  Mailbox(int rank, int G, bool ipc) : rank_(rank), G_(G) {
+  static constexpr size_t kSlot = (size_t)kCap + PX_MAX_WG;
+  Mailbox(int rank, int G) : rank_(rank), G_(G), timeout_(px_timeout_ticks()) {
     if (G < 1 || G > PX_MAX_RANKS) throw std::runtime_error("push exchange: 1-16 ranks");
-    const size_t bytes = (size_t)2 * G * kCap * sizeof(uint2);
-    // uncached (fine-grained) memory for the cross-process case: peers' stores land in HBM and this rank's
-    // system-scope loads read HBM (the same-process group shares one device's L2 and takes plain memory)
-    if (ipc) LLMI_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&mine_), bytes, hipDeviceMallocUncached));
-    else LLMI_HIP(hipMalloc(&mine_, bytes));
-    LLMI_HIP(hipMemset(mine_, 0, bytes));  // tag 0: nothing published (the first exchange's tag is 1)
+    if (rank < 0 || rank >= G) throw std::runtime_error("push exchange: rank out of range");
+    const size_t bytes = (size_t)2 * G * kSlot * sizeof(uint2);
+    LLMI_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&mine_), bytes, hipDeviceMallocUncached));
+    LLMI_HIP(hipMemset(mine_, 0, bytes));  // tag 0: nothing published (tags are >= 1)
     LLMI_HIP(hipMalloc(&ctl_, 4 * sizeof(unsigned)));
     LLMI_HIP(hipMemset(ctl_, 0, 4 * sizeof(unsigned)));
     LLMI_HIP(hipDeviceSynchronize());
@@ -58,9 +81,16 @@ class Mailbox {
     (void)hipFree(mine_);
     (void)hipFree(ctl_);
   }
+  // the group's first tag (before the first exchange: the counter is then at seed - 1)
+  void seed(uint32_t first_tag) {
+    const unsigned c = first_tag - 1u;
+    LLMI_HIP(hipMemcpy(ctl_, &c, sizeof(c), hipMemcpyHostToDevice));
+    seeded_ = true;
+  }
   uint2* mine() const { return mine_; }
   void set_peer(int q, uint2* p) { peers_[q] = p; }
   bool connected() const {
+    if (!seeded_) return false;
     for (uint2* p : peers_)
       if (!p) return false;
     return true;
@@ -82,6 +112,11 @@ class Mailbox {
       peers_[q] = static_cast<uint2*>(p);
     }
     opened_ = true;
+    // every rank hashes the same handle bytes: the same seed, unique to these allocations
+    uint64_t h = 1469598103934665603ull;
+    const unsigned char* b = static_cast<const unsigned char*>(handles);
+    for (size_t i = 0; i < (size_t)G_ * PEER_HANDLE_BYTES; i++) h = (h ^ b[i]) * 1099511628211ull;
+    seed(seed_from(h));
   }
   // the all-gather of `bytes` per rank at buf (rank q's slice at buf + q bytes), as `phase` launches
   void run(void* buf, size_t bytes, int phase, hipStream_t s) {
@@ -105,17 +140,20 @@ class Mailbox {
     a.epoch = ctl_;
     a.ticket = ctl_ + 1;
     a.err = reinterpret_cast<int*>(ctl_ + 2);
+    a.timeout = timeout_;
     launch_push_exchange(a, s);
   }
-  bool failed() {  // reads and clears the device flag (callers have synchronised the stream)
+  int failed() {  // reads and clears the device flag (callers have synchronised the stream)
     int e = 0;
     LLMI_HIP(hipMemcpy(&e, ctl_ + 2, sizeof(int), hipMemcpyDeviceToHost));
     if (e) LLMI_HIP(hipMemset(ctl_ + 2, 0, sizeof(int)));
-    return e != 0;
+    return e;
   }
 
  private:
   int rank_, G_;
+  uint64_t timeout_;
+  bool seeded_ = false;
   uint2* mine_ = nullptr;
   unsigned* ctl_ = nullptr;  // [0] exchange count, [1] ticket, [2] error flag
   std::vector<uint2*> peers_;
@@ -125,11 +163,11 @@ class Mailbox {
 // one process per GPU, the push exchange through IPC-mapped mailboxes
 class PeerCollective : public Collective {
  public:
-  PeerCollective(int rank, int size) : Collective(rank, size), mb_(rank, size, true) {}
+  PeerCollective(int rank, int size) : Collective(rank, size), mb_(rank, size) {}
   bool graph_safe() const override { return true; }
   int kind() const override { return EX_PUSH; }
   void all_gather(void* buf, size_t bytes, hipStream_t s) override { mb_.run(buf, bytes, PX_PUSH | PX_GATHER, s); }
-  bool failed() override { return mb_.failed(); }
+  int failed() override { return mb_.failed(); }
   void peer_handle(void* out) const override { mb_.handle(out); }
   void peer_connect(const void* handles) override { mb_.open(handles); }
 
@@ -163,9 +201,18 @@ class LocalCollective : public Collective {
   LocalCollective(LocalGroup* g, int rank) : Collective(rank, g->n), g_(g) {
     const char* ex = getenv("LLMI_TP_EXCHANGE");
     push_ = !(ex && std::string(ex) == "copy");
-    if (push_) mb_.reset(new Mailbox(rank, g->n, false));
+    {
+      std::lock_guard<std::mutex> lk(g->mu);
+      if (rank < 0 || rank >= g->n || g->joined[rank]) throw std::runtime_error("local group: bad or duplicate rank");
+    }
+    if (push_) {
+      mb_.reset(new Mailbox(rank, g->n));
+      mb_->seed(g->seed);
+    }
+    if (const char* d = getenv("LLMI_PX_TEST_DROP"))  // test hook: this rank skips its first push
+      drop_ = atoi(d) == rank;
     std::lock_guard<std::mutex> lk(g->mu);
-    if (rank < 0 || rank >= g->n || g->joined[rank]) throw std::runtime_error("local group: bad or duplicate rank");
+    if (g->joined[rank]) throw std::runtime_error("local group: bad or duplicate rank");
     g->joined[rank] = true;
     if (push_) g->mail[rank] = mb_->mine();
     LLMI_HIP(hipEventCreateWithFlags(&g->ready[rank], hipEventDisableTiming));
@@ -181,7 +228,7 @@ class LocalCollective : public Collective {
   }
   bool graph_safe() const override { return false; }
   int kind() const override { return push_ ? EX_PUSH : EX_COPY; }
-  bool failed() override { return push_ && mb_->failed(); }
+  int failed() override { return push_ ? mb_->failed() : 0; }
   void all_gather(void* buf, size_t bytes, hipStream_t s) override {
     if (push_) return push_gather(buf, bytes, s);
     LocalGroup& g = *g_;
@@ -214,7 +261,8 @@ class LocalCollective : public Collective {
       for (int q = 0; q < size_; q++) mb_->set_peer(q, g.mail[q]);
     }
     for (size_t c = 0; c < Mailbox::chunks(bytes); c++) {
-      mb_->run_chunk(buf, bytes, c, PX_PUSH, s);
+      if (drop_) drop_ = false;  // the test hook: the peers' gathers wait past their bound
+      else mb_->run_chunk(buf, bytes, c, PX_PUSH, s);
       LLMI_HIP(hipEventRecord(g.ready[rank_], s));
       g.barrier();
       for (int q = 0; q < size_; q++)
@@ -225,7 +273,7 @@ class LocalCollective : public Collective {
   }
 
   LocalGroup* g_;
-  bool push_ = true;
+  bool push_ = true, drop_ = false;
   std::unique_ptr<Mailbox> mb_;
 };
 
@@ -248,6 +296,9 @@ std::unique_ptr<Collective> make_null(int rank, int size) {
 LocalGroup::LocalGroup(int n_)
     : n(n_), joined(n_, false), bufs(n_, nullptr), ready(n_, nullptr), done(n_, nullptr), mail(n_, nullptr) {
   if (n_ < 1) throw std::runtime_error("local group: size < 1");
+  static std::atomic<uint64_t> groups{0};
+  std::random_device rd;
+  seed = seed_from(((uint64_t)rd() << 32) ^ rd() ^ (++groups * 0x9E3779B97F4A7C15ull));
 }
 
 LocalGroup::~LocalGroup() = default;
@@ -269,7 +320,8 @@ std::unique_ptr<Collective> make_rccl(int rank, int size, const void* id128) {
   return std::unique_ptr<Collective>(new RcclCollective(rank, size, id128));
 }
 
-std::unique_ptr<Collective> make_local(LocalGroup* g, int rank) {
+std::unique_ptr<Collective> make_local(LocalGroup* g, int rank, int size) {
+  if (!g || size != g->n) throw std::runtime_error("local group: tp_size differs from the group's size");
   return std::unique_ptr<Collective>(new LocalCollective(g, rank));
 }
 

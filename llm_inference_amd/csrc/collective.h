@@ -46,8 +46,9 @@ class Collective {
   virtual int kind() const = 0;
   // in place: this rank's slice is already at buf + rank * bytes
   virtual void all_gather(void* buf, size_t bytes, hipStream_t s) = 0;
-  // a bounded device-side wait of the exchange timed out since the last call (flag cleared)
-  virtual bool failed() { return false; }
+  // the exchange failed on the device since the last call (a bounded wait timed out, or a received slice
+  // failed its checksum); 0 = no.  The ranks' exchange counts may then differ: the session stops.
+  virtual int failed() { return 0; }
   // push exchange between processes: this rank's mailbox handle, then every rank's (rank order)
   virtual void peer_handle(void* out) const;
   virtual void peer_connect(const void* handles);
@@ -58,16 +59,18 @@ class Collective {
 
 // ---- the one-shot push all-gather (k_exchange.hip) ----
 constexpr int PX_MAX_RANKS = 16;
+constexpr int PX_MAX_WG = 64;  // work-groups per exchange launch (= checksum granules per sender slot)
 constexpr int PX_PUSH = 1, PX_GATHER = 2;
 struct PushArgs {
-  uint2* mail[PX_MAX_RANKS];  // every rank's mailbox [2][G][cap] granules (this process's mapping of it)
+  uint2* mail[PX_MAX_RANKS];  // every rank's mailbox [2][G][cap + PX_MAX_WG] granules (this process's mapping)
   uint32_t* buf;              // rank q's slice of this exchange at buf + q * stride (words)
   size_t stride;
   int words;                  // per rank, <= cap
   int rank, G, cap, phase;    // phase: PX_PUSH | PX_GATHER
-  unsigned* epoch;            // exchanges completed (tag = epoch + 1)
+  unsigned* epoch;            // seed - 1 + exchanges completed (tag = epoch + 1)
   unsigned* ticket;           // work-groups done with the gather (the last one advances epoch)
-  int* err;                   // set when a wait times out
+  int* err;                   // 1: a wait timed out; 2: a received slice failed its checksum
+  uint64_t timeout;           // bound of every wait, in ticks of the 100 MHz wall clock
 };
 void launch_push_exchange(const PushArgs& a, hipStream_t s);
 constexpr int PEER_HANDLE_BYTES = 64;
@@ -93,9 +96,10 @@ struct LocalGroup {
   std::vector<void*> bufs;
   std::vector<hipEvent_t> ready, done;
   std::vector<uint2*> mail;  // push exchange: every rank's mailbox (same process, same device)
+  uint32_t seed;             // push exchange: first tag of this group's lifetime (collective.cpp px_seed)
 };
 
-std::unique_ptr<Collective> make_local(LocalGroup* g, int rank);
+std::unique_ptr<Collective> make_local(LocalGroup* g, int rank, int size);
 // one process per GPU, push exchange; all_gather throws until peer_connect
 std::unique_ptr<Collective> make_peer(int rank, int size);
 // no exchange at all (diagnostics only: per-rank kernel time of a shard)

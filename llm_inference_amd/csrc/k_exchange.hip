@@ -12,14 +12,20 @@
 //   gather -- the rank re-loads its own mailbox's other slots until every
 //             granule carries this exchange's tag and writes the words into
 //             the destination buffer.
-// tag = the rank's exchange count + 1 (a device counter the last gathering
+// tag = seed + the rank's exchange count (a device counter the last gathering
 // work-group advances, so it lives inside the token's hipGraph); every rank
-// makes the same exchanges in the same order, so the counts agree.  Halves
-// alternate with the tag's parity: a rank can push exchange n + 1 while a
-// slower peer still reads exchange n (other half), but not n + 2 -- that needs
-// the slow peer's own n + 1 push, which comes after its n gather.
-// The waits are bounded by wall-clock time (a rank that stopped sets *err; the
-// session reports it at the next sync).
+// makes the same exchanges in the same order, so the counts agree.  The seed
+// is drawn per group lifetime (collective.cpp) so a mailbox whose memory held
+// an earlier group's granules can never match them.  Halves alternate with the
+// tag's parity: a rank can push exchange n + 1 while a slower peer still reads
+// exchange n (other half), but not n + 2 -- that needs the slow peer's own
+// n + 1 push, which comes after its n gather.
+// Self-check: work-group b of every pusher also stores a checksum granule of
+// its words (slot index cap + b); the gatherer's work-group b sums what it
+// received from each peer the same way and compares, so a stale or torn slice
+// raises an error (*err = 2) instead of passing wrong words on.
+// The waits are bounded by wall-clock time (*err = 1; the session reports it
+// at the next sync and refuses further work: the ranks' counts may differ).
 #include "collective.h"
 #include "common.h"
 
@@ -29,7 +35,6 @@ namespace {
 
 constexpr int PX_T = 256;                          // threads per work-group
 constexpr int PX_B = 4;                            // granules per thread per gather batch
-constexpr uint64_t PX_TIMEOUT = 1000000000ull;     // 10 s of the 100 MHz wall clock (a peer's host may lag)
 
 __device__ __forceinline__ void px_store(uint2* g, uint32_t v, uint32_t tag) {
   __hip_atomic_store(reinterpret_cast<uint64_t*>(g), ((uint64_t)tag << 32) | v, __ATOMIC_RELAXED,
@@ -39,24 +44,39 @@ __device__ __forceinline__ uint64_t px_load(const uint2* g) {
   return __hip_atomic_load(reinterpret_cast<const uint64_t*>(g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+__device__ __forceinline__ uint32_t px_mix(uint32_t v, uint32_t idx) {  // order-free checksum term
+  return (v ^ (idx * 0x9E3779B9u)) * 0x85EBCA6Bu + idx;
+}
+
 // work-group b handles words [b per, (b + 1) per) of every rank's slice
 __global__ __launch_bounds__(PX_T) void push_exchange_kernel(PushArgs a) {
   __shared__ uint32_t s_tag;
+  __shared__ uint32_t s_sum[PX_MAX_RANKS];
   const int t = threadIdx.x;
   if (t == 0) s_tag = __hip_atomic_load(a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  if (t < PX_MAX_RANKS) s_sum[t] = 0;
   __syncthreads();
   const uint32_t tag = s_tag;
   const size_t half = tag & 1u;
+  const size_t slot_w = (size_t)a.cap + PX_MAX_WG;  // granules per sender slot: words, then checksums
   const int per = (a.words + gridDim.x - 1) / gridDim.x;
   const int w0 = blockIdx.x * per, n = max(0, min(a.words, w0 + per) - w0);
   if (a.phase & PX_PUSH) {
     const uint32_t* src = a.buf + (size_t)a.rank * a.stride;
-    const size_t slot = (half * a.G + a.rank) * (size_t)a.cap;
+    const size_t slot = (half * a.G + a.rank) * slot_w;
+    uint32_t sum = 0;
     for (int i = t; i < n; i += PX_T) {
       const uint32_t v = src[w0 + i];
+      sum += px_mix(v, (uint32_t)(w0 + i));
 #pragma unroll 4
       for (int q = 0; q < a.G; q++) px_store(a.mail[q] + slot + w0 + i, v, tag);
     }
+    atomicAdd(&s_sum[0], sum);
+    __syncthreads();
+    if (t < a.G) px_store(a.mail[t] + slot + a.cap + blockIdx.x, s_sum[0], tag);
+    __syncthreads();
+    if (t == 0) s_sum[0] = 0;
+    __syncthreads();
   }
   if (a.phase & PX_GATHER) {
     // items (peer q != rank, word i) in batches of PX_B per thread: every load of a batch is issued before any
@@ -66,7 +86,7 @@ __global__ __launch_bounds__(PX_T) void push_exchange_kernel(PushArgs a) {
     const uint64_t t0 = wall_clock64();
     bool late = false;
     for (int j0 = t; j0 < items; j0 += PX_T * PX_B) {
-      int dst[PX_B];
+      int dst[PX_B], qk[PX_B], ik[PX_B];
       const uint2* src[PX_B];
       uint64_t g[PX_B];
       bool ok[PX_B];
@@ -74,7 +94,9 @@ __global__ __launch_bounds__(PX_T) void push_exchange_kernel(PushArgs a) {
       for (int k = 0; k < PX_B; k++) {
         const int j = min(j0 + k * PX_T, items - 1);  // clamped: the tail repeats the last item
         const int qi = j / n, i = j % n, q = qi + (qi >= a.rank ? 1 : 0);
-        src[k] = mine + (half * a.G + q) * (size_t)a.cap + w0 + i;
+        qk[k] = q;
+        ik[k] = w0 + i;
+        src[k] = mine + (half * a.G + q) * slot_w + w0 + i;
         dst[k] = (int)((size_t)q * a.stride) + w0 + i;
         g[k] = px_load(src[k]);
       }
@@ -86,7 +108,7 @@ __global__ __launch_bounds__(PX_T) void push_exchange_kernel(PushArgs a) {
           all = all && ok[k];
         }
         if (all || late) break;
-        if (wall_clock64() - t0 > PX_TIMEOUT) {
+        if (wall_clock64() - t0 > a.timeout) {
           late = true;
           __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
@@ -98,7 +120,26 @@ __global__ __launch_bounds__(PX_T) void push_exchange_kernel(PushArgs a) {
       }
 #pragma unroll
       for (int k = 0; k < PX_B; k++)
-        if (j0 + k * PX_T < items) a.buf[dst[k]] = (uint32_t)g[k];
+        if (j0 + k * PX_T < items) {
+          a.buf[dst[k]] = (uint32_t)g[k];
+          atomicAdd(&s_sum[qk[k]], px_mix((uint32_t)g[k], (uint32_t)ik[k]));
+        }
+    }
+    __syncthreads();
+    // every peer's checksum granule for this work-group's words
+    if (t < a.G && t != a.rank && n > 0) {
+      const uint2* cs = mine + (half * a.G + t) * slot_w + a.cap + blockIdx.x;
+      uint64_t g = px_load(cs);
+      while ((uint32_t)(g >> 32) != tag && !late) {
+        if (wall_clock64() - t0 > a.timeout) {
+          late = true;
+          __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        g = px_load(cs);
+      }
+      if (!late && (uint32_t)g != s_sum[t]) __hip_atomic_store(a.err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     // the last work-group to finish advances the exchange count (the next exchange's tag)
     __syncthreads();
@@ -125,7 +166,7 @@ void launch_push_exchange(const PushArgs& a, hipStream_t s) {
   if (a.words == 0) return;
   // one work-group per 256 words up to 64 (a 1 MB prefill chunk: 4096 words each) -- a few CUs' worth of
   // spinning waves, whatever the peers are running
-  const int nwg = std::max(1, std::min(64, (a.words + PX_T - 1) / PX_T));
+  const int nwg = std::max(1, std::min(PX_MAX_WG, (a.words + PX_T - 1) / PX_T));
   hipLaunchKernelGGL(push_exchange_kernel, dim3(nwg), dim3(PX_T), 0, s, a);
   LLMI_HIP(hipGetLastError());
 }

@@ -549,7 +549,7 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
   try {
     if (tp_) {
       coll_ = tp_solo         ? make_null(tp_rank_, tp_size_)
-              : opts.tp_group ? make_local(reinterpret_cast<LocalGroup*>(opts.tp_group), tp_rank_)
+              : opts.tp_group ? make_local(reinterpret_cast<LocalGroup*>(opts.tp_group), tp_rank_, tp_size_)
               : tp_peer       ? make_peer(tp_rank_, tp_size_)
                               : make_rccl(tp_rank_, tp_size_, opts.tp_id);
       if (!coll_->graph_safe()) use_graph_ = false;
@@ -1608,26 +1608,44 @@ void Session::set_token_pos(int32_t token, int pos, bool reset_ring) {
   launch_set_token_pos(d_token_, d_pos_, ring_idx_, token, pos, reset_ring, stream_);
 }
 
+void Session::ensure_usable() const {
+  if (broken_)
+    throw status_error(LLMI_E_HIP, "tensor-parallel session unusable after a failed exchange (its exchange count may "
+                                   "differ from its peers'): destroy and re-create every rank's session");
+}
+
+template <class F> void Session::tp_guarded(F&& f) {
+  ensure_usable();
+  try {
+    f();
+  } catch (...) {
+    if (tp_) broken_ = true;
+    throw;
+  }
+}
+
 void Session::forward(const int32_t* tokens, int n, int pos, float* logits, int32_t* argmax) {
   if (n <= 0) throw status_error(LLMI_E_ARG, "forward: no tokens");
   if (pos < 0 || pos + n > max_ctx_) throw status_error(LLMI_E_RANGE, "forward: context overflow");
   for (int i = 0; i < n; i++)
     if (tokens[i] < 0 || tokens[i] >= vocab_) throw status_error(LLMI_E_RANGE, "forward: token id out of range");
-  if (n > 1 && prefill_ok_ && getenv("LLMI_NO_PREFILL") == nullptr) {
-    set_token_pos(tokens[n - 1], pos + n - 1, true);  // what the token loop leaves behind
-    prefill(tokens, n, pos);
-  } else {
-    for (int i = 0; i < n; i++) {
-      set_token_pos(tokens[i], pos + i, i == 0);
-      run_step();
+  tp_guarded([&] {
+    if (n > 1 && prefill_ok_ && getenv("LLMI_NO_PREFILL") == nullptr) {
+      set_token_pos(tokens[n - 1], pos + n - 1, true);  // what the token loop leaves behind
+      prefill(tokens, n, pos);
+    } else {
+      for (int i = 0; i < n; i++) {
+        set_token_pos(tokens[i], pos + i, i == 0);
+        run_step();
+      }
     }
-  }
-  // every rank of a tensor-parallel group gathers the full logits (collective)
-  if (tp_) coll_->all_gather(logits_, (size_t)v_sh_ * sizeof(float), stream_);
-  if (logits) LLMI_HIP(hipMemcpyAsync(logits, logits_, (size_t)vocab_ * 4, hipMemcpyDeviceToHost, stream_));
-  if (argmax) LLMI_HIP(hipMemcpyAsync(argmax, d_token_, 4, hipMemcpyDeviceToHost, stream_));
-  LLMI_HIP(hipStreamSynchronize(stream_));
-  check_device_error();
+    // every rank of a tensor-parallel group gathers the full logits (collective)
+    if (tp_) coll_->all_gather(logits_, (size_t)v_sh_ * sizeof(float), stream_);
+    if (logits) LLMI_HIP(hipMemcpyAsync(logits, logits_, (size_t)vocab_ * 4, hipMemcpyDeviceToHost, stream_));
+    if (argmax) LLMI_HIP(hipMemcpyAsync(argmax, d_token_, 4, hipMemcpyDeviceToHost, stream_));
+    LLMI_HIP(hipStreamSynchronize(stream_));
+    check_device_error();
+  });
 }
 
 // tensor.h print_tensor_generic for a {n, 1, 1, 1} tensor: 3 leading and 3
@@ -1730,19 +1748,24 @@ void Session::forward_dump(const int32_t* tokens, int n, int pos, const char* pa
 void Session::enqueue(int32_t first, int pos, int n_steps) {
   if (first < 0 || first >= vocab_) throw status_error(LLMI_E_RANGE, "token id out of range");
   if (pos < 0 || pos + n_steps > max_ctx_) throw status_error(LLMI_E_RANGE, "generate: context overflow");
-  set_token_pos(first, pos, true);
-  if (n_steps > 0 && screen_ && embed_fold_ok()) {  // the folded step graph starts at layer 0: the first embedding here
-    const int E = hp_.n_embd;
-    launch_embed_norm(embd_.type, embd_raw_, embd_row_bytes_, d_token_, std::sqrt(static_cast<float>(E)), resid_,
-                      L_[0].attn_norm, embed_out(), E, hp_.eps, ex_norm_, stream_);
-  }
-  for (int i = 0; i < n_steps; i++) run_step(true);
+  tp_guarded([&] {
+    set_token_pos(first, pos, true);
+    if (n_steps > 0 && screen_ && embed_fold_ok()) {  // the folded step graph starts at layer 0: the first embedding here
+      const int E = hp_.n_embd;
+      launch_embed_norm(embd_.type, embd_raw_, embd_row_bytes_, d_token_, std::sqrt(static_cast<float>(E)), resid_,
+                        L_[0].attn_norm, embed_out(), E, hp_.eps, ex_norm_, stream_);
+    }
+    for (int i = 0; i < n_steps; i++) run_step(true);
+  });
 }
 
 void Session::sync(int32_t* out, int n) {
-  if (out && n > 0) LLMI_HIP(hipMemcpyAsync(out, ring_, (size_t)std::min(n, max_ctx_) * 4, hipMemcpyDeviceToHost, stream_));
-  LLMI_HIP(hipStreamSynchronize(stream_));
-  check_device_error();
+  tp_guarded([&] {
+    if (out && n > 0)
+      LLMI_HIP(hipMemcpyAsync(out, ring_, (size_t)std::min(n, max_ctx_) * 4, hipMemcpyDeviceToHost, stream_));
+    LLMI_HIP(hipStreamSynchronize(stream_));
+    check_device_error();
+  });
 }
 
 // a bounded in-kernel wait that gave up (k_attn.hip attention block): the
@@ -1759,8 +1782,13 @@ void Session::peer_connect(const void* handles) {
 }
 
 void Session::check_device_error() {
-  if (coll_ && coll_->failed())  // a push exchange waited past its bound for a peer's slice
-    throw status_error(LLMI_E_HIP, "tensor-parallel push exchange: a peer's slice did not arrive (device results invalid)");
+  if (const int e = coll_ ? coll_->failed() : 0) {  // the push exchange: a wait past its bound, or a bad checksum
+    broken_ = true;
+    throw status_error(LLMI_E_HIP, e == 2 ? "tensor-parallel push exchange: a received slice failed its checksum "
+                                            "(device results invalid)"
+                                          : "tensor-parallel push exchange: a peer's slice did not arrive within "
+                                            "LLMI_PX_TIMEOUT_MS (device results invalid)");
+  }
   if (blk_trace_) {  // development: append the last traced launch (work-group x 8 clocks) to LLMI_BLOCK_TRACE_OUT
     std::vector<unsigned long long> h(4096 * 8);
     LLMI_HIP(hipMemcpy(h.data(), blk_trace_, h.size() * 8, hipMemcpyDeviceToHost));

@@ -160,6 +160,11 @@ class Session {
   XBlock* hq_ = nullptr;         // the GELU launch's Q8_0 blocks of hid (down as a PLAIN launch, 32-unit groups)
   XBlock* blk_xo_ = nullptr;     // attention output Q8_0 blocks (layer 0's qkv still reads act_.q8 in the launch)
   void check_device_error();
+  // a tensor-parallel session whose exchange failed (or that threw between two exchanges) may be out of step with
+  // its peers: every later call is refused until the group is re-created
+  void ensure_usable() const;
+  template <class F> void tp_guarded(F&& f);
+  bool broken_ = false;
   bool ex_gemv_ = false, ex_norm_ = false, ex_attn_ = false, ex_logits_ = false;  // per kernel family
   HParams hp_;
   int vocab_ = 0, max_ctx_ = 4096;

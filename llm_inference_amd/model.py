@@ -27,7 +27,8 @@ def tp_unique_id() -> bytes:
 class TPGroup:
     """Ranks of one tensor-parallel group sharing ONE device (tests: RCCL
     refuses two ranks per GPU).  Each rank's session is driven by its own
-    host thread; the all-gathers are device-to-device copies."""
+    host thread; the all-gathers are the push exchange split around host
+    barriers (LLMI_TP_EXCHANGE=copy: device-to-device copies)."""
 
     def __init__(self, size: int):
         h = C.c_void_p()

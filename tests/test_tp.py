@@ -205,3 +205,66 @@ def test_tp_argument_errors():
         Model(g, tp_rank=3, tp_size=3, tp_group=grp)
     assert ei.value.status == "E_ARG"
     grp.close()
+
+
+def test_group_recreated_bit_identical(monkeypatch):
+    """The round-3 wrong-logits case (mini-27b at tp 8, batched prefill): groups created, destroyed and
+    re-created in one process reuse the freed mailboxes' memory.  Tags are seeded per group lifetime and the
+    mailboxes are uncached, so a new group can never accept an old group's granules: three lifetimes in a row
+    give the whole model's bits (a stale or torn slice would raise through the gather's checksum instead)."""
+    from llm_inference_amd.model import Model
+    from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
+    cfg = CONFIGS["mini-27b"]
+    g = build_gemma3_gguf(cfg, seed=13)
+    prompt = np.random.default_rng(15).integers(4, cfg.vocab, 70).astype(np.int32)
+    monkeypatch.setenv("LLMI_NO_BLOCK", "1")
+    whole = Model(g, exact=False, max_ctx=128)
+    ref = whole.forward(prompt, 0)
+    ref_toks = whole.generate(int(np.argmax(ref)), len(prompt), 6)
+    whole.close()
+    for _ in range(3):
+        for lg, toks, _info in _run_ranks(g, 8, prompt, 6, max_ctx=128):
+            np.testing.assert_array_equal(lg, ref)
+            assert toks.tolist() == ref_toks.tolist()
+
+
+def test_exchange_failure_is_sticky(monkeypatch):
+    """A push exchange whose gather waits past LLMI_PX_TIMEOUT_MS (test hook LLMI_PX_TEST_DROP: rank 1 skips its
+    first push) reports LLMI_E_HIP at the end of the call, never logits, and the session then refuses every
+    later call (its exchange count may differ from its peers'): ADVICE r3."""
+    from llm_inference_amd._lib import LLMIError
+    from llm_inference_amd.model import Model, TPGroup
+    from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
+    cfg = CONFIGS["mini-1b"]
+    g = build_gemma3_gguf(cfg, seed=31)
+    monkeypatch.setenv("LLMI_NO_PREFILL", "1")
+    monkeypatch.setenv("LLMI_PX_TIMEOUT_MS", "200")
+    monkeypatch.setenv("LLMI_PX_TEST_DROP", "1")
+    grp = TPGroup(2)
+    res = [None, None]
+
+    def rank(r):
+        m = Model(g, exact=False, max_ctx=32, tp_rank=r, tp_size=2, tp_group=grp)
+        try:
+            m.forward([5], 0)
+            res[r] = "ok"
+        except LLMIError as e:
+            res[r] = e
+        if r == 0 and isinstance(res[0], LLMIError):
+            try:  # refused at once: no exchange (and no host barrier) is entered
+                m.generate(7, 1, 2)
+                res[r] = "second call ran"
+            except LLMIError as e:
+                res[r] = (res[r], e)
+        m.close()
+
+    th = [threading.Thread(target=rank, args=(r,)) for r in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    grp.close()
+    assert isinstance(res[0], tuple), res
+    first, second = res[0]
+    assert first.status == "E_HIP" and "did not arrive" in str(first)
+    assert second.status == "E_HIP" and "unusable" in str(second)
