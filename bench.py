@@ -402,6 +402,7 @@ def main():
                             if tp else f"replicas{d.world}")
                            if d.world > 1 else "single",
             "kernels_per_token": info.kernels_per_token,
+            **({"exact_engine": bool(info.exact_engine)} if a.exact else {}),
         },
         "hbm": {
             "bytes_per_token": int(tok_bytes),

@@ -212,6 +212,8 @@ typedef struct {
   int ffn_engine;             /* 1: gate_up + GELU + down of each layer are ONE launch (the FFN engine) */
   int tp_exchange;            /* tensor-parallel exchange: 0 none, 1 RCCL, 2 device copies, 3 one-shot push */
   long long block_slow_waits; /* attention-block hand-off waits (per wave) that took over 20 us, since creation */
+  int exact_engine;           /* 1: LLMI_EXACT runs on the exact-order engine (k_exact.hip: the reference's
+                                 arithmetic with streamed GEMVs and fused norms), 0: the per-op exact kernels */
 } llmi_session_info;
 int llmi_session_get_info(const llmi_session* s, llmi_session_info* info);
 

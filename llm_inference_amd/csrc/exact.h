@@ -1,0 +1,61 @@
+// exact.h -- the exact-order decode engine (k_exact.hip): the reference's AVX2
+// arithmetic, bit for bit, at streaming speed.
+//
+// The reference's Q4_0 row (ops.cpp:364-399) keeps eight fp32 accumulators,
+// one per 4-element slot of a 32-element block, each a serial fma chain over
+// the row's blocks in order, then hsum_float_8.  A lane here is one row's pair
+// of slots (jj, jj + 4): it walks every block of its row in order, so the chains
+// are the reference's, while 16 rows x 4 lanes per wave read whole lines from
+// the XL weight layout below.
+//
+// XL layout of a Q4_0 weight [rows][nb] (nb % 4 == 0), group g = blocks 4g..4g+3:
+//   qs [g][row][jj] 16 B = bytes 4jj..4jj+3 of the four blocks' 16-B quants
+//   d  [g][row]     8 B  = the four blocks' f16 scales
+// so one wave-instruction of a group reads 16 rows x 64 B = 1 KB contiguous.
+#pragma once
+
+#include "session_kernels.h"
+
+namespace llmi {
+
+struct XlWeight {
+  uint4* qs = nullptr;
+  uint2* d = nullptr;
+  int rows = 0, nb = 0;
+  size_t bytes = 0;  // algorithmic (GGUF) bytes
+};
+
+// sources of an XL weight: rows [0, n) of each device Q4_0 weight (row-major blocks), concatenated, or (gelu32)
+// two weights gate / up interleaved in groups of 32 rows (gate 32 k.., up 32 k..) for the GELU epilogue
+struct XlSrc {
+  const DevWeight* w[3] = {nullptr, nullptr, nullptr};
+  int n = 0;
+  bool gelu32 = false;
+};
+bool xl_supported(const DevWeight& w);
+XlWeight make_xl_weight(const XlSrc& src, hipStream_t s);
+void free_xl_weight(XlWeight& w);
+
+enum XlRole {
+  XL_PLAIN = 0,  // x = the Q8_0 blocks at xb
+  XL_QUANT = 1,  // x = quantize_row_q8_0(y)
+  XL_PRE = 2,    // h = resid_in (+ rms(y) * w_post when y); resid_out = h; x = Q8_0(rms(h) * w_next)
+  XL_GELU = 3,   // XL_PRE, then GELU(gate) * up of the work-group's 32 units -> hid, hq (one Q8_0 block)
+};
+struct XlArgs {
+  const XBlock* xb = nullptr;
+  const float* y = nullptr;
+  const float* w_post = nullptr;
+  const float* resid_in = nullptr;
+  float* resid_out = nullptr;
+  const float* w_next = nullptr;
+  float* xn_out = nullptr;  // optional: x before quantization (work-group 0)
+  int n = 0;                // input length (= nb * 32)
+  double eps = 0;
+  float* out = nullptr;     // PLAIN / QUANT / PRE: [rows]
+  float* hid = nullptr;     // GELU: [rows / 2]
+  XBlock* hq = nullptr;     // GELU: [rows / 64]
+};
+void launch_exact_gemv(const XlWeight& w, const XlArgs& a, int role, hipStream_t s);
+
+}  // namespace llmi

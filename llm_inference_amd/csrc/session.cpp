@@ -560,6 +560,7 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
     upload(g);
     alloc_buffers();
     build_rope_tables();
+    setup_xl();
     // batched prefill: the fast fused layout on one device, shapes the
     // prefill kernels cover (otherwise forward() runs the token loop)
     // (a tensor-parallel rank: its shards' GEMMs, the slices all-gathered per
@@ -656,6 +657,7 @@ void Session::release() {
   graph_gen_ = nullptr;
   free_screen_table(scr_);
   for (auto& l : L_) {
+    for (XlWeight* x : {&l.xqkv, &l.xo, &l.xgu, &l.xdn}) free_xl_weight(*x);
     if (l.aliased) continue;  // LLMI_SHARE_LAYERS: another layer's weights
     for (auto& p : l.qkv) free_weight(p.w);
     for (auto& p : l.gate_up) free_weight(p.w);
@@ -805,7 +807,9 @@ void Session::record_step(hipStream_t s, bool gen, bool fold_embed) {
   bool fused = fuse_layers_;
   for (const auto& l : L_) fused &= l.fused;
   if (tp_ && !fused) throw status_error(LLMI_E_ARG, "tensor parallel needs the fused layer path");
-  if (fused && engine_ && !dump_ && !trace_fn_) {
+  if (xl_ && !dump_ && !trace_fn_ && x_q8 && x_blocks == (const void*)act_.q8.xb) {
+    record_layers_xl(s);
+  } else if (fused && engine_ && !dump_ && !trace_fn_) {
     record_layers_engine(s, x_q8);
   } else if (fused) {
     record_layers_fused(s, x_q8);
@@ -1487,6 +1491,120 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
   dump("result_norm", xn_, E, s);
 }
 
+// Exact mode on the exact-order engine (exact.h): every Gemma-3 layer with Q4_0 q, k, v, o, gate, up and down
+// (the 4B / 1B / 27B Q4_0 files) gets XL copies of its weights; LLMI_EXACT_XL=0 keeps the per-op exact kernels.
+void Session::setup_xl() {
+  if (!exact_ || tp_ || hp_.gemma4 || ple_table_.qs || getenv("LLMI_EXACT_PARTS")) return;
+  if (const char* e = getenv("LLMI_EXACT_XL"))
+    if (atoi(e) == 0) return;
+  if (hp_.n_embd % 128 || hp_.n_ff % 128 || 2 * (size_t)hp_.n_embd * 4 + hp_.n_embd / 32 * 68 > 60 * 1024) return;
+  for (const auto& l : L_) {
+    bool ok = l.has_kv && !l.qkv.empty() && !l.gate_up.empty() && (hp_.n_head * l.hd) % 128 == 0;
+    for (const auto& p : l.qkv) ok = ok && xl_supported(p.w);
+    for (const auto& p : l.gate_up) ok = ok && xl_supported(p.w);
+    int gu_rows = 0;
+    for (const auto& p : l.gate_up) gu_rows += p.w.rows;
+    ok = ok && xl_supported(l.o.w) && xl_supported(l.down.w) && gu_rows == 2 * hp_.n_ff && !l.gu_interleaved &&
+         (l.gate_up.size() == 1 || l.gate_up[0].w.rows == hp_.n_ff) && l.down.w.cols == hp_.n_ff;
+    if (!ok) return;
+  }
+  for (auto& l : L_) {
+    // gate and up: one part of rows [gate; up] (same type) or two parts
+    DevWeight gate = l.gate_up[0].w, up;
+    if (l.gate_up.size() == 1) {
+      const int F = hp_.n_ff, nb = gate.cols / 32;
+      gate.rows = F;
+      up = gate;
+      up.qs = static_cast<uint8_t*>(gate.qs) + (size_t)F * nb * 16;
+      up.d = gate.d + (size_t)F * nb;
+      gate.bytes = up.bytes = gguf_bytes(T_Q4_0, F, gate.cols);
+    } else {
+      up = l.gate_up[1].w;
+    }
+    XlSrc q;
+    for (auto& p : l.qkv) q.w[q.n++] = &p.w;
+    l.xqkv = make_xl_weight(q, stream_);
+    XlSrc o;
+    o.w[o.n++] = &l.o.w;
+    l.xo = make_xl_weight(o, stream_);
+    XlSrc gu;
+    gu.w[gu.n++] = &gate;
+    gu.w[gu.n++] = &up;
+    gu.gelu32 = true;
+    l.xgu = make_xl_weight(gu, stream_);
+    XlSrc d;
+    d.w[d.n++] = &l.down.w;
+    l.xdn = make_xl_weight(d, stream_);
+  }
+  LLMI_HIP(hipStreamSynchronize(stream_));
+  xl_ = true;
+}
+
+// One decode step's layers on the exact-order engine: per layer q|k|v (the previous layer's post-FFN norm and
+// residual + this layer's attn_norm in its prologue), q/k norm + rope + KV append, attention, o (its input
+// quantized in the prologue), gate|up (post-attention norm + residual + ffn_norm in the prologue, GELU * up and
+// the hidden Q8_0 blocks in the epilogue), down.  The residual stream alternates between resid_ and resid2_ (a
+// prologue's work-group 0 writes the new residual while the others still read the old one).
+void Session::record_layers_xl(hipStream_t s) {
+  const int E = hp_.n_embd;
+  float* ra = resid_;
+  float* rb = resid2_;
+  for (int l = 0; l < hp_.n_layer; l++) {
+    LayerDev& Ld = L_[l];
+    const int hd = Ld.hd;
+    XlArgs q;
+    q.n = E;
+    q.eps = hp_.eps;
+    q.out = qkv_;
+    if (l == 0) {  // the embedding launch wrote attn_norm(x)'s Q8_0 blocks
+      q.xb = act_.q8.xb;
+      launch_exact_gemv(Ld.xqkv, q, XL_PLAIN, s);
+    } else {
+      q.y = d_out_;
+      q.w_post = L_[l - 1].post_ffw_norm;
+      q.resid_in = ra;
+      q.resid_out = rb;
+      q.w_next = Ld.attn_norm;
+      launch_exact_gemv(Ld.xqkv, q, XL_PRE, s);
+      std::swap(ra, rb);
+    }
+    QKVArgs qa{qkv_, Ld.k_off, Ld.v_off, hp_.n_head, hp_.n_head_kv, hd, Ld.q_norm, Ld.k_norm,
+               Ld.is_swa ? rope_swa_ : rope_glb_, hp_.attn_scale, hp_.eps, q_, Ld.kc, Ld.vc, max_ctx_, d_pos_};
+    launch_qk_norm_rope_kv(qa, true, s);
+    AttnArgs aa{q_, Ld.kc, Ld.vc, hp_.n_head, hp_.n_head_kv, hd, max_ctx_, d_pos_, part_, attn_, ticket_, nullptr};
+    launch_attention(aa, true, s);
+    XlArgs o;
+    o.y = attn_;
+    o.n = hp_.n_head * hd;
+    o.out = o_out_;
+    launch_exact_gemv(Ld.xo, o, XL_QUANT, s);
+    XlArgs gu;
+    gu.y = o_out_;
+    gu.w_post = Ld.post_attn_norm;
+    gu.resid_in = ra;
+    gu.resid_out = rb;
+    gu.w_next = Ld.ffn_norm;
+    gu.n = E;
+    gu.eps = hp_.eps;
+    gu.hid = hid_;
+    gu.hq = hq_;
+    launch_exact_gemv(Ld.xgu, gu, XL_GELU, s);
+    std::swap(ra, rb);
+    XlArgs dn;
+    dn.xb = hq_;
+    dn.out = d_out_;
+    launch_exact_gemv(Ld.xdn, dn, XL_PLAIN, s);
+    kernels_per_token_ += 6;
+  }
+  // the last layer's post-FFN norm + residual, then output_norm (model.cpp:915-924, 986)
+  NormOut o2;
+  o2.xn = xn_;
+  if (embd_.type == T_F16) o2.x16 = act_.x16;
+  screen_norm(o2);
+  launch_residual_norm(d_out_, L_.back().post_ffw_norm, ra, out_norm_, o2, E, hp_.eps, true, s);
+  kernels_per_token_++;
+}
+
 void Session::record_layers(hipStream_t s, bool x_q8) {
   const int E = hp_.n_embd, F = hp_.n_ff;
   auto is_q8 = [](uint32_t t) { return t == T_Q4_0 || t == T_Q8_0; };
@@ -1833,6 +1951,7 @@ void Session::info(llmi_session_info* o) const {
   o->ffn_engine = ffn_engine_ ? 1 : 0;
   o->tp_exchange = coll_ ? coll_->kind() : 0;
   o->block_slow_waits = slow_waits_;
+  o->exact_engine = xl_ ? 1 : 0;
   size_t b = logits_w_.bytes;  // this rank's bytes
   for (const auto& l : L_) {
     for (const auto& p : l.qkv) b += p.w.bytes;

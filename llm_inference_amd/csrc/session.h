@@ -9,6 +9,7 @@
 
 #include "../../include/llmi.h"
 #include "collective.h"
+#include "exact.h"
 #include "gguf_reader.h"
 #include "session_kernels.h"
 
@@ -58,6 +59,8 @@ struct LayerDev {
   GemvPart ple_gate, ple_proj;   // per-layer embedding step (model.cpp:926-966), BF16 usually
   float* ple_post_norm = nullptr;
   float out_scale = 1.0f;        // layer output scale (model.cpp:968-977)
+  // the exact-order engine (exact.h): q|k|v, o, gate/up (32-unit interleave), down in the XL layout
+  XlWeight xqkv, xo, xgu, xdn;
 };
 
 class Session {
@@ -98,6 +101,10 @@ class Session {
   void ensure_prefill_buffers(int cap);
   void record_layers(hipStream_t s, bool x_q8);
   void record_layers_fused(hipStream_t s, bool x_q8);
+  // exact mode on the exact-order engine (k_exact.hip): Q4_0 Gemma-3 layers, reference arithmetic, streamed
+  bool xl_ = false;
+  void setup_xl();
+  void record_layers_xl(hipStream_t s);
   void setup_engine(const GGUFView& g);
   void setup_ffn_engine(const GGUFView& g);
   void record_layers_engine(hipStream_t s, bool x_q8);
