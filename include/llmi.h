@@ -231,6 +231,13 @@ int llmi_session_get_info(const llmi_session* s, llmi_session_info* info);
  * (0 / 0 when the family does not exist on this session). */
 int llmi_session_time_kernel(llmi_session* s, int which, int reps, double* us_per_launch, double* bytes_per_launch);
 
+/* Device self-tests of arithmetic the exact kernels rely on (synchronous, current device):
+ *   0 = every f32 bit pattern through the hardware f32 -> f16 conversion vs the reference's f32_to_f16
+ *       (gguf.cpp:68-95): out[0] non-NaN mismatches, out[1] NaN mismatches, out[2] first non-NaN mismatch;
+ *   1 = the exact engine's speculative rms_norm sum-of-squares chain vs the serial chain (ops.cpp:33-36) on 8192
+ *       vectors of 2560: out[0] differing results (must be 0), out[1] segments recomputed serially. */
+int llmi_selftest(int which, unsigned long long* out);
+
 #ifdef __cplusplus
 }
 #endif

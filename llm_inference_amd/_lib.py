@@ -92,6 +92,7 @@ _SIGS = {
     "llmi_session_sync": (C.c_int, [_vp, _vp, C.c_int]),
     "llmi_session_get_info": (C.c_int, [_vp, C.POINTER(SessionInfo)]),
     "llmi_session_time_kernel": (C.c_int, [_vp, C.c_int, C.c_int, C.POINTER(_f64), C.POINTER(_f64)]),
+    "llmi_selftest": (C.c_int, [C.c_int, _vp]),
 }
 
 

@@ -488,6 +488,22 @@ int llmi_session_peer_connect(llmi_session* s, const void* handles) {
   });
 }
 
+int llmi_selftest(int which, unsigned long long* out) {
+  return guard([&] {
+    if (!out) throw status_error(LLMI_E_ARG, "null pointer");
+    if (which == 0) {
+      exact_selftest_f16(out);
+    } else if (which == 1) {
+      unsigned r[2];
+      exact_selftest_chain(r);
+      out[0] = r[0];
+      out[1] = r[1];
+    } else {
+      throw status_error(LLMI_E_ARG, "selftest: unknown test");
+    }
+  });
+}
+
 int llmi_session_get_info(const llmi_session* s, llmi_session_info* info) {
   return guard([&] { s->s->info(info); });
 }

@@ -55,7 +55,46 @@ struct XlArgs {
   float* out = nullptr;     // PLAIN / QUANT / PRE: [rows]
   float* hid = nullptr;     // GELU: [rows / 2]
   XBlock* hq = nullptr;     // GELU: [rows / 64]
+  int serial_norms = 0;     // set by the launcher (LLMI_EXACT_SERIAL_NORMS: the norm chains without speculation)
 };
 void launch_exact_gemv(const XlWeight& w, const XlArgs& a, int role, hipStream_t s);
+
+// Exact decode attention of one layer (model.cpp:430-550 with the q / k norms, rope and scale of
+// model.cpp:762-794 and the KV append of model.cpp:440-474), as two wide launches:
+//   scores: grid (n_head, XA_NSPLIT), one wave each: the head's q row (its serial norm chain, rope, scale,
+//           f16 rounding), the new key's K / V rows where the wave owns the current position (the same bits
+//           written by every q head of the kv head), then one key per lane -- the reference's sequential
+//           double sum over the head dims -- into scores[head][key];
+//   accum:  one work-group per head: per 1024-key chunk the exclusive prefix max of the scores in double
+//           (the reference's running max is always the float rounding of it), every key's branch and its
+//           e / pe (glibc expf), then per head dim the f16 V accumulator in key order (vec_scale_f16 /
+//           vec_mad_f16) and, on an extra wave, s_acc in key order; out = f16(v) * (1 / s_acc), and its
+//           Q8_0 blocks for the o projection.
+constexpr int XA_NSPLIT = 32;  // scores: work-groups per head, each taking key chunks of 64 split apart
+struct XAttnArgs {
+  const float* qkv = nullptr;
+  int k_off = 0, v_off = 0;
+  int n_head = 0, n_head_kv = 0, head_dim = 0;
+  const float* q_norm_w = nullptr;
+  const float* k_norm_w = nullptr;
+  const float* rope_cs = nullptr;  // [max_ctx][head_dim / 2][2]
+  float attn_scale = 1.0f;
+  double eps = 0;
+  uint16_t* k_cache = nullptr;
+  uint16_t* v_cache = nullptr;
+  int max_ctx = 0;
+  const int* d_pos = nullptr;
+  double* scores = nullptr;  // [n_head][max_ctx]
+  float* out = nullptr;      // [n_head][head_dim]
+  XBlock* xq = nullptr;      // [n_head * head_dim / 32]
+};
+bool exact_attn_supported(int head_dim, int n_head, int n_head_kv);
+void launch_exact_attn(const XAttnArgs& a, hipStream_t s);
+// self-test (synchronous): over every f32 bit pattern, out[0] = non-NaN inputs whose hardware f16 conversion
+// differs from the reference's f32_to_f16, out[1] = NaN inputs that differ, out[2] = the first non-NaN one
+void exact_selftest_f16(unsigned long long* out3);
+// self-test (synchronous): 8192 vectors of 2560 floats through the speculative norm chain and the serial one:
+// out[0] = results that differ, out[1] = segments that fell back to the serial chain
+void exact_selftest_chain(unsigned* out2);
 
 }  // namespace llmi

@@ -5,12 +5,13 @@
 #include <stdexcept>
 
 #include "exact.h"
+#include "glibc_math.h"
 
 namespace llmi {
 
 namespace {
 
-constexpr int XL_P = 8;  // groups (4 blocks each) per chunk of loads
+constexpr int XL_P = 8;   // groups (4 blocks each) per chunk of loads
 
 __device__ __forceinline__ float xl_rms_scale(float sum, int n, double eps) {  // ops.cpp:37-38
   return 1.0f / sqrtf((float)((double)(sum / (float)n) + eps));
@@ -19,10 +20,9 @@ __device__ __forceinline__ float xl_rms_scale(float sum, int n, double eps) {  /
 // The reference's serial sum of squares (ops.cpp:33-36, contracted to fma by its build) over s[0..n) in LDS.
 // Every lane of the calling wave runs the same chain (broadcast reads); the reads of the next 32 values are
 // issued before the current 32 are consumed, so the chain is the fma latency alone (~4 cycles a step).
-__device__ __forceinline__ float xl_chain(const float* s, int n) {
+__device__ __forceinline__ float xl_chain(const float* s, int n, float sum = 0.0f) {
   const float4* s4 = reinterpret_cast<const float4*>(s);
   const int n4 = n >> 2, nfull = n4 & ~7;
-  float sum = 0.0f;
   float4 a[8], b[8];
   if (nfull > 0) {
 #pragma unroll
@@ -56,6 +56,72 @@ __device__ __forceinline__ float xl_chain(const float* s, int n) {
   }
   for (int i = nfull * 4; i < n; i++) sum = fmaf(s[i], s[i], sum);
   return sum;
+}
+
+// The same serial chain, its latency divided by speculation (every work-group thread calls it; the result is
+// bit-identical to xl_chain).  The n terms split into K = 2 NW segments of L; half-wave k runs segment k's chain
+// from 32 candidate start values at once -- the floats from 16 below to 15 above fl(P_k), P_k the f64 sum of the
+// earlier segments' squares (within ~2^-50 of exact, while the float chain's accumulated rounding stays within a
+// few ulps: |s - fl(P)| < 16 ulps at ~97.5 % of the boundaries of a 2560-term chain in a CPU simulation of random
+// vectors, scripts/dev/spec_chain.c).  Wave 0 then walks the boundaries: the true start of segment k is the chain
+// value after segment k - 1; if it is one of the candidates its end value is that lane's, otherwise the segment
+// is recomputed serially from it.  Either way every step is the reference's fma on the reference's value.
+template <int NW>
+__device__ __forceinline__ float xl_chain_spec(const float* s, int n, unsigned* fallbacks = nullptr) {
+  constexpr int K = 2 * NW;
+  __shared__ double s_seg[K];
+  __shared__ float s_e[K * 32];
+  __shared__ int s_base[K];
+  __shared__ float s_res;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int k = t >> 5, c = lane & 31, L = n / K;
+  double p = 0.0;
+  for (int i = c; i < L; i += 32) {
+    const double v = (double)s[k * L + i];
+    p = fma(v, v, p);
+  }
+#pragma unroll
+  for (int m = 16; m >= 1; m >>= 1) p += __shfl_xor(p, m);
+  if (c == 0) s_seg[k] = p;
+  __syncthreads();
+  double pre = 0.0;
+  for (int j = 0; j < k; j++) pre += s_seg[j];
+  const int base = k == 0 ? 0 : max(0, (int)__float_as_uint((float)pre) - 16);
+  const float x0 = k == 0 ? 0.0f : __uint_as_float((uint32_t)(base + c));
+  const float e = xl_chain(s + k * L, L, x0);
+  s_e[k * 32 + c] = e;
+  if (c == 0) s_base[k] = base;
+  __syncthreads();
+  if (wave == 0) {
+    float ev[K];
+#pragma unroll
+    for (int kk = 0; kk < K; kk++) ev[kk] = s_e[kk * 32 + (lane & 31)];
+    float cur = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(ev[0])));
+#pragma unroll
+    for (int kk = 1; kk < K; kk++) {
+      const int i = __builtin_amdgcn_readfirstlane((int)__float_as_uint(cur) - s_base[kk]);
+      if (i >= 0 && i < 32) cur = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ev[kk]), i));
+      else {  // the true start is not a candidate: this segment serially
+        cur = xl_chain(s + kk * L, L, cur);
+        if (fallbacks && lane == 0) atomicAdd(fallbacks, 1u);
+      }
+    }
+    if (lane == 0) s_res = cur;
+  }
+  __syncthreads();
+  return s_res;
+}
+
+// the serial chain by the calling work-group: speculative where n splits into 2 NW segments of whole float4s
+template <int NW>
+__device__ __forceinline__ float xl_sumsq(const float* s, int n, float* s_out, bool serial) {
+  if (n % (8 * NW) == 0 && !serial) return xl_chain_spec<NW>(s, n);
+  if ((threadIdx.x >> 6) == 0) {
+    const float v = xl_chain(s, n);
+    if ((threadIdx.x & 63) == 0) *s_out = v;
+  }
+  __syncthreads();
+  return *s_out;
 }
 
 // The activation of one XL lane: per block b and slot jj, {q[4jj..4jj+3], q[16+4jj..16+4jj+3], -8 sum of the
@@ -108,7 +174,7 @@ __device__ __forceinline__ void xl_eat(const XlChunk& c, int g0, int ng, int jj,
   }
 }
 
-template <int NW, int ROLE>
+template <int NW, int ROLE, int XL_K4>  // XL_K4: PRE / GELU float4 of each operand per thread (n <= 4 XL_K4 T)
 __global__ __launch_bounds__(NW * 64) void exact_gemv_kernel(const uint4* __restrict__ wq, const uint2* __restrict__ wd,
                                                              int rows, int nb, XlArgs a) {
   extern __shared__ int4 s_dyn[];
@@ -133,52 +199,98 @@ __global__ __launch_bounds__(NW * 64) void exact_gemv_kernel(const uint4* __rest
   xl_load(ca, rq, rd, voq, vod, sq, sd, 0, ng);
   xl_load(cb, rq, rd, voq, vod, sq, sd, XL_P, ng);
 
-  // ---- the activation: XE entries + scales in LDS ----
+  // ---- the activation: XE entries + scales in LDS.  Every global operand a thread needs is loaded in one
+  // batch before any is used (a load per loop trip would pay one memory latency per trip) ----
   if constexpr (ROLE == XL_PLAIN) {
-    for (int i = t; i < nb * 4; i += T) {
-      const XBlock& xb = a.xb[i >> 2];
-      s_xe[i] = xe_entry(xb, i & 3);
-      if ((i & 3) == 0) s_xd[i >> 2] = xb.d;
+    const uint4* xg = reinterpret_cast<const uint4*>(a.xb);  // 3 uint4 per XBlock
+    for (int b0 = 0; b0 < nb; b0 += 4 * T) {
+      uint4 lo[4], hi[4];
+      float d[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int b = min(b0 + k * T + t, nb - 1);
+        lo[k] = xg[3 * b];
+        hi[k] = xg[3 * b + 1];
+        d[k] = __uint_as_float(xg[3 * b + 2].x);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int b = b0 + k * T + t;
+        if (b < nb) {
+          const uint32_t l4[4] = {lo[k].x, lo[k].y, lo[k].z, lo[k].w}, h4[4] = {hi[k].x, hi[k].y, hi[k].z, hi[k].w};
+#pragma unroll
+          for (int j = 0; j < 4; j++)
+            s_xe[b * 4 + j] = make_int4((int)l4[j], (int)h4[j], -8 * sdot4((int)l4[j], 0x01010101, 0),
+                                        -8 * sdot4((int)h4[j], 0x01010101, 0));
+          s_xd[b] = d[k];
+        }
+      }
     }
   } else {
-    const int n = a.n;
+    const int n = a.n, n4 = n >> 2;
     XBlock* s_xb = reinterpret_cast<XBlock*>(s_a);
+    float4* s_a4 = reinterpret_cast<float4*>(s_a);
+    float4* s_b4 = reinterpret_cast<float4*>(s_b);
     if constexpr (ROLE == XL_QUANT) {
-      for (int i = t; i < n; i += T) s_b[i] = a.y[i];
+      const float4* y4 = reinterpret_cast<const float4*>(a.y);
+      for (int i0 = 0; i0 < n4; i0 += 8 * T) {
+        float4 v[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) v[k] = y4[min(i0 + k * T + t, n4 - 1)];
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+          if (i0 + k * T + t < n4) s_b4[i0 + k * T + t] = v[k];
+      }
     } else {
+      // thread t owns float4 i = t + k T (k < XL_K4) of every operand
+      const float4* y4 = reinterpret_cast<const float4*>(a.y);
+      const float4* r4 = reinterpret_cast<const float4*>(a.resid_in);
+      const float4* wp4 = reinterpret_cast<const float4*>(a.w_post);
+      const float4* wn4 = reinterpret_cast<const float4*>(a.w_next);
+      float4 yv[XL_K4], hv[XL_K4], wv[XL_K4];
+#pragma unroll
+      for (int k = 0; k < XL_K4; k++) {
+        const int i = min(k * T + t, n4 - 1);
+        hv[k] = r4[i];
+        if (a.y) {
+          yv[k] = y4[i];
+          wv[k] = wp4[i];
+        }
+      }
+      auto own = [&](int k) { return k * T + t < n4; };
       if (a.y) {
-        for (int i = t; i < n; i += T) s_a[i] = a.y[i];
+#pragma unroll
+        for (int k = 0; k < XL_K4; k++)
+          if (own(k)) s_a4[k * T + t] = yv[k];
         __syncthreads();
-        if (wave == 0) {
-          const float sc = xl_rms_scale(xl_chain(s_a, n), n, a.eps);
-          if (lane == 0) s_scale[0] = sc;
-        }
-        __syncthreads();
-        const float sc1 = s_scale[0];
-        for (int i = t; i < n; i += T) {  // model.cpp:843-858: the post norm, then the residual add
-          const float h = a.resid_in[i] + (sc1 * s_a[i]) * a.w_post[i];
-          s_b[i] = h;
-          if (blockIdx.x == 0) a.resid_out[i] = h;
-        }
-      } else {
-        for (int i = t; i < n; i += T) {
-          const float h = a.resid_in[i];
-          s_b[i] = h;
-          if (blockIdx.x == 0 && a.resid_out != a.resid_in) a.resid_out[i] = h;
+        const float sc1 = xl_rms_scale(xl_sumsq<NW>(s_a, n, &s_scale[0], a.serial_norms), n, a.eps);
+#pragma unroll
+        for (int k = 0; k < XL_K4; k++) {  // model.cpp:843-858: the post norm, then the residual add
+          hv[k].x = hv[k].x + (sc1 * yv[k].x) * wv[k].x;
+          hv[k].y = hv[k].y + (sc1 * yv[k].y) * wv[k].y;
+          hv[k].z = hv[k].z + (sc1 * yv[k].z) * wv[k].z;
+          hv[k].w = hv[k].w + (sc1 * yv[k].w) * wv[k].w;
         }
       }
+#pragma unroll
+      for (int k = 0; k < XL_K4; k++) wv[k] = wn4[min(k * T + t, n4 - 1)];  // in flight behind the chain
+#pragma unroll
+      for (int k = 0; k < XL_K4; k++)
+        if (own(k)) {
+          s_b4[k * T + t] = hv[k];
+          if (blockIdx.x == 0 && (a.y || a.resid_out != a.resid_in))
+            reinterpret_cast<float4*>(a.resid_out)[k * T + t] = hv[k];
+        }
       __syncthreads();
-      if (wave == 0) {
-        const float sc = xl_rms_scale(xl_chain(s_b, n), n, a.eps);
-        if (lane == 0) s_scale[1] = sc;
-      }
-      __syncthreads();
-      const float sc2 = s_scale[1];
-      for (int i = t; i < n; i += T) {  // run_norm: (scale * x) * w (model.cpp:352-357)
-        const float x = (sc2 * s_b[i]) * a.w_next[i];
-        s_b[i] = x;
-        if (blockIdx.x == 0 && a.xn_out) a.xn_out[i] = x;
-      }
+      const float sc2 = xl_rms_scale(xl_sumsq<NW>(s_b, n, &s_scale[1], a.serial_norms), n, a.eps);
+#pragma unroll
+      for (int k = 0; k < XL_K4; k++)
+        if (own(k)) {  // run_norm: (scale * x) * w (model.cpp:352-357)
+          const float4 x = make_float4((sc2 * hv[k].x) * wv[k].x, (sc2 * hv[k].y) * wv[k].y,
+                                       (sc2 * hv[k].z) * wv[k].z, (sc2 * hv[k].w) * wv[k].w);
+          s_b4[k * T + t] = x;
+          if (blockIdx.x == 0 && a.xn_out) reinterpret_cast<float4*>(a.xn_out)[k * T + t] = x;
+        }
     }
     __syncthreads();
     // quantize_row_q8_0 (ops.cpp:116-139): a DPP quad per block
@@ -261,7 +373,284 @@ __global__ void xl_repack_kernel(const uint4* __restrict__ q0, const uint16_t* _
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// exact attention (exact.h)
+// ---------------------------------------------------------------------------
+// the q or k row of one head held by a wave: element i = lane + 64 k (EPL per lane); run_norm's serial chain
+// (ops.cpp:28-43) on the row staged in s_x, (scale * x) * w, then NEOX rope at pos (ops.cpp:67-95, the pinned
+// build's contractions: v0 c - v1 s and v0 s + v1 c as one fma each) -- pairs (i, i + HD / 2) sit in one lane
+template <int HD>
+__device__ __forceinline__ void xa_row(const float* __restrict__ src, const float* __restrict__ nw,
+                                       const float* __restrict__ cs, double eps, float* s_x, float (&r)[HD / 64]) {
+  constexpr int EPL = HD / 64, HALF = HD / 2;
+  const int lane = threadIdx.x & 63;
+  float v[EPL];
+#pragma unroll
+  for (int k = 0; k < EPL; k++) {
+    v[k] = src[lane + 64 * k];
+    s_x[lane + 64 * k] = v[k];
+  }
+  __syncthreads();
+  const float sc = xl_rms_scale(xl_chain(s_x, HD), HD, eps);
+  float nv[EPL];
+#pragma unroll
+  for (int k = 0; k < EPL; k++) nv[k] = (sc * v[k]) * nw[lane + 64 * k];
+#pragma unroll
+  for (int k = 0; k < EPL; k++) {
+    const int i = lane + 64 * k;
+    if (i < HALF) {
+      const int kp = k + EPL / 2;  // element i + HALF
+      const float c = cs[2 * i], sn = cs[2 * i + 1];
+      r[k] = fmaf(nv[k], c, -(nv[kp] * sn));
+      r[kp] = fmaf(nv[k], sn, nv[kp] * c);
+    }
+  }
+  __syncthreads();  // s_x reuse
+}
+
+template <int HD>
+__global__ __launch_bounds__(64) void xattn_scores_kernel(XAttnArgs a) {
+  constexpr int EPL = HD / 64;
+  __shared__ float s_x[HD];
+  __shared__ __attribute__((aligned(16))) double s_q[HD];
+  __shared__ __attribute__((aligned(16))) uint16_t s_k[HD];
+  const int h = blockIdx.x, split = blockIdx.y, lane = threadIdx.x;
+  const int pos = *a.d_pos, n_keys = pos + 1;
+  if (split * 64 >= n_keys) return;  // no key chunk for this work-group (whole wave)
+  const int hkv = h / (a.n_head / a.n_head_kv);
+  const float* cs = a.rope_cs + (size_t)pos * HD;
+  float r[EPL];
+  xa_row<HD>(a.qkv + (size_t)h * HD, a.q_norm_w, cs, a.eps, s_x, r);
+#pragma unroll
+  for (int k = 0; k < EPL; k++)  // model.cpp:767 scale, then the score's f16 query (model.cpp:507)
+    s_q[lane + 64 * k] = (double)h2f(f2h_ggml(r[k] * a.attn_scale));
+  const bool own_pos = (pos >> 6) % XA_NSPLIT == split;
+  if (own_pos) {  // the new key: k norm + rope, K and V rows appended (model.cpp:440-474)
+    xa_row<HD>(a.qkv + a.k_off + (size_t)hkv * HD, a.k_norm_w, cs, a.eps, s_x, r);
+    uint16_t* kc = a.k_cache + ((size_t)hkv * a.max_ctx + pos) * HD;
+    uint16_t* vc = a.v_cache + ((size_t)hkv * a.max_ctx + pos) * HD;
+    const float* vs = a.qkv + a.v_off + (size_t)hkv * HD;
+#pragma unroll
+    for (int k = 0; k < EPL; k++) {
+      const uint16_t kb = f2h_ggml(r[k]);
+      s_k[lane + 64 * k] = kb;
+      kc[lane + 64 * k] = kb;
+      vc[lane + 64 * k] = f2h_ggml(vs[lane + 64 * k]);
+    }
+  }
+  __syncthreads();
+  const uint16_t* kb = a.k_cache + (size_t)hkv * a.max_ctx * HD;
+  double* sc_out = a.scores + (size_t)h * a.max_ctx;
+  for (int c = split; c * 64 < n_keys; c += XA_NSPLIT) {
+    const int j = c * 64 + lane;
+    if (j >= n_keys) break;
+    const uint4* kr = reinterpret_cast<const uint4*>(j == pos ? s_k : kb + (size_t)j * HD);
+    double acc = 0.0;
+    // score += (double)(f16(k_i) * f16(q_i)), i in order (model.cpp:504-509); the f32 product of two f16 values
+    // is exact, so one f64 fma per element is the same rounding as the reference's add.  The row streams in
+    // batches of 64 elements, the next batch loaded before the current one is summed.
+    uint4 wa[8], wb[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) wa[u] = kr[u];
+    auto eat = [&](const uint4 (&w)[8], int i0) {
+      const double2* q2 = reinterpret_cast<const double2*>(s_q + i0 * 8);
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const uint32_t ww[4] = {w[u].x, w[u].y, w[u].z, w[u].w};
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+          const double2 q = q2[u * 4 + e];
+          acc = fma((double)h2f((uint16_t)(ww[e] & 0xFFFF)), q.x, acc);
+          acc = fma((double)h2f((uint16_t)(ww[e] >> 16)), q.y, acc);
+        }
+      }
+    };
+#pragma unroll 1
+    for (int i0 = 0; i0 < HD / 8; i0 += 16) {
+#pragma unroll
+      for (int u = 0; u < 8; u++) wb[u] = kr[i0 + 8 + u];
+      eat(wa, i0);
+      if (i0 + 16 < HD / 8) {
+#pragma unroll
+        for (int u = 0; u < 8; u++) wa[u] = kr[i0 + 16 + u];
+      }
+      eat(wb, i0 + 8);
+    }
+    sc_out[j] = acc;
+  }
+}
+
+constexpr int XA_CH = 1024;  // accum: keys per chunk in LDS
+
+template <int HD>
+__global__ __launch_bounds__((HD / 64 + 1) * 64) void xattn_accum_kernel(XAttnArgs a) {
+  constexpr int NWV = HD / 64, T = (NWV + 1) * 64;
+  constexpr int KPT = XA_CH / 256;  // keys per scan thread (threads 0..255)
+  __shared__ double s_sc[XA_CH];
+  __shared__ float2 s_ep[XA_CH];   // (e, pe) per key
+  __shared__ uint32_t s_up[XA_CH / 32];
+  __shared__ double s_tmax[256];
+  __shared__ float s_sacc;
+  const int h = blockIdx.x, t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  const int n_keys = *a.d_pos + 1;
+  const int hkv = h / (a.n_head / a.n_head_kv);
+  const uint16_t* vb = a.v_cache + (size_t)hkv * a.max_ctx * HD + wave * 64 + lane;
+  const double* sc_in = a.scores + (size_t)h * a.max_ctx;
+  double run_max = -INFINITY;
+  uint16_t v16 = 0;  // f32_to_f16(0.0f)
+  float s_acc = 0.0f;
+  for (int c0 = 0; c0 < n_keys; c0 += XA_CH) {
+    const int nk = min(XA_CH, n_keys - c0);
+    for (int i = t; i < nk; i += T) s_sc[i] = sc_in[c0 + i];
+    for (int i = t; i < XA_CH / 32; i += T) s_up[i] = 0u;
+    __syncthreads();
+    double tmax = -INFINITY;
+    if (t < 256) {
+#pragma unroll
+      for (int k = 0; k < KPT; k++) {
+        const int j = t * KPT + k;
+        if (j < nk) tmax = fmax(tmax, s_sc[j]);
+      }
+      s_tmax[t] = tmax;
+    }
+    __syncthreads();
+    for (int o = 1; o < 256; o <<= 1) {  // inclusive prefix max over the 256 segments (max is exact)
+      const double v = (t < 256 && t >= o) ? s_tmax[t - o] : -INFINITY;
+      __syncthreads();
+      if (t < 256) s_tmax[t] = fmax(s_tmax[t], v);
+      __syncthreads();
+    }
+    if (t < 256) {
+      double pm = fmax(run_max, t > 0 ? s_tmax[t - 1] : -INFINITY);  // max of every key before this segment
+#pragma unroll
+      for (int k = 0; k < KPT; k++) {
+        const int j = t * KPT + k;
+        if (j >= nk) break;
+        const double score = s_sc[j];
+        const float prev = (float)pm;  // the reference's max_score before key j
+        if (score > (double)prev) {    // model.cpp:520-532
+          s_ep[j] = make_float2(1.0f, llmi_glibc::expf(prev - (float)score));
+          atomicOr(&s_up[j >> 5], 1u << (j & 31));
+        } else {
+          s_ep[j] = make_float2(llmi_glibc::expf((float)(score - (double)prev)), 1.0f);
+        }
+        pm = fmax(pm, score);
+      }
+    }
+    run_max = fmax(run_max, s_tmax[255]);
+    __syncthreads();
+    if (wave < NWV) {  // this lane's head dim: vec_scale_f16 when the max moved, then vec_mad_f16 (ops.cpp:1084-1099)
+      const uint16_t* vp = vb + (size_t)c0 * HD;
+      // V of 32 keys per batch, the next batch's loads issued before this one is summed (clamped keys past the
+      // chunk are loaded but never summed)
+      uint16_t va[32], vn[32];
+#pragma unroll
+      for (int u = 0; u < 32; u++) va[u] = vp[(size_t)min(u, nk - 1) * HD];
+      for (int j0 = 0; j0 < nk; j0 += 32) {
+#pragma unroll
+        for (int u = 0; u < 32; u++) vn[u] = vp[(size_t)min(j0 + 32 + u, nk - 1) * HD];
+        const uint32_t up = s_up[j0 >> 5];
+        const int m = min(32, nk - j0);
+#pragma unroll
+        for (int u = 0; u < 32; u++) {
+          if (u < m) {
+            const float2 ep = s_ep[j0 + u];
+            // each result is rounded to f32 first, then to f16 (the asm fence keeps the compiler from fusing the
+            // pair into v_fma_mixlo_f16, one rounding: another f16 whenever the f32 rounding lands on a midpoint)
+            if (up & (1u << u)) {
+              float sv = (float)__builtin_bit_cast(_Float16, v16) * ep.y;
+              asm volatile("" : "+v"(sv));
+              v16 = f2h(sv);
+            }
+            float nv = fmaf((float)__builtin_bit_cast(_Float16, va[u]), ep.x, (float)__builtin_bit_cast(_Float16, v16));
+            asm volatile("" : "+v"(nv));
+            v16 = f2h(nv);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 32; u++) va[u] = vn[u];
+      }
+    } else {  // s_acc = s_acc * pe + e, keys in order (model.cpp:540)
+      for (int j = 0; j < nk; j++) {
+        const float2 ep = s_ep[j];
+        s_acc = s_acc * ep.y + ep.x;
+      }
+    }
+    __syncthreads();  // the chunk's LDS is reused by the next one
+  }
+  if (wave == NWV && lane == 0) s_sacc = s_acc == 0.0f ? 0.0f : 1.0f / s_acc;
+  __syncthreads();
+  if (wave < NWV) {
+    const int d = wave * 64 + lane;
+    const float o = h2f(v16) * s_sacc;  // model.cpp:543-547
+    a.out[(size_t)h * HD + d] = o;
+    q8_block_store(o, true, a.xq + ((size_t)h * HD + wave * 64) / 32 + (lane >> 5), lane & 31);
+  }
+}
+
+// every f32 bit pattern: the hardware f32 -> f16 conversion (round to nearest even) against the reference's
+// f32_to_f16 (gguf.cpp:68-95, f2h_ggml) -- the exact attention's accumulator chain uses the hardware one
+__global__ void f16_selftest_kernel(unsigned long long* out) {
+  const uint64_t n = 1ull << 32;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const float f = __uint_as_float((uint32_t)i);
+    const uint16_t hw = f2h(f), sw = f2h_ggml(f);
+    if (hw != sw) {
+      const bool nan = f != f;
+      atomicAdd(out + (nan ? 1 : 0), 1ull);
+      if (!nan) atomicMin(out + 2, (unsigned long long)i);
+    }
+  }
+}
+
+// speculative chain vs the serial one: work-group g fills n = 2560 floats from a hash of (g, i) with a
+// per-group scale and a sprinkling of large values (wide dynamic range: fallbacks happen), out[0] += mismatches,
+// out[1] += fallback segments
+__global__ __launch_bounds__(256) void chain_selftest_kernel(unsigned* out) {
+  __shared__ __attribute__((aligned(16))) float s[2560];
+  __shared__ float s_ref;
+  const int g = blockIdx.x;
+  const float scale = exp2f((float)((g * 37) % 41) - 20.0f);
+  for (int i = threadIdx.x; i < 2560; i += 256) {
+    uint32_t h = (uint32_t)(g * 2654435761u) ^ (uint32_t)(i * 2246822519u);
+    h ^= h >> 15; h *= 0x2c1b3c6du; h ^= h >> 12; h *= 0x297a2d39u; h ^= h >> 15;
+    float v = ((float)(h & 0xFFFFFF) / 16777216.0f - 0.5f) * scale;
+    if ((h >> 24) == 0x7F && (g & 3) == 0) v *= 4096.0f;  // rare large terms: the chain jumps past the window
+    s[i] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const float r = xl_chain(s, 2560);
+    if (threadIdx.x == 0) s_ref = r;
+  }
+  __syncthreads();
+  const float v = xl_chain_spec<4>(s, 2560, out + 1);
+  if (threadIdx.x == 0 && __float_as_uint(v) != __float_as_uint(s_ref)) atomicAdd(out, 1u);
+}
+
 }  // namespace
+
+void exact_selftest_chain(unsigned* host_out2) {
+  unsigned* d = nullptr;
+  LLMI_HIP(hipMalloc(&d, 8));
+  LLMI_HIP(hipMemset(d, 0, 8));
+  hipLaunchKernelGGL(chain_selftest_kernel, dim3(8192), dim3(256), 0, 0, d);
+  LLMI_HIP(hipGetLastError());
+  LLMI_HIP(hipMemcpy(host_out2, d, 8, hipMemcpyDeviceToHost));
+  LLMI_HIP(hipFree(d));
+}
+
+void exact_selftest_f16(unsigned long long* host_out3) {
+  unsigned long long* d = nullptr;
+  LLMI_HIP(hipMalloc(&d, 24));
+  const unsigned long long init[3] = {0, 0, ~0ull};
+  LLMI_HIP(hipMemcpy(d, init, 24, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(f16_selftest_kernel, dim3(4096), dim3(256), 0, 0, d);
+  LLMI_HIP(hipGetLastError());
+  LLMI_HIP(hipMemcpy(host_out3, d, 24, hipMemcpyDeviceToHost));
+  LLMI_HIP(hipFree(d));
+}
 
 bool xl_supported(const DevWeight& w) {
   return w.type == T_Q4_0 && !w.slab && w.cols % 128 == 0 && w.rows > 0;
@@ -302,10 +691,31 @@ void free_xl_weight(XlWeight& w) {
   w = XlWeight{};
 }
 
-void launch_exact_gemv(const XlWeight& w, const XlArgs& a, int role, hipStream_t s) {
+bool exact_attn_supported(int head_dim, int n_head, int n_head_kv) {
+  return (head_dim == 256 || head_dim == 128) && n_head_kv > 0 && n_head % n_head_kv == 0;
+}
+
+void launch_exact_attn(const XAttnArgs& a, hipStream_t s) {
+  if (!exact_attn_supported(a.head_dim, a.n_head, a.n_head_kv) || !a.scores || !a.xq)
+    throw std::runtime_error("exact attention: unsupported shape");
+  if (a.head_dim == 256) {
+    hipLaunchKernelGGL(xattn_scores_kernel<256>, dim3(a.n_head, XA_NSPLIT), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(xattn_accum_kernel<256>, dim3(a.n_head), dim3(320), 0, s, a);
+  } else {
+    hipLaunchKernelGGL(xattn_scores_kernel<128>, dim3(a.n_head, XA_NSPLIT), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(xattn_accum_kernel<128>, dim3(a.n_head), dim3(192), 0, s, a);
+  }
+  LLMI_HIP(hipGetLastError());
+}
+
+void launch_exact_gemv(const XlWeight& w, const XlArgs& a_in, int role, hipStream_t s) {
+  static const bool serial = getenv("LLMI_EXACT_SERIAL_NORMS") != nullptr;  // A/B: the chains without speculation
+  XlArgs a = a_in;
+  a.serial_norms = serial ? 1 : 0;
   if (!w.qs || w.nb % 4 || w.rows % 16) throw std::runtime_error("exact gemv: bad weight");
   if (role != XL_PLAIN && a.n != w.nb * 32) throw std::runtime_error("exact gemv: input length != cols");
   if (role == XL_GELU && w.rows % 64) throw std::runtime_error("exact gemv: GELU rows % 64 != 0");
+  if ((role == XL_PRE || role == XL_GELU) && a.n > 24 * 256) throw std::runtime_error("exact gemv: n > 6144");
   const size_t xe = (size_t)w.nb * 64 + (size_t)w.nb * 4;
   const size_t lds = xe + (role == XL_PLAIN ? 0 : (size_t)2 * a.n * 4);
   if (lds > 64 * 1024) throw std::runtime_error("exact gemv: activation exceeds LDS");
@@ -313,11 +723,20 @@ void launch_exact_gemv(const XlWeight& w, const XlArgs& a, int role, hipStream_t
     const unsigned grid = (unsigned)((w.rows + 16 * nw - 1) / (16 * nw));
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * nw), lds, s, w.qs, w.d, w.rows, w.nb, a);
   };
+  // PRE / GELU: each thread holds 4 XL_K4 elements of the residual-step operands in registers
+  const bool k3_2 = a.n <= 12 * 128, k3_4 = a.n <= 12 * 256;
   switch (role) {
-    case XL_PLAIN: go(exact_gemv_kernel<1, XL_PLAIN>, 1); break;
-    case XL_QUANT: go(exact_gemv_kernel<1, XL_QUANT>, 1); break;
-    case XL_PRE: go(exact_gemv_kernel<2, XL_PRE>, 2); break;
-    case XL_GELU: go(exact_gemv_kernel<4, XL_GELU>, 4); break;
+    case XL_PLAIN: go(exact_gemv_kernel<1, XL_PLAIN, 1>, 1); break;
+    case XL_QUANT: go(exact_gemv_kernel<1, XL_QUANT, 1>, 1); break;
+    case XL_PRE:
+      if (k3_2) go(exact_gemv_kernel<2, XL_PRE, 3>, 2);
+      else if (k3_4) go(exact_gemv_kernel<4, XL_PRE, 3>, 4);
+      else go(exact_gemv_kernel<4, XL_PRE, 6>, 4);
+      break;
+    case XL_GELU:
+      if (k3_4) go(exact_gemv_kernel<4, XL_GELU, 3>, 4);
+      else go(exact_gemv_kernel<4, XL_GELU, 6>, 4);
+      break;
     default: throw std::runtime_error("exact gemv: bad role");
   }
   LLMI_HIP(hipGetLastError());

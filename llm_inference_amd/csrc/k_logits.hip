@@ -252,6 +252,71 @@ __global__ __launch_bounds__(256) void screen_rescore_kernel(const uint4* __rest
   if (lane == 0 && best) atomicMax(amax_key, best);
 }
 
+// Exact-order rescoring (exact mode): every candidate row recomputed as the reference's AVX2
+// mat_vec_mul_fp16 (ops.cpp:552-585) computes it -- 4 lanes per row, lane l = accumulator register sum[l]
+// (8 fp32 lanes m), the 32-element chunks in order, then (S0 + S1) + (S2 + S3), t_m = V_m + V_m+4,
+// (t0 + t1) + (t2 + t3) and the serial tail -- so the argmax is the reference's own (the screening bound holds
+// for any summation order).  A work-group's 64 candidate slots at a time, chunks loaded 16 ahead.
+__global__ __launch_bounds__(256) void screen_rescore_exact_kernel(const uint16_t* __restrict__ w, int rows, int cols,
+                                                                   const uint16_t* __restrict__ x16,
+                                                                   const float* __restrict__ hi,
+                                                                   const unsigned* __restrict__ m_key, int slice,
+                                                                   unsigned long long* __restrict__ amax_key) {
+  extern __shared__ int s_cand[];  // [slice]
+  __shared__ int s_n;
+  const int t = threadIdx.x;
+  if (t == 0) s_n = 0;
+  __syncthreads();
+  const float M = fkey_inv(*m_key);
+  const int r0 = blockIdx.x * slice, r1 = min(rows, r0 + slice);
+  for (int r = r0 + t; r < r1; r += 256)
+    if (hi[r] >= M) s_cand[atomicAdd(&s_n, 1)] = r;
+  __syncthreads();
+  const int n = s_n;
+  const int np = cols & ~31, l = t & 3;
+  unsigned long long best = 0;
+  for (int c0 = 0; c0 < n; c0 += 64) {
+    const int ci = c0 + (t >> 2);
+    const bool ok = ci < n;
+    const int row = ok ? s_cand[ci] : s_cand[0];
+    const uint16_t* wr = w + (size_t)row * cols;
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int k0 = 0; k0 < np; k0 += 32 * 16) {
+      uint4 wv[16], xv[16];
+#pragma unroll
+      for (int u = 0; u < 16; u++) {
+        const int k = min(k0 + 32 * u, np - 32);
+        wv[u] = *reinterpret_cast<const uint4*>(wr + k + 8 * l);
+        xv[u] = *reinterpret_cast<const uint4*>(x16 + k + 8 * l);
+      }
+#pragma unroll
+      for (int u = 0; u < 16; u++) {
+        if (k0 + 32 * u >= np) break;
+        const uint32_t ww[4] = {wv[u].x, wv[u].y, wv[u].z, wv[u].w}, xx[4] = {xv[u].x, xv[u].y, xv[u].z, xv[u].w};
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+          acc[2 * e] = fmaf(h2f((uint16_t)(ww[e] & 0xFFFF)), h2f((uint16_t)(xx[e] & 0xFFFF)), acc[2 * e]);
+          acc[2 * e + 1] = fmaf(h2f((uint16_t)(ww[e] >> 16)), h2f((uint16_t)(xx[e] >> 16)), acc[2 * e + 1]);
+        }
+      }
+    }
+    float v[8];
+#pragma unroll
+    for (int m = 0; m < 8; m++) {
+      const float a = acc[m] + __shfl_xor(acc[m], 1);  // l0: S0 + S1, l2: S2 + S3
+      v[m] = a + __shfl_xor(a, 2);                     // l0: (S0 + S1) + (S2 + S3)
+    }
+    if (ok && l == 0) {
+      const float t0 = v[0] + v[4], t1 = v[1] + v[5], t2 = v[2] + v[6], t3 = v[3] + v[7];
+      float r = (t0 + t1) + (t2 + t3);
+      for (int k = np; k < cols; k++) r = fmaf(h2f(wr[k]), h2f(x16[k]), r);
+      const unsigned long long key = argmax_key(r, (uint32_t)row);
+      best = key > best ? key : best;
+    }
+  }
+  if (best) atomicMax(amax_key, best);  // a few candidate lanes per launch
+}
+
 constexpr int RESCORE_SLICE = 1024;
 
 }  // namespace
@@ -287,7 +352,7 @@ void free_screen_table(ScreenTable& st) {
 }
 
 void launch_screen_argmax(const DevWeight& table, const ScreenTable& st, const uint16_t* x16,
-                          unsigned long long* amax_key, hipStream_t s, bool prepped) {
+                          unsigned long long* amax_key, hipStream_t s, bool prepped, bool exact) {
   if (table.rows != st.rows || table.cols != st.cols) throw std::runtime_error("screen: table mismatch");
   if (!screen_supported(table)) throw std::runtime_error("screen: unsupported logits table");
   const int n = table.cols, nb = n / 32;
@@ -321,6 +386,12 @@ void launch_screen_argmax(const DevWeight& table, const ScreenTable& st, const u
   const int u4 = n / 8, P = u4 / 64, T = u4 % 64;
   const dim3 rg((rows + RESCORE_SLICE - 1) / RESCORE_SLICE);
   const size_t lds = RESCORE_SLICE * sizeof(int);
+  if (exact) {
+    hipLaunchKernelGGL(screen_rescore_exact_kernel, rg, dim3(256), lds, s, reinterpret_cast<const uint16_t*>(table.qs),
+                       rows, n, x16, st.hi, st.m_key, RESCORE_SLICE, amax_key);
+    LLMI_HIP(hipGetLastError());
+    return;
+  }
   switch (P * 4 + T / 16) {
 #define LLMI_RSC(PP, TT)                                                                                          \
   case PP * 4 + TT / 16:                                                                                          \

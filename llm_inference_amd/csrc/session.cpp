@@ -609,7 +609,9 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
     // greedy token ids by screening (k_logits.hip): the fast F16 logits path
     // (a tensor-parallel rank screens its vocabulary shard; the keys meet in
     // finalize as before); LLMI_FULL_LOGITS=1 keeps the full GEMV in the loop
-    screen_ = !ex_logits_ && embd_.type == T_F16 && logits_w_.type == T_F16 && screen_supported(logits_w_) &&
+    // exact mode: the same screening with the candidates rescored in the reference's order (the exact-order
+    // engine; LLMI_EXACT_PARTS / per-op exact kernels keep the full exact GEMV)
+    screen_ = (!ex_logits_ || (xl_ && getenv("LLMI_EXACT_SCREEN"))) && embd_.type == T_F16 && logits_w_.type == T_F16 && screen_supported(logits_w_) &&
               hp_.final_softcap <= 0.0f &&
               getenv("LLMI_FULL_LOGITS") == nullptr;
     if (screen_) alloc_screen_table(logits_w_, scr_, stream_);
@@ -830,7 +832,7 @@ void Session::record_logits(hipStream_t s, bool gen) {
   float* lg = logits_ + (size_t)tp_rank_ * v_sh_;
   unsigned long long* key = amax_key_ + tp_rank_;
   if (gen && screen_) {  // token id only: int8 screening + exact rescoring of the candidates
-    launch_screen_argmax(logits_w_, scr_, act_.x16, key, s, scr_prepped_);
+    launch_screen_argmax(logits_w_, scr_, act_.x16, key, s, scr_prepped_, ex_logits_);
     kernels_per_token_ += scr_prepped_ ? 2 : 3;
     tap("x16", -1, act_.x16, (size_t)E * 2, s);
   } else {
@@ -1499,7 +1501,8 @@ void Session::setup_xl() {
     if (atoi(e) == 0) return;
   if (hp_.n_embd % 128 || hp_.n_ff % 128 || 2 * (size_t)hp_.n_embd * 4 + hp_.n_embd / 32 * 68 > 60 * 1024) return;
   for (const auto& l : L_) {
-    bool ok = l.has_kv && !l.qkv.empty() && !l.gate_up.empty() && (hp_.n_head * l.hd) % 128 == 0;
+    bool ok = l.has_kv && !l.qkv.empty() && !l.gate_up.empty() && (hp_.n_head * l.hd) % 128 == 0 &&
+              exact_attn_supported(l.hd, hp_.n_head, hp_.n_head_kv);
     for (const auto& p : l.qkv) ok = ok && xl_supported(p.w);
     for (const auto& p : l.gate_up) ok = ok && xl_supported(p.w);
     int gu_rows = 0;
@@ -1536,6 +1539,10 @@ void Session::setup_xl() {
     d.w[d.n++] = &l.down.w;
     l.xdn = make_xl_weight(d, stream_);
   }
+  int maxhd = 0;
+  for (const auto& l : L_) maxhd = std::max(maxhd, l.hd);
+  xa_scores_ = dalloc<double>((size_t)hp_.n_head * max_ctx_);
+  xa_xq_ = dalloc<XBlock>((size_t)hp_.n_head * maxhd / 32);
   LLMI_HIP(hipStreamSynchronize(stream_));
   xl_ = true;
 }
@@ -1568,16 +1575,30 @@ void Session::record_layers_xl(hipStream_t s) {
       launch_exact_gemv(Ld.xqkv, q, XL_PRE, s);
       std::swap(ra, rb);
     }
-    QKVArgs qa{qkv_, Ld.k_off, Ld.v_off, hp_.n_head, hp_.n_head_kv, hd, Ld.q_norm, Ld.k_norm,
-               Ld.is_swa ? rope_swa_ : rope_glb_, hp_.attn_scale, hp_.eps, q_, Ld.kc, Ld.vc, max_ctx_, d_pos_};
-    launch_qk_norm_rope_kv(qa, true, s);
-    AttnArgs aa{q_, Ld.kc, Ld.vc, hp_.n_head, hp_.n_head_kv, hd, max_ctx_, d_pos_, part_, attn_, ticket_, nullptr};
-    launch_attention(aa, true, s);
+    XAttnArgs xa;
+    xa.qkv = qkv_;
+    xa.k_off = Ld.k_off;
+    xa.v_off = Ld.v_off;
+    xa.n_head = hp_.n_head;
+    xa.n_head_kv = hp_.n_head_kv;
+    xa.head_dim = hd;
+    xa.q_norm_w = Ld.q_norm;
+    xa.k_norm_w = Ld.k_norm;
+    xa.rope_cs = Ld.is_swa ? rope_swa_ : rope_glb_;
+    xa.attn_scale = hp_.attn_scale;
+    xa.eps = hp_.eps;
+    xa.k_cache = Ld.kc;
+    xa.v_cache = Ld.vc;
+    xa.max_ctx = max_ctx_;
+    xa.d_pos = d_pos_;
+    xa.scores = xa_scores_;
+    xa.out = attn_;
+    xa.xq = xa_xq_;
+    launch_exact_attn(xa, s);
     XlArgs o;
-    o.y = attn_;
-    o.n = hp_.n_head * hd;
+    o.xb = xa_xq_;
     o.out = o_out_;
-    launch_exact_gemv(Ld.xo, o, XL_QUANT, s);
+    launch_exact_gemv(Ld.xo, o, XL_PLAIN, s);
     XlArgs gu;
     gu.y = o_out_;
     gu.w_post = Ld.post_attn_norm;
@@ -1999,7 +2020,7 @@ void Session::time_kernel(int which, int reps, double* us, double* bytes) {
     LLMI_HIP(hipStreamSynchronize(stream_));
     for (int r = 0; r < reps; r++) {
       LLMI_HIP(hipEventRecord(ev[2 * r], stream_));
-      launch_screen_argmax(logits_w_, scr_, act_.x16, amax_key_, stream_);
+      launch_screen_argmax(logits_w_, scr_, act_.x16, amax_key_, stream_, false, ex_logits_);
       LLMI_HIP(hipEventRecord(ev[2 * r + 1], stream_));
     }
     LLMI_HIP(hipStreamSynchronize(stream_));

@@ -103,6 +103,8 @@ class Session {
   void record_layers_fused(hipStream_t s, bool x_q8);
   // exact mode on the exact-order engine (k_exact.hip): Q4_0 Gemma-3 layers, reference arithmetic, streamed
   bool xl_ = false;
+  double* xa_scores_ = nullptr;  // exact attention scores [n_head][max_ctx]
+  XBlock* xa_xq_ = nullptr;      // exact attention output's Q8_0 blocks (the o projection's x)
   void setup_xl();
   void record_layers_xl(hipStream_t s);
   void setup_engine(const GGUFView& g);

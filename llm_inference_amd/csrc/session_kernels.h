@@ -239,8 +239,9 @@ bool screen_supported(const DevWeight& table);
 void alloc_screen_table(const DevWeight& table, ScreenTable& st, hipStream_t s);
 void free_screen_table(ScreenTable& st);
 // prepped: st.xs / st.m_key already hold this token's x16 blocks (a norm with NormOut::scr wrote them)
+// exact: the candidates are rescored in the reference's AVX2 order (gemv_f16_exact) instead of the fast GEMV's
 void launch_screen_argmax(const DevWeight& table, const ScreenTable& st, const uint16_t* x16,
-                          unsigned long long* amax_key, hipStream_t s, bool prepped = false);
+                          unsigned long long* amax_key, hipStream_t s, bool prepped = false, bool exact = false);
 
 // ---- the screening's x16 blocks (k_logits.hip step 1), shared by screen_prep_kernel and norm_outputs ----
 constexpr float SCREEN_DENORM = 6.103515625e-05f;  // 2^-14: smallest normal f16

@@ -197,3 +197,30 @@ def test_gemv_q5_0_fast_vs_oracle(ops, oracle, rows, cols):
     np.testing.assert_array_equal(bits(ops.mat_vec_mul_raw(T.Q5_0, w, rows, cols, x, exact=True)), bits(ref))
     o = ops.mat_vec_mul_raw(T.Q5_0, w, rows, cols, x, exact=False)
     assert np.abs(o - ref).max() <= 1e-4 * np.abs(ref).max() + 1e-6
+
+
+@pytest.mark.gpu
+def test_f16_conversion_selftest():
+    """The exact attention's f16 V accumulator (k_exact.hip) rounds with the hardware f32 -> f16 conversion:
+    over every one of the 2^32 f32 bit patterns it must equal the reference's f32_to_f16 (gguf.cpp:68-95) for
+    every non-NaN input."""
+    import ctypes as C
+    from llm_inference_amd._lib import check, lib
+    out = (C.c_ulonglong * 3)()
+    check(lib().llmi_selftest(0, C.cast(out, C.c_void_p)))
+    print(f"f32->f16: non-NaN mismatches {out[0]}, NaN mismatches {out[1]}")
+    assert out[0] == 0, f"first mismatching f32 bits 0x{out[2]:08x}"
+
+
+@pytest.mark.gpu
+def test_speculative_chain_selftest():
+    """The exact engine's rms_norm chain (ops.cpp:33-36: sum = fma(x, x, sum) serially) runs speculatively
+    (k_exact.hip xl_chain_spec): its result must equal the serial chain's bits on every vector, including
+    vectors whose large terms push the true start of a segment outside the candidate window (serial fallback)."""
+    import ctypes as C
+    from llm_inference_amd._lib import check, lib
+    out = (C.c_ulonglong * 3)()
+    check(lib().llmi_selftest(1, C.cast(out, C.c_void_p)))
+    print(f"speculative chain: {out[0]} mismatches, {out[1]} fallback segments over 8192 x 7 boundaries")
+    assert out[0] == 0
+    assert out[1] > 0  # the fallback path ran

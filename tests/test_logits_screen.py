@@ -25,11 +25,18 @@ def _embd(g, cfg):
     return g[s:s + t.nbytes].view(np.float16).reshape(cfg.vocab, cfg.n_embd)
 
 
-def _pair(g, monkeypatch, max_ctx=256):
+@pytest.fixture(params=[False, True], ids=["fast", "exact"])
+def exact(request):
+    """fast: rescoring in the fast F16 GEMV's order; exact (the exact-order engine): in the reference's AVX2
+    order (ops.cpp:552-585), against the full exact F16 GEMV + argmax."""
+    return request.param
+
+
+def _pair(g, monkeypatch, max_ctx=256, exact=False):
     from llm_inference_amd.model import Model
-    scr = Model(g, max_ctx=max_ctx)
+    scr = Model(g, max_ctx=max_ctx, exact=exact)
     monkeypatch.setenv("LLMI_FULL_LOGITS", "1")
-    full = Model(g, max_ctx=max_ctx)
+    full = Model(g, max_ctx=max_ctx, exact=exact)
     monkeypatch.delenv("LLMI_FULL_LOGITS")
     assert scr.get_info().screened_logits == 1
     assert full.get_info().screened_logits == 0
@@ -49,30 +56,30 @@ def _run(scr, full, cfg, seed, n=48):
 
 
 @pytest.mark.parametrize("cfg_name", ["mini-1b", "mini-4b"])
-def test_screen_ids_match_full_logits(cfg_name, monkeypatch):
+def test_screen_ids_match_full_logits(cfg_name, monkeypatch, exact):
     from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
     cfg = CONFIGS[cfg_name]
     g = build_gemma3_gguf(cfg, seed=13)
-    scr, full = _pair(g, monkeypatch)
+    scr, full = _pair(g, monkeypatch, exact=exact)
     _run(scr, full, cfg, 2, n=64)
     # the screened step's two launches (screening GEMV, rescoring; its prep runs in the final norm launch) replace
     # the one F16 GEMV launch, and its token feedback carries the next step's embed_norm (one launch fewer)
     assert scr.get_info().kernels_per_token == full.get_info().kernels_per_token
 
 
-def test_screen_ties_first_index(monkeypatch):
+def test_screen_ties_first_index(monkeypatch, exact):
     from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
     cfg = CONFIGS["mini-4b"]
     g = build_gemma3_gguf(cfg, seed=17)
     e = _embd(g, cfg)
     h = cfg.vocab // 2
     e[h:2 * h] = e[:h]  # every row has an exact twin V/2 later
-    scr, full = _pair(g, monkeypatch)
+    scr, full = _pair(g, monkeypatch, exact=exact)
     ids = _run(scr, full, cfg, 5)
     assert (ids < h).all()  # the lower index of each tied pair
 
 
-def test_screen_near_ties(monkeypatch):
+def test_screen_near_ties(monkeypatch, exact):
     from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
     cfg = CONFIGS["mini-1b"]
     g = build_gemma3_gguf(cfg, seed=19)
@@ -82,7 +89,7 @@ def test_screen_near_ties(monkeypatch):
     bits = e[h:2 * h].view(np.uint16)
     col = np.random.default_rng(1).integers(0, cfg.n_embd, h)
     bits[np.arange(h), col] += np.uint16(1)  # one f16 ulp in one column of each twin
-    scr, full = _pair(g, monkeypatch)
+    scr, full = _pair(g, monkeypatch, exact=exact)
     _run(scr, full, cfg, 7)
 
 
