@@ -609,9 +609,8 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
     // greedy token ids by screening (k_logits.hip): the fast F16 logits path
     // (a tensor-parallel rank screens its vocabulary shard; the keys meet in
     // finalize as before); LLMI_FULL_LOGITS=1 keeps the full GEMV in the loop
-    // exact mode: the same screening with the candidates rescored in the reference's order (the exact-order
-    // engine; LLMI_EXACT_PARTS / per-op exact kernels keep the full exact GEMV)
-    screen_ = (!ex_logits_ || (xl_ && getenv("LLMI_EXACT_SCREEN"))) && embd_.type == T_F16 && logits_w_.type == T_F16 && screen_supported(logits_w_) &&
+    // exact mode: the same screening, the candidates rescored in the reference's order
+    screen_ = embd_.type == T_F16 && logits_w_.type == T_F16 && screen_supported(logits_w_) &&
               hp_.final_softcap <= 0.0f &&
               getenv("LLMI_FULL_LOGITS") == nullptr;
     if (screen_) alloc_screen_table(logits_w_, scr_, stream_);
@@ -809,7 +808,7 @@ void Session::record_step(hipStream_t s, bool gen, bool fold_embed) {
   bool fused = fuse_layers_;
   for (const auto& l : L_) fused &= l.fused;
   if (tp_ && !fused) throw status_error(LLMI_E_ARG, "tensor parallel needs the fused layer path");
-  if (xl_ && !dump_ && !trace_fn_ && x_q8 && x_blocks == (const void*)act_.q8.xb) {
+  if (xl_ && !dump_ && !(trace_fn_ && getenv("LLMI_TRACE_PER_OP")) && x_q8 && x_blocks == (const void*)act_.q8.xb) {
     record_layers_xl(s);
   } else if (fused && engine_ && !dump_ && !trace_fn_) {
     record_layers_engine(s, x_q8);
@@ -846,7 +845,7 @@ void Session::record_logits(hipStream_t s, bool gen) {
     dump("result_output", lg, v_rows_, s);  // model.cpp:1046
     tap("logits", -1, lg, (size_t)v_rows_ * 4, s);
   }
-  if (!fold) {
+  if (!fold && !(gen && screen_)) {  // (the screened selection folds its own key; logits_ is stale then)
     launch_argmax(lg, v_rows_, key, s);
     kernels_per_token_++;
   }

@@ -14,6 +14,7 @@ from llm_inference_amd.gguf import GGUFFile, TensorType  # noqa: E402
 from llm_inference_amd.model import Model  # noqa: E402
 from oracle.bind import Oracle  # noqa: E402
 
+os.environ["LLMI_EXACT_SCREEN"] = "1"
 cfg, g, f = _fixture("g1b")
 prompt, toks = f["prompt"], f["tokens"]
 m = Model(g, exact=True, max_ctx=64)
@@ -27,6 +28,8 @@ if d is not None:
     for i in range(d - 1):
         m2.forward([int(toks[i])], len(prompt) + i)
     tr = m2.trace([int(toks[d - 1])], len(prompt) + d - 1, gen=True)
+    names = sorted(set(n for (n, l, b) in tr))
+    print("taps", names)
     x16 = [b for (n, l, b) in tr if n == "x16"][-1]
     tok = [b for (n, l, b) in tr if n == "token"][-1]
     x = np.frombuffer(x16, np.float16).astype(np.float32)

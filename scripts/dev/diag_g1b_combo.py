@@ -10,6 +10,7 @@ from test_full_models import _fixture  # noqa: E402
 
 from llm_inference_amd.model import Model  # noqa: E402
 
+os.environ["LLMI_EXACT_SCREEN"] = "1"
 cfg, g, f = _fixture("g1b")
 prompt, toks = f["prompt"], f["tokens"]
 for env in ({}, {"LLMI_NO_EMBED_FOLD": "1"}, {"LLMI_EXACT_XL": "0"}, {"LLMI_SCREEN_PREP": "1"},

@@ -63,8 +63,9 @@ def test_screen_ids_match_full_logits(cfg_name, monkeypatch, exact):
     scr, full = _pair(g, monkeypatch, exact=exact)
     _run(scr, full, cfg, 2, n=64)
     # the screened step's two launches (screening GEMV, rescoring; its prep runs in the final norm launch) replace
-    # the one F16 GEMV launch, and its token feedback carries the next step's embed_norm (one launch fewer)
-    assert scr.get_info().kernels_per_token == full.get_info().kernels_per_token
+    # the one F16 GEMV launch (exact mode: the exact GEMV and its argmax launch), and its token feedback carries
+    # the next step's embed_norm (one launch fewer)
+    assert scr.get_info().kernels_per_token == full.get_info().kernels_per_token - (1 if exact else 0)
 
 
 def test_screen_ties_first_index(monkeypatch, exact):
