@@ -13,6 +13,18 @@ namespace {
 
 constexpr int XL_P = 8;   // groups (4 blocks each) per chunk of loads
 
+#ifdef XL_TRACE  // development (scripts/dev/xl_bench.hip): per-work-group phase clocks of the last launch
+__device__ unsigned long long g_xl_trace[8192 * 8];
+#define XL_MARK(ph)                                                                                          \
+  do {                                                                                                       \
+    if (threadIdx.x == 0 && blockIdx.x < 8192) g_xl_trace[blockIdx.x * 8 + (ph)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define XL_MARK(ph) \
+  do {              \
+  } while (0)
+#endif
+
 __device__ __forceinline__ float xl_rms_scale(float sum, int n, double eps) {  // ops.cpp:37-38
   return 1.0f / sqrtf((float)((double)(sum / (float)n) + eps));
 }
@@ -115,6 +127,9 @@ __device__ __forceinline__ float xl_chain_spec(const float* s, int n, unsigned* 
 // the serial chain by the calling work-group: speculative where n splits into 2 NW segments of whole float4s
 template <int NW>
 __device__ __forceinline__ float xl_sumsq(const float* s, int n, float* s_out, bool serial) {
+#ifdef XL_DIAG_NOCHAIN  // development timing build (results wrong): the chains left out
+  return (float)n;
+#endif
   if (n % (8 * NW) == 0 && !serial) return xl_chain_spec<NW>(s, n);
   if ((threadIdx.x >> 6) == 0) {
     const float v = xl_chain(s, n);
@@ -174,7 +189,8 @@ __device__ __forceinline__ void xl_eat(const XlChunk& c, int g0, int ng, int jj,
   }
 }
 
-template <int NW, int ROLE, int XL_K4>  // XL_K4: PRE / GELU float4 of each operand per thread (n <= 4 XL_K4 T)
+// XL_K4: PRE / GELU float4 of each operand per thread (n <= 4 XL_K4 T); NCH: chunks of XL_P groups in flight
+template <int NW, int ROLE, int XL_K4, int NCH>
 __global__ __launch_bounds__(NW * 64) void exact_gemv_kernel(const uint4* __restrict__ wq, const uint2* __restrict__ wd,
                                                              int rows, int nb, XlArgs a) {
   extern __shared__ int4 s_dyn[];
@@ -195,9 +211,10 @@ __global__ __launch_bounds__(NW * 64) void exact_gemv_kernel(const uint4* __rest
   const bool row_ok = row < rows;
   const int voq = row_ok ? (row * 4 + jj) * 16 : (1 << 30), vod = row_ok ? row * 8 : (1 << 30);
   const int sq = rows * 64, sd = rows * 8;
-  XlChunk ca, cb;
-  xl_load(ca, rq, rd, voq, vod, sq, sd, 0, ng);
-  xl_load(cb, rq, rd, voq, vod, sq, sd, XL_P, ng);
+  XL_MARK(0);
+  XlChunk ck[NCH];
+#pragma unroll
+  for (int k = 0; k < NCH; k++) xl_load(ck[k], rq, rd, voq, vod, sq, sd, k * XL_P, ng);
 
   // ---- the activation: XE entries + scales in LDS.  Every global operand a thread needs is loaded in one
   // batch before any is used (a load per loop trip would pay one memory latency per trip) ----
@@ -263,7 +280,9 @@ __global__ __launch_bounds__(NW * 64) void exact_gemv_kernel(const uint4* __rest
         for (int k = 0; k < XL_K4; k++)
           if (own(k)) s_a4[k * T + t] = yv[k];
         __syncthreads();
+        XL_MARK(1);
         const float sc1 = xl_rms_scale(xl_sumsq<NW>(s_a, n, &s_scale[0], a.serial_norms), n, a.eps);
+        XL_MARK(2);
 #pragma unroll
         for (int k = 0; k < XL_K4; k++) {  // model.cpp:843-858: the post norm, then the residual add
           hv[k].x = hv[k].x + (sc1 * yv[k].x) * wv[k].x;
@@ -282,7 +301,9 @@ __global__ __launch_bounds__(NW * 64) void exact_gemv_kernel(const uint4* __rest
             reinterpret_cast<float4*>(a.resid_out)[k * T + t] = hv[k];
         }
       __syncthreads();
+      XL_MARK(3);
       const float sc2 = xl_rms_scale(xl_sumsq<NW>(s_b, n, &s_scale[1], a.serial_norms), n, a.eps);
+      XL_MARK(4);
 #pragma unroll
       for (int k = 0; k < XL_K4; k++)
         if (own(k)) {  // run_norm: (scale * x) * w (model.cpp:352-357)
@@ -311,20 +332,24 @@ __global__ __launch_bounds__(NW * 64) void exact_gemv_kernel(const uint4* __rest
   }
   __syncthreads();
 
-  // ---- the rows: every block in order, chunks double-buffered ----
+  XL_MARK(5);
+  // ---- the rows: every block in order, NCH chunks in flight ----
   float lo = 0.0f, hi = 0.0f;
   const float4* s_xd4 = reinterpret_cast<const float4*>(s_xd);
-  for (int g0 = 0; g0 < ng; g0 += 2 * XL_P) {
-    xl_eat(ca, g0, ng, jj, s_xe, s_xd4, lo, hi);
-    if (g0 + 2 * XL_P < ng) xl_load(ca, rq, rd, voq, vod, sq, sd, g0 + 2 * XL_P, ng);
-    if (g0 + XL_P >= ng) break;
-    xl_eat(cb, g0 + XL_P, ng, jj, s_xe, s_xd4, lo, hi);
-    if (g0 + 3 * XL_P < ng) xl_load(cb, rq, rd, voq, vod, sq, sd, g0 + 3 * XL_P, ng);
+  for (int g0 = 0; g0 < ng; g0 += NCH * XL_P) {
+#pragma unroll
+    for (int k = 0; k < NCH; k++) {
+      const int gk = g0 + k * XL_P;
+      if (gk >= ng) break;
+      xl_eat(ck[k], gk, ng, jj, s_xe, s_xd4, lo, hi);
+      if (gk + NCH * XL_P < ng) xl_load(ck[k], rq, rd, voq, vod, sq, sd, gk + NCH * XL_P, ng);
+    }
   }
   // hsum_float_8 (ops.cpp:324-330): ((a0 + a4) + (a2 + a6)) + ((a1 + a5) + (a3 + a7)); lane jj holds a_jj, a_jj+4
   const float t4 = lo + hi;
   const float u = t4 + dpp_f<DPP_QUAD_2301>(t4);  // jj 0: t0 + t2, jj 1: t1 + t3
   const float r = u + dpp_f<DPP_QUAD_1032>(u);    // jj 0: (t0 + t2) + (t1 + t3)
+  XL_MARK(6);
   if constexpr (ROLE == XL_GELU) {
     if (jj == 0) s_rows[wave * 16 + rl] = r;
     __syncthreads();
@@ -377,41 +402,51 @@ __global__ void xl_repack_kernel(const uint4* __restrict__ q0, const uint16_t* _
 // ---------------------------------------------------------------------------
 // exact attention (exact.h)
 // ---------------------------------------------------------------------------
-// the q or k row of one head held by a wave: element i = lane + 64 k (EPL per lane); run_norm's serial chain
-// (ops.cpp:28-43) on the row staged in s_x, (scale * x) * w, then NEOX rope at pos (ops.cpp:67-95, the pinned
-// build's contractions: v0 c - v1 s and v0 s + v1 c as one fma each) -- pairs (i, i + HD / 2) sit in one lane
+// the q or k row of one head held by a wave: element i = lane + 64 k (EPL per lane), its norm weights and the
+// rope table entries loaded by the caller (every global operand of the kernel is issued at its start);
+// run_norm's serial chain (ops.cpp:28-43) on the row staged in s_x, (scale * x) * w, then NEOX rope at pos
+// (ops.cpp:67-95, the pinned build's contractions: v0 c - v1 s and v0 s + v1 c as one fma each) -- pairs
+// (i, i + HD / 2) sit in one lane
 template <int HD>
-__device__ __forceinline__ void xa_row(const float* __restrict__ src, const float* __restrict__ nw,
-                                       const float* __restrict__ cs, double eps, float* s_x, float (&r)[HD / 64]) {
+struct XaRow {
+  static constexpr int EPL = HD / 64;
+  float v[EPL], w[EPL];
+};
+template <int HD>
+__device__ __forceinline__ void xa_load(XaRow<HD>& r, const float* __restrict__ src, const float* __restrict__ nw) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 0; k < XaRow<HD>::EPL; k++) {
+    r.v[k] = src[lane + 64 * k];
+    r.w[k] = nw[lane + 64 * k];
+  }
+}
+template <int HD>
+__device__ __forceinline__ void xa_row(const XaRow<HD>& in, const float (&c)[HD / 128 > 0 ? HD / 128 : 1],
+                                       const float (&sn)[HD / 128 > 0 ? HD / 128 : 1], double eps, float* s_x,
+                                       float (&r)[HD / 64]) {
   constexpr int EPL = HD / 64, HALF = HD / 2;
   const int lane = threadIdx.x & 63;
-  float v[EPL];
 #pragma unroll
-  for (int k = 0; k < EPL; k++) {
-    v[k] = src[lane + 64 * k];
-    s_x[lane + 64 * k] = v[k];
-  }
+  for (int k = 0; k < EPL; k++) s_x[lane + 64 * k] = in.v[k];
   __syncthreads();
   const float sc = xl_rms_scale(xl_chain(s_x, HD), HD, eps);
   float nv[EPL];
 #pragma unroll
-  for (int k = 0; k < EPL; k++) nv[k] = (sc * v[k]) * nw[lane + 64 * k];
+  for (int k = 0; k < EPL; k++) nv[k] = (sc * in.v[k]) * in.w[k];
 #pragma unroll
-  for (int k = 0; k < EPL; k++) {
-    const int i = lane + 64 * k;
-    if (i < HALF) {
-      const int kp = k + EPL / 2;  // element i + HALF
-      const float c = cs[2 * i], sn = cs[2 * i + 1];
-      r[k] = fmaf(nv[k], c, -(nv[kp] * sn));
-      r[kp] = fmaf(nv[k], sn, nv[kp] * c);
-    }
+  for (int k = 0; k < EPL / 2; k++) {  // element lane + 64 k < HALF pairs with lane + 64 k + HALF
+    const int kp = k + EPL / 2;
+    r[k] = fmaf(nv[k], c[k], -(nv[kp] * sn[k]));
+    r[kp] = fmaf(nv[k], sn[k], nv[kp] * c[k]);
   }
   __syncthreads();  // s_x reuse
+  (void)HALF;
 }
 
 template <int HD>
 __global__ __launch_bounds__(64) void xattn_scores_kernel(XAttnArgs a) {
-  constexpr int EPL = HD / 64;
+  constexpr int EPL = HD / 64, CPL = EPL / 2;
   __shared__ float s_x[HD];
   __shared__ __attribute__((aligned(16))) double s_q[HD];
   __shared__ __attribute__((aligned(16))) uint16_t s_k[HD];
@@ -419,40 +454,64 @@ __global__ __launch_bounds__(64) void xattn_scores_kernel(XAttnArgs a) {
   const int pos = *a.d_pos, n_keys = pos + 1;
   if (split * 64 >= n_keys) return;  // no key chunk for this work-group (whole wave)
   const int hkv = h / (a.n_head / a.n_head_kv);
+  const bool own_pos = (pos >> 6) % XA_NSPLIT == split;
+  // every global operand first: q row + weights, the rope entries, the new key's k / v rows, the first K rows
   const float* cs = a.rope_cs + (size_t)pos * HD;
+  float c[CPL], sn[CPL];
+#pragma unroll
+  for (int k = 0; k < CPL; k++) {
+    const float2 t = reinterpret_cast<const float2*>(cs)[lane + 64 * k];
+    c[k] = t.x;
+    sn[k] = t.y;
+  }
+  XaRow<HD> qr, kr_;
+  xa_load<HD>(qr, a.qkv + (size_t)h * HD, a.q_norm_w);
+  float vrow[EPL];
+  if (own_pos) {
+    xa_load<HD>(kr_, a.qkv + a.k_off + (size_t)hkv * HD, a.k_norm_w);
+#pragma unroll
+    for (int k = 0; k < EPL; k++) vrow[k] = a.qkv[a.v_off + (size_t)hkv * HD + lane + 64 * k];
+  }
+  const uint16_t* kb = a.k_cache + (size_t)hkv * a.max_ctx * HD;
+  const int j1 = split * 64 + lane;  // this lane's first key
+  const uint4* kr0 = reinterpret_cast<const uint4*>(kb + (size_t)min(j1, pos) * HD);
+  uint4 wa[8];
+#pragma unroll
+  for (int u = 0; u < 8; u++) wa[u] = kr0[u];  // the first batch of the first key row (re-read for key pos)
   float r[EPL];
-  xa_row<HD>(a.qkv + (size_t)h * HD, a.q_norm_w, cs, a.eps, s_x, r);
+  xa_row<HD>(qr, c, sn, a.eps, s_x, r);
 #pragma unroll
   for (int k = 0; k < EPL; k++)  // model.cpp:767 scale, then the score's f16 query (model.cpp:507)
     s_q[lane + 64 * k] = (double)h2f(f2h_ggml(r[k] * a.attn_scale));
-  const bool own_pos = (pos >> 6) % XA_NSPLIT == split;
   if (own_pos) {  // the new key: k norm + rope, K and V rows appended (model.cpp:440-474)
-    xa_row<HD>(a.qkv + a.k_off + (size_t)hkv * HD, a.k_norm_w, cs, a.eps, s_x, r);
+    xa_row<HD>(kr_, c, sn, a.eps, s_x, r);
     uint16_t* kc = a.k_cache + ((size_t)hkv * a.max_ctx + pos) * HD;
     uint16_t* vc = a.v_cache + ((size_t)hkv * a.max_ctx + pos) * HD;
-    const float* vs = a.qkv + a.v_off + (size_t)hkv * HD;
 #pragma unroll
     for (int k = 0; k < EPL; k++) {
-      const uint16_t kb = f2h_ggml(r[k]);
-      s_k[lane + 64 * k] = kb;
-      kc[lane + 64 * k] = kb;
-      vc[lane + 64 * k] = f2h_ggml(vs[lane + 64 * k]);
+      const uint16_t kbits = f2h_ggml(r[k]);
+      s_k[lane + 64 * k] = kbits;
+      kc[lane + 64 * k] = kbits;
+      vc[lane + 64 * k] = f2h_ggml(vrow[k]);
     }
   }
   __syncthreads();
-  const uint16_t* kb = a.k_cache + (size_t)hkv * a.max_ctx * HD;
   double* sc_out = a.scores + (size_t)h * a.max_ctx;
-  for (int c = split; c * 64 < n_keys; c += XA_NSPLIT) {
-    const int j = c * 64 + lane;
+  bool first = true;
+  for (int cc = split; cc * 64 < n_keys; cc += XA_NSPLIT) {
+    const int j = cc * 64 + lane;
     if (j >= n_keys) break;
     const uint4* kr = reinterpret_cast<const uint4*>(j == pos ? s_k : kb + (size_t)j * HD);
+    if (!first || j == pos) {
+#pragma unroll
+      for (int u = 0; u < 8; u++) wa[u] = kr[u];
+    }
+    first = false;
     double acc = 0.0;
     // score += (double)(f16(k_i) * f16(q_i)), i in order (model.cpp:504-509); the f32 product of two f16 values
     // is exact, so one f64 fma per element is the same rounding as the reference's add.  The row streams in
     // batches of 64 elements, the next batch loaded before the current one is summed.
-    uint4 wa[8], wb[8];
-#pragma unroll
-    for (int u = 0; u < 8; u++) wa[u] = kr[u];
+    uint4 wb[8];
     auto eat = [&](const uint4 (&w)[8], int i0) {
       const double2* q2 = reinterpret_cast<const double2*>(s_q + i0 * 8);
 #pragma unroll
@@ -483,12 +542,47 @@ __global__ __launch_bounds__(64) void xattn_scores_kernel(XAttnArgs a) {
 
 constexpr int XA_CH = 1024;  // accum: keys per chunk in LDS
 
+// eight steps of vec_mad_f16 for one head dim: acc (f16 in the low half) = f16(fma(f16 V[u], e[u], acc)), each
+// step v_fma_mix_f32 (f16 operands widened exactly, one f32 rounding) then v_cvt_f16_f32 (round to nearest even):
+// the reference's f32 fma and f32_to_f16, two dependent instructions per key with no padding between them
+__device__ __forceinline__ void xa_mad8(uint32_t& acc, const uint32_t* v, const float* e) {
+  asm volatile(
+      "v_fma_mix_f32 %0, %1, %9, %0 op_sel_hi:[1,0,1]\n\t"
+      "v_cvt_f16_f32_e32 %0, %0\n\t"
+      "v_fma_mix_f32 %0, %2, %10, %0 op_sel_hi:[1,0,1]\n\t"
+      "v_cvt_f16_f32_e32 %0, %0\n\t"
+      "v_fma_mix_f32 %0, %3, %11, %0 op_sel_hi:[1,0,1]\n\t"
+      "v_cvt_f16_f32_e32 %0, %0\n\t"
+      "v_fma_mix_f32 %0, %4, %12, %0 op_sel_hi:[1,0,1]\n\t"
+      "v_cvt_f16_f32_e32 %0, %0\n\t"
+      "v_fma_mix_f32 %0, %5, %13, %0 op_sel_hi:[1,0,1]\n\t"
+      "v_cvt_f16_f32_e32 %0, %0\n\t"
+      "v_fma_mix_f32 %0, %6, %14, %0 op_sel_hi:[1,0,1]\n\t"
+      "v_cvt_f16_f32_e32 %0, %0\n\t"
+      "v_fma_mix_f32 %0, %7, %15, %0 op_sel_hi:[1,0,1]\n\t"
+      "v_cvt_f16_f32_e32 %0, %0\n\t"
+      "v_fma_mix_f32 %0, %8, %16, %0 op_sel_hi:[1,0,1]\n\t"
+      "v_cvt_f16_f32_e32 %0, %0"
+      : "+v"(acc)
+      : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]), "v"(e[0]), "v"(e[1]),
+        "v"(e[2]), "v"(e[3]), "v"(e[4]), "v"(e[5]), "v"(e[6]), "v"(e[7]));
+}
+
+// f32 -> f16, round to nearest even (= the reference's f32_to_f16 for every non-NaN input: llmi_selftest 0), as
+// one instruction the compiler cannot fuse with the fma that produced its input
+__device__ __forceinline__ uint16_t cvt_f16_rne(float f) {
+  uint32_t r;
+  asm volatile("v_cvt_f16_f32_e32 %0, %1" : "=v"(r) : "v"(f));
+  return (uint16_t)r;
+}
+
 template <int HD>
 __global__ __launch_bounds__((HD / 64 + 1) * 64) void xattn_accum_kernel(XAttnArgs a) {
   constexpr int NWV = HD / 64, T = (NWV + 1) * 64;
   constexpr int KPT = XA_CH / 256;  // keys per scan thread (threads 0..255)
   __shared__ double s_sc[XA_CH];
-  __shared__ float2 s_ep[XA_CH];   // (e, pe) per key
+  __shared__ __attribute__((aligned(16))) float s_e[XA_CH];   // e per key
+  __shared__ __attribute__((aligned(16))) float s_pe[XA_CH];  // pe per key
   __shared__ uint32_t s_up[XA_CH / 32];
   __shared__ double s_tmax[256];
   __shared__ float s_sacc;
@@ -530,10 +624,12 @@ __global__ __launch_bounds__((HD / 64 + 1) * 64) void xattn_accum_kernel(XAttnAr
         const double score = s_sc[j];
         const float prev = (float)pm;  // the reference's max_score before key j
         if (score > (double)prev) {    // model.cpp:520-532
-          s_ep[j] = make_float2(1.0f, llmi_glibc::expf(prev - (float)score));
+          s_e[j] = 1.0f;
+          s_pe[j] = llmi_glibc::expf(prev - (float)score);
           atomicOr(&s_up[j >> 5], 1u << (j & 31));
         } else {
-          s_ep[j] = make_float2(llmi_glibc::expf((float)(score - (double)prev)), 1.0f);
+          s_e[j] = llmi_glibc::expf((float)(score - (double)prev));
+          s_pe[j] = 1.0f;
         }
         pm = fmax(pm, score);
       }
@@ -544,37 +640,48 @@ __global__ __launch_bounds__((HD / 64 + 1) * 64) void xattn_accum_kernel(XAttnAr
       const uint16_t* vp = vb + (size_t)c0 * HD;
       // V of 32 keys per batch, the next batch's loads issued before this one is summed (clamped keys past the
       // chunk are loaded but never summed)
-      uint16_t va[32], vn[32];
+      uint32_t va[32], vn[32];  // one f16 per register (low half): the mad8 asm reads them as they are
 #pragma unroll
       for (int u = 0; u < 32; u++) va[u] = vp[(size_t)min(u, nk - 1) * HD];
       for (int j0 = 0; j0 < nk; j0 += 32) {
 #pragma unroll
         for (int u = 0; u < 32; u++) vn[u] = vp[(size_t)min(j0 + 32 + u, nk - 1) * HD];
-        const uint32_t up = s_up[j0 >> 5];
-        const int m = min(32, nk - j0);
+        // the batch's max moves (wave-uniform, a scalar branch per key) and e values (broadcast LDS reads)
+        const uint32_t up = __builtin_amdgcn_readfirstlane(s_up[j0 >> 5]);
+        const int m = __builtin_amdgcn_readfirstlane(min(32, nk - j0));
+        float e[32];
 #pragma unroll
-        for (int u = 0; u < 32; u++) {
-          if (u < m) {
-            const float2 ep = s_ep[j0 + u];
-            // each result is rounded to f32 first, then to f16 (the asm fence keeps the compiler from fusing the
-            // pair into v_fma_mixlo_f16, one rounding: another f16 whenever the f32 rounding lands on a midpoint)
-            if (up & (1u << u)) {
-              float sv = (float)__builtin_bit_cast(_Float16, v16) * ep.y;
-              asm volatile("" : "+v"(sv));
-              v16 = f2h(sv);
+        for (int u4 = 0; u4 < 8; u4++) {
+          const float4 q = reinterpret_cast<const float4*>(s_e + j0)[u4];
+          e[4 * u4] = q.x; e[4 * u4 + 1] = q.y; e[4 * u4 + 2] = q.z; e[4 * u4 + 3] = q.w;
+        }
+        // each step rounds to f32 (the fma), then to f16 (the conversion as its own instruction: fused by the
+        // compiler into v_fma_mixlo_f16 it would round once, another f16 whenever the f32 value is a midpoint)
+        if (up == 0 && m == 32) {  // the common batch: the max did not move, 32 straight fma + round steps
+          uint32_t acc = v16;
+#pragma unroll
+          for (int u = 0; u < 32; u += 8) xa_mad8(acc, va + u, e + u);
+          v16 = (uint16_t)acc;
+        } else {
+#pragma unroll
+          for (int u = 0; u < 32; u++) {
+            if (u < m) {
+              if (up & (1u << u)) v16 = cvt_f16_rne((float)__builtin_bit_cast(_Float16, v16) * s_pe[j0 + u]);
+              v16 = cvt_f16_rne(fmaf((float)__builtin_bit_cast(_Float16, (uint16_t)va[u]), e[u], (float)__builtin_bit_cast(_Float16, v16)));
             }
-            float nv = fmaf((float)__builtin_bit_cast(_Float16, va[u]), ep.x, (float)__builtin_bit_cast(_Float16, v16));
-            asm volatile("" : "+v"(nv));
-            v16 = f2h(nv);
           }
         }
 #pragma unroll
         for (int u = 0; u < 32; u++) va[u] = vn[u];
       }
     } else {  // s_acc = s_acc * pe + e, keys in order (model.cpp:540)
-      for (int j = 0; j < nk; j++) {
-        const float2 ep = s_ep[j];
-        s_acc = s_acc * ep.y + ep.x;
+      for (int j0 = 0; j0 < nk; j0 += 4) {
+        const float4 e4 = reinterpret_cast<const float4*>(s_e + j0)[0];
+        const float4 p4 = reinterpret_cast<const float4*>(s_pe + j0)[0];
+        const float ev[4] = {e4.x, e4.y, e4.z, e4.w}, pv[4] = {p4.x, p4.y, p4.z, p4.w};
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+          if (j0 + u < nk) s_acc = s_acc * pv[u] + ev[u];
       }
     }
     __syncthreads();  // the chunk's LDS is reused by the next one
@@ -726,16 +833,18 @@ void launch_exact_gemv(const XlWeight& w, const XlArgs& a_in, int role, hipStrea
   // PRE / GELU: each thread holds 4 XL_K4 elements of the residual-step operands in registers
   const bool k3_2 = a.n <= 12 * 128, k3_4 = a.n <= 12 * 256;
   switch (role) {
-    case XL_PLAIN: go(exact_gemv_kernel<1, XL_PLAIN, 1>, 1); break;
-    case XL_QUANT: go(exact_gemv_kernel<1, XL_QUANT, 1>, 1); break;
+    // PLAIN / QUANT: one wave per work-group, few of them (a row group per wave), so the registers go to weight
+    // chunks in flight: 4 x 8 groups (32 KB per wave)
+    case XL_PLAIN: go(exact_gemv_kernel<1, XL_PLAIN, 1, 4>, 1); break;
+    case XL_QUANT: go(exact_gemv_kernel<1, XL_QUANT, 1, 4>, 1); break;
     case XL_PRE:
-      if (k3_2) go(exact_gemv_kernel<2, XL_PRE, 3>, 2);
-      else if (k3_4) go(exact_gemv_kernel<4, XL_PRE, 3>, 4);
-      else go(exact_gemv_kernel<4, XL_PRE, 6>, 4);
+      if (k3_2) go(exact_gemv_kernel<2, XL_PRE, 3, 2>, 2);
+      else if (k3_4) go(exact_gemv_kernel<4, XL_PRE, 3, 2>, 4);
+      else go(exact_gemv_kernel<4, XL_PRE, 6, 2>, 4);
       break;
     case XL_GELU:
-      if (k3_4) go(exact_gemv_kernel<4, XL_GELU, 3>, 4);
-      else go(exact_gemv_kernel<4, XL_GELU, 6>, 4);
+      if (k3_4) go(exact_gemv_kernel<4, XL_GELU, 3, 2>, 4);
+      else go(exact_gemv_kernel<4, XL_GELU, 6, 2>, 4);
       break;
     default: throw std::runtime_error("exact gemv: bad role");
   }

@@ -618,7 +618,8 @@ __global__ void finalize_token_kernel(unsigned long long* __restrict__ keys, int
     const unsigned long long kg = (k & 0xFFFFFFFF00000000ull) | (0xFFFFFFFFu - gi);
     if (kg > best) best = kg;
   }
-  const uint32_t tok = argmax_key_index(best);
+  // no key at all (every logit NaN: no row compared as a maximum): token 0 rather than an index past the table
+  const uint32_t tok = best ? argmax_key_index(best) : 0u;
   *d_token = (int32_t)tok;
   *d_pos = pos + 1;
   if (i < ring_cap) ring[i] = (int32_t)tok;
@@ -716,7 +717,7 @@ __global__ __launch_bounds__(1024) void finalize_embed_norm_kernel(
       const unsigned long long kg = (k & 0xFFFFFFFF00000000ull) | (0xFFFFFFFFu - gi);
       if (kg > best) best = kg;
     }
-    const uint32_t tok = argmax_key_index(best);
+    const uint32_t tok = best ? argmax_key_index(best) : 0u;  // no key (NaN logits): a valid row, not 2^32 - 1
     *d_token = (int32_t)tok;
     *d_pos = pos + 1;
     if (i < ring_cap) ring[i] = (int32_t)tok;
