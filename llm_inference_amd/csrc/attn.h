@@ -41,6 +41,7 @@ struct AttnArgs {
   unsigned* ticket;       // fast path: [n_head_kv] zeroed counters (reset by the kernel)
   XBlock* q8;             // optional: Q8_0 blocks of out (head_dim % 32 == 0)
   int q8k = 0;            // 1: q8 holds Q8_K quants instead (q8k_block_quad; G * head_dim % 256 == 0): kq o projection
+  float softcap = 0.0f;   // attention.logit_softcapping (model.cpp:511-513); 0: none
 };
 
 void launch_qk_norm_rope_kv(const QKVArgs& a, bool exact, hipStream_t s);

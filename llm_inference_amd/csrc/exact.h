@@ -87,6 +87,7 @@ struct XAttnArgs {
   double* scores = nullptr;  // [n_head][max_ctx]
   float* out = nullptr;      // [n_head][head_dim]
   XBlock* xq = nullptr;      // [n_head * head_dim / 32]
+  float softcap = 0.0f;      // attention.logit_softcapping (model.cpp:511-513); 0: none
 };
 bool exact_attn_supported(int head_dim, int n_head, int n_head_kv);
 void launch_exact_attn(const XAttnArgs& a, hipStream_t s);

@@ -197,4 +197,8 @@ LLMI_HD float tanhf(float x) {
   return (jx >> 31) == 0 ? z : -z;
 }
 
+// the attention logit soft-cap (model.cpp:511-513): the double score over the float cap is a double division,
+// tanhf takes its float rounding, and the float product cap * tanhf(...) goes back into the double
+LLMI_HD double softcap_score(double score, float cap) { return (double)(cap * tanhf((float)(score / (double)cap))); }
+
 }  // namespace llmi_glibc

@@ -158,6 +158,7 @@ __global__ __launch_bounds__(256) void attn_exact_kernel(AttnArgs a) {
       } else {
         for (int i = 0; i < hd; i++) score += (double)(h2f(kr[i]) * s_q[i]);
       }
+      if (a.softcap > 0.0f) score = llmi_glibc::softcap_score(score, a.softcap);
       s_sc[j] = score;
       tmax = fmax(tmax, score);
     }
@@ -516,6 +517,7 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, const QKVArgs
       float sc = s0 + s1;
 #pragma unroll
       for (int o = 1; o < TP; o <<= 1) sc += __shfl_xor(sc, o);
+      if (a.softcap > 0.0f) sc = a.softcap * tanhf(sc / a.softcap);  // model.cpp:511-513
       if (part == 0) s_p[g][j] = tile * TK + j < n_keys ? sc : -INFINITY;
     }
     __syncthreads();

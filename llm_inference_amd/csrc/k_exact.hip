@@ -596,7 +596,8 @@ __global__ __launch_bounds__((HD / 64 + 1) * 64) void xattn_accum_kernel(XAttnAr
   float s_acc = 0.0f;
   for (int c0 = 0; c0 < n_keys; c0 += XA_CH) {
     const int nk = min(XA_CH, n_keys - c0);
-    for (int i = t; i < nk; i += T) s_sc[i] = sc_in[c0 + i];
+    for (int i = t; i < nk; i += T)
+      s_sc[i] = a.softcap > 0.0f ? llmi_glibc::softcap_score(sc_in[c0 + i], a.softcap) : sc_in[c0 + i];
     for (int i = t; i < XA_CH / 32; i += T) s_up[i] = 0u;
     __syncthreads();
     double tmax = -INFINITY;

@@ -1025,6 +1025,7 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(PrefillAttn a) {
       float sc = s0 + s1;
 #pragma unroll
       for (int o = 1; o < TP; o <<= 1) sc += __shfl_xor(sc, o);
+      if (a.softcap > 0.0f) sc = a.softcap * tanhf(sc / a.softcap);  // model.cpp:511-513
       if (part == 0) s_p[g][j] = tile * 64 + j < n_keys ? sc : -INFINITY;
     }
     __syncthreads();
@@ -1284,6 +1285,10 @@ __global__ __launch_bounds__(64 * G * S) void prefill_attn_mfma_kernel(PrefillAt
     for (int c = 0; c < HD / 16; c++) {
       const f16x8 kf = *reinterpret_cast<const f16x8*>(kt + r * ROWB + (((2 * c + h) ^ (r & SWM)) * 16));
       sc = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[c], sc, 0, 0, 0);
+    }
+    if (a.softcap > 0.0f) {  // model.cpp:511-513 (before the mask: a masked score is replaced, never read)
+#pragma unroll
+      for (int reg = 0; reg < 16; reg++) sc[reg] = a.softcap * tanhf(sc[reg] / a.softcap);
     }
     // causal mask (select, never arithmetic on a masked score) + online softmax
     const bool diag = 32 * t + 31 > first_pos;

@@ -46,8 +46,7 @@ void Session::load_hparams(const GGUFView& g) {  // model.cpp:58-167
   hp_.attn_scale = 1.0f / std::sqrt(float(hp_.hd_k));  // model.cpp:120
   if (const GValue* sw = g.find(p + "attention.sliding_window_pattern"))
     for (const auto& v : sw->arr) hp_.swa_layers.push_back((v.u32 & 0xFF) != 0);
-  if (const GValue* v = g.find(p + "attention.logit_softcapping"))
-    if (v->f32() > 0.0f) throw status_error(LLMI_E_GGUF, "unsupported: " + p + "attention.logit_softcapping");
+  if (const GValue* v = g.find(p + "attention.logit_softcapping")) hp_.attn_softcap = v->f32();
   // ALiBi (model.cpp:125-128, 492-518): no Gemma file sets it, and the reference's bias term
   // slope * (t_k - (pos + t)) is evaluated in uint32_t (a wrapped, huge positive bias); refused, never ignored
   if (const GValue* v = g.find(p + "attention.max_alibi_bias"))
@@ -1013,6 +1012,7 @@ bool Session::prefill_run(const int32_t* tokens, int n, int pos, bool allow_f16)
       qk.pos0 = p0;
       launch_prefill_qk(qk, T, s);
       PrefillAttn at;
+      at.softcap = hp_.attn_softcap;
       at.q = pf_q_;
       at.k_cache = Ld.kc;
       at.v_cache = Ld.vc;
@@ -1099,6 +1099,7 @@ void Session::setup_engine(const GGUFView& g) {
   const char* on = getenv("LLMI_ENGINE");
   if (!on || atoi(on) == 0) return;
   if (!fuse_layers_ || tp_ || !dup_.empty() || ple_table_.qs || hp_.gemma4) return;
+  if (hp_.attn_softcap > 0.0f) return;  // the engine's attention has no soft-cap (the attention block has)
   if (embd_.type != T_F16 && embd_.type != T_Q8_0) return;
   for (const auto& l : L_) {
     const bool q40 = l.qkv.size() == 1 && l.qkv[0].w.type == T_Q4_0 && l.o.w.type == T_Q4_0 &&
@@ -1326,6 +1327,7 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
       if (blk_trace_ && l == blk_trace_layer_) bs.trace = blk_trace_;
       if (trace_fn_ && qrole == LAYER_PRO) g.xn_out = xn_;
       aa.q8k = Ld.o.w.kq ? 1 : 0;
+      aa.softcap = hp_.attn_softcap;
       launch_attn_block(Ld.qkv[0].w, Ld.qkv.size() > 1 ? &Ld.qkv[1].w : nullptr, g, qrole, Ld.o.w, go, aa, qa, bs, s);
       kernels_per_token_++;
       if (trace_fn_) {  // the launch's products: residual / norm (prologue), q|k|v and xo granules, attention, o
@@ -1389,6 +1391,7 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
       AttnArgs aa{q_, Ld.kc, Ld.vc, nh_, nkv_, hd, max_ctx_, d_pos_, part_, attn_,
                   ticket_, q8_in_combine ? act_.q8.xb + (size_t)hr * hb : nullptr};
       aa.q8k = Ld.o.w.kq ? 1 : 0;  // the kq o projection reads Q8_K quants
+      aa.softcap = hp_.attn_softcap;
       for (int r = 0; r < dup("attn"); r++) launch_attention(aa, false, s, &qa);
       kernels_per_token_++;
       tap("attn", l, attn_, (size_t)nh_ * hd * 4, s);
@@ -1593,6 +1596,7 @@ void Session::record_layers_xl(hipStream_t s) {
     xa.scores = xa_scores_;
     xa.out = attn_;
     xa.xq = xa_xq_;
+    xa.softcap = hp_.attn_softcap;
     launch_exact_attn(xa, s);
     XlArgs o;
     o.xb = xa_xq_;
@@ -1664,6 +1668,7 @@ void Session::record_layers(hipStream_t s, bool x_q8) {
     const bool fused_q8 = !ex_attn_ && o_q8 && hd % 32 == 0;
     AttnArgs aa{q_, Ld.kc, Ld.vc, hp_.n_head, hp_.n_head_kv, hd, max_ctx_, d_pos_, part_, attn_,
                 ticket_, fused_q8 ? act_.q8.xb : nullptr};
+    aa.softcap = hp_.attn_softcap;
     for (int r = 0; r < dup("attn"); r++) launch_attention(aa, ex_attn_, s, fuse_qk ? &qa : nullptr);
     kernels_per_token_++;
     dump("kqv_out-" + L, attn_, hp_.n_head * hd, s);
@@ -2087,6 +2092,7 @@ void Session::time_kernel(int which, int reps, double* us, double* bytes) {
                          bs.g_xo = blk_gxo_ + i * blk_gxo_stride_;
                          bs.err = blk_err_;
                          aa.q8k = Ld.o.w.kq ? 1 : 0;
+                         aa.softcap = hp_.attn_softcap;
                          LayerGemv qq = q;  // PLAIN block (27B): the x blocks of the last norm launch
                          if (!block_pro_) qq.xg = act_.q8.xb;
                          launch_attn_block(Ld.qkv[0].w, Ld.qkv.size() > 1 ? &Ld.qkv[1].w : nullptr, qq,

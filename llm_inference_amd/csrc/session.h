@@ -32,6 +32,7 @@ struct HParams {  // model.h:22-43 (Gemma-3 subset)
   int n_epl = 0;             // embedding_length_per_layer(_input)
   int kv_from = -1;          // n_layer_kv_from_start: layers >= kv_from read an earlier layer's cache
   float final_softcap = 0;   // attention.final_logit_softcapping
+  float attn_softcap = 0;    // attention.logit_softcapping (model.cpp:130-133, 511-513)
 };
 
 struct GemvPart {  // one weight GEMV writing rows [out_off, out_off + rows)

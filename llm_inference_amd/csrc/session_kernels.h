@@ -193,6 +193,7 @@ struct PrefillAttn {
   // partials [head][query block][ks] (64 (head_dim / 2 + 2) floats each), combined by a merge launch
   int ks = 1;
   float* part = nullptr;
+  float softcap = 0.0f;     // attention.logit_softcapping (model.cpp:511-513); 0: none
 };
 constexpr int PREFILL_ATTN_KS_MAX = 8;
 void launch_prefill_norm(const PrefillNorm& a, int T, hipStream_t s);

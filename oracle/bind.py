@@ -57,6 +57,8 @@ class Oracle:
         L.orc_gelu_mul.argtypes = [_f32p, _f32p, _f32p, C.c_size_t]
         L.orc_attn_head.argtypes = [_f32p, _u16p, _u16p, C.c_size_t, C.c_size_t, _f32p]
         L.orc_attn_head_f64.argtypes = [_f32p, _u16p, _u16p, C.c_size_t, C.c_size_t, _f32p]
+        L.orc_attn_head_cap.argtypes = [_f32p, _u16p, _u16p, C.c_size_t, C.c_size_t, C.c_float, _f32p]
+        L.orc_attn_head_f64_cap.argtypes = [_f32p, _u16p, _u16p, C.c_size_t, C.c_size_t, C.c_float, _f32p]
         L.orc_model_create.restype = C.c_void_p
         L.orc_model_create.argtypes = [C.c_void_p, C.c_size_t, C.c_int, C.c_int]
         L.orc_model_forward.argtypes = [C.c_void_p, _i32p, C.c_int, C.c_int, _f32p]
@@ -148,11 +150,11 @@ class Oracle:
         self.lib.orc_gelu_mul(o, g, np.ascontiguousarray(u, np.float32), g.size)
         return o
 
-    def attn_head(self, q, k, v):
+    def attn_head(self, q, k, v, softcap: float = 0.0):
         q = np.ascontiguousarray(q, np.float32)
         out = np.zeros_like(q)
-        self.lib.orc_attn_head(q, np.ascontiguousarray(k, np.uint16), np.ascontiguousarray(v, np.uint16),
-                               k.shape[0], q.size, out)
+        self.lib.orc_attn_head_cap(q, np.ascontiguousarray(k, np.uint16), np.ascontiguousarray(v, np.uint16),
+                                   k.shape[0], q.size, softcap, out)
         return out
 
     # --- model ---

@@ -500,8 +500,15 @@ void orc_gelu_mul(float* o, const float* gate, const float* up, size_t n) {  /* 
   }
 }
 
-void orc_attn_head(const float* q, const uint16_t* k, const uint16_t* v, size_t n_keys,
-                   size_t hd, float* out) {  /* model.cpp:481-547 (softcap/ALiBi 0) */
+/* the attention logit soft-cap (model.cpp:511-513): score is a double, the cap a float, so
+ * score / cap is a double division, tanhf takes its float rounding, and cap * tanhf(...) is a float
+ * product stored back into the double */
+static inline double softcap_score(double score, float cap) {
+  return cap > 0.0f ? (double)(cap * tanhf((float)(score / (double)cap))) : score;
+}
+
+void orc_attn_head_cap(const float* q, const uint16_t* k, const uint16_t* v, size_t n_keys,
+                       size_t hd, float cap, float* out) {  /* model.cpp:481-547 (ALiBi 0) */
   pthread_once(&g_table_once, table_init);
   uint16_t* vacc = (uint16_t*)malloc(hd * 2);
   uint16_t* q16 = (uint16_t*)malloc(hd * 2);
@@ -511,6 +518,7 @@ void orc_attn_head(const float* q, const uint16_t* k, const uint16_t* v, size_t 
   for (size_t t = 0; t < n_keys; t++) {
     double score = 0.0;
     for (size_t i = 0; i < hd; i++) score += (double)(F16(k[t * hd + i]) * F16(q16[i]));
+    score = softcap_score(score, cap);
     const float prev_max = max_score;
     float e, pe;
     if (score > (double)prev_max) {
@@ -530,18 +538,23 @@ void orc_attn_head(const float* q, const uint16_t* k, const uint16_t* v, size_t 
   free(vacc); free(q16);
 }
 
+void orc_attn_head(const float* q, const uint16_t* k, const uint16_t* v, size_t n_keys, size_t hd, float* out) {
+  orc_attn_head_cap(q, k, v, n_keys, hd, 0.0f, out);
+}
+
 /* NOT the reference: the same attention in float64 math (no f16 V
  * accumulator rounding).  Used only to pin the fast GPU path, whose fp32
  * split-K accumulation is closer to exact math than the reference itself
  * (whose f16 accumulator carries ~1e-3 absolute error). */
-void orc_attn_head_f64(const float* q, const uint16_t* k, const uint16_t* v, size_t n_keys, size_t hd,
-                       float* out) {
+void orc_attn_head_f64_cap(const float* q, const uint16_t* k, const uint16_t* v, size_t n_keys, size_t hd,
+                           float cap, float* out) {
   pthread_once(&g_table_once, table_init);
   double* s = (double*)malloc(sizeof(double) * n_keys);
   double mx = -INFINITY, l = 0.0;
   for (size_t t = 0; t < n_keys; t++) {
     double sc = 0.0;
     for (size_t i = 0; i < hd; i++) sc += (double)F16(k[t * hd + i]) * (double)F16(orc_f32_to_f16(q[i]));
+    if (cap > 0.0f) sc = (double)cap * tanh(sc / (double)cap);
     s[t] = sc;
     if (sc > mx) mx = sc;
   }
@@ -552,6 +565,10 @@ void orc_attn_head_f64(const float* q, const uint16_t* k, const uint16_t* v, siz
     out[i] = (float)(a / l);
   }
   free(s);
+}
+
+void orc_attn_head_f64(const float* q, const uint16_t* k, const uint16_t* v, size_t n_keys, size_t hd, float* out) {
+  orc_attn_head_f64_cap(q, k, v, n_keys, hd, 0.0f, out);
 }
 
 /* ------------------------------------------------------------------ */
@@ -897,8 +914,8 @@ int orc_model_forward(orc_model* m, const int* tokens, int T, int pos, float* lo
             memcpy(kh + (size_t)tk * hk, &m->kc[src][((size_t)tk * HK + hkv) * hk], 2 * hk);
             memcpy(vh + (size_t)tk * hv, &m->vc[src][((size_t)tk * HK + hkv) * hv], 2 * hv);
           }
-          (m->attn_f64 ? orc_attn_head_f64 : orc_attn_head)(qv + ((size_t)t * H + h) * hk, kh, vh, nk, hv,
-                                                            att + ((size_t)t * H + h) * hv);
+          (m->attn_f64 ? orc_attn_head_f64_cap : orc_attn_head_cap)(qv + ((size_t)t * H + h) * hk, kh, vh, nk, hv,
+                                                                    m->attn_softcap, att + ((size_t)t * H + h) * hv);
         }
       free(kh); free(vh);
     }

@@ -83,6 +83,9 @@ void orc_gelu_mul(float* o, const float* gate, const float* up, size_t n);
  * [head_dim] (already normed/roped/scaled).  out: f32 [head_dim]. */
 void orc_attn_head(const float* q, const uint16_t* k, const uint16_t* v,
                    size_t n_keys, size_t head_dim, float* out);
+/* the same with the attention logit soft-cap of model.cpp:511-513 (cap <= 0: none) */
+void orc_attn_head_cap(const float* q, const uint16_t* k, const uint16_t* v,
+                       size_t n_keys, size_t head_dim, float cap, float* out);
 
 /* ---- whole-model forward (Gemma-3 GGUF), model.cpp:706-1049 ---- */
 typedef struct orc_model orc_model;
@@ -99,6 +102,8 @@ int orc_model_vocab(const orc_model* m);
 void orc_model_set_attn_f64(orc_model* m, int on);
 void orc_attn_head_f64(const float* q, const uint16_t* k, const uint16_t* v, size_t n_keys, size_t head_dim,
                        float* out);
+void orc_attn_head_f64_cap(const float* q, const uint16_t* k, const uint16_t* v, size_t n_keys, size_t head_dim,
+                           float cap, float* out);
 const char* orc_last_error(void);
 
 #ifdef __cplusplus

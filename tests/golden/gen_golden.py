@@ -8,7 +8,8 @@ deterministic cases of tests/golden/cases.py:
   ops_ref.npz        op-level outputs (bit patterns) + input hashes
   model_test.gguf    byte-identical rebuild of ModelTest's in-memory GGUF
   model_ref.npz      reference logits / greedy tokens on model_test.gguf and
-                     on the seeded synthetic 'tiny' Gemma-3 model
+                     on the seeded synthetic 'tiny' Gemma-3 model, with and
+                     without the attention logit soft-cap
 No reference source or binary is committed; only these data files.
 """
 from __future__ import annotations
@@ -27,6 +28,7 @@ from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf, build_model_
 import cases as K  # noqa: E402
 
 OUT = os.path.dirname(os.path.abspath(__file__))
+SOFTCAP = 0.25
 
 
 def gen_ops(ref: Reference) -> dict:
@@ -84,6 +86,20 @@ def gen_models(ref: Reference) -> dict:
     d["tiny__prompt"] = prompt
     d["tiny__logits"] = np.stack(logits)
     d["tiny__tokens"] = np.array(toks, np.int32)
+    # the same model with the attention logit soft-cap (model.cpp:511-513) set low enough to bend most scores
+    gc = build_gemma3_gguf(cfg, seed=7, swa_pattern=[True, False, True],
+                           extra_meta={"attention.logit_softcapping": SOFTCAP})
+    m = ref.model(gc)
+    logits = [m.forward(prompt, 0)]
+    toks = [int(np.argmax(logits[-1]))]
+    pos = len(prompt)
+    for _ in range(5):
+        logits.append(m.forward([toks[-1]], pos))
+        pos += 1
+        toks.append(int(np.argmax(logits[-1])))
+    d["tinycap__logits"] = np.stack(logits)
+    d["tinycap__tokens"] = np.array(toks, np.int32)
+    d["tinycap__cap"] = np.float32(SOFTCAP)
     return d
 
 

@@ -7,7 +7,12 @@ seeded synthetic GGUFs (VERDICT r2 'Next round' 1 and 2):
            the 5-local : 1-global sliding-window rope pattern, a 512-token
            prompt, then 64 greedy steps;
   g27b     Gemma-3 27B Q4_0 (configs[4]'s model): 62 layers, 32 / 16 heads of
-           128, 21,504 hidden units, an 8-token prompt, then 6 greedy steps.
+           128, 21,504 hidden units, an 8-token prompt, then 6 greedy steps;
+  g4b_512f the g4b_512 model and prompt, then 64 steps whose INPUTS are seeded
+           random ids (a random-init model's free-running greedy ids collapse
+           onto a few tokens -- g4b_512 has 4 distinct ids in 65 steps -- while
+           every forced step's argmax is a function of a different context:
+           the reference's own ids, many distinct ones, at every step).
 
 Run in the build container (needs /root/reference; ~25 GB of host memory for
 the 27B file):
@@ -17,6 +22,8 @@ Writes tests/golden/long_ref.npz with, per case:
                     file from the same seed and checks it first)
   <case>__prompt    prompt ids;  <case>__tokens  the reference's greedy ids
                     (first = argmax of the prompt's logits, then one per step)
+  <case>__inputs    (forced cases) the ids fed at each step instead of the
+                    previous step's argmax
   <case>__top_idx / __top_val  the 16 largest logits of every step
 Only data is committed; no reference source or binary.
 """
@@ -47,7 +54,15 @@ def swa_4b():
 CASES = {
     "g4b_512": ("gemma-3-4b", 4343, 512, 64, dict(centered=True, swa_pattern=swa_4b())),
     "g27b": ("gemma-3-27b", 2727, 8, 6, dict(centered=True)),
+    "g4b_512f": ("gemma-3-4b", 4343, 512, 64, dict(centered=True, swa_pattern=swa_4b())),
 }
+FORCED = {"g4b_512f"}
+
+
+def inputs_of(case):
+    """The forced cases' step inputs: seeded random ids (step i feeds inputs[i] at position len(prompt) + i)."""
+    cfg_name, seed, _, n_steps, _ = CASES[case]
+    return np.random.default_rng(seed + 1).integers(4, CONFIGS[cfg_name].vocab, n_steps).astype(np.int32)
 
 
 def gguf_of(case):
@@ -70,6 +85,7 @@ def run_case(ref, case):
     lg = m.forward(prompt, 0)
     toks, tops_i, tops_v = [], [], []
     pos = len(prompt)
+    forced = inputs_of(case) if case in FORCED else None
     for step in range(n_steps + 1):
         idx = np.argsort(-lg, kind="stable")[:TOPK]
         tops_i.append(idx.astype(np.int32))
@@ -77,12 +93,15 @@ def run_case(ref, case):
         toks.append(int(np.argmax(lg)))
         if step == n_steps:
             break
-        lg = m.forward([toks[-1]], pos)
+        lg = m.forward([int(forced[step]) if forced is not None else toks[-1]], pos)
         pos += 1
     del m
-    return {f"{case}__sha": np.frombuffer(sha.encode(), np.uint8),
-            f"{case}__prompt": prompt, f"{case}__tokens": np.array(toks, np.int32),
-            f"{case}__top_idx": np.stack(tops_i), f"{case}__top_val": np.stack(tops_v)}
+    out = {f"{case}__sha": np.frombuffer(sha.encode(), np.uint8),
+           f"{case}__prompt": prompt, f"{case}__tokens": np.array(toks, np.int32),
+           f"{case}__top_idx": np.stack(tops_i), f"{case}__top_val": np.stack(tops_v)}
+    if forced is not None:
+        out[f"{case}__inputs"] = forced
+    return out
 
 
 def main():

@@ -11,11 +11,15 @@ Tolerances:
     Q8_0 activation re-quantization of every GEMV input, these ulp-level
     differences are amplified on random-init models: the reference vs the
     same reference with float64 attention differ by up to 3.7e-2 on mini-1b
-    (scripts/diag_parts.py).  Fast mode is therefore held to |dlogit| <=
-    6e-2 vs the oracle with float64 attention, and vs the reference to
-    6e-2 + |reference - f64-attention oracle| on the same input (the
-    reference's own attention rounding; 8.4e-2 on ModelTest's 2nd token),
-    with greedy token ids identical.
+    (scripts/diag_parts.py).  Fast mode is therefore held, per input, to the
+    reference's OWN distance from exact math: |fast - f64-attention oracle|
+    <= max(3e-3, 1.5 x |reference - f64-attention oracle|) -- ModelTest's
+    3e-3 where the reference is itself exact to that (model_test.gguf:
+    fast is 2.4e-7 from the oracle there), and never more than half again the
+    reference's own attention-rounding deviation (measured worst: fast 0.033
+    vs the reference's 0.037 on the same mini input) -- and vs the reference
+    to that budget + |reference - oracle|, with greedy token ids identical.
+    Cross-layout checks below (fused vs unfused launches) keep FAST_VS_REF.
   both modes: greedy token ids identical to the reference.
 """
 import os
@@ -25,7 +29,8 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-FAST_VS_REF = 6e-2
+FAST_VS_REF = 6e-2  # fused vs unfused fast layouts (reassociation through Q8_0 re-quantization)
+REF_TOL = 3e-3  # ModelTest's own tolerance (model_test.cpp:422)
 
 
 @pytest.fixture(scope="module", params=[True, False], ids=["exact", "fast"])
@@ -39,11 +44,12 @@ def check(got, ref, ideal, exact):
     else:
         print(f"fast: vs_ref {np.abs(got - ref).max():.3g} vs_f64attn {np.abs(got - ideal).max():.3g} "
               f"(ref vs f64attn {np.abs(ref - ideal).max():.3g})")
-        # the f64-attention restatement is the target; vs the reference itself
-        # the budget grows by the reference's own attention-rounding deviation
-        # measured on this very input (|ref - ideal|)
-        np.testing.assert_allclose(got, ideal, atol=FAST_VS_REF, rtol=0)
-        np.testing.assert_allclose(got, ref, atol=FAST_VS_REF + float(np.abs(ref - ideal).max()), rtol=0)
+        # the f64-attention restatement is the target, held to the reference's own distance from it on this very
+        # input (|ref - ideal|, its f16 accumulator's rounding), floored at ModelTest's 3e-3
+        dev = float(np.abs(np.asarray(ref) - ideal).max())
+        budget = max(REF_TOL, 1.5 * dev)
+        np.testing.assert_allclose(got, ideal, atol=budget, rtol=0)
+        np.testing.assert_allclose(got, ref, atol=budget + dev, rtol=0)
 
 
 def test_model_test_gguf(oracle, golden_models, exact):
@@ -124,14 +130,48 @@ def test_session_errors():
     assert ei.value.status == "E_RANGE"
     with pytest.raises(LLMIError):
         m.forward([10], 0)  # vocab is 10
-    # attention features no Gemma-3 file sets are refused at load, never silently ignored
-    # (model.cpp:125-133, 492-518): ALiBi and the attention logit soft-cap
+    # ALiBi (model.cpp:125-128, 492-518), which no Gemma file sets, is refused at load, never silently ignored
     from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
-    for key in ("attention.max_alibi_bias", "attention.logit_softcapping"):
-        with pytest.raises(LLMIError) as ei:
-            Model(build_gemma3_gguf(CONFIGS["tiny"], seed=1, extra_meta={key: 8.0}), max_ctx=16)
-        assert ei.value.status == "E_GGUF" and key in str(ei.value)
-    Model(build_gemma3_gguf(CONFIGS["tiny"], seed=1, extra_meta={"attention.max_alibi_bias": 0.0}), max_ctx=16).close()
+    key = "attention.max_alibi_bias"
+    with pytest.raises(LLMIError) as ei:
+        Model(build_gemma3_gguf(CONFIGS["tiny"], seed=1, extra_meta={key: 8.0}), max_ctx=16)
+    assert ei.value.status == "E_GGUF" and key in str(ei.value)
+    Model(build_gemma3_gguf(CONFIGS["tiny"], seed=1, extra_meta={key: 0.0}), max_ctx=16).close()
+
+
+@pytest.mark.parametrize("path", ["default", "token_loop", "per_op"])
+def test_attention_softcap(oracle, golden_models, exact, path, monkeypatch):
+    """attention.logit_softcapping (model.cpp:130-133, 511-513) on the tiny model, cap 0.25 (it moves the logits
+    by 0.5): the reference's own logits (tests/golden/model_ref.npz tinycap, oracle pinned to them in
+    test_oracle_golden.py) -- exact mode bit-identical, fast mode within the module's budget of the f64-attention
+    oracle with the same cap -- through the batched prefill (default), the decode launches only (token_loop), and
+    the per-projection launches (per_op: no attention block / fused layer launches)."""
+    from llm_inference_amd.model import Model
+    from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
+    if path != "default":
+        monkeypatch.setenv("LLMI_NO_PREFILL", "1")
+    if path == "per_op":
+        monkeypatch.setenv("LLMI_NO_FUSE", "1")
+        monkeypatch.setenv("LLMI_NO_BLOCK", "1")
+    cap = float(golden_models["tinycap__cap"])
+    g = build_gemma3_gguf(CONFIGS["tiny"], seed=7, swa_pattern=[True, False, True],
+                          extra_meta={"attention.logit_softcapping": cap})
+    ideal = oracle.model(g, n_threads=4, max_ctx=64, attn_f64=True)
+    m = Model(g, exact=exact, max_ctx=64)
+    prompt = golden_models["tiny__prompt"]
+    ref_logits, ref_toks = golden_models["tinycap__logits"], golden_models["tinycap__tokens"]
+    lg = m.forward(prompt, 0)
+    check(lg, ref_logits[0], ideal.forward(prompt, 0), exact)
+    pos = len(prompt)
+    for i in range(1, len(ref_toks)):
+        lg = m.forward([int(ref_toks[i - 1])], pos)
+        check(lg, ref_logits[i], ideal.forward([int(ref_toks[i - 1])], pos), exact)
+        pos += 1
+    m.close()
+    m = Model(g, exact=exact, max_ctx=64)
+    first = int(np.argmax(m.forward(prompt, 0)))
+    assert [first] + m.generate(first, len(prompt), len(ref_toks) - 1).tolist() == ref_toks.tolist()
+    m.close()
 
 
 def test_unfused_fast_path_matches_fused(oracle, monkeypatch):
@@ -274,3 +314,28 @@ def test_kquant_fused_matches_unfused(oracle, monkeypatch, vtype):
     first = int(np.argmax(lf))
     assert first == int(np.argmax(lp))
     assert fused.generate(first, len(prompt), 8).tolist() == plain.generate(first, len(prompt), 8).tolist()
+
+
+def test_attention_softcap_exact_engine(oracle):
+    """The soft-cap in the exact-order engine (k_exact.hip, taken on real 4B layer shapes): logits and greedy ids
+    bit-identical to the oracle with the same cap (the oracle's soft-cap is pinned to the reference's own logits
+    in test_oracle_golden.py::test_tiny_model_prefill_decode[tinycap])."""
+    from llm_inference_amd.model import Model
+    from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
+    cfg = CONFIGS["mini-4b"]
+    g = build_gemma3_gguf(cfg, seed=3, extra_meta={"attention.logit_softcapping": 0.25})
+    plain = oracle.model(build_gemma3_gguf(cfg, seed=3), n_threads=8, max_ctx=64)
+    om = oracle.model(g, n_threads=8, max_ctx=64)
+    m = Model(g, exact=True, max_ctx=64)
+    assert m.get_info().exact_engine == 1
+    prompt = np.random.default_rng(5).integers(4, cfg.vocab, 12).astype(np.int32)
+    ref = om.forward(prompt, 0)
+    assert np.abs(ref - plain.forward(prompt, 0)).max() > 1e-2  # the cap changes this model's logits
+    got = m.forward(prompt, 0)
+    np.testing.assert_array_equal(got.view(np.uint32), ref.view(np.uint32))
+    toks_ref, pos = [int(np.argmax(ref))], len(prompt)
+    for _ in range(7):
+        toks_ref.append(int(np.argmax(om.forward([toks_ref[-1]], pos))))
+        pos += 1
+    assert [int(np.argmax(got))] + m.generate(int(np.argmax(got)), len(prompt), 7).tolist() == toks_ref
+    m.close()

@@ -114,12 +114,15 @@ def test_model_test_forward(oracle, golden_models):
     assert abs(l2.sum() - 2.540453) < 0.003
 
 
-def test_tiny_model_prefill_decode(oracle, golden_models):
+@pytest.mark.parametrize("case", ["tiny", "tinycap"])
+def test_tiny_model_prefill_decode(oracle, golden_models, case):
+    """tinycap: the same model with attention.logit_softcapping 0.25 (model.cpp:511-513)."""
     from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
-    g = build_gemma3_gguf(CONFIGS["tiny"], seed=7, swa_pattern=[True, False, True])
+    extra = {"attention.logit_softcapping": float(golden_models["tinycap__cap"])} if case == "tinycap" else None
+    g = build_gemma3_gguf(CONFIGS["tiny"], seed=7, swa_pattern=[True, False, True], extra_meta=extra)
     m = oracle.model(g)
     prompt = golden_models["tiny__prompt"]
-    ref_logits, ref_toks = golden_models["tiny__logits"], golden_models["tiny__tokens"]
+    ref_logits, ref_toks = golden_models[f"{case}__logits"], golden_models[f"{case}__tokens"]
     lg = m.forward(prompt, 0)
     np.testing.assert_array_equal(bits(lg), bits(ref_logits[0]))
     pos = len(prompt)
