@@ -66,24 +66,52 @@ def pmc_key(a) -> str:
     return f"{a.config}/{a.quant}/pos{a.prefill + a.warmup + a.steps}/reps{a.kernel_reps}"
 
 
-def pmc_traffic(kernel_substr: str, key: str):
+def pmc_traffic(kernel_substr: str, key: str, kv_bytes_per_key: float = 0.0):
     """HBM bytes per launch of the kernel whose name contains kernel_substr,
     from the newest committed rocprofv3 --pmc FETCH_SIZE pass (profiles/,
     x2 gfx950 correction: scripts/pmc_summary.py) OF THE SAME WORKLOAD (`key`,
     pmc_key), over that pass's last dispatches of the kernel -- the ones the
     bench's roofline timing (Model.time_kernel, after the decode loop) made, at
-    the position it reports; (None, None) when no such pass is committed."""
+    the position it reports.  With no pass at this position, the pass of the
+    same model / weights / reps nearest in position, its bytes moved by the KV
+    history difference (kv_bytes_per_key per key attended: the attention
+    block's only position-dependent stream; 0 for the GEMVs and the screening
+    table), and the source says so.  (None, None) when no such pass is
+    committed."""
     import glob
+    import re
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_fetch*.json")))
-    for f in reversed(files):
-        d = json.load(open(f))
-        if d.get("config") != key:
-            continue
+
+    def lookup(d):
         hits = [v for k, v in d.get("kernels", {}).items() if kernel_substr in k]
-        if hits:
-            v = max(hits, key=lambda h: h["dispatches"])
-            return round(v.get("hbm_bytes_tail_mean", v["hbm_bytes_mean"])), os.path.relpath(f, ROOT)
-    return None, None
+        if not hits:
+            return None
+        v = max(hits, key=lambda h: h["dispatches"])
+        return v.get("hbm_bytes_tail_mean", v["hbm_bytes_mean"])
+
+    passes = [(f, json.load(open(f))) for f in reversed(files)]
+    for f, d in passes:
+        if d.get("config") == key:
+            t = lookup(d)
+            if t is not None:
+                return round(t), os.path.relpath(f, ROOT)
+    m = re.fullmatch(r"(.*)/pos(\d+)/(reps\d+)", key)
+    if m is None:
+        return None, None
+    best = None
+    for f, d in passes:
+        mm = re.fullmatch(r"(.*)/pos(\d+)/(reps\d+)", d.get("config") or "")
+        if mm is None or (mm.group(1), mm.group(3)) != (m.group(1), m.group(3)):
+            continue
+        t = lookup(d)
+        if t is not None and (best is None or abs(int(mm.group(2)) - int(m.group(2))) < abs(best[0] - int(m.group(2)))):
+            best = (int(mm.group(2)), t, f)
+    if best is None:
+        return None, None
+    p0, t, f = best
+    delta = (int(m.group(2)) - p0) * kv_bytes_per_key
+    return round(t + delta), (f"{os.path.relpath(f, ROOT)} (pass at pos{p0}; "
+                              f"{'+' if delta >= 0 else '-'}{abs(delta):.0f} B of KV history to pos{m.group(2)})")
 
 
 class Dist:
@@ -355,7 +383,9 @@ def main():
     dom = fams.get(dom_name, {})
     kpat = {"layer_engine": "layer_engine_kernel", "ffn_engine": "ffn_engine_kernel", "attention_block": "attn_block_kernel", "gate_up": "gemv_q4_0_layer<8, 10, 10",
             "down": "gemv_q4_0_layer<1, 10, 5", "token_selection": "screen_gemv_kernel"}.get(dom_name, "-")
-    traffic, traffic_src = pmc_traffic(kpat, pmc_key(a))
+    # the attention block's position-dependent stream: K and V rows of every kv head, per key attended
+    kv_key = info.kv_bytes_per_pos / L if dom_name == "attention_block" else 0.0
+    traffic, traffic_src = pmc_traffic(kpat, pmc_key(a), kv_key)
     # the timed steps decode positions pos .. pos + steps - 1; the step at
     # position p attends to p + 1 keys, so the mean KV history read is
     # pos + (steps + 1) / 2 keys per layer

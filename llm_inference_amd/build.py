@@ -52,6 +52,11 @@ def _compile(src: str) -> str:
     return out
 
 
+# the measured-slower layer / FFN engines: only in the development variant that defines LLMI_DEV_ENGINES
+if "-DLLMI_DEV_ENGINES" not in FLAGS:
+    SOURCES = [s for s in SOURCES if s != "k_engine.hip"]
+
+
 def build(force: bool = False, jobs: int = 0) -> str:
     os.makedirs(OBJ, exist_ok=True)
     hdr_t = max(_mtime(os.path.join(CSRC, h)) for h in HEADERS + ["../../include/llmi.h"])

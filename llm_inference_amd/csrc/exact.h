@@ -55,7 +55,6 @@ struct XlArgs {
   float* out = nullptr;     // PLAIN / QUANT / PRE: [rows]
   float* hid = nullptr;     // GELU: [rows / 2]
   XBlock* hq = nullptr;     // GELU: [rows / 64]
-  int serial_norms = 0;     // set by the launcher (LLMI_EXACT_SERIAL_NORMS: the norm chains without speculation)
 };
 void launch_exact_gemv(const XlWeight& w, const XlArgs& a, int role, hipStream_t s);
 

@@ -735,18 +735,7 @@ __global__ __launch_bounds__(256) void attn_split_kernel(AttnArgs a, QKVArgs qa)
 
 template <int HD, int G>
 static void launch_split_g(const AttnArgs& a, const QKVArgs* fused, hipStream_t s) {
-  // LLMI_ATTN_KVD=2 (A/B): GQA pairs as two virtual kv heads of one q head (twice the work-groups, two merges)
-  static const int kvd_env = getenv("LLMI_ATTN_KVD") ? atoi(getenv("LLMI_ATTN_KVD")) : 1;
-  if constexpr (G == 2) {
-    if (kvd_env == 2 && (!a.q8k || HD % 256 == 0)) {
-      const dim3 grid(a.n_head_kv * 2, ATTN_NSPLIT);
-      if (fused)
-        hipLaunchKernelGGL((attn_split_kernel<HD, 1, true, 2>), grid, dim3(256), 0, s, a, *fused);
-      else
-        hipLaunchKernelGGL((attn_split_kernel<HD, 1, false, 2>), grid, dim3(256), 0, s, a, QKVArgs{});
-      return;
-    }
-  }
+  // (GQA pairs as two virtual kv heads of one q head measured slower on 27B: 213 vs 216 tok/s)
   const dim3 grid(a.n_head_kv, ATTN_NSPLIT);
   if (fused)
     hipLaunchKernelGGL((attn_split_kernel<HD, G, true>), grid, dim3(256), 0, s, a, *fused);
@@ -949,10 +938,9 @@ int wt_of_w(const DevWeight* w) {
 
 const BlockCfg* find_block_cfg(int nb_qkv, int nb_o, int hd, int g, int qrole, int wtq = 0, int wtqb = 0,
                                int wto = 0) {
-  static const bool no_kvd = getenv("LLMI_BLOCK_NO_KVD") != nullptr;  // A/B: whole GQA groups per work-group
   for (const auto& c : kBlockCfgs)
     if (c.nb_qkv == nb_qkv && c.nb_o == nb_o && c.hd == hd && c.g == g && c.qrole == qrole && c.wtq == wtq &&
-        c.wtqb == wtqb && c.wto == wto && !(no_kvd && c.kvd > 1))
+        c.wtqb == wtqb && c.wto == wto)
       return &c;
   return nullptr;
 }

@@ -126,11 +126,8 @@ __device__ __forceinline__ float xl_chain_spec(const float* s, int n, unsigned* 
 
 // the serial chain by the calling work-group: speculative where n splits into 2 NW segments of whole float4s
 template <int NW>
-__device__ __forceinline__ float xl_sumsq(const float* s, int n, float* s_out, bool serial) {
-#ifdef XL_DIAG_NOCHAIN  // development timing build (results wrong): the chains left out
-  return (float)n;
-#endif
-  if (n % (8 * NW) == 0 && !serial) return xl_chain_spec<NW>(s, n);
+__device__ __forceinline__ float xl_sumsq(const float* s, int n, float* s_out) {
+  if (n % (8 * NW) == 0) return xl_chain_spec<NW>(s, n);
   if ((threadIdx.x >> 6) == 0) {
     const float v = xl_chain(s, n);
     if ((threadIdx.x & 63) == 0) *s_out = v;
@@ -281,7 +278,7 @@ __global__ __launch_bounds__(NW * 64) void exact_gemv_kernel(const uint4* __rest
           if (own(k)) s_a4[k * T + t] = yv[k];
         __syncthreads();
         XL_MARK(1);
-        const float sc1 = xl_rms_scale(xl_sumsq<NW>(s_a, n, &s_scale[0], a.serial_norms), n, a.eps);
+        const float sc1 = xl_rms_scale(xl_sumsq<NW>(s_a, n, &s_scale[0]), n, a.eps);
         XL_MARK(2);
 #pragma unroll
         for (int k = 0; k < XL_K4; k++) {  // model.cpp:843-858: the post norm, then the residual add
@@ -302,7 +299,7 @@ __global__ __launch_bounds__(NW * 64) void exact_gemv_kernel(const uint4* __rest
         }
       __syncthreads();
       XL_MARK(3);
-      const float sc2 = xl_rms_scale(xl_sumsq<NW>(s_b, n, &s_scale[1], a.serial_norms), n, a.eps);
+      const float sc2 = xl_rms_scale(xl_sumsq<NW>(s_b, n, &s_scale[1]), n, a.eps);
       XL_MARK(4);
 #pragma unroll
       for (int k = 0; k < XL_K4; k++)
@@ -817,9 +814,7 @@ void launch_exact_attn(const XAttnArgs& a, hipStream_t s) {
 }
 
 void launch_exact_gemv(const XlWeight& w, const XlArgs& a_in, int role, hipStream_t s) {
-  static const bool serial = getenv("LLMI_EXACT_SERIAL_NORMS") != nullptr;  // A/B: the chains without speculation
   XlArgs a = a_in;
-  a.serial_norms = serial ? 1 : 0;
   if (!w.qs || w.nb % 4 || w.rows % 16) throw std::runtime_error("exact gemv: bad weight");
   if (role != XL_PLAIN && a.n != w.nb * 32) throw std::runtime_error("exact gemv: input length != cols");
   if (role == XL_GELU && w.rows % 64) throw std::runtime_error("exact gemv: GELU rows % 64 != 0");

@@ -177,7 +177,9 @@ const LayerCfg kLayerCfgs[] = {
     // work-group of the tp-8 rank's 84; P does not change a row's pass order: 2.12-2.13 vs 2.08 ms per rank token,
     // and the 2-row-wave qkv shard 2.13; not kept)
     LLMI_LCFG(168, ROLE_GELU, 8, 8, 4, 11, true, false, 1),    // 27B 43008 rows, H 32 -> 672 WGs
-    LLMI_LCFG(168, ROLE_GELU_X, 8, 8, 4, 1, true, false, 1),   // 27B gate_up on the norm launch's x blocks
+#ifdef LLMI_DEV_ENGINES  // LLMI_GELU_X (development variant): 27B gate_up on the norm launch's x blocks
+    LLMI_LCFG(168, ROLE_GELU_X, 8, 8, 4, 1, true, false, 1),
+#endif
     // PLAIN down: the GELU launch (32 units per work-group) wrote the Q8_0 blocks (LayerGemv::hq), so the down
     // launch copies 24-42 KB of blocks instead of quantizing the whole f32 hid in every work-group
     // (scripts/gemv_sweep 27b.down: plain R1 NW8 P6 15.0 us vs quant 19.5 us)
@@ -213,9 +215,8 @@ int wt_of(uint32_t type) { return type == T_Q4_K ? WT_Q4_K : type == T_Q6_K ? WT
 // rows: the weight's row count (0: unknown -- only whole-matrix entries); shard entries come first in the table
 const LayerCfg* find_cfg(int nb, int role, uint32_t type = T_Q4_0, int rows = 0) {
   if (type != T_Q4_0 && type != T_Q8_0 && type != T_Q4_K && type != T_Q6_K) return nullptr;
-  static const bool no_shard = getenv("LLMI_NO_SHARD_CFG") != nullptr;  // A/B: whole-matrix entries only
   for (const auto& c : kLayerCfgs) {
-    if (c.rows_max > 0 && (no_shard || rows <= 0 || rows > c.rows_max)) continue;
+    if (c.rows_max > 0 && (rows <= 0 || rows > c.rows_max)) continue;
     if (c.nb == nb && c.role == role && c.w8 == (type == T_Q8_0) && c.wt == wt_of(type)) return &c;
   }
   return nullptr;

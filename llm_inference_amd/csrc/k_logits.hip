@@ -359,12 +359,11 @@ void launch_screen_argmax(const DevWeight& table, const ScreenTable& st, const u
   if (nb > 256) throw std::runtime_error("screen: n_embd > 8192");
   if (!prepped) hipLaunchKernelGGL(screen_prep_kernel, dim3(1), dim3(1024), 0, s, x16, n, st.xs, st.m_key);
   const int rows = table.rows;
-  static const int wpc = getenv("LLMI_SCREEN_WPC") ? atoi(getenv("LLMI_SCREEN_WPC")) : 8;  // waves per CU (A/B)
-  // row groups in flight per lane group (A/B on the 4B bench: 1 -> 2 = 132.8 -> 127.7 us; 4 or 12 waves per CU slower)
-  static const int ahead = getenv("LLMI_SCREEN_AHEAD") ? atoi(getenv("LLMI_SCREEN_AHEAD")) : 2;
-  // lanes per row: a quarter wave for short rows (<= 80 chunks: the 1B table's 72), else half a wave
-  static const int lpr_env = getenv("LLMI_SCREEN_LPR") ? atoi(getenv("LLMI_SCREEN_LPR")) : 0;
-  const int lpr = lpr_env == 16 || lpr_env == 32 ? lpr_env : (2 * nb <= 80 ? 16 : 32);
+  constexpr int wpc = 8;  // waves per CU (4B bench: 4, 12 and 16 slower, profiles/r03_screen_sweep.txt)
+  // row groups in flight per lane group (4B bench: 1 -> 2 = 132.8 -> 127.7 us)
+  constexpr int ahead = 2;
+  // lanes per row: a quarter wave for short rows (<= 80 chunks: the 1B table's 72; 91 -> 74 us), else half a wave
+  const int lpr = 2 * nb <= 80 ? 16 : 32;
   const int cpl = (2 * nb + lpr - 1) / lpr, rpw = 64 / lpr;
   const dim3 grid((std::min((rows + rpw - 1) / rpw, 256 * wpc) + 3) / 4);
   auto go = [&](auto kern) {

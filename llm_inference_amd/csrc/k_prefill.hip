@@ -1487,7 +1487,7 @@ void launch_prefill_norm(const PrefillNorm& a, int T, hipStream_t s) {
   if (a.n > 256 * PN_EPT || a.n % 32) throw std::runtime_error("prefill_norm: n_embd");
   if (a.q8k && (a.n % 256 || a.x16)) throw std::runtime_error("prefill_norm: Q8_K blocks need n % 256 == 0");
   const int eb = (a.n / 32 + 63) / 64;
-  if (!a.table && eb <= 3 && !getenv("LLMI_PREFILL_NORM_V1")) {
+  if (!a.table && eb <= 3) {
     switch (eb) {
       case 1: hipLaunchKernelGGL(prefill_norm_res_kernel<1>, dim3(T), dim3(256), 0, s, a); break;
       case 2: hipLaunchKernelGGL(prefill_norm_res_kernel<2>, dim3(T), dim3(256), 0, s, a); break;
@@ -1554,10 +1554,7 @@ static bool try_gemm6(const PrefillGemm16& a, hipStream_t s) {
 
 template <int WQ>
 static bool gemm6_geometry(const PrefillGemm16& a, hipStream_t s) {
-  const char* f = getenv("LLMI_PG6");
-  const std::string c = f ? f : a.nb >= 160 ? "k4" : "k2";
-  if (c == "big" && try_gemm6<4, 2, 1, 2, 2, 3, WQ>(a, s)) return true;
-  if (c == "k4" && try_gemm6<2, 1, 4, 2, 4, 3, WQ>(a, s)) return true;
+  if (a.nb >= 160 && try_gemm6<2, 1, 4, 2, 4, 3, WQ>(a, s)) return true;
   return try_gemm6<2, 2, 2, 2, 2, 3, WQ>(a, s);
 }
 
@@ -1566,7 +1563,7 @@ bool prefill_gemm16_supported(const DevWeight& w) {
   return (w.type == T_Q4_K || w.type == T_Q6_K) && w.kq && w.rows % 64 == 0 && w.cols % 256 == 0;
 }
 
-// v6 geometry (LLMI_PG6=<name> forces one for A/B); the K split depends on K alone (tensor-parallel shards
+// v6 geometry: the K split depends on K alone (tensor-parallel shards
 // sum in the same order as the whole weight)
 void launch_prefill_gemm16(const DevWeight& w, const uint16_t* x, int xstride, int T, float* out, int ostride,
                            hipStream_t s) {
@@ -1686,7 +1683,7 @@ void launch_prefill_gelu(const float* gu, int F, int H, XBlock* xq, int xstride,
   if (q8k && (H % 8 || F % 256)) throw std::runtime_error("prefill_gelu: Q8_K output needs H % 8 == 0, F % 256 == 0");
   if (F % 32 || H <= 0 || F % H) throw std::runtime_error("prefill_gelu: shape");
   if (x16 && H % 8) throw std::runtime_error("prefill_gelu: f16 output needs H % 8 == 0");
-  if (H % 8 == 0 && (x16 || q8k || !getenv("LLMI_PREFILL_GELU_V1"))) {
+  if (H % 8 == 0) {
     hipLaunchKernelGGL(prefill_gelu8_kernel, dim3((F / 8 + 255) / 256, T), dim3(256), 0, s, gu, F, H, xq, xstride, x16,
                        x16stride, q8k);
     LLMI_HIP(hipGetLastError());

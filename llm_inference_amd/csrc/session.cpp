@@ -427,25 +427,6 @@ void Session::upload(const GGUFView& g) {  // model.cpp:169-238 tensor map
       relayout(Ld.down.w, LAYER_QUANT);
     }
   }
-  // LLMI_SHARE_LAYERS=N (diagnostics, timing only -- results are wrong): layer
-  // l >= N reads layer l % N's weights, so the per-token weight working set
-  // is N layers (cache-residency experiments)
-  if (const char* sh = getenv("LLMI_SHARE_LAYERS")) {
-    const int N = std::max(1, atoi(sh));
-    for (int l = N; l < hp_.n_layer; l++) {
-      LayerDev& Ld = L_[l];
-      for (auto& p : Ld.qkv) free_weight(p.w);
-      for (auto& p : Ld.gate_up) free_weight(p.w);
-      free_weight(Ld.o.w);
-      free_weight(Ld.down.w);
-      const LayerDev& S = L_[l % N];
-      Ld.qkv = S.qkv;
-      Ld.o = S.o;
-      Ld.gate_up = S.gate_up;
-      Ld.down = S.down;
-      Ld.aliased = true;
-    }
-  }
 }
 
 void Session::alloc_buffers() {
@@ -658,7 +639,6 @@ void Session::release() {
   free_screen_table(scr_);
   for (auto& l : L_) {
     for (XlWeight* x : {&l.xqkv, &l.xo, &l.xgu, &l.xdn}) free_xl_weight(*x);
-    if (l.aliased) continue;  // LLMI_SHARE_LAYERS: another layer's weights
     for (auto& p : l.qkv) free_weight(p.w);
     for (auto& p : l.gate_up) free_weight(p.w);
     free_weight(l.o.w);
@@ -717,20 +697,18 @@ void Session::gemv_parts(const std::vector<GemvPart>& parts, const float* x, int
 // One decode token.  Reads *d_token_/*d_pos_, ends with the token feedback.
 // the down projection as a PLAIN launch on the GELU launch's Q8_0 blocks: one device (a rank's hid slice is
 // all-gathered as f32), 32 hidden units per GELU work-group, a PLAIN table entry for the shape
-// (LLMI_DOWN_QUANT=1 keeps the QUANT launch, A/B)
+// (27B down 19.3 -> 14.5 us against the QUANT launch, profiles/r02_down_plain_ab.txt)
 bool Session::down_plain(const LayerDev& Ld) const {
-  static const bool off = getenv("LLMI_DOWN_QUANT") != nullptr;
   const DevWeight& g = Ld.gate_up[0].w;
   // a tensor-parallel rank: its GELU blocks are all-gathered instead of its f32 hid (whole blocks per rank)
-  return !off && (!tp_ || f_sh_ % 32 == 0) && (Ld.down.w.type == T_Q4_0 || Ld.down.w.type == T_Q8_0) &&
+  return (!tp_ || f_sh_ % 32 == 0) && (Ld.down.w.type == T_Q4_0 || Ld.down.w.type == T_Q8_0) &&
          layer_gemv_gelu_group(g.cols, g.type) == 32 && layer_gemv_supported(Ld.down.w, LAYER_PLAIN);
 }
 
 // the screened token selection's step 1 (k_logits.hip screen_prep) in the final norm's launch: its x16 blocks,
-// A and the M reset from the same f16 roundings (LLMI_SCREEN_PREP=1 keeps the separate launch, A/B)
+// A and the M reset from the same f16 roundings
 void Session::screen_norm(NormOut& o) {
-  static const bool sep = getenv("LLMI_SCREEN_PREP") != nullptr;
-  if (sep || !rec_gen_ || !screen_ || o.x16 != act_.x16 || hp_.n_embd > 8192) return;
+  if (!rec_gen_ || !screen_ || o.x16 != act_.x16 || hp_.n_embd > 8192) return;
   o.scr = scr_.xs;
   o.scr_mkey = scr_.m_key;
   scr_prepped_ = true;
@@ -755,10 +733,9 @@ static NormOut norm_out_for(const std::vector<GemvPart>& consumer, float* xn, co
 NormOut Session::embed_out() const { return norm_out_for(L_[0].qkv, xn_, act_, ex_norm_); }
 
 // the decode-loop graph may end with the next token's embed_norm (launch_finalize_embed_norm): one launch fewer
-// per token (LLMI_NO_EMBED_FOLD=1 keeps finalize_token + embed_norm, A/B)
+// per token
 bool Session::embed_fold_ok() const {
-  static const bool off = getenv("LLMI_NO_EMBED_FOLD") != nullptr;
-  return !off && use_graph_ && screen_ && (embd_.type == T_F16 || embd_.type == T_Q8_0) && !ple_table_.qs;
+  return use_graph_ && screen_ && (embd_.type == T_F16 || embd_.type == T_Q8_0) && !ple_table_.qs;
 }
 
 void Session::record_step(hipStream_t s, bool gen, bool fold_embed) {
@@ -1440,7 +1417,11 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
     // residual + FFN norm as their own launch too, and gate_up on its x blocks -- gate_up 29.4 -> 24.6 us (672
     // work-groups no longer re-read 86 KB of prologue operands each), but the one-work-group norm launch takes
     // 5.7 us: 214.8 vs 214.9 tok/s
+#ifdef LLMI_DEV_ENGINES  // development variant only (measured at parity)
     static const bool gelu_x_env = getenv("LLMI_GELU_X") != nullptr;
+#else
+    constexpr bool gelu_x_env = false;
+#endif
     const bool gelu_x = gelu_x_env && block_ && !block_pro_ && !dump_ &&
                         layer_gemv_supported(Ld.gate_up[0].w, LAYER_GELU_X);
     if (gelu_x) {

@@ -51,7 +51,6 @@ struct LayerDev {
   bool is_swa = false;
   bool gu_interleaved = false;  // gate_up rows in groups of 32 (k_layer.hip GELU epilogue)
   bool fused = false;           // every projection runs as gemv_q4_0_layer
-  bool aliased = false;         // LLMI_SHARE_LAYERS diagnostics: weights owned by another layer
   int hd = 0;
   uint16_t *kc = nullptr, *vc = nullptr;
   // Gemma-4

@@ -121,6 +121,10 @@ struct EngineLayer {
   unsigned long long* trace = nullptr;  // development: [CU][16] phase clocks (LLMI_BLOCK_TRACE builds)
   unsigned* blk_epoch = nullptr;        // FFN engine: the attention block's per-layer epoch, advanced at the end
 };
+// The engines were measured slower than the three launches per layer: they are built
+// only into the development variant (LLMI_VARIANT=engines LLMI_EXTRA_FLAGS=-DLLMI_DEV_ENGINES ->
+// libllmi_engines.so, loaded with LLMI_LIB=...), never into libllmi.so, whose plans report "no fit".
+#ifdef LLMI_DEV_ENGINES
 // fills the per-CU split of `a` and checks the launch fits (shapes, LDS, occupancy)
 bool engine_plan(int E, int F, int n_head, int n_kv, int hd, int qkv_rows, EngineLayer& a);
 void launch_layer_engine(const EngineLayer& a, bool first, hipStream_t s);
@@ -128,6 +132,12 @@ void launch_layer_engine(const EngineLayer& a, bool first, hipStream_t s);
 // block's o output; gate_up interleaved in groups of ru, row-major; the down rows with >= 8 KB of slack)
 bool ffn_engine_plan(int E, int F, EngineLayer& a);
 void launch_ffn_engine(const EngineLayer& a, hipStream_t s);
+#else
+inline bool engine_plan(int, int, int, int, int, int, EngineLayer&) { return false; }
+inline void launch_layer_engine(const EngineLayer&, bool, hipStream_t) {}
+inline bool ffn_engine_plan(int, int, EngineLayer&) { return false; }
+inline void launch_ffn_engine(const EngineLayer&, hipStream_t) {}
+#endif
 bool layer_gemv_supported(const DevWeight& w, int role);
 // ---- batched prefill (k_prefill.hip) ----
 struct PrefillNorm {  // per token: embedding (table != null) or residual + norm, then x -> Q8_0

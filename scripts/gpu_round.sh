@@ -30,10 +30,14 @@ if want prof; then  # the timed decode graph itself (hipGraph replay), after a 5
   run rocprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- \
     python3 bench.py --steps 64 --warmup 4 --prefill 512 --no-cpu-baseline
 fi
-if want pmc; then  # FETCH_SIZE of the launches the default bench line times: position 784 (512 + 16 + 256), 2 reps
-  run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- \
-    python3 bench.py --prefill 768 --warmup 2 --steps 14 --no-cpu-baseline
-  python3 scripts/pmc_summary.py gpurun_out/pmc_fetch/run_counter_collection.csv gpurun_out/pmc_fetch_summary.json \
-    gemma-3-4b/q4_0/pos784/reps2 68 > gpurun_out/pmc_summary.log 2>&1
+if want pmc; then  # FETCH_SIZE of the launches the bench line times, 2 reps, at the position it ends on:
+  # 784 = the default line (512 + 16 + 256), 537 = the driver's line (512 + 25 decode steps)
+  for spec in "784 768 2 14" "537 512 5 20"; do
+    set -- $spec
+    run pmc_fetch_$1 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch_$1 -o run -- \
+      python3 bench.py --prefill $2 --warmup $3 --steps $4 --no-cpu-baseline
+    python3 scripts/pmc_summary.py gpurun_out/pmc_fetch_$1/run_counter_collection.csv \
+      gpurun_out/pmc_fetch_summary_$1.json gemma-3-4b/q4_0/pos$1/reps2 68 > gpurun_out/pmc_summary_$1.log 2>&1
+  done
 fi
 echo "== done"

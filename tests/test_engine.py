@@ -2,7 +2,10 @@
 decode layer as ONE launch of one 1024-thread work-group per CU.
 
 Opt-in (LLMI_ENGINE=1; measured slower than the default three launches per
-layer).  Parity bar (the fast path's,
+layer) and built only into the development variant
+(LLMI_VARIANT=engines LLMI_EXTRA_FLAGS=-DLLMI_DEV_ENGINES python -m
+llm_inference_amd.build; run these tests with
+LLMI_LIB=llm_inference_amd/libllmi_engines.so), never into libllmi.so.  Parity bar (the fast path's,
 tests/test_hip_model.py): logits within 6e-2 of the oracle with float64
 attention (= the reference's arithmetic with exact attention, pinned to the
 reference build), greedy token ids identical to the oracle's.  Against the
@@ -12,10 +15,14 @@ budget and its ids must be identical.  Cases: Gemma-3 1B and 4B layer shapes,
 decode positions inside the first key tile, past 32 tiles (a split walks two
 tiles, the later one loaded inside the loop), and at tile boundaries.
 """
+import os
+
 import numpy as np
 import pytest
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(not os.environ.get("LLMI_LIB", "").endswith("libllmi_engines.so"),
+                                 reason="the engines are in the development variant only (LLMI_LIB=...engines.so)")]
 FAST_VS_REF = 6e-2
 
 

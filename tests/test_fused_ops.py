@@ -7,6 +7,8 @@ norm, the logits / screened token, and every prefill_gemm_kernel output
 row -- each against the oracle restatement of the reference op computed
 from the device's OWN inputs to that launch (tests/oplevel.py states the
 per-tensor tolerances and why)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -83,6 +85,8 @@ def test_ops_mini27b_shapes(oracle):
     _run(oracle, "mini-27b", 26, 8, 2, 64, swa_pattern=[True, False])
 
 
+@pytest.mark.skipif(not os.environ.get("LLMI_LIB", "").endswith("libllmi_engines.so"),
+                    reason="LLMI_GELU_X is in the development variant only (LLMI_LIB=...engines.so)")
 def test_ops_mini27b_gelu_x(oracle, monkeypatch):
     """LLMI_GELU_X=1 on the 27B shapes: the post-attention residual + FFN norm as their own launch and gate_up
     on its Q8_0 blocks (LAYER_GELU_X: the x-block prologue with the GELU epilogue), each op against the oracle."""
