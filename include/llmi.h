@@ -210,7 +210,8 @@ typedef struct {
   int layer_engine;           /* 1: each decode layer is ONE launch of the layer engine (one 1024-thread work-group
                                  per CU, the layer's weights issued at launch start: DESIGN.md section 4.3) */
   int ffn_engine;             /* 1: gate_up + GELU + down of each layer are ONE launch (the FFN engine) */
-  int tp_exchange;            /* tensor-parallel exchange: 0 none, 1 RCCL, 2 device copies, 3 one-shot push */
+  int tp_exchange;            /* tensor-parallel exchange: 0 none, 1 RCCL, 2 device copies, 3 one-shot push, 4 one-shot
+                                 push fused into the decode launches (the default push mode) */
   long long block_slow_waits; /* attention-block hand-off waits (per wave) that took over 20 us, since creation */
   int exact_engine;           /* 1: LLMI_EXACT runs on the exact-order engine (k_exact.hip: the reference's
                                  arithmetic with streamed GEMVs and fused norms), 0: the per-op exact kernels */

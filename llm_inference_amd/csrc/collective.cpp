@@ -22,6 +22,7 @@ namespace llmi {
     if (r_ != ncclSuccess) throw hip_error(std::string(#call) + ": " + ncclGetErrorString(r_)); \
   } while (0)
 
+void Collective::fused_link(PxLink&) { throw std::runtime_error("fused exchange: not a push-exchange session"); }
 void Collective::peer_handle(void*) const { throw std::runtime_error("peer handle: not a push-exchange (LLMI_TP_PEER) session"); }
 void Collective::peer_connect(const void*) { throw std::runtime_error("peer connect: not a push-exchange (LLMI_TP_PEER) session"); }
 
@@ -119,19 +120,42 @@ class Mailbox {
     seed(seed_from(h));
   }
   // the all-gather of `bytes` per rank at buf (rank q's slice at buf + q bytes), as `phase` launches
-  void run(void* buf, size_t bytes, int phase, hipStream_t s) {
-    for (size_t c = 0; c < chunks(bytes); c++) run_chunk(buf, bytes, c, phase, s);
+  void run(void* buf, size_t bytes, int phase, hipStream_t s, int skip) {
+    for (size_t c = 0; c < chunks(bytes); c++) run_chunk(buf, bytes, c, phase, s, c == 0 ? skip : 0);
   }
+  // column slices (Collective::all_gather_cols): `rows` rows of pitch bytes, rank q's slice of slice bytes each
+  void run_cols(void* buf, size_t pitch, size_t slice, int rows, int phase, hipStream_t s, int skip) {
+    for (size_t c = 0; c < chunks(slice * rows); c++)
+      run_chunk(buf, slice * rows, c, phase, s, c == 0 ? skip : 0, pitch, slice);
+  }
+  // the mailboxes as the fused exchanges see them (px.h)
+  void link(PxLink& l) const {
+    if (!connected()) throw std::runtime_error("push exchange: peers not connected (llmi_session_peer_connect)");
+    l = PxLink{};
+    for (int q = 0; q < G_; q++) l.mail[q] = peers_[q];
+    l.ctl = ctl_;
+    l.err = reinterpret_cast<int*>(ctl_ + 2);
+    l.timeout = timeout_;
+    l.slot_w = (uint32_t)kSlot;
+    l.rank = rank_;
+    l.G = G_;
+  }
+  static constexpr int cap() { return kCap; }
   // a chunked message is a sequence of exchanges: the split (push / gather) caller needs them one at a time
   static size_t chunks(size_t bytes) { return (bytes / 4 + kCap - 1) / kCap; }
-  void run_chunk(void* buf, size_t bytes, size_t c, int phase, hipStream_t s) {
+  // pitch / slice (bytes, column slices of rows) or 0 (the message contiguous per rank)
+  void run_chunk(void* buf, size_t bytes, size_t c, int phase, hipStream_t s, int skip = 0, size_t pitch = 0,
+                 size_t slice = 0) {
     if (!connected()) throw std::runtime_error("push exchange: peers not connected (llmi_session_peer_connect)");
-    if (bytes % 4) throw std::runtime_error("push exchange: slice bytes % 4 != 0");
+    if (bytes % 4 || pitch % 4 || slice % 4) throw std::runtime_error("push exchange: bytes % 4 != 0");
     const size_t words = bytes / 4, off = c * kCap;
     PushArgs a{};
     for (int q = 0; q < G_; q++) a.mail[q] = peers_[q];
-    a.buf = static_cast<uint32_t*>(buf) + off;
+    a.buf = static_cast<uint32_t*>(buf);
+    a.off = off;
     a.stride = words;
+    a.pitch = pitch / 4;
+    a.row_w = (int)(slice / 4);
     a.words = (int)std::min<size_t>(kCap, words - off);
     a.rank = rank_;
     a.G = G_;
@@ -141,6 +165,7 @@ class Mailbox {
     a.ticket = ctl_ + 1;
     a.err = reinterpret_cast<int*>(ctl_ + 2);
     a.timeout = timeout_;
+    a.skip = skip;
     launch_push_exchange(a, s);
   }
   int failed() {  // reads and clears the device flag (callers have synchronised the stream)
@@ -166,7 +191,15 @@ class PeerCollective : public Collective {
   PeerCollective(int rank, int size) : Collective(rank, size), mb_(rank, size) {}
   bool graph_safe() const override { return true; }
   int kind() const override { return EX_PUSH; }
-  void all_gather(void* buf, size_t bytes, hipStream_t s) override { mb_.run(buf, bytes, PX_PUSH | PX_GATHER, s); }
+  void all_gather(void* buf, size_t bytes, hipStream_t s, int skip) override {
+    mb_.run(buf, bytes, PX_PUSH | PX_GATHER, s, skip);
+  }
+  bool all_gather_cols(void* buf, size_t pitch, size_t slice, int rows, hipStream_t s, int skip) override {
+    mb_.run_cols(buf, pitch, slice, rows, PX_PUSH | PX_GATHER, s, skip);
+    return true;
+  }
+  bool fused_capable() const override { return true; }
+  void fused_link(PxLink& l) override { mb_.link(l); }
   int failed() override { return mb_.failed(); }
   void peer_handle(void* out) const override { mb_.handle(out); }
   void peer_connect(const void* handles) override { mb_.open(handles); }
@@ -187,7 +220,7 @@ class RcclCollective : public Collective {
   }
   bool graph_safe() const override { return true; }
   int kind() const override { return EX_RCCL; }
-  void all_gather(void* buf, size_t bytes, hipStream_t s) override {
+  void all_gather(void* buf, size_t bytes, hipStream_t s, int) override {
     char* b = static_cast<char*>(buf);
     LLMI_NCCL(ncclAllGather(b + (size_t)rank_ * bytes, b, bytes, ncclUint8, comm_, s));
   }
@@ -229,8 +262,29 @@ class LocalCollective : public Collective {
   bool graph_safe() const override { return false; }
   int kind() const override { return push_ ? EX_PUSH : EX_COPY; }
   int failed() override { return push_ ? mb_->failed() : 0; }
-  void all_gather(void* buf, size_t bytes, hipStream_t s) override {
-    if (push_) return push_gather(buf, bytes, s);
+  bool fused_capable() const override { return push_; }
+  void fused_link(PxLink& l) override {
+    if (!push_) Collective::fused_link(l);
+    connect();
+    mb_->link(l);
+  }
+  // every rank's producing launch has completed before this rank's consumer runs (the ranks' streams share the
+  // process's hardware queues: a consumer spinning ahead of a peer's producer could block it)
+  void fused_point(hipStream_t s) override {
+    LocalGroup& g = *g_;
+    LLMI_HIP(hipEventRecord(g.ready[rank_], s));
+    g.barrier();
+    for (int q = 0; q < size_; q++)
+      if (q != rank_) LLMI_HIP(hipStreamWaitEvent(s, g.ready[q], 0));
+    g.barrier();  // nobody re-records its event before every peer has waited on it
+  }
+  bool all_gather_cols(void* buf, size_t pitch, size_t slice, int rows, hipStream_t s, int skip) override {
+    if (!push_) return false;
+    push_gather(buf, slice * rows, s, skip, pitch, slice);
+    return true;
+  }
+  void all_gather(void* buf, size_t bytes, hipStream_t s, int skip) override {
+    if (push_) return push_gather(buf, bytes, s, skip);
     LocalGroup& g = *g_;
     char* b = static_cast<char*>(buf);
     // 1. publish this rank's buffer once its slice is written
@@ -254,20 +308,23 @@ class LocalCollective : public Collective {
  private:
   // push launch, host barrier, then the gather launch once every peer's push has run (the ranks' streams
   // share this process's hardware queues: a gather spinning ahead of a peer's push could block it)
-  void push_gather(void* buf, size_t bytes, hipStream_t s) {
+  void connect() {  // first exchange: every rank has registered its mailbox
+    if (mb_->connected()) return;
+    g_->barrier();
+    for (int q = 0; q < size_; q++) mb_->set_peer(q, g_->mail[q]);
+  }
+  void push_gather(void* buf, size_t bytes, hipStream_t s, int skip, size_t pitch = 0, size_t slice = 0) {
     LocalGroup& g = *g_;
-    if (!mb_->connected()) {  // first exchange: every rank has registered its mailbox
-      g.barrier();
-      for (int q = 0; q < size_; q++) mb_->set_peer(q, g.mail[q]);
-    }
+    connect();
     for (size_t c = 0; c < Mailbox::chunks(bytes); c++) {
+      const int sk = c == 0 ? skip : 0;
       if (drop_) drop_ = false;  // the test hook: the peers' gathers wait past their bound
-      else mb_->run_chunk(buf, bytes, c, PX_PUSH, s);
+      else mb_->run_chunk(buf, bytes, c, PX_PUSH, s, sk, pitch, slice);
       LLMI_HIP(hipEventRecord(g.ready[rank_], s));
       g.barrier();
       for (int q = 0; q < size_; q++)
         if (q != rank_) LLMI_HIP(hipStreamWaitEvent(s, g.ready[q], 0));
-      mb_->run_chunk(buf, bytes, c, PX_GATHER, s);
+      mb_->run_chunk(buf, bytes, c, PX_GATHER, s, sk, pitch, slice);
       g.barrier();  // nobody records its next push event before every peer has waited on this one
     }
   }
@@ -284,7 +341,7 @@ class NullCollective : public Collective {
   using Collective::Collective;
   bool graph_safe() const override { return true; }
   int kind() const override { return EX_NONE; }
-  void all_gather(void*, size_t, hipStream_t) override {}
+  void all_gather(void*, size_t, hipStream_t, int) override {}
 };
 
 }  // namespace

@@ -31,10 +31,12 @@
 #include <mutex>
 #include <vector>
 
+#include "px.h"
+
 namespace llmi {
 
 // exchange kinds (llmi_session_info.tp_exchange)
-enum { EX_NONE = 0, EX_RCCL = 1, EX_COPY = 2, EX_PUSH = 3 };
+enum { EX_NONE = 0, EX_RCCL = 1, EX_COPY = 2, EX_PUSH = 3, EX_PUSH_FUSED = 4 };
 
 class Collective {
  public:
@@ -44,8 +46,23 @@ class Collective {
   int size() const { return size_; }
   virtual bool graph_safe() const = 0;
   virtual int kind() const = 0;
-  // in place: this rank's slice is already at buf + rank * bytes
-  virtual void all_gather(void* buf, size_t bytes, hipStream_t s) = 0;
+  // in place: this rank's slice is already at buf + rank * bytes.  skip (push exchange): the fused exchanges
+  // (px.h) recorded since the previous standalone one -- this exchange's tag follows theirs
+  virtual void all_gather(void* buf, size_t bytes, hipStream_t s, int skip = 0) = 0;
+  // column slices of `rows` rows in place (rank q's slice of row i at buf + i * pitch + q * slice bytes), read and
+  // written by the exchange kernel itself; false: not supported (the caller packs, all_gathers and unpacks)
+  virtual bool all_gather_cols(void*, size_t, size_t, int, hipStream_t, int skip = 0) {
+    (void)skip;
+    return false;
+  }
+  // fused exchanges (px.h), push-exchange collectives only: the mailboxes as the launches see them (every
+  // message of ws <= fused_cap() words per rank); fused_point sits between a producing and a consuming launch (a
+  // LocalCollective makes every rank's producer complete first -- its ranks share one process's hardware queues
+  // -- others do nothing)
+  virtual bool fused_capable() const { return false; }
+  virtual void fused_link(PxLink& l);
+  static constexpr int fused_cap() { return 1 << 18; }
+  virtual void fused_point(hipStream_t) {}
   // the exchange failed on the device since the last call (a bounded wait timed out, or a received slice
   // failed its checksum); 0 = no.  The ranks' exchange counts may then differ: the session stops.
   virtual int failed() { return 0; }
@@ -58,19 +75,22 @@ class Collective {
 };
 
 // ---- the one-shot push all-gather (k_exchange.hip) ----
-constexpr int PX_MAX_RANKS = 16;
 constexpr int PX_MAX_WG = 64;  // work-groups per exchange launch (= checksum granules per sender slot)
 constexpr int PX_PUSH = 1, PX_GATHER = 2;
 struct PushArgs {
   uint2* mail[PX_MAX_RANKS];  // every rank's mailbox [2][G][cap + PX_MAX_WG] granules (this process's mapping)
-  uint32_t* buf;              // rank q's slice of this exchange at buf + q * stride (words)
-  size_t stride;
+  uint32_t* buf;              // word j of rank q's message at buf + q * stride + j (row_w == 0), or at
+  size_t stride;              // buf + (j / row_w) * pitch + q * row_w + j % row_w (column slices of rows)
+  size_t pitch;
+  int row_w;
+  size_t off;                 // this exchange's first word of the message (a chunk of a longer one)
   int words;                  // per rank, <= cap
   int rank, G, cap, phase;    // phase: PX_PUSH | PX_GATHER
   unsigned* epoch;            // seed - 1 + exchanges completed (tag = epoch + 1)
   unsigned* ticket;           // work-groups done with the gather (the last one advances epoch)
   int* err;                   // 1: a wait timed out; 2: a received slice failed its checksum
   uint64_t timeout;           // bound of every wait, in ticks of the 100 MHz wall clock
+  int skip;                   // fused exchanges since the previous standalone one: tag = epoch + 1 + skip
 };
 void launch_push_exchange(const PushArgs& a, hipStream_t s);
 constexpr int PEER_HANDLE_BYTES = 64;

@@ -333,17 +333,25 @@ struct Q8Act {
 // id, 1.5*2^23)), stored scale = f16(d).  Every lane of the 32-lane group must
 // execute this (lane swizzles), and the group is a half-wave (lanes 0-31 or
 // 32-63); `ok` masks the stores.
-__device__ __forceinline__ void q8_block_store(float v, bool ok, XBlock* blk, int e) {
+struct Q8Lane {  // one element's share of a half-wave's Q8_0 block
+  int q;          // its quant
+  float d;        // the block's f16-rounded scale
+  int nsum8;      // -8 x the block's quant sum
+};
+__device__ __forceinline__ Q8Lane q8_block_lane(float v) {
   const float amax = half_max(fabsf(v));  // max and integer sum: order-free, exact
   const float dd = amax / 127.0f;
   const float id = dd != 0.0f ? 1.0f / dd : 0.0f;
   const int q = nearest_int_fma(v, id);
-  const int s = half_isum(q);
+  return Q8Lane{q, h2f(f2h_ggml(dd)), -8 * half_isum(q)};
+}
+__device__ __forceinline__ void q8_block_store(float v, bool ok, XBlock* blk, int e) {
+  const Q8Lane b = q8_block_lane(v);
   if (ok) {
-    reinterpret_cast<int8_t*>(blk)[e] = (int8_t)q;
+    reinterpret_cast<int8_t*>(blk)[e] = (int8_t)b.q;
     if (e == 0) {
-      blk->d = h2f(f2h_ggml(dd));
-      blk->nsum8 = -8 * s;
+      blk->d = b.d;
+      blk->nsum8 = b.nsum8;
     }
   }
 }

@@ -53,7 +53,7 @@ __global__ __launch_bounds__(PX_T) void push_exchange_kernel(PushArgs a) {
   __shared__ uint32_t s_tag;
   __shared__ uint32_t s_sum[PX_MAX_RANKS];
   const int t = threadIdx.x;
-  if (t == 0) s_tag = __hip_atomic_load(a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  if (t == 0) s_tag = __hip_atomic_load(a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u + (uint32_t)a.skip;
   if (t < PX_MAX_RANKS) s_sum[t] = 0;
   __syncthreads();
   const uint32_t tag = s_tag;
@@ -61,12 +61,16 @@ __global__ __launch_bounds__(PX_T) void push_exchange_kernel(PushArgs a) {
   const size_t slot_w = (size_t)a.cap + PX_MAX_WG;  // granules per sender slot: words, then checksums
   const int per = (a.words + gridDim.x - 1) / gridDim.x;
   const int w0 = blockIdx.x * per, n = max(0, min(a.words, w0 + per) - w0);
+  auto word = [&](int q, int i) -> uint32_t* {  // word i of this exchange in rank q's part of the buffer
+    const size_t j = a.off + (size_t)i;
+    return a.row_w ? a.buf + (j / a.row_w) * a.pitch + (size_t)q * a.row_w + j % a.row_w
+                   : a.buf + (size_t)q * a.stride + j;
+  };
   if (a.phase & PX_PUSH) {
-    const uint32_t* src = a.buf + (size_t)a.rank * a.stride;
     const size_t slot = (half * a.G + a.rank) * slot_w;
     uint32_t sum = 0;
     for (int i = t; i < n; i += PX_T) {
-      const uint32_t v = src[w0 + i];
+      const uint32_t v = *word(a.rank, w0 + i);
       sum += px_mix(v, (uint32_t)(w0 + i));
 #pragma unroll 4
       for (int q = 0; q < a.G; q++) px_store(a.mail[q] + slot + w0 + i, v, tag);
@@ -86,7 +90,8 @@ __global__ __launch_bounds__(PX_T) void push_exchange_kernel(PushArgs a) {
     const uint64_t t0 = wall_clock64();
     bool late = false;
     for (int j0 = t; j0 < items; j0 += PX_T * PX_B) {
-      int dst[PX_B], qk[PX_B], ik[PX_B];
+      uint32_t* dst[PX_B];
+      int qk[PX_B], ik[PX_B];
       const uint2* src[PX_B];
       uint64_t g[PX_B];
       bool ok[PX_B];
@@ -97,7 +102,7 @@ __global__ __launch_bounds__(PX_T) void push_exchange_kernel(PushArgs a) {
         qk[k] = q;
         ik[k] = w0 + i;
         src[k] = mine + (half * a.G + q) * slot_w + w0 + i;
-        dst[k] = (int)((size_t)q * a.stride) + w0 + i;
+        dst[k] = word(q, w0 + i);
         g[k] = px_load(src[k]);
       }
       for (;;) {
@@ -121,7 +126,7 @@ __global__ __launch_bounds__(PX_T) void push_exchange_kernel(PushArgs a) {
 #pragma unroll
       for (int k = 0; k < PX_B; k++)
         if (j0 + k * PX_T < items) {
-          a.buf[dst[k]] = (uint32_t)g[k];
+          *dst[k] = (uint32_t)g[k];
           atomicAdd(&s_sum[qk[k]], px_mix((uint32_t)g[k], (uint32_t)ik[k]));
         }
     }
@@ -161,7 +166,7 @@ __global__ __launch_bounds__(PX_T) void push_exchange_kernel(PushArgs a) {
 
 void launch_push_exchange(const PushArgs& a, hipStream_t s) {
   if (a.G < 1 || a.G > PX_MAX_RANKS || a.rank < 0 || a.rank >= a.G || a.words < 0 || a.words > a.cap ||
-      (size_t)a.words > a.stride)
+      (!a.row_w && a.off + (size_t)a.words > a.stride) || a.skip < 0 || a.row_w < 0)
     throw std::runtime_error("push exchange: bad arguments");
   if (a.words == 0) return;
   // one work-group per 256 words up to 64 (a 1 MB prefill chunk: 4096 words each) -- a few CUs' worth of

@@ -273,13 +273,34 @@ __device__ unsigned long long* g_layer_trace = nullptr;
 // GELU(gate) * up of a work-group's H hidden units -> hid; with H = 32 (one Q8_0 block per work-group) and
 // a.hq also the block (quantize_row_q8_0, ops.cpp:116-139, of the same f32 values, 32 lanes), so the down
 // launch reads blocks (PLAIN) instead of quantizing the whole hid in every work-group (QUANT)
+// fused exchange (a.px_out): the hq block's 12 words (8 of quants, d, nsum8, two zero pads) or the hid values
+// are pushed to every rank's mailbox as well
 template <int H>
-__device__ __forceinline__ void gelu_out(const LayerGemv& a, int bid, const float* s_rows, int t) {
+__device__ __forceinline__ void gelu_out(const LayerGemv& a, int bid, const float* s_rows, int t, uint32_t tout) {
   if (t >= H) return;
   const float g = gelu_mul1(s_rows[t], s_rows[H + t]);
   a.hid[bid * H + t] = g;
-  if constexpr (H == 32)
-    if (a.hq) q8_block_store(g, true, a.hq + bid, t);
+  if constexpr (H == 32) {
+    if (a.hq) {
+      const Q8Lane b = q8_block_lane(g);
+      reinterpret_cast<int8_t*>(a.hq + bid)[t] = (int8_t)b.q;
+      if (t == 0) {
+        a.hq[bid].d = b.d;
+        a.hq[bid].nsum8 = b.nsum8;
+      }
+      if (a.px_out >= 0) {
+        const int j = t & 7;
+        uint32_t w = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) w |= (uint32_t)(__shfl(b.q, 4 * j + k) & 0xFF) << (8 * k);
+        if (t < 12)
+          px_push_word(*a.px, tout, bid * 12 + t,
+                       t < 8 ? w : t == 8 ? __float_as_uint(b.d) : t == 9 ? (uint32_t)b.nsum8 : 0u);
+      }
+      return;
+    }
+  }
+  if (a.px_out >= 0) px_push_word(*a.px, tout, bid * H + t, __float_as_uint(g));
 }
 
 enum { SYNC_SIG = 1, SYNC_WAIT = 2 };
@@ -348,11 +369,18 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
   static_assert(SYNC != SYNC_WAIT || ROLE == ROLE_PLAIN, "WAIT: the o projection (<- g_xo)");
   // this launch's granule tag, loaded up front (its latency hides under the prologue)
   const uint32_t btag = SYNC != 0 ? *bs.epoch + 1u : 0u;
+  // fused exchanges (tensor-parallel ranks): the tags of the exchange read and of the one written
+  const uint32_t tin = a.px_in >= 0 ? px_link_tag(*a.px, a.px_in) : 0u;
+  const uint32_t tout = a.px_out >= 0 ? px_link_tag(*a.px, a.px_out) : 0u;
   // SIG: rows are published write-through; the work-group's rows lie in one
   // kv head's group (host-checked: rows per work-group divide head_dim)
   auto put_out = [&](float* p, float v) {
-    if constexpr (SYNC == SYNC_SIG) st_granule(bs.g_qkv + (p - a.out), __float_as_uint(v), btag);
-    else *p = v;
+    if constexpr (SYNC == SYNC_SIG) {
+      st_granule(bs.g_qkv + (p - a.out), __float_as_uint(v), btag);
+    } else {
+      *p = v;
+      if (a.px_out >= 0) px_push_word(*a.px, tout, (int)(p - a.out), __float_as_uint(v));
+    }
   };
   // (RW0 == 0: the expressions of the all-waves launch exactly -- a select the compiler cannot fold away
   // reshuffled the attention block's registers and cost it 1 %)
@@ -564,13 +592,14 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
     const uint32_t vbytes = (uint32_t)nb * 128;
     const __amdgpu_buffer_rsrc_t ry = buf_rsrc(a.y, vbytes), rr = buf_rsrc(a.resid_in, vbytes),
                                  rp = buf_rsrc(a.w_post, a.w_post ? vbytes : 0u), rn = buf_rsrc(a.w_next, vbytes);
+    const bool yfx = a.px_in >= 0;  // y from this rank's mailbox (fused exchange), after the local operands
 #pragma unroll
     for (int k = 0; k < EB; k++) {
       const int b = t / 4 + k * QB;
       const int off = b < nb ? (b * 32 + sub * 8) * 4 : (1 << 30);
 #pragma unroll
       for (int h = 0; h < 2; h++) {
-        y4[k][h] = buf_ldf4(ry, off + 16 * h);
+        if (!yfx) y4[k][h] = buf_ldf4(ry, off + 16 * h);
         r4[k][h] = buf_ldf4(rr, off + 16 * h);
         p4[k][h] = buf_ldf4(rp, off + 16 * h);
         n4[k][h] = buf_ldf4(rn, off + 16 * h);
@@ -578,6 +607,15 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
     }
     if constexpr (EARLY) issue_weights();
     else issue_head();
+    if (yfx) {  // (the weights' first passes are in flight while the peers' words arrive)
+#pragma unroll
+      for (int k = 0; k < EB; k++) {
+        const int b = t / 4 + k * QB;
+#pragma unroll
+        for (int h = 0; h < 2; h++)
+          y4[k][h] = b < nb ? px_read_f4(*a.px, tin, a.px_in_ws, b * 32 + sub * 8 + 4 * h) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
     auto in_row = [&](int k) { return t / 4 + k * QB < nb; };
     float ss = 0.0f;
 #pragma unroll
@@ -653,14 +691,24 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
     // floats are loaded before the weights and quantized while they stream
     const float4* yb = reinterpret_cast<const float4*>(a.y);
     float4 xr[E][2];
+    if (a.px_in < 0) {
 #pragma unroll
-    for (int r = 0; r < E; r++) {
-      const int i = min(t + r * T, 4 * nb - 1);
-      xr[r][0] = yb[2 * i];
-      xr[r][1] = yb[2 * i + 1];
+      for (int r = 0; r < E; r++) {
+        const int i = min(t + r * T, 4 * nb - 1);
+        xr[r][0] = yb[2 * i];
+        xr[r][1] = yb[2 * i + 1];
+      }
     }
     if constexpr (EARLY) issue_weights();
     else issue_head();
+    if (a.px_in >= 0) {  // fused exchange: from this rank's mailbox, the weights' first passes in flight
+#pragma unroll
+      for (int r = 0; r < E; r++) {
+        const int i = min(t + r * T, 4 * nb - 1);
+        xr[r][0] = px_read_f4(*a.px, tin, a.px_in_ws, 8 * i);
+        xr[r][1] = px_read_f4(*a.px, tin, a.px_in_ws, 8 * i + 4);
+      }
+    }
 #pragma unroll
     for (int r = 0; r < E; r++) {
       const int i = t + r * T;
@@ -691,6 +739,14 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
         xr[k] = make_uint4(v[0], v[1], v[2], v[3]);
       }
       BLK_MARK(bs, 4);
+    } else if (a.px_in >= 0) {  // fused exchange: the blocks from this rank's mailbox (the weights in flight first)
+      issue_weights();  // (all of them: the late tail issue below is skipped)
+#pragma unroll
+      for (int k = 0; k < X_LD; k++) {
+        uint32_t v[4];
+        px_read_words<4>(*a.px, tin, a.px_in_ws, 4 * min(t + k * T, n16 - 1), v);
+        xr[k] = make_uint4(v[0], v[1], v[2], v[3]);
+      }
     } else {
 #pragma unroll
       for (int k = 0; k < X_LD; k++) xr[k] = src[min(t + k * T, n16 - 1)];
@@ -707,7 +763,8 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
   // (HELPER roles: handled above.)
   if constexpr (!HELP) {
     __syncthreads();
-    if constexpr (!EARLY && SYNC != SYNC_WAIT) issue_tail();
+    if constexpr (!EARLY && SYNC != SYNC_WAIT)
+      if (!(ROLE == ROLE_PLAIN && a.px_in >= 0)) issue_tail();
   }
 
   LAYER_MARK(4);
@@ -747,7 +804,7 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
       }
       __syncthreads();
       constexpr int H = RW * R / 2;  // hidden units of this work-group
-      gelu_out<H>(a, bid, s_rows, t);
+      gelu_out<H>(a, bid, s_rows, t, tout);
     } else if (!helper) {
       if constexpr (R <= 2) {
         if (lane == 0)
@@ -788,7 +845,7 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
     }
     __syncthreads();
     constexpr int H = RW * R / 2;  // hidden units of this work-group
-    gelu_out<H>(a, bid, s_rows, t);
+    gelu_out<H>(a, bid, s_rows, t, tout);
   } else {
 #pragma unroll
     for (int k = 0; k < R; k++) {

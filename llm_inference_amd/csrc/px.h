@@ -1,0 +1,86 @@
+// px.h -- the push exchange fused into the decode launches ("a one-shot P2P push over xGMI
+// ... with flag signaling, fused into the GEMV epilogue").
+//
+// The standalone exchange (k_exchange.hip) is one launch between a producer and its consumer.  Fused, the
+// producing launch's epilogue stores each output word, tagged, straight into slot [half][rank] of every rank's
+// mailbox (its own included), and the consuming launch's prologue reads the whole vector from its own mailbox,
+// re-loading each granule until it carries this exchange's tag -- no exchange launch, no launch boundary.
+//
+// Tags: a step's fused exchanges are numbered k = 0, 1, ... in recording order and use tag = *ctl + 1 + k,
+// where *ctl (the mailbox's exchange count) is constant during the step; the next standalone exchange (the
+// step's argmax keys, always last) takes tag = *ctl + 1 + (fused count) and leaves *ctl there, so the tags of
+// consecutive exchanges stay consecutive and never repeat within a group's lifetime (seeded per group).
+// Halves alternate with the tag's parity.  Safe reuse of a half (exchange n + 2 lands where n was read): every
+// launch that reads exchange n pushes its words of n + 1 only after reading, and every word of n + 1 is read by
+// every consumer of n + 1 -- so a rank pushing n + 2 has consumed n + 1 from all its peers, each of which had
+// finished reading n.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace llmi {
+
+constexpr int PX_MAX_RANKS = 16;
+
+// a rank's mailboxes as its launches see them (device-resident, one per session); an exchange is (k, ws): its
+// number within the step and its words per rank (word W of the whole vector is rank W / ws's word W % ws)
+struct PxLink {
+  uint2* mail[PX_MAX_RANKS];  // every rank's mailbox [2][G][slot_w] granules, as mapped in this process
+  const unsigned* ctl;        // the rank's exchange count (constant during a step)
+  int* err;                   // 1: a wait timed out
+  uint64_t timeout;           // bound of every wait, ticks of the 100 MHz wall clock
+  uint32_t slot_w;            // granules per sender slot
+  int rank, G;
+};
+
+#ifdef __HIPCC__
+__device__ __forceinline__ uint32_t px_link_tag(const PxLink& l, int k) {
+  return __hip_atomic_load(l.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u + (uint32_t)k;
+}
+
+// word w of this rank's slice -> every rank's mailbox (one 8-byte system-scope store each: word and tag together)
+__device__ __forceinline__ void px_push_word(const PxLink& l, uint32_t tag, int w, uint32_t v) {
+  const size_t slot = ((size_t)(tag & 1u) * l.G + l.rank) * l.slot_w + (size_t)w;
+  const uint64_t g = ((uint64_t)tag << 32) | v;
+  for (int q = 0; q < l.G; q++)
+    __hip_atomic_store(reinterpret_cast<uint64_t*>(l.mail[q] + slot), g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// N (1 or 4) consecutive words W.. of the whole vector from this rank's mailbox (W % N == 0 and ws % N == 0, so
+// they lie in one sender's slot); bounded: on timeout *err = 1 and the words are garbage (the grid drains)
+template <int N>
+__device__ __forceinline__ void px_read_words(const PxLink& l, uint32_t tag, int ws, int W, uint32_t (&v)[N]) {
+  const int q = W / ws, w = W - q * ws;
+  const uint64_t* g = reinterpret_cast<const uint64_t*>(l.mail[l.rank] + ((size_t)(tag & 1u) * l.G + q) * l.slot_w + w);
+  uint64_t x[N];
+#pragma unroll
+  for (int i = 0; i < N; i++) x[i] = __hip_atomic_load(g + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  uint64_t t0 = 0;
+  for (int n = 0;; n++) {
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < N; i++) ok = ok && (uint32_t)(x[i] >> 32) == tag;
+    if (ok) break;
+    if (n == 0) t0 = wall_clock64();
+    else if (wall_clock64() - t0 > l.timeout) {
+      __hip_atomic_store(l.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+    for (int i = 0; i < N; i++)
+      if ((uint32_t)(x[i] >> 32) != tag) x[i] = __hip_atomic_load(g + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+#pragma unroll
+  for (int i = 0; i < N; i++) v[i] = (uint32_t)x[i];
+}
+
+__device__ __forceinline__ float4 px_read_f4(const PxLink& l, uint32_t tag, int ws, int W) {
+  uint32_t v[4];
+  px_read_words<4>(l, tag, ws, W, v);
+  return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+}
+#endif
+
+}  // namespace llmi

@@ -533,6 +533,8 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
               : tp_peer       ? make_peer(tp_rank_, tp_size_)
                               : make_rccl(tp_rank_, tp_size_, opts.tp_id);
       if (!coll_->graph_safe()) use_graph_ = false;
+      const char* fx = getenv("LLMI_TP_FUSED");
+      px_fused_ = coll_->fused_capable() && !(fx && atoi(fx) == 0);
     }
     GGUFView g(gguf, size);
     load_hparams(g);
@@ -740,6 +742,7 @@ bool Session::embed_fold_ok() const {
 
 void Session::record_step(hipStream_t s, bool gen, bool fold_embed) {
   kernels_per_token_ = 0;
+  px_k_ = 0;
   rec_gen_ = gen;
   scr_prepped_ = false;
   rec_fold_ = fold_embed && gen && embed_fold_ok() && !dump_ && !trace_fn_;
@@ -825,7 +828,7 @@ void Session::record_logits(hipStream_t s, bool gen) {
     launch_argmax(lg, v_rows_, key, s);
     kernels_per_token_++;
   }
-  if (tp_) coll_->all_gather(amax_key_, sizeof(unsigned long long), s);
+  if (tp_) coll_->all_gather(amax_key_, sizeof(unsigned long long), s, px_take());
   if (rec_fold_)
     launch_finalize_embed_norm(amax_key_, tp_size_, v_sh_, d_token_, d_pos_, ring_, ring_idx_, max_ctx_, embd_.type,
                                embd_raw_, embd_row_bytes_, std::sqrt(static_cast<float>(E)), resid_, L_[0].attn_norm,
@@ -871,6 +874,9 @@ void Session::ensure_prefill_buffers(int cap) {
 // packs it into pf_gather_, all-gathers the per-rank [T][slice_b] blocks and
 // scatters every rank's block back to its columns of buf.
 void Session::gather_cols(void* buf, size_t pitch_b, size_t slice_b, int T, hipStream_t s) {
+  // push exchange: the exchange kernel reads this rank's column slice and writes the peers' in place (no staging
+  // copies: every byte moves in a kernel, ordered and cache-coherent with the GEMMs around it)
+  if (coll_->all_gather_cols(buf, pitch_b, slice_b, T, s, px_take())) return;
   const size_t blk = slice_b * T;
   uint8_t* g = reinterpret_cast<uint8_t*>(pf_gather_);
   uint8_t* b = reinterpret_cast<uint8_t*>(buf);
@@ -1253,6 +1259,22 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
   const int E = hp_.n_embd;
   float* cur = resid_;
   float* other = resid2_;
+  // tensor-parallel ranks: the o, GELU and down outputs go to the peers from the producing launches' epilogues
+  // and the consumers read their mailbox (px.h) -- no exchange launches but the attention output's (head-sharded
+  // mode), the last layer's down and the argmax keys
+  const bool pxf = tp_ && px_on() && !ffn_engine_;
+  int k_d = -1;  // the previous layer's down exchange, read by this layer's qkv prologue
+  auto fx_in = [&](LayerGemv& g, int k, int ws) {
+    if (k < 0) return;
+    g.px = d_px_;
+    g.px_in = k;
+    g.px_in_ws = ws;
+  };
+  auto fx_out = [&](LayerGemv& g) {
+    g.px = d_px_;
+    g.px_out = px_k_++;
+    return g.px_out;
+  };
   for (int l = 0; l < hp_.n_layer; l++) {
     LayerDev& Ld = L_[l];
     const int hd = Ld.hd;
@@ -1278,6 +1300,7 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
         g.resid_out = other;
         g.w_next = Ld.attn_norm;
         g.eps = hp_.eps;
+        fx_in(g, k_d, e_sh_);
         std::swap(cur, other);
       } else {  // model.cpp:722-756: residual + post-FFN norm, attention norm, Q8_0 blocks; the block reads them
         NormOut on;
@@ -1296,6 +1319,7 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
       LayerGemv go;
       go.xg = blk_xo_;
       go.out = o_out_ + (size_t)tp_rank_ * e_sh_;  // this rank's o rows (all of them on one device)
+      if (pxf) fx_out(go);
       BlockSync bs;
       bs.epoch = epoch;
       bs.g_qkv = blk_gqkv_ + (size_t)l * blk_gqkv_stride_;
@@ -1346,6 +1370,7 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
         g.eps = hp_.eps;
         g.out = qkv_;
         if (dump_ || trace_fn_) g.xn_out = xn_;
+        fx_in(g, k_d, e_sh_);
         for (int r = 0; r < dup("qkv"); r++) qkv_launch(g, LAYER_PRO);
         tap("attn_resid", l, other, (size_t)E * 4, s);
         tap("attn_norm", l, xn_, (size_t)E * 4, s);
@@ -1379,16 +1404,19 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
         launch_quantize_q8_0(attn_, hp_.n_head * hd, act_.q8, s);
         kernels_per_token_++;
       }
-      if (tp_ && !tp_rep_attn_) coll_->all_gather(act_.q8.xb, (size_t)hb * sizeof(XBlock), s);
+      if (tp_ && !tp_rep_attn_) coll_->all_gather(act_.q8.xb, (size_t)hb * sizeof(XBlock), s, px_take());
       LayerGemv go;
       go.xg = act_.q8.xb;
       go.out = o_out_ + (size_t)tp_rank_ * e_sh_;
+      if (pxf) fx_out(go);
       tap("xo", l, act_.q8.xb, (size_t)hp_.n_head * hd / 32 * sizeof(XBlock), s);
       for (int r = 0; r < dup("o_proj"); r++) launch_layer_gemv(Ld.o.w, go, LAYER_PLAIN, s);
       tap("o", l, o_out_, (size_t)E * 4, s);
       dump("attention results (node_30 for MUL_MAT)-" + L, o_out_, E, s);
     }
-    if (tp_) coll_->all_gather(o_out_, (size_t)e_sh_ * sizeof(float), s);
+    const int k_o = pxf ? px_k_ - 1 : -1;  // the o launch's exchange (the block's or the standalone o's)
+    if (pxf) coll_->fused_point(s);
+    else if (tp_) coll_->all_gather(o_out_, (size_t)e_sh_ * sizeof(float), s, px_take());
     if (ffn_engine_ && !dump_ && !trace_fn_) {  // gate_up + GELU + down: one launch
       EngineLayer a = eng_;
       a.g_qs = (const uint4*)eng_w_[l].g.qs;
@@ -1443,6 +1471,12 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
     if (dplain) gg.hq = hq_ + (size_t)tp_rank_ * (f_sh_ / 32);
     gg.epoch = epoch;  // advances the attention block's granule tag of this layer
     if (dump_ || trace_fn_) gg.xn_out = xn_;
+    const bool gfx = pxf && !gelu_x;
+    int k_h = -1;
+    if (gfx) {
+      fx_in(gg, k_o, e_sh_);
+      k_h = fx_out(gg);
+    }
     for (int r = 0; r < dup("gate_up"); r++) launch_layer_gemv(Ld.gate_up[0].w, gg, gelu_x ? LAYER_GELU_X : LAYER_GELU, s);
     tap("ffn_resid", l, gelu_x ? cur : other, (size_t)E * 4, s);
     tap("ffn_norm", l, xn_, (size_t)E * 4, s);
@@ -1451,15 +1485,22 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
     dump("ffn_norm-" + L, xn_, E, s);
     dump("ffn_geglu-" + L, hid_, hp_.n_ff, s);
     if (!gelu_x) std::swap(cur, other);  // (the norm launch updated cur in place)
-    if (tp_ && dplain) coll_->all_gather(hq_, (size_t)(f_sh_ / 32) * sizeof(XBlock), s);
-    else if (tp_) coll_->all_gather(hid_, (size_t)f_sh_ * sizeof(float), s);
+    if (gfx) coll_->fused_point(s);
+    else if (tp_ && dplain) coll_->all_gather(hq_, (size_t)(f_sh_ / 32) * sizeof(XBlock), s, px_take());
+    else if (tp_) coll_->all_gather(hid_, (size_t)f_sh_ * sizeof(float), s, px_take());
     LayerGemv gd;
     gd.y = hid_;  // QUANT: GELU output quantized per block in the down launch
     gd.xg = hq_;  // PLAIN: the blocks the GELU launch wrote
     gd.out = d_out_ + (size_t)tp_rank_ * e_sh_;
+    fx_in(gd, k_h, dplain ? f_sh_ / 32 * 12 : f_sh_);
+    // the next layer's qkv prologue reads the down exchange from its mailbox (the 27B attention block's PLAIN
+    // role reads the blocks of a residual_norm launch instead, and the last layer's feeds the final norm)
+    const bool dfx = gfx && l + 1 < hp_.n_layer && (!block_ || block_pro_);
+    k_d = dfx ? fx_out(gd) : -1;
     for (int r = 0; r < dup("down"); r++) launch_layer_gemv(Ld.down.w, gd, dplain ? LAYER_PLAIN : LAYER_QUANT, s);
     tap("down", l, d_out_, (size_t)E * 4, s);
-    if (tp_) coll_->all_gather(d_out_, (size_t)e_sh_ * sizeof(float), s);
+    if (dfx) coll_->fused_point(s);
+    else if (tp_) coll_->all_gather(d_out_, (size_t)e_sh_ * sizeof(float), s, px_take());
     dump("ffn_out-" + L, d_out_, E, s);
     kernels_per_token_ += block_ ? 2 : 3;  // (o, when not in the attention block,) gate_up, down
   }
@@ -1714,7 +1755,19 @@ void Session::ensure_graph(bool gen) {
 
 // gen: a decode-loop step (only the token id is kept); otherwise the full
 // logits vector is produced (forward)
+// the fused exchanges' device-resident link, once the collective is connected (before the first recorded step:
+// no allocation or copy inside a graph capture)
+void Session::px_prepare() {
+  if (!px_fused_ || d_px_) return;
+  PxLink l;
+  coll_->fused_link(l);
+  PxLink* d = dalloc<PxLink>(1);
+  LLMI_HIP(hipMemcpy(d, &l, sizeof(l), hipMemcpyHostToDevice));
+  d_px_ = d;
+}
+
 void Session::run_step(bool gen) {
+  px_prepare();
   gen = gen && screen_;
   if (use_graph_) {
     ensure_graph(gen);
@@ -1764,7 +1817,7 @@ void Session::forward(const int32_t* tokens, int n, int pos, float* logits, int3
       }
     }
     // every rank of a tensor-parallel group gathers the full logits (collective)
-    if (tp_) coll_->all_gather(logits_, (size_t)v_sh_ * sizeof(float), stream_);
+    if (tp_) coll_->all_gather(logits_, (size_t)v_sh_ * sizeof(float), stream_, px_take());
     if (logits) LLMI_HIP(hipMemcpyAsync(logits, logits_, (size_t)vocab_ * 4, hipMemcpyDeviceToHost, stream_));
     if (argmax) LLMI_HIP(hipMemcpyAsync(argmax, d_token_, 4, hipMemcpyDeviceToHost, stream_));
     LLMI_HIP(hipStreamSynchronize(stream_));
@@ -1955,7 +2008,7 @@ void Session::info(llmi_session_info* o) const {
   o->prefill_f16_redo = pf_f16_redo_;
   o->layer_engine = engine_ ? 1 : 0;
   o->ffn_engine = ffn_engine_ ? 1 : 0;
-  o->tp_exchange = coll_ ? coll_->kind() : 0;
+  o->tp_exchange = coll_ ? (px_fused_ && coll_->kind() == EX_PUSH ? EX_PUSH_FUSED : coll_->kind()) : 0;
   o->block_slow_waits = slow_waits_;
   o->exact_engine = xl_ ? 1 : 0;
   size_t b = logits_w_.bytes;  // this rank's bytes

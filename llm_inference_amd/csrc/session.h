@@ -216,6 +216,18 @@ class Session {
   std::unique_ptr<Collective> coll_;
   int nh_ = 0, nkv_ = 0, kv0_ = 0, e_sh_ = 0, f_sh_ = 0, v_sh_ = 0, v_rows_ = 0;
   bool tp_rep_attn_ = false;  // tensor parallel: qkv + attention replicated on every rank (setup_tp)
+  // fused exchanges (px.h): the producing launches push, the consuming ones read their mailbox -- push-exchange
+  // collectives, the fused layer path, no dumps / traces (LLMI_TP_FUSED=0: standalone exchange launches)
+  bool px_fused_ = false;
+  PxLink* d_px_ = nullptr;  // the device-resident link (px_prepare, before the first recorded step)
+  int px_k_ = 0;            // fused exchanges recorded since the last standalone one
+  void px_prepare();
+  bool px_on() const { return px_fused_ && d_px_ && !dump_ && !trace_fn_; }
+  int px_take() {  // the skip of a standalone exchange recorded now (its tag follows the fused ones)
+    const int k = px_k_;
+    px_k_ = 0;
+    return k;
+  }
   DevWeight logits_w_;  // the logits GEMV's rows: embd_ itself, or this rank's slice
   bool own_logits_w_ = false;
   // batched prefill (fast fused path, one device): chunk buffers

@@ -3,6 +3,7 @@
 
 #include "attn.h"
 #include "kernels.h"
+#include "px.h"
 
 namespace llmi {
 
@@ -77,6 +78,13 @@ struct LayerGemv {
   unsigned* epoch = nullptr;  // optional: work-group 0 advances *epoch (the attention block's granule tag)
   const uint32_t* kdd = nullptr;  // kq weights (Q4_K / Q6_K): super-block d words, Q6_K high bits
   const uint2* kqh = nullptr;
+  // tensor-parallel ranks, fused exchanges (px.h; px: the session's device-resident link): px_in -- the
+  // activation (y for PRO / GELU / QUANT, the x blocks for PLAIN) is read from this rank's mailbox instead of
+  // y / xg; px_out -- every output word (out rows; GELU: hid, or the hq blocks when hq is set) is also pushed
+  // to every rank's mailbox
+  const PxLink* px = nullptr;
+  int px_in = -1, px_in_ws = 0;  // >= 0: the exchange (step number, words per rank) read instead of y / xg
+  int px_out = -1;               // >= 0: the exchange the outputs are pushed into
 };
 // Cross-work-group hand-offs of the attention-block kernel (k_attn.hip):
 // qkv rows -> the kv head's attention work-groups -> the o projection, as

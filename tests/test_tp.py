@@ -88,7 +88,7 @@ def test_sharded_matches_whole_model(cfg_name, tp, mode, monkeypatch):
         np.testing.assert_array_equal(lg, ref)
         assert toks.tolist() == ref_toks.tolist()
         assert info.tp_rank == r and info.tp_size == tp
-        assert info.tp_exchange == 3  # the push exchange (the default)
+        assert info.tp_exchange == 4  # the push exchange fused into the decode launches (the default)
         # each rank streams about 1/tp of the projection + logits bytes (+ the replicated q|k|v)
         rep = _qkv_bytes(g) if mode == "rep" else 0
         assert info.bytes_per_token < (full_bytes - rep) / tp * 1.2 + rep
@@ -144,9 +144,10 @@ def test_sharded_attention_block(cfg_name, tp, monkeypatch):
         assert info.batched_prefill == 1
 
 
-@pytest.mark.parametrize("exchange", ["copy", "push"])
+@pytest.mark.parametrize("exchange", ["copy", "push", "fused"])
 def test_exchange_ab_and_chunked_messages(exchange, monkeypatch):
-    """The two single-device exchanges give the same bits: 4B layer shapes at tp 2 with a 300-token batched
+    """The single-device exchanges give the same bits (copy: device-to-device slice copies; push: the
+    standalone push-exchange launches, LLMI_TP_FUSED=0; fused: the default, pushes from the producing launches): 4B layer shapes at tp 2 with a 300-token batched
     prefill, whose GELU-block all-gather (300 tokens x 5.8 KB per rank) exceeds the push mailbox's 1 MB slot
     and goes as two consecutive exchanges (tags 2 apart: both halves of the mailbox reused)."""
     from llm_inference_amd.model import Model
@@ -159,10 +160,12 @@ def test_exchange_ab_and_chunked_messages(exchange, monkeypatch):
     ref = whole.forward(prompt, 0)
     ref_toks = whole.generate(int(np.argmax(ref)), len(prompt), 5)
     whole.close()
-    monkeypatch.setenv("LLMI_TP_EXCHANGE", exchange)
+    monkeypatch.setenv("LLMI_TP_EXCHANGE", "copy" if exchange == "copy" else "push")
+    if exchange == "push":
+        monkeypatch.setenv("LLMI_TP_FUSED", "0")
     out = _run_ranks(g, 2, prompt, 5, max_ctx=384)
     for r, (lg, toks, info) in enumerate(out):
-        assert info.tp_exchange == (3 if exchange == "push" else 2)
+        assert info.tp_exchange == {"copy": 2, "push": 3, "fused": 4}[exchange]
         np.testing.assert_array_equal(lg, ref)
         assert toks.tolist() == ref_toks.tolist()
 

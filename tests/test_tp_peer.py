@@ -50,16 +50,22 @@ def _peer_ranks(g, size, prompt, n_gen, env):
     return results
 
 
-@pytest.mark.parametrize("cfg_name,prefill", [("mini-4b", True), ("mini-1b", False)])
-def test_peer_push_processes_match_whole_model(cfg_name, prefill, monkeypatch):
+@pytest.mark.parametrize("cfg_name,prefill,mode", [("mini-4b", True, "fused"), ("mini-1b", False, "fused"),
+                                                   ("mini-1b", False, "standalone"), ("mini-4b", False, "block")])
+def test_peer_push_processes_match_whole_model(cfg_name, prefill, mode, monkeypatch):
+    """mode fused (default): the o / GELU / down outputs pushed from the producing launches, read by the consumers
+    from their mailboxes (csrc/px.h); standalone (LLMI_TP_FUSED=0): an exchange launch per all-gather; block: the
+    fused exchanges around the ranks' attention blocks (replicated attention), against the whole model's block."""
     from llm_inference_amd.model import Model
     from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
     cfg = CONFIGS[cfg_name]
     g = build_gemma3_gguf(cfg, seed=31)
     prompt = np.random.default_rng(37).integers(4, cfg.vocab, 40).astype(np.int32)
-    env = {"LLMI_NO_BLOCK": "1"}  # the per-projection launches on both sides (as tests/test_tp.py)
+    env = {} if mode == "block" else {"LLMI_NO_BLOCK": "1"}  # else the per-projection launches on both sides
     if not prefill:
         env["LLMI_NO_PREFILL"] = "1"  # the prompt token by token through the decode graph's exchanges
+    if mode == "standalone":
+        env["LLMI_TP_FUSED"] = "0"
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     whole = Model(g, exact=False, max_ctx=128)
@@ -68,7 +74,7 @@ def test_peer_push_processes_match_whole_model(cfg_name, prefill, monkeypatch):
     whole.close()
     out = _peer_ranks(g, 2, prompt, 10, env)
     for r, (lg, toks, exchange, kpt) in enumerate(out):
-        print(f"{cfg_name} peer rank {r}: kernels/token {kpt}, max|dlogit| {float(np.abs(lg - ref).max()):.3g}")
-        assert exchange == 3
+        print(f"{cfg_name} peer rank {r} ({mode}): kernels/token {kpt}, max|dlogit| {float(np.abs(lg - ref).max()):.3g}")
+        assert exchange == (3 if mode == "standalone" else 4)
         np.testing.assert_array_equal(lg, ref)
         assert toks.tolist() == ref_toks.tolist()
