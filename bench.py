@@ -427,7 +427,9 @@ def main():
             "workload": f"{cfg.name}-{a.quant} greedy decode after a {a.prefill}-token prefill "
                         f"(BASELINE {base_cfg})",
             "prefill_tokens": a.prefill, "decode_tokens": a.steps, "mode": "exact" if a.exact else "fast",
-            "parallelism": (f"tp{d.world} (row-sharded, " + ("one-shot push all-gather over IPC-mapped mailboxes"
+            "parallelism": (f"tp{d.world} (row-sharded, " + (("one-shot push all-gather over IPC-mapped mailboxes"
+                                                               + (", fused into the decode launches"
+                                                                  if info.tp_exchange == 4 else ""))
                                                               if exchange == "push" else "RCCL all-gather") + ")"
                             if tp else f"replicas{d.world}")
                            if d.world > 1 else "single",

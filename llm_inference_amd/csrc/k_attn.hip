@@ -820,8 +820,9 @@ constexpr size_t block_attn_lds() {  // s_k + s_v (32-key tiles) + s_red
 // after the first weight's rows
 constexpr int WT_W8 = 3;  // Q8_0 weights in the block (layer_body W8), beside the kq formats WT_Q4_K / WT_Q6_K
 
+// PXF: the qkv prologue / o epilogue honour the fused exchange (tensor-parallel ranks; layer_body PXF)
 template <int HD, int G, int QR, int QP, int QE, int QROLE, int OR, int OP, int OE, int WTQ = 0, int WTQB = 0,
-          int WTO = 0, int KVD = 1, int NS = ATTN_NSPLIT>
+          int WTO = 0, int KVD = 1, int NS = ATTN_NSPLIT, bool PXF = false>
 __global__ __launch_bounds__(256) void attn_block_kernel(LayerGemv qg, LayerGemv og, AttnArgs aa, QKVArgs qa,
                                                         BlockSync bs, int nq, LayerGemv qgb, int nqa) {
   extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
@@ -835,7 +836,8 @@ __global__ __launch_bounds__(256) void attn_block_kernel(LayerGemv qg, LayerGemv
         return;
       }
     }
-    layer_body<QR, 4, QP, QE, QROLE, false, true, SYNC_SIG, 0, WTQ == WT_W8, WTQ == WT_W8 ? 0 : WTQ>(qg, b, s_dyn, bs);
+    layer_body<QR, 4, QP, QE, QROLE, false, true, SYNC_SIG, 0, WTQ == WT_W8, WTQ == WT_W8 ? 0 : WTQ, 0, PXF>(qg, b, s_dyn,
+                                                                                                         bs);
     return;
   }
   b -= nq;
@@ -850,7 +852,8 @@ __global__ __launch_bounds__(256) void attn_block_kernel(LayerGemv qg, LayerGemv
     return;
   }
   b -= na;
-  layer_body<OR, 4, OP, OE, ROLE_PLAIN, false, true, SYNC_WAIT, 0, WTO == WT_W8, WTO == WT_W8 ? 0 : WTO>(og, b, s_dyn, bs);
+  layer_body<OR, 4, OP, OE, ROLE_PLAIN, false, true, SYNC_WAIT, 0, WTO == WT_W8, WTO == WT_W8 ? 0 : WTO, 0, PXF>(og, b, s_dyn,
+                                                                                                          bs);
 }
 
 using BlockFn = void (*)(dim3, size_t, const LayerGemv&, const LayerGemv&, const AttnArgs&, const QKVArgs&,
@@ -860,6 +863,17 @@ template <int HD, int G, int QR, int QP, int QE, int QROLE, int OR, int OP, int 
           int KVD = 1, int NS = ATTN_NSPLIT>
 void block_launch(dim3 grid, size_t lds, const LayerGemv& qg, const LayerGemv& og, const AttnArgs& aa,
                   const QKVArgs& qa, const BlockSync& bs, int nq, const LayerGemv& qgb, int nqa, hipStream_t s) {
+  if (qg.px || og.px) {  // the fused-exchange variant (tensor-parallel ranks): co-resident too, or refused
+    auto kern = attn_block_kernel<HD, G, QR, QP, QE, QROLE, OR, OP, OE, WTQ, WTQB, WTO, KVD, NS, true>;
+    int per_cu = 0, n_cu = 0, dev = 0;
+    LLMI_HIP(hipGetDevice(&dev));
+    LLMI_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+    LLMI_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kern), 256, lds));
+    if ((long)grid.x > (long)std::max(0, per_cu - 1) * n_cu)
+      throw std::runtime_error("attention block: the fused-exchange variant's grid is not co-resident");
+    hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, qg, og, aa, qa, bs, nq, qgb, nqa);
+    return;
+  }
   KernelTiming& kt = kernel_timing();
   if (kt.start) {  // bench: events signalled by this dispatch itself (its duration as rocprofv3 reports it)
     hipExtLaunchKernelGGL((attn_block_kernel<HD, G, QR, QP, QE, QROLE, OR, OP, OE, WTQ, WTQB, WTO, KVD, NS>), grid, dim3(256),

@@ -573,10 +573,32 @@ __device__ __forceinline__ uint16_t cvt_f16_rne(float f) {
   return (uint16_t)r;
 }
 
+// 16 B per lane global -> LDS (lane l's at lds_wave_base + 16 l) as inline asm, outside hipcc's s_waitcnt
+// bookkeeping: the kernel's own counted waits are the only ones (the prefill GEMM's LDS-DMA issue, k_prefill.hip)
+__device__ __forceinline__ void xa_glds16(const void* g, unsigned char* lds_wave_base) {
+  const uint32_t dst = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)lds_wave_base);
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(g), "s"(dst)
+               : "memory");
+}
+
+// The V rows reach the accumulator chains through an LDS ring: stages of XA_SK keys, XA_NST of them, streamed by
+// LDS-DMA (16 B per lane, whole 1-KB runs of rows) by the dim waves, so ~3 stages of V are in flight while one is
+// summed (a chain's per-key loads, 2 B per lane, left it waiting a memory latency every 32 keys).
+constexpr int XA_SK = 64, XA_NST = 4;
+
 template <int HD>
 __global__ __launch_bounds__((HD / 64 + 1) * 64) void xattn_accum_kernel(XAttnArgs a) {
   constexpr int NWV = HD / 64, T = (NWV + 1) * 64;
   constexpr int KPT = XA_CH / 256;  // keys per scan thread (threads 0..255)
+  constexpr int KB = 2 * HD;        // bytes per V row
+  constexpr int KPI = 1024 / KB;    // rows per wave DMA instruction
+  constexpr int NI = XA_SK / KPI;   // DMA instructions per stage
+  constexpr int LPW = NI / NWV;     // ... per dim wave
+  static_assert(NI % NWV == 0 && XA_SK % 32 == 0 && XA_CH % XA_SK == 0, "V staging geometry");
+  __shared__ __attribute__((aligned(16))) unsigned char s_v[XA_NST][XA_SK * KB];
   __shared__ double s_sc[XA_CH];
   __shared__ __attribute__((aligned(16))) float s_e[XA_CH];   // e per key
   __shared__ __attribute__((aligned(16))) float s_pe[XA_CH];  // pe per key
@@ -586,13 +608,27 @@ __global__ __launch_bounds__((HD / 64 + 1) * 64) void xattn_accum_kernel(XAttnAr
   const int h = blockIdx.x, t = threadIdx.x, wave = t >> 6, lane = t & 63;
   const int n_keys = *a.d_pos + 1;
   const int hkv = h / (a.n_head / a.n_head_kv);
-  const uint16_t* vb = a.v_cache + (size_t)hkv * a.max_ctx * HD + wave * 64 + lane;
+  const uint16_t* vh = a.v_cache + (size_t)hkv * a.max_ctx * HD;  // this head's V rows
   const double* sc_in = a.scores + (size_t)h * a.max_ctx;
   double run_max = -INFINITY;
   uint16_t v16 = 0;  // f32_to_f16(0.0f)
   float s_acc = 0.0f;
   for (int c0 = 0; c0 < n_keys; c0 += XA_CH) {
     const int nk = min(XA_CH, n_keys - c0);
+    // stage st of the chunk (keys c0 + st XA_SK ..) into ring slot st % XA_NST; keys past the context are clamped
+    // (loaded, never summed), so every dim wave always has LPW loads per stage outstanding
+    auto issue = [&](int st) {
+      if (wave >= NWV) return;
+      unsigned char* slot = s_v[st % XA_NST];
+#pragma unroll
+      for (int i = 0; i < LPW; i++) {
+        const int ins = wave + i * NWV;
+        const int key = min(c0 + st * XA_SK + ins * KPI + lane / (64 / KPI), n_keys - 1);
+        xa_glds16(vh + (size_t)key * HD + (lane % (64 / KPI)) * 8, slot + ins * 1024);
+      }
+    };
+#pragma unroll
+    for (int st = 0; st < XA_NST - 1; st++) issue(st);  // in flight during the scores / prefix-max phase
     for (int i = t; i < nk; i += T)
       s_sc[i] = a.softcap > 0.0f ? llmi_glibc::softcap_score(sc_in[c0 + i], a.softcap) : sc_in[c0 + i];
     for (int i = t; i < XA_CH / 32; i += T) s_up[i] = 0u;
@@ -634,54 +670,63 @@ __global__ __launch_bounds__((HD / 64 + 1) * 64) void xattn_accum_kernel(XAttnAr
     }
     run_max = fmax(run_max, s_tmax[255]);
     __syncthreads();
-    if (wave < NWV) {  // this lane's head dim: vec_scale_f16 when the max moved, then vec_mad_f16 (ops.cpp:1084-1099)
-      const uint16_t* vp = vb + (size_t)c0 * HD;
-      // V of 32 keys per batch, the next batch's loads issued before this one is summed (clamped keys past the
-      // chunk are loaded but never summed)
-      uint32_t va[32], vn[32];  // one f16 per register (low half): the mad8 asm reads them as they are
+    const int nst = (nk + XA_SK - 1) / XA_SK;
+    const int d = wave * 64 + lane;  // dim waves: this lane's head dim
+    for (int st = 0; st < nst; st++) {
+      issue(st + XA_NST - 1);  // into the slot summed in the previous stage (free since its closing barrier)
+      if (wave < NWV) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((XA_NST - 1) * LPW) : "memory");  // stage st landed
+      __syncthreads();
+      const uint16_t* sv = reinterpret_cast<const uint16_t*>(s_v[st % XA_NST]);
+      if (wave < NWV) {  // vec_scale_f16 when the max moved, then vec_mad_f16 (ops.cpp:1084-1099), keys in order
 #pragma unroll
-      for (int u = 0; u < 32; u++) va[u] = vp[(size_t)min(u, nk - 1) * HD];
-      for (int j0 = 0; j0 < nk; j0 += 32) {
+        for (int sb = 0; sb < XA_SK / 32; sb++) {
+          const int j0 = st * XA_SK + sb * 32;
+          if (j0 >= nk) break;
+          uint32_t va[32];  // one f16 per register (low half): the mad8 asm reads them as they are
 #pragma unroll
-        for (int u = 0; u < 32; u++) vn[u] = vp[(size_t)min(j0 + 32 + u, nk - 1) * HD];
-        // the batch's max moves (wave-uniform, a scalar branch per key) and e values (broadcast LDS reads)
-        const uint32_t up = __builtin_amdgcn_readfirstlane(s_up[j0 >> 5]);
-        const int m = __builtin_amdgcn_readfirstlane(min(32, nk - j0));
-        float e[32];
+          for (int u = 0; u < 32; u++) va[u] = sv[(sb * 32 + u) * HD + d];
+          // the batch's max moves (wave-uniform, a scalar branch per key) and e values (broadcast LDS reads)
+          const uint32_t up = __builtin_amdgcn_readfirstlane(s_up[j0 >> 5]);
+          const int m = __builtin_amdgcn_readfirstlane(min(32, nk - j0));
+          float e[32];
 #pragma unroll
-        for (int u4 = 0; u4 < 8; u4++) {
-          const float4 q = reinterpret_cast<const float4*>(s_e + j0)[u4];
-          e[4 * u4] = q.x; e[4 * u4 + 1] = q.y; e[4 * u4 + 2] = q.z; e[4 * u4 + 3] = q.w;
-        }
-        // each step rounds to f32 (the fma), then to f16 (the conversion as its own instruction: fused by the
-        // compiler into v_fma_mixlo_f16 it would round once, another f16 whenever the f32 value is a midpoint)
-        if (up == 0 && m == 32) {  // the common batch: the max did not move, 32 straight fma + round steps
-          uint32_t acc = v16;
+          for (int u4 = 0; u4 < 8; u4++) {
+            const float4 q = reinterpret_cast<const float4*>(s_e + j0)[u4];
+            e[4 * u4] = q.x; e[4 * u4 + 1] = q.y; e[4 * u4 + 2] = q.z; e[4 * u4 + 3] = q.w;
+          }
+          // each step rounds to f32 (the fma), then to f16 (the conversion as its own instruction: fused by the
+          // compiler into v_fma_mixlo_f16 it would round once, another f16 whenever the f32 value is a midpoint)
+          if (up == 0 && m == 32) {  // the common batch: the max did not move, 32 straight fma + round steps
+            uint32_t acc = v16;
 #pragma unroll
-          for (int u = 0; u < 32; u += 8) xa_mad8(acc, va + u, e + u);
-          v16 = (uint16_t)acc;
-        } else {
+            for (int u = 0; u < 32; u += 8) xa_mad8(acc, va + u, e + u);
+            v16 = (uint16_t)acc;
+          } else {
 #pragma unroll
-          for (int u = 0; u < 32; u++) {
-            if (u < m) {
-              if (up & (1u << u)) v16 = cvt_f16_rne((float)__builtin_bit_cast(_Float16, v16) * s_pe[j0 + u]);
-              v16 = cvt_f16_rne(fmaf((float)__builtin_bit_cast(_Float16, (uint16_t)va[u]), e[u], (float)__builtin_bit_cast(_Float16, v16)));
+            for (int u = 0; u < 32; u++) {
+              if (u < m) {
+                if (up & (1u << u)) v16 = cvt_f16_rne((float)__builtin_bit_cast(_Float16, v16) * s_pe[j0 + u]);
+                v16 = cvt_f16_rne(fmaf((float)__builtin_bit_cast(_Float16, (uint16_t)va[u]), e[u],
+                                       (float)__builtin_bit_cast(_Float16, v16)));
+              }
             }
           }
         }
+      } else {  // s_acc = s_acc * pe + e, keys in order (model.cpp:540)
+        const int j1 = min(nk, st * XA_SK + XA_SK);
+        for (int j0 = st * XA_SK; j0 < j1; j0 += 4) {
+          const float4 e4 = reinterpret_cast<const float4*>(s_e + j0)[0];
+          const float4 p4 = reinterpret_cast<const float4*>(s_pe + j0)[0];
+          const float ev[4] = {e4.x, e4.y, e4.z, e4.w}, pv[4] = {p4.x, p4.y, p4.z, p4.w};
 #pragma unroll
-        for (int u = 0; u < 32; u++) va[u] = vn[u];
+          for (int u = 0; u < 4; u++)
+            if (j0 + u < j1) s_acc = s_acc * pv[u] + ev[u];
+        }
       }
-    } else {  // s_acc = s_acc * pe + e, keys in order (model.cpp:540)
-      for (int j0 = 0; j0 < nk; j0 += 4) {
-        const float4 e4 = reinterpret_cast<const float4*>(s_e + j0)[0];
-        const float4 p4 = reinterpret_cast<const float4*>(s_pe + j0)[0];
-        const float ev[4] = {e4.x, e4.y, e4.z, e4.w}, pv[4] = {p4.x, p4.y, p4.z, p4.w};
-#pragma unroll
-        for (int u = 0; u < 4; u++)
-          if (j0 + u < nk) s_acc = s_acc * pv[u] + ev[u];
-      }
+      __syncthreads();  // the slot is free for the stage issued next
     }
+    // the stages issued past the chunk's end land before the next chunk (or the work-group's end) reuses the ring
+    if (wave < NWV) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // the chunk's LDS is reused by the next one
   }
   if (wave == NWV && lane == 0) s_sacc = s_acc == 0.0f ? 0.0f : 1.0f / s_acc;

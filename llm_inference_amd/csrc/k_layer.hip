@@ -31,13 +31,14 @@ namespace llmi {
 
 namespace {
 
+// PXF: the fused-exchange variant (tensor-parallel ranks: a.px set; layer_body PXF)
 template <int R, int NW, int P, int E, int ROLE, bool MULTI, bool EARLY, int PE = 0, bool W8 = false, int WT = 0,
-          int RW = 0>
+          int RW = 0, bool PXF = false>
 __global__ __launch_bounds__(NW * 64 + (role_help(ROLE) ? E * 64 : 0)) void gemv_q4_0_layer(LayerGemv a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
   // the attention block's granule tag of this layer, for its next launch
   if (a.epoch && blockIdx.x == 0 && threadIdx.x == 0) *a.epoch += 1u;
-  layer_body<R, NW, P, E, ROLE, MULTI, EARLY, 0, PE, W8, WT, RW>(a, blockIdx.x, s_dyn, BlockSync{});
+  layer_body<R, NW, P, E, ROLE, MULTI, EARLY, 0, PE, W8, WT, RW, PXF>(a, blockIdx.x, s_dyn, BlockSync{});
 }
 
 // K-quant q|k|v of two weight types in one launch (Q4_K_M: q, k Q4_K, v Q6_K):
@@ -70,6 +71,10 @@ template <int R, int NW, int P, int E, int ROLE, bool MULTI, bool EARLY, int PE 
           int RW = 0>
 void launch_cfg(dim3 grid, size_t lds, const LayerGemv& a, hipStream_t s) {
   const dim3 block(NW * 64 + (role_help(ROLE) ? E * 64 : 0));
+  if (a.px) {  // the fused-exchange variant (tensor-parallel ranks)
+    hipLaunchKernelGGL((gemv_q4_0_layer<R, NW, P, E, ROLE, MULTI, EARLY, PE, W8, WT, RW, true>), grid, block, lds, s, a);
+    return;
+  }
   KernelTiming& kt = kernel_timing();
   if (kt.start) {
     hipExtLaunchKernelGGL((gemv_q4_0_layer<R, NW, P, E, ROLE, MULTI, EARLY, PE, W8, WT, RW>), grid, block, (uint32_t)lds,

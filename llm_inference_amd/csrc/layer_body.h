@@ -276,7 +276,8 @@ __device__ unsigned long long* g_layer_trace = nullptr;
 // fused exchange (a.px_out): the hq block's 12 words (8 of quants, d, nsum8, two zero pads) or the hid values
 // are pushed to every rank's mailbox as well
 template <int H>
-__device__ __forceinline__ void gelu_out(const LayerGemv& a, int bid, const float* s_rows, int t, uint32_t tout) {
+__device__ __forceinline__ void gelu_out(const LayerGemv& a, int bid, const float* s_rows, int t, bool fout,
+                                         uint32_t tout) {
   if (t >= H) return;
   const float g = gelu_mul1(s_rows[t], s_rows[H + t]);
   a.hid[bid * H + t] = g;
@@ -288,7 +289,7 @@ __device__ __forceinline__ void gelu_out(const LayerGemv& a, int bid, const floa
         a.hq[bid].d = b.d;
         a.hq[bid].nsum8 = b.nsum8;
       }
-      if (a.px_out >= 0) {
+      if (fout) {
         const int j = t & 7;
         uint32_t w = 0;
 #pragma unroll
@@ -300,7 +301,7 @@ __device__ __forceinline__ void gelu_out(const LayerGemv& a, int bid, const floa
       return;
     }
   }
-  if (a.px_out >= 0) px_push_word(*a.px, tout, bid * H + t, __float_as_uint(g));
+  if (fout) px_push_word(*a.px, tout, bid * H + t, __float_as_uint(g));
 }
 
 enum { SYNC_SIG = 1, SYNC_WAIT = 2 };
@@ -340,8 +341,9 @@ constexpr int HELP_K4 = 6;  // float4 per helper lane and operand: n <= E * 256 
 // launch while a work-group owns fewer rows (tensor-parallel shard entries:
 // more work-groups for a rank's slice, rows bit-identical to one device's;
 // row-major weights only).
+// PXF: the fused-exchange code (a.px_in / a.px_out honoured); false compiles it out (the one-device launches)
 template <int R, int NW, int P, int E, int ROLE, bool MULTI, bool EARLY, int SYNC = 0, int PE = 0, bool W8 = false,
-          int WT = 0, int RW0 = 0>
+          int WT = 0, int RW0 = 0, bool PXF = false>
 __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, unsigned char* s_dyn,
                                            const BlockSync& bs) {
   constexpr bool HELP = role_help(ROLE);
@@ -370,8 +372,9 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
   // this launch's granule tag, loaded up front (its latency hides under the prologue)
   const uint32_t btag = SYNC != 0 ? *bs.epoch + 1u : 0u;
   // fused exchanges (tensor-parallel ranks): the tags of the exchange read and of the one written
-  const uint32_t tin = a.px_in >= 0 ? px_link_tag(*a.px, a.px_in) : 0u;
-  const uint32_t tout = a.px_out >= 0 ? px_link_tag(*a.px, a.px_out) : 0u;
+  const bool fin = PXF && a.px_in >= 0, fout = PXF && a.px_out >= 0;
+  const uint32_t tin = fin ? px_link_tag(*a.px, a.px_in) : 0u;
+  const uint32_t tout = fout ? px_link_tag(*a.px, a.px_out) : 0u;
   // SIG: rows are published write-through; the work-group's rows lie in one
   // kv head's group (host-checked: rows per work-group divide head_dim)
   auto put_out = [&](float* p, float v) {
@@ -379,7 +382,7 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
       st_granule(bs.g_qkv + (p - a.out), __float_as_uint(v), btag);
     } else {
       *p = v;
-      if (a.px_out >= 0) px_push_word(*a.px, tout, (int)(p - a.out), __float_as_uint(v));
+      if (fout) px_push_word(*a.px, tout, (int)(p - a.out), __float_as_uint(v));
     }
   };
   // (RW0 == 0: the expressions of the all-waves launch exactly -- a select the compiler cannot fold away
@@ -592,7 +595,7 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
     const uint32_t vbytes = (uint32_t)nb * 128;
     const __amdgpu_buffer_rsrc_t ry = buf_rsrc(a.y, vbytes), rr = buf_rsrc(a.resid_in, vbytes),
                                  rp = buf_rsrc(a.w_post, a.w_post ? vbytes : 0u), rn = buf_rsrc(a.w_next, vbytes);
-    const bool yfx = a.px_in >= 0;  // y from this rank's mailbox (fused exchange), after the local operands
+    const bool yfx = fin;  // y from this rank's mailbox (fused exchange), after the local operands
 #pragma unroll
     for (int k = 0; k < EB; k++) {
       const int b = t / 4 + k * QB;
@@ -691,7 +694,7 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
     // floats are loaded before the weights and quantized while they stream
     const float4* yb = reinterpret_cast<const float4*>(a.y);
     float4 xr[E][2];
-    if (a.px_in < 0) {
+    if (!fin) {
 #pragma unroll
       for (int r = 0; r < E; r++) {
         const int i = min(t + r * T, 4 * nb - 1);
@@ -701,7 +704,7 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
     }
     if constexpr (EARLY) issue_weights();
     else issue_head();
-    if (a.px_in >= 0) {  // fused exchange: from this rank's mailbox, the weights' first passes in flight
+    if (fin) {  // fused exchange: from this rank's mailbox, the weights' first passes in flight
 #pragma unroll
       for (int r = 0; r < E; r++) {
         const int i = min(t + r * T, 4 * nb - 1);
@@ -739,7 +742,7 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
         xr[k] = make_uint4(v[0], v[1], v[2], v[3]);
       }
       BLK_MARK(bs, 4);
-    } else if (a.px_in >= 0) {  // fused exchange: the blocks from this rank's mailbox (the weights in flight first)
+    } else if (fin) {  // fused exchange: the blocks from this rank's mailbox (the weights in flight first)
       issue_weights();  // (all of them: the late tail issue below is skipped)
 #pragma unroll
       for (int k = 0; k < X_LD; k++) {
@@ -764,7 +767,7 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
   if constexpr (!HELP) {
     __syncthreads();
     if constexpr (!EARLY && SYNC != SYNC_WAIT)
-      if (!(ROLE == ROLE_PLAIN && a.px_in >= 0)) issue_tail();
+      if (!(ROLE == ROLE_PLAIN && fin)) issue_tail();
   }
 
   LAYER_MARK(4);
@@ -804,7 +807,7 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
       }
       __syncthreads();
       constexpr int H = RW * R / 2;  // hidden units of this work-group
-      gelu_out<H>(a, bid, s_rows, t, tout);
+      gelu_out<H>(a, bid, s_rows, t, fout, tout);
     } else if (!helper) {
       if constexpr (R <= 2) {
         if (lane == 0)
@@ -845,7 +848,7 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
     }
     __syncthreads();
     constexpr int H = RW * R / 2;  // hidden units of this work-group
-    gelu_out<H>(a, bid, s_rows, t, tout);
+    gelu_out<H>(a, bid, s_rows, t, fout, tout);
   } else {
 #pragma unroll
     for (int k = 0; k < R; k++) {

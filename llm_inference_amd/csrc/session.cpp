@@ -1262,7 +1262,8 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
   // tensor-parallel ranks: the o, GELU and down outputs go to the peers from the producing launches' epilogues
   // and the consumers read their mailbox (px.h) -- no exchange launches but the attention output's (head-sharded
   // mode), the last layer's down and the argmax keys
-  const bool pxf = tp_ && px_on() && !ffn_engine_;
+  bool pxf = tp_ && px_on() && !ffn_engine_;
+  for (const auto& l : L_) pxf = pxf && l.qkv.size() == 1;  // (the two-weight q|k|v launch has no fused variant)
   int k_d = -1;  // the previous layer's down exchange, read by this layer's qkv prologue
   auto fx_in = [&](LayerGemv& g, int k, int ws) {
     if (k < 0) return;
