@@ -396,6 +396,15 @@ def main():
     tok_bytes = info.bytes_per_token + info.kv_bytes_per_pos * mean_ctx
     if info.screened_logits:  # the decode loop streams the int8 screening table instead of the F16 one
         tok_bytes += info.screen_bytes - info.vocab * info.n_embd * 2
+    if a.exact and getattr(info, "exact_engine", 0):
+        # exact mode: the exact-order engine's launches are not timed family by family -- the roofline is the
+        # whole decode step (its 6 launches per layer + token selection), bytes = what the step streams
+        us_step = ms * 1000.0
+        dom_name = "exact_step"
+        dom = {"us_per_launch": round(us_step, 3), "bytes_per_launch": int(tok_bytes),
+               "GBps": round(tok_bytes / (us_step * 1e-6) / 1e9, 1),
+               "frac": round(tok_bytes / (us_step * 1e-6) / 1e9 / PEAK_HBM_GBS, 4)}
+        traffic, traffic_src = None, None
     # BASELINE.json / SURVEY 8(d) definition: every linear weight + the F16
     # logits table + KV read per token (4B: 3147.4 MB + 139.3 KB x L)
     base_bytes = info.bytes_per_token + info.kv_bytes_per_pos * mean_ctx
@@ -447,7 +456,10 @@ def main():
             "baseline_frac_of_peak": round(base_bytes * value / per_gpu / 1e9 / PEAK_HBM_GBS, 4),
         },
         "roofline": ({
-            "kernel": f"{dom_name}: the dominant kernel of the timed decode graph by time per token",
+            "kernel": (f"{dom_name}: the dominant kernel of the timed decode graph by time per token"
+                       if dom_name != "exact_step" else
+                       "exact_step: the whole exact-mode decode step (6 exact-order launches per layer + token "
+                       "selection), per token"),
             "bound": "hbm", "achieved": dom["GBps"], "peak": PEAK_HBM_GBS, "unit": "GB/s",
             "frac": dom["frac"], "traffic": traffic, "traffic_unit": "HBM bytes per launch (FETCH_SIZE x2)",
             "traffic_source": traffic_src,

@@ -186,8 +186,32 @@ __device__ __forceinline__ void xl_eat(const XlChunk& c, int g0, int ng, int jj,
   }
 }
 
-// XL_K4: PRE / GELU float4 of each operand per thread (n <= 4 XL_K4 T); NCH: chunks of XL_P groups in flight
-template <int NW, int ROLE, int XL_K4, int NCH>
+// one slot per lane (LPR 8): slot jj of the low (sh 0) or high (sh 4) nibbles -- the reference's accumulator jj or
+// jj + 4 -- over the row's blocks in order
+__device__ __forceinline__ void xl_eat1(const XlChunk& c, int g0, int ng, int jj, int sh, const int4* s_xe,
+                                        const float4* s_xd4, float& acc) {
+#pragma unroll
+  for (int p = 0; p < XL_P; p++) {
+    const int g = g0 + p;
+    if (g >= ng) break;  // wave-uniform: the chain skips what the row does not have (no +0 step)
+    const float4 xd = s_xd4[g];
+    const int4* xe = s_xe + (size_t)g * 16 + jj;
+    const uint32_t w4[4] = {c.q[p].x, c.q[p].y, c.q[p].z, c.q[p].w};
+    const uint32_t d16[4] = {c.d[p].x & 0xFFFFu, c.d[p].x >> 16, c.d[p].y & 0xFFFFu, c.d[p].y >> 16};
+    const float xdv[4] = {xd.x, xd.y, xd.z, xd.w};
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+      const int4 x = xe[4 * b];
+      const int is = sdot4((int)((w4[b] >> sh) & 0x0F0F0F0Fu), sh ? x.y : x.x, sh ? x.w : x.z);
+      acc = fmaf(h2f((uint16_t)d16[b]) * xdv[b], (float)is, acc);
+    }
+  }
+}
+
+// XL_K4: PRE / GELU float4 of each operand per thread (n <= 4 XL_K4 T); NCH: chunks of XL_P groups in flight;
+// LPR: lanes per row -- 4 (lane jj holds the reference's accumulators jj and jj + 4) or 8 (PLAIN: one accumulator
+// per lane, twice the waves over the same rows: more of the weight stream in flight for the long down rows)
+template <int NW, int ROLE, int XL_K4, int NCH, int LPR = 4>
 __global__ __launch_bounds__(NW * 64) void exact_gemv_kernel(const uint4* __restrict__ wq, const uint2* __restrict__ wd,
                                                              int rows, int nb, XlArgs a) {
   extern __shared__ int4 s_dyn[];
@@ -197,10 +221,11 @@ __global__ __launch_bounds__(NW * 64) void exact_gemv_kernel(const uint4* __rest
   float* s_b = s_a + a.n;                                            // PRE: [n] h
   __shared__ float s_scale[2];
   __shared__ float s_rows[NW * 16];
-  constexpr int T = NW * 64;
+  static_assert(LPR == 4 || (LPR == 8 && ROLE == XL_PLAIN), "8 lanes per row: the PLAIN role");
+  constexpr int T = NW * 64, RPW = 64 / LPR;  // rows per wave
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int rl = lane >> 2, jj = lane & 3;
-  const int row = (blockIdx.x * NW + wave) * 16 + rl;
+  const int rl = lane / LPR, jl = lane % LPR, jj = jl & 3;
+  const int row = (blockIdx.x * NW + wave) * RPW + rl;
   const int ng = nb >> 2;
   // weight stream: issued first, the activation prologue runs while it is in flight
   const __amdgpu_buffer_rsrc_t rq = buf_rsrc(wq, (uint32_t)((size_t)ng * rows * 64));
@@ -338,12 +363,14 @@ __global__ __launch_bounds__(NW * 64) void exact_gemv_kernel(const uint4* __rest
     for (int k = 0; k < NCH; k++) {
       const int gk = g0 + k * XL_P;
       if (gk >= ng) break;
-      xl_eat(ck[k], gk, ng, jj, s_xe, s_xd4, lo, hi);
+      if constexpr (LPR == 4) xl_eat(ck[k], gk, ng, jj, s_xe, s_xd4, lo, hi);
+      else xl_eat1(ck[k], gk, ng, jj, jl & 4, s_xe, s_xd4, lo);
       if (gk + NCH * XL_P < ng) xl_load(ck[k], rq, rd, voq, vod, sq, sd, gk + NCH * XL_P, ng);
     }
   }
   // hsum_float_8 (ops.cpp:324-330): ((a0 + a4) + (a2 + a6)) + ((a1 + a5) + (a3 + a7)); lane jj holds a_jj, a_jj+4
-  const float t4 = lo + hi;
+  // (LPR 8: lane jl < 4 holds a_jl, lane jl + 4 holds a_jl+4)
+  const float t4 = LPR == 4 ? lo + hi : lo + __shfl_xor(lo, 4);
   const float u = t4 + dpp_f<DPP_QUAD_2301>(t4);  // jj 0: t0 + t2, jj 1: t1 + t3
   const float r = u + dpp_f<DPP_QUAD_1032>(u);    // jj 0: (t0 + t2) + (t1 + t3)
   XL_MARK(6);
@@ -357,7 +384,7 @@ __global__ __launch_bounds__(NW * 64) void exact_gemv_kernel(const uint4* __rest
       q8_block_store(gv, true, a.hq + blockIdx.x, t);
     }
   } else {
-    if (jj == 0 && row_ok) a.out[row] = r;
+    if (jl == 0 && row_ok) a.out[row] = r;
   }
 }
 
@@ -867,8 +894,9 @@ void launch_exact_gemv(const XlWeight& w, const XlArgs& a_in, int role, hipStrea
   const size_t xe = (size_t)w.nb * 64 + (size_t)w.nb * 4;
   const size_t lds = xe + (role == XL_PLAIN ? 0 : (size_t)2 * a.n * 4);
   if (lds > 64 * 1024) throw std::runtime_error("exact gemv: activation exceeds LDS");
-  auto go = [&](auto kern, int nw) {
-    const unsigned grid = (unsigned)((w.rows + 16 * nw - 1) / (16 * nw));
+  auto go = [&](auto kern, int nw, int lpr = 4) {
+    const int rpg = 64 / lpr * nw;  // rows per work-group
+    const unsigned grid = (unsigned)((w.rows + rpg - 1) / rpg);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * nw), lds, s, w.qs, w.d, w.rows, w.nb, a);
   };
   // PRE / GELU: each thread holds 4 XL_K4 elements of the residual-step operands in registers
@@ -876,7 +904,7 @@ void launch_exact_gemv(const XlWeight& w, const XlArgs& a_in, int role, hipStrea
   switch (role) {
     // PLAIN / QUANT: one wave per work-group, few of them (a row group per wave), so the registers go to weight
     // chunks in flight: 4 x 8 groups (32 KB per wave)
-    case XL_PLAIN: go(exact_gemv_kernel<1, XL_PLAIN, 1, 4>, 1); break;
+    case XL_PLAIN: go(exact_gemv_kernel<1, XL_PLAIN, 1, 4, 8>, 1, 8); break;
     case XL_QUANT: go(exact_gemv_kernel<1, XL_QUANT, 1, 4>, 1); break;
     case XL_PRE:
       if (k3_2) go(exact_gemv_kernel<2, XL_PRE, 3, 2>, 2);

@@ -7,6 +7,7 @@
 #include "../../llm_inference_amd/csrc/k_exact.hip"
 
 #include <algorithm>
+#include <cstring>
 #include <cstdio>
 #include <random>
 #include <vector>
@@ -74,6 +75,75 @@ static void run(const char* name, const XlWeight& w, const XlArgs& a, int role) 
   LLMI_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_xl_trace), z.data(), z.size() * 8));
 }
 
+template <typename K>
+static void time_launch(const char* name, K launch, int reps = 20) {
+  hipEvent_t e0, e1;
+  LLMI_HIP(hipEventCreate(&e0));
+  LLMI_HIP(hipEventCreate(&e1));
+  for (int i = 0; i < 3; i++) launch();
+  LLMI_HIP(hipDeviceSynchronize());
+  LLMI_HIP(hipEventRecord(e0, 0));
+  for (int i = 0; i < reps; i++) launch();
+  LLMI_HIP(hipEventRecord(e1, 0));
+  LLMI_HIP(hipEventSynchronize(e1));
+  float ms = 0;
+  LLMI_HIP(hipEventElapsedTime(&ms, e0, e1));
+  std::printf("%-24s %8.2f us/launch\n", name, ms * 1000.0 / reps);
+  std::fflush(stdout);
+}
+
+// the PLAIN role at 4 or 8 lanes per row (down: 2560 rows of 320 blocks)
+template <int LPR, int NCH>
+static void plain_variant(const char* name, const XlWeight& w, const XlArgs& a) {
+  const size_t lds = (size_t)w.nb * 64 + (size_t)w.nb * 4;
+  const int rpg = 64 / LPR;
+  time_launch(name, [&] {
+    hipLaunchKernelGGL((exact_gemv_kernel<1, XL_PLAIN, 1, NCH, LPR>), dim3((w.rows + rpg - 1) / rpg), dim3(64), lds, 0,
+                       w.qs, w.d, w.rows, w.nb, a);
+  });
+}
+
+// the exact attention of one 4B layer at a given position (random K / V history, q|k|v row, norms, rope)
+static void attn_bench(std::mt19937& g, int pos) {
+  const int H = 8, HK = 4, HD = 256, MC = 4096;
+  XAttnArgs x;
+  x.qkv = rand_vec((H + 2 * HK) * HD, g, 1.0f);
+  x.k_off = H * HD;
+  x.v_off = (H + HK) * HD;
+  x.n_head = H;
+  x.n_head_kv = HK;
+  x.head_dim = HD;
+  x.q_norm_w = rand_vec(HD, g, 0.3f);
+  x.k_norm_w = rand_vec(HD, g, 0.3f);
+  x.rope_cs = rand_vec(MC * HD, g, 0.7f);
+  x.attn_scale = 0.0625f;
+  x.eps = 1e-6;
+  const size_t kvn = (size_t)HK * MC * HD;
+  std::vector<uint16_t> hk(kvn);
+  std::normal_distribution<float> N(0.0f, 1.0f);
+  for (auto& v : hk) { const _Float16 hv = (_Float16)N(g); std::memcpy(&v, &hv, 2); }
+  LLMI_HIP(hipMalloc(&x.k_cache, kvn * 2));
+  LLMI_HIP(hipMalloc(&x.v_cache, kvn * 2));
+  LLMI_HIP(hipMemcpy(x.k_cache, hk.data(), kvn * 2, hipMemcpyHostToDevice));
+  for (auto& v : hk) { const _Float16 hv = (_Float16)N(g); std::memcpy(&v, &hv, 2); }
+  LLMI_HIP(hipMemcpy(x.v_cache, hk.data(), kvn * 2, hipMemcpyHostToDevice));
+  x.max_ctx = MC;
+  int* dp;
+  LLMI_HIP(hipMalloc(&dp, 4));
+  LLMI_HIP(hipMemcpy(dp, &pos, 4, hipMemcpyHostToDevice));
+  x.d_pos = dp;
+  LLMI_HIP(hipMalloc(&x.scores, (size_t)H * MC * 8));
+  LLMI_HIP(hipMalloc(&x.out, (size_t)H * HD * 4));
+  LLMI_HIP(hipMalloc(&x.xq, (size_t)H * HD / 32 * sizeof(XBlock)));
+  char nm[64];
+  std::snprintf(nm, sizeof nm, "attn both (pos %d)", pos);
+  time_launch(nm, [&] { launch_exact_attn(x, 0); });
+  std::snprintf(nm, sizeof nm, "attn scores (pos %d)", pos);
+  time_launch(nm, [&] { hipLaunchKernelGGL(xattn_scores_kernel<256>, dim3(H, XA_NSPLIT), dim3(64), 0, 0, x); });
+  std::snprintf(nm, sizeof nm, "attn accum (pos %d)", pos);
+  time_launch(nm, [&] { hipLaunchKernelGGL(xattn_accum_kernel<256>, dim3(H), dim3(320), 0, 0, x); });
+}
+
 int main() {
   std::mt19937 g(1);
   const int E = 2560, F = 10240;
@@ -98,5 +168,10 @@ int main() {
   XlArgs dn;
   dn.xb = hq; dn.out = out;
   run("down", xd, dn, XL_PLAIN);
+  plain_variant<4, 4>("down LPR4 NCH4", xd, dn);
+  plain_variant<8, 4>("down LPR8 NCH4", xd, dn);
+  plain_variant<8, 2>("down LPR8 NCH2", xd, dn);
+  attn_bench(g, 600);
+  attn_bench(g, 2000);
   return 0;
 }
