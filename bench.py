@@ -174,7 +174,7 @@ def cpu_share() -> int:
     return max(1, min(n, int(os.environ.get("LLMI_CPU_SHARE", "16"))))
 
 
-def cpu_baseline(g, cfg, n_decode: int, gpu_ids=None, mean_ctx=None):
+def cpu_baseline(g, cfg, n_decode: int, gpu_ids=None, mean_ctx=None, ctx_prompt=None):
     """BASELINE.md section 4 on this host: the reference's own Model::forward
     (oracle/_ref, built from its sources) -- or, where the reference is not
     built, the oracle restatement ("port") -- timed on a bounded sample.
@@ -187,7 +187,9 @@ def cpu_baseline(g, cfg, n_decode: int, gpu_ids=None, mean_ctx=None):
       rate extrapolated to the GPU run's mean context;
     * GEMV-only timings at the 4B shapes (mat_vec_mul / mat_vec_mul_fp16);
     * configs[0]: Gemma-3 1B Q4_0, --predict 64;
-    * the CPU's greedy ids vs the GPU's on the same prompt (gpu_ids)."""
+    * the CPU's greedy ids vs the GPU's on the same prompt (gpu_ids);
+    * at the GPU line's own context (ctx_prompt: the GPU run's prompt, one untimed Model::forward of it, then
+      8 timed greedy steps at its positions): a measurement, not the extrapolation."""
     from oracle import bind
     from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf, random_tensor
     from llm_inference_amd.gguf import TensorType as TT
@@ -237,6 +239,24 @@ def cpu_baseline(g, cfg, n_decode: int, gpu_ids=None, mean_ctx=None):
         out["estimated_at_gpu_mean_context"] = {
             "position": int(mean_ctx), "value": round(1.0 / (icpt + max(slope, 0.0) * mean_ctx), 3),
             "unit": "tokens/s", "how": "step time = a + b * pos fitted to the measured per-step times"}
+    # (bounded: the reference's T-token forward costs about T decode steps, so it runs when that is <= 40 s here)
+    if ctx_prompt is not None and kind == "reference" and len(ctx_prompt) * float(np.median(per)) <= 40.0:
+        kind_c, eng_c = engine(threads)
+        mc = model(eng_c, kind_c, g, threads)
+        t0 = time.perf_counter()
+        lg = mc.forward(np.asarray(ctx_prompt, np.int32), 0)
+        t_pf = time.perf_counter() - t0
+        tok, pos, per_c = int(np.argmax(lg)), len(ctx_prompt), []
+        for _ in range(8):
+            t0 = time.perf_counter()
+            lg = mc.forward(np.array([tok], np.int32), pos)
+            per_c.append(time.perf_counter() - t0)
+            tok, pos = int(np.argmax(lg)), pos + 1
+        del mc
+        out["measured_at_gpu_context"] = {
+            "positions": f"{len(ctx_prompt)}-{len(ctx_prompt) + 7}", "value": round(8 / sum(per_c), 3),
+            "unit": "tokens/s", "threads": threads, "prefill_s": round(t_pf, 2),
+            "how": "the GPU line's prompt through one untimed Model::forward, then 8 timed greedy steps"}
     out["ids"] = ids
     if gpu_ids is not None:
         k = min(len(ids), len(gpu_ids))
@@ -486,7 +506,7 @@ def main():
     if d.rank == 0 and d.world == 1 and not a.no_cpu_baseline:
         m.close()
         try:
-            out["cpu_baseline"] = cpu_baseline(g, cfg, a.cpu_decode, gpu_ids, mean_ctx)
+            out["cpu_baseline"] = cpu_baseline(g, cfg, a.cpu_decode, gpu_ids, mean_ctx, ctx_prompt=prompt)
         except Exception as e:  # report, never hide
             out["cpu_baseline"] = {"error": repr(e)}
     if d.rank == 0:
