@@ -87,6 +87,10 @@ struct XAttnArgs {
   float* out = nullptr;      // [n_head][head_dim]
   XBlock* xq = nullptr;      // [n_head * head_dim / 32]
   float softcap = 0.0f;      // attention.logit_softcapping (model.cpp:511-513); 0: none
+  // the V cache transposed, [n_head_kv][head_dim][vt_stride] f16 (vt_stride % 8 == 0): the scores kernel appends
+  // the new key's column, the accumulate kernel reads 8 keys of its head dim per 16-B load
+  uint16_t* vt = nullptr;
+  int vt_stride = 0;
 };
 bool exact_attn_supported(int head_dim, int n_head, int n_head_kv);
 void launch_exact_attn(const XAttnArgs& a, hipStream_t s);

@@ -74,7 +74,8 @@ LLMI_HD uint64_t exp2f_tab(int i) {
 //   kd = fma(InvLn2N, x, SHIFT); ki = bits(kd); kd -= SHIFT;
 //   r = fma(InvLn2N, x, -kd); s = double(tab[ki % 32] + (ki << 47));
 //   y = fma(fma(C0, r, C1), r*r, fma(C2, r, 1)) * s;  return (float)y
-LLMI_HD float expf(float x) {
+// (tab: the 32 entries of exp2f_tab, e.g. staged in LDS by a kernel that calls this per element)
+LLMI_HD float expf_tab(float x, const uint64_t* tab) {
   const uint32_t abstop = (fbits(x) >> 20) & 0x7ff;
   if (abstop > 0x42a) {                             // |x| >= 88 or NaN (top12(88.0f) = 0x42b)
     if (fbits(x) == 0xff800000u) return 0.0f;       // -inf
@@ -93,13 +94,20 @@ LLMI_HD float expf(float x) {
   const uint64_t ki = dbits(kd);
   kd -= SHIFT;
   const double r = __builtin_fma(InvLn2N, xd, -kd);
-  const uint64_t t = exp2f_tab((int)(ki & 31)) + (ki << 47);
+  const uint64_t t = tab[ki & 31] + (ki << 47);
   const double s = bitsd(t);
   const double z = __builtin_fma(C0, r, C1);
   const double r2 = r * r;
   const double y1 = __builtin_fma(C2, r, 1.0);
   const double y = __builtin_fma(z, r2, y1) * s;
   return (float)y;
+}
+LLMI_HD float expf(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return expf_tab(x, kExp2fTabDev);
+#else
+  return expf_tab(x, kExp2fTabHost);
+#endif
 }
 
 // glibc 2.35 __expm1f (sysdeps/ieee754/flt-32/s_expm1f.c, fdlibm; SSE, no FMA)

@@ -625,6 +625,36 @@ __global__ __launch_bounds__(256) void gemv_bf16_exact(const uint16_t* __restric
   out[row] = sum;
 }
 
+// BF16 fast (ops.cpp:895-931 restated with reassociated sums): R rows per wave, L = 64 / R lanes per row, each
+// lane streams 16-B runs of 8 weights (bf16 -> f32 is a 16-bit shift) against float4 pairs of x, then a
+// row-group butterfly.  Rows whose length is not a multiple of 8 take the exact kernel.
+template <int R>
+__global__ __launch_bounds__(256) void gemv_bf16_fast(const uint4* __restrict__ w, int rows, int nc,
+                                                      const float4* __restrict__ x, float* __restrict__ out) {
+  constexpr int L = 64 / R;
+  const int lane = threadIdx.x & 63, j = lane % L;
+  const int row = (blockIdx.x * 4 + (threadIdx.x >> 6)) * R + lane / L;
+  const bool ok = row < rows;
+  const uint4* wr = w + (size_t)(ok ? row : 0) * nc;
+  float a0 = 0.0f, a1 = 0.0f;
+  for (int c = j; c < nc; c += L) {
+    const uint4 q = ok ? wr[c] : make_uint4(0, 0, 0, 0);
+    const float4 x0 = x[2 * c], x1 = x[2 * c + 1];
+    a0 = fmaf(__uint_as_float(q.x << 16), x0.x, a0);
+    a1 = fmaf(__uint_as_float(q.x & 0xFFFF0000u), x0.y, a1);
+    a0 = fmaf(__uint_as_float(q.y << 16), x0.z, a0);
+    a1 = fmaf(__uint_as_float(q.y & 0xFFFF0000u), x0.w, a1);
+    a0 = fmaf(__uint_as_float(q.z << 16), x1.x, a0);
+    a1 = fmaf(__uint_as_float(q.z & 0xFFFF0000u), x1.y, a1);
+    a0 = fmaf(__uint_as_float(q.w << 16), x1.z, a0);
+    a1 = fmaf(__uint_as_float(q.w & 0xFFFF0000u), x1.w, a1);
+  }
+  float v = a0 + a1;
+#pragma unroll
+  for (int o = L / 2; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  if (j == 0 && ok) out[row] = v;
+}
+
 // ===========================================================================
 // launcher
 // ===========================================================================
@@ -780,8 +810,22 @@ void launch_gemv(const DevWeight& w, const ActBuf& x, float* o, GemvMode mode, h
       break;
     }
     case T_BF16:
-      hipLaunchKernelGGL(gemv_bf16_exact, dim3((rows + 255) / 256), dim3(256), 0, s, (const uint16_t*)w.qs, rows,
-                         w.cols, x.xf, o);
+      if (mode == GEMV_EXACT || w.cols % 8 != 0) {
+        hipLaunchKernelGGL(gemv_bf16_exact, dim3((rows + 255) / 256), dim3(256), 0, s, (const uint16_t*)w.qs, rows,
+                           w.cols, x.xf, o);
+      } else {  // lanes per row: the row's 16-B runs in about one pass, at least 8 lanes
+        const int nc = w.cols / 8;
+        const int R = nc >= 64 ? 1 : nc >= 32 ? 2 : nc >= 16 ? 4 : 8;
+        const dim3 grid((rows + 4 * R - 1) / (4 * R));
+        switch (R) {
+#define LLMI_BF(RR)                                                                                               \
+  case RR:                                                                                                        \
+    hipLaunchKernelGGL(gemv_bf16_fast<RR>, grid, dim3(256), 0, s, (const uint4*)w.qs, rows, nc, (const float4*)x.xf, o); \
+    break;
+          LLMI_BF(1) LLMI_BF(2) LLMI_BF(4) LLMI_BF(8)
+#undef LLMI_BF
+        }
+      }
       break;
     default:
       throw std::runtime_error("mat_vec_mul: unsupported tensor type " + std::to_string(w.type));

@@ -1568,6 +1568,12 @@ void Session::setup_xl() {
   for (const auto& l : L_) maxhd = std::max(maxhd, l.hd);
   xa_scores_ = dalloc<double>((size_t)hp_.n_head * max_ctx_);
   xa_xq_ = dalloc<XBlock>((size_t)hp_.n_head * maxhd / 32);
+  xa_vt_stride_ = (max_ctx_ + 7) / 8 * 8;
+  for (auto& l : L_) {  // the transposed V caches (zeroed: columns past the context are loaded, never summed)
+    const size_t n = (size_t)hp_.n_head_kv * l.hd * xa_vt_stride_;
+    l.vt = dalloc<uint16_t>(n);
+    LLMI_HIP(hipMemsetAsync(l.vt, 0, n * 2, stream_));
+  }
   LLMI_HIP(hipStreamSynchronize(stream_));
   xl_ = true;
 }
@@ -1620,6 +1626,8 @@ void Session::record_layers_xl(hipStream_t s) {
     xa.out = attn_;
     xa.xq = xa_xq_;
     xa.softcap = hp_.attn_softcap;
+    xa.vt = Ld.vt;
+    xa.vt_stride = xa_vt_stride_;
     launch_exact_attn(xa, s);
     XlArgs o;
     o.xb = xa_xq_;

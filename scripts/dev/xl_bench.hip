@@ -75,6 +75,267 @@ static void run(const char* name, const XlWeight& w, const XlArgs& a, int role) 
   LLMI_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_xl_trace), z.data(), z.size() * 8));
 }
 
+#define XL_MARK_NL(ph) do { } while (0)
+// the round-4 first cut of the accumulate kernel (per-lane V loads), for the A/B
+namespace llmi {
+namespace {
+template <int HD>
+__global__ __launch_bounds__((HD / 64 + 1) * 64) void xattn_accum_kernel_old(XAttnArgs a) {
+  constexpr int NWV = HD / 64, T = (NWV + 1) * 64;
+  constexpr int KPT = XA_CH / 256;  // keys per scan thread (threads 0..255)
+  __shared__ double s_sc[XA_CH];
+  __shared__ __attribute__((aligned(16))) float s_e[XA_CH];   // e per key
+  __shared__ __attribute__((aligned(16))) float s_pe[XA_CH];  // pe per key
+  __shared__ uint32_t s_up[XA_CH / 32];
+  __shared__ double s_tmax[256];
+  __shared__ float s_sacc;
+  const int h = blockIdx.x, t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  const int n_keys = *a.d_pos + 1;
+  const int hkv = h / (a.n_head / a.n_head_kv);
+  const uint16_t* vb = a.v_cache + (size_t)hkv * a.max_ctx * HD + wave * 64 + lane;
+  const double* sc_in = a.scores + (size_t)h * a.max_ctx;
+  XL_MARK(0);
+  double run_max = -INFINITY;
+  uint16_t v16 = 0;  // f32_to_f16(0.0f)
+  float s_acc = 0.0f;
+  for (int c0 = 0; c0 < n_keys; c0 += XA_CH) {
+    const int nk = min(XA_CH, n_keys - c0);
+    for (int i = t; i < nk; i += T)
+      s_sc[i] = a.softcap > 0.0f ? llmi_glibc::softcap_score(sc_in[c0 + i], a.softcap) : sc_in[c0 + i];
+    for (int i = t; i < XA_CH / 32; i += T) s_up[i] = 0u;
+    __syncthreads();
+    XL_MARK(1);
+    double tmax = -INFINITY;
+    if (t < 256) {
+#pragma unroll
+      for (int k = 0; k < KPT; k++) {
+        const int j = t * KPT + k;
+        if (j < nk) tmax = fmax(tmax, s_sc[j]);
+      }
+      s_tmax[t] = tmax;
+    }
+    __syncthreads();
+    for (int o = 1; o < 256; o <<= 1) {  // inclusive prefix max over the 256 segments (max is exact)
+      const double v = (t < 256 && t >= o) ? s_tmax[t - o] : -INFINITY;
+      __syncthreads();
+      if (t < 256) s_tmax[t] = fmax(s_tmax[t], v);
+      __syncthreads();
+    }
+    XL_MARK(2);
+    if (t < 256) {
+      double pm = fmax(run_max, t > 0 ? s_tmax[t - 1] : -INFINITY);  // max of every key before this segment
+#pragma unroll
+      for (int k = 0; k < KPT; k++) {
+        const int j = t * KPT + k;
+        if (j >= nk) break;
+        const double score = s_sc[j];
+        const float prev = (float)pm;  // the reference's max_score before key j
+        if (score > (double)prev) {    // model.cpp:520-532
+          s_e[j] = 1.0f;
+          s_pe[j] = llmi_glibc::expf(prev - (float)score);
+          atomicOr(&s_up[j >> 5], 1u << (j & 31));
+        } else {
+          s_e[j] = llmi_glibc::expf((float)(score - (double)prev));
+          s_pe[j] = 1.0f;
+        }
+        pm = fmax(pm, score);
+      }
+    }
+    run_max = fmax(run_max, s_tmax[255]);
+    __syncthreads();
+    XL_MARK(3);
+    if (wave < NWV) {  // this lane's head dim: vec_scale_f16 when the max moved, then vec_mad_f16 (ops.cpp:1084-1099)
+      const uint16_t* vp = vb + (size_t)c0 * HD;
+      // V of 32 keys per batch, the next batch's loads issued before this one is summed (clamped keys past the
+      // chunk are loaded but never summed)
+      uint32_t va[32], vn[32];  // one f16 per register (low half): the mad8 asm reads them as they are
+#pragma unroll
+      for (int u = 0; u < 32; u++) va[u] = vp[(size_t)min(u, nk - 1) * HD];
+      for (int j0 = 0; j0 < nk; j0 += 32) {
+#pragma unroll
+        for (int u = 0; u < 32; u++) vn[u] = vp[(size_t)min(j0 + 32 + u, nk - 1) * HD];
+        // the batch's max moves (wave-uniform, a scalar branch per key) and e values (broadcast LDS reads)
+        const uint32_t up = __builtin_amdgcn_readfirstlane(s_up[j0 >> 5]);
+        const int m = __builtin_amdgcn_readfirstlane(min(32, nk - j0));
+        float e[32];
+#pragma unroll
+        for (int u4 = 0; u4 < 8; u4++) {
+          const float4 q = reinterpret_cast<const float4*>(s_e + j0)[u4];
+          e[4 * u4] = q.x; e[4 * u4 + 1] = q.y; e[4 * u4 + 2] = q.z; e[4 * u4 + 3] = q.w;
+        }
+        // each step rounds to f32 (the fma), then to f16 (the conversion as its own instruction: fused by the
+        // compiler into v_fma_mixlo_f16 it would round once, another f16 whenever the f32 value is a midpoint)
+        if (up == 0 && m == 32) {  // the common batch: the max did not move, 32 straight fma + round steps
+          uint32_t acc = v16;
+#pragma unroll
+          for (int u = 0; u < 32; u += 8) xa_mad8(acc, va + u, e + u);
+          v16 = (uint16_t)acc;
+        } else {
+#pragma unroll
+          for (int u = 0; u < 32; u++) {
+            if (u < m) {
+              if (up & (1u << u)) v16 = cvt_f16_rne((float)__builtin_bit_cast(_Float16, v16) * s_pe[j0 + u]);
+              v16 = cvt_f16_rne(fmaf((float)__builtin_bit_cast(_Float16, (uint16_t)va[u]), e[u], (float)__builtin_bit_cast(_Float16, v16)));
+            }
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 32; u++) va[u] = vn[u];
+      }
+    } else {  // s_acc = s_acc * pe + e, keys in order (model.cpp:540)
+      for (int j0 = 0; j0 < nk; j0 += 4) {
+        const float4 e4 = reinterpret_cast<const float4*>(s_e + j0)[0];
+        const float4 p4 = reinterpret_cast<const float4*>(s_pe + j0)[0];
+        const float ev[4] = {e4.x, e4.y, e4.z, e4.w}, pv[4] = {p4.x, p4.y, p4.z, p4.w};
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+          if (j0 + u < nk) s_acc = s_acc * pv[u] + ev[u];
+      }
+    }
+    XL_MARK(4);
+    __syncthreads();  // the chunk's LDS is reused by the next one
+    XL_MARK(5);
+  }
+  if (wave == NWV && lane == 0) s_sacc = s_acc == 0.0f ? 0.0f : 1.0f / s_acc;
+  __syncthreads();
+  if (wave < NWV) {
+    const int d = wave * 64 + lane;
+    const float o = h2f(v16) * s_sacc;  // model.cpp:543-547
+    a.out[(size_t)h * HD + d] = o;
+    q8_block_store(o, true, a.xq + ((size_t)h * HD + wave * 64) / 32 + (lane >> 5), lane & 31);
+  }
+}
+
+template <int HD>
+__global__ __launch_bounds__((HD / 64 + 1) * 64) void xattn_accum_kernel_noload(XAttnArgs a) {
+  constexpr int NWV = HD / 64, T = (NWV + 1) * 64;
+  constexpr int KPT = XA_CH / 256;  // keys per scan thread (threads 0..255)
+  __shared__ double s_sc[XA_CH];
+  __shared__ __attribute__((aligned(16))) float s_e[XA_CH];   // e per key
+  __shared__ __attribute__((aligned(16))) float s_pe[XA_CH];  // pe per key
+  __shared__ uint32_t s_up[XA_CH / 32];
+  __shared__ double s_tmax[256];
+  __shared__ float s_sacc;
+  const int h = blockIdx.x, t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  const int n_keys = *a.d_pos + 1;
+  const int hkv = h / (a.n_head / a.n_head_kv);
+  const uint16_t* vb = a.v_cache + (size_t)hkv * a.max_ctx * HD + wave * 64 + lane;
+  const double* sc_in = a.scores + (size_t)h * a.max_ctx;
+  XL_MARK_NL(0);
+  double run_max = -INFINITY;
+  uint16_t v16 = 0;  // f32_to_f16(0.0f)
+  float s_acc = 0.0f;
+  for (int c0 = 0; c0 < n_keys; c0 += XA_CH) {
+    const int nk = min(XA_CH, n_keys - c0);
+    for (int i = t; i < nk; i += T)
+      s_sc[i] = a.softcap > 0.0f ? llmi_glibc::softcap_score(sc_in[c0 + i], a.softcap) : sc_in[c0 + i];
+    for (int i = t; i < XA_CH / 32; i += T) s_up[i] = 0u;
+    __syncthreads();
+    XL_MARK_NL(1);
+    double tmax = -INFINITY;
+    if (t < 256) {
+#pragma unroll
+      for (int k = 0; k < KPT; k++) {
+        const int j = t * KPT + k;
+        if (j < nk) tmax = fmax(tmax, s_sc[j]);
+      }
+      s_tmax[t] = tmax;
+    }
+    __syncthreads();
+    for (int o = 1; o < 256; o <<= 1) {  // inclusive prefix max over the 256 segments (max is exact)
+      const double v = (t < 256 && t >= o) ? s_tmax[t - o] : -INFINITY;
+      __syncthreads();
+      if (t < 256) s_tmax[t] = fmax(s_tmax[t], v);
+      __syncthreads();
+    }
+    XL_MARK_NL(2);
+    if (t < 256) {
+      double pm = fmax(run_max, t > 0 ? s_tmax[t - 1] : -INFINITY);  // max of every key before this segment
+#pragma unroll
+      for (int k = 0; k < KPT; k++) {
+        const int j = t * KPT + k;
+        if (j >= nk) break;
+        const double score = s_sc[j];
+        const float prev = (float)pm;  // the reference's max_score before key j
+        if (score > (double)prev) {    // model.cpp:520-532
+          s_e[j] = 1.0f;
+          s_pe[j] = llmi_glibc::expf(prev - (float)score);
+          atomicOr(&s_up[j >> 5], 1u << (j & 31));
+        } else {
+          s_e[j] = llmi_glibc::expf((float)(score - (double)prev));
+          s_pe[j] = 1.0f;
+        }
+        pm = fmax(pm, score);
+      }
+    }
+    run_max = fmax(run_max, s_tmax[255]);
+    __syncthreads();
+    XL_MARK_NL(3);
+    if (wave < NWV) {  // this lane's head dim: vec_scale_f16 when the max moved, then vec_mad_f16 (ops.cpp:1084-1099)
+      const uint16_t* vp = vb + (size_t)c0 * HD;
+      // V of 32 keys per batch, the next batch's loads issued before this one is summed (clamped keys past the
+      // chunk are loaded but never summed)
+      uint32_t va[32], vn[32];  // one f16 per register (low half): the mad8 asm reads them as they are
+#pragma unroll
+      for (int u = 0; u < 32; u++) va[u] = vp[(size_t)min(u, nk - 1) * HD];
+      for (int j0 = 0; j0 < nk; j0 += 32) {
+#pragma unroll
+        for (int u = 0; u < 32; u++) vn[u] = va[u] ^ 1u;  // (timing variant: no V loads in the loop)
+        // the batch's max moves (wave-uniform, a scalar branch per key) and e values (broadcast LDS reads)
+        const uint32_t up = __builtin_amdgcn_readfirstlane(s_up[j0 >> 5]);
+        const int m = __builtin_amdgcn_readfirstlane(min(32, nk - j0));
+        float e[32];
+#pragma unroll
+        for (int u4 = 0; u4 < 8; u4++) {
+          const float4 q = reinterpret_cast<const float4*>(s_e + j0)[u4];
+          e[4 * u4] = q.x; e[4 * u4 + 1] = q.y; e[4 * u4 + 2] = q.z; e[4 * u4 + 3] = q.w;
+        }
+        // each step rounds to f32 (the fma), then to f16 (the conversion as its own instruction: fused by the
+        // compiler into v_fma_mixlo_f16 it would round once, another f16 whenever the f32 value is a midpoint)
+        if (up == 0 && m == 32) {  // the common batch: the max did not move, 32 straight fma + round steps
+          uint32_t acc = v16;
+#pragma unroll
+          for (int u = 0; u < 32; u += 8) xa_mad8(acc, va + u, e + u);
+          v16 = (uint16_t)acc;
+        } else {
+#pragma unroll
+          for (int u = 0; u < 32; u++) {
+            if (u < m) {
+              if (up & (1u << u)) v16 = cvt_f16_rne((float)__builtin_bit_cast(_Float16, v16) * s_pe[j0 + u]);
+              v16 = cvt_f16_rne(fmaf((float)__builtin_bit_cast(_Float16, (uint16_t)va[u]), e[u], (float)__builtin_bit_cast(_Float16, v16)));
+            }
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 32; u++) va[u] = vn[u];
+      }
+    } else {  // s_acc = s_acc * pe + e, keys in order (model.cpp:540)
+      for (int j0 = 0; j0 < nk; j0 += 4) {
+        const float4 e4 = reinterpret_cast<const float4*>(s_e + j0)[0];
+        const float4 p4 = reinterpret_cast<const float4*>(s_pe + j0)[0];
+        const float ev[4] = {e4.x, e4.y, e4.z, e4.w}, pv[4] = {p4.x, p4.y, p4.z, p4.w};
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+          if (j0 + u < nk) s_acc = s_acc * pv[u] + ev[u];
+      }
+    }
+    XL_MARK_NL(4);
+    __syncthreads();  // the chunk's LDS is reused by the next one
+    XL_MARK_NL(5);
+  }
+  if (wave == NWV && lane == 0) s_sacc = s_acc == 0.0f ? 0.0f : 1.0f / s_acc;
+  __syncthreads();
+  if (wave < NWV) {
+    const int d = wave * 64 + lane;
+    const float o = h2f(v16) * s_sacc;  // model.cpp:543-547
+    a.out[(size_t)h * HD + d] = o;
+    q8_block_store(o, true, a.xq + ((size_t)h * HD + wave * 64) / 32 + (lane >> 5), lane & 31);
+  }
+}
+
+}  // namespace
+}  // namespace llmi
+
 template <typename K>
 static void time_launch(const char* name, K launch, int reps = 20) {
   hipEvent_t e0, e1;
@@ -104,6 +365,7 @@ static void plain_variant(const char* name, const XlWeight& w, const XlArgs& a) 
 }
 
 // the exact attention of one 4B layer at a given position (random K / V history, q|k|v row, norms, rope)
+static void phases(const char* what, int H);
 static void attn_bench(std::mt19937& g, int pos) {
   const int H = 8, HK = 4, HD = 256, MC = 4096;
   XAttnArgs x;
@@ -127,6 +389,15 @@ static void attn_bench(std::mt19937& g, int pos) {
   LLMI_HIP(hipMemcpy(x.k_cache, hk.data(), kvn * 2, hipMemcpyHostToDevice));
   for (auto& v : hk) { const _Float16 hv = (_Float16)N(g); std::memcpy(&v, &hv, 2); }
   LLMI_HIP(hipMemcpy(x.v_cache, hk.data(), kvn * 2, hipMemcpyHostToDevice));
+  {  // the transposed copy the scores kernel maintains ([kv][hd][stride])
+    x.vt_stride = MC;
+    std::vector<uint16_t> vt(kvn);
+    for (int kv = 0; kv < HK; kv++)
+      for (int p = 0; p < MC; p++)
+        for (int d = 0; d < HD; d++) vt[((size_t)kv * HD + d) * MC + p] = hk[((size_t)kv * MC + p) * HD + d];
+    LLMI_HIP(hipMalloc(&x.vt, kvn * 2));
+    LLMI_HIP(hipMemcpy(x.vt, vt.data(), kvn * 2, hipMemcpyHostToDevice));
+  }
   x.max_ctx = MC;
   int* dp;
   LLMI_HIP(hipMalloc(&dp, 4));
@@ -142,6 +413,40 @@ static void attn_bench(std::mt19937& g, int pos) {
   time_launch(nm, [&] { hipLaunchKernelGGL(xattn_scores_kernel<256>, dim3(H, XA_NSPLIT), dim3(64), 0, 0, x); });
   std::snprintf(nm, sizeof nm, "attn accum (pos %d)", pos);
   time_launch(nm, [&] { hipLaunchKernelGGL(xattn_accum_kernel<256>, dim3(H), dim3(320), 0, 0, x); });
+  phases("accum", H);
+  {  // the same launch with every Vt load inside one 1-KB run per wave (L1 hits, 8 lines per load): the V fetch
+     // shape's share of the accumulate
+    const int st = x.vt_stride;
+    x.vt_stride = 8;
+    std::snprintf(nm, sizeof nm, "attn accum cheapV (pos %d)", pos);
+    time_launch(nm, [&] { hipLaunchKernelGGL(xattn_accum_kernel<256>, dim3(H), dim3(320), 0, 0, x); });
+    phases("accum cheapV", H);
+    x.vt_stride = st;
+  }
+  std::snprintf(nm, sizeof nm, "attn accum old (pos %d)", pos);
+  time_launch(nm, [&] { hipLaunchKernelGGL(xattn_accum_kernel_old<256>, dim3(H), dim3(320), 0, 0, x); });
+  std::snprintf(nm, sizeof nm, "attn accum no-V (pos %d)", pos);
+  time_launch(nm, [&] { hipLaunchKernelGGL(xattn_accum_kernel_noload<256>, dim3(H), dim3(320), 0, 0, x); });
+  phases("accum old", H);
+}
+
+// phase clocks of the last launch, median over the heads' work-groups
+static void phases(const char* what, int H) {
+  {
+    std::vector<unsigned long long> tr(8192 * 8);
+    LLMI_HIP(hipMemcpyFromSymbol(tr.data(), HIP_SYMBOL(g_xl_trace), tr.size() * 8));
+    std::printf("   %s phases (cycles): ", what);
+    for (int ph = 1; ph <= 5; ph++) {
+      std::vector<long long> v;
+      for (int b = 0; b < H; b++)
+        if (tr[b * 8] && tr[b * 8 + ph]) v.push_back((long long)(tr[b * 8 + ph] - tr[b * 8]));
+      std::sort(v.begin(), v.end());
+      std::printf(" %d:%lld", ph, v.empty() ? -1LL : v[v.size() / 2]);
+    }
+    std::printf("\n");
+    std::vector<unsigned long long> z(8192 * 8, 0);
+    LLMI_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_xl_trace), z.data(), z.size() * 8));
+  }
 }
 
 int main() {
@@ -171,6 +476,8 @@ int main() {
   plain_variant<4, 4>("down LPR4 NCH4", xd, dn);
   plain_variant<8, 4>("down LPR8 NCH4", xd, dn);
   plain_variant<8, 2>("down LPR8 NCH2", xd, dn);
+  attn_bench(g, 1);
+  attn_bench(g, 64);
   attn_bench(g, 600);
   attn_bench(g, 2000);
   return 0;

@@ -199,6 +199,20 @@ def test_gemv_q5_0_fast_vs_oracle(ops, oracle, rows, cols):
     assert np.abs(o - ref).max() <= 1e-4 * np.abs(ref).max() + 1e-6
 
 
+@pytest.mark.parametrize("rows,cols", [(5, 8), (300, 96), (77, 2560), (40, 8192), (3, 100)])
+def test_gemv_bf16_fast_vs_oracle(ops, oracle, rows, cols):
+    """Fast BF16 GEMV (k_gemv.hip gemv_bf16_fast: the Gemma-4 per-layer model projection, ops.cpp:895-931) vs the
+    oracle at lane-group widths 8..64 (cols 100: not a multiple of 8, the exact kernel): the fast-GEMV tolerance;
+    the exact kernel bit-identical."""
+    from llm_inference_amd.synthetic import random_tensor
+    w = random_tensor(T.BF16, rows, cols, seed=rows * 7 + cols)
+    x = np.random.default_rng(cols + 1).standard_normal(cols).astype(np.float32)
+    ref = oracle.mat_vec_mul(T.BF16, w, rows, cols, x)
+    np.testing.assert_array_equal(bits(ops.mat_vec_mul_raw(T.BF16, w, rows, cols, x, exact=True)), bits(ref))
+    o = ops.mat_vec_mul_raw(T.BF16, w, rows, cols, x, exact=False)
+    assert np.abs(o - ref).max() <= 1e-4 * np.abs(ref).max() + 1e-6
+
+
 @pytest.mark.gpu
 def test_f16_conversion_selftest():
     """The exact attention's f16 V accumulator (k_exact.hip) rounds with the hardware f32 -> f16 conversion:
