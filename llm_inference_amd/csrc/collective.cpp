@@ -69,9 +69,15 @@ class Mailbox {
     if (rank < 0 || rank >= G) throw std::runtime_error("push exchange: rank out of range");
     const size_t bytes = (size_t)2 * G * kSlot * sizeof(uint2);
     LLMI_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&mine_), bytes, hipDeviceMallocUncached));
+    // (the one-GPU 4-rank test: about one run in 15 timed out on a peer's checksum granule holding the same
+    // foreign granule every time -- a dirty L2 line of this memory's earlier owner, written back after the
+    // zeroing; scripts/dev/tp_repeat4.py)
+    l2_writeback_all();
     LLMI_HIP(hipMemset(mine_, 0, bytes));  // tag 0: nothing published (tags are >= 1)
-    LLMI_HIP(hipMalloc(&ctl_, 4 * sizeof(unsigned)));
-    LLMI_HIP(hipMemset(ctl_, 0, 4 * sizeof(unsigned)));
+    // the exchange count uncached too: every work-group reads it (px_link_tag, the exchange kernels' tag), and a
+    // cached line could outlive this allocation's reuse of an earlier group's memory
+    LLMI_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&ctl_), 8 * sizeof(unsigned), hipDeviceMallocUncached));
+    LLMI_HIP(hipMemset(ctl_, 0, 8 * sizeof(unsigned)));
     LLMI_HIP(hipDeviceSynchronize());
     peers_.assign(G, nullptr);
     peers_[rank] = mine_;
@@ -169,18 +175,27 @@ class Mailbox {
     launch_push_exchange(a, s);
   }
   int failed() {  // reads and clears the device flag (callers have synchronised the stream)
-    int e = 0;
-    LLMI_HIP(hipMemcpy(&e, ctl_ + 2, sizeof(int), hipMemcpyDeviceToHost));
-    if (e) LLMI_HIP(hipMemset(ctl_ + 2, 0, sizeof(int)));
-    return e;
+    int e[6] = {0, 0, 0, 0, 0, 0};
+    LLMI_HIP(hipMemcpy(e, ctl_ + 2, sizeof(e), hipMemcpyDeviceToHost));
+    if (e[0]) {
+      LLMI_HIP(hipMemset(ctl_ + 2, 0, sizeof(e)));
+      // a timed-out wait: the word it last saw (its tag relative to the expected one), kind and place
+      detail_ = e[0] == 2 ? "" : std::string(e[0] == 3 ? " [fused" : " [standalone") + " exchange, tag " +
+                                     std::to_string((unsigned)e[3]) + ", word " + std::to_string(e[2]) +
+                                     " held tag " + (e[1] >= 0 ? "+" : "") + std::to_string(e[1]) + " word " +
+                                     std::to_string((unsigned)e[4]) + " at " + std::to_string(e[5]) + "]";
+    }
+    return e[0];
   }
+  const std::string& detail() const { return detail_; }
 
  private:
   int rank_, G_;
   uint64_t timeout_;
   bool seeded_ = false;
   uint2* mine_ = nullptr;
-  unsigned* ctl_ = nullptr;  // [0] exchange count, [1] ticket, [2] error flag
+  unsigned* ctl_ = nullptr;  // [0] exchange count, [1] ticket, [2] error flag, [3..5] its diagnostics
+  std::string detail_;
   std::vector<uint2*> peers_;
   bool opened_ = false;
 };
@@ -201,6 +216,7 @@ class PeerCollective : public Collective {
   bool fused_capable() const override { return true; }
   void fused_link(PxLink& l) override { mb_.link(l); }
   int failed() override { return mb_.failed(); }
+  std::string fail_detail() const override { return mb_.detail(); }
   void peer_handle(void* out) const override { mb_.handle(out); }
   void peer_connect(const void* handles) override { mb_.open(handles); }
 
@@ -262,21 +278,21 @@ class LocalCollective : public Collective {
   bool graph_safe() const override { return false; }
   int kind() const override { return push_ ? EX_PUSH : EX_COPY; }
   int failed() override { return push_ ? mb_->failed() : 0; }
+  std::string fail_detail() const override { return push_ ? mb_->detail() : std::string(); }
   bool fused_capable() const override { return push_; }
   void fused_link(PxLink& l) override {
     if (!push_) Collective::fused_link(l);
     connect();
     mb_->link(l);
   }
-  // every rank's producing launch has completed before this rank's consumer runs (the ranks' streams share the
-  // process's hardware queues: a consumer spinning ahead of a peer's producer could block it)
+  // every rank's producing launch has completed before any rank's consumer is enqueued (the ranks' streams share
+  // the process's hardware queues: a consumer spinning ahead of a peer's producer could block it).  Host-side:
+  // each rank drains its own stream, then the host barrier -- no cross-stream event waits (with the ranks'
+  // streams folded onto shared hardware queues those let a wait and a peer's launches interleave; the one-GPU
+  // 4-rank test timed out about once in 25 runs with them, scripts/dev/tp_repeat4.py)
   void fused_point(hipStream_t s) override {
-    LocalGroup& g = *g_;
-    LLMI_HIP(hipEventRecord(g.ready[rank_], s));
-    g.barrier();
-    for (int q = 0; q < size_; q++)
-      if (q != rank_) LLMI_HIP(hipStreamWaitEvent(s, g.ready[q], 0));
-    g.barrier();  // nobody re-records its event before every peer has waited on it
+    LLMI_HIP(hipStreamSynchronize(s));
+    g_->barrier();
   }
   bool all_gather_cols(void* buf, size_t pitch, size_t slice, int rows, hipStream_t s, int skip) override {
     if (!push_) return false;
@@ -320,12 +336,9 @@ class LocalCollective : public Collective {
       const int sk = c == 0 ? skip : 0;
       if (drop_) drop_ = false;  // the test hook: the peers' gathers wait past their bound
       else mb_->run_chunk(buf, bytes, c, PX_PUSH, s, sk, pitch, slice);
-      LLMI_HIP(hipEventRecord(g.ready[rank_], s));
+      LLMI_HIP(hipStreamSynchronize(s));  // (as fused_point: every push done before any gather is enqueued)
       g.barrier();
-      for (int q = 0; q < size_; q++)
-        if (q != rank_) LLMI_HIP(hipStreamWaitEvent(s, g.ready[q], 0));
       mb_->run_chunk(buf, bytes, c, PX_GATHER, s, sk, pitch, slice);
-      g.barrier();  // nobody records its next push event before every peer has waited on this one
     }
   }
 

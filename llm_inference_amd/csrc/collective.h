@@ -25,6 +25,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <string>
+
 #include <condition_variable>
 #include <cstddef>
 #include <memory>
@@ -66,6 +68,7 @@ class Collective {
   // the exchange failed on the device since the last call (a bounded wait timed out, or a received slice
   // failed its checksum); 0 = no.  The ranks' exchange counts may then differ: the session stops.
   virtual int failed() { return 0; }
+  virtual std::string fail_detail() const { return std::string(); }  // after failed(): what the wait last saw
   // push exchange between processes: this rank's mailbox handle, then every rank's (rank order)
   virtual void peer_handle(void* out) const;
   virtual void peer_connect(const void* handles);
@@ -93,6 +96,9 @@ struct PushArgs {
   int skip;                   // fused exchanges since the previous standalone one: tag = epoch + 1 + skip
 };
 void launch_push_exchange(const PushArgs& a, hipStream_t s);
+// every XCD's L2 written back (a system-scope release on each), on the null stream, synchronised: run before a
+// new mailbox is zeroed, so no dirty line that an earlier owner of its memory left in an L2 lands on it later
+void l2_writeback_all();
 constexpr int PEER_HANDLE_BYTES = 64;
 
 // unique id for a new RCCL communicator (rank 0 makes it, the caller

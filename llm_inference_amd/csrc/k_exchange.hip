@@ -115,6 +115,12 @@ __global__ __launch_bounds__(PX_T) void push_exchange_kernel(PushArgs a) {
         if (all || late) break;
         if (wall_clock64() - t0 > a.timeout) {
           late = true;
+          for (int k = PX_B - 1; k >= 0; k--)
+            if (!ok[k]) {
+              __hip_atomic_store(a.err + 1, (int)((uint32_t)(g[k] >> 32) - tag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              __hip_atomic_store(a.err + 2, ik[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              __hip_atomic_store(a.err + 3, (int)tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
           __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
         }
@@ -137,7 +143,13 @@ __global__ __launch_bounds__(PX_T) void push_exchange_kernel(PushArgs a) {
       uint64_t g = px_load(cs);
       while ((uint32_t)(g >> 32) != tag && !late) {
         if (wall_clock64() - t0 > a.timeout) {
-          late = true;
+          late = true;  // (diagnostics: word -1 - peer = that peer's checksum granule)
+          __hip_atomic_store(a.err + 1, (int)((uint32_t)(g >> 32) - tag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(a.err + 2, -1 - t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(a.err + 3, (int)tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(a.err + 4, (int)(uint32_t)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(a.err + 5, (int)(half * 100000 + blockIdx.x * 1000 + gridDim.x), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
         }
@@ -163,6 +175,19 @@ __global__ __launch_bounds__(PX_T) void push_exchange_kernel(PushArgs a) {
 }
 
 }  // namespace
+
+namespace {
+__global__ void l2_writeback_kernel() {  // work-group b runs on XCD b % 8: 64 of them cover every XCD
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+}  // namespace
+
+void l2_writeback_all() {
+  hipLaunchKernelGGL(l2_writeback_kernel, dim3(64), dim3(64), 0, nullptr);
+  LLMI_HIP(hipGetLastError());
+  LLMI_HIP(hipDeviceSynchronize());
+}
 
 void launch_push_exchange(const PushArgs& a, hipStream_t s) {
   if (a.G < 1 || a.G > PX_MAX_RANKS || a.rank < 0 || a.rank >= a.G || a.words < 0 || a.words > a.cap ||

@@ -28,7 +28,8 @@ constexpr int PX_MAX_RANKS = 16;
 struct PxLink {
   uint2* mail[PX_MAX_RANKS];  // every rank's mailbox [2][G][slot_w] granules, as mapped in this process
   const unsigned* ctl;        // the rank's exchange count (constant during a step)
-  int* err;                   // 1: a wait timed out
+  int* err;                   // 3: a fused wait timed out; err[1..3]: that word's tag - the expected one, its
+                              // number in the whole vector, the expected tag
   uint64_t timeout;           // bound of every wait, ticks of the 100 MHz wall clock
   uint32_t slot_w;            // granules per sender slot
   int rank, G;
@@ -64,7 +65,14 @@ __device__ __forceinline__ void px_read_words(const PxLink& l, uint32_t tag, int
     if (ok) break;
     if (n == 0) t0 = wall_clock64();
     else if (wall_clock64() - t0 > l.timeout) {
-      __hip_atomic_store(l.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      int bad = 0;
+#pragma unroll
+      for (int i = N - 1; i >= 0; i--)
+        if ((uint32_t)(x[i] >> 32) != tag) bad = i;
+      __hip_atomic_store(l.err + 1, (int)((uint32_t)(x[bad] >> 32) - tag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(l.err + 2, W + bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(l.err + 3, (int)tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(l.err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       break;
     }
     __builtin_amdgcn_s_sleep(1);

@@ -527,6 +527,10 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
   LLMI_HIP(hipSetDevice(opts.device));
   LLMI_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   try {
+    // write back every XCD's L2 before this session's memory gets its contents: a line that memory's previous
+    // owner (a destroyed session or mailbox) left dirty in one XCD's L2 must not land on it later (the mailbox
+    // case was measured, collective.cpp Mailbox)
+    l2_writeback_all();
     if (tp_) {
       coll_ = tp_solo         ? make_null(tp_rank_, tp_size_)
               : opts.tp_group ? make_local(reinterpret_cast<LocalGroup*>(opts.tp_group), tp_rank_, tp_size_)
@@ -1973,7 +1977,7 @@ void Session::check_device_error() {
     throw status_error(LLMI_E_HIP, e == 2 ? "tensor-parallel push exchange: a received slice failed its checksum "
                                             "(device results invalid)"
                                           : "tensor-parallel push exchange: a peer's slice did not arrive within "
-                                            "LLMI_PX_TIMEOUT_MS (device results invalid)");
+                                            "LLMI_PX_TIMEOUT_MS (device results invalid)" + coll_->fail_detail());
   }
   if (blk_trace_) {  // development: append the last traced launch (work-group x 8 clocks) to LLMI_BLOCK_TRACE_OUT
     std::vector<unsigned long long> h(4096 * 8);
