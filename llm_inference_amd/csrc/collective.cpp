@@ -74,9 +74,7 @@ class Mailbox {
     // zeroing; scripts/dev/tp_repeat4.py)
     l2_writeback_all();
     LLMI_HIP(hipMemset(mine_, 0, bytes));  // tag 0: nothing published (tags are >= 1)
-    // the exchange count uncached too: every work-group reads it (px_link_tag, the exchange kernels' tag), and a
-    // cached line could outlive this allocation's reuse of an earlier group's memory
-    LLMI_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&ctl_), 8 * sizeof(unsigned), hipDeviceMallocUncached));
+    LLMI_HIP(hipMalloc(&ctl_, 8 * sizeof(unsigned)));
     LLMI_HIP(hipMemset(ctl_, 0, 8 * sizeof(unsigned)));
     LLMI_HIP(hipDeviceSynchronize());
     peers_.assign(G, nullptr);
