@@ -178,7 +178,7 @@ __global__ __launch_bounds__(PX_T) void push_exchange_kernel(PushArgs a) {
 
 namespace {
 __global__ void l2_writeback_kernel() {  // work-group b runs on XCD b % 8: 64 of them cover every XCD
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "");  // write back, then invalidate: no stale clean line either
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 }  // namespace

@@ -634,6 +634,7 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
 Session::~Session() { release(); }
 
 void Session::release() {
+  if (stream_) (void)hipStreamSynchronize(stream_);  // nothing of this session in flight while its memory is freed
   if (graph_exec_) (void)hipGraphExecDestroy(graph_exec_);
   if (graph_) (void)hipGraphDestroy(graph_);
   graph_exec_ = nullptr;
