@@ -69,12 +69,12 @@ class Mailbox {
     if (rank < 0 || rank >= G) throw std::runtime_error("push exchange: rank out of range");
     const size_t bytes = (size_t)2 * G * kSlot * sizeof(uint2);
     LLMI_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&mine_), bytes, hipDeviceMallocUncached));
-    // (the one-GPU 4-rank test: about one run in 15 timed out on a peer's checksum granule holding the same
-    // foreign granule every time -- a dirty L2 line of this memory's earlier owner, written back after the
-    // zeroing; scripts/dev/tp_repeat4.py)
+    // (the one-GPU 4-rank repeat: about one run in 15 timed out on a peer's checksum granule holding the same
+    // foreign granule every time, a line of this memory's earlier owner; with the L2 written back first and the
+    // host-side exchange points: 0 in 800 runs, scripts/dev/tp_repeat4.py)
     l2_writeback_all();
     LLMI_HIP(hipMemset(mine_, 0, bytes));  // tag 0: nothing published (tags are >= 1)
-    LLMI_HIP(hipMalloc(&ctl_, 8 * sizeof(unsigned)));
+    LLMI_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&ctl_), 8 * sizeof(unsigned), hipDeviceMallocUncached));
     LLMI_HIP(hipMemset(ctl_, 0, 8 * sizeof(unsigned)));
     LLMI_HIP(hipDeviceSynchronize());
     peers_.assign(G, nullptr);
@@ -285,9 +285,8 @@ class LocalCollective : public Collective {
   }
   // every rank's producing launch has completed before any rank's consumer is enqueued (the ranks' streams share
   // the process's hardware queues: a consumer spinning ahead of a peer's producer could block it).  Host-side:
-  // each rank drains its own stream, then the host barrier -- no cross-stream event waits (with the ranks'
-  // streams folded onto shared hardware queues those let a wait and a peer's launches interleave; the one-GPU
-  // 4-rank test timed out about once in 25 runs with them, scripts/dev/tp_repeat4.py)
+  // each rank drains its own stream, then the host barrier (with cross-stream event waits instead, the one-GPU
+  // 4-rank repeat, scripts/dev/tp_repeat4.py, timed out about once in 15 runs)
   void fused_point(hipStream_t s) override {
     LLMI_HIP(hipStreamSynchronize(s));
     g_->barrier();
@@ -367,6 +366,7 @@ LocalGroup::LocalGroup(int n_)
   static std::atomic<uint64_t> groups{0};
   std::random_device rd;
   seed = seed_from(((uint64_t)rd() << 32) ^ rd() ^ (++groups * 0x9E3779B97F4A7C15ull));
+  if (const char* e = getenv("LLMI_PX_SEED")) seed = (uint32_t)strtoul(e, nullptr, 10);  // development: a fixed first tag
 }
 
 LocalGroup::~LocalGroup() = default;

@@ -96,9 +96,8 @@ struct PushArgs {
   int skip;                   // fused exchanges since the previous standalone one: tag = epoch + 1 + skip
 };
 void launch_push_exchange(const PushArgs& a, hipStream_t s);
-// every XCD's L2 written back and invalidated (a system-scope acquire-release on each), on the null stream,
-// synchronised: run before a new mailbox is zeroed or a session loads, so no line that an earlier owner of the
-// memory left in an L2 (dirty: written back later over the new contents; clean: read instead of them) survives
+// every XCD's L2 written back (a system-scope release on each), on the null stream, synchronised: run before a
+// new mailbox is zeroed, so no line an earlier owner of its memory left dirty in an L2 lands on it later
 void l2_writeback_all();
 constexpr int PEER_HANDLE_BYTES = 64;
 

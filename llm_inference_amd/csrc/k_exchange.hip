@@ -178,7 +178,9 @@ __global__ __launch_bounds__(PX_T) void push_exchange_kernel(PushArgs a) {
 
 namespace {
 __global__ void l2_writeback_kernel() {  // work-group b runs on XCD b % 8: 64 of them cover every XCD
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "");  // write back, then invalidate: no stale clean line either
+  // write back only: an invalidate here would also drop lines other sessions' kernels, running now, just wrote
+  // (measured: the acquire-release form broke the one-GPU group tests)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 }  // namespace

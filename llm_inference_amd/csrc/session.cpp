@@ -527,10 +527,6 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
   LLMI_HIP(hipSetDevice(opts.device));
   LLMI_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   try {
-    // write back every XCD's L2 before this session's memory gets its contents: a line that memory's previous
-    // owner (a destroyed session or mailbox) left dirty in one XCD's L2 must not land on it later (the mailbox
-    // case was measured, collective.cpp Mailbox)
-    l2_writeback_all();
     if (tp_) {
       coll_ = tp_solo         ? make_null(tp_rank_, tp_size_)
               : opts.tp_group ? make_local(reinterpret_cast<LocalGroup*>(opts.tp_group), tp_rank_, tp_size_)
@@ -634,7 +630,6 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
 Session::~Session() { release(); }
 
 void Session::release() {
-  if (stream_) (void)hipStreamSynchronize(stream_);  // nothing of this session in flight while its memory is freed
   if (graph_exec_) (void)hipGraphExecDestroy(graph_exec_);
   if (graph_) (void)hipGraphDestroy(graph_);
   graph_exec_ = nullptr;
