@@ -59,7 +59,8 @@ void launch_attention(const AttnArgs& a, bool exact, hipStream_t s, const QKVArg
 // wqkv_b: the second qkv weight of a q|k Q4_K + v Q6_K layer (kq layout), or null
 bool attn_block_supported(const DevWeight& wqkv, const DevWeight* wqkv_b, const DevWeight& wo, int head_dim,
                           int n_head, int n_head_kv, int qrole);
-void launch_attn_block(const DevWeight& wqkv, const DevWeight* wqkv_b, LayerGemv qg, int qrole, const DevWeight& wo,
+// returns the o projection's work-group count (the producers of its fused exchange)
+int launch_attn_block(const DevWeight& wqkv, const DevWeight* wqkv_b, LayerGemv qg, int qrole, const DevWeight& wo,
                        LayerGemv og,
                        const AttnArgs& aa, const QKVArgs& qa, BlockSync bs, hipStream_t s);
 void launch_bump_epoch(unsigned* epoch, hipStream_t s);

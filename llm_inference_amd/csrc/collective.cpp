@@ -7,6 +7,7 @@
 #include <atomic>
 #include <chrono>
 #include <random>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <stdexcept>
@@ -63,20 +64,25 @@ uint64_t px_timeout_ticks() {  // LLMI_PX_TIMEOUT_MS (default 10 s): the bound o
 class Mailbox {
  public:
   static constexpr int kCap = 1 << 18;  // words per rank slot (1 MB of payload): every decode exchange in one
-  static constexpr size_t kSlot = (size_t)kCap + PX_MAX_WG;
-  Mailbox(int rank, int G) : rank_(rank), G_(G), timeout_(px_timeout_ticks()) {
+  static constexpr size_t kSlot = (size_t)kCap + PX_MAX_CS;  // words, then checksum granules (px.h)
+  // zeroed on the owning session's stream and complete on return (a null-stream hipMemset is not ordered with the
+  // session's non-blocking stream)
+  Mailbox(int rank, int G, hipStream_t s) : rank_(rank), G_(G), timeout_(px_timeout_ticks()), s_(s) {
     if (G < 1 || G > PX_MAX_RANKS) throw std::runtime_error("push exchange: 1-16 ranks");
     if (rank < 0 || rank >= G) throw std::runtime_error("push exchange: rank out of range");
     const size_t bytes = (size_t)2 * G * kSlot * sizeof(uint2);
     LLMI_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&mine_), bytes, hipDeviceMallocUncached));
-    // (the one-GPU 4-rank repeat: about one run in 15 timed out on a peer's checksum granule holding the same
-    // foreign granule every time, a line of this memory's earlier owner; with the L2 written back first and the
-    // host-side exchange points: 0 in 800 runs, scripts/dev/tp_repeat4.py)
-    l2_writeback_all();
-    LLMI_HIP(hipMemset(mine_, 0, bytes));  // tag 0: nothing published (tags are >= 1)
     LLMI_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&ctl_), 8 * sizeof(unsigned), hipDeviceMallocUncached));
-    LLMI_HIP(hipMemset(ctl_, 0, 8 * sizeof(unsigned)));
-    LLMI_HIP(hipDeviceSynchronize());
+    if (getenv("LLMI_DEV_OLD_INIT")) {  // round-5 A/B only: the round-4 null-stream form
+      l2_writeback_all();
+      LLMI_HIP(hipMemset(mine_, 0, bytes));
+      LLMI_HIP(hipMemset(ctl_, 0, 8 * sizeof(unsigned)));
+      LLMI_HIP(hipDeviceSynchronize());
+    } else {
+      LLMI_HIP(hipMemsetAsync(mine_, 0, bytes, s_));  // tag 0: nothing published (tags are >= 1)
+      LLMI_HIP(hipMemsetAsync(ctl_, 0, 8 * sizeof(unsigned), s_));
+      LLMI_HIP(hipStreamSynchronize(s_));
+    }
     peers_.assign(G, nullptr);
     peers_[rank] = mine_;
   }
@@ -89,7 +95,8 @@ class Mailbox {
   // the group's first tag (before the first exchange: the counter is then at seed - 1)
   void seed(uint32_t first_tag) {
     const unsigned c = first_tag - 1u;
-    LLMI_HIP(hipMemcpy(ctl_, &c, sizeof(c), hipMemcpyHostToDevice));
+    LLMI_HIP(hipMemcpyAsync(ctl_, &c, sizeof(c), hipMemcpyHostToDevice, s_));
+    LLMI_HIP(hipStreamSynchronize(s_));
     seeded_ = true;
   }
   uint2* mine() const { return mine_; }
@@ -141,6 +148,7 @@ class Mailbox {
     l.err = reinterpret_cast<int*>(ctl_ + 2);
     l.timeout = timeout_;
     l.slot_w = (uint32_t)kSlot;
+    l.cs0 = (uint32_t)kCap;
     l.rank = rank_;
     l.G = G_;
   }
@@ -174,11 +182,15 @@ class Mailbox {
   }
   int failed() {  // reads and clears the device flag (callers have synchronised the stream)
     int e[6] = {0, 0, 0, 0, 0, 0};
-    LLMI_HIP(hipMemcpy(e, ctl_ + 2, sizeof(e), hipMemcpyDeviceToHost));
+    LLMI_HIP(hipMemcpyAsync(e, ctl_ + 2, sizeof(e), hipMemcpyDeviceToHost, s_));
+    LLMI_HIP(hipStreamSynchronize(s_));
     if (e[0]) {
-      LLMI_HIP(hipMemset(ctl_ + 2, 0, sizeof(e)));
+      LLMI_HIP(hipMemsetAsync(ctl_ + 2, 0, sizeof(e), s_));
+      LLMI_HIP(hipStreamSynchronize(s_));
       // a timed-out wait: the word it last saw (its tag relative to the expected one), kind and place
-      detail_ = e[0] == 2 ? "" : std::string(e[0] == 3 ? " [fused" : " [standalone") + " exchange, tag " +
+      detail_ = e[0] == 2 ? " [checksum mismatch, tag " + std::to_string((unsigned)e[3]) + ": read " +
+                                std::to_string((unsigned)e[4]) + ", pushed " + std::to_string((unsigned)e[5]) + "]"
+                          : std::string(e[0] == 3 ? " [fused" : " [standalone") + " exchange, tag " +
                                      std::to_string((unsigned)e[3]) + ", word " + std::to_string(e[2]) +
                                      " held tag " + (e[1] >= 0 ? "+" : "") + std::to_string(e[1]) + " word " +
                                      std::to_string((unsigned)e[4]) + " at " + std::to_string(e[5]) + "]";
@@ -186,10 +198,25 @@ class Mailbox {
     return e[0];
   }
   const std::string& detail() const { return detail_; }
+  // test hook (LLMI_PX_TEST_CORRUPT): in this rank's mailbox, word 0 of sender q's slot in the half holding the newer
+  // exchange gets its low bit flipped, its tag kept (the consumer accepts it; the checksum must not)
+  void corrupt_newest(int q) {
+    uint64_t g[2];
+    for (int h = 0; h < 2; h++)
+      LLMI_HIP(hipMemcpyAsync(&g[h], mine_ + ((size_t)h * G_ + q) * kSlot, 8, hipMemcpyDeviceToHost, s_));
+    LLMI_HIP(hipStreamSynchronize(s_));
+    const int h = (uint32_t)(g[1] >> 32) > (uint32_t)(g[0] >> 32) ? 1 : 0;
+    const uint64_t bad = g[h] ^ 1ull;
+    fprintf(stderr, "[px test] rank %d: sender %d word 0, half 0 {tag %u, %08x}, half 1 {tag %u, %08x}: half %d altered\n",
+            rank_, q, (unsigned)(g[0] >> 32), (unsigned)g[0], (unsigned)(g[1] >> 32), (unsigned)g[1], h);
+    LLMI_HIP(hipMemcpyAsync(mine_ + ((size_t)h * G_ + q) * kSlot, &bad, 8, hipMemcpyHostToDevice, s_));
+    LLMI_HIP(hipStreamSynchronize(s_));
+  }
 
  private:
   int rank_, G_;
   uint64_t timeout_;
+  hipStream_t s_;  // the owning session's stream
   bool seeded_ = false;
   uint2* mine_ = nullptr;
   unsigned* ctl_ = nullptr;  // [0] exchange count, [1] ticket, [2] error flag, [3..5] its diagnostics
@@ -201,7 +228,7 @@ class Mailbox {
 // one process per GPU, the push exchange through IPC-mapped mailboxes
 class PeerCollective : public Collective {
  public:
-  PeerCollective(int rank, int size) : Collective(rank, size), mb_(rank, size) {}
+  PeerCollective(int rank, int size, hipStream_t s) : Collective(rank, size), mb_(rank, size, s) {}
   bool graph_safe() const override { return true; }
   int kind() const override { return EX_PUSH; }
   void all_gather(void* buf, size_t bytes, hipStream_t s, int skip) override {
@@ -245,19 +272,22 @@ class RcclCollective : public Collective {
 
 class LocalCollective : public Collective {
  public:
-  LocalCollective(LocalGroup* g, int rank) : Collective(rank, g->n), g_(g) {
+  LocalCollective(LocalGroup* g, int rank, hipStream_t s) : Collective(rank, g->n), g_(g) {
     const char* ex = getenv("LLMI_TP_EXCHANGE");
     push_ = !(ex && std::string(ex) == "copy");
     {
       std::lock_guard<std::mutex> lk(g->mu);
-      if (rank < 0 || rank >= g->n || g->joined[rank]) throw std::runtime_error("local group: bad or duplicate rank");
+      if (rank < 0 || rank >= g->n || g->joined[rank])
+        throw std::runtime_error("local group: bad rank, or the rank already joined this group (re-create the group)");
     }
     if (push_) {
-      mb_.reset(new Mailbox(rank, g->n));
+      mb_.reset(new Mailbox(rank, g->n, s));
       mb_->seed(g->seed);
     }
     if (const char* d = getenv("LLMI_PX_TEST_DROP"))  // test hook: this rank skips its first push
       drop_ = atoi(d) == rank;
+    if (const char* d = getenv("LLMI_PX_TEST_CORRUPT"))  // test hook: one received word altered, its tag kept
+      corrupt_ = atoi(d) == rank;
     std::lock_guard<std::mutex> lk(g->mu);
     if (g->joined[rank]) throw std::runtime_error("local group: bad or duplicate rank");
     g->joined[rank] = true;
@@ -267,7 +297,8 @@ class LocalCollective : public Collective {
   }
   ~LocalCollective() override {
     std::lock_guard<std::mutex> lk(g_->mu);
-    g_->joined[rank_] = false;
+    // joined[rank] stays set: a group's ranks join once (a rejoining rank's new mailbox would restart the group's
+    // tags at its seed, so its tags would repeat within the group's lifetime: ADVICE r4)
     g_->mail[rank_] = nullptr;
     (void)hipEventDestroy(g_->ready[rank_]);
     (void)hipEventDestroy(g_->done[rank_]);
@@ -290,6 +321,10 @@ class LocalCollective : public Collective {
   void fused_point(hipStream_t s) override {
     LLMI_HIP(hipStreamSynchronize(s));
     g_->barrier();
+    if (corrupt_) {  // (test hook) the newest granule of the next peer's word 0: its word flipped, its tag kept
+      corrupt_ = false;
+      mb_->corrupt_newest((rank_ + 1) % size_);
+    }
   }
   bool all_gather_cols(void* buf, size_t pitch, size_t slice, int rows, hipStream_t s, int skip) override {
     if (!push_) return false;
@@ -340,7 +375,7 @@ class LocalCollective : public Collective {
   }
 
   LocalGroup* g_;
-  bool push_ = true, drop_ = false;
+  bool push_ = true, drop_ = false, corrupt_ = false;
   std::unique_ptr<Mailbox> mb_;
 };
 
@@ -366,7 +401,11 @@ LocalGroup::LocalGroup(int n_)
   static std::atomic<uint64_t> groups{0};
   std::random_device rd;
   seed = seed_from(((uint64_t)rd() << 32) ^ rd() ^ (++groups * 0x9E3779B97F4A7C15ull));
-  if (const char* e = getenv("LLMI_PX_SEED")) seed = (uint32_t)strtoul(e, nullptr, 10);  // development: a fixed first tag
+  if (const char* e = getenv("LLMI_PX_SEED")) {  // development: a fixed first tag, in [1, 2^31) (tag 0 = unwritten)
+    const unsigned long v = strtoul(e, nullptr, 10);
+    if (v < 1 || v >= (1ul << 31)) throw std::runtime_error("LLMI_PX_SEED must lie in [1, 2^31)");
+    seed = (uint32_t)v;
+  }
 }
 
 LocalGroup::~LocalGroup() = default;
@@ -380,7 +419,8 @@ void LocalGroup::barrier() {
     cv.notify_all();
     return;
   }
-  if (!cv.wait_for(lk, std::chrono::seconds(120), [&] { return gen != my; }))
+  static const int secs = getenv("LLMI_TP_BARRIER_S") ? std::max(1, atoi(getenv("LLMI_TP_BARRIER_S"))) : 120;
+  if (!cv.wait_for(lk, std::chrono::seconds(secs), [&] { return gen != my; }))
     throw std::runtime_error("local group: barrier timeout (a rank stopped)");
 }
 
@@ -388,13 +428,13 @@ std::unique_ptr<Collective> make_rccl(int rank, int size, const void* id128) {
   return std::unique_ptr<Collective>(new RcclCollective(rank, size, id128));
 }
 
-std::unique_ptr<Collective> make_local(LocalGroup* g, int rank, int size) {
+std::unique_ptr<Collective> make_local(LocalGroup* g, int rank, int size, hipStream_t s) {
   if (!g || size != g->n) throw std::runtime_error("local group: tp_size differs from the group's size");
-  return std::unique_ptr<Collective>(new LocalCollective(g, rank));
+  return std::unique_ptr<Collective>(new LocalCollective(g, rank, s));
 }
 
-std::unique_ptr<Collective> make_peer(int rank, int size) {
-  return std::unique_ptr<Collective>(new PeerCollective(rank, size));
+std::unique_ptr<Collective> make_peer(int rank, int size, hipStream_t s) {
+  return std::unique_ptr<Collective>(new PeerCollective(rank, size, s));
 }
 
 }  // namespace llmi

@@ -1038,8 +1038,8 @@ bool attn_block_supported(const DevWeight& wqkv, const DevWeight* wqkv_b, const 
          wo.cols == n_head * head_dim;
 }
 
-void launch_attn_block(const DevWeight& wqkv, const DevWeight* wqkv_b, LayerGemv qg, int qrole, const DevWeight& wo,
-                       LayerGemv og, const AttnArgs& aa, const QKVArgs& qa, BlockSync bs, hipStream_t s) {
+int launch_attn_block(const DevWeight& wqkv, const DevWeight* wqkv_b, LayerGemv qg, int qrole, const DevWeight& wo,
+                      LayerGemv og, const AttnArgs& aa, const QKVArgs& qa, BlockSync bs, hipStream_t s) {
   if (!attn_block_supported(wqkv, wqkv_b, wo, aa.head_dim, aa.n_head, aa.n_head_kv, qrole))
     throw std::runtime_error("attention block: unsupported shapes");
   const int g = aa.n_head / aa.n_head_kv, hd = aa.head_dim;
@@ -1074,8 +1074,11 @@ void launch_attn_block(const DevWeight& wqkv, const DevWeight* wqkv_b, LayerGemv
   const int nqa = wqkv_b ? wqkv.rows / (4 * c.QR) : bg.nq;
   AttnArgs av = aa;  // virtual kv heads: the attention role's head count
   av.n_head_kv *= c.kvd;
+  if (og.px && og.px_out >= 0 && bg.no > PX_MAX_CS) throw std::runtime_error("attention block: more fused-exchange producers than checksum slots");
+  if (qg.px && qg.px_in >= 0 && (qg.px_in_nwg <= 0 || qg.px_in_nwg > PX_MAX_CS)) throw std::runtime_error("attention block: fused exchange read without its producer count");
   c.fn(dim3(bg.nq + bg.na + bg.no), bg.lds, qg, og, av, qa, bs, bg.nq, qgb, nqa, s);
   LLMI_HIP(hipGetLastError());
+  return bg.no;
 }
 
 }  // namespace llmi

@@ -58,7 +58,7 @@ __global__ __launch_bounds__(PX_T) void push_exchange_kernel(PushArgs a) {
   __syncthreads();
   const uint32_t tag = s_tag;
   const size_t half = tag & 1u;
-  const size_t slot_w = (size_t)a.cap + PX_MAX_WG;  // granules per sender slot: words, then checksums
+  const size_t slot_w = (size_t)a.cap + PX_MAX_CS;  // granules per sender slot: words, then checksums
   const int per = (a.words + gridDim.x - 1) / gridDim.x;
   const int w0 = blockIdx.x * per, n = max(0, min(a.words, w0 + per) - w0);
   auto word = [&](int q, int i) -> uint32_t* {  // word i of this exchange in rank q's part of the buffer

@@ -257,7 +257,7 @@ int layer_gemv_gelu_group(int cols, uint32_t type) {
   return c ? c->R * (c->rw ? c->rw : c->NW) / 2 : 0;
 }
 
-void launch_layer_gemv(const DevWeight& w, LayerGemv a, int role, hipStream_t s) {
+int launch_layer_gemv(const DevWeight& w, LayerGemv a, int role, hipStream_t s) {
   if (!layer_gemv_supported(w, role)) throw std::runtime_error("layer gemv: unsupported weight");
   const bool pro = role == LAYER_PRO || role == LAYER_GELU;
   if (pro && (!a.y || !a.resid_in || !a.resid_out || !a.w_next || a.resid_in == a.resid_out))
@@ -291,8 +291,12 @@ void launch_layer_gemv(const DevWeight& w, LayerGemv a, int role, hipStream_t s)
   // x blocks + pad slot of the x copy (+ the f32 x staging of the prologue)
   const size_t lds = (size_t)nb * sizeof(XBlock) + 16 + (pro ? (size_t)w.cols * 4 : 0);
   const int rows_per_wg = (c.rw ? c.rw : c.NW) * c.R;
-  c.fn(dim3((w.rows + rows_per_wg - 1) / rows_per_wg), lds, a, s);
+  const int nwg = (w.rows + rows_per_wg - 1) / rows_per_wg;
+  if (a.px && a.px_out >= 0 && nwg > PX_MAX_CS) throw std::runtime_error("layer gemv: more fused-exchange producers than checksum slots");
+  if (a.px && a.px_in >= 0 && (a.px_in_nwg <= 0 || a.px_in_nwg > PX_MAX_CS)) throw std::runtime_error("layer gemv: fused exchange read without its producer count");
+  c.fn(dim3(nwg), lds, a, s);
   LLMI_HIP(hipGetLastError());
+  return nwg;
 }
 
 // q|k (Q4_K) and v (Q6_K) rows of one q|k|v projection in one launch: the

@@ -275,10 +275,11 @@ __device__ unsigned long long* g_layer_trace = nullptr;
 // launch reads blocks (PLAIN) instead of quantizing the whole hid in every work-group (QUANT)
 // fused exchange (a.px_out): the hq block's 12 words (8 of quants, d, nsum8, two zero pads) or the hid values
 // are pushed to every rank's mailbox as well
+// (returns this thread's checksum terms of the pushed words, px.h)
 template <int H>
-__device__ __forceinline__ void gelu_out(const LayerGemv& a, int bid, const float* s_rows, int t, bool fout,
-                                         uint32_t tout) {
-  if (t >= H) return;
+__device__ __forceinline__ uint32_t gelu_out(const LayerGemv& a, int bid, const float* s_rows, int t, bool fout,
+                                             uint32_t tout) {
+  if (t >= H) return 0u;
   const float g = gelu_mul1(s_rows[t], s_rows[H + t]);
   a.hid[bid * H + t] = g;
   if constexpr (H == 32) {
@@ -294,14 +295,20 @@ __device__ __forceinline__ void gelu_out(const LayerGemv& a, int bid, const floa
         uint32_t w = 0;
 #pragma unroll
         for (int k = 0; k < 4; k++) w |= (uint32_t)(__shfl(b.q, 4 * j + k) & 0xFF) << (8 * k);
-        if (t < 12)
-          px_push_word(*a.px, tout, bid * 12 + t,
-                       t < 8 ? w : t == 8 ? __float_as_uint(b.d) : t == 9 ? (uint32_t)b.nsum8 : 0u);
+        if (t < 12) {
+          const uint32_t v = t < 8 ? w : t == 8 ? __float_as_uint(b.d) : t == 9 ? (uint32_t)b.nsum8 : 0u;
+          px_push_word(*a.px, tout, bid * 12 + t, v);
+          return px_term(v, a.px->rank, bid * 12 + t);
+        }
       }
-      return;
+      return 0u;
     }
   }
-  if (fout) px_push_word(*a.px, tout, bid * H + t, __float_as_uint(g));
+  if (fout) {
+    px_push_word(*a.px, tout, bid * H + t, __float_as_uint(g));
+    return px_term(__float_as_uint(g), a.px->rank, bid * H + t);
+  }
+  return 0u;
 }
 
 enum { SYNC_SIG = 1, SYNC_WAIT = 2 };
@@ -355,6 +362,7 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
   static_assert(PE == 0 || (RB && !MULTI && !EARLY && PE < P), "PE: single-chunk row-bound late roles");
   static_assert(!W8 || (RB && R <= 16), "W8: row-bound lanes");
   static_assert(WT == 0 || (RB && R <= 8 && !MULTI && !HELP && !W8), "kq: single-chunk row-bound lanes");
+  static_assert(!(PXF && HELP), "fused exchange: not in the helper roles (their LDS words are ordered differently)");
   LAYER_MARK(0);
   BLK_MARK(bs, 0);
   constexpr int EPT = E, X_LD = E;
@@ -375,6 +383,18 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
   const bool fin = PXF && a.px_in >= 0, fout = PXF && a.px_out >= 0;
   const uint32_t tin = fin ? px_link_tag(*a.px, a.px_in) : 0u;
   const uint32_t tout = fout ? px_link_tag(*a.px, a.px_out) : 0u;
+  // checksum terms (px.h): of the words this thread pushed / read; the LDS words of their work-group sums
+  uint32_t pxs = 0u, pxc = 0u;
+  __shared__ uint32_t s_pxs[PXF ? 3 : 1];
+  if (PXF && t < 3) s_pxs[t] = 0u;  // (ordered before their use by the barrier after the prologue)
+  // the checksum granule of the pushed words, and (the first PX_CHECK_WG work-groups) the check of the words read:
+  // every thread of the work-group, at each exit
+  auto px_finish = [&]() {
+    if constexpr (PXF) {
+      if (fout) px_push_checksum(*a.px, tout, bid, pxs, &s_pxs[0]);
+      if (fin && bid < PX_CHECK_WG) px_verify(*a.px, tin, a.px_in_nwg, pxc, &s_pxs[1]);
+    }
+  };
   // SIG: rows are published write-through; the work-group's rows lie in one
   // kv head's group (host-checked: rows per work-group divide head_dim)
   auto put_out = [&](float* p, float v) {
@@ -382,7 +402,10 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
       st_granule(bs.g_qkv + (p - a.out), __float_as_uint(v), btag);
     } else {
       *p = v;
-      if (fout) px_push_word(*a.px, tout, (int)(p - a.out), __float_as_uint(v));
+      if (fout) {
+        px_push_word(*a.px, tout, (int)(p - a.out), __float_as_uint(v));
+        pxs += px_term(__float_as_uint(v), a.px->rank, (int)(p - a.out));
+      }
     }
   };
   // (RW0 == 0: the expressions of the all-waves launch exactly -- a select the compiler cannot fold away
@@ -616,7 +639,8 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
         const int b = t / 4 + k * QB;
 #pragma unroll
         for (int h = 0; h < 2; h++)
-          y4[k][h] = b < nb ? px_read_f4(*a.px, tin, a.px_in_ws, b * 32 + sub * 8 + 4 * h) : make_float4(0.f, 0.f, 0.f, 0.f);
+          y4[k][h] = b < nb ? px_read_f4(*a.px, tin, a.px_in_ws, b * 32 + sub * 8 + 4 * h, pxc, true)
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
       }
     }
     auto in_row = [&](int k) { return t / 4 + k * QB < nb; };
@@ -708,8 +732,9 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
 #pragma unroll
       for (int r = 0; r < E; r++) {
         const int i = min(t + r * T, 4 * nb - 1);
-        xr[r][0] = px_read_f4(*a.px, tin, a.px_in_ws, 8 * i);
-        xr[r][1] = px_read_f4(*a.px, tin, a.px_in_ws, 8 * i + 4);
+        const bool own = t + r * T < 4 * nb;  // (clamped duplicates are not counted)
+        xr[r][0] = px_read_f4(*a.px, tin, a.px_in_ws, 8 * i, pxc, own);
+        xr[r][1] = px_read_f4(*a.px, tin, a.px_in_ws, 8 * i + 4, pxc, own);
       }
     }
 #pragma unroll
@@ -747,7 +772,7 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
 #pragma unroll
       for (int k = 0; k < X_LD; k++) {
         uint32_t v[4];
-        px_read_words<4>(*a.px, tin, a.px_in_ws, 4 * min(t + k * T, n16 - 1), v);
+        px_read_words<4>(*a.px, tin, a.px_in_ws, 4 * min(t + k * T, n16 - 1), v, pxc, t + k * T < n16);
         xr[k] = make_uint4(v[0], v[1], v[2], v[3]);
       }
     } else {
@@ -807,7 +832,7 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
       }
       __syncthreads();
       constexpr int H = RW * R / 2;  // hidden units of this work-group
-      gelu_out<H>(a, bid, s_rows, t, fout, tout);
+      pxs += gelu_out<H>(a, bid, s_rows, t, fout, tout);
     } else if (!helper) {
       if constexpr (R <= 2) {
         if (lane == 0)
@@ -819,6 +844,7 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
     }
     BLK_MARK(bs, 3);
     LAYER_MARK(6);
+    px_finish();
     return;
   }
   float acc[R];
@@ -848,7 +874,7 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
     }
     __syncthreads();
     constexpr int H = RW * R / 2;  // hidden units of this work-group
-    gelu_out<H>(a, bid, s_rows, t, fout, tout);
+    pxs += gelu_out<H>(a, bid, s_rows, t, fout, tout);
   } else {
 #pragma unroll
     for (int k = 0; k < R; k++) {
@@ -857,6 +883,7 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
     }
   }
   LAYER_MARK(6);
+  px_finish();
 }
 
 

@@ -14,6 +14,13 @@
 // launch that reads exchange n pushes its words of n + 1 only after reading, and every word of n + 1 is read by
 // every consumer of n + 1 -- so a rank pushing n + 2 has consumed n + 1 from all its peers, each of which had
 // finished reading n.
+//
+// Self-check (round 5): every producing work-group also pushes ONE checksum granule -- the sum of
+// px_term(word, rank, index) over the words it pushed -- at granule cs0 + its index of the slot, and the first
+// PX_CHECK_WG work-groups of every consuming launch (at least one per XCD when work-groups are dealt round-robin)
+// sum the same terms over every word they read and compare with the sum of all producers' checksum granules
+// (px_in_nwg per rank): a stale, torn or foreign word sets *err = 2 (the session raises LLMI_E_HIP and refuses
+// further work) instead of reaching the logits.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -22,6 +29,8 @@
 namespace llmi {
 
 constexpr int PX_MAX_RANKS = 16;
+constexpr int PX_MAX_CS = 1024;  // checksum granules per sender slot: producing work-groups of one exchange
+constexpr int PX_CHECK_WG = 8;   // consuming work-groups per launch that verify the checksums
 
 // a rank's mailboxes as its launches see them (device-resident, one per session); an exchange is (k, ws): its
 // number within the step and its words per rank (word W of the whole vector is rank W / ws's word W % ws)
@@ -29,9 +38,11 @@ struct PxLink {
   uint2* mail[PX_MAX_RANKS];  // every rank's mailbox [2][G][slot_w] granules, as mapped in this process
   const unsigned* ctl;        // the rank's exchange count (constant during a step)
   int* err;                   // 3: a fused wait timed out; err[1..3]: that word's tag - the expected one, its
-                              // number in the whole vector, the expected tag
+                              // number in the whole vector (-1 - producer work-group: a checksum granule), the
+                              // expected tag; 2: a checksum mismatch (err[3]: the tag, err[4]/[5]: read/expected sum)
   uint64_t timeout;           // bound of every wait, ticks of the 100 MHz wall clock
   uint32_t slot_w;            // granules per sender slot
+  uint32_t cs0;               // first checksum granule of a slot (words [0, cs0), checksums [cs0, slot_w))
   int rank, G;
 };
 
@@ -48,10 +59,25 @@ __device__ __forceinline__ void px_push_word(const PxLink& l, uint32_t tag, int 
     __hip_atomic_store(reinterpret_cast<uint64_t*>(l.mail[q] + slot), g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// order-free checksum term of word w of rank q's slice (w < 2^24)
+__device__ __forceinline__ uint32_t px_term(uint32_t v, int q, int w) {
+  const uint32_t idx = (uint32_t)w | ((uint32_t)q << 24);
+  return (v ^ (idx * 0x9E3779B9u)) * 0x85EBCA6Bu + idx;
+}
+
+__device__ __forceinline__ void px_timeout(const PxLink& l, uint32_t seen, uint32_t tag, int where) {
+  __hip_atomic_store(l.err + 1, (int)(seen - tag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(l.err + 2, where, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(l.err + 3, (int)tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(l.err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // N (1 or 4) consecutive words W.. of the whole vector from this rank's mailbox (W % N == 0 and ws % N == 0, so
-// they lie in one sender's slot); bounded: on timeout *err = 1 and the words are garbage (the grid drains)
+// they lie in one sender's slot); bounded: on timeout *err = 3 and the words are garbage (the grid drains).  count:
+// add the words' checksum terms to cs (false for a clamped duplicate read)
 template <int N>
-__device__ __forceinline__ void px_read_words(const PxLink& l, uint32_t tag, int ws, int W, uint32_t (&v)[N]) {
+__device__ __forceinline__ void px_read_words(const PxLink& l, uint32_t tag, int ws, int W, uint32_t (&v)[N],
+                                              uint32_t& cs, bool count) {
   const int q = W / ws, w = W - q * ws;
   const uint64_t* g = reinterpret_cast<const uint64_t*>(l.mail[l.rank] + ((size_t)(tag & 1u) * l.G + q) * l.slot_w + w);
   uint64_t x[N];
@@ -69,10 +95,7 @@ __device__ __forceinline__ void px_read_words(const PxLink& l, uint32_t tag, int
 #pragma unroll
       for (int i = N - 1; i >= 0; i--)
         if ((uint32_t)(x[i] >> 32) != tag) bad = i;
-      __hip_atomic_store(l.err + 1, (int)((uint32_t)(x[bad] >> 32) - tag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(l.err + 2, W + bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(l.err + 3, (int)tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(l.err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      px_timeout(l, (uint32_t)(x[bad] >> 32), tag, W + bad);
       break;
     }
     __builtin_amdgcn_s_sleep(1);
@@ -81,12 +104,70 @@ __device__ __forceinline__ void px_read_words(const PxLink& l, uint32_t tag, int
       if ((uint32_t)(x[i] >> 32) != tag) x[i] = __hip_atomic_load(g + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 #pragma unroll
-  for (int i = 0; i < N; i++) v[i] = (uint32_t)x[i];
+  for (int i = 0; i < N; i++) {
+    v[i] = (uint32_t)x[i];
+    if (count) cs += px_term(v[i], q, w + i);
+  }
 }
 
-__device__ __forceinline__ float4 px_read_f4(const PxLink& l, uint32_t tag, int ws, int W) {
+__device__ __forceinline__ uint32_t px_wave_add(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// a work-group's sum of one value per thread (every thread of the work-group calls it; s: a zeroed LDS word whose
+// zeroing a barrier has ordered before this call)
+__device__ __forceinline__ uint32_t px_wg_add(uint32_t v, uint32_t* s) {
+  v = px_wave_add(v);
+  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(s, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __syncthreads();
+  return *s;
+}
+
+// producer: work-group bid's checksum granule (cs: this thread's terms) to every rank's mailbox
+__device__ __forceinline__ void px_push_checksum(const PxLink& l, uint32_t tag, int bid, uint32_t cs, uint32_t* s) {
+  const uint32_t tot = px_wg_add(cs, s);
+  if ((int)threadIdx.x < l.G) {
+    const size_t slot = ((size_t)(tag & 1u) * l.G + l.rank) * l.slot_w + l.cs0 + (size_t)bid;
+    __hip_atomic_store(reinterpret_cast<uint64_t*>(l.mail[threadIdx.x] + slot), ((uint64_t)tag << 32) | tot,
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// consumer: the terms of every word this work-group read (cs) against the nwg checksum granules of every rank
+// (s: two zeroed LDS words, as px_wg_add)
+__device__ __forceinline__ void px_verify(const PxLink& l, uint32_t tag, int nwg, uint32_t cs, uint32_t* s) {
+  const uint32_t got = px_wg_add(cs, s);
+  uint32_t want = 0;
+  const uint64_t t0 = wall_clock64();
+  for (int i = threadIdx.x; i < l.G * nwg; i += blockDim.x) {
+    const int q = i / nwg, b = i - q * nwg;
+    const uint64_t* g =
+        reinterpret_cast<const uint64_t*>(l.mail[l.rank] + ((size_t)(tag & 1u) * l.G + q) * l.slot_w + l.cs0 + b);
+    uint64_t x = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    while ((uint32_t)(x >> 32) != tag) {
+      if (wall_clock64() - t0 > l.timeout) {
+        px_timeout(l, (uint32_t)(x >> 32), tag, -1 - b);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      x = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    want += (uint32_t)x;
+  }
+  want = px_wg_add(want, s + 1);
+  if (threadIdx.x == 0 && want != got) {
+    __hip_atomic_store(l.err + 3, (int)tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(l.err + 4, (int)got, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(l.err + 5, (int)want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(l.err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+__device__ __forceinline__ float4 px_read_f4(const PxLink& l, uint32_t tag, int ws, int W, uint32_t& cs, bool count) {
   uint32_t v[4];
-  px_read_words<4>(l, tag, ws, W, v);
+  px_read_words<4>(l, tag, ws, W, v, cs, count);
   return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
 }
 #endif

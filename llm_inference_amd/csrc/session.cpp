@@ -71,7 +71,7 @@ float* Session::dev_f32_copy(const GGUFView& g, const GTensor* t, int n) {
   if (t->type != T_F32) throw status_error(LLMI_E_TYPE, "norm weight " + t->name + " is not F32");
   if ((int)t->shape[0] < n) throw status_error(LLMI_E_SIZE, "norm weight " + t->name + " too short");
   float* d = dalloc<float>(t->shape[0] + 256);  // + 1 KB: the layer engine copies norm vectors in whole 1-KB pieces
-  LLMI_HIP(hipMemcpy(d, g.tensor_data(*t), t->shape[0] * 4, hipMemcpyHostToDevice));
+  h2d(d, g.tensor_data(*t), t->shape[0] * 4);
   return d;
 }
 
@@ -193,7 +193,7 @@ void Session::upload(const GGUFView& g) {  // model.cpp:169-238 tensor map
   embd_raw_ = (const uint8_t*)embd_.qs;
   if (te->type == T_Q8_0) {  // the GEMV copy is repacked; keep GGUF rows for lookups
     uint8_t* raw = dalloc<uint8_t>(embd_.bytes);
-    LLMI_HIP(hipMemcpy(raw, g.tensor_data(*te), embd_.bytes, hipMemcpyHostToDevice));
+    h2d(raw, g.tensor_data(*te), embd_.bytes);
     embd_raw_ = raw;
   }
   weight_bytes_ += embd_.bytes;
@@ -226,7 +226,7 @@ void Session::upload(const GGUFView& g) {  // model.cpp:169-238 tensor map
     ple_row_bytes_ = gguf_bytes(pt->type, 1, row_el);
     ple_table_.bytes = ple_row_bytes_ * pt->shape[1];
     uint8_t* raw = dalloc<uint8_t>(ple_table_.bytes);
-    LLMI_HIP(hipMemcpy(raw, g.tensor_data(*pt), ple_table_.bytes, hipMemcpyHostToDevice));
+    h2d(raw, g.tensor_data(*pt), ple_table_.bytes);
     ple_table_.qs = raw;
     if (const GTensor* mp = g.tensor("per_layer_model_proj.weight")) {
       if ((int)mp->shape[0] != hp_.n_embd || (int)mp->shape[1] != row_el)
@@ -489,7 +489,7 @@ void Session::build_rope_tables() {
       }
     }
     float* d = dalloc<float>(h.size());
-    LLMI_HIP(hipMemcpy(d, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+    h2d(d, h.data(), h.size() * 4);
     return d;
   };
   rope_swa_ = make(10000.0f, hp_.hd_k_swa);  // model.cpp:732
@@ -498,6 +498,7 @@ void Session::build_rope_tables() {
 
 Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts) : opts_(opts) {
   exact_ = (opts.flags & LLMI_EXACT) != 0;
+  dev_old_init_ = getenv("LLMI_DEV_OLD_INIT") != nullptr;
   ex_gemv_ = ex_norm_ = ex_attn_ = ex_logits_ = exact_;
   if (const char* e = getenv("LLMI_EXACT_PARTS")) {  // diagnostics: mix exact/fast kernel families
     const std::string s(e);
@@ -529,8 +530,8 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
   try {
     if (tp_) {
       coll_ = tp_solo         ? make_null(tp_rank_, tp_size_)
-              : opts.tp_group ? make_local(reinterpret_cast<LocalGroup*>(opts.tp_group), tp_rank_, tp_size_)
-              : tp_peer       ? make_peer(tp_rank_, tp_size_)
+              : opts.tp_group ? make_local(reinterpret_cast<LocalGroup*>(opts.tp_group), tp_rank_, tp_size_, stream_)
+              : tp_peer       ? make_peer(tp_rank_, tp_size_, stream_)
                               : make_rccl(tp_rank_, tp_size_, opts.tp_id);
       if (!coll_->graph_safe()) use_graph_ = false;
       const char* fx = getenv("LLMI_TP_FUSED");
@@ -618,6 +619,7 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
     }
     setup_engine(g);
     if (!engine_) setup_ffn_engine(g);
+    LLMI_HIP(hipStreamSynchronize(stream_));  // every zeroing and copy above complete before the first call
   } catch (const gguf_error& e) {
     release();
     throw status_error(LLMI_E_GGUF, e.what());
@@ -630,6 +632,9 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
 Session::~Session() { release(); }
 
 void Session::release() {
+  // nothing of this session may still run when its graphs and memory go (a broken session's kernels may still be
+  // spinning up to LLMI_PX_TIMEOUT_MS; enqueue() without sync() leaves work in flight): drain, errors ignored
+  if (stream_) (void)hipStreamSynchronize(stream_);
   if (graph_exec_) (void)hipGraphExecDestroy(graph_exec_);
   if (graph_) (void)hipGraphDestroy(graph_);
   graph_exec_ = nullptr;
@@ -1265,16 +1270,23 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
   bool pxf = tp_ && px_on() && !ffn_engine_;
   for (const auto& l : L_) pxf = pxf && l.qkv.size() == 1;  // (the two-weight q|k|v launch has no fused variant)
   int k_d = -1;  // the previous layer's down exchange, read by this layer's qkv prologue
+  std::vector<int> px_nwg;  // exchange k -> the work-groups that push it (their checksum granules, px.h)
   auto fx_in = [&](LayerGemv& g, int k, int ws) {
     if (k < 0) return;
     g.px = d_px_;
     g.px_in = k;
     g.px_in_ws = ws;
+    g.px_in_nwg = k < (int)px_nwg.size() ? px_nwg[k] : 0;
   };
   auto fx_out = [&](LayerGemv& g) {
     g.px = d_px_;
     g.px_out = px_k_++;
     return g.px_out;
+  };
+  auto fx_nwg = [&](const LayerGemv& g, int nwg) {  // after the producing launch
+    if (g.px_out < 0) return;
+    if ((int)px_nwg.size() <= g.px_out) px_nwg.resize(g.px_out + 1, 0);
+    px_nwg[g.px_out] = nwg;
   };
   for (int l = 0; l < hp_.n_layer; l++) {
     LayerDev& Ld = L_[l];
@@ -1330,7 +1342,8 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
       if (trace_fn_ && qrole == LAYER_PRO) g.xn_out = xn_;
       aa.q8k = Ld.o.w.kq ? 1 : 0;
       aa.softcap = hp_.attn_softcap;
-      launch_attn_block(Ld.qkv[0].w, Ld.qkv.size() > 1 ? &Ld.qkv[1].w : nullptr, g, qrole, Ld.o.w, go, aa, qa, bs, s);
+      fx_nwg(go, launch_attn_block(Ld.qkv[0].w, Ld.qkv.size() > 1 ? &Ld.qkv[1].w : nullptr, g, qrole, Ld.o.w, go, aa,
+                                   qa, bs, s));
       kernels_per_token_++;
       if (trace_fn_) {  // the launch's products: residual / norm (prologue), q|k|v and xo granules, attention, o
         if (qrole == LAYER_PRO) {
@@ -1411,7 +1424,7 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
       go.out = o_out_ + (size_t)tp_rank_ * e_sh_;
       if (pxf) fx_out(go);
       tap("xo", l, act_.q8.xb, (size_t)hp_.n_head * hd / 32 * sizeof(XBlock), s);
-      for (int r = 0; r < dup("o_proj"); r++) launch_layer_gemv(Ld.o.w, go, LAYER_PLAIN, s);
+      for (int r = 0; r < dup("o_proj"); r++) fx_nwg(go, launch_layer_gemv(Ld.o.w, go, LAYER_PLAIN, s));
       tap("o", l, o_out_, (size_t)E * 4, s);
       dump("attention results (node_30 for MUL_MAT)-" + L, o_out_, E, s);
     }
@@ -1478,7 +1491,8 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
       fx_in(gg, k_o, e_sh_);
       k_h = fx_out(gg);
     }
-    for (int r = 0; r < dup("gate_up"); r++) launch_layer_gemv(Ld.gate_up[0].w, gg, gelu_x ? LAYER_GELU_X : LAYER_GELU, s);
+    for (int r = 0; r < dup("gate_up"); r++)
+      fx_nwg(gg, launch_layer_gemv(Ld.gate_up[0].w, gg, gelu_x ? LAYER_GELU_X : LAYER_GELU, s));
     tap("ffn_resid", l, gelu_x ? cur : other, (size_t)E * 4, s);
     tap("ffn_norm", l, xn_, (size_t)E * 4, s);
     tap("hid", l, hid_, (size_t)hp_.n_ff * 4, s);
@@ -1498,7 +1512,7 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
     // role reads the blocks of a residual_norm launch instead, and the last layer's feeds the final norm)
     const bool dfx = gfx && l + 1 < hp_.n_layer && (!block_ || block_pro_);
     k_d = dfx ? fx_out(gd) : -1;
-    for (int r = 0; r < dup("down"); r++) launch_layer_gemv(Ld.down.w, gd, dplain ? LAYER_PLAIN : LAYER_QUANT, s);
+    for (int r = 0; r < dup("down"); r++) fx_nwg(gd, launch_layer_gemv(Ld.down.w, gd, dplain ? LAYER_PLAIN : LAYER_QUANT, s));
     tap("down", l, d_out_, (size_t)E * 4, s);
     if (dfx) coll_->fused_point(s);
     else if (tp_) coll_->all_gather(d_out_, (size_t)e_sh_ * sizeof(float), s, px_take());
@@ -1771,7 +1785,7 @@ void Session::px_prepare() {
   PxLink l;
   coll_->fused_link(l);
   PxLink* d = dalloc<PxLink>(1);
-  LLMI_HIP(hipMemcpy(d, &l, sizeof(l), hipMemcpyHostToDevice));
+  h2d(d, &l, sizeof(l));
   d_px_ = d;
 }
 
@@ -1970,10 +1984,11 @@ void Session::peer_connect(const void* handles) {
 void Session::check_device_error() {
   if (const int e = coll_ ? coll_->failed() : 0) {  // the push exchange: a wait past its bound, or a bad checksum
     broken_ = true;
-    throw status_error(LLMI_E_HIP, e == 2 ? "tensor-parallel push exchange: a received slice failed its checksum "
-                                            "(device results invalid)"
-                                          : "tensor-parallel push exchange: a peer's slice did not arrive within "
-                                            "LLMI_PX_TIMEOUT_MS (device results invalid)" + coll_->fail_detail());
+    throw status_error(LLMI_E_HIP, (e == 2 ? std::string("tensor-parallel push exchange: a received slice failed its "
+                                                         "checksum (device results invalid)")
+                                           : std::string("tensor-parallel push exchange: a peer's slice did not arrive "
+                                                         "within LLMI_PX_TIMEOUT_MS (device results invalid)")) +
+                                       coll_->fail_detail());
   }
   if (blk_trace_) {  // development: append the last traced launch (work-group x 8 clocks) to LLMI_BLOCK_TRACE_OUT
     std::vector<unsigned long long> h(4096 * 8);
@@ -1986,15 +2001,18 @@ void Session::check_device_error() {
   }
   if (!blk_err_) return;
   int ev[2] = {0, 0};
-  LLMI_HIP(hipMemcpy(ev, blk_err_, sizeof(ev), hipMemcpyDeviceToHost));
+  LLMI_HIP(hipMemcpyAsync(ev, blk_err_, sizeof(ev), hipMemcpyDeviceToHost, stream_));
+  LLMI_HIP(hipStreamSynchronize(stream_));
   const int e = ev[0];
   if (ev[1]) {
     slow_waits_ += ev[1];
-    LLMI_HIP(hipMemset(blk_err_ + 1, 0, sizeof(int)));
+    LLMI_HIP(hipMemsetAsync(blk_err_ + 1, 0, sizeof(int), stream_));
+    LLMI_HIP(hipStreamSynchronize(stream_));
   }
   if (e) {  // reported once: the flag and every attention ticket are cleared so the session's next call starts clean
-    LLMI_HIP(hipMemset(blk_err_, 0, sizeof(int)));
-    LLMI_HIP(hipMemset(ticket_, 0, sizeof(unsigned) * (size_t)hp_.n_head));
+    LLMI_HIP(hipMemsetAsync(blk_err_, 0, sizeof(int), stream_));
+    LLMI_HIP(hipMemsetAsync(ticket_, 0, sizeof(unsigned) * (size_t)hp_.n_head, stream_));
+    LLMI_HIP(hipStreamSynchronize(stream_));
     throw status_error(LLMI_E_HIP, "attention block: a cross-work-group wait timed out (device results invalid)");
   }
 }

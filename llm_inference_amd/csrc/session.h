@@ -129,14 +129,28 @@ class Session {
   void tap(const char* name, int layer, const void* dev, size_t bytes, hipStream_t s);
   void run_step(bool gen = false);
   float* dev_f32_copy(const GGUFView& g, const GTensor* t, int n);
+  // every allocation is zeroed ON THE SESSION'S STREAM, so the zeroing is ordered before every kernel of this
+  // session that uses the buffer (null-stream hipMemset / hipMemcpy are not ordered with a non-blocking stream;
+  // DESIGN.md section 7, the round-5 tensor-parallel finding)
   template <typename T>
   T* dalloc(size_t count) {
     void* p = nullptr;
     LLMI_HIP(hipMalloc(&p, count * sizeof(T) + 64));
-    LLMI_HIP(hipMemset(p, 0, count * sizeof(T) + 64));
     allocs_.push_back(p);
+    if (dev_old_init_) LLMI_HIP(hipMemset(p, 0, count * sizeof(T) + 64));
+    else LLMI_HIP(hipMemsetAsync(p, 0, count * sizeof(T) + 64, stream_));
     return static_cast<T*>(p);
   }
+  // host bytes -> device, on the session's stream, complete on return (the host buffer may go away)
+  void h2d(void* dst, const void* src, size_t bytes) {
+    if (dev_old_init_) {
+      LLMI_HIP(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+      return;
+    }
+    LLMI_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, stream_));
+    LLMI_HIP(hipStreamSynchronize(stream_));
+  }
+  bool dev_old_init_ = false;  // LLMI_DEV_OLD_INIT (round-5 A/B only): the null-stream zeroing and copies
 
   llmi_session_opts opts_;
   bool exact_ = false, use_graph_ = true;

@@ -84,6 +84,7 @@ struct LayerGemv {
   // to every rank's mailbox
   const PxLink* px = nullptr;
   int px_in = -1, px_in_ws = 0;  // >= 0: the exchange (step number, words per rank) read instead of y / xg
+  int px_in_nwg = 0;             // the work-groups that pushed it (checksum granules per rank)
   int px_out = -1;               // >= 0: the exchange the outputs are pushed into
 };
 // Cross-work-group hand-offs of the attention-block kernel (k_attn.hip):
@@ -230,7 +231,8 @@ void launch_prefill_gelu(const float* gu, int F, int H, XBlock* xq, int xstride,
 int layer_gemv_slab(const DevWeight& w, int role);
 // GELU role: hidden units per work-group (the gate/up interleave group), 0 if unsupported
 int layer_gemv_gelu_group(int cols, uint32_t type = T_Q4_0);
-void launch_layer_gemv(const DevWeight& w, LayerGemv a, int role, hipStream_t s);
+// returns the launch's work-group count (a fused exchange's producing work-groups: px.h checksums)
+int launch_layer_gemv(const DevWeight& w, LayerGemv a, int role, hipStream_t s);
 // K-quant q|k (Q4_K) + v (Q6_K), both in the kq layout, in one launch (qkv roles)
 bool layer_gemv2_supported(const DevWeight& wa, const DevWeight& wb, int role);
 void launch_layer_gemv2(const DevWeight& wa, const DevWeight& wb, LayerGemv a, int role, hipStream_t s);

@@ -271,3 +271,87 @@ def test_exchange_failure_is_sticky(monkeypatch):
     first, second = res[0]
     assert first.status == "E_HIP" and "did not arrive" in str(first)
     assert second.status == "E_HIP" and "unusable" in str(second)
+
+
+def test_fused_checksum_catches_a_bad_word(monkeypatch):
+    """A received word whose tag is right but whose value is not (test hook LLMI_PX_TEST_CORRUPT: rank 0's own
+    mailbox copy of its peer's word 0 flipped between the producing and the consuming launch) is accepted by the
+    tag check but not by the fused exchange's checksum (px.h): rank 0 raises LLMI_E_HIP at the end of the call
+    instead of returning logits, and refuses later calls (VERDICT r4 #1: no silent wrong vector)."""
+    from llm_inference_amd._lib import LLMIError
+    from llm_inference_amd.model import Model, TPGroup
+    from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
+    cfg = CONFIGS["mini-1b"]
+    g = build_gemma3_gguf(cfg, seed=37)
+    monkeypatch.setenv("LLMI_NO_PREFILL", "1")
+    monkeypatch.setenv("LLMI_PX_TEST_CORRUPT", "0")
+    grp = TPGroup(2)
+    res = [None, None]
+
+    def rank(r):
+        m = Model(g, exact=False, max_ctx=32, tp_rank=r, tp_size=2, tp_group=grp)
+        assert m.get_info().tp_exchange == 4
+        try:
+            m.forward([5], 0)
+            res[r] = "ok"
+        except LLMIError as e:
+            res[r] = e
+        if r == 0 and isinstance(res[0], LLMIError):
+            try:
+                m.forward([7], 1)
+                res[r] = "second call ran"
+            except LLMIError as e:
+                res[r] = (res[r], e)
+        m.close()
+
+    th = [threading.Thread(target=rank, args=(r,)) for r in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    grp.close()
+    assert isinstance(res[0], tuple), res
+    first, second = res[0]
+    assert first.status == "E_HIP" and "checksum" in str(first), str(first)
+    assert second.status == "E_HIP" and "unusable" in str(second)
+
+
+def test_sessions_created_concurrently_first_forward(monkeypatch):
+    """The round-4 wrong-logits cause (DESIGN.md section 7): sessions created at the same time by the group's
+    threads zeroed their buffers with null-stream hipMemset / copies, which are not ordered with the sessions'
+    non-blocking streams -- the FIRST forward then read buffers the zeroing overwrote (all ranks the same wrong
+    logits, up to 12 off; the second forward on the same sessions right; 24 of 338 lifetimes on one box, 0 with the
+    sessions constructed one at a time).  Every allocation is now zeroed and every copy made on the session's own
+    stream: 16 lifetimes of 8 ranks created together, each rank's first and second forward equal to the whole
+    model's."""
+    from llm_inference_amd.model import Model, TPGroup
+    from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
+    cfg = CONFIGS["mini-27b"]
+    g = build_gemma3_gguf(cfg, seed=13)
+    prompt = np.random.default_rng(15).integers(4, cfg.vocab, 70).astype(np.int32)
+    monkeypatch.setenv("LLMI_NO_BLOCK", "1")
+    whole = Model(g, exact=False, max_ctx=128)
+    ref = whole.forward(prompt, 0)
+    whole.close()
+    for it in range(16):
+        grp = TPGroup(8)
+        out, errs = [None] * 8, []
+
+        def rank(r):
+            try:
+                m = Model(g, exact=False, max_ctx=128, tp_rank=r, tp_size=8, tp_group=grp)
+                out[r] = (m.forward(prompt, 0), m.forward(prompt, 0))
+                m.close()
+            except Exception as e:  # noqa: BLE001 -- reported below
+                errs.append((r, e))
+
+        th = [threading.Thread(target=rank, args=(r,)) for r in range(8)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(300)
+        grp.close()
+        assert not errs, errs
+        for r, (lg1, lg2) in enumerate(out):
+            assert np.array_equal(lg1, ref), f"lifetime {it} rank {r}: first forward off by {np.abs(lg1 - ref).max()}"
+            assert np.array_equal(lg2, ref), f"lifetime {it} rank {r}: second forward off by {np.abs(lg2 - ref).max()}"
