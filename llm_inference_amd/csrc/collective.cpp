@@ -14,6 +14,7 @@
 #include <string>
 
 #include "common.h"
+#include "session_kernels.h"
 
 namespace llmi {
 
@@ -89,8 +90,8 @@ class Mailbox {
   ~Mailbox() {
     for (int q = 0; q < G_; q++)
       if (q != rank_ && opened_ && peers_[q]) (void)hipIpcCloseMemHandle(peers_[q]);
-    (void)hipFree(mine_);
-    (void)hipFree(ctl_);
+    dev_free(mine_);
+    dev_free(ctl_);
   }
   // the group's first tag (before the first exchange: the counter is then at seed - 1)
   void seed(uint32_t first_tag) {

@@ -897,8 +897,8 @@ XlWeight make_xl_weight(const XlSrc& src, hipStream_t s) {
 }
 
 void free_xl_weight(XlWeight& w) {
-  if (w.qs) (void)hipFree(w.qs);
-  if (w.d) (void)hipFree(w.d);
+  dev_free(w.qs);
+  dev_free(w.d);
   w = XlWeight{};
 }
 

@@ -347,7 +347,7 @@ void alloc_screen_table(const DevWeight& table, ScreenTable& st, hipStream_t s) 
 
 void free_screen_table(ScreenTable& st) {
   for (void* p : {(void*)st.qs, (void*)st.d, (void*)st.xs, (void*)st.hi, (void*)st.m_key})
-    if (p) (void)hipFree(p);
+    dev_free(p);
   st = ScreenTable{};
 }
 

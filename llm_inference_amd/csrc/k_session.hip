@@ -2,6 +2,9 @@
 // decode step (residual + norms, GELU + quantize, argmax, token feedback).
 #include "session_kernels.h"
 
+#include <mutex>
+#include <vector>
+
 namespace llmi {
 
 // ---------------------------------------------------------------------------
@@ -54,6 +57,34 @@ bool gemv_type_supported(uint32_t type) {
          type == T_BF16;
 }
 
+// Device memory of the sessions goes back to the allocator only while no OTHER session of the process is alive
+// (DESIGN.md section 7, round 5): with several sessions in one process (the one-GPU tensor-parallel group), memory
+// one session freed and another reallocated at the same time was read wrong on its first use -- one word of a
+// weight row, right on every later read (a one-GPU 4-rank group: 8 of 23 lifetimes; 0 of 2,868 with the frees held
+// back, scripts/dev/tp_diag.py).  Frees made while other sessions live wait in a graveyard released when the last
+// session ends; a lone session (the production case: one process per GPU) frees at once.
+namespace {
+std::mutex g_mem_mu;
+int g_live_sessions = 0;
+std::vector<void*> g_graveyard;
+}  // namespace
+
+void dev_free(void* p) {
+  if (!p) return;
+  std::lock_guard<std::mutex> lk(g_mem_mu);
+  if (g_live_sessions > 1) g_graveyard.push_back(p);
+  else (void)hipFree(p);
+}
+
+void session_live(int delta) {
+  std::lock_guard<std::mutex> lk(g_mem_mu);
+  g_live_sessions += delta;
+  if (g_live_sessions == 0) {
+    for (void* p : g_graveyard) (void)hipFree(p);
+    g_graveyard.clear();
+  }
+}
+
 // Upload `rows` rows of a GGUF weight (host bytes in block layout) to the
 // device, appending after `dst_row0` rows of an existing allocation `w`
 // (used to fuse q|k|v and gate|up into one GEMV).  w must be pre-allocated.
@@ -74,7 +105,7 @@ void upload_rows(DevWeight& w, int dst_row0, const void* host, int rows, hipStre
                          (uint4*)w.qs + 2 * b0, w.d + b0);
     LLMI_HIP(hipGetLastError());
     LLMI_HIP(hipStreamSynchronize(s));
-    LLMI_HIP(hipFree(tmp));
+    dev_free(tmp);
   } else {
     const size_t off = gguf_bytes(w.type, dst_row0, w.cols);
     LLMI_HIP(hipMemcpyAsync((uint8_t*)w.qs + off, host, bytes, hipMemcpyHostToDevice, s));
@@ -122,18 +153,18 @@ void to_slab_layout(DevWeight& w, hipStream_t s) {
                      nb, (uint4*)q2, d2);
   LLMI_HIP(hipGetLastError());
   LLMI_HIP(hipStreamSynchronize(s));
-  (void)hipFree(w.qs);
-  (void)hipFree(w.d);
+  dev_free(w.qs);
+  dev_free(w.d);
   w.qs = q2;
   w.d = d2;
   w.slab = 1;
 }
 
 void free_weight(DevWeight& w) {
-  if (w.qs) (void)hipFree(w.qs);
-  if (w.d) (void)hipFree(w.d);
-  if (w.kdd) (void)hipFree(w.kdd);
-  if (w.kqh) (void)hipFree(w.kqh);
+  dev_free(w.qs);
+  dev_free(w.d);
+  dev_free(w.kdd);
+  dev_free(w.kqh);
   w.qs = nullptr;
   w.d = nullptr;
   w.kdd = nullptr;
@@ -236,7 +267,7 @@ void to_kq_layout(DevWeight& w, hipStream_t s, int slab) {
   }
   LLMI_HIP(hipGetLastError());
   LLMI_HIP(hipStreamSynchronize(s));
-  LLMI_HIP(hipFree(w.qs));
+  dev_free(w.qs);
   w.qs = qs;
   w.d = sc;
   w.kdd = dd;

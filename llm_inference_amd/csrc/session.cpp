@@ -526,8 +526,10 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
       throw status_error(LLMI_E_ARG, "tensor parallel needs the fused fast path (no LLMI_EXACT / LLMI_NO_FUSE)");
   }
   LLMI_HIP(hipSetDevice(opts.device));
-  LLMI_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  session_live(+1);  // (release() ends it: every path out of here, normal or not, runs release())
+  live_ = true;
   try {
+    LLMI_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     if (tp_) {
       coll_ = tp_solo         ? make_null(tp_rank_, tp_size_)
               : opts.tp_group ? make_local(reinterpret_cast<LocalGroup*>(opts.tp_group), tp_rank_, tp_size_, stream_)
@@ -667,13 +669,15 @@ void Session::release() {
   if (own_logits_w_) free_weight(logits_w_);
   own_logits_w_ = false;
   free_weight(embd_);
-  for (void* p : allocs_) (void)hipFree(p);
+  for (void* p : allocs_) dev_free(p);
   allocs_.clear();
   if (h_stage_) (void)hipHostFree(h_stage_);
   h_stage_ = nullptr;
   coll_.reset();
   if (stream_) (void)hipStreamDestroy(stream_);
   stream_ = nullptr;
+  if (live_) session_live(-1);
+  live_ = false;
 }
 
 // Activation format each weight type consumes (ops.cpp:209-210, 630-631, 724-725, 542-551)
@@ -1886,7 +1890,7 @@ void Session::forward_trace(const int32_t* tokens, int n, int pos, bool gen, llm
   if (pos < 0 || pos + n > max_ctx_) throw status_error(LLMI_E_RANGE, "trace: context overflow");
   for (int i = 0; i < n; i++)
     if (tokens[i] < 0 || tokens[i] >= vocab_) throw status_error(LLMI_E_RANGE, "trace: token id out of range");
-  if (tp_) throw status_error(LLMI_E_ARG, "trace: one device only");
+  // (a tensor-parallel rank traces too -- every rank of the group must call it: the standalone exchanges run)
   const bool graph = use_graph_;
   use_graph_ = false;
   trace_fn_ = fn;

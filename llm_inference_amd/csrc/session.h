@@ -151,6 +151,7 @@ class Session {
     LLMI_HIP(hipStreamSynchronize(stream_));
   }
   bool dev_old_init_ = false;  // LLMI_DEV_OLD_INIT (round-5 A/B only): the null-stream zeroing and copies
+  bool live_ = false;          // counted in session_live (k_session.hip)
 
   llmi_session_opts opts_;
   bool exact_ = false, use_graph_ = true;

@@ -12,6 +12,10 @@ bool gemv_type_supported(uint32_t type);
 DevWeight alloc_weight(uint32_t type, int rows, int cols, size_t slack = 64);  // slack: bytes allocated past qs / d
 void upload_rows(DevWeight& w, int dst_row0, const void* host, int rows, hipStream_t s);
 void free_weight(DevWeight& w);
+// device memory of the sessions (k_session.hip): freed at once only while no other session of the process is alive,
+// else when the last one ends; session_live(+1 / -1) brackets a session's lifetime
+void dev_free(void* p);
+void session_live(int delta);
 // Q4_0 row-major blocks -> slab-major (k_layer.hip's a.slab layout): slabs of
 // 8 blocks x all rows, block b of row r at (b / 8) rows 8 + r 8 + b % 8.
 void to_slab_layout(DevWeight& w, hipStream_t s);

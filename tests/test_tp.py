@@ -316,42 +316,52 @@ def test_fused_checksum_catches_a_bad_word(monkeypatch):
     assert second.status == "E_HIP" and "unusable" in str(second)
 
 
-def test_sessions_created_concurrently_first_forward(monkeypatch):
-    """The round-4 wrong-logits cause: sessions created at the same time by the group's
-    threads zeroed their buffers with null-stream hipMemset / copies, which are not ordered with the sessions'
-    non-blocking streams -- the FIRST forward then read buffers the zeroing overwrote (all ranks the same wrong
-    logits, up to 12 off; the second forward on the same sessions right; 24 of 338 lifetimes on one box, 0 with the
-    sessions constructed one at a time).  Every allocation is now zeroed and every copy made on the session's own
-    stream: 16 lifetimes of 8 ranks created together, each rank's first and second forward equal to the whole
+@pytest.mark.parametrize("case", ["27b-8-prefill", "1b-4-shard"])
+def test_sessions_created_concurrently_first_forward(case, monkeypatch):
+    """The round-4 wrong-logits causes, both in sessions a group's threads create at the same
+    time, both seen as a wrong FIRST forward (the second forward on the same sessions right):
+    (1) zeroing and copies made with null-stream hipMemset / hipMemcpy, which are not ordered with the sessions'
+    non-blocking streams (mini-27b tp 8, batched prefill: 24 of 338 lifetimes; every allocation is now zeroed and
+    every copy made on the session's own stream);
+    (2) device memory one session freed during its construction (upload staging, old weight layouts) and another
+    reallocated at the same time, read wrong on first use (mini-1b tp 4, heads sharded: one hidden unit of one
+    rank's first GELU launch; 8 of 23 lifetimes; frees are now held back while other sessions live).
+    16 lifetimes, the ranks' sessions created together, each rank's first and second forward equal to the whole
     model's."""
     from llm_inference_amd.model import Model, TPGroup
     from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
-    cfg = CONFIGS["mini-27b"]
-    g = build_gemma3_gguf(cfg, seed=13)
-    prompt = np.random.default_rng(15).integers(4, cfg.vocab, 70).astype(np.int32)
+    if case == "27b-8-prefill":
+        cfg, tp, n, seed, pseed = CONFIGS["mini-27b"], 8, 70, 13, 15
+    else:
+        cfg, tp, n, seed, pseed = CONFIGS["mini-1b"], 4, 12, 3, 5
+        monkeypatch.setenv("LLMI_TP_HEAD_SHARD", "1")
+        monkeypatch.setenv("LLMI_NO_PREFILL", "1")
+    g = build_gemma3_gguf(cfg, seed=seed)
+    prompt = np.random.default_rng(pseed).integers(4, cfg.vocab, n).astype(np.int32)
     monkeypatch.setenv("LLMI_NO_BLOCK", "1")
+    monkeypatch.setenv("LLMI_TP_BARRIER_S", "20")  # a failing rank's peers give up soon
     whole = Model(g, exact=False, max_ctx=128)
     ref = whole.forward(prompt, 0)
     whole.close()
     for it in range(16):
-        grp = TPGroup(8)
-        out, errs = [None] * 8, []
+        grp = TPGroup(tp)
+        out, errs = [None] * tp, []
 
         def rank(r):
             try:
-                m = Model(g, exact=False, max_ctx=128, tp_rank=r, tp_size=8, tp_group=grp)
+                m = Model(g, exact=False, max_ctx=128, tp_rank=r, tp_size=tp, tp_group=grp)
                 out[r] = (m.forward(prompt, 0), m.forward(prompt, 0))
                 m.close()
             except Exception as e:  # noqa: BLE001 -- reported below
                 errs.append((r, e))
 
-        th = [threading.Thread(target=rank, args=(r,)) for r in range(8)]
+        th = [threading.Thread(target=rank, args=(r,)) for r in range(tp)]
         for t in th:
             t.start()
         for t in th:
             t.join(300)
         grp.close()
-        assert not errs, errs
+        assert not errs, f"lifetime {it}: {errs}"
         for r, (lg1, lg2) in enumerate(out):
             assert np.array_equal(lg1, ref), f"lifetime {it} rank {r}: first forward off by {np.abs(lg1 - ref).max()}"
             assert np.array_equal(lg2, ref), f"lifetime {it} rank {r}: second forward off by {np.abs(lg2 - ref).max()}"
