@@ -64,34 +64,34 @@ uint64_t px_timeout_ticks() {  // LLMI_PX_TIMEOUT_MS (default 10 s): the bound o
 // inside one process on one device.
 class Mailbox {
  public:
-  static constexpr int kCap = 1 << 18;  // words per rank slot (1 MB of payload): every decode exchange in one
+  static constexpr int kCap = (1 << 18) - PX_MAX_CS;  // words per rank slot (~1 MB of payload): every decode exchange in one
   static constexpr size_t kSlot = (size_t)kCap + PX_MAX_CS;  // words, then checksum granules (px.h)
   // zeroed on the owning session's stream and complete on return (a null-stream hipMemset is not ordered with the
   // session's non-blocking stream)
   Mailbox(int rank, int G, hipStream_t s) : rank_(rank), G_(G), timeout_(px_timeout_ticks()), s_(s) {
     if (G < 1 || G > PX_MAX_RANKS) throw std::runtime_error("push exchange: 1-16 ranks");
     if (rank < 0 || rank >= G) throw std::runtime_error("push exchange: rank out of range");
+    // ONE uncached allocation, a whole number of 2 MiB: the exchange counter / error words in its first 4 KiB, the
+    // mailbox after them.  (An uncached allocation of 16 MiB + 64 KiB held another buffer's bytes past its last 2 MiB
+    // boundary -- sender 3's checksum granules of half 1, the mailbox's tail: 5 of 1,832 one-GPU 4-rank lifetimes,
+    // 0 of 2,712 with the mailbox an exact 16 MiB; round 4's "foreign granule" sat at the same tail position of a
+    // 16 MiB + 4 KiB mailbox.  DESIGN.md section 7.)
     const size_t bytes = (size_t)2 * G * kSlot * sizeof(uint2);
-    LLMI_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&mine_), bytes, hipDeviceMallocUncached));
-    LLMI_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&ctl_), 8 * sizeof(unsigned), hipDeviceMallocUncached));
-    if (getenv("LLMI_DEV_OLD_INIT")) {  // round-5 A/B only: the round-4 null-stream form
-      l2_writeback_all();
-      LLMI_HIP(hipMemset(mine_, 0, bytes));
-      LLMI_HIP(hipMemset(ctl_, 0, 8 * sizeof(unsigned)));
-      LLMI_HIP(hipDeviceSynchronize());
-    } else {
-      LLMI_HIP(hipMemsetAsync(mine_, 0, bytes, s_));  // tag 0: nothing published (tags are >= 1)
-      LLMI_HIP(hipMemsetAsync(ctl_, 0, 8 * sizeof(unsigned), s_));
-      LLMI_HIP(hipStreamSynchronize(s_));
-    }
+    constexpr size_t kHead = 4096, kAlign = (size_t)2 << 20;
+    bytes_ = bytes;
+    alloc_ = (kHead + bytes + kAlign - 1) / kAlign * kAlign;
+    LLMI_HIP(hipExtMallocWithFlags(&base_, alloc_, hipDeviceMallocUncached));
+    ctl_ = reinterpret_cast<unsigned*>(base_);
+    mine_ = reinterpret_cast<uint2*>(reinterpret_cast<char*>(base_) + kHead);
+    LLMI_HIP(hipMemsetAsync(base_, 0, kHead + bytes, s_));  // tag 0: nothing published (tags are >= 1)
+    LLMI_HIP(hipStreamSynchronize(s_));
     peers_.assign(G, nullptr);
     peers_[rank] = mine_;
   }
   ~Mailbox() {
     for (int q = 0; q < G_; q++)
-      if (q != rank_ && opened_ && peers_[q]) (void)hipIpcCloseMemHandle(peers_[q]);
-    dev_free(mine_);
-    dev_free(ctl_);
+      if (q != rank_ && opened_ && opened_base_[q]) (void)hipIpcCloseMemHandle(opened_base_[q]);
+    dev_free(base_);
   }
   // the group's first tag (before the first exchange: the counter is then at seed - 1)
   void seed(uint32_t first_tag) {
@@ -111,7 +111,7 @@ class Mailbox {
   void handle(void* out) const {
     static_assert(sizeof(hipIpcMemHandle_t) <= PEER_HANDLE_BYTES, "IPC handle size");
     hipIpcMemHandle_t h;
-    LLMI_HIP(hipIpcGetMemHandle(&h, mine_));
+    LLMI_HIP(hipIpcGetMemHandle(&h, base_));  // (the allocation's base; a peer adds the counter's 4 KiB)
     std::memset(out, 0, PEER_HANDLE_BYTES);
     std::memcpy(out, &h, sizeof(h));
   }
@@ -122,7 +122,8 @@ class Mailbox {
       std::memcpy(&h, static_cast<const char*>(handles) + (size_t)q * PEER_HANDLE_BYTES, sizeof(h));
       void* p = nullptr;
       LLMI_HIP(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
-      peers_[q] = static_cast<uint2*>(p);
+      opened_base_[q] = p;
+      peers_[q] = reinterpret_cast<uint2*>(static_cast<char*>(p) + 4096);
     }
     opened_ = true;
     // every rank hashes the same handle bytes: the same seed, unique to these allocations
@@ -182,15 +183,24 @@ class Mailbox {
     launch_push_exchange(a, s);
   }
   int failed() {  // reads and clears the device flag (callers have synchronised the stream)
-    int e[6] = {0, 0, 0, 0, 0, 0};
+    int e[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     LLMI_HIP(hipMemcpyAsync(e, ctl_ + 2, sizeof(e), hipMemcpyDeviceToHost, s_));
     LLMI_HIP(hipStreamSynchronize(s_));
     if (e[0]) {
       LLMI_HIP(hipMemsetAsync(ctl_ + 2, 0, sizeof(e), s_));
       LLMI_HIP(hipStreamSynchronize(s_));
       // a timed-out wait: the word it last saw (its tag relative to the expected one), kind and place
-      detail_ = e[0] == 2 ? " [checksum mismatch, tag " + std::to_string((unsigned)e[3]) + ": read " +
-                                std::to_string((unsigned)e[4]) + ", pushed " + std::to_string((unsigned)e[5]) + "]"
+      detail_ = e[0] == 2 ? " [checksum mismatch, tag " + std::to_string((unsigned)e[3]) + " (consumer role " +
+                                std::to_string(e[1] / 1000) + ", fused exchange " + std::to_string(e[1] % 1000) +
+                                " of the step, work-group " + std::to_string(e[2]) + "): read " +
+                                std::to_string((unsigned)e[4]) + ", pushed " + std::to_string((unsigned)e[5]) +
+                                "; read again " + std::to_string((unsigned)e[6]) + ", granules of another tag: words " +
+                                std::to_string(e[7] & 0xFFFF) + " checksums " + std::to_string(e[7] >> 16) +
+                                "; first sender whose words and checksums differ " + std::to_string(e[10]) + "; " +
+                                std::to_string(e[8]) + " checking work-groups failed, mask " + std::to_string(e[9]) +
+                                "; a checksum granule of another tag: sender*10000+wg " + std::to_string(e[11]) +
+                                " {tag " + std::to_string((unsigned)e[12]) + ", word " + std::to_string((unsigned)e[13]) +
+                                "}]"
                           : std::string(e[0] == 3 ? " [fused" : " [standalone") + " exchange, tag " +
                                      std::to_string((unsigned)e[3]) + ", word " + std::to_string(e[2]) +
                                      " held tag " + (e[1] >= 0 ? "+" : "") + std::to_string(e[1]) + " word " +
@@ -218,6 +228,9 @@ class Mailbox {
   int rank_, G_;
   uint64_t timeout_;
   hipStream_t s_;  // the owning session's stream
+  size_t bytes_ = 0, alloc_ = 0;
+  void* base_ = nullptr;  // the allocation: ctl_ at its start, then mine_
+  void* opened_base_[PX_MAX_RANKS] = {};  // peers' allocations as IPC-mapped here
   bool seeded_ = false;
   uint2* mine_ = nullptr;
   unsigned* ctl_ = nullptr;  // [0] exchange count, [1] ticket, [2] error flag, [3..5] its diagnostics

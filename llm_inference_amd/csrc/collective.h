@@ -96,9 +96,6 @@ struct PushArgs {
   int skip;                   // fused exchanges since the previous standalone one: tag = epoch + 1 + skip
 };
 void launch_push_exchange(const PushArgs& a, hipStream_t s);
-// every XCD's L2 written back (a system-scope release on each), on the null stream, synchronised: run before a
-// new mailbox is zeroed, so no line an earlier owner of its memory left dirty in an L2 lands on it later
-void l2_writeback_all();
 constexpr int PEER_HANDLE_BYTES = 64;
 
 // unique id for a new RCCL communicator (rank 0 makes it, the caller

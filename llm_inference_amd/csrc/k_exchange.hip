@@ -176,21 +176,6 @@ __global__ __launch_bounds__(PX_T) void push_exchange_kernel(PushArgs a) {
 
 }  // namespace
 
-namespace {
-__global__ void l2_writeback_kernel() {  // work-group b runs on XCD b % 8: 64 of them cover every XCD
-  // write back only: an invalidate here would also drop lines other sessions' kernels, running now, just wrote
-  // (measured: the acquire-release form broke the one-GPU group tests)
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-}  // namespace
-
-void l2_writeback_all() {
-  hipLaunchKernelGGL(l2_writeback_kernel, dim3(64), dim3(64), 0, nullptr);
-  LLMI_HIP(hipGetLastError());
-  LLMI_HIP(hipDeviceSynchronize());
-}
-
 void launch_push_exchange(const PushArgs& a, hipStream_t s) {
   if (a.G < 1 || a.G > PX_MAX_RANKS || a.rank < 0 || a.rank >= a.G || a.words < 0 || a.words > a.cap ||
       (!a.row_w && a.off + (size_t)a.words > a.stride) || a.skip < 0 || a.row_w < 0)

@@ -385,14 +385,15 @@ __device__ __forceinline__ void layer_body(const LayerGemv& a, const int bid, un
   const uint32_t tout = fout ? px_link_tag(*a.px, a.px_out) : 0u;
   // checksum terms (px.h): of the words this thread pushed / read; the LDS words of their work-group sums
   uint32_t pxs = 0u, pxc = 0u;
-  __shared__ uint32_t s_pxs[PXF ? 3 : 1];
-  if (PXF && t < 3) s_pxs[t] = 0u;  // (ordered before their use by the barrier after the prologue)
+  __shared__ uint32_t s_pxs[PXF ? 5 + 2 * PX_MAX_RANKS : 1];
+  if (PXF && t < 5 + 2 * PX_MAX_RANKS) s_pxs[t] = 0u;  // (ordered before their use by the barrier after the prologue)
   // the checksum granule of the pushed words, and (the first PX_CHECK_WG work-groups) the check of the words read:
   // every thread of the work-group, at each exit
   auto px_finish = [&]() {
     if constexpr (PXF) {
       if (fout) px_push_checksum(*a.px, tout, bid, pxs, &s_pxs[0]);
-      if (fin && bid < PX_CHECK_WG) px_verify(*a.px, tin, a.px_in_nwg, pxc, &s_pxs[1]);
+      if (fin && bid < PX_CHECK_WG) px_verify(*a.px, tin, a.px_in_nwg, pxc, &s_pxs[1], ROLE * 1000 + a.px_in, bid, a.px_in_ws,
+                                                   ROLE == ROLE_PLAIN ? a.nb * 12 : a.nb * 32);
     }
   };
   // SIG: rows are published write-through; the work-group's rows lie in one

@@ -137,7 +137,9 @@ __device__ __forceinline__ void px_push_checksum(const PxLink& l, uint32_t tag, 
 
 // consumer: the terms of every word this work-group read (cs) against the nwg checksum granules of every rank
 // (s: two zeroed LDS words, as px_wg_add)
-__device__ __forceinline__ void px_verify(const PxLink& l, uint32_t tag, int nwg, uint32_t cs, uint32_t* s) {
+// (where: the consumer's role * 1000 + the exchange's number in the step, and its work-group: err[1] / err[2])
+__device__ __forceinline__ void px_verify(const PxLink& l, uint32_t tag, int nwg, uint32_t cs, uint32_t* s, int where,
+                                          int bid, int ws, int nwords) {
   const uint32_t got = px_wg_add(cs, s);
   uint32_t want = 0;
   const uint64_t t0 = wall_clock64();
@@ -157,7 +159,49 @@ __device__ __forceinline__ void px_verify(const PxLink& l, uint32_t tag, int nwg
     want += (uint32_t)x;
   }
   want = px_wg_add(want, s + 1);
+  if (want != got) {  // (uniform, rare) diagnostics: the whole vector and the checksums read once more, per sender
+    uint32_t* sg = s + 4;                 // [G] words' terms read again, per sender
+    uint32_t* sw = s + 4 + PX_MAX_RANKS;  // [G] checksum granules read again, per sender
+    uint32_t other = 0;
+    for (int W = threadIdx.x; W < nwords; W += blockDim.x) {
+      const int q = W / ws, w = W - q * ws;
+      const uint64_t x = __hip_atomic_load(
+          reinterpret_cast<const uint64_t*>(l.mail[l.rank] + ((size_t)(tag & 1u) * l.G + q) * l.slot_w + w),
+          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_fetch_add(sg + q, px_term((uint32_t)x, q, w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      other += (uint32_t)(x >> 32) != tag ? 1u : 0u;
+    }
+    for (int i = threadIdx.x; i < l.G * nwg; i += blockDim.x) {
+      const int q = i / nwg, b = i - q * nwg;
+      const uint64_t x = __hip_atomic_load(
+          reinterpret_cast<const uint64_t*>(l.mail[l.rank] + ((size_t)(tag & 1u) * l.G + q) * l.slot_w + l.cs0 + b),
+          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_fetch_add(sw + q, (uint32_t)x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if ((uint32_t)(x >> 32) != tag) {
+        other += 0x10000u;
+        __hip_atomic_store(l.err + 11, q * 10000 + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(l.err + 12, (int)(uint32_t)(x >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(l.err + 13, (int)(uint32_t)x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    other = px_wg_add(other, s + 3);  // (its barrier also orders the per-sender sums)
+    if (threadIdx.x == 0) {
+      uint32_t again = 0;
+      int bad = -1;
+      for (int q = 0; q < l.G; q++) {
+        again += sg[q];
+        if (bad < 0 && sg[q] != sw[q]) bad = q;
+      }
+      __hip_atomic_store(l.err + 6, (int)again, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(l.err + 7, (int)other, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(l.err + 10, bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(l.err + 8, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_or(l.err + 9, 1 << (bid & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
   if (threadIdx.x == 0 && want != got) {
+    __hip_atomic_store(l.err + 1, where, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(l.err + 2, bid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(l.err + 3, (int)tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(l.err + 4, (int)got, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(l.err + 5, (int)want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

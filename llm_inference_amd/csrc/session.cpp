@@ -498,7 +498,6 @@ void Session::build_rope_tables() {
 
 Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts) : opts_(opts) {
   exact_ = (opts.flags & LLMI_EXACT) != 0;
-  dev_old_init_ = getenv("LLMI_DEV_OLD_INIT") != nullptr;
   ex_gemv_ = ex_norm_ = ex_attn_ = ex_logits_ = exact_;
   if (const char* e = getenv("LLMI_EXACT_PARTS")) {  // diagnostics: mix exact/fast kernel families
     const std::string s(e);

@@ -137,20 +137,14 @@ class Session {
     void* p = nullptr;
     LLMI_HIP(hipMalloc(&p, count * sizeof(T) + 64));
     allocs_.push_back(p);
-    if (dev_old_init_) LLMI_HIP(hipMemset(p, 0, count * sizeof(T) + 64));
-    else LLMI_HIP(hipMemsetAsync(p, 0, count * sizeof(T) + 64, stream_));
+    LLMI_HIP(hipMemsetAsync(p, 0, count * sizeof(T) + 64, stream_));
     return static_cast<T*>(p);
   }
   // host bytes -> device, on the session's stream, complete on return (the host buffer may go away)
   void h2d(void* dst, const void* src, size_t bytes) {
-    if (dev_old_init_) {
-      LLMI_HIP(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
-      return;
-    }
     LLMI_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, stream_));
     LLMI_HIP(hipStreamSynchronize(stream_));
   }
-  bool dev_old_init_ = false;  // LLMI_DEV_OLD_INIT (round-5 A/B only): the null-stream zeroing and copies
   bool live_ = false;          // counted in session_live (k_session.hip)
 
   llmi_session_opts opts_;

@@ -4,10 +4,12 @@ Per run: a whole-model session again, then a TPGroup lifetime whose ranks each r
 forward overwrites the same KV rows: a persistent corruption -- weights, tables -- repeats, a transient race does not)
 and a short greedy decode.  Modes switch the suspects one at a time (the environment is read at session creation):
   default  -- the fused push exchange (the product default)
-  nowb     -- no L2 write-back kernel in the mailbox constructor (LLMI_PX_NO_WB=1)
   copy     -- device-to-device slice copies (no mailbox at all)
   serial   -- the ranks' sessions constructed one at a time (a lock around Model())
   fused0   -- the standalone push-exchange launches (LLMI_TP_FUSED=0)
+  ctorbar  -- every rank's session constructed before any rank's first forward (ctorbar0: and LLMI_TP_FUSED=0)
+(round 5: the modes that split the three causes of DESIGN.md section 7; the removed A/B builds -- null-stream
+initialisation, no deferred frees, a 16 MiB + 64 KiB mailbox -- are recorded there with their counts)
 usage: python scripts/dev/tp_diag.py case seconds_per_mode mode[,mode...]
   case: 27b8pf (mini-27b tp 8, 70-token batched prefill) | 4b2dec (mini-4b tp 2, decode kernels only)"""
 import os
@@ -30,8 +32,8 @@ CASES = {
     "1b4dec": dict(cfg="mini-1b", tp=4, seed=3, pseed=5, n=12, gen=11, ctx=64,
                    env={"LLMI_NO_BLOCK": "1", "LLMI_NO_PREFILL": "1"}),
 }
-MODES = {"default": {}, "old": {"LLMI_DEV_OLD_INIT": "1"}, "nowb": {"LLMI_PX_NO_WB": "1"}, "copy": {"LLMI_TP_EXCHANGE": "copy"}, "serial": {},
-         "fused0": {"LLMI_TP_FUSED": "0"}, "ctorbar": {}, "ctorbar0": {"LLMI_TP_FUSED": "0"}}
+MODES = {"default": {}, "copy": {"LLMI_TP_EXCHANGE": "copy"}, "serial": {}, "fused0": {"LLMI_TP_FUSED": "0"},
+         "ctorbar": {}, "ctorbar0": {"LLMI_TP_FUSED": "0"}}
 
 
 def lifetime(g, c, prompt, serial, ctorbar=False):
