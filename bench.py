@@ -42,6 +42,8 @@ def parse():
     p.add_argument("--config", default="gemma-3-4b")
     p.add_argument("--exact", action="store_true")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-exact", action="store_true",
+                   help="skip the exact-mode sub-measurement (the reference's operation order: bit-exact greedy ids)")
     p.add_argument("--full-logits", action="store_true",
                    help="decode loop: full F16 logits GEMV + argmax instead of int8 screening + exact rescoring")
     p.add_argument("--cpu-decode", type=int, default=32, help="decode tokens in the CPU baseline sample")
@@ -174,6 +176,31 @@ def cpu_share() -> int:
     return max(1, min(n, int(os.environ.get("LLMI_CPU_SHARE", "16"))))
 
 
+FORCED = 8  # teacher-forced steps after the GPU line's prompt (parity check of exact and fast mode vs the reference)
+
+
+def forced_tokens(vocab: int) -> np.ndarray:
+    return np.random.default_rng(2024).integers(4, vocab, FORCED).astype(np.int32)
+
+
+def forced_logits(m, prompt, vocab):
+    """Logits after the prompt, then after each of FORCED teacher-forced tokens (positions len(prompt)..): the
+    same inputs on the device session and on the reference, so the comparison does not depend on the greedy ids
+    a random-init model settles into."""
+    out = [m.forward(prompt, 0)]
+    for i, t in enumerate(forced_tokens(vocab)):
+        out.append(m.forward(np.array([t], np.int32), len(prompt) + i))
+    return np.stack(out)
+
+
+def parity(ref, got) -> dict:
+    """Device logits vs the reference's at the same FORCED + 1 positions."""
+    same_bits = [bool(np.array_equal(r.view(np.uint32), x.view(np.uint32))) for r, x in zip(ref, got)]
+    return {"positions": len(ref), "logits_bit_identical": int(sum(same_bits)),
+            "argmax_identical": int(sum(int(np.argmax(r)) == int(np.argmax(x)) for r, x in zip(ref, got))),
+            "max_abs_logit_diff": float(np.abs(ref - got).max())}
+
+
 def cpu_baseline(g, cfg, n_decode: int, gpu_ids=None, mean_ctx=None, ctx_prompt=None):
     """BASELINE.md section 4 on this host: the reference's own Model::forward
     (oracle/_ref, built from its sources) -- or, where the reference is not
@@ -246,17 +273,21 @@ def cpu_baseline(g, cfg, n_decode: int, gpu_ids=None, mean_ctx=None, ctx_prompt=
         t0 = time.perf_counter()
         lg = mc.forward(np.asarray(ctx_prompt, np.int32), 0)
         t_pf = time.perf_counter() - t0
-        tok, pos, per_c = int(np.argmax(lg)), len(ctx_prompt), []
-        for _ in range(8):
+        # FORCED timed steps on teacher-forced tokens (bench.forced_tokens): their logits are the parity fixture
+        pos, per_c, ref_lg = len(ctx_prompt), [], [lg.copy()]
+        for t in forced_tokens(cfg.vocab):
             t0 = time.perf_counter()
-            lg = mc.forward(np.array([tok], np.int32), pos)
+            lg = mc.forward(np.array([t], np.int32), pos)
             per_c.append(time.perf_counter() - t0)
-            tok, pos = int(np.argmax(lg)), pos + 1
+            ref_lg.append(lg.copy())
+            pos += 1
         del mc
+        out["_ref_forced_logits"] = np.stack(ref_lg)  # (popped before printing)
         out["measured_at_gpu_context"] = {
-            "positions": f"{len(ctx_prompt)}-{len(ctx_prompt) + 7}", "value": round(8 / sum(per_c), 3),
+            "positions": f"{len(ctx_prompt)}-{len(ctx_prompt) + FORCED - 1}", "value": round(FORCED / sum(per_c), 3),
             "unit": "tokens/s", "threads": threads, "prefill_s": round(t_pf, 2),
-            "how": "the GPU line's prompt through one untimed Model::forward, then 8 timed greedy steps"}
+            "how": f"the GPU line's prompt through one untimed Model::forward, then {FORCED} timed steps on "
+                   "teacher-forced tokens (their logits: the parity check of the GPU line)"}
     out["ids"] = ids
     if gpu_ids is not None:
         k = min(len(ids), len(gpu_ids))
@@ -354,10 +385,12 @@ def main():
     m.forward(prompt, 0, want_logits=False)
     t_prefill = time.time() - t0
     first = m.last_argmax
+    first_after_prefill, warm_ids = first, []
     pos = a.prefill
     if a.warmup:
         m.enqueue(first, pos, a.warmup)
         toks = m.sync(a.warmup)
+        warm_ids = toks.tolist()
         first, pos = int(toks[-1]), pos + a.warmup
     d.barrier()
     m.sync()
@@ -497,6 +530,42 @@ def main():
                           # (prefill tail, warmup, timed steps, kernel timing): the spin-wait outlier check
                           "block_slow_waits": m.get_info().block_slow_waits},
     }
+    # Exact mode in the same invocation (north_star: "bit-exact token ids for greedy decode"): a second session on
+    # the exact-order engine (the reference's operation order), the same prompt, then the
+    # same timed decode; its first ids are checked against the reference's own (cpu_baseline, below) and the
+    # fast line's.  Single GPU only (exact mode has no tensor-parallel ranks).
+    exact_ids = None
+    gpu_forced = {}
+    if d.world == 1 and not a.no_cpu_baseline:  # this session's logits on the parity fixture's inputs
+        gpu_forced["exact" if a.exact else "fast"] = forced_logits(m, prompt, cfg.vocab)
+    if d.world == 1 and not a.exact and not a.no_exact:
+        mx = Model(g, device=dev, exact=True, max_ctx=max_ctx, use_graph=not a.no_graph)
+        t0 = time.time()
+        mx.forward(prompt, 0, want_logits=False)
+        t_pf_x = time.time() - t0
+        n_chk = max(a.warmup, 8)  # the warmup steps double as the id check (positions prefill .. prefill + 7)
+        mx.enqueue(mx.last_argmax, a.prefill, n_chk)
+        wt = mx.sync(n_chk)
+        exact_ids = [mx.last_argmax] + wt.tolist()
+        mx.sync()
+        t0 = time.perf_counter()
+        mx.enqueue(int(wt[-1]), a.prefill + n_chk, a.steps)
+        mx.sync(a.steps)
+        el_x = time.perf_counter() - t0
+        xinfo = mx.get_info()
+        gpu_forced["exact"] = forced_logits(mx, prompt, cfg.vocab) if not a.no_cpu_baseline else None
+        mx.close()
+        fast_ids = [first_after_prefill] + warm_ids
+        k = min(len(fast_ids), len(exact_ids))
+        out["exact"] = {
+            "value": round(a.steps / el_x, 3), "unit": "tokens/s", "steps": a.steps,
+            "ms_per_step": round(el_x * 1000.0 / a.steps, 4),
+            "positions": f"{a.prefill + n_chk}-{a.prefill + n_chk + a.steps - 1}",
+            "exact_engine": bool(getattr(xinfo, "exact_engine", 0)), "kernels_per_token": xinfo.kernels_per_token,
+            "prefill_s": round(t_pf_x, 3), "ids": exact_ids,
+            "fast_ids_agree": {"steps": k, "identical": fast_ids[:k] == exact_ids[:k]},
+            "how": "a second session with LLMI_EXACT (bit-identical to the reference's logits), the same prompt; "
+                   "first ids = argmax after the prompt + the first greedy steps; then the same timed decode"}
     gpu_ids = None
     if d.rank == 0 and d.world == 1 and not a.no_cpu_baseline:
         # the CPU sample's prompt on the GPU too: the same greedy ids?
@@ -509,6 +578,14 @@ def main():
             out["cpu_baseline"] = cpu_baseline(g, cfg, a.cpu_decode, gpu_ids, mean_ctx, ctx_prompt=prompt)
         except Exception as e:  # report, never hide
             out["cpu_baseline"] = {"error": repr(e)}
+        ref_lg = out["cpu_baseline"].pop("_ref_forced_logits", None)
+        if ref_lg is not None:  # device logits vs the reference's own on the same prompt + teacher-forced tokens
+            out["parity_vs_reference"] = {
+                k: parity(ref_lg, v) for k, v in gpu_forced.items() if v is not None}
+            out["parity_vs_reference"]["how"] = (
+                f"the reference (oracle/_ref: its own ops.cpp / model.cpp) and the device sessions on the GPU line's "
+                f"prompt, then {FORCED} teacher-forced tokens: logits compared bit for bit at each of the "
+                f"{FORCED + 1} positions (exact: the reference's operation order; fast: fp32 reassociation)")
     if d.rank == 0:
         print(json.dumps(out), flush=True)
 
