@@ -156,6 +156,12 @@ void Session::setup_tp() {
   const char* hs = getenv("LLMI_TP_HEAD_SHARD");
   const bool wide = hp_.n_embd >= 4096 && hp_.n_head % G == 0 && hp_.n_head_kv % G == 0;
   tp_rep_attn_ = hs ? atoi(hs) == 0 : !wide;
+  // exact mode: the exact-order engine's attention runs every head on every rank (its two launches read the whole
+  // q|k|v row set); o, gate/up and down are row-sharded -- each row's accumulator chains are the whole model's
+  if (exact_) {
+    if (tp_ && hs && atoi(hs) != 0) throw status_error(LLMI_E_ARG, "tensor parallel exact mode: heads are not sharded");
+    tp_rep_attn_ = true;
+  }
   if (tp_rep_attn_) {
     nh_ = hp_.n_head;
     nkv_ = hp_.n_head_kv;
@@ -332,7 +338,7 @@ void Session::upload(const GGUFView& g) {  // model.cpp:169-238 tensor map
       }
     }
     want_fused = want_fused || kq_path;
-    if (tp_ && !want_fused)
+    if (tp_ && !want_fused && !exact_)
       throw status_error(LLMI_E_ARG, "tensor parallel: layer " + std::to_string(l) +
                                          " shards are not in the fused Q4_0 launch table");
     if (want_fused) {
@@ -356,6 +362,8 @@ void Session::upload(const GGUFView& g) {  // model.cpp:169-238 tensor map
       weight_bytes_ += p.w.bytes;
       Ld.gate_up = {p};
       Ld.gu_interleaved = true;
+    } else if (tp_) {  // (exact mode) this rank's hidden units of gate and of up
+      Ld.gate_up = make_parts(g, {RowSlice{gt, r * f_sh_, f_sh_}, RowSlice{up, r * f_sh_, f_sh_}}, stream_, weight_bytes_);
     } else {
       Ld.gate_up = make_parts(g, {all_rows(gt), all_rows(up)}, stream_, weight_bytes_);
     }
@@ -521,8 +529,11 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
     tp_size_ = opts.tp_size;
     if (tp_size_ < 1 || tp_rank_ < 0 || tp_rank_ >= tp_size_)
       throw status_error(LLMI_E_ARG, "tensor parallel: tp_rank / tp_size out of range");
-    if (!fuse_layers_ || !dup_.empty())
-      throw status_error(LLMI_E_ARG, "tensor parallel needs the fused fast path (no LLMI_EXACT / LLMI_NO_FUSE)");
+    // the fused fast path, or exact mode on the exact-order engine (rows sharded, the chains of each row kept)
+    const bool exact_all = exact_ && ex_gemv_ && ex_norm_ && ex_attn_ && ex_logits_;
+    if ((!fuse_layers_ && !exact_all) || !dup_.empty())
+      throw status_error(LLMI_E_ARG, "tensor parallel needs the fused fast path or exact mode (no LLMI_NO_FUSE / "
+                                     "LLMI_EXACT_PARTS / LLMI_DUP)");
   }
   LLMI_HIP(hipSetDevice(opts.device));
   session_live(+1);  // (release() ends it: every path out of here, normal or not, runs release())
@@ -545,6 +556,9 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
     alloc_buffers();
     build_rope_tables();
     setup_xl();
+    if (tp_ && exact_ && !xl_)
+      throw status_error(LLMI_E_ARG, "tensor parallel exact mode needs the exact-order engine (Q4_0 Gemma-3 layers, "
+                                     "hidden units per rank % 32 == 0, embedding rows per rank % 16 == 0)");
     // batched prefill: the fast fused layout on one device, shapes the
     // prefill kernels cover (otherwise forward() runs the token loop)
     // (a tensor-parallel rank: its shards' GEMMs, the slices all-gathered per
@@ -794,7 +808,7 @@ void Session::record_step(hipStream_t s, bool gen, bool fold_embed) {
   if (x_q8) tap("xq", 0, x_blocks, x_blocks == (const void*)act_.q8k ? (size_t)(E / 256) * 292 : (size_t)(E / 32) * sizeof(XBlock), s);
   bool fused = fuse_layers_;
   for (const auto& l : L_) fused &= l.fused;
-  if (tp_ && !fused) throw status_error(LLMI_E_ARG, "tensor parallel needs the fused layer path");
+  if (tp_ && !fused && !xl_) throw status_error(LLMI_E_ARG, "tensor parallel needs the fused layer path");
   if (xl_ && !dump_ && !(trace_fn_ && getenv("LLMI_TRACE_PER_OP")) && x_q8 && x_blocks == (const void*)act_.q8.xb) {
     record_layers_xl(s);
   } else if (fused && engine_ && !dump_ && !trace_fn_) {
@@ -1538,10 +1552,13 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
 // Exact mode on the exact-order engine (exact.h): every Gemma-3 layer with Q4_0 q, k, v, o, gate, up and down
 // (the 4B / 1B / 27B Q4_0 files) gets XL copies of its weights; LLMI_EXACT_XL=0 keeps the per-op exact kernels.
 void Session::setup_xl() {
-  if (!exact_ || tp_ || hp_.gemma4 || ple_table_.qs || getenv("LLMI_EXACT_PARTS")) return;
+  if (!exact_ || hp_.gemma4 || ple_table_.qs || getenv("LLMI_EXACT_PARTS")) return;
   if (const char* e = getenv("LLMI_EXACT_XL"))
-    if (atoi(e) == 0) return;
-  if (hp_.n_embd % 128 || hp_.n_ff % 128 || 2 * (size_t)hp_.n_embd * 4 + hp_.n_embd / 32 * 68 > 60 * 1024) return;
+    if (atoi(e) == 0 && !tp_) return;
+  const int F = tp_ ? f_sh_ : hp_.n_ff;  // this rank's hidden units
+  if (hp_.n_embd % 128 || hp_.n_ff % 128 || F % 32 || (tp_ && e_sh_ % 16) ||
+      2 * (size_t)hp_.n_embd * 4 + hp_.n_embd / 32 * 68 > 60 * 1024)
+    return;
   for (const auto& l : L_) {
     bool ok = l.has_kv && !l.qkv.empty() && !l.gate_up.empty() && (hp_.n_head * l.hd) % 128 == 0 &&
               exact_attn_supported(l.hd, hp_.n_head, hp_.n_head_kv);
@@ -1549,15 +1566,15 @@ void Session::setup_xl() {
     for (const auto& p : l.gate_up) ok = ok && xl_supported(p.w);
     int gu_rows = 0;
     for (const auto& p : l.gate_up) gu_rows += p.w.rows;
-    ok = ok && xl_supported(l.o.w) && xl_supported(l.down.w) && gu_rows == 2 * hp_.n_ff && !l.gu_interleaved &&
-         (l.gate_up.size() == 1 || l.gate_up[0].w.rows == hp_.n_ff) && l.down.w.cols == hp_.n_ff;
+    ok = ok && xl_supported(l.o.w) && xl_supported(l.down.w) && gu_rows == 2 * F && !l.gu_interleaved &&
+         (l.gate_up.size() == 1 || l.gate_up[0].w.rows == F) && l.down.w.cols == hp_.n_ff;
     if (!ok) return;
   }
   for (auto& l : L_) {
     // gate and up: one part of rows [gate; up] (same type) or two parts
     DevWeight gate = l.gate_up[0].w, up;
     if (l.gate_up.size() == 1) {
-      const int F = hp_.n_ff, nb = gate.cols / 32;
+      const int nb = gate.cols / 32;
       gate.rows = F;
       up = gate;
       up.qs = static_cast<uint8_t*>(gate.qs) + (size_t)F * nb * 16;
@@ -1646,10 +1663,13 @@ void Session::record_layers_xl(hipStream_t s) {
     xa.vt = Ld.vt;
     xa.vt_stride = xa_vt_stride_;
     launch_exact_attn(xa, s);
+    // tensor-parallel ranks: this rank's rows of o, gate/up (its hidden units) and down, each slice all-gathered
+    // before its consumer (whose residual / norm prologue runs on the whole vector on every rank)
     XlArgs o;
     o.xb = xa_xq_;
-    o.out = o_out_;
+    o.out = o_out_ + (size_t)tp_rank_ * e_sh_;
     launch_exact_gemv(Ld.xo, o, XL_PLAIN, s);
+    if (tp_) coll_->all_gather(o_out_, (size_t)e_sh_ * sizeof(float), s, px_take());
     XlArgs gu;
     gu.y = o_out_;
     gu.w_post = Ld.post_attn_norm;
@@ -1658,14 +1678,16 @@ void Session::record_layers_xl(hipStream_t s) {
     gu.w_next = Ld.ffn_norm;
     gu.n = E;
     gu.eps = hp_.eps;
-    gu.hid = hid_;
-    gu.hq = hq_;
+    gu.hid = hid_ + (size_t)tp_rank_ * f_sh_;
+    gu.hq = hq_ + (size_t)tp_rank_ * (f_sh_ / 32);
     launch_exact_gemv(Ld.xgu, gu, XL_GELU, s);
+    if (tp_) coll_->all_gather(hq_, (size_t)(f_sh_ / 32) * sizeof(XBlock), s, px_take());
     std::swap(ra, rb);
     XlArgs dn;
     dn.xb = hq_;
-    dn.out = d_out_;
+    dn.out = d_out_ + (size_t)tp_rank_ * e_sh_;
     launch_exact_gemv(Ld.xdn, dn, XL_PLAIN, s);
+    if (tp_) coll_->all_gather(d_out_, (size_t)e_sh_ * sizeof(float), s, px_take());
     kernels_per_token_ += 6;
   }
   // the last layer's post-FFN norm + residual, then output_norm (model.cpp:915-924, 986)

@@ -179,6 +179,51 @@ def _tp8_ranks(g, body, tp=8, max_ctx=32):
     return out
 
 
+def test_27b_tp8_exact_matches_reference(monkeypatch):
+    """configs[4]'s model at full depth, a tp 8 group in EXACT mode (the exact-order engine, rows sharded): every
+    rank's teacher-forced top-16 logits are the REFERENCE's own bits at every step and its argmax the reference's
+    ids (VERDICT r4 #5: a bit-exact path for configs[4])."""
+    for k in ("LLMI_NO_PREFILL", "LLMI_NO_BLOCK", "LLMI_TP_HEAD_SHARD"):
+        monkeypatch.delenv(k, raising=False)
+    g, f = _fixture("g27b")
+    max_ctx = len(f["prompt"]) + len(f["tokens"]) + 8
+
+    def body(m):
+        assert m.get_info().exact_engine == 1
+        return _teacher_forced(m, f)
+
+    out = _tp8_ranks_exact(g, body, max_ctx)
+    for r, L in enumerate(out):
+        assert L.argmax(1).tolist() == f["tokens"].tolist(), f"rank {r} ids"
+        got = _top(L, f)
+        bad = np.nonzero((got.view(np.uint32) != f["top_val"].view(np.uint32)).any(1))[0]
+        assert bad.size == 0, f"rank {r}: steps {bad.tolist()[:8]} differ from the reference's bits"
+    print(f"27B tp8 exact: 8 ranks, {len(out[0])} steps, top-16 logits bit-identical to the reference")
+
+
+def _tp8_ranks_exact(g, body, max_ctx, tp=8):
+    from llm_inference_amd.model import Model, TPGroup
+    grp = TPGroup(tp)
+    out, errs = [None] * tp, []
+
+    def rank(r):
+        try:
+            m = Model(g, exact=True, max_ctx=max_ctx, tp_rank=r, tp_size=tp, tp_group=grp)
+            out[r] = body(m)
+            m.close()
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errs.append((r, e))
+
+    th = [threading.Thread(target=rank, args=(r,)) for r in range(tp)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(900)
+    grp.close()
+    assert not errs, errs
+    return out
+
+
 def test_27b_tp8_production_path(monkeypatch):
     """The tp 8 group on the production path (no switches: the ranks' batched prefill and default decode
     launches) against the REFERENCE's own 62-layer fixture: every rank's teacher-forced top-16 logits within

@@ -170,6 +170,49 @@ def test_exchange_ab_and_chunked_messages(exchange, monkeypatch):
         assert toks.tolist() == ref_toks.tolist()
 
 
+@pytest.mark.parametrize("cfg_name,tp", [("mini-4b", 2), ("mini-4b", 4), ("mini-1b", 2), ("mini-27b", 8)])
+def test_exact_sharded_bit_identical(cfg_name, tp):
+    """Exact mode on tensor-parallel ranks (row sharding is bit-exact): the
+    exact-order engine with o, gate/up and down row-sharded -- every row keeps the reference's accumulator chains
+    -- and the norms, q|k|v and the exact attention replicated; the slices all-gathered by the standalone push
+    exchange.  Logits and greedy ids bit-identical to the whole-model exact session (itself bit-identical to the
+    reference: tests/test_long_models.py)."""
+    from llm_inference_amd.model import Model, TPGroup
+    from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
+    cfg = CONFIGS[cfg_name]
+    g = build_gemma3_gguf(cfg, seed=41)
+    prompt = np.random.default_rng(43).integers(4, cfg.vocab, 9).astype(np.int32)
+    whole = Model(g, exact=True, max_ctx=64)
+    assert whole.get_info().exact_engine == 1
+    ref = whole.forward(prompt, 0)
+    ref_toks = whole.generate(int(np.argmax(ref)), len(prompt), 6)
+    whole.close()
+    grp = TPGroup(tp)
+    out, errs = [None] * tp, []
+
+    def rank(r):
+        try:
+            m = Model(g, exact=True, max_ctx=64, tp_rank=r, tp_size=tp, tp_group=grp)
+            info = m.get_info()
+            lg = m.forward(prompt, 0)
+            out[r] = (lg, m.generate(int(np.argmax(lg)), len(prompt), 6), info)
+            m.close()
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errs.append((r, e))
+
+    th = [threading.Thread(target=rank, args=(r,)) for r in range(tp)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(300)
+    grp.close()
+    assert not errs, errs
+    for r, (lg, toks, info) in enumerate(out):
+        assert info.exact_engine == 1 and info.tp_size == tp
+        np.testing.assert_array_equal(lg.view(np.uint32), ref.view(np.uint32), err_msg=f"rank {r}")
+        assert toks.tolist() == ref_toks.tolist(), f"rank {r} ids"
+
+
 def test_rccl_single_rank_in_graph(monkeypatch):
     """ncclAllGather captured into the per-token hipGraph (one-rank
     communicator): identical to the whole-model session."""
@@ -201,8 +244,10 @@ def test_tp_argument_errors():
         Model(g, tp_rank=0, tp_size=3, tp_group=grp)
     assert ei.value.status == "E_ARG"
     monkeypatch_env.undo()
-    with pytest.raises(LLMIError) as ei:  # sharding needs the fast fused kernels
-        Model(g, exact=True, tp_rank=0, tp_size=3, tp_group=grp)
+    with pytest.raises(LLMIError) as ei:  # exact mode shards rows, never heads
+        monkeypatch_env.setenv("LLMI_TP_HEAD_SHARD", "1")
+        Model(g, exact=True, tp_rank=1, tp_size=3, tp_group=grp)
+    monkeypatch_env.undo()
     assert ei.value.status == "E_ARG"
     with pytest.raises(LLMIError) as ei:
         Model(g, tp_rank=3, tp_size=3, tp_group=grp)
