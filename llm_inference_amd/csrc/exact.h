@@ -87,8 +87,10 @@ struct XAttnArgs {
   float* out = nullptr;      // [n_head][head_dim]
   XBlock* xq = nullptr;      // [n_head * head_dim / 32]
   float softcap = 0.0f;      // attention.logit_softcapping (model.cpp:511-513); 0: none
-  // the V cache transposed, [n_head_kv][head_dim][vt_stride] f16 (vt_stride % 8 == 0): the scores kernel appends
-  // the new key's column, the accumulate kernel reads 8 keys of its head dim per 16-B load
+  // the V cache in the accumulate kernel's read order (vt_stride % 32 == 0 keys per kv head): tiles of 64 head
+  // dims x 32 keys, [n_head_kv][head_dim / 64][vt_stride / 32][4 key octets][64 dims][8 keys] f16 (xa_vt_index):
+  // the scores kernel appends the new key's column, the accumulate kernel's 64 lanes (dims) read one key octet of
+  // a tile as one contiguous 1-KB load (16 B = 8 keys per lane)
   uint16_t* vt = nullptr;
   int vt_stride = 0;
 };

@@ -17,7 +17,8 @@ constexpr int XL_P = 8;   // groups (4 blocks each) per chunk of loads
 __device__ unsigned long long g_xl_trace[8192 * 8];
 #define XL_MARK(ph)                                                                                          \
   do {                                                                                                       \
-    if (threadIdx.x == 0 && blockIdx.x < 8192) g_xl_trace[blockIdx.x * 8 + (ph)] = __builtin_amdgcn_s_memtime(); \
+    const unsigned xl_b_ = blockIdx.y * gridDim.x + blockIdx.x;                                              \
+    if (threadIdx.x == 0 && xl_b_ < 8192) g_xl_trace[xl_b_ * 8 + (ph)] = __builtin_amdgcn_s_memtime();      \
   } while (0)
 #else
 #define XL_MARK(ph) \
@@ -70,6 +71,44 @@ __device__ __forceinline__ float xl_chain(const float* s, int n, float sum = 0.0
   return sum;
 }
 
+// The boundary walk of the speculative chains (wave 0): the true start of segment k is the chain value after
+// segment k - 1; if it is one of the segment's 32 candidates (s_base[k] + c) its end value is that candidate's
+// (s_e[k * 32 + c]), otherwise the segment is recomputed serially from it.  The walk over hits is unrolled with
+// the end values in registers; the first miss leaves it for a rolled loop with one serial chain in the code
+// (round 5: one inlined chain per boundary, 2 x 15 per launch in the 16-segment form, bloated the GEMV kernels)
+template <int K>
+__device__ __forceinline__ float xl_spec_walk(const float* s, int L, const float* s_e, const int* s_base,
+                                              unsigned* fallbacks) {
+  const int lane = threadIdx.x & 63;
+  float ev[K];
+#pragma unroll
+  for (int kk = 0; kk < K; kk++) ev[kk] = s_e[kk * 32 + (lane & 31)];
+  int bs[K];
+#pragma unroll
+  for (int kk = 0; kk < K; kk++) bs[kk] = s_base[kk];
+  float cur = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(ev[0])));
+  int miss = K;
+#pragma unroll
+  for (int kk = 1; kk < K; kk++) {
+    if (miss == K) {
+      const int i = __builtin_amdgcn_readfirstlane((int)__float_as_uint(cur) - bs[kk]);
+      if (i >= 0 && i < 32) cur = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ev[kk]), i));
+      else miss = kk;
+    }
+  }
+#pragma unroll 1
+  for (int kk = miss; kk < K; kk++) {  // (rare) from the first miss on: serial where the start is not a candidate
+    const int i = __builtin_amdgcn_readfirstlane((int)__float_as_uint(cur) - s_base[kk]);
+    if (kk > miss && i >= 0 && i < 32) {
+      cur = s_e[kk * 32 + i];
+    } else {
+      cur = xl_chain(s + kk * L, L, cur);
+      if (fallbacks && lane == 0) atomicAdd(fallbacks, 1u);
+    }
+  }
+  return cur;
+}
+
 // The same serial chain, its latency divided by speculation (every work-group thread calls it; the result is
 // bit-identical to xl_chain).  The n terms split into K = 2 NW segments of L; half-wave k runs segment k's chain
 // from 32 candidate start values at once -- the floats from 16 below to 15 above fl(P_k), P_k the f64 sum of the
@@ -104,29 +143,146 @@ __device__ __forceinline__ float xl_chain_spec(const float* s, int n, unsigned* 
   s_e[k * 32 + c] = e;
   if (c == 0) s_base[k] = base;
   __syncthreads();
-  if (wave == 0) {
-    float ev[K];
-#pragma unroll
-    for (int kk = 0; kk < K; kk++) ev[kk] = s_e[kk * 32 + (lane & 31)];
-    float cur = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(ev[0])));
-#pragma unroll
-    for (int kk = 1; kk < K; kk++) {
-      const int i = __builtin_amdgcn_readfirstlane((int)__float_as_uint(cur) - s_base[kk]);
-      if (i >= 0 && i < 32) cur = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ev[kk]), i));
-      else {  // the true start is not a candidate: this segment serially
-        cur = xl_chain(s + kk * L, L, cur);
-        if (fallbacks && lane == 0) atomicAdd(fallbacks, 1u);
-      }
-    }
-    if (lane == 0) s_res = cur;
-  }
+  if (wave == 0) s_res = xl_spec_walk<K>(s, L, s_e, s_base, fallbacks);
   __syncthreads();
   return s_res;
 }
 
-// the serial chain by the calling work-group: speculative where n splits into 2 NW segments of whole float4s
+// xl_chain for two start values at once over the same terms: two independent dependency chains interleaved, so
+// each step's latency is paid once for both (the same fma on the same value as xl_chain, per chain)
+__device__ __forceinline__ void xl_chain2(const float* s, int n, float& sa, float& sb) {
+  const float4* s4 = reinterpret_cast<const float4*>(s);
+  const int n4 = n >> 2;
+  float4 a[8], b[8];
+  auto ld = [&](float4 (&d)[8], int i) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) d[k] = s4[min(i + k, n4 - 1)];
+  };
+  auto eat = [&](const float4 (&d)[8], int i) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      if (i + k >= n4) break;  // wave-uniform
+      sa = fmaf(d[k].x, d[k].x, sa);
+      sb = fmaf(d[k].x, d[k].x, sb);
+      sa = fmaf(d[k].y, d[k].y, sa);
+      sb = fmaf(d[k].y, d[k].y, sb);
+      sa = fmaf(d[k].z, d[k].z, sa);
+      sb = fmaf(d[k].z, d[k].z, sb);
+      sa = fmaf(d[k].w, d[k].w, sa);
+      sb = fmaf(d[k].w, d[k].w, sb);
+    }
+  };
+  ld(a, 0);
+  for (int i = 0; i < n4; i += 16) {
+    ld(b, i + 8);
+    eat(a, i);
+    if (i + 8 >= n4) break;
+    ld(a, i + 16);
+    eat(b, i + 8);
+  }
+}
+
+// xl_chain_spec with twice the segments: K = 4 NW segments of n / K terms, a quarter-wave per segment whose lane c
+// runs the chains from the candidates base + c and base + 16 + c at once (xl_chain2) -- the same 32-candidate
+// window around fl(P_k) as xl_chain_spec, each chain half as long, the two chains of a lane sharing each step's
+// latency (round 5: the exact engine's norm chains, 6.6K -> see DESIGN.md section 4.4).  Bit-identical to
+// xl_chain: every step is the reference's fma on the reference's value; a boundary whose true start is not a
+// candidate runs its segment serially.
+template <int NW>
+__device__ __forceinline__ float xl_chain_spec2(const float* s, int n, unsigned* fallbacks = nullptr) {
+  constexpr int K = 4 * NW;
+  __shared__ double s_seg[K];
+  __shared__ float s_e[K * 32];
+  __shared__ int s_base[K];
+  __shared__ float s_res;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int k = t >> 4, c = lane & 15, L = n / K;
+  double p = 0.0;
+  for (int i = c; i < L; i += 16) {
+    const double v = (double)s[k * L + i];
+    p = fma(v, v, p);
+  }
+#pragma unroll
+  for (int m = 8; m >= 1; m >>= 1) p += __shfl_xor(p, m);
+  if (c == 0) s_seg[k] = p;
+  __syncthreads();
+  double pre = 0.0;
+  for (int j = 0; j < k; j++) pre += s_seg[j];
+  const int base = k == 0 ? 0 : max(0, (int)__float_as_uint((float)pre) - 16);
+  float ea = k == 0 ? 0.0f : __uint_as_float((uint32_t)(base + c));
+  float eb = k == 0 ? 0.0f : __uint_as_float((uint32_t)(base + 16 + c));
+  xl_chain2(s + k * L, L, ea, eb);
+  s_e[k * 32 + c] = ea;
+  s_e[k * 32 + 16 + c] = eb;
+  if (c == 0) s_base[k] = base;
+  __syncthreads();
+  if (wave == 0) s_res = xl_spec_walk<K>(s, L, s_e, s_base, fallbacks);
+  __syncthreads();
+  return s_res;
+}
+
+// f64 DPP step (both halves moved by the same row-local control)
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  const int lo = dpp_i<CTRL>(__double2loint(v)), hi = dpp_i<CTRL>(__double2hiint(v));
+  return __hiloint2double(hi, lo);
+}
+
+// xl_chain_spec with its fixed costs cut (round 5: 6.4K cycles per 2560-term chain of which the chain is ~2.6K,
+// scripts/dev/xl_bench): the segment's f64 sum of squares from float4 loads issued together (not one dependent
+// load per step) and reduced on DPP within each 16-lane row plus one cross-row shuffle (not five ds_bpermute
+// steps), and every wave walking the boundaries itself (no result broadcast).  n % (8 NW) == 0, n / (8 NW) <= 192
+// float4s per segment.  Bit-identical to xl_chain (the sums only place the candidate window).
+template <int NW>
+__device__ __forceinline__ float xl_chain_spec_fast(const float* s, int n) {
+  constexpr int K = 2 * NW, R = 6;
+  __shared__ double s_seg[K];
+  __shared__ float s_e[K * 32];
+  __shared__ int s_base[K];
+  const int t = threadIdx.x, lane = t & 63;
+  const int k = t >> 5, c = lane & 31, L = n / K, L4 = L / 4;
+  const float4* s4 = reinterpret_cast<const float4*>(s + k * L);
+  float4 v[R];
+#pragma unroll
+  for (int r = 0; r < R; r++) v[r] = s4[min(c + 32 * r, L4 - 1)];
+  double p0 = 0.0, p1 = 0.0;
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    if (c + 32 * r < L4) {
+      const double x = v[r].x, y = v[r].y, z = v[r].z, w = v[r].w;
+      p0 = fma(x, x, fma(y, y, p0));
+      p1 = fma(z, z, fma(w, w, p1));
+    }
+  }
+  double p = p0 + p1;
+  p += dpp_d<DPP_QUAD_1032>(p);
+  p += dpp_d<DPP_QUAD_2301>(p);
+  p += dpp_d<DPP_ROW_MIRROR>(p);
+  p += dpp_d<DPP_ROW_HALF_MIRROR>(p);
+  p += __shfl_xor(p, 16);
+  if (c == 0) s_seg[k] = p;
+  __syncthreads();
+  double pre = 0.0;
+#pragma unroll
+  for (int j = 0; j < K - 1; j++)
+    if (j < k) pre += s_seg[j];
+  const int base = k == 0 ? 0 : max(0, (int)__float_as_uint((float)pre) - 16);
+  const float x0 = k == 0 ? 0.0f : __uint_as_float((uint32_t)(base + c));
+  const float e = xl_chain(s + k * L, L, x0);
+  s_e[k * 32 + c] = e;
+  if (c == 0) s_base[k] = base;
+  __syncthreads();
+  const float res = xl_spec_walk<K>(s, L, s_e, s_base, nullptr);
+  __syncthreads();  // the LDS words are reused by the next call
+  return res;
+}
+
+// the serial chain by the calling work-group: speculative where n splits into 4 NW segments of whole float4s
 template <int NW>
 __device__ __forceinline__ float xl_sumsq(const float* s, int n, float* s_out) {
+  // (xl_chain_spec2 here: 14.40 / 19.94 us for the 4B qkv / gate_up launches vs 13.37 / 18.95 with xl_chain_spec,
+  // scripts/dev/xl_bench -- its halved chain is paid back in the 16-segment prefix and walk)
+  if (n % (8 * NW) == 0 && n / (8 * NW) <= 192) return xl_chain_spec_fast<NW>(s, n);
   if (n % (8 * NW) == 0) return xl_chain_spec<NW>(s, n);
   if ((threadIdx.x >> 6) == 0) {
     const float v = xl_chain(s, n);
@@ -234,9 +390,14 @@ __global__ __launch_bounds__(NW * 64) void exact_gemv_kernel(const uint4* __rest
   const int voq = row_ok ? (row * 4 + jj) * 16 : (1 << 30), vod = row_ok ? row * 8 : (1 << 30);
   const int sq = rows * 64, sd = rows * 8;
   XL_MARK(0);
+  // the weight stream is issued right AFTER the activation operands' first loads: loads return in issue order, so
+  // operands issued behind 32 KB per wave of weights waited for them (round 5: the operands-in-LDS phase of the
+  // PRE / GELU roles 3.2-3.9K cycles; scripts/dev/xl_bench)
   XlChunk ck[NCH];
+  auto issue_w = [&]() {
 #pragma unroll
-  for (int k = 0; k < NCH; k++) xl_load(ck[k], rq, rd, voq, vod, sq, sd, k * XL_P, ng);
+    for (int k = 0; k < NCH; k++) xl_load(ck[k], rq, rd, voq, vod, sq, sd, k * XL_P, ng);
+  };
 
   // ---- the activation: XE entries + scales in LDS.  Every global operand a thread needs is loaded in one
   // batch before any is used (a load per loop trip would pay one memory latency per trip) ----
@@ -252,6 +413,7 @@ __global__ __launch_bounds__(NW * 64) void exact_gemv_kernel(const uint4* __rest
         hi[k] = xg[3 * b + 1];
         d[k] = __uint_as_float(xg[3 * b + 2].x);
       }
+      if (b0 == 0) issue_w();
 #pragma unroll
       for (int k = 0; k < 4; k++) {
         const int b = b0 + k * T + t;
@@ -276,9 +438,26 @@ __global__ __launch_bounds__(NW * 64) void exact_gemv_kernel(const uint4* __rest
         float4 v[8];
 #pragma unroll
         for (int k = 0; k < 8; k++) v[k] = y4[min(i0 + k * T + t, n4 - 1)];
+        if (i0 == 0) issue_w();
 #pragma unroll
         for (int k = 0; k < 8; k++)
           if (i0 + k * T + t < n4) s_b4[i0 + k * T + t] = v[k];
+      }
+      __syncthreads();
+      // quantize_row_q8_0 (ops.cpp:116-139): a DPP quad per block, then the XE entries
+      for (int q0 = 0; q0 < nb * 4; q0 += T) {
+        const int qi = q0 + t, b = qi >> 2, sub = qi & 3;
+        if (b < nb) {  // whole quads (the quad's DPP steps stay inside it)
+          float v[8];
+#pragma unroll
+          for (int k = 0; k < 8; k++) v[k] = s_b[b * 32 + sub * 8 + k];
+          q8_block_quad(v, sub, s_xb + b);
+        }
+      }
+      __syncthreads();
+      for (int i = t; i < nb * 4; i += T) {
+        s_xe[i] = xe_entry(s_xb[i >> 2], i & 3);
+        if ((i & 3) == 0) s_xd[i >> 2] = s_xb[i >> 2].d;
       }
     } else {
       // thread t owns float4 i = t + k T (k < XL_K4) of every operand
@@ -286,7 +465,7 @@ __global__ __launch_bounds__(NW * 64) void exact_gemv_kernel(const uint4* __rest
       const float4* r4 = reinterpret_cast<const float4*>(a.resid_in);
       const float4* wp4 = reinterpret_cast<const float4*>(a.w_post);
       const float4* wn4 = reinterpret_cast<const float4*>(a.w_next);
-      float4 yv[XL_K4], hv[XL_K4], wv[XL_K4];
+      float4 yv[XL_K4], hv[XL_K4], wv[XL_K4], nv[XL_K4];
 #pragma unroll
       for (int k = 0; k < XL_K4; k++) {
         const int i = min(k * T + t, n4 - 1);
@@ -295,7 +474,9 @@ __global__ __launch_bounds__(NW * 64) void exact_gemv_kernel(const uint4* __rest
           yv[k] = y4[i];
           wv[k] = wp4[i];
         }
+        nv[k] = wn4[i];
       }
+      issue_w();
       auto own = [&](int k) { return k * T + t < n4; };
       if (a.y) {
 #pragma unroll
@@ -314,8 +495,6 @@ __global__ __launch_bounds__(NW * 64) void exact_gemv_kernel(const uint4* __rest
         }
       }
 #pragma unroll
-      for (int k = 0; k < XL_K4; k++) wv[k] = wn4[min(k * T + t, n4 - 1)];  // in flight behind the chain
-#pragma unroll
       for (int k = 0; k < XL_K4; k++)
         if (own(k)) {
           s_b4[k * T + t] = hv[k];
@@ -326,30 +505,34 @@ __global__ __launch_bounds__(NW * 64) void exact_gemv_kernel(const uint4* __rest
       XL_MARK(3);
       const float sc2 = xl_rms_scale(xl_sumsq<NW>(s_b, n, &s_scale[1]), n, a.eps);
       XL_MARK(4);
+      // run_norm: (scale * x) * w (model.cpp:352-357), then quantize_row_q8_0 (ops.cpp:116-139) straight from the
+      // registers: 8 consecutive lanes hold a block's 32 elements (a float4 each; blocks never straddle a k
+      // round: n4 and T are multiples of 8), amax over the octet and the per-slot quant sums (order-free,
+      // exact), the XE entries written by the octet's lanes 0-3 with the high words from lanes 4-7 (round 5:
+      // two LDS passes and two barriers fewer than staging x and the XBlocks in LDS)
 #pragma unroll
-      for (int k = 0; k < XL_K4; k++)
-        if (own(k)) {  // run_norm: (scale * x) * w (model.cpp:352-357)
-          const float4 x = make_float4((sc2 * hv[k].x) * wv[k].x, (sc2 * hv[k].y) * wv[k].y,
-                                       (sc2 * hv[k].z) * wv[k].z, (sc2 * hv[k].w) * wv[k].w);
-          s_b4[k * T + t] = x;
-          if (blockIdx.x == 0 && a.xn_out) reinterpret_cast<float4*>(a.xn_out)[k * T + t] = x;
-        }
-    }
-    __syncthreads();
-    // quantize_row_q8_0 (ops.cpp:116-139): a DPP quad per block
-    for (int q0 = 0; q0 < nb * 4; q0 += T) {
-      const int qi = q0 + t, b = qi >> 2, sub = qi & 3;
-      if (b < nb) {  // whole quads (the quad's DPP steps stay inside it)
-        float v[8];
-#pragma unroll
-        for (int k = 0; k < 8; k++) v[k] = s_b[b * 32 + sub * 8 + k];
-        q8_block_quad(v, sub, s_xb + b);
+      for (int k = 0; k < XL_K4; k++) {
+        const bool ok = own(k);  // (whole octets)
+        const float4 x = make_float4((sc2 * hv[k].x) * nv[k].x, (sc2 * hv[k].y) * nv[k].y,
+                                     (sc2 * hv[k].z) * nv[k].z, (sc2 * hv[k].w) * nv[k].w);
+        if (ok && blockIdx.x == 0 && a.xn_out) reinterpret_cast<float4*>(a.xn_out)[k * T + t] = x;
+        float amax = ok ? fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w))) : 0.0f;
+        amax = fmaxf(amax, __shfl_xor(amax, 1));
+        amax = fmaxf(amax, __shfl_xor(amax, 2));
+        amax = fmaxf(amax, __shfl_xor(amax, 4));
+        const float dd = amax / 127.0f;
+        const float id = dd != 0.0f ? 1.0f / dd : 0.0f;
+        const int q0 = nearest_int_fma(x.x, id), q1 = nearest_int_fma(x.y, id), q2 = nearest_int_fma(x.z, id),
+                  q3 = nearest_int_fma(x.w, id);
+        const uint32_t w = (uint32_t)(q0 & 0xFF) | ((uint32_t)(q1 & 0xFF) << 8) | ((uint32_t)(q2 & 0xFF) << 16) |
+                           ((uint32_t)(q3 & 0xFF) << 24);
+        const int sum = q0 + q1 + q2 + q3;
+        const uint32_t wh = __shfl_xor(w, 4);  // the octet's lanes 4-7: elements 16-31 of the block
+        const int sumh = __shfl_xor(sum, 4);
+        const int i4 = k * T + t, b = i4 >> 3, sl = i4 & 7;
+        if (ok && sl < 4) s_xe[b * 4 + sl] = make_int4((int)w, (int)wh, -8 * sum, -8 * sumh);
+        if (ok && sl == 0) s_xd[b] = h2f(f2h_ggml(dd));
       }
-    }
-    __syncthreads();
-    for (int i = t; i < nb * 4; i += T) {
-      s_xe[i] = xe_entry(s_xb[i >> 2], i & 3);
-      if ((i & 3) == 0) s_xd[i >> 2] = s_xb[i >> 2].d;
     }
   }
   __syncthreads();
@@ -385,6 +568,136 @@ __global__ __launch_bounds__(NW * 64) void exact_gemv_kernel(const uint4* __rest
     }
   } else {
     if (jl == 0 && row_ok) a.out[row] = r;
+  }
+}
+
+// The PLAIN role split into the parallel part and the chains (round 5: down 16.9 us on 160 single-wave
+// work-groups, each lane's 320-block loop one wave's VALU work on one SIMD of the CU).  Every accumulator update
+// is acc = fma(d_b, (float)isum_b, acc) in block order (ops.cpp:380-395); d_b and the integer dots isum_b depend
+// on nothing before them.  So a work-group of 4 waves owns 8 rows: per chunk of XS_CB blocks all 256 lanes compute
+// the dots (sdot4 of the row's nibbles with the XE entries, exact integers, stored as floats) and the products
+// d_b = f16(w.d) * x.d into LDS, then wave 0 -- lane R * 8 + k the accumulator k of row R -- runs the chains over
+// the chunk: one LDS read per four steps, one fma per step.  Bit-identical to exact_gemv_kernel<.., XL_PLAIN>:
+// the same values in the same fma chain, combined in the same order (hsum_float_8).
+constexpr int XS_ROWS = 8, XS_CB = 160, XS_LD = XS_CB + 4;  // rows per WG, blocks per chunk, LDS row stride
+constexpr int XS_IPL = XS_ROWS * (XS_CB / 4) * 4 / 256;      // items (group, row, slot) per lane per chunk
+
+__global__ __launch_bounds__(256) void exact_plain_split_kernel(const uint4* __restrict__ wq, const uint2* __restrict__ wd,
+                                                                int rows, int nb, XlArgs a) {
+  extern __shared__ int4 s_dyn[];
+  int4* s_xe = s_dyn;                                              // [nb][4]
+  float* s_xd = reinterpret_cast<float*>(s_dyn + (size_t)nb * 4);  // [nb]
+  __shared__ __attribute__((aligned(16))) float s_p[XS_ROWS * 8 * XS_LD];  // (float)isum per accumulator and block
+  __shared__ __attribute__((aligned(16))) float s_d[XS_ROWS * XS_LD];      // d per row and block
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int row0 = blockIdx.x * XS_ROWS, ng = nb >> 2;
+  const __amdgpu_buffer_rsrc_t rq = buf_rsrc(wq, (uint32_t)((size_t)ng * rows * 64));
+  const __amdgpu_buffer_rsrc_t rd = buf_rsrc(wd, (uint32_t)((size_t)ng * rows * 8));
+  XL_MARK(0);
+  // item m of this lane in a chunk: local group gl, row R, slot jj (32 consecutive lanes: one group's 8 rows x 4
+  // slots, 512 contiguous bytes of the XL stream)
+  uint4 qa[XS_IPL], qb[XS_IPL];  // two chunks' weights in flight: the next chunk's issued before this one is used
+  uint2 da[XS_IPL], db[XS_IPL];
+  auto issue = [&](uint4 (&q)[XS_IPL], uint2 (&dq)[XS_IPL], int c0) {
+#pragma unroll
+    for (int m = 0; m < XS_IPL; m++) {
+      const int i = t + 256 * m, jj = i & 3, R = (i >> 2) & 7, g = (c0 >> 2) + (i >> 5);
+      const bool in = g < ng;
+      q[m] = buf_ld16(rq, in ? ((g * rows + row0 + R) * 4 + jj) * 16 : (1 << 30), 0);
+      typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+      const u32x2_t v = __builtin_amdgcn_raw_buffer_load_b64(rd, in && jj == 0 ? (g * rows + row0 + R) * 8 : (1 << 30), 0, BUF_NT);
+      dq[m] = make_uint2(v.x, v.y);
+    }
+  };
+  {  // the activation's XE entries (as exact_gemv_kernel's PLAIN role), the first chunk's weights issued behind
+     // the activation's loads
+    const uint4* xg = reinterpret_cast<const uint4*>(a.xb);
+    for (int b0 = 0; b0 < nb; b0 += 4 * 256) {
+      uint4 lo[4], hi[4];
+      float d[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int b = min(b0 + k * 256 + t, nb - 1);
+        lo[k] = xg[3 * b];
+        hi[k] = xg[3 * b + 1];
+        d[k] = __uint_as_float(xg[3 * b + 2].x);
+      }
+      if (b0 == 0) issue(qa, da, 0);
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int b = b0 + k * 256 + t;
+        if (b < nb) {
+          const uint32_t l4[4] = {lo[k].x, lo[k].y, lo[k].z, lo[k].w}, h4[4] = {hi[k].x, hi[k].y, hi[k].z, hi[k].w};
+#pragma unroll
+          for (int j = 0; j < 4; j++)
+            s_xe[b * 4 + j] = make_int4((int)l4[j], (int)h4[j], -8 * sdot4((int)l4[j], 0x01010101, 0),
+                                        -8 * sdot4((int)h4[j], 0x01010101, 0));
+          s_xd[b] = d[k];
+        }
+      }
+    }
+  }
+  __syncthreads();
+  XL_MARK(1);
+  float acc = 0.0f;  // wave 0: accumulator k = lane & 7 of row lane >> 3
+  const float4* s_xd4 = reinterpret_cast<const float4*>(s_xd);
+  auto chunk = [&](const uint4 (&q)[XS_IPL], const uint2 (&dq)[XS_IPL], int c0) {
+    // the dots and products of this chunk
+#pragma unroll
+    for (int m = 0; m < XS_IPL; m++) {
+      const int i = t + 256 * m, jj = i & 3, R = (i >> 2) & 7, gl = i >> 5, g = (c0 >> 2) + gl;
+      if (g < ng) {
+        const uint32_t w4[4] = {q[m].x, q[m].y, q[m].z, q[m].w};
+        float4 pl, ph;
+        float* plv = reinterpret_cast<float*>(&pl);
+        float* phv = reinterpret_cast<float*>(&ph);
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const int4 x = s_xe[(4 * g + u) * 4 + jj];
+          plv[u] = (float)sdot4((int)(w4[u] & 0x0F0F0F0Fu), x.x, x.z);
+          phv[u] = (float)sdot4((int)((w4[u] >> 4) & 0x0F0F0F0Fu), x.y, x.w);
+        }
+        *reinterpret_cast<float4*>(s_p + (R * 8 + jj) * XS_LD + 4 * gl) = pl;
+        *reinterpret_cast<float4*>(s_p + (R * 8 + jj + 4) * XS_LD + 4 * gl) = ph;
+        if (jj == 0) {
+          const float4 xd = s_xd4[g];
+          *reinterpret_cast<float4*>(s_d + R * XS_LD + 4 * gl) =
+              make_float4(h2f((uint16_t)(dq[m].x & 0xFFFFu)) * xd.x, h2f((uint16_t)(dq[m].x >> 16)) * xd.y,
+                          h2f((uint16_t)(dq[m].y & 0xFFFFu)) * xd.z, h2f((uint16_t)(dq[m].y >> 16)) * xd.w);
+        }
+      }
+    }
+    __syncthreads();
+    if (wave == 0) {  // the chains over the chunk, block order
+      const int nbc = min(XS_CB, nb - c0);
+      const float4* p4 = reinterpret_cast<const float4*>(s_p + lane * XS_LD);
+      const float4* d4 = reinterpret_cast<const float4*>(s_d + (lane >> 3) * XS_LD);
+#pragma unroll 4
+      for (int b4 = 0; b4 < nbc / 4; b4++) {
+        const float4 p = p4[b4], d = d4[b4];
+        acc = fmaf(d.x, p.x, acc);
+        acc = fmaf(d.y, p.y, acc);
+        acc = fmaf(d.z, p.z, acc);
+        acc = fmaf(d.w, p.w, acc);
+      }
+    }
+    __syncthreads();  // the chunk's LDS is refilled next
+  };
+  for (int c0 = 0; c0 < nb; c0 += 2 * XS_CB) {
+    if (c0 + XS_CB < nb) issue(qb, db, c0 + XS_CB);
+    chunk(qa, da, c0);
+    if (c0 + XS_CB >= nb) break;
+    if (c0 + 2 * XS_CB < nb) issue(qa, da, c0 + 2 * XS_CB);
+    chunk(qb, db, c0 + XS_CB);
+  }
+  XL_MARK(2);
+  if (wave == 0) {
+    // hsum_float_8 (ops.cpp:324-330): ((a0 + a4) + (a2 + a6)) + ((a1 + a5) + (a3 + a7)), lanes R * 8 + k
+    const float t4 = acc + __shfl_xor(acc, 4);
+    const float u = t4 + __shfl_xor(t4, 2);
+    const float r = u + __shfl_xor(u, 1);
+    const int row = row0 + (lane >> 3);
+    if ((lane & 7) == 0 && row < rows) a.out[row] = r;
   }
 }
 
@@ -431,6 +744,13 @@ __global__ void xl_repack_kernel(const uint4* __restrict__ q0, const uint16_t* _
 // run_norm's serial chain (ops.cpp:28-43) on the row staged in s_x, (scale * x) * w, then NEOX rope at pos
 // (ops.cpp:67-95, the pinned build's contractions: v0 c - v1 s and v0 s + v1 c as one fma each) -- pairs
 // (i, i + HD / 2) sit in one lane
+// element (kv head hkv, head dim d, key j) of the tiled V copy (exact.h XAttnArgs::vt)
+template <int HD>
+__device__ __forceinline__ size_t xa_vt_index(int hkv, int d, int j, int stride) {
+  return (((size_t)hkv * (HD / 64) + d / 64) * (stride / 32) + j / 32) * 2048 + ((j & 31) >> 3) * 512 + (d & 63) * 8 +
+         (j & 7);
+}
+
 template <int HD>
 struct XaRow {
   static constexpr int EPL = HD / 64;
@@ -450,11 +770,12 @@ __device__ __forceinline__ void xa_row(const XaRow<HD>& in, const float (&c)[HD 
                                        const float (&sn)[HD / 128 > 0 ? HD / 128 : 1], double eps, float* s_x,
                                        float (&r)[HD / 64]) {
   constexpr int EPL = HD / 64, HALF = HD / 2;
+  static_assert(HD % 16 == 0, "xl_chain_spec2<1>: four segments of whole float4s");
   const int lane = threadIdx.x & 63;
 #pragma unroll
   for (int k = 0; k < EPL; k++) s_x[lane + 64 * k] = in.v[k];
   __syncthreads();
-  const float sc = xl_rms_scale(xl_chain(s_x, HD), HD, eps);
+  const float sc = xl_rms_scale(xl_chain_spec2<1>(s_x, HD), HD, eps);  // the serial chain (one wave), speculative
   float nv[EPL];
 #pragma unroll
   for (int k = 0; k < EPL; k++) nv[k] = (sc * in.v[k]) * in.w[k];
@@ -471,13 +792,14 @@ __device__ __forceinline__ void xa_row(const XaRow<HD>& in, const float (&c)[HD 
 template <int HD>
 __global__ __launch_bounds__(64) void xattn_scores_kernel(XAttnArgs a) {
   constexpr int EPL = HD / 64, CPL = EPL / 2;
-  __shared__ float s_x[HD];
+  __shared__ __attribute__((aligned(16))) float s_x[HD];
   __shared__ __attribute__((aligned(16))) double s_q[HD];
   __shared__ __attribute__((aligned(16))) uint16_t s_k[HD];
   const int h = blockIdx.x, split = blockIdx.y, lane = threadIdx.x;
   const int pos = *a.d_pos, n_keys = pos + 1;
   if (split * 64 >= n_keys) return;  // no key chunk for this work-group (whole wave)
   const int hkv = h / (a.n_head / a.n_head_kv);
+  XL_MARK(0);
   const bool own_pos = (pos >> 6) % XA_NSPLIT == split;
   // every global operand first: q row + weights, the rope entries, the new key's k / v rows, the first K rows
   const float* cs = a.rope_cs + (size_t)pos * HD;
@@ -504,6 +826,7 @@ __global__ __launch_bounds__(64) void xattn_scores_kernel(XAttnArgs a) {
   for (int u = 0; u < 8; u++) wa[u] = kr0[u];  // the first batch of the first key row (re-read for key pos)
   float r[EPL];
   xa_row<HD>(qr, c, sn, a.eps, s_x, r);
+  XL_MARK(1);
 #pragma unroll
   for (int k = 0; k < EPL; k++)  // model.cpp:767 scale, then the score's f16 query (model.cpp:507)
     s_q[lane + 64 * k] = (double)h2f(f2h_ggml(r[k] * a.attn_scale));
@@ -511,17 +834,18 @@ __global__ __launch_bounds__(64) void xattn_scores_kernel(XAttnArgs a) {
     xa_row<HD>(kr_, c, sn, a.eps, s_x, r);
     uint16_t* kc = a.k_cache + ((size_t)hkv * a.max_ctx + pos) * HD;
     uint16_t* vc = a.v_cache + ((size_t)hkv * a.max_ctx + pos) * HD;
-    uint16_t* vt = a.vt + (size_t)hkv * HD * a.vt_stride + pos;
 #pragma unroll
     for (int k = 0; k < EPL; k++) {
       const uint16_t kbits = f2h_ggml(r[k]), vbits = f2h_ggml(vrow[k]);
       s_k[lane + 64 * k] = kbits;
       kc[lane + 64 * k] = kbits;
       vc[lane + 64 * k] = vbits;
-      vt[(size_t)(lane + 64 * k) * a.vt_stride] = vbits;  // the transposed copy's column
+      a.vt[xa_vt_index<HD>(hkv, lane + 64 * k, pos, a.vt_stride)] = vbits;  // the tiled copy's column
     }
+    XL_MARK(2);
   }
   __syncthreads();
+  XL_MARK(3);
   double* sc_out = a.scores + (size_t)h * a.max_ctx;
   bool first = true;
   for (int cc = split; cc * 64 < n_keys; cc += XA_NSPLIT) {
@@ -564,6 +888,7 @@ __global__ __launch_bounds__(64) void xattn_scores_kernel(XAttnArgs a) {
     }
     sc_out[j] = acc;
   }
+  XL_MARK(4);
 }
 
 constexpr int XA_CH = 1024;  // accum: keys per chunk in LDS
@@ -642,6 +967,7 @@ __global__ __launch_bounds__((HD / 64 + 1) * 64) void xattn_accum_kernel(XAttnAr
   constexpr int NWV = HD / 64, T = (NWV + 1) * 64;
   constexpr int KPT = XA_CH / 256;  // keys per scan thread (threads 0..255)
   __shared__ double s_sc[XA_CH];
+  static_assert(XA_CH / 32 <= 32, "the chunk's max-move words: one per lane of a half-wave");
   __shared__ __attribute__((aligned(16))) float s_e[XA_CH];   // e per key
   __shared__ __attribute__((aligned(16))) float s_pe[XA_CH];  // pe per key
   __shared__ uint32_t s_up[XA_CH / 32];
@@ -655,15 +981,16 @@ __global__ __launch_bounds__((HD / 64 + 1) * 64) void xattn_accum_kernel(XAttnAr
   double run_max = -INFINITY;
   uint16_t v16 = 0;  // f32_to_f16(0.0f)
   float s_acc = 0.0f;
-  // this lane's head dim of the transposed V (wave < NWV), 16-B loads of 8 keys; loads past the context stay
-  // inside the row and are never summed
-  constexpr int NB = 4;
-  const uint4* vtp = reinterpret_cast<const uint4*>(a.vt + ((size_t)hkv * HD + min(wave, NWV - 1) * 64 + lane) * a.vt_stride);
-  const int q_last = a.vt_stride / 8 - 1;
+  // this lane's head dim of the tiled V (wave < NWV: dims 64 wave ..), a 32-key batch as 4 loads of 8 keys, each
+  // load one contiguous KB across the wave; tiles past the context stay inside the kv head and are never summed
+  constexpr int NB = 4;  // V batches in flight (the tiled loads: 6 measured the same as an all-L1 copy)
+  const uint4* vtp = reinterpret_cast<const uint4*>(a.vt + xa_vt_index<HD>(hkv, min(wave, NWV - 1) * 64 + lane, 0, a.vt_stride));
+  const int kb_last = a.vt_stride / 32 - 1;
   uint4 vb4[NB][4];
-  auto ld = [&](uint4 (&dst)[4], int jb) {
+  auto ld = [&](uint4 (&dst)[4], int jb) {  // jb % 32 == 0
+    const uint4* tp = vtp + (size_t)min(jb / 32, kb_last) * 256;  // a tile: 4 KB = 256 uint4
 #pragma unroll
-    for (int i = 0; i < 4; i++) dst[i] = vtp[min(jb / 8 + i, q_last)];
+    for (int i = 0; i < 4; i++) dst[i] = tp[i * 64];
   };
   if (t < 32) s_etab[t] = llmi_glibc::exp2f_tab(t);
   XL_MARK(0);
@@ -733,6 +1060,7 @@ __global__ __launch_bounds__((HD / 64 + 1) * 64) void xattn_accum_kernel(XAttnAr
         }
       };
       lde(eb[0], 0);
+      const uint32_t upv = s_up[lane & 31];  // batch i's max-move bits in lane i (read per batch by readlane)
       for (int j00 = 0; j00 < nk; j00 += 32 * NB) {
 #pragma unroll
         for (int b = 0; b < NB; b++) {
@@ -740,7 +1068,7 @@ __global__ __launch_bounds__((HD / 64 + 1) * 64) void xattn_accum_kernel(XAttnAr
           ld(vb4[(b + NB - 1) % NB], c0 + j0 + (NB - 1) * 32);  // into the slot summed in the previous batch
           if (j0 >= nk) continue;
           lde(eb[(b + 1) & 1], j0 + 32);
-          const uint32_t up = __builtin_amdgcn_readfirstlane(s_up[j0 >> 5]);
+          const uint32_t up = __builtin_amdgcn_readlane(upv, j0 >> 5);
           const int m = __builtin_amdgcn_readfirstlane(min(32, nk - j0));
           const float* e = eb[b & 1];
           if (up == 0 && m == 32) {
@@ -758,32 +1086,67 @@ __global__ __launch_bounds__((HD / 64 + 1) * 64) void xattn_accum_kernel(XAttnAr
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // no LDS wait inside the key steps
             uint32_t acc = v16;
 #pragma unroll
-            for (int u = 0; u < 32; u++) {
-              if (u < m) {  // wave-uniform
-                if (up & (1u << u)) acc = cvt_f16_rne((float)__builtin_bit_cast(_Float16, (uint16_t)acc) * pe[u]);
-                const uint4 w4 = vb4[b][u >> 3];
-                const uint32_t wv = ((u >> 1) & 3) == 0 ? w4.x : ((u >> 1) & 3) == 1 ? w4.y : ((u >> 1) & 3) == 2 ? w4.z : w4.w;
-                xa_mad1(acc, wv, e[u], u & 1);
+            for (int i = 0; i < 4; i++) {  // eight keys at a time: straight steps where the eight have no move
+              if (((up >> (8 * i)) & 0xFFu) == 0 && m >= 8 * (i + 1)) {
+                xa_mad8p(acc, vb4[b][i], e + 8 * i);
+                continue;
+              }
+#pragma unroll
+              for (int u = 8 * i; u < 8 * i + 8; u++) {
+                if (u < m) {  // wave-uniform
+                  if (up & (1u << u)) acc = cvt_f16_rne((float)__builtin_bit_cast(_Float16, (uint16_t)acc) * pe[u]);
+                  const uint4 w4 = vb4[b][u >> 3];
+                  const uint32_t wv = ((u >> 1) & 3) == 0 ? w4.x : ((u >> 1) & 3) == 1 ? w4.y : ((u >> 1) & 3) == 2 ? w4.z : w4.w;
+                  xa_mad1(acc, wv, e[u], u & 1);
+                }
               }
             }
             v16 = (uint16_t)acc;
           }
         }
       }
-    } else if (wave == NWV) {  // s_acc = s_acc * pe + e, keys in order (model.cpp:540), 32 keys' e / pe per read
-      for (int j0 = 0; j0 < nk; j0 += 32) {
-        float ev[32], pv[32];
+    } else if (wave == NWV) {  // s_acc = s_acc * pe + e, keys in order (model.cpp:540), 32 keys' e per read, the
+      // next batch's read in flight; pe is exactly 1 where the max did not move, so those steps are the add alone
+      // (s_acc * 1.0f == s_acc: round 5, the mul + add chain outlasted the V chains once their loads were tiled)
+      const uint32_t upv = s_up[lane & 31];
+      float eb[2][32];
+      auto lde = [&](float (&dst)[32], int j0) {
+        const float4* q4 = reinterpret_cast<const float4*>(s_e + min(j0, XA_CH - 32));
 #pragma unroll
         for (int u4 = 0; u4 < 8; u4++) {
-          const float4 q = reinterpret_cast<const float4*>(s_e + j0)[u4];
-          const float4 p = reinterpret_cast<const float4*>(s_pe + j0)[u4];
-          ev[4 * u4] = q.x; ev[4 * u4 + 1] = q.y; ev[4 * u4 + 2] = q.z; ev[4 * u4 + 3] = q.w;
-          pv[4 * u4] = p.x; pv[4 * u4 + 1] = p.y; pv[4 * u4 + 2] = p.z; pv[4 * u4 + 3] = p.w;
+          const float4 q = q4[u4];
+          dst[4 * u4] = q.x; dst[4 * u4 + 1] = q.y; dst[4 * u4 + 2] = q.z; dst[4 * u4 + 3] = q.w;
         }
-        const int m = min(32, nk - j0);
+      };
+      lde(eb[0], 0);
+      for (int j00 = 0; j00 < nk; j00 += 64) {
 #pragma unroll
-        for (int u = 0; u < 32; u++)
-          if (u < m) s_acc = s_acc * pv[u] + ev[u];
+        for (int b = 0; b < 2; b++) {
+          const int j0 = j00 + 32 * b;
+          if (j0 >= nk) break;
+          lde(eb[b ^ 1], j0 + 32);
+          const uint32_t up = __builtin_amdgcn_readlane(upv, j0 >> 5);
+          const int m = __builtin_amdgcn_readfirstlane(min(32, nk - j0));
+          const float* ev = eb[b];
+          if (up == 0 && m == 32) {
+#pragma unroll
+            for (int u = 0; u < 32; u++) s_acc = s_acc + ev[u];
+          } else {
+            float pv[32];
+#pragma unroll
+            for (int u4 = 0; u4 < 8; u4++) {
+              const float4 p = reinterpret_cast<const float4*>(s_pe + j0)[u4];
+              pv[4 * u4] = p.x; pv[4 * u4 + 1] = p.y; pv[4 * u4 + 2] = p.z; pv[4 * u4 + 3] = p.w;
+            }
+#pragma unroll
+            for (int u = 0; u < 32; u++) {
+              if (u < m) {
+                if (up & (1u << u)) s_acc = s_acc * pv[u];
+                s_acc = s_acc + ev[u];
+              }
+            }
+          }
+        }
       }
     }
     XL_MARK(3);
@@ -836,7 +1199,7 @@ __global__ __launch_bounds__(256) void chain_selftest_kernel(unsigned* out) {
     if (threadIdx.x == 0) s_ref = r;
   }
   __syncthreads();
-  const float v = xl_chain_spec<4>(s, 2560, out + 1);
+  const float v = (g & 1) ? xl_chain_spec2<4>(s, 2560, out + 1) : xl_chain_spec<4>(s, 2560, out + 1);
   if (threadIdx.x == 0 && __float_as_uint(v) != __float_as_uint(s_ref)) atomicAdd(out, 1u);
 }
 
@@ -938,7 +1301,10 @@ void launch_exact_gemv(const XlWeight& w, const XlArgs& a_in, int role, hipStrea
   switch (role) {
     // PLAIN / QUANT: one wave per work-group, few of them (a row group per wave), so the registers go to weight
     // chunks in flight: 4 x 8 groups (32 KB per wave)
-    case XL_PLAIN: go(exact_gemv_kernel<1, XL_PLAIN, 1, 4>, 1); break;  // (8 lanes per row: 19.3 vs 17.1 us for down)
+    case XL_PLAIN:  // the dots in parallel, the chains by one wave (exact_plain_split_kernel)
+      hipLaunchKernelGGL(exact_plain_split_kernel, dim3((unsigned)(w.rows / XS_ROWS)), dim3(256), xe, s, w.qs, w.d, w.rows,
+                         w.nb, a);
+      break;
     case XL_QUANT: go(exact_gemv_kernel<1, XL_QUANT, 1, 4>, 1); break;
     case XL_PRE:
       if (k3_2) go(exact_gemv_kernel<2, XL_PRE, 3, 2>, 2);

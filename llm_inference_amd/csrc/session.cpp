@@ -1602,8 +1602,8 @@ void Session::setup_xl() {
   for (const auto& l : L_) maxhd = std::max(maxhd, l.hd);
   xa_scores_ = dalloc<double>((size_t)hp_.n_head * max_ctx_);
   xa_xq_ = dalloc<XBlock>((size_t)hp_.n_head * maxhd / 32);
-  xa_vt_stride_ = (max_ctx_ + 7) / 8 * 8;
-  for (auto& l : L_) {  // the transposed V caches (zeroed: columns past the context are loaded, never summed)
+  xa_vt_stride_ = (max_ctx_ + 31) / 32 * 32;
+  for (auto& l : L_) {  // the tiled V caches (zeroed: columns past the context are loaded, never summed)
     const size_t n = (size_t)hp_.n_head_kv * l.hd * xa_vt_stride_;
     l.vt = dalloc<uint16_t>(n);
     LLMI_HIP(hipMemsetAsync(l.vt, 0, n * 2, stream_));

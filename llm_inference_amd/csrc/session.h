@@ -53,7 +53,7 @@ struct LayerDev {
   bool fused = false;           // every projection runs as gemv_q4_0_layer
   int hd = 0;
   uint16_t *kc = nullptr, *vc = nullptr;
-  uint16_t* vt = nullptr;      // exact-order engine: the V cache transposed ([kv][hd][xa_vt_stride_], exact.h)
+  uint16_t* vt = nullptr;      // exact-order engine: the V cache in 64-dim x 32-key tiles (exact.h)
   // Gemma-4
   bool has_kv = true;            // false: shared-KV layer, kc/vc alias layer kv_src's cache
   int kv_src = -1;
@@ -228,7 +228,7 @@ class Session {
   bool tp_rep_attn_ = false;  // tensor parallel: qkv + attention replicated on every rank (setup_tp)
   // fused exchanges (px.h): the producing launches push, the consuming ones read their mailbox -- push-exchange
   // collectives, the fused layer path, no dumps / traces (LLMI_TP_FUSED=0: standalone exchange launches)
-  int xa_vt_stride_ = 0;  // exact-order engine: keys per row of the transposed V caches (max_ctx rounded up to 8)
+  int xa_vt_stride_ = 0;  // exact-order engine: keys per kv head of the tiled V caches (max_ctx rounded up to 32)
   bool px_fused_ = false;
   PxLink* d_px_ = nullptr;  // the device-resident link (px_prepare, before the first recorded step)
   int px_k_ = 0;            // fused exchanges recorded since the last standalone one

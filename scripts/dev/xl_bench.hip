@@ -6,6 +6,10 @@
 //        scripts/dev/xl_bench.hip -o scripts/dev/xl_bench
 #include "../../llm_inference_amd/csrc/k_exact.hip"
 
+namespace llmi {
+void dev_free(void* p) { (void)hipFree(p); }  // (libllmi's graveyard-aware free, k_session.hip; not linked here)
+}  // namespace llmi
+
 #include <algorithm>
 #include <cstring>
 #include <cstdio>
@@ -364,8 +368,23 @@ static void plain_variant(const char* name, const XlWeight& w, const XlArgs& a) 
   });
 }
 
+// the split PLAIN kernel against exact_gemv_kernel's PLAIN role: bit-identical rows
+static void split_check(const char* name, const XlWeight& w, const XlArgs& a) {
+  std::vector<float> o1(w.rows), o2(w.rows);
+  const size_t lds = (size_t)w.nb * 64 + (size_t)w.nb * 4;
+  hipLaunchKernelGGL((exact_gemv_kernel<1, XL_PLAIN, 1, 4, 4>), dim3(w.rows / 16), dim3(64), lds, 0, w.qs, w.d, w.rows, w.nb, a);
+  LLMI_HIP(hipMemcpy(o1.data(), a.out, w.rows * 4, hipMemcpyDeviceToHost));
+  LLMI_HIP(hipMemset(a.out, 0, w.rows * 4));
+  launch_exact_gemv(w, a, XL_PLAIN, 0);
+  LLMI_HIP(hipMemcpy(o2.data(), a.out, w.rows * 4, hipMemcpyDeviceToHost));
+  int bad = 0;
+  for (int i = 0; i < w.rows; i++) bad += std::memcmp(&o1[i], &o2[i], 4) != 0;
+  std::printf("%s split vs serial-lane kernel: %d of %d rows differ (row 0: %.6g %.6g)\n", name, bad, w.rows, o1[0], o2[0]);
+}
+
 // the exact attention of one 4B layer at a given position (random K / V history, q|k|v row, norms, rope)
 static void phases(const char* what, int H);
+static void phases_quiet();
 static void attn_bench(std::mt19937& g, int pos) {
   const int H = 8, HK = 4, HD = 256, MC = 4096;
   XAttnArgs x;
@@ -389,12 +408,14 @@ static void attn_bench(std::mt19937& g, int pos) {
   LLMI_HIP(hipMemcpy(x.k_cache, hk.data(), kvn * 2, hipMemcpyHostToDevice));
   for (auto& v : hk) { const _Float16 hv = (_Float16)N(g); std::memcpy(&v, &hv, 2); }
   LLMI_HIP(hipMemcpy(x.v_cache, hk.data(), kvn * 2, hipMemcpyHostToDevice));
-  {  // the transposed copy the scores kernel maintains ([kv][hd][stride])
+  {  // the tiled copy the scores kernel maintains (exact.h XAttnArgs::vt)
     x.vt_stride = MC;
     std::vector<uint16_t> vt(kvn);
     for (int kv = 0; kv < HK; kv++)
       for (int p = 0; p < MC; p++)
-        for (int d = 0; d < HD; d++) vt[((size_t)kv * HD + d) * MC + p] = hk[((size_t)kv * MC + p) * HD + d];
+        for (int d = 0; d < HD; d++)
+          vt[(((size_t)kv * (HD / 64) + d / 64) * (MC / 32) + p / 32) * 2048 + ((p & 31) >> 3) * 512 + (d & 63) * 8 +
+             (p & 7)] = hk[((size_t)kv * MC + p) * HD + d];
     LLMI_HIP(hipMalloc(&x.vt, kvn * 2));
     LLMI_HIP(hipMemcpy(x.vt, vt.data(), kvn * 2, hipMemcpyHostToDevice));
   }
@@ -409,15 +430,16 @@ static void attn_bench(std::mt19937& g, int pos) {
   char nm[64];
   std::snprintf(nm, sizeof nm, "attn both (pos %d)", pos);
   time_launch(nm, [&] { launch_exact_attn(x, 0); });
+  phases_quiet();
   std::snprintf(nm, sizeof nm, "attn scores (pos %d)", pos);
   time_launch(nm, [&] { hipLaunchKernelGGL(xattn_scores_kernel<256>, dim3(H, XA_NSPLIT), dim3(64), 0, 0, x); });
+  phases("scores (all WGs)", H * XA_NSPLIT);
   std::snprintf(nm, sizeof nm, "attn accum (pos %d)", pos);
   time_launch(nm, [&] { hipLaunchKernelGGL(xattn_accum_kernel<256>, dim3(H), dim3(320), 0, 0, x); });
   phases("accum", H);
-  {  // the same launch with every Vt load inside one 1-KB run per wave (L1 hits, 8 lines per load): the V fetch
-     // shape's share of the accumulate
+  {  // the same launch with every V load inside the first 4-KB tile (L1 hits): the V fetch's share
     const int st = x.vt_stride;
-    x.vt_stride = 8;
+    x.vt_stride = 32;
     std::snprintf(nm, sizeof nm, "attn accum cheapV (pos %d)", pos);
     time_launch(nm, [&] { hipLaunchKernelGGL(xattn_accum_kernel<256>, dim3(H), dim3(320), 0, 0, x); });
     phases("accum cheapV", H);
@@ -430,6 +452,10 @@ static void attn_bench(std::mt19937& g, int pos) {
   phases("accum old", H);
 }
 
+static void phases_quiet() {
+  std::vector<unsigned long long> z(8192 * 8, 0);
+  LLMI_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_xl_trace), z.data(), z.size() * 8));
+}
 // phase clocks of the last launch, median over the heads' work-groups
 static void phases(const char* what, int H) {
   {
@@ -449,7 +475,104 @@ static void phases(const char* what, int H) {
   }
 }
 
+// dependent-chain latency of the accumulate's step shapes: one wave, 1024 steps, cycles per step
+__device__ unsigned long long g_lat[8];
+template <int MODE>
+__global__ __launch_bounds__(64) void lat_kernel(float e, uint32_t v) {
+  uint32_t a = threadIdx.x, b = threadIdx.x + 7;
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  for (int i = 0; i < 1024; i++) {
+    if (MODE == 0)
+      asm volatile("v_fma_mix_f32 %0, %1, %2, %0 op_sel_hi:[1,0,1]\n\tv_cvt_f16_f32_e32 %0, %0" : "+v"(a) : "v"(v), "v"(e));
+    else if (MODE == 1)
+      asm volatile("v_fma_f32 %0, %1, %2, %0" : "+v"(a) : "v"(v), "v"(e));
+    else if (MODE == 2)
+      asm volatile("v_cvt_f16_f32_e32 %0, %0" : "+v"(a));
+    else if (MODE == 3)
+      asm volatile("v_fma_mix_f32 %0, %2, %3, %0 op_sel_hi:[1,0,1]\n\tv_fma_mix_f32 %1, %2, %3, %1 op_sel_hi:[1,0,1]\n\t"
+                   "v_cvt_f16_f32_e32 %0, %0\n\tv_cvt_f16_f32_e32 %1, %1"
+                   : "+v"(a), "+v"(b) : "v"(v), "v"(e));
+    else if (MODE == 4)
+      asm volatile("v_fma_mix_f32 %0, %1, %2, %0 op_sel_hi:[1,0,1]" : "+v"(a) : "v"(v), "v"(e));
+    else if (MODE == 5)
+      asm volatile("v_fma_mixlo_f16 %0, %1, %2, %0 op_sel_hi:[1,0,1]" : "+v"(a) : "v"(v), "v"(e));
+  }
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) g_lat[MODE] = t1 - t0 + (a + b == 12345u ? 1 : 0);
+}
+static void latency_bench() {
+  const char* nm[] = {"fma_mix+cvt", "fma_f32", "cvt_f16", "2 chains fma_mix+cvt", "fma_mix", "fma_mixlo"};
+  hipLaunchKernelGGL(lat_kernel<0>, dim3(1), dim3(64), 0, 0, 0.5f, 0x3c00u);
+  hipLaunchKernelGGL(lat_kernel<1>, dim3(1), dim3(64), 0, 0, 0.5f, 0x3c00u);
+  hipLaunchKernelGGL(lat_kernel<2>, dim3(1), dim3(64), 0, 0, 0.5f, 0x3c00u);
+  hipLaunchKernelGGL(lat_kernel<3>, dim3(1), dim3(64), 0, 0, 0.5f, 0x3c00u);
+  hipLaunchKernelGGL(lat_kernel<4>, dim3(1), dim3(64), 0, 0, 0.5f, 0x3c00u);
+  hipLaunchKernelGGL(lat_kernel<5>, dim3(1), dim3(64), 0, 0, 0.5f, 0x3c00u);
+  LLMI_HIP(hipDeviceSynchronize());
+  unsigned long long l[8];
+  LLMI_HIP(hipMemcpyFromSymbol(l, HIP_SYMBOL(g_lat), sizeof l));
+  for (int m = 0; m < 6; m++) std::printf("latency %-22s %6.2f cycles/step\n", nm[m], l[m] / 1024.0);
+}
+
+// the norm chain variants alone: 256 threads, 2560 random floats per work-group in LDS, cycles + fallbacks
+template <int V>
+__global__ __launch_bounds__(256) void sumsq_kernel(const float* x, unsigned long long* cyc, float* res, unsigned* fb) {
+  __shared__ __attribute__((aligned(16))) float s[2560];
+  __shared__ float s_out;
+  for (int i = threadIdx.x; i < 2560; i += 256) s[i] = x[(size_t)blockIdx.x * 2560 + i];
+  __syncthreads();
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  float r;
+  if (V == 0) r = xl_chain_spec<4>(s, 2560, fb);
+  else if (V == 1) r = xl_chain_spec2<4>(s, 2560, fb);
+  else if (V == 3) r = xl_chain_spec_fast<4>(s, 2560);
+  else {
+    if (threadIdx.x < 64) { const float v = xl_chain(s, 2560); if (threadIdx.x == 0) s_out = v; }
+    __syncthreads();
+    r = s_out;
+  }
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) { cyc[blockIdx.x] = t1 - t0; res[blockIdx.x] = r; }
+}
+static void sumsq_bench(std::mt19937& g) {
+  const int NB = 64;
+  float* x = rand_vec(NB * 2560, g, 1.0f);
+  unsigned long long* cyc; float* res; unsigned* fb;
+  LLMI_HIP(hipMalloc(&cyc, NB * 8)); LLMI_HIP(hipMalloc(&res, NB * 4)); LLMI_HIP(hipMalloc(&fb, 4));
+  std::vector<float> r[4];
+  const char* nm[] = {"spec<4> (8 segs)", "spec2<4> (16 segs x 2)", "serial", "spec_fast<4> (8 segs)"};
+  for (int v = 0; v < 4; v++) {
+    LLMI_HIP(hipMemset(fb, 0, 4));
+    for (int rep = 0; rep < 2; rep++) {
+      if (v == 0) hipLaunchKernelGGL(sumsq_kernel<0>, dim3(NB), dim3(256), 0, 0, x, cyc, res, fb);
+      if (v == 1) hipLaunchKernelGGL(sumsq_kernel<1>, dim3(NB), dim3(256), 0, 0, x, cyc, res, fb);
+      if (v == 2) hipLaunchKernelGGL(sumsq_kernel<2>, dim3(NB), dim3(256), 0, 0, x, cyc, res, fb);
+      if (v == 3) hipLaunchKernelGGL(sumsq_kernel<3>, dim3(NB), dim3(256), 0, 0, x, cyc, res, fb);
+    }
+    LLMI_HIP(hipDeviceSynchronize());
+    std::vector<unsigned long long> c(NB);
+    r[v].resize(NB);
+    unsigned f;
+    LLMI_HIP(hipMemcpy(c.data(), cyc, NB * 8, hipMemcpyDeviceToHost));
+    LLMI_HIP(hipMemcpy(r[v].data(), res, NB * 4, hipMemcpyDeviceToHost));
+    LLMI_HIP(hipMemcpy(&f, fb, 4, hipMemcpyDeviceToHost));
+    std::sort(c.begin(), c.end());
+    std::printf("sumsq %-24s median %llu cycles (min %llu max %llu), fallbacks %u over 2 x %d chains\n", nm[v], c[NB / 2],
+                c[0], c[NB - 1], f, NB);
+  }
+  int bad = 0;
+  for (int i = 0; i < NB; i++)
+    bad += (std::memcmp(&r[0][i], &r[2][i], 4) != 0) + (std::memcmp(&r[1][i], &r[2][i], 4) != 0) +
+           (std::memcmp(&r[3][i], &r[2][i], 4) != 0);
+  std::printf("sumsq variants vs serial: %d mismatches\n", bad);
+}
+
 int main() {
+  latency_bench();
+  {
+    std::mt19937 g0(7);
+    sumsq_bench(g0);
+  }
   std::mt19937 g(1);
   const int E = 2560, F = 10240;
   DevWeight wq = rand_q4(4096, E, g), wgate = rand_q4(F, E, g), wup = rand_q4(F, E, g), wd = rand_q4(E, F, g);
@@ -474,6 +597,17 @@ int main() {
   dn.xb = hq; dn.out = out;
   run("down", xd, dn, XL_PLAIN);
   plain_variant<4, 4>("down LPR4 NCH4", xd, dn);
+  split_check("down", xd, dn);
+  {  // the o projection's shape (2560 x 2048)
+    DevWeight wo = rand_q4(E, 2048, g);
+    XlSrc so; so.w[so.n++] = &wo;
+    XlWeight xo = make_xl_weight(so, 0);
+    XlArgs oa;
+    oa.xb = hq; oa.out = out;
+    run("o", xo, oa, XL_PLAIN);
+    plain_variant<4, 4>("o LPR4 NCH4 (old)", xo, oa);
+    split_check("o", xo, oa);
+  }
   plain_variant<8, 4>("down LPR8 NCH4", xd, dn);
   plain_variant<8, 2>("down LPR8 NCH2", xd, dn);
   attn_bench(g, 1);

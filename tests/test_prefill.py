@@ -182,8 +182,10 @@ def test_kquant_batched_prefill(monkeypatch, oracle, mode):
     cond = float(np.abs(ref - ref64).max())
     d = float(np.abs(lp - ll).max())
     dp, dl = float(np.abs(lp - ref).max()), float(np.abs(ll - ref).max())
+    ep, el = float(np.abs(lp - ref64).max()), float(np.abs(ll - ref64).max())
     print(f"mini-4b Q4_K_M n={len(prompt)}: |reference - f64-attention reference| {cond:.3g}; |{mode} batched "
-          f"prefill - reference| {dp:.3g}; |token loop - reference| {dl:.3g}; |batched - token loop| {d:.3g}")
+          f"prefill - reference| {dp:.3g} (- f64-attention reference {ep:.3g}); |token loop - reference| {dl:.3g} "
+          f"(- f64-attention reference {el:.3g}); |batched - token loop| {d:.3g}")
     assert dl <= FAST_VS_REF + cond
     if mode == "int8":
         assert dp <= FAST_VS_REF + cond
