@@ -198,7 +198,8 @@ def parity(ref, got) -> dict:
     same_bits = [bool(np.array_equal(r.view(np.uint32), x.view(np.uint32))) for r, x in zip(ref, got)]
     return {"positions": len(ref), "logits_bit_identical": int(sum(same_bits)),
             "argmax_identical": int(sum(int(np.argmax(r)) == int(np.argmax(x)) for r, x in zip(ref, got))),
-            "max_abs_logit_diff": float(np.abs(ref - got).max())}
+            "max_abs_logit_diff": float(np.abs(ref - got).max()),
+            "max_abs_reference_logit": float(np.abs(ref).max())}
 
 
 def cpu_baseline(g, cfg, n_decode: int, gpu_ids=None, mean_ctx=None, ctx_prompt=None):

@@ -17,6 +17,7 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 FAST_VS_REF = 6e-2
+KQ_VS_REF64 = 0.25  # test_kquant_batched_prefill: the K-quant paths vs the f64-attention reference
 
 
 def _model(g, monkeypatch, no_prefill=False, chunk=None, max_ctx=1024):
@@ -158,10 +159,14 @@ def test_kquant_batched_prefill(monkeypatch, oracle, mode):
     a defect of either path.  Over other seeds / lengths (the same script) that sensitivity is 0.04-0.12 and
     every path is within 0.16 of the oracle.
 
-    Stated bound (the fast budget of tests/test_hip_model.py widened by the input's measured conditioning):
-    |device - reference| <= FAST_VS_REF + |reference - reference with f64 attention| for each path, the same
-    argmax, the same greedy continuation; chunk-exact.  f16 (opt-in LLMI_PREFILL_F16=1: f16 activations,
-    GEMM v6 on the kq weights): the same ids and chunk-exactness; its gap is reported."""
+    Stated bounds: (1) |device - reference| <= FAST_VS_REF + |reference - reference with f64 attention| for each
+    path (the fast budget of tests/test_hip_model.py widened by the input's measured conditioning); (2) the
+    tight one, against the well-conditioned f64-attention reference: |device - f64-attention reference| <=
+    KQ_VS_REF64 = 0.25 for the token loop and the int8 batched prefill (measured round 5: 0.185 and 0.087, while
+    both sit 0.42 / 0.52 from the reference itself -- the spread is the reference's f16 attention, not the
+    device); the same argmax, the same greedy continuation; chunk-exact.  f16 (opt-in LLMI_PREFILL_F16=1: f16
+    activations, GEMM v6 on the kq weights; 0.47 from the f64-attention reference, 0.19 from the reference): the
+    same ids and chunk-exactness; its gap is reported."""
     n_prompt = 150
     if mode == "f16":
         monkeypatch.setenv("LLMI_PREFILL_F16", "1")
@@ -187,8 +192,10 @@ def test_kquant_batched_prefill(monkeypatch, oracle, mode):
           f"prefill - reference| {dp:.3g} (- f64-attention reference {ep:.3g}); |token loop - reference| {dl:.3g} "
           f"(- f64-attention reference {el:.3g}); |batched - token loop| {d:.3g}")
     assert dl <= FAST_VS_REF + cond
+    assert el <= KQ_VS_REF64
     if mode == "int8":
         assert dp <= FAST_VS_REF + cond
+        assert ep <= KQ_VS_REF64
     assert int(np.argmax(lp)) == int(np.argmax(ll)) == int(np.argmax(ref))
     assert ids_p.tolist() == ids_l.tolist()
     np.testing.assert_array_equal(_model(g, monkeypatch, chunk=41).forward(prompt, 0), lp)
