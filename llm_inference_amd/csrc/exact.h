@@ -93,6 +93,9 @@ struct XAttnArgs {
   // a tile as one contiguous 1-KB load (16 B = 8 keys per lane)
   uint16_t* vt = nullptr;
   int vt_stride = 0;
+  // per key [n_head_kv][max_ctx]: (min over its nonzero elements of max(f16 exponent field, 1)) << 16 | max |k| as
+  // f16 bits, written with the K row; 0 = unknown (the score then takes the serial chain)
+  uint32_t* kmeta = nullptr;
 };
 bool exact_attn_supported(int head_dim, int n_head, int n_head_kv);
 void launch_exact_attn(const XAttnArgs& a, hipStream_t s);

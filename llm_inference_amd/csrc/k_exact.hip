@@ -744,6 +744,36 @@ __global__ void xl_repack_kernel(const uint4* __restrict__ q0, const uint16_t* _
 // run_norm's serial chain (ops.cpp:28-43) on the row staged in s_x, (scale * x) * w, then NEOX rope at pos
 // (ops.cpp:67-95, the pinned build's contractions: v0 c - v1 s and v0 s + v1 c as one fma each) -- pairs
 // (i, i + HD / 2) sit in one lane
+// f16 bits -> max(exponent field, 1) for a nonzero value (its ulp is 2^(code - 25)), 31 for +-0
+__device__ __forceinline__ int xa_exp_code(uint16_t b) {
+  return (b & 0x7FFF) == 0 ? 31 : max((b >> 10) & 0x1F, 1);
+}
+__device__ __forceinline__ int xa_wave_min(int v) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) v = min(v, __shfl_xor(v, o));
+  return v;
+}
+__device__ __forceinline__ int xa_wave_max(int v) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) v = max(v, __shfl_xor(v, o));
+  return v;
+}
+__device__ __forceinline__ double xa_wave_sum_d(double v) {  // (a bound: any order)
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) v += __shfl_xor(v, o);
+  return v;
+}
+// No add of the score chain rounds: every product q_i k_i (exact in f32) is a multiple of 2^m, m = (qcode - 25) +
+// (kcode - 25), and every partial sum is at most |q|_1 max|k| < 2^(m + 52) in magnitude, so each is a multiple of
+// 2^m below 2^(m + 53): representable, in any order.  kmeta 0 (unknown key) or a non-finite bound: false.
+__device__ __forceinline__ bool xa_exact_ok(int qcode, double qn1, uint32_t kmeta) {
+  const int kcode = (int)(kmeta >> 16);
+  if (kcode == 0) return false;
+  const int m = (qcode - 25) + (kcode - 25);
+  const double bound = qn1 * (double)h2f((uint16_t)(kmeta & 0x7FFFu));
+  return bound < __longlong_as_double((long long)(m + 52 + 1023) << 52);
+}
+
 // element (kv head hkv, head dim d, key j) of the tiled V copy (exact.h XAttnArgs::vt)
 template <int HD>
 __device__ __forceinline__ size_t xa_vt_index(int hkv, int d, int j, int stride) {
@@ -791,17 +821,21 @@ __device__ __forceinline__ void xa_row(const XaRow<HD>& in, const float (&c)[HD 
 
 template <int HD>
 __global__ __launch_bounds__(64) void xattn_scores_kernel(XAttnArgs a) {
-  constexpr int EPL = HD / 64, CPL = EPL / 2;
+  constexpr int EPL = HD / 64, CPL = EPL / 2, QW = HD / 32;  // QW: 16-B words of a quarter row
+  constexpr int KPC = 16;                                    // keys per chunk: 4 lanes (row quarters) per key
   __shared__ __attribute__((aligned(16))) float s_x[HD];
   __shared__ __attribute__((aligned(16))) double s_q[HD];
   __shared__ __attribute__((aligned(16))) uint16_t s_k[HD];
   const int h = blockIdx.x, split = blockIdx.y, lane = threadIdx.x;
-  const int pos = *a.d_pos, n_keys = pos + 1;
-  if (split * 64 >= n_keys) return;  // no key chunk for this work-group (whole wave)
+  const int pos = *a.d_pos;
+  // work-groups split < XA_NSPLIT: the keys before pos in chunks of 16, chunk split, split + XA_NSPLIT, ..; the
+  // last one (split == XA_NSPLIT): the new key -- k norm + rope, the K / V append and its score
+  const bool pos_wg = split == XA_NSPLIT;
+  if (!pos_wg && split * KPC >= pos) return;  // no key chunk for this work-group (whole wave)
   const int hkv = h / (a.n_head / a.n_head_kv);
+  const int kl = lane >> 2, qt = lane & 3;  // key of the chunk, quarter of its row
   XL_MARK(0);
-  const bool own_pos = (pos >> 6) % XA_NSPLIT == split;
-  // every global operand first: q row + weights, the rope entries, the new key's k / v rows, the first K rows
+  // every global operand first: q row + weights, the rope entries, the new key's k / v rows or the first K rows
   const float* cs = a.rope_cs + (size_t)pos * HD;
   float c[CPL], sn[CPL];
 #pragma unroll
@@ -813,24 +847,42 @@ __global__ __launch_bounds__(64) void xattn_scores_kernel(XAttnArgs a) {
   XaRow<HD> qr, kr_;
   xa_load<HD>(qr, a.qkv + (size_t)h * HD, a.q_norm_w);
   float vrow[EPL];
-  if (own_pos) {
+  const uint16_t* kb = a.k_cache + (size_t)hkv * a.max_ctx * HD;
+  const uint32_t* km = a.kmeta ? a.kmeta + (size_t)hkv * a.max_ctx : nullptr;
+  uint4 wa[QW];
+  uint32_t meta = 0u;
+  auto ld_quarter = [&](uint4 (&w)[QW], int j) {
+    const uint4* src = reinterpret_cast<const uint4*>(kb + (size_t)j * HD) + qt * QW;
+#pragma unroll
+    for (int u = 0; u < QW; u++) w[u] = src[u];
+  };
+  if (pos_wg) {
     xa_load<HD>(kr_, a.qkv + a.k_off + (size_t)hkv * HD, a.k_norm_w);
 #pragma unroll
     for (int k = 0; k < EPL; k++) vrow[k] = a.qkv[a.v_off + (size_t)hkv * HD + lane + 64 * k];
+  } else {
+    const int j1 = min(split * KPC + kl, pos - 1);
+    ld_quarter(wa, j1);
+    meta = km ? km[j1] : 0u;
   }
-  const uint16_t* kb = a.k_cache + (size_t)hkv * a.max_ctx * HD;
-  const int j1 = split * 64 + lane;  // this lane's first key
-  const uint4* kr0 = reinterpret_cast<const uint4*>(kb + (size_t)min(j1, pos) * HD);
-  uint4 wa[8];
-#pragma unroll
-  for (int u = 0; u < 8; u++) wa[u] = kr0[u];  // the first batch of the first key row (re-read for key pos)
   float r[EPL];
   xa_row<HD>(qr, c, sn, a.eps, s_x, r);
   XL_MARK(1);
+  // the query's exactness words (xa_exact_ok): min over its nonzero elements of max(exponent field, 1), |q|_1
+  int qcode = 31;
+  double qn1 = 0.0;
 #pragma unroll
-  for (int k = 0; k < EPL; k++)  // model.cpp:767 scale, then the score's f16 query (model.cpp:507)
-    s_q[lane + 64 * k] = (double)h2f(f2h_ggml(r[k] * a.attn_scale));
-  if (own_pos) {  // the new key: k norm + rope, K and V rows appended (model.cpp:440-474)
+  for (int k = 0; k < EPL; k++) {  // model.cpp:767 scale, then the score's f16 query (model.cpp:507)
+    const uint16_t qb = f2h_ggml(r[k] * a.attn_scale);
+    s_q[lane + 64 * k] = (double)h2f(qb);
+    qcode = min(qcode, xa_exp_code(qb));
+    qn1 += fabs((double)h2f(qb));
+  }
+  qcode = xa_wave_min(qcode);
+  qn1 = xa_wave_sum_d(qn1);
+  int kcode_new = 31;
+  uint32_t kmag_new = 0;
+  if (pos_wg) {  // the new key: k norm + rope, K and V rows appended (model.cpp:440-474)
     xa_row<HD>(kr_, c, sn, a.eps, s_x, r);
     uint16_t* kc = a.k_cache + ((size_t)hkv * a.max_ctx + pos) * HD;
     uint16_t* vc = a.v_cache + ((size_t)hkv * a.max_ctx + pos) * HD;
@@ -841,52 +893,87 @@ __global__ __launch_bounds__(64) void xattn_scores_kernel(XAttnArgs a) {
       kc[lane + 64 * k] = kbits;
       vc[lane + 64 * k] = vbits;
       a.vt[xa_vt_index<HD>(hkv, lane + 64 * k, pos, a.vt_stride)] = vbits;  // the tiled copy's column
+      kcode_new = min(kcode_new, xa_exp_code(kbits));
+      kmag_new = max(kmag_new, (uint32_t)(kbits & 0x7FFFu));
     }
+    kcode_new = xa_wave_min(kcode_new);
+    kmag_new = (uint32_t)xa_wave_max((int)kmag_new);
+    if (lane == 0 && km) a.kmeta[(size_t)hkv * a.max_ctx + pos] = ((uint32_t)kcode_new << 16) | kmag_new;
     XL_MARK(2);
   }
   __syncthreads();
   XL_MARK(3);
   double* sc_out = a.scores + (size_t)h * a.max_ctx;
-  bool first = true;
-  for (int cc = split; cc * 64 < n_keys; cc += XA_NSPLIT) {
-    const int j = cc * 64 + lane;
-    if (j >= n_keys) break;
-    const uint4* kr = reinterpret_cast<const uint4*>(j == pos ? s_k : kb + (size_t)j * HD);
-    if (!first || j == pos) {
-#pragma unroll
-      for (int u = 0; u < 8; u++) wa[u] = kr[u];
-    }
-    first = false;
+  // score = sum_i (double)(f16(k_i) * f16(q_i)), i in order, from 0.0 (model.cpp:504-509): the f32 product of two
+  // f16 values is exact, so one f64 fma per element is the reference's rounding.  Where xa_exact_ok holds no add
+  // of that chain rounds, so the row's four quarters are summed by four lanes and combined (the same bits); the
+  // f64 element step costs ~25 cycles of one wave's issue (round 5, scripts/dev/xl_bench), so a key per lane was a
+  // 6.4K-cycle loop.  Otherwise the serial chain, by one lane.
+  auto serial = [&](const uint16_t* row) __attribute__((always_inline)) {
+    const uint4* r4 = reinterpret_cast<const uint4*>(row);
     double acc = 0.0;
-    // score += (double)(f16(k_i) * f16(q_i)), i in order (model.cpp:504-509); the f32 product of two f16 values
-    // is exact, so one f64 fma per element is the same rounding as the reference's add.  The row streams in
-    // batches of 64 elements, the next batch loaded before the current one is summed.
-    uint4 wb[8];
-    auto eat = [&](const uint4 (&w)[8], int i0) {
-      const double2* q2 = reinterpret_cast<const double2*>(s_q + i0 * 8);
+#pragma unroll 1
+    for (int i0 = 0; i0 < HD / 8; i0 += 8) {
+      uint4 w[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) w[u] = r4[i0 + u];
 #pragma unroll
       for (int u = 0; u < 8; u++) {
         const uint32_t ww[4] = {w[u].x, w[u].y, w[u].z, w[u].w};
 #pragma unroll
         for (int e = 0; e < 4; e++) {
-          const double2 q = q2[u * 4 + e];
-          acc = fma((double)h2f((uint16_t)(ww[e] & 0xFFFF)), q.x, acc);
-          acc = fma((double)h2f((uint16_t)(ww[e] >> 16)), q.y, acc);
+          const int i = (i0 + u) * 8 + 2 * e;
+          acc = fma((double)h2f((uint16_t)(ww[e] & 0xFFFF)), s_q[i], acc);
+          acc = fma((double)h2f((uint16_t)(ww[e] >> 16)), s_q[i + 1], acc);
         }
       }
-    };
-#pragma unroll 1
-    for (int i0 = 0; i0 < HD / 8; i0 += 16) {
-#pragma unroll
-      for (int u = 0; u < 8; u++) wb[u] = kr[i0 + 8 + u];
-      eat(wa, i0);
-      if (i0 + 16 < HD / 8) {
-#pragma unroll
-        for (int u = 0; u < 8; u++) wa[u] = kr[i0 + 16 + u];
-      }
-      eat(wb, i0 + 8);
     }
-    sc_out[j] = acc;
+    return acc;
+  };
+  if (pos_wg) {
+    if (xa_exact_ok(qcode, qn1, ((uint32_t)kcode_new << 16) | kmag_new)) {  // (uniform) elements lane + 64 k
+      double p = 0.0;
+#pragma unroll
+      for (int k = 0; k < EPL; k++) p = fma((double)h2f(s_k[lane + 64 * k]), s_q[lane + 64 * k], p);
+      p = xa_wave_sum_d(p);
+      if (lane == 0) sc_out[pos] = p;
+    } else if (lane == 0) {
+      sc_out[pos] = serial(s_k);
+    }
+  } else {
+    const double2* q2 = reinterpret_cast<const double2*>(s_q + qt * (HD / 4));
+    for (int cc = split; cc * KPC < pos; cc += XA_NSPLIT) {
+      const int j = cc * KPC + kl;
+      const bool valid = j < pos;
+      uint4 wn[QW];
+      uint32_t mn = 0u;
+      const bool more = (cc + XA_NSPLIT) * KPC < pos;  // (uniform) the next chunk's rows in flight
+      if (more) {
+        const int jn = min((cc + XA_NSPLIT) * KPC + kl, pos - 1);
+        ld_quarter(wn, jn);
+        mn = km ? km[jn] : 0u;
+      }
+      const bool ok = xa_exact_ok(qcode, qn1, meta);
+      double p = 0.0;
+#pragma unroll
+      for (int u = 0; u < QW; u++) {
+        const uint32_t ww[4] = {wa[u].x, wa[u].y, wa[u].z, wa[u].w};
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+          const double2 q = q2[u * 4 + e];
+          p = fma((double)h2f((uint16_t)(ww[e] & 0xFFFF)), q.x, p);
+          p = fma((double)h2f((uint16_t)(ww[e] >> 16)), q.y, p);
+        }
+      }
+      p += dpp_d<DPP_QUAD_1032>(p);  // the key's four quarters (exact where ok)
+      p += dpp_d<DPP_QUAD_2301>(p);
+      if (valid && qt == 0) sc_out[j] = ok ? p : serial(kb + (size_t)j * HD);
+      if (more) {
+#pragma unroll
+        for (int u = 0; u < QW; u++) wa[u] = wn[u];
+        meta = mn;
+      }
+    }
   }
   XL_MARK(4);
 }
@@ -1273,10 +1360,10 @@ void launch_exact_attn(const XAttnArgs& a, hipStream_t s) {
   if (!exact_attn_supported(a.head_dim, a.n_head, a.n_head_kv) || !a.scores || !a.xq)
     throw std::runtime_error("exact attention: unsupported shape");
   if (a.head_dim == 256) {
-    hipLaunchKernelGGL(xattn_scores_kernel<256>, dim3(a.n_head, XA_NSPLIT), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(xattn_scores_kernel<256>, dim3(a.n_head, XA_NSPLIT + 1), dim3(64), 0, s, a);
     hipLaunchKernelGGL(xattn_accum_kernel<256>, dim3(a.n_head), dim3(320), 0, s, a);
   } else {
-    hipLaunchKernelGGL(xattn_scores_kernel<128>, dim3(a.n_head, XA_NSPLIT), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(xattn_scores_kernel<128>, dim3(a.n_head, XA_NSPLIT + 1), dim3(64), 0, s, a);
     hipLaunchKernelGGL(xattn_accum_kernel<128>, dim3(a.n_head), dim3(192), 0, s, a);
   }
   LLMI_HIP(hipGetLastError());

@@ -1607,6 +1607,7 @@ void Session::setup_xl() {
     const size_t n = (size_t)hp_.n_head_kv * l.hd * xa_vt_stride_;
     l.vt = dalloc<uint16_t>(n);
     LLMI_HIP(hipMemsetAsync(l.vt, 0, n * 2, stream_));
+    l.kmeta = dalloc<uint32_t>((size_t)hp_.n_head_kv * max_ctx_);  // (dalloc zeroes: every key unknown)
   }
   LLMI_HIP(hipStreamSynchronize(stream_));
   xl_ = true;
@@ -1662,6 +1663,7 @@ void Session::record_layers_xl(hipStream_t s) {
     xa.softcap = hp_.attn_softcap;
     xa.vt = Ld.vt;
     xa.vt_stride = xa_vt_stride_;
+    xa.kmeta = Ld.kmeta;
     launch_exact_attn(xa, s);
     // tensor-parallel ranks: this rank's rows of o, gate/up (its hidden units) and down, each slice all-gathered
     // before its consumer (whose residual / norm prologue runs on the whole vector on every rank)

@@ -54,6 +54,7 @@ struct LayerDev {
   int hd = 0;
   uint16_t *kc = nullptr, *vc = nullptr;
   uint16_t* vt = nullptr;      // exact-order engine: the V cache in 64-dim x 32-key tiles (exact.h)
+  uint32_t* kmeta = nullptr;   // exact-order engine: per-key exponent / magnitude words (exact.h XAttnArgs::kmeta)
   // Gemma-4
   bool has_kv = true;            // false: shared-KV layer, kc/vc alias layer kv_src's cache
   int kv_src = -1;

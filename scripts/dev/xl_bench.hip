@@ -406,6 +406,21 @@ static void attn_bench(std::mt19937& g, int pos) {
   LLMI_HIP(hipMalloc(&x.k_cache, kvn * 2));
   LLMI_HIP(hipMalloc(&x.v_cache, kvn * 2));
   LLMI_HIP(hipMemcpy(x.k_cache, hk.data(), kvn * 2, hipMemcpyHostToDevice));
+  {  // the per-key exactness words (exact.h XAttnArgs::kmeta) of the random K rows
+    std::vector<uint32_t> km((size_t)HK * MC);
+    for (size_t r = 0; r < (size_t)HK * MC; r++) {
+      int code = 31;
+      uint32_t mag = 0;
+      for (int d = 0; d < HD; d++) {
+        const uint16_t b = hk[r * HD + d];
+        if (b & 0x7FFF) code = std::min(code, std::max((b >> 10) & 0x1F, 1));
+        mag = std::max(mag, (uint32_t)(b & 0x7FFF));
+      }
+      km[r] = ((uint32_t)code << 16) | mag;
+    }
+    LLMI_HIP(hipMalloc(&x.kmeta, km.size() * 4));
+    LLMI_HIP(hipMemcpy(x.kmeta, km.data(), km.size() * 4, hipMemcpyHostToDevice));
+  }
   for (auto& v : hk) { const _Float16 hv = (_Float16)N(g); std::memcpy(&v, &hv, 2); }
   LLMI_HIP(hipMemcpy(x.v_cache, hk.data(), kvn * 2, hipMemcpyHostToDevice));
   {  // the tiled copy the scores kernel maintains (exact.h XAttnArgs::vt)
@@ -432,8 +447,8 @@ static void attn_bench(std::mt19937& g, int pos) {
   time_launch(nm, [&] { launch_exact_attn(x, 0); });
   phases_quiet();
   std::snprintf(nm, sizeof nm, "attn scores (pos %d)", pos);
-  time_launch(nm, [&] { hipLaunchKernelGGL(xattn_scores_kernel<256>, dim3(H, XA_NSPLIT), dim3(64), 0, 0, x); });
-  phases("scores (all WGs)", H * XA_NSPLIT);
+  time_launch(nm, [&] { hipLaunchKernelGGL(xattn_scores_kernel<256>, dim3(H, XA_NSPLIT + 1), dim3(64), 0, 0, x); });
+  phases("scores (all WGs)", H * (XA_NSPLIT + 1));
   std::snprintf(nm, sizeof nm, "attn accum (pos %d)", pos);
   time_launch(nm, [&] { hipLaunchKernelGGL(xattn_accum_kernel<256>, dim3(H), dim3(320), 0, 0, x); });
   phases("accum", H);
@@ -500,6 +515,32 @@ __global__ __launch_bounds__(64) void lat_kernel(float e, uint32_t v) {
   const unsigned long long t1 = __builtin_amdgcn_s_memtime();
   if (threadIdx.x == 0) g_lat[MODE] = t1 - t0 + (a + b == 12345u ? 1 : 0);
 }
+// f64: the scores kernel's element step (f16 -> f32 -> f64, fma) as one dependent chain (MODE 0) or four (1)
+__device__ unsigned long long g_lat64[4];
+template <int MODE>
+__global__ __launch_bounds__(64) void lat64_kernel(const uint32_t* kw, double q) {
+  double a0 = threadIdx.x, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  uint32_t w = kw[threadIdx.x];
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  for (int i = 0; i < 256; i++) {
+    w = w * 1664525u + 1013904223u;  // (independent of the chain)
+    const double x = (double)h2f((uint16_t)(w & 0x7BFF)), y = (double)h2f((uint16_t)((w >> 16) & 0x7BFF));
+    if (MODE == 0) {
+      a0 = fma(x, q, a0);
+      a0 = fma(y, q, a0);
+    } else if (MODE == 1) {
+      a0 = fma(x, q, a0);
+      a1 = fma(y, q, a1);
+      i++;
+      w = w * 1664525u + 1013904223u;
+      const double x2 = (double)h2f((uint16_t)(w & 0x7BFF)), y2 = (double)h2f((uint16_t)((w >> 16) & 0x7BFF));
+      a2 = fma(x2, q, a2);
+      a3 = fma(y2, q, a3);
+    }
+  }
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) g_lat64[MODE] = t1 - t0 + (a0 + a1 + a2 + a3 == 1.2345 ? 1 : 0);
+}
 static void latency_bench() {
   const char* nm[] = {"fma_mix+cvt", "fma_f32", "cvt_f16", "2 chains fma_mix+cvt", "fma_mix", "fma_mixlo"};
   hipLaunchKernelGGL(lat_kernel<0>, dim3(1), dim3(64), 0, 0, 0.5f, 0x3c00u);
@@ -512,6 +553,16 @@ static void latency_bench() {
   unsigned long long l[8];
   LLMI_HIP(hipMemcpyFromSymbol(l, HIP_SYMBOL(g_lat), sizeof l));
   for (int m = 0; m < 6; m++) std::printf("latency %-22s %6.2f cycles/step\n", nm[m], l[m] / 1024.0);
+  uint32_t* kw;
+  LLMI_HIP(hipMalloc(&kw, 256));
+  LLMI_HIP(hipMemset(kw, 0x11, 256));
+  hipLaunchKernelGGL(lat64_kernel<0>, dim3(1), dim3(64), 0, 0, kw, 0.37);
+  hipLaunchKernelGGL(lat64_kernel<1>, dim3(1), dim3(64), 0, 0, kw, 0.37);
+  LLMI_HIP(hipDeviceSynchronize());
+  unsigned long long l64[4];
+  LLMI_HIP(hipMemcpyFromSymbol(l64, HIP_SYMBOL(g_lat64), sizeof l64));
+  std::printf("f64 element step, one chain  %6.2f cycles/element\n", l64[0] / 512.0);
+  std::printf("f64 element step, four chains %6.2f cycles/element\n", l64[1] / 512.0);
 }
 
 // the norm chain variants alone: 256 threads, 2560 random floats per work-group in LDS, cycles + fallbacks
