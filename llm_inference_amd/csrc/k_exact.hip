@@ -71,6 +71,15 @@ __device__ __forceinline__ float xl_chain(const float* s, int n, float sum = 0.0
   return sum;
 }
 
+// f64 DPP step (both halves moved by the same row-local control)
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  const int lo = dpp_i<CTRL>(__double2loint(v)), hi = dpp_i<CTRL>(__double2hiint(v));
+  return __hiloint2double(hi, lo);
+}
+
+constexpr int DPP_ROW_SHL4 = 0x104;  // lane i reads lane i + 4 of its 16-lane row
+
 // The boundary walk of the speculative chains (wave 0): the true start of segment k is the chain value after
 // segment k - 1; if it is one of the segment's 32 candidates (s_base[k] + c) its end value is that candidate's
 // (s_e[k * 32 + c]), otherwise the segment is recomputed serially from it.  The walk over hits is unrolled with
@@ -198,12 +207,25 @@ __device__ __forceinline__ float xl_chain_spec2(const float* s, int n, unsigned*
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int k = t >> 4, c = lane & 15, L = n / K;
   double p = 0.0;
-  for (int i = c; i < L; i += 16) {
-    const double v = (double)s[k * L + i];
-    p = fma(v, v, p);
-  }
+  if (L <= 64) {  // (the attention rows: every load issued before the sums; a 16-lane row on DPP)
+    float v[4];
 #pragma unroll
-  for (int m = 8; m >= 1; m >>= 1) p += __shfl_xor(p, m);
+    for (int r = 0; r < 4; r++) v[r] = s[k * L + min(c + 16 * r, L - 1)];
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+      if (c + 16 * r < L) p = fma((double)v[r], (double)v[r], p);
+    p += dpp_d<DPP_QUAD_1032>(p);
+    p += dpp_d<DPP_QUAD_2301>(p);
+    p += dpp_d<DPP_ROW_MIRROR>(p);
+    p += dpp_d<DPP_ROW_HALF_MIRROR>(p);
+  } else {
+    for (int i = c; i < L; i += 16) {
+      const double v = (double)s[k * L + i];
+      p = fma(v, v, p);
+    }
+#pragma unroll
+    for (int m = 8; m >= 1; m >>= 1) p += __shfl_xor(p, m);
+  }
   if (c == 0) s_seg[k] = p;
   __syncthreads();
   double pre = 0.0;
@@ -219,13 +241,6 @@ __device__ __forceinline__ float xl_chain_spec2(const float* s, int n, unsigned*
   if (wave == 0) s_res = xl_spec_walk<K>(s, L, s_e, s_base, fallbacks);
   __syncthreads();
   return s_res;
-}
-
-// f64 DPP step (both halves moved by the same row-local control)
-template <int CTRL>
-__device__ __forceinline__ double dpp_d(double v) {
-  const int lo = dpp_i<CTRL>(__double2loint(v)), hi = dpp_i<CTRL>(__double2hiint(v));
-  return __hiloint2double(hi, lo);
 }
 
 // xl_chain_spec with its fixed costs cut (round 5: 6.4K cycles per 2560-term chain of which the chain is ~2.6K,
@@ -517,9 +532,9 @@ __global__ __launch_bounds__(NW * 64) void exact_gemv_kernel(const uint4* __rest
                                      (sc2 * hv[k].z) * nv[k].z, (sc2 * hv[k].w) * nv[k].w);
         if (ok && blockIdx.x == 0 && a.xn_out) reinterpret_cast<float4*>(a.xn_out)[k * T + t] = x;
         float amax = ok ? fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w))) : 0.0f;
-        amax = fmaxf(amax, __shfl_xor(amax, 1));
-        amax = fmaxf(amax, __shfl_xor(amax, 2));
-        amax = fmaxf(amax, __shfl_xor(amax, 4));
+        amax = fmaxf(amax, dpp_f<DPP_QUAD_1032>(amax));  // (max: exact in any order; the octet on DPP)
+        amax = fmaxf(amax, dpp_f<DPP_QUAD_2301>(amax));
+        amax = fmaxf(amax, dpp_f<DPP_ROW_HALF_MIRROR>(amax));
         const float dd = amax / 127.0f;
         const float id = dd != 0.0f ? 1.0f / dd : 0.0f;
         const int q0 = nearest_int_fma(x.x, id), q1 = nearest_int_fma(x.y, id), q2 = nearest_int_fma(x.z, id),
@@ -527,8 +542,8 @@ __global__ __launch_bounds__(NW * 64) void exact_gemv_kernel(const uint4* __rest
         const uint32_t w = (uint32_t)(q0 & 0xFF) | ((uint32_t)(q1 & 0xFF) << 8) | ((uint32_t)(q2 & 0xFF) << 16) |
                            ((uint32_t)(q3 & 0xFF) << 24);
         const int sum = q0 + q1 + q2 + q3;
-        const uint32_t wh = __shfl_xor(w, 4);  // the octet's lanes 4-7: elements 16-31 of the block
-        const int sumh = __shfl_xor(sum, 4);
+        const uint32_t wh = (uint32_t)dpp_i<DPP_ROW_SHL4>((int)w);  // octet lanes 4-7: elements 16-31 of the block
+        const int sumh = dpp_i<DPP_ROW_SHL4>(sum);
         const int i4 = k * T + t, b = i4 >> 3, sl = i4 & 7;
         if (ok && sl < 4) s_xe[b * 4 + sl] = make_int4((int)w, (int)wh, -8 * sum, -8 * sumh);
         if (ok && sl == 0) s_xd[b] = h2f(f2h_ggml(dd));
@@ -693,9 +708,9 @@ __global__ __launch_bounds__(256) void exact_plain_split_kernel(const uint4* __r
   XL_MARK(2);
   if (wave == 0) {
     // hsum_float_8 (ops.cpp:324-330): ((a0 + a4) + (a2 + a6)) + ((a1 + a5) + (a3 + a7)), lanes R * 8 + k
-    const float t4 = acc + __shfl_xor(acc, 4);
-    const float u = t4 + __shfl_xor(t4, 2);
-    const float r = u + __shfl_xor(u, 1);
+    const float t4 = acc + dpp_f<DPP_ROW_SHL4>(acc);  // (lanes R * 8 + 0..3: a_k + a_k+4)
+    const float u = t4 + dpp_f<DPP_QUAD_2301>(t4);
+    const float r = u + dpp_f<DPP_QUAD_1032>(u);
     const int row = row0 + (lane >> 3);
     if ((lane & 7) == 0 && row < rows) a.out[row] = r;
   }
@@ -748,20 +763,30 @@ __global__ void xl_repack_kernel(const uint4* __restrict__ q0, const uint16_t* _
 __device__ __forceinline__ int xa_exp_code(uint16_t b) {
   return (b & 0x7FFF) == 0 ? 31 : max((b >> 10) & 0x1F, 1);
 }
+// wave reductions: the 16-lane rows on DPP, then two cross-row shuffles
 __device__ __forceinline__ int xa_wave_min(int v) {
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) v = min(v, __shfl_xor(v, o));
-  return v;
+  v = min(v, dpp_i<DPP_QUAD_1032>(v));
+  v = min(v, dpp_i<DPP_QUAD_2301>(v));
+  v = min(v, dpp_i<DPP_ROW_MIRROR>(v));
+  v = min(v, dpp_i<DPP_ROW_HALF_MIRROR>(v));
+  v = min(v, __shfl_xor(v, 16));
+  return min(v, __shfl_xor(v, 32));
 }
 __device__ __forceinline__ int xa_wave_max(int v) {
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) v = max(v, __shfl_xor(v, o));
-  return v;
+  v = max(v, dpp_i<DPP_QUAD_1032>(v));
+  v = max(v, dpp_i<DPP_QUAD_2301>(v));
+  v = max(v, dpp_i<DPP_ROW_MIRROR>(v));
+  v = max(v, dpp_i<DPP_ROW_HALF_MIRROR>(v));
+  v = max(v, __shfl_xor(v, 16));
+  return max(v, __shfl_xor(v, 32));
 }
-__device__ __forceinline__ double xa_wave_sum_d(double v) {  // (a bound: any order)
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) v += __shfl_xor(v, o);
-  return v;
+__device__ __forceinline__ double xa_wave_sum_d(double v) {  // (exact where the summands allow: xa_exact_ok)
+  v += dpp_d<DPP_QUAD_1032>(v);
+  v += dpp_d<DPP_QUAD_2301>(v);
+  v += dpp_d<DPP_ROW_MIRROR>(v);
+  v += dpp_d<DPP_ROW_HALF_MIRROR>(v);
+  v += __shfl_xor(v, 16);
+  return v + __shfl_xor(v, 32);
 }
 // No add of the score chain rounds: every product q_i k_i (exact in f32) is a multiple of 2^m, m = (qcode - 25) +
 // (kcode - 25), and every partial sum is at most |q|_1 max|k| < 2^(m + 52) in magnitude, so each is a multiple of
@@ -978,6 +1003,25 @@ __global__ __launch_bounds__(64) void xattn_scores_kernel(XAttnArgs a) {
   XL_MARK(4);
 }
 
+// f64 DPP move with a fill value for lanes without a source (row_mask ROWS: the rows written)
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double xa_dpp_d_old(double v, double old) {
+  const int lo = __builtin_amdgcn_update_dpp(__double2loint(old), __double2loint(v), CTRL, ROWS, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(__double2hiint(old), __double2hiint(v), CTRL, ROWS, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+// inclusive prefix max across the wave: row_shr 1, 2, 4, 8 within the 16-lane rows, then row_bcast 15 / 31
+__device__ __forceinline__ double xa_wave_incl_max(double v) {
+  const double ninf = -INFINITY;
+  v = fmax(v, xa_dpp_d_old<0x111, 0xF>(v, ninf));
+  v = fmax(v, xa_dpp_d_old<0x112, 0xF>(v, ninf));
+  v = fmax(v, xa_dpp_d_old<0x114, 0xF>(v, ninf));
+  v = fmax(v, xa_dpp_d_old<0x118, 0xF>(v, ninf));
+  v = fmax(v, xa_dpp_d_old<0x142, 0xA>(v, ninf));
+  v = fmax(v, xa_dpp_d_old<0x143, 0xC>(v, ninf));
+  return v;
+}
+
 constexpr int XA_CH = 1024;  // accum: keys per chunk in LDS
 
 // eight steps of vec_mad_f16 for one head dim: acc (f16 in the low half) = f16(fma(f16 V[u], e[u], acc)), each
@@ -1052,13 +1096,13 @@ __device__ __forceinline__ uint16_t cvt_f16_rne(float f) {
 template <int HD>
 __global__ __launch_bounds__((HD / 64 + 1) * 64) void xattn_accum_kernel(XAttnArgs a) {
   constexpr int NWV = HD / 64, T = (NWV + 1) * 64;
-  constexpr int KPT = XA_CH / 256;  // keys per scan thread (threads 0..255)
+  constexpr int NWS = T / 64, KPT = (XA_CH + T - 1) / T;  // the branch pass: every wave, KPT keys per thread
   __shared__ double s_sc[XA_CH];
   static_assert(XA_CH / 32 <= 32, "the chunk's max-move words: one per lane of a half-wave");
   __shared__ __attribute__((aligned(16))) float s_e[XA_CH];   // e per key
   __shared__ __attribute__((aligned(16))) float s_pe[XA_CH];  // pe per key
   __shared__ uint32_t s_up[XA_CH / 32];
-  __shared__ double s_tmax[4];  // the four scan waves' maxima
+  __shared__ double s_tmax[NWS];  // the scan waves' maxima
   __shared__ float s_sacc;
   __shared__ uint64_t s_etab[32];  // expf's table (a per-lane global load each call, on the branch pass's chain)
   const int h = blockIdx.x, t = threadIdx.x, wave = t >> 6, lane = t & 63;
@@ -1089,31 +1133,26 @@ __global__ __launch_bounds__((HD / 64 + 1) * 64) void xattn_accum_kernel(XAttnAr
     __syncthreads();
     XL_MARK(1);
     // the max of every key before each key (max is exact, so any grouping): segments of KPT keys per thread,
-    // an inclusive prefix max across each wave's 64 segments by shuffles, then across the four waves' totals
+    // an inclusive prefix max across each wave's 64 segments on DPP, then across the waves' totals.  (Round 5:
+    // all T threads scan -- the 256-thread scan left keys 768.. of a chunk unscanned at head_dim 128.)
     double tmax = -INFINITY;
-    if (t < 256) {
 #pragma unroll
-      for (int k = 0; k < KPT; k++) {
-        const int j = t * KPT + k;
-        if (j < nk) tmax = fmax(tmax, s_sc[j]);
-      }
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const double v = __shfl_up(tmax, o, 64);
-        if (lane >= o) tmax = fmax(tmax, v);
-      }
-      if (lane == 63) s_tmax[wave] = tmax;
+    for (int k = 0; k < KPT; k++) {
+      const int j = t * KPT + k;
+      if (j < nk) tmax = fmax(tmax, s_sc[j]);
     }
+    tmax = xa_wave_incl_max(tmax);
+    if (lane == 63) s_tmax[wave] = tmax;
     if (wave < NWV) {  // the chunk's first V batches, in flight during the branch pass below
 #pragma unroll
       for (int b = 0; b < NB - 1; b++) ld(vb4[b], c0 + b * 32);
     }
     __syncthreads();
-    if (t < 256) {
-      const double left = __shfl_up(tmax, 1, 64);  // inclusive max of the previous segments in this wave
-      double pm = run_max;                          // max of every key before this segment
+    {
+      const double left = xa_dpp_d_old<0x138, 0xF>(tmax, -INFINITY);  // wave_shr:1: the previous segments' max
+      double pm = run_max;                                             // max of every key before this segment
       for (int w = 0; w < wave; w++) pm = fmax(pm, s_tmax[w]);
-      if (lane > 0) pm = fmax(pm, left);
+      pm = fmax(pm, left);
 #pragma unroll
       for (int k = 0; k < KPT; k++) {
         const int j = t * KPT + k;
@@ -1131,7 +1170,8 @@ __global__ __launch_bounds__((HD / 64 + 1) * 64) void xattn_accum_kernel(XAttnAr
         pm = fmax(pm, score);
       }
     }
-    run_max = fmax(fmax(run_max, fmax(s_tmax[0], s_tmax[1])), fmax(s_tmax[2], s_tmax[3]));
+#pragma unroll
+    for (int w = 0; w < NWS; w++) run_max = fmax(run_max, s_tmax[w]);
     __syncthreads();
     XL_MARK(2);
     if (wave < NWV) {  // this lane's head dim from the transposed V: 8 keys per 16-B load, NB - 1 batches

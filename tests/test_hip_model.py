@@ -117,6 +117,24 @@ def test_mini_models_vs_oracle(oracle, cfg_name, exact):
     assert [int(np.argmax(got))] + toks.tolist() == toks_ref
 
 
+@pytest.mark.parametrize("cfg_name", ["mini-27b", "mini-4b"])
+def test_exact_attention_past_a_key_chunk(oracle, cfg_name):
+    """The exact attention's accumulate runs its keys in chunks of XA_CH = 1024 (k_exact.hip), each with a branch
+    pass that scans the chunk's scores for the running max: a 1100-token prompt crosses a chunk, at head_dim 128
+    (mini-27b) and 256 (mini-4b); the logits after it bit-identical to the reference's (round 5: at head_dim 128
+    the scan covered 768 keys of a chunk)."""
+    from llm_inference_amd.model import Model
+    from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
+    cfg = CONFIGS[cfg_name]
+    g = build_gemma3_gguf(cfg, seed=11)
+    prompt = np.random.default_rng(17).integers(4, cfg.vocab, 1100).astype(np.int32)
+    ref = oracle.model(g, n_threads=16, max_ctx=1152).forward(prompt, 0)
+    m = Model(g, exact=True, max_ctx=1152)
+    got = m.forward(prompt, 0)
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), float(np.abs(got - ref).max())
+    m.close()
+
+
 def test_session_errors():
     from llm_inference_amd._lib import LLMIError
     from llm_inference_amd.model import Model
