@@ -20,7 +20,7 @@ OBJ = os.path.join(HERE, "_build")
 LIB = os.path.join(HERE, "libllmi.so")
 SOURCES = ["k_gemv.hip", "k_layer.hip", "k_engine.hip", "k_elem.hip", "k_attn.hip", "k_session.hip", "k_prefill.hip", "k_logits.hip", "k_exchange.hip", "k_exact.hip", "session.cpp", "collective.cpp", "capi.cpp"]
 HEADERS = ["common.h", "kernels.h", "attn.h", "layer_body.h", "session_kernels.h", "session.h", "gguf_reader.h", "collective.h",
-           "exact.h", "px.h", "glibc_math.h"]
+           "exact.h", "px.h", "glibc_math.h", "spec_chain.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "--offload-arch=gfx950", "-Wall",
          "-Wno-unused-function", "-Wno-unused-variable", "-Wno-unused-result"]

@@ -1,6 +1,7 @@
 // k_session.hip -- weight upload/repack and the fused glue kernels of the
 // decode step (residual + norms, GELU + quantize, argmax, token feedback).
 #include "session_kernels.h"
+#include "spec_chain.h"
 
 #include <mutex>
 #include <vector>
@@ -453,11 +454,14 @@ __device__ __forceinline__ void norm_outputs(const float (&xv)[NORM_EPT], int n,
 
 template <bool EXACT>
 __device__ __forceinline__ float sumsq_regs(const float (&v)[NORM_EPT], int n, float* s_h, float* sh) {
-  if (EXACT) {  // stage, then the reference's serial fma chain (ops.cpp:33-36)
+  if (EXACT) {  // stage, then the reference's serial fma chain (ops.cpp:33-36): speculative over the block's first
+    // 4 waves where n splits into 8 segments of whole float4s (round 5: one thread's chain of dependent LDS loads
+    // was ~25K cycles per 2560-term norm), bit-identical (spec_chain.h)
 #pragma unroll
     for (int k = 0; k < NORM_EPT; k++)
       if (threadIdx.x + k * 1024 < n) s_h[threadIdx.x + k * 1024] = v[k];
     __syncthreads();
+    if (n % 32 == 0 && n / 32 <= 192) return xl_chain_spec_fast<4, 1024>(s_h, n);
     return serial_sumsq(s_h, n, sh);
   }
   float sq = 0.0f;
