@@ -978,7 +978,7 @@ __global__ __launch_bounds__((HD / 64 + 1) * 64) void xattn_accum_kernel(XAttnAr
   float s_acc = 0.0f;
   // this lane's head dim of the tiled V (wave < NWV: dims 64 wave ..), a 32-key batch as 4 loads of 8 keys, each
   // load one contiguous KB across the wave; tiles past the context stay inside the kv head and are never summed
-  constexpr int NB = 4;  // V batches in flight (the tiled loads: 6 measured the same as an all-L1 copy)
+  constexpr int NB = 4;  // V batches in flight (6: 5 spilled VGPRs, 354 vs 360 tok/s)
   const uint4* vtp = reinterpret_cast<const uint4*>(a.vt + xa_vt_index<HD>(hkv, min(wave, NWV - 1) * 64 + lane, 0, a.vt_stride));
   const int kb_last = a.vt_stride / 32 - 1;
   uint4 vb4[NB][4];
@@ -989,6 +989,10 @@ __global__ __launch_bounds__((HD / 64 + 1) * 64) void xattn_accum_kernel(XAttnAr
   };
   if (t < 32) s_etab[t] = llmi_glibc::exp2f_tab(t);
   XL_MARK(0);
+#ifdef XA_STATS
+  int st_batches = 0, st_slow = 0, st_moves = 0;
+  const unsigned long long st_t0 = __builtin_amdgcn_s_memtime();
+#endif
   for (int c0 = 0; c0 < n_keys; c0 += XA_CH) {
     const int nk = min(XA_CH, n_keys - c0);
     for (int i = t; i < nk; i += T)
@@ -1062,6 +1066,9 @@ __global__ __launch_bounds__((HD / 64 + 1) * 64) void xattn_accum_kernel(XAttnAr
           const uint32_t up = __builtin_amdgcn_readlane(upv, j0 >> 5);
           const int m = __builtin_amdgcn_readfirstlane(min(32, nk - j0));
           const float* e = eb[b & 1];
+#ifdef XA_STATS
+          if (wave == 0) { st_batches++; st_slow += up != 0; st_moves += __builtin_popcount(up); }
+#endif
           if (up == 0 && m == 32) {
             uint32_t acc = v16;
 #pragma unroll
@@ -1144,6 +1151,11 @@ __global__ __launch_bounds__((HD / 64 + 1) * 64) void xattn_accum_kernel(XAttnAr
     __syncthreads();  // the chunk's LDS is reused by the next one
   }
   XL_MARK(4);
+#ifdef XA_STATS
+  if (wave == 0 && lane == 0 && h == 0)
+    printf("xa_stats pos %d batches %d slow %d moves %d (cycles %lld)\n", n_keys - 1, st_batches, st_slow, st_moves,
+           (long long)(__builtin_amdgcn_s_memtime() - st_t0));
+#endif
   if (wave == NWV && lane == 0) s_sacc = s_acc == 0.0f ? 0.0f : 1.0f / s_acc;
   __syncthreads();
   if (wave < NWV) {
