@@ -2,6 +2,7 @@
 // reference's operation order (ops.cpp:364-399 mat_vec_mul_q4_0, ops.cpp:28-43
 // rms_norm, ops.cpp:116-139 quantize_row_q8_0, model.cpp:843-924 residual /
 // norm / GELU) with the weights streamed like the fast path's layer GEMVs.
+#include <cstdlib>
 #include <stdexcept>
 
 #include "exact.h"
@@ -246,7 +247,10 @@ __device__ __forceinline__ void xl_eat1(const XlChunk& c, int g0, int ng, int jj
 // XL_K4: PRE / GELU float4 of each operand per thread (n <= 4 XL_K4 T); NCH: chunks of XL_P groups in flight;
 // LPR: lanes per row -- 4 (lane jj holds the reference's accumulators jj and jj + 4) or 8 (PLAIN: one accumulator
 // per lane, twice the waves over the same rows: more of the weight stream in flight for the long down rows)
-template <int NW, int ROLE, int XL_K4, int NCH, int LPR = 4>
+// SPR (PRE only, 0: off): SPR rows per work-group with the rows' dots split over all lanes and the chains run
+// after them (as exact_plain_split_kernel): the qkv launch's 64 work-groups of 64 rows left 192 CUs idle in
+// its GEMV phase
+template <int NW, int ROLE, int XL_K4, int NCH, int LPR = 4, int SPR = 0>
 __global__ __launch_bounds__(NW * 64) void exact_gemv_kernel(const uint4* __restrict__ wq, const uint2* __restrict__ wd,
                                                              int rows, int nb, XlArgs a) {
   extern __shared__ int4 s_dyn[];
@@ -272,10 +276,27 @@ __global__ __launch_bounds__(NW * 64) void exact_gemv_kernel(const uint4* __rest
   // the weight stream is issued right AFTER the activation operands' first loads: loads return in issue order, so
   // operands issued behind 32 KB per wave of weights waited for them (round 5: the operands-in-LDS phase of the
   // PRE / GELU roles 3.2-3.9K cycles; scripts/dev/xl_bench)
-  XlChunk ck[NCH];
+  static_assert(SPR == 0 || (ROLE == XL_PRE && NW == 4 && SPR * 8 % 64 == 0 && (SPR & (SPR - 1)) == 0), "SPR: PRE");
+  constexpr int SIPL = SPR ? (SPR * 4 * (XL_K4 * T / 32) + T - 1) / T : 1;  // split items per lane (ng <= XL_K4 T / 32)
+  XlChunk ck[SPR ? 1 : NCH];
+  uint4 sq4[SIPL];
+  uint2 sd2[SIPL];
+  const int srow0 = blockIdx.x * (SPR ? SPR : 1);
   auto issue_w = [&]() {
+    if constexpr (SPR > 0) {  // item i = t + T m: slot jj = i % 4, row R = (i / 4) % SPR, group g = i / (4 SPR)
 #pragma unroll
-    for (int k = 0; k < NCH; k++) xl_load(ck[k], rq, rd, voq, vod, sq, sd, k * XL_P, ng);
+      for (int m = 0; m < SIPL; m++) {
+        const int i = t + T * m, jj4 = i & 3, R = (i >> 2) & (SPR - 1), g = i / (4 * SPR);
+        const bool in = g < ng;
+        sq4[m] = buf_ld16(rq, in ? ((g * rows + srow0 + R) * 4 + jj4) * 16 : (1 << 30), 0);
+        typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+        const u32x2_t v = __builtin_amdgcn_raw_buffer_load_b64(rd, in && jj4 == 0 ? (g * rows + srow0 + R) * 8 : (1 << 30), 0, BUF_NT);
+        sd2[m] = make_uint2(v.x, v.y);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < NCH; k++) xl_load(ck[k], rq, rd, voq, vod, sq, sd, k * XL_P, ng);
+    }
   };
 
   // ---- the activation: XE entries + scales in LDS.  Every global operand a thread needs is loaded in one
@@ -417,6 +438,59 @@ __global__ __launch_bounds__(NW * 64) void exact_gemv_kernel(const uint4* __rest
   __syncthreads();
 
   XL_MARK(5);
+  if constexpr (SPR > 0) {  // ---- split rows: every (row, block, slot) dot by all lanes, then the chains ----
+    constexpr int NBMAX = XL_K4 * T / 8;  // blocks per row: n <= 4 XL_K4 T
+    __shared__ __attribute__((aligned(16))) float s_p[SPR * 8 * (NBMAX + 4)];
+    __shared__ __attribute__((aligned(16))) float s_d[SPR * (NBMAX + 4)];
+    const int ld = nb + 4;  // (conflict-free float4 rows: ld % 64 == 20 for nb = 80)
+    const float4* s_xd4c = reinterpret_cast<const float4*>(s_xd);
+#pragma unroll
+    for (int m = 0; m < SIPL; m++) {
+      const int i = t + T * m, jj4 = i & 3, R = (i >> 2) & (SPR - 1), g = i / (4 * SPR);
+      if (g < ng) {
+        const uint32_t w4[4] = {sq4[m].x, sq4[m].y, sq4[m].z, sq4[m].w};
+        float4 pl, ph;
+        float* plv = reinterpret_cast<float*>(&pl);
+        float* phv = reinterpret_cast<float*>(&ph);
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const int4 x = s_xe[(4 * g + u) * 4 + jj4];
+          plv[u] = (float)sdot4((int)(w4[u] & 0x0F0F0F0Fu), x.x, x.z);
+          phv[u] = (float)sdot4((int)((w4[u] >> 4) & 0x0F0F0F0Fu), x.y, x.w);
+        }
+        *reinterpret_cast<float4*>(s_p + (R * 8 + jj4) * ld + 4 * g) = pl;
+        *reinterpret_cast<float4*>(s_p + (R * 8 + jj4 + 4) * ld + 4 * g) = ph;
+        if (jj4 == 0) {
+          const float4 xd = s_xd4c[g];
+          *reinterpret_cast<float4*>(s_d + R * ld + 4 * g) =
+              make_float4(h2f((uint16_t)(sd2[m].x & 0xFFFFu)) * xd.x, h2f((uint16_t)(sd2[m].x >> 16)) * xd.y,
+                          h2f((uint16_t)(sd2[m].y & 0xFFFFu)) * xd.z, h2f((uint16_t)(sd2[m].y >> 16)) * xd.w);
+        }
+      }
+    }
+    __syncthreads();
+    if (t < SPR * 8) {  // chain t: accumulator t % 8 of row t / 8, block order (ops.cpp:380-395)
+      const float4* p4 = reinterpret_cast<const float4*>(s_p + t * ld);
+      const float4* d4 = reinterpret_cast<const float4*>(s_d + (t >> 3) * ld);
+      float acc = 0.0f;
+#pragma unroll 4
+      for (int b4 = 0; b4 < nb / 4; b4++) {
+        const float4 p = p4[b4], d = d4[b4];
+        acc = fmaf(d.x, p.x, acc);
+        acc = fmaf(d.y, p.y, acc);
+        acc = fmaf(d.z, p.z, acc);
+        acc = fmaf(d.w, p.w, acc);
+      }
+      // hsum_float_8 (ops.cpp:324-330): ((a0 + a4) + (a2 + a6)) + ((a1 + a5) + (a3 + a7))
+      const float t4 = acc + dpp_f<DPP_ROW_SHL4>(acc);
+      const float u = t4 + dpp_f<DPP_QUAD_2301>(t4);
+      const float r = u + dpp_f<DPP_QUAD_1032>(u);
+      const int orow = srow0 + (t >> 3);
+      if ((t & 7) == 0 && orow < rows) a.out[orow] = r;
+    }
+    XL_MARK(6);
+    return;
+  }
   // ---- the rows: every block in order, NCH chunks in flight ----
   float lo = 0.0f, hi = 0.0f;
   const float4* s_xd4 = reinterpret_cast<const float4*>(s_xd);
@@ -1311,6 +1385,9 @@ void launch_exact_gemv(const XlWeight& w, const XlArgs& a_in, int role, hipStrea
     case XL_QUANT: go(exact_gemv_kernel<1, XL_QUANT, 1, 4>, 1); break;
     case XL_PRE:
       if (k3_2) go(exact_gemv_kernel<2, XL_PRE, 3, 2>, 2);
+      else if (k3_4 && w.rows % 16 == 0 && getenv("LLMI_XL_PRE_ROWS") == nullptr)  // (dev A/B: the 64-row form)
+        hipLaunchKernelGGL((exact_gemv_kernel<4, XL_PRE, 3, 2, 4, 16>), dim3((unsigned)(w.rows / 16)), dim3(256), lds, s, w.qs,
+                           w.d, w.rows, w.nb, a);
       else if (k3_4) go(exact_gemv_kernel<4, XL_PRE, 3, 2>, 4);
       else go(exact_gemv_kernel<4, XL_PRE, 6, 2>, 4);
       break;

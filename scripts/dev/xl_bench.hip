@@ -641,6 +641,23 @@ int main() {
   pre.y = y; pre.w_post = wp; pre.resid_in = r0; pre.resid_out = r1; pre.w_next = wn; pre.n = E; pre.eps = 1e-6;
   pre.out = out;
   run("qkv PRE", xq, pre, XL_PRE);
+  {  // the split-row PRE (SPR 16) against the 64-row form: bit-identical q|k|v rows
+    std::vector<float> o1(xq.rows), o2(xq.rows);
+    const size_t lds = (size_t)xq.nb * 64 + (size_t)xq.nb * 4 + (size_t)2 * pre.n * 4;
+    hipLaunchKernelGGL((exact_gemv_kernel<4, XL_PRE, 3, 2>), dim3(xq.rows / 64), dim3(256), lds, 0, xq.qs, xq.d, xq.rows,
+                       xq.nb, pre);
+    LLMI_HIP(hipMemcpy(o1.data(), pre.out, xq.rows * 4, hipMemcpyDeviceToHost));
+    LLMI_HIP(hipMemset(pre.out, 0, xq.rows * 4));
+    hipLaunchKernelGGL((exact_gemv_kernel<4, XL_PRE, 3, 2, 4, 16>), dim3(xq.rows / 16), dim3(256), lds, 0, xq.qs, xq.d,
+                       xq.rows, xq.nb, pre);
+    LLMI_HIP(hipGetLastError());
+    LLMI_HIP(hipMemcpy(o2.data(), pre.out, xq.rows * 4, hipMemcpyDeviceToHost));
+    int bad = 0, first = -1;
+    for (int i = 0; i < xq.rows; i++)
+      if (std::memcmp(&o1[i], &o2[i], 4) != 0) { bad++; if (first < 0) first = i; }
+    std::printf("qkv split vs 64-row PRE: %d of %d rows differ (first %d: %.6g vs %.6g)\n", bad, xq.rows, first,
+                first >= 0 ? o1[first] : 0.f, first >= 0 ? o2[first] : 0.f);
+  }
   XlArgs gu = pre;
   gu.out = nullptr; gu.hid = hid; gu.hq = hq;
   run("gate_up", xgu, gu, XL_GELU);
