@@ -1392,7 +1392,7 @@ void launch_exact_gemv(const XlWeight& w, const XlArgs& a_in, int role, hipStrea
       else go(exact_gemv_kernel<4, XL_PRE, 6, 2>, 4);
       break;
     case XL_GELU:
-      if (k3_4) go(exact_gemv_kernel<4, XL_GELU, 3, 2>, 4);
+      if (k3_4) go(exact_gemv_kernel<4, XL_GELU, 3, 1>, 4);  // (one chunk in flight: its operands return sooner)
       else go(exact_gemv_kernel<4, XL_GELU, 6, 2>, 4);
       break;
     default: throw std::runtime_error("exact gemv: bad role");
