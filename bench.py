@@ -199,6 +199,7 @@ def parity(ref, got) -> dict:
     return {"positions": len(ref), "logits_bit_identical": int(sum(same_bits)),
             "argmax_identical": int(sum(int(np.argmax(r)) == int(np.argmax(x)) for r, x in zip(ref, got))),
             "max_abs_logit_diff": float(np.abs(ref - got).max()),
+            "max_abs_logit_diff_per_position": [round(float(np.abs(r - x).max()), 4) for r, x in zip(ref, got)],
             "max_abs_reference_logit": float(np.abs(ref).max())}
 
 
