@@ -697,6 +697,9 @@ __global__ void xl_repack_kernel(const uint4* __restrict__ q0, const uint16_t* _
 // run_norm's serial chain (ops.cpp:28-43) on the row staged in s_x, (scale * x) * w, then NEOX rope at pos
 // (ops.cpp:67-95, the pinned build's contractions: v0 c - v1 s and v0 s + v1 c as one fma each) -- pairs
 // (i, i + HD / 2) sit in one lane
+#ifdef XA_STATS
+__device__ unsigned g_xa_serial;  // scores taking the serial chain (all heads, one launch)
+#endif
 // f16 bits -> max(exponent field, 1) for a nonzero value (its ulp is 2^(code - 25)), 31 for +-0
 __device__ __forceinline__ int xa_exp_code(uint16_t b) {
   return (b & 0x7FFF) == 0 ? 31 : max((b >> 10) & 0x1F, 1);
@@ -729,6 +732,21 @@ __device__ __forceinline__ double xa_wave_sum_d(double v) {  // (exact where the
 // No add of the score chain rounds: every product q_i k_i (exact in f32) is a multiple of 2^m, m = (qcode - 25) +
 // (kcode - 25), and every partial sum is at most |q|_1 max|k| < 2^(m + 52) in magnitude, so each is a multiple of
 // 2^m below 2^(m + 53): representable, in any order.  kmeta 0 (unknown key) or a non-finite bound: false.
+// The same with the product quanta bounded pair by pair: epair = min over i of the raw exponent fields of q_i
+// and k_i summed (2^(e - 25) bounds the ulp of an f16 of exponent field e from below, zero and subnormals
+// included), so every product is a multiple of 2^(epair - 50) -- a tiny q_i no longer needs a tiny k_i's
+// bound at the same time (round 5: with the per-vector minima ~1 % of the 4B model's keys failed, each a
+// 256-step serial chain in its work-group).
+__device__ __forceinline__ bool xa_exact_ok_pair(int epair, double qn1, uint32_t kmeta) {
+  if ((kmeta >> 16) == 0) return false;  // unknown key
+  const double bound = qn1 * (double)h2f((uint16_t)(kmeta & 0x7FFFu));
+  return bound < __longlong_as_double((long long)(epair - 50 + 52 + 1023) << 52);
+}
+typedef unsigned short xa_u16x2 __attribute__((ext_vector_type(2)));
+// the packed exponent fields of a word of two f16 values
+__device__ __forceinline__ xa_u16x2 xa_exp2(uint32_t w) {
+  return __builtin_bit_cast(xa_u16x2, (w >> 10) & 0x001F001Fu);
+}
 __device__ __forceinline__ bool xa_exact_ok(int qcode, double qn1, uint32_t kmeta) {
   const int kcode = (int)(kmeta >> 16);
   if (kcode == 0) return false;
@@ -789,6 +807,7 @@ __global__ __launch_bounds__(64) void xattn_scores_kernel(XAttnArgs a) {
   __shared__ __attribute__((aligned(16))) float s_x[HD];
   __shared__ __attribute__((aligned(16))) double s_q[HD];
   __shared__ __attribute__((aligned(16))) uint16_t s_k[HD];
+  __shared__ __attribute__((aligned(16))) uint16_t s_qe[HD];  // the f16 query's exponent fields
   const int h = blockIdx.x, split = blockIdx.y, lane = threadIdx.x;
   const int pos = *a.d_pos;
   // work-groups split < XA_NSPLIT: the keys before pos in chunks of 16, chunk split, split + XA_NSPLIT, ..; the
@@ -838,6 +857,7 @@ __global__ __launch_bounds__(64) void xattn_scores_kernel(XAttnArgs a) {
   for (int k = 0; k < EPL; k++) {  // model.cpp:767 scale, then the score's f16 query (model.cpp:507)
     const uint16_t qb = f2h_ggml(r[k] * a.attn_scale);
     s_q[lane + 64 * k] = (double)h2f(qb);
+    s_qe[lane + 64 * k] = (qb >> 10) & 0x1F;
     qcode = min(qcode, xa_exp_code(qb));
     qn1 += fabs((double)h2f(qb));
   }
@@ -894,7 +914,11 @@ __global__ __launch_bounds__(64) void xattn_scores_kernel(XAttnArgs a) {
     return acc;
   };
   if (pos_wg) {
-    if (xa_exact_ok(qcode, qn1, ((uint32_t)kcode_new << 16) | kmag_new)) {  // (uniform) elements lane + 64 k
+    int ep = 64;
+#pragma unroll
+    for (int k = 0; k < EPL; k++) ep = min(ep, (int)((s_k[lane + 64 * k] >> 10) & 0x1F) + (int)s_qe[lane + 64 * k]);
+    ep = xa_wave_min(ep);
+    if (xa_exact_ok_pair(ep, qn1, ((uint32_t)kcode_new << 16) | kmag_new)) {  // (uniform) elements lane + 64 k
       double p = 0.0;
 #pragma unroll
       for (int k = 0; k < EPL; k++) p = fma((double)h2f(s_k[lane + 64 * k]), s_q[lane + 64 * k], p);
@@ -905,6 +929,7 @@ __global__ __launch_bounds__(64) void xattn_scores_kernel(XAttnArgs a) {
     }
   } else {
     const double2* q2 = reinterpret_cast<const double2*>(s_q + qt * (HD / 4));
+    const xa_u16x2* qe2 = reinterpret_cast<const xa_u16x2*>(s_qe + qt * (HD / 4));
     for (int cc = split; cc * KPC < pos; cc += XA_NSPLIT) {
       const int j = cc * KPC + kl;
       const bool valid = j < pos;
@@ -916,8 +941,8 @@ __global__ __launch_bounds__(64) void xattn_scores_kernel(XAttnArgs a) {
         ld_quarter(wn, jn);
         mn = km ? km[jn] : 0u;
       }
-      const bool ok = xa_exact_ok(qcode, qn1, meta);
       double p = 0.0;
+      xa_u16x2 pm = {64, 64};  // min over this quarter's pairs of the two exponent fields' sum
 #pragma unroll
       for (int u = 0; u < QW; u++) {
         const uint32_t ww[4] = {wa[u].x, wa[u].y, wa[u].z, wa[u].w};
@@ -926,11 +951,22 @@ __global__ __launch_bounds__(64) void xattn_scores_kernel(XAttnArgs a) {
           const double2 q = q2[u * 4 + e];
           p = fma((double)h2f((uint16_t)(ww[e] & 0xFFFF)), q.x, p);
           p = fma((double)h2f((uint16_t)(ww[e] >> 16)), q.y, p);
+          pm = __builtin_elementwise_min(pm, xa_exp2(ww[e]) + qe2[u * 4 + e]);
         }
       }
       p += dpp_d<DPP_QUAD_1032>(p);  // the key's four quarters (exact where ok)
       p += dpp_d<DPP_QUAD_2301>(p);
+      int ep = min((int)pm.x, (int)pm.y);
+      ep = min(ep, dpp_i<DPP_QUAD_1032>(ep));
+      ep = min(ep, dpp_i<DPP_QUAD_2301>(ep));
+      const bool ok = xa_exact_ok_pair(ep, qn1, meta);
       if (valid && qt == 0) sc_out[j] = ok ? p : serial(kb + (size_t)j * HD);
+#ifdef XA_STATS
+      {
+        const unsigned long long bal = __ballot(valid && qt == 0 && !ok);
+        if (lane == 0 && bal) atomicAdd(&g_xa_serial, (unsigned)__popcll(bal));
+      }
+#endif
       if (more) {
 #pragma unroll
         for (int u = 0; u < QW; u++) wa[u] = wn[u];
@@ -1165,8 +1201,9 @@ __global__ __launch_bounds__((HD / 64 + 1) * 64) void xattn_accum_kernel(XAttnAr
               }
 #pragma unroll
               for (int u = 8 * i; u < 8 * i + 8; u++) {
-                if (u < m) {  // wave-uniform
-                  if (up & (1u << u)) acc = cvt_f16_rne((float)__builtin_bit_cast(_Float16, (uint16_t)acc) * pe[u]);
+                if (__builtin_expect(u < m, 1)) {  // wave-uniform; a move is the rare key (the branch falls through)
+                  if (__builtin_expect((up & (1u << u)) != 0, 0))
+                    acc = cvt_f16_rne((float)__builtin_bit_cast(_Float16, (uint16_t)acc) * pe[u]);
                   const uint4 w4 = vb4[b][u >> 3];
                   const uint32_t wv = ((u >> 1) & 3) == 0 ? w4.x : ((u >> 1) & 3) == 1 ? w4.y : ((u >> 1) & 3) == 2 ? w4.z : w4.w;
                   xa_mad1(acc, wv, e[u], u & 1);
@@ -1227,8 +1264,11 @@ __global__ __launch_bounds__((HD / 64 + 1) * 64) void xattn_accum_kernel(XAttnAr
   XL_MARK(4);
 #ifdef XA_STATS
   if (wave == 0 && lane == 0 && h == 0)
-    printf("xa_stats pos %d batches %d slow %d moves %d (cycles %lld)\n", n_keys - 1, st_batches, st_slow, st_moves,
-           (long long)(__builtin_amdgcn_s_memtime() - st_t0));
+  {
+    printf("xa_stats pos %d batches %d slow %d moves %d (cycles %lld) serial scores %u\n", n_keys - 1, st_batches, st_slow,
+           st_moves, (long long)(__builtin_amdgcn_s_memtime() - st_t0), g_xa_serial);
+    g_xa_serial = 0u;
+  }
 #endif
   if (wave == NWV && lane == 0) s_sacc = s_acc == 0.0f ? 0.0f : 1.0f / s_acc;
   __syncthreads();
