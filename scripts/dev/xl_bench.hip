@@ -590,6 +590,7 @@ static void sumsq_bench(std::mt19937& g) {
   float* x = rand_vec(NB * 2560, g, 1.0f);
   unsigned long long* cyc; float* res; unsigned* fb;
   LLMI_HIP(hipMalloc(&cyc, NB * 8)); LLMI_HIP(hipMalloc(&res, NB * 4)); LLMI_HIP(hipMalloc(&fb, 4));
+  // (a 16-segment x 2-candidate form with spec_fast's costs measured 5.5K vs 5.3K cycles: not kept)
   std::vector<float> r[4];
   const char* nm[] = {"spec<4> (8 segs)", "spec2<4> (16 segs x 2)", "serial", "spec_fast<4> (8 segs)"};
   for (int v = 0; v < 4; v++) {
