@@ -1248,10 +1248,18 @@ __global__ __launch_bounds__((HD / 64 + 1) * 64) void xattn_accum_kernel(XAttnAr
               pv[4 * u4] = p.x; pv[4 * u4 + 1] = p.y; pv[4 * u4 + 2] = p.z; pv[4 * u4 + 3] = p.w;
             }
 #pragma unroll
-            for (int u = 0; u < 32; u++) {
-              if (u < m) {
-                if (up & (1u << u)) s_acc = s_acc * pv[u];
-                s_acc = s_acc + ev[u];
+            for (int i = 0; i < 4; i++) {  // eight keys at a time: plain adds where the eight have no move
+              if (((up >> (8 * i)) & 0xFFu) == 0 && m >= 8 * (i + 1)) {
+#pragma unroll
+                for (int u = 8 * i; u < 8 * i + 8; u++) s_acc = s_acc + ev[u];
+                continue;
+              }
+#pragma unroll
+              for (int u = 8 * i; u < 8 * i + 8; u++) {
+                if (u < m) {
+                  if (up & (1u << u)) s_acc = s_acc * pv[u];
+                  s_acc = s_acc + ev[u];
+                }
               }
             }
           }
