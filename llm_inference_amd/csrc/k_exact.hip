@@ -800,11 +800,81 @@ __device__ __forceinline__ void xa_row(const XaRow<HD>& in, const float (&c)[HD 
   (void)HALF;
 }
 
+// The q row's and the new key's k row's norms at once (the new key's work-group, one wave): the half-wave h
+// (0: q, 1: k) runs its row's serial chain speculatively over 2 segments of HD / 2, 16 lanes per segment with
+// two candidates each (xl_chain2), so both rows' chains share the wave's issue slots instead of running one
+// after the other (round 5: the new key's work-group was the scores launch's critical path).  Each row's scale
+// is bit-identical to xl_chain's.
+template <int HD>
+__device__ __forceinline__ void xa_row2(const XaRow<HD>& inq, const XaRow<HD>& ink, const float (&c)[HD / 128 > 0 ? HD / 128 : 1],
+                                        const float (&sn)[HD / 128 > 0 ? HD / 128 : 1], double eps, float* s_xq,
+                                        float* s_xk, float (&rq)[HD / 64], float (&rk)[HD / 64]) {
+  constexpr int EPL = HD / 64, L = HD / 2, L4 = L / 4, R = (L4 + 15) / 16;
+  static_assert(HD % 32 == 0, "xa_row2: two segments of whole float4s");
+  __shared__ double s_seg2[2][2];
+  __shared__ float s_e2[2][64];
+  __shared__ int s_base2[2][2];
+  const int lane = threadIdx.x & 63, hh = lane >> 5, seg = (lane >> 4) & 1, c16 = lane & 15;
+#pragma unroll
+  for (int k = 0; k < EPL; k++) {
+    s_xq[lane + 64 * k] = inq.v[k];
+    s_xk[lane + 64 * k] = ink.v[k];
+  }
+  __syncthreads();
+  const float* sx = hh ? s_xk : s_xq;
+  {
+    const float4* s4 = reinterpret_cast<const float4*>(sx + seg * L);
+    float4 v[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) v[r] = s4[min(c16 + 16 * r, L4 - 1)];
+    double p = 0.0;
+#pragma unroll
+    for (int r = 0; r < R; r++)
+      if (c16 + 16 * r < L4) {
+        const double x = v[r].x, y = v[r].y, z = v[r].z, w = v[r].w;
+        p = fma(x, x, fma(y, y, fma(z, z, fma(w, w, p))));
+      }
+    p += dpp_d<DPP_QUAD_1032>(p);
+    p += dpp_d<DPP_QUAD_2301>(p);
+    p += dpp_d<DPP_ROW_MIRROR>(p);
+    p += dpp_d<DPP_ROW_HALF_MIRROR>(p);
+    if (c16 == 0) s_seg2[hh][seg] = p;
+  }
+  __syncthreads();
+  const int base = seg == 0 ? 0 : max(0, (int)__float_as_uint((float)s_seg2[hh][0]) - 16);
+  float ea = seg == 0 ? 0.0f : __uint_as_float((uint32_t)(base + c16));
+  float eb = seg == 0 ? 0.0f : __uint_as_float((uint32_t)(base + 16 + c16));
+  xl_chain2(sx + seg * L, L, ea, eb);
+  s_e2[hh][seg * 32 + c16] = ea;
+  s_e2[hh][seg * 32 + 16 + c16] = eb;
+  if (c16 == 0) s_base2[hh][seg] = base;
+  __syncthreads();
+  const float sq = xl_spec_walk<2>(s_xq, L, s_e2[0], s_base2[0], nullptr);
+  const float sk = xl_spec_walk<2>(s_xk, L, s_e2[1], s_base2[1], nullptr);
+  const float scq = xl_rms_scale(sq, HD, eps), sck = xl_rms_scale(sk, HD, eps);
+  float nq[EPL], nk[EPL];
+#pragma unroll
+  for (int k = 0; k < EPL; k++) {
+    nq[k] = (scq * inq.v[k]) * inq.w[k];
+    nk[k] = (sck * ink.v[k]) * ink.w[k];
+  }
+#pragma unroll
+  for (int k = 0; k < EPL / 2; k++) {  // NEOX rope, as xa_row
+    const int kp = k + EPL / 2;
+    rq[k] = fmaf(nq[k], c[k], -(nq[kp] * sn[k]));
+    rq[kp] = fmaf(nq[k], sn[k], nq[kp] * c[k]);
+    rk[k] = fmaf(nk[k], c[k], -(nk[kp] * sn[k]));
+    rk[kp] = fmaf(nk[k], sn[k], nk[kp] * c[k]);
+  }
+  __syncthreads();  // s_xq / s_xk / s_e2 reuse
+}
+
 template <int HD>
 __global__ __launch_bounds__(64) void xattn_scores_kernel(XAttnArgs a) {
   constexpr int EPL = HD / 64, CPL = EPL / 2, QW = HD / 32;  // QW: 16-B words of a quarter row
   constexpr int KPC = 16;                                    // keys per chunk: 4 lanes (row quarters) per key
   __shared__ __attribute__((aligned(16))) float s_x[HD];
+  __shared__ __attribute__((aligned(16))) float s_x2[HD];
   __shared__ __attribute__((aligned(16))) double s_q[HD];
   __shared__ __attribute__((aligned(16))) uint16_t s_k[HD];
   __shared__ __attribute__((aligned(16))) uint16_t s_qe[HD];  // the f16 query's exponent fields
@@ -847,8 +917,9 @@ __global__ __launch_bounds__(64) void xattn_scores_kernel(XAttnArgs a) {
     ld_quarter(wa, j1);
     meta = km ? km[j1] : 0u;
   }
-  float r[EPL];
-  xa_row<HD>(qr, c, sn, a.eps, s_x, r);
+  float r[EPL], rk2[EPL];
+  if (pos_wg) xa_row2<HD>(qr, kr_, c, sn, a.eps, s_x, s_x2, r, rk2);  // (uniform per work-group)
+  else xa_row<HD>(qr, c, sn, a.eps, s_x, r);
   XL_MARK(1);
   // the query's exactness words (xa_exact_ok): min over its nonzero elements of max(exponent field, 1), |q|_1
   int qcode = 31;
@@ -865,8 +936,9 @@ __global__ __launch_bounds__(64) void xattn_scores_kernel(XAttnArgs a) {
   qn1 = xa_wave_sum_d(qn1);
   int kcode_new = 31;
   uint32_t kmag_new = 0;
-  if (pos_wg) {  // the new key: k norm + rope, K and V rows appended (model.cpp:440-474)
-    xa_row<HD>(kr_, c, sn, a.eps, s_x, r);
+  if (pos_wg) {  // the new key: k norm + rope (xa_row2 above), K and V rows appended (model.cpp:440-474)
+#pragma unroll
+    for (int k = 0; k < EPL; k++) r[k] = rk2[k];
     uint16_t* kc = a.k_cache + ((size_t)hkv * a.max_ctx + pos) * HD;
     uint16_t* vc = a.v_cache + ((size_t)hkv * a.max_ctx + pos) * HD;
 #pragma unroll
