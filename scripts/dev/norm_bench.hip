@@ -23,58 +23,67 @@ static float* rnd(int n, std::mt19937& g) {
 
 __device__ unsigned long long g_ph[8];
 #define PH(i) do { if (threadIdx.x == 0) g_ph[i] = __builtin_amdgcn_s_memtime(); } while (0)
-// xl_chain_spec_fast with phase stamps (development copy)
-template <int NW>
+// xl_chain_spec_fast<NW, NT> with phase stamps (development copy of spec_chain.h)
+template <int NW, int NT>
 __device__ float spec_fast_traced(const float* s, int n) {
   constexpr int K = 2 * NW, R = 6;
+  constexpr bool ALL = NT == NW * 64;
   __shared__ double s_seg[K];
   __shared__ float s_e[K * 32];
   __shared__ int s_base[K];
+  __shared__ float s_res;
   const int t = threadIdx.x, lane = t & 63;
-  const int k = t >> 5, c = lane & 31, L = n / K, L4 = L / 4;
+  const bool act = ALL || t < NW * 64;
+  const int k = min(t >> 5, K - 1), c = lane & 31, L = n / K, L4 = L / 4;
   PH(0);
-  const float4* s4 = reinterpret_cast<const float4*>(s + k * L);
-  float4 v[R];
+  if (act) {
+    const float4* s4 = reinterpret_cast<const float4*>(s + k * L);
+    float4 v[R];
 #pragma unroll
-  for (int r = 0; r < R; r++) v[r] = s4[min(c + 32 * r, L4 - 1)];
-  double p0 = 0.0, p1 = 0.0;
+    for (int r = 0; r < R; r++) v[r] = s4[min(c + 32 * r, L4 - 1)];
+    double p0 = 0.0, p1 = 0.0;
 #pragma unroll
-  for (int r = 0; r < R; r++) {
-    if (c + 32 * r < L4) {
-      const double x = v[r].x, y = v[r].y, z = v[r].z, w = v[r].w;
-      p0 = fma(x, x, fma(y, y, p0));
-      p1 = fma(z, z, fma(w, w, p1));
+    for (int r = 0; r < R; r++) {
+      if (c + 32 * r < L4) {
+        const double x = v[r].x, y = v[r].y, z = v[r].z, w = v[r].w;
+        p0 = fma(x, x, fma(y, y, p0));
+        p1 = fma(z, z, fma(w, w, p1));
+      }
     }
+    double p = p0 + p1;
+    p += dpp_d<DPP_QUAD_1032>(p);
+    p += dpp_d<DPP_QUAD_2301>(p);
+    p += dpp_d<DPP_ROW_MIRROR>(p);
+    p += dpp_d<DPP_ROW_HALF_MIRROR>(p);
+    p += __shfl_xor(p, 16);
+    if (c == 0) s_seg[k] = p;
   }
-  double p = p0 + p1;
-  p += dpp_d<DPP_QUAD_1032>(p);
-  p += dpp_d<DPP_QUAD_2301>(p);
-  p += dpp_d<DPP_ROW_MIRROR>(p);
-  p += dpp_d<DPP_ROW_HALF_MIRROR>(p);
-  p += __shfl_xor(p, 16);
-  if (c == 0) s_seg[k] = p;
   PH(1);
   __syncthreads();
   PH(2);
-  double pre = 0.0;
+  if (act) {
+    double pre = 0.0;
 #pragma unroll
-  for (int j = 0; j < K - 1; j++)
-    if (j < k) pre += s_seg[j];
-  const int base = k == 0 ? 0 : max(0, (int)__float_as_uint((float)pre) - 16);
-  const float x0 = k == 0 ? 0.0f : __uint_as_float((uint32_t)(base + c));
-  PH(3);
-  const float e = xl_chain(s + k * L, L, x0);
-  PH(4);
-  s_e[k * 32 + c] = e;
-  if (c == 0) s_base[k] = base;
+    for (int j = 0; j < K - 1; j++)
+      if (j < k) pre += s_seg[j];
+    const int base = k == 0 ? 0 : max(0, (int)__float_as_uint((float)pre) - 16);
+    const float x0 = k == 0 ? 0.0f : __uint_as_float((uint32_t)(base + c));
+    PH(3);
+    const float e = xl_chain(s + k * L, L, x0);
+    PH(4);
+    s_e[k * 32 + c] = e;
+    if (c == 0) s_base[k] = base;
+  }
   __syncthreads();
   PH(5);
-  unsigned fb = 0;
-  const float res = xl_spec_walk<K>(s, L, s_e, s_base, &fb);
+  if (t < 64) {
+    const float res = xl_spec_walk<K>(s, L, s_e, s_base, nullptr);
+    if (t == 0) s_res = res;
+  }
   PH(6);
   __syncthreads();
   PH(7);
-  return res;
+  return s_res;
 }
 __device__ unsigned long long g_cyc[4];
 __device__ float g_res[4];
@@ -86,7 +95,7 @@ __global__ __launch_bounds__(1024) void chain_kernel(const float* x, int n) {
   const unsigned long long t0 = __builtin_amdgcn_s_memtime();
   float r;
   if (V == 0) r = xl_chain_spec_fast<4, 1024>(s_h, n);
-  else if (V == 2) r = spec_fast_traced<16>(s_h, n);
+  else if (V == 2) r = spec_fast_traced<4, 1024>(s_h, n);
   else {
     __shared__ float s_r;
     if (threadIdx.x == 0) {
@@ -137,7 +146,7 @@ int main() {
   LLMI_HIP(hipDeviceSynchronize());
   unsigned long long ph[8];
   LLMI_HIP(hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_ph), sizeof ph));
-  std::printf("spec_fast<16> phases (cycles from start):");
+  std::printf("spec_fast<4, 1024> phases (cycles from start):");
   for (int i = 1; i < 8; i++) std::printf(" %d:%llu", i, ph[i] - ph[0]);
   std::printf("\n");
   unsigned long long c[4];
