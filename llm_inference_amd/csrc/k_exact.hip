@@ -1444,8 +1444,8 @@ XlWeight make_xl_weight(const XlSrc& src, hipStream_t s) {
   x.nb = cols / 32;
   x.bytes = bytes;
   const size_t ng = (size_t)x.nb / 4;
-  LLMI_HIP(hipMalloc(&x.qs, ng * rows * 64 + 256));
-  LLMI_HIP(hipMalloc(&x.d, ng * rows * 8 + 256));
+  x.qs = static_cast<uint4*>(dev_alloc(ng * rows * 64 + 256));
+  x.d = static_cast<uint2*>(dev_alloc(ng * rows * 8 + 256));
   auto Q = [&](int k) { return k < src.n ? reinterpret_cast<const uint4*>(src.w[k]->qs) : nullptr; };
   auto D = [&](int k) { return k < src.n ? src.w[k]->d : nullptr; };
   auto R = [&](int k) { return k < src.n ? src.w[k]->rows : 0; };

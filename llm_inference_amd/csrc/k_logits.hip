@@ -330,11 +330,11 @@ bool screen_supported(const DevWeight& table) {
 void alloc_screen_table(const DevWeight& table, ScreenTable& st, hipStream_t s) {
   const int nb = table.cols / 32;
   const size_t n_blocks = (size_t)table.rows * nb;
-  LLMI_HIP(hipMalloc(&st.qs, n_blocks * 32));
-  LLMI_HIP(hipMalloc(&st.d, n_blocks * 2 + 64));
-  LLMI_HIP(hipMalloc(&st.xs, (size_t)(nb + 1) * sizeof(ScreenX)));
-  LLMI_HIP(hipMalloc(&st.hi, (size_t)table.rows * 4));
-  LLMI_HIP(hipMalloc(&st.m_key, 64));
+  st.qs = static_cast<decltype(st.qs)>(dev_alloc(n_blocks * 32));
+  st.d = static_cast<decltype(st.d)>(dev_alloc(n_blocks * 2 + 64));
+  st.xs = static_cast<decltype(st.xs)>(dev_alloc((size_t)(nb + 1) * sizeof(ScreenX)));
+  st.hi = static_cast<decltype(st.hi)>(dev_alloc((size_t)table.rows * 4));
+  st.m_key = static_cast<decltype(st.m_key)>(dev_alloc(64));
   LLMI_HIP(hipMemsetAsync(st.xs, 0, (size_t)(nb + 1) * sizeof(ScreenX), s));
   LLMI_HIP(hipMemsetAsync(st.m_key, 0, 64, s));
   st.rows = table.rows;

@@ -4,6 +4,7 @@
 #include "spec_chain.h"
 
 #include <mutex>
+#include <unordered_map>
 #include <vector>
 
 namespace llmi {
@@ -58,30 +59,75 @@ bool gemv_type_supported(uint32_t type) {
          type == T_BF16;
 }
 
-// Device memory of the sessions goes back to the allocator only while no OTHER session of the process is alive
-// (DESIGN.md section 7, round 5): with several sessions in one process (the one-GPU tensor-parallel group), memory
-// one session freed and another reallocated at the same time was read wrong on its first use -- one word of a
-// weight row, right on every later read (a one-GPU 4-rank group: 8 of 23 lifetimes; 0 of 2,868 with the frees held
-// back, scripts/dev/tp_diag.py).  Frees made while other sessions live wait in a graveyard released when the last
-// session ends; a lone session (the production case: one process per GPU) frees at once.
+// Device memory of the sessions.  (1) It goes back to reuse only while no OTHER
+// session of the process is alive: with several sessions in one process (the one-GPU tensor-parallel group),
+// memory one session freed and another reallocated at the same time was read wrong on its first use -- one word
+// of a weight row, right on every later read (a one-GPU 4-rank group: 8 of 23 lifetimes; 0 of 2,868 with the
+// frees held back, scripts/dev/tp_diag.py); frees made while other sessions live wait in a graveyard released
+// when the last session ends.  (2) Released blocks stay mapped: they are kept by size and handed to the next
+// allocation of that size instead of hipFree + hipMalloc (a 4-rank group constructed after a whole-model session
+// closed still read 0.012-off logits once in a full suite run: the same signature); the cache is returned to
+// the allocator when an allocation fails or it exceeds kCacheCap.
 namespace {
 std::mutex g_mem_mu;
 int g_live_sessions = 0;
 std::vector<void*> g_graveyard;
+std::unordered_map<void*, size_t> g_sizes;       // live blocks from dev_alloc: rounded size
+std::unordered_multimap<size_t, void*> g_cache;  // released blocks, still mapped
+size_t g_cached = 0;
+constexpr size_t kGran = 64 << 10, kCacheCap = (size_t)48 << 30;
+
+void flush_cache_locked() {
+  for (auto& kv : g_cache) (void)hipFree(kv.second);
+  g_cache.clear();
+  g_cached = 0;
+}
+void release_locked(void* p) {  // (no other session alive)
+  auto it = g_sizes.find(p);
+  if (it == g_sizes.end()) {  // not from dev_alloc
+    (void)hipFree(p);
+    return;
+  }
+  g_cache.emplace(it->second, p);
+  g_cached += it->second;
+  g_sizes.erase(it);
+  if (g_cached > kCacheCap) flush_cache_locked();
+}
 }  // namespace
+
+void* dev_alloc(size_t bytes) {
+  const size_t sz = (bytes + kGran - 1) / kGran * kGran;
+  std::lock_guard<std::mutex> lk(g_mem_mu);
+  auto it = g_cache.find(sz);
+  if (it != g_cache.end()) {
+    void* p = it->second;
+    g_cache.erase(it);
+    g_cached -= sz;
+    g_sizes[p] = sz;
+    return p;
+  }
+  void* p = nullptr;
+  if (hipMalloc(&p, sz) != hipSuccess) {  // out of memory: the cached blocks back to the allocator, once
+    (void)hipGetLastError();
+    flush_cache_locked();
+    LLMI_HIP(hipMalloc(&p, sz));
+  }
+  g_sizes[p] = sz;
+  return p;
+}
 
 void dev_free(void* p) {
   if (!p) return;
   std::lock_guard<std::mutex> lk(g_mem_mu);
   if (g_live_sessions > 1) g_graveyard.push_back(p);
-  else (void)hipFree(p);
+  else release_locked(p);
 }
 
 void session_live(int delta) {
   std::lock_guard<std::mutex> lk(g_mem_mu);
   g_live_sessions += delta;
   if (g_live_sessions == 0) {
-    for (void* p : g_graveyard) (void)hipFree(p);
+    for (void* p : g_graveyard) release_locked(p);
     g_graveyard.clear();
   }
 }
@@ -95,7 +141,7 @@ void upload_rows(DevWeight& w, int dst_row0, const void* host, int rows, hipStre
     const int nb = w.cols / 32;
     const size_t nblk = (size_t)rows * nb;
     void* tmp = nullptr;
-    LLMI_HIP(hipMalloc(&tmp, bytes));
+    tmp = dev_alloc(bytes);
     LLMI_HIP(hipMemcpyAsync(tmp, host, bytes, hipMemcpyHostToDevice, s));
     const size_t b0 = (size_t)dst_row0 * nb;
     if (w.type == T_Q4_0)
@@ -124,10 +170,10 @@ DevWeight alloc_weight(uint32_t type, int rows, int cols, size_t slack) {
   w.bytes = gguf_bytes(type, rows, cols);
   if (type == T_Q4_0 || type == T_Q8_0) {
     const size_t nblk = (size_t)rows * (cols / 32);
-    LLMI_HIP(hipMalloc(&w.qs, nblk * (type == T_Q4_0 ? 16 : 32) + slack));
-    LLMI_HIP(hipMalloc((void**)&w.d, nblk * 2 + slack));
+    w.qs = dev_alloc(nblk * (type == T_Q4_0 ? 16 : 32) + slack);
+    w.d = static_cast<uint16_t*>(dev_alloc(nblk * 2 + slack));
   } else {
-    LLMI_HIP(hipMalloc(&w.qs, w.bytes + slack));
+    w.qs = dev_alloc(w.bytes + slack);
   }
   return w;
 }
@@ -148,8 +194,8 @@ void to_slab_layout(DevWeight& w, hipStream_t s) {
   const size_t nblk = (size_t)w.rows * nb;
   void* q2 = nullptr;
   uint16_t* d2 = nullptr;
-  LLMI_HIP(hipMalloc(&q2, nblk * 16 + 64));
-  LLMI_HIP(hipMalloc((void**)&d2, nblk * 2 + 64));
+  q2 = dev_alloc(nblk * 16 + 64);
+  d2 = static_cast<uint16_t*>(dev_alloc(nblk * 2 + 64));
   hipLaunchKernelGGL(slab_permute_kernel, dim3((nblk + 255) / 256), dim3(256), 0, s, (const uint4*)w.qs, w.d, w.rows,
                      nb, (uint4*)q2, d2);
   LLMI_HIP(hipGetLastError());
@@ -256,14 +302,14 @@ void to_kq_layout(DevWeight& w, hipStream_t s, int slab) {
   uint16_t* sc;
   uint32_t* dd;
   uint2* qh = nullptr;
-  LLMI_HIP(hipMalloc(&qs, nsub * 16 + 64));
-  LLMI_HIP(hipMalloc(&sc, nsub * 2 + 64));
-  LLMI_HIP(hipMalloc(&dd, nsb * 4 + 64));
+  qs = static_cast<uint4*>(dev_alloc(nsub * 16 + 64));
+  sc = static_cast<uint16_t*>(dev_alloc(nsub * 2 + 64));
+  dd = static_cast<uint32_t*>(dev_alloc(nsb * 4 + 64));
   const dim3 grid((unsigned)((nsub + 255) / 256));
   if (w.type == T_Q4_K) {
     hipLaunchKernelGGL(repack_q4_k_kernel, grid, dim3(256), 0, s, (const uint8_t*)w.qs, nsub, qs, sc, dd, srows, rsb);
   } else {
-    LLMI_HIP(hipMalloc(&qh, nsub * 8 + 64));
+    qh = static_cast<uint2*>(dev_alloc(nsub * 8 + 64));
     hipLaunchKernelGGL(repack_q6_k_kernel, grid, dim3(256), 0, s, (const uint8_t*)w.qs, nsub, qs, sc, dd, qh, srows, rsb);
   }
   LLMI_HIP(hipGetLastError());

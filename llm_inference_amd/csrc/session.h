@@ -135,8 +135,7 @@ class Session {
   // DESIGN.md section 7, the round-5 tensor-parallel finding)
   template <typename T>
   T* dalloc(size_t count) {
-    void* p = nullptr;
-    LLMI_HIP(hipMalloc(&p, count * sizeof(T) + 64));
+    void* p = dev_alloc(count * sizeof(T) + 64);
     allocs_.push_back(p);
     LLMI_HIP(hipMemsetAsync(p, 0, count * sizeof(T) + 64, stream_));
     return static_cast<T*>(p);

@@ -14,6 +14,7 @@ void upload_rows(DevWeight& w, int dst_row0, const void* host, int rows, hipStre
 void free_weight(DevWeight& w);
 // device memory of the sessions (k_session.hip): freed at once only while no other session of the process is alive,
 // else when the last one ends; session_live(+1 / -1) brackets a session's lifetime
+void* dev_alloc(size_t bytes);  // session / weight memory (cached when released, k_session.hip)
 void dev_free(void* p);
 void session_live(int delta);
 // Q4_0 row-major blocks -> slab-major (k_layer.hip's a.slab layout): slabs of

@@ -7,7 +7,12 @@
 #include "../../llm_inference_amd/csrc/k_exact.hip"
 
 namespace llmi {
-void dev_free(void* p) { (void)hipFree(p); }  // (libllmi's graveyard-aware free, k_session.hip; not linked here)
+void dev_free(void* p) { (void)hipFree(p); }  // (libllmi's cached allocator, k_session.hip; not linked here)
+void* dev_alloc(size_t b) {
+  void* p = nullptr;
+  (void)hipMalloc(&p, b);
+  return p;
+}
 }  // namespace llmi
 
 #include <algorithm>
