@@ -179,6 +179,31 @@ def cpu_share() -> int:
 FORCED = 8  # teacher-forced steps after the GPU line's prompt (parity check of exact and fast mode vs the reference)
 
 
+def bench_prompt(cfg, n: int, offset: int = 0) -> np.ndarray:
+    """The GPU line's seeded prompt (BOS then n - 1 ids; offset: a replica's own stream)."""
+    rng = np.random.default_rng(99 + offset)
+    return np.concatenate([[2], rng.integers(4, cfg.vocab, n - 1)]).astype(np.int32)
+
+
+def parity_key(config: str, quant: str, prefill: int) -> str:
+    """The workload a committed conditioning fixture (tests/golden/bench_conditioning.json) was computed on."""
+    return f"{config}/{quant}/prefill{prefill}/forced{FORCED}"
+
+
+def load_spread(key: str):
+    """The reference's own f16-vs-f64-attention spread per parity position for this workload, or None."""
+    p = os.path.join(ROOT, "tests", "golden", "bench_conditioning.json")
+    try:
+        return json.load(open(p)).get(key, {}).get("spread_per_position")
+    except (OSError, ValueError):
+        return None
+
+
+def progress(msg: str) -> None:
+    """A line on stderr per phase (a run that prints nothing for minutes looks hung)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def forced_tokens(vocab: int) -> np.ndarray:
     return np.random.default_rng(2024).integers(4, vocab, FORCED).astype(np.int32)
 
@@ -193,17 +218,44 @@ def forced_logits(m, prompt, vocab):
     return np.stack(out)
 
 
-def parity(ref, got) -> dict:
-    """Device logits vs the reference's at the same FORCED + 1 positions."""
+# The fast path's stated parity bound per position p (fp32 reassociation and fp32 split-K attention where the
+# reference rounds an f16 accumulator at every key): |fast - reference|_p <= FAST_ABS + FAST_SPREAD x s_p, s_p =
+# the reference's own distance from the same computation with f64 attention at p (its conditioning there: the
+# oracle with attn_f64 on the same inputs, committed per workload by scripts/bench_conditioning.py -- two oracle
+# runs over the 512-token prompt take minutes of CPU).  FAST_ABS is the full-depth 4B budget of tests/test_long_models.py.  And
+# wherever the reference's top-2 margin exceeds twice the measured difference, the argmax must be the reference's.
+FAST_ABS, FAST_SPREAD = 0.05, 3.0
+
+
+def parity(ref, got, spread=None, exact=False) -> dict:
+    """Device logits vs the reference's at the same FORCED + 1 positions; `ok` False when the mode's stated
+    bound is exceeded (exact: every bit; fast: the bound above, where the spread s_p was measured)."""
     same_bits = [bool(np.array_equal(r.view(np.uint32), x.view(np.uint32))) for r, x in zip(ref, got)]
-    return {"positions": len(ref), "logits_bit_identical": int(sum(same_bits)),
-            "argmax_identical": int(sum(int(np.argmax(r)) == int(np.argmax(x)) for r, x in zip(ref, got))),
-            "max_abs_logit_diff": float(np.abs(ref - got).max()),
-            "max_abs_logit_diff_per_position": [round(float(np.abs(r - x).max()), 4) for r, x in zip(ref, got)],
-            "max_abs_reference_logit": float(np.abs(ref).max())}
+    diff = [float(np.abs(r - x).max()) for r, x in zip(ref, got)]
+    srt = np.sort(ref, 1)
+    margin = srt[:, -1] - srt[:, -2]
+    agree = [int(np.argmax(r)) == int(np.argmax(x)) for r, x in zip(ref, got)]
+    out = {"positions": len(ref), "logits_bit_identical": int(sum(same_bits)), "argmax_identical": int(sum(agree)),
+           "max_abs_logit_diff": max(diff),
+           "max_abs_logit_diff_per_position": [round(d, 4) for d in diff],
+           "max_abs_reference_logit": float(np.abs(ref).max()),
+           "reference_top2_margin_per_position": [round(float(m), 4) for m in margin]}
+    if exact:
+        out["bound"] = "bit-identical logits at every position"
+        out["ok"] = all(same_bits)
+    elif spread is not None:
+        bound = [FAST_ABS + FAST_SPREAD * s for s in spread]
+        decided = [m > 2.0 * d for m, d in zip(margin, diff)]
+        out["reference_f64_attention_spread_per_position"] = [round(s, 4) for s in spread]
+        out["bound_per_position"] = [round(b, 4) for b in bound]
+        out["bound"] = (f"|fast - reference|_p <= {FAST_ABS} + {FAST_SPREAD} x s_p (s_p: the reference's own "
+                        "f16-vs-f64-attention spread at p); argmax = the reference's wherever its top-2 margin "
+                        "exceeds twice the difference")
+        out["ok"] = all(d <= b for d, b in zip(diff, bound)) and all(a for a, k in zip(agree, decided) if k)
+    return out
 
 
-def cpu_baseline(g, cfg, n_decode: int, gpu_ids=None, mean_ctx=None, ctx_prompt=None):
+def cpu_baseline(g, cfg, n_decode: int, mean_ctx=None, ctx_prompt=None):
     """BASELINE.md section 4 on this host: the reference's own Model::forward
     (oracle/_ref, built from its sources) -- or, where the reference is not
     built, the oracle restatement ("port") -- timed on a bounded sample.
@@ -216,9 +268,9 @@ def cpu_baseline(g, cfg, n_decode: int, gpu_ids=None, mean_ctx=None, ctx_prompt=
       rate extrapolated to the GPU run's mean context;
     * GEMV-only timings at the 4B shapes (mat_vec_mul / mat_vec_mul_fp16);
     * configs[0]: Gemma-3 1B Q4_0, --predict 64;
-    * the CPU's greedy ids vs the GPU's on the same prompt (gpu_ids);
     * at the GPU line's own context (ctx_prompt: the GPU run's prompt, one untimed Model::forward of it, then
-      8 timed greedy steps at its positions): a measurement, not the extrapolation."""
+      FORCED timed steps on teacher-forced tokens): a measurement, not the extrapolation; their logits are the
+      parity fixture of the GPU line."""
     from oracle import bind
     from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf, random_tensor
     from llm_inference_amd.gguf import TensorType as TT
@@ -237,6 +289,7 @@ def cpu_baseline(g, cfg, n_decode: int, gpu_ids=None, mean_ctx=None, ctx_prompt=
     out = {"cores": threads, "cpu_model": _cpu_model_name(), "compiler": "g++ -std=c++17 -O2 -DNDEBUG -mavx2 -mfma -mf16c (BUILD:41-53)"}
     runs = {}
     for n in (threads, max(1, threads // 2)):
+        progress(f"cpu baseline: decode sample on {n} threads")
         kind, eng = engine(n)
         m = model(eng, kind, g, n)
         lg = m.forward(np.array(prompt, np.int32), 0)
@@ -270,6 +323,7 @@ def cpu_baseline(g, cfg, n_decode: int, gpu_ids=None, mean_ctx=None, ctx_prompt=
             "unit": "tokens/s", "how": "step time = a + b * pos fitted to the measured per-step times"}
     # (bounded: the reference's T-token forward costs about T decode steps, so it runs when that is <= 40 s here)
     if ctx_prompt is not None and kind == "reference" and len(ctx_prompt) * float(np.median(per)) <= 40.0:
+        progress(f"cpu baseline: the GPU line's {len(ctx_prompt)}-token prompt on the reference")
         kind_c, eng_c = engine(threads)
         mc = model(eng_c, kind_c, g, threads)
         t0 = time.perf_counter()
@@ -290,12 +344,7 @@ def cpu_baseline(g, cfg, n_decode: int, gpu_ids=None, mean_ctx=None, ctx_prompt=
             "unit": "tokens/s", "threads": threads, "prefill_s": round(t_pf, 2),
             "how": f"the GPU line's prompt through one untimed Model::forward, then {FORCED} timed steps on "
                    "teacher-forced tokens (their logits: the parity check of the GPU line)"}
-    out["ids"] = ids
-    if gpu_ids is not None:
-        k = min(len(ids), len(gpu_ids))
-        same = [a == b for a, b in zip(ids[:k], gpu_ids[:k])]
-        out["id_check"] = {"steps": k, "identical": all(same),
-                           "first_difference": (same.index(False) if not all(same) else None)}
+    progress("cpu baseline: GEMV-only timings, configs[0]")
     # GEMV-only (the reference's mat_vec_mul, 4B shapes; BASELINE.md section 4 / SURVEY section 6)
     kind_t, eng = engine(threads)
     gemv = {}
@@ -381,19 +430,18 @@ def main():
             exchange = "rccl"
             m = rccl_model()
     info = m.info
-    rng = np.random.default_rng(99 + (0 if tp else d.rank))  # tensor-parallel ranks decode the same stream
-    prompt = np.concatenate([[2], rng.integers(4, cfg.vocab, a.prefill - 1)]).astype(np.int32)
+    prompt = bench_prompt(cfg, a.prefill, 0 if tp else d.rank)  # tensor-parallel ranks decode the same stream
+    progress(f"session ready; prefill {a.prefill} tokens")
     t0 = time.time()
     m.forward(prompt, 0, want_logits=False)
     t_prefill = time.time() - t0
     first = m.last_argmax
-    first_after_prefill, warm_ids = first, []
     pos = a.prefill
     if a.warmup:
         m.enqueue(first, pos, a.warmup)
         toks = m.sync(a.warmup)
-        warm_ids = toks.tolist()
         first, pos = int(toks[-1]), pos + a.warmup
+    progress(f"prefill {t_prefill:.3f} s; timed decode of {a.steps} steps")
     d.barrier()
     m.sync()
     t0 = time.perf_counter()
@@ -413,19 +461,14 @@ def main():
     # block reads the KV history at the position the decode loop ended on.
     L = info.n_layer
     fams = {}
-    # (with the layer engine the whole layer is ONE launch: info.layer_engine, family 6)
-    engine = bool(getattr(info, "layer_engine", 0))
-    ffn = bool(getattr(info, "ffn_engine", 0))
-    in_graph = {6: engine, 0: not engine, 7: ffn and not engine, 3: not (engine or ffn), 4: not (engine or ffn),
-                2: bool(info.screened_logits)}
-    for name, which, per_tok, kern in (("layer_engine", 6, L, "layer_engine_kernel"),
-                                       ("attention_block", 0, L, "attn_block_kernel"),
-                                       ("ffn_engine", 7, L, "ffn_engine_kernel"),
+    in_graph = {0: True, 3: True, 4: True, 2: bool(info.screened_logits)}
+    for name, which, per_tok, kern in (("attention_block", 0, L, "attn_block_kernel"),
                                        ("gate_up", 3, L, "gemv_q4_0_layer"),
                                        ("down", 4, L, "gemv_q4_0_layer"),
                                        ("token_selection", 2, 1, "screen_gemv_kernel")):
         if not in_graph[which]:  # only the families the timed graph launches
             continue
+        progress(f"kernel timing: {name}")
         us_f, by_f = m.time_kernel(which, a.kernel_reps if which != 2 else 8)
         if us_f <= 0:
             continue
@@ -436,7 +479,7 @@ def main():
     us_l, by_l = m.time_kernel(1, 2)
     dom_name = max(fams, key=lambda k: fams[k]["us_per_token"]) if fams else None
     dom = fams.get(dom_name, {})
-    kpat = {"layer_engine": "layer_engine_kernel", "ffn_engine": "ffn_engine_kernel", "attention_block": "attn_block_kernel", "gate_up": "gemv_q4_0_layer<8, 10, 10",
+    kpat = {"attention_block": "attn_block_kernel", "gate_up": "gemv_q4_0_layer<8, 10, 10",
             "down": "gemv_q4_0_layer<1, 10, 5", "token_selection": "screen_gemv_kernel"}.get(dom_name, "-")
     # the attention block's position-dependent stream: K and V rows of every kv head, per key attended
     kv_key = info.kv_bytes_per_pos / L if dom_name == "attention_block" else 0.0
@@ -534,21 +577,20 @@ def main():
     }
     # Exact mode in the same invocation (north_star: "bit-exact token ids for greedy decode"): a second session on
     # the exact-order engine (the reference's operation order), the same prompt, then the
-    # same timed decode; its first ids are checked against the reference's own (cpu_baseline, below) and the
-    # fast line's.  Single GPU only (exact mode has no tensor-parallel ranks).
-    exact_ids = None
+    # same timed decode; its logits on the parity fixture's inputs are checked against the reference's own
+    # (cpu_baseline, below).  Single GPU only.
     gpu_forced = {}
     if d.world == 1 and not a.no_cpu_baseline:  # this session's logits on the parity fixture's inputs
         gpu_forced["exact" if a.exact else "fast"] = forced_logits(m, prompt, cfg.vocab)
     if d.world == 1 and not a.exact and not a.no_exact:
+        progress("exact-mode session")
         mx = Model(g, device=dev, exact=True, max_ctx=max_ctx, use_graph=not a.no_graph)
         t0 = time.time()
         mx.forward(prompt, 0, want_logits=False)
         t_pf_x = time.time() - t0
-        n_chk = max(a.warmup, 8)  # the warmup steps double as the id check (positions prefill .. prefill + 7)
+        n_chk = max(a.warmup, 8)  # warmup steps (positions prefill .. prefill + n_chk - 1)
         mx.enqueue(mx.last_argmax, a.prefill, n_chk)
         wt = mx.sync(n_chk)
-        exact_ids = [mx.last_argmax] + wt.tolist()
         mx.sync()
         t0 = time.perf_counter()
         mx.enqueue(int(wt[-1]), a.prefill + n_chk, a.steps)
@@ -557,39 +599,44 @@ def main():
         xinfo = mx.get_info()
         gpu_forced["exact"] = forced_logits(mx, prompt, cfg.vocab) if not a.no_cpu_baseline else None
         mx.close()
-        fast_ids = [first_after_prefill] + warm_ids
-        k = min(len(fast_ids), len(exact_ids))
         out["exact"] = {
             "value": round(a.steps / el_x, 3), "unit": "tokens/s", "steps": a.steps,
             "ms_per_step": round(el_x * 1000.0 / a.steps, 4),
             "positions": f"{a.prefill + n_chk}-{a.prefill + n_chk + a.steps - 1}",
             "exact_engine": bool(getattr(xinfo, "exact_engine", 0)), "kernels_per_token": xinfo.kernels_per_token,
-            "prefill_s": round(t_pf_x, 3), "ids": exact_ids,
-            "fast_ids_agree": {"steps": k, "identical": fast_ids[:k] == exact_ids[:k]},
-            "how": "a second session with LLMI_EXACT (bit-identical to the reference's logits), the same prompt; "
-                   "first ids = argmax after the prompt + the first greedy steps; then the same timed decode"}
-    gpu_ids = None
-    if d.rank == 0 and d.world == 1 and not a.no_cpu_baseline:
-        # the CPU sample's prompt on the GPU too: the same greedy ids?
-        cp = np.array([2] + list(range(100, 107)), np.int32)
-        lg = m.forward(cp, 0, want_logits=False)
-        gpu_ids = [m.last_argmax] + m.generate(m.last_argmax, len(cp), a.cpu_decode).tolist()
+            "prefill_s": round(t_pf_x, 3),
+            "how": "a second session with LLMI_EXACT (bit-identical to the reference's logits: "
+                   "parity_vs_reference.exact), the same prompt, then the same timed decode"}
+    parity_ok = True
     if d.rank == 0 and d.world == 1 and not a.no_cpu_baseline:
         m.close()
         try:
-            out["cpu_baseline"] = cpu_baseline(g, cfg, a.cpu_decode, gpu_ids, mean_ctx, ctx_prompt=prompt)
+            progress("cpu baseline (the reference on the host cores)")
+            out["cpu_baseline"] = cpu_baseline(g, cfg, a.cpu_decode, mean_ctx, ctx_prompt=prompt)
         except Exception as e:  # report, never hide
             out["cpu_baseline"] = {"error": repr(e)}
         ref_lg = out["cpu_baseline"].pop("_ref_forced_logits", None)
+        key = parity_key(a.config, a.quant, a.prefill)
+        spread = load_spread(key)
         if ref_lg is not None:  # device logits vs the reference's own on the same prompt + teacher-forced tokens
             out["parity_vs_reference"] = {
-                k: parity(ref_lg, v) for k, v in gpu_forced.items() if v is not None}
+                k: parity(ref_lg, v, spread, exact=(k == "exact")) for k, v in gpu_forced.items() if v is not None}
             out["parity_vs_reference"]["how"] = (
                 f"the reference (oracle/_ref: its own ops.cpp / model.cpp) and the device sessions on the GPU line's "
-                f"prompt, then {FORCED} teacher-forced tokens: logits compared bit for bit at each of the "
-                f"{FORCED + 1} positions (exact: the reference's operation order; fast: fp32 reassociation)")
+                f"prompt, then {FORCED} teacher-forced tokens, logits compared at each of the {FORCED + 1} positions "
+                f"(exact: the reference's operation order, every bit; fast: fp32 reassociation, within `bound`); "
+                f"the fast session ran the whole timed decode loop and the kernel timing before, so a result that "
+                f"depends on what ran before shows here")
+            out["parity_vs_reference"]["conditioning"] = (
+                f"tests/golden/bench_conditioning.json[{key}]" if spread is not None else
+                f"no committed conditioning for {key}: the fast path is reported, not gated")
+            parity_ok = all(v.get("ok", True) for k, v in out["parity_vs_reference"].items() if isinstance(v, dict))
+            out["parity_vs_reference"]["ok"] = parity_ok
     if d.rank == 0:
         print(json.dumps(out), flush=True)
+    if not parity_ok:  # the line is printed (the record), but a result outside its stated bound fails the run
+        print("[bench] parity_vs_reference outside its stated bound", file=sys.stderr)
+        sys.exit(3)
 
 
 if __name__ == "__main__":

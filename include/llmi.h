@@ -207,9 +207,9 @@ typedef struct {
   size_t screen_bytes;        /* bytes of the int8 screening table streamed per decode-loop token */
   int prefill_f16_redo;       /* opt-in f16 prefills (LLMI_PREFILL_F16) whose f16 activations overflowed and were
                                  recomputed on the int8 path (never a non-finite result) */
-  int layer_engine;           /* 1: each decode layer is ONE launch of the layer engine (one 1024-thread work-group
-                                 per CU, the layer's weights issued at launch start: DESIGN.md section 4.3) */
-  int ffn_engine;             /* 1: gate_up + GELU + down of each layer are ONE launch (the FFN engine) */
+  int layer_engine;           /* always 0: the round-3 layer engine (one launch per decode layer) measured slower
+                                 than three launches and was removed in round 6 */
+  int ffn_engine;             /* always 0: the FFN engine (gate_up + GELU + down as one launch), likewise */
   int tp_exchange;            /* tensor-parallel exchange: 0 none, 1 RCCL, 2 device copies, 3 one-shot push, 4 one-shot
                                  push fused into the decode launches (the default push mode) */
   long long block_slow_waits; /* attention-block hand-off waits (per wave) that took over 20 us, since creation */
@@ -226,8 +226,7 @@ int llmi_session_get_info(const llmi_session* s, llmi_session_info* info);
  *   1 = F16 logits GEMV, 2 = the decode loop's screened token selection,
  *   3 = gate_up (+ norm prologue + GELU), 4 = down (+ Q8_0 prologue),
  *   5 = qkv / o / gate_up / down as standalone layer GEMVs (round-1 family),
- *   6 = the layer engine (one launch per decode layer: qkv + attention + o + gate_up + down),
- *   7 = the FFN engine (gate_up + GELU + down, one launch per layer).
+ *   6, 7 = the removed layer / FFN engines (always 0 / 0).
  * Returns the mean microseconds and the mean algorithmic bytes per launch
  * (0 / 0 when the family does not exist on this session). */
 int llmi_session_time_kernel(llmi_session* s, int which, int reps, double* us_per_launch, double* bytes_per_launch);
@@ -236,7 +235,9 @@ int llmi_session_time_kernel(llmi_session* s, int which, int reps, double* us_pe
  *   0 = every f32 bit pattern through the hardware f32 -> f16 conversion vs the reference's f32_to_f16
  *       (gguf.cpp:68-95): out[0] non-NaN mismatches, out[1] NaN mismatches, out[2] first non-NaN mismatch;
  *   1 = the exact engine's speculative rms_norm sum-of-squares chain vs the serial chain (ops.cpp:33-36) on 8192
- *       vectors of 2560: out[0] differing results (must be 0), out[1] segments recomputed serially. */
+ *       vectors of 2560: out[0] differing results (must be 0), out[1] segments recomputed serially;
+ *   2 = (no GPU work) the sessions' device memory: out[0] bytes allocated, out[1] bytes released and kept for
+ *       reuse, out[2] bytes held back while sessions were constructed concurrently. */
 int llmi_selftest(int which, unsigned long long* out);
 
 #ifdef __cplusplus

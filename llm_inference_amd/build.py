@@ -18,7 +18,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OBJ = os.path.join(HERE, "_build")
 LIB = os.path.join(HERE, "libllmi.so")
-SOURCES = ["k_gemv.hip", "k_layer.hip", "k_engine.hip", "k_elem.hip", "k_attn.hip", "k_session.hip", "k_prefill.hip", "k_logits.hip", "k_exchange.hip", "k_exact.hip", "session.cpp", "collective.cpp", "capi.cpp"]
+SOURCES = ["k_gemv.hip", "k_layer.hip", "k_elem.hip", "k_attn.hip", "k_session.hip", "k_prefill.hip", "k_logits.hip", "k_exchange.hip", "k_exact.hip", "session.cpp", "collective.cpp", "capi.cpp"]
 HEADERS = ["common.h", "kernels.h", "attn.h", "layer_body.h", "session_kernels.h", "session.h", "gguf_reader.h", "collective.h",
            "exact.h", "px.h", "glibc_math.h", "spec_chain.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -51,11 +51,6 @@ def _compile(src: str) -> str:
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr[-4000:]}")
     return out
-
-
-# the measured-slower layer / FFN engines: only in the development variant that defines LLMI_DEV_ENGINES
-if "-DLLMI_DEV_ENGINES" not in FLAGS:
-    SOURCES = [s for s in SOURCES if s != "k_engine.hip"]
 
 
 def build(force: bool = False, jobs: int = 0) -> str:

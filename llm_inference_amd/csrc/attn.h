@@ -63,6 +63,5 @@ bool attn_block_supported(const DevWeight& wqkv, const DevWeight* wqkv_b, const 
 int launch_attn_block(const DevWeight& wqkv, const DevWeight* wqkv_b, LayerGemv qg, int qrole, const DevWeight& wo,
                        LayerGemv og,
                        const AttnArgs& aa, const QKVArgs& qa, BlockSync bs, hipStream_t s);
-void launch_bump_epoch(unsigned* epoch, hipStream_t s);
 
 }  // namespace llmi

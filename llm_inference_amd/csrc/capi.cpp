@@ -498,6 +498,12 @@ int llmi_selftest(int which, unsigned long long* out) {
       exact_selftest_chain(r);
       out[0] = r[0];
       out[1] = r[1];
+    } else if (which == 2) {
+      size_t live = 0, cached = 0, grave = 0;
+      dev_mem_stats(&live, &cached, &grave);
+      out[0] = live;
+      out[1] = cached;
+      out[2] = grave;
     } else {
       throw status_error(LLMI_E_ARG, "selftest: unknown test");
     }

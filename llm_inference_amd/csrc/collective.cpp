@@ -64,8 +64,8 @@ uint64_t px_timeout_ticks() {  // LLMI_PX_TIMEOUT_MS (default 10 s): the bound o
 // inside one process on one device.
 class Mailbox {
  public:
-  static constexpr int kCap = (1 << 18) - PX_MAX_CS;  // words per rank slot (~1 MB of payload): every decode exchange in one
-  static constexpr size_t kSlot = (size_t)kCap + PX_MAX_CS;  // words, then checksum granules (px.h)
+  static constexpr int kCap = (1 << 18) - PX_CS_RING * PX_MAX_CS;  // words per rank slot (~1 MB of payload): every decode exchange in one
+  static constexpr size_t kSlot = (size_t)kCap + PX_CS_RING * PX_MAX_CS;  // words, then checksum granules (px.h)
   // zeroed on the owning session's stream and complete on return (a null-stream hipMemset is not ordered with the
   // session's non-blocking stream)
   Mailbox(int rank, int G, hipStream_t s) : rank_(rank), G_(G), timeout_(px_timeout_ticks()), s_(s) {

@@ -81,7 +81,7 @@ class Collective {
 constexpr int PX_MAX_WG = 64;  // work-groups per exchange launch (= checksum granules per sender slot)
 constexpr int PX_PUSH = 1, PX_GATHER = 2;
 struct PushArgs {
-  uint2* mail[PX_MAX_RANKS];  // every rank's mailbox [2][G][cap + PX_MAX_CS] granules (this process's mapping)
+  uint2* mail[PX_MAX_RANKS];  // every rank's mailbox [2][G][cap + PX_CS_RING * PX_MAX_CS] granules (this process's mapping)
   uint32_t* buf;              // word j of rank q's message at buf + q * stride + j (row_w == 0), or at
   size_t stride;              // buf + (j / row_w) * pitch + q * row_w + j % row_w (column slices of rows)
   size_t pitch;

@@ -802,7 +802,7 @@ void launch_attention(const AttnArgs& a, bool exact, hipStream_t s, const QKVArg
 // re-load the block granules.  So the o weights and the K/V history stream
 // while the qkv GEMV runs, and no hand-off waits on a drain or a counter.
 // The tag is the layer's launch count + 1 (BlockSync::epoch, advanced by the
-// gate_up launch that follows); waits are bounded (a timeout sets bs.err, the
+// launch's last retiring work-group: block_retire); waits are bounded (a timeout sets bs.err, the
 // host reports it).  Numerics are those of the three separate kernels (same
 // bodies, same per-row order) except the o rows' lane order (R4).
 // ---------------------------------------------------------------------------
@@ -821,39 +821,55 @@ constexpr size_t block_attn_lds() {  // s_k + s_v (32-key tiles) + s_red
 constexpr int WT_W8 = 3;  // Q8_0 weights in the block (layer_body W8), beside the kq formats WT_Q4_K / WT_Q6_K
 
 // PXF: the qkv prologue / o epilogue honour the fused exchange (tensor-parallel ranks; layer_body PXF)
+// The launch's own tag advance (BlockSync::epoch / done): every work-group, once all its threads are past their
+// last granule access, adds one to *done; the one that completes the count resets it and advances the epoch.
+// Every work-group read the epoch at its start and the last one to retire is, by the count, after all of them,
+// so the tag changes exactly once per launch and only when no work-group of the launch can still read it.
+__device__ __forceinline__ void block_retire(const BlockSync& bs) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add(bs.done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == gridDim.x - 1u) {
+      __hip_atomic_store(bs.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(bs.epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 template <int HD, int G, int QR, int QP, int QE, int QROLE, int OR, int OP, int OE, int WTQ = 0, int WTQB = 0,
           int WTO = 0, int KVD = 1, int NS = ATTN_NSPLIT, bool PXF = false>
 __global__ __launch_bounds__(256) void attn_block_kernel(LayerGemv qg, LayerGemv og, AttnArgs aa, QKVArgs qa,
                                                         BlockSync bs, int nq, LayerGemv qgb, int nqa) {
   extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
   int b = blockIdx.x;
+  const int na = aa.n_head_kv * NS;
   if (b < nq) {
+    bool second = false;
     if constexpr (WTQB != 0) {
       if (b >= nqa) {
+        second = true;
         BlockSync bsb = bs;
         bsb.g_qkv += qg.rows;
         layer_body<QR, 4, QP, QE, QROLE, false, true, SYNC_SIG, 0, false, WTQB == WT_W8 ? 0 : WTQB>(qgb, b - nqa, s_dyn, bsb);
-        return;
       }
     }
-    layer_body<QR, 4, QP, QE, QROLE, false, true, SYNC_SIG, 0, WTQ == WT_W8, WTQ == WT_W8 ? 0 : WTQ, 0, PXF>(qg, b, s_dyn,
-                                                                                                         bs);
-    return;
-  }
-  b -= nq;
-  const int na = aa.n_head_kv * NS;
-  if (b < na) {
+    if (!second)
+      layer_body<QR, 4, QP, QE, QROLE, false, true, SYNC_SIG, 0, WTQ == WT_W8, WTQ == WT_W8 ? 0 : WTQ, 0, PXF>(qg, b, s_dyn,
+                                                                                                           bs);
+  } else if (b - nq < na) {
+    b -= nq;
     constexpr int KS = attn_ks<HD, G>();
     uint16_t* s_k = reinterpret_cast<uint16_t*>(s_dyn);
     uint16_t* s_v = s_k + 32 * KS;
     float* s_red = reinterpret_cast<float*>(s_v + 32 * HD);
     // KVD > 1: aa.n_head_kv counts virtual kv heads (G q heads each, KVD per cache head)
     attn_split_body<HD, G, true, 32, true, KVD, NS>(aa, qa, s_k, s_v, s_red, b % aa.n_head_kv, b / aa.n_head_kv, bs);
-    return;
+  } else {
+    b -= nq + na;
+    layer_body<OR, 4, OP, OE, ROLE_PLAIN, false, true, SYNC_WAIT, 0, WTO == WT_W8, WTO == WT_W8 ? 0 : WTO, 0, PXF>(og, b, s_dyn,
+                                                                                                            bs);
   }
-  b -= na;
-  layer_body<OR, 4, OP, OE, ROLE_PLAIN, false, true, SYNC_WAIT, 0, WTO == WT_W8, WTO == WT_W8 ? 0 : WTO, 0, PXF>(og, b, s_dyn,
-                                                                                                          bs);
+  block_retire(bs);
 }
 
 using BlockFn = void (*)(dim3, size_t, const LayerGemv&, const LayerGemv&, const AttnArgs&, const QKVArgs&,
@@ -973,12 +989,6 @@ void fill_gemv(const DevWeight& w, LayerGemv& a) {
 
 }  // namespace
 
-__global__ void bump_epoch_kernel(unsigned* e) { *e += 1u; }
-void launch_bump_epoch(unsigned* e, hipStream_t s) {  // bench: a fresh granule tag between timed block launches
-  hipLaunchKernelGGL(bump_epoch_kernel, dim3(1), dim3(1), 0, s, e);
-  LLMI_HIP(hipGetLastError());
-}
-
 // grid and dynamic LDS of one attention-block launch (qkv WGs, attention WGs, o WGs)
 struct BlockGeom {
   int nq, na, no;
@@ -1047,7 +1057,7 @@ int launch_attn_block(const DevWeight& wqkv, const DevWeight* wqkv_b, LayerGemv 
                                       wt_of_w(&wo));
   if ((c.wto == WT_Q4_K || c.wto == WT_Q6_K) != (aa.q8k != 0))
     throw std::runtime_error("attention block: a kq o projection reads Q8_K blocks (and only it)");
-  if (!bs.epoch || !bs.g_qkv || !bs.g_xo || !bs.err || !aa.q8 || !aa.partial || !aa.ticket || !qa.qkv ||
+  if (!bs.epoch || !bs.done || !bs.g_qkv || !bs.g_xo || !bs.err || !aa.q8 || !aa.partial || !aa.ticket || !qa.qkv ||
       qa.qkv != qg.out)
     throw std::runtime_error("attention block: missing buffers");
   if (qrole == ROLE_PRO ? (!qg.y || !qg.resid_in || !qg.resid_out || !qg.w_next || qg.resid_in == qg.resid_out)

@@ -58,7 +58,8 @@ __global__ __launch_bounds__(PX_T) void push_exchange_kernel(PushArgs a) {
   __syncthreads();
   const uint32_t tag = s_tag;
   const size_t half = tag & 1u;
-  const size_t slot_w = (size_t)a.cap + PX_MAX_CS;  // granules per sender slot: words, then checksums
+  const size_t slot_w = (size_t)a.cap + PX_CS_RING * PX_MAX_CS;  // granules per sender slot: words, then checksums
+  const size_t cs = px_cs((uint32_t)a.cap, tag);                  // this exchange's checksum region (px.h)
   const int per = (a.words + gridDim.x - 1) / gridDim.x;
   const int w0 = blockIdx.x * per, n = max(0, min(a.words, w0 + per) - w0);
   auto word = [&](int q, int i) -> uint32_t* {  // word i of this exchange in rank q's part of the buffer
@@ -77,7 +78,7 @@ __global__ __launch_bounds__(PX_T) void push_exchange_kernel(PushArgs a) {
     }
     atomicAdd(&s_sum[0], sum);
     __syncthreads();
-    if (t < a.G) px_store(a.mail[t] + slot + a.cap + blockIdx.x, s_sum[0], tag);
+    if (t < a.G) px_store(a.mail[t] + slot + cs + blockIdx.x, s_sum[0], tag);
     __syncthreads();
     if (t == 0) s_sum[0] = 0;
     __syncthreads();
@@ -139,8 +140,8 @@ __global__ __launch_bounds__(PX_T) void push_exchange_kernel(PushArgs a) {
     __syncthreads();
     // every peer's checksum granule for this work-group's words
     if (t < a.G && t != a.rank && n > 0) {
-      const uint2* cs = mine + (half * a.G + t) * slot_w + a.cap + blockIdx.x;
-      uint64_t g = px_load(cs);
+      const uint2* csg = mine + (half * a.G + t) * slot_w + cs + blockIdx.x;
+      uint64_t g = px_load(csg);
       while ((uint32_t)(g >> 32) != tag && !late) {
         if (wall_clock64() - t0 > a.timeout) {
           late = true;  // (diagnostics: word -1 - peer = that peer's checksum granule)
@@ -154,7 +155,7 @@ __global__ __launch_bounds__(PX_T) void push_exchange_kernel(PushArgs a) {
           break;
         }
         __builtin_amdgcn_s_sleep(1);
-        g = px_load(cs);
+        g = px_load(csg);
       }
       if (!late && (uint32_t)g != s_sum[t]) __hip_atomic_store(a.err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }

@@ -36,8 +36,6 @@ template <int R, int NW, int P, int E, int ROLE, bool MULTI, bool EARLY, int PE 
           int RW = 0, bool PXF = false>
 __global__ __launch_bounds__(NW * 64 + (role_help(ROLE) ? E * 64 : 0)) void gemv_q4_0_layer(LayerGemv a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
-  // the attention block's granule tag of this layer, for its next launch
-  if (a.epoch && blockIdx.x == 0 && threadIdx.x == 0) *a.epoch += 1u;
   layer_body<R, NW, P, E, ROLE, MULTI, EARLY, 0, PE, W8, WT, RW, PXF>(a, blockIdx.x, s_dyn, BlockSync{});
 }
 
@@ -182,9 +180,6 @@ const LayerCfg kLayerCfgs[] = {
     // work-group of the tp-8 rank's 84; P does not change a row's pass order: 2.12-2.13 vs 2.08 ms per rank token,
     // and the 2-row-wave qkv shard 2.13; not kept)
     LLMI_LCFG(168, ROLE_GELU, 8, 8, 4, 11, true, false, 1),    // 27B 43008 rows, H 32 -> 672 WGs
-#ifdef LLMI_DEV_ENGINES  // LLMI_GELU_X (development variant): 27B gate_up on the norm launch's x blocks
-    LLMI_LCFG(168, ROLE_GELU_X, 8, 8, 4, 1, true, false, 1),
-#endif
     // PLAIN down: the GELU launch (32 units per work-group) wrote the Q8_0 blocks (LayerGemv::hq), so the down
     // launch copies 24-42 KB of blocks instead of quantizing the whole f32 hid in every work-group
     // (scripts/gemv_sweep 27b.down: plain R1 NW8 P6 15.0 us vs quant 19.5 us)
@@ -337,7 +332,6 @@ void launch_layer_gemv2(const DevWeight& wa, const DevWeight& wb, LayerGemv a, i
   b.out = a.out + wa.rows;
   b.resid_out = nullptr;
   b.xn_out = nullptr;
-  b.epoch = nullptr;
   const int rpw = c.NW * c.R, nwa = wa.rows / rpw, nwb = (wb.rows + rpw - 1) / rpw;
   const size_t lds = (size_t)nb * sizeof(XBlock) + 16 + (role == LAYER_PRO ? (size_t)wa.cols * 4 : 0);
   c.fn2(dim3(nwa + nwb), lds, a, b, nwa, s);

@@ -59,19 +59,22 @@ bool gemv_type_supported(uint32_t type) {
          type == T_BF16;
 }
 
-// Device memory of the sessions.  (1) It goes back to reuse only while no OTHER
-// session of the process is alive: with several sessions in one process (the one-GPU tensor-parallel group),
-// memory one session freed and another reallocated at the same time was read wrong on its first use -- one word
-// of a weight row, right on every later read (a one-GPU 4-rank group: 8 of 23 lifetimes; 0 of 2,868 with the
-// frees held back, scripts/dev/tp_diag.py); frees made while other sessions live wait in a graveyard released
-// when the last session ends.  (2) Released blocks stay mapped: they are kept by size and handed to the next
+// Device memory of the sessions.  (1) While a session is being CONSTRUCTED and
+// another is alive, released memory does not go back to reuse: with several sessions constructed together in one
+// process (the one-GPU tensor-parallel group), memory one session freed and another reallocated at the same time
+// was read wrong on its first use -- one word of a weight row, right on every later read (a one-GPU 4-rank group:
+// 8 of 23 lifetimes; 0 of 2,868 with the frees held back, scripts/dev/tp_diag.py).  Such frees wait in a
+// graveyard released when the last construction ends (round 6: was the last session's end, which let a
+// long-lived session plus repeatedly created and closed ones grow device memory without bound).  (2) Released blocks stay mapped: they are kept by size and handed to the next
 // allocation of that size instead of hipFree + hipMalloc (a 4-rank group constructed after a whole-model session
 // closed still read 0.012-off logits once in a full suite run: the same signature); the cache is returned to
 // the allocator when an allocation fails or it exceeds kCacheCap.
 namespace {
 std::mutex g_mem_mu;
 int g_live_sessions = 0;
+int g_constructing = 0;            // sessions between session_live(+1) and session_constructed()
 std::vector<void*> g_graveyard;
+size_t g_grave_bytes = 0;
 std::unordered_map<void*, size_t> g_sizes;       // live blocks from dev_alloc: rounded size
 std::unordered_multimap<size_t, void*> g_cache;  // released blocks, still mapped
 size_t g_cached = 0;
@@ -116,20 +119,47 @@ void* dev_alloc(size_t bytes) {
   return p;
 }
 
+namespace {
+void flush_graveyard_locked() {
+  for (void* p : g_graveyard) release_locked(p);
+  g_graveyard.clear();
+  g_grave_bytes = 0;
+}
+}  // namespace
+
 void dev_free(void* p) {
   if (!p) return;
   std::lock_guard<std::mutex> lk(g_mem_mu);
-  if (g_live_sessions > 1) g_graveyard.push_back(p);
-  else release_locked(p);
+  if (g_constructing > 0 && g_live_sessions > 1) {
+    g_graveyard.push_back(p);
+    auto it = g_sizes.find(p);
+    g_grave_bytes += it != g_sizes.end() ? it->second : 0;
+  } else {
+    release_locked(p);
+  }
 }
 
 void session_live(int delta) {
   std::lock_guard<std::mutex> lk(g_mem_mu);
   g_live_sessions += delta;
-  if (g_live_sessions == 0) {
-    for (void* p : g_graveyard) release_locked(p);
-    g_graveyard.clear();
-  }
+  if (delta > 0) g_constructing += delta;
+  if (g_constructing == 0 || g_live_sessions == 0) flush_graveyard_locked();
+}
+
+void session_constructed(bool ok) {  // the end of a constructor (ok) or of a failed one (its release ran first)
+  std::lock_guard<std::mutex> lk(g_mem_mu);
+  if (g_constructing > 0) g_constructing--;
+  if (g_constructing == 0) flush_graveyard_locked();
+  (void)ok;
+}
+
+void dev_mem_stats(size_t* live, size_t* cached, size_t* grave) {
+  std::lock_guard<std::mutex> lk(g_mem_mu);
+  size_t n = 0;
+  for (const auto& kv : g_sizes) n += kv.second;
+  *live = n;
+  *cached = g_cached;
+  *grave = g_grave_bytes;
 }
 
 // Upload `rows` rows of a GGUF weight (host bytes in block layout) to the

@@ -16,11 +16,15 @@
 // finished reading n.
 //
 // Self-check (round 5): every producing work-group also pushes ONE checksum granule -- the sum of
-// px_term(word, rank, index) over the words it pushed -- at granule cs0 + its index of the slot, and the first
+// px_term(word, rank, index) over the words it pushed -- at granule px_cs(tag) + its index of the slot, and the first
 // PX_CHECK_WG work-groups of every consuming launch (at least one per XCD when work-groups are dealt round-robin)
 // sum the same terms over every word they read and compare with the sum of all producers' checksum granules
 // (px_in_nwg per rank): a stale, torn or foreign word sets *err = 2 (the session raises LLMI_E_HIP and refuses
 // further work) instead of reaching the logits.
+// The checksum granules are read LATER than the words: a verifying work-group checks them when it retires, after
+// its launch has pushed its own words of exchange n + 1 -- so a peer may already have read n + 1 and pushed n + 2
+// (ADVICE r5).  n + 2 shares n's half, so the checksums take a second ring level on the tag's next bit: n + 2's
+// land beside n's, and n + 4 (their next user) needs this rank's push of n + 3, which only a later launch makes.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -31,6 +35,7 @@ namespace llmi {
 constexpr int PX_MAX_RANKS = 16;
 constexpr int PX_MAX_CS = 1024;  // checksum granules per sender slot: producing work-groups of one exchange
 constexpr int PX_CHECK_WG = 8;   // consuming work-groups per launch that verify the checksums
+constexpr int PX_CS_RING = 2;    // checksum regions per half (selected by tag bit 1; see above)
 
 // a rank's mailboxes as its launches see them (device-resident, one per session); an exchange is (k, ws): its
 // number within the step and its words per rank (word W of the whole vector is rank W / ws's word W % ws)
@@ -42,9 +47,15 @@ struct PxLink {
                               // expected tag; 2: a checksum mismatch (err[3]: the tag, err[4]/[5]: read/expected sum)
   uint64_t timeout;           // bound of every wait, ticks of the 100 MHz wall clock
   uint32_t slot_w;            // granules per sender slot
-  uint32_t cs0;               // first checksum granule of a slot (words [0, cs0), checksums [cs0, slot_w))
+  uint32_t cs0;               // first checksum granule of a slot (words [0, cs0), checksums [cs0, slot_w):
+                              // PX_CS_RING regions of PX_MAX_CS)
   int rank, G;
 };
+
+// the checksum region of exchange `tag` within its half's slots (granule offset from the slot start)
+__host__ __device__ __forceinline__ uint32_t px_cs(uint32_t cs0, uint32_t tag) {
+  return cs0 + ((tag >> 1) & 1u) * (uint32_t)PX_MAX_CS;
+}
 
 #ifdef __HIPCC__
 __device__ __forceinline__ uint32_t px_link_tag(const PxLink& l, int k) {
@@ -129,14 +140,14 @@ __device__ __forceinline__ uint32_t px_wg_add(uint32_t v, uint32_t* s) {
 __device__ __forceinline__ void px_push_checksum(const PxLink& l, uint32_t tag, int bid, uint32_t cs, uint32_t* s) {
   const uint32_t tot = px_wg_add(cs, s);
   if ((int)threadIdx.x < l.G) {
-    const size_t slot = ((size_t)(tag & 1u) * l.G + l.rank) * l.slot_w + l.cs0 + (size_t)bid;
+    const size_t slot = ((size_t)(tag & 1u) * l.G + l.rank) * l.slot_w + px_cs(l.cs0, tag) + (size_t)bid;
     __hip_atomic_store(reinterpret_cast<uint64_t*>(l.mail[threadIdx.x] + slot), ((uint64_t)tag << 32) | tot,
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
 // consumer: the terms of every word this work-group read (cs) against the nwg checksum granules of every rank
-// (s: two zeroed LDS words, as px_wg_add)
+// (s: zeroed LDS words, as px_wg_add: s[0], s[1] the sums, s[2] the timeout flag, s[3..] diagnostics)
 // (where: the consumer's role * 1000 + the exchange's number in the step, and its work-group: err[1] / err[2])
 __device__ __forceinline__ void px_verify(const PxLink& l, uint32_t tag, int nwg, uint32_t cs, uint32_t* s, int where,
                                           int bid, int ws, int nwords) {
@@ -145,12 +156,13 @@ __device__ __forceinline__ void px_verify(const PxLink& l, uint32_t tag, int nwg
   const uint64_t t0 = wall_clock64();
   for (int i = threadIdx.x; i < l.G * nwg; i += blockDim.x) {
     const int q = i / nwg, b = i - q * nwg;
-    const uint64_t* g =
-        reinterpret_cast<const uint64_t*>(l.mail[l.rank] + ((size_t)(tag & 1u) * l.G + q) * l.slot_w + l.cs0 + b);
+    const uint64_t* g = reinterpret_cast<const uint64_t*>(l.mail[l.rank] + ((size_t)(tag & 1u) * l.G + q) * l.slot_w +
+                                                          px_cs(l.cs0, tag) + b);
     uint64_t x = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     while ((uint32_t)(x >> 32) != tag) {
       if (wall_clock64() - t0 > l.timeout) {
         px_timeout(l, (uint32_t)(x >> 32), tag, -1 - b);
+        __hip_atomic_store(s + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         break;
       }
       __builtin_amdgcn_s_sleep(1);
@@ -158,8 +170,9 @@ __device__ __forceinline__ void px_verify(const PxLink& l, uint32_t tag, int nwg
     }
     want += (uint32_t)x;
   }
-  want = px_wg_add(want, s + 1);
-  if (want != got) {  // (uniform, rare) diagnostics: the whole vector and the checksums read once more, per sender
+  want = px_wg_add(want, s + 1);  // (its barrier also orders the timeout flag)
+  const bool timed_out = *(volatile uint32_t*)(s + 2) != 0u;  // reported as a timeout (err 3), not as a mismatch
+  if (!timed_out && want != got) {  // (uniform, rare) diagnostics: the whole vector and the checksums read once more, per sender
     uint32_t* sg = s + 4;                 // [G] words' terms read again, per sender
     uint32_t* sw = s + 4 + PX_MAX_RANKS;  // [G] checksum granules read again, per sender
     uint32_t other = 0;
@@ -174,7 +187,8 @@ __device__ __forceinline__ void px_verify(const PxLink& l, uint32_t tag, int nwg
     for (int i = threadIdx.x; i < l.G * nwg; i += blockDim.x) {
       const int q = i / nwg, b = i - q * nwg;
       const uint64_t x = __hip_atomic_load(
-          reinterpret_cast<const uint64_t*>(l.mail[l.rank] + ((size_t)(tag & 1u) * l.G + q) * l.slot_w + l.cs0 + b),
+          reinterpret_cast<const uint64_t*>(l.mail[l.rank] + ((size_t)(tag & 1u) * l.G + q) * l.slot_w +
+                                            px_cs(l.cs0, tag) + b),
           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __hip_atomic_fetch_add(sw + q, (uint32_t)x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       if ((uint32_t)(x >> 32) != tag) {
@@ -199,7 +213,7 @@ __device__ __forceinline__ void px_verify(const PxLink& l, uint32_t tag, int nwg
       __hip_atomic_fetch_or(l.err + 9, 1 << (bid & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
-  if (threadIdx.x == 0 && want != got) {
+  if (threadIdx.x == 0 && !timed_out && want != got) {
     __hip_atomic_store(l.err + 1, where, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(l.err + 2, bid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(l.err + 3, (int)tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -70,7 +70,7 @@ float* Session::dev_f32_copy(const GGUFView& g, const GTensor* t, int n) {
   if (!t) return nullptr;
   if (t->type != T_F32) throw status_error(LLMI_E_TYPE, "norm weight " + t->name + " is not F32");
   if ((int)t->shape[0] < n) throw status_error(LLMI_E_SIZE, "norm weight " + t->name + " too short");
-  float* d = dalloc<float>(t->shape[0] + 256);  // + 1 KB: the layer engine copies norm vectors in whole 1-KB pieces
+  float* d = dalloc<float>(t->shape[0] + 256);  // + 1 KB of slack past the vector
   h2d(d, g.tensor_data(*t), t->shape[0] * 4);
   return d;
 }
@@ -538,6 +538,7 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
   LLMI_HIP(hipSetDevice(opts.device));
   session_live(+1);  // (release() ends it: every path out of here, normal or not, runs release())
   live_ = true;
+  constructing_ = true;
   try {
     LLMI_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     if (tp_) {
@@ -619,6 +620,7 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
         maxhd0 = std::max(maxhd0, l.hd);
       }
       blk_epoch_ = dalloc<unsigned>(hp_.n_layer);
+      blk_done_ = dalloc<unsigned>(1);
       blk_gqkv_stride_ = (size_t)maxrows;
       blk_gxo_stride_ = (size_t)nh_ * maxhd0 / 32 * 12;
       blk_gqkv_ = dalloc<uint2>((size_t)hp_.n_layer * blk_gqkv_stride_);
@@ -632,9 +634,9 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
       for (const auto& l : L_) maxhd = std::max(maxhd, l.hd);
       blk_xo_ = dalloc<XBlock>((size_t)nh_ * maxhd / 32 + 1);
     }
-    setup_engine(g);
-    if (!engine_) setup_ffn_engine(g);
     LLMI_HIP(hipStreamSynchronize(stream_));  // every zeroing and copy above complete before the first call
+    constructing_ = false;
+    session_constructed(true);
   } catch (const gguf_error& e) {
     release();
     throw status_error(LLMI_E_GGUF, e.what());
@@ -650,14 +652,12 @@ void Session::release() {
   // nothing of this session may still run when its graphs and memory go (a broken session's kernels may still be
   // spinning up to LLMI_PX_TIMEOUT_MS; enqueue() without sync() leaves work in flight): drain, errors ignored
   if (stream_) (void)hipStreamSynchronize(stream_);
-  if (graph_exec_) (void)hipGraphExecDestroy(graph_exec_);
-  if (graph_) (void)hipGraphDestroy(graph_);
-  graph_exec_ = nullptr;
-  graph_ = nullptr;
-  if (graph_gen_exec_) (void)hipGraphExecDestroy(graph_gen_exec_);
-  if (graph_gen_) (void)hipGraphDestroy(graph_gen_);
-  graph_gen_exec_ = nullptr;
-  graph_gen_ = nullptr;
+  for (int k = 0; k < N_STEP_KINDS; k++) {
+    if (graph_execs_[k]) (void)hipGraphExecDestroy(graph_execs_[k]);
+    if (graphs_[k]) (void)hipGraphDestroy(graphs_[k]);
+    graph_execs_[k] = nullptr;
+    graphs_[k] = nullptr;
+  }
   free_screen_table(scr_);
   for (auto& l : L_) {
     for (XlWeight* x : {&l.xqkv, &l.xo, &l.xgu, &l.xdn}) free_xl_weight(*x);
@@ -669,13 +669,6 @@ void Session::release() {
     free_weight(l.ple_proj.w);
   }
   L_.clear();
-  for (auto& e : eng_w_) {
-    free_weight(e.q);
-    free_weight(e.o);
-    free_weight(e.g);
-    free_weight(e.d);
-  }
-  eng_w_.clear();
   for (auto& p : ple_model_proj_) free_weight(p.w);
   ple_model_proj_.clear();
   ple_table_ = DevWeight{};  // its bytes are an allocs_ entry
@@ -689,6 +682,8 @@ void Session::release() {
   coll_.reset();
   if (stream_) (void)hipStreamDestroy(stream_);
   stream_ = nullptr;
+  if (constructing_) session_constructed(false);
+  constructing_ = false;
   if (live_) session_live(-1);
   live_ = false;
 }
@@ -762,7 +757,7 @@ bool Session::embed_fold_ok() const {
   return use_graph_ && screen_ && (embd_.type == T_F16 || embd_.type == T_Q8_0) && !ple_table_.qs;
 }
 
-void Session::record_step(hipStream_t s, bool gen, bool fold_embed) {
+void Session::record_step(hipStream_t s, bool gen, bool fold_embed, bool logits) {
   kernels_per_token_ = 0;
   px_k_ = 0;
   rec_gen_ = gen;
@@ -809,16 +804,21 @@ void Session::record_step(hipStream_t s, bool gen, bool fold_embed) {
   bool fused = fuse_layers_;
   for (const auto& l : L_) fused &= l.fused;
   if (tp_ && !fused && !xl_) throw status_error(LLMI_E_ARG, "tensor parallel needs the fused layer path");
-  if (xl_ && !dump_ && !(trace_fn_ && getenv("LLMI_TRACE_PER_OP")) && x_q8 && x_blocks == (const void*)act_.q8.xb) {
+  const bool xl_step =
+      xl_ && !dump_ && !(trace_fn_ && getenv("LLMI_TRACE_PER_OP")) && x_q8 && x_blocks == (const void*)act_.q8.xb;
+  // an exact tensor-parallel rank has only the exact-order engine's shards (record_layers runs whole matrices
+  // and has no exchanges): refuse rather than produce a wrong step
+  if (tp_ && exact_ && !xl_step)
+    throw status_error(LLMI_E_ARG, "tensor parallel exact mode: this step cannot run on the exact-order engine "
+                                   "(dumps and per-op traces are single-device only)");
+  if (xl_step) {
     record_layers_xl(s);
-  } else if (fused && engine_ && !dump_ && !trace_fn_) {
-    record_layers_engine(s, x_q8);
   } else if (fused) {
     record_layers_fused(s, x_q8);
   } else {
     record_layers(s, x_q8);
   }
-  record_logits(s, gen);
+  if (logits) record_logits(s, gen);
   rec_gen_ = scr_prepped_ = rec_fold_ = false;
 }
 
@@ -1094,189 +1094,6 @@ bool Session::prefill_run(const int32_t* tokens, int n, int pos, bool allow_f16)
 // GELU epilogue], down [+ Q8_0 of the GELU output]).  The residual stream
 // ping-pongs between resid_ and resid2_ (a prologue's work-group 0 writes the
 // buffer its sibling work-groups are not reading).
-// The layer engine (k_engine.hip): Gemma-3 layers whose four projections are Q4_0,
-// head_dim 256, two q heads per (virtual) kv head, on one device.  Opt-in (LLMI_ENGINE=1): measured slower than
-// the three launches per layer (attention block, gate_up, down) -- 38 vs 29 us per 4B layer; the layer's weight
-// stream, issued at launch start, queues every cross-CU hand-off behind it (profiles/r03_engine_trace.txt).
-// Dumps and op-level traces always use the three launches.
-void Session::setup_engine(const GGUFView& g) {
-  engine_ = false;
-  const char* on = getenv("LLMI_ENGINE");
-  if (!on || atoi(on) == 0) return;
-  if (!fuse_layers_ || tp_ || !dup_.empty() || ple_table_.qs || hp_.gemma4) return;
-  if (hp_.attn_softcap > 0.0f) return;  // the engine's attention has no soft-cap (the attention block has)
-  if (embd_.type != T_F16 && embd_.type != T_Q8_0) return;
-  for (const auto& l : L_) {
-    const bool q40 = l.qkv.size() == 1 && l.qkv[0].w.type == T_Q4_0 && l.o.w.type == T_Q4_0 &&
-                     l.gate_up.size() == 1 && l.gate_up[0].w.type == T_Q4_0 && l.down.w.type == T_Q4_0;
-    if (!l.fused || !q40 || !l.has_kv || l.hd != 256 || l.out_scale != 1.0f || l.qkv_rows != L_[0].qkv_rows ||
-        !l.post_ffw_norm || !l.post_attn_norm || !l.ffn_norm || !l.attn_norm || !l.q_norm || !l.k_norm)
-      return;
-  }
-  EngineLayer plan;
-  if (!engine_plan(hp_.n_embd, hp_.n_ff, nh_, nkv_, 256, L_[0].qkv_rows, plan)) return;
-  const int E = hp_.n_embd, F = hp_.n_ff, H = plan.ru;
-  constexpr size_t kSlack = 8192;  // the down rows are read in whole 1-KB LDS-DMA pieces
-  eng_w_.resize(hp_.n_layer);
-  for (int l = 0; l < hp_.n_layer; l++) {
-    const std::string b = "blk." + std::to_string(l) + ".";
-    const GTensor *q = g.tensor(b + "attn_q.weight"), *k = g.tensor(b + "attn_k.weight"), *v = g.tensor(b + "attn_v.weight");
-    const GTensor *o = g.tensor(b + "attn_output.weight"), *gt = g.tensor(b + "ffn_gate.weight");
-    const GTensor *up = g.tensor(b + "ffn_up.weight"), *dn = g.tensor(b + "ffn_down.weight");
-    EngWeights& w = eng_w_[l];
-    w.q = alloc_weight(T_Q4_0, L_[l].qkv_rows, E, kSlack);
-    int r0 = 0;
-    for (const GTensor* t : {q, k, v}) {
-      const int n = (int)t->shape[1];
-      upload_rows(w.q, r0, g.tensor_data(*t), n, stream_);
-      r0 += n;
-    }
-    w.o = alloc_weight(T_Q4_0, E, (int)o->shape[0], kSlack);
-    upload_rows(w.o, 0, g.tensor_data(*o), E, stream_);
-    // gate / up interleaved in groups of H = n_ff / CUs: CU c's 2H rows are one contiguous run
-    const size_t rb = gguf_bytes(T_Q4_0, 1, E);
-    std::vector<uint8_t> il((size_t)2 * F * rb);
-    const uint8_t *sg = (const uint8_t*)g.tensor_data(*gt), *su = (const uint8_t*)g.tensor_data(*up);
-    for (int c = 0; c < F / H; c++) {
-      std::memcpy(&il[(size_t)(2 * H * c) * rb], sg + (size_t)(H * c) * rb, H * rb);
-      std::memcpy(&il[(size_t)(2 * H * c + H) * rb], su + (size_t)(H * c) * rb, H * rb);
-    }
-    w.g = alloc_weight(T_Q4_0, 2 * F, E, kSlack);
-    upload_rows(w.g, 0, il.data(), 2 * F, stream_);
-    w.d = alloc_weight(T_Q4_0, E, F, kSlack);
-    upload_rows(w.d, 0, g.tensor_data(*dn), E, stream_);
-  }
-  eng_ = plan;
-  eng_epoch_ = dalloc<unsigned>(1);
-  eng_gqkv_ = dalloc<uint2>(L_[0].qkv_rows);
-  eng_gxo_ = dalloc<uint2>((size_t)nh_ * 256 / 32 * 12);
-  eng_go_ = dalloc<uint2>(E);
-  eng_ghid_ = dalloc<uint2>(F);
-  eng_zero_ = dalloc<uint4>(256);
-  if (!blk_err_) blk_err_ = dalloc<int>(2);
-  if (!blk_trace_)
-    if (const char* tr = getenv("LLMI_BLOCK_TRACE")) {  // development: per-CU phase clocks of one layer
-      blk_trace_layer_ = atoi(tr);
-      blk_trace_ = dalloc<unsigned long long>(4096 * 8);
-    }
-  engine_ = true;
-}
-
-// The FFN engine (k_engine.hip): gate_up + GELU + down of a Q4_0 layer as one launch of one 1024-thread
-// work-group per CU, both weights issued at launch start.  Opt-in (LLMI_FFN_ENGINE=1): measured slower than the
-// two launches (747 vs 926 tok/s on 4B: the prologue's operands and the GELU exchange queue behind the 44 MB
-// weight stream; profiles/r03_engine_trace.txt).
-void Session::setup_ffn_engine(const GGUFView& g) {
-  ffn_engine_ = false;
-  const char* on = getenv("LLMI_FFN_ENGINE");
-  if (!on || atoi(on) == 0) return;
-  if (!fuse_layers_ || tp_ || !dup_.empty() || ple_table_.qs || hp_.gemma4) return;
-  for (const auto& l : L_)
-    if (!l.fused || l.gate_up.size() != 1 || l.gate_up[0].w.type != T_Q4_0 || l.down.w.type != T_Q4_0 ||
-        l.out_scale != 1.0f || !l.post_attn_norm || !l.ffn_norm)
-      return;
-  EngineLayer plan;
-  if (!ffn_engine_plan(hp_.n_embd, hp_.n_ff, plan)) return;
-  const int E = hp_.n_embd, F = hp_.n_ff, H = plan.ru;
-  constexpr size_t kSlack = 8192;  // the down rows are read in whole 1-KB LDS-DMA pieces
-  eng_w_.resize(hp_.n_layer);
-  for (int l = 0; l < hp_.n_layer; l++) {
-    const std::string b = "blk." + std::to_string(l) + ".";
-    const GTensor *gt = g.tensor(b + "ffn_gate.weight"), *up = g.tensor(b + "ffn_up.weight");
-    const GTensor* dn = g.tensor(b + "ffn_down.weight");
-    EngWeights& w = eng_w_[l];
-    const size_t rb = gguf_bytes(T_Q4_0, 1, E);
-    std::vector<uint8_t> il((size_t)2 * F * rb);
-    const uint8_t *sg = (const uint8_t*)g.tensor_data(*gt), *su = (const uint8_t*)g.tensor_data(*up);
-    for (int c = 0; c < F / H; c++) {
-      std::memcpy(&il[(size_t)(2 * H * c) * rb], sg + (size_t)(H * c) * rb, H * rb);
-      std::memcpy(&il[(size_t)(2 * H * c + H) * rb], su + (size_t)(H * c) * rb, H * rb);
-    }
-    w.g = alloc_weight(T_Q4_0, 2 * F, E, kSlack);
-    upload_rows(w.g, 0, il.data(), 2 * F, stream_);
-    w.d = alloc_weight(T_Q4_0, E, F, kSlack);
-    upload_rows(w.d, 0, g.tensor_data(*dn), E, stream_);
-  }
-  eng_ = plan;
-  eng_epoch_ = dalloc<unsigned>(1);
-  eng_ghid_ = dalloc<uint2>(F);
-  if (!blk_err_) blk_err_ = dalloc<int>(2);
-  if (!blk_trace_)
-    if (const char* tr = getenv("LLMI_BLOCK_TRACE")) {
-      blk_trace_layer_ = atoi(tr);
-      blk_trace_ = dalloc<unsigned long long>(4096 * 8);
-    }
-  ffn_engine_ = true;
-}
-
-EngineLayer Session::engine_args(int l, float* resid_in, float* resid_out) const {
-  const LayerDev& Ld = L_[l];
-  const EngWeights& w = eng_w_[l];
-  EngineLayer a = eng_;
-  a.q_qs = (const uint4*)w.q.qs;
-  a.q_d = w.q.d;
-  a.o_qs = (const uint4*)w.o.qs;
-  a.o_d = w.o.d;
-  a.g_qs = (const uint4*)w.g.qs;
-  a.g_d = w.g.d;
-  a.d_qs = (const uint4*)w.d.qs;
-  a.d_d = w.d.d;
-  a.k_off = Ld.k_off;
-  a.v_off = Ld.v_off;
-  a.w_post = l > 0 ? L_[l - 1].post_ffw_norm : Ld.post_ffw_norm;  // (layer 0 reads x0 instead)
-  a.attn_norm = Ld.attn_norm;
-  a.q_norm = Ld.q_norm;
-  a.k_norm = Ld.k_norm;
-  a.post_attn_norm = Ld.post_attn_norm;
-  a.ffn_norm = Ld.ffn_norm;
-  a.y_in = d_out_;  // every CU reads it before any CU writes this layer's rows (those follow the GELU exchange)
-  a.x0 = act_.q8.xb;
-  a.resid_in = resid_in;
-  a.resid_out = resid_out;
-  a.y_out = d_out_;
-  a.rope_cs = Ld.is_swa ? rope_swa_ : rope_glb_;
-  a.attn_scale = hp_.attn_scale;
-  a.eps = hp_.eps;
-  a.k_cache = Ld.kc;
-  a.v_cache = Ld.vc;
-  a.max_ctx = max_ctx_;
-  a.d_pos = d_pos_;
-  a.partial = part_;
-  a.ticket = ticket_;
-  a.zero = eng_zero_;
-  a.epoch = eng_epoch_;
-  a.g_qkv = eng_gqkv_;
-  a.g_xo = eng_gxo_;
-  a.g_o = eng_go_;
-  a.g_hid = eng_ghid_;
-  a.err = blk_err_;
-  return a;
-}
-
-void Session::record_layers_engine(hipStream_t s, bool x_q8) {
-  const int E = hp_.n_embd;
-  if (!x_q8) {  // layer 0 reads the Q8_0 blocks of attn_norm(embedding)
-    launch_quantize_q8_0(xn_, E, act_.q8, s);
-    kernels_per_token_++;
-  }
-  float* cur = resid_;
-  float* other = resid2_;
-  for (int l = 0; l < hp_.n_layer; l++) {
-    EngineLayer a = engine_args(l, cur, other);
-    if (blk_trace_ && l == blk_trace_layer_) a.trace = blk_trace_;
-    launch_layer_engine(a, l == 0, s);
-    kernels_per_token_++;
-    std::swap(cur, other);
-  }
-  // final residual + output_norm (-> xn_, and f16 x for an F16 logits table)
-  NormOut o2;
-  o2.xn = xn_;
-  if (embd_.type == T_F16) o2.x16 = act_.x16;
-  screen_norm(o2);
-  launch_residual_norm(d_out_, L_.back().post_ffw_norm, cur, out_norm_, o2, E, hp_.eps, false, s);
-  kernels_per_token_++;
-}
-
 void Session::record_layers_fused(hipStream_t s, bool x_q8) {
   const int E = hp_.n_embd;
   float* cur = resid_;
@@ -1284,7 +1101,7 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
   // tensor-parallel ranks: the o, GELU and down outputs go to the peers from the producing launches' epilogues
   // and the consumers read their mailbox (px.h) -- no exchange launches but the attention output's (head-sharded
   // mode), the last layer's down and the argmax keys
-  bool pxf = tp_ && px_on() && !ffn_engine_;
+  bool pxf = tp_ && px_on();
   for (const auto& l : L_) pxf = pxf && l.qkv.size() == 1;  // (the two-weight q|k|v launch has no fused variant)
   int k_d = -1;  // the previous layer's down exchange, read by this layer's qkv prologue
   std::vector<int> px_nwg;  // exchange k -> the work-groups that push it (their checksum granules, px.h)
@@ -1352,6 +1169,7 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
       if (pxf) fx_out(go);
       BlockSync bs;
       bs.epoch = epoch;
+      bs.done = blk_done_;
       bs.g_qkv = blk_gqkv_ + (size_t)l * blk_gqkv_stride_;
       bs.g_xo = blk_gxo_ + (size_t)l * blk_gxo_stride_;
       bs.err = blk_err_;
@@ -1448,49 +1266,7 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
     const int k_o = pxf ? px_k_ - 1 : -1;  // the o launch's exchange (the block's or the standalone o's)
     if (pxf) coll_->fused_point(s);
     else if (tp_) coll_->all_gather(o_out_, (size_t)e_sh_ * sizeof(float), s, px_take());
-    if (ffn_engine_ && !dump_ && !trace_fn_) {  // gate_up + GELU + down: one launch
-      EngineLayer a = eng_;
-      a.g_qs = (const uint4*)eng_w_[l].g.qs;
-      a.g_d = eng_w_[l].g.d;
-      a.d_qs = (const uint4*)eng_w_[l].d.qs;
-      a.d_d = eng_w_[l].d.d;
-      a.post_attn_norm = Ld.post_attn_norm;
-      a.ffn_norm = Ld.ffn_norm;
-      a.y_in = o_out_;
-      a.resid_in = cur;
-      a.resid_out = other;
-      a.y_out = d_out_;
-      a.eps = hp_.eps;
-      a.epoch = eng_epoch_;
-      a.g_hid = eng_ghid_;
-      a.err = blk_err_;
-      a.blk_epoch = epoch;  // the attention block's granule tag of this layer (the gate_up launch's job before)
-      if (blk_trace_ && l == blk_trace_layer_) a.trace = blk_trace_;
-      launch_ffn_engine(a, s);
-      std::swap(cur, other);
-      kernels_per_token_ += block_ ? 1 : 2;
-      continue;
-    }
     LayerGemv gg;
-    // LLMI_GELU_X=1 (27B, the block without its in-launch prologue; opt-in, measured even): the post-attention
-    // residual + FFN norm as their own launch too, and gate_up on its x blocks -- gate_up 29.4 -> 24.6 us (672
-    // work-groups no longer re-read 86 KB of prologue operands each), but the one-work-group norm launch takes
-    // 5.7 us: 214.8 vs 214.9 tok/s
-#ifdef LLMI_DEV_ENGINES  // development variant only (measured at parity)
-    static const bool gelu_x_env = getenv("LLMI_GELU_X") != nullptr;
-#else
-    constexpr bool gelu_x_env = false;
-#endif
-    const bool gelu_x = gelu_x_env && block_ && !block_pro_ && !dump_ &&
-                        layer_gemv_supported(Ld.gate_up[0].w, LAYER_GELU_X);
-    if (gelu_x) {
-      NormOut on;
-      on.xn = xn_;
-      on.q8 = act_.q8.xb;
-      launch_residual_norm(o_out_, Ld.post_attn_norm, cur, Ld.ffn_norm, on, E, hp_.eps, false, s);
-      kernels_per_token_++;
-      gg.xg = act_.q8.xb;
-    }
     gg.y = o_out_;
     gg.w_post = Ld.post_attn_norm;
     gg.resid_in = cur;
@@ -1500,23 +1276,22 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
     gg.hid = hid_ + (size_t)tp_rank_ * f_sh_;
     const bool dplain = down_plain(Ld);
     if (dplain) gg.hq = hq_ + (size_t)tp_rank_ * (f_sh_ / 32);
-    gg.epoch = epoch;  // advances the attention block's granule tag of this layer
     if (dump_ || trace_fn_) gg.xn_out = xn_;
-    const bool gfx = pxf && !gelu_x;
+    const bool gfx = pxf;
     int k_h = -1;
     if (gfx) {
       fx_in(gg, k_o, e_sh_);
       k_h = fx_out(gg);
     }
     for (int r = 0; r < dup("gate_up"); r++)
-      fx_nwg(gg, launch_layer_gemv(Ld.gate_up[0].w, gg, gelu_x ? LAYER_GELU_X : LAYER_GELU, s));
-    tap("ffn_resid", l, gelu_x ? cur : other, (size_t)E * 4, s);
+      fx_nwg(gg, launch_layer_gemv(Ld.gate_up[0].w, gg, LAYER_GELU, s));
+    tap("ffn_resid", l, other, (size_t)E * 4, s);
     tap("ffn_norm", l, xn_, (size_t)E * 4, s);
     tap("hid", l, hid_, (size_t)hp_.n_ff * 4, s);
     dump("sa_out-" + L, other, E, s);
     dump("ffn_norm-" + L, xn_, E, s);
     dump("ffn_geglu-" + L, hid_, hp_.n_ff, s);
-    if (!gelu_x) std::swap(cur, other);  // (the norm launch updated cur in place)
+    std::swap(cur, other);
     if (gfx) coll_->fused_point(s);
     else if (tp_ && dplain) coll_->all_gather(hq_, (size_t)(f_sh_ / 32) * sizeof(XBlock), s, px_take());
     else if (tp_) coll_->all_gather(hid_, (size_t)f_sh_ * sizeof(float), s, px_take());
@@ -1787,13 +1562,14 @@ void Session::record_layers(hipStream_t s, bool x_q8) {
   }
 }
 
-void Session::ensure_graph(bool gen) {
-  hipGraph_t& g = gen ? graph_gen_ : graph_;
-  hipGraphExec_t& ge = gen ? graph_gen_exec_ : graph_exec_;
+void Session::ensure_graph(int kind) {
+  hipGraph_t& g = graphs_[kind];
+  hipGraphExec_t& ge = graph_execs_[kind];
   if (!use_graph_ || ge) return;
+  const bool gen = kind == STEP_GEN;
   LLMI_HIP(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
   try {
-    record_step(stream_, gen, gen);
+    record_step(stream_, gen, gen, kind != STEP_HIDDEN);
   } catch (...) {
     hipGraph_t gg;
     (void)hipStreamEndCapture(stream_, &gg);
@@ -1816,14 +1592,17 @@ void Session::px_prepare() {
   d_px_ = d;
 }
 
-void Session::run_step(bool gen) {
+void Session::run_step(int kind) {
   px_prepare();
-  gen = gen && screen_;
+  if (kind == STEP_GEN && !screen_) kind = STEP_LOGITS;
+  // a tensor-parallel rank keeps the logits of every step: the standalone exchanges of the skipped launches are
+  // counted by every rank alike, but the argmax keys' all-gather is part of the logits tail
+  if (kind == STEP_HIDDEN && tp_) kind = STEP_LOGITS;
   if (use_graph_) {
-    ensure_graph(gen);
-    LLMI_HIP(hipGraphLaunch(gen ? graph_gen_exec_ : graph_exec_, stream_));
+    ensure_graph(kind);
+    LLMI_HIP(hipGraphLaunch(graph_execs_[kind], stream_));
   } else {
-    record_step(stream_, gen);
+    record_step(stream_, kind == STEP_GEN, false, kind != STEP_HIDDEN);
   }
 }
 
@@ -1861,9 +1640,9 @@ void Session::forward(const int32_t* tokens, int n, int pos, float* logits, int3
       set_token_pos(tokens[n - 1], pos + n - 1, true);  // what the token loop leaves behind
       prefill(tokens, n, pos);
     } else {
-      for (int i = 0; i < n; i++) {
+      for (int i = 0; i < n; i++) {  // only the last token's logits are computed (model.cpp:983-1001)
         set_token_pos(tokens[i], pos + i, i == 0);
-        run_step();
+        run_step(i + 1 < n ? STEP_HIDDEN : STEP_LOGITS);
       }
     }
     // every rank of a tensor-parallel group gathers the full logits (collective)
@@ -1982,7 +1761,7 @@ void Session::enqueue(int32_t first, int pos, int n_steps) {
       launch_embed_norm(embd_.type, embd_raw_, embd_row_bytes_, d_token_, std::sqrt(static_cast<float>(E)), resid_,
                         L_[0].attn_norm, embed_out(), E, hp_.eps, ex_norm_, stream_);
     }
-    for (int i = 0; i < n_steps; i++) run_step(true);
+    for (int i = 0; i < n_steps; i++) run_step(STEP_GEN);
   });
 }
 
@@ -2060,8 +1839,8 @@ void Session::info(llmi_session_info* o) const {
   o->screened_logits = screen_ ? 1 : 0;
   o->screen_bytes = screen_ ? scr_.bytes : 0;
   o->prefill_f16_redo = pf_f16_redo_;
-  o->layer_engine = engine_ ? 1 : 0;
-  o->ffn_engine = ffn_engine_ ? 1 : 0;
+  o->layer_engine = 0;  // (the round-3 engines were removed in round 6: DESIGN.md section 4.3)
+  o->ffn_engine = 0;
   o->tp_exchange = coll_ ? (px_fused_ && coll_->kind() == EX_PUSH ? EX_PUSH_FUSED : coll_->kind()) : 0;
   o->block_slow_waits = slow_waits_;
   o->exact_engine = xl_ ? 1 : 0;
@@ -2140,7 +1919,7 @@ void Session::time_kernel(int which, int reps, double* us, double* bytes) {
   //   5: the r01 family: qkv PRO, o PLAIN, gate_up, down as standalone launches
   bool fused = fuse_layers_;
   for (const auto& l : L_) fused &= l.fused;
-  if (!fused || (which == 0 && !block_) || (which == 6 && !engine_) || (which == 7 && !ffn_engine_) || which < 0 ||
+  if (!fused || (which == 0 && !block_) || which == 6 || which == 7 || which < 0 ||
       which > 7 || reps <= 0) {
     *us = *bytes = 0.0;
     return;
@@ -2175,7 +1954,8 @@ void Session::time_kernel(int which, int reps, double* us, double* bytes) {
                          go.xg = blk_xo_;
                          go.out = o_out_;
                          BlockSync bs;
-                         bs.epoch = blk_epoch_ + i;
+                         bs.epoch = blk_epoch_ + i;  // (the launch advances it itself: every timed launch waits)
+                         bs.done = blk_done_;
                          bs.g_qkv = blk_gqkv_ + i * blk_gqkv_stride_;
                          bs.g_xo = blk_gxo_ + i * blk_gxo_stride_;
                          bs.err = blk_err_;
@@ -2187,31 +1967,6 @@ void Session::time_kernel(int which, int reps, double* us, double* bytes) {
                                            block_pro_ ? LAYER_PRO : LAYER_PLAIN, Ld.o.w, go, aa, qa, bs, stream_);
                        },
                        (double)Ld.qkv[0].w.bytes + (double)Ld.o.w.bytes + kv});
-    }
-    if (which == 6) {  // the layer engine: the whole layer, its own weights, the KV history at the current pos
-      const double kv = 2.0 * nkv_ * hd * 2.0 * (pos + 1);
-      const EngineLayer ea = engine_args((int)i, resid_, resid_scratch_);
-      items.push_back({[this, ea]() { launch_layer_engine(ea, false, stream_); },
-                       (double)(Ld.qkv[0].w.bytes + Ld.o.w.bytes + Ld.gate_up[0].w.bytes + Ld.down.w.bytes) + kv});
-    }
-    if (which == 7) {  // the FFN engine: gate_up + GELU + down, its own weights
-      EngineLayer ea = eng_;
-      ea.g_qs = (const uint4*)eng_w_[i].g.qs;
-      ea.g_d = eng_w_[i].g.d;
-      ea.d_qs = (const uint4*)eng_w_[i].d.qs;
-      ea.d_d = eng_w_[i].d.d;
-      ea.post_attn_norm = Ld.post_attn_norm;
-      ea.ffn_norm = Ld.ffn_norm;
-      ea.y_in = o_out_;
-      ea.resid_in = resid_;
-      ea.resid_out = resid_scratch_;
-      ea.y_out = d_out_;
-      ea.eps = hp_.eps;
-      ea.epoch = eng_epoch_;
-      ea.g_hid = eng_ghid_;
-      ea.err = blk_err_;
-      items.push_back({[this, ea]() { launch_ffn_engine(ea, stream_); },
-                       (double)(Ld.gate_up[0].w.bytes + Ld.down.w.bytes)});
     }
     if (which == 5) {
       items.push_back({[this, &Ld, q]() { launch_layer_gemv(Ld.qkv[0].w, q, LAYER_PRO, stream_); },
@@ -2246,7 +2001,6 @@ void Session::time_kernel(int which, int reps, double* us, double* bytes) {
   double tot_bytes = 0;
   for (int r = 0; r < reps; r++)
     for (size_t j = 0; j < items.size(); j++) {
-      if (which == 0) launch_bump_epoch(blk_epoch_ + j, stream_);  // fresh granule tags: every hand-off waits
       kernel_timing() = KernelTiming{ev[k], ev[k + 1]};
       k += 2;
       items[j].launch();

@@ -92,7 +92,9 @@ class Session {
   // gen: the decode loop's step (token id only: screened logits when screen_)
   // fold_embed: the step ends with the NEXT step's embed_norm inside the token feedback launch and starts at
   // layer 0 (the decode-loop graph; enqueue launches the first embed_norm itself)
-  void record_step(hipStream_t s, bool gen = false, bool fold_embed = false);
+  // logits false: the layers and the final norm only (a prompt token whose logits nobody reads: model.cpp:983-1001
+  // computes the logits of the last prompt position only)
+  void record_step(hipStream_t s, bool gen = false, bool fold_embed = false, bool logits = true);
   bool embed_fold_ok() const;
   NormOut embed_out() const;
   bool down_plain(const LayerDev& Ld) const;
@@ -109,10 +111,6 @@ class Session {
   XBlock* xa_xq_ = nullptr;      // exact attention output's Q8_0 blocks (the o projection's x)
   void setup_xl();
   void record_layers_xl(hipStream_t s);
-  void setup_engine(const GGUFView& g);
-  void setup_ffn_engine(const GGUFView& g);
-  void record_layers_engine(hipStream_t s, bool x_q8);
-  EngineLayer engine_args(int l, float* resid_in, float* resid_out) const;
   void prepare_act(uint32_t wtype, const float* x, int n, ActBuf& act, hipStream_t s);
   void gemv_parts(const std::vector<GemvPart>& parts, const float* x, int n_in, float* out, hipStream_t s,
                   bool x_ready);
@@ -120,7 +118,10 @@ class Session {
   // so the step-time delta is that family's in-graph cost
   int dup(const char* k) const { return dup_.find(k) != std::string::npos ? 2 : 1; }
   void set_token_pos(int32_t token, int pos, bool reset_ring);
-  void ensure_graph(bool gen);
+  // the step graphs: STEP_LOGITS (forward: full logits + argmax), STEP_GEN (the decode loop: token id only, the
+  // next embedding folded in), STEP_HIDDEN (a prompt token before the last: no logits)
+  enum { STEP_LOGITS = 0, STEP_GEN = 1, STEP_HIDDEN = 2, N_STEP_KINDS = 3 };
+  void ensure_graph(int kind);
   // llmi_session_dump: eager steps with print_tensor-format dumps (dump_ set)
   std::FILE* dump_ = nullptr;
   void dump(const std::string& name, const float* dev, int n, hipStream_t s);
@@ -128,7 +129,7 @@ class Session {
   llmi_trace_fn trace_fn_ = nullptr;
   void* trace_user_ = nullptr;
   void tap(const char* name, int layer, const void* dev, size_t bytes, hipStream_t s);
-  void run_step(bool gen = false);
+  void run_step(int kind = STEP_LOGITS);
   float* dev_f32_copy(const GGUFView& g, const GTensor* t, int n);
   // every allocation is zeroed ON THE SESSION'S STREAM, so the zeroing is ordered before every kernel of this
   // session that uses the buffer (null-stream hipMemset / hipMemcpy are not ordered with a non-blocking stream;
@@ -146,24 +147,18 @@ class Session {
     LLMI_HIP(hipStreamSynchronize(stream_));
   }
   bool live_ = false;          // counted in session_live (k_session.hip)
+  bool constructing_ = false;  // between session_live(+1) and session_constructed()
 
   llmi_session_opts opts_;
   bool exact_ = false, use_graph_ = true;
   bool fuse_layers_ = false;  // fast path: norms / GELU folded into the Q4_0 GEMVs
   bool block_ = false;        // fast path: qkv + attention + o as one launch per layer (k_attn.hip)
   bool block_pro_ = false;
-  long long slow_waits_ = 0;  // block hand-off waits over 20 us (blk_err_[1], accumulated at every sync)    // ... with the residual + norms in its prologue (else their own launch first: 27B)
-  // the layer engine (k_engine.hip): a whole decode layer per launch, one 1024-thread work-group per CU;
-  // its own row-major copies of the four projections (gate/up interleaved in groups of eng_.ru)
-  bool engine_ = false;
-  bool ffn_engine_ = false;               // gate_up + down of each layer as one launch (k_engine.hip FFN engine)
-  EngineLayer eng_{};                     // the per-CU split (engine_plan / ffn_engine_plan)
-  struct EngWeights { DevWeight q, o, g, d; };
-  std::vector<EngWeights> eng_w_;
-  unsigned* eng_epoch_ = nullptr;
-  uint2 *eng_gqkv_ = nullptr, *eng_gxo_ = nullptr, *eng_go_ = nullptr, *eng_ghid_ = nullptr;
-  uint4* eng_zero_ = nullptr;
-  unsigned* blk_epoch_ = nullptr;  // [n_layer] attention-block launch counts (granule tags)
+  long long slow_waits_ = 0;  // block hand-off waits over 20 us (blk_err_[1], accumulated at every sync)
+  // the attention block's granule tags: [n_layer] launch counts, each advanced by its own launch's last
+  // retiring work-group (blk_done_: the launch's retired work-groups, back to 0 at its end)
+  unsigned* blk_epoch_ = nullptr;
+  unsigned* blk_done_ = nullptr;
   uint2* blk_gqkv_ = nullptr;      // [n_layer][qkv rows] granules
   // Gemma-4 per-layer inputs (model.cpp:568-704)
   DevWeight ple_table_{};          // raw GGUF rows [vocab][n_layer * n_epl] (F16 / Q6_K / Q4_K), lookups only
@@ -204,10 +199,8 @@ class Session {
   int32_t *d_token_ = nullptr, *d_pos_ = nullptr, *ring_ = nullptr, *ring_idx_ = nullptr;
   unsigned long long* amax_key_ = nullptr;
   int32_t* h_stage_ = nullptr;  // pinned: token, pos, ring_idx
-  hipGraph_t graph_ = nullptr;
-  hipGraphExec_t graph_exec_ = nullptr;
-  hipGraph_t graph_gen_ = nullptr;          // the decode loop's step (screened token selection)
-  hipGraphExec_t graph_gen_exec_ = nullptr;
+  hipGraph_t graphs_[N_STEP_KINDS] = {};          // per step kind (ensure_graph)
+  hipGraphExec_t graph_execs_[N_STEP_KINDS] = {};
   bool screen_ = false;                     // k_logits.hip: token ids by screening + exact rescoring
   ScreenTable scr_;
   bool rec_gen_ = false;       // record_step: this step ends with the screened token selection

@@ -12,11 +12,14 @@ bool gemv_type_supported(uint32_t type);
 DevWeight alloc_weight(uint32_t type, int rows, int cols, size_t slack = 64);  // slack: bytes allocated past qs / d
 void upload_rows(DevWeight& w, int dst_row0, const void* host, int rows, hipStream_t s);
 void free_weight(DevWeight& w);
-// device memory of the sessions (k_session.hip): freed at once only while no other session of the process is alive,
-// else when the last one ends; session_live(+1 / -1) brackets a session's lifetime
+// device memory of the sessions (k_session.hip): released for reuse at once unless a session is being constructed
+// while another is alive (then when the last construction ends); session_live(+1 / -1) brackets a session's
+// lifetime, session_constructed() the end of its constructor
 void* dev_alloc(size_t bytes);  // session / weight memory (cached when released, k_session.hip)
 void dev_free(void* p);
 void session_live(int delta);
+void session_constructed(bool ok);
+void dev_mem_stats(size_t* live, size_t* cached, size_t* grave);  // (llmi_selftest 2)
 // Q4_0 row-major blocks -> slab-major (k_layer.hip's a.slab layout): slabs of
 // 8 blocks x all rows, block b of row r at (b / 8) rows 8 + r 8 + b % 8.
 void to_slab_layout(DevWeight& w, hipStream_t s);
@@ -80,7 +83,6 @@ struct LayerGemv {
   float* out = nullptr;     // PLAIN / PRO / QUANT: [rows]
   float* hid = nullptr;     // GELU: [rows / 2] = GELU(gate) * up
   XBlock* hq = nullptr;     // GELU with 32 units per work-group: also their Q8_0 block (the down launch's x)
-  unsigned* epoch = nullptr;  // optional: work-group 0 advances *epoch (the attention block's granule tag)
   const uint32_t* kdd = nullptr;  // kq weights (Q4_K / Q6_K): super-block d words, Q6_K high bits
   const uint2* kqh = nullptr;
   // tensor-parallel ranks, fused exchanges (px.h; px: the session's device-resident link): px_in -- the
@@ -96,62 +98,17 @@ struct LayerGemv {
 // qkv rows -> the kv head's attention work-groups -> the o projection, as
 // data-tagged granules (common.h st_granule / ld_granules) in per-layer buffers.
 struct BlockSync {
-  const unsigned* epoch = nullptr;  // this layer's launch count (advanced by the gate_up launch): tag = *epoch + 1
+  // this layer's launch count: tag = *epoch + 1, read by every work-group at its start; the launch advances it
+  // itself -- every work-group adds one to *done when it retires, and the last (done = grid size) resets done and
+  // advances the epoch, so no launch sequence (timed launches alone, a skipped or repeated neighbour launch) can
+  // leave a tag that the next launch would take for its own
+  unsigned* epoch = nullptr;
+  unsigned* done = nullptr;
   uint2* g_qkv = nullptr;           // [qkv rows] granules of the qkv GEMV output
   uint2* g_xo = nullptr;            // [n_head * head_dim / 32][12] granules of the attention output's Q8_0 blocks
   int* err = nullptr;               // set when a bounded wait gives up (the step's results are invalid)
   unsigned long long* trace = nullptr;  // development: [work-group][8] wall clocks (LLMI_BLOCK_TRACE)
 };
-// The layer engine (k_engine.hip): one Gemma-3 decode layer, Q4_0 weights, as one
-// persistent launch of one 1024-thread work-group per CU.
-struct EngineLayer {
-  // row-major Q4_0 weights (qs [rows][nb] 16-B blocks, d [rows][nb] f16), each
-  // allocated with >= 4 KB of slack (the down rows are copied in whole 1-KB pieces)
-  const uint4 *q_qs = nullptr, *o_qs = nullptr, *g_qs = nullptr, *d_qs = nullptr;
-  const uint16_t *q_d = nullptr, *o_d = nullptr, *g_d = nullptr, *d_d = nullptr;
-  int E = 0, Fu = 0;              // n_embd, n_ff
-  int nq = 0, k_off = 0, v_off = 0;  // qkv rows (q | k | v) and the k / v offsets
-  int n_head = 0, n_kv = 0, kvd = 1;  // kvd: virtual kv heads (2 q heads each) per cache head
-  int rq = 0, ro = 0, ru = 0, rd = 0;  // per CU: qkv rows, o rows, gate/up units (gate_up interleaved in groups of ru), down rows
-  const float *w_post = nullptr, *attn_norm = nullptr, *q_norm = nullptr, *k_norm = nullptr;
-  const float *post_attn_norm = nullptr, *ffn_norm = nullptr;
-  const float* y_in = nullptr;    // previous layer's down output (layer > 0)
-  const XBlock* x0 = nullptr;     // layer 0: the Q8_0 blocks of attn_norm(embedding)
-  const float* resid_in = nullptr;
-  float* resid_out = nullptr;
-  float* y_out = nullptr;
-  const float* rope_cs = nullptr;
-  float attn_scale = 1.0f;
-  double eps = 0;
-  uint16_t *k_cache = nullptr, *v_cache = nullptr;
-  int max_ctx = 0;
-  const int* d_pos = nullptr;
-  float* partial = nullptr;   // [n_head][ATTN_NSPLIT][head_dim + 2]
-  unsigned* ticket = nullptr;  // [n_kv kvd], zeroed, reset by the merging work-group
-  const uint4* zero = nullptr;  // >= 512 B of zeros (K / V rows past the context)
-  unsigned* epoch = nullptr;    // launch count: granule tag = *epoch + 1
-  uint2 *g_qkv = nullptr, *g_xo = nullptr, *g_o = nullptr, *g_hid = nullptr;
-  int* err = nullptr;
-  unsigned long long* trace = nullptr;  // development: [CU][16] phase clocks (LLMI_BLOCK_TRACE builds)
-  unsigned* blk_epoch = nullptr;        // FFN engine: the attention block's per-layer epoch, advanced at the end
-};
-// The engines were measured slower than the three launches per layer: they are built
-// only into the development variant (LLMI_VARIANT=engines LLMI_EXTRA_FLAGS=-DLLMI_DEV_ENGINES ->
-// libllmi_engines.so, loaded with LLMI_LIB=...), never into libllmi.so, whose plans report "no fit".
-#ifdef LLMI_DEV_ENGINES
-// fills the per-CU split of `a` and checks the launch fits (shapes, LDS, occupancy)
-bool engine_plan(int E, int F, int n_head, int n_kv, int hd, int qkv_rows, EngineLayer& a);
-void launch_layer_engine(const EngineLayer& a, bool first, hipStream_t s);
-// The FFN engine: gate_up + GELU + down of one layer in one launch after the attention block (y_in = the
-// block's o output; gate_up interleaved in groups of ru, row-major; the down rows with >= 8 KB of slack)
-bool ffn_engine_plan(int E, int F, EngineLayer& a);
-void launch_ffn_engine(const EngineLayer& a, hipStream_t s);
-#else
-inline bool engine_plan(int, int, int, int, int, int, EngineLayer&) { return false; }
-inline void launch_layer_engine(const EngineLayer&, bool, hipStream_t) {}
-inline bool ffn_engine_plan(int, int, EngineLayer&) { return false; }
-inline void launch_ffn_engine(const EngineLayer&, hipStream_t) {}
-#endif
 bool layer_gemv_supported(const DevWeight& w, int role);
 // ---- batched prefill (k_prefill.hip) ----
 struct PrefillNorm {  // per token: embedding (table != null) or residual + norm, then x -> Q8_0

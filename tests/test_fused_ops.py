@@ -85,16 +85,6 @@ def test_ops_mini27b_shapes(oracle):
     _run(oracle, "mini-27b", 26, 8, 2, 64, swa_pattern=[True, False])
 
 
-@pytest.mark.skipif(not os.environ.get("LLMI_LIB", "").endswith("libllmi_engines.so"),
-                    reason="LLMI_GELU_X is in the development variant only (LLMI_LIB=...engines.so)")
-def test_ops_mini27b_gelu_x(oracle, monkeypatch):
-    """LLMI_GELU_X=1 on the 27B shapes: the post-attention residual + FFN norm as their own launch and gate_up
-    on its Q8_0 blocks (LAYER_GELU_X: the x-block prologue with the GELU epilogue), each op against the oracle."""
-    chk = _run(oracle, "mini-27b", 28, 8, 2, 64, monkeypatch, {"LLMI_GELU_X": "1"}, check_prefill=False,
-               swa_pattern=[False, True])
-    assert "gemv_gate_up_gelu" in chk.report and "gemv_down" in chk.report
-
-
 @pytest.mark.parametrize("cfg_name", ["mini-4b", "mini-27b"])
 def test_ops_prefill_f16_gemm(oracle, monkeypatch, cfg_name):
     """The opt-in f16 prefill (LLMI_PREFILL_F16=1: f16 activations from the norm / attention / GELU producers,
