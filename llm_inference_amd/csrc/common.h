@@ -155,8 +155,9 @@ __device__ __forceinline__ uint64_t ld_sc1(const uint64_t* p) {
 // 8-byte write-through store {value, tag}; the consumer re-loads it (sc1)
 // until the tag is this launch's, so a hand-off costs one store + one load --
 // no drain, no counter, no flag.  Tags never repeat for a buffer (the
-// producer's epoch + 1, the epoch advancing once per launch), and the
-// buffers start zeroed (epoch 0 -> tag 1).
+// launch count + 1, the count advanced once per launch by the launch itself:
+// block_count / block_count_done below), and the buffers start zeroed (count
+// 0 -> tag 1).
 constexpr int BLOCK_SPIN_LIMIT = 1 << 21;  // ~0.1-0.3 s of polls: a wait that never ends is a bug
 // a wait that took longer than this (wall clock, 100 MHz ticks) adds 1 to err[1]: how often a hand-off stalls,
 // reported by the session (llmi_session_info.block_slow_waits).  Product builds count the merge's ticket wait
@@ -210,6 +211,20 @@ __device__ __forceinline__ void ld_granules(uint32_t (&v)[N], const uint2* g, in
 #ifdef LLMI_SLOW_WAITS  // diagnostic builds only: any count here reshuffles the attention block's registers (-0.5 %)
   count_slow_wait(n > 0 && wall_clock64() - t0 > BLOCK_SLOW_TICKS, err);
 #endif
+}
+
+// The attention block's tag advance (BlockSync::epoch / done / done_n): a counted work-group's thread 0 adds one
+// to *done once all of the work-group's waves are past their last use of the tag (block_count, relaxed: the
+// tag loads were consumed before; the return is left in flight) and checks the return at its end
+// (block_count_done): the add that completes the count resets *done and advances *epoch for the next launch
+__device__ __forceinline__ unsigned block_count(unsigned* done) {
+  return __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void block_count_done(unsigned old, unsigned n, unsigned* done, unsigned* epoch) {
+  if (old == n - 1u) {
+    __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // development trace of the block kernels (builds with -DLLMI_BLOCK_TRACE

@@ -96,9 +96,40 @@ struct XAttnArgs {
   // per key [n_head_kv][max_ctx]: (min over its nonzero elements of max(f16 exponent field, 1)) << 16 | max |k| as
   // f16 bits, written with the K row; 0 = unknown (the score then takes the serial chain)
   uint32_t* kmeta = nullptr;
+  // batched prefill (launch_exact_attn_batch): T tokens at positions *d_pos + z, z < T; their q|k|v rows at
+  // qkv + z qkv_stride; the f16 query rows [T][n_head][head_dim] (written by the batch's q/k launch); scores at
+  // [T][n_head][max_ctx], out at [T][n_head * head_dim], xq at [T][n_head * head_dim / 32]
+  uint16_t* qh = nullptr;
+  int qkv_stride = 0;
 };
 bool exact_attn_supported(int head_dim, int n_head, int n_head_kv);
 void launch_exact_attn(const XAttnArgs& a, hipStream_t s);
+// The exact attention of T prompt tokens at once (model.cpp:430-550 per token, causal over keys 0 .. pos + z):
+// every token's q / k row norms, rope, the K / V appends, then every (token, head)'s scores and its accumulator
+// chain -- each token's arithmetic exactly that of its own decode step.
+void launch_exact_attn_batch(const XAttnArgs& a, int T, hipStream_t s);
+
+// Batched exact prefill (k_exact.hip): the prompt's tokens before the last run layer by layer, T at a time, each
+// (row, token) with the reference's own accumulator chains.
+// norm: per token, h = (embed ? table row * emb_scale : resid + rms(y) * w_post), resid = h, x = Q8_0(rms(h) * w_next)
+struct XpNormArgs {
+  const uint8_t* table = nullptr;  // embed: the GGUF rows (F16 / F32 / Q8_0), row_bytes apart
+  size_t row_bytes = 0;
+  uint32_t type = 0;
+  const int32_t* tokens = nullptr;
+  float emb_scale = 1.0f;
+  const float* y = nullptr;        // [T][n] (pre)
+  const float* w_post = nullptr;
+  float* resid = nullptr;          // [T][n], in place
+  const float* w_next = nullptr;
+  XBlock* xq = nullptr;            // [T][n / 32]
+  int n = 0;
+  double eps = 0;
+};
+void launch_exact_norm_batch(const XpNormArgs& a, int T, hipStream_t s);
+// rows x T tokens of an XL weight on the tokens' Q8_0 blocks x [T][nb]: out [T][ldo] (plain), or (gelu32 weights)
+// GELU(gate) * up of each 32-unit group -> hq [T][rows / 64] Q8_0 blocks
+void launch_exact_gemm(const XlWeight& w, const XBlock* x, int T, float* out, int ldo, XBlock* hq, hipStream_t s);
 // self-test (synchronous): over every f32 bit pattern, out[0] = non-NaN inputs whose hardware f16 conversion
 // differs from the reference's f32_to_f16, out[1] = NaN inputs that differ, out[2] = the first non-NaN one
 void exact_selftest_f16(unsigned long long* out3);

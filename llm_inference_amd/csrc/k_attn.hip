@@ -712,6 +712,9 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, const QKVArgs
   } else {
     merge_heads(std::integral_constant<int, G>{}, 0, true);
   }
+  // the launch's tag advance (BlockSync::done): the kv head's last split counts once, its merged blocks published
+  // (every split of the head incremented the ticket after its granule waits, so each had used the tag)
+  if (BLK && role == 1 && t == 0) block_count_done(block_count(bs.done), bs.done_n, bs.done, bs.epoch);
 }
 
 // Key tiles of 32 keys while every split owns at most one tile (short
@@ -801,9 +804,10 @@ void launch_attention(const AttnArgs& a, bool exact, hipStream_t s, const QKVArg
 // blocks as granules; the o work-groups issue their weight slices, then
 // re-load the block granules.  So the o weights and the K/V history stream
 // while the qkv GEMV runs, and no hand-off waits on a drain or a counter.
-// The tag is the layer's launch count + 1 (BlockSync::epoch, advanced by the
-// launch's last retiring work-group: block_retire); waits are bounded (a timeout sets bs.err, the
-// host reports it).  Numerics are those of the three separate kernels (same
+// The tag is the layer's launch count + 1 (BlockSync::epoch), advanced by the
+// launch itself once every wave of it has used it (BlockSync::done, common.h
+// block_count); waits are bounded (a timeout sets bs.err, the host reports
+// it).  Numerics are those of the three separate kernels (same
 // bodies, same per-row order) except the o rows' lane order (R4).
 // ---------------------------------------------------------------------------
 namespace {
@@ -821,21 +825,6 @@ constexpr size_t block_attn_lds() {  // s_k + s_v (32-key tiles) + s_red
 constexpr int WT_W8 = 3;  // Q8_0 weights in the block (layer_body W8), beside the kq formats WT_Q4_K / WT_Q6_K
 
 // PXF: the qkv prologue / o epilogue honour the fused exchange (tensor-parallel ranks; layer_body PXF)
-// The launch's own tag advance (BlockSync::epoch / done): every work-group, once all its threads are past their
-// last granule access, adds one to *done; the one that completes the count resets it and advances the epoch.
-// Every work-group read the epoch at its start and the last one to retire is, by the count, after all of them,
-// so the tag changes exactly once per launch and only when no work-group of the launch can still read it.
-__device__ __forceinline__ void block_retire(const BlockSync& bs) {
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned old = __hip_atomic_fetch_add(bs.done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (old == gridDim.x - 1u) {
-      __hip_atomic_store(bs.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_fetch_add(bs.epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
 template <int HD, int G, int QR, int QP, int QE, int QROLE, int OR, int OP, int OE, int WTQ = 0, int WTQB = 0,
           int WTO = 0, int KVD = 1, int NS = ATTN_NSPLIT, bool PXF = false>
 __global__ __launch_bounds__(256) void attn_block_kernel(LayerGemv qg, LayerGemv og, AttnArgs aa, QKVArgs qa,
@@ -869,7 +858,6 @@ __global__ __launch_bounds__(256) void attn_block_kernel(LayerGemv qg, LayerGemv
     layer_body<OR, 4, OP, OE, ROLE_PLAIN, false, true, SYNC_WAIT, 0, WTO == WT_W8, WTO == WT_W8 ? 0 : WTO, 0, PXF>(og, b, s_dyn,
                                                                                                             bs);
   }
-  block_retire(bs);
 }
 
 using BlockFn = void (*)(dim3, size_t, const LayerGemv&, const LayerGemv&, const AttnArgs&, const QKVArgs&,
@@ -1086,6 +1074,7 @@ int launch_attn_block(const DevWeight& wqkv, const DevWeight* wqkv_b, LayerGemv 
   av.n_head_kv *= c.kvd;
   if (og.px && og.px_out >= 0 && bg.no > PX_MAX_CS) throw std::runtime_error("attention block: more fused-exchange producers than checksum slots");
   if (qg.px && qg.px_in >= 0 && (qg.px_in_nwg <= 0 || qg.px_in_nwg > PX_MAX_CS)) throw std::runtime_error("attention block: fused exchange read without its producer count");
+  bs.done_n = (unsigned)(bg.no + av.n_head_kv);  // the o work-groups and the kv heads' final merges (k_attn: role 1)
   c.fn(dim3(bg.nq + bg.na + bg.no), bg.lds, qg, og, av, qa, bs, bg.nq, qgb, nqa, s);
   LLMI_HIP(hipGetLastError());
   return bg.no;

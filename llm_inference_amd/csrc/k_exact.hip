@@ -869,7 +869,10 @@ __device__ __forceinline__ void xa_row2(const XaRow<HD>& inq, const XaRow<HD>& i
   __syncthreads();  // s_xq / s_xk / s_e2 reuse
 }
 
-template <int HD>
+// BATCH (the batched prefill, launch_exact_attn_batch): token z = blockIdx.z at pos = *d_pos + z; its f16 query
+// row comes from a.qh (the q/k launch normalised, roped and scaled it, and appended every token's K / V), and the
+// split work-groups take all its keys 0 .. pos (no new-key work-group)
+template <int HD, bool BATCH = false>
 __global__ __launch_bounds__(64) void xattn_scores_kernel(XAttnArgs a) {
   constexpr int EPL = HD / 64, CPL = EPL / 2, QW = HD / 32;  // QW: 16-B words of a quarter row
   constexpr int KPC = 16;                                    // keys per chunk: 4 lanes (row quarters) per key
@@ -879,25 +882,35 @@ __global__ __launch_bounds__(64) void xattn_scores_kernel(XAttnArgs a) {
   __shared__ __attribute__((aligned(16))) uint16_t s_k[HD];
   __shared__ __attribute__((aligned(16))) uint16_t s_qe[HD];  // the f16 query's exponent fields
   const int h = blockIdx.x, split = blockIdx.y, lane = threadIdx.x;
-  const int pos = *a.d_pos;
-  // work-groups split < XA_NSPLIT: the keys before pos in chunks of 16, chunk split, split + XA_NSPLIT, ..; the
-  // last one (split == XA_NSPLIT): the new key -- k norm + rope, the K / V append and its score
-  const bool pos_wg = split == XA_NSPLIT;
-  if (!pos_wg && split * KPC >= pos) return;  // no key chunk for this work-group (whole wave)
+  const int z = BATCH ? (int)blockIdx.z : 0;
+  const int pos = *a.d_pos + z;
+  // work-groups split < XA_NSPLIT: the keys before pos (BATCH: up to pos) in chunks of 16, chunk split, split +
+  // XA_NSPLIT, ..; the last one (split == XA_NSPLIT, decode only): the new key -- k norm + rope, the K / V append
+  // and its score
+  const int nk = BATCH ? pos + 1 : pos;
+  const bool pos_wg = !BATCH && split == XA_NSPLIT;
+  if (!pos_wg && split * KPC >= nk) return;  // no key chunk for this work-group (whole wave)
   const int hkv = h / (a.n_head / a.n_head_kv);
   const int kl = lane >> 2, qt = lane & 3;  // key of the chunk, quarter of its row
   XL_MARK(0);
   // every global operand first: q row + weights, the rope entries, the new key's k / v rows or the first K rows
-  const float* cs = a.rope_cs + (size_t)pos * HD;
   float c[CPL], sn[CPL];
-#pragma unroll
-  for (int k = 0; k < CPL; k++) {
-    const float2 t = reinterpret_cast<const float2*>(cs)[lane + 64 * k];
-    c[k] = t.x;
-    sn[k] = t.y;
-  }
   XaRow<HD> qr, kr_;
-  xa_load<HD>(qr, a.qkv + (size_t)h * HD, a.q_norm_w);
+  uint16_t qb16[EPL];
+  if constexpr (BATCH) {
+    const uint16_t* qh = a.qh + ((size_t)z * a.n_head + h) * HD;
+#pragma unroll
+    for (int k = 0; k < EPL; k++) qb16[k] = qh[lane + 64 * k];
+  } else {
+    const float* cs = a.rope_cs + (size_t)pos * HD;
+#pragma unroll
+    for (int k = 0; k < CPL; k++) {
+      const float2 t = reinterpret_cast<const float2*>(cs)[lane + 64 * k];
+      c[k] = t.x;
+      sn[k] = t.y;
+    }
+    xa_load<HD>(qr, a.qkv + (size_t)h * HD, a.q_norm_w);
+  }
   float vrow[EPL];
   const uint16_t* kb = a.k_cache + (size_t)hkv * a.max_ctx * HD;
   const uint32_t* km = a.kmeta ? a.kmeta + (size_t)hkv * a.max_ctx : nullptr;
@@ -913,20 +926,22 @@ __global__ __launch_bounds__(64) void xattn_scores_kernel(XAttnArgs a) {
 #pragma unroll
     for (int k = 0; k < EPL; k++) vrow[k] = a.qkv[a.v_off + (size_t)hkv * HD + lane + 64 * k];
   } else {
-    const int j1 = min(split * KPC + kl, pos - 1);
+    const int j1 = min(split * KPC + kl, nk - 1);
     ld_quarter(wa, j1);
     meta = km ? km[j1] : 0u;
   }
   float r[EPL], rk2[EPL];
-  if (pos_wg) xa_row2<HD>(qr, kr_, c, sn, a.eps, s_x, s_x2, r, rk2);  // (uniform per work-group)
-  else xa_row<HD>(qr, c, sn, a.eps, s_x, r);
+  if constexpr (!BATCH) {
+    if (pos_wg) xa_row2<HD>(qr, kr_, c, sn, a.eps, s_x, s_x2, r, rk2);  // (uniform per work-group)
+    else xa_row<HD>(qr, c, sn, a.eps, s_x, r);
+  }
   XL_MARK(1);
   // the query's exactness words (xa_exact_ok): min over its nonzero elements of max(exponent field, 1), |q|_1
   int qcode = 31;
   double qn1 = 0.0;
 #pragma unroll
   for (int k = 0; k < EPL; k++) {  // model.cpp:767 scale, then the score's f16 query (model.cpp:507)
-    const uint16_t qb = f2h_ggml(r[k] * a.attn_scale);
+    const uint16_t qb = BATCH ? qb16[k] : f2h_ggml(r[k] * a.attn_scale);
     s_q[lane + 64 * k] = (double)h2f(qb);
     s_qe[lane + 64 * k] = (qb >> 10) & 0x1F;
     qcode = min(qcode, xa_exp_code(qb));
@@ -958,7 +973,7 @@ __global__ __launch_bounds__(64) void xattn_scores_kernel(XAttnArgs a) {
   }
   __syncthreads();
   XL_MARK(3);
-  double* sc_out = a.scores + (size_t)h * a.max_ctx;
+  double* sc_out = a.scores + ((size_t)z * a.n_head + h) * a.max_ctx;
   // score = sum_i (double)(f16(k_i) * f16(q_i)), i in order, from 0.0 (model.cpp:504-509): the f32 product of two
   // f16 values is exact, so one f64 fma per element is the reference's rounding.  Where xa_exact_ok holds no add
   // of that chain rounds, so the row's four quarters are summed by four lanes and combined (the same bits); the
@@ -1002,14 +1017,14 @@ __global__ __launch_bounds__(64) void xattn_scores_kernel(XAttnArgs a) {
   } else {
     const double2* q2 = reinterpret_cast<const double2*>(s_q + qt * (HD / 4));
     const xa_u16x2* qe2 = reinterpret_cast<const xa_u16x2*>(s_qe + qt * (HD / 4));
-    for (int cc = split; cc * KPC < pos; cc += XA_NSPLIT) {
+    for (int cc = split; cc * KPC < nk; cc += XA_NSPLIT) {
       const int j = cc * KPC + kl;
-      const bool valid = j < pos;
+      const bool valid = j < nk;
       uint4 wn[QW];
       uint32_t mn = 0u;
-      const bool more = (cc + XA_NSPLIT) * KPC < pos;  // (uniform) the next chunk's rows in flight
+      const bool more = (cc + XA_NSPLIT) * KPC < nk;  // (uniform) the next chunk's rows in flight
       if (more) {
-        const int jn = min((cc + XA_NSPLIT) * KPC + kl, pos - 1);
+        const int jn = min((cc + XA_NSPLIT) * KPC + kl, nk - 1);
         ld_quarter(wn, jn);
         mn = km ? km[jn] : 0u;
       }
@@ -1139,7 +1154,8 @@ __device__ __forceinline__ uint16_t cvt_f16_rne(float f) {
 
 // (Tried: the V rows through an LDS ring filled by LDS-DMA three 64-key stages ahead -- 28.3 vs 24.6 us at 600
 // keys in scripts/dev/xl_bench: the per-key chain, not the V loads, bounds this kernel.)
-template <int HD>
+// BATCH: token z = blockIdx.y at pos = *d_pos + z (scores / out / xq at the token's rows)
+template <int HD, bool BATCH = false>
 __global__ __launch_bounds__((HD / 64 + 1) * 64) void xattn_accum_kernel(XAttnArgs a) {
   constexpr int NWV = HD / 64, T = (NWV + 1) * 64;
   constexpr int NWS = T / 64, KPT = (XA_CH + T - 1) / T;  // the branch pass: every wave, KPT keys per thread
@@ -1152,9 +1168,10 @@ __global__ __launch_bounds__((HD / 64 + 1) * 64) void xattn_accum_kernel(XAttnAr
   __shared__ float s_sacc;
   __shared__ uint64_t s_etab[32];  // expf's table (a per-lane global load each call, on the branch pass's chain)
   const int h = blockIdx.x, t = threadIdx.x, wave = t >> 6, lane = t & 63;
-  const int n_keys = *a.d_pos + 1;
+  const int z = BATCH ? (int)blockIdx.y : 0;
+  const int n_keys = *a.d_pos + z + 1;
   const int hkv = h / (a.n_head / a.n_head_kv);
-  const double* sc_in = a.scores + (size_t)h * a.max_ctx;
+  const double* sc_in = a.scores + ((size_t)z * a.n_head + h) * a.max_ctx;
   double run_max = -INFINITY;
   uint16_t v16 = 0;  // f32_to_f16(0.0f)
   float s_acc = 0.0f;
@@ -1355,8 +1372,9 @@ __global__ __launch_bounds__((HD / 64 + 1) * 64) void xattn_accum_kernel(XAttnAr
   if (wave < NWV) {
     const int d = wave * 64 + lane;
     const float o = h2f(v16) * s_sacc;  // model.cpp:543-547
-    a.out[(size_t)h * HD + d] = o;
-    q8_block_store(o, true, a.xq + ((size_t)h * HD + wave * 64) / 32 + (lane >> 5), lane & 31);
+    const size_t zo = (size_t)z * a.n_head * HD;
+    a.out[zo + (size_t)h * HD + d] = o;
+    q8_block_store(o, true, a.xq + (zo + (size_t)h * HD + wave * 64) / 32 + (lane >> 5), lane & 31);
   }
 }
 
@@ -1398,6 +1416,292 @@ __global__ __launch_bounds__(256) void chain_selftest_kernel(unsigned* out) {
   __syncthreads();
   const float v = (g & 1) ? xl_chain_spec2<4>(s, 2560, out + 1) : xl_chain_spec<4>(s, 2560, out + 1);
   if (threadIdx.x == 0 && __float_as_uint(v) != __float_as_uint(s_ref)) atomicAdd(out, 1u);
+}
+
+// ---------------------------------------------------------------------------
+// Batched exact prefill (exact.h launch_exact_norm_batch / launch_exact_gemm / launch_exact_attn_batch): the
+// prompt's tokens layer by layer, T at a time.  Every (row, token) keeps the reference's own chains: the same
+// per-token norm chains as the decode prologues, the eight fma chains of ops.cpp:364-399 per (row, token), the
+// per-token causal attention of model.cpp:478-550.  Only the order in which independent chains run changes.
+// ---------------------------------------------------------------------------
+
+// the q row (q heads) or the k row + V append (kv heads) of one token: blockIdx.x < n_head a q head, else kv head
+// blockIdx.x - n_head; blockIdx.y the token (pos = *d_pos + y).  The same norm chain, rope and roundings as the
+// decode scores kernel's xa_row / xa_row2 (bit-identical: every speculative chain equals the serial one)
+template <int HD>
+__global__ __launch_bounds__(64) void xattn_qk_batch_kernel(XAttnArgs a) {
+  constexpr int EPL = HD / 64, CPL = EPL / 2;
+  __shared__ __attribute__((aligned(16))) float s_x[HD];
+  const int r = blockIdx.x, z = blockIdx.y, lane = threadIdx.x;
+  const int pos = *a.d_pos + z;
+  const float* qkv = a.qkv + (size_t)z * a.qkv_stride;
+  const float* cs = a.rope_cs + (size_t)pos * HD;
+  float c[CPL], sn[CPL];
+#pragma unroll
+  for (int k = 0; k < CPL; k++) {
+    const float2 t = reinterpret_cast<const float2*>(cs)[lane + 64 * k];
+    c[k] = t.x;
+    sn[k] = t.y;
+  }
+  XaRow<HD> in;
+  float rr[EPL];
+  if (r < a.n_head) {  // the query: norm, rope, scale, the score's f16 rounding (model.cpp:762-794, 507)
+    xa_load<HD>(in, qkv + (size_t)r * HD, a.q_norm_w);
+    xa_row<HD>(in, c, sn, a.eps, s_x, rr);
+    uint16_t* qh = a.qh + ((size_t)z * a.n_head + r) * HD;
+#pragma unroll
+    for (int k = 0; k < EPL; k++) qh[lane + 64 * k] = f2h_ggml(rr[k] * a.attn_scale);
+    return;
+  }
+  const int hkv = r - a.n_head;  // the key: norm + rope, K and V appended at pos (model.cpp:440-474)
+  float vrow[EPL];
+  xa_load<HD>(in, qkv + a.k_off + (size_t)hkv * HD, a.k_norm_w);
+#pragma unroll
+  for (int k = 0; k < EPL; k++) vrow[k] = qkv[a.v_off + (size_t)hkv * HD + lane + 64 * k];
+  xa_row<HD>(in, c, sn, a.eps, s_x, rr);
+  uint16_t* kc = a.k_cache + ((size_t)hkv * a.max_ctx + pos) * HD;
+  uint16_t* vc = a.v_cache + ((size_t)hkv * a.max_ctx + pos) * HD;
+  int kcode = 31;
+  uint32_t kmag = 0;
+#pragma unroll
+  for (int k = 0; k < EPL; k++) {
+    const uint16_t kbits = f2h_ggml(rr[k]), vbits = f2h_ggml(vrow[k]);
+    kc[lane + 64 * k] = kbits;
+    vc[lane + 64 * k] = vbits;
+    a.vt[xa_vt_index<HD>(hkv, lane + 64 * k, pos, a.vt_stride)] = vbits;
+    kcode = min(kcode, xa_exp_code(kbits));
+    kmag = max(kmag, (uint32_t)(kbits & 0x7FFFu));
+  }
+  kcode = xa_wave_min(kcode);
+  kmag = (uint32_t)xa_wave_max((int)kmag);
+  if (lane == 0 && a.kmeta) a.kmeta[(size_t)hkv * a.max_ctx + pos] = ((uint32_t)kcode << 16) | kmag;
+}
+
+// embedding rows as the decode's embed_norm_kernel reads them (model.cpp:240-344; F16 / F32 / Q8_0 tables)
+__device__ __forceinline__ float xp_deq(uint32_t type, const uint8_t* row, int i) {
+  switch (type) {
+    case T_F16: return h2f(reinterpret_cast<const uint16_t*>(row)[i]);
+    case T_F32: return reinterpret_cast<const float*>(row)[i];
+    case T_Q8_0: {
+      const uint8_t* b = row + (i / 32) * 34;
+      return h2f((uint16_t)(b[0] | (b[1] << 8))) * (float)(int8_t)b[2 + (i & 31)];
+    }
+    default: return 0.0f;
+  }
+}
+
+// One work-group per token: the residual step + norm + quantize_row_q8_0 of the decode's XL_PRE prologue
+// (model.cpp:843-858 then 346-357, ops.cpp:116-139), or the embedding row * sqrt(n_embd) + attn_norm
+// (model.cpp:709-736), each serial chain by xl_sumsq; the Q8_0 blocks to global memory.
+template <int K4>
+__global__ __launch_bounds__(256) void xp_norm_kernel(XpNormArgs a) {
+  constexpr int NW = 4, T = 256;
+  extern __shared__ float4 s_n4[];
+  float* s_a = reinterpret_cast<float*>(s_n4);
+  float* s_b = s_a + a.n;
+  __shared__ float s_scale[2];
+  const int t = threadIdx.x, z = blockIdx.x;
+  const int n = a.n, n4 = n >> 2, nb = n / 32;
+  float4* resid4 = reinterpret_cast<float4*>(a.resid + (size_t)z * n);
+  const float4* wn4 = reinterpret_cast<const float4*>(a.w_next);
+  float4 hv[K4], yv[K4], wv[K4], nv[K4];
+  const bool embed = a.table != nullptr;
+  const uint8_t* row = embed ? a.table + (size_t)a.tokens[z] * a.row_bytes : nullptr;
+#pragma unroll
+  for (int k = 0; k < K4; k++) {
+    const int i = min(k * T + t, n4 - 1);
+    if (embed) {
+      hv[k] = make_float4(xp_deq(a.type, row, 4 * i) * a.emb_scale, xp_deq(a.type, row, 4 * i + 1) * a.emb_scale,
+                          xp_deq(a.type, row, 4 * i + 2) * a.emb_scale, xp_deq(a.type, row, 4 * i + 3) * a.emb_scale);
+    } else {
+      hv[k] = resid4[i];
+      yv[k] = reinterpret_cast<const float4*>(a.y + (size_t)z * n)[i];
+      wv[k] = reinterpret_cast<const float4*>(a.w_post)[i];
+    }
+    nv[k] = wn4[i];
+  }
+  auto own = [&](int k) { return k * T + t < n4; };
+  if (!embed) {
+#pragma unroll
+    for (int k = 0; k < K4; k++)
+      if (own(k)) reinterpret_cast<float4*>(s_a)[k * T + t] = yv[k];
+    __syncthreads();
+    const float sc1 = xl_rms_scale(xl_sumsq<NW>(s_a, n, &s_scale[0]), n, a.eps);
+#pragma unroll
+    for (int k = 0; k < K4; k++) {  // the post norm, then the residual add
+      hv[k].x = hv[k].x + (sc1 * yv[k].x) * wv[k].x;
+      hv[k].y = hv[k].y + (sc1 * yv[k].y) * wv[k].y;
+      hv[k].z = hv[k].z + (sc1 * yv[k].z) * wv[k].z;
+      hv[k].w = hv[k].w + (sc1 * yv[k].w) * wv[k].w;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < K4; k++)
+    if (own(k)) {
+      reinterpret_cast<float4*>(s_b)[k * T + t] = hv[k];
+      resid4[k * T + t] = hv[k];
+    }
+  __syncthreads();
+  const float sc2 = xl_rms_scale(xl_sumsq<NW>(s_b, n, &s_scale[1]), n, a.eps);
+  XBlock* xq = a.xq + (size_t)z * nb;
+#pragma unroll
+  for (int k = 0; k < K4; k++) {  // run_norm's (scale * x) * w, then the octet's Q8_0 block (8 lanes, a float4 each)
+    const bool ok = own(k);       // (whole octets: n4 and T are multiples of 8)
+    const float4 x = make_float4((sc2 * hv[k].x) * nv[k].x, (sc2 * hv[k].y) * nv[k].y, (sc2 * hv[k].z) * nv[k].z,
+                                 (sc2 * hv[k].w) * nv[k].w);
+    float amax = ok ? fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w))) : 0.0f;
+    amax = fmaxf(amax, dpp_f<DPP_QUAD_1032>(amax));
+    amax = fmaxf(amax, dpp_f<DPP_QUAD_2301>(amax));
+    amax = fmaxf(amax, dpp_f<DPP_ROW_HALF_MIRROR>(amax));
+    const float dd = amax / 127.0f;
+    const float id = dd != 0.0f ? 1.0f / dd : 0.0f;
+    const int q0 = nearest_int_fma(x.x, id), q1 = nearest_int_fma(x.y, id), q2 = nearest_int_fma(x.z, id),
+              q3 = nearest_int_fma(x.w, id);
+    const uint32_t w = (uint32_t)(q0 & 0xFF) | ((uint32_t)(q1 & 0xFF) << 8) | ((uint32_t)(q2 & 0xFF) << 16) |
+                       ((uint32_t)(q3 & 0xFF) << 24);
+    int sum = q0 + q1 + q2 + q3;
+    sum += __shfl_xor(sum, 1);
+    sum += __shfl_xor(sum, 2);
+    sum += __shfl_xor(sum, 4);
+    const int i4 = k * T + t, b = i4 >> 3, sl = i4 & 7;
+    if (ok) {
+      reinterpret_cast<uint32_t*>(xq + b)[sl] = w;  // words 0-3: q[0..15] (lo), 4-7: q[16..31] (hi)
+      if (sl == 0) {
+        xq[b].d = h2f(f2h_ggml(dd));
+        xq[b].nsum8 = -8 * sum;
+      }
+    }
+  }
+}
+
+// rows x tokens of an XL weight: a work-group owns 64 rows x 64 tokens, thread (rg, tg) = (t % 16, t / 16) the
+// rows 4 rg .. and tokens 4 tg .., each (row, token) with the reference's eight accumulators over the blocks in
+// order (ops.cpp:380-395: acc_j = fma(d, (float)isum_j, acc_j), d = f16(w.d) * f16(x.d)), then hsum_float_8.
+// The integer dots take the nibbles as 16 (n - 8) (one shift-and-xor, signed bytes) and the scale as d / 16:
+// 16 isum and d / 16 are exact rescalings, so every fma sees the reference's product d * isum.  Chunks of
+// XG_CB blocks of the rows' weights and the tokens' quants are staged in LDS.
+constexpr int XG_R = 64, XG_T = 64, XG_CB = 16;
+__global__ __launch_bounds__(256, 2) void xp_gemm_kernel(const uint4* __restrict__ wq, const uint2* __restrict__ wd,
+                                                         int rows, int nb, const XBlock* __restrict__ x, int T,
+                                                         float* __restrict__ out, int ldo, XBlock* __restrict__ hq) {
+  __shared__ __attribute__((aligned(16))) uint4 s_w[XG_CB][XG_R];      // the row's 16 nibble bytes of the block
+  __shared__ float s_wd[XG_CB][XG_R];                                   // f16(w.d) / 16
+  __shared__ __attribute__((aligned(16))) uint4 s_x[XG_CB][XG_T][2];   // the token's 32 quants
+  __shared__ float s_xd[XG_CB][XG_T];
+  const int t = threadIdx.x, rg = t & 15, tg = t >> 4;
+  const int row0 = blockIdx.x * XG_R, tok0 = blockIdx.y * XG_T, ng = nb >> 2;
+  float acc[4][4][8];
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+#pragma unroll
+      for (int s = 0; s < 8; s++) acc[i][j][s] = 0.0f;
+  for (int c0 = 0; c0 < nb; c0 += XG_CB) {
+    // weights: XL qs[g][row][jj] = word jj of the group's 4 blocks -> s_w[block][row] words jj
+#pragma unroll
+    for (int m = 0; m < 4; m++) {
+      const int i = t + 256 * m, jj = i & 3, R = (i >> 2) & 63, gl = i >> 8, g = (c0 >> 2) + gl;
+      const bool in = g < ng && row0 + R < rows;
+      const uint4 v = in ? wq[((size_t)g * rows + row0 + R) * 4 + jj] : make_uint4(0, 0, 0, 0);
+      reinterpret_cast<uint32_t*>(&s_w[4 * gl + 0][R])[jj] = v.x;
+      reinterpret_cast<uint32_t*>(&s_w[4 * gl + 1][R])[jj] = v.y;
+      reinterpret_cast<uint32_t*>(&s_w[4 * gl + 2][R])[jj] = v.z;
+      reinterpret_cast<uint32_t*>(&s_w[4 * gl + 3][R])[jj] = v.w;
+    }
+    {
+      const int R = t & 63, gl = t >> 6, g = (c0 >> 2) + gl;
+      const bool in = g < ng && row0 + R < rows;
+      const uint2 dv = in ? wd[(size_t)g * rows + row0 + R] : make_uint2(0, 0);
+      s_wd[4 * gl + 0][R] = h2f((uint16_t)(dv.x & 0xFFFFu)) * 0.0625f;
+      s_wd[4 * gl + 1][R] = h2f((uint16_t)(dv.x >> 16)) * 0.0625f;
+      s_wd[4 * gl + 2][R] = h2f((uint16_t)(dv.y & 0xFFFFu)) * 0.0625f;
+      s_wd[4 * gl + 3][R] = h2f((uint16_t)(dv.y >> 16)) * 0.0625f;
+    }
+    // the tokens' quants and scales
+#pragma unroll
+    for (int m = 0; m < 8; m++) {
+      const int i = t + 256 * m, half = i & 1, tk = (i >> 1) & 63, bl = i >> 7, b = c0 + bl, tok = tok0 + tk;
+      const bool in = b < nb && tok < T;
+      const XBlock* xb = x + (size_t)(in ? tok : 0) * nb + (in ? b : 0);
+      s_x[bl][tk][half] = in ? (half ? *reinterpret_cast<const uint4*>(&xb->hi) : *reinterpret_cast<const uint4*>(&xb->lo))
+                             : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int m = 0; m < 4; m++) {
+      const int i = t + 256 * m, tk = i & 63, bl = i >> 6, b = c0 + bl, tok = tok0 + tk;
+      const bool in = b < nb && tok < T;
+      s_xd[bl][tk] = in ? x[(size_t)tok * nb + b].d : 0.0f;
+    }
+    __syncthreads();
+    const int nbc = min(XG_CB, nb - c0);
+    for (int bl = 0; bl < nbc; bl++) {
+      uint32_t xl[4][4], xh[4][4];  // the four tokens' quants (lo: elements 0-15, hi: 16-31), one row at a time below
+      float xd[4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const uint4 a0 = s_x[bl][4 * tg + j][0], a1 = s_x[bl][4 * tg + j][1];
+        xl[j][0] = a0.x; xl[j][1] = a0.y; xl[j][2] = a0.z; xl[j][3] = a0.w;
+        xh[j][0] = a1.x; xh[j][1] = a1.y; xh[j][2] = a1.z; xh[j][3] = a1.w;
+        xd[j] = s_xd[bl][4 * tg + j];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const uint4 w = s_w[bl][4 * rg + i];
+        const float dw = s_wd[bl][4 * rg + i];
+        const uint32_t w4[4] = {w.x, w.y, w.z, w.w};
+        uint32_t wl[4], wh[4];
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+          wl[s] = ((w4[s] << 4) & 0xF0F0F0F0u) ^ 0x80808080u;  // 16 (low nibble - 8) per byte
+          wh[s] = (w4[s] & 0xF0F0F0F0u) ^ 0x80808080u;         // 16 (high nibble - 8)
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const float d = dw * xd[j];
+#pragma unroll
+          for (int s = 0; s < 4; s++) {
+            acc[i][j][s] = fmaf(d, (float)sdot4((int)wl[s], (int)xl[j][s], 0), acc[i][j][s]);
+            acc[i][j][s + 4] = fmaf(d, (float)sdot4((int)wh[s], (int)xh[j][s], 0), acc[i][j][s + 4]);
+          }
+        }
+      }
+    }
+    __syncthreads();  // the chunk's LDS is refilled next
+  }
+  // hsum_float_8 (ops.cpp:324-330): ((a0 + a4) + (a2 + a6)) + ((a1 + a5) + (a3 + a7))
+  float r[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const float* v = acc[i][j];
+      r[i][j] = ((v[0] + v[4]) + (v[2] + v[6])) + ((v[1] + v[5]) + (v[3] + v[7]));
+    }
+  if (!hq) {
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const int row = row0 + 4 * rg + i, tok = tok0 + 4 * tg + j;
+        if (row < rows && tok < T) out[(size_t)tok * ldo + row] = r[i][j];
+      }
+    return;
+  }
+  // GELU epilogue (gelu32 rows: 32 gate rows, then their 32 up rows): GELU(gate) * up of the work-group's 32
+  // hidden units for each token (model.cpp:892-899), quantized as one Q8_0 block per token (ops.cpp:116-139)
+  float* s_r = reinterpret_cast<float*>(&s_x[0][0][0]);  // [64 rows][65]
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+#pragma unroll
+    for (int j = 0; j < 4; j++) s_r[(4 * rg + i) * 65 + 4 * tg + j] = r[i][j];
+  __syncthreads();
+  const int u = t & 31, nh = rows / 64;
+  for (int tk = t >> 5; tk < XG_T; tk += 8) {
+    const int tok = tok0 + tk;
+    const float v = gelu_mul1<true>(s_r[u * 65 + tk], s_r[(32 + u) * 65 + tk]);
+    q8_block_store(v, tok < T, hq + (size_t)min(tok, T - 1) * nh + blockIdx.x, u);
+  }
 }
 
 }  // namespace
@@ -1517,6 +1821,42 @@ void launch_exact_gemv(const XlWeight& w, const XlArgs& a_in, int role, hipStrea
       break;
     default: throw std::runtime_error("exact gemv: bad role");
   }
+  LLMI_HIP(hipGetLastError());
+}
+
+
+void launch_exact_attn_batch(const XAttnArgs& a, int T, hipStream_t s) {
+  if (!exact_attn_supported(a.head_dim, a.n_head, a.n_head_kv) || !a.scores || !a.xq || !a.qh || !a.vt || T <= 0)
+    throw std::runtime_error("exact attention batch: unsupported shape");
+  const int nr = a.n_head + a.n_head_kv;
+  if (a.head_dim == 256) {
+    hipLaunchKernelGGL(xattn_qk_batch_kernel<256>, dim3(nr, T), dim3(64), 0, s, a);
+    hipLaunchKernelGGL((xattn_scores_kernel<256, true>), dim3(a.n_head, XA_NSPLIT, T), dim3(64), 0, s, a);
+    hipLaunchKernelGGL((xattn_accum_kernel<256, true>), dim3(a.n_head, T), dim3(320), 0, s, a);
+  } else {
+    hipLaunchKernelGGL(xattn_qk_batch_kernel<128>, dim3(nr, T), dim3(64), 0, s, a);
+    hipLaunchKernelGGL((xattn_scores_kernel<128, true>), dim3(a.n_head, XA_NSPLIT, T), dim3(64), 0, s, a);
+    hipLaunchKernelGGL((xattn_accum_kernel<128, true>), dim3(a.n_head, T), dim3(192), 0, s, a);
+  }
+  LLMI_HIP(hipGetLastError());
+}
+
+void launch_exact_norm_batch(const XpNormArgs& a, int T, hipStream_t s) {
+  if (a.n % 256 || a.n > 6 * 4 * 256 || T <= 0 || !a.resid || !a.w_next || !a.xq || (!a.table && (!a.y || !a.w_post)))
+    throw std::runtime_error("exact norm batch: bad arguments");
+  if (a.table && a.type != T_F16 && a.type != T_F32 && a.type != T_Q8_0)
+    throw std::runtime_error("exact norm batch: embedding table type");
+  const size_t lds = (size_t)2 * a.n * 4;
+  if (a.n <= 3 * 4 * 256) hipLaunchKernelGGL(xp_norm_kernel<3>, dim3(T), dim3(256), lds, s, a);
+  else hipLaunchKernelGGL(xp_norm_kernel<6>, dim3(T), dim3(256), lds, s, a);
+  LLMI_HIP(hipGetLastError());
+}
+
+void launch_exact_gemm(const XlWeight& w, const XBlock* x, int T, float* out, int ldo, XBlock* hq, hipStream_t s) {
+  if (!w.qs || w.nb % 4 || w.rows % 16 || T <= 0 || !x || (!out && !hq)) throw std::runtime_error("exact gemm: bad arguments");
+  if (hq && w.rows % 64) throw std::runtime_error("exact gemm: GELU rows % 64 != 0");
+  const dim3 grid((unsigned)((w.rows + XG_R - 1) / XG_R), (unsigned)((T + XG_T - 1) / XG_T));
+  hipLaunchKernelGGL(xp_gemm_kernel, grid, dim3(256), 0, s, w.qs, w.d, w.rows, w.nb, x, T, out, ldo, hq);
   LLMI_HIP(hipGetLastError());
 }
 

@@ -620,7 +620,7 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
         maxhd0 = std::max(maxhd0, l.hd);
       }
       blk_epoch_ = dalloc<unsigned>(hp_.n_layer);
-      blk_done_ = dalloc<unsigned>(1);
+      blk_done_ = dalloc<unsigned>((size_t)hp_.n_layer * 32);  // (a 128-B line per layer)
       blk_gqkv_stride_ = (size_t)maxrows;
       blk_gxo_stride_ = (size_t)nh_ * maxhd0 / 32 * 12;
       blk_gqkv_ = dalloc<uint2>((size_t)hp_.n_layer * blk_gqkv_stride_);
@@ -1169,7 +1169,7 @@ void Session::record_layers_fused(hipStream_t s, bool x_q8) {
       if (pxf) fx_out(go);
       BlockSync bs;
       bs.epoch = epoch;
-      bs.done = blk_done_;
+      bs.done = blk_done_ + (size_t)l * 32;
       bs.g_qkv = blk_gqkv_ + (size_t)l * blk_gqkv_stride_;
       bs.g_xo = blk_gxo_ + (size_t)l * blk_gxo_stride_;
       bs.err = blk_err_;
@@ -1476,6 +1476,104 @@ void Session::record_layers_xl(hipStream_t s) {
   kernels_per_token_++;
 }
 
+bool Session::xp_ok() const {
+  return xl_ && !tp_ && !dump_ && !trace_fn_ && (embd_.type == T_F16 || embd_.type == T_F32 || embd_.type == T_Q8_0) &&
+         hp_.n_embd % 256 == 0 && hp_.n_embd <= 6144 && getenv("LLMI_XP_OFF") == nullptr;
+}
+
+void Session::exact_prefill(const int32_t* tokens, int n, int pos) {
+  hipStream_t s = stream_;
+  const int E = hp_.n_embd, F = hp_.n_ff;
+  int chunk = 256;
+  if (const char* c = getenv("LLMI_XP_CHUNK")) chunk = std::max(1, atoi(c));
+  const int cap = std::min(chunk, n);
+  if (cap > xp_cap_) {  // grow-only chunk buffers
+    int maxq = 0, maxqkv = 0;
+    for (const auto& l : L_) {
+      maxq = std::max(maxq, hp_.n_head * l.hd);
+      maxqkv = std::max(maxqkv, l.qkv_rows);
+    }
+    xp_tok_ = dalloc<int32_t>(cap);
+    xp_resid_ = dalloc<float>((size_t)cap * E);
+    xp_o_ = dalloc<float>((size_t)cap * E);
+    xp_d_ = dalloc<float>((size_t)cap * E);
+    xp_qkv_ = dalloc<float>((size_t)cap * maxqkv);
+    xp_att_ = dalloc<float>((size_t)cap * maxq);
+    xp_xq_ = dalloc<XBlock>((size_t)cap * (E / 32));
+    xp_hq_ = dalloc<XBlock>((size_t)cap * (F / 32));
+    xp_axq_ = dalloc<XBlock>((size_t)cap * (maxq / 32));
+    xp_qh_ = dalloc<uint16_t>((size_t)cap * maxq);
+    xp_sc_ = dalloc<double>((size_t)cap * hp_.n_head * max_ctx_);
+    xp_cap_ = cap;
+  }
+  for (int c0 = 0; c0 < n; c0 += cap) {
+    const int T = std::min(cap, n - c0);
+    LLMI_HIP(hipMemcpyAsync(xp_tok_, tokens + c0, (size_t)T * 4, hipMemcpyHostToDevice, s));
+    LLMI_HIP(hipStreamSynchronize(s));  // (the host array may go away)
+    set_token_pos(tokens[c0], pos + c0, c0 == 0);  // d_pos: the chunk's first position
+    for (int l = 0; l < hp_.n_layer; l++) {
+      LayerDev& Ld = L_[l];
+      XpNormArgs na;  // residual step + attn_norm, or the embedding (model.cpp:709-736, 843-858)
+      na.resid = xp_resid_;
+      na.w_next = Ld.attn_norm;
+      na.xq = xp_xq_;
+      na.n = E;
+      na.eps = hp_.eps;
+      if (l == 0) {
+        na.table = embd_raw_;
+        na.row_bytes = embd_row_bytes_;
+        na.type = embd_.type;
+        na.tokens = xp_tok_;
+        na.emb_scale = std::sqrt(static_cast<float>(E));  // model.cpp:337-338
+      } else {
+        na.y = xp_d_;
+        na.w_post = L_[l - 1].post_ffw_norm;
+      }
+      launch_exact_norm_batch(na, T, s);
+      launch_exact_gemm(Ld.xqkv, xp_xq_, T, xp_qkv_, Ld.qkv_rows, nullptr, s);
+      XAttnArgs xa;
+      xa.qkv = xp_qkv_;
+      xa.qkv_stride = Ld.qkv_rows;
+      xa.k_off = Ld.k_off;
+      xa.v_off = Ld.v_off;
+      xa.n_head = hp_.n_head;
+      xa.n_head_kv = hp_.n_head_kv;
+      xa.head_dim = Ld.hd;
+      xa.q_norm_w = Ld.q_norm;
+      xa.k_norm_w = Ld.k_norm;
+      xa.rope_cs = Ld.is_swa ? rope_swa_ : rope_glb_;
+      xa.attn_scale = hp_.attn_scale;
+      xa.eps = hp_.eps;
+      xa.k_cache = Ld.kc;
+      xa.v_cache = Ld.vc;
+      xa.max_ctx = max_ctx_;
+      xa.d_pos = d_pos_;
+      xa.scores = xp_sc_;
+      xa.out = xp_att_;
+      xa.xq = xp_axq_;
+      xa.softcap = hp_.attn_softcap;
+      xa.vt = Ld.vt;
+      xa.vt_stride = xa_vt_stride_;
+      xa.kmeta = Ld.kmeta;
+      xa.qh = xp_qh_;
+      launch_exact_attn_batch(xa, T, s);
+      if (l + 1 == hp_.n_layer) break;  // the last layer's K / V are in the cache: nothing after it is kept
+      launch_exact_gemm(Ld.xo, xp_axq_, T, xp_o_, E, nullptr, s);
+      XpNormArgs nf;  // post-attention norm + residual, ffn_norm (model.cpp:843-858, 872-881)
+      nf.y = xp_o_;
+      nf.w_post = Ld.post_attn_norm;
+      nf.resid = xp_resid_;
+      nf.w_next = Ld.ffn_norm;
+      nf.xq = xp_xq_;
+      nf.n = E;
+      nf.eps = hp_.eps;
+      launch_exact_norm_batch(nf, T, s);
+      launch_exact_gemm(Ld.xgu, xp_xq_, T, nullptr, 0, xp_hq_, s);
+      launch_exact_gemm(Ld.xdn, xp_hq_, T, xp_d_, E, nullptr, s);
+    }
+  }
+}
+
 void Session::record_layers(hipStream_t s, bool x_q8) {
   const int E = hp_.n_embd, F = hp_.n_ff;
   auto is_q8 = [](uint32_t t) { return t == T_Q4_0 || t == T_Q8_0; };
@@ -1639,6 +1737,10 @@ void Session::forward(const int32_t* tokens, int n, int pos, float* logits, int3
     if (n > 1 && prefill_ok_ && getenv("LLMI_NO_PREFILL") == nullptr) {
       set_token_pos(tokens[n - 1], pos + n - 1, true);  // what the token loop leaves behind
       prefill(tokens, n, pos);
+    } else if (n > 1 && xp_ok()) {  // exact mode: the prompt but its last token batched, then the last one's step
+      exact_prefill(tokens, n - 1, pos);
+      set_token_pos(tokens[n - 1], pos + n - 1, false);
+      run_step(STEP_LOGITS);
     } else {
       for (int i = 0; i < n; i++) {  // only the last token's logits are computed (model.cpp:983-1001)
         set_token_pos(tokens[i], pos + i, i == 0);
@@ -1955,7 +2057,7 @@ void Session::time_kernel(int which, int reps, double* us, double* bytes) {
                          go.out = o_out_;
                          BlockSync bs;
                          bs.epoch = blk_epoch_ + i;  // (the launch advances it itself: every timed launch waits)
-                         bs.done = blk_done_;
+                         bs.done = blk_done_ + i * 32;
                          bs.g_qkv = blk_gqkv_ + i * blk_gqkv_stride_;
                          bs.g_xo = blk_gxo_ + i * blk_gxo_stride_;
                          bs.err = blk_err_;

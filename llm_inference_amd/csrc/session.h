@@ -111,6 +111,17 @@ class Session {
   XBlock* xa_xq_ = nullptr;      // exact attention output's Q8_0 blocks (the o projection's x)
   void setup_xl();
   void record_layers_xl(hipStream_t s);
+  // exact mode's prompt: tokens [0, n) at positions pos.. through every layer, T at a time (k_exact.hip batched
+  // kernels), leaving their K / V in the caches -- the reference computes nothing else of them that is kept
+  // (model.cpp:983-1001: the logits of the last prompt position only, which runs as a decode step)
+  bool xp_ok() const;
+  void exact_prefill(const int32_t* tokens, int n, int pos);
+  int xp_cap_ = 0;
+  int32_t* xp_tok_ = nullptr;
+  float *xp_resid_ = nullptr, *xp_o_ = nullptr, *xp_d_ = nullptr, *xp_qkv_ = nullptr, *xp_att_ = nullptr;
+  XBlock *xp_xq_ = nullptr, *xp_hq_ = nullptr, *xp_axq_ = nullptr;
+  uint16_t* xp_qh_ = nullptr;
+  double* xp_sc_ = nullptr;
   void prepare_act(uint32_t wtype, const float* x, int n, ActBuf& act, hipStream_t s);
   void gemv_parts(const std::vector<GemvPart>& parts, const float* x, int n_in, float* out, hipStream_t s,
                   bool x_ready);
@@ -155,8 +166,8 @@ class Session {
   bool block_ = false;        // fast path: qkv + attention + o as one launch per layer (k_attn.hip)
   bool block_pro_ = false;
   long long slow_waits_ = 0;  // block hand-off waits over 20 us (blk_err_[1], accumulated at every sync)
-  // the attention block's granule tags: [n_layer] launch counts, each advanced by its own launch's last
-  // retiring work-group (blk_done_: the launch's retired work-groups, back to 0 at its end)
+  // the attention block's granule tags: [n_layer] launch counts, each advanced by its own launch
+  // (BlockSync::done: [n_layer] the launch's counted work-groups, back to 0 when it advances)
   unsigned* blk_epoch_ = nullptr;
   unsigned* blk_done_ = nullptr;
   uint2* blk_gqkv_ = nullptr;      // [n_layer][qkv rows] granules

@@ -98,12 +98,15 @@ struct LayerGemv {
 // qkv rows -> the kv head's attention work-groups -> the o projection, as
 // data-tagged granules (common.h st_granule / ld_granules) in per-layer buffers.
 struct BlockSync {
-  // this layer's launch count: tag = *epoch + 1, read by every work-group at its start; the launch advances it
-  // itself -- every work-group adds one to *done when it retires, and the last (done = grid size) resets done and
-  // advances the epoch, so no launch sequence (timed launches alone, a skipped or repeated neighbour launch) can
-  // leave a tag that the next launch would take for its own
+  // this layer's launch count: granule tag = *epoch + 1, read by every wave at its start.  The launch advances it
+  // itself, once every wave of it has read it: *done counts the o work-groups (each once its waves have used
+  // their tag) and the kv heads' final merges (each once every split of its head -- and so every qkv work-group
+  // those splits waited on -- has used it); the add that completes the count (done_n) resets *done and advances
+  // *epoch.  So no launch sequence (timed launches alone, a skipped or repeated neighbour launch) can leave a tag
+  // that the next launch would take for its own, and no add sits on the launch's critical path
   unsigned* epoch = nullptr;
   unsigned* done = nullptr;
+  unsigned done_n = 0;
   uint2* g_qkv = nullptr;           // [qkv rows] granules of the qkv GEMV output
   uint2* g_xo = nullptr;            // [n_head * head_dim / 32][12] granules of the attention output's Q8_0 blocks
   int* err = nullptr;               // set when a bounded wait gives up (the step's results are invalid)
