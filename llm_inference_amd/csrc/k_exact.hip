@@ -1580,7 +1580,12 @@ __global__ __launch_bounds__(256) void xp_norm_kernel(XpNormArgs a) {
 // The integer dots take the nibbles as 16 (n - 8) (one shift-and-xor, signed bytes) and the scale as d / 16:
 // 16 isum and d / 16 are exact rescalings, so every fma sees the reference's product d * isum.  Chunks of
 // XG_CB blocks of the rows' weights and the tokens' quants are staged in LDS.
+// The integer dot's conversion and the fma run packed (XG_PK, default): sdot4 accumulates onto the bits of 1.5 x 2^23,
+// so the int32 result read as a float is 12582912 + 16 isum exactly (|16 isum| < 2^22), one v_pk_add_f32 removes the
+// offset for two accumulators (exact: Sterbenz) and one v_pk_fma_f32 updates both (each lane's fma rounds once, as
+// fmaf): 17 instead of 25 VALU issues per (row, token, block).  -DXG_NO_PK: the scalar form.
 constexpr int XG_R = 64, XG_T = 64, XG_CB = 16;
+typedef float xg_f2 __attribute__((ext_vector_type(2)));
 __global__ __launch_bounds__(256, 2) void xp_gemm_kernel(const uint4* __restrict__ wq, const uint2* __restrict__ wd,
                                                          int rows, int nb, const XBlock* __restrict__ x, int T,
                                                          float* __restrict__ out, int ldo, XBlock* __restrict__ hq) {
@@ -1590,13 +1595,13 @@ __global__ __launch_bounds__(256, 2) void xp_gemm_kernel(const uint4* __restrict
   __shared__ float s_xd[XG_CB][XG_T];
   const int t = threadIdx.x, rg = t & 15, tg = t >> 4;
   const int row0 = blockIdx.x * XG_R, tok0 = blockIdx.y * XG_T, ng = nb >> 2;
-  float acc[4][4][8];
+  xg_f2 acc[4][4][4];  // accumulators s (x) and s + 4 (y) of (row 4 rg + i, token 4 tg + j)
 #pragma unroll
   for (int i = 0; i < 4; i++)
 #pragma unroll
     for (int j = 0; j < 4; j++)
 #pragma unroll
-      for (int s = 0; s < 8; s++) acc[i][j][s] = 0.0f;
+      for (int s = 0; s < 4; s++) acc[i][j][s] = xg_f2{0.0f, 0.0f};
   for (int c0 = 0; c0 < nb; c0 += XG_CB) {
     // weights: XL qs[g][row][jj] = word jj of the group's 4 blocks -> s_w[block][row] words jj
 #pragma unroll
@@ -1661,8 +1666,16 @@ __global__ __launch_bounds__(256, 2) void xp_gemm_kernel(const uint4* __restrict
           const float d = dw * xd[j];
 #pragma unroll
           for (int s = 0; s < 4; s++) {
-            acc[i][j][s] = fmaf(d, (float)sdot4((int)wl[s], (int)xl[j][s], 0), acc[i][j][s]);
-            acc[i][j][s + 4] = fmaf(d, (float)sdot4((int)wh[s], (int)xh[j][s], 0), acc[i][j][s + 4]);
+#ifdef XG_NO_PK
+            acc[i][j][s].x = fmaf(d, (float)sdot4((int)wl[s], (int)xl[j][s], 0), acc[i][j][s].x);
+            acc[i][j][s].y = fmaf(d, (float)sdot4((int)wh[s], (int)xh[j][s], 0), acc[i][j][s].y);
+#else
+            constexpr int MAGIC = 0x4B400000;  // 1.5 x 2^23
+            const xg_f2 p = xg_f2{__int_as_float(sdot4((int)wl[s], (int)xl[j][s], MAGIC)),
+                                  __int_as_float(sdot4((int)wh[s], (int)xh[j][s], MAGIC))} -
+                            xg_f2{12582912.0f, 12582912.0f};
+            acc[i][j][s] = __builtin_elementwise_fma(xg_f2{d, d}, p, acc[i][j][s]);
+#endif
           }
         }
       }
@@ -1675,8 +1688,8 @@ __global__ __launch_bounds__(256, 2) void xp_gemm_kernel(const uint4* __restrict
   for (int i = 0; i < 4; i++)
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-      const float* v = acc[i][j];
-      r[i][j] = ((v[0] + v[4]) + (v[2] + v[6])) + ((v[1] + v[5]) + (v[3] + v[7]));
+      const xg_f2* v = acc[i][j];  // v[s].x = a_s, v[s].y = a_(s + 4)
+      r[i][j] = ((v[0].x + v[0].y) + (v[2].x + v[2].y)) + ((v[1].x + v[1].y) + (v[3].x + v[3].y));
     }
   if (!hq) {
 #pragma unroll

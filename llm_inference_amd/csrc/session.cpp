@@ -634,6 +634,9 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
       for (const auto& l : L_) maxhd = std::max(maxhd, l.hd);
       blk_xo_ = dalloc<XBlock>((size_t)nh_ * maxhd / 32 + 1);
     }
+    // the batched prefill's chunk buffers for a default-sized prompt now, not inside the first forward (the
+    // allocations and their zeroing were ~3 ms of the first 512-token prefill: 14.3 vs 11.0 ms)
+    if (prefill_ok_) ensure_prefill_buffers(std::min(512, max_ctx_));
     LLMI_HIP(hipStreamSynchronize(stream_));  // every zeroing and copy above complete before the first call
     constructing_ = false;
     session_constructed(true);
@@ -956,19 +959,23 @@ bool Session::prefill_run(const int32_t* tokens, int n, int pos, bool allow_f16)
                    !getenv("LLMI_PREFILL_ATTN_V1") && (G == 1 || G == 2 || G == 4) &&
                    layer_gemv_gelu_group(L_[0].gate_up[0].w.cols, L_[0].gate_up[0].w.type) % 8 == 0;
   const int q8k = pf_kq_ && !f16 ? 1 : 0;
+  // t0: the first token row the rest of a layer runs on (the last layer: only the prompt's final token needs its
+  // o / FFN -- every other token's last-layer state is its K / V rows, already in the cache: model.cpp:983-1001)
+  int t0 = 0;
   auto gemm = [&](const DevWeight& w, float* out, int ostride) {
-    if (f16) launch_prefill_gemm16(w, pf_x16_, X16, T_cur_, out, ostride, s);
-    else launch_prefill_gemm(w, pf_xq_, XS, T_cur_, out, ostride, s);
+    if (f16) launch_prefill_gemm16(w, pf_x16_ + (size_t)t0 * X16, X16, T_cur_, out + (size_t)t0 * ostride, ostride, s);
+    else launch_prefill_gemm(w, pf_xq_ + (size_t)t0 * XS, XS, T_cur_, out + (size_t)t0 * ostride, ostride, s);
   };
   auto xtap = [&](const char* name, int l) {
-    if (f16) tap(name, l, pf_x16_, (size_t)T_cur_ * X16 * 2, s);
-    else tap(name, l, pf_xq_, (size_t)T_cur_ * XS * sizeof(XBlock), s);
+    if (f16) tap(name, l, pf_x16_ + (size_t)t0 * X16, (size_t)T_cur_ * X16 * 2, s);
+    else tap(name, l, pf_xq_ + (size_t)t0 * XS, (size_t)T_cur_ * XS * sizeof(XBlock), s);
   };
   auto xgather = [&](int cols) {  // this rank's activation columns [r * cols, (r + 1) * cols) to every rank
     if (!tp_) return;
-    if (f16) gather_cols(pf_x16_, (size_t)X16 * 2, (size_t)cols * 2, T_cur_, s);
-    else gather_cols(pf_xq_, (size_t)XS * sizeof(XBlock), (size_t)(cols / 32) * sizeof(XBlock), T_cur_, s);
+    if (f16) gather_cols(pf_x16_ + (size_t)t0 * X16, (size_t)X16 * 2, (size_t)cols * 2, T_cur_, s);
+    else gather_cols(pf_xq_ + (size_t)t0 * XS, (size_t)XS * sizeof(XBlock), (size_t)(cols / 32) * sizeof(XBlock), T_cur_, s);
   };
+  const bool trim = getenv("LLMI_PREFILL_FULL_LAST") == nullptr;  // (A/B: the last layer over every token)
   for (int c0 = 0; c0 < n; c0 += pf_cap_) {
     const int T = std::min(pf_cap_, n - c0), p0 = pos + c0;
     T_cur_ = T;
@@ -993,6 +1000,8 @@ bool Session::prefill_run(const int32_t* tokens, int n, int pos, bool allow_f16)
     for (int l = 0; l < hp_.n_layer; l++) {
       const LayerDev& Ld = L_[l];
       const int hd = Ld.hd;
+      t0 = 0;
+      T_cur_ = T;
       xtap("pf_x_qkv", l);
       for (size_t pi = 0, r0 = 0; pi < Ld.qkv.size(); r0 += Ld.qkv[pi].w.rows, pi++)  // q|k|v, or q|k and v (kq)
         gemm(Ld.qkv[pi].w, pf_out_ + r0, Ld.qkv_rows);
@@ -1016,59 +1025,66 @@ bool Session::prefill_run(const int32_t* tokens, int n, int pos, bool allow_f16)
       qk.max_ctx = max_ctx_;
       qk.pos0 = p0;
       launch_prefill_qk(qk, T, s);
+      if (trim && l + 1 == hp_.n_layer) {  // the last layer past its K / V appends: the final token only
+        if (!last_chunk) break;
+        t0 = T - 1;
+        T_cur_ = 1;
+      }
+      const int Tq = T_cur_;
       PrefillAttn at;
       at.softcap = hp_.attn_softcap;
-      at.q = pf_q_;
+      at.q = pf_q_ + (size_t)t0 * nh_ * hd;
       at.k_cache = Ld.kc;
       at.v_cache = Ld.vc;
       at.n_head = nh_;
       at.n_head_kv = nkv_;
       at.head_dim = hd;
       at.max_ctx = max_ctx_;
-      at.pos0 = p0;
+      at.pos0 = p0 + t0;
       const int hb = nh_ * hd / 32;  // this rank's heads' Q8_0 blocks per token
       const int hr = tp_rep_attn_ ? 0 : r;  // replicated attention: every rank has all heads
-      at.xq = pf_xq_ + (size_t)hr * hb;
+      at.xq = pf_xq_ + (size_t)t0 * XS + (size_t)hr * hb;
       at.xstride = XS;
-      at.x16 = f16 ? pf_x16_ + (size_t)hr * nh_ * hd : nullptr;
+      at.x16 = f16 ? pf_x16_ + (size_t)t0 * X16 + (size_t)hr * nh_ * hd : nullptr;
       at.x16stride = X16;
       at.q8k = q8k;
       at.ks = pf_attn_ks_;
       at.part = pf_apart_;
-      launch_prefill_attn(at, T, s);
+      launch_prefill_attn(at, Tq, s);
       if (!tp_rep_attn_) xgather(nh_ * hd);
       tap("pf_q", l, pf_q_, (size_t)T * nh_ * hd * 2, s);
       tap("kc", l, Ld.kc, (size_t)nkv_ * max_ctx_ * hd * 2, s);
       tap("vc", l, Ld.vc, (size_t)nkv_ * max_ctx_ * hd * 2, s);
       xtap("pf_x_o", l);
       gemm(Ld.o.w, pf_out_ + (size_t)r * e_sh_, E);
-      if (tp_) gather_cols(pf_out_, (size_t)E * 4, (size_t)e_sh_ * 4, T, s);
-      tap("pf_o", l, pf_out_, (size_t)T * E * 4, s);
+      if (tp_) gather_cols(pf_out_ + (size_t)t0 * E, (size_t)E * 4, (size_t)e_sh_ * 4, Tq, s);
+      tap("pf_o", l, pf_out_ + (size_t)t0 * E, (size_t)Tq * E * 4, s);
       PrefillNorm rn;  // post-attention norm + residual, then ffn_norm
-      rn.y = pf_out_;
+      rn.y = pf_out_ + (size_t)t0 * E;
       rn.w_post = Ld.post_attn_norm;
-      rn.resid = pf_resid_;
+      rn.resid = pf_resid_ + (size_t)t0 * E;
       rn.w_next = Ld.ffn_norm;
-      rn.xq = pf_xq_;
+      rn.xq = pf_xq_ + (size_t)t0 * XS;
       rn.xstride = XS;
       rn.n = E;
       rn.eps = hp_.eps;
-      rn.x16 = f16 ? pf_x16_ : nullptr;
+      rn.x16 = f16 ? pf_x16_ + (size_t)t0 * X16 : nullptr;
       rn.x16stride = X16;
       rn.q8k = q8k;
-      launch_prefill_norm(rn, T, s);
-      tap("pf_resid_attn", l, pf_resid_, (size_t)T * E * 4, s);
+      launch_prefill_norm(rn, Tq, s);
+      tap("pf_resid_attn", l, rn.resid, (size_t)Tq * E * 4, s);
       xtap("pf_x_gate_up", l);
       const int FL = tp_ ? f_sh_ : F;  // this rank's hidden units
       gemm(Ld.gate_up[0].w, pf_out_, 2 * FL);
-      tap("pf_gate_up", l, pf_out_, (size_t)T * 2 * F * 4, s);
-      launch_prefill_gelu(pf_out_, FL, layer_gemv_gelu_group(Ld.gate_up[0].w.cols, Ld.gate_up[0].w.type),
-                          pf_xq_ + (size_t)r * (FL / 32), XS, T, s, f16 ? pf_x16_ + (size_t)r * FL : nullptr, X16, q8k);
+      tap("pf_gate_up", l, pf_out_ + (size_t)t0 * 2 * FL, (size_t)Tq * 2 * F * 4, s);
+      launch_prefill_gelu(pf_out_ + (size_t)t0 * 2 * FL, FL, layer_gemv_gelu_group(Ld.gate_up[0].w.cols, Ld.gate_up[0].w.type),
+                          pf_xq_ + (size_t)t0 * XS + (size_t)r * (FL / 32), XS, Tq, s,
+                          f16 ? pf_x16_ + (size_t)t0 * X16 + (size_t)r * FL : nullptr, X16, q8k);
       xgather(FL);
       xtap("pf_x_down", l);
       gemm(Ld.down.w, pf_out_ + (size_t)r * e_sh_, E);
-      if (tp_) gather_cols(pf_out_, (size_t)E * 4, (size_t)e_sh_ * 4, T, s);
-      tap("pf_down", l, pf_out_, (size_t)T * E * 4, s);
+      if (tp_) gather_cols(pf_out_ + (size_t)t0 * E, (size_t)E * 4, (size_t)e_sh_ * 4, Tq, s);
+      tap("pf_down", l, pf_out_ + (size_t)t0 * E, (size_t)Tq * E * 4, s);
       if (l + 1 < hp_.n_layer) {  // post-ffw norm + residual, then the next attn_norm
         PrefillNorm fn = rn;
         fn.w_post = Ld.post_ffw_norm;

@@ -199,3 +199,30 @@ def test_kquant_batched_prefill(monkeypatch, oracle, mode):
     assert int(np.argmax(lp)) == int(np.argmax(ll)) == int(np.argmax(ref))
     assert ids_p.tolist() == ids_l.tolist()
     np.testing.assert_array_equal(_model(g, monkeypatch, chunk=41).forward(prompt, 0), lp)
+
+
+@pytest.mark.parametrize("cfg_name,n_prompt,chunk", [("mini-4b", 300, None), ("mini-4b", 300, 128),
+                                                      ("mini-1b", 77, None), ("mini-27b", 45, None)])
+def test_prefill_last_layer_final_token_only(cfg_name, n_prompt, chunk, monkeypatch):
+    """Round 6: past its K / V appends the last layer runs its attention, o and FFN for the prompt's final token
+    only (nothing else a prompt token computes there is kept: model.cpp:983-1001), and a non-final chunk skips
+    them.  A token's rows do not depend on the other tokens of the launch, so the logits and the decode that
+    follows must equal the full last layer's (LLMI_PREFILL_FULL_LAST=1) bit for bit."""
+    from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
+    cfg = CONFIGS[cfg_name]
+    g = build_gemma3_gguf(cfg, seed=31)
+    rng = np.random.default_rng(n_prompt)
+    prompt = np.concatenate([[2], rng.integers(4, cfg.vocab, n_prompt - 1)]).astype(np.int32)
+    out = {}
+    for full in (True, False):
+        if full:
+            monkeypatch.setenv("LLMI_PREFILL_FULL_LAST", "1")
+        else:
+            monkeypatch.delenv("LLMI_PREFILL_FULL_LAST", raising=False)
+        m = _model(g, monkeypatch, chunk=chunk)
+        lg = m.forward(prompt, 0)
+        ids = m.generate(int(np.argmax(lg)), n_prompt, 8).tolist()
+        m.close()
+        out[full] = (lg, ids)
+    np.testing.assert_array_equal(out[False][0].view(np.uint32), out[True][0].view(np.uint32))
+    assert out[False][1] == out[True][1]
