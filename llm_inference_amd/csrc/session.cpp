@@ -638,6 +638,15 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
     // allocations and their zeroing were ~3 ms of the first 512-token prefill: 14.3 vs 11.0 ms)
     if (prefill_ok_) ensure_prefill_buffers(std::min(512, max_ctx_));
     LLMI_HIP(hipStreamSynchronize(stream_));  // every zeroing and copy above complete before the first call
+    // one two-token batched prefill at position 0 (one device): the first forward of a session paid ~3 ms more
+    // than later ones (14.3 vs 11.2 ms for 512 tokens: the prefill kernels' first launches), now paid here; the
+    // K / V rows it writes are rewritten by the first prompt (LLMI_NO_WARMUP=1: skip)
+    if (prefill_ok_ && !tp_ && max_ctx_ >= 2 && getenv("LLMI_NO_WARMUP") == nullptr) {
+      const int32_t warm[2] = {0, 0};
+      set_token_pos(warm[1], 1, true);
+      prefill(warm, 2, 0);
+      LLMI_HIP(hipStreamSynchronize(stream_));
+    }
     constructing_ = false;
     session_constructed(true);
   } catch (const gguf_error& e) {

@@ -13,5 +13,5 @@ for p in sys.argv[1:]:
     fam = {k: v["us_per_launch"] for k, v in d.get("kernel_families", {}).items()}
     ex = d.get("exact", {})
     print(f"{p}: {d['value']} tok/s ({d['ms_per_step']} ms)", fam,
-          f"exact {ex.get('value')} tok/s prefill {ex.get('prefill_s')} s" if ex else "",
-          f"prefill {d['timing_detail']['prefill_s']} s")
+          f"exact {ex.get('value')} tok/s prefill {ex.get('prefill_s')} / warm {ex.get('prefill_warm_s')} s" if ex else "",
+          f"prefill {d['timing_detail']['prefill_s']} / warm {d['timing_detail'].get('prefill_warm_s')} s")
