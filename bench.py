@@ -613,6 +613,7 @@ def main():
             "ms_per_step": round(el_x * 1000.0 / a.steps, 4),
             "positions": f"{a.prefill + n_chk}-{a.prefill + n_chk + a.steps - 1}",
             "exact_engine": bool(getattr(xinfo, "exact_engine", 0)), "kernels_per_token": xinfo.kernels_per_token,
+            "batched_prefill": bool(getattr(xinfo, "exact_batched_prefill", 0)),
             "prefill_s": round(t_pf_x, 3), "prefill_warm_s": round(t_pf_xw, 3),
             "how": "a second session with LLMI_EXACT (bit-identical to the reference's logits: "
                    "parity_vs_reference.exact), the same prompt, then the same timed decode"}

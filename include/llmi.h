@@ -215,6 +215,8 @@ typedef struct {
   long long block_slow_waits; /* attention-block hand-off waits (per wave) that took over 20 us, since creation */
   int exact_engine;           /* 1: LLMI_EXACT runs on the exact-order engine (k_exact.hip: the reference's
                                  arithmetic with streamed GEMVs and fused norms), 0: the per-op exact kernels */
+  int exact_batched_prefill;  /* 1: an exact session runs a prompt's tokens before the last layer by layer, T at a
+                                 time (the reference's chains per (row, token)), then the last as a decode step */
 } llmi_session_info;
 int llmi_session_get_info(const llmi_session* s, llmi_session_info* info);
 

@@ -1855,7 +1855,7 @@ void launch_exact_attn_batch(const XAttnArgs& a, int T, hipStream_t s) {
 }
 
 void launch_exact_norm_batch(const XpNormArgs& a, int T, hipStream_t s) {
-  if (a.n % 256 || a.n > 6 * 4 * 256 || T <= 0 || !a.resid || !a.w_next || !a.xq || (!a.table && (!a.y || !a.w_post)))
+  if (a.n % 128 || a.n > 6 * 4 * 256 || T <= 0 || !a.resid || !a.w_next || !a.xq || (!a.table && (!a.y || !a.w_post)))
     throw std::runtime_error("exact norm batch: bad arguments");
   if (a.table && a.type != T_F16 && a.type != T_F32 && a.type != T_Q8_0)
     throw std::runtime_error("exact norm batch: embedding table type");

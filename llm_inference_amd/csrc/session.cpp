@@ -1503,7 +1503,7 @@ void Session::record_layers_xl(hipStream_t s) {
 
 bool Session::xp_ok() const {
   return xl_ && !tp_ && !dump_ && !trace_fn_ && (embd_.type == T_F16 || embd_.type == T_F32 || embd_.type == T_Q8_0) &&
-         hp_.n_embd % 256 == 0 && hp_.n_embd <= 6144 && getenv("LLMI_XP_OFF") == nullptr;
+         hp_.n_embd % 128 == 0 && hp_.n_embd <= 6144 && getenv("LLMI_XP_OFF") == nullptr;
 }
 
 void Session::exact_prefill(const int32_t* tokens, int n, int pos) {
@@ -1971,6 +1971,7 @@ void Session::info(llmi_session_info* o) const {
   o->tp_exchange = coll_ ? (px_fused_ && coll_->kind() == EX_PUSH ? EX_PUSH_FUSED : coll_->kind()) : 0;
   o->block_slow_waits = slow_waits_;
   o->exact_engine = xl_ ? 1 : 0;
+  o->exact_batched_prefill = xp_ok() ? 1 : 0;
   size_t b = logits_w_.bytes;  // this rank's bytes
   for (const auto& l : L_) {
     for (const auto& p : l.qkv) b += p.w.bytes;

@@ -16,6 +16,7 @@ def _run(g, prompt, forced, monkeypatch, env):
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     m = Model(g, exact=True, max_ctx=len(prompt) + len(forced) + 8)
+    assert m.get_info().exact_batched_prefill == (0 if "LLMI_XP_OFF" in env else 1)
     out = [m.forward(prompt, 0)]
     for i, t in enumerate(forced):
         out.append(m.forward(np.array([t], np.int32), len(prompt) + i))
