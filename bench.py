@@ -576,7 +576,11 @@ def main():
         "timing_detail": {"synthetic_build_s": round(t_build, 1), "prefill_s": round(t_prefill, 4),
                           "prefill_tokens_per_s": round(a.prefill / t_prefill, 1),
                           "prefill_warm_s": round(t_prefill_warm, 4),
-                          "prefill_mode": "batched int8-MFMA" if info.batched_prefill else "token loop",
+                          "prefill_mode": ({7: "batched f16-MFMA (GEMM v7 gate_up, v6 qkv / o / down; f16 rows of the "
+                                                "dequantized Q8_0 activations)", 6: "batched f16-MFMA (v6, K-quants)",
+                                            5: "batched int8-MFMA (GEMM v5, Q8_0 activation blocks)"}
+                                           .get(getattr(info, "prefill_gemm", 5), "batched")
+                                           if info.batched_prefill else "token loop"),
                           # attention-block hand-off waits (per wave) over 20 us since the session was created
                           # (prefill tail, warmup, timed steps, kernel timing): the spin-wait outlier check
                           "block_slow_waits": m.get_info().block_slow_waits},

@@ -205,8 +205,9 @@ typedef struct {
   int screened_logits;        /* 1: llmi_session_enqueue/generate pick each greedy token by int8 screening +
                                  exact f16 rescoring (same ids as the full F16 logits GEMV; forward keeps it) */
   size_t screen_bytes;        /* bytes of the int8 screening table streamed per decode-loop token */
-  int prefill_f16_redo;       /* opt-in f16 prefills (LLMI_PREFILL_F16) whose f16 activations overflowed and were
-                                 recomputed on the int8 path (never a non-finite result) */
+  int prefill_f16_redo;       /* f16 prefills whose final norm row came out non-finite and were recomputed on the
+                                 int8 path (never a non-finite result; the per-token scales make it unreachable short
+                                 of an attention output past 65504) */
   int layer_engine;           /* always 0: the round-3 layer engine (one launch per decode layer) measured slower
                                  than three launches and was removed in round 6 */
   int ffn_engine;             /* always 0: the FFN engine (gate_up + GELU + down as one launch), likewise */
@@ -217,6 +218,10 @@ typedef struct {
                                  arithmetic with streamed GEMVs and fused norms), 0: the per-op exact kernels */
   int exact_batched_prefill;  /* 1: an exact session runs a prompt's tokens before the last layer by layer, T at a
                                  time (the reference's chains per (row, token)), then the last as a decode step */
+  int prefill_gemm;           /* the batched prefill's GEMM: 7 f16 MFMA on f16 rows of the dequantized Q8_0 activation
+                                 blocks (Q4_0 layers, one device: the default), 5 int8 MFMA on Q8_0 / Q8_K blocks
+                                 (LLMI_PREFILL_F16=0, Q8_0 weights, tensor-parallel ranks), 6 f16 for K-quant layers
+                                 (LLMI_PREFILL_F16=1); 0 no batched prefill */
 } llmi_session_info;
 int llmi_session_get_info(const llmi_session* s, llmi_session_info* info);
 

@@ -51,7 +51,8 @@ class SessionInfo(C.Structure):
                 ("tp_rank", C.c_int), ("tp_size", C.c_int), ("batched_prefill", C.c_int),
                 ("screened_logits", C.c_int), ("screen_bytes", C.c_size_t), ("prefill_f16_redo", C.c_int),
                 ("layer_engine", C.c_int), ("ffn_engine", C.c_int), ("tp_exchange", C.c_int),
-                ("block_slow_waits", C.c_longlong), ("exact_engine", C.c_int), ("exact_batched_prefill", C.c_int)]
+                ("block_slow_waits", C.c_longlong), ("exact_engine", C.c_int), ("exact_batched_prefill", C.c_int),
+                ("prefill_gemm", C.c_int)]
 
 
 _lib = None

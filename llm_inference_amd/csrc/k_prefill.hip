@@ -50,6 +50,48 @@ __device__ __forceinline__ float block_sum(float v, float* red) {  // fixed orde
   __syncthreads();
   return s;
 }
+template <int NWAVE>
+__device__ __forceinline__ float block_max(float v, float* red) {
+  v = wave_max(v);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  float m = 0.0f;
+#pragma unroll
+  for (int i = 0; i < NWAVE; i++) m = fmaxf(m, red[i]);
+  __syncthreads();
+  return m;
+}
+
+// f16 activations of the f16 prefill (GEMM v7): a token's row is its Q8_0 blocks (quantize_row_q8_0,
+// ops.cpp:116-139 -- the values the reference's mat_vec_mul reads) dequantized and scaled by 2^-s, s chosen per
+// token from the row's max |x| so that the largest value lands in [2^14, 2^15): f16(f16(d) q 2^-s) is the
+// reference's d q to one f16 rounding with no overflow, and the power of two is exact (the GEMM multiplies its
+// outputs by 2^s).  token_xs returns 2^-s (1 for an all-zero or non-finite row) and stores 2^s.
+__device__ __forceinline__ float token_xs(float amax, float* tscale) {
+  int f = 127;
+  if (amax > 0.0f && amax <= 3.4e38f) {
+    const int e = (int)((__float_as_uint(amax) >> 23) & 0xFFu) - 127;
+    f = min(max(127 + 14 - e, 2), 252);
+  }
+  if (tscale) *tscale = __uint_as_float((uint32_t)(254 - f) << 23);
+  return __uint_as_float((uint32_t)f << 23);
+}
+// one Q8_0 block held by a DPP quad of lanes (8 elements each, as q8_block_quad: the same max, d and quants),
+// written as the 8 f16 values f16(f16(d) q xs); every lane of the quad must execute it
+__device__ __forceinline__ void q8_f16_quad(const float (&v)[8], float xs, uint16_t* dst) {
+  float amax = 0.0f;
+#pragma unroll
+  for (int k = 0; k < 8; k++) amax = fmaxf(amax, fabsf(v[k]));
+  amax = fmaxf(amax, dpp_f<DPP_QUAD_1032>(amax));
+  amax = fmaxf(amax, dpp_f<DPP_QUAD_2301>(amax));
+  const float dd = amax / 127.0f;
+  const float id = dd != 0.0f ? 1.0f / dd : 0.0f;
+  const float ds = h2f(f2h_ggml(dd)) * xs;  // exact (a power of two)
+  float o[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) o[k] = (float)nearest_int_fma(v[k], id) * ds;  // exact in f32: 11 x 7 bits
+  store_f16x8(dst, o);
+}
 
 // ---------------------------------------------------------------------------
 // per-token residual / norm -> Q8_0
@@ -111,11 +153,14 @@ __global__ __launch_bounds__(256) void prefill_norm_kernel(PrefillNorm a) {
     if (i < n) s_x[i] = (sc2 * v[k]) * a.w_next[i];
   }
   __syncthreads();
-  if (a.x16) {
-    for (int i = t; i < n / 8; i += 256) {
+  if (a.x16) {  // f16 rows of the token's dequantized Q8_0 blocks, scaled per token (token_xs)
+    float amax = 0.0f;
+    for (int i = t; i < n; i += 256) amax = fmaxf(amax, fabsf(s_x[i]));
+    const float xs = token_xs(block_max<4>(amax, s_red), t == 0 && a.tscale ? a.tscale + tok : nullptr);
+    for (int i = t; i < n / 8; i += 256) {  // a DPP quad per block (n % 32 == 0: whole quads)
       const float4 f0 = reinterpret_cast<const float4*>(s_x)[2 * i], f1 = reinterpret_cast<const float4*>(s_x)[2 * i + 1];
       const float vv[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
-      store_f16x8(a.x16 + (size_t)tok * a.x16stride + 8 * i, vv);
+      q8_f16_quad(vv, xs, a.x16 + (size_t)tok * a.x16stride + 8 * i);
     }
     return;
   }
@@ -195,22 +240,32 @@ __global__ __launch_bounds__(256) void prefill_norm_res_kernel(PrefillNorm a) {
   }
   const float sc2 = rms_scale_pf(block_sum<4>(ss2, s_red), n, a.eps);
   XBlock* xq = a.xq + (size_t)tok * a.xstride;
+  float v[EB][8];
+  float amax = 0.0f;
 #pragma unroll
   for (int k = 0; k < EB; k++) {
     const int b = min(t / 4 + 64 * k, nb - 1), e = (b * 32 + sub * 8) / 4;
-    float v[8];
 #pragma unroll
     for (int h = 0; h < 2; h++) {
       const float4 r = r4[k][h], wn = reinterpret_cast<const float4*>(a.w_next)[e + h];
-      v[4 * h + 0] = (sc2 * r.x) * wn.x;
-      v[4 * h + 1] = (sc2 * r.y) * wn.y;
-      v[4 * h + 2] = (sc2 * r.z) * wn.z;
-      v[4 * h + 3] = (sc2 * r.w) * wn.w;
+      v[k][4 * h + 0] = (sc2 * r.x) * wn.x;
+      v[k][4 * h + 1] = (sc2 * r.y) * wn.y;
+      v[k][4 * h + 2] = (sc2 * r.z) * wn.z;
+      v[k][4 * h + 3] = (sc2 * r.w) * wn.w;
     }
+    if (in_row(k))
+#pragma unroll
+      for (int i = 0; i < 8; i++) amax = fmaxf(amax, fabsf(v[k][i]));
+  }
+  // f16 rows: the token's scale 2^-s from its max |x| first (token_xs)
+  const float xs = a.x16 ? token_xs(block_max<4>(amax, s_red), t == 0 && a.tscale ? a.tscale + tok : nullptr) : 1.0f;
+#pragma unroll
+  for (int k = 0; k < EB; k++) {
+    const int b = min(t / 4 + 64 * k, nb - 1);
     if (!in_row(k)) continue;  // whole quads in or out
-    if (a.x16) store_f16x8(a.x16 + (size_t)tok * a.x16stride + b * 32 + sub * 8, v);
-    else if (a.q8k) q8k_block_quad(v, sub, xq + b);  // half-waves = super-blocks (blocks t / 4 + 64 k)
-    else q8_block_quad(v, sub, xq + b);
+    if (a.x16) q8_f16_quad(v[k], xs, a.x16 + (size_t)tok * a.x16stride + b * 32 + sub * 8);
+    else if (a.q8k) q8k_block_quad(v[k], sub, xq + b);  // half-waves = super-blocks (blocks t / 4 + 64 k)
+    else q8_block_quad(v[k], sub, xq + b);
   }
 }
 
@@ -889,9 +944,207 @@ __global__ __launch_bounds__(512, 2) void prefill_gemm6_kernel(PrefillGemm16 a) 
         const float p = ep[(size_t)ww * 32 * 33 + tk * 33 + row % 32];
         v = g ? v + p : p;
       }
-      if (tok < a.T) a.out[(size_t)tok * a.ostride + n0 + row] = v;
+      if (tok < a.T) a.out[(size_t)tok * a.ostride + n0 + row] = a.tscale ? v * a.tscale[tok] : v;
     }
   }
+}
+
+// ---------------------------------------------------------------------------
+// GEMM v7 (the default prefill GEMM for Q4_0 weights; BASELINE configs[2]'s "F16 MFMA prefill GEMM"):
+//   out[t][n] = 2^s_t sum_k f16(d_w (q - 8))[n][k] x16[t][k]
+// on v_mfma_f32_32x32x16_f16 with the fp32 accumulator carried over all of K in k order, where x16 holds the
+// producers' Q8_0 blocks dequantized and scaled by 2^-s_t per token (token_xs): every product is the reference's
+// Q8_0 x Q4_0 term (ops.cpp:364-399) to two f16 roundings, with no per-block epilogue (v5's bound: a conversion
+// and an FMA per output and block on the VALU) and no per-wave dequantization (v6's: every wave unpacked its rows
+// for its own token tile).
+//  * Work-group tile MR x TN = (32 NR WR) x (32 NT WT): WR x WT waves, each NR x NT MFMA tiles of 32 x 32.
+//  * Stage = 64 k (two Q4_0 blocks).  Every thread loads its weight row's blocks (ATPR threads per row) and its
+//    token's 64 f16 (BTPT threads per token) into registers two stages ahead, then writes them to an f16 LDS
+//    tile pair (double-buffered): the weights dequantized ONCE per work-group (f16(1024 + n) - 1032 exactly,
+//    then x d: one rounding), the activations as loaded.  LDS rows are 128 B (64 f16), 16-B units XOR-swizzled
+//    (pg7_slot) so the fragment reads and the writes are conflict-free.
+//  * Software-pipelined, one barrier per stage: the MFMAs of stage c (buffer c & 1) run with stage c + 1's
+//    dequantization and LDS writes (buffer (c + 1) & 1) placed between their k steps; the barrier before
+//    stage c + 1 sees every wave's writes of it and every read of stage c.
+//  * Deterministic and independent of the chunking (a token's outputs read only its own x16 row).
+// ---------------------------------------------------------------------------
+template <int WR, int WT, int NR, int NT>
+struct PG7 {
+  static constexpr int NW = WR * WT, NTH = 64 * NW, MR = 32 * NR * WR, TN = 32 * NT * WT;
+  static constexpr int ATPR = NTH / MR;  // threads per weight row: 1 (the stage's two blocks) or 2 (one each)
+  static constexpr int BTPT = NTH / TN;  // threads per token row (TN * BTPT == NTH)
+  static constexpr int BU = 8 / BTPT;    // 16-B units of the stage's token rows per thread: unit g = u NTH + t is
+                                         // unit g % 8 of token g / 8 (8 lanes read a token's 128-B run)
+  static constexpr int BUF = (MR + TN) * 128, LDS = 2 * BUF;
+  static_assert((ATPR == 1 || ATPR == 2) && MR * ATPR == NTH, "weight rows per thread");
+  static_assert((BTPT == 1 || BTPT == 2 || BTPT == 4 || BTPT == 8) && TN * BTPT == NTH, "token rows per thread");
+};
+
+// 16-B unit u of LDS row `row` (128-B rows): XOR swizzle by the Gray code of the row's low bits, conflict-free for
+// the fragment reads (ds_read_b128's 16-lane groups: rows {0-3, 12-15, 20-27} and {4-11, 16-19, 28-31} of a tile,
+// one unit each) and the writes (ds_write_b128's 8-lane groups: 8 rows, or 4 rows x 2 blocks, or a token's 8 units)
+__device__ __forceinline__ int pg7_slot(int row, int u) { return row * 8 + (u ^ ((row ^ (row >> 1)) & 7)); }
+
+// 8 quants' low (or high) nibbles -> 8 f16 weights f16(d (n - 8)), as a 16-B unit
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u32x4 pg7_deq(uint32_t w0, uint32_t w1, f16x2v s) {
+  const f16x2v m1032 = {(_Float16)-1032.0f, (_Float16)-1032.0f};
+  const uint32_t n0 = w0 & 0x0F0F0F0Fu, n1 = w1 & 0x0F0F0F0Fu;
+  u32x4 o;  // bytes {b, 0x64} = f16 1024 + b: v_perm with the constant 0x64 bytes as its second source
+  o.x = __builtin_bit_cast(uint32_t, (__builtin_bit_cast(f16x2v, __builtin_amdgcn_perm(0x64646464u, n0, 0x04010400u)) + m1032) * s);
+  o.y = __builtin_bit_cast(uint32_t, (__builtin_bit_cast(f16x2v, __builtin_amdgcn_perm(0x64646464u, n0, 0x04030402u)) + m1032) * s);
+  o.z = __builtin_bit_cast(uint32_t, (__builtin_bit_cast(f16x2v, __builtin_amdgcn_perm(0x64646464u, n1, 0x04010400u)) + m1032) * s);
+  o.w = __builtin_bit_cast(uint32_t, (__builtin_bit_cast(f16x2v, __builtin_amdgcn_perm(0x64646464u, n1, 0x04030402u)) + m1032) * s);
+  return o;
+}
+
+template <int WR, int WT, int NR, int NT, int OCC = 1, int NS = 2>
+__global__ __launch_bounds__(64 * WR * WT, OCC) void prefill_gemm7_kernel(PrefillGemm16 a) {
+  using C = PG7<WR, WT, NR, NT>;
+  typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+  __shared__ __attribute__((aligned(16))) unsigned char s_t[C::LDS];
+  const int t = threadIdx.x, lane = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6), r = lane & 31, h = lane >> 5;
+  const int wr = w % WR, wt = w / WR;
+  const int nb = a.nb, nst = nb / 2;
+  const int n_rt = a.rows / C::MR, n_tt = (a.T + C::TN - 1) / C::TN;
+  const int bid = blockIdx.x;
+  int rt, tt;
+  if (n_rt % 8 == 0) {  // the token tiles of a row tile on one XCD (round-robin placement: speed only)
+    const int j = bid >> 3;
+    rt = (j / n_tt) * 8 + (bid & 7);
+    tt = j % n_tt;
+  } else {
+    rt = bid / n_tt;
+    tt = bid % n_tt;
+  }
+  const int n0 = rt * C::MR, tk0 = tt * C::TN;
+  // this thread's loads: weight row arow (block ablk of a stage when two threads share the row), token btok
+  const int arow = t / C::ATPR, ablk = t % C::ATPR;
+  int xoff[C::BU];  // element offset of this thread's units u (stage 0)
+  static_for<C::BU>([&](auto uc) {
+    constexpr int u = decltype(uc)::value;
+    const int g = u * C::NTH + t;
+    xoff[u] = min(tk0 + (g >> 3), a.T - 1) * a.xstride + (g & 7) * 8;
+  });
+  // the register stages (two, ping-pong): the row's quants (blocks 2c, 2c + 1, or block 2c + ablk), their f16
+  // scales, the token's f16 values
+  constexpr int NQ = 3 - C::ATPR;
+  u32x4 qr[NS][NQ], xr[NS][C::BU];  // NS register sets (native vectors: HIP's uint4 copies are memcpys SROA
+  uint32_t dr[NS];                   // leaves in scratch)
+  auto load = [&](u32x4 (&q)[NQ], uint32_t& d, u32x4 (&x)[C::BU], int c) {
+    const size_t qi = q4_block_index(a.slab, a.rows, nb, n0 + arow, 2 * c + ablk);  // 2c, 2c + 1 adjacent (even)
+    const u32x4* qs = reinterpret_cast<const u32x4*>(a.qs);
+    q[0] = qs[qi];
+    if constexpr (C::ATPR == 1) {
+      q[1] = qs[qi + 1];
+      d = *reinterpret_cast<const uint32_t*>(a.wd + qi);
+    } else {
+      d = a.wd[qi];
+    }
+    static_for<C::BU>([&](auto uc) {
+      constexpr int u = decltype(uc)::value;
+      x[u] = *reinterpret_cast<const u32x4*>(a.x + xoff[u] + 64 * c);
+    });
+  };
+  // (compile-time indices throughout: a private array indexed in a loop before unrolling is promoted to LDS /
+  // scratch by the backend)
+  // the next stage's LDS writes in four parts, each placed after one k step's MFMAs (part p: weight units of
+  // block-unit group p -- dequantized -- and a quarter of the token's units)
+  auto put_part = [&](const u32x4 (&q)[NQ], uint32_t d, const u32x4 (&x)[C::BU], int buf, auto pc) {
+    constexpr int p = decltype(pc)::value;
+    unsigned char* As = s_t + buf * C::BUF;
+    unsigned char* Bs = As + C::MR * 128;
+    // weights: NQ blocks x 4 units; part p takes units 4 NQ p / 4 .. (block j = unit / 4)
+    static_for<NQ>([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      static_for<4>([&](auto uc) {
+        constexpr int u = decltype(uc)::value;
+        if constexpr ((4 * j + u) * 4 / (4 * NQ) == p) {
+          const int blk = C::ATPR == 1 ? j : ablk;
+          const uint32_t dh = j ? d >> 16 : d & 0xFFFFu;
+          const f16x2v sc = __builtin_bit_cast(f16x2v, dh | (dh << 16));
+          // block element e < 16: low nibble of byte e (units 0, 1); e >= 16: high nibble of byte e - 16 (2, 3)
+          const uint32_t w0 = u & 1 ? q[j].z : q[j].x, w1 = u & 1 ? q[j].w : q[j].y;
+          *reinterpret_cast<u32x4*>(As + pg7_slot(arow, 4 * blk + u) * 16) =
+              u >= 2 ? pg7_deq(w0 >> 4, w1 >> 4, sc) : pg7_deq(w0, w1, sc);
+        }
+      });
+    });
+    static_for<C::BU>([&](auto uc) {
+      constexpr int u = decltype(uc)::value;
+      if constexpr (u * 4 / C::BU == p) {
+        const int g = u * C::NTH + t;
+        *reinterpret_cast<u32x4*>(Bs + pg7_slot(g >> 3, g & 7) * 16) = x[u];
+      }
+    });
+  };
+  auto put = [&](const u32x4 (&q)[NQ], uint32_t d, const u32x4 (&x)[C::BU], int buf) {
+    static_for<4>([&](auto pc) { put_part(q, d, x, buf, pc); });
+  };
+  v16f acc[NR][NT];
+  static_for<NR>([&](auto ic) { static_for<NT>([&](auto jc) { acc[decltype(ic)::value][decltype(jc)::value] = v16f{}; }); });
+  // stage in buffer buf through the MFMAs, the next stage's writes (into the other buffer) between the k steps
+  auto compute = [&](int buf, const u32x4 (&q)[NQ], uint32_t d, const u32x4 (&x)[C::BU]) {
+    const unsigned char* As = s_t + buf * C::BUF;
+    const unsigned char* Bs = As + C::MR * 128;
+    static_for<4>([&](auto kc) {  // 16 k per MFMA: lane half h holds k 16 ks + 8 h .. + 7 (unit 2 ks + h)
+      constexpr int ks = decltype(kc)::value;
+      f16x8 A[NR], B[NT];
+      static_for<NR>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        A[i] = *reinterpret_cast<const f16x8*>(As + pg7_slot(32 * (NR * wr + i) + r, 2 * ks + h) * 16);
+      });
+      static_for<NT>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        B[j] = *reinterpret_cast<const f16x8*>(Bs + pg7_slot(32 * (NT * wt + j) + r, 2 * ks + h) * 16);
+      });
+      static_for<NR>([&](auto ic) {
+        static_for<NT>([&](auto jc) {
+          constexpr int i = decltype(ic)::value, j = decltype(jc)::value;
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[i], B[j], acc[i][j], 0, 0, 0);
+        });
+      });
+      put_part(q, d, x, buf ^ 1, kc);
+    });
+  };
+  // Pipeline: register set s holds stage c (even c: set 0) two stages after its loads were issued; iteration c
+  // waits at the barrier for every wave's writes of stage c (and so for every read of the other buffer by
+  // stage c - 1), computes stage c while writing stage c + 1 from the other set, then reloads that set with
+  // stage c + 3
+  // Register set s % NS holds stage s from NS stages before its LDS writes (the load latency hidden behind NS
+  // stages of MFMAs).  nst % NS == 0: the unrolled loop body is branch-free; past the last stage the loads repeat
+  // it and the writes land in the buffer nothing reads any more.
+  static_for<NS>([&](auto sc) {
+    constexpr int k = decltype(sc)::value;
+    load(qr[k], dr[k], xr[k], k);
+  });
+  put(qr[0], dr[0], xr[0], 0);
+  load(qr[0], dr[0], xr[0], min(NS, nst - 1));
+  for (int c0 = 0; c0 < nst; c0 += NS) {
+    static_for<NS>([&](auto jc) {
+      constexpr int j = decltype(jc)::value, nx = (j + 1) % NS;
+      __syncthreads();
+      compute(j & 1, qr[nx], dr[nx], xr[nx]);  // stage c0 + j; writes stage c0 + j + 1 from set nx
+      load(qr[nx], dr[nx], xr[nx], min(c0 + j + 1 + NS, nst - 1));
+    });
+  }
+  // D[row 8 (i >> 2) + 4 h + (i & 3)][token r] of every tile, times the token's 2^s: float4 row runs
+  static_for<NT>([&](auto jc) {
+    constexpr int j = decltype(jc)::value;
+    const int tok = tk0 + 32 * (NT * wt + j) + r;
+    if (tok < a.T) {
+      const float sc = a.tscale ? a.tscale[tok] : 1.0f;
+      float* orow = a.out + (size_t)tok * a.ostride + n0 + 4 * h;
+      static_for<NR>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        static_for<4>([&](auto gc) {
+          constexpr int g = decltype(gc)::value;
+          *reinterpret_cast<float4*>(orow + 32 * (NR * wr + i) + 8 * g) = make_float4(
+              acc[i][j][4 * g] * sc, acc[i][j][4 * g + 1] * sc, acc[i][j][4 * g + 2] * sc, acc[i][j][4 * g + 3] * sc);
+        });
+      });
+    }
+  });
 }
 
 // ---------------------------------------------------------------------------
@@ -1121,17 +1374,32 @@ typedef __fp16 fp16x4 __attribute__((__vector_size__(4 * sizeof(__fp16))));
 template <int HD, int NI>
 __device__ __forceinline__ void attn_emit(const PrefillAttn& a, const v16f (&o)[NI], float l_run, int i0, int tok,
                                           int hq, int h) {
-  if (a.x16) {
+  if (a.x16) {  // f16 rows of the dequantized Q8_0 blocks (as below), unscaled: |O| <= max |V| of the f16 cache
     uint16_t* xo16 = a.x16 + (size_t)tok * a.x16stride + (size_t)hq * HD + 32 * i0;
 #pragma unroll
-    for (int i = 0; i < NI; i++)
+    for (int i = 0; i < NI; i++) {
+      float v[16];
+      float amax = 0.0f;
+#pragma unroll
+      for (int reg = 0; reg < 16; reg++) {
+        v[reg] = o[i][reg] / l_run;
+        amax = fmaxf(amax, fabsf(v[reg]));
+      }
+      amax = fmaxf(amax, __shfl_xor(amax, 32));
+      const float dd = amax / 127.0f;
+      const float id = dd != 0.0f ? 1.0f / dd : 0.0f;
+      const float ds = h2f(f2h_ggml(dd));
 #pragma unroll
       for (int gq = 0; gq < 4; gq++) {  // dims 32 i + 8 gq + 4 h .. + 3
+        float q[4];
+#pragma unroll
+        for (int e = 0; e < 4; e++) q[e] = (float)nearest_int_fma(v[4 * gq + e], id) * ds;
         uint2 o2;
-        o2.x = __builtin_bit_cast(uint32_t, f16x2v{(_Float16)(o[i][4 * gq] / l_run), (_Float16)(o[i][4 * gq + 1] / l_run)});
-        o2.y = __builtin_bit_cast(uint32_t, f16x2v{(_Float16)(o[i][4 * gq + 2] / l_run), (_Float16)(o[i][4 * gq + 3] / l_run)});
+        o2.x = __builtin_bit_cast(uint32_t, f16x2v{(_Float16)q[0], (_Float16)q[1]});
+        o2.y = __builtin_bit_cast(uint32_t, f16x2v{(_Float16)q[2], (_Float16)q[3]});
         *reinterpret_cast<uint2*>(xo16 + 32 * i + 8 * gq + 4 * h) = o2;
       }
+    }
     return;
   }
   XBlock* xo = a.xq + (size_t)tok * a.xstride + (size_t)hq * HD / 32 + i0;
@@ -1466,8 +1734,7 @@ __global__ __launch_bounds__(256) void prefill_gelu_kernel(const float* __restri
 // GELU(gate) * up -> Q8_0, vectorized: a thread per 8 consecutive hidden units (one DPP quad per Q8_0 block),
 // float4 loads from the interleaved gate/up rows (H % 8 == 0: the 8 units sit in one H-group)
 __global__ __launch_bounds__(256) void prefill_gelu8_kernel(const float* __restrict__ gu, int F, int H,
-                                                            XBlock* __restrict__ xq, int xstride,
-                                                            uint16_t* __restrict__ x16, int x16stride, int q8k) {
+                                                            XBlock* __restrict__ xq, int xstride, int q8k) {
   const int tok = blockIdx.y, i = blockIdx.x * 256 + threadIdx.x;
   if (i * 8 >= F) return;  // whole quads (F % 32 == 0); Q8_K: whole half-waves (F % 256 == 0)
   const int u = 8 * i;
@@ -1476,9 +1743,46 @@ __global__ __launch_bounds__(256) void prefill_gelu8_kernel(const float* __restr
   const float4 u0 = reinterpret_cast<const float4*>(g + H)[0], u1 = reinterpret_cast<const float4*>(g + H)[1];
   const float v[8] = {gelu_mul1(g0.x, u0.x), gelu_mul1(g0.y, u0.y), gelu_mul1(g0.z, u0.z), gelu_mul1(g0.w, u0.w),
                       gelu_mul1(g1.x, u1.x), gelu_mul1(g1.y, u1.y), gelu_mul1(g1.z, u1.z), gelu_mul1(g1.w, u1.w)};
-  if (x16) store_f16x8(x16 + (size_t)tok * x16stride + u, v);
-  else if (q8k) q8k_block_quad(v, i & 3, xq + (size_t)tok * xstride + i / 4);
+  if (q8k) q8k_block_quad(v, i & 3, xq + (size_t)tok * xstride + i / 4);
   else q8_block_quad(v, i & 3, xq + (size_t)tok * xstride + i / 4);
+}
+
+// GELU(gate) * up -> f16 rows (the f16 prefill): one work-group per token, NJ groups of 8 hidden units per thread
+// held in registers until the token's max |x| is known (token_xs), then written as the dequantized Q8_0 blocks
+template <int NJ>
+__global__ __launch_bounds__(256) void prefill_gelu16_kernel(const float* __restrict__ gu, int F, int H,
+                                                             uint16_t* __restrict__ x16, int x16stride,
+                                                             float* __restrict__ tscale) {
+  __shared__ float s_red[4];
+  const int tok = blockIdx.x, t = threadIdx.x, n8 = F / 8;
+  float v[NJ][8];
+  float amax = 0.0f;
+#pragma unroll
+  for (int j = 0; j < NJ; j++) {
+    const int i = t + 256 * j;
+    if (i >= n8) break;
+    const int u = 8 * i;
+    const float* g = gu + (size_t)tok * 2 * F + 2 * H * (u / H) + u % H;
+    const float4 g0 = reinterpret_cast<const float4*>(g)[0], g1 = reinterpret_cast<const float4*>(g)[1];
+    const float4 u0 = reinterpret_cast<const float4*>(g + H)[0], u1 = reinterpret_cast<const float4*>(g + H)[1];
+    v[j][0] = gelu_mul1(g0.x, u0.x);
+    v[j][1] = gelu_mul1(g0.y, u0.y);
+    v[j][2] = gelu_mul1(g0.z, u0.z);
+    v[j][3] = gelu_mul1(g0.w, u0.w);
+    v[j][4] = gelu_mul1(g1.x, u1.x);
+    v[j][5] = gelu_mul1(g1.y, u1.y);
+    v[j][6] = gelu_mul1(g1.z, u1.z);
+    v[j][7] = gelu_mul1(g1.w, u1.w);
+#pragma unroll
+    for (int e = 0; e < 8; e++) amax = fmaxf(amax, fabsf(v[j][e]));
+  }
+  const float xs = token_xs(block_max<4>(amax, s_red), t == 0 ? tscale + tok : nullptr);
+#pragma unroll
+  for (int j = 0; j < NJ; j++) {
+    const int i = t + 256 * j;
+    if (i >= n8) break;  // whole quads (F % 32 == 0)
+    q8_f16_quad(v[j], xs, x16 + (size_t)tok * x16stride + 8 * i);
+  }
 }
 
 }  // namespace
@@ -1563,12 +1867,75 @@ bool prefill_gemm16_supported(const DevWeight& w) {
   return (w.type == T_Q4_K || w.type == T_Q6_K) && w.kq && w.rows % 64 == 0 && w.cols % 256 == 0;
 }
 
+bool prefill_gemm7_supported(const DevWeight& w) {
+  return w.type == T_Q4_0 && w.rows % 128 == 0 && w.cols % 128 == 0 && (!w.slab || (w.cols / 32) % 8 == 0);
+}
+
+template <int WR, int WT, int NR, int NT, int OCC = 1>
+static bool try_gemm7(const PrefillGemm16& a, hipStream_t s) {
+  using C = PG7<WR, WT, NR, NT>;
+  if (a.rows % C::MR || a.nb % 4) return false;  // an even number of 64-k stages
+  const int n = (a.rows / C::MR) * ((a.T + C::TN - 1) / C::TN);
+  // register stages in flight: 2 (LLMI_PG7_NS=4 for four: slower on the 4B shapes, scripts/dev/pg7_bench)
+  static const int ns = getenv("LLMI_PG7_NS") ? atoi(getenv("LLMI_PG7_NS")) : 2;
+  if (ns == 4 && a.nb % 8 == 0)  // four register stages in flight (a multiple of 4 stages)
+    hipLaunchKernelGGL((prefill_gemm7_kernel<WR, WT, NR, NT, OCC, 4>), dim3(n), dim3(C::NTH), 0, s, a);
+  else
+    hipLaunchKernelGGL((prefill_gemm7_kernel<WR, WT, NR, NT, OCC, 2>), dim3(n), dim3(C::NTH), 0, s, a);
+  return true;
+}
+
+// v7 geometry (LLMI_PG7=<name> forces one for A/B)
+static bool launch_gemm7(const PrefillGemm16& a, hipStream_t s) {
+  const char* f = getenv("LLMI_PG7");
+  const std::string c = f ? f : "";
+  if (c == "256x256") return try_gemm7<2, 2, 4, 4>(a, s);
+  if (c == "256x128") return try_gemm7<2, 2, 4, 2>(a, s);
+  if (c == "128x256") return try_gemm7<2, 2, 2, 4>(a, s);
+  if (c == "128x128") return try_gemm7<2, 2, 2, 2>(a, s);
+  if (c == "256x64") return try_gemm7<4, 1, 2, 2>(a, s);
+  if (c == "128x64") return try_gemm7<2, 1, 2, 2>(a, s);
+  if (c == "128x128o2") return try_gemm7<2, 2, 2, 2, 2>(a, s);
+  if (c == "64x128") return try_gemm7<1, 2, 2, 2>(a, s);
+  if (c == "64x64") return try_gemm7<1, 1, 2, 2>(a, s);
+  if (c == "64x128o2") return try_gemm7<1, 2, 2, 2, 2>(a, s);
+  if (c == "128x64o2") return try_gemm7<2, 1, 2, 2, 2>(a, s);
+  if (c == "256x64o2") return try_gemm7<4, 1, 2, 2, 2>(a, s);
+  if (c == "64x64o4") return try_gemm7<1, 1, 2, 2, 4>(a, s);
+  if (a.T <= 32) return try_gemm7<4, 1, 2, 1>(a, s) || try_gemm7<2, 1, 2, 1>(a, s);
+  if (a.T <= 64) return try_gemm7<4, 1, 2, 2>(a, s) || try_gemm7<2, 1, 2, 2>(a, s);
+  return try_gemm7<2, 2, 2, 2, 2>(a, s);
+}
+
 // v6 geometry: the K split depends on K alone (tensor-parallel shards
 // sum in the same order as the whole weight)
 void launch_prefill_gemm16(const DevWeight& w, const uint16_t* x, int xstride, int T, float* out, int ostride,
-                           hipStream_t s) {
+                           const float* tscale, hipStream_t s) {
+  // Q4_0: v7 where its 128 x 128 tiles fill the chip twice over (gate_up: 640 work-groups at T = 512), v6 for the
+  // narrow and long-K projections (its K split over wave groups keeps 256-320 work-groups of 8 waves busy where
+  // v7 has 80-128): scripts/dev/pg7_bench, 4B shapes at T = 512 -- qkv 29.7 (v6) / 35.7 (v7) / 31.3 (int8 v5) us,
+  // o 23.7 / 27.9 / 25.0, gate_up 105.1 / 92.8 / 143.9, down 80.2 / 118.3 / 98.6
+  const bool wide = (w.rows / 128) * ((T + 127) / 128) >= 512;
+  if (prefill_gemm7_supported(w) && !getenv("LLMI_PG6") && (wide || getenv("LLMI_PG7") || !prefill_gemm16_supported(w))) {
+    PrefillGemm16 a;
+    a.qs = reinterpret_cast<const uint4*>(w.qs);
+    a.wd = w.d;
+    a.rows = w.rows;
+    a.nb = w.cols / 32;
+    a.slab = w.slab;
+    a.x = x;
+    a.xstride = xstride;
+    a.T = T;
+    a.out = out;
+    a.ostride = ostride;
+    a.tscale = tscale;
+    if (!launch_gemm7(a, s)) throw std::runtime_error("prefill_gemm16: shape outside the v7 geometries");
+    LLMI_HIP(hipGetLastError());
+    return;
+  }
   if (!prefill_gemm16_supported(w)) throw std::runtime_error("prefill_gemm16: unsupported weight");
   PrefillGemm16 a;
+  a.tscale = tscale;
   a.qs = reinterpret_cast<const uint4*>(w.qs);
   a.wd = w.d;
   a.kdd = w.kdd;
@@ -1679,13 +2046,25 @@ void launch_prefill_attn(const PrefillAttn& a, int T, hipStream_t s) {
 }
 
 void launch_prefill_gelu(const float* gu, int F, int H, XBlock* xq, int xstride, int T, hipStream_t s, uint16_t* x16,
-                         int x16stride, int q8k) {
+                         int x16stride, int q8k, float* tscale) {
   if (q8k && (H % 8 || F % 256)) throw std::runtime_error("prefill_gelu: Q8_K output needs H % 8 == 0, F % 256 == 0");
   if (F % 32 || H <= 0 || F % H) throw std::runtime_error("prefill_gelu: shape");
-  if (x16 && H % 8) throw std::runtime_error("prefill_gelu: f16 output needs H % 8 == 0");
+  if (x16) {
+    if (H % 8 || !tscale) throw std::runtime_error("prefill_gelu: f16 output needs H % 8 == 0 and the token scales");
+    const int nj = (F / 8 + 255) / 256;
+#define LLMI_GELU16(N) \
+  case N: hipLaunchKernelGGL(prefill_gelu16_kernel<N>, dim3(T), dim3(256), 0, s, gu, F, H, x16, x16stride, tscale); break;
+    switch (nj) {
+      LLMI_GELU16(1) LLMI_GELU16(2) LLMI_GELU16(3) LLMI_GELU16(4) LLMI_GELU16(5) LLMI_GELU16(6)
+      LLMI_GELU16(7) LLMI_GELU16(8) LLMI_GELU16(9) LLMI_GELU16(10) LLMI_GELU16(11) LLMI_GELU16(12)
+      default: throw std::runtime_error("prefill_gelu: f16 output needs n_ff <= 24576");
+    }
+#undef LLMI_GELU16
+    LLMI_HIP(hipGetLastError());
+    return;
+  }
   if (H % 8 == 0) {
-    hipLaunchKernelGGL(prefill_gelu8_kernel, dim3((F / 8 + 255) / 256, T), dim3(256), 0, s, gu, F, H, xq, xstride, x16,
-                       x16stride, q8k);
+    hipLaunchKernelGGL(prefill_gelu8_kernel, dim3((F / 8 + 255) / 256, T), dim3(256), 0, s, gu, F, H, xq, xstride, q8k);
     LLMI_HIP(hipGetLastError());
     return;
   }

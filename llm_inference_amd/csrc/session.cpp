@@ -80,6 +80,13 @@ struct RowSlice {
   const GTensor* t;
   int r0, n;
 };
+// LLMI_PREFILL_F16: unset -1 (the f16 prefill for Q4_0 layers on one device, GEMM v7), "0" off (the int8 GEMM v5
+// everywhere), "1" on (K-quant layers too, GEMM v6)
+static int prefill_f16_env() {
+  const char* e = getenv("LLMI_PREFILL_F16");
+  return e ? (e[0] == '1' ? 1 : 0) : -1;
+}
+
 static RowSlice all_rows(const GTensor* t) { return RowSlice{t, 0, (int)t->shape[1]}; }
 static const void* slice_data(const GGUFView& g, const RowSlice& r) {
   return (const uint8_t*)g.tensor_data(*r.t) + gguf_bytes(r.t->type, r.r0, (int)r.t->shape[0]);
@@ -566,11 +573,11 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
     // projection; Q8_0 block slices need 32-aligned head and hidden shards)
     bool pf = fuse_layers_ && (embd_.type == T_F16 || embd_.type == T_Q8_0) && hp_.n_embd <= 8192 &&
               hp_.n_embd % 32 == 0 && hp_.n_ff % 32 == 0 && (!tp_ || (f_sh_ % 32 == 0 && coll_));
-    // Q4_0 layers: the int8 GEMM (v5) or the f16 one (v6, LLMI_PREFILL_F16); Q8_0 layers: v5; K-quant (kq)
-    // layers: the f16 GEMM
+    // Q4_0 layers: the f16 GEMM (v7, default on one device) or the int8 one (v5); Q8_0 layers: v5; K-quant (kq)
+    // layers: v5 on Q8_K blocks, or the f16 GEMM v6 (LLMI_PREFILL_F16=1)
     auto q40 = [](const DevWeight& w) { return w.type == T_Q4_0 || w.type == T_Q8_0; };
     auto gemm_ok = [&](const DevWeight& w) {
-      return prefill_gemm_supported(w) || (!q40(w) && getenv("LLMI_PREFILL_F16") && prefill_gemm16_supported(w));
+      return prefill_gemm_supported(w) || (!q40(w) && prefill_f16_env() == 1 && prefill_gemm16_supported(w));
     };
     for (const auto& l : L_) {
       bool ok = l.fused && (l.hd == 64 || l.hd == 128 || l.hd == 256) && gemm_ok(l.o.w) && gemm_ok(l.gate_up[0].w) &&
@@ -580,7 +587,7 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
       for (const auto& part : l.qkv) kq = kq || !q40(part.w);
       if (ok && kq)  // 8-unit GELU writes; Q8_K blocks: whole super-blocks (a head of 256, 256-aligned rank slices)
         ok = layer_gemv_gelu_group(l.gate_up[0].w.cols, l.gate_up[0].w.type) % 8 == 0 &&
-             (getenv("LLMI_PREFILL_F16") ||
+             (prefill_f16_env() == 1 ||
               (l.hd == 256 && hp_.n_embd % 256 == 0 && hp_.n_ff % 256 == 0 && (!tp_ || f_sh_ % 256 == 0)));
       pf = pf && ok;
       pf_kq_ = pf_kq_ || kq;
@@ -889,6 +896,7 @@ void Session::ensure_prefill_buffers(int cap) {
   pf_out_ = dalloc<float>((size_t)cap * pf_ostride_);
   pf_xq_ = dalloc<XBlock>((size_t)cap * pf_xs_);
   pf_x16_ = dalloc<uint16_t>((size_t)cap * pf_xs_ * 32);
+  pf_tscale_ = dalloc<float>((size_t)cap);
   pf_q_ = dalloc<uint16_t>((size_t)cap * maxq);
   int maxhd = 0;
   for (const auto& l : L_) maxhd = std::max(maxhd, l.hd);
@@ -922,8 +930,9 @@ void Session::gather_cols(void* buf, size_t pitch_b, size_t slice_b, int T, hipS
       LLMI_HIP(hipMemcpy2DAsync(b + r * slice_b, pitch_b, g + r * blk, slice_b, slice_b, T, hipMemcpyDeviceToDevice, s));
 }
 
-// The opt-in f16 path (LLMI_PREFILL_F16) writes its activations as f16: a value past 65504 becomes inf and the
-// GEMMs then produce non-finite rows.  Such a row reaches the last token's final norm through the residual stream
+// The f16 path writes its activations as f16 rows scaled per token so that none overflows (token_xs); only an
+// attention output past 65504 (the f16 cache's limit) could still become inf, and the GEMMs then produce
+// non-finite rows.  Such a row reaches the last token's final norm through the residual stream
 // or, via the KV cache, through attention (a non-last token's row can escape only in the last layer's FFN, whose
 // output feeds nothing but that token's own residual).  So a finite final norm row proves no f16 activation that
 // matters overflowed; otherwise the prefill is recomputed on the int8 path (the reference's Q8 numerics), which
@@ -939,6 +948,19 @@ void Session::prefill(const int32_t* tokens, int n, int pos) {
       prefill_run(tokens, n, pos, false);
       return;
     }
+}
+
+bool Session::prefill_f16_ok() const {
+  const int G = nh_ / std::max(nkv_, 1);
+  const int fmode = prefill_f16_env();
+  bool v7 = true;  // every projection of every layer a GEMM v7 weight
+  for (const auto& l : L_) {
+    v7 = v7 && prefill_gemm7_supported(l.o.w) && prefill_gemm7_supported(l.gate_up[0].w) && prefill_gemm7_supported(l.down.w);
+    for (const auto& part : l.qkv) v7 = v7 && prefill_gemm7_supported(part.w);
+  }
+  return !tp_ && ((fmode == -1 && v7) || (fmode == 1 && (pf_kq_ || L_[0].o.w.type == T_Q4_0))) &&
+         !getenv("LLMI_PREFILL_ATTN_V1") && (G == 1 || G == 2 || G == 4) &&
+         layer_gemv_gelu_group(L_[0].gate_up[0].w.cols, L_[0].gate_up[0].w.type) % 8 == 0;
 }
 
 bool Session::prefill_run(const int32_t* tokens, int n, int pos, bool allow_f16) {
@@ -958,26 +980,30 @@ bool Session::prefill_run(const int32_t* tokens, int n, int pos, bool allow_f16)
   const int XS = pf_xs_, X16 = pf_xs_ * 32;
   const int r = tp_rank_;  // tensor parallel: this rank's column slices (0 on one device)
   const float emb_scale = std::sqrt(static_cast<float>(E));  // model.cpp:337-338
-  // Q8_0 activation blocks + the int8 GEMM (v5, default: the reference's Q8_0 numerics), or f16 activations + the
-  // f16 MFMA GEMM (v6, LLMI_PREFILL_F16=1: not faster yet -- activation tile re-reads bound it -- and further from
-  // the reference's Q8_0 arithmetic)
-  const int G = nh_ / std::max(nkv_, 1);
-  // K-quant (kq) layers: Q8_K activation blocks from the same producers (the decode's quantization) and the int8
-  // GEMM's K-quant variant, or the opt-in f16 path
-  const bool f16 = allow_f16 && getenv("LLMI_PREFILL_F16") && (pf_kq_ || L_[0].o.w.type == T_Q4_0) &&
-                   !getenv("LLMI_PREFILL_ATTN_V1") && (G == 1 || G == 2 || G == 4) &&
-                   layer_gemv_gelu_group(L_[0].gate_up[0].w.cols, L_[0].gate_up[0].w.type) % 8 == 0;
+  // Activations: f16 rows of the dequantized Q8_0 blocks, scaled per token by 2^-s (the producers' token_xs), and
+  // the f16 MFMA GEMM v7 (Q4_0 layers, one device: the default) -- every product the reference's Q8_0 x Q4_0 term
+  // to two f16 roundings; or Q8_0 blocks and the int8 GEMM v5 (LLMI_PREFILL_F16=0, Q8_0 weights, tensor-parallel
+  // ranks: a token's scale would differ between the ranks' GELU slices); K-quant layers: Q8_K blocks and v5's
+  // K-quant form, or (LLMI_PREFILL_F16=1) f16 rows and GEMM v6.  DESIGN.md section 4.2
+  const bool f16 = allow_f16 && prefill_f16_ok();
   const int q8k = pf_kq_ && !f16 ? 1 : 0;
   // t0: the first token row the rest of a layer runs on (the last layer: only the prompt's final token needs its
   // o / FFN -- every other token's last-layer state is its K / V rows, already in the cache: model.cpp:983-1001)
   int t0 = 0;
-  auto gemm = [&](const DevWeight& w, float* out, int ostride) {
-    if (f16) launch_prefill_gemm16(w, pf_x16_ + (size_t)t0 * X16, X16, T_cur_, out + (size_t)t0 * ostride, ostride, s);
+  // scaled: the x16 rows carry the token scales in pf_tscale_ (the attention's output rows do not: |O| <= max |V|)
+  auto gemm = [&](const DevWeight& w, float* out, int ostride, bool scaled) {
+    if (f16)
+      launch_prefill_gemm16(w, pf_x16_ + (size_t)t0 * X16, X16, T_cur_, out + (size_t)t0 * ostride, ostride,
+                            scaled ? pf_tscale_ + t0 : nullptr, s);
     else launch_prefill_gemm(w, pf_xq_ + (size_t)t0 * XS, XS, T_cur_, out + (size_t)t0 * ostride, ostride, s);
   };
-  auto xtap = [&](const char* name, int l) {
-    if (f16) tap(name, l, pf_x16_ + (size_t)t0 * X16, (size_t)T_cur_ * X16 * 2, s);
-    else tap(name, l, pf_xq_ + (size_t)t0 * XS, (size_t)T_cur_ * XS * sizeof(XBlock), s);
+  auto xtap = [&](const char* name, const char* sname, int l) {  // sname: the token scales' tap (scaled rows)
+    if (f16) {
+      tap(name, l, pf_x16_ + (size_t)t0 * X16, (size_t)T_cur_ * X16 * 2, s);
+      if (sname) tap(sname, l, pf_tscale_ + t0, (size_t)T_cur_ * 4, s);
+    } else {
+      tap(name, l, pf_xq_ + (size_t)t0 * XS, (size_t)T_cur_ * XS * sizeof(XBlock), s);
+    }
   };
   auto xgather = [&](int cols) {  // this rank's activation columns [r * cols, (r + 1) * cols) to every rank
     if (!tp_) return;
@@ -1004,6 +1030,7 @@ bool Session::prefill_run(const int32_t* tokens, int n, int pos, bool allow_f16)
     en.eps = hp_.eps;
     en.x16 = f16 ? pf_x16_ : nullptr;
     en.x16stride = X16;
+    en.tscale = f16 ? pf_tscale_ : nullptr;
     en.q8k = q8k;
     launch_prefill_norm(en, T, s);
     for (int l = 0; l < hp_.n_layer; l++) {
@@ -1011,9 +1038,9 @@ bool Session::prefill_run(const int32_t* tokens, int n, int pos, bool allow_f16)
       const int hd = Ld.hd;
       t0 = 0;
       T_cur_ = T;
-      xtap("pf_x_qkv", l);
+      xtap("pf_x_qkv", "pf_xs_qkv", l);
       for (size_t pi = 0, r0 = 0; pi < Ld.qkv.size(); r0 += Ld.qkv[pi].w.rows, pi++)  // q|k|v, or q|k and v (kq)
-        gemm(Ld.qkv[pi].w, pf_out_ + r0, Ld.qkv_rows);
+        gemm(Ld.qkv[pi].w, pf_out_ + r0, Ld.qkv_rows, true);
       tap("pf_qkv", l, pf_out_, (size_t)T * Ld.qkv_rows * 4, s);
       PrefillQK qk;
       qk.qkv = pf_out_;
@@ -1064,8 +1091,8 @@ bool Session::prefill_run(const int32_t* tokens, int n, int pos, bool allow_f16)
       tap("pf_q", l, pf_q_, (size_t)T * nh_ * hd * 2, s);
       tap("kc", l, Ld.kc, (size_t)nkv_ * max_ctx_ * hd * 2, s);
       tap("vc", l, Ld.vc, (size_t)nkv_ * max_ctx_ * hd * 2, s);
-      xtap("pf_x_o", l);
-      gemm(Ld.o.w, pf_out_ + (size_t)r * e_sh_, E);
+      xtap("pf_x_o", nullptr, l);
+      gemm(Ld.o.w, pf_out_ + (size_t)r * e_sh_, E, false);
       if (tp_) gather_cols(pf_out_ + (size_t)t0 * E, (size_t)E * 4, (size_t)e_sh_ * 4, Tq, s);
       tap("pf_o", l, pf_out_ + (size_t)t0 * E, (size_t)Tq * E * 4, s);
       PrefillNorm rn;  // post-attention norm + residual, then ffn_norm
@@ -1079,19 +1106,21 @@ bool Session::prefill_run(const int32_t* tokens, int n, int pos, bool allow_f16)
       rn.eps = hp_.eps;
       rn.x16 = f16 ? pf_x16_ + (size_t)t0 * X16 : nullptr;
       rn.x16stride = X16;
+      rn.tscale = f16 ? pf_tscale_ + t0 : nullptr;
       rn.q8k = q8k;
       launch_prefill_norm(rn, Tq, s);
       tap("pf_resid_attn", l, rn.resid, (size_t)Tq * E * 4, s);
-      xtap("pf_x_gate_up", l);
+      xtap("pf_x_gate_up", "pf_xs_gate_up", l);
       const int FL = tp_ ? f_sh_ : F;  // this rank's hidden units
-      gemm(Ld.gate_up[0].w, pf_out_, 2 * FL);
+      gemm(Ld.gate_up[0].w, pf_out_, 2 * FL, true);
       tap("pf_gate_up", l, pf_out_ + (size_t)t0 * 2 * FL, (size_t)Tq * 2 * F * 4, s);
       launch_prefill_gelu(pf_out_ + (size_t)t0 * 2 * FL, FL, layer_gemv_gelu_group(Ld.gate_up[0].w.cols, Ld.gate_up[0].w.type),
                           pf_xq_ + (size_t)t0 * XS + (size_t)r * (FL / 32), XS, Tq, s,
-                          f16 ? pf_x16_ + (size_t)t0 * X16 + (size_t)r * FL : nullptr, X16, q8k);
+                          f16 ? pf_x16_ + (size_t)t0 * X16 + (size_t)r * FL : nullptr, X16, q8k,
+                          f16 ? pf_tscale_ + t0 : nullptr);
       xgather(FL);
-      xtap("pf_x_down", l);
-      gemm(Ld.down.w, pf_out_ + (size_t)r * e_sh_, E);
+      xtap("pf_x_down", "pf_xs_down", l);
+      gemm(Ld.down.w, pf_out_ + (size_t)r * e_sh_, E, true);
       if (tp_) gather_cols(pf_out_ + (size_t)t0 * E, (size_t)E * 4, (size_t)e_sh_ * 4, Tq, s);
       tap("pf_down", l, pf_out_ + (size_t)t0 * E, (size_t)Tq * E * 4, s);
       if (l + 1 < hp_.n_layer) {  // post-ffw norm + residual, then the next attn_norm
@@ -1972,6 +2001,7 @@ void Session::info(llmi_session_info* o) const {
   o->block_slow_waits = slow_waits_;
   o->exact_engine = xl_ ? 1 : 0;
   o->exact_batched_prefill = xp_ok() ? 1 : 0;
+  o->prefill_gemm = !prefill_ok_ ? 0 : prefill_f16_ok() ? (pf_kq_ ? 6 : 7) : 5;
   size_t b = logits_w_.bytes;  // this rank's bytes
   for (const auto& l : L_) {
     for (const auto& p : l.qkv) b += p.w.bytes;

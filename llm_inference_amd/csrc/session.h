@@ -100,6 +100,7 @@ class Session {
   bool down_plain(const LayerDev& Ld) const;
   void record_logits(hipStream_t s, bool gen = false);  // xn_ / act_.x16 -> logits, argmax key, token feedback
   void prefill(const int32_t* tokens, int n, int pos);  // batched (k_prefill.hip)
+  bool prefill_f16_ok() const;  // the batched prefill's activations as f16 rows (GEMM v7 / v6)
   bool prefill_run(const int32_t* tokens, int n, int pos, bool allow_f16);  // true: ran the f16 path
   void gather_cols(void* buf, size_t pitch_b, size_t slice_b, int T, hipStream_t s);
   void ensure_prefill_buffers(int cap);
@@ -251,7 +252,8 @@ class Session {
   int32_t* pf_tokens_ = nullptr;
   float *pf_resid_ = nullptr, *pf_out_ = nullptr;
   XBlock* pf_xq_ = nullptr;
-  uint16_t* pf_x16_ = nullptr;  // f16 prefill activations [cap][pf_xs_ * 32] (GEMM v6)
+  uint16_t* pf_x16_ = nullptr;  // f16 prefill activations [cap][pf_xs_ * 32]: dequantized Q8_0 blocks x 2^-s (v7 / v6)
+  float* pf_tscale_ = nullptr;  // [cap] 2^s per token of pf_x16_ (the GEMMs' output scale)
   int T_cur_ = 0;              // tokens of the prefill chunk being enqueued
   int pf_f16_redo_ = 0;        // f16 prefills whose activations overflowed f16 and were recomputed on the int8 path
   bool pf_kq_ = false;         // K-quant layers: the batched prefill runs the f16 path

@@ -127,8 +127,9 @@ struct PrefillNorm {  // per token: embedding (table != null) or residual + norm
   XBlock* xq = nullptr;           // [T][xstride] out
   int xstride = 0, n = 0;
   double eps = 0;
-  uint16_t* x16 = nullptr;        // non-null: x as f16 rows [T][x16stride] instead of Q8_0 blocks (GEMM v6)
-  int x16stride = 0;
+  uint16_t* x16 = nullptr;        // non-null: f16 rows [T][x16stride] of the dequantized Q8_0 blocks, scaled per
+  int x16stride = 0;              // token by 2^-s (GEMMs v6 / v7)
+  float* tscale = nullptr;        // [T] 2^s per token (x16 rows)
   int q8k = 0;                    // 1: Q8_K quants in the blocks (super-block d, block sums; n % 256 == 0)
 };
 struct PrefillGemm {
@@ -153,6 +154,7 @@ struct PrefillGemm16 {  // f16 activations [T][xstride elements] (k_prefill.hip 
   int xstride = 0, T = 0;
   float* out = nullptr;
   int ostride = 0;
+  const float* tscale = nullptr;  // [T] 2^s of the x16 rows (null: 1)
 };
 struct PrefillQK {
   const float* qkv = nullptr;  // [T][qkv_stride]
@@ -184,13 +186,16 @@ void launch_prefill_norm(const PrefillNorm& a, int T, hipStream_t s);
 bool prefill_gemm_supported(const DevWeight& w);
 void launch_prefill_gemm(const DevWeight& w, const XBlock* x, int xstride, int T, float* out, int ostride,
                          hipStream_t s);
+// f16 activations (x16 rows scaled per token, tscale = 2^s per token or null for 1): GEMM v7 for Q4_0 weights
+// (the default prefill GEMM where prefill_gemm7_supported), v6 for the K-quants
 bool prefill_gemm16_supported(const DevWeight& w);
+bool prefill_gemm7_supported(const DevWeight& w);
 void launch_prefill_gemm16(const DevWeight& w, const uint16_t* x, int xstride, int T, float* out, int ostride,
-                           hipStream_t s);
+                           const float* tscale, hipStream_t s);
 void launch_prefill_qk(const PrefillQK& a, int T, hipStream_t s);
 void launch_prefill_attn(const PrefillAttn& a, int T, hipStream_t s);
 void launch_prefill_gelu(const float* gu, int F, int H, XBlock* xq, int xstride, int T, hipStream_t s,
-                         uint16_t* x16 = nullptr, int x16stride = 0, int q8k = 0);
+                         uint16_t* x16 = nullptr, int x16stride = 0, int q8k = 0, float* tscale = nullptr);
 
 // the weight layout the launch-table entry for (w's shape, role) reads
 int layer_gemv_slab(const DevWeight& w, int role);

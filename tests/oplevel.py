@@ -287,9 +287,10 @@ class OpChecker:
     def prefill(self, taps, T_tok):
         """Traced batched prefill: every projection GEMM, token by token, from
         the device's own inputs -- Q8_0 blocks (int8 GEMM v5 vs the reference's
-        per-token mat_vec_mul rows, GEMV tolerance) or f16 rows (the default f16
-        GEMM v6 vs the exactly dequantized Q4_0 weights times those f16 values in
-        float64: the kernel's weights are f16(d (q - 8)), PREFILL16_RTOL)."""
+        per-token mat_vec_mul rows, GEMV tolerance) or f16 rows (the f16 GEMMs v7 /
+        v6 vs the exactly dequantized weights times those f16 values, times the
+        token's scale 2^s, in float64: the kernel's weights are f16(d (q - 8)),
+        PREFILL16_RTOL)."""
         c = self.cfg
         E, F = c.n_embd, c.n_ff
         D = taps_by_layer(taps)
@@ -306,11 +307,14 @@ class OpChecker:
                                        ("o", [f"blk.{l}.attn_output.weight"], c.n_head * c.head_dim),
                                        ("gate_up", None, E),
                                        ("down", [f"blk.{l}.ffn_down.weight"], F)):
-                xs = np.frombuffer(D[(f"pf_x_{proj}", l)][-1], np.uint32).reshape(T_tok, -1, 12)
-                out = f32(D[(f"pf_{proj}", l)][-1]).reshape(T_tok, -1)
+                # (the last layer runs o / FFN for the prompt's final token only: its taps hold one row)
+                raw = np.frombuffer(D[(f"pf_x_{proj}", l)][-1], np.uint32)
+                n_t = raw.size // (row_bytes // 4)
+                xs = raw.reshape(n_t, -1, 12)
+                out = f32(D[(f"pf_{proj}", l)][-1]).reshape(n_t, -1)
                 ws = [self.w.raw(n) for n in (names or [f"blk.{l}.ffn_gate.weight", f"blk.{l}.ffn_up.weight"])]
                 kq = ws[0][1] in kq_types  # Q8_K activation blocks (K-quant layers), else Q8_0
-                for t in range(T_tok):
+                for t in range(n_t):
                     if kq:
                         try:
                             xf = xblocks_q8k_to_f32(xs[t, : ncols // 32])
@@ -330,14 +334,21 @@ class OpChecker:
 
     def _prefill_f16(self, D, T_tok, H):
         c = self.cfg
+        row_elems = len(D[("pf_x_qkv", 0)][-1]) // 2 // T_tok
         E, F = c.n_embd, c.n_ff
         for l in range(c.n_layer):
             for proj, names, ncols in (("qkv", [f"blk.{l}.attn_{p}.weight" for p in "qkv"], E),
                                        ("o", [f"blk.{l}.attn_output.weight"], c.n_head * c.head_dim),
                                        ("gate_up", None, E),
                                        ("down", [f"blk.{l}.ffn_down.weight"], F)):
-                x = np.frombuffer(D[(f"pf_x_{proj}", l)][-1], np.float16).reshape(T_tok, -1)[:, :ncols].astype(np.float64)
-                out = f32(D[(f"pf_{proj}", l)][-1]).reshape(T_tok, -1)
+                raw = np.frombuffer(D[(f"pf_x_{proj}", l)][-1], np.float16)
+                n_t = raw.size // row_elems  # (the last layer's o / FFN: the final token only)
+                x = raw.reshape(n_t, -1)[:, :ncols].astype(np.float64)
+                if (f"pf_xs_{proj}", l) in D:  # the rows' per-token scales 2^s (the attention's rows: none)
+                    ts = f32(D[(f"pf_xs_{proj}", l)][-1]).astype(np.float64)
+                    assert ts.size == n_t and np.all(ts > 0) and np.all(np.frexp(ts)[0] == 0.5), "token scales: powers of two"
+                    x = x * ts[:, None]
+                out = f32(D[(f"pf_{proj}", l)][-1]).reshape(n_t, -1)
                 if proj == "gate_up":
                     g = self.dequant(self.w.raw(f"blk.{l}.ffn_gate.weight"))
                     u = self.dequant(self.w.raw(f"blk.{l}.ffn_up.weight"))
@@ -345,7 +356,7 @@ class OpChecker:
                 else:
                     W = np.concatenate([self.dequant(self.w.raw(n)) for n in names])
                 ref = x @ W.T
-                for t in range(T_tok):
+                for t in range(n_t):
                     self.note(f"prefill_gemm16_{proj}", rel_err(out[t, : ref.shape[1]], ref[t]), PREFILL16_RTOL)
 
 

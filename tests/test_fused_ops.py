@@ -52,7 +52,7 @@ def test_ops_mini4b_block(oracle):
     """Gemma-3 4B layer shapes on the attention-block path, global and local
     rope layers; prefill GEMMs of a 12-token prompt, then 3 decode steps."""
     chk = _run(oracle, "mini-4b", 21, 12, 3, 64, swa_pattern=[True, False])
-    assert "gemv_qkv" in chk.report and "prefill_gemm_gate_up" in chk.report
+    assert "gemv_qkv" in chk.report and "prefill_gemm16_gate_up" in chk.report  # the f16 prefill (GEMM v7 / v6)
 
 
 def test_ops_mini4b_three_launch_attention(oracle, monkeypatch):
@@ -64,6 +64,13 @@ def test_ops_mini4b_three_launch_attention(oracle, monkeypatch):
 
 def test_ops_mini1b_block(oracle):
     _run(oracle, "mini-1b", 23, 12, 3, 64, swa_pattern=[True, False])
+
+
+def test_ops_mini4b_int8_prefill(oracle, monkeypatch):
+    """The int8 batched prefill (LLMI_PREFILL_F16=0: Q8_0 activation blocks, GEMM v5) op by op: every GEMM row
+    against the reference's Q8_0 x Q4_0 rows of the device's own blocks (GEMV tolerance)."""
+    chk = _run(oracle, "mini-4b", 21, 12, 1, 64, monkeypatch, {"LLMI_PREFILL_F16": "0"}, swa_pattern=[True, False])
+    assert "prefill_gemm_gate_up" in chk.report and "prefill_gemm_down" in chk.report
 
 
 def test_ops_mini1b_q8_0_fused(oracle):
@@ -85,12 +92,15 @@ def test_ops_mini27b_shapes(oracle):
     _run(oracle, "mini-27b", 26, 8, 2, 64, swa_pattern=[True, False])
 
 
-@pytest.mark.parametrize("cfg_name", ["mini-4b", "mini-27b"])
-def test_ops_prefill_f16_gemm(oracle, monkeypatch, cfg_name):
-    """The opt-in f16 prefill (LLMI_PREFILL_F16=1: f16 activations from the norm / attention / GELU producers,
-    GEMM v6 with Q4_0 weights dequantized to f16 on v_mfma_f32_32x32x16_f16): every GEMM output row against the
-    exactly dequantized weights times the device's own f16 inputs in float64 (tests/oplevel.py PREFILL16_RTOL)."""
-    chk = _run(oracle, cfg_name, 27, 40, 1, 64, monkeypatch, {"LLMI_PREFILL_F16": "1"})
+@pytest.mark.parametrize("cfg_name,env", [("mini-4b", {}), ("mini-27b", {}), ("mini-1b", {}),
+                                          ("mini-4b", {"LLMI_PG7": "128x64"}), ("mini-4b", {"LLMI_PG6": "1"})])
+def test_ops_prefill_f16_gemm(oracle, monkeypatch, cfg_name, env):
+    """The default f16 prefill of Q4_0 layers: f16 rows of the dequantized Q8_0 activation blocks scaled per token
+    by 2^-s from the norm / attention / GELU producers, GEMM v7 (weights dequantized once per work-group to f16 in
+    LDS, v_mfma_f32_32x32x16_f16 over all of K; another tile geometry; GEMM v6 on the same rows): every GEMM output
+    row against the exactly dequantized weights times the device's own f16 inputs times the token's 2^s in
+    float64 (tests/oplevel.py PREFILL16_RTOL)."""
+    chk = _run(oracle, cfg_name, 27, 40, 1, 64, monkeypatch, env)
     assert "prefill_gemm16_gate_up" in chk.report and "prefill_gemm16_down" in chk.report
 
 

@@ -25,6 +25,13 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _int8_prefill(monkeypatch):
+    """Tensor-parallel ranks run the batched prefill on the int8 GEMM (a token's f16 scale would differ between
+    the ranks' GELU slices), so the whole-model sessions these tests compare against do too."""
+    monkeypatch.setenv("LLMI_PREFILL_F16", "0")
+
+
 def _run_ranks(g, tp, prompt, n_gen, max_ctx=64):
     from llm_inference_amd.model import Model, TPGroup
     grp = TPGroup(tp)
