@@ -1120,14 +1120,16 @@ __global__ __launch_bounds__(64 * WR * WT, OCC) void prefill_gemm7_kernel(Prefil
   });
   put(qr[0], dr[0], xr[0], 0);
   load(qr[0], dr[0], xr[0], min(NS, nst - 1));
-  for (int c0 = 0; c0 < nst; c0 += NS) {
+  int c0 = 0;
+  do {  // (a do-while with a straight body: the accumulators stay in place, no per-iteration copies)
     static_for<NS>([&](auto jc) {
       constexpr int j = decltype(jc)::value, nx = (j + 1) % NS;
       __syncthreads();
       compute(j & 1, qr[nx], dr[nx], xr[nx]);  // stage c0 + j; writes stage c0 + j + 1 from set nx
       load(qr[nx], dr[nx], xr[nx], min(c0 + j + 1 + NS, nst - 1));
     });
-  }
+    c0 += NS;
+  } while (c0 < nst);
   // D[row 8 (i >> 2) + 4 h + (i & 3)][token r] of every tile, times the token's 2^s: float4 row runs
   static_for<NT>([&](auto jc) {
     constexpr int j = decltype(jc)::value;
@@ -1885,8 +1887,9 @@ static bool try_gemm7(const PrefillGemm16& a, hipStream_t s) {
   return true;
 }
 
-// v7 geometry (LLMI_PG7=<name> forces one for A/B)
-static bool launch_gemm7(const PrefillGemm16& a, hipStream_t s) {
+// v7 geometry (LLMI_PG7=<name> forces one for A/B): 128 x 128 tiles for the wide projections, 64 x 128 for the
+// narrow ones (more work-groups), narrower token tiles for short chunks
+static bool launch_gemm7(const PrefillGemm16& a, bool wide, hipStream_t s) {
   const char* f = getenv("LLMI_PG7");
   const std::string c = f ? f : "";
   if (c == "256x256") return try_gemm7<2, 2, 4, 4>(a, s);
@@ -1897,26 +1900,23 @@ static bool launch_gemm7(const PrefillGemm16& a, hipStream_t s) {
   if (c == "128x64") return try_gemm7<2, 1, 2, 2>(a, s);
   if (c == "128x128o2") return try_gemm7<2, 2, 2, 2, 2>(a, s);
   if (c == "64x128") return try_gemm7<1, 2, 2, 2>(a, s);
-  if (c == "64x64") return try_gemm7<1, 1, 2, 2>(a, s);
-  if (c == "64x128o2") return try_gemm7<1, 2, 2, 2, 2>(a, s);
-  if (c == "128x64o2") return try_gemm7<2, 1, 2, 2, 2>(a, s);
-  if (c == "256x64o2") return try_gemm7<4, 1, 2, 2, 2>(a, s);
-  if (c == "64x64o4") return try_gemm7<1, 1, 2, 2, 4>(a, s);
   if (a.T <= 32) return try_gemm7<4, 1, 2, 1>(a, s) || try_gemm7<2, 1, 2, 1>(a, s);
   if (a.T <= 64) return try_gemm7<4, 1, 2, 2>(a, s) || try_gemm7<2, 1, 2, 2>(a, s);
-  return try_gemm7<2, 2, 2, 2, 2>(a, s);
+  return wide ? try_gemm7<2, 2, 2, 2>(a, s) : try_gemm7<1, 2, 2, 2>(a, s);
 }
 
 // v6 geometry: the K split depends on K alone (tensor-parallel shards
 // sum in the same order as the whole weight)
 void launch_prefill_gemm16(const DevWeight& w, const uint16_t* x, int xstride, int T, float* out, int ostride,
                            const float* tscale, hipStream_t s) {
-  // Q4_0: v7 where its 128 x 128 tiles fill the chip twice over (gate_up: 640 work-groups at T = 512), v6 for the
-  // narrow and long-K projections (its K split over wave groups keeps 256-320 work-groups of 8 waves busy where
-  // v7 has 80-128): scripts/dev/pg7_bench, 4B shapes at T = 512 -- qkv 29.7 (v6) / 35.7 (v7) / 31.3 (int8 v5) us,
-  // o 23.7 / 27.9 / 25.0, gate_up 105.1 / 92.8 / 143.9, down 80.2 / 118.3 / 98.6
+  // Q4_0: v7 with 128 x 128 tiles where they fill the chip twice over (gate_up: 640 work-groups at T = 512), v6
+  // elsewhere (its K split over wave groups keeps 256-320 work-groups of 8 waves busy where v7 has 80-128).
+  // In-model, 4B 512-token prefill (scripts/dev/pfprof_geo.sh): 9.76 ms this way, 9.97 with v7 64 x 128 tiles
+  // for qkv / o (which scripts/dev/pg7_bench -- 20 launches of one GEMM, weights warm in the Infinity Cache --
+  // has ahead), 10.2 with v6 everywhere, 10.9-11.2 with the int8 v5
   const bool wide = (w.rows / 128) * ((T + 127) / 128) >= 512;
-  if (prefill_gemm7_supported(w) && !getenv("LLMI_PG6") && (wide || getenv("LLMI_PG7") || !prefill_gemm16_supported(w))) {
+  const bool v6 = getenv("LLMI_PG6") || (!getenv("LLMI_PG7") && !wide && prefill_gemm16_supported(w));
+  if (prefill_gemm7_supported(w) && !v6) {
     PrefillGemm16 a;
     a.qs = reinterpret_cast<const uint4*>(w.qs);
     a.wd = w.d;
@@ -1929,7 +1929,7 @@ void launch_prefill_gemm16(const DevWeight& w, const uint16_t* x, int xstride, i
     a.out = out;
     a.ostride = ostride;
     a.tscale = tscale;
-    if (!launch_gemm7(a, s)) throw std::runtime_error("prefill_gemm16: shape outside the v7 geometries");
+    if (!launch_gemm7(a, wide, s)) throw std::runtime_error("prefill_gemm16: shape outside the v7 geometries");
     LLMI_HIP(hipGetLastError());
     return;
   }
