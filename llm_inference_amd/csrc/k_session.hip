@@ -85,9 +85,17 @@ void flush_cache_locked() {
   g_cache.clear();
   g_cached = 0;
 }
+// LLMI_DEV_CACHE=0: released blocks go straight back through hipFree (the cache is a speed measure -- repeated
+// session creation without remapping -- not the correctness fix: tests/test_tp.py runs the concurrent-construction
+// case with it off)
+bool cache_off() {
+  const char* e = getenv("LLMI_DEV_CACHE");
+  return e && e[0] == '0';
+}
 void release_locked(void* p) {  // (no other session alive)
   auto it = g_sizes.find(p);
-  if (it == g_sizes.end()) {  // not from dev_alloc
+  if (it == g_sizes.end() || cache_off()) {  // not from dev_alloc, or the cache off
+    if (it != g_sizes.end()) g_sizes.erase(it);
     (void)hipFree(p);
     return;
   }

@@ -368,7 +368,7 @@ def test_fused_checksum_catches_a_bad_word(monkeypatch):
     assert second.status == "E_HIP" and "unusable" in str(second)
 
 
-@pytest.mark.parametrize("case", ["27b-8-prefill", "1b-4-shard"])
+@pytest.mark.parametrize("case", ["27b-8-prefill", "1b-4-shard", "1b-4-shard-nocache"])
 def test_sessions_created_concurrently_first_forward(case, monkeypatch):
     """The round-4 wrong-logits causes, both in sessions a group's threads create at the same
     time, both seen as a wrong FIRST forward (the second forward on the same sessions right):
@@ -379,9 +379,12 @@ def test_sessions_created_concurrently_first_forward(case, monkeypatch):
     reallocated at the same time, read wrong on first use (mini-1b tp 4, heads sharded: one hidden unit of one
     rank's first GELU launch; 8 of 23 lifetimes; frees are now held back while other sessions live).
     16 lifetimes, the ranks' sessions created together, each rank's first and second forward equal to the whole
-    model's."""
+    model's.  "-nocache": the same with the allocator's cache of released blocks off (LLMI_DEV_CACHE=0, every
+    free a hipFree): the cache is a speed measure, the fixes are (1) and the held-back frees of (2)."""
     from llm_inference_amd.model import Model, TPGroup
     from llm_inference_amd.synthetic import CONFIGS, build_gemma3_gguf
+    if case.endswith("-nocache"):
+        monkeypatch.setenv("LLMI_DEV_CACHE", "0")
     if case == "27b-8-prefill":
         cfg, tp, n, seed, pseed = CONFIGS["mini-27b"], 8, 70, 13, 15
     else:
