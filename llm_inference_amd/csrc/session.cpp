@@ -985,8 +985,11 @@ bool Session::prefill_run(const int32_t* tokens, int n, int pos, bool allow_f16)
   // to two f16 roundings; or Q8_0 blocks and the int8 GEMM v5 (LLMI_PREFILL_F16=0, Q8_0 weights, tensor-parallel
   // ranks: a token's scale would differ between the ranks' GELU slices); K-quant layers: Q8_K blocks and v5's
   // K-quant form, or (LLMI_PREFILL_F16=1) f16 rows and GEMM v6.  DESIGN.md section 4.2
-  const bool f16 = allow_f16 && prefill_f16_ok();
-  const int q8k = pf_kq_ && !f16 ? 1 : 0;
+  const bool f16_all = allow_f16 && prefill_f16_ok();
+  // the last layer past its K / V appends (one token: the trim below) takes the int8 path: the f16 GEMMs' tiles
+  // are slow for T = 1 (4B: gate_up 38 vs 24 us, down 52 vs 43)
+  bool f16 = f16_all;
+  int q8k = pf_kq_ && !f16 ? 1 : 0;
   // t0: the first token row the rest of a layer runs on (the last layer: only the prompt's final token needs its
   // o / FFN -- every other token's last-layer state is its K / V rows, already in the cache: model.cpp:983-1001)
   int t0 = 0;
@@ -1038,6 +1041,8 @@ bool Session::prefill_run(const int32_t* tokens, int n, int pos, bool allow_f16)
       const int hd = Ld.hd;
       t0 = 0;
       T_cur_ = T;
+      f16 = f16_all;
+      q8k = pf_kq_ && !f16 ? 1 : 0;
       xtap("pf_x_qkv", "pf_xs_qkv", l);
       for (size_t pi = 0, r0 = 0; pi < Ld.qkv.size(); r0 += Ld.qkv[pi].w.rows, pi++)  // q|k|v, or q|k and v (kq)
         gemm(Ld.qkv[pi].w, pf_out_ + r0, Ld.qkv_rows, true);
@@ -1066,6 +1071,9 @@ bool Session::prefill_run(const int32_t* tokens, int n, int pos, bool allow_f16)
         t0 = T - 1;
         T_cur_ = 1;
       }
+      // the last layer's attention output and FFN on the int8 path (Q4_0 layers: v5 takes every shape the f16
+      // path does), trimmed or not (LLMI_PREFILL_FULL_LAST: the same arithmetic for the final token)
+      if (l + 1 == hp_.n_layer && !pf_kq_) f16 = false;
       const int Tq = T_cur_;
       PrefillAttn at;
       at.softcap = hp_.attn_softcap;
@@ -1140,7 +1148,7 @@ bool Session::prefill_run(const int32_t* tokens, int n, int pos, bool allow_f16)
       record_logits(s);
     }
   }
-  return f16;
+  return f16_all;
 }
 
 // Fast path with every projection a gemv_q4_0_layer launch: 5 launches per

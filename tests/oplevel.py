@@ -290,7 +290,8 @@ class OpChecker:
         per-token mat_vec_mul rows, GEMV tolerance) or f16 rows (the f16 GEMMs v7 /
         v6 vs the exactly dequantized weights times those f16 values, times the
         token's scale 2^s, in float64: the kernel's weights are f16(d (q - 8)),
-        PREFILL16_RTOL)."""
+        PREFILL16_RTOL).  Each tap's format from its size: the f16 path's last
+        layer runs its one remaining token on the int8 path."""
         c = self.cfg
         E, F = c.n_embd, c.n_ff
         D = taps_by_layer(taps)
@@ -298,67 +299,62 @@ class OpChecker:
         xs = max(E, F, c.n_head * c.head_dim) // 32  # activation blocks per token (session pf_xs_)
         row_bytes = len(D[("pf_x_qkv", 0)][-1]) // T_tok
         assert row_bytes in (48 * xs, 64 * xs), f"prefill activation row of {row_bytes} B"
-        f16_in = row_bytes == 64 * xs
-        if f16_in:
-            return self._prefill_f16(D, T_tok, H)
-        kq_types = (TT.Q4_K, TT.Q6_K)
         for l in range(c.n_layer):
             for proj, names, ncols in (("qkv", [f"blk.{l}.attn_{p}.weight" for p in "qkv"], E),
                                        ("o", [f"blk.{l}.attn_output.weight"], c.n_head * c.head_dim),
                                        ("gate_up", None, E),
                                        ("down", [f"blk.{l}.ffn_down.weight"], F)):
-                # (the last layer runs o / FFN for the prompt's final token only: its taps hold one row)
-                raw = np.frombuffer(D[(f"pf_x_{proj}", l)][-1], np.uint32)
-                n_t = raw.size // (row_bytes // 4)
-                xs = raw.reshape(n_t, -1, 12)
-                out = f32(D[(f"pf_{proj}", l)][-1]).reshape(n_t, -1)
-                ws = [self.w.raw(n) for n in (names or [f"blk.{l}.ffn_gate.weight", f"blk.{l}.ffn_up.weight"])]
-                kq = ws[0][1] in kq_types  # Q8_K activation blocks (K-quant layers), else Q8_0
-                for t in range(n_t):
-                    if kq:
-                        try:
-                            xf = xblocks_q8k_to_f32(xs[t, : ncols // 32])
-                        except AssertionError as e:
-                            raise AssertionError(f"layer {l} {proj} token {t}: {e}") from None
-                        dot = lambda w: self.gemv(w, xf)  # noqa: E731
-                    else:
-                        xq = xblocks_to_q8_0(xs[t, : ncols // 32])
-                        dot = lambda w: self.gemv_q8(w, xq)  # noqa: E731
-                    if proj == "gate_up":
-                        g, u = dot(ws[0]), dot(ws[1])
-                        ref = np.concatenate([np.concatenate([g[k * H:(k + 1) * H], u[k * H:(k + 1) * H]])
-                                              for k in range(F // H)])
-                    else:
-                        ref = np.concatenate([dot(w) for w in ws])
-                    self.note(f"prefill_gemm_{proj}", rel_err(out[t, : ref.size], ref), GEMV_RTOL)
-
-    def _prefill_f16(self, D, T_tok, H):
-        c = self.cfg
-        row_elems = len(D[("pf_x_qkv", 0)][-1]) // 2 // T_tok
-        E, F = c.n_embd, c.n_ff
-        for l in range(c.n_layer):
-            for proj, names, ncols in (("qkv", [f"blk.{l}.attn_{p}.weight" for p in "qkv"], E),
-                                       ("o", [f"blk.{l}.attn_output.weight"], c.n_head * c.head_dim),
-                                       ("gate_up", None, E),
-                                       ("down", [f"blk.{l}.ffn_down.weight"], F)):
-                raw = np.frombuffer(D[(f"pf_x_{proj}", l)][-1], np.float16)
-                n_t = raw.size // row_elems  # (the last layer's o / FFN: the final token only)
-                x = raw.reshape(n_t, -1)[:, :ncols].astype(np.float64)
-                if (f"pf_xs_{proj}", l) in D:  # the rows' per-token scales 2^s (the attention's rows: none)
-                    ts = f32(D[(f"pf_xs_{proj}", l)][-1]).astype(np.float64)
-                    assert ts.size == n_t and np.all(ts > 0) and np.all(np.frexp(ts)[0] == 0.5), "token scales: powers of two"
-                    x = x * ts[:, None]
-                out = f32(D[(f"pf_{proj}", l)][-1]).reshape(n_t, -1)
-                if proj == "gate_up":
-                    g = self.dequant(self.w.raw(f"blk.{l}.ffn_gate.weight"))
-                    u = self.dequant(self.w.raw(f"blk.{l}.ffn_up.weight"))
-                    W = np.concatenate([np.concatenate([g[k * H:(k + 1) * H], u[k * H:(k + 1) * H]]) for k in range(F // H)])
+                nbytes = len(D[(f"pf_x_{proj}", l)][-1])
+                f16_rows = nbytes % (64 * xs) == 0 and (nbytes // (64 * xs) == T_tok or nbytes == 64 * xs)
+                if f16_rows and row_bytes == 64 * xs:
+                    self._prefill_f16_one(D, l, proj, names, ncols, nbytes // (64 * xs), H)
                 else:
-                    W = np.concatenate([self.dequant(self.w.raw(n)) for n in names])
-                ref = x @ W.T
-                for t in range(n_t):
-                    self.note(f"prefill_gemm16_{proj}", rel_err(out[t, : ref.shape[1]], ref[t]), PREFILL16_RTOL)
+                    self._prefill_q8_one(D, l, proj, names, ncols, nbytes // (48 * xs), H)
 
+    def _prefill_q8_one(self, D, l, proj, names, ncols, n_t, H):
+        c = self.cfg
+        F = c.n_ff
+        kq_types = (TT.Q4_K, TT.Q6_K)
+        xs = np.frombuffer(D[(f"pf_x_{proj}", l)][-1], np.uint32).reshape(n_t, -1, 12)
+        out = f32(D[(f"pf_{proj}", l)][-1]).reshape(n_t, -1)
+        ws = [self.w.raw(n) for n in (names or [f"blk.{l}.ffn_gate.weight", f"blk.{l}.ffn_up.weight"])]
+        kq = ws[0][1] in kq_types  # Q8_K activation blocks (K-quant layers), else Q8_0
+        for t in range(n_t):
+            if kq:
+                try:
+                    xf = xblocks_q8k_to_f32(xs[t, : ncols // 32])
+                except AssertionError as e:
+                    raise AssertionError(f"layer {l} {proj} token {t}: {e}") from None
+                dot = lambda w: self.gemv(w, xf)  # noqa: E731
+            else:
+                xq = xblocks_to_q8_0(xs[t, : ncols // 32])
+                dot = lambda w: self.gemv_q8(w, xq)  # noqa: E731
+            if proj == "gate_up":
+                g, u = dot(ws[0]), dot(ws[1])
+                ref = np.concatenate([np.concatenate([g[k * H:(k + 1) * H], u[k * H:(k + 1) * H]])
+                                      for k in range(F // H)])
+            else:
+                ref = np.concatenate([dot(w) for w in ws])
+            self.note(f"prefill_gemm_{proj}", rel_err(out[t, : ref.size], ref), GEMV_RTOL)
+
+    def _prefill_f16_one(self, D, l, proj, names, ncols, n_t, H):
+        c = self.cfg
+        F = c.n_ff
+        x = np.frombuffer(D[(f"pf_x_{proj}", l)][-1], np.float16).reshape(n_t, -1)[:, :ncols].astype(np.float64)
+        if (f"pf_xs_{proj}", l) in D:  # the rows' per-token scales 2^s (the attention's rows: none)
+            ts = f32(D[(f"pf_xs_{proj}", l)][-1]).astype(np.float64)
+            assert ts.size == n_t and np.all(ts > 0) and np.all(np.frexp(ts)[0] == 0.5), "token scales: powers of two"
+            x = x * ts[:, None]
+        out = f32(D[(f"pf_{proj}", l)][-1]).reshape(n_t, -1)
+        if proj == "gate_up":
+            g = self.dequant(self.w.raw(f"blk.{l}.ffn_gate.weight"))
+            u = self.dequant(self.w.raw(f"blk.{l}.ffn_up.weight"))
+            W = np.concatenate([np.concatenate([g[k * H:(k + 1) * H], u[k * H:(k + 1) * H]]) for k in range(F // H)])
+        else:
+            W = np.concatenate([self.dequant(self.w.raw(n)) for n in names])
+        ref = x @ W.T
+        for t in range(n_t):
+            self.note(f"prefill_gemm16_{proj}", rel_err(out[t, : ref.shape[1]], ref[t]), PREFILL16_RTOL)
 
     def dequant(self, w):
         """Weight rows -> float64: Q4_0 in numpy, other types through the oracle's dequantize_row."""
