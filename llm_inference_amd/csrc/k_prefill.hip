@@ -1749,19 +1749,20 @@ __global__ __launch_bounds__(256) void prefill_gelu8_kernel(const float* __restr
   else q8_block_quad(v, i & 3, xq + (size_t)tok * xstride + i / 4);
 }
 
-// GELU(gate) * up -> f16 rows (the f16 prefill): one work-group per token, NJ groups of 8 hidden units per thread
-// held in registers until the token's max |x| is known (token_xs), then written as the dequantized Q8_0 blocks
+// GELU(gate) * up -> f16 rows (the f16 prefill): one 1024-thread work-group per token, NJ groups of 8 hidden units
+// per thread held in registers until the token's max |x| is known (token_xs), then written as the dequantized
+// Q8_0 blocks
 template <int NJ>
-__global__ __launch_bounds__(256) void prefill_gelu16_kernel(const float* __restrict__ gu, int F, int H,
-                                                             uint16_t* __restrict__ x16, int x16stride,
-                                                             float* __restrict__ tscale) {
-  __shared__ float s_red[4];
+__global__ __launch_bounds__(1024) void prefill_gelu16_kernel(const float* __restrict__ gu, int F, int H,
+                                                              uint16_t* __restrict__ x16, int x16stride,
+                                                              float* __restrict__ tscale) {
+  __shared__ float s_red[16];
   const int tok = blockIdx.x, t = threadIdx.x, n8 = F / 8;
   float v[NJ][8];
   float amax = 0.0f;
 #pragma unroll
   for (int j = 0; j < NJ; j++) {
-    const int i = t + 256 * j;
+    const int i = t + 1024 * j;
     if (i >= n8) break;
     const int u = 8 * i;
     const float* g = gu + (size_t)tok * 2 * F + 2 * H * (u / H) + u % H;
@@ -1778,10 +1779,10 @@ __global__ __launch_bounds__(256) void prefill_gelu16_kernel(const float* __rest
 #pragma unroll
     for (int e = 0; e < 8; e++) amax = fmaxf(amax, fabsf(v[j][e]));
   }
-  const float xs = token_xs(block_max<4>(amax, s_red), t == 0 ? tscale + tok : nullptr);
+  const float xs = token_xs(block_max<16>(amax, s_red), t == 0 ? tscale + tok : nullptr);
 #pragma unroll
   for (int j = 0; j < NJ; j++) {
-    const int i = t + 256 * j;
+    const int i = t + 1024 * j;
     if (i >= n8) break;  // whole quads (F % 32 == 0)
     q8_f16_quad(v[j], xs, x16 + (size_t)tok * x16stride + 8 * i);
   }
@@ -2051,13 +2052,12 @@ void launch_prefill_gelu(const float* gu, int F, int H, XBlock* xq, int xstride,
   if (F % 32 || H <= 0 || F % H) throw std::runtime_error("prefill_gelu: shape");
   if (x16) {
     if (H % 8 || !tscale) throw std::runtime_error("prefill_gelu: f16 output needs H % 8 == 0 and the token scales");
-    const int nj = (F / 8 + 255) / 256;
+    const int nj = (F / 8 + 1023) / 1024;
 #define LLMI_GELU16(N) \
-  case N: hipLaunchKernelGGL(prefill_gelu16_kernel<N>, dim3(T), dim3(256), 0, s, gu, F, H, x16, x16stride, tscale); break;
+  case N: hipLaunchKernelGGL(prefill_gelu16_kernel<N>, dim3(T), dim3(1024), 0, s, gu, F, H, x16, x16stride, tscale); break;
     switch (nj) {
-      LLMI_GELU16(1) LLMI_GELU16(2) LLMI_GELU16(3) LLMI_GELU16(4) LLMI_GELU16(5) LLMI_GELU16(6)
-      LLMI_GELU16(7) LLMI_GELU16(8) LLMI_GELU16(9) LLMI_GELU16(10) LLMI_GELU16(11) LLMI_GELU16(12)
-      default: throw std::runtime_error("prefill_gelu: f16 output needs n_ff <= 24576");
+      LLMI_GELU16(1) LLMI_GELU16(2) LLMI_GELU16(3) LLMI_GELU16(4)
+      default: throw std::runtime_error("prefill_gelu: f16 output needs n_ff <= 32768");
     }
 #undef LLMI_GELU16
     LLMI_HIP(hipGetLastError());
