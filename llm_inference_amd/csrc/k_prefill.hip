@@ -1861,8 +1861,21 @@ static bool try_gemm6(const PrefillGemm16& a, hipStream_t s) {
 
 template <int WQ>
 static bool gemm6_geometry(const PrefillGemm16& a, hipStream_t s) {
+  if (const char* f = getenv("LLMI_PG6_GEO")) {  // development A/B (scripts/dev/pg7_bench)
+    const std::string c = f;
+    if (c == "a") return try_gemm6<2, 1, 4, 2, 4, 3, WQ>(a, s);  // 64 x 64, K split 4
+    if (c == "b") return try_gemm6<2, 2, 2, 2, 2, 3, WQ>(a, s);  // 64 x 128, K split 2
+    if (c == "c") return try_gemm6<4, 1, 2, 2, 4, 3, WQ>(a, s);  // 128 x 64, K split 2
+    if (c == "d") return try_gemm6<2, 1, 4, 1, 4, 3, WQ>(a, s);  // 64 x 32, K split 4
+    if (c == "e") return try_gemm6<2, 1, 4, 2, 4, 4, WQ>(a, s);  // 64 x 64, K split 4, 4 stages
+    if (c == "f") return try_gemm6<2, 2, 2, 2, 4, 3, WQ>(a, s);  // 64 x 128, K split 2, KB 4
+    if (c == "g") return try_gemm6<4, 2, 1, 2, 2, 3, WQ>(a, s);  // 128 x 128, no K split
+  }
+  // K >= 5120: 64 x 64 tiles, K split 4; shorter K: 128 x 64 tiles with K split 2 where the rows allow (4B qkv /
+  // o 27.7 / 21.1 us against 31.0 / 24.6 for 64 x 128, scripts/dev/pg7_bench) -- block b to K group b % WK in
+  // every form, so the sums do not depend on the tile
   if (a.nb >= 160 && try_gemm6<2, 1, 4, 2, 4, 3, WQ>(a, s)) return true;
-  return try_gemm6<2, 2, 2, 2, 2, 3, WQ>(a, s);
+  return try_gemm6<4, 1, 2, 2, 4, 3, WQ>(a, s) || try_gemm6<2, 2, 2, 2, 2, 3, WQ>(a, s);
 }
 
 bool prefill_gemm16_supported(const DevWeight& w) {

@@ -3,7 +3,7 @@
 // int8 v5 on Q8_0 blocks, 20 launches each timed by events; prints us per launch and TFLOP/s.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -I llm_inference_amd/csrc \
 //         scripts/dev/pg7_bench.hip -o scripts/dev/pg7_bench
-//   scripts/dev/pg7_bench [geometry ...]
+//   scripts/dev/pg7_bench [geometry ...]   (128x128 ... for v7, v6 or v6:<LLMI_PG6_GEO> for v6, v5)
 #include "../../llm_inference_amd/csrc/k_prefill.hip"
 
 namespace llmi {
@@ -70,8 +70,13 @@ int main(int argc, char** argv) {
     for (const auto& geo : geos) {
       unsetenv("LLMI_PG6");
       unsetenv("LLMI_PG7");
-      if (geo == "v6") setenv("LLMI_PG6", "1", 1);
-      else if (geo != "v5") setenv("LLMI_PG7", geo.c_str(), 1);
+      unsetenv("LLMI_PG6_GEO");
+      if (geo.rfind("v6", 0) == 0) {  // v6 or v6:<LLMI_PG6_GEO>
+        setenv("LLMI_PG6", "1", 1);
+        if (geo.size() > 3) setenv("LLMI_PG6_GEO", geo.c_str() + 3, 1);
+      } else if (geo != "v5") {
+        setenv("LLMI_PG7", geo.c_str(), 1);
+      }
       auto run = [&]() {
         if (geo == "v5") launch_prefill_gemm(w, dxb, nb, T, out, sh.rows, s);
         else launch_prefill_gemm16(w, dx, sh.cols, T, out, sh.rows, nullptr, s);

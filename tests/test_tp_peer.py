@@ -15,6 +15,13 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _int8_prefill(monkeypatch):
+    """Tensor-parallel ranks run the batched prefill on the int8 GEMM (tests/test_tp.py), so the whole-model
+    sessions compared against them do too (the spawned rank processes inherit the environment)."""
+    monkeypatch.setenv("LLMI_PREFILL_F16", "0")
+
+
 def _peer_ranks(g, size, prompt, n_gen, env):
     from _peer_worker import run
     ctx = mp.get_context("spawn")
