@@ -652,6 +652,11 @@ Session::Session(const uint8_t* gguf, size_t size, const llmi_session_opts& opts
       const int32_t warm[2] = {0, 0};
       set_token_pos(warm[1], 1, true);
       prefill(warm, 2, 0);
+      // the f16 path's wide-tile GEMM (v7: gate_up at full chunks only) is not launched by two tokens: once more
+      // over the whole chunk buffer into scratch (4B: ~80 us here instead of the first prompt's)
+      if (prefill_f16_ok() && pf_cap_ > 256)
+        for (const auto& part : L_[0].gate_up)
+          launch_prefill_gemm16(part.w, pf_x16_, pf_xs_ * 32, pf_cap_, pf_out_, pf_ostride_, pf_tscale_, stream_);
       LLMI_HIP(hipStreamSynchronize(stream_));
     }
     constructing_ = false;
