@@ -1135,6 +1135,27 @@ __device__ __forceinline__ void xa_mad8p(uint32_t& acc, const uint4 v, const flo
         "v"(e[6]), "v"(e[7]));
 }
 
+// xa_mad8p for eight keys holding a max move: before every key's step vec_scale_f16's acc = f16(f32(acc) * pe)
+// (ops.cpp:1084-1090), as v_fma_mix_f32 with a -0.0 addend (x * pe + -0.0 is x * pe rounded once, the sign of a
+// zero product kept) then v_cvt_f16_f32; pe is exactly 1.0 on the keys without a move, where the scale returns
+// acc's own bits.  Branch-free: four dependent instructions per key instead of a uniform branch per key
+#define XA_SCALE_STEP(V, E, P, SEL)                                          \
+  "v_fma_mix_f32 %0, %0, " P ", %13 op_sel_hi:[1,0,0]\n\t"                  \
+  "v_cvt_f16_f32_e32 %0, %0\n\t"                                             \
+  "v_fma_mix_f32 %0, " V ", " E ", %0 " SEL "op_sel_hi:[1,0,1]\n\t"          \
+  "v_cvt_f16_f32_e32 %0, %0\n\t"
+__device__ __forceinline__ void xa_mad8s(uint32_t& acc, const uint4 v, const float* e, const float* pe) {
+  asm volatile(XA_SCALE_STEP("%1", "%5", "%14", "") XA_SCALE_STEP("%1", "%6", "%15", "op_sel:[1,0,0] ")
+               XA_SCALE_STEP("%2", "%7", "%16", "") XA_SCALE_STEP("%2", "%8", "%17", "op_sel:[1,0,0] ")
+               XA_SCALE_STEP("%3", "%9", "%18", "") XA_SCALE_STEP("%3", "%10", "%19", "op_sel:[1,0,0] ")
+               XA_SCALE_STEP("%4", "%11", "%20", "") XA_SCALE_STEP("%4", "%12", "%21", "op_sel:[1,0,0] ")
+               : "+v"(acc)
+               : "v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w), "v"(e[0]), "v"(e[1]), "v"(e[2]), "v"(e[3]), "v"(e[4]),
+                 "v"(e[5]), "v"(e[6]), "v"(e[7]), "v"(0x80000000u), "v"(pe[0]), "v"(pe[1]), "v"(pe[2]), "v"(pe[3]),
+                 "v"(pe[4]), "v"(pe[5]), "v"(pe[6]), "v"(pe[7]));
+}
+#undef XA_SCALE_STEP
+
 // one step of xa_mad8p: key in the low (hi = 0) or high half of v
 __device__ __forceinline__ void xa_mad1(uint32_t& acc, uint32_t v, float e, int hi) {
   if (hi)
@@ -1273,7 +1294,7 @@ __global__ __launch_bounds__((HD / 64 + 1) * 64) void xattn_accum_kernel(XAttnAr
 #pragma unroll
             for (int i = 0; i < 4; i++) xa_mad8p(acc, vb4[b][i], e + 8 * i);
             v16 = (uint16_t)acc;
-          } else {  // a max move in the batch, or its last keys: the pe values in registers too, then key by key
+          } else {  // a max move in the batch, or its last keys: the pe values in registers too
             float pe[32];
 #pragma unroll
             for (int u4 = 0; u4 < 8; u4++) {
@@ -1283,9 +1304,11 @@ __global__ __launch_bounds__((HD / 64 + 1) * 64) void xattn_accum_kernel(XAttnAr
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // no LDS wait inside the key steps
             uint32_t acc = v16;
 #pragma unroll
-            for (int i = 0; i < 4; i++) {  // eight keys at a time: straight steps where the eight have no move
-              if (((up >> (8 * i)) & 0xFFu) == 0 && m >= 8 * (i + 1)) {
-                xa_mad8p(acc, vb4[b][i], e + 8 * i);
+            for (int i = 0; i < 4; i++) {  // eight keys at a time: straight steps where the eight have no move,
+              // scale + step for all eight where they hold one; key by key only in the context's last keys
+              if (m >= 8 * (i + 1)) {
+                if (((up >> (8 * i)) & 0xFFu) == 0) xa_mad8p(acc, vb4[b][i], e + 8 * i);
+                else xa_mad8s(acc, vb4[b][i], e + 8 * i, pe + 8 * i);
                 continue;
               }
 #pragma unroll
@@ -1337,10 +1360,16 @@ __global__ __launch_bounds__((HD / 64 + 1) * 64) void xattn_accum_kernel(XAttnAr
               pv[4 * u4] = p.x; pv[4 * u4 + 1] = p.y; pv[4 * u4 + 2] = p.z; pv[4 * u4 + 3] = p.w;
             }
 #pragma unroll
-            for (int i = 0; i < 4; i++) {  // eight keys at a time: plain adds where the eight have no move
-              if (((up >> (8 * i)) & 0xFFu) == 0 && m >= 8 * (i + 1)) {
+            for (int i = 0; i < 4; i++) {  // eight keys at a time: plain adds where the eight have no move, the
+              // reference's s_acc * pe + e on all eight where they hold one (pe 1.0: the mul returns s_acc)
+              if (m >= 8 * (i + 1)) {
+                if (((up >> (8 * i)) & 0xFFu) == 0) {
 #pragma unroll
-                for (int u = 8 * i; u < 8 * i + 8; u++) s_acc = s_acc + ev[u];
+                  for (int u = 8 * i; u < 8 * i + 8; u++) s_acc = s_acc + ev[u];
+                } else {
+#pragma unroll
+                  for (int u = 8 * i; u < 8 * i + 8; u++) s_acc = s_acc * pv[u] + ev[u];
+                }
                 continue;
               }
 #pragma unroll

@@ -457,6 +457,8 @@ static void attn_bench(std::mt19937& g, int pos) {
   std::snprintf(nm, sizeof nm, "attn accum (pos %d)", pos);
   time_launch(nm, [&] { hipLaunchKernelGGL(xattn_accum_kernel<256>, dim3(H), dim3(320), 0, 0, x); });
   phases("accum", H);
+  std::vector<uint32_t> o_new((size_t)H * HD), o_old((size_t)H * HD);
+  LLMI_HIP(hipMemcpy(o_new.data(), x.out, o_new.size() * 4, hipMemcpyDeviceToHost));
   {  // the same launch with every V load inside the first 4-KB tile (L1 hits): the V fetch's share
     const int st = x.vt_stride;
     x.vt_stride = 32;
@@ -467,6 +469,12 @@ static void attn_bench(std::mt19937& g, int pos) {
   }
   std::snprintf(nm, sizeof nm, "attn accum old (pos %d)", pos);
   time_launch(nm, [&] { hipLaunchKernelGGL(xattn_accum_kernel_old<256>, dim3(H), dim3(320), 0, 0, x); });
+  LLMI_HIP(hipMemcpy(o_old.data(), x.out, o_old.size() * 4, hipMemcpyDeviceToHost));
+  {
+    int bad = 0;
+    for (size_t i = 0; i < o_new.size(); i++) bad += o_new[i] != o_old[i];
+    std::printf("   accum vs the round-4 kernel (pos %d): %d of %zu outputs differ\n", pos, bad, o_new.size());
+  }
   std::snprintf(nm, sizeof nm, "attn accum no-V (pos %d)", pos);
   time_launch(nm, [&] { hipLaunchKernelGGL(xattn_accum_kernel_noload<256>, dim3(H), dim3(320), 0, 0, x); });
   phases("accum old", H);
